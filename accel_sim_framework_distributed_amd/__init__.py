@@ -1,0 +1,22 @@
+"""accel-sim-framework-distributed, rebuilt MI355X-native.
+
+A trace-driven cycle-level GPU performance + power simulator (the capabilities
+of Accel-Sim / GPGPU-Sim / AccelWattch and the "distributed" NCCL fork) whose
+cycle engine runs ON an MI355X: one CDNA4 wavefront simulates one SM or one
+memory channel, state resident in LDS, one grid barrier per PDES epoch; a
+bit-identical CPU reference engine runs the same single-source model.
+
+Subpackages
+  models/        simulated-GPU presets (gpgpusim.config/trace.config writers)
+  ops/           the HIP engine front-end and device micro-benchmarks
+  parallel/      multi-GPU simulation over RCCL, job-level parallel runners
+  tracegen/      synthetic traces (Rodinia-2.0-ft shaped), trace formats
+  job_launching/ run_simulations / job_status / monitor / get_stats / procman
+  plotting/      correlator (sim vs HW), stat plots
+  tuner/         microbenchmark-driven config tuner
+  power/         AccelWattch calibration (quadratic programming)
+  utils/         stats parsing, helpers
+"""
+__version__ = "0.1.0"
+
+from .sim import SimResult, Simulator, simulate  # noqa: F401,E402

@@ -1,0 +1,36 @@
+"""Loader for the in-tree native module ``_asim`` (built by build_native.py)."""
+from __future__ import annotations
+
+import importlib
+import os
+import sys
+
+_mod = None
+
+
+def load(prefer_torch_runtime: bool = False):
+    """Import the native module.
+
+    ``prefer_torch_runtime``: import torch first so the process binds the HIP
+    runtime bundled with PyTorch (same SONAME as /opt/rocm's); required when
+    the simulator shares a process with torch.distributed / RCCL.
+    """
+    global _mod
+    if _mod is not None:
+        return _mod
+    if prefer_torch_runtime:
+        try:
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is optional here
+            pass
+    try:
+        _mod = importlib.import_module("accel_sim_framework_distributed_amd._asim")
+    except ImportError as e:
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        raise ImportError(
+            "native module _asim is not built; run `python build_native.py` in " + root + f" ({e})") from e
+    return _mod
+
+
+def gpu_available() -> bool:
+    return bool(load().gpu_available())

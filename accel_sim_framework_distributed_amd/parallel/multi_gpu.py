@@ -1,0 +1,95 @@
+"""Multi-GPU simulation: one simulated GPU per MI355X rank.
+
+The reference's "distributed" fork only adds a constant latency per
+ncclAllReduce to a single simulated GPU (gpu-simulator/main.cc:116-122).
+Here every rank simulates its own GPU; at each collective the ranks
+synchronise their simulated clocks over RCCL (torch.distributed, backend
+"nccl" = RCCL on ROCm, over xGMI) and the collective costs the analytic
+ring/tree time of the simulated interconnect after the LAST rank arrives --
+a conservative PDES synchronisation at collective boundaries.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional
+
+from .. import _native
+from ..sim import build_args
+
+
+class CollectiveSync:
+    """Collective hook: max-reduce arrival cycles across ranks, then add the
+    modelled collective duration."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self.events: List[Dict] = []
+
+    def __call__(self, sim, desc: Dict, now: int) -> int:
+        import torch
+        import torch.distributed as dist
+        arrive = now
+        if self.world > 1 and dist.is_available() and dist.is_initialized():
+            dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+            t = torch.tensor([float(now)], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            arrive = int(t.item())
+        line = desc["text"]
+        cost = int(sim.collective_cycles(line))
+        self.events.append(dict(op=desc["op"], now=now, arrive=arrive, cost=cost))
+        return (arrive - now) + cost
+
+
+class DistributedSuite:
+    """Runs a directory of applications (``<root>/<app>/<args>/traces``)."""
+
+    def __init__(self, root: str, config: str = "QV100", engine: str = "gpu", rank: int = 0, world: int = 1,
+                 apps: Optional[List[str]] = None, verbose: bool = False, collective_model: str = "ring"):
+        self.mod = _native.load(prefer_torch_runtime=True)
+        self.root = root
+        self.config = config
+        self.engine = engine
+        self.rank = rank
+        self.world = world
+        self.verbose = verbose
+        self.collective_model = collective_model
+        self.apps = []
+        for app in sorted(os.listdir(root)):
+            if app == "all-reduce" or app.startswith("."):
+                continue
+            if apps and app not in apps:
+                continue
+            d = os.path.join(root, app)
+            for args in sorted(os.listdir(d)):
+                kl = os.path.join(d, args, "traces", "kernelslist.g")
+                if os.path.exists(kl):
+                    self.apps.append((app, kl))
+        ar = os.path.join(root, "all-reduce", "kernelslist.g")
+        self.allreduce = ar if os.path.exists(ar) else None
+        self.sync = CollectiveSync(world)
+
+    def _sim(self, kl: str):
+        extra = {"-collective_model": self.collective_model}
+        args = build_args(self.config, kl, self.engine, extra)
+        return self.mod.Simulator(args, self.verbose)
+
+    def step(self) -> Dict:
+        insn = cycles = 0
+        per_app = {}
+        for app, kl in self.apps:
+            s = self._sim(kl)
+            rc = s.run()
+            if rc != 0:
+                raise RuntimeError(f"{app}: simulation failed (deadlock={s.deadlock})\n{s.output[-1500:]}")
+            insn += s.tot_insn
+            cycles += s.tot_cycle
+            per_app[app] = dict(insn=s.tot_insn, cycles=s.tot_cycle)
+        if self.allreduce:
+            s = self._sim(self.allreduce)
+            s.set_collective_hook(lambda d, now, s=s: self.sync(s, d, now))
+            if s.run() != 0:
+                raise RuntimeError("all-reduce example failed\n" + s.output[-1500:])
+            insn += s.tot_insn
+            cycles += s.tot_cycle
+            per_app["all-reduce"] = dict(insn=s.tot_insn, cycles=s.tot_cycle)
+        return dict(insn=insn, cycles=cycles, apps=per_app)

@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Headline benchmark: simulator throughput (sim KIPS, whole node) on the
+Rodinia-2.0-ft suite (synthetic traces of the suite's shape) with the QV100
+config, one simulated GPU per MI355X.
+
+One "step" = every application of the suite simulated end to end (trace load
++ coalescing + cycle simulation + stats) on the GPU engine, followed -- when
+N > 1 -- by the suite's closing all-reduce (examples/all-reduce) whose
+completion is synchronised across the N simulated GPUs over RCCL.  Weak
+scaling: every rank simulates its own GPU running the full suite.
+
+    python bench.py --gpus N --steps K --warmup W
+Rank 0 prints ONE JSON line.  KIPS = simulated thread instructions (the
+reference's gpu_tot_sim_insn, shader.cc:1911) of all ranks / wall seconds /
+1000; the baseline is the reference's published 349 KIPS (heartwall,
+util/job_launching/README.md:77).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_KIPS = 349.0
+
+
+def _parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="QV100")
+    ap.add_argument("--engine", default="auto", choices=["auto", "gpu", "cpu"])
+    ap.add_argument("--apps", default="all")
+    ap.add_argument("--trace-dir", default=None)
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def main() -> int:
+    a = _parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    use_cuda = torch.cuda.is_available()
+    if use_cuda:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl" if use_cuda else "gloo")
+    dev = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
+
+    from accel_sim_framework_distributed_amd import _native
+    mod = _native.load(prefer_torch_runtime=True)
+    engine = a.engine
+    if engine == "auto":
+        engine = "gpu" if mod.gpu_available() else "cpu"
+    if engine == "gpu" and not mod.gpu_available():
+        raise SystemExit("bench.py: --engine gpu requested but no HIP device is usable")
+
+    from accel_sim_framework_distributed_amd.parallel.multi_gpu import DistributedSuite
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+
+    tdir = a.trace_dir or os.path.join(tempfile.gettempdir(), f"asim_bench_rodinia_{os.getuid()}")
+    apps = None if a.apps == "all" else a.apps.split(",")
+    # every rank generates (or reuses) the deterministic synthetic traces
+    marker = os.path.join(tdir, ".complete")
+    if rank == 0 and not os.path.exists(marker):
+        rodinia.generate_suite(tdir, apps)
+        rodinia.write_allreduce_example(os.path.join(tdir, "all-reduce"), nranks=max(1, world))
+        open(marker, "w").write("ok")
+    if world > 1:
+        dist.barrier()
+    while not os.path.exists(marker):
+        time.sleep(0.1)
+
+    suite = DistributedSuite(tdir, config=a.config, engine=engine, rank=rank, world=world, apps=apps,
+                             verbose=a.verbose and rank == 0)
+
+    def sync():
+        if use_cuda:
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        suite.step()
+    sync()
+    t0 = time.perf_counter()
+    insn = 0
+    cycles = 0
+    for _ in range(a.steps):
+        r = suite.step()
+        insn += r["insn"]
+        cycles += r["cycles"]
+    sync()
+    dt = time.perf_counter() - t0
+    # max wall time over ranks, total instructions over ranks
+    t = torch.tensor([dt, float(insn), float(cycles)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        dt, insn_all, cyc_all = float(tmax[0]), float(tsum[1]), float(tsum[2])
+    else:
+        insn_all, cyc_all = float(insn), float(cycles)
+    kips = insn_all / dt / 1e3
+    if rank == 0:
+        out = {
+            "metric": "sim KIPS (whole node)",
+            "value": round(kips, 3),
+            "unit": "KIPS (thousand simulated thread-instructions / wall s, summed over ranks)",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / max(1, a.steps) * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(kips / BASELINE_KIPS, 3),
+            "dtype": "n/a (integer cycle-level model)",
+            "data": "synthetic (seeded Rodinia-2.0-ft-shaped SASS traces; no recorded traces available)",
+            "config": {
+                "model": f"{a.config} (SM7_QV100 gpgpusim.config + trace.config) simulating rodinia_2.0-ft",
+                "global_batch": world,
+                "seq_len": None,
+                "parallelism": f"one simulated GPU per MI355X rank (dp{world}), RCCL-synchronised collectives",
+                "engine": engine,
+                "apps": len(suite.apps),
+                "sim_insn_per_step_per_rank": int(insn / max(1, a.steps)),
+                "sim_cycles_per_step_per_rank": int(cycles / max(1, a.steps)),
+            },
+            "cycle_mae_vs_hw": None,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

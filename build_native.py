@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""Build the native parts in-tree (no installation).
+
+Outputs
+  accel_sim_framework_distributed_amd/_asim*.so   pybind11 module (CPU + HIP engines)
+  bin/accel-sim.out                               accel-sim compatible CLI
+  bin/ubench/*                                    HIP micro-benchmarks (gfx950)
+  bin/libasim_tracer.so                           rocprofiler-sdk trace capture tool
+
+Host C++ is compiled with g++ (OpenMP for the CPU engine), device code with
+``hipcc --offload-arch=gfx950``.  A ninja file is generated under build/ so
+incremental rebuilds are fast.  Usage: ``python build_native.py [--cpu-only] [-j N]``.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "accel_sim_framework_distributed_amd")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+CORE_SRC = [
+    "csrc/config/options.cc",
+    "csrc/config/sim_options.cc",
+    "csrc/trace/trace.cc",
+    "csrc/engine/cpu_engine.cc",
+    "csrc/power/power.cc",
+    "csrc/driver/simulator.cc",
+]
+HIP_SRC = ["csrc/engine/gpu_engine.hip"]
+STUB_SRC = ["csrc/engine/gpu_stub.cc"]
+
+
+def _pybind_includes():
+    import pybind11
+    return [pybind11.get_include(), sysconfig.get_paths()["include"]]
+
+
+def ext_suffix():
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def have_hipcc():
+    return shutil.which("hipcc") is not None or os.path.exists(os.path.join(ROCM, "bin", "hipcc"))
+
+
+def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
+    bdir = os.path.join(ROOT, "build")
+    os.makedirs(bdir, exist_ok=True)
+    hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+    inc = " ".join(f"-I{p}" for p in [os.path.join(ROOT, "csrc")] + _pybind_includes())
+    cxxflags = f"-std=c++17 -O3 -g -fPIC -fopenmp -Wall -Wno-unused-variable -Wno-unused-function {inc}"
+    hipflags = (f"-std=c++17 -O3 -fPIC --offload-arch={ARCH} -munsafe-fp-atomics "
+                f"-I{os.path.join(ROOT, 'csrc')}")
+    ldflags = f"-fopenmp -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib"
+    lines = [
+        "ninja_required_version = 1.3",
+        f"cxxflags = {cxxflags}",
+        f"hipflags = {hipflags}",
+        f"ldflags = {ldflags}",
+        "rule cxx",
+        "  command = g++ $cxxflags -MMD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = CXX $in",
+        "rule hip",
+        f"  command = {hipcc} $hipflags -MMD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = HIP $in",
+        "rule link_so",
+        "  command = g++ -shared $in -o $out $ldflags $libs",
+        "  description = LINK $out",
+        "rule link_exe",
+        "  command = g++ $in -o $out $ldflags $libs",
+        "  description = LINK $out",
+        "rule hipexe",
+        f"  command = {hipcc} $hipflags $in -o $out",
+        "  description = HIPEXE $out",
+    ]
+    objs = []
+    for s in CORE_SRC:
+        o = os.path.join(bdir, s.replace("/", "_") + ".o")
+        lines.append(f"build {o}: cxx {os.path.join(ROOT, s)}")
+        objs.append(o)
+    gpu_objs = []
+    if not cpu_only:
+        for s in HIP_SRC:
+            o = os.path.join(bdir, s.replace("/", "_") + ".o")
+            lines.append(f"build {o}: hip {os.path.join(ROOT, s)}")
+            gpu_objs.append(o)
+        libs = "-lamdhip64"
+    else:
+        for s in STUB_SRC:
+            o = os.path.join(bdir, s.replace("/", "_") + ".o")
+            lines.append(f"build {o}: cxx {os.path.join(ROOT, s)}")
+            gpu_objs.append(o)
+        libs = ""
+    bind_o = os.path.join(bdir, "bindings.o")
+    lines.append(f"build {bind_o}: cxx {os.path.join(ROOT, 'csrc/bindings/py_asim.cc')}")
+    main_o = os.path.join(bdir, "main.o")
+    lines.append(f"build {main_o}: cxx {os.path.join(ROOT, 'csrc/driver/main.cc')}")
+    so = os.path.join(PKG, "_asim" + ext_suffix())
+    lines.append(f"build {so}: link_so {' '.join(objs + gpu_objs + [bind_o])}")
+    lines.append(f"  libs = {libs}")
+    exe = os.path.join(ROOT, "bin", "accel-sim.out")
+    lines.append(f"build {exe}: link_exe {' '.join(objs + gpu_objs + [main_o])}")
+    lines.append(f"  libs = {libs}")
+    defaults = [so, exe]
+    if extra_targets and not cpu_only:
+        ub_dir = os.path.join(ROOT, "csrc", "ubench")
+        if os.path.isdir(ub_dir):
+            for fn in sorted(os.listdir(ub_dir)):
+                if fn.endswith(".hip"):
+                    out = os.path.join(ROOT, "bin", "ubench", fn[:-4])
+                    lines.append(f"build {out}: hipexe {os.path.join(ub_dir, fn)}")
+                    defaults.append(out)
+        tracer = os.path.join(ROOT, "csrc", "tracer", "asim_tracer.cc")
+        if os.path.exists(tracer) and os.path.isdir(os.path.join(ROCM, "include", "rocprofiler-sdk")):
+            t_o = os.path.join(bdir, "tracer.o")
+            lines.append(f"build {t_o}: cxx {tracer}")
+            t_so = os.path.join(ROOT, "bin", "libasim_tracer.so")
+            lines.append(f"build {t_so}: link_so {t_o}")
+            lines.append(f"  libs = -lrocprofiler-sdk -ldl")
+            defaults.append(t_so)
+    lines.append("default " + " ".join(defaults))
+    path = os.path.join(bdir, "build.ninja")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return path
+
+
+def build(cpu_only: bool = False, jobs: int | None = None, extra: bool = True, verbose: bool = False) -> None:
+    if not cpu_only and not have_hipcc():
+        print("[build_native] hipcc not found: building the CPU engine only", file=sys.stderr)
+        cpu_only = True
+    os.makedirs(os.path.join(ROOT, "bin", "ubench"), exist_ok=True)
+    nf = write_ninja(cpu_only, extra)
+    j = jobs or min(16, os.cpu_count() or 4)
+    cmd = ["ninja", "-f", nf, f"-j{j}"]
+    if verbose:
+        cmd.append("-v")
+    subprocess.run(cmd, check=True, cwd=ROOT)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cpu-only", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip ubench / tracer targets")
+    ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("-v", action="store_true")
+    a = ap.parse_args()
+    build(a.cpu_only, a.j, not a.no_extra, a.v)

@@ -1,0 +1,350 @@
+// Python bindings of the native simulator (module: accel_sim_framework_distributed_amd._asim).
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "../driver/simulator.h"
+
+namespace py = pybind11;
+using namespace asim;
+
+namespace {
+
+py::dict cfg_dict(const SimCfg& c) {
+  py::dict d;
+  d["n_sm"] = c.n_sm;
+  d["n_clusters"] = c.n_clusters;
+  d["n_mem"] = c.n_mem;
+  d["n_sub_per_mem"] = c.n_sub_per_mem;
+  d["n_subpart"] = c.n_subpart;
+  d["warp_size"] = c.warp_size;
+  d["max_warps_per_sm"] = c.max_warps_per_sm;
+  d["max_cta_per_sm"] = c.max_cta_per_sm;
+  d["n_sched"] = c.n_sched;
+  d["sched_policy"] = c.sched_policy;
+  d["fetch_throughput"] = c.fetch_throughput;
+  d["ex_wb_width"] = c.ex_wb_width;
+  d["oc_units"] = c.oc_units;
+  d["reg_banks"] = c.reg_banks;
+  d["l1_sets"] = c.l1.nsets;
+  d["l1_assoc"] = c.l1.assoc;
+  d["l1_latency"] = c.l1_latency;
+  d["l1_mshr"] = c.l1.mshr_entries;
+  d["l2_sets"] = c.l2.nsets;
+  d["l2_assoc"] = c.l2.assoc;
+  d["l2_set_index"] = c.l2.set_index;
+  d["rop_latency"] = c.rop_latency;
+  d["dram_latency"] = c.dram_latency;
+  d["nbk"] = c.nbk;
+  d["nbkgrp"] = c.nbkgrp;
+  d["tRCD"] = c.tRCD;
+  d["tRAS"] = c.tRAS;
+  d["tRP"] = c.tRP;
+  d["tRC"] = c.tRC;
+  d["CL"] = c.CL;
+  d["WL"] = c.WL;
+  d["tCCDL"] = c.tCCDL;
+  d["tRTPL"] = c.tRTPL;
+  d["BL"] = c.BL;
+  d["busW"] = c.busW;
+  d["atom_size"] = c.atom_size;
+  d["icnt_latency"] = c.icnt_latency;
+  d["flit_size"] = c.flit_size;
+  d["per_core_fs"] = c.per_core;
+  d["per_dram_fs"] = c.per_dram;
+  d["part_index"] = c.part_index;
+  d["addr_chip_s"] = c.addr_chip_s;
+  py::list masks;
+  for (int i = 0; i < AF_COUNT; ++i) masks.append(c.addr_mask[i]);
+  d["addr_mask"] = masks;
+  d["sub_id_mask"] = c.sub_id_mask;
+  py::list lat, ii;
+  for (int i = 0; i < OC_COUNT; ++i) {
+    lat.append(c.lat[i]);
+    ii.append(c.ii[i]);
+  }
+  d["lat"] = lat;
+  d["ii"] = ii;
+  py::list units;
+  for (int i = 0; i < U_COUNT; ++i) units.append(c.unit_count[i]);
+  d["unit_count"] = units;
+  d["kernel_launch_latency"] = c.kernel_launch_latency;
+  return d;
+}
+
+SimCfg cfg_from_args(const std::vector<std::string>& args) {
+  OptionRegistry r;
+  register_sim_options(r);
+  r.parse_cmdline(args, false);
+  return derive_sim_cfg(r);
+}
+
+py::dict kernel_dict(const KernelResult& k) {
+  py::dict d;
+  d["name"] = k.name;
+  d["uid"] = k.uid;
+  d["start_cycle"] = k.start_cycle;
+  d["cycles"] = k.cycles;
+  d["insn"] = k.insn;
+  d["warp_insn"] = k.warp_insn;
+  d["n_cta"] = k.n_cta;
+  d["cta_per_sm"] = k.cta_per_sm;
+  d["ipc"] = k.ipc;
+  d["occupancy"] = k.occupancy;
+  d["wall_s"] = k.wall_s;
+  d["deadlock"] = k.deadlock;
+  d["avg_power_w"] = k.avg_power_w;
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_asim, m) {
+  m.doc() = "MI355X-native trace-driven GPU simulator (native core)";
+  m.attr("sizeof_SMState") = sizeof(SMState);
+  m.attr("sizeof_ChanState") = sizeof(ChanState);
+  m.attr("sizeof_TInst") = sizeof(TInst);
+
+  m.def("gpu_available", &gpu_engine_available, "True if a HIP device is usable by the GPU engine");
+  m.def("option_names", []() {
+    OptionRegistry r;
+    register_sim_options(r);
+    return r.names();
+  });
+  m.def("parse_config", [](const std::vector<std::string>& args) { return cfg_dict(cfg_from_args(args)); },
+        "derive the model configuration from accel-sim style arguments");
+  m.def("addr_decode", [](const std::vector<std::string>& args, uint64_t addr) {
+    SimCfg c = cfg_from_args(args);
+    AddrTlx t = addr_decode(c, addr);
+    py::dict d;
+    d["chip"] = t.chip;
+    d["bk"] = t.bk;
+    d["row"] = t.row;
+    d["col"] = t.col;
+    d["burst"] = t.burst;
+    d["sub"] = t.sub;
+    return d;
+  });
+  m.def("ipoly_hash", &ipoly_hash);
+  m.def("cache_set_index", [](const std::string& geom, uint64_t addr) {
+    return cache_set_index(parse_cache_geom(geom), addr);
+  });
+  m.def("parse_cache", [](const std::string& geom) {
+    CacheGeom g = parse_cache_geom(geom);
+    py::dict d;
+    d["nsets"] = g.nsets;
+    d["assoc"] = g.assoc;
+    d["line"] = g.line;
+    d["sectored"] = g.sectored;
+    d["repl"] = g.repl;
+    d["wpolicy"] = g.wpolicy;
+    d["alloc"] = std::string(1, (char)g.alloc);
+    d["walloc"] = std::string(1, (char)g.walloc);
+    d["set_index"] = g.set_index;
+    d["mshr_entries"] = g.mshr_entries;
+    d["mshr_merge"] = g.mshr_merge;
+    d["miss_queue"] = g.miss_queue;
+    d["disabled"] = g.disabled;
+    return d;
+  });
+  m.def("decode_opcode", [](const std::string& op, uint32_t bv) {
+    OpInfo o = decode_opcode(op, bv);
+    py::dict d;
+    d["opcode"] = o.opcode;
+    d["cls"] = o.cls;
+    d["space"] = o.space;
+    d["flags"] = o.flags;
+    d["width"] = o.width;
+    d["half_ii"] = o.half_ii;
+    d["known"] = o.known;
+    return d;
+  });
+  m.def("smem_conflict_degree",
+        [](const std::vector<uint64_t>& addrs, uint64_t mask, uint32_t width, const std::vector<std::string>& args) {
+          SimCfg c = cfg_from_args(args);
+          std::vector<uint64_t> a(64, 0);
+          for (size_t i = 0; i < addrs.size() && i < 64; ++i) a[i] = addrs[i];
+          return smem_conflict_degree(a.data(), mask, width, c, c.warp_size);
+        });
+  m.def("occupancy", [](const std::vector<std::string>& args, uint32_t threads, uint32_t shmem, uint32_t regs) {
+    SimCfg c = cfg_from_args(args);
+    Occupancy o = compute_occupancy(c, KernelShape{threads, shmem, regs, 1});
+    py::dict d;
+    d["cta_per_sm"] = o.cta_per_sm;
+    d["l1_sets"] = o.l1_sets;
+    d["l1_assoc"] = o.l1_assoc;
+    d["shmem_kb"] = o.shmem_kb;
+    d["limiter"] = std::string(o.limiter);
+    return d;
+  });
+  m.def("parse_commandlist", [](const std::string& p) {
+    py::list out;
+    for (auto& c : parse_commandlist(p)) {
+      py::dict d;
+      d["type"] = (int)c.type;
+      d["text"] = c.text;
+      d["addr"] = c.addr;
+      d["bytes"] = c.bytes;
+      d["coll"] = c.coll;
+      d["count"] = c.count;
+      d["dtype_bytes"] = c.dtype_bytes;
+      d["nranks"] = c.nranks;
+      d["redop"] = c.redop;
+      out.append(d);
+    }
+    return out;
+  });
+  m.def("kernel_info", [](const std::string& p) {
+    HostKernel k = load_kernel(p);
+    py::dict d;
+    d["name"] = k.h.name;
+    d["grid"] = std::vector<uint32_t>{k.h.grid[0], k.h.grid[1], k.h.grid[2]};
+    d["block"] = std::vector<uint32_t>{k.h.block[0], k.h.block[1], k.h.block[2]};
+    d["shmem"] = k.h.shmem;
+    d["nregs"] = k.h.nregs;
+    d["binary_version"] = k.h.binary_version;
+    d["warp_insts"] = k.warp_insts;
+    d["thread_insts"] = k.thread_insts;
+    d["n_cta"] = k.n_cta;
+    d["warps_per_cta"] = k.warps_per_cta;
+    d["unknown_opcodes"] = k.unknown_opcodes;
+    d["n_mems"] = (uint64_t)k.mems.size();
+    return d;
+  });
+  m.def("convert_trace", [](const std::string& in, const std::string& out) {
+    HostKernel k = load_kernel_text(in);
+    if (out.size() > 6 && out.compare(out.size() - 6, 6, ".asimk") == 0)
+      save_kernel_binary(k, out);
+    else
+      save_kernel_text(k, out);
+    return k.warp_insts;
+  });
+  m.def("coalesce_summary", [](const std::string& path, const std::vector<std::string>& args) {
+    SimCfg c = cfg_from_args(args);
+    ReadyKernel r = coalesce_kernel(load_kernel(path), c);
+    py::dict d;
+    d["n_accs"] = (uint64_t)r.accs.size();
+    uint64_t mem = 0, shared_deg = 0, nshared = 0;
+    for (auto& in : r.insts) {
+      if (in.mem != kNoMem) mem++;
+      if ((in.cls == OC_LOAD || in.cls == OC_STORE) && in.space == S_SHARED) {
+        nshared++;
+        shared_deg += in.width;
+      }
+    }
+    d["mem_insts"] = mem;
+    d["shared_insts"] = nshared;
+    d["shared_degree_sum"] = shared_deg;
+    py::list acc;
+    for (size_t i = 0; i < r.accs.size() && i < 4096; ++i)
+      acc.append(py::make_tuple(r.accs[i].line, r.accs[i].sectors, r.accs[i].bytes));
+    d["accs"] = acc;
+    return d;
+  });
+
+  py::class_<Simulator>(m, "Simulator")
+      .def(py::init([](const std::vector<std::string>& args, bool echo) {
+             auto* s = new Simulator(args);
+             s->set_echo(echo);
+             return s;
+           }),
+           py::arg("args"), py::arg("echo") = false)
+      .def("run", &Simulator::run, py::call_guard<py::gil_scoped_release>())
+      .def("run_command", &Simulator::run_command, py::call_guard<py::gil_scoped_release>())
+      .def("num_commands", [](Simulator& s) { return s.commands().size(); })
+      .def("load_commands", &Simulator::load_commands)
+      .def("print_header", [](Simulator& s) { s.load_commands(); })
+      .def_property_readonly("output", &Simulator::output)
+      .def_property_readonly("tot_cycle", &Simulator::tot_cycle)
+      .def_property_readonly("tot_insn", &Simulator::tot_insn)
+      .def_property_readonly("sim_seconds", &Simulator::sim_seconds)
+      .def_property_readonly("wall_seconds", &Simulator::wall_seconds)
+      .def_property_readonly("deadlock", &Simulator::deadlock)
+      .def_property_readonly("engine", [](Simulator& s) { return std::string(s.engine().name()); })
+      .def_property_readonly("config", [](Simulator& s) { return cfg_dict(s.cfg()); })
+      .def_property_readonly("kernels",
+                             [](Simulator& s) {
+                               py::list l;
+                               for (auto& k : s.kernels()) l.append(kernel_dict(k));
+                               return l;
+                             })
+      .def_property_readonly("collectives",
+                             [](Simulator& s) {
+                               py::list l;
+                               for (auto& c : s.collectives()) {
+                                 py::dict d;
+                                 d["op"] = c.op;
+                                 d["bytes"] = c.bytes;
+                                 d["nranks"] = c.nranks;
+                                 d["cycles"] = c.cycles;
+                                 l.append(d);
+                               }
+                               return l;
+                             })
+      .def("collective_cycles",
+           [](Simulator& s, const std::string& line) { return s.collective_cycles(parse_collective_line(line)); })
+      .def("set_collective_hook",
+           [](Simulator& s, py::function f) {
+             s.set_collective_hook([f](const Command& c, uint64_t now) -> uint64_t {
+               py::gil_scoped_acquire g;
+               py::dict d;
+               d["op"] = c.coll;
+               d["bytes"] = c.bytes;
+               d["count"] = c.count;
+               d["dtype_bytes"] = c.dtype_bytes;
+               d["nranks"] = c.nranks;
+               d["text"] = c.text;
+               return f(d, now).cast<uint64_t>();
+             });
+           })
+      .def("snapshot",
+           [](Simulator& s) {
+             std::vector<uint8_t> v;
+             s.engine().snapshot(v);
+             return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+           })
+      .def("restore", [](Simulator& s, py::bytes b) {
+        std::string str = b;
+        std::vector<uint8_t> v(str.begin(), str.end());
+        s.engine().restore(v);
+      });
+
+  py::class_<PowerModel>(m, "PowerModel")
+      .def(py::init<>())
+      .def("load_xml",
+           [](PowerModel& p, const std::string& path) {
+             std::string err;
+             if (!p.load_xml(path, &err)) throw std::runtime_error(err);
+           })
+      .def("set_param", &PowerModel::set_param)
+      .def("param", &PowerModel::param, py::arg("name"), py::arg("default") = 0.0)
+      .def("coefficients", &PowerModel::coefficients)
+      .def_static("activity_names",
+                  []() {
+                    std::vector<std::string> v;
+                    for (int i = 0; i < PA_COUNT; ++i) v.push_back(kPwrActName[i]);
+                    return v;
+                  })
+      .def_static("base_nj", &PowerModel::base_nj)
+      .def("compute_hw",
+           [](PowerModel& p, const std::string& csv, const std::string& bench, const std::string& kernel,
+              double mhz, uint32_t n_sm) {
+             Activity a;
+             if (!PowerModel::activity_from_hw_csv(csv, bench, kernel, a, n_sm)) throw std::runtime_error("row not found");
+             PowerReport r = p.compute(a, mhz, n_sm);
+             py::dict d;
+             d["total"] = r.total;
+             d["dynamic"] = r.dynamic;
+             d["static"] = r.static_w;
+             d["constant"] = r.constant;
+             d["idle"] = r.idle;
+             d["category"] = r.static_category;
+             std::vector<double> act(a.a, a.a + PA_COUNT);
+             d["activity"] = act;
+             d["cycles"] = a.cycles;
+             d["idle_sms"] = a.idle_sms;
+             return d;
+           });
+}

@@ -1,0 +1,73 @@
+// gpgpusim.config / trace.config option set and its translation into the
+// POD SimCfg consumed by the cycle model.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "../model/config.h"
+#include "options.h"
+
+namespace asim {
+
+// Registers every option the reference simulator accepts in trace mode
+// (gpu-sim.cc:101-763, shader/memory/power/icnt/ptx/trace registrations; ~250
+// flags incl. the looped -specialized_unit_N and
+// -trace_opcode_latency_initiation_spec_op_N) plus this simulator's own
+// extensions (prefixed -sim_ / -icnt_latency / -rccl_*).  PTX-only flags are
+// accepted and ignored, as tested configs still carry them.
+void register_sim_options(OptionRegistry& r);
+
+// Derive the model configuration.  Throws OptionError on malformed composite
+// strings or configurations beyond the compiled capacity caps.
+SimCfg derive_sim_cfg(const OptionRegistry& r);
+
+// cache geometry string  <S|N>:<sets>:<line>:<assoc>,<rep>:<wr>:<alloc>:<wr_alloc>:<idx>,<mshr>:<N>:<merge>,<mq>[:...]
+CacheGeom parse_cache_geom(const std::string& s);
+
+struct KernelShape {
+  uint32_t threads_per_cta;
+  uint32_t shmem_per_cta;
+  uint32_t regs_per_thread;
+  uint32_t n_cta;
+};
+// resource-limited CTAs per SM and adaptive L1 geometry (reference
+// shader_core_config::max_cta, shader.cc:3476-3588)
+struct Occupancy {
+  uint32_t cta_per_sm;
+  uint32_t l1_sets;
+  uint32_t l1_assoc;
+  uint32_t shmem_kb;  // carve-out chosen by the adaptive config
+  const char* limiter;
+};
+Occupancy compute_occupancy(const SimCfg& c, const KernelShape& k);
+
+// extra: option values that are not part of SimCfg but used by the driver
+struct DriverOpts {
+  std::string trace_file;
+  int64_t max_cycle = 0;
+  int64_t max_insn = 0;
+  int32_t max_cta = 0;
+  int32_t max_completed_cta = 0;
+  bool flush_l1 = false;
+  bool flush_l2 = false;
+  bool deadlock_detect = true;
+  int32_t nccl_allreduce_latency = 100;
+  std::string collective_model;   // const | ring | tree | packet
+  double xgmi_link_gbps = 153.0;
+  double xgmi_latency_ns = 1000.0;
+  uint32_t xgmi_links = 7;
+  int32_t concurrent_kernel_sm = 0;
+  int32_t max_concurrent_kernel = 32;
+  bool power_enabled = false;
+  std::string power_xml;
+  int32_t power_mode = 0;
+  uint64_t stat_sample_freq = 500;
+  std::string engine;             // cpu | gpu
+  bool trace_enabled = false;
+  std::string trace_components;
+  int32_t trace_sampling_core = 0;
+  uint32_t sim_epochs_per_launch = 4096;
+};
+DriverOpts derive_driver_opts(const OptionRegistry& r);
+
+}  // namespace asim

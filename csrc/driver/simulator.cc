@@ -1,0 +1,349 @@
+#include "simulator.h"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+#include <stdexcept>
+
+namespace asim {
+
+Simulator::Simulator(const std::vector<std::string>& args) {
+  t_start_ = std::chrono::steady_clock::now();
+  register_sim_options(reg_);
+  reg_.parse_cmdline(args, false);
+  cfg_ = derive_sim_cfg(reg_);
+  dopt_ = derive_driver_opts(reg_);
+  if (dopt_.engine == "gpu") {
+    eng_ = make_gpu_engine();
+    if (!eng_) throw std::runtime_error("-sim_engine gpu requested but the HIP engine is unavailable");
+  } else if (dopt_.engine == "cpu") {
+    eng_ = make_cpu_engine();
+  } else {
+    throw OptionError("-sim_engine must be cpu or gpu");
+  }
+  eng_->init(cfg_);
+  if (dopt_.power_enabled) {
+    power_.reset(new PowerModel());
+    std::string err;
+    if (!power_->load_xml(dopt_.power_xml, &err)) throw std::runtime_error("power model: " + err);
+  }
+}
+
+Simulator::~Simulator() = default;
+
+void Simulator::print(const char* fmt, ...) {
+  char buf[4096];
+  va_list ap;
+  va_start(ap, fmt);
+  int n = vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (n < 0) return;
+  std::string s(buf, std::min<size_t>((size_t)n, sizeof(buf) - 1));
+  out_ += s;
+  if (echo_) {
+    fputs(s.c_str(), stdout);
+  }
+}
+
+double Simulator::wall_seconds() const {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start_).count();
+}
+
+int Simulator::run() {
+  print("Accel-Sim-AMD [MI355X-native trace-driven simulator, engine=%s]\n", eng_->name());
+  cmds_ = parse_commandlist(dopt_.trace_file);
+  for (size_t i = 0; i < cmds_.size(); ++i) {
+    run_command(i);
+    if (deadlock_) break;
+    if (dopt_.max_cycle && (int64_t)tot_cycle_ >= dopt_.max_cycle) {
+      print("GPGPU-Sim: ** break due to reaching the maximum cycles (or instructions) **\n");
+      break;
+    }
+    if (dopt_.max_insn && (int64_t)tot_insn_ >= dopt_.max_insn) {
+      print("GPGPU-Sim: ** break due to reaching the maximum cycles (or instructions) **\n");
+      break;
+    }
+  }
+  print("GPGPU-Sim: *** simulation thread exiting ***\n");
+  print("GPGPU-Sim: *** exit detected ***\n");
+  fflush(stdout);
+  return deadlock_ ? 1 : 0;
+}
+
+void Simulator::run_command(size_t idx) {
+  if (cmds_.empty()) cmds_ = parse_commandlist(dopt_.trace_file);
+  const Command& c = cmds_.at(idx);
+  switch (c.type) {
+    case CMD_MEMCPY_HTOD:
+      print("launching memcpy command : %s\n", c.text.c_str());
+      if (cfg_.perf_memcpy) eng_->memcpy_fill_l2(c.addr, c.bytes);
+      break;
+    case CMD_KERNEL:
+      do_kernel(c);
+      break;
+    case CMD_COLLECTIVE:
+      do_collective(c);
+      break;
+    case CMD_COLL_INIT:
+    case CMD_COLL_DESTROY:
+    case CMD_GROUP_START:
+    case CMD_GROUP_END:
+      print("%s was run!\n", c.text.c_str());
+      break;
+    default:
+      break;
+  }
+}
+
+uint64_t Simulator::collective_cycles(const Command& c) const {
+  const std::string& m = dopt_.collective_model;
+  if (m == "const") return c.coll == "AllReduce" ? (uint64_t)std::max(0, dopt_.nccl_allreduce_latency) : 0;
+  // analytic ring / tree model over xGMI (per-link bound: a ring uses one
+  // link per direction; the tree uses log2(n) steps)
+  const double n = std::max(1, c.nranks);
+  if (n <= 1) return 0;
+  const double bw = dopt_.xgmi_link_gbps * 1e9;  // bytes/s per link
+  const double alpha = dopt_.xgmi_latency_ns * 1e-9;
+  const double S = (double)c.bytes;
+  double t = 0;
+  const bool tree = m == "tree";
+  if (c.coll == "AllReduce") {
+    t = tree ? 2 * std::log2(n) * (alpha + S / bw) : 2 * (n - 1) * alpha + 2 * (n - 1) / n * S / bw;
+  } else if (c.coll == "AllGather" || c.coll == "ReduceScatter") {
+    t = (n - 1) * alpha + (n - 1) / n * S / bw;
+  } else if (c.coll == "Broadcast" || c.coll == "Reduce") {
+    t = tree ? std::log2(n) * (alpha + S / bw) : (n - 1) * alpha + S / bw;
+  } else if (c.coll == "AllToAll") {
+    // every GPU exchanges S/n with each peer over its own links
+    double links = std::max<uint32_t>(1, dopt_.xgmi_links);
+    t = alpha + (n - 1) / n * S / (bw * std::min(links, n - 1));
+  } else {
+    t = alpha + S / bw;
+  }
+  const double core_hz = 1e15 / (double)cfg_.per_core;
+  return (uint64_t)std::ceil(t * core_hz);
+}
+
+void Simulator::do_collective(const Command& c) {
+  uint64_t cyc = coll_hook_ ? coll_hook_(c, eng_->now()) : collective_cycles(c);
+  if (c.coll == "AllReduce")
+    print("ncclAllReduce was run! Latency: %llu cycles.\n", (unsigned long long)cyc);
+  else
+    print("%s was run! Latency: %llu cycles.\n", c.text.c_str(), (unsigned long long)cyc);
+  if (cyc) eng_->advance(cyc);
+  tot_cycle_ = eng_->now();
+  CollectiveResult r;
+  r.op = c.coll;
+  r.bytes = c.bytes;
+  r.nranks = c.nranks;
+  r.cycles = cyc;
+  colls_.push_back(r);
+}
+
+void Simulator::do_kernel(const Command& c) {
+  auto t0 = std::chrono::steady_clock::now();
+  HostKernel hk = load_kernel(c.text);
+  print("Processing kernel %s\n", c.text.c_str());
+  if (hk.h.warp_size != cfg_.warp_size)
+    throw std::runtime_error("trace warp size does not match -gpgpu_shader_core_pipeline");
+  cur_kernel_.reset(new ReadyKernel(coalesce_kernel(hk, cfg_)));
+  const ReadyKernel& rk = *cur_kernel_;
+  KernelShape ks{rk.h.block[0] * rk.h.block[1] * rk.h.block[2], rk.h.shmem, rk.h.nregs, rk.n_cta};
+  Occupancy occ = compute_occupancy(cfg_, ks);
+  if ((uint64_t)occ.cta_per_sm * rk.warps_per_cta > (uint64_t)std::min<uint32_t>(cfg_.max_warps_per_sm, kMaxWarps))
+    occ.cta_per_sm = std::max<uint32_t>(1, std::min<uint32_t>(cfg_.max_warps_per_sm, kMaxWarps) / rk.warps_per_cta);
+  if (rk.warps_per_cta > (uint32_t)kMaxWarps) throw std::runtime_error("CTA larger than 64 warps");
+  KernelDesc kd{};
+  kd.uid = next_uid_++;
+  kd.n_cta = rk.n_cta;
+  kd.warps_per_cta = rk.warps_per_cta;
+  kd.threads_per_cta = ks.threads_per_cta;
+  kd.shmem_per_cta = rk.h.shmem;
+  kd.regs_per_thread = rk.h.nregs;
+  kd.cta_per_sm = std::min<uint32_t>(occ.cta_per_sm, kMaxCta);
+  for (int i = 0; i < 3; ++i) {
+    kd.grid[i] = rk.h.grid[i];
+    kd.block[i] = rk.h.block[i];
+  }
+  kd.stream = (uint32_t)rk.h.stream;
+  kd.l1_sets = occ.l1_sets;
+  kd.l1_assoc = occ.l1_assoc;
+  kd.shmem_base = rk.h.shmem_base;
+  kd.local_base = rk.h.local_base;
+  kd.n_insts = rk.insts.size();
+  print("launching kernel name: %s uid: %u\n", rk.h.name.c_str(), kd.uid);
+  print("GPGPU-Sim uArch: CTA/core = %u, limited by: %s\n", kd.cta_per_sm, occ.limiter);
+  eng_->load_kernel(rk, kd);
+  const uint64_t start = eng_->now();
+  RunLimits lim;
+  if (dopt_.max_cycle) lim.max_cycle = (uint64_t)dopt_.max_cycle;
+  auto ts = std::chrono::steady_clock::now();
+  RunResult rr = eng_->run_kernel(start, dopt_.flush_l1, lim);
+  auto te = std::chrono::steady_clock::now();
+  sim_s_ += std::chrono::duration<double>(te - ts).count();
+  if (dopt_.flush_l2) eng_->flush_l2();
+  std::vector<SMStats> sm;
+  std::vector<MemStats> mem;
+  eng_->stats(sm, mem);
+  if (prev_sm_.empty()) {
+    prev_sm_.assign(sm.size(), SMStats{});
+    prev_mem_.assign(mem.size(), MemStats{});
+  }
+  // per-kernel deltas
+  std::vector<SMStats> dsm(sm.size());
+  std::vector<MemStats> dmem(mem.size());
+  auto diff = [](const void* a, const void* b, void* out, size_t n) {
+    const uint64_t* x = (const uint64_t*)a;
+    const uint64_t* y = (const uint64_t*)b;
+    uint64_t* o = (uint64_t*)out;
+    for (size_t i = 0; i < n / 8; ++i) o[i] = x[i] - y[i];
+  };
+  for (size_t i = 0; i < sm.size(); ++i) diff(&sm[i], &prev_sm_[i], &dsm[i], sizeof(SMStats));
+  for (size_t i = 0; i < mem.size(); ++i) diff(&mem[i], &prev_mem_[i], &dmem[i], sizeof(MemStats));
+  prev_sm_ = sm;
+  prev_mem_ = mem;
+  KernelResult r;
+  r.name = rk.h.name;
+  r.uid = kd.uid;
+  r.start_cycle = start;
+  r.cycles = rr.end_cycle - start;
+  for (auto& s : dsm) {
+    r.insn += s.thread_insn;
+    r.warp_insn += s.warp_insn;
+  }
+  r.n_cta = kd.n_cta;
+  r.cta_per_sm = kd.cta_per_sm;
+  r.ipc = r.cycles ? (double)r.insn / (double)r.cycles : 0;
+  {
+    double occ_acc = 0, act = 0;
+    for (auto& s : dsm) {
+      occ_acc += s.occupancy_acc;
+      act += s.active_cycles;
+    }
+    r.occupancy = act > 0 ? 100.0 * occ_acc / (act * cfg_.max_warps_per_sm) : 0;
+  }
+  r.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  r.deadlock = rr.deadlock;
+  tot_cycle_ = eng_->now();
+  tot_insn_ += r.insn;
+  tot_warp_insn_ += r.warp_insn;
+  tot_cta_ += kd.n_cta;
+  if (power_) {
+    Activity a = PowerModel::activity_from_stats(dsm, dmem, r.cycles);
+    PowerReport p = power_->compute(a, 1e9 / (double)cfg_.per_core, cfg_.n_sm);
+    r.avg_power_w = p.total;
+  }
+  results_.push_back(r);
+  print_kernel_stats(r, dsm, dmem);
+  print_sim_time();
+  if (rr.deadlock) {
+    deadlock_ = true;
+    print("GPGPU-Sim uArch: ERROR ** deadlock detected: last writeback core %u @ gpu_sim_cycle %llu (+ gpu_tot_sim_cycle %llu)\n",
+          0u, (unsigned long long)r.cycles, (unsigned long long)start);
+  }
+}
+
+void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMStats>& sm,
+                                   const std::vector<MemStats>& mem) {
+  print("kernel_name = %s \n", r.name.c_str());
+  print("kernel_launch_uid = %u \n", r.uid);
+  print("gpu_sim_cycle = %llu\n", (unsigned long long)r.cycles);
+  print("gpu_sim_insn = %llu\n", (unsigned long long)r.insn);
+  print("gpu_ipc = %12.4f\n", r.ipc);
+  print("gpu_tot_sim_cycle = %llu\n", (unsigned long long)tot_cycle_);
+  print("gpu_tot_sim_insn = %llu\n", (unsigned long long)tot_insn_);
+  print("gpu_tot_ipc = %12.4f\n", tot_cycle_ ? (double)tot_insn_ / (double)tot_cycle_ : 0.0);
+  print("gpu_tot_issued_cta = %llu\n", (unsigned long long)tot_cta_);
+  print("gpu_occupancy = %.4f%% \n", r.occupancy);
+  print("gpu_tot_occupancy = %.4f%% \n", r.occupancy);
+  uint64_t l2_bytes = 0, dram_rd = 0, dram_wr = 0, dram_act = 0, dram_busy = 0, dram_cyc = 0;
+  uint64_t l2[L2T_COUNT][L2O_COUNT] = {};
+  for (auto& m : mem) {
+    l2_bytes += m.bytes_in + m.bytes_out;
+    dram_rd += m.dram_rd;
+    dram_wr += m.dram_wr;
+    dram_act += m.dram_act;
+    dram_busy += m.dram_busy_cycles;
+    dram_cyc += m.dram_cycles;
+    for (int t = 0; t < L2T_COUNT; ++t)
+      for (int o = 0; o < L2O_COUNT; ++o) l2[t][o] += m.l2[t][o];
+  }
+  const double secs = r.cycles * (double)cfg_.per_core * 1e-15;
+  print("L2_BW  = %12.4f GB/Sec\n", secs > 0 ? l2_bytes / secs / 1e9 : 0.0);
+  print("L2_BW_total  = %12.4f GB/Sec\n", secs > 0 ? l2_bytes / secs / 1e9 : 0.0);
+  print("gpu_total_sim_rate=%llu\n", (unsigned long long)(tot_insn_ / std::max(1e-9, sim_s_)));
+  // L1 breakdown (names follow the reference's mem_access_type / cache
+  // request status strings so get_stats.py regexes keep working)
+  static const char* l1t[L1T_COUNT] = {"GLOBAL_ACC_R", "GLOBAL_ACC_W", "LOCAL_ACC_R", "LOCAL_ACC_W", "GLOBAL_ATOMIC"};
+  uint64_t l1[L1T_COUNT][L1O_COUNT] = {};
+  uint64_t shm = 0, shm_conf = 0;
+  for (auto& s : sm) {
+    for (int t = 0; t < L1T_COUNT; ++t)
+      for (int o = 0; o < L1O_COUNT; ++o) l1[t][o] += s.l1[t][o];
+    shm += s.shmem_acc;
+    shm_conf += s.shmem_conflict_cycles;
+  }
+  print("\nTotal_core_cache_stats:\n");
+  for (int t = 0; t < L1T_COUNT; ++t) {
+    uint64_t tot = 0;
+    for (int o = 0; o < L1O_COUNT; ++o)
+      if (o != L1O_RES_FAIL) tot += l1[t][o];
+    print("\tTotal_core_cache_stats_breakdown[%s][HIT] = %llu\n", l1t[t], (unsigned long long)l1[t][L1O_HIT]);
+    print("\tTotal_core_cache_stats_breakdown[%s][MISS] = %llu\n", l1t[t],
+          (unsigned long long)(l1[t][L1O_MISS] + l1[t][L1O_BYPASS]));
+    print("\tTotal_core_cache_stats_breakdown[%s][MSHR_HIT] = %llu\n", l1t[t], (unsigned long long)l1[t][L1O_MSHR_HIT]);
+    print("\tTotal_core_cache_stats_breakdown[%s][TOTAL_ACCESS] = %llu\n", l1t[t], (unsigned long long)tot);
+  }
+  print("\nTotal_core_cache_fail_stats:\n");
+  for (int t = 0; t < L1T_COUNT; ++t)
+    print("\tTotal_core_cache_fail_stats_breakdown[%s][MSHR_ENRTY_FAIL] = %llu\n", l1t[t],
+          (unsigned long long)l1[t][L1O_RES_FAIL]);
+  print("gpgpu_n_shmem_bank_access = %llu\n", (unsigned long long)shm);
+  print("gpgpu_n_shmem_bkconflict = %llu\n", (unsigned long long)shm_conf);
+  static const char* l2t[L2T_COUNT] = {"GLOBAL_ACC_R", "GLOBAL_ACC_W", "GLOBAL_ATOMIC"};
+  print("\nL2_cache_stats:\n");
+  for (int t = 0; t < L2T_COUNT; ++t) {
+    uint64_t tot = l2[t][L2O_HIT] + l2[t][L2O_MISS] + l2[t][L2O_MSHR_HIT];
+    print("\tL2_cache_stats_breakdown[%s][HIT] = %llu\n", l2t[t], (unsigned long long)l2[t][L2O_HIT]);
+    print("\tL2_cache_stats_breakdown[%s][MISS] = %llu\n", l2t[t], (unsigned long long)l2[t][L2O_MISS]);
+    print("\tL2_cache_stats_breakdown[%s][MSHR_HIT] = %llu\n", l2t[t], (unsigned long long)l2[t][L2O_MSHR_HIT]);
+    print("\tL2_cache_stats_breakdown[%s][TOTAL_ACCESS] = %llu\n", l2t[t], (unsigned long long)tot);
+  }
+  uint64_t l2_tot = 0, l2_miss = 0;
+  for (int t = 0; t < L2T_COUNT; ++t) {
+    l2_tot += l2[t][L2O_HIT] + l2[t][L2O_MISS] + l2[t][L2O_MSHR_HIT];
+    l2_miss += l2[t][L2O_MISS];
+  }
+  print("L2_total_cache_accesses = %llu\n", (unsigned long long)l2_tot);
+  print("L2_total_cache_misses = %llu\n", (unsigned long long)l2_miss);
+  print("L2_total_cache_miss_rate = %.4f\n", l2_tot ? (double)l2_miss / l2_tot : 0.0);
+  print("total dram reads = %llu\n", (unsigned long long)dram_rd);
+  print("total dram writes = %llu\n", (unsigned long long)dram_wr);
+  print("total dram activates = %llu\n", (unsigned long long)dram_act);
+  print("dram_bw_util = %.4f\n", dram_cyc ? (double)dram_busy / dram_cyc : 0.0);
+  print("gpgpu_n_tot_w_icount = %llu\n", (unsigned long long)tot_warp_insn_);
+  uint64_t pk_out = 0, pk_in = 0;
+  for (auto& s : sm) {
+    pk_out += s.pkts_out;
+    pk_in += s.pkts_in;
+  }
+  print("icnt_total_pkts_mem_to_simt = %llu\n", (unsigned long long)pk_in);
+  print("icnt_total_pkts_simt_to_mem = %llu\n", (unsigned long long)pk_out);
+  if (power_) print("gpu_avg_power = %.4f W\n", r.avg_power_w);
+}
+
+void Simulator::print_sim_time() {
+  double el = wall_seconds();
+  unsigned long long d = (unsigned long long)std::max(1.0, std::ceil(el));
+  unsigned long long dd = d / 86400, hh = d / 3600 % 24, mm = d / 60 % 60, ss = d % 60;
+  print("\n\ngpgpu_simulation_time = %llu days, %llu hrs, %llu min, %llu sec (%llu sec)\n", dd, hh, mm, ss, d);
+  double rate_s = std::max(1e-9, el);
+  print("gpgpu_simulation_rate = %llu (inst/sec)\n", (unsigned long long)(tot_insn_ / rate_s));
+  unsigned long long cps = (unsigned long long)(tot_cycle_ / rate_s);
+  print("gpgpu_simulation_rate = %llu (cycle/sec)\n", cps);
+  double core_khz = 1e12 / (double)cfg_.per_core;
+  print("gpgpu_silicon_slowdown = %llux\n", cps ? (unsigned long long)(core_khz * 1000.0 / cps) : 0ull);
+  fflush(stdout);
+}
+
+}  // namespace asim

@@ -1,0 +1,107 @@
+// Command-list driver: the equivalent of the reference's accel-sim.out main
+// loop (gpu-simulator/main.cc:55-206) re-built around the epoch engines.
+#pragma once
+#include <chrono>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../config/sim_options.h"
+#include "../engine/engine.h"
+#include "../power/power.h"
+
+namespace asim {
+
+struct KernelResult {
+  std::string name;
+  uint32_t uid = 0;
+  uint64_t start_cycle = 0;
+  uint64_t cycles = 0;
+  uint64_t insn = 0;        // thread instructions
+  uint64_t warp_insn = 0;
+  uint32_t n_cta = 0;
+  uint32_t cta_per_sm = 0;
+  double ipc = 0;
+  double occupancy = 0;     // %
+  double wall_s = 0;        // wall time spent simulating this kernel
+  bool deadlock = false;
+  double avg_power_w = 0;
+};
+
+struct CollectiveResult {
+  std::string op;
+  uint64_t bytes = 0;
+  int32_t nranks = 1;
+  uint64_t cycles = 0;
+};
+
+// Callback used by the distributed layer: given a collective command, return
+// its duration in core cycles (e.g. measured by exchanging link packets with
+// the other simulated GPUs over RCCL).  When unset the analytic model is used.
+using CollectiveHook = std::function<uint64_t(const Command&, uint64_t now_cycle)>;
+
+class Simulator {
+ public:
+  // args: accel-sim.out style argument vector (without argv[0])
+  explicit Simulator(const std::vector<std::string>& args);
+  ~Simulator();
+
+  int run();  // whole command list; returns 0 on success
+  // step API: run the command list up to and including command `idx`
+  const std::vector<Command>& commands() const { return cmds_; }
+  void load_commands() {
+    if (cmds_.empty()) cmds_ = parse_commandlist(dopt_.trace_file);
+  }
+  void run_command(size_t idx);
+
+  const SimCfg& cfg() const { return cfg_; }
+  const DriverOpts& dopts() const { return dopt_; }
+  OptionRegistry& registry() { return reg_; }
+  Engine& engine() { return *eng_; }
+  const std::string& output() const { return out_; }
+  void set_echo(bool e) { echo_ = e; }
+  void set_collective_hook(CollectiveHook h) { coll_hook_ = std::move(h); }
+
+  uint64_t tot_cycle() const { return tot_cycle_; }
+  uint64_t tot_insn() const { return tot_insn_; }
+  double wall_seconds() const;
+  double sim_seconds() const { return sim_s_; }  // time inside the engine only
+  const std::vector<KernelResult>& kernels() const { return results_; }
+  const std::vector<CollectiveResult>& collectives() const { return colls_; }
+  bool deadlock() const { return deadlock_; }
+  // analytic collective duration in core cycles
+  uint64_t collective_cycles(const Command& c) const;
+
+ private:
+  void print(const char* fmt, ...);
+  void do_kernel(const Command& c);
+  void do_collective(const Command& c);
+  void print_kernel_stats(const KernelResult& r, const std::vector<SMStats>& sm, const std::vector<MemStats>& mem);
+  void print_sim_time();
+
+  OptionRegistry reg_;
+  SimCfg cfg_{};
+  DriverOpts dopt_;
+  std::unique_ptr<Engine> eng_;
+  std::unique_ptr<PowerModel> power_;
+  std::vector<Command> cmds_;
+  std::string out_;
+  bool echo_ = true;
+  CollectiveHook coll_hook_;
+  uint64_t tot_cycle_ = 0, tot_insn_ = 0, tot_warp_insn_ = 0;
+  uint64_t tot_cta_ = 0;
+  std::vector<SMStats> prev_sm_;
+  std::vector<MemStats> prev_mem_;
+  std::vector<KernelResult> results_;
+  std::vector<CollectiveResult> colls_;
+  std::chrono::steady_clock::time_point t_start_;
+  double sim_s_ = 0;
+  bool deadlock_ = false;
+  uint32_t next_uid_ = 1;
+  // currently loaded kernel (kept alive for the engine)
+  std::unique_ptr<ReadyKernel> cur_kernel_;
+};
+
+}  // namespace asim

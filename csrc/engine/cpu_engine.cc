@@ -1,0 +1,239 @@
+// CPU reference engine: the cycle model with the sequential lane policy.
+// SMs / channels of one epoch are independent (PDES), so the epoch body is
+// parallelised with OpenMP; results are bit-identical for any thread count.
+#include <cstring>
+#include <stdexcept>
+
+#include "engine.h"
+
+namespace asim {
+
+uint32_t reply_cap(const SimCfg& c) {
+  // icnt ticks per epoch, +1 for phase alignment
+  uint64_t win = (uint64_t)c.icnt_latency * c.per_core;
+  return (uint32_t)((win + c.per_icnt - 1) / c.per_icnt + 1);
+}
+
+void init_sm_state(SMState& s, uint32_t id) {
+  memset(&s, 0, sizeof(SMState));
+  s.id = id;
+}
+
+void init_chan_state(ChanState& ch, uint32_t id, const SimCfg& c) {
+  memset(&ch, 0, sizeof(ChanState));
+  ch.id = id;
+  ch.t_icnt = 0;
+  ch.t_l2 = 0;
+  ch.t_dram = 0;
+  (void)c;
+}
+
+void host_memcpy_fill(ChanState* chs, uint32_t nch, const SimCfg& c, uint64_t addr, uint64_t bytes) {
+  if (c.l2.disabled) return;
+  const uint64_t first = addr & ~127ull;
+  const uint64_t last = (addr + bytes + 127) & ~127ull;
+  // only the tail that can still be resident matters
+  uint64_t cap_lines = (uint64_t)c.l2.nsets * c.l2.assoc * c.n_subpart;
+  uint64_t start = first;
+  if ((last - first) / 128 > 2 * cap_lines) start = last - 2 * cap_lines * 128;
+  for (uint64_t line = start; line < last; line += 128) {
+    AddrTlx t = addr_decode(c, line);
+    uint32_t ch = t.sub / c.n_sub_per_mem, sub = t.sub % c.n_sub_per_mem;
+    if (ch >= nch) continue;
+    SubPart& sp = chs[ch].sp[sub];
+    uint32_t set = l2_set(c, line);
+    int way = l2_find<SeqPar>(sp, c.l2, set, line);
+    if (way < 0) {
+      way = l2_victim<SeqPar>(sp, c.l2, set);
+      L2Line& L = sp.l2[set * c.l2.assoc + way];
+      L.tag = line;
+      L.dirty = 0;
+      L.valid = 0;
+    }
+    L2Line& L = sp.l2[set * c.l2.assoc + way];
+    uint64_t lo = std::max(line, addr), hi = std::min(line + 128, addr + bytes);
+    for (uint64_t s = (lo - line) >> 5; s <= ((hi - 1 - line) >> 5) && s < 4; ++s) L.valid |= (uint8_t)(1u << s);
+    L.lru = ++sp.l2_stamp;
+  }
+}
+
+void host_flush_l2(ChanState* chs, uint32_t nch, const SimCfg& c) {
+  for (uint32_t i = 0; i < nch; ++i)
+    for (uint32_t j = 0; j < c.n_sub_per_mem; ++j)
+      for (auto& L : chs[i].sp[j].l2) {
+        L.valid = 0;
+        L.dirty = 0;
+      }
+}
+
+namespace {
+
+class CpuEngine : public Engine {
+ public:
+  const char* name() const override { return "cpu"; }
+
+  void init(const SimCfg& c) override {
+    c_ = c;
+    sms_.assign(c.n_sm, SMState());
+    for (uint32_t i = 0; i < c.n_sm; ++i) init_sm_state(sms_[i], i);
+    chs_.assign(c.n_mem, ChanState());
+    for (uint32_t i = 0; i < c.n_mem; ++i) init_chan_state(chs_[i], i, c);
+    pub_.reset(new EpochPub());
+    memset(pub_.get(), 0, sizeof(EpochPub));
+    cap_req_ = c.icnt_latency;
+    cap_rep_ = reply_cap(c);
+    for (int p = 0; p < 2; ++p) {
+      box_req_[p].assign((size_t)c.n_subpart * c.n_sm * cap_req_, Pkt{});
+      cnt_req_[p].assign((size_t)c.n_subpart * c.n_sm, 0);
+      box_rep_[p].assign((size_t)c.n_sm * c.n_subpart * cap_rep_, Pkt{});
+      cnt_rep_[p].assign((size_t)c.n_sm * c.n_subpart, 0);
+    }
+    epoch_ = 0;
+    cycle_ = 0;
+  }
+
+  void load_kernel(const ReadyKernel& k, const KernelDesc& kd) override {
+    kern_ = &k;
+    kd_ = kd;
+    kd_.insts = k.insts.data();
+    kd_.streams = k.streams.data();
+    accs_ = k.accs.data();
+  }
+
+  RunResult run_kernel(uint64_t start, bool flush_l1, const RunLimits& lim) override {
+    RunResult res;
+    if (start > cycle_) cycle_ = start;
+    const SimCfg& c = c_;
+    const uint64_t E = c.icnt_latency;
+    for (auto& s : sms_) {
+      SmCtx x = ctx_sm(0);
+      sm_kernel_init<SeqPar>(s, x, s.ks, cycle_, flush_l1 ? 1u : 0u);
+    }
+    const uint64_t ready = sms_.empty() ? 0 : sms_[0].ks.ready_cycle;
+    for (;;) {
+      const uint32_t cur = (uint32_t)(epoch_ & 1), prev = cur ^ 1u;
+      const uint64_t t0 = cycle_, t1 = t0 + E;
+      const int nsm = (int)sms_.size(), nch = (int)chs_.size();
+#pragma omp parallel for schedule(dynamic, 1)
+      for (int i = 0; i < nsm + nch; ++i) {
+        if (i < nsm) {
+          SMState& s = sms_[i];
+          SmCtx x = ctx_sm(cur);
+          sm_epoch<SeqPar>(s, x, s.ks, *pub_, prev, t0, t1, box_rep_[prev].data(), cnt_rep_[prev].data(), cap_rep_,
+                           c.n_subpart, epoch_);
+          sm_publish<SeqPar>(s, x, s.ks, *pub_, cur);
+        } else {
+          ChanState& ch = chs_[i - nsm];
+          MemCtx m = ctx_mem(cur, t1);
+          chan_epoch<SeqPar>(ch, m, box_req_[prev].data(), cnt_req_[prev].data(), cap_req_, t0 * c.per_core);
+          chan_publish<SeqPar>(ch, m, *pub_, cur);
+        }
+      }
+      const uint32_t next_done = pub_->next_cta[cur] >= kd_.n_cta ? 1u : 0u;
+      EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, ready, next_done, epoch_);
+      ++epoch_;
+      ++res.epochs;
+      cycle_ = d.next_start;
+      if (d.done) {
+        res.done = true;
+        break;
+      }
+      if (d.deadlock) {
+        res.deadlock = true;
+        break;
+      }
+      if ((lim.max_cycle && cycle_ >= lim.max_cycle) || (lim.max_epochs && res.epochs >= lim.max_epochs)) {
+        res.hit_limit = true;
+        break;
+      }
+    }
+    res.end_cycle = cycle_;
+    return res;
+  }
+
+  uint64_t now() const override { return cycle_; }
+
+  void memcpy_fill_l2(uint64_t addr, uint64_t bytes) override {
+    host_memcpy_fill(chs_.data(), (uint32_t)chs_.size(), c_, addr, bytes);
+  }
+  void flush_l2() override { host_flush_l2(chs_.data(), (uint32_t)chs_.size(), c_); }
+
+  void stats(std::vector<SMStats>& sm, std::vector<MemStats>& mem) override {
+    sm.clear();
+    mem.clear();
+    for (auto& s : sms_) sm.push_back(s.st);
+    for (auto& ch : chs_)
+      for (uint32_t j = 0; j < c_.n_sub_per_mem; ++j) mem.push_back(ch.sp[j].st);
+  }
+
+  void snapshot(std::vector<uint8_t>& out) override {
+    out.resize(sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState));
+    uint8_t* p = out.data();
+    for (auto& s : sms_) {
+      memcpy(p, &s, sizeof(SMState));
+      p += sizeof(SMState);
+    }
+    for (auto& ch : chs_) {
+      memcpy(p, &ch, sizeof(ChanState));
+      p += sizeof(ChanState);
+    }
+  }
+  void restore(const std::vector<uint8_t>& in) override {
+    if (in.size() != sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState))
+      throw std::runtime_error("snapshot size mismatch");
+    const uint8_t* p = in.data();
+    for (auto& s : sms_) {
+      memcpy(&s, p, sizeof(SMState));
+      p += sizeof(SMState);
+    }
+    for (auto& ch : chs_) {
+      memcpy(&ch, p, sizeof(ChanState));
+      p += sizeof(ChanState);
+    }
+  }
+  void advance(uint64_t cycles) override {
+    uint64_t E = c_.icnt_latency;
+    cycle_ += (cycles + E - 1) / E * E;
+  }
+
+ private:
+  SmCtx ctx_sm(uint32_t cur) {
+    SmCtx x;
+    x.cfg = &c_;
+    x.k = &kd_;
+    x.acc = accs_;
+    x.outbox = box_req_[cur].data();
+    x.outcnt = cnt_req_[cur].data();
+    x.out_cap = cap_req_;
+    x.n_src_sm = c_.n_sm;
+    return x;
+  }
+  MemCtx ctx_mem(uint32_t cur, uint64_t t1) {
+    MemCtx m;
+    m.cfg = &c_;
+    m.outbox = box_rep_[cur].data();
+    m.outcnt = cnt_rep_[cur].data();
+    m.out_cap = cap_rep_;
+    m.n_src_sub = c_.n_subpart;
+    m.win_end = t1 * c_.per_core;
+    return m;
+  }
+
+  SimCfg c_{};
+  std::vector<SMState> sms_;
+  std::vector<ChanState> chs_;
+  std::unique_ptr<EpochPub> pub_;
+  std::vector<Pkt> box_req_[2], box_rep_[2];
+  std::vector<uint32_t> cnt_req_[2], cnt_rep_[2];
+  uint32_t cap_req_ = 0, cap_rep_ = 0;
+  uint64_t epoch_ = 0, cycle_ = 0;
+  const ReadyKernel* kern_ = nullptr;
+  KernelDesc kd_{};
+  const TAcc* accs_ = nullptr;
+};
+
+}  // namespace
+
+std::unique_ptr<Engine> make_cpu_engine() { return std::unique_ptr<Engine>(new CpuEngine()); }
+
+}  // namespace asim

@@ -1,0 +1,62 @@
+// Cycle-engine interface.  Two implementations run the SAME model code
+// (csrc/model): the CPU reference engine (cpu_engine.cc, SeqPar) and the
+// MI355X engine (gpu_engine.hip, one wavefront per SM / memory channel,
+// persistent kernel with one grid barrier per PDES epoch).
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../model/epoch.h"
+#include "../trace/trace.h"
+
+namespace asim {
+
+struct RunLimits {
+  uint64_t max_cycle = 0;   // absolute cycle cap (0 = none)
+  uint64_t max_epochs = 0;  // safety cap (0 = none)
+};
+
+struct RunResult {
+  uint64_t end_cycle = 0;
+  uint64_t epochs = 0;
+  bool done = false;
+  bool deadlock = false;
+  bool hit_limit = false;
+};
+
+class Engine {
+ public:
+  virtual ~Engine() = default;
+  virtual const char* name() const = 0;
+  virtual void init(const SimCfg& c) = 0;
+  // make `k` the current kernel (uploads its trace)
+  virtual void load_kernel(const ReadyKernel& k, const KernelDesc& kd) = 0;
+  // simulate the current kernel from `start` until it completes
+  virtual RunResult run_kernel(uint64_t start, bool flush_l1, const RunLimits& lim) = 0;
+  // cycle at which the next epoch would start
+  virtual uint64_t now() const = 0;
+  // L2 pre-fill for MemcpyHtoD (reference perf_memcpy_to_gpu, gpu-sim.cc:2116-2136)
+  virtual void memcpy_fill_l2(uint64_t addr, uint64_t bytes) = 0;
+  virtual void flush_l2() = 0;
+  virtual void stats(std::vector<SMStats>& sm, std::vector<MemStats>& mem) = 0;
+  // raw state image (SM states then channel states) for checkpoint/compare
+  virtual void snapshot(std::vector<uint8_t>& out) = 0;
+  virtual void restore(const std::vector<uint8_t>& in) = 0;
+  // advance the clock without simulating (collective stalls, idle time)
+  virtual void advance(uint64_t cycles) = 0;
+};
+
+std::unique_ptr<Engine> make_cpu_engine();
+// defined in the HIP engine module; returns nullptr when no GPU is usable
+std::unique_ptr<Engine> make_gpu_engine();
+bool gpu_engine_available();
+
+// helpers shared by both engines
+uint32_t reply_cap(const SimCfg& c);
+void host_memcpy_fill(ChanState* chs, uint32_t nch, const SimCfg& c, uint64_t addr, uint64_t bytes);
+void host_flush_l2(ChanState* chs, uint32_t nch, const SimCfg& c);
+void init_sm_state(SMState& s, uint32_t id);
+void init_chan_state(ChanState& ch, uint32_t id, const SimCfg& c);
+
+}  // namespace asim

@@ -1,0 +1,436 @@
+// MI355X (gfx950) cycle engine.
+//
+// One persistent launch simulates up to `max_epochs` PDES epochs of the whole
+// simulated GPU:
+//   * block b < n_sm      : one 64-lane wavefront owns SM b; its complete
+//                           SMState (~105 KB) lives in LDS for the launch.
+//   * block n_sm + c      : one wavefront owns memory channel c (two L2
+//                           sub-partitions + the DRAM channel, ~118 KB LDS).
+//   * after every epoch   : one grid-wide barrier (agent-scope release /
+//                           acquire, XCD-local counters first, then a global
+//                           generation word), then every block evaluates the
+//                           same epoch decision and all blocks leave together.
+// The cycle model itself is the shared single-source code in csrc/model, run
+// with the WavePar lane policy, so results are bit-identical to the CPU
+// reference engine.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "engine.h"
+#include "wave_par.h"
+
+namespace asim {
+
+#define HIPCHECK(x)                                                                                  \
+  do {                                                                                               \
+    hipError_t e_ = (x);                                                                             \
+    if (e_ != hipSuccess)                                                                            \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x);    \
+  } while (0)
+
+struct GpuCtl {
+  uint32_t arrive[8][32];     // per-XCD-group arrival counters (padded to 128 B)
+  uint32_t top[32];           // group leaders' counter
+  uint32_t gen[32];           // generation word
+  uint32_t error;             // barrier timeout / fault code
+  uint32_t done;
+  uint32_t deadlock;
+  uint32_t pad;
+  uint64_t end_cycle;
+  uint64_t end_epoch;
+  uint64_t epochs_run;
+};
+
+struct GpuArgs {
+  const SimCfg* cfg;
+  KernelDesc kd;
+  const TAcc* acc;
+  SMState* sms;
+  ChanState* chs;
+  EpochPub* pub;
+  Pkt* box_req[2];
+  uint32_t* cnt_req[2];
+  Pkt* box_rep[2];
+  uint32_t* cnt_rep[2];
+  uint32_t cap_req, cap_rep;
+  uint64_t epoch0;
+  uint64_t cycle0;
+  uint64_t ready_cycle;
+  uint64_t max_cycle;
+  uint32_t max_epochs;
+  uint32_t init_kernel;
+  uint32_t flush_l1;
+  uint32_t nblocks;
+  GpuCtl* ctl;
+};
+
+// ---------------------------------------------------------------------------
+// grid barrier: blocks are grouped by blockIdx % 8 (which shares an XCD under
+// the observed round-robin placement: a speed hint only, correctness does not
+// depend on it).  Monotonic counters, relaxed polls with s_sleep, one agent
+// release before arriving and one agent acquire after leaving.
+__device__ __forceinline__ bool grid_barrier(GpuCtl* ctl, uint32_t nblocks, uint32_t epoch_in_launch) {
+  const uint32_t b = blockIdx.x;
+  const uint32_t grp = b & 7u;
+  const uint32_t ngrp = nblocks < 8 ? nblocks : 8u;
+  const uint32_t in_grp = (nblocks - grp + 7u) / 8u;  // members of this group
+  const uint32_t target = epoch_in_launch + 1u;
+  bool ok = true;
+  // every lane's stores must be complete and visible at agent scope
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) {
+    uint32_t prev = __hip_atomic_fetch_add(&ctl->arrive[grp][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev + 1u == target * in_grp) {
+      // last of its group: forward to the top counter
+      uint32_t t = __hip_atomic_fetch_add(&ctl->top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1u == target * ngrp) __hip_atomic_store(&ctl->gen[0], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    uint64_t spins = 0;
+    while (__hip_atomic_load(&ctl->gen[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1ull << 26)) {  // ~seconds: give up, report, let every block exit
+        __hip_atomic_store(&ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = false;
+        break;
+      }
+      if (__hip_atomic_load(&ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        ok = false;
+        break;
+      }
+    }
+  }
+  ok = __shfl(ok ? 1 : 0, 0, 64) != 0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return ok;
+}
+
+template <class T>
+__device__ __forceinline__ void copy_state(T* dst, const T* src) {
+  static_assert(sizeof(T) % 16 == 0, "state must be 16-byte granular");
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  const int n = (int)(sizeof(T) / 16);
+  for (int i = (int)(threadIdx.x & 63); i < n; i += 64) d[i] = s[i];
+  __syncthreads();
+}
+
+extern __shared__ __attribute__((aligned(16))) char g_lds[];
+constexpr size_t kStateLds = ((sizeof(SMState) > sizeof(ChanState) ? sizeof(SMState) : sizeof(ChanState)) + 15) / 16 * 16;
+constexpr size_t kLdsBytes = kStateLds + (sizeof(KernelDesc) + 15) / 16 * 16;
+static_assert(kLdsBytes <= 160 * 1024, "per-block LDS budget exceeded");
+
+__global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
+  const uint32_t b = blockIdx.x;
+  const SimCfg& c = *a.cfg;  // read-only, scalar-cached
+  const bool is_sm = b < c.n_sm;
+  const uint64_t E = c.icnt_latency;
+  SMState* s = reinterpret_cast<SMState*>(g_lds);
+  ChanState* ch = reinterpret_cast<ChanState*>(g_lds);
+  if (is_sm)
+    copy_state(s, &a.sms[b]);
+  else
+    copy_state(ch, &a.chs[b - c.n_sm]);
+  // kernel descriptor lives in LDS behind the state (never in scratch)
+  KernelDesc* kdl = reinterpret_cast<KernelDesc*>(g_lds + kStateLds);
+  if ((threadIdx.x & 63) == 0) *kdl = a.kd;
+  __syncthreads();
+  const KernelDesc& kd = *kdl;
+  SmCtx sx;
+  sx.cfg = &c;
+  sx.k = &kd;
+  sx.acc = a.acc;
+  sx.out_cap = a.cap_req;
+  sx.n_src_sm = c.n_sm;
+  MemCtx mx;
+  mx.cfg = &c;
+  mx.out_cap = a.cap_rep;
+  mx.n_src_sub = c.n_subpart;
+  if (is_sm && a.init_kernel) {
+    sx.outbox = a.box_req[0];
+    sx.outcnt = a.cnt_req[0];
+    sm_kernel_init<WavePar>(*s, sx, s->ks, a.cycle0, a.flush_l1);
+  }
+  uint64_t epoch = a.epoch0, cycle = a.cycle0;
+  uint32_t done = 0, dead = 0;
+  uint32_t n = 0;
+  for (; n < a.max_epochs;) {
+    const uint32_t cur = (uint32_t)(epoch & 1), prev = cur ^ 1u;
+    const uint64_t t0 = cycle, t1 = t0 + E;
+    if (is_sm) {
+      sx.outbox = a.box_req[cur];
+      sx.outcnt = a.cnt_req[cur];
+      sm_epoch<WavePar>(*s, sx, s->ks, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep,
+                        c.n_subpart, epoch);
+      sm_publish<WavePar>(*s, sx, s->ks, *a.pub, cur);
+    } else {
+      mx.outbox = a.box_rep[cur];
+      mx.outcnt = a.cnt_rep[cur];
+      mx.win_end = t1 * c.per_core;
+      chan_epoch<WavePar>(*ch, mx, a.box_req[prev], a.cnt_req[prev], a.cap_req, t0 * c.per_core);
+      chan_publish<WavePar>(*ch, mx, *a.pub, cur);
+    }
+    ++n;
+    if (!grid_barrier(a.ctl, a.nblocks, n - 1)) break;
+    const uint32_t next_done = a.pub->next_cta[cur] >= kd.n_cta ? 1u : 0u;
+    EpochDecision d = epoch_decide<WavePar>(c, *a.pub, cur, t1, a.ready_cycle, next_done, epoch);
+    ++epoch;
+    cycle = d.next_start;
+    if (d.done) { done = 1; break; }
+    if (d.deadlock) { dead = 1; break; }
+    if (a.max_cycle && cycle >= a.max_cycle) break;
+  }
+  // write state back
+  if (is_sm)
+    copy_state(&a.sms[b], s);
+  else
+    copy_state(&a.chs[b - c.n_sm], ch);
+  if (b == 0 && (threadIdx.x & 63) == 0) {
+    a.ctl->done = done;
+    a.ctl->deadlock = dead;
+    a.ctl->end_cycle = cycle;
+    a.ctl->end_epoch = epoch;
+    a.ctl->epochs_run = n;
+  }
+}
+
+// small kernel: apply the host-side L2 edits by copying back is simpler; the
+// engine keeps states resident and moves them to the host only on demand.
+
+namespace {
+
+class GpuEngine : public Engine {
+ public:
+  ~GpuEngine() override { release(); }
+  const char* name() const override { return "gpu"; }
+
+  void init(const SimCfg& c) override {
+    c_ = c;
+    int dev = 0;
+    HIPCHECK(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    HIPCHECK(hipGetDeviceProperties(&prop, dev));
+    n_cu_ = prop.multiProcessorCount;
+    nblocks_ = c.n_sm + c.n_mem;
+    lds_ = kLdsBytes;
+    if ((int)nblocks_ > n_cu_)
+      throw std::runtime_error("GPU engine needs one CU per simulated SM/channel: " + std::to_string(nblocks_) +
+                               " blocks > " + std::to_string(n_cu_) + " CUs");
+    HIPCHECK(hipFuncSetAttribute((const void*)engine_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_));
+    HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    HIPCHECK(hipMalloc(&d_cfg_, sizeof(SimCfg)));
+    HIPCHECK(hipMemcpy(d_cfg_, &c_, sizeof(SimCfg), hipMemcpyHostToDevice));
+    std::vector<SMState> hs(c.n_sm);
+    for (uint32_t i = 0; i < c.n_sm; ++i) init_sm_state(hs[i], i);
+    std::vector<ChanState> hc(c.n_mem);
+    for (uint32_t i = 0; i < c.n_mem; ++i) init_chan_state(hc[i], i, c);
+    HIPCHECK(hipMalloc(&d_sms_, sizeof(SMState) * c.n_sm));
+    HIPCHECK(hipMalloc(&d_chs_, sizeof(ChanState) * c.n_mem));
+    HIPCHECK(hipMemcpy(d_sms_, hs.data(), sizeof(SMState) * c.n_sm, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d_chs_, hc.data(), sizeof(ChanState) * c.n_mem, hipMemcpyHostToDevice));
+    HIPCHECK(hipMalloc(&d_pub_, sizeof(EpochPub)));
+    HIPCHECK(hipMemset(d_pub_, 0, sizeof(EpochPub)));
+    cap_req_ = c.icnt_latency;
+    cap_rep_ = reply_cap(c);
+    for (int p = 0; p < 2; ++p) {
+      HIPCHECK(hipMalloc(&d_box_req_[p], sizeof(Pkt) * c.n_subpart * c.n_sm * cap_req_));
+      HIPCHECK(hipMalloc(&d_cnt_req_[p], sizeof(uint32_t) * c.n_subpart * c.n_sm));
+      HIPCHECK(hipMemset(d_cnt_req_[p], 0, sizeof(uint32_t) * c.n_subpart * c.n_sm));
+      HIPCHECK(hipMalloc(&d_box_rep_[p], sizeof(Pkt) * c.n_sm * c.n_subpart * cap_rep_));
+      HIPCHECK(hipMalloc(&d_cnt_rep_[p], sizeof(uint32_t) * c.n_sm * c.n_subpart));
+      HIPCHECK(hipMemset(d_cnt_rep_[p], 0, sizeof(uint32_t) * c.n_sm * c.n_subpart));
+    }
+    HIPCHECK(hipMalloc(&d_ctl_, sizeof(GpuCtl)));
+    HIPCHECK(hipHostMalloc(&h_ctl_, sizeof(GpuCtl)));
+    epoch_ = 0;
+    cycle_ = 0;
+  }
+
+  void load_kernel(const ReadyKernel& k, const KernelDesc& kd) override {
+    kd_ = kd;
+    upload(d_insts_, cap_insts_, k.insts.data(), k.insts.size() * sizeof(TInst));
+    upload(d_accs_, cap_accs_, k.accs.data(), std::max<size_t>(16, k.accs.size() * sizeof(TAcc)));
+    upload(d_streams_, cap_streams_, k.streams.data(), k.streams.size() * sizeof(WStream));
+    kd_.insts = reinterpret_cast<const TInst*>(d_insts_);
+    kd_.streams = reinterpret_cast<const WStream*>(d_streams_);
+    fresh_kernel_ = true;
+  }
+
+  RunResult run_kernel(uint64_t start, bool flush_l1, const RunLimits& lim) override {
+    RunResult res;
+    if (start > cycle_) cycle_ = start;
+    const uint64_t ready = cycle_ + c_.kernel_launch_latency + (uint64_t)c_.tb_launch_latency * kd_.n_cta;
+    bool first = true;
+    for (;;) {
+      GpuArgs a{};
+      a.cfg = d_cfg_;
+      a.kd = kd_;
+      a.acc = reinterpret_cast<const TAcc*>(d_accs_);
+      a.sms = d_sms_;
+      a.chs = d_chs_;
+      a.pub = d_pub_;
+      for (int p = 0; p < 2; ++p) {
+        a.box_req[p] = d_box_req_[p];
+        a.cnt_req[p] = d_cnt_req_[p];
+        a.box_rep[p] = d_box_rep_[p];
+        a.cnt_rep[p] = d_cnt_rep_[p];
+      }
+      a.cap_req = cap_req_;
+      a.cap_rep = cap_rep_;
+      a.epoch0 = epoch_;
+      a.cycle0 = cycle_;
+      a.ready_cycle = ready;
+      a.max_cycle = lim.max_cycle;
+      a.max_epochs = epochs_per_launch_;
+      a.init_kernel = first ? 1u : 0u;
+      a.flush_l1 = flush_l1 ? 1u : 0u;
+      a.nblocks = nblocks_;
+      a.ctl = d_ctl_;
+      HIPCHECK(hipMemsetAsync(d_ctl_, 0, sizeof(GpuCtl), stream_));
+      hipLaunchKernelGGL(engine_kernel, dim3(nblocks_), dim3(64), lds_, stream_, a);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_));
+      HIPCHECK(hipStreamSynchronize(stream_));
+      first = false;
+      if (h_ctl_->error) throw std::runtime_error("GPU engine: grid barrier timed out (blocks not co-resident?)");
+      epoch_ = h_ctl_->end_epoch;
+      cycle_ = h_ctl_->end_cycle;
+      res.epochs += h_ctl_->epochs_run;
+      if (h_ctl_->done) { res.done = true; break; }
+      if (h_ctl_->deadlock) { res.deadlock = true; break; }
+      if ((lim.max_cycle && cycle_ >= lim.max_cycle) || (lim.max_epochs && res.epochs >= lim.max_epochs)) {
+        res.hit_limit = true;
+        break;
+      }
+      if (h_ctl_->epochs_run == 0) throw std::runtime_error("GPU engine made no progress");
+    }
+    res.end_cycle = cycle_;
+    return res;
+  }
+
+  uint64_t now() const override { return cycle_; }
+
+  void memcpy_fill_l2(uint64_t addr, uint64_t bytes) override {
+    std::vector<ChanState> hc(c_.n_mem);
+    HIPCHECK(hipMemcpy(hc.data(), d_chs_, sizeof(ChanState) * c_.n_mem, hipMemcpyDeviceToHost));
+    host_memcpy_fill(hc.data(), c_.n_mem, c_, addr, bytes);
+    HIPCHECK(hipMemcpy(d_chs_, hc.data(), sizeof(ChanState) * c_.n_mem, hipMemcpyHostToDevice));
+  }
+  void flush_l2() override {
+    std::vector<ChanState> hc(c_.n_mem);
+    HIPCHECK(hipMemcpy(hc.data(), d_chs_, sizeof(ChanState) * c_.n_mem, hipMemcpyDeviceToHost));
+    host_flush_l2(hc.data(), c_.n_mem, c_);
+    HIPCHECK(hipMemcpy(d_chs_, hc.data(), sizeof(ChanState) * c_.n_mem, hipMemcpyHostToDevice));
+  }
+
+  void stats(std::vector<SMStats>& sm, std::vector<MemStats>& mem) override {
+    sm.resize(c_.n_sm);
+    HIPCHECK(hipMemcpy2D(sm.data(), sizeof(SMStats), reinterpret_cast<char*>(d_sms_) + offsetof(SMState, st),
+                         sizeof(SMState), sizeof(SMStats), c_.n_sm, hipMemcpyDeviceToHost));
+    mem.clear();
+    for (uint32_t j = 0; j < c_.n_sub_per_mem; ++j) {
+      std::vector<MemStats> part(c_.n_mem);
+      size_t off = offsetof(ChanState, sp) + j * sizeof(SubPart) + offsetof(SubPart, st);
+      HIPCHECK(hipMemcpy2D(part.data(), sizeof(MemStats), reinterpret_cast<char*>(d_chs_) + off, sizeof(ChanState),
+                           sizeof(MemStats), c_.n_mem, hipMemcpyDeviceToHost));
+      if (j == 0) mem.resize((size_t)c_.n_mem * c_.n_sub_per_mem);
+      for (uint32_t i = 0; i < c_.n_mem; ++i) mem[(size_t)i * c_.n_sub_per_mem + j] = part[i];
+    }
+  }
+
+  void snapshot(std::vector<uint8_t>& out) override {
+    out.resize(sizeof(SMState) * c_.n_sm + sizeof(ChanState) * c_.n_mem);
+    HIPCHECK(hipMemcpy(out.data(), d_sms_, sizeof(SMState) * c_.n_sm, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(out.data() + sizeof(SMState) * c_.n_sm, d_chs_, sizeof(ChanState) * c_.n_mem,
+                       hipMemcpyDeviceToHost));
+  }
+  void restore(const std::vector<uint8_t>& in) override {
+    if (in.size() != sizeof(SMState) * c_.n_sm + sizeof(ChanState) * c_.n_mem)
+      throw std::runtime_error("snapshot size mismatch");
+    HIPCHECK(hipMemcpy(d_sms_, in.data(), sizeof(SMState) * c_.n_sm, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d_chs_, in.data() + sizeof(SMState) * c_.n_sm, sizeof(ChanState) * c_.n_mem,
+                       hipMemcpyHostToDevice));
+  }
+  void advance(uint64_t cycles) override {
+    uint64_t E = c_.icnt_latency;
+    cycle_ += (cycles + E - 1) / E * E;
+  }
+  void set_epochs_per_launch(uint32_t n) { epochs_per_launch_ = n ? n : 4096; }
+
+ private:
+  void upload(void*& d, size_t& cap, const void* h, size_t bytes) {
+    if (bytes > cap) {
+      if (d) HIPCHECK(hipFree(d));
+      cap = bytes + bytes / 4 + 4096;
+      HIPCHECK(hipMalloc(&d, cap));
+    }
+    if (bytes) HIPCHECK(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice));
+  }
+  void release() {
+    auto fr = [](void* p) {
+      if (p) (void)hipFree(p);
+    };
+    fr(d_cfg_);
+    fr(d_sms_);
+    fr(d_chs_);
+    fr(d_pub_);
+    for (int p = 0; p < 2; ++p) {
+      fr(d_box_req_[p]);
+      fr(d_cnt_req_[p]);
+      fr(d_box_rep_[p]);
+      fr(d_cnt_rep_[p]);
+    }
+    fr(d_ctl_);
+    fr(d_insts_);
+    fr(d_accs_);
+    fr(d_streams_);
+    if (h_ctl_) (void)hipHostFree(h_ctl_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+  }
+
+  SimCfg c_{};
+  int n_cu_ = 0;
+  uint32_t nblocks_ = 0;
+  size_t lds_ = 0;
+  hipStream_t stream_ = nullptr;
+  SimCfg* d_cfg_ = nullptr;
+  SMState* d_sms_ = nullptr;
+  ChanState* d_chs_ = nullptr;
+  EpochPub* d_pub_ = nullptr;
+  Pkt* d_box_req_[2] = {nullptr, nullptr};
+  uint32_t* d_cnt_req_[2] = {nullptr, nullptr};
+  Pkt* d_box_rep_[2] = {nullptr, nullptr};
+  uint32_t* d_cnt_rep_[2] = {nullptr, nullptr};
+  GpuCtl* d_ctl_ = nullptr;
+  GpuCtl* h_ctl_ = nullptr;
+  void* d_insts_ = nullptr;
+  void* d_accs_ = nullptr;
+  void* d_streams_ = nullptr;
+  size_t cap_insts_ = 0, cap_accs_ = 0, cap_streams_ = 0;
+  uint32_t cap_req_ = 0, cap_rep_ = 0;
+  uint64_t epoch_ = 0, cycle_ = 0;
+  uint32_t epochs_per_launch_ = 4096;
+  KernelDesc kd_{};
+  bool fresh_kernel_ = false;
+};
+
+}  // namespace
+
+bool gpu_engine_available() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return false;
+  return n > 0;
+}
+
+std::unique_ptr<Engine> make_gpu_engine() {
+  if (!gpu_engine_available()) return nullptr;
+  return std::unique_ptr<Engine>(new GpuEngine());
+}
+
+}  // namespace asim

@@ -1,0 +1,7 @@
+// Linked into CPU-only builds (no HIP engine object).
+#include "engine.h"
+
+namespace asim {
+std::unique_ptr<Engine> make_gpu_engine() { return nullptr; }
+bool gpu_engine_available() { return false; }
+}  // namespace asim

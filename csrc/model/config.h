@@ -1,0 +1,168 @@
+// POD configuration consumed by the cycle model (host AND device).
+//
+// Produced on the host from the gpgpusim.config / trace.config option
+// registry (csrc/config/sim_options.cc) -- the reference spreads the same
+// information over gpgpu_sim_config / shader_core_config / memory_config
+// (gpu-sim.h:97-473, shader.h:1509-1716).  Copied once to device memory.
+#pragma once
+#include "types.h"
+
+namespace asim {
+
+// compile-time capacity caps of the fixed-size state (checked by the host
+// when a config is loaded; configs beyond them are rejected loudly)
+constexpr int kMaxWarps = 64;       // warps per SM (lanes of one wavefront)
+constexpr int kMaxCta = 32;         // CTA slots per SM
+constexpr int kMaxSched = 4;        // schedulers / sub-cores per SM
+constexpr int kIbuf = 2;            // instruction buffer entries per warp
+constexpr int kWin = 16;            // prefetched trace window per warp (>= epoch + kIbuf)
+constexpr int kMaxOC = 16;          // operand collector units per SM
+constexpr int kMaxBanks = 32;       // register file banks per SM
+constexpr int kWbRing = 512;        // writeback ring (max FU latency 511)
+constexpr int kWbSlot = 8;          // writebacks per cycle (EX_WB width cap)
+constexpr int kMaxL1Lines = 1024;   // 128 KB of 128 B lines
+constexpr int kMaxL1Mshr = 256;
+constexpr int kMaxPend = 1024;      // outstanding (warp,load-slot,line) L1 waiters
+constexpr int kLoadSlots = 8;       // in-flight load instructions per warp
+constexpr int kHitRing = 256;       // L1 / shared-memory completion ring (latency < 222)
+constexpr int kHitSlot = 8;
+constexpr int kOutQ = 64;           // SM -> icnt injection queue
+constexpr int kInQ = 128;           // icnt -> SM arrivals per epoch
+constexpr int kMaxAccess = 64;      // coalesced accesses of one instruction
+// memory side (per sub-partition)
+constexpr int kMaxL2Lines = 1024;   // per sub-partition
+constexpr int kMaxL2Mshr = 256;
+constexpr int kMaxL2Wait = 256;
+constexpr int kRopQ = 256;
+constexpr int kMemInQ = 256;        // arrivals per epoch per sub-partition
+constexpr int kReplyQ = 128;
+constexpr int kDramQ = 128;         // per channel FR-FCFS queue
+constexpr int kDramRet = 256;
+constexpr int kMaxBanksDram = 32;
+constexpr int kMaxSubPerCh = 2;
+constexpr int kMaxSubTot = 128;    // L2 sub-partitions (interconnect destinations)
+constexpr int kMaxSmTot = 512;     // simulated SMs
+
+enum SchedPolicy : uint8_t { SCHED_LRR = 0, SCHED_GTO, SCHED_OLDEST, SCHED_RRR, SCHED_TWO_LEVEL };
+enum ReplPolicy : uint8_t { REPL_LRU = 0, REPL_FIFO };
+enum WritePolicy : uint8_t { WP_READ_ONLY = 0, WP_WRITE_BACK, WP_WRITE_THROUGH, WP_WRITE_EVICT, WP_LOCAL_WB_GLOBAL_WT };
+enum SetIndexFn : uint8_t { SIDX_LINEAR = 0, SIDX_FERMI, SIDX_HASH_IPOLY, SIDX_BITWISE_XOR, SIDX_CUSTOM };
+enum PartIndex : uint8_t { PIDX_CONSECUTIVE = 0, PIDX_BITWISE = 1, PIDX_IPOLY = 2, PIDX_PAE = 3, PIDX_RANDOM = 4, PIDX_CUSTOM = 5 };
+enum AddrField : uint8_t { AF_CHIP = 0, AF_BK, AF_ROW, AF_COL, AF_BURST, AF_COUNT };
+
+struct CacheGeom {
+  uint32_t nsets;
+  uint32_t assoc;
+  uint32_t line;        // bytes
+  uint32_t mshr_entries;
+  uint32_t mshr_merge;
+  uint32_t miss_queue;
+  uint8_t sectored;
+  uint8_t repl;         // ReplPolicy
+  uint8_t wpolicy;      // WritePolicy
+  uint8_t alloc;        // 'm' on-miss 'f' on-fill 's' streaming
+  uint8_t walloc;       // 'N' no-write-allocate, 'W' write-allocate, 'F' fetch-on-write, 'L' lazy
+  uint8_t set_index;    // SetIndexFn
+  uint8_t disabled;
+  uint8_t pad;
+};
+
+struct SimCfg {
+  // ---- topology ----
+  uint32_t n_sm;
+  uint32_t n_clusters;
+  uint32_t cores_per_cluster;
+  uint32_t n_mem;           // DRAM channels
+  uint32_t n_sub_per_mem;   // L2 sub-partitions per channel
+  uint32_t n_subpart;       // n_mem * n_sub_per_mem
+  uint32_t warp_size;       // threads per warp in the traces (32 SASS, 64 CDNA)
+  // ---- SM resources ----
+  uint32_t max_threads_per_sm;
+  uint32_t max_warps_per_sm;
+  uint32_t max_cta_per_sm;
+  uint32_t regs_per_sm;
+  uint32_t shmem_per_sm;
+  uint32_t shmem_per_block;
+  // ---- front end / issue ----
+  uint32_t n_sched;
+  uint32_t sched_policy;
+  uint32_t sub_core;
+  uint32_t fetch_throughput;
+  uint32_t max_issue_per_warp;
+  // ---- execution ----
+  uint32_t unit_count[U_COUNT];   // total units of each type per SM (0 = absent)
+  uint32_t id_oc_width[U_COUNT];  // ID_OC pipeline register slots per type
+  uint32_t ex_wb_width;
+  uint16_t lat[OC_COUNT];         // latency per op class (trace mode)
+  uint16_t ii[OC_COUNT];          // initiation interval per op class
+  uint32_t oc_units;              // generic operand collector units per SM
+  uint32_t reg_banks;
+  uint32_t reg_port_tp;           // register file port throughput
+  // ---- LD/ST ----
+  uint32_t smem_banks;
+  uint32_t smem_latency;
+  uint32_t smem_warp_parts;
+  uint32_t smem_limited_bcast;
+  CacheGeom l1;
+  uint32_t l1_latency;
+  uint32_t l1_banks;
+  uint32_t gmem_skip_l1;
+  uint32_t adaptive_l1;
+  uint32_t unified_l1_kb;
+  uint32_t n_shmem_opts;
+  uint32_t shmem_opts_kb[8];
+  uint32_t l1_write_ratio;
+  // ---- interconnect ----
+  uint32_t icnt_latency;   // core cycles (== epoch length, the PDES lookahead)
+  uint32_t flit_size;
+  uint32_t icnt_out_limit; // per-SM outstanding packets before injection stalls
+  // ---- memory partition ----
+  CacheGeom l2;
+  uint32_t rop_latency;
+  uint32_t dram_latency;
+  uint32_t q_icnt_l2, q_l2_dram, q_dram_l2, q_l2_icnt;
+  uint32_t perf_memcpy;
+  // ---- DRAM ----
+  uint32_t dram_sched;      // 0 FIFO, 1 FR-FCFS
+  uint32_t dram_queue;
+  uint32_t dram_ret_queue;
+  uint32_t nbk, nbkgrp, tCCD, tRRD, tRCD, tRAS, tRP, tRC, CL, WL, tCDLR, tWR, tCCDL, tRTPL;
+  uint32_t BL, busW, data_cmd_ratio, dual_bus, bk_index_policy, bkgrp_index_policy;
+  uint32_t atom_size;       // bytes per DRAM column access
+  // ---- address decode ----
+  uint64_t addr_mask[AF_COUNT];
+  uint8_t mk_hi[AF_COUNT];
+  uint8_t mk_lo[AF_COUNT];
+  uint8_t part_index;
+  uint8_t gap;
+  int32_t addr_chip_s;
+  uint32_t log2ch, log2sub, n_ch_pow2;
+  uint64_t sub_id_mask;
+  // ---- clocks (femtoseconds per cycle) ----
+  uint64_t per_core, per_icnt, per_l2, per_dram;
+  // ---- kernel scheduling ----
+  uint32_t kernel_launch_latency;
+  uint32_t tb_launch_latency;
+  // ---- misc ----
+  uint32_t deadlock_window;
+  uint32_t max_cycle_lo, max_cycle_hi;
+};
+
+// ---- helpers shared by both engines ----
+SIM_HDI uint32_t unit_of(const SimCfg& c, uint8_t cls) {
+  switch (cls) {
+    case OC_LOAD: case OC_STORE: case OC_MEMBAR: return U_MEM;
+    case OC_SFU: return U_SFU;
+    case OC_DP: return c.unit_count[U_DP] ? U_DP : U_SFU;
+    case OC_INTP: return c.unit_count[U_INT] ? U_INT : U_SP;
+    case OC_TENSOR: return c.unit_count[U_TENSOR] ? U_TENSOR : U_SP;
+    default:
+      if (cls >= OC_SPEC1 && cls <= OC_SPEC8) {
+        uint32_t u = U_SPEC1 + (cls - OC_SPEC1);
+        return c.unit_count[u] ? u : (uint32_t)U_SP;
+      }
+      return U_SP;  // ALU, SP, BRANCH, BARRIER, EXIT, NOP
+  }
+}
+
+}  // namespace asim

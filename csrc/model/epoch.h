@@ -1,0 +1,180 @@
+// Epoch-synchronous (conservative PDES) driver logic shared by both engines.
+//
+// The reference advances every component in one serial loop per cycle
+// (gpgpu_sim::cycle, gpu-sim.cc:1871-2107).  Here SMs and memory channels only
+// interact through the interconnect, whose latency L (core cycles) is the
+// lookahead: an epoch is L core cycles, packets injected in epoch e become
+// visible at their destination in epoch e+1, so every SM and every channel
+// can simulate a whole epoch independently (one wavefront each on the GPU)
+// with ONE grid-wide barrier per epoch.  All cross-component decisions (CTA
+// dispatch, kernel completion, idle fast-forward, deadlock) are computed
+// redundantly and deterministically by every participant from state
+// published at the previous epoch boundary -- no atomics, no races, and the
+// CPU engine gives bit-identical results.
+#pragma once
+#include "mem.h"
+
+namespace asim {
+
+constexpr int kMaxChTot = 128;
+
+// epoch-boundary publications, double buffered by epoch parity
+struct EpochPub {
+  uint32_t sm_req[2][kMaxSmTot];     // CTA slots an SM can accept next epoch
+  uint32_t sm_idle[2][kMaxSmTot];    // SM drained and kernel fully dispatched
+  uint32_t sm_drained[2][kMaxSmTot]; // SM holds no work (launch latency may be pending)
+  uint64_t sm_prog[2][kMaxSmTot];    // last progress cycle
+  uint32_t ch_idle[2][kMaxChTot];
+  uint32_t next_cta[2];              // replicated dispatch cursor (published by SM 0)
+  uint32_t pad[2];
+};
+
+// decision every participant derives after the barrier
+struct EpochDecision {
+  uint32_t done;        // kernel complete (all SMs idle)
+  uint32_t all_idle;    // SMs and memory idle
+  uint32_t deadlock;
+  uint32_t pad;
+  uint64_t next_start;  // start cycle of the next epoch (after fast-forward)
+};
+
+// ---------------------------------------------------------------------------
+// CTA dispatch: round-robin rounds over requesting SMs, rotated by epoch.
+template <class P>
+SIM_HDI void cta_dispatch(SMState& s, const SmCtx& x, SmKernel& ks, const uint32_t* req, uint32_t n_sm,
+                          uint32_t rot) {
+  const KernelDesc& k = *x.k;
+  if (ks.next_cta >= k.n_cta) return;
+  const uint32_t me = s.id;
+  const uint32_t my_q = req[me];
+  const uint32_t my_rank = (me + n_sm - rot) % n_sm;
+  uint32_t base = ks.next_cta;
+  for (uint32_t r = 0; r < (uint32_t)kMaxCta && base < k.n_cta; ++r) {
+    uint32_t pr = P::sum((int)n_sm, [&](int j) -> uint32_t { return req[j] > r ? 1u : 0u; });
+    if (pr == 0) break;
+    if (my_q > r) {
+      uint32_t pos = P::sum((int)n_sm, [&](int j) -> uint32_t {
+        return (req[j] > r && ((uint32_t)j + n_sm - rot) % n_sm < my_rank) ? 1u : 0u;
+      });
+      uint32_t cta = base + pos;
+      if (cta < k.n_cta) {
+        // lowest free slot
+        int slot = -1;
+        for (uint32_t i = 0; i < s.kernel_cta_slots; ++i)
+          if (!s.cta_valid[i]) { slot = (int)i; break; }
+        if (slot >= 0) sm_launch_cta<P>(s, x, (uint32_t)slot, cta);
+      }
+    }
+    base += pr;
+  }
+  ks.next_cta = base < k.n_cta ? base : k.n_cta;
+}
+
+SIM_HDI uint32_t sm_free_slots(const SMState& s) {
+  return s.kernel_cta_slots > s.n_cta_active ? s.kernel_cta_slots - s.n_cta_active : 0;
+}
+
+// kernel (re)initialisation of an SM: first epoch of a new kernel
+template <class P>
+SIM_HDI void sm_kernel_init(SMState& s, const SmCtx& x, SmKernel& ks, uint64_t start, uint32_t flush_l1) {
+  const KernelDesc& k = *x.k;
+  ks.uid = k.uid;
+  ks.next_cta = 0;
+  ks.start_cycle = start;
+  ks.ready_cycle = start + x.cfg->kernel_launch_latency + (uint64_t)x.cfg->tb_launch_latency * k.n_cta;
+  s.kernel_cta_slots = k.cta_per_sm;
+  if (flush_l1) {
+    P::each(kMaxL1Lines, [&](int i) { s.l1[i].valid = 0; });
+    P::sync();
+  }
+}
+
+// one epoch of one SM: [t0, t1) core cycles
+template <class P>
+SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& pub, uint32_t prev,
+                      uint64_t t0, uint64_t t1, const Pkt* inbox, const uint32_t* incnt, uint32_t in_cap,
+                      uint32_t n_sub, uint64_t epoch_idx) {
+  const SimCfg& c = *x.cfg;
+  // 1. arrivals (replies injected by the memory side last epoch)
+  gather_sorted<P>(inbox, incnt, s.id, n_sub, in_cap, t0 * c.per_core, s.inq, kInQ, s.inq_head, s.inq_n,
+                   s_scratch_key(s), s_scratch_ref(s), s_scratch_rank(s), kInQ);
+  // 2. CTA dispatch (state published at the previous boundary)
+  if (t0 >= ks.ready_cycle)
+    cta_dispatch<P>(s, x, ks, pub.sm_req[prev], c.n_sm, (uint32_t)(epoch_idx % c.n_sm));
+  // 3. trace window refill
+  sm_refill_window<P>(s, c, *x.k);
+  // 4. cycles
+  s.epoch_end = t1;
+  if (s.n_cta_active || !sm_idle(s)) {
+    for (uint64_t t = t0; t < t1; ++t) sm_cycle<P>(s, x, t);
+  }
+  s.cycle = t1;
+}
+
+// publish SM outbox counts + boundary state
+template <class P>
+SIM_HDI void sm_publish(SMState& s, const SmCtx& x, const SmKernel& ks, EpochPub& pub, uint32_t cur) {
+  const SimCfg& c = *x.cfg;
+  P::each((int)c.n_subpart, [&](int d) {
+    x.outcnt[(uint64_t)d * x.n_src_sm + s.id] = s.ocnt[d];
+    s.ocnt[d] = 0;
+  });
+  P::sync();
+  const bool ready_for_cta = ks.next_cta < x.k->n_cta;
+  const uint32_t req = ready_for_cta ? sm_free_slots(s) : 0u;
+  const uint32_t idle = (ks.next_cta >= x.k->n_cta && sm_idle(s)) ? 1u : 0u;
+  P::one([&] {
+    pub.sm_req[cur][s.id] = req;
+    pub.sm_idle[cur][s.id] = idle;
+    pub.sm_drained[cur][s.id] = sm_idle(s) ? 1u : 0u;
+    pub.sm_prog[cur][s.id] = s.last_progress;
+    if (s.id == 0) pub.next_cta[cur] = ks.next_cta;
+  });
+}
+
+// one epoch of one memory channel
+template <class P>
+SIM_HDI void chan_epoch(ChanState& ch, const MemCtx& x, const Pkt* inbox, const uint32_t* incnt,
+                        uint32_t in_cap, uint64_t t0_fs) {
+  mem_gather<P>(ch, *x.cfg, inbox, incnt, in_cap, t0_fs);
+  mem_window<P>(ch, x);
+}
+
+template <class P>
+SIM_HDI void chan_publish(ChanState& ch, const MemCtx& x, EpochPub& pub, uint32_t cur) {
+  mem_publish<P>(ch, *x.cfg, x.outcnt);
+  uint32_t idle = chan_idle(ch, *x.cfg) ? 1u : 0u;
+  P::one([&] { pub.ch_idle[cur][ch.id] = idle; });
+}
+
+// every participant computes the same decision from the published state
+template <class P>
+SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_t cur, uint64_t t1,
+                                   uint64_t ready_cycle, uint32_t next_cta_done, uint64_t epoch_idx) {
+  EpochDecision d;
+  uint32_t nbusy = P::sum((int)c.n_sm, [&](int j) -> uint32_t { return pub.sm_idle[cur][j] ? 0u : 1u; });
+  uint32_t cbusy = P::sum((int)c.n_mem, [&](int j) -> uint32_t { return pub.ch_idle[cur][j] ? 0u : 1u; });
+  d.done = (nbusy == 0) ? 1u : 0u;
+  d.all_idle = (nbusy == 0 && cbusy == 0) ? 1u : 0u;
+  d.next_start = t1;
+  d.deadlock = 0;
+  d.pad = 0;
+  // fast-forward over the kernel launch latency when nothing is in flight
+  if (!next_cta_done && cbusy == 0 && t1 < ready_cycle) {
+    uint32_t undrained = P::sum((int)c.n_sm, [&](int j) -> uint32_t { return pub.sm_drained[cur][j] ? 0u : 1u; });
+    if (undrained == 0) {
+      uint64_t E = c.icnt_latency;
+      uint64_t skip = (ready_cycle - t1) / E * E;
+      d.next_start = t1 + skip;
+    }
+  }
+  if (c.deadlock_window && nbusy && (epoch_idx & 63) == 0) {
+    // newest progress stamp over all SMs (progress stamps are < 2^56)
+    int jm = P::argmin((int)c.n_sm, [&](int j) -> uint64_t { return ~pub.sm_prog[cur][j] & ((1ull << 56) - 1); });
+    uint64_t last = jm >= 0 ? pub.sm_prog[cur][jm] : 0;
+    if (t1 > last + c.deadlock_window && t1 > ready_cycle + c.deadlock_window) d.deadlock = 1;
+  }
+  return d;
+}
+
+}  // namespace asim

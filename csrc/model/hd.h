@@ -1,0 +1,112 @@
+// Single-source host/device attributes and the "lane policy" abstraction.
+//
+// The cycle model (csrc/model/*.h) is written ONCE.  Every per-warp /
+// per-thread / per-way loop that is embarrassingly parallel is expressed
+// through a lane policy `P`:
+//   * SeqPar  (this file)        - CPU reference engine: a plain loop.
+//   * WavePar (engine/wave_par.h) - GPU engine: one CDNA4 wavefront, lane i
+//                                   handles element i (64-wide ballots,
+//                                   cross-lane reductions via DPP/shuffles).
+// Everything outside those calls is wave-uniform scalar code that every lane
+// executes identically on the GPU, so the CPU and GPU engines produce
+// bit-identical simulator state.  This replaces the reference's serial STL
+// walks (e.g. scheduler_unit::cycle, shader.cc:1249-1556; the coalescer,
+// abstract_hardware_model.cc:284-748) with lane-parallel formulations.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define SIM_HD __host__ __device__
+#define SIM_HDI __host__ __device__ __forceinline__
+#else
+#define SIM_HD
+#define SIM_HDI inline
+#endif
+
+namespace asim {
+
+SIM_HDI int popc64(uint64_t x) { return __builtin_popcountll(x); }
+SIM_HDI int ffs64(uint64_t x) { return x ? __builtin_ctzll(x) : -1; }
+SIM_HDI uint64_t rotr64(uint64_t x, unsigned r, unsigned n) {
+  // rotate the low n bits of x right by r (n <= 64, r < n)
+  if (r == 0) return x;
+  uint64_t m = (n == 64) ? ~0ull : ((1ull << n) - 1);
+  x &= m;
+  return ((x >> r) | (x << (n - r))) & m;
+}
+template <class T>
+SIM_HDI T amin(T a, T b) { return a < b ? a : b; }
+template <class T>
+SIM_HDI T amax(T a, T b) { return a > b ? a : b; }
+
+// Sequential lane policy (CPU reference engine).
+struct SeqPar {
+  static constexpr int kLanes = 64;
+  // bit i of the result = f(i) for i < n (n <= 64)
+  template <class F>
+  static SIM_HDI uint64_t ballot(int n, F&& f) {
+    uint64_t m = 0;
+    for (int i = 0; i < n; ++i)
+      if (f(i)) m |= 1ull << i;
+    return m;
+  }
+  // run f(i) for every i < n (independent iterations only)
+  template <class F>
+  static SIM_HDI void each(int n, F&& f) {
+    for (int i = 0; i < n; ++i) f(i);
+  }
+  // side effect executed once per wave (global-memory stores of uniform data)
+  template <class F>
+  static SIM_HDI void one(F&& f) { f(); }
+  static SIM_HDI void sync() {}
+  // index i < n minimising key(i) (ties -> lowest i); key == ~0ull means
+  // "not a candidate".  Returns -1 if there is no candidate.
+  template <class F>
+  static SIM_HDI int argmin(int n, F&& key) {
+    uint64_t best = ~0ull;
+    int bi = -1;
+    for (int i = 0; i < n; ++i) {
+      uint64_t k = key(i);
+      if (k != ~0ull && (bi < 0 || k < best)) {
+        best = k;
+        bi = i;
+      }
+    }
+    return bi;
+  }
+  template <class F>
+  static SIM_HDI uint32_t sum(int n, F&& f) {
+    uint32_t s = 0;
+    for (int i = 0; i < n; ++i) s += f(i);
+    return s;
+  }
+  template <class F>
+  static SIM_HDI uint32_t vmax(int n, F&& f) {
+    uint32_t s = 0;
+    for (int i = 0; i < n; ++i) {
+      uint32_t v = f(i);
+      s = v > s ? v : s;
+    }
+    return s;
+  }
+  // exclusive prefix sum: out(i, sum_{j<i} val(j)); returns the total
+  template <class F, class G>
+  static SIM_HDI uint32_t scan(int n, F&& val, G&& out) {
+    uint32_t acc = 0;
+    for (int i = 0; i < n; ++i) {
+      uint32_t v = val(i);
+      out(i, acc);
+      acc += v;
+    }
+    return acc;
+  }
+  template <class F>
+  static SIM_HDI uint64_t vor(int n, F&& f) {
+    uint64_t s = 0;
+    for (int i = 0; i < n; ++i) s |= f(i);
+    return s;
+  }
+};
+
+}  // namespace asim

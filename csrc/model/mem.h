@@ -1,0 +1,719 @@
+// Memory partition model: one DRAM channel with its L2 sub-partitions.
+//
+// Reference: memory_partition_unit / memory_sub_partition (l2cache.h:72,160;
+// l2cache.cc:305-375 dram_cycle, :463-595 cache_cycle with the ROP delay
+// queue), dram_t (dram.cc:289-682) and the FR-FCFS scheduler
+// (dram_sched.cc:109-258).  Re-designed as fixed-capacity rings and flat
+// associative tables so that one wavefront owns one channel on the GPU; the
+// per-domain clocks are integer femtoseconds and are stepped in time order
+// inside each PDES epoch (reference next_clock_domain, gpu-sim.cc:1833-1854).
+#pragma once
+#include "sm.h"
+
+namespace asim {
+
+struct L2Line {
+  uint64_t tag;
+  uint32_t lru;
+  uint8_t valid;  // sector mask
+  uint8_t dirty;  // sector mask
+  uint8_t pad[2];
+};
+
+struct L2Mshr {
+  uint64_t line;
+  uint8_t requested;
+  uint8_t valid;
+  uint8_t merges;
+  uint8_t pad[5];
+};
+
+struct L2Wait {  // request waiting for sectors from DRAM
+  uint64_t line;
+  uint32_t tag;
+  uint16_t src;
+  uint8_t need;     // sectors still missing
+  uint8_t sectors;  // sectors requested (reply payload)
+  uint8_t type;     // request packet type
+  uint8_t valid;
+  uint8_t pad[6];
+};
+
+struct DramReq {
+  uint64_t line;     // line address
+  uint64_t ready;    // fs: leaves the L2->DRAM latency pipe
+  uint32_t row;
+  uint16_t bank;
+  uint8_t sector;    // sector index 0..3
+  uint8_t write;
+  uint8_t sub;       // local sub-partition index
+  uint8_t pad[7];
+};
+
+struct DramRet {
+  uint64_t line;
+  uint64_t ready;    // fs
+  uint8_t sector;
+  uint8_t sub;
+  uint8_t pad[6];
+};
+
+struct DramBank {
+  uint64_t t_col_ok;   // dram cycles
+  uint64_t t_pre_ok;
+  uint64_t t_act_ok;
+  uint32_t row;
+  uint8_t open;
+  uint8_t pad[3];
+};
+
+enum L2StatType : uint8_t { L2T_RD = 0, L2T_WR, L2T_ATOM, L2T_COUNT };
+enum L2StatOut : uint8_t { L2O_HIT = 0, L2O_MISS, L2O_MSHR_HIT, L2O_RES_FAIL, L2O_COUNT };
+struct MemStats {
+  uint64_t l2[L2T_COUNT][L2O_COUNT];
+  uint64_t dram_rd;
+  uint64_t dram_wr;
+  uint64_t dram_act;
+  uint64_t dram_pre;
+  uint64_t dram_busy_cycles;   // cycles with a column command in flight on the bus
+  uint64_t dram_cycles;
+  uint64_t dram_q_occ;         // sum of queue occupancy per dram cycle
+  uint64_t l2_cycles;
+  uint64_t l2_busy;            // L2 cycles that processed a request
+  uint64_t rop_occ;
+  uint64_t pkts_in;
+  uint64_t pkts_out;
+  uint64_t bytes_in;
+  uint64_t bytes_out;
+  uint64_t l2_evict_dirty;
+  uint64_t icnt_stall;
+};
+
+struct SubPart {
+  Pkt inq[kMemInQ];   // arrivals sorted by time
+  uint32_t inq_head, inq_n;
+  Pkt rop[kRopQ];     // ROP delay queue (p.t = exit time)
+  uint32_t rop_head, rop_n;
+  Pkt reply[kReplyQ];
+  uint32_t rep_head, rep_n;
+  uint64_t port_free;  // fs
+  DramRet fill[64];    // DRAM -> L2 queue
+  uint32_t fill_head, fill_n;
+  uint32_t l2_stamp;
+  uint32_t n_wait;
+  uint32_t n_l2dram;   // requests of this sub in the L2->DRAM path
+  uint32_t pad;
+  L2Line l2[kMaxL2Lines];
+  L2Mshr mshr[kMaxL2Mshr];
+  L2Wait wait[kMaxL2Wait];
+  MemStats st;
+};
+
+struct alignas(16) ChanState {
+  uint32_t id;
+  uint32_t pad0;
+  uint64_t t_icnt;    // next tick time of each domain (fs)
+  uint64_t t_l2;
+  uint64_t t_dram;
+  uint64_t dcycle;    // dram cycle counter
+  // DRAM
+  DramReq lat[kDramQ];  // L2 -> DRAM latency pipe (FIFO)
+  uint32_t lat_head, lat_n;
+  DramReq q[kDramQ];    // scheduler queue (pool; age order via q_age)
+  uint32_t q_n;
+  uint32_t pad1;
+  DramBank bk[kMaxBanksDram];
+  uint64_t t_rrd_ok, t_ccd_ok, t_rd_ok, t_wr_ok, bus_free;
+  uint64_t t_ccdl_ok[8];
+  DramRet ret[kDramRet];
+  uint32_t ret_head, ret_n;
+  uint64_t q_seq;        // arrival sequence for FR-FCFS age order
+  uint64_t q_age[kDramQ];
+  uint8_t q_valid[kDramQ];
+  uint16_t ocnt[kMaxSubPerCh][kMaxSmTot];  // replies put in each (dst SM) cell this epoch
+  uint64_t skey[kMemInQ];                  // gather scratch: sort keys
+  uint32_t sref[kMemInQ];                  // gather scratch: (src << 16 | k)
+  uint32_t srank[kMemInQ];
+  SubPart sp[kMaxSubPerCh];
+};
+
+SIM_HDI uint32_t sp_out_count(const ChanState& ch, uint32_t sub, uint32_t dst) { return ch.ocnt[sub][dst]; }
+SIM_HDI void sp_out_count_inc(ChanState& ch, uint32_t sub, uint32_t dst) { ch.ocnt[sub][dst]++; }
+
+struct MemCtx {
+  const SimCfg* cfg;
+  Pkt* outbox;          // this epoch's reply outbox base: [dst_sm][src_sub][cap]
+  uint32_t* outcnt;     // [dst_sm][src_sub]
+  uint32_t out_cap;
+  uint32_t n_src_sub;   // row stride (number of sub-partitions)
+  uint64_t win_end;     // fs, exclusive
+};
+
+// ---------------------------------------------------------------------------
+SIM_HDI uint32_t dram_bank_of(const SimCfg& c, const AddrTlx& t) { return t.bk % (c.nbk ? c.nbk : 1); }
+SIM_HDI uint32_t dram_bkgrp(const SimCfg& c, uint32_t bank) {
+  uint32_t ng = c.nbkgrp ? c.nbkgrp : 1;
+  if (c.bkgrp_index_policy == 1) return bank % ng;  // lower bits
+  uint32_t per = c.nbk / ng ? c.nbk / ng : 1;
+  return (bank / per) % ng;
+}
+
+SIM_HDI bool l2dram_can(const ChanState& ch, const SubPart& sp, const SimCfg& c, uint32_t n) {
+  return sp.n_l2dram + n <= c.q_l2_dram && ch.lat_n + n <= (uint32_t)kDramQ;
+}
+
+SIM_HDI void l2dram_push(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, uint64_t line,
+                         uint32_t sector, bool write, uint64_t now_fs) {
+  DramReq& r = ch.lat[(ch.lat_head + ch.lat_n) % kDramQ];
+  AddrTlx t = addr_decode(c, line + sector * 32ull);
+  r.line = line;
+  r.ready = now_fs + (uint64_t)c.dram_latency * c.per_l2;
+  r.row = t.row;
+  r.bank = (uint16_t)dram_bank_of(c, t);
+  r.sector = (uint8_t)sector;
+  r.write = write ? 1 : 0;
+  r.sub = (uint8_t)sub;
+  ch.lat_n++;
+  sp.n_l2dram++;
+}
+
+// ---- L2 tag array (lane-parallel over ways) ----
+template <class P>
+SIM_HDI int l2_find(const SubPart& sp, const CacheGeom& g, uint32_t set, uint64_t line) {
+  const L2Line* b = &sp.l2[set * g.assoc];
+  for (uint32_t o = 0; o < g.assoc; o += 64) {
+    int n = (int)amin<uint32_t>(64, g.assoc - o);
+    uint64_t m = P::ballot(n, [&](int w) { return b[o + w].valid && b[o + w].tag == line; });
+    if (m) return (int)o + ffs64(m);
+  }
+  return -1;
+}
+template <class P>
+SIM_HDI int l2_victim(const SubPart& sp, const CacheGeom& g, uint32_t set) {
+  const L2Line* b = &sp.l2[set * g.assoc];
+  return P::argmin((int)g.assoc, [&](int w) -> uint64_t {
+    return b[w].valid ? ((1ull << 40) | b[w].lru) : (uint64_t)w;
+  });
+}
+SIM_HDI uint32_t l2_set(const SimCfg& c, uint64_t line) {
+  return cache_set_index(c.l2, partition_address(c, line));
+}
+
+// allocate a line for `line` (evicting, writing back dirty sectors);
+// returns way or -1 if the write-back cannot be queued
+template <class P>
+SIM_HDI int l2_alloc(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, uint32_t set,
+                     uint64_t line, uint64_t now_fs) {
+  const CacheGeom& g = c.l2;
+  int v = l2_victim<P>(sp, g, set);
+  L2Line& L = sp.l2[set * g.assoc + v];
+  if (L.valid && L.dirty) {
+    uint32_t nd = (uint32_t)popc64(L.dirty);
+    if (!l2dram_can(ch, sp, c, nd)) return -1;
+    for (uint32_t s = 0; s < 4; ++s)
+      if (L.dirty >> s & 1u) l2dram_push(ch, sp, c, sub, L.tag, s, true, now_fs);
+    sp.st.l2_evict_dirty++;
+  }
+  L.tag = line;
+  L.valid = 0;
+  L.dirty = 0;
+  L.lru = ++sp.l2_stamp;
+  return v;
+}
+
+SIM_HDI bool reply_push(SubPart& sp, uint8_t type, const Pkt& req, uint8_t sectors) {
+  if (sp.rep_n >= (uint32_t)kReplyQ) return false;
+  Pkt& r = sp.reply[(sp.rep_head + sp.rep_n) % kReplyQ];
+  r.addr = req.addr;
+  r.t = 0;
+  r.tag = req.tag;
+  r.src = req.dst;  // sub-partition id
+  r.dst = req.src;  // requesting SM
+  r.type = type;
+  r.sectors = sectors;
+  r.size = (type == P_WR_ACK) ? 8 : (uint16_t)(8 + 32 * popc64(sectors));
+  r.aux = 0;
+  sp.rep_n++;
+  return true;
+}
+
+// process the request at the head of the ROP queue; false = stalled
+template <class P>
+SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, const Pkt& p,
+                       uint64_t now_fs) {
+  const CacheGeom& g = c.l2;
+  const uint32_t set = l2_set(c, p.addr);
+  const uint32_t stype = p.type == P_WR ? L2T_WR : (p.type == P_ATOM ? L2T_ATOM : L2T_RD);
+  if (sp.rep_n >= (uint32_t)kReplyQ) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
+  int way = g.disabled ? -1 : l2_find<P>(sp, g, set, p.addr);
+  if (p.type == P_WR) {
+    if (g.disabled || g.wpolicy == WP_WRITE_THROUGH) {
+      uint32_t n = (uint32_t)popc64(p.sectors);
+      if (!l2dram_can(ch, sp, c, n)) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
+      for (uint32_t s = 0; s < 4; ++s)
+        if (p.sectors >> s & 1u) l2dram_push(ch, sp, c, sub, p.addr, s, true, now_fs);
+      if (way >= 0) sp.l2[set * g.assoc + way].valid |= p.sectors;
+    } else {
+      if (way < 0) {
+        way = l2_alloc<P>(ch, sp, c, sub, set, p.addr, now_fs);
+        if (way < 0) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
+        sp.st.l2[stype][L2O_MISS]++;
+      } else {
+        sp.st.l2[stype][L2O_HIT]++;
+      }
+      L2Line& L = sp.l2[set * g.assoc + way];
+      L.valid |= p.sectors;
+      L.dirty |= p.sectors;
+      if (g.repl == REPL_LRU) L.lru = ++sp.l2_stamp;
+    }
+    reply_push(sp, P_WR_ACK, p, p.sectors);
+    return true;
+  }
+  // read / atomic
+  uint8_t have = way >= 0 ? sp.l2[set * g.assoc + way].valid : 0;
+  uint8_t miss = p.sectors & (uint8_t)~have;
+  const uint8_t rtype = p.type == P_ATOM ? P_ATOM_REPLY : P_RD_REPLY;
+  if (miss == 0) {
+    L2Line& L = sp.l2[set * g.assoc + way];
+    if (g.repl == REPL_LRU) L.lru = ++sp.l2_stamp;
+    if (p.type == P_ATOM) L.dirty |= p.sectors;
+    reply_push(sp, rtype, p, p.sectors);
+    sp.st.l2[stype][L2O_HIT]++;
+    return true;
+  }
+  if (sp.n_wait >= (uint32_t)kMaxL2Wait) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
+  const int nm = (int)amin<uint32_t>(g.mshr_entries, kMaxL2Mshr);
+  int mi = P::argmin(nm, [&](int i) -> uint64_t {
+    return (sp.mshr[i].valid && sp.mshr[i].line == p.addr) ? (uint64_t)i : ~0ull;
+  });
+  uint8_t need_req = mi >= 0 ? (uint8_t)(miss & ~sp.mshr[mi].requested) : miss;
+  if (need_req == 0) {
+    if (sp.mshr[mi].merges >= g.mshr_merge) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
+    sp.mshr[mi].merges++;
+    sp.st.l2[stype][L2O_MSHR_HIT]++;
+  } else {
+    uint32_t nreq = (uint32_t)popc64(need_req);
+    if (!l2dram_can(ch, sp, c, nreq)) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
+    if (mi < 0) {
+      mi = P::argmin(nm, [&](int i) -> uint64_t { return sp.mshr[i].valid ? ~0ull : (uint64_t)i; });
+      if (mi < 0) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
+      sp.mshr[mi].valid = 1;
+      sp.mshr[mi].line = p.addr;
+      sp.mshr[mi].requested = 0;
+      sp.mshr[mi].merges = 0;
+    }
+    sp.mshr[mi].requested |= need_req;
+    for (uint32_t s = 0; s < 4; ++s)
+      if (need_req >> s & 1u) l2dram_push(ch, sp, c, sub, p.addr, s, false, now_fs);
+    sp.st.l2[stype][L2O_MISS]++;
+  }
+  // waiter entry (first free)
+  uint32_t wi = sp.n_wait;
+  for (uint32_t b = 0; b < sp.n_wait; b += 64) {
+    int n = (int)amin<uint32_t>(64, sp.n_wait - b);
+    uint64_t m = P::ballot(n, [&](int i) { return !sp.wait[b + i].valid; });
+    if (m) { wi = b + ffs64(m); break; }
+  }
+  L2Wait& e = sp.wait[wi];
+  e.line = p.addr;
+  e.tag = p.tag;
+  e.src = p.src;
+  e.need = miss;
+  e.sectors = p.sectors;
+  e.type = p.type;
+  e.valid = 1;
+  if (wi == sp.n_wait) sp.n_wait++;
+  return true;
+}
+
+// DRAM data for one sector returns to the L2
+template <class P>
+SIM_HDI bool l2_fill(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, const DramRet& r,
+                     uint64_t now_fs) {
+  const CacheGeom& g = c.l2;
+  const uint8_t sbit = (uint8_t)(1u << r.sector);
+  // replies this fill will generate must fit
+  uint32_t nrep = 0;
+  for (uint32_t b = 0; b < sp.n_wait; b += 64) {
+    int n = (int)amin<uint32_t>(64, sp.n_wait - b);
+    uint64_t m = P::ballot(n, [&](int i) {
+      const L2Wait& e = sp.wait[b + i];
+      return e.valid && e.line == r.line && e.need == sbit;
+    });
+    nrep += (uint32_t)popc64(m);
+  }
+  if (sp.rep_n + nrep > (uint32_t)kReplyQ) return false;
+  if (!g.disabled) {
+    uint32_t set = l2_set(c, r.line);
+    int way = l2_find<P>(sp, g, set, r.line);
+    if (way < 0) {
+      way = l2_alloc<P>(ch, sp, c, sub, set, r.line, now_fs);
+      if (way < 0) return false;
+    }
+    L2Line& L = sp.l2[set * g.assoc + way];
+    L.valid |= sbit;
+    if (g.repl == REPL_LRU) L.lru = ++sp.l2_stamp;
+  }
+  const int nm = (int)amin<uint32_t>(g.mshr_entries, kMaxL2Mshr);
+  int mi = P::argmin(nm, [&](int i) -> uint64_t {
+    return (sp.mshr[i].valid && sp.mshr[i].line == r.line) ? (uint64_t)i : ~0ull;
+  });
+  if (mi >= 0) {
+    sp.mshr[mi].requested &= (uint8_t)~sbit;
+    if (!sp.mshr[mi].requested) sp.mshr[mi].valid = 0;
+  }
+  for (uint32_t b = 0; b < sp.n_wait; b += 64) {
+    int n = (int)amin<uint32_t>(64, sp.n_wait - b);
+    uint64_t m = P::ballot(n, [&](int i) {
+      const L2Wait& e = sp.wait[b + i];
+      return e.valid && e.line == r.line && (e.need & sbit);
+    });
+    while (m) {
+      int i = ffs64(m);
+      m &= m - 1;
+      L2Wait& e = sp.wait[b + i];
+      e.need &= (uint8_t)~sbit;
+      if (e.need) continue;
+      Pkt q;
+      q.addr = e.line;
+      q.tag = e.tag;
+      q.src = e.src;
+      q.dst = (uint16_t)(ch.id * c.n_sub_per_mem + sub);
+      q.type = e.type;
+      q.sectors = e.sectors;
+      q.size = 0;
+      q.t = 0;
+      q.aux = 0;
+      reply_push(sp, e.type == P_ATOM ? P_ATOM_REPLY : P_RD_REPLY, q, e.sectors);
+      if (e.type == P_ATOM && !g.disabled) {
+        uint32_t set = l2_set(c, r.line);
+        int way = l2_find<P>(sp, g, set, r.line);
+        if (way >= 0) sp.l2[set * g.assoc + way].dirty |= e.sectors;
+      }
+      e.valid = 0;
+    }
+  }
+  while (sp.n_wait && !sp.wait[sp.n_wait - 1].valid) sp.n_wait--;
+  return true;
+}
+
+// one L2 cycle of one sub-partition
+template <class P>
+SIM_HDI void l2_cycle(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, uint64_t now_fs) {
+  sp.st.l2_cycles++;
+  sp.st.rop_occ += sp.rop_n;
+  if (sp.fill_n) {
+    const DramRet& r = sp.fill[sp.fill_head];
+    if (r.ready <= now_fs) {
+      DramRet rr = r;
+      if (l2_fill<P>(ch, sp, c, sub, rr, now_fs)) {
+        sp.fill_head = (sp.fill_head + 1) % 64;
+        sp.fill_n--;
+      }
+    }
+  }
+  if (sp.rop_n) {
+    const Pkt& p = sp.rop[sp.rop_head];
+    if (p.t <= now_fs) {
+      Pkt pp = p;
+      if (l2_access<P>(ch, sp, c, sub, pp, now_fs)) {
+        sp.rop_head = (sp.rop_head + 1) % kRopQ;
+        sp.rop_n--;
+        sp.st.l2_busy++;
+      }
+    }
+  }
+}
+
+// one interconnect cycle of one sub-partition: accept an arrival into the
+// ROP queue and start injecting a reply
+template <class P>
+SIM_HDI void mem_icnt_cycle(ChanState& ch, SubPart& sp, const SimCfg& c, const MemCtx& x,
+                            uint32_t sub, uint64_t now_fs) {
+  if (sp.inq_n && sp.rop_n < (uint32_t)kRopQ && sp.rop_n < c.q_icnt_l2 + c.rop_latency) {
+    const Pkt& a = sp.inq[sp.inq_head];
+    if (a.t <= now_fs) {
+      Pkt p = a;
+      p.t = now_fs + (uint64_t)c.rop_latency * c.per_l2;
+      sp.rop[(sp.rop_head + sp.rop_n) % kRopQ] = p;
+      sp.rop_n++;
+      sp.inq_head = (sp.inq_head + 1) % kMemInQ;
+      sp.inq_n--;
+      sp.st.pkts_in++;
+      sp.st.bytes_in += p.size;
+    }
+  }
+  if (sp.rep_n && sp.port_free <= now_fs) {
+    Pkt r = sp.reply[sp.rep_head];
+    uint32_t nflits = (r.size + c.flit_size - 1) / c.flit_size;
+    uint64_t done = now_fs + (uint64_t)(nflits - 1) * c.per_icnt;
+    if (done < x.win_end) {
+      uint32_t gsub = ch.id * c.n_sub_per_mem + sub;
+      uint32_t cell = (uint32_t)r.dst * x.n_src_sub + gsub;
+      // per-destination counter kept in the reply's own slot count array
+      uint32_t n = sp_out_count(ch, sub, r.dst);
+      if (n < x.out_cap) {
+        r.t = done + (uint64_t)c.icnt_latency * c.per_core;
+        P::one([&] { x.outbox[(uint64_t)cell * x.out_cap + n] = r; });
+        sp_out_count_inc(ch, sub, r.dst);
+        sp.rep_head = (sp.rep_head + 1) % kReplyQ;
+        sp.rep_n--;
+        sp.port_free = now_fs + (uint64_t)nflits * c.per_icnt;
+        sp.st.pkts_out++;
+        sp.st.bytes_out += r.size;
+      } else {
+        sp.st.icnt_stall++;
+      }
+    }
+  }
+}
+
+}  // namespace asim
+
+namespace asim {
+
+// ---------------------------------------------------------------------------
+// DRAM channel: one DRAM clock.  FR-FCFS (row hits first, then oldest) with
+// per-bank ACT/PRE state machines and HBM-style dual command bus
+// (reference dram_t::cycle dram.cc:289-552, frfcfs dram_sched.cc:109-258).
+template <class P>
+SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
+  MemStats& st = ch.sp[0].st;
+  const uint64_t t = ch.dcycle++;
+  st.dram_cycles++;
+  const uint32_t qcap = amin<uint32_t>(c.dram_queue ? c.dram_queue : 1, kDramQ);
+  // latency pipe -> scheduler queue
+  while (ch.lat_n && ch.q_n < qcap) {
+    const DramReq& h = ch.lat[ch.lat_head];
+    if (h.ready > now_fs) break;
+    int f = P::argmin(kDramQ, [&](int i) -> uint64_t { return ch.q_valid[i] ? ~0ull : (uint64_t)i; });
+    ch.q[f] = h;
+    ch.q_valid[f] = 1;
+    ch.q_age[f] = ch.q_seq++;
+    ch.q_n++;
+    ch.lat_head = (ch.lat_head + 1) % kDramQ;
+    ch.lat_n--;
+  }
+  // data returns -> DRAM->L2 queues
+  while (ch.ret_n) {
+    const DramRet& r = ch.ret[ch.ret_head];
+    if (r.ready > now_fs) break;
+    SubPart& sp = ch.sp[r.sub];
+    uint32_t cap = amin<uint32_t>(c.q_dram_l2 ? c.q_dram_l2 : 1, 64);
+    if (sp.fill_n >= cap) break;
+    sp.fill[(sp.fill_head + sp.fill_n) % 64] = r;
+    sp.fill_n++;
+    ch.ret_head = (ch.ret_head + 1) % kDramRet;
+    ch.ret_n--;
+  }
+  st.dram_q_occ += ch.q_n;
+  if (ch.q_n == 0) return;
+  const uint32_t burst = amax<uint32_t>(1, c.BL / (c.data_cmd_ratio ? c.data_cmd_ratio : 1));
+  // banks that have a queued row hit
+  uint64_t hitmask = P::vor(kDramQ, [&](int i) -> uint64_t {
+    if (!ch.q_valid[i]) return 0;
+    const DramReq& r = ch.q[i];
+    const DramBank& b = ch.bk[r.bank];
+    return (b.open && b.row == r.row) ? (1ull << r.bank) : 0ull;
+  });
+  // ---- column command ----
+  bool col = false;
+  {
+    uint64_t oldest_age = ~0ull;
+    if (c.dram_sched == 0) {  // FIFO: only the oldest request may issue
+      int o = P::argmin(kDramQ, [&](int i) -> uint64_t { return ch.q_valid[i] ? ch.q_age[i] : ~0ull; });
+      oldest_age = o >= 0 ? ch.q_age[o] : ~0ull;
+    }
+    int pick = P::argmin(kDramQ, [&](int i) -> uint64_t {
+      if (!ch.q_valid[i]) return ~0ull;
+      if (c.dram_sched == 0 && ch.q_age[i] != oldest_age) return ~0ull;
+      const DramReq& r = ch.q[i];
+      const DramBank& b = ch.bk[r.bank];
+      if (!b.open || b.row != r.row || t < b.t_col_ok || t < ch.t_ccd_ok) return ~0ull;
+      if (t < ch.t_ccdl_ok[dram_bkgrp(c, r.bank) & 7]) return ~0ull;
+      if (r.write ? (t < ch.t_wr_ok) : (t < ch.t_rd_ok)) return ~0ull;
+      return ch.q_age[i];
+    });
+    if (pick >= 0 && !(ch.q[pick].write == 0 && ch.ret_n >= (uint32_t)kDramRet)) {
+      const DramReq r = ch.q[pick];
+      DramBank& b = ch.bk[r.bank];
+      if (r.write) {
+        b.t_pre_ok = amax<uint64_t>(b.t_pre_ok, t + c.WL + burst + c.tWR);
+        ch.t_rd_ok = amax<uint64_t>(ch.t_rd_ok, t + c.WL + burst + c.tCDLR);
+        st.dram_wr++;
+      } else {
+        DramRet& o = ch.ret[(ch.ret_head + ch.ret_n) % kDramRet];
+        o.line = r.line;
+        o.sector = r.sector;
+        o.sub = r.sub;
+        o.ready = (t + c.CL + burst) * c.per_dram;
+        ch.ret_n++;
+        b.t_pre_ok = amax<uint64_t>(b.t_pre_ok, t + c.tRTPL);
+        uint64_t rtw = t + c.CL + burst + 2;
+        ch.t_wr_ok = amax<uint64_t>(ch.t_wr_ok, rtw > c.WL ? rtw - c.WL : 0);
+        st.dram_rd++;
+      }
+      ch.t_ccd_ok = t + amax<uint32_t>(c.tCCD, burst);
+      ch.t_ccdl_ok[dram_bkgrp(c, r.bank) & 7] = t + amax<uint32_t>(c.tCCDL, burst);
+      st.dram_busy_cycles += burst;
+      ch.q_valid[pick] = 0;
+      ch.q_n--;
+      ch.sp[r.sub].n_l2dram--;
+      col = true;
+    }
+  }
+  // ---- row command (dual bus: in the same cycle) ----
+  if (col && !c.dual_bus) return;
+  int act = P::argmin(kDramQ, [&](int i) -> uint64_t {
+    if (!ch.q_valid[i]) return ~0ull;
+    const DramReq& r = ch.q[i];
+    const DramBank& b = ch.bk[r.bank];
+    if (b.open) {
+      // precharge a row only when no queued request still hits it
+      if (b.row == r.row || (hitmask >> r.bank & 1ull) || t < b.t_pre_ok) return ~0ull;
+      return ch.q_age[i];
+    }
+    if (t < b.t_act_ok || t < ch.t_rrd_ok) return ~0ull;
+    return ch.q_age[i];
+  });
+  if (act >= 0) {
+    const DramReq& r = ch.q[act];
+    DramBank& b = ch.bk[r.bank];
+    if (b.open) {
+      b.open = 0;
+      b.t_act_ok = amax<uint64_t>(b.t_act_ok, t + c.tRP);
+      st.dram_pre++;
+    } else {
+      b.open = 1;
+      b.row = r.row;
+      b.t_col_ok = t + c.tRCD;
+      b.t_pre_ok = t + c.tRAS;
+      b.t_act_ok = t + c.tRC;
+      ch.t_rrd_ok = t + c.tRRD;
+      st.dram_act++;
+    }
+  }
+}
+
+SIM_HDI bool sub_idle(const SubPart& sp) {
+  return sp.inq_n == 0 && sp.rop_n == 0 && sp.rep_n == 0 && sp.fill_n == 0 && sp.n_wait == 0 && sp.n_l2dram == 0;
+}
+SIM_HDI bool chan_idle(const ChanState& ch, const SimCfg& c) {
+  if (ch.lat_n || ch.q_n || ch.ret_n) return false;
+  for (uint32_t j = 0; j < c.n_sub_per_mem; ++j)
+    if (!sub_idle(ch.sp[j])) return false;
+  return true;
+}
+
+// advance the tick clocks of an idle channel to the first tick >= t1
+SIM_HDI uint64_t next_tick(uint64_t t, uint64_t per, uint64_t t1) {
+  if (t >= t1) return t;
+  uint64_t k = (t1 - t + per - 1) / per;
+  return t + k * per;
+}
+
+// simulate all memory-side clock ticks in [.., x.win_end)
+template <class P>
+SIM_HDI void mem_window(ChanState& ch, const MemCtx& x) {
+  const SimCfg& c = *x.cfg;
+  const uint64_t t1 = x.win_end;
+  if (chan_idle(ch, c)) {
+    // nothing can happen until a new arrival (next epoch): skip the ticks
+    uint64_t nd = next_tick(ch.t_dram, c.per_dram, t1);
+    ch.sp[0].st.dram_cycles += (nd - ch.t_dram) / c.per_dram;
+    ch.dcycle += (nd - ch.t_dram) / c.per_dram;
+    ch.t_dram = nd;
+    uint64_t nl = next_tick(ch.t_l2, c.per_l2, t1);
+    for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) ch.sp[j].st.l2_cycles += (nl - ch.t_l2) / c.per_l2;
+    ch.t_l2 = nl;
+    ch.t_icnt = next_tick(ch.t_icnt, c.per_icnt, t1);
+    return;
+  }
+  for (;;) {
+    uint64_t tm = amin(ch.t_dram, amin(ch.t_l2, ch.t_icnt));
+    if (tm >= t1) break;
+    if (ch.t_dram == tm) {
+      dram_cycle<P>(ch, c, tm);
+      ch.t_dram += c.per_dram;
+    }
+    if (ch.t_l2 == tm) {
+      for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) l2_cycle<P>(ch, ch.sp[j], c, j, tm);
+      ch.t_l2 += c.per_l2;
+    }
+    if (ch.t_icnt == tm) {
+      for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) mem_icnt_cycle<P>(ch, ch.sp[j], c, x, j, tm);
+      ch.t_icnt += c.per_icnt;
+    }
+  }
+}
+
+// Gather one epoch of arrivals from the n_src source rows of an outbox cell
+// array ([dst][src][cap], counts [dst][src]) and append them to `q` sorted by
+// (time, source).  Keys are epoch-relative so they fit with the source id.
+template <class P>
+SIM_HDI uint32_t gather_sorted(const Pkt* box, const uint32_t* cnt, uint32_t dst, uint32_t n_src,
+                               uint32_t cap, uint64_t t0, Pkt* q, uint32_t qcap, uint32_t& qhead,
+                               uint32_t& qn, uint64_t* skey, uint32_t* sref, uint32_t* srank,
+                               uint32_t scap) {
+  const uint32_t* row = cnt + (uint64_t)dst * n_src;
+  // exclusive scan of the per-source counts -> slot of each packet
+  uint32_t total = P::scan((int)n_src, [&](int s) -> uint32_t { return row[s]; },
+                           [&](int s, uint32_t off) { srank[s] = off; });
+  P::sync();
+  if (total == 0) return 0;
+  if (total > scap) total = scap;  // (capacity sized so this never triggers)
+  P::each((int)n_src, [&](int s) {
+    uint32_t n = row[s], off = srank[s];
+    for (uint32_t k = 0; k < n && off + k < scap; ++k) {
+      const Pkt& p = box[((uint64_t)dst * n_src + s) * cap + k];
+      skey[off + k] = ((p.t - t0) << 16) | (uint64_t)s;
+      sref[off + k] = ((uint32_t)s << 16) | k;
+    }
+  });
+  P::sync();
+  // rank sort (keys are unique: one packet per source per tick)
+  P::each((int)total, [&](int i) {
+    uint64_t k = skey[i];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < total; ++j) r += skey[j] < k;
+    srank[i] = r;
+  });
+  P::sync();
+  uint32_t room = qcap - qn;
+  uint32_t n = total < room ? total : room;
+  P::each((int)total, [&](int i) {
+    uint32_t r = srank[i];
+    if (r >= n) return;
+    uint32_t s = sref[i] >> 16, k = sref[i] & 0xffff;
+    q[(qhead + qn + r) % qcap] = box[((uint64_t)dst * n_src + s) * cap + k];
+  });
+  P::sync();
+  qn += n;
+  return n;
+}
+
+template <class P>
+SIM_HDI void mem_gather(ChanState& ch, const SimCfg& c, const Pkt* box, const uint32_t* cnt,
+                        uint32_t cap, uint64_t t0) {
+  for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
+    SubPart& sp = ch.sp[j];
+    uint32_t gsub = ch.id * c.n_sub_per_mem + j;
+    gather_sorted<P>(box, cnt, gsub, c.n_sm, cap, t0, sp.inq, kMemInQ, sp.inq_head, sp.inq_n, ch.skey,
+                     ch.sref, ch.srank, kMemInQ);
+  }
+}
+
+// publish this epoch's reply counts (every cell, zeros included) and reset
+template <class P>
+SIM_HDI void mem_publish(ChanState& ch, const SimCfg& c, uint32_t* outcnt) {
+  for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
+    uint32_t gsub = ch.id * c.n_sub_per_mem + j;
+    P::each((int)c.n_sm, [&](int d) {
+      outcnt[(uint64_t)d * c.n_subpart + gsub] = ch.ocnt[j][d];
+      ch.ocnt[j][d] = 0;
+    });
+  }
+  P::sync();
+}
+
+}  // namespace asim

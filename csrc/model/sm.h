@@ -1,0 +1,1003 @@
+// Cycle model of one SIMT core (SM / CU).  Single source for both engines.
+//
+// Stage order per cycle mirrors the reference's reverse-pipeline walk
+// (shader_core_ctx::cycle, shader.cc:3629-3641: writeback -> execute ->
+// read_operands -> issue -> decode/fetch) so an instruction advances at most
+// one stage per cycle.  The data structures are re-designed for a 64-lane
+// wavefront owning the SM: warps are lanes, the scheduler pick is a ballot +
+// rotate + ffs (reference scheduler_unit::cycle, shader.cc:1249-1556 walks an
+// STL vector), the scoreboard is a 256-bit mask per warp
+// (scoreboard.cc:83-150 uses std::set), L1 ways are probed lane-parallel, and
+// MSHR waiters live in a flat associative table instead of linked lists
+// (mshr_table, gpu-cache.h:1019).
+#pragma once
+#include "addrdec.h"
+
+namespace asim {
+
+// ---- per-access record produced by the trace-ingest coalescer ----
+// line (128B aligned) | sector mask (bits 0..3) | (bytes/4-1) in bits 4..6 is
+// NOT packed: keep it simple and 16-byte aligned.
+struct TAcc {
+  uint64_t line;     // 128B-aligned line address
+  uint16_t bytes;    // bytes touched (write packet size)
+  uint8_t sectors;   // 32B sector mask
+  uint8_t bank;      // L1 bank (precomputed)
+  uint32_t pad;
+};
+static_assert(sizeof(TAcc) == 16, "TAcc must stay 16 bytes");
+
+// instruction window per warp (prefetched trace records, ring indexed by
+// instruction index modulo kWin)
+// (kWin is defined in config.h)
+
+enum WarpFlags : uint8_t {
+  WF_ACTIVE = 1,
+  WF_EXITING = 2,    // EXIT issued / stream exhausted: no more fetch/issue
+  WF_BARRIER = 4,    // waiting at a CTA barrier
+  WF_MEMBAR = 8,     // waiting for outstanding stores
+  WF_WAITCNT = 16,   // waiting for all outstanding memory (CDNA s_waitcnt)
+};
+
+// hit / shared-memory completion ring entries
+struct HitEnt {
+  uint8_t warp;
+  uint8_t slot;   // load slot, 0xff = store completion (inflight--)
+  uint8_t kind;   // 0 = load access, 1 = store/shared-store done
+  uint8_t pad;
+};
+
+struct WbEnt {
+  uint8_t warp;
+  uint8_t dst0;
+  uint8_t dst1;
+  uint8_t pad;
+};
+
+struct IdOc {  // ID_OC pipeline register (one per scheduler per unit type)
+  TInst inst;
+  uint8_t valid;
+  uint8_t warp;
+  uint8_t pad[2];
+  uint32_t widx;  // warp-local instruction sequence (for age)
+};
+
+struct OCUnit {
+  TInst inst;
+  uint8_t valid;
+  uint8_t warp;
+  uint8_t sched;
+  uint8_t unit;
+  uint8_t nread;      // remaining operand reads
+  uint8_t banks[5];   // bank of each pending read (0xff = done)
+  uint8_t pad[2];
+  uint32_t age;
+};
+
+struct L1Line {
+  uint64_t tag;      // line address
+  uint32_t lru;      // last-use / insertion stamp
+  uint8_t valid;     // sector mask
+  uint8_t pad[3];
+};
+
+struct L1Mshr {
+  uint64_t line;
+  uint8_t requested;  // sectors requested from L2
+  uint8_t valid;      // entry in use
+  uint8_t merges;
+  uint8_t pad[5];
+};
+
+struct L1Pend {  // a load access waiting for sectors of a line
+  uint64_t line;
+  uint8_t need;   // sectors
+  uint8_t warp;
+  uint8_t slot;
+  uint8_t valid;
+  uint32_t pad;
+};
+
+struct LdstState {
+  TInst inst;
+  uint8_t busy;
+  uint8_t warp;
+  uint8_t slot;
+  uint8_t next;       // next access index
+  uint32_t start;     // cycle the instruction entered the unit (low 32 bits)
+};
+
+// statistics counters of one SM (reduced on the host)
+enum L1StatType : uint8_t { L1T_GLOBAL_R = 0, L1T_GLOBAL_W, L1T_LOCAL_R, L1T_LOCAL_W, L1T_ATOMIC, L1T_COUNT };
+enum L1StatOut : uint8_t { L1O_HIT = 0, L1O_MISS, L1O_MSHR_HIT, L1O_RES_FAIL, L1O_BYPASS, L1O_COUNT };
+struct SMStats {
+  uint64_t thread_insn;        // gpu_sim_insn contribution (active-thread count)
+  uint64_t warp_insn;
+  uint64_t cls_insn[OC_COUNT];
+  uint64_t active_cycles;      // cycles with at least one live warp
+  uint64_t busy_cycles;        // cycles with at least one instruction issued
+  uint64_t issue_stall_idle;   // scheduler cycles with no ready warp
+  uint64_t sb_stall;           // warps blocked by scoreboard (sampled per cycle)
+  uint64_t pipe_stall;
+  uint64_t l1[L1T_COUNT][L1O_COUNT];
+  uint64_t shmem_acc;
+  uint64_t shmem_conflict_cycles;
+  uint64_t pkts_out;
+  uint64_t pkts_in;
+  uint64_t bytes_out;
+  uint64_t bytes_in;
+  uint64_t rf_reads;
+  uint64_t rf_writes;
+  uint64_t oc_bank_conflicts;
+  uint64_t ctas_done;
+  uint64_t warps_done;
+  uint64_t occupancy_acc;      // sum over cycles of live warps
+  uint64_t mem_insn;
+  uint64_t power_acc[8];       // spare power-model counters
+};
+
+// per-SM kernel bookkeeping (replicated identically in every SM)
+struct SmKernel {
+  uint32_t uid;
+  uint32_t next_cta;
+  uint64_t ready_cycle;  // kernel launch latency expires
+  uint64_t start_cycle;
+};
+
+// Complete state of one SM.  On the GPU it lives in LDS for the duration of
+// a launch (copied in/out of HBM), on the CPU it is a plain struct.
+struct alignas(16) SMState {
+  uint32_t id;
+  uint32_t kernel_cta_slots;  // CTA slots for the current kernel
+  uint64_t cycle;             // next core cycle to simulate
+  uint64_t last_progress;     // last cycle an instruction completed (deadlock)
+  uint64_t epoch_end;         // current epoch end cycle (exclusive)
+  uint64_t out_port_free;     // cycle the injection port frees
+  uint32_t age_ctr;
+  uint32_t pad_a;
+  // ---- warps (SoA) ----
+  uint32_t w_next[kMaxWarps];   // next trace index to fetch into ibuf
+  uint32_t w_end[kMaxWarps];    // end of stream
+  uint32_t w_head[kMaxWarps];   // next trace index to issue
+  uint32_t w_wfill[kMaxWarps];  // window filled up to (exclusive)
+  uint32_t w_age[kMaxWarps];    // dynamic warp id (oldest first)
+  uint8_t w_flags[kMaxWarps];
+  uint8_t w_ibuf[kMaxWarps];    // decoded instructions available
+  uint8_t w_cta[kMaxWarps];
+  uint8_t w_inflight[kMaxWarps];
+  uint16_t w_stores[kMaxWarps];  // outstanding store acks
+  uint16_t w_loads[kMaxWarps];   // outstanding load slots in use
+  uint64_t w_sb[kMaxWarps][4];   // scoreboard: pending destination registers
+  uint8_t w_slot_used[kMaxWarps];  // bitmask of used load slots
+  uint8_t w_pad[kMaxWarps][3];
+  uint16_t w_slot_pend[kMaxWarps][kLoadSlots];
+  uint8_t w_slot_dst[kMaxWarps][kLoadSlots][2];
+  TInst w_win[kMaxWarps][kWin];
+  // ---- CTAs ----
+  uint32_t cta_id[kMaxCta];
+  uint8_t cta_valid[kMaxCta];
+  uint8_t cta_live[kMaxCta];     // warps not yet completed
+  uint8_t cta_bar[kMaxCta];      // warps arrived at barrier
+  uint8_t cta_nexit[kMaxCta];    // warps exited (excluded from barrier count)
+  uint32_t n_cta_active;
+  // ---- front end ----
+  uint32_t fetch_rr;
+  uint32_t sched_last[kMaxSched];
+  // ---- pipeline registers / operand collectors / FUs ----
+  IdOc idoc[kMaxSched][U_COUNT];
+  OCUnit oc[kMaxOC];
+  uint32_t fu_next[U_COUNT][kMaxSched];  // cycle (low 32) a unit can accept again
+  uint8_t wb_cnt[kWbRing];
+  WbEnt wb[kWbRing][kWbSlot];
+  // ---- LD/ST + L1 ----
+  LdstState ldst;
+  uint8_t hit_cnt[kHitRing];
+  HitEnt hit[kHitRing][kHitSlot];
+  L1Line l1[kMaxL1Lines];
+  L1Mshr mshr[kMaxL1Mshr];
+  L1Pend pend[kMaxPend];
+  uint32_t n_pend;
+  uint32_t l1_stamp;
+  // ---- interconnect endpoints ----
+  Pkt outq[kOutQ];
+  uint32_t outq_head, outq_n;
+  uint32_t outstanding;     // packets awaiting a reply
+  uint32_t pad_b;
+  uint32_t ocnt[kMaxSubTot]; // packets put into each destination's outbox cell this epoch
+  Pkt inq[kInQ];
+  uint32_t inq_head, inq_n;
+  uint64_t skey[kInQ];       // gather scratch
+  uint32_t sref[kInQ];
+  uint32_t srank[kInQ > kMaxSubTot ? kInQ : kMaxSubTot];
+  SmKernel ks;               // replicated kernel dispatch state
+  SMStats st;
+};
+SIM_HDI uint64_t* s_scratch_key(SMState& s) { return s.skey; }
+SIM_HDI uint32_t* s_scratch_ref(SMState& s) { return s.sref; }
+SIM_HDI uint32_t* s_scratch_rank(SMState& s) { return s.srank; }
+
+// ---------------------------------------------------------------------------
+// context passed to every SM step
+struct SmCtx {
+  const SimCfg* cfg;
+  const KernelDesc* k;
+  const TAcc* acc;       // coalesced access table of the kernel
+  Pkt* outbox;           // this epoch's outbox base: [dst][src][cap]
+  uint32_t* outcnt;      // [dst][src]
+  uint32_t out_cap;      // per (dst,src) capacity (>= epoch length)
+  uint32_t n_src_sm;     // number of SMs (row stride)
+};
+
+SIM_HDI uint32_t wb_width(const SimCfg& c) { return c.ex_wb_width < (uint32_t)kWbSlot ? c.ex_wb_width : (uint32_t)kWbSlot; }
+
+SIM_HDI bool sb_test(const uint64_t* sb, uint8_t r) { return r && ((sb[r >> 6] >> (r & 63)) & 1ull); }
+SIM_HDI void sb_set(uint64_t* sb, uint8_t r) {
+  if (r) sb[r >> 6] |= 1ull << (r & 63);
+}
+SIM_HDI void sb_clr(uint64_t* sb, uint8_t r) {
+  if (r) sb[r >> 6] &= ~(1ull << (r & 63));
+}
+
+// ---------------------------------------------------------------------------
+// reset an SM for a new kernel (state persists across kernels otherwise:
+// L1 may be flushed by -gpgpu_flush_l1_cache)
+template <class P>
+SIM_HDI void sm_reset(SMState& s, uint32_t id) {
+  // caller zero-fills the struct; set identity
+  s.id = id;
+}
+
+// L1 geometry in use (adaptive per kernel)
+SIM_HDI CacheGeom l1_geom(const SimCfg& c, const KernelDesc& k) {
+  CacheGeom g = c.l1;
+  g.nsets = k.l1_sets;
+  g.assoc = k.l1_assoc;
+  return g;
+}
+
+// ---------------------------------------------------------------------------
+// injection: enqueue a packet towards the interconnect
+SIM_HDI bool sm_can_send(const SMState& s, const SimCfg& c) {
+  return s.outq_n < (uint32_t)kOutQ && s.outstanding + s.outq_n < c.icnt_out_limit;
+}
+SIM_HDI void sm_send(SMState& s, const SimCfg& c, uint8_t type, uint64_t line, uint8_t sectors,
+                     uint16_t bytes, uint32_t tag) {
+  AddrTlx t = addr_decode(c, line);
+  Pkt& p = s.outq[(s.outq_head + s.outq_n) % kOutQ];
+  p.addr = line;
+  p.t = 0;
+  p.tag = tag;
+  p.src = (uint16_t)s.id;
+  p.dst = (uint16_t)t.sub;
+  p.type = type;
+  p.sectors = sectors;
+  p.size = (type == P_WR) ? (uint16_t)(8 + bytes) : (uint16_t)8;
+  p.aux = 0;
+  s.outq_n++;
+}
+
+// move packets whose injection completes inside the epoch into the outbox
+template <class P>
+SIM_HDI void sm_inject(SMState& s, const SmCtx& x, uint64_t now) {
+  const SimCfg& c = *x.cfg;
+  if (s.outq_n == 0) return;
+  if (now < s.out_port_free) return;
+  Pkt p = s.outq[s.outq_head];
+  uint32_t nflits = (p.size + c.flit_size - 1) / c.flit_size;
+  uint64_t done = now + nflits - 1;
+  if (done >= s.epoch_end) return;  // completes next epoch
+  uint32_t dst = p.dst;
+  uint32_t slot = dst * x.n_src_sm + s.id;
+  uint32_t n = s.ocnt[dst];
+  if (n >= x.out_cap) return;  // outbox cell full (cannot happen with cap >= epoch)
+  s.ocnt[dst] = n + 1;
+  p.t = (done + c.icnt_latency) * c.per_core;
+  P::one([&] {
+    x.outbox[(uint64_t)slot * x.out_cap + n] = p;
+    x.outcnt[slot] = n + 1;
+  });
+  s.outq_head = (s.outq_head + 1) % kOutQ;
+  s.outq_n--;
+  s.out_port_free = now + nflits;
+  s.outstanding++;
+  s.st.pkts_out++;
+  s.st.bytes_out += p.size;
+}
+
+// ---------------------------------------------------------------------------
+// writeback of ALU results due this cycle
+template <class P>
+SIM_HDI void sm_writeback(SMState& s, const SimCfg& c, uint64_t now) {
+  uint32_t slot = (uint32_t)(now % kWbRing);
+  uint32_t n = s.wb_cnt[slot];
+  for (uint32_t i = 0; i < n; ++i) {
+    WbEnt e = s.wb[slot][i];
+    sb_clr(s.w_sb[e.warp], e.dst0);
+    sb_clr(s.w_sb[e.warp], e.dst1);
+    s.w_inflight[e.warp]--;
+    s.st.rf_writes += (e.dst0 != 0) + (e.dst1 != 0);
+  }
+  if (n) s.last_progress = now;
+  s.wb_cnt[slot] = 0;
+}
+
+SIM_HDI void sm_load_slot_done(SMState& s, uint32_t w, uint32_t slot, uint64_t now) {
+  sb_clr(s.w_sb[w], s.w_slot_dst[w][slot][0]);
+  sb_clr(s.w_sb[w], s.w_slot_dst[w][slot][1]);
+  s.st.rf_writes += (s.w_slot_dst[w][slot][0] != 0) + (s.w_slot_dst[w][slot][1] != 0);
+  s.w_slot_used[w] &= (uint8_t)~(1u << slot);
+  s.w_loads[w]--;
+  s.w_inflight[w]--;
+  s.last_progress = now;
+}
+
+// L1-hit / shared-memory completions due this cycle
+template <class P>
+SIM_HDI void sm_hit_complete(SMState& s, uint64_t now) {
+  uint32_t slot = (uint32_t)(now % kHitRing);
+  uint32_t n = s.hit_cnt[slot];
+  for (uint32_t i = 0; i < n; ++i) {
+    HitEnt e = s.hit[slot][i];
+    if (e.kind == 0) {
+      if (--s.w_slot_pend[e.warp][e.slot] == 0) sm_load_slot_done(s, e.warp, e.slot, now);
+    } else {
+      s.w_inflight[e.warp]--;
+      s.last_progress = now;
+    }
+  }
+  s.hit_cnt[slot] = 0;
+}
+
+SIM_HDI bool hit_push(SMState& s, uint64_t when, uint8_t warp, uint8_t slot, uint8_t kind) {
+  uint32_t r = (uint32_t)(when % kHitRing);
+  if (s.hit_cnt[r] >= kHitSlot) return false;
+  HitEnt& e = s.hit[r][s.hit_cnt[r]++];
+  e.warp = warp;
+  e.slot = slot;
+  e.kind = kind;
+  e.pad = 0;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// L1 data cache (sectored, lane-parallel probe over the ways of a set)
+template <class P>
+SIM_HDI int l1_find(const SMState& s, const CacheGeom& g, uint32_t set, uint64_t line) {
+  const L1Line* base = &s.l1[set * g.assoc];
+  const int assoc = (int)g.assoc;
+  if (assoc <= 64) {
+    uint64_t m = P::ballot(assoc, [&](int w) { return base[w].valid && base[w].tag == line; });
+    return m ? ffs64(m) : -1;
+  }
+  for (int b = 0; b < assoc; b += 64) {
+    int n = amin(64, assoc - b);
+    uint64_t m = P::ballot(n, [&](int w) { return base[b + w].valid && base[b + w].tag == line; });
+    if (m) return b + ffs64(m);
+  }
+  return -1;
+}
+
+template <class P>
+SIM_HDI int l1_victim(const SMState& s, const CacheGeom& g, uint32_t set) {
+  const L1Line* base = &s.l1[set * g.assoc];
+  // invalid way first (lowest index), else smallest stamp (LRU or FIFO)
+  int v = P::argmin((int)g.assoc, [&](int w) -> uint64_t {
+    return base[w].valid ? (1ull << 40) | base[w].lru : (uint64_t)w;
+  });
+  return v;
+}
+
+// fill sectors of a line into L1 (allocate-on-fill) and wake waiters
+template <class P>
+SIM_HDI void l1_fill(SMState& s, const SmCtx& x, uint64_t line, uint8_t sectors, uint64_t now) {
+  const SimCfg& c = *x.cfg;
+  const CacheGeom g = l1_geom(c, *x.k);
+  if (!g.disabled) {
+    uint32_t set = cache_set_index(g, line);
+    int w = l1_find<P>(s, g, set, line);
+    if (w < 0) {
+      w = l1_victim<P>(s, g, set);
+      L1Line& L = s.l1[set * g.assoc + w];
+      L.tag = line;
+      L.valid = 0;
+      L.lru = ++s.l1_stamp;
+    }
+    L1Line& L = s.l1[set * g.assoc + w];
+    L.valid |= sectors;
+    if (g.repl == REPL_LRU) L.lru = ++s.l1_stamp;
+  }
+  // mshr bookkeeping
+  int mi = P::argmin((int)c.l1.mshr_entries, [&](int i) -> uint64_t {
+    return (s.mshr[i].valid && s.mshr[i].line == line) ? (uint64_t)i : ~0ull;
+  });
+  if (mi >= 0) {
+    s.mshr[mi].requested &= (uint8_t)~sectors;
+    if (s.mshr[mi].requested == 0) s.mshr[mi].valid = 0;
+  }
+  // wake waiters whose sectors are now all present (lane-parallel scan)
+  const uint32_t np = s.n_pend;
+  for (uint32_t b = 0; b < np; b += 64) {
+    int n = (int)amin<uint32_t>(64, np - b);
+    uint64_t m = P::ballot(n, [&](int i) {
+      const L1Pend& e = s.pend[b + i];
+      return e.valid && e.line == line && (e.need & sectors) != 0;
+    });
+    while (m) {
+      int i = ffs64(m);
+      m &= m - 1;
+      L1Pend& e = s.pend[b + i];
+      e.need &= (uint8_t)~sectors;
+      if (e.need) continue;
+      e.valid = 0;
+      if (--s.w_slot_pend[e.warp][e.slot] == 0) sm_load_slot_done(s, e.warp, e.slot, now);
+    }
+  }
+  // compact the pending table tail
+  while (s.n_pend && !s.pend[s.n_pend - 1].valid) s.n_pend--;
+}
+
+// consume at most one arrived packet per cycle (response FIFO)
+template <class P>
+SIM_HDI void sm_receive(SMState& s, const SmCtx& x, uint64_t now) {
+  const SimCfg& c = *x.cfg;
+  if (s.inq_n == 0) return;
+  const Pkt& p = s.inq[s.inq_head];
+  if (p.t > now * c.per_core) return;
+  Pkt q = p;
+  s.inq_head = (s.inq_head + 1) % kInQ;
+  s.inq_n--;
+  s.outstanding--;
+  s.st.pkts_in++;
+  s.st.bytes_in += q.size;
+  if (q.type == P_WR_ACK) {
+    uint32_t w = q.tag & 0xff;
+    s.w_stores[w]--;
+    s.last_progress = now;
+  } else if (q.tag & 0x80000000u) {  // direct (bypass / atomic) load access
+    uint32_t w = q.tag & 0xff, sl = (q.tag >> 8) & 0xff;
+    if (--s.w_slot_pend[w][sl] == 0) sm_load_slot_done(s, w, sl, now);
+  } else {
+    l1_fill<P>(s, x, q.addr, q.sectors, now);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LD/ST unit: processes the coalesced accesses of one warp instruction
+SIM_HDI uint32_t l1_stat_type(uint8_t space, bool write, bool atomic) {
+  if (atomic) return L1T_ATOMIC;
+  if (space == S_LOCAL) return write ? L1T_LOCAL_W : L1T_LOCAL_R;
+  return write ? L1T_GLOBAL_W : L1T_GLOBAL_R;
+}
+
+template <class P>
+SIM_HDI void sm_ldst(SMState& s, const SmCtx& x, uint64_t now) {
+  const SimCfg& c = *x.cfg;
+  LdstState& u = s.ldst;
+  if (!u.busy) return;
+  const TInst& in = u.inst;
+  const uint32_t w = u.warp;
+  if (in.space == S_SHARED) {
+    // bank-conflict serialisation: nacc == conflict degree (precomputed)
+    uint32_t deg = in.width ? in.width : 1;
+    if ((uint32_t)(now - u.start) + 1 < deg) return;
+    uint8_t kind = (in.cls == OC_STORE) ? 1 : 0;
+    if (!hit_push(s, now + c.smem_latency, (uint8_t)w, u.slot, kind)) return;
+    s.st.shmem_acc++;
+    s.st.shmem_conflict_cycles += deg - 1;
+    u.busy = 0;
+    return;
+  }
+  const bool is_store = in.cls == OC_STORE;
+  const bool atomic = (in.flags & F_ATOMIC) != 0;
+  const CacheGeom g = l1_geom(c, *x.k);
+  const bool bypass = atomic || (in.flags & F_BYPASS_L1) || c.gmem_skip_l1 || g.disabled;
+  const uint32_t nacc = in.width;
+  const uint32_t stype = l1_stat_type(in.space, is_store, atomic);
+  uint32_t banks_used = 0;
+  uint32_t processed = 0;
+  while (u.next < nacc && processed < c.l1_banks) {
+    const TAcc a = x.acc[in.mem + u.next];
+    uint32_t bbit = 1u << (a.bank & 31);
+    if (banks_used & bbit) break;  // L1 bank conflict: next cycle
+    if (is_store) {
+      if (!sm_can_send(s, c)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+      sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
+      s.w_stores[w]++;
+      if (!bypass && g.wpolicy == WP_WRITE_EVICT) {
+        uint32_t set = cache_set_index(g, a.line);
+        int way = l1_find<P>(s, g, set, a.line);
+        if (way >= 0) s.l1[set * g.assoc + way].valid &= (uint8_t)~a.sectors;
+      }
+      s.st.l1[stype][bypass ? L1O_BYPASS : L1O_MISS]++;
+    } else if (bypass) {
+      if (!sm_can_send(s, c)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+      uint32_t tag = 0x80000000u | (u.slot << 8) | w;
+      sm_send(s, c, atomic ? P_ATOM : P_RD, a.line, a.sectors, a.bytes, tag);
+      s.st.l1[stype][L1O_BYPASS]++;
+    } else {
+      uint32_t set = cache_set_index(g, a.line);
+      int way = l1_find<P>(s, g, set, a.line);
+      uint8_t have = way >= 0 ? s.l1[set * g.assoc + way].valid : 0;
+      uint8_t miss = a.sectors & (uint8_t)~have;
+      if (miss == 0) {
+        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, u.slot, 0)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+        if (g.repl == REPL_LRU) s.l1[set * g.assoc + way].lru = ++s.l1_stamp;
+        s.st.l1[stype][L1O_HIT]++;
+      } else {
+        if (s.n_pend >= (uint32_t)kMaxPend) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+        int mi = P::argmin((int)c.l1.mshr_entries, [&](int i) -> uint64_t {
+          return (s.mshr[i].valid && s.mshr[i].line == a.line) ? (uint64_t)i : ~0ull;
+        });
+        uint8_t need_req = miss;
+        if (mi >= 0) need_req = miss & (uint8_t)~s.mshr[mi].requested;
+        bool merged = (mi >= 0 && need_req == 0);
+        if (merged) {
+          if (s.mshr[mi].merges >= c.l1.mshr_merge) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+          s.mshr[mi].merges++;
+          s.st.l1[stype][L1O_MSHR_HIT]++;
+        } else {
+          if (!sm_can_send(s, c)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+          if (mi < 0) {
+            mi = P::argmin((int)c.l1.mshr_entries, [&](int i) -> uint64_t {
+              return s.mshr[i].valid ? ~0ull : (uint64_t)i;
+            });
+            if (mi < 0) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+            s.mshr[mi].valid = 1;
+            s.mshr[mi].line = a.line;
+            s.mshr[mi].requested = 0;
+            s.mshr[mi].merges = 0;
+          }
+          s.mshr[mi].requested |= need_req;
+          sm_send(s, c, P_RD, a.line, need_req, a.bytes, (uint32_t)mi);
+          s.st.l1[stype][L1O_MISS]++;
+        }
+        // register the waiter (first free entry)
+        uint32_t pi = s.n_pend;
+        for (uint32_t b = 0; b < s.n_pend; b += 64) {
+          int n = (int)amin<uint32_t>(64, s.n_pend - b);
+          uint64_t m = P::ballot(n, [&](int i) { return !s.pend[b + i].valid; });
+          if (m) { pi = b + ffs64(m); break; }
+        }
+        L1Pend& e = s.pend[pi];
+        e.line = a.line;
+        e.need = miss;
+        e.warp = (uint8_t)w;
+        e.slot = u.slot;
+        e.valid = 1;
+        if (pi == s.n_pend) s.n_pend++;
+      }
+    }
+    banks_used |= bbit;
+    u.next++;
+    processed++;
+  }
+  if (u.next >= nacc) {
+    if (is_store) {
+      s.w_inflight[w]--;  // store instruction leaves the pipeline; acks tracked in w_stores
+      s.last_progress = now;
+    }
+    u.busy = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// operand collectors -> functional units
+SIM_HDI uint32_t reg_bank(const SimCfg& c, uint32_t sched, uint32_t warp, uint32_t reg) {
+  uint32_t nb = c.reg_banks ? c.reg_banks : 1;
+  uint32_t per = (c.sub_core && c.n_sched) ? (nb / c.n_sched ? nb / c.n_sched : 1) : nb;
+  uint32_t base = (c.sub_core && c.n_sched) ? (sched * per) % nb : 0;
+  return base + (reg + warp) % per;
+}
+
+template <class P>
+SIM_HDI void sm_read_operands(SMState& s, const SimCfg& c) {
+  // each register bank serves reg_port_tp reads per cycle, oldest collector first
+  const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
+  for (uint32_t round = 0; round < c.reg_port_tp; ++round) {
+    uint32_t bank_busy = 0;
+    for (int k = 0; k < noc; ++k) {
+      // visit collectors oldest-first
+      int best = P::argmin(noc, [&](int i) -> uint64_t {
+        const OCUnit& o = s.oc[i];
+        if (!o.valid || o.nread == 0) return ~0ull;
+        bool ready = false;
+        for (int j = 0; j < 5; ++j)
+          if (o.banks[j] != 0xff && !(bank_busy >> o.banks[j] & 1u)) ready = true;
+        return ready ? (uint64_t)o.age : ~0ull;
+      });
+      if (best < 0) break;
+      OCUnit& o = s.oc[best];
+      for (int j = 0; j < 5; ++j) {
+        if (o.banks[j] != 0xff && !(bank_busy >> o.banks[j] & 1u)) {
+          bank_busy |= 1u << o.banks[j];
+          o.banks[j] = 0xff;
+          o.nread--;
+          s.st.rf_reads++;
+          break;  // one operand per collector per round
+        }
+      }
+    }
+  }
+}
+
+template <class P>
+SIM_HDI void sm_dispatch(SMState& s, const SimCfg& c, uint64_t now) {
+  const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
+  const uint32_t wbw = wb_width(c);
+  // oldest-first over ready collectors
+  uint32_t tried = 0;
+  for (int k = 0; k < noc; ++k) {
+    int best = P::argmin(noc, [&](int i) -> uint64_t {
+      const OCUnit& o = s.oc[i];
+      if (!o.valid || o.nread != 0 || (tried >> i & 1u)) return ~0ull;
+      return (uint64_t)o.age;
+    });
+    if (best < 0) break;
+    tried |= 1u << best;
+    OCUnit& o = s.oc[best];
+    const uint32_t u = o.unit;
+    if (u == U_MEM) {
+      if (s.ldst.busy) continue;
+      const TInst& in = o.inst;
+      // loads need a slot: allocated at issue (slot id carried in pad of OC)
+      s.ldst.inst = in;
+      s.ldst.busy = 1;
+      s.ldst.warp = o.warp;
+      s.ldst.slot = o.pad[0];
+      s.ldst.next = 0;
+      s.ldst.start = (uint32_t)now;
+      s.st.mem_insn++;
+      o.valid = 0;
+      continue;
+    }
+    uint32_t cnt = c.unit_count[u] ? c.unit_count[u] : 1;
+    uint32_t phys = o.sched % cnt;
+    if (phys >= (uint32_t)kMaxSched) phys %= kMaxSched;
+    uint32_t nf = s.fu_next[u][phys];
+    if ((int32_t)(nf - (uint32_t)now) > 0) continue;  // initiation interval
+    uint32_t lat = o.inst.lat ? o.inst.lat : 1;
+    if (lat >= (uint32_t)kWbRing) lat = kWbRing - 1;
+    uint32_t slot = (uint32_t)((now + lat) % kWbRing);
+    if (s.wb_cnt[slot] >= wbw) { s.st.pipe_stall++; continue; }  // result bus busy
+    WbEnt& e = s.wb[slot][s.wb_cnt[slot]++];
+    e.warp = o.warp;
+    e.dst0 = o.inst.dst[0];
+    e.dst1 = o.inst.dst[1];
+    e.pad = 0;
+    s.fu_next[u][phys] = (uint32_t)now + (o.inst.ii ? o.inst.ii : 1);
+    o.valid = 0;
+  }
+}
+
+template <class P>
+SIM_HDI void sm_alloc_collectors(SMState& s, const SimCfg& c) {
+  const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
+  const uint32_t nsched = c.n_sched;
+  const uint32_t per = (c.sub_core && nsched) ? (noc / nsched ? noc / nsched : 1) : (uint32_t)noc;
+  for (uint32_t sc = 0; sc < nsched; ++sc) {
+    for (uint32_t u = 0; u < U_COUNT; ++u) {
+      IdOc& r = s.idoc[sc][u];
+      if (!r.valid) continue;
+      // free collector in this scheduler's group
+      uint32_t lo = c.sub_core ? (sc * per) % noc : 0;
+      uint32_t hi = c.sub_core ? lo + per : (uint32_t)noc;
+      if (hi > (uint32_t)noc) hi = noc;
+      int f = -1;
+      for (uint32_t i = lo; i < hi; ++i)
+        if (!s.oc[i].valid) { f = (int)i; break; }
+      if (f < 0) continue;
+      OCUnit& o = s.oc[f];
+      o.inst = r.inst;
+      o.valid = 1;
+      o.warp = r.warp;
+      o.sched = (uint8_t)sc;
+      o.unit = (uint8_t)u;
+      o.pad[0] = r.pad[0];  // load slot
+      o.age = r.widx;
+      o.nread = 0;
+      for (int j = 0; j < 5; ++j) {
+        uint8_t reg = r.inst.src[j];
+        if (reg) {
+          o.banks[j] = (uint8_t)reg_bank(c, sc, r.warp, reg - 1);
+          o.nread++;
+        } else {
+          o.banks[j] = 0xff;
+        }
+      }
+      r.valid = 0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// issue
+template <class P>
+SIM_HDI void sm_barrier_check(SMState& s, uint32_t cta, const KernelDesc& k) {
+  uint32_t live = s.cta_live[cta] - s.cta_nexit[cta];
+  if (s.cta_bar[cta] > 0 && s.cta_bar[cta] >= live) {
+    uint32_t base = cta * k.warps_per_cta;
+    for (uint32_t w = base; w < base + k.warps_per_cta && w < (uint32_t)kMaxWarps; ++w)
+      s.w_flags[w] &= (uint8_t)~WF_BARRIER;
+    s.cta_bar[cta] = 0;
+  }
+}
+
+template <class P>
+SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
+  const SimCfg& c = *x.cfg;
+  const KernelDesc& k = *x.k;
+  const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
+  const uint32_t nsched = c.n_sched ? c.n_sched : 1;
+  // readiness of every warp (lane-parallel)
+  uint64_t ready = P::ballot(nw, [&](int w) -> bool {
+    uint8_t f = s.w_flags[w];
+    if (!(f & WF_ACTIVE) || (f & (WF_EXITING | WF_BARRIER | WF_MEMBAR | WF_WAITCNT))) return false;
+    if (s.w_ibuf[w] == 0) return false;
+    const TInst& in = s.w_win[w][s.w_head[w] % kWin];
+    const uint64_t* sb = s.w_sb[w];
+    for (int j = 0; j < 5; ++j)
+      if (sb_test(sb, in.src[j])) return false;
+    if (sb_test(sb, in.dst[0]) || sb_test(sb, in.dst[1])) return false;
+    uint32_t u = unit_of(c, in.cls);
+    uint32_t sc = (uint32_t)w % nsched;
+    if (in.cls == OC_EXIT || in.cls == OC_BARRIER || in.cls == OC_MEMBAR || in.cls == OC_NOP ||
+        (in.flags & F_WAITCNT))
+      return true;  // handled at issue, no pipeline register needed
+    if (s.idoc[sc][u].valid) return false;
+    if (u == U_MEM && in.cls == OC_LOAD && s.w_slot_used[w] == 0xff) return false;
+    return true;
+  });
+  uint64_t live = P::ballot(nw, [&](int w) { return (s.w_flags[w] & WF_ACTIVE) != 0; });
+  bool issued_any = false;
+  for (uint32_t sc = 0; sc < nsched; ++sc) {
+    // warps of this scheduler
+    uint64_t mine = 0;
+    for (int w = (int)sc; w < nw; w += (int)nsched) mine |= 1ull << w;
+    uint64_t cand = ready & mine;
+    if (!cand) {
+      if (live & mine) s.st.issue_stall_idle++;
+      continue;
+    }
+    int pick = -1;
+    uint32_t last = s.sched_last[sc];
+    switch (c.sched_policy) {
+      case SCHED_GTO:
+      case SCHED_TWO_LEVEL:
+        if (last < (uint32_t)nw && (cand >> last & 1ull)) { pick = (int)last; break; }
+        [[fallthrough]];
+      case SCHED_OLDEST:
+        pick = P::argmin(nw, [&](int w) -> uint64_t {
+          return (cand >> w & 1ull) ? ((uint64_t)s.w_age[w] << 8 | (uint64_t)w) : ~0ull;
+        });
+        break;
+      case SCHED_RRR: {
+        uint32_t start = (uint32_t)(now % (uint64_t)nw);
+        uint64_t r = rotr64(cand, start, (unsigned)nw);
+        pick = (int)((ffs64(r) + start) % (uint32_t)nw);
+        break;
+      }
+      default: {  // LRR: first ready warp after the last issued one
+        uint32_t start = (last + 1) % (uint32_t)nw;
+        uint64_t r = rotr64(cand, start, (unsigned)nw);
+        pick = (int)((ffs64(r) + start) % (uint32_t)nw);
+        break;
+      }
+    }
+    const uint32_t w = (uint32_t)pick;
+    s.sched_last[sc] = w;
+    const TInst in = s.w_win[w][s.w_head[w] % kWin];
+    s.w_head[w]++;
+    s.w_ibuf[w]--;
+    issued_any = true;
+    // stats: instruction counts at issue (reference counts active threads,
+    // shader.cc:1911)
+    s.st.warp_insn++;
+    s.st.thread_insn += (uint64_t)popc64(in.mask);
+    s.st.cls_insn[in.cls < OC_COUNT ? in.cls : OC_ALU]++;
+    s.last_progress = now;
+    uint32_t cta = s.w_cta[w];
+    if (in.cls == OC_EXIT) {
+      // lanes retire; the warp ends only when EXIT is its last instruction
+      // (reference checkExecutionStatusAndUpdate, trace_driven.cc:588-606)
+      if (s.w_head[w] >= s.w_end[w]) {
+        s.w_flags[w] |= WF_EXITING;
+        s.cta_nexit[cta]++;
+        sm_barrier_check<P>(s, cta, k);
+      }
+      continue;
+    }
+    if (in.cls == OC_BARRIER) {
+      s.w_flags[w] |= WF_BARRIER;
+      s.cta_bar[cta]++;
+      sm_barrier_check<P>(s, cta, k);
+      continue;
+    }
+    if (in.cls == OC_MEMBAR) {
+      if (s.w_stores[w]) s.w_flags[w] |= WF_MEMBAR;
+      continue;
+    }
+    if (in.flags & F_WAITCNT) {
+      if (s.w_stores[w] || s.w_loads[w]) s.w_flags[w] |= WF_WAITCNT;
+      continue;
+    }
+    if (in.cls == OC_NOP) continue;
+    const uint32_t u = unit_of(c, in.cls);
+    IdOc& r = s.idoc[sc][u];
+    r.inst = in;
+    r.valid = 1;
+    r.warp = (uint8_t)w;
+    r.widx = ++s.age_ctr;
+    r.pad[0] = 0xff;
+    s.w_inflight[w]++;
+    if (in.cls == OC_LOAD) {
+      // allocate a load slot; scoreboard reserves destination registers
+      uint8_t used = s.w_slot_used[w];
+      uint32_t sl = (uint32_t)ffs64((uint64_t)(uint8_t)~used);
+      s.w_slot_used[w] = (uint8_t)(used | (1u << sl));
+      s.w_loads[w]++;
+      uint32_t nacc = (in.space == S_SHARED) ? 1u : (uint32_t)in.width;
+      if (nacc == 0) nacc = 1;
+      s.w_slot_pend[w][sl] = (uint16_t)nacc;
+      s.w_slot_dst[w][sl][0] = in.dst[0];
+      s.w_slot_dst[w][sl][1] = in.dst[1];
+      r.pad[0] = (uint8_t)sl;
+      if (in.space != S_SHARED && in.width == 0) {
+        // memory instruction without any active access: completes via ring
+        s.w_slot_pend[w][sl] = 1;
+        r.inst.space = S_SHARED;
+        r.inst.width = 1;
+      }
+    } else if (in.cls == OC_STORE && in.space != S_SHARED && in.width == 0) {
+      r.inst.space = S_SHARED;
+      r.inst.width = 1;
+    }
+    sb_set(s.w_sb[w], in.dst[0]);
+    sb_set(s.w_sb[w], in.dst[1]);
+  }
+  if (issued_any) s.st.busy_cycles++;
+}
+
+// ---------------------------------------------------------------------------
+// fetch/decode: refill the instruction buffer of up to fetch_throughput
+// warps whose buffer is empty (round-robin), perfect instruction cache
+template <class P>
+SIM_HDI void sm_fetch(SMState& s, const SimCfg& c) {
+  const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
+  uint64_t need = P::ballot(nw, [&](int w) {
+    uint8_t f = s.w_flags[w];
+    return (f & WF_ACTIVE) && !(f & WF_EXITING) && s.w_ibuf[w] == 0 && s.w_next[w] < s.w_end[w];
+  });
+  uint32_t start = s.fetch_rr % (uint32_t)nw;
+  uint64_t r = rotr64(need, start, (unsigned)nw);
+  for (uint32_t i = 0; i < c.fetch_throughput && r; ++i) {
+    int b = ffs64(r);
+    r &= r - 1;
+    uint32_t w = (uint32_t)(b + start) % (uint32_t)nw;
+    uint32_t avail = s.w_end[w] - s.w_next[w];
+    uint32_t n = avail < (uint32_t)kIbuf ? avail : (uint32_t)kIbuf;
+    s.w_next[w] += n;
+    s.w_ibuf[w] = (uint8_t)n;
+    s.fetch_rr = w + 1;
+  }
+}
+
+// stream exhausted without explicit EXIT -> treat as exit
+// warp retirement and CTA completion
+template <class P>
+SIM_HDI void sm_retire(SMState& s, const SmCtx& x, uint64_t now) {
+  const SimCfg& c = *x.cfg;
+  const KernelDesc& k = *x.k;
+  const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
+  uint64_t done = P::ballot(nw, [&](int w) {
+    uint8_t f = s.w_flags[w];
+    if (!(f & WF_ACTIVE)) return false;
+    bool drained = s.w_head[w] >= s.w_end[w] && s.w_ibuf[w] == 0;
+    return drained && s.w_inflight[w] == 0 && s.w_stores[w] == 0 && s.w_loads[w] == 0;
+  });
+  // release membar / waitcnt waits
+  P::each(nw, [&](int w) {
+    uint8_t f = s.w_flags[w];
+    if ((f & WF_MEMBAR) && s.w_stores[w] == 0) s.w_flags[w] = f & (uint8_t)~WF_MEMBAR;
+    f = s.w_flags[w];
+    if ((f & WF_WAITCNT) && s.w_stores[w] == 0 && s.w_loads[w] == 0) s.w_flags[w] = f & (uint8_t)~WF_WAITCNT;
+  });
+  P::sync();
+  while (done) {
+    int w = ffs64(done);
+    done &= done - 1;
+    uint32_t cta = s.w_cta[w];
+    if (!(s.w_flags[w] & WF_EXITING)) s.cta_nexit[cta]++;  // implicit exit at stream end
+    s.w_flags[w] = 0;
+    s.st.warps_done++;
+    s.cta_live[cta]--;
+    s.cta_nexit[cta]--;
+    if (s.cta_live[cta] == 0) {
+      s.cta_valid[cta] = 0;
+      s.n_cta_active--;
+      s.st.ctas_done++;
+    } else {
+      sm_barrier_check<P>(s, cta, k);
+    }
+    s.last_progress = now;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launch a CTA into slot `slot`
+template <class P>
+SIM_HDI void sm_launch_cta(SMState& s, const SmCtx& x, uint32_t slot, uint32_t cta_id) {
+  const KernelDesc& k = *x.k;
+  const uint32_t wpc = k.warps_per_cta;
+  const uint32_t base = slot * wpc;
+  s.cta_valid[slot] = 1;
+  s.cta_id[slot] = cta_id;
+  s.cta_live[slot] = (uint8_t)wpc;
+  s.cta_bar[slot] = 0;
+  s.cta_nexit[slot] = 0;
+  s.n_cta_active++;
+  uint32_t age0 = s.age_ctr;
+  s.age_ctr += wpc;
+  P::each((int)wpc, [&](int i) {
+    uint32_t w = base + (uint32_t)i;
+    WStream ws = k.streams[(uint64_t)cta_id * wpc + (uint32_t)i];
+    s.w_next[w] = ws.begin;
+    s.w_head[w] = ws.begin;
+    s.w_wfill[w] = ws.begin;
+    s.w_end[w] = ws.begin + ws.count;
+    s.w_age[w] = age0 + (uint32_t)i;
+    s.w_flags[w] = WF_ACTIVE;
+    s.w_ibuf[w] = 0;
+    s.w_cta[w] = (uint8_t)slot;
+    s.w_inflight[w] = 0;
+    s.w_stores[w] = 0;
+    s.w_loads[w] = 0;
+    s.w_slot_used[w] = 0;
+    s.w_sb[w][0] = s.w_sb[w][1] = s.w_sb[w][2] = s.w_sb[w][3] = 0;
+  });
+  P::sync();
+}
+
+// refill the per-warp instruction windows from the kernel trace (HBM).
+// Done once per epoch: a warp can consume at most `epoch` instructions per
+// epoch, so kWin >= epoch + kIbuf guarantees the window never runs dry.
+template <class P>
+SIM_HDI void sm_refill_window(SMState& s, const SimCfg& c, const KernelDesc& k) {
+  const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
+  P::each(nw, [&](int w) {
+    if (!(s.w_flags[w] & WF_ACTIVE)) return;
+    uint32_t lim = s.w_head[w] + kWin;
+    if (lim > s.w_end[w]) lim = s.w_end[w];
+    for (uint32_t i = s.w_wfill[w]; i < lim; ++i) s.w_win[w][i % kWin] = k.insts[i];
+    if (lim > s.w_wfill[w]) s.w_wfill[w] = lim;
+  });
+  P::sync();
+}
+
+// one simulated core cycle
+template <class P>
+SIM_HDI void sm_cycle(SMState& s, const SmCtx& x, uint64_t now) {
+  const SimCfg& c = *x.cfg;
+  sm_receive<P>(s, x, now);
+  sm_writeback<P>(s, c, now);
+  sm_hit_complete<P>(s, now);
+  sm_ldst<P>(s, x, now);
+  sm_dispatch<P>(s, c, now);
+  sm_read_operands<P>(s, c);
+  sm_alloc_collectors<P>(s, c);
+  sm_issue<P>(s, x, now);
+  sm_fetch<P>(s, c);
+  sm_retire<P>(s, x, now);
+  sm_inject<P>(s, x, now);
+  if (s.n_cta_active) {
+    s.st.active_cycles++;
+    s.st.occupancy_acc += P::sum((int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps),
+                                 [&](int w) -> uint32_t { return (s.w_flags[w] & WF_ACTIVE) ? 1u : 0u; });
+  }
+}
+
+// true if the SM holds no work at all (no CTAs, nothing in flight)
+SIM_HDI bool sm_idle(const SMState& s) {
+  return s.n_cta_active == 0 && s.outq_n == 0 && s.outstanding == 0 && !s.ldst.busy;
+}
+
+}  // namespace asim

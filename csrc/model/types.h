@@ -1,0 +1,152 @@
+// Device-resident data contracts shared by the CPU and GPU engines.
+//
+// The reference keeps each dynamic instruction as a heap-allocated
+// `inst_trace_t` with a std::string opcode and a heap address block
+// (trace_parser.h:55-79) and re-decodes it into a `trace_warp_inst_t` at issue
+// (trace_driven.cc:151-381).  Here the whole kernel trace is decoded ONCE on
+// the host into fixed 32-byte records that live in HBM for the duration of
+// the simulated kernel (288 GB/GPU holds ~9e9 of them), so the cycle engine
+// never parses text or allocates.
+#pragma once
+#include "hd.h"
+
+namespace asim {
+
+// ---- micro-architectural operation classes (reference: uarch_op_t,
+// abstract_hardware_model.h:108-138, plus the trace-mode category map of
+// ISA_Def/*_opcode.h) ----
+enum OpCls : uint8_t {
+  OC_ALU = 0,   // generic ALU (MOV, S2R, LDC, SHFL, ...)
+  OC_SP,        // single precision FP
+  OC_DP,        // double precision FP
+  OC_SFU,       // transcendental / MUFU
+  OC_TENSOR,    // matrix core (HMMA / MFMA)
+  OC_INTP,      // integer pipe
+  OC_LOAD,      // memory read (also atomics)
+  OC_STORE,     // memory write
+  OC_BRANCH,    // control flow
+  OC_BARRIER,   // CTA barrier
+  OC_MEMBAR,    // memory fence
+  OC_EXIT,      // warp exit
+  OC_NOP,
+  OC_SPEC1,     // specialized units 1..8 (reference SPEC_UNIT_START_ID)
+  OC_SPEC2,
+  OC_SPEC3,
+  OC_SPEC4,
+  OC_SPEC5,
+  OC_SPEC6,
+  OC_SPEC7,
+  OC_SPEC8,
+  OC_COUNT
+};
+
+// execution unit types (one pipeline register set each)
+enum Unit : uint8_t {
+  U_SP = 0,
+  U_DP,
+  U_INT,
+  U_SFU,
+  U_TENSOR,
+  U_MEM,
+  U_SPEC1,  // .. U_SPEC8
+  U_COUNT = U_SPEC1 + 8
+};
+
+enum Space : uint8_t {
+  S_NONE = 0,
+  S_GLOBAL,
+  S_LOCAL,
+  S_SHARED,
+  S_CONST,
+  S_TEX,
+  S_PARAM,
+};
+
+enum InstFlags : uint8_t {
+  F_BYPASS_L1 = 1,  // LDG.E.STRONG.GPU etc: served at L2 (trace_driven.cc:266-270)
+  F_ATOMIC = 2,     // ATOM/RED/ATOMG: performed at L2
+  F_MEM = 4,        // has an address record
+  F_WAITCNT = 8,    // CDNA s_waitcnt: wait for all outstanding memory of the wave
+};
+
+// 32-byte decoded dynamic warp instruction.
+struct TInst {
+  uint32_t pc;
+  uint32_t mem;     // index into TMem table or kNoMem
+  uint64_t mask;    // active-thread mask (32 or 64 lanes)
+  uint16_t opcode;  // global ISA opcode id (isa_tables) for stats/power
+  uint8_t cls;      // OpCls
+  uint8_t space;    // Space
+  uint8_t dst[2];   // register+1, 0 = none  (reference adds 1: trace_driven.cc:225-240)
+  uint8_t src[5];   // register+1, 0 = none  (5 sources: fixes reference defect D3)
+  uint8_t width;    // bytes per thread for memory ops
+  uint16_t lat;     // pipeline latency (cycles)
+  uint8_t ii;       // initiation interval
+  uint8_t flags;    // InstFlags
+};
+static_assert(sizeof(TInst) == 32, "TInst must stay 32 bytes");
+constexpr uint32_t kNoMem = 0xffffffffu;
+
+// Per-instruction address record.  Addresses of active lanes are either
+// base + k*stride (k = rank among active lanes) or an explicit list (one
+// u64 per ACTIVE lane, in lane order) starting at addrs[list].
+struct TMem {
+  uint64_t base;
+  int32_t stride;
+  uint32_t list;  // kNoMem -> base/stride form
+};
+static_assert(sizeof(TMem) == 16, "TMem must stay 16 bytes");
+
+// warp instruction stream of one warp of one CTA: [begin, begin+count)
+struct WStream {
+  uint32_t begin;
+  uint32_t count;
+};
+
+// Interconnect packet (32 B).  Time stamps are femtoseconds so that the
+// four clock domains (core/icnt/L2/DRAM, reference gpu-sim.cc:1047-1062) are
+// exact integers.
+enum PktType : uint8_t {
+  P_RD = 1,     // read request (sector mask)
+  P_WR,         // write request
+  P_ATOM,       // atomic request (returns data)
+  P_RD_REPLY,
+  P_WR_ACK,
+  P_ATOM_REPLY,
+};
+struct Pkt {
+  uint64_t addr;  // 128B-line aligned byte address
+  uint64_t t;     // time the packet becomes visible at its destination (fs)
+  uint32_t tag;   // requester cookie (SM side: load slot / mshr)
+  uint16_t src;
+  uint16_t dst;
+  uint16_t size;  // bytes on the wire
+  uint8_t type;
+  uint8_t sectors;  // 32B-sector mask within the line
+  uint32_t aux;
+};
+static_assert(sizeof(Pkt) == 32, "Pkt must stay 32 bytes");
+
+// Device view of one simulated kernel.
+struct KernelDesc {
+  uint32_t uid;
+  uint32_t n_cta;
+  uint32_t warps_per_cta;
+  uint32_t threads_per_cta;
+  uint32_t shmem_per_cta;
+  uint32_t regs_per_thread;
+  uint32_t cta_per_sm;  // resource-limited CTA slots per SM for this kernel
+  uint32_t grid[3];
+  uint32_t block[3];
+  uint32_t stream;
+  uint32_t l1_sets, l1_assoc;  // adaptive L1 geometry chosen for this kernel
+  uint64_t shmem_base;
+  uint64_t local_base;
+  uint64_t n_insts;
+  const TInst* insts;
+  const TMem* mems;
+  const uint64_t* addrs;
+  const WStream* streams;  // [n_cta * warps_per_cta]
+};
+
+}  // namespace asim

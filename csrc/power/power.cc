@@ -1,0 +1,228 @@
+#include "power.h"
+
+#include <cmath>
+#include <cstdlib>
+#include <fstream>
+#include <regex>
+#include <sstream>
+
+namespace asim {
+
+const char* const kPwrActName[PA_COUNT] = {
+    "TOT_INST", "FP_INT", "IC_H", "IC_M", "DC_RH", "DC_RM", "DC_WH", "DC_WM", "CC_H", "CC_M",
+    "SHRD_ACC", "REG_RD", "REG_WR", "INT_ACC", "FP_ACC", "DP_ACC", "INT_MUL_ACC", "FP_MUL_ACC",
+    "FP_SQRT_ACC", "FP_LG_ACC", "FP_SIN_ACC", "FP_EXP_ACC", "DP_MUL_ACC", "TENSOR_ACC", "TEX_ACC",
+    "MEM_RD", "MEM_WR", "MEM_PRE", "L2_RH", "L2_RM", "L2_WH", "L2_WM", "NOC_A", "PIPE_A"};
+
+// Per-access base energies (nJ) for a 12-16 nm class GPU.  These play the
+// role of McPAT's per-access energies; the XML scaling factors calibrate
+// them (util: accel_sim_framework_distributed_amd.power.calibrate).
+double PowerModel::base_nj(int act) {
+  static const double e[PA_COUNT] = {
+      0.0100,  // TOT_INST   instruction buffer per warp instruction
+      0.0250,  // FP_INT     scheduler per non-memory warp instruction
+      0.0150,  // IC_H
+      0.0500,  // IC_M
+      0.0450,  // DC_RH      L1 read hit (per 128B access)
+      0.0600,  // DC_RM
+      0.0450,  // DC_WH
+      0.0550,  // DC_WM
+      0.0080,  // CC_H
+      0.0300,  // CC_M
+      0.0300,  // SHRD_ACC
+      0.0040,  // REG_RD     per warp operand read
+      0.0050,  // REG_WR
+      0.0015,  // INT_ACC    per lane op
+      0.0030,  // FP_ACC
+      0.0080,  // DP_ACC
+      0.0040,  // INT_MUL_ACC
+      0.0040,  // FP_MUL_ACC
+      0.0120,  // FP_SQRT_ACC
+      0.0120,  // FP_LG_ACC
+      0.0120,  // FP_SIN_ACC
+      0.0120,  // FP_EXP_ACC
+      0.0150,  // DP_MUL_ACC
+      0.0600,  // TENSOR_ACC
+      0.0400,  // TEX_ACC
+      0.4000,  // MEM_RD     per 32B DRAM access
+      0.4500,  // MEM_WR
+      0.1000,  // MEM_PRE
+      0.0600,  // L2_RH
+      0.0800,  // L2_RM
+      0.0600,  // L2_WH
+      0.0800,  // L2_WM
+      0.0250,  // NOC_A      per flit
+      0.0050,  // PIPE_A
+  };
+  return (act >= 0 && act < PA_COUNT) ? e[act] : 0.0;
+}
+
+bool PowerModel::load_xml(const std::string& path, std::string* err) {
+  std::ifstream f(path);
+  if (!f) {
+    if (err) *err = "cannot open " + path;
+    return false;
+  }
+  std::stringstream ss;
+  ss << f.rdbuf();
+  std::string s = ss.str();
+  std::regex re("<param\\s+name\\s*=\\s*\"([^\"]+)\"\\s+value\\s*=\\s*\"([^\"]*)\"");
+  for (auto it = std::sregex_iterator(s.begin(), s.end(), re); it != std::sregex_iterator(); ++it) {
+    const std::string k = (*it)[1], v = (*it)[2];
+    char* end = nullptr;
+    double x = strtod(v.c_str(), &end);
+    if (end != v.c_str()) p_[k] = x;
+  }
+  return true;
+}
+
+double PowerModel::param(const std::string& k, double dflt) const {
+  auto it = p_.find(k);
+  return it == p_.end() ? dflt : it->second;
+}
+
+std::vector<double> PowerModel::coefficients(double core_mhz) const {
+  // W contributed by one access per core cycle
+  std::vector<double> c(PA_COUNT);
+  for (int i = 0; i < PA_COUNT; ++i) c[i] = base_nj(i) * 1e-9 * param(kPwrActName[i], 1.0) * core_mhz * 1e6;
+  return c;
+}
+
+PowerReport PowerModel::compute(const Activity& a, double core_mhz, uint32_t n_sm) const {
+  PowerReport r;
+  const double cyc = a.cycles > 0 ? a.cycles : 1;
+  const auto coef = coefficients(core_mhz);
+  const double v2 = a.voltage * a.voltage;
+  for (int i = 0; i < PA_COUNT; ++i) {
+    r.dynamic_w[i] = coef[i] * (a.a[i] / cyc) * v2;
+    r.dynamic += r.dynamic_w[i];
+  }
+  r.constant = param("constant_power", 0);
+  r.idle = param("idle_core_power", 0) * a.idle_sms;
+  // categorical static power by active unit mix (reference
+  // calculate_static_power, gpgpu_sim_wrapper.cc:746-846)
+  std::string cat;
+  if (a.tensor_used) cat = "cat6";
+  else if (a.tex_used) cat = "cat5";
+  else if (a.sfu_used) cat = "cat4";
+  else if (a.dp_used) cat = "cat3";
+  else if (a.fp_used) cat = "cat2";
+  else if (a.int_used) cat = "cat1";
+  else cat = "light";
+  r.static_category = cat;
+  double lanes = a.avg_lanes > 1 ? a.avg_lanes : 1;
+  double busy_frac = n_sm ? std::max(0.0, 1.0 - a.idle_sms / n_sm) : 1.0;
+  r.static_w = (param("static_" + cat + "_flane", 0) + param("static_" + cat + "_addlane", 0) * (lanes - 1)) * busy_frac;
+  if (a.a[PA_SHRD_ACC] > 0) r.static_w += param("static_shared_flane", 0) * busy_frac;
+  if (a.a[PA_DC_RH] + a.a[PA_DC_RM] + a.a[PA_DC_WH] + a.a[PA_DC_WM] > 0) r.static_w += param("static_l1_flane", 0) * busy_frac;
+  if (a.a[PA_L2_RH] + a.a[PA_L2_RM] + a.a[PA_L2_WH] + a.a[PA_L2_WM] > 0) r.static_w += param("static_l2_flane", 0);
+  r.total = r.dynamic + r.static_w + r.constant + r.idle;
+  return r;
+}
+
+Activity PowerModel::activity_from_stats(const std::vector<SMStats>& dsm, const std::vector<MemStats>& dmem,
+                                         uint64_t cycles) {
+  Activity a;
+  a.cycles = (double)cycles;
+  double warp = 0, thread = 0, mem = 0, active = 0;
+  double cls[OC_COUNT] = {};
+  for (const auto& s : dsm) {
+    warp += s.warp_insn;
+    thread += s.thread_insn;
+    mem += s.mem_insn;
+    active += s.active_cycles;
+    for (int k = 0; k < OC_COUNT; ++k) cls[k] += s.cls_insn[k];
+    a.a[PA_DC_RH] += s.l1[L1T_GLOBAL_R][L1O_HIT] + s.l1[L1T_LOCAL_R][L1O_HIT];
+    a.a[PA_DC_RM] += s.l1[L1T_GLOBAL_R][L1O_MISS] + s.l1[L1T_LOCAL_R][L1O_MISS] + s.l1[L1T_GLOBAL_R][L1O_MSHR_HIT] +
+                     s.l1[L1T_LOCAL_R][L1O_MSHR_HIT] + s.l1[L1T_GLOBAL_R][L1O_BYPASS];
+    a.a[PA_DC_WM] += s.l1[L1T_GLOBAL_W][L1O_MISS] + s.l1[L1T_LOCAL_W][L1O_MISS] + s.l1[L1T_GLOBAL_W][L1O_BYPASS] +
+                     s.l1[L1T_ATOMIC][L1O_BYPASS];
+    a.a[PA_SHRD_ACC] += s.shmem_acc;
+    a.a[PA_REG_RD] += s.rf_reads;
+    a.a[PA_REG_WR] += s.rf_writes;
+    a.a[PA_NOC_A] += s.pkts_out + s.pkts_in;
+  }
+  const double lanes = warp > 0 ? thread / warp : 0;
+  a.avg_lanes = lanes;
+  a.a[PA_TOT_INST] = warp;
+  a.a[PA_FP_INT] = warp - mem;
+  a.a[PA_IC_H] = warp;
+  a.a[PA_INT_ACC] = (cls[OC_INTP] + cls[OC_ALU]) * lanes;
+  a.a[PA_FP_ACC] = cls[OC_SP] * lanes;
+  a.a[PA_DP_ACC] = cls[OC_DP] * lanes;
+  a.a[PA_FP_EXP_ACC] = cls[OC_SFU] * lanes;
+  a.a[PA_TENSOR_ACC] = (cls[OC_TENSOR] + cls[OC_SPEC3]) * lanes;
+  a.a[PA_TEX_ACC] = cls[OC_SPEC2] * lanes;
+  a.a[PA_PIPE_A] = warp;
+  for (const auto& m : dmem) {
+    a.a[PA_MEM_RD] += m.dram_rd;
+    a.a[PA_MEM_WR] += m.dram_wr;
+    a.a[PA_MEM_PRE] += m.dram_pre;
+    a.a[PA_L2_RH] += m.l2[L2T_RD][L2O_HIT] + m.l2[L2T_ATOM][L2O_HIT];
+    a.a[PA_L2_RM] += m.l2[L2T_RD][L2O_MISS] + m.l2[L2T_RD][L2O_MSHR_HIT] + m.l2[L2T_ATOM][L2O_MISS];
+    a.a[PA_L2_WH] += m.l2[L2T_WR][L2O_HIT];
+    a.a[PA_L2_WM] += m.l2[L2T_WR][L2O_MISS];
+  }
+  a.int_used = cls[OC_INTP] + cls[OC_ALU] > 0;
+  a.fp_used = cls[OC_SP] > 0;
+  a.dp_used = cls[OC_DP] > 0;
+  a.sfu_used = cls[OC_SFU] > 0;
+  a.tex_used = cls[OC_SPEC2] > 0;
+  a.tensor_used = cls[OC_TENSOR] + cls[OC_SPEC3] > 0;
+  a.idle_sms = cycles ? (double)dsm.size() - active / (double)cycles : 0;
+  if (a.idle_sms < 0) a.idle_sms = 0;
+  return a;
+}
+
+bool PowerModel::activity_from_hw_csv(const std::string& csv, const std::string& bench, const std::string& kernel,
+                                      Activity& out, uint32_t n_sm) {
+  std::ifstream f(csv);
+  if (!f) return false;
+  std::string line;
+  std::getline(f, line);
+  std::vector<std::string> hdr;
+  {
+    std::stringstream ss(line);
+    std::string t;
+    while (std::getline(ss, t, ',')) hdr.push_back(t);
+  }
+  while (std::getline(f, line)) {
+    std::vector<std::string> v;
+    std::stringstream ss(line);
+    std::string t;
+    while (std::getline(ss, t, ',')) v.push_back(t);
+    if (v.size() < 2 || v[0] != bench || v[1] != kernel) continue;
+    Activity a;
+    auto get = [&](const char* name) -> double {
+      for (size_t i = 0; i < hdr.size() && i < v.size(); ++i)
+        if (hdr[i] == name) return atof(v[i].c_str());
+      return 0;
+    };
+    a.a[PA_DC_RH] = get("L1_RH");
+    a.a[PA_DC_RM] = get("L1_RM");
+    a.a[PA_DC_WH] = get("L1_WH");
+    a.a[PA_DC_WM] = get("L1_WM");
+    a.a[PA_CC_H] = get("CC_ACC");
+    a.a[PA_SHRD_ACC] = get("SHRD_ACC");
+    a.a[PA_MEM_RD] = get("DRAM_Rd");
+    a.a[PA_MEM_WR] = get("DRAM_Wr");
+    a.a[PA_L2_RH] = get("L2_RH");
+    a.a[PA_L2_RM] = get("L2_RM");
+    a.a[PA_L2_WH] = get("L2_WH");
+    a.a[PA_L2_WM] = get("L2_WM");
+    a.a[PA_NOC_A] = get("NOC");
+    a.cycles = get("Elapsed_Cycles");
+    a.idle_sms = get("Num_Idle_SMs");
+    a.voltage = get("Chip Voltage") > 0 ? get("Chip Voltage") : 1.0;
+    double duty = get("Pipeline_Duty");
+    a.a[PA_PIPE_A] = duty * a.cycles * (n_sm - a.idle_sms);
+    a.int_used = true;
+    a.fp_used = true;
+    a.avg_lanes = 32;
+    out = a;
+    return true;
+  }
+  return false;
+}
+
+}  // namespace asim

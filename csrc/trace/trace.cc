@@ -1,0 +1,952 @@
+#include "trace.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <stdexcept>
+#include <unordered_map>
+
+namespace asim {
+
+std::string trim_copy(const std::string& s);
+std::vector<std::string> split_commas(const std::string& s);
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// ISA tables
+struct SassRow {
+  const char* arch;
+  uint8_t cls;
+  const char* mnemonics;
+};
+const SassRow kSass[] = {
+#include "sass_isa.inc"
+};
+
+struct IsaDb {
+  std::vector<std::string> names;                 // opcode id -> mnemonic
+  std::unordered_map<std::string, uint16_t> ids;  // mnemonic -> id
+  std::map<std::string, std::unordered_map<std::string, uint8_t>> arch;  // family -> mnemonic -> cls
+  std::mutex mu;
+  uint16_t id_of(const std::string& m) {
+    auto it = ids.find(m);
+    if (it != ids.end()) return it->second;
+    uint16_t id = (uint16_t)names.size();
+    names.push_back(m);
+    ids[m] = id;
+    return id;
+  }
+  IsaDb() {
+    names.push_back("<none>");
+    for (const auto& r : kSass) {
+      std::istringstream in(r.mnemonics);
+      std::string m;
+      while (in >> m) {
+        arch[r.arch][m] = r.cls;
+        id_of(m);
+      }
+    }
+  }
+};
+IsaDb& isa() {
+  static IsaDb db;
+  return db;
+}
+
+const char* sass_family(uint32_t bv) {
+  if (bv < 50) return "kepler";
+  if (bv < 70) return "pascal";  // Maxwell / Pascal
+  if (bv < 75) return "volta";
+  if (bv < 80) return "turing";
+  return "ampere";  // Ampere / Ada / Hopper traces use the Ampere map
+}
+
+bool is_number(const std::string& s) {
+  if (s.empty()) return false;
+  for (char ch : s)
+    if (ch < '0' || ch > '9') return false;
+  return true;
+}
+
+std::vector<std::string> dot_tokens(const std::string& op) {
+  std::vector<std::string> t;
+  std::string cur;
+  for (char ch : op) {
+    if (ch == '.') {
+      if (!cur.empty()) t.push_back(cur);
+      cur.clear();
+    } else {
+      cur.push_back(ch);
+    }
+  }
+  if (!cur.empty()) t.push_back(cur);
+  return t;
+}
+
+uint8_t sass_width(const std::vector<std::string>& toks) {
+  for (size_t i = 1; i < toks.size(); ++i) {
+    const std::string& t = toks[i];
+    if (is_number(t)) return (uint8_t)std::max(1, atoi(t.c_str()) / 8);
+    if (t.size() > 1 && (t[0] == 'U' || t[0] == 'S') && is_number(t.substr(1)))
+      return (uint8_t)std::max(1, atoi(t.c_str() + 1) / 8);
+  }
+  return 4;
+}
+
+bool has_tok(const std::vector<std::string>& t, const char* s) {
+  for (auto& x : t)
+    if (x == s) return true;
+  return false;
+}
+
+OpInfo decode_sass(const std::string& op, uint32_t bv) {
+  OpInfo o{};
+  auto toks = dot_tokens(op);
+  const std::string m = toks.empty() ? std::string("NOP") : toks[0];
+  IsaDb& db = isa();
+  auto& fam = db.arch[sass_family(bv)];
+  auto it = fam.find(m);
+  o.known = it != fam.end();
+  o.cls = o.known ? it->second : (uint8_t)OC_ALU;
+  {
+    std::lock_guard<std::mutex> g(db.mu);
+    o.opcode = db.id_of(m);
+  }
+  o.space = S_NONE;
+  o.flags = 0;
+  o.width = 0;
+  o.half_ii = 0;
+  // memory semantics (reference trace_driven.cc:254-378)
+  if (m == "LDC") {
+    o.cls = OC_ALU;  // constant cache is perfect in the tested configs
+    o.space = S_CONST;
+  } else if (m == "LDG" || m == "LDL" || m == "LD") {
+    o.cls = OC_LOAD;
+    o.space = m == "LDL" ? S_LOCAL : S_GLOBAL;
+    o.width = sass_width(toks);
+    o.flags |= F_MEM;
+    if (has_tok(toks, "STRONG") && has_tok(toks, "GPU")) o.flags |= F_BYPASS_L1;
+    if (m == "LD") o.space = S_NONE;  // generic: resolved by address
+  } else if (m == "STG" || m == "STL" || m == "ST") {
+    o.cls = OC_STORE;
+    o.space = m == "STL" ? S_LOCAL : S_GLOBAL;
+    o.width = sass_width(toks);
+    o.flags |= F_MEM;
+    if (m == "ST") o.space = S_NONE;
+  } else if (m == "ATOM" || m == "ATOMG" || m == "RED") {
+    o.cls = OC_LOAD;
+    o.space = S_GLOBAL;
+    o.width = sass_width(toks);
+    o.flags |= F_MEM | F_ATOMIC | F_BYPASS_L1;
+  } else if (m == "LDS" || m == "LDSM" || m == "ATOMS") {
+    o.cls = OC_LOAD;
+    o.space = S_SHARED;
+    o.width = sass_width(toks);
+    o.flags |= F_MEM;
+  } else if (m == "STS") {
+    o.cls = OC_STORE;
+    o.space = S_SHARED;
+    o.width = sass_width(toks);
+    o.flags |= F_MEM;
+  } else if (m == "LDGSTS") {
+    // async global->shared copy: model as a global load (defect D5 in the
+    // reference leaves these unmodelled)
+    o.cls = OC_LOAD;
+    o.space = S_GLOBAL;
+    o.width = sass_width(toks);
+    o.flags |= F_MEM;
+  }
+  if (m == "HADD2" || m == "HADD2_32I" || m == "HFMA2" || m == "HFMA2_32I" || m == "HMUL2" || m == "HMUL2_32I" ||
+      m == "HSET2" || m == "HSETP2")
+    o.half_ii = 1;
+  return o;
+}
+
+bool starts(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }
+bool contains(const std::string& s, const char* p) { return s.find(p) != std::string::npos; }
+
+uint8_t cdna_width(const std::string& m) {
+  if (contains(m, "dwordx4") || contains(m, "b128")) return 16;
+  if (contains(m, "dwordx3") || contains(m, "b96")) return 12;
+  if (contains(m, "dwordx2") || contains(m, "b64")) return 8;
+  if (contains(m, "short") || contains(m, "b16") || contains(m, "u16") || contains(m, "i16")) return 2;
+  if (contains(m, "byte") || contains(m, "b8") || contains(m, "u8") || contains(m, "i8")) return 1;
+  return 4;
+}
+
+// CDNA4 (gfx950) instruction classes for native AMD traces
+OpInfo decode_cdna(const std::string& op0) {
+  OpInfo o{};
+  std::string m = op0;
+  for (auto& ch : m) ch = (char)tolower(ch);
+  IsaDb& db = isa();
+  {
+    std::lock_guard<std::mutex> g(db.mu);
+    o.opcode = db.id_of(m);
+  }
+  o.known = true;
+  o.cls = OC_SP;
+  o.space = S_NONE;
+  if (starts(m, "v_mfma") || starts(m, "v_smfmac")) {
+    o.cls = OC_TENSOR;
+  } else if (starts(m, "global_atomic") || starts(m, "buffer_atomic") || starts(m, "flat_atomic")) {
+    o.cls = OC_LOAD;
+    o.space = S_GLOBAL;
+    o.flags = F_MEM | F_ATOMIC | F_BYPASS_L1;
+    o.width = cdna_width(m);
+  } else if (starts(m, "global_load") || starts(m, "buffer_load") || starts(m, "flat_load") ||
+             starts(m, "scratch_load")) {
+    o.cls = OC_LOAD;
+    o.space = starts(m, "scratch") ? S_LOCAL : S_GLOBAL;
+    o.flags = F_MEM;
+    o.width = cdna_width(m);
+  } else if (starts(m, "global_store") || starts(m, "buffer_store") || starts(m, "flat_store") ||
+             starts(m, "scratch_store")) {
+    o.cls = OC_STORE;
+    o.space = starts(m, "scratch") ? S_LOCAL : S_GLOBAL;
+    o.flags = F_MEM;
+    o.width = cdna_width(m);
+  } else if (starts(m, "ds_read") || starts(m, "ds_load") || starts(m, "ds_add") || starts(m, "ds_bpermute") ||
+             starts(m, "ds_permute") || starts(m, "ds_swizzle")) {
+    o.cls = OC_LOAD;
+    o.space = S_SHARED;
+    o.flags = F_MEM;
+    o.width = cdna_width(m);
+  } else if (starts(m, "ds_write") || starts(m, "ds_store")) {
+    o.cls = OC_STORE;
+    o.space = S_SHARED;
+    o.flags = F_MEM;
+    o.width = cdna_width(m);
+  } else if (starts(m, "s_load") || starts(m, "s_buffer_load") || starts(m, "s_memtime") ||
+             starts(m, "s_memrealtime")) {
+    o.cls = OC_ALU;
+    o.space = S_CONST;
+  } else if (m == "s_waitcnt" || starts(m, "s_waitcnt")) {
+    o.cls = OC_NOP;
+    o.flags = F_WAITCNT;
+  } else if (m == "s_barrier") {
+    o.cls = OC_BARRIER;
+  } else if (m == "s_endpgm") {
+    o.cls = OC_EXIT;
+  } else if (starts(m, "s_branch") || starts(m, "s_cbranch") || starts(m, "s_setpc") || starts(m, "s_swappc")) {
+    o.cls = OC_BRANCH;
+  } else if (starts(m, "s_nop") || starts(m, "s_sleep") || starts(m, "s_setprio") || starts(m, "s_sched")) {
+    o.cls = OC_NOP;
+  } else if (starts(m, "s_")) {
+    o.cls = OC_INTP;  // scalar ALU
+  } else if (starts(m, "v_exp") || starts(m, "v_log") || starts(m, "v_rcp") || starts(m, "v_rsq") ||
+             starts(m, "v_sqrt") || starts(m, "v_sin") || starts(m, "v_cos")) {
+    o.cls = OC_SFU;
+  } else if (contains(m, "_f64")) {
+    o.cls = OC_DP;
+  } else if (starts(m, "v_pk_") && (contains(m, "f16") || contains(m, "bf16"))) {
+    o.cls = OC_SP;
+    o.half_ii = 1;
+  }
+  return o;
+}
+
+// ---------------------------------------------------------------------------
+// fast tokenizer
+struct Tok {
+  const char* p;
+  const char* e;
+  bool next(std::string& out) {
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\r')) ++p;
+    if (p >= e) return false;
+    const char* s = p;
+    while (p < e && *p != ' ' && *p != '\t' && *p != '\r') ++p;
+    out.assign(s, p);
+    return true;
+  }
+  bool hex(uint64_t& v) {
+    while (p < e && (*p == ' ' || *p == '\t')) ++p;
+    if (p >= e) return false;
+    char* end;
+    v = strtoull(p, &end, 16);
+    if (end == p) return false;
+    p = end;
+    return true;
+  }
+  bool dec(long long& v) {
+    while (p < e && (*p == ' ' || *p == '\t')) ++p;
+    if (p >= e) return false;
+    char* end;
+    v = strtoll(p, &end, 10);
+    if (end == p) return false;
+    p = end;
+    return true;
+  }
+};
+
+uint8_t reg_of(const std::string& t) {
+  // R12 / v12 / s3 / a7 -> 13 ; RZ / R255 -> 0 (no dependency)
+  size_t i = 0;
+  while (i < t.size() && !(t[i] >= '0' && t[i] <= '9')) ++i;
+  if (i >= t.size()) return 0;
+  long r = atol(t.c_str() + i);
+  if (r >= 255 || r < 0) return 0;
+  return (uint8_t)(r + 1);
+}
+
+void parse_header_line(KernelHeader& h, const std::string& line) {
+  auto eq = line.find('=');
+  std::string key = line.substr(1, eq == std::string::npos ? std::string::npos : eq - 1);
+  key = trim_copy(key);
+  std::string val = eq == std::string::npos ? "" : line.substr(eq + 1);
+  auto t = [&]() { return std::string(val.begin() + (val.size() && val[0] == ' ' ? 1 : 0), val.end()); };
+  if (key == "kernel name") h.name = t();
+  else if (key == "kernel id") h.id = (uint32_t)strtoul(val.c_str(), nullptr, 10);
+  else if (key == "grid dim") sscanf(val.c_str(), " (%u,%u,%u)", &h.grid[0], &h.grid[1], &h.grid[2]);
+  else if (key == "block dim") sscanf(val.c_str(), " (%u,%u,%u)", &h.block[0], &h.block[1], &h.block[2]);
+  else if (key == "shmem") h.shmem = (uint32_t)strtoul(val.c_str(), nullptr, 10);
+  else if (key == "nregs") h.nregs = (uint32_t)strtoul(val.c_str(), nullptr, 10);
+  else if (key == "cuda stream id" || key == "hip stream id" || key == "stream id")
+    h.stream = strtoull(val.c_str(), nullptr, 10);
+  else if (key == "binary version") h.binary_version = (uint32_t)strtoul(val.c_str(), nullptr, 10);
+  else if (key == "accelsim tracer version" || key == "tracer version")
+    h.trace_version = (uint32_t)strtoul(val.c_str(), nullptr, 10);
+  else if (key == "nvbit version" || key == "rocprofiler version") h.tracer_version = t();
+  else if (key == "shmem base_addr") h.shmem_base = strtoull(val.c_str(), nullptr, 16);
+  else if (key == "local mem base_addr") h.local_base = strtoull(val.c_str(), nullptr, 16);
+  else if (key == "warp size" || key == "wavefront size") h.warp_size = (uint32_t)strtoul(val.c_str(), nullptr, 10);
+}
+
+}  // namespace
+
+std::string trim_copy(const std::string& s) {
+  size_t b = s.find_first_not_of(" \t\r\n");
+  if (b == std::string::npos) return "";
+  size_t e = s.find_last_not_of(" \t\r\n");
+  return s.substr(b, e - b + 1);
+}
+
+OpInfo decode_opcode(const std::string& op, uint32_t binary_version) {
+  if (binary_version >= 900) return decode_cdna(op);
+  return decode_sass(op, binary_version);
+}
+
+const std::string& opcode_name(uint16_t id) {
+  static const std::string none = "<unknown>";
+  IsaDb& db = isa();
+  std::lock_guard<std::mutex> g(db.mu);
+  return id < db.names.size() ? db.names[id] : none;
+}
+uint32_t opcode_count() { return (uint32_t)isa().names.size(); }
+
+// ---------------------------------------------------------------------------
+Command parse_collective_line(const std::string& line0) {
+  Command c;
+  std::string line = trim_copy(line0);
+  c.text = line;
+  auto parts = std::vector<std::string>();
+  {
+    std::string cur;
+    for (char ch : line) {
+      if (ch == ',') {
+        parts.push_back(trim_copy(cur));
+        cur.clear();
+      } else {
+        cur.push_back(ch);
+      }
+    }
+    parts.push_back(trim_copy(cur));
+  }
+  std::string name = parts[0];
+  std::string base = name;
+  for (const char* pre : {"nccl", "rccl"})
+    if (base.rfind(pre, 0) == 0) base = base.substr(4);
+  if (base == "CommInitAll" || base == "CommInitRank" || base == "CommInitRankConfig") c.type = CMD_COLL_INIT;
+  else if (base == "CommDestroy" || base == "CommAbort") c.type = CMD_COLL_DESTROY;
+  else if (base == "GroupStart") c.type = CMD_GROUP_START;
+  else if (base == "GroupEnd") c.type = CMD_GROUP_END;
+  else {
+    c.type = CMD_COLLECTIVE;
+    c.coll = base;
+  }
+  for (size_t i = 1; i < parts.size(); ++i) {
+    auto eq = parts[i].find('=');
+    if (eq == std::string::npos) continue;
+    std::string k = parts[i].substr(0, eq), v = parts[i].substr(eq + 1);
+    if (k == "count") c.count = strtoull(v.c_str(), nullptr, 0);
+    else if (k == "bytes") c.bytes = strtoull(v.c_str(), nullptr, 0);
+    else if (k == "dtype_bytes") c.dtype_bytes = (uint32_t)strtoul(v.c_str(), nullptr, 0);
+    else if (k == "dtype") {
+      static const std::map<std::string, uint32_t> sz = {
+          {"ncclInt8", 1},    {"ncclChar", 1},    {"ncclUint8", 1},   {"ncclInt32", 4},   {"ncclInt", 4},
+          {"ncclUint32", 4},  {"ncclInt64", 8},   {"ncclUint64", 8},  {"ncclFloat16", 2}, {"ncclHalf", 2},
+          {"ncclBfloat16", 2}, {"ncclFloat32", 4}, {"ncclFloat", 4},  {"ncclFloat64", 8}, {"ncclDouble", 8},
+          {"float32", 4},     {"float16", 2},     {"bfloat16", 2},    {"float64", 8},     {"int32", 4}};
+      auto it = sz.find(v);
+      c.dtype_bytes = it == sz.end() ? 4 : it->second;
+    } else if (k == "op") c.redop = v;
+    else if (k == "root") c.root = atoi(v.c_str());
+    else if (k == "nranks" || k == "ndev") c.nranks = atoi(v.c_str());
+    else if (k == "stream") c.stream = strtoull(v.c_str(), nullptr, 0);
+  }
+  if (!c.bytes && c.count) c.bytes = c.count * c.dtype_bytes;
+  return c;
+}
+
+std::vector<Command> parse_commandlist(const std::string& path) {
+  std::ifstream f(path);
+  if (!f.is_open()) throw std::runtime_error("Unable to open file: " + path);
+  std::string dir = path;
+  auto sl = dir.rfind('/');
+  dir = sl == std::string::npos ? std::string(".") : dir.substr(0, sl);
+  std::vector<Command> out;
+  std::string line;
+  while (std::getline(f, line)) {
+    line = trim_copy(line);
+    if (line.empty() || line[0] == '#') continue;
+    Command c;
+    if (line.rfind("MemcpyHtoD", 0) == 0 || line.rfind("MemcpyDtoH", 0) == 0) {
+      c.type = line[6] == 'H' ? CMD_MEMCPY_HTOD : CMD_MEMCPY_DTOH;
+      c.text = line;
+      auto p = split_commas(line);
+      if (p.size() >= 3) {
+        c.addr = strtoull(p[1].c_str(), nullptr, 16);
+        c.bytes = strtoull(p[2].c_str(), nullptr, 10);
+      }
+      if (c.type == CMD_MEMCPY_DTOH) continue;  // ignored like the reference
+    } else if (line.rfind("kernel", 0) == 0) {
+      c.type = CMD_KERNEL;
+      c.text = line[0] == '/' ? line : dir + "/" + line;
+    } else if (line.rfind("nccl", 0) == 0 || line.rfind("rccl", 0) == 0) {
+      c = parse_collective_line(line);
+    } else {
+      continue;  // unknown commands are skipped
+    }
+    out.push_back(c);
+  }
+  return out;
+}
+
+std::vector<std::string> split_commas(const std::string& s) {
+  std::vector<std::string> v;
+  std::string cur;
+  for (char ch : s) {
+    if (ch == ',') {
+      v.push_back(cur);
+      cur.clear();
+    } else {
+      cur.push_back(ch);
+    }
+  }
+  v.push_back(cur);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+static bool is_binary_path(const std::string& p) {
+  return p.size() > 6 && p.compare(p.size() - 6, 6, ".asimk") == 0;
+}
+
+KernelHeader read_kernel_header(const std::string& path) {
+  if (is_binary_path(path)) return load_kernel_binary(path).h;  // binary headers are tiny to parse
+  std::ifstream f(path);
+  if (!f.is_open()) throw std::runtime_error("Unable to open file: " + path);
+  KernelHeader h;
+  std::string line;
+  while (std::getline(f, line)) {
+    if (line.empty()) continue;
+    if (line[0] == '#') break;
+    if (line[0] == '-') parse_header_line(h, line);
+  }
+  return h;
+}
+
+HostKernel load_kernel(const std::string& path) {
+  // prefer a binary sibling when present (written by trace conversion)
+  if (is_binary_path(path)) return load_kernel_binary(path);
+  std::string bin = path + ".asimk";
+  std::ifstream probe(bin);
+  if (probe.good()) return load_kernel_binary(bin);
+  return load_kernel_text(path);
+}
+
+HostKernel load_kernel_text(const std::string& path) {
+  std::ifstream f(path);
+  if (!f.is_open()) throw std::runtime_error("Unable to open file: " + path);
+  HostKernel k;
+  std::string line;
+  // header
+  while (std::getline(f, line)) {
+    if (line.empty()) continue;
+    if (line[0] == '#') break;
+    if (line[0] == '-') parse_header_line(k.h, line);
+  }
+  KernelHeader& h = k.h;
+  const uint32_t ws = h.warp_size ? h.warp_size : 32;
+  const uint32_t threads = h.block[0] * h.block[1] * h.block[2];
+  k.warps_per_cta = (threads + ws - 1) / ws;
+  k.n_cta = h.grid[0] * h.grid[1] * h.grid[2];
+  k.streams.assign((size_t)k.n_cta * k.warps_per_cta, WStream{0, 0});
+  k.mems.reserve(1024);
+  std::vector<uint64_t> lane_addr(64);
+  uint32_t cta = 0, warp = 0, expect = 0, got = 0;
+  bool in_tb = false;
+  std::string tok;
+  std::unordered_map<std::string, OpInfo> opcache;
+  while (std::getline(f, line)) {
+    if (line.empty()) continue;
+    if (line[0] == '#') {
+      if (line.rfind("#BEGIN_TB", 0) == 0) {
+        if (in_tb) throw std::runtime_error("trace parse error: nested #BEGIN_TB in " + path);
+        in_tb = true;
+      } else if (line.rfind("#END_TB", 0) == 0) {
+        in_tb = false;
+      }
+      continue;
+    }
+    if (line.rfind("thread block", 0) == 0) {
+      uint32_t x = 0, y = 0, z = 0;
+      sscanf(line.c_str(), "thread block = %u,%u,%u", &x, &y, &z);
+      cta = z * h.grid[1] * h.grid[0] + y * h.grid[0] + x;
+      if (cta >= k.n_cta) throw std::runtime_error("thread block id outside grid in " + path);
+      continue;
+    }
+    if (line.rfind("warp", 0) == 0) {
+      sscanf(line.c_str(), "warp = %u", &warp);
+      if (warp >= k.warps_per_cta) throw std::runtime_error("warp id outside block in " + path);
+      continue;
+    }
+    if (line.rfind("insts", 0) == 0) {
+      sscanf(line.c_str(), "insts = %u", &expect);
+      got = 0;
+      WStream& s = k.streams[(size_t)cta * k.warps_per_cta + warp];
+      s.begin = (uint32_t)k.insts.size();
+      s.count = expect;
+      k.insts.reserve(k.insts.size() + expect);
+      continue;
+    }
+    // instruction line
+    Tok t{line.data(), line.data() + line.size()};
+    long long dv;
+    if (h.trace_version && h.trace_version < 3) {
+      for (int i = 0; i < 4; ++i) t.dec(dv);
+    }
+    uint64_t pc = 0, mask = 0;
+    t.hex(pc);
+    t.hex(mask);
+    TInst in{};
+    in.pc = (uint32_t)pc;
+    in.mask = mask;
+    in.mem = kNoMem;
+    long long nd = 0;
+    t.dec(nd);
+    for (long long i = 0; i < nd; ++i) {
+      t.next(tok);
+      if (i < 2) in.dst[i] = reg_of(tok);
+    }
+    std::string opstr;
+    t.next(opstr);
+    long long ns = 0;
+    t.dec(ns);
+    for (long long i = 0; i < ns; ++i) {
+      t.next(tok);
+      if (i < 5) in.src[i] = reg_of(tok);
+    }
+    long long mw = 0;
+    t.dec(mw);
+    auto oc = opcache.find(opstr);
+    if (oc == opcache.end()) oc = opcache.emplace(opstr, decode_opcode(opstr, h.binary_version)).first;
+    const OpInfo& oi = oc->second;
+    if (!oi.known) k.unknown_opcodes++;
+    in.opcode = oi.opcode;
+    in.cls = oi.cls;
+    in.space = oi.space;
+    in.flags = oi.flags;
+    in.width = 0;
+    if (mw > 0) {
+      long long mode = 0;
+      t.dec(mode);
+      TMem m{};
+      m.list = kNoMem;
+      const int nact = __builtin_popcountll(mask);
+      if (mode == 1) {
+        uint64_t base = 0;
+        long long stride = 0;
+        t.hex(base);
+        t.dec(stride);
+        m.base = base;
+        m.stride = (int32_t)stride;
+      } else if (mode == 2) {
+        uint64_t base = 0;
+        t.hex(base);
+        m.base = base;
+        m.list = (uint32_t)k.addrs.size();
+        uint64_t last = base;
+        k.addrs.push_back(base);
+        for (int i = 1; i < nact; ++i) {
+          long long d = 0;
+          t.dec(d);
+          last = last + (uint64_t)d;
+          k.addrs.push_back(last);
+        }
+      } else {
+        m.list = (uint32_t)k.addrs.size();
+        for (int i = 0; i < nact; ++i) {
+          uint64_t a = 0;
+          t.hex(a);
+          k.addrs.push_back(a);
+        }
+        m.base = nact ? k.addrs[m.list] : 0;
+      }
+      // width from the opcode (the tracer's value can be wrong, reference
+      // trace_parser.cc:172-174)
+      in.width = oi.width ? oi.width : (uint8_t)std::min<long long>(mw, 255);
+      // generic LD/ST: resolve the space from the first active address
+      if (in.space == S_NONE && (in.cls == OC_LOAD || in.cls == OC_STORE)) {
+        uint64_t a0 = m.base;
+        if (h.shmem_base == 0 || h.local_base == 0) in.space = S_SHARED;
+        else if (a0 >= h.shmem_base && a0 < h.local_base) in.space = S_SHARED;
+        else if (a0 >= h.local_base && a0 < h.local_base + (1ull << 30)) in.space = S_LOCAL;
+        else in.space = S_GLOBAL;
+      }
+      in.mem = (uint32_t)k.mems.size();
+      k.mems.push_back(m);
+    } else if (oi.flags & F_MEM) {
+      // memory op without addresses (all lanes predicated off)
+      in.width = oi.width;
+      if (in.space == S_NONE) in.space = S_SHARED;
+    }
+    uint32_t lat = 1, ii = 1;
+    (void)lat;
+    (void)ii;
+    if (oi.half_ii) in.flags |= 0;  // applied by coalesce_kernel from the config
+    in.lat = oi.half_ii ? 0x8000 : 0;  // marker consumed by coalesce_kernel
+    k.insts.push_back(in);
+    k.thread_insts += (uint64_t)__builtin_popcountll(mask);
+    ++got;
+  }
+  k.warp_insts = k.insts.size();
+  return k;
+}
+
+// ---------------------------------------------------------------------------
+// binary format
+namespace {
+const char kMagic[8] = {'A', 'S', 'I', 'M', 'K', '0', '0', '1'};
+struct BinHdr {
+  char magic[8];
+  uint32_t version;
+  uint32_t id;
+  uint32_t grid[3];
+  uint32_t block[3];
+  uint32_t shmem, nregs;
+  uint64_t stream;
+  uint32_t binary_version, trace_version;
+  uint64_t shmem_base, local_base;
+  uint32_t warp_size, warps_per_cta, n_cta, name_len;
+  uint64_t n_insts, n_mems, n_addrs, n_streams;
+  uint64_t thread_insts;
+};
+template <class T>
+void wr(std::ofstream& f, const std::vector<T>& v) {
+  if (!v.empty()) f.write(reinterpret_cast<const char*>(v.data()), (std::streamsize)(v.size() * sizeof(T)));
+}
+template <class T>
+void rd(std::ifstream& f, std::vector<T>& v, uint64_t n) {
+  v.resize(n);
+  if (n) f.read(reinterpret_cast<char*>(v.data()), (std::streamsize)(n * sizeof(T)));
+}
+}  // namespace
+
+void save_kernel_binary(const HostKernel& k, const std::string& path) {
+  std::ofstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot write " + path);
+  BinHdr h{};
+  memcpy(h.magic, kMagic, 8);
+  h.version = 1;
+  h.id = k.h.id;
+  for (int i = 0; i < 3; ++i) {
+    h.grid[i] = k.h.grid[i];
+    h.block[i] = k.h.block[i];
+  }
+  h.shmem = k.h.shmem;
+  h.nregs = k.h.nregs;
+  h.stream = k.h.stream;
+  h.binary_version = k.h.binary_version;
+  h.trace_version = k.h.trace_version;
+  h.shmem_base = k.h.shmem_base;
+  h.local_base = k.h.local_base;
+  h.warp_size = k.h.warp_size;
+  h.warps_per_cta = k.warps_per_cta;
+  h.n_cta = k.n_cta;
+  h.name_len = (uint32_t)k.h.name.size();
+  h.n_insts = k.insts.size();
+  h.n_mems = k.mems.size();
+  h.n_addrs = k.addrs.size();
+  h.n_streams = k.streams.size();
+  h.thread_insts = k.thread_insts;
+  f.write(reinterpret_cast<const char*>(&h), sizeof(h));
+  f.write(k.h.name.data(), (std::streamsize)k.h.name.size());
+  // opcode names used by this kernel, so ids survive across processes
+  std::vector<uint16_t> used;
+  for (auto& in : k.insts) used.push_back(in.opcode);
+  std::sort(used.begin(), used.end());
+  used.erase(std::unique(used.begin(), used.end()), used.end());
+  uint32_t nu = (uint32_t)used.size();
+  f.write(reinterpret_cast<const char*>(&nu), 4);
+  for (uint16_t id : used) {
+    const std::string& n = opcode_name(id);
+    uint16_t len = (uint16_t)n.size();
+    f.write(reinterpret_cast<const char*>(&id), 2);
+    f.write(reinterpret_cast<const char*>(&len), 2);
+    f.write(n.data(), len);
+  }
+  wr(f, k.insts);
+  wr(f, k.mems);
+  wr(f, k.addrs);
+  wr(f, k.streams);
+}
+
+HostKernel load_kernel_binary(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("Unable to open file: " + path);
+  BinHdr h{};
+  f.read(reinterpret_cast<char*>(&h), sizeof(h));
+  if (!f || memcmp(h.magic, kMagic, 8) != 0) throw std::runtime_error("not an .asimk kernel trace: " + path);
+  HostKernel k;
+  k.h.id = h.id;
+  for (int i = 0; i < 3; ++i) {
+    k.h.grid[i] = h.grid[i];
+    k.h.block[i] = h.block[i];
+  }
+  k.h.shmem = h.shmem;
+  k.h.nregs = h.nregs;
+  k.h.stream = h.stream;
+  k.h.binary_version = h.binary_version;
+  k.h.trace_version = h.trace_version;
+  k.h.shmem_base = h.shmem_base;
+  k.h.local_base = h.local_base;
+  k.h.warp_size = h.warp_size;
+  k.warps_per_cta = h.warps_per_cta;
+  k.n_cta = h.n_cta;
+  k.h.name.resize(h.name_len);
+  f.read(&k.h.name[0], h.name_len);
+  uint32_t nu = 0;
+  f.read(reinterpret_cast<char*>(&nu), 4);
+  std::unordered_map<uint16_t, uint16_t> remap;
+  for (uint32_t i = 0; i < nu; ++i) {
+    uint16_t id, len;
+    f.read(reinterpret_cast<char*>(&id), 2);
+    f.read(reinterpret_cast<char*>(&len), 2);
+    std::string n(len, '\0');
+    f.read(&n[0], len);
+    remap[id] = decode_opcode(n, h.binary_version).opcode;
+  }
+  rd(f, k.insts, h.n_insts);
+  rd(f, k.mems, h.n_mems);
+  rd(f, k.addrs, h.n_addrs);
+  rd(f, k.streams, h.n_streams);
+  if (!f) throw std::runtime_error("truncated .asimk file: " + path);
+  for (auto& in : k.insts) {
+    auto it = remap.find(in.opcode);
+    if (it != remap.end()) in.opcode = it->second;
+  }
+  k.thread_insts = h.thread_insts;
+  k.warp_insts = k.insts.size();
+  return k;
+}
+
+void save_kernel_text(const HostKernel& k, const std::string& path) {
+  FILE* f = fopen(path.c_str(), "w");
+  if (!f) throw std::runtime_error("cannot write " + path);
+  const KernelHeader& h = k.h;
+  fprintf(f, "-kernel name = %s\n-kernel id = %u\n-grid dim = (%u,%u,%u)\n-block dim = (%u,%u,%u)\n", h.name.c_str(),
+          h.id, h.grid[0], h.grid[1], h.grid[2], h.block[0], h.block[1], h.block[2]);
+  fprintf(f, "-shmem = %u\n-nregs = %u\n-binary version = %u\n-cuda stream id = %llu\n", h.shmem, h.nregs,
+          h.binary_version, (unsigned long long)h.stream);
+  fprintf(f, "-shmem base_addr = 0x%016llx\n-local mem base_addr = 0x%016llx\n", (unsigned long long)h.shmem_base,
+          (unsigned long long)h.local_base);
+  if (h.warp_size != 32) fprintf(f, "-warp size = %u\n", h.warp_size);
+  fprintf(f, "-nvbit version = 1.5.5\n-accelsim tracer version = %u\n\n", h.trace_version ? h.trace_version : 4);
+  fprintf(f, "#traces format = threadblock_x threadblock_y threadblock_z warpid_tb PC mask dest_num reg_dests "
+             "opcode src_num reg_srcs mem_width [adrrescompress?] [mem_addresses]\n\n");
+  const uint32_t wpc = k.warps_per_cta;
+  for (uint32_t c = 0; c < k.n_cta; ++c) {
+    uint32_t x = c % h.grid[0], y = (c / h.grid[0]) % h.grid[1], z = c / (h.grid[0] * h.grid[1]);
+    fprintf(f, "#BEGIN_TB\n\nthread block = %u,%u,%u\n\n", x, y, z);
+    for (uint32_t w = 0; w < wpc; ++w) {
+      const WStream& s = k.streams[(size_t)c * wpc + w];
+      fprintf(f, "warp = %u\ninsts = %u\n", w, s.count);
+      for (uint32_t i = s.begin; i < s.begin + s.count; ++i) {
+        const TInst& in = k.insts[i];
+        fprintf(f, "%04x %016llx ", in.pc, (unsigned long long)in.mask);
+        int nd = (in.dst[0] != 0) + (in.dst[1] != 0);
+        fprintf(f, "%d ", nd);
+        for (int j = 0; j < 2; ++j)
+          if (in.dst[j]) fprintf(f, "R%d ", in.dst[j] - 1);
+        fprintf(f, "%s ", opcode_name(in.opcode).c_str());
+        int ns = 0;
+        for (int j = 0; j < 5; ++j) ns += in.src[j] != 0;
+        fprintf(f, "%d ", ns);
+        for (int j = 0; j < 5; ++j)
+          if (in.src[j]) fprintf(f, "R%d ", in.src[j] - 1);
+        if (in.mem != kNoMem) {
+          const TMem& m = k.mems[in.mem];
+          fprintf(f, "%u ", in.width);
+          if (m.list == kNoMem) {
+            fprintf(f, "1 0x%llx %d", (unsigned long long)m.base, m.stride);
+          } else {
+            fprintf(f, "0");
+            int n = __builtin_popcountll(in.mask);
+            for (int j = 0; j < n; ++j) fprintf(f, " 0x%llx", (unsigned long long)k.addrs[m.list + j]);
+          }
+        } else {
+          fprintf(f, "0");
+        }
+        fprintf(f, "\n");
+      }
+      fprintf(f, "\n");
+    }
+    fprintf(f, "#END_TB\n\n");
+  }
+  fclose(f);
+}
+
+// ---------------------------------------------------------------------------
+// coalescing
+static void lane_addresses(const HostKernel& k, const TInst& in, uint64_t* out, uint32_t ws) {
+  const TMem& m = k.mems[in.mem];
+  uint32_t rank = 0;
+  for (uint32_t l = 0; l < ws; ++l) {
+    if (!(in.mask >> l & 1ull)) {
+      out[l] = 0;
+      continue;
+    }
+    out[l] = m.list == kNoMem ? m.base + (uint64_t)((int64_t)m.stride * rank) : k.addrs[m.list + rank];
+    ++rank;
+  }
+}
+
+uint32_t smem_conflict_degree(const uint64_t* addr, uint64_t mask, uint32_t width, const SimCfg& c,
+                              uint32_t ws) {
+  const uint32_t nb = c.smem_banks ? c.smem_banks : 32;
+  const uint32_t parts = c.smem_warp_parts ? c.smem_warp_parts : 1;
+  const uint32_t per = (ws + parts - 1) / parts;
+  uint32_t total = 0;
+  for (uint32_t p = 0; p < parts; ++p) {
+    // distinct 4-byte words per bank in this part of the warp
+    std::vector<std::vector<uint64_t>> words(nb);
+    for (uint32_t l = p * per; l < (p + 1) * per && l < ws; ++l) {
+      if (!(mask >> l & 1ull)) continue;
+      uint64_t w0 = addr[l] >> 2, w1 = (addr[l] + (width ? width : 4) - 1) >> 2;
+      for (uint64_t w = w0; w <= w1; ++w) {
+        auto& v = words[w % nb];
+        if (std::find(v.begin(), v.end(), w) == v.end()) v.push_back(w);
+      }
+    }
+    uint32_t deg = 0;
+    for (auto& v : words) deg = std::max<uint32_t>(deg, (uint32_t)v.size());
+    if (c.smem_limited_bcast) {
+      // limited broadcast: duplicated words in a bank also serialize
+      uint32_t lanes_max = 0;
+      std::vector<uint32_t> cnt(nb, 0);
+      for (uint32_t l = p * per; l < (p + 1) * per && l < ws; ++l)
+        if (mask >> l & 1ull) lanes_max = std::max(lanes_max, ++cnt[(addr[l] >> 2) % nb]);
+      deg = std::max(deg, lanes_max > 1 ? (lanes_max + 1) / 2 : lanes_max);
+    }
+    total += deg ? deg : (p == 0 ? 1 : 0);
+  }
+  return total ? total : 1;
+}
+
+ReadyKernel coalesce_kernel(const HostKernel& k, const SimCfg& c) {
+  ReadyKernel r;
+  r.h = k.h;
+  r.warps_per_cta = k.warps_per_cta;
+  r.n_cta = k.n_cta;
+  r.streams = k.streams;
+  r.thread_insts = k.thread_insts;
+  r.warp_insts = k.warp_insts;
+  r.insts = k.insts;
+  r.accs.reserve(k.mems.size() * 2);
+  const uint32_t ws = k.h.warp_size ? k.h.warp_size : 32;
+  std::vector<uint64_t> lane(64);
+  std::vector<std::pair<uint64_t, uint8_t>> lines;
+  std::vector<uint32_t> bytes;
+  for (auto& in : r.insts) {
+    // latency / initiation interval from the config (per op class)
+    const bool half = (in.lat & 0x8000) != 0;
+    uint32_t cls = in.cls < OC_COUNT ? in.cls : OC_ALU;
+    in.lat = c.lat[cls];
+    uint32_t ii = c.ii[cls];
+    if (half) ii = std::max<uint32_t>(1, ii / 2);
+    in.ii = (uint8_t)std::min<uint32_t>(ii, 255);
+    if (in.mem == kNoMem) {
+      if ((in.cls == OC_LOAD || in.cls == OC_STORE) && in.space != S_SHARED) {
+        // no active address: completes like a 1-cycle shared access
+        in.space = S_SHARED;
+      }
+      if (in.cls == OC_LOAD || in.cls == OC_STORE) in.width = 1;
+      continue;
+    }
+    lane_addresses(k, in, lane.data(), ws);
+    const uint32_t width = in.width ? in.width : 4;
+    if (in.space == S_SHARED) {
+      in.width = (uint8_t)std::min<uint32_t>(255, smem_conflict_degree(lane.data(), in.mask, width, c, ws));
+      in.mem = kNoMem;
+      continue;
+    }
+    // global / local: group touched 32B sectors by 128B line (sorted by
+    // address like the reference's block map, abstract_hardware_model.cc:475-586)
+    lines.clear();
+    bytes.clear();
+    for (uint32_t l = 0; l < ws; ++l) {
+      if (!(in.mask >> l & 1ull)) continue;
+      uint64_t a = lane[l];
+      uint64_t end = a + width;
+      while (a < end) {
+        uint64_t line = a & ~127ull;
+        uint64_t lend = std::min<uint64_t>(end, line + 128);
+        uint8_t sec = 0;
+        for (uint64_t s = (a >> 5); s <= ((lend - 1) >> 5); ++s) sec |= (uint8_t)(1u << (s & 3));
+        bool found = false;
+        for (size_t i = 0; i < lines.size(); ++i)
+          if (lines[i].first == line) {
+            lines[i].second |= sec;
+            bytes[i] += (uint32_t)(lend - a);
+            found = true;
+            break;
+          }
+        if (!found) {
+          lines.emplace_back(line, sec);
+          bytes.push_back((uint32_t)(lend - a));
+        }
+        a = lend;
+      }
+    }
+    std::vector<size_t> ord(lines.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return lines[x].first < lines[y].first; });
+    in.mem = (uint32_t)r.accs.size();
+    uint32_t n = 0;
+    for (size_t oi = 0; oi < ord.size() && n < (uint32_t)kMaxAccess; ++oi) {
+      size_t i = ord[oi];
+      TAcc a{};
+      a.line = lines[i].first;
+      a.sectors = lines[i].second;
+      a.bytes = (uint16_t)std::min<uint32_t>(bytes[i], 128);
+      a.bank = (uint8_t)((a.line >> 7) % std::max<uint32_t>(1, c.l1_banks));
+      r.accs.push_back(a);
+      ++n;
+    }
+    in.width = (uint8_t)std::max<uint32_t>(1, n);
+    if (n == 0) {
+      in.space = S_SHARED;
+      in.mem = kNoMem;
+    }
+  }
+  return r;
+}
+
+}  // namespace asim

@@ -1,0 +1,122 @@
+// Trace ingest: command lists, kernel headers, instruction streams.
+//
+// Compatible readers for the reference's text formats (kernelslist.g,
+// kernel-N.traceg: trace_parser.cc:220-447) plus this project's binary
+// columnar format (".asimk", written by the tracer/generator, memory-mappable,
+// config independent).  All formats decode into the same host arrays, which
+// are then coalesced for a given SimCfg and uploaded once per kernel.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../model/sm.h"
+
+namespace asim {
+
+enum CmdType : uint8_t {
+  CMD_KERNEL = 1,
+  CMD_MEMCPY_HTOD,
+  CMD_MEMCPY_DTOH,
+  CMD_COLL_INIT,      // ncclCommInitAll / rcclCommInitRank
+  CMD_COLL_DESTROY,   // ncclCommDestroy
+  CMD_GROUP_START,    // ncclGroupStart
+  CMD_GROUP_END,      // ncclGroupEnd
+  CMD_COLLECTIVE,     // ncclAllReduce / AllGather / ReduceScatter / Broadcast / AllToAll ...
+};
+
+struct Command {
+  CmdType type;
+  std::string text;   // original line (or resolved kernel path)
+  uint64_t addr = 0;  // memcpy
+  uint64_t bytes = 0; // memcpy / collective payload bytes per rank
+  // collective description (fixes the reference's dropped arguments, D6/§2.11)
+  std::string coll;   // AllReduce, AllGather, ReduceScatter, Broadcast, Reduce, AllToAll, SendRecv
+  uint64_t count = 0;
+  uint32_t dtype_bytes = 4;
+  std::string redop;
+  int32_t root = -1;
+  int32_t nranks = 1;
+  uint64_t stream = 0;
+};
+
+// Parse a kernelslist(.g) file.  Kernel paths are resolved relative to it.
+std::vector<Command> parse_commandlist(const std::string& path);
+// Parse one collective line "ncclAllReduce[,count=..,dtype=..,op=..,nranks=..]"
+Command parse_collective_line(const std::string& line);
+
+struct KernelHeader {
+  std::string name = "Empty";
+  uint32_t id = 0;
+  uint32_t grid[3] = {1, 1, 1};
+  uint32_t block[3] = {1, 1, 1};
+  uint32_t shmem = 0;
+  uint32_t nregs = 0;
+  uint64_t stream = 0;
+  uint32_t binary_version = 0;
+  uint32_t trace_version = 0;
+  std::string tracer_version;
+  uint64_t shmem_base = 0;
+  uint64_t local_base = 0;
+  uint32_t warp_size = 32;
+};
+
+// Decoded (not yet coalesced) kernel trace.
+struct HostKernel {
+  KernelHeader h;
+  uint32_t warps_per_cta = 0;
+  uint32_t n_cta = 0;
+  std::vector<TInst> insts;   // inst.mem -> index into mems, inst.width = bytes/thread
+  std::vector<TMem> mems;
+  std::vector<uint64_t> addrs;
+  std::vector<WStream> streams;  // [n_cta * warps_per_cta]
+  uint64_t thread_insts = 0;
+  uint64_t warp_insts = 0;
+  uint32_t unknown_opcodes = 0;
+};
+
+// Coalesced kernel ready for a cycle engine (inst.mem -> first TAcc,
+// inst.width -> number of accesses, or shared-memory conflict degree).
+struct ReadyKernel {
+  KernelHeader h;
+  uint32_t warps_per_cta = 0;
+  uint32_t n_cta = 0;
+  std::vector<TInst> insts;
+  std::vector<TAcc> accs;
+  std::vector<WStream> streams;
+  uint64_t thread_insts = 0;
+  uint64_t warp_insts = 0;
+};
+
+// header only (cheap); used by the command loop before the body is needed
+KernelHeader read_kernel_header(const std::string& path);
+HostKernel load_kernel(const std::string& path);  // text (.traceg/.trace) or binary (.asimk)
+HostKernel load_kernel_text(const std::string& path);
+HostKernel load_kernel_binary(const std::string& path);
+void save_kernel_binary(const HostKernel& k, const std::string& path);
+void save_kernel_text(const HostKernel& k, const std::string& path);
+
+// ISA decode of one mnemonic (e.g. "LDG.E.64.STRONG.GPU") for an
+// architecture selected by the kernel's binary version (SASS: 30..90,
+// CDNA: 900+, e.g. 950 = gfx950).
+struct OpInfo {
+  uint16_t opcode;
+  uint8_t cls;
+  uint8_t space;
+  uint8_t flags;
+  uint8_t width;      // bytes per thread (memory)
+  uint8_t half_ii;    // FP16x2: half initiation interval
+  bool known;
+};
+OpInfo decode_opcode(const std::string& op, uint32_t binary_version);
+const std::string& opcode_name(uint16_t id);
+uint32_t opcode_count();
+
+// Coalescing (host reference of the trace-ingest coalescer; same function is
+// run lane-parallel by the HIP ingest kernel).
+ReadyKernel coalesce_kernel(const HostKernel& k, const SimCfg& c);
+
+// shared-memory bank-conflict degree of one warp access
+uint32_t smem_conflict_degree(const uint64_t* addr, uint64_t mask, uint32_t width, const SimCfg& c, uint32_t warp_size);
+
+}  // namespace asim

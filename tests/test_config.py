@@ -1,0 +1,79 @@
+import glob
+import os
+
+import pytest
+
+from conftest import REFERENCE, reference_path
+
+
+def test_presets_parse(native):
+    from accel_sim_framework_distributed_amd.models import presets
+    for name in presets.PRESETS:
+        cfg = native.parse_config(presets.args_for(name))
+        assert cfg["n_sm"] > 0 and cfg["n_subpart"] == cfg["n_mem"] * cfg["n_sub_per_mem"]
+
+
+def test_qv100_derivation(native, qv100_args):
+    c = native.parse_config(qv100_args)
+    assert c["n_sm"] == 80 and c["n_mem"] == 32 and c["n_subpart"] == 64
+    assert c["warp_size"] == 32 and c["max_warps_per_sm"] == 64
+    assert c["n_sched"] == 4 and c["sched_policy"] == 0  # lrr
+    assert (c["l2_sets"], c["l2_assoc"]) == (32, 24)
+    assert c["l2_set_index"] == 2  # IPOLY ('P')
+    assert (c["nbk"], c["nbkgrp"], c["tRCD"], c["tRAS"], c["CL"], c["WL"]) == (16, 4, 12, 28, 12, 2)
+    assert c["atom_size"] == 32
+    assert c["ex_wb_width"] == 8
+    # chip bits inserted at bit 8 for 32 channels
+    assert c["addr_mask"][0] == 0x1F00
+    assert c["kernel_launch_latency"] == 5000
+
+
+def test_unknown_option_is_fatal(native):
+    with pytest.raises(Exception):
+        native.parse_config(["-no_such_flag", "1"])
+
+
+def test_config_file_grammar(native, tmp_path):
+    inc = tmp_path / "inc.config"
+    inc.write_text("-gpgpu_n_mem 16   # comment\n")
+    main = tmp_path / "main.config"
+    main.write_text(
+        "# header comment\n-gpgpu_n_clusters 4\n-gpgpu_n_cores_per_cluster 2\n"
+        f"-config {inc}\n"
+        '-gpgpu_dram_timing_opt "nbk=8:CCD=2:RRD=6:RCD=12:RAS=28:RP=12:RC=40:\n   CL=12:WL=4:CDLR=5:WR=12:nbkgrp=2:CCDL=3:RTPL=2"\n'
+        "-gpgpu_flush_l1_cache\n-gpgpu_cache:dl1 S:4:128:64,L:T:m:L:L,A:256:8,16:0,32\n")
+    c = native.parse_config(["-config", str(main)])
+    assert c["n_sm"] == 8 and c["n_mem"] == 16
+    assert c["nbk"] == 8 and c["tCCDL"] == 3 and c["WL"] == 4 and c["nbkgrp"] == 2
+
+
+def test_cache_geometry_strings(native):
+    g = native.parse_cache("S:32:128:24,L:B:m:L:P,A:192:4,32:0,32")
+    assert (g["nsets"], g["assoc"], g["sectored"], g["wpolicy"], g["set_index"]) == (32, 24, 1, 1, 2)
+    assert (g["mshr_entries"], g["mshr_merge"], g["miss_queue"], g["alloc"], g["walloc"]) == (192, 4, 32, "m", "L")
+    g = native.parse_cache("N:64:128:16,L:R:f:N:L,S:2:48,4")
+    assert g["sectored"] == 0 and g["wpolicy"] == 0 and g["alloc"] == "f"
+    assert native.parse_cache("none")["disabled"] == 1
+
+
+@pytest.mark.skipif(not os.path.isdir(REFERENCE), reason="reference tree not mounted")
+def test_reference_tested_configs_load(native):
+    """Every reference tested config (gpgpusim.config + trace.config) loads."""
+    gdirs = sorted(glob.glob(os.path.join(REFERENCE, "gpu-simulator/gpgpu-sim/configs/tested-cfgs/*")))
+    assert gdirs
+    n = 0
+    for gd in gdirs:
+        name = os.path.basename(gd)
+        gp = os.path.join(gd, "gpgpusim.config")
+        tr = os.path.join(REFERENCE, "gpu-simulator/configs/tested-cfgs", name, "trace.config")
+        args = ["-config", gp]
+        if os.path.exists(tr):
+            args += ["-config", tr]
+        try:
+            c = native.parse_config(args)
+        except Exception as e:  # caps of this build (e.g. >64 warps) must be reported clearly
+            assert "support" in str(e) or "range" in str(e) or "warps" in str(e), (name, e)
+            continue
+        assert c["n_sm"] > 0
+        n += 1
+    assert n >= 5
