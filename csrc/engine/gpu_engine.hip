@@ -66,6 +66,7 @@ struct GpuArgs {
   uint32_t flush_l1;
   uint32_t nblocks;
   GpuCtl* ctl;
+  uint64_t* prof;  // [nblocks][kProfSlots] shader-clock cycles per stage (profiling build)
 };
 
 // ---------------------------------------------------------------------------
@@ -123,9 +124,33 @@ __device__ __forceinline__ void copy_state(T* dst, const T* src) {
 
 extern __shared__ __attribute__((aligned(16))) char g_lds[];
 constexpr size_t kStateLds = ((sizeof(SMState) > sizeof(ChanState) ? sizeof(SMState) : sizeof(ChanState)) + 15) / 16 * 16;
-constexpr size_t kLdsBytes = kStateLds + (sizeof(KernelDesc) + 15) / 16 * 16;
+constexpr size_t kProfOff = kStateLds + (sizeof(KernelDesc) + 15) / 16 * 16;
+constexpr int kProfSlots = 32;
+struct ProfLds {
+  uint64_t last;
+  uint32_t slot;
+  uint32_t pad;
+  uint64_t acc[kProfSlots];
+};
+constexpr size_t kLdsBytes = kProfOff + sizeof(ProfLds);
 static_assert(kLdsBytes <= 160 * 1024, "per-block LDS budget exceeded");
 
+// profiling build of the lane policy: P::prof(k) charges the shader-clock
+// time since the previous stamp to the previous stage and enters stage k
+struct WaveParProf : WavePar {
+  static __device__ __forceinline__ void prof(int k) {
+    ProfLds* p = reinterpret_cast<ProfLds*>(g_lds + kProfOff);
+    uint64_t t = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0) {
+      p->acc[p->slot] += t - p->last;
+      p->slot = (uint32_t)k;
+      p->last = t;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+};
+
+template <class P>
 __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   const uint32_t b = blockIdx.x;
   const SimCfg& c = *a.cfg;  // read-only, scalar-cached
@@ -139,7 +164,13 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     copy_state(ch, &a.chs[b - c.n_sm]);
   // kernel descriptor lives in LDS behind the state (never in scratch)
   KernelDesc* kdl = reinterpret_cast<KernelDesc*>(g_lds + kStateLds);
-  if ((threadIdx.x & 63) == 0) *kdl = a.kd;
+  ProfLds* pl = reinterpret_cast<ProfLds*>(g_lds + kProfOff);
+  if ((threadIdx.x & 63) == 0) {
+    *kdl = a.kd;
+    pl->last = __builtin_amdgcn_s_memtime();
+    pl->slot = kProfSlots - 1;
+    for (int i = 0; i < kProfSlots; ++i) pl->acc[i] = 0;
+  }
   __syncthreads();
   const KernelDesc& kd = *kdl;
   SmCtx sx;
@@ -155,7 +186,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   if (is_sm && a.init_kernel) {
     sx.outbox = a.box_req[0];
     sx.outcnt = a.cnt_req[0];
-    sm_kernel_init<WavePar>(*s, sx, s->ks, a.cycle0, a.flush_l1);
+    sm_kernel_init<P>(*s, sx, s->ks, a.cycle0, a.flush_l1);
   }
   uint64_t epoch = a.epoch0, cycle = a.cycle0;
   uint32_t done = 0, dead = 0;
@@ -166,31 +197,36 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     if (is_sm) {
       sx.outbox = a.box_req[cur];
       sx.outcnt = a.cnt_req[cur];
-      sm_epoch<WavePar>(*s, sx, s->ks, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep,
-                        c.n_subpart, epoch);
-      sm_publish<WavePar>(*s, sx, s->ks, *a.pub, cur);
+      sm_epoch<P>(*s, sx, s->ks, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep,
+                  c.n_subpart, epoch);
+      sm_publish<P>(*s, sx, s->ks, *a.pub, cur);
     } else {
       mx.outbox = a.box_rep[cur];
       mx.outcnt = a.cnt_rep[cur];
       mx.win_end = t1 * c.per_core;
-      chan_epoch<WavePar>(*ch, mx, a.box_req[prev], a.cnt_req[prev], a.cap_req, t0 * c.per_core);
-      chan_publish<WavePar>(*ch, mx, *a.pub, cur);
+      chan_epoch<P>(*ch, mx, a.box_req[prev], a.cnt_req[prev], a.cap_req, t0 * c.per_core);
+      chan_publish<P>(*ch, mx, *a.pub, cur);
     }
     ++n;
+    P::prof(26);  // barrier
     if (!grid_barrier(a.ctl, a.nblocks, n - 1)) break;
+    P::prof(27);  // decision
     const uint32_t next_done = a.pub->next_cta[cur] >= kd.n_cta ? 1u : 0u;
-    EpochDecision d = epoch_decide<WavePar>(c, *a.pub, cur, t1, a.ready_cycle, next_done, epoch);
+    EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, a.ready_cycle, next_done, epoch);
+    P::prof(28);
     ++epoch;
     cycle = d.next_start;
     if (d.done) { done = 1; break; }
     if (d.deadlock) { dead = 1; break; }
     if (a.max_cycle && cycle >= a.max_cycle) break;
   }
+  P::prof(kProfSlots - 1);
   // write state back
   if (is_sm)
     copy_state(&a.sms[b], s);
   else
     copy_state(&a.chs[b - c.n_sm], ch);
+  if (a.prof && (threadIdx.x & 63) < kProfSlots) a.prof[(size_t)b * kProfSlots + (threadIdx.x & 63)] += pl->acc[threadIdx.x & 63];
   if (b == 0 && (threadIdx.x & 63) == 0) {
     a.ctl->done = done;
     a.ctl->deadlock = dead;
@@ -207,7 +243,14 @@ namespace {
 
 class GpuEngine : public Engine {
  public:
-  ~GpuEngine() override { release(); }
+  ~GpuEngine() override {
+    try {
+      dump_profile();
+    } catch (...) {
+    }
+    if (d_prof_) (void)hipFree(d_prof_);
+    release();
+  }
   const char* name() const override { return "gpu"; }
 
   void init(const SimCfg& c) override {
@@ -222,7 +265,16 @@ class GpuEngine : public Engine {
     if ((int)nblocks_ > n_cu_)
       throw std::runtime_error("GPU engine needs one CU per simulated SM/channel: " + std::to_string(nblocks_) +
                                " blocks > " + std::to_string(n_cu_) + " CUs");
-    HIPCHECK(hipFuncSetAttribute((const void*)engine_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_));
+    HIPCHECK(hipFuncSetAttribute((const void*)engine_kernel<WavePar>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds_));
+    HIPCHECK(hipFuncSetAttribute((const void*)engine_kernel<WaveParProf>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_));
+    const char* pe = getenv("ASIM_GPU_PROFILE");
+    profiling_ = pe && *pe && *pe != '0';
+    if (profiling_) {
+      HIPCHECK(hipMalloc(&d_prof_, sizeof(uint64_t) * nblocks_ * kProfSlots));
+      HIPCHECK(hipMemset(d_prof_, 0, sizeof(uint64_t) * nblocks_ * kProfSlots));
+    }
     HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     HIPCHECK(hipMalloc(&d_cfg_, sizeof(SimCfg)));
     HIPCHECK(hipMemcpy(d_cfg_, &c_, sizeof(SimCfg), hipMemcpyHostToDevice));
@@ -293,7 +345,11 @@ class GpuEngine : public Engine {
       a.nblocks = nblocks_;
       a.ctl = d_ctl_;
       HIPCHECK(hipMemsetAsync(d_ctl_, 0, sizeof(GpuCtl), stream_));
-      hipLaunchKernelGGL(engine_kernel, dim3(nblocks_), dim3(64), lds_, stream_, a);
+      a.prof = d_prof_;
+      if (profiling_)
+        hipLaunchKernelGGL(engine_kernel<WaveParProf>, dim3(nblocks_), dim3(64), lds_, stream_, a);
+      else
+        hipLaunchKernelGGL(engine_kernel<WavePar>, dim3(nblocks_), dim3(64), lds_, stream_, a);
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_));
       HIPCHECK(hipStreamSynchronize(stream_));
@@ -416,6 +472,35 @@ class GpuEngine : public Engine {
   uint32_t cap_req_ = 0, cap_rep_ = 0;
   uint64_t epoch_ = 0, cycle_ = 0;
   uint32_t epochs_per_launch_ = 4096;
+  bool profiling_ = false;
+  uint64_t* d_prof_ = nullptr;
+
+ public:
+  // per-stage shader-clock totals: [0] = mean over SM blocks, [1] = mean over channel blocks
+  void dump_profile() {
+    if (!profiling_) return;
+    std::vector<uint64_t> h((size_t)nblocks_ * kProfSlots);
+    HIPCHECK(hipMemcpy(h.data(), d_prof_, h.size() * 8, hipMemcpyDeviceToHost));
+    static const char* names[kProfSlots] = {
+        "sm.receive", "sm.writeback", "sm.hit_complete", "sm.ldst", "sm.dispatch", "sm.read_operands",
+        "sm.alloc_oc", "sm.issue", "sm.fetch", "sm.retire", "sm.inject", "sm.occupancy", "sm.gather",
+        "sm.cta_dispatch", "sm.refill", "sm.cycle_loop", "sm.publish", "-", "-", "-", "mem.gather", "mem.dram",
+        "mem.l2", "mem.icnt", "mem.window_other", "mem.publish", "barrier", "decide", "post", "-", "-", "launch_rest"};
+    double sm[kProfSlots] = {}, mc[kProfSlots] = {}, smt = 0, mct = 0;
+    for (uint32_t b = 0; b < nblocks_; ++b)
+      for (int k = 0; k < kProfSlots; ++k) {
+        double v = (double)h[(size_t)b * kProfSlots + k];
+        if (b < c_.n_sm) { sm[k] += v / c_.n_sm; smt += v / c_.n_sm; }
+        else { mc[k] += v / c_.n_mem; mct += v / c_.n_mem; }
+      }
+    fprintf(stderr, "[asim gpu profile] shader-clock cycles per block (mean), share of block time\n");
+    for (int k = 0; k < kProfSlots; ++k)
+      if (sm[k] + mc[k] > 0)
+        fprintf(stderr, "  %-18s SM %14.0f (%5.1f%%)   MEM %14.0f (%5.1f%%)\n", names[k], sm[k], 100 * sm[k] / smt, mc[k],
+                100 * mc[k] / mct);
+  }
+
+ private:
   KernelDesc kd_{};
   bool fresh_kernel_ = false;
 };

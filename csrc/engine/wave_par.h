@@ -29,6 +29,7 @@ struct WavePar {
   static __device__ __forceinline__ void one(F&& f) {
     if (lane() == 0) f();
   }
+  static __device__ __forceinline__ void prof(int) {}
   static __device__ __forceinline__ void sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -96,19 +96,24 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& 
                       uint32_t n_sub, uint64_t epoch_idx) {
   const SimCfg& c = *x.cfg;
   // 1. arrivals (replies injected by the memory side last epoch)
+  P::prof(12);
   gather_sorted<P>(inbox, incnt, s.id, n_sub, in_cap, t0 * c.per_core, s.inq, kInQ, s.inq_head, s.inq_n,
                    s_scratch_key(s), s_scratch_ref(s), s_scratch_rank(s), kInQ);
   // 2. CTA dispatch (state published at the previous boundary)
+  P::prof(13);
   if (t0 >= ks.ready_cycle)
     cta_dispatch<P>(s, x, ks, pub.sm_req[prev], c.n_sm, (uint32_t)(epoch_idx % c.n_sm));
   // 3. trace window refill
+  P::prof(14);
   sm_refill_window<P>(s, c, *x.k);
   // 4. cycles
+  P::prof(15);
   s.epoch_end = t1;
   if (s.n_cta_active || !sm_idle(s)) {
     for (uint64_t t = t0; t < t1; ++t) sm_cycle<P>(s, x, t);
   }
   s.cycle = t1;
+  P::prof(16);
 }
 
 // publish SM outbox counts + boundary state
@@ -136,8 +141,11 @@ SIM_HDI void sm_publish(SMState& s, const SmCtx& x, const SmKernel& ks, EpochPub
 template <class P>
 SIM_HDI void chan_epoch(ChanState& ch, const MemCtx& x, const Pkt* inbox, const uint32_t* incnt,
                         uint32_t in_cap, uint64_t t0_fs) {
+  P::prof(20);
   mem_gather<P>(ch, *x.cfg, inbox, incnt, in_cap, t0_fs);
+  P::prof(24);
   mem_window<P>(ch, x);
+  P::prof(25);
 }
 
 template <class P>

@@ -60,6 +60,9 @@ struct SeqPar {
   template <class F>
   static SIM_HDI void one(F&& f) { f(); }
   static SIM_HDI void sync() {}
+  // stage profiling stamp (no-op on the CPU; the GPU profiling build records
+  // s_memtime deltas per stage)
+  static SIM_HDI void prof(int) {}
   // index i < n minimising key(i) (ties -> lowest i); key == ~0ull means
   // "not a candidate".  Returns -1 if there is no candidate.
   template <class F>

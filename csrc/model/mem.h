@@ -633,17 +633,21 @@ SIM_HDI void mem_window(ChanState& ch, const MemCtx& x) {
     uint64_t tm = amin(ch.t_dram, amin(ch.t_l2, ch.t_icnt));
     if (tm >= t1) break;
     if (ch.t_dram == tm) {
+      P::prof(21);
       dram_cycle<P>(ch, c, tm);
       ch.t_dram += c.per_dram;
     }
     if (ch.t_l2 == tm) {
+      P::prof(22);
       for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) l2_cycle<P>(ch, ch.sp[j], c, j, tm);
       ch.t_l2 += c.per_l2;
     }
     if (ch.t_icnt == tm) {
+      P::prof(23);
       for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) mem_icnt_cycle<P>(ch, ch.sp[j], c, x, j, tm);
       ch.t_icnt += c.per_icnt;
     }
+    P::prof(24);
   }
 }
 

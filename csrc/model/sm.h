@@ -197,6 +197,9 @@ struct alignas(16) SMState {
   L1Mshr mshr[kMaxL1Mshr];
   L1Pend pend[kMaxPend];
   uint32_t n_pend;
+  uint64_t idoc_mask;     // bit sched*U_COUNT+unit: ID_OC register occupied
+  uint32_t oc_mask;       // occupied operand collectors
+  uint32_t oc_read_mask;  // collectors still reading operands
   uint32_t l1_stamp;
   // ---- interconnect endpoints ----
   Pkt outq[kOutQ];
@@ -592,14 +595,16 @@ SIM_HDI uint32_t reg_bank(const SimCfg& c, uint32_t sched, uint32_t warp, uint32
 template <class P>
 SIM_HDI void sm_read_operands(SMState& s, const SimCfg& c) {
   // each register bank serves reg_port_tp reads per cycle, oldest collector first
+  if (!s.oc_read_mask) return;
   const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
-  for (uint32_t round = 0; round < c.reg_port_tp; ++round) {
+  for (uint32_t round = 0; round < c.reg_port_tp && s.oc_read_mask; ++round) {
     uint32_t bank_busy = 0;
+    const uint32_t want = s.oc_read_mask;
     for (int k = 0; k < noc; ++k) {
       // visit collectors oldest-first
       int best = P::argmin(noc, [&](int i) -> uint64_t {
+        if (!(want >> i & 1u)) return ~0ull;
         const OCUnit& o = s.oc[i];
-        if (!o.valid || o.nread == 0) return ~0ull;
         bool ready = false;
         for (int j = 0; j < 5; ++j)
           if (o.banks[j] != 0xff && !(bank_busy >> o.banks[j] & 1u)) ready = true;
@@ -612,6 +617,7 @@ SIM_HDI void sm_read_operands(SMState& s, const SimCfg& c) {
           bank_busy |= 1u << o.banks[j];
           o.banks[j] = 0xff;
           o.nread--;
+          if (o.nread == 0) s.oc_read_mask &= ~(1u << best);
           s.st.rf_reads++;
           break;  // one operand per collector per round
         }
@@ -624,13 +630,16 @@ template <class P>
 SIM_HDI void sm_dispatch(SMState& s, const SimCfg& c, uint64_t now) {
   const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
   const uint32_t wbw = wb_width(c);
-  // oldest-first over ready collectors
+  // oldest-first over ready collectors (valid, all operands read)
+  const uint32_t ready = s.oc_mask & ~s.oc_read_mask;
+  if (!ready) return;
   uint32_t tried = 0;
   for (int k = 0; k < noc; ++k) {
-    int best = P::argmin(noc, [&](int i) -> uint64_t {
-      const OCUnit& o = s.oc[i];
-      if (!o.valid || o.nread != 0 || (tried >> i & 1u)) return ~0ull;
-      return (uint64_t)o.age;
+    const uint32_t cand = ready & ~tried;
+    if (!cand) break;
+    int best = (cand & (cand - 1)) == 0 ? ffs64(cand) : P::argmin(noc, [&](int i) -> uint64_t {
+      if (!(cand >> i & 1u)) return ~0ull;
+      return (uint64_t)s.oc[i].age;
     });
     if (best < 0) break;
     tried |= 1u << best;
@@ -648,6 +657,7 @@ SIM_HDI void sm_dispatch(SMState& s, const SimCfg& c, uint64_t now) {
       s.ldst.start = (uint32_t)now;
       s.st.mem_insn++;
       o.valid = 0;
+      s.oc_mask &= ~(1u << best);
       continue;
     }
     uint32_t cnt = c.unit_count[u] ? c.unit_count[u] : 1;
@@ -666,6 +676,7 @@ SIM_HDI void sm_dispatch(SMState& s, const SimCfg& c, uint64_t now) {
     e.pad = 0;
     s.fu_next[u][phys] = (uint32_t)now + (o.inst.ii ? o.inst.ii : 1);
     o.valid = 0;
+    s.oc_mask &= ~(1u << best);
   }
 }
 
@@ -674,19 +685,24 @@ SIM_HDI void sm_alloc_collectors(SMState& s, const SimCfg& c) {
   const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
   const uint32_t nsched = c.n_sched;
   const uint32_t per = (c.sub_core && nsched) ? (noc / nsched ? noc / nsched : 1) : (uint32_t)noc;
-  for (uint32_t sc = 0; sc < nsched; ++sc) {
-    for (uint32_t u = 0; u < U_COUNT; ++u) {
+  // visit pending pipeline registers in (scheduler, unit) order via the mask
+  uint64_t pend = s.idoc_mask;
+  while (pend) {
+    const int bit = ffs64(pend);
+    pend &= pend - 1;
+    const uint32_t sc = (uint32_t)bit / U_COUNT, u = (uint32_t)bit % U_COUNT;
+    {
       IdOc& r = s.idoc[sc][u];
-      if (!r.valid) continue;
       // free collector in this scheduler's group
       uint32_t lo = c.sub_core ? (sc * per) % noc : 0;
       uint32_t hi = c.sub_core ? lo + per : (uint32_t)noc;
       if (hi > (uint32_t)noc) hi = noc;
-      int f = -1;
-      for (uint32_t i = lo; i < hi; ++i)
-        if (!s.oc[i].valid) { f = (int)i; break; }
-      if (f < 0) continue;
+      const uint32_t grp = ((hi >= 32 ? 0xffffffffu : ((1u << hi) - 1)) & ~((1u << lo) - 1));
+      const uint32_t freem = grp & ~s.oc_mask;
+      if (!freem) continue;
+      const int f = ffs64(freem);
       OCUnit& o = s.oc[f];
+      s.oc_mask |= 1u << f;
       o.inst = r.inst;
       o.valid = 1;
       o.warp = r.warp;
@@ -704,7 +720,9 @@ SIM_HDI void sm_alloc_collectors(SMState& s, const SimCfg& c) {
           o.banks[j] = 0xff;
         }
       }
+      if (o.nread) s.oc_read_mask |= 1u << f;
       r.valid = 0;
+      s.idoc_mask &= ~(1ull << bit);
     }
   }
 }
@@ -728,6 +746,7 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
   const KernelDesc& k = *x.k;
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
+  const uint64_t idoc_busy = s.idoc_mask;
   // readiness of every warp (lane-parallel)
   uint64_t ready = P::ballot(nw, [&](int w) -> bool {
     uint8_t f = s.w_flags[w];
@@ -743,7 +762,7 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
     if (in.cls == OC_EXIT || in.cls == OC_BARRIER || in.cls == OC_MEMBAR || in.cls == OC_NOP ||
         (in.flags & F_WAITCNT))
       return true;  // handled at issue, no pipeline register needed
-    if (s.idoc[sc][u].valid) return false;
+    if (idoc_busy >> (sc * U_COUNT + u) & 1ull) return false;
     if (u == U_MEM && in.cls == OC_LOAD && s.w_slot_used[w] == 0xff) return false;
     return true;
   });
@@ -825,6 +844,7 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
     IdOc& r = s.idoc[sc][u];
     r.inst = in;
     r.valid = 1;
+    s.idoc_mask |= 1ull << (sc * U_COUNT + u);
     r.warp = (uint8_t)w;
     r.widx = ++s.age_ctr;
     r.pad[0] = 0xff;
@@ -977,17 +997,29 @@ SIM_HDI void sm_refill_window(SMState& s, const SimCfg& c, const KernelDesc& k) 
 template <class P>
 SIM_HDI void sm_cycle(SMState& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
+  P::prof(0);
   sm_receive<P>(s, x, now);
+  P::prof(1);
   sm_writeback<P>(s, c, now);
+  P::prof(2);
   sm_hit_complete<P>(s, now);
+  P::prof(3);
   sm_ldst<P>(s, x, now);
+  P::prof(4);
   sm_dispatch<P>(s, c, now);
+  P::prof(5);
   sm_read_operands<P>(s, c);
+  P::prof(6);
   sm_alloc_collectors<P>(s, c);
+  P::prof(7);
   sm_issue<P>(s, x, now);
+  P::prof(8);
   sm_fetch<P>(s, c);
+  P::prof(9);
   sm_retire<P>(s, x, now);
+  P::prof(10);
   sm_inject<P>(s, x, now);
+  P::prof(11);
   if (s.n_cta_active) {
     s.st.active_cycles++;
     s.st.occupancy_acc += P::sum((int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps),
