@@ -64,6 +64,8 @@ class DistributedSuite:
                 kl = os.path.join(d, args, "traces", "kernelslist.g")
                 if os.path.exists(kl):
                     self.apps.append((app, kl))
+        self.max_concurrency = None
+        self.weights: Dict[str, int] = {}
         ar = os.path.join(root, "all-reduce", "kernelslist.g")
         self.allreduce = ar if os.path.exists(ar) else None
         self.sync = CollectiveSync(world)
@@ -73,17 +75,41 @@ class DistributedSuite:
         args = build_args(self.config, kl, self.engine, extra)
         return self.mod.Simulator(args, self.verbose)
 
+    def concurrency(self) -> int:
+        """Simulations that fit on this GPU at once (each needs one CU per
+        simulated SM and per memory channel, all co-resident)."""
+        if self.engine != "gpu":
+            return 1
+        cus = int(self.mod.gpu_cu_count())
+        cfg = self.mod.parse_config(build_args(self.config, None, "cpu"))
+        per = cfg["n_sm"] + cfg["n_mem"]
+        return max(1, cus // per) if cus else 1
+
+    def _run_app(self, app_kl):
+        app, kl = app_kl
+        s = self._sim(kl)
+        rc = s.run()
+        if rc != 0:
+            raise RuntimeError(f"{app}: simulation failed (deadlock={s.deadlock})\n{s.output[-1500:]}")
+        return app, s.tot_insn, s.tot_cycle
+
     def step(self) -> Dict:
         insn = cycles = 0
         per_app = {}
-        for app, kl in self.apps:
-            s = self._sim(kl)
-            rc = s.run()
-            if rc != 0:
-                raise RuntimeError(f"{app}: simulation failed (deadlock={s.deadlock})\n{s.output[-1500:]}")
-            insn += s.tot_insn
-            cycles += s.tot_cycle
-            per_app[app] = dict(insn=s.tot_insn, cycles=s.tot_cycle)
+        conc = self.concurrency() if self.max_concurrency is None else self.max_concurrency
+        if conc <= 1:
+            results = [self._run_app(x) for x in self.apps]
+        else:
+            from concurrent.futures import ThreadPoolExecutor
+            # longest first keeps both CU groups busy
+            order = sorted(self.apps, key=lambda x: -self.weights.get(x[0], 0))
+            with ThreadPoolExecutor(max_workers=conc) as ex:
+                results = list(ex.map(self._run_app, order))
+        for app, i, c in results:
+            insn += i
+            cycles += c
+            per_app[app] = dict(insn=i, cycles=c)
+            self.weights[app] = i
         if self.allreduce:
             s = self._sim(self.allreduce)
             s.set_collective_hook(lambda d, now, s=s: self.sync(s, d, now))

@@ -108,6 +108,7 @@ PYBIND11_MODULE(_asim, m) {
   m.attr("sizeof_TInst") = sizeof(TInst);
 
   m.def("gpu_available", &gpu_engine_available, "True if a HIP device is usable by the GPU engine");
+  m.def("gpu_cu_count", &gpu_cu_count, "compute units of the current HIP device");
   m.def("option_names", []() {
     OptionRegistry r;
     register_sim_options(r);

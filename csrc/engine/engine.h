@@ -51,6 +51,7 @@ std::unique_ptr<Engine> make_cpu_engine();
 // defined in the HIP engine module; returns nullptr when no GPU is usable
 std::unique_ptr<Engine> make_gpu_engine();
 bool gpu_engine_available();
+int gpu_cu_count();  // compute units of the current HIP device (0 if none)
 
 // helpers shared by both engines
 uint32_t reply_cap(const SimCfg& c);

@@ -18,6 +18,8 @@
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
+#include <condition_variable>
+#include <mutex>
 #include <vector>
 
 #include "engine.h"
@@ -241,6 +243,43 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
 
 namespace {
 
+// Process-wide CU reservation.  Every simulation needs ALL its blocks
+// co-resident (grid barrier) and each block takes one CU (LDS-bound), so
+// concurrent simulations in one process (job-level parallelism on one GPU)
+// must never oversubscribe the CUs: a launch waits until its CUs are free.
+class CuPool {
+ public:
+  static CuPool& get() {
+    static CuPool p;
+    return p;
+  }
+  void init(int cus) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (cap_ == 0) cap_ = free_ = cus;
+  }
+  void acquire(int n) {
+    std::unique_lock<std::mutex> g(mu_);
+    cv_.wait(g, [&] { return free_ >= n; });
+    free_ -= n;
+  }
+  void release(int n) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      free_ += n;
+    }
+    cv_.notify_all();
+  }
+  int capacity() {
+    std::lock_guard<std::mutex> g(mu_);
+    return cap_;
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int cap_ = 0, free_ = 0;
+};
+
 class GpuEngine : public Engine {
  public:
   ~GpuEngine() override {
@@ -260,6 +299,7 @@ class GpuEngine : public Engine {
     hipDeviceProp_t prop;
     HIPCHECK(hipGetDeviceProperties(&prop, dev));
     n_cu_ = prop.multiProcessorCount;
+    CuPool::get().init(n_cu_);
     nblocks_ = c.n_sm + c.n_mem;
     lds_ = kLdsBytes;
     if ((int)nblocks_ > n_cu_)
@@ -346,13 +386,19 @@ class GpuEngine : public Engine {
       a.ctl = d_ctl_;
       HIPCHECK(hipMemsetAsync(d_ctl_, 0, sizeof(GpuCtl), stream_));
       a.prof = d_prof_;
+      CuPool::get().acquire((int)nblocks_);
+      hipError_t le;
       if (profiling_)
         hipLaunchKernelGGL(engine_kernel<WaveParProf>, dim3(nblocks_), dim3(64), lds_, stream_, a);
       else
         hipLaunchKernelGGL(engine_kernel<WavePar>, dim3(nblocks_), dim3(64), lds_, stream_, a);
-      HIPCHECK(hipGetLastError());
-      HIPCHECK(hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_));
-      HIPCHECK(hipStreamSynchronize(stream_));
+      le = hipGetLastError();
+      hipError_t ce = hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_);
+      hipError_t se = hipStreamSynchronize(stream_);
+      CuPool::get().release((int)nblocks_);
+      HIPCHECK(le);
+      HIPCHECK(ce);
+      HIPCHECK(se);
       first = false;
       if (h_ctl_->error) throw std::runtime_error("GPU engine: grid barrier timed out (blocks not co-resident?)");
       epoch_ = h_ctl_->end_epoch;
@@ -518,4 +564,14 @@ std::unique_ptr<Engine> make_gpu_engine() {
   return std::unique_ptr<Engine>(new GpuEngine());
 }
 
+}  // namespace asim
+
+namespace asim {
+int gpu_cu_count() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
+  return p.multiProcessorCount;
+}
 }  // namespace asim

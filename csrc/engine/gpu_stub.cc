@@ -5,3 +5,7 @@ namespace asim {
 std::unique_ptr<Engine> make_gpu_engine() { return nullptr; }
 bool gpu_engine_available() { return false; }
 }  // namespace asim
+
+namespace asim {
+int gpu_cu_count() { return 0; }
+}  // namespace asim
