@@ -2,11 +2,14 @@
 
 The reference's "distributed" fork only adds a constant latency per
 ncclAllReduce to a single simulated GPU (gpu-simulator/main.cc:116-122).
-Here every rank simulates its own GPU; at each collective the ranks
-synchronise their simulated clocks over RCCL (torch.distributed, backend
-"nccl" = RCCL on ROCm, over xGMI) and the collective costs the analytic
-ring/tree time of the simulated interconnect after the LAST rank arrives --
-a conservative PDES synchronisation at collective boundaries.
+Here every rank simulates its own GPU.  At each collective the ranks either
+
+* ``packet`` (default): run the packet-level link model together, exchanging
+  link packets every lookahead epoch with an all-to-all over RCCL/xGMI
+  (parallel/collectives.py, csrc/parallel/linksim.h); or
+* ``ring``/``tree``/``const``: synchronise their simulated clocks (MAX of the
+  arrival cycles over RCCL) and charge the analytic cost after the last rank
+  arrives (CollectiveSync).
 """
 from __future__ import annotations
 
@@ -15,6 +18,7 @@ from typing import Dict, List, Optional
 
 from .. import _native
 from ..sim import build_args
+from .collectives import PacketCollective
 
 
 class CollectiveSync:
@@ -44,7 +48,7 @@ class DistributedSuite:
     """Runs a directory of applications (``<root>/<app>/<args>/traces``)."""
 
     def __init__(self, root: str, config: str = "QV100", engine: str = "gpu", rank: int = 0, world: int = 1,
-                 apps: Optional[List[str]] = None, verbose: bool = False, collective_model: str = "ring"):
+                 apps: Optional[List[str]] = None, verbose: bool = False, collective_model: str = "packet"):
         self.mod = _native.load(prefer_torch_runtime=True)
         self.root = root
         self.config = config
@@ -68,7 +72,7 @@ class DistributedSuite:
         self.weights: Dict[str, int] = {}
         ar = os.path.join(root, "all-reduce", "kernelslist.g")
         self.allreduce = ar if os.path.exists(ar) else None
-        self.sync = CollectiveSync(world)
+        self.sync = PacketCollective() if collective_model == "packet" else CollectiveSync(world)
 
     def _sim(self, kl: str):
         extra = {"-collective_model": self.collective_model}

@@ -9,8 +9,39 @@
 
 namespace py = pybind11;
 using namespace asim;
+static const size_t kLinkPktBytes = sizeof(LinkPkt);
 
 namespace {
+
+py::dict link_dict(const LinkParams& p) {
+  py::dict d;
+  d["link_gbps"] = p.link_gbps;
+  d["latency_ns"] = p.latency_ns;
+  d["links"] = p.links;
+  d["slice_bytes"] = p.slice_bytes;
+  d["max_channels"] = p.max_channels;
+  d["reduce_gbps"] = p.reduce_gbps;
+  return d;
+}
+
+LinkParams link_from(const py::dict& d) {
+  LinkParams p;
+  if (d.contains("link_gbps")) p.link_gbps = d["link_gbps"].cast<double>();
+  if (d.contains("latency_ns")) p.latency_ns = d["latency_ns"].cast<double>();
+  if (d.contains("links")) p.links = d["links"].cast<uint32_t>();
+  if (d.contains("slice_bytes")) p.slice_bytes = d["slice_bytes"].cast<uint32_t>();
+  if (d.contains("max_channels")) p.max_channels = d["max_channels"].cast<uint32_t>();
+  if (d.contains("reduce_gbps")) p.reduce_gbps = d["reduce_gbps"].cast<double>();
+  return p;
+}
+
+CollSpec coll_from(const std::string& kind, uint64_t bytes, int root) {
+  CollSpec c;
+  c.kind = coll_kind(kind);
+  c.bytes = bytes;
+  c.root = root;
+  return c;
+}
 
 py::dict cfg_dict(const SimCfg& c) {
   py::dict d;
@@ -286,6 +317,8 @@ PYBIND11_MODULE(_asim, m) {
                              })
       .def("collective_cycles",
            [](Simulator& s, const std::string& line) { return s.collective_cycles(parse_collective_line(line)); })
+      .def("link_params", [](Simulator& s) { return link_dict(s.link_params()); })
+      .def_property_readonly("core_period_ps", &Simulator::core_period_ps)
       .def("set_collective_hook",
            [](Simulator& s, py::function f) {
              s.set_collective_hook([f](const Command& c, uint64_t now) -> uint64_t {
@@ -296,6 +329,7 @@ PYBIND11_MODULE(_asim, m) {
                d["count"] = c.count;
                d["dtype_bytes"] = c.dtype_bytes;
                d["nranks"] = c.nranks;
+               d["root"] = c.root;
                d["text"] = c.text;
                return f(d, now).cast<uint64_t>();
              });
@@ -311,6 +345,47 @@ PYBIND11_MODULE(_asim, m) {
         std::vector<uint8_t> v(str.begin(), str.end());
         s.engine().restore(v);
       });
+
+  py::class_<LinkSim>(m, "LinkSim")
+      .def(py::init([](const py::dict& p, const std::string& kind, uint64_t bytes, int root, int rank, int world,
+                       uint64_t start_ps) { return new LinkSim(link_from(p), coll_from(kind, bytes, root), rank, world,
+                                                              start_ps); }),
+           py::arg("params"), py::arg("kind"), py::arg("bytes"), py::arg("root"), py::arg("rank"), py::arg("world"),
+           py::arg("start_ps"))
+      .def("emit",
+           [](LinkSim& l, uint64_t t_end) {
+             std::vector<LinkPkt> out;
+             l.emit(t_end, out);
+             return py::bytes(reinterpret_cast<const char*>(out.data()), out.size() * sizeof(LinkPkt));
+           })
+      .def("receive",
+           [](LinkSim& l, py::bytes b) {
+             std::string s = b;
+             if (s.size() % sizeof(LinkPkt)) throw std::invalid_argument("LinkSim.receive: ragged packet buffer");
+             std::vector<LinkPkt> v(s.size() / sizeof(LinkPkt));
+             if (!v.empty()) memcpy(v.data(), s.data(), s.size());
+             l.receive(v.data(), v.size());
+           })
+      .def("next_event", &LinkSim::next_event)
+      .def("done", &LinkSim::done)
+      .def_property_readonly("finish_ps", &LinkSim::finish_ps)
+      .def_property_readonly("epoch_ps", &LinkSim::epoch_ps)
+      .def_property_readonly("channels", &LinkSim::channels)
+      .def_property_readonly("packets_sent", &LinkSim::packets_sent)
+      .def_readonly_static("packet_bytes", &kLinkPktBytes);
+
+  m.def(
+      "linksim_run_local",
+      [](const py::dict& p, const std::string& kind, uint64_t bytes, int root, const std::vector<uint64_t>& start) {
+        uint64_t ep = 0, pk = 0;
+        auto fin = linksim_run_local(link_from(p), coll_from(kind, bytes, root), start, &ep, &pk);
+        py::dict d;
+        d["finish_ps"] = fin;
+        d["epochs"] = ep;
+        d["packets"] = pk;
+        return d;
+      },
+      py::arg("params"), py::arg("kind"), py::arg("bytes"), py::arg("root"), py::arg("start_ps"));
 
   py::class_<PowerModel>(m, "PowerModel")
       .def(py::init<>())

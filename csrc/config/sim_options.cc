@@ -267,6 +267,9 @@ const OptDef kOptions[] = {
     {"-xgmi_link_bandwidth_gbps", 'f', "153.0", "per-link xGMI bandwidth (GB/s)"},
     {"-xgmi_link_latency_ns", 'f', "1000.0", "collective step latency (ns)"},
     {"-xgmi_links_per_gpu", 'u', "7", "xGMI links per GPU"},
+    {"-collective_slice_bytes", 'u', "131072", "packet model: bytes per link packet (RCCL slice)"},
+    {"-collective_max_channels", 'u', "16", "packet model: max parallel rings (channels)"},
+    {"-collective_reduce_gbps", 'f', "900.0", "packet model: local memory bandwidth for reduce/copy (GB/s)"},
 };
 
 uint32_t parse_u(const std::string& s, const char* what) {
@@ -768,6 +771,9 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.xgmi_link_gbps = r.getd("-xgmi_link_bandwidth_gbps");
   d.xgmi_latency_ns = r.getd("-xgmi_link_latency_ns");
   d.xgmi_links = (uint32_t)r.getu("-xgmi_links_per_gpu");
+  d.coll_slice_bytes = (uint32_t)r.getu("-collective_slice_bytes");
+  d.coll_max_channels = (uint32_t)r.getu("-collective_max_channels");
+  d.coll_reduce_gbps = r.getd("-collective_reduce_gbps");
   d.concurrent_kernel_sm = r.getb("-gpgpu_concurrent_kernel_sm") ? 1 : 0;
   d.max_concurrent_kernel = (int32_t)r.geti("-gpgpu_max_concurrent_kernel");
   d.power_enabled = r.getb("-power_simulation_enabled");

@@ -56,6 +56,9 @@ struct DriverOpts {
   double xgmi_link_gbps = 153.0;
   double xgmi_latency_ns = 1000.0;
   uint32_t xgmi_links = 7;
+  uint32_t coll_slice_bytes = 131072;
+  uint32_t coll_max_channels = 16;
+  double coll_reduce_gbps = 900.0;
   int32_t concurrent_kernel_sm = 0;
   int32_t max_concurrent_kernel = 32;
   bool power_enabled = false;

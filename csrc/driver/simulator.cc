@@ -1,5 +1,6 @@
 #include "simulator.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstring>
@@ -102,6 +103,26 @@ uint64_t Simulator::collective_cycles(const Command& c) const {
   // link per direction; the tree uses log2(n) steps)
   const double n = std::max(1, c.nranks);
   if (n <= 1) return 0;
+  bool packet_ok = m == "packet";
+  if (packet_ok) {
+    try {
+      coll_kind(c.coll);
+    } catch (const std::invalid_argument&) {
+      packet_ok = false;  // unknown collective: analytic ring cost below
+    }
+  }
+  if (packet_ok) {
+    // standalone run: every rank reaches the collective at the same time and
+    // the link model emulates all of them in this process
+    CollSpec cs;
+    cs.kind = coll_kind(c.coll);
+    cs.bytes = c.bytes;
+    cs.root = std::max(0, c.root);
+    std::vector<uint64_t> start((size_t)c.nranks, 0);
+    auto fin = linksim_run_local(link_params(), cs, start);
+    uint64_t mx = *std::max_element(fin.begin(), fin.end());
+    return (uint64_t)std::ceil((double)mx / core_period_ps());
+  }
   const double bw = dopt_.xgmi_link_gbps * 1e9;  // bytes/s per link
   const double alpha = dopt_.xgmi_latency_ns * 1e-9;
   const double S = (double)c.bytes;
@@ -122,6 +143,17 @@ uint64_t Simulator::collective_cycles(const Command& c) const {
   }
   const double core_hz = 1e15 / (double)cfg_.per_core;
   return (uint64_t)std::ceil(t * core_hz);
+}
+
+LinkParams Simulator::link_params() const {
+  LinkParams p;
+  p.link_gbps = dopt_.xgmi_link_gbps;
+  p.latency_ns = dopt_.xgmi_latency_ns;
+  p.links = std::max<uint32_t>(1, dopt_.xgmi_links);
+  p.slice_bytes = dopt_.coll_slice_bytes;
+  p.max_channels = std::max<uint32_t>(1, dopt_.coll_max_channels);
+  p.reduce_gbps = dopt_.coll_reduce_gbps;
+  return p;
 }
 
 void Simulator::do_collective(const Command& c) {

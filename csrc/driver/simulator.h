@@ -10,6 +10,7 @@
 
 #include "../config/sim_options.h"
 #include "../engine/engine.h"
+#include "../parallel/linksim.h"
 #include "../power/power.h"
 
 namespace asim {
@@ -73,6 +74,10 @@ class Simulator {
   bool deadlock() const { return deadlock_; }
   // analytic collective duration in core cycles
   uint64_t collective_cycles(const Command& c) const;
+  // parameters of the packet-level link model (-collective_model packet)
+  LinkParams link_params() const;
+  // simulated core clock period in picoseconds
+  double core_period_ps() const { return (double)cfg_.per_core / 1000.0; }
 
  private:
   void print(const char* fmt, ...);

@@ -1,0 +1,115 @@
+// Packet-level inter-GPU link model for collectives (-collective_model packet).
+//
+// The reference only charges a constant latency per ncclAllReduce
+// (gpu-simulator/main.cc:116-122, -nccl_allreduce_latency gpu-sim.cc:760-762)
+// and drops the call's arguments (tracer_tool.cu:800-819).  Here a collective
+// is decomposed the way RCCL executes it -- channels of ring/chain pipelines
+// (or direct all-to-all sends), each chunk cut into slices -- and every slice
+// is a packet on a point-to-point xGMI link with serialisation (bytes / link
+// bandwidth), link latency, per-link FIFO contention, and a local reduce/copy
+// cost on the receiving GPU.
+//
+// Execution is a conservative parallel discrete-event simulation: one LinkSim
+// per simulated GPU (= per MI355X rank).  Time advances in epochs no longer
+// than the link latency, so a packet sent in an epoch can only arrive in a
+// later one; after every epoch the ranks exchange the packets they emitted
+// with an all-to-all (RCCL over xGMI in parallel/collectives.py).  The same
+// classes run all ranks inside one process (run_local) -- the two paths are
+// bit-identical, which is what the multi-process tests check.
+#pragma once
+#include <cstdint>
+#include <queue>
+#include <string>
+#include <vector>
+
+namespace asim {
+
+struct LinkParams {
+  double link_gbps = 153.0;     // per direction, per link (GB/s = bytes/ns)
+  double latency_ns = 1000.0;   // per hop
+  uint32_t links = 7;           // links per GPU (fully connected: one per peer when world-1 <= links)
+  uint32_t slice_bytes = 131072;
+  uint32_t max_channels = 16;
+  double reduce_gbps = 900.0;   // local memory bandwidth used by reduce / copy
+};
+
+enum CollKind : int32_t { CK_ALLREDUCE = 0, CK_ALLGATHER, CK_REDUCESCATTER, CK_BROADCAST, CK_REDUCE, CK_ALLTOALL,
+                          CK_SENDRECV };
+
+CollKind coll_kind(const std::string& name);  // AllReduce, AllGather, ... (throws if unknown)
+
+struct CollSpec {
+  CollKind kind = CK_ALLREDUCE;
+  uint64_t bytes = 0;  // buffer size (same convention as the analytic model)
+  int32_t root = 0;
+};
+
+// one slice on the wire: 32 bytes, packed into 4 x int64 for the exchange
+struct LinkPkt {
+  int32_t src, dst;
+  int32_t chan, step;
+  int32_t slice;
+  uint32_t bytes;
+  uint64_t arrive_ps;
+};
+static_assert(sizeof(LinkPkt) == 32, "LinkPkt must stay 32 bytes");
+
+class LinkSim {
+ public:
+  LinkSim(const LinkParams& p, const CollSpec& c, int rank, int world, uint64_t start_ps);
+  // emit every packet whose send starts before t_end (appended to out)
+  void emit(uint64_t t_end, std::vector<LinkPkt>& out);
+  // deliver packets addressed to this rank (any order; processed deterministically)
+  void receive(const LinkPkt* p, size_t n);
+  // earliest time this rank has local work (UINT64_MAX if none)
+  uint64_t next_event() const;
+  bool done() const { return recv_left_ == 0 && send_left_ == 0; }
+  uint64_t finish_ps() const { return finish_ps_; }
+  uint64_t epoch_ps() const { return epoch_ps_; }
+  uint32_t channels() const { return nch_; }
+  uint64_t packets_sent() const { return sent_; }
+
+  // the rank's role at (channel, step): peer it sends to / receives from (-1 none)
+  int send_peer(int c, int k) const;
+  int recv_peer(int c, int k) const;
+  bool recv_reduces(int k) const;
+
+ private:
+  struct Ready {
+    uint64_t t;
+    int32_t chan, step, slice;
+    bool operator>(const Ready& o) const {
+      if (t != o.t) return t > o.t;
+      if (chan != o.chan) return chan > o.chan;
+      if (step != o.step) return step > o.step;
+      return slice > o.slice;
+    }
+  };
+  uint32_t slice_len(int s) const;
+  int link_of(int dst) const;
+  void push_send(uint64_t t, int c, int k, int s);
+
+  LinkParams p_;
+  CollSpec c_;
+  int rank_, world_;
+  uint64_t start_ps_;
+  uint32_t nch_ = 1;
+  std::vector<int> stride_;  // ring stride per channel
+  int nsteps_ = 0;
+  uint64_t chunk_ = 0;       // bytes per (channel, step)
+  uint32_t nslices_ = 1;
+  double ps_per_byte_link_ = 0, ps_per_byte_mem_ = 0;
+  uint64_t lat_ps_ = 0, epoch_ps_ = 0;
+  std::priority_queue<Ready, std::vector<Ready>, std::greater<Ready>> ready_;
+  std::vector<uint64_t> link_free_;
+  uint64_t recv_left_ = 0, send_left_ = 0, sent_ = 0;
+  uint64_t finish_ps_ = 0;
+};
+
+// Run all `world` ranks in one process (identical results to the distributed
+// driver).  start_ps[r] = when rank r reaches the collective.  Returns the
+// finish time of every rank.
+std::vector<uint64_t> linksim_run_local(const LinkParams& p, const CollSpec& c, const std::vector<uint64_t>& start_ps,
+                                        uint64_t* epochs = nullptr, uint64_t* packets = nullptr);
+
+}  // namespace asim
