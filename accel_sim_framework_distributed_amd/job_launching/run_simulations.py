@@ -102,6 +102,10 @@ def setup_run(o, reg: common.Registry, cfg_name: str, extra: str, base_cfg: str,
         text += "\n# Accel-Sim Parameters\n" + open(tcfg).read()
     with open(os.path.join(run_dir, "gpgpusim.config"), "w") as f:
         f.write(text)
+    # side files the config refers to by relative name (power XMLs, icnt, hw csv)
+    for side in glob.glob(os.path.join(os.path.dirname(base_cfg), "*")):
+        if side.endswith((".xml", ".icnt", ".csv")):
+            shutil.copy2(side, run_dir)
 
     if o.trace_dir:
         command = f"{sim_bin} -config ./gpgpusim.config -trace ./traces/kernelslist.g"

@@ -320,6 +320,14 @@ def write_config(name_or_opts, out_dir: str, extra: Dict[str, str] | None = None
         f.write(render(gp, sorted(gp)))
     with open(p2, "w") as f:
         f.write(render(tr, sorted(tr)))
+    # AccelWattch XMLs next to the configs (SIM / HW / HYBRID modes share the
+    # uncalibrated defaults until power.calibrate rewrites them)
+    from ..power.xmlcfg import default_params, write_xml
+    pname = name_or_opts if isinstance(name_or_opts, str) else "custom"
+    for mode in ("sim", "hw", "hybrid"):
+        xp = os.path.join(out_dir, f"accelwattch_sass_{mode}.xml")
+        if not os.path.exists(xp):
+            write_xml(xp, default_params(pname), comment=f"{pname} defaults (uncalibrated)")
     return p1, p2
 
 

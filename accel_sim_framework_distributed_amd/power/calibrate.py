@@ -1,0 +1,113 @@
+"""Calibrate AccelWattch scaling factors against measured power.
+
+Same formulation as the reference's util/accelwattch/quadprog_solver.m:30-92
+(solved there with MATLAB ``lsqlin``): rows are kernels, columns the
+simulated per-component average power at the current scaling factors, ``b``
+the measured hardware power; find multiplicative corrections ``x`` with
+``lower <= x <= upper`` and optional ordering constraints ``C x <= d``
+("an INT op costs no more than an FP op" ...) minimising ``||A x - b||^2``.
+Solved with scipy (bounded least squares, or SLSQP when constraints are
+given).  ``apply_factors`` folds ``x`` back into an XML.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .report import COMPONENTS
+from .xmlcfg import read_xml, write_xml
+
+# report component -> XML parameters it scales
+COMPONENT_PARAMS: Dict[str, List[str]] = {
+    "IBP": ["TOT_INST"], "ICP": ["IC_H", "IC_M"], "DCP": ["DC_RH", "DC_RM", "DC_WH", "DC_WM"], "TCP": [],
+    "CCP": ["CC_H", "CC_M"], "SHRDP": ["SHRD_ACC"], "RFP": ["REG_RD", "REG_WR"], "INTP": ["INT_ACC"],
+    "FPUP": ["FP_ACC"], "DPUP": ["DP_ACC"], "INT_MUL24P": [], "INT_MUL32P": [], "INT_MULP": ["INT_MUL_ACC"],
+    "INT_DIVP": [], "FP_MULP": ["FP_MUL_ACC"], "FP_DIVP": [], "FP_SQRTP": ["FP_SQRT_ACC"], "FP_LGP": ["FP_LG_ACC"],
+    "FP_SINP": ["FP_SIN_ACC"], "FP_EXP": ["FP_EXP_ACC"], "DP_MULP": ["DP_MUL_ACC"], "DP_DIVP": [],
+    "TENSORP": ["TENSOR_ACC"], "TEXP": ["TEX_ACC"], "SCHEDP": ["FP_INT"], "L2CP": ["L2_RH", "L2_RM", "L2_WH", "L2_WM"],
+    "MCP": ["MEM_PRE"], "NOCP": ["NOC_A"], "DRAMP": ["MEM_RD", "MEM_WR"], "PIPEP": ["PIPE_A"],
+    "IDLE_COREP": ["idle_core_power"], "CONSTP": ["constant_power"], "STATICP": None,  # None: every static_* param
+}
+
+
+def design_matrix(kernels: Sequence[Dict], components: Sequence[str] = COMPONENTS) -> np.ndarray:
+    return np.array([[k["avg"].get(c, 0.0) for c in components] for k in kernels], dtype=np.float64)
+
+
+def fit_scaling(A: np.ndarray, b: np.ndarray, lower: float | np.ndarray = 0.1, upper: float | np.ndarray = 1000.0,
+                C: Optional[np.ndarray] = None, d: Optional[np.ndarray] = None,
+                fixed: Optional[Iterable[int]] = None) -> np.ndarray:
+    """x >= 0 minimising ||A x - b||^2 with bounds and C x <= d.  Columns that
+    are identically zero (component never active) keep x = 1, as do ``fixed``."""
+    A = np.asarray(A, np.float64)
+    b = np.asarray(b, np.float64)
+    n = A.shape[1]
+    lo = np.broadcast_to(np.asarray(lower, np.float64), (n,)).copy()
+    hi = np.broadcast_to(np.asarray(upper, np.float64), (n,)).copy()
+    free = np.abs(A).sum(axis=0) > 0
+    for i in fixed or ():
+        free[i] = False
+    x = np.ones(n)
+    idx = np.flatnonzero(free)
+    if len(idx) == 0:
+        return x
+    # account for the fixed columns at x = 1
+    b_eff = b - A[:, ~free].sum(axis=1)
+    Af = A[:, idx]
+    # column scaling keeps the problem well conditioned (powers span 0.01..100 W)
+    scale = np.linalg.norm(Af, axis=0)
+    scale[scale == 0] = 1.0
+    As = Af / scale
+    lo_s, hi_s = lo[idx] * scale, hi[idx] * scale
+    if C is None:
+        from scipy.optimize import lsq_linear
+        r = lsq_linear(As, b_eff, bounds=(lo_s, hi_s), method="bvls", lsmr_tol="auto")
+        x[idx] = r.x / scale
+        return x
+    from scipy.optimize import minimize
+    C = np.asarray(C, np.float64)
+    d = np.asarray(d, np.float64) - C[:, ~free].sum(axis=1)
+    Cs = C[:, idx] / scale
+
+    def f(z):
+        r = As @ z - b_eff
+        return 0.5 * float(r @ r), As.T @ r
+
+    z0 = np.clip(scale, lo_s, hi_s)
+    cons = [dict(type="ineq", fun=lambda z: d - Cs @ z, jac=lambda z: -Cs)]
+    r = minimize(f, z0, jac=True, bounds=list(zip(lo_s, hi_s)), constraints=cons, method="SLSQP",
+                 options=dict(maxiter=500, ftol=1e-12))
+    x[idx] = r.x / scale
+    return x
+
+
+def mape(pred: Sequence[float], meas: Sequence[float]) -> Tuple[float, float]:
+    """(mean absolute percentage error %, mean absolute error W)."""
+    p, m = np.asarray(pred, np.float64), np.asarray(meas, np.float64)
+    return float(np.mean(np.abs(p - m) / np.abs(m)) * 100.0), float(np.mean(np.abs(p - m)))
+
+
+def leave_one_out(A: np.ndarray, b: np.ndarray, **kw) -> np.ndarray:
+    """Predictions where each kernel's power comes from a fit that excluded it."""
+    A = np.asarray(A, np.float64)
+    b = np.asarray(b, np.float64)
+    out = np.zeros(len(b))
+    for i in range(len(b)):
+        keep = np.arange(len(b)) != i
+        x = fit_scaling(A[keep], b[keep], **kw)
+        out[i] = A[i] @ x
+    return out
+
+
+def apply_factors(xml_in: str, xml_out: str, x: Sequence[float], components: Sequence[str] = COMPONENTS) -> Dict:
+    """Multiply the XML parameters behind every component by its factor."""
+    p = read_xml(xml_in)
+    for c, f in zip(components, x):
+        keys = COMPONENT_PARAMS.get(c)
+        if keys is None:
+            keys = [k for k in p if k.startswith("static_")]
+        for k in keys:
+            p[k] = p.get(k, 1.0) * float(f)
+    write_xml(xml_out, p, comment=f"calibrated from {xml_in}")
+    return p

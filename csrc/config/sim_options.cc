@@ -247,7 +247,8 @@ const OptDef kOptions[] = {
     {"-accelwattch_hybrid_perfsim_CYCLES", 'b', "0", ""},
     {"-accelwattch_hybrid_perfsim_VOLTAGE", 'b', "0", ""},
     {"-power_trace_enabled", 'b', "0", ""},
-    {"-power_trace_zlevel", 'i', "6", ""},
+    {"-power_trace_zlevel", 'i', "6", "(traces are written uncompressed)"},
+    {"-power_report_file", 's', "accelwattch_power_report.log", "per-kernel power report (extension)"},
     {"-steady_power_levels_enabled", 'b', "0", ""},
     {"-steady_state_definition", 's', "8:4", ""},
     // ---- legacy / misspelled names used by shipped configs (reference
@@ -779,6 +780,24 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.power_enabled = r.getb("-power_simulation_enabled");
   d.power_xml = r.gets("-accelwattch_xml_file");
   d.power_mode = (int32_t)r.geti("-power_simulation_mode");
+  d.hw_perf_file = r.gets("-hw_perf_file_name");
+  d.hw_perf_bench = r.gets("-hw_perf_bench_name");
+  {
+    static const char* hw[17] = {"L1_RH", "L1_RM", "L1_WH", "L1_WM", "CC_ACC", "SHARED_ACC", "DRAM_RD", "DRAM_WR",
+                                 "L2_RH", "L2_RM", "L2_WH", "L2_WM", "NOC", "PIPE_DUTY", "NUM_SM_IDLE", "CYCLES",
+                                 "VOLTAGE"};
+    for (int i = 0; i < 17; ++i) d.hybrid_use_sim[i] = r.getb(std::string("-accelwattch_hybrid_perfsim_") + hw[i]);
+  }
+  d.power_trace = r.getb("-power_trace_enabled");
+  d.steady_power = r.getb("-steady_power_levels_enabled");
+  {
+    auto v = split(strip_ws(r.gets("-steady_state_definition")), ':');
+    if (v.size() == 2) {
+      d.steady_dev_pct = atof(v[0].c_str());
+      d.steady_samples = (uint32_t)std::max(1, atoi(v[1].c_str()));
+    }
+  }
+  d.power_report_file = r.gets("-power_report_file");
   {
     auto v = split(strip_ws(r.gets("-gpgpu_runtime_stat")), ':');
     d.stat_sample_freq = v.empty() || v[0].empty() ? 500 : parse_u(v[0], "-gpgpu_runtime_stat");

@@ -64,6 +64,14 @@ struct DriverOpts {
   bool power_enabled = false;
   std::string power_xml;
   int32_t power_mode = 0;
+  std::string hw_perf_file;
+  std::string hw_perf_bench;
+  bool hybrid_use_sim[17] = {};   // indexed by asim::HwCounter
+  bool power_trace = false;
+  bool steady_power = false;
+  double steady_dev_pct = 8;
+  uint32_t steady_samples = 4;
+  std::string power_report_file;
   uint64_t stat_sample_freq = 500;
   std::string engine;             // cpu | gpu
   bool trace_enabled = false;

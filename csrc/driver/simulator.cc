@@ -8,6 +8,23 @@
 
 namespace asim {
 
+// out = a - b for POD stat vectors of 64-bit counters (b empty = zeros)
+template <class T>
+static void stat_delta(const std::vector<T>& a, const std::vector<T>& b, std::vector<T>& out) {
+  static_assert(sizeof(T) % 8 == 0, "stat structs are arrays of 64-bit counters");
+  out.resize(a.size());
+  for (size_t i = 0; i < a.size(); ++i) {
+    const uint64_t* x = (const uint64_t*)&a[i];
+    uint64_t* o = (uint64_t*)&out[i];
+    if (i < b.size()) {
+      const uint64_t* y = (const uint64_t*)&b[i];
+      for (size_t k = 0; k < sizeof(T) / 8; ++k) o[k] = x[k] - y[k];
+    } else {
+      for (size_t k = 0; k < sizeof(T) / 8; ++k) o[k] = x[k];
+    }
+  }
+}
+
 Simulator::Simulator(const std::vector<std::string>& args) {
   t_start_ = std::chrono::steady_clock::now();
   register_sim_options(reg_);
@@ -27,6 +44,16 @@ Simulator::Simulator(const std::vector<std::string>& args) {
     power_.reset(new PowerModel());
     std::string err;
     if (!power_->load_xml(dopt_.power_xml, &err)) throw std::runtime_error("power model: " + err);
+    power_report_.reset(new std::ofstream(dopt_.power_report_file));
+    if (dopt_.power_trace) {
+      power_trace_.reset(new std::ofstream("accelwattch_power_trace.csv"));
+      ptrack_.write_trace_header(*power_trace_);
+    }
+    if (dopt_.steady_power) {
+      power_steady_.reset(new std::ofstream("accelwattch_steady_state.csv"));
+      *power_steady_ << "kernel,start_cycle,end_cycle,samples,avg_power\n";
+      ptrack_.set_steady(dopt_.steady_dev_pct, dopt_.steady_samples);
+    }
   }
 }
 
@@ -210,7 +237,13 @@ void Simulator::do_kernel(const Command& c) {
   RunLimits lim;
   if (dopt_.max_cycle) lim.max_cycle = (uint64_t)dopt_.max_cycle;
   auto ts = std::chrono::steady_clock::now();
-  RunResult rr = eng_->run_kernel(start, dopt_.flush_l1, lim);
+  RunResult rr;
+  if (power_) {
+    ptrack_.begin_kernel();
+    rr = run_sampled(start, lim, rk.h.name);
+  } else {
+    rr = eng_->run_kernel(start, dopt_.flush_l1, lim);
+  }
   auto te = std::chrono::steady_clock::now();
   sim_s_ += std::chrono::duration<double>(te - ts).count();
   if (dopt_.flush_l2) eng_->flush_l2();
@@ -224,14 +257,8 @@ void Simulator::do_kernel(const Command& c) {
   // per-kernel deltas
   std::vector<SMStats> dsm(sm.size());
   std::vector<MemStats> dmem(mem.size());
-  auto diff = [](const void* a, const void* b, void* out, size_t n) {
-    const uint64_t* x = (const uint64_t*)a;
-    const uint64_t* y = (const uint64_t*)b;
-    uint64_t* o = (uint64_t*)out;
-    for (size_t i = 0; i < n / 8; ++i) o[i] = x[i] - y[i];
-  };
-  for (size_t i = 0; i < sm.size(); ++i) diff(&sm[i], &prev_sm_[i], &dsm[i], sizeof(SMStats));
-  for (size_t i = 0; i < mem.size(); ++i) diff(&mem[i], &prev_mem_[i], &dmem[i], sizeof(MemStats));
+  stat_delta(sm, prev_sm_, dsm);
+  stat_delta(mem, prev_mem_, dmem);
   prev_sm_ = sm;
   prev_mem_ = mem;
   KernelResult r;
@@ -261,9 +288,16 @@ void Simulator::do_kernel(const Command& c) {
   tot_warp_insn_ += r.warp_insn;
   tot_cta_ += kd.n_cta;
   if (power_) {
-    Activity a = PowerModel::activity_from_stats(dsm, dmem, r.cycles);
-    PowerReport p = power_->compute(a, 1e9 / (double)cfg_.per_core, cfg_.n_sm);
-    r.avg_power_w = p.total;
+    r.avg_power_w = ptrack_.kernel_avg_power();
+    char hdr[512];
+    snprintf(hdr, sizeof(hdr), "kernel_name = %s\nkernel_launch_uid = %u\ngpu_sim_cycle = %llu", r.name.c_str(), r.uid,
+             (unsigned long long)r.cycles);
+    ptrack_.write_kernel(*power_report_, hdr);
+    if (power_steady_) {
+      ptrack_.write_steady(*power_steady_, r.name);
+      power_steady_->flush();
+    }
+    if (power_trace_) power_trace_->flush();
   }
   results_.push_back(r);
   print_kernel_stats(r, dsm, dmem);
@@ -273,6 +307,64 @@ void Simulator::do_kernel(const Command& c) {
     print("GPGPU-Sim uArch: ERROR ** deadlock detected: last writeback core %u @ gpu_sim_cycle %llu (+ gpu_tot_sim_cycle %llu)\n",
           0u, (unsigned long long)r.cycles, (unsigned long long)start);
   }
+}
+
+RunResult Simulator::run_sampled(uint64_t start, const RunLimits& lim0, const std::string& kname) {
+  // HW / HYBRID modes take one sample per kernel (the hardware counters are per kernel)
+  const bool hw = dopt_.power_mode == 1 || dopt_.power_mode == 2;
+  const uint64_t freq = std::max<uint64_t>(dopt_.stat_sample_freq, std::max<uint32_t>(1, cfg_.icnt_latency));
+  const double mhz = 1e9 / (double)cfg_.per_core;
+  Activity hwa;
+  bool have_hw = false;
+  if (hw) {
+    have_hw = PowerModel::activity_from_hw_csv(dopt_.hw_perf_file, dopt_.hw_perf_bench, kname, hwa, cfg_.n_sm);
+    if (!have_hw)
+      print("GPGPU-Sim: WARNING no hw_perf entry for bench '%s' kernel '%s' in %s: power uses simulated counters\n",
+            dopt_.hw_perf_bench.c_str(), kname.c_str(), dopt_.hw_perf_file.c_str());
+  }
+  std::vector<SMStats> sm0, sm1, dsm;
+  std::vector<MemStats> m0, m1, dm;
+  eng_->stats(sm0, m0);
+  RunResult tot;
+  bool resume = false;
+  uint64_t t_prev = std::max(start, eng_->now());
+  for (;;) {
+    RunLimits l = lim0;
+    l.resume = resume;
+    resume = true;
+    if (!hw) {
+      const uint64_t nxt = t_prev + freq;
+      l.max_cycle = lim0.max_cycle ? std::min<uint64_t>(lim0.max_cycle, nxt) : nxt;
+    }
+    RunResult r = eng_->run_kernel(start, dopt_.flush_l1, l);
+    tot.epochs += r.epochs;
+    tot.end_cycle = r.end_cycle;
+    tot.done = r.done;
+    tot.deadlock = r.deadlock;
+    const uint64_t now = eng_->now();
+    eng_->stats(sm1, m1);
+    stat_delta(sm1, sm0, dsm);
+    stat_delta(m1, m0, dm);
+    Activity a = PowerModel::activity_from_stats(dsm, dm, now > t_prev ? now - t_prev : 1);
+    if (hw && have_hw) {
+      bool use_sim[HW_COUNT];
+      for (int i = 0; i < HW_COUNT; ++i) use_sim[i] = dopt_.power_mode == 2 && dopt_.hybrid_use_sim[i];
+      a = PowerModel::merge_hw(a, hwa, use_sim);
+    }
+    PowerReport p = power_->compute(a, mhz, cfg_.n_sm);
+    ptrack_.add_sample(p, a, now);
+    if (power_trace_) ptrack_.write_trace_line(*power_trace_, p, now);
+    sm0.swap(sm1);
+    m0.swap(m1);
+    t_prev = now;
+    if (r.done || r.deadlock) break;
+    if (lim0.max_cycle && now >= lim0.max_cycle) {
+      tot.hit_limit = true;
+      break;
+    }
+    if (r.epochs == 0) throw std::runtime_error("power sampling: engine made no progress");
+  }
+  return tot;
 }
 
 void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMStats>& sm,

@@ -2,6 +2,7 @@
 // loop (gpu-simulator/main.cc:55-206) re-built around the epoch engines.
 #pragma once
 #include <chrono>
+#include <fstream>
 #include <functional>
 #include <map>
 #include <memory>
@@ -85,12 +86,16 @@ class Simulator {
   void do_collective(const Command& c);
   void print_kernel_stats(const KernelResult& r, const std::vector<SMStats>& sm, const std::vector<MemStats>& mem);
   void print_sim_time();
+  // run the current kernel in gpu_stat_sample_freq slices, one power sample per slice
+  RunResult run_sampled(uint64_t start, const RunLimits& lim, const std::string& kname);
 
   OptionRegistry reg_;
   SimCfg cfg_{};
   DriverOpts dopt_;
   std::unique_ptr<Engine> eng_;
   std::unique_ptr<PowerModel> power_;
+  PowerTracker ptrack_;
+  std::unique_ptr<std::ofstream> power_report_, power_trace_, power_steady_;
   std::vector<Command> cmds_;
   std::string out_;
   bool echo_ = true;

@@ -105,11 +105,14 @@ class CpuEngine : public Engine {
     if (start > cycle_) cycle_ = start;
     const SimCfg& c = c_;
     const uint64_t E = c.icnt_latency;
-    for (auto& s : sms_) {
-      SmCtx x = ctx_sm(0);
-      sm_kernel_init<SeqPar>(s, x, s.ks, cycle_, flush_l1 ? 1u : 0u);
+    if (!lim.resume) {
+      for (auto& s : sms_) {
+        SmCtx x = ctx_sm(0);
+        sm_kernel_init<SeqPar>(s, x, s.ks, cycle_, flush_l1 ? 1u : 0u);
+      }
+      ready_ = sms_.empty() ? 0 : sms_[0].ks.ready_cycle;
     }
-    const uint64_t ready = sms_.empty() ? 0 : sms_[0].ks.ready_cycle;
+    const uint64_t ready = ready_;
     for (;;) {
       const uint32_t cur = (uint32_t)(epoch_ & 1), prev = cur ^ 1u;
       const uint64_t t0 = cycle_, t1 = t0 + E;
@@ -152,6 +155,7 @@ class CpuEngine : public Engine {
   }
 
   uint64_t now() const override { return cycle_; }
+  uint64_t ready_ = 0;  // cycle the current kernel may start issuing CTAs
 
   void memcpy_fill_l2(uint64_t addr, uint64_t bytes) override {
     host_memcpy_fill(chs_.data(), (uint32_t)chs_.size(), c_, addr, bytes);

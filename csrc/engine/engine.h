@@ -15,6 +15,7 @@ namespace asim {
 struct RunLimits {
   uint64_t max_cycle = 0;   // absolute cycle cap (0 = none)
   uint64_t max_epochs = 0;  // safety cap (0 = none)
+  bool resume = false;      // continue the current kernel after a hit_limit stop (no re-init)
 };
 
 struct RunResult {

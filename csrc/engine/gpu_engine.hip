@@ -357,8 +357,9 @@ class GpuEngine : public Engine {
   RunResult run_kernel(uint64_t start, bool flush_l1, const RunLimits& lim) override {
     RunResult res;
     if (start > cycle_) cycle_ = start;
-    const uint64_t ready = cycle_ + c_.kernel_launch_latency + (uint64_t)c_.tb_launch_latency * kd_.n_cta;
-    bool first = true;
+    if (!lim.resume) ready_ = cycle_ + c_.kernel_launch_latency + (uint64_t)c_.tb_launch_latency * kd_.n_cta;
+    const uint64_t ready = ready_;
+    bool first = !lim.resume;
     for (;;) {
       GpuArgs a{};
       a.cfg = d_cfg_;
@@ -417,6 +418,7 @@ class GpuEngine : public Engine {
   }
 
   uint64_t now() const override { return cycle_; }
+  uint64_t ready_ = 0;
 
   void memcpy_fill_l2(uint64_t addr, uint64_t bytes) override {
     std::vector<ChanState> hc(c_.n_mem);

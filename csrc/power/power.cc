@@ -14,6 +14,22 @@ const char* const kPwrActName[PA_COUNT] = {
     "FP_SQRT_ACC", "FP_LG_ACC", "FP_SIN_ACC", "FP_EXP_ACC", "DP_MUL_ACC", "TENSOR_ACC", "TEX_ACC",
     "MEM_RD", "MEM_WR", "MEM_PRE", "L2_RH", "L2_RM", "L2_WH", "L2_WM", "NOC_A", "PIPE_A"};
 
+const char* const kPwrCmpName[PC_COUNT] = {
+    "IBP", "ICP", "DCP", "TCP", "CCP", "SHRDP", "RFP", "INTP", "FPUP", "DPUP", "INT_MUL24P", "INT_MUL32P", "INT_MULP",
+    "INT_DIVP", "FP_MULP", "FP_DIVP", "FP_SQRTP", "FP_LGP", "FP_SINP", "FP_EXP", "DP_MULP", "DP_DIVP", "TENSORP", "TEXP",
+    "SCHEDP", "L2CP", "MCP", "NOCP", "DRAMP", "PIPEP", "IDLE_COREP", "CONSTP", "STATICP"};
+
+const char* const kHwCounterName[HW_COUNT] = {"L1_RH", "L1_RM", "L1_WH", "L1_WM", "CC_ACC", "SHARED_ACC",
+                                              "DRAM_RD", "DRAM_WR", "L2_RH", "L2_RM", "L2_WH", "L2_WM",
+                                              "NOC", "PIPE_DUTY", "NUM_SM_IDLE", "CYCLES", "VOLTAGE"};
+
+// activity -> report component
+static const int kActCmp[PA_COUNT] = {
+    PC_IB,  PC_SCHED, PC_IC,     PC_IC,     PC_DC,      PC_DC,     PC_DC,     PC_DC,     PC_CC,
+    PC_CC,  PC_SHRD,  PC_RF,     PC_RF,     PC_INT,     PC_FPU,    PC_DPU,    PC_INT_MUL, PC_FP_MUL,
+    PC_FP_SQRT, PC_FP_LG, PC_FP_SIN, PC_FP_EXP, PC_DP_MUL, PC_TENSOR, PC_TEX,
+    PC_DRAM, PC_DRAM, PC_MC,     PC_L2C,    PC_L2C,     PC_L2C,    PC_L2C,    PC_NOC,    PC_PIPE};
+
 // Per-access base energies (nJ) for a 12-16 nm class GPU.  These play the
 // role of McPAT's per-access energies; the XML scaling factors calibrate
 // them (util: accel_sim_framework_distributed_amd.power.calibrate).
@@ -117,7 +133,117 @@ PowerReport PowerModel::compute(const Activity& a, double core_mhz, uint32_t n_s
   if (a.a[PA_DC_RH] + a.a[PA_DC_RM] + a.a[PA_DC_WH] + a.a[PA_DC_WM] > 0) r.static_w += param("static_l1_flane", 0) * busy_frac;
   if (a.a[PA_L2_RH] + a.a[PA_L2_RM] + a.a[PA_L2_WH] + a.a[PA_L2_WM] > 0) r.static_w += param("static_l2_flane", 0);
   r.total = r.dynamic + r.static_w + r.constant + r.idle;
+  for (int i = 0; i < PA_COUNT; ++i) r.cmp[kActCmp[i]] += r.dynamic_w[i];
+  r.cmp[PC_IDLE_CORE] = r.idle;
+  r.cmp[PC_CONST] = r.constant;
+  r.cmp[PC_STATIC] = r.static_w;
   return r;
+}
+
+Activity PowerModel::merge_hw(const Activity& sim, const Activity& hw, const bool use_sim[HW_COUNT]) {
+  Activity a = sim;
+  auto pick = [&](int hwc, int act) {
+    if (!use_sim[hwc]) a.a[act] = hw.a[act];
+  };
+  pick(HW_L1_RH, PA_DC_RH);
+  pick(HW_L1_RM, PA_DC_RM);
+  pick(HW_L1_WH, PA_DC_WH);
+  pick(HW_L1_WM, PA_DC_WM);
+  pick(HW_CC_ACC, PA_CC_H);
+  pick(HW_SHRD_ACC, PA_SHRD_ACC);
+  pick(HW_DRAM_RD, PA_MEM_RD);
+  pick(HW_DRAM_WR, PA_MEM_WR);
+  pick(HW_L2_RH, PA_L2_RH);
+  pick(HW_L2_RM, PA_L2_RM);
+  pick(HW_L2_WH, PA_L2_WH);
+  pick(HW_L2_WM, PA_L2_WM);
+  pick(HW_NOC, PA_NOC_A);
+  pick(HW_PIPE_DUTY, PA_PIPE_A);
+  if (!use_sim[HW_NUM_SM_IDLE]) a.idle_sms = hw.idle_sms;
+  if (!use_sim[HW_VOLTAGE]) a.voltage = hw.voltage;
+  if (!use_sim[HW_CYCLES] && hw.cycles > 0) {
+    // the simulated instruction-side counts stay; the sample spans the HW time
+    a.cycles = hw.cycles;
+  }
+  return a;
+}
+
+void PowerTracker::begin_kernel() {
+  for (auto& x : k_cmp_) x = Agg{};
+  for (auto& x : k_act_) x = Agg{};
+  k_tot_ = Agg{};
+  k_lanes_ = 0;
+  k_n_ = 0;
+  k_series_.clear();
+}
+
+void PowerTracker::add_sample(const PowerReport& r, const Activity& a, uint64_t cycle) {
+  for (int i = 0; i < PC_COUNT; ++i) k_cmp_[i].add(r.cmp[i]);
+  for (int i = 0; i < PA_COUNT; ++i) k_act_[i].add(a.a[i]);
+  k_tot_.add(r.total);
+  g_tot_.add(r.total);
+  k_lanes_ += a.avg_lanes;
+  ++k_n_;
+  ++g_n_;
+  k_series_.emplace_back(cycle, r.total);
+}
+
+void PowerTracker::write_kernel(std::ostream& os, const std::string& header) const {
+  const double n = k_n_ ? (double)k_n_ : 1.0;
+  os << header << "\n";
+  os << "Kernel Average Power Data:\n";
+  os << "kernel_avg_power = " << k_tot_.sum / n << "\n";
+  for (int i = 0; i < PC_COUNT; ++i) os << "gpu_avg_" << kPwrCmpName[i] << " = " << k_cmp_[i].sum / n << "\n";
+  for (int i = 0; i < PA_COUNT; ++i) os << "gpu_avg_" << kPwrActName[i] << " = " << k_act_[i].sum / n << "\n";
+  os << "gpu_avg_threads_per_warp = " << k_lanes_ / n << "\n";
+  for (int i = 0; i < PA_COUNT; ++i) os << "gpu_tot_" << kPwrActName[i] << " = " << k_act_[i].sum << "\n";
+  os << "\nKernel Maximum Power Data:\n";
+  os << "kernel_max_power = " << k_tot_.mx << "\n";
+  for (int i = 0; i < PC_COUNT; ++i) os << "gpu_max_" << kPwrCmpName[i] << " = " << k_cmp_[i].mx << "\n";
+  for (int i = 0; i < PA_COUNT; ++i) os << "gpu_max_" << kPwrActName[i] << " = " << k_act_[i].mx << "\n";
+  os << "\nKernel Minimum Power Data:\n";
+  os << "kernel_min_power = " << k_tot_.mn << "\n";
+  for (int i = 0; i < PC_COUNT; ++i) os << "gpu_min_" << kPwrCmpName[i] << " = " << k_cmp_[i].mn << "\n";
+  for (int i = 0; i < PA_COUNT; ++i) os << "gpu_min_" << kPwrActName[i] << " = " << k_act_[i].mn << "\n";
+  os << "\nAccumulative Power Statistics Over Previous Kernels:\n";
+  os << "gpu_tot_avg_power = " << (g_n_ ? g_tot_.sum / (double)g_n_ : 0.0) << "\n";
+  os << "gpu_tot_max_power = " << g_tot_.mx << "\n";
+  os << "gpu_tot_min_power = " << g_tot_.mn << "\n\n\n";
+  os.flush();
+}
+
+void PowerTracker::write_trace_header(std::ostream& os) const {
+  os << "cycle,total_power";
+  for (int i = 0; i < PC_COUNT; ++i) os << "," << kPwrCmpName[i];
+  os << "\n";
+}
+
+void PowerTracker::write_trace_line(std::ostream& os, const PowerReport& r, uint64_t cycle) const {
+  os << cycle << "," << r.total;
+  for (int i = 0; i < PC_COUNT; ++i) os << "," << r.cmp[i];
+  os << "\n";
+}
+
+void PowerTracker::write_steady(std::ostream& os, const std::string& kernel) const {
+  // greedy left-to-right segmentation of the sample series
+  size_t i = 0;
+  while (i < k_series_.size()) {
+    size_t j = i + 1;
+    double sum = k_series_[i].second;
+    while (j < k_series_.size()) {
+      const double mean = (sum + k_series_[j].second) / (double)(j - i + 1);
+      bool ok = true;
+      for (size_t q = i; q <= j && ok; ++q)
+        ok = std::fabs(k_series_[q].second - mean) <= mean * st_dev_ / 100.0;
+      if (!ok) break;
+      sum += k_series_[j].second;
+      ++j;
+    }
+    if (j - i >= st_n_)
+      os << kernel << "," << k_series_[i].first << "," << k_series_[j - 1].first << "," << (j - i) << ","
+         << sum / (double)(j - i) << "\n";
+    i = j;
+  }
 }
 
 Activity PowerModel::activity_from_stats(const std::vector<SMStats>& dsm, const std::vector<MemStats>& dmem,

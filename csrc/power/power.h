@@ -13,6 +13,7 @@
 // product (counters x coefficients) and the host evaluates per kernel.
 #pragma once
 #include <map>
+#include <ostream>
 #include <string>
 #include <vector>
 
@@ -38,7 +39,25 @@ struct Activity {
   bool int_used = false, fp_used = false, dp_used = false, sfu_used = false, tex_used = false, tensor_used = false;
 };
 
+// report components (labels of the reference's pwr_cmp_t,
+// accelwattch/gpgpu_sim_wrapper.cc:42-77)
+enum PwrCmp : int {
+  PC_IB = 0, PC_IC, PC_DC, PC_TC, PC_CC, PC_SHRD, PC_RF, PC_INT, PC_FPU, PC_DPU, PC_INT_MUL24, PC_INT_MUL32, PC_INT_MUL,
+  PC_INT_DIV, PC_FP_MUL, PC_FP_DIV, PC_FP_SQRT, PC_FP_LG, PC_FP_SIN, PC_FP_EXP, PC_DP_MUL, PC_DP_DIV, PC_TENSOR, PC_TEX,
+  PC_SCHED, PC_L2C, PC_MC, PC_NOC, PC_DRAM, PC_PIPE, PC_IDLE_CORE, PC_CONST, PC_STATIC, PC_COUNT
+};
+extern const char* const kPwrCmpName[PC_COUNT];
+
+// hardware counters of hw_perf.csv usable in HW / HYBRID mode
+// (reference hw_perf_t, power_interface.cc:194-226; -accelwattch_hybrid_perfsim_<name>)
+enum HwCounter : int {
+  HW_L1_RH = 0, HW_L1_RM, HW_L1_WH, HW_L1_WM, HW_CC_ACC, HW_SHRD_ACC, HW_DRAM_RD, HW_DRAM_WR, HW_L2_RH, HW_L2_RM,
+  HW_L2_WH, HW_L2_WM, HW_NOC, HW_PIPE_DUTY, HW_NUM_SM_IDLE, HW_CYCLES, HW_VOLTAGE, HW_COUNT
+};
+extern const char* const kHwCounterName[HW_COUNT];  // option suffixes (SHARED_ACC, DRAM_RD, ...)
+
 struct PowerReport {
+  double cmp[PC_COUNT] = {};
   double dynamic_w[PA_COUNT] = {};
   double dynamic = 0;
   double static_w = 0;
@@ -62,12 +81,50 @@ class PowerModel {
   // hw_perf.csv row -> activity (HW mode); returns false if not found
   static bool activity_from_hw_csv(const std::string& csv, const std::string& bench, const std::string& kernel,
                                    Activity& out, uint32_t n_sm);
+  // HW (all counters from hardware) / HYBRID (counters with use_sim[i] set
+  // come from the simulator) merge; instruction-side activity is always simulated
+  static Activity merge_hw(const Activity& sim, const Activity& hw, const bool use_sim[HW_COUNT]);
   static double base_nj(int act);
   // coefficient vector (W per access-per-cycle at 1 MHz) for matrix evaluation
   std::vector<double> coefficients(double core_mhz) const;
 
  private:
   std::map<std::string, double> p_;
+};
+
+// Per-kernel and cumulative avg / max / min of every component over the
+// samples of a kernel (reference print_power_kernel_stats,
+// gpgpu_sim_wrapper.cc:974-1041) and the optional per-sample trace.
+class PowerTracker {
+ public:
+  void begin_kernel();
+  void add_sample(const PowerReport& r, const Activity& a, uint64_t cycle);
+  size_t kernel_samples() const { return k_n_; }
+  double kernel_avg_power() const { return k_n_ ? k_tot_.sum / (double)k_n_ : 0.0; }
+  void write_kernel(std::ostream& os, const std::string& header) const;
+  void write_trace_header(std::ostream& os) const;
+  void write_trace_line(std::ostream& os, const PowerReport& r, uint64_t cycle) const;
+  // steady-state levels: runs of >= n samples within +-dev% of their mean
+  void set_steady(double dev_pct, uint32_t n) { st_dev_ = dev_pct; st_n_ = n; }
+  void write_steady(std::ostream& os, const std::string& kernel) const;
+
+ private:
+  struct Agg {
+    double sum = 0, mx = 0, mn = 0;
+    bool any = false;
+    void add(double v) {
+      sum += v;
+      mx = any ? (v > mx ? v : mx) : v;
+      mn = any ? (v < mn ? v : mn) : v;
+      any = true;
+    }
+  };
+  Agg k_cmp_[PC_COUNT], k_act_[PA_COUNT], k_tot_, g_tot_;
+  double k_lanes_ = 0;
+  size_t k_n_ = 0, g_n_ = 0;
+  std::vector<std::pair<uint64_t, double>> k_series_;
+  double st_dev_ = 8;
+  uint32_t st_n_ = 4;
 };
 
 }  // namespace asim
