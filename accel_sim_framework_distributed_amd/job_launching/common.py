@@ -103,7 +103,8 @@ class Registry:
     def base_file(self, base: str) -> str:
         desc = self.base[base]
         if "base_file" in desc:
-            return os.path.expandvars(desc["base_file"])
+            p = os.path.expandvars(desc["base_file"])
+            return p if os.path.isabs(p) else os.path.join(REPO_ROOT, p)
         from ..models import presets
         d = os.path.join(config_root(), desc["preset"])
         p = os.path.join(d, "gpgpusim.config")

@@ -1,0 +1,287 @@
+#!/usr/bin/env python3
+"""Correlate simulated per-kernel stats with hardware measurements.
+
+Reference: util/plotting/plot-correlation.py (getAppData :32-103 -- error %,
+MAE :77-90, Pearson correlation :95, NRMSE :99; options :657-710) and
+correl_mappings.py (CorrelStat table).  Inputs here:
+
+* simulation: a ``get_stats.py -k -K`` CSV (rows ``app/args--kernel--N``,
+  one column per config);
+* hardware: ``hw_stats`` output -- ``<hw_dir>/<app>/<args>/run_<i>/`` with
+  rocprofv3 ``*kernel_trace.csv`` files (MI355X) -- or a flat CSV
+  ``app,args,kernel,instance,<stat>...`` for data measured elsewhere.
+
+Kernels are matched by launch order within an application; per-app values
+are the sum over kernels (the reference's per-app aggregation), and the
+headline **cycle MAE** is the mean over apps of |sim - hw| / hw x 100.
+Stats are described by Python callables (``CorrelStat``) instead of the
+reference's eval'd strings; ``-d`` loads extra mappings from a Python file
+defining ``CORREL_STATS``.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import math
+import os
+import re
+import sys
+from collections import OrderedDict, defaultdict
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+if __package__ in (None, ""):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    from accel_sim_framework_distributed_amd.job_launching import get_stats  # noqa: E402
+    from accel_sim_framework_distributed_amd.plotting import svg  # noqa: E402
+else:
+    from ..job_launching import get_stats
+    from . import svg
+
+
+@dataclass
+class CorrelStat:
+    chart_name: str
+    sim_stat: str                                  # get_stats stat regex (block name)
+    hw_eval: Callable[[Dict[str, List[float]], float], float]   # (hw columns over runs, clock MHz) -> value
+    plotfile: str
+    hw_names: Sequence[str] = ()                   # device names this mapping applies to ('' = any)
+    drop_hw_below: float = 0.0
+    log: bool = True
+    sim_scale: float = 1.0
+
+
+def _mean(v):
+    return float(np.mean(v)) if len(v) else float("nan")
+
+
+CORREL_STATS: List[CorrelStat] = [
+    CorrelStat("Cycles", r"gpu_sim_cycle\s*=\s*(.*)",
+               lambda hw, mhz: _mean(hw["duration_ns"]) * mhz / 1000.0, "cycles"),
+    CorrelStat("Instructions (thread)", r"gpu_sim_insn\s*=\s*(.*)",
+               lambda hw, mhz: _mean(hw["thread_insts"]) if "thread_insts" in hw else float("nan"), "insn"),
+    CorrelStat("L2 read accesses", r"\s+L2_cache_stats_breakdown\[GLOBAL_ACC_R\]\[TOTAL_ACCESS\]\s*=\s*(.*)",
+               lambda hw, mhz: _mean(hw["TCC_REQ_sum"]) if "TCC_REQ_sum" in hw else float("nan"), "l2-reads"),
+]
+
+
+# --------------------------------------------------------------------------- HW
+def _norm_kernel(name: str) -> str:
+    n = name.strip().strip('"')
+    n = re.sub(r"\s*\[clone .*\]$", "", n)
+    return n.split("(")[0].split("<")[0].strip()
+
+
+def load_hw_rocprof(hw_dir: str, burn: int = 0) -> Dict[str, List[Dict[str, List[float]]]]:
+    """{app/args: [kernel_0 {col: [values over runs]}, kernel_1 ...]} from
+    ``<hw_dir>/<app>/<args>/run_<i>/**/*kernel_trace.csv``."""
+    out: Dict[str, List[Dict[str, List[float]]]] = {}
+    for args_dir in sorted(glob.glob(os.path.join(hw_dir, "*", "*"))):
+        if not os.path.isdir(args_dir):
+            continue
+        app = f"{os.path.basename(os.path.dirname(args_dir))}/{os.path.basename(args_dir)}"
+        runs = sorted(glob.glob(os.path.join(args_dir, "run_*")), key=lambda p: int(p.rsplit("_", 1)[1]))[burn:]
+        kernels: List[Dict[str, List[float]]] = []
+        for r in runs:
+            rows = []
+            for f in glob.glob(os.path.join(r, "**", "*kernel_trace.csv"), recursive=True):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        try:
+                            t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
+                        except (KeyError, ValueError):
+                            continue
+                        rows.append((t0, t1, row.get("Kernel_Name", "")))
+            rows.sort()
+            counters = _load_counters(r)
+            for i, (t0, t1, name) in enumerate(rows):
+                while len(kernels) <= i:
+                    kernels.append(defaultdict(list))
+                kernels[i]["duration_ns"].append(float(t1 - t0))
+                kernels[i]["name"] = [_norm_kernel(name)]  # type: ignore[list-item]
+                for k, v in (counters[i] if i < len(counters) else {}).items():
+                    kernels[i][k].append(v)
+        if kernels:
+            out[app] = [dict(k) for k in kernels]
+    return out
+
+
+def _load_counters(run_dir: str) -> List[Dict[str, float]]:
+    """Per-dispatch counter values from rocprofv3 ``*counter_collection.csv``."""
+    per: Dict[int, Dict[str, float]] = {}
+    for f in glob.glob(os.path.join(run_dir, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                try:
+                    d = int(row["Dispatch_Id"])
+                    per.setdefault(d, {})[row["Counter_Name"] + "_sum"] = \
+                        per.get(d, {}).get(row["Counter_Name"] + "_sum", 0.0) + float(row["Counter_Value"])
+                except (KeyError, ValueError):
+                    continue
+    return [per[k] for k in sorted(per)]
+
+
+def load_hw_flat(path: str) -> Dict[str, List[Dict[str, List[float]]]]:
+    """Flat CSV: app,args,kernel,instance,<stat columns> (one row per run)."""
+    tmp: Dict[str, Dict[int, Dict[str, List[float]]]] = defaultdict(dict)
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            key = f"{row['app']}/{row['args']}"
+            i = int(row.get("instance", 0))
+            k = tmp[key].setdefault(i, defaultdict(list))
+            k["name"] = [_norm_kernel(row.get("kernel", ""))]
+            for c, v in row.items():
+                if c in ("app", "args", "kernel", "instance"):
+                    continue
+                try:
+                    k[c].append(float(v))
+                except (TypeError, ValueError):
+                    pass
+    return {a: [dict(d[i]) for i in sorted(d)] for a, d in tmp.items()}
+
+
+# -------------------------------------------------------------------------- SIM
+def load_sim(csv_path: str) -> Tuple[Dict[str, Dict[str, Dict[str, List[float]]]], List[str]]:
+    """{stat: {config: {app/args: [per-kernel values in launch order]}}}, configs."""
+    blocks = get_stats.parse_csv_blocks(open(csv_path).read())
+    out: Dict[str, Dict[str, Dict[str, List[float]]]] = {}
+    configs: List[str] = []
+    for stat, rows in blocks.items():
+        per_cfg: Dict[str, Dict[str, List[Tuple[int, float]]]] = defaultdict(lambda: defaultdict(list))
+        for order, (row, vals) in enumerate(rows.items()):
+            app = row.split("--")[0]
+            for cfg, v in vals.items():
+                if cfg not in configs:
+                    configs.append(cfg)
+                try:
+                    per_cfg[cfg][app].append((order, float(v)))
+                except (TypeError, ValueError):
+                    pass
+        out[stat] = {c: {a: [v for _, v in sorted(lst)] for a, lst in apps.items()} for c, apps in per_cfg.items()}
+    return out, configs
+
+
+# ------------------------------------------------------------------------ stats
+def error_metrics(hw: Sequence[float], sim: Sequence[float]) -> Dict[str, float]:
+    h, s = np.asarray(hw, np.float64), np.asarray(sim, np.float64)
+    ok = (h > 0) & np.isfinite(h) & np.isfinite(s)
+    h, s = h[ok], s[ok]
+    if len(h) == 0:
+        return dict(n=0)
+    err = (s - h) / h * 100.0
+    r = dict(n=int(len(h)), mae=float(np.mean(np.abs(err))), mean_err=float(np.mean(err)),
+             agg_err=float(np.sum(np.abs(s - h)) / np.sum(h) * 100.0),
+             nrmse=float(np.sqrt(np.mean((s - h) ** 2)) / np.mean(h)),
+             rpd=float(np.mean(np.abs(s - h) / ((s + h) / 2)) * 100.0))
+    r["correl"] = float(np.corrcoef(h, s)[0, 1]) if len(h) > 1 and np.std(h) > 0 and np.std(s) > 0 else float("nan")
+    return r
+
+
+def correlate(sim_csv: str, hw: Dict[str, List[Dict[str, List[float]]]], clock_mhz: float,
+              stats: Sequence[CorrelStat] = CORREL_STATS, blacklist: Sequence[str] = (),
+              hw_err_tolerance: float = 30.0, err_threshold: float = 9e9) -> Dict:
+    sim, configs = load_sim(sim_csv)
+    bl = [re.compile(b) for b in blacklist if b.strip()]
+    result = OrderedDict()
+    for st in stats:
+        if st.sim_stat not in sim:
+            continue
+        per_cfg = OrderedDict()
+        for cfg in configs:
+            apps = sim[st.sim_stat].get(cfg, {})
+            app_pts, k_pts = [], []
+            for app, svals in apps.items():
+                if app not in hw or any(b.search(app) for b in bl):
+                    continue
+                hk = hw[app]
+                n = min(len(hk), len(svals))
+                if n == 0:
+                    continue
+                hv = [st.hw_eval(hk[i], clock_mhz) for i in range(n)]
+                sv = [svals[i] * st.sim_scale for i in range(n)]
+                # HW spread check (max-min over runs relative to mean) on cycles
+                spread = [np.ptp(hk[i]["duration_ns"]) / max(1e-9, np.mean(hk[i]["duration_ns"])) * 100
+                          for i in range(n) if "duration_ns" in hk[i] and len(hk[i]["duration_ns"]) > 1]
+                noisy = bool(spread) and max(spread) > hw_err_tolerance
+                for i in range(n):
+                    if math.isfinite(hv[i]) and hv[i] > st.drop_hw_below:
+                        k_pts.append((hv[i], sv[i], f"{app}--{i}"))
+                ha, sa = float(np.nansum(hv)), float(np.sum(sv))
+                if math.isfinite(ha) and ha > st.drop_hw_below and not noisy:
+                    if abs(sa - ha) / ha * 100 <= err_threshold:
+                        app_pts.append((ha, sa, app))
+            per_cfg[cfg] = dict(apps=app_pts, kernels=k_pts,
+                                app_metrics=error_metrics([p[0] for p in app_pts], [p[1] for p in app_pts]),
+                                kernel_metrics=error_metrics([p[0] for p in k_pts], [p[1] for p in k_pts]))
+        result[st.chart_name] = dict(stat=st, configs=per_cfg)
+    return result
+
+
+def write_outputs(res: Dict, out_dir: str, plotname: str = "correl") -> List[str]:
+    os.makedirs(out_dir, exist_ok=True)
+    files, summary = [], {}
+    for chart, d in res.items():
+        st: CorrelStat = d["stat"]
+        series = {cfg: v["apps"] for cfg, v in d["configs"].items()}
+        body = [f"<h2>{chart}</h2>"]
+        for cfg, v in d["configs"].items():
+            m = v["app_metrics"]
+            if m.get("n"):
+                body.append(f"<p><b>{cfg}</b>: {m['n']} apps, MAE {m['mae']:.2f}%, aggregate error "
+                            f"{m['agg_err']:.2f}%, correl {m['correl']:.4f}, NRMSE {m['nrmse']:.4f}</p>")
+            summary.setdefault(chart, {})[cfg] = dict(app=v["app_metrics"], kernel=v["kernel_metrics"])
+        body.append(svg.scatter(series, f"{chart}: simulation vs hardware (per app)", f"hardware {chart}",
+                                f"simulated {chart}", log=st.log))
+        kseries = {cfg: v["kernels"] for cfg, v in d["configs"].items()}
+        body.append(svg.scatter(kseries, f"{chart}: per kernel", f"hardware {chart}", f"simulated {chart}",
+                                log=st.log))
+        p = os.path.join(out_dir, f"{plotname}-{st.plotfile}.html")
+        with open(p, "w") as f:
+            f.write(svg.page(chart, body))
+        files.append(p)
+    p = os.path.join(out_dir, f"{plotname}-summary.json")
+    with open(p, "w") as f:
+        json.dump(summary, f, indent=1)
+    files.append(p)
+    return files
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("-c", "--csv_file", required=True, help="get_stats.py -k -K output")
+    ap.add_argument("-H", "--hardware_dir", default="", help="hw_stats output directory (rocprofv3 runs)")
+    ap.add_argument("-F", "--hardware_csv", default="", help="flat hardware CSV instead of -H")
+    ap.add_argument("-d", "--data_mappings", default="", help="python file defining CORREL_STATS")
+    ap.add_argument("-B", "--cycle_runs_to_burn", type=int, default=1)
+    ap.add_argument("-b", "--blacklist", default="", help="file of app regexes to exclude")
+    ap.add_argument("-t", "--hw_err_tolerance", type=float, default=30.0)
+    ap.add_argument("-E", "--err_calc_threadhold", type=float, default=9e9)
+    ap.add_argument("--clock_mhz", type=float, default=2400.0, help="shader clock of the measured GPU")
+    ap.add_argument("-p", "--plotname", default="correl")
+    ap.add_argument("-o", "--out_dir", default="correl-html")
+    o = ap.parse_args(argv)
+    hw = load_hw_flat(o.hardware_csv) if o.hardware_csv else load_hw_rocprof(o.hardware_dir, o.cycle_runs_to_burn)
+    stats = CORREL_STATS
+    if o.data_mappings:
+        ns: Dict = {}
+        exec(compile(open(o.data_mappings).read(), o.data_mappings, "exec"), ns)  # user's own mapping file
+        stats = ns.get("CORREL_STATS", stats)
+    bl = open(o.blacklist).read().splitlines() if o.blacklist else []
+    res = correlate(o.csv_file, hw, o.clock_mhz, stats, bl, o.hw_err_tolerance, o.err_calc_threadhold)
+    for chart, d in res.items():
+        for cfg, v in d["configs"].items():
+            m = v["app_metrics"]
+            if m.get("n"):
+                print(f"{chart:28s} {cfg:24s} apps={m['n']:3d} MAE={m['mae']:7.2f}% agg_err={m['agg_err']:7.2f}% "
+                      f"correl={m['correl']:.4f} nrmse={m['nrmse']:.4f}")
+    for f in write_outputs(res, o.out_dir, o.plotname):
+        print("wrote", f)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""Tune a simulator configuration to the GPU the micro-benchmarks ran on.
+
+Reference behaviour (util/tuner/tuner.py:15-68, README.md): parse the
+``-option value`` lines printed by the micro-benchmark suite, substitute them
+into a config template, and write ``<device>/gpgpusim.config`` +
+``trace.config``; then search the parameters micro-benchmarks cannot
+demystify (warp scheduler x L2 interleave granularity x partition hash x DRAM
+scheduler) by simulating every combination and keeping the one with the
+lowest cycle error against hardware.
+
+Differences by design: the template is a preset of this framework
+(models/presets.py, default MI355X) rendered on the fly; every tuned flag is
+validated against the simulator's option registry (an unknown flag would be
+fatal at simulation time); the suite is the CDNA4 HIP one (csrc/ubench,
+``tools/run_ubench.sh``).
+
+    tuner.py -s gpurun_out/ubench [-b MI355X] [-o configs/tuned]
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import itertools
+import os
+import re
+import sys
+from typing import Dict, List, Optional, Tuple
+
+if __package__ in (None, ""):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    from accel_sim_framework_distributed_amd.models import presets  # noqa: E402
+else:
+    from ..models import presets
+
+_OPT = re.compile(r"^(-[A-Za-z0-9_:]+)\s+(.+?)\s*$")
+_DEV = re.compile(r"^#\s*device:\s*([^(]+?)\s*\(")
+
+
+def parse_stats(paths: List[str]) -> Tuple[Dict[str, str], Dict[str, str], str]:
+    """(option -> value, '# key value' measurements, device name) from ubench logs."""
+    files: List[str] = []
+    for p in paths:
+        files += sorted(glob.glob(os.path.join(p, "*.log"))) if os.path.isdir(p) else [p]
+    opts: Dict[str, str] = {}
+    meas: Dict[str, str] = {}
+    device = "undefined"
+    for f in files:
+        for line in open(f, errors="replace"):
+            m = _OPT.match(line)
+            if m:
+                opts[m.group(1)] = m.group(2)
+                continue
+            d = _DEV.match(line)
+            if d:
+                device = d.group(1).strip().replace(" ", "_")
+                continue
+            if line.startswith("# "):
+                toks = line[2:].split()
+                if len(toks) == 2:
+                    meas[toks[0]] = toks[1]
+    return opts, meas, device
+
+
+def validate(opts: Dict[str, str]) -> List[str]:
+    """Flags the simulator does not know (would be fatal)."""
+    from .. import _native
+    names = set(_native.load().option_names())
+    return [k for k in opts if k not in names]
+
+
+def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/tuned",
+         name: Optional[str] = None) -> Tuple[str, Dict[str, str]]:
+    opts, meas, device = parse_stats(stats_paths)
+    bad = validate(opts)
+    if bad:
+        raise ValueError(f"micro-benchmarks printed unknown options: {bad}")
+    cfg = presets.get_preset(base)
+    notes = []
+    # the cycle model's per-sub-partition L2 capacity is a compile-time limit
+    # (its tag arrays live in LDS on the GPU engine): keep the geometry,
+    # reduce the set count to fit and say so
+    if "-gpgpu_cache:dl2" in opts:
+        from .. import _native
+        max_lines = int(_native.load().limits["l2_lines"])
+        head, rest = opts["-gpgpu_cache:dl2"].split(",", 1)
+        f = head.split(":")
+        sets, assoc = int(f[1]), int(f[3])
+        if sets * assoc > max_lines:
+            new_sets = max(1, max_lines // assoc)
+            f[1] = str(new_sets)
+            opts["-gpgpu_cache:dl2"] = ":".join(f) + "," + rest
+            notes.append(f"L2 per sub-partition clamped from {sets}x{assoc} to {new_sets}x{assoc} lines "
+                         f"(simulator limit {max_lines} lines)")
+    applied = {}
+    for k, v in opts.items():
+        if cfg.get(k) != v:
+            applied[k] = v
+        cfg[k] = v
+    out = os.path.join(out_root, name or device)
+    presets.write_config(cfg, out)
+    with open(os.path.join(out, "TUNING.md"), "w") as f:
+        f.write(f"# Tuned configuration for {device}\n\nBase preset: {base}\n\n")
+        f.write("| option | tuned value | preset value |\n|---|---|---|\n")
+        base_cfg = presets.get_preset(base)
+        for k in sorted(applied):
+            f.write(f"| `{k}` | `{applied[k]}` | `{base_cfg.get(k, '-')}` |\n")
+        for n in notes:
+            f.write(f"\nNote: {n}\n")
+        if meas:
+            f.write("\n## Raw measurements\n\n")
+            for k in sorted(meas):
+                f.write(f"- {k}: {meas[k]}\n")
+    return out, applied
+
+
+# --- search over the parameters the micro-benchmarks cannot demystify --------
+SEARCH_SPACE = [("LINEAR", "IPOLY"), ("RR", "GTO"), ("32B", "256B"), ("FRFCFS", "FCFS")]
+
+
+def search_configs(base: str) -> List[str]:
+    """The 16 ``BASE-SASS-<hash>-<sched>-<gran>-<dram>`` config names
+    (reference util/tuner/tune_search_command.txt)."""
+    return [f"{base}-SASS-" + "-".join(c) for c in itertools.product(*SEARCH_SPACE)]
+
+
+def pick_best(sim_cycles: Dict[str, Dict[str, float]], hw_cycles: Dict[str, float]) -> Tuple[str, float]:
+    """sim_cycles[config][kernel] vs hw_cycles[kernel]: config with the lowest MAE (%)."""
+    best, best_err = "", float("inf")
+    for cfg, ks in sim_cycles.items():
+        errs = [abs(ks[k] - hw) / hw * 100 for k, hw in hw_cycles.items() if k in ks and hw > 0]
+        if not errs:
+            continue
+        e = sum(errs) / len(errs)
+        if e < best_err:
+            best, best_err = cfg, e
+    return best, best_err
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("-s", "--stats_output", action="append", default=[],
+                    help="ubench output file or directory of *.log (repeatable)")
+    ap.add_argument("-b", "--base", default="MI355X", help="preset used as the template")
+    ap.add_argument("-o", "--out", default="configs/tuned")
+    ap.add_argument("-n", "--name", default=None, help="config folder name (default: device name)")
+    ap.add_argument("--print-search", action="store_true", help="print the 16 search configs for run_simulations -C")
+    o = ap.parse_args(argv)
+    if o.print_search:
+        print(",".join(search_configs(o.name or o.base)))
+        return 0
+    if not o.stats_output:
+        ap.error("-s is required")
+    out, applied = tune(o.stats_output, o.base, o.out, o.name)
+    print(f"wrote {out}/gpgpusim.config and trace.config ({len(applied)} tuned options)")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

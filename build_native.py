@@ -82,7 +82,7 @@ def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
         "  command = g++ $in -o $out $ldflags $libs",
         "  description = LINK $out",
         "rule hipexe",
-        f"  command = {hipcc} $hipflags $in -o $out",
+        f"  command = {hipcc} $hipflags $in -o $out $libs",
         "  description = HIPEXE $out",
     ]
     objs = []
@@ -120,7 +120,20 @@ def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
             for fn in sorted(os.listdir(ub_dir)):
                 if fn.endswith(".hip"):
                     out = os.path.join(ROOT, "bin", "ubench", fn[:-4])
-                    lines.append(f"build {out}: hipexe {os.path.join(ub_dir, fn)}")
+                    src = os.path.join(ub_dir, fn)
+                    lines.append(f"build {out}: hipexe {src} | {os.path.join(ub_dir, 'ubench.h')}")
+                    first = open(src).readline()
+                    if first.startswith("// UB_LIBS:"):
+                        lines.append(f"  libs = {first.split(':', 1)[1].strip()}")
+                    defaults.append(out)
+        # HIP applications with asim_trace annotations (trace capture + HW timing)
+        app_dir = os.path.join(ROOT, "csrc", "apps")
+        if os.path.isdir(app_dir):
+            hdr = os.path.join(ROOT, "csrc", "tracer", "asim_trace.h")
+            for fn in sorted(os.listdir(app_dir)):
+                if fn.endswith(".hip"):
+                    out = os.path.join(ROOT, "bin", "apps", fn[:-4])
+                    lines.append(f"build {out}: hipexe {os.path.join(app_dir, fn)} | {hdr}")
                     defaults.append(out)
         tracer = os.path.join(ROOT, "csrc", "tracer", "asim_tracer.cc")
         if os.path.exists(tracer) and os.path.isdir(os.path.join(ROCM, "include", "rocprofiler-sdk")):

@@ -139,6 +139,19 @@ PYBIND11_MODULE(_asim, m) {
   m.attr("sizeof_TInst") = sizeof(TInst);
 
   m.def("gpu_available", &gpu_engine_available, "True if a HIP device is usable by the GPU engine");
+  // compile-time capacities of the cycle model (per SM / per memory sub-partition)
+  {
+    py::dict lim;
+    lim["max_warps"] = kMaxWarps;
+    lim["max_cta"] = kMaxCta;
+    lim["l1_lines"] = kMaxL1Lines;
+    lim["l1_mshr"] = kMaxL1Mshr;
+    lim["l2_lines"] = kMaxL2Lines;
+    lim["l2_mshr"] = kMaxL2Mshr;
+    lim["sm_total"] = kMaxSmTot;
+    lim["sub_total"] = kMaxSubTot;
+    m.attr("limits") = lim;
+  }
   m.def("gpu_cu_count", &gpu_cu_count, "compute units of the current HIP device");
   m.def("option_names", []() {
     OptionRegistry r;

@@ -1,0 +1,117 @@
+"""Tuner, correlator, hw_stats and plotting helpers (CPU)."""
+import csv
+import json
+import os
+
+import numpy as np
+import pytest
+
+from accel_sim_framework_distributed_amd.job_launching import common, get_stats
+from accel_sim_framework_distributed_amd.plotting import correlate, stats_plots
+from accel_sim_framework_distributed_amd.tuner import tuner
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+UBENCH = os.path.join(ROOT, "profiles", "ubench_mi355x")
+
+
+def test_tuner_from_measured_mi355x_logs(native, tmp_path):
+    opts, meas, dev = tuner.parse_stats([UBENCH])
+    assert dev == "AMD_Instinct_MI355X"
+    assert opts["-gpgpu_n_clusters"] == "256" and "-gpgpu_l1_latency" in opts
+    assert float(meas["hbm_read_gbps"]) > 1000
+    out, applied = tuner.tune([UBENCH], "MI355X", str(tmp_path))
+    cfg = native.parse_config(["-config", os.path.join(out, "gpgpusim.config"), "-config",
+                               os.path.join(out, "trace.config")])
+    assert cfg["n_sm"] == 256 and cfg["l1_latency"] == int(opts["-gpgpu_l1_latency"])
+    assert "TUNING.md" in os.listdir(out)
+
+
+def test_tuner_rejects_unknown_flags(tmp_path):
+    p = tmp_path / "x.log"
+    p.write_text("-not_a_real_flag 3\n")
+    with pytest.raises(ValueError):
+        tuner.tune([str(p)], "QV100", str(tmp_path))
+
+
+def test_tuner_search_space_resolves(native):
+    from accel_sim_framework_distributed_amd.models import presets
+    names = tuner.search_configs("QV100")
+    assert len(names) == 16
+    reg = common.Registry()
+    for n in names:
+        name, extra, base = reg.config(n)
+        assert os.path.exists(base)
+        for tok in n.split("-")[1:]:
+            assert f"#{tok}\n" in extra
+        args = list(presets.args_for("QV100"))
+        for line in extra.splitlines():
+            if line.startswith("-"):
+                k, v = line.split(None, 1)
+                args += [k, v]
+        native.parse_config(args)  # every combination is a valid configuration
+
+
+def _write_sim_csv(path, rows, cfg="MI355X"):
+    # rows: {app/args: [cycles per kernel]}
+    t = get_stats.StatTable()
+    t.stats = [r"gpu_sim_cycle\s*=\s*(.*)"]
+    for app, ks in rows.items():
+        for i, c in enumerate(ks):
+            t.set(app, f"k{i}--0", cfg, t.stats[0], str(c))
+    open(path, "w").write(get_stats.render_csv(t))
+
+
+def test_correlator_metrics_flat_hw(tmp_path):
+    sim = {"a/x": [100, 200], "b/y": [300], "c/z": [1000]}
+    hw_cycles = {"a/x": [110, 190], "b/y": [250], "c/z": [1000]}
+    _write_sim_csv(tmp_path / "s.csv", sim)
+    with open(tmp_path / "hw.csv", "w") as f:
+        f.write("app,args,kernel,instance,duration_ns\n")
+        for app, ks in hw_cycles.items():
+            a, g = app.split("/")
+            for i, c in enumerate(ks):
+                for rep in range(3):
+                    f.write(f"{a},{g},k{i},{i},{c * 1000 / 2000.0}\n")  # ns at 2000 MHz
+    hw = correlate.load_hw_flat(str(tmp_path / "hw.csv"))
+    res = correlate.correlate(str(tmp_path / "s.csv"), hw, 2000.0)
+    m = res["Cycles"]["configs"]["MI355X"]["app_metrics"]
+    # per app: a 300 vs 300 (0%), b 300 vs 250 (20%), c 0%  -> MAE 6.67%
+    assert m["n"] == 3 and m["mae"] == pytest.approx(20 / 3, rel=1e-6)
+    files = correlate.write_outputs(res, str(tmp_path / "out"))
+    summ = json.load(open([f for f in files if f.endswith(".json")][0]))
+    assert summ["Cycles"]["MI355X"]["app"]["n"] == 3
+    assert any(f.endswith(".html") and "<svg" in open(f).read() for f in files)
+
+
+def test_correlator_rocprof_loader(tmp_path):
+    d = tmp_path / "hw" / "vectoradd" / "NO_ARGS"
+    for r in range(3):
+        rd = d / f"run_{r}" / "host" / "123"
+        rd.mkdir(parents=True)
+        with open(rd / "run_kernel_trace.csv", "w") as f:
+            w = csv.writer(f)
+            w.writerow(["Kind", "Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+            w.writerow(["KERNEL_DISPATCH", 2, "void k2(int*)", 5000, 5000 + 800 + r])
+            w.writerow(["KERNEL_DISPATCH", 1, "void k1(int*) [clone .kd]", 1000, 1000 + 400 + r])
+    hw = correlate.load_hw_rocprof(str(tmp_path / "hw"), burn=1)
+    ks = hw["vectoradd/NO_ARGS"]
+    assert len(ks) == 2 and ks[0]["duration_ns"] == [401.0, 402.0] and ks[1]["name"] == ["void k2"]
+
+
+def test_run_hw_dry_run(capsys):
+    from accel_sim_framework_distributed_amd.hw_stats import run_hw
+    assert run_hw.main(["-B", "asim_hip_apps", "-R", "2", "-n", "-o", "/tmp/x"]) == 0
+    out = capsys.readouterr().out
+    assert out.count("rocprofv3 --kernel-trace") == 10 and "bin/apps/vectoradd 262144" in out
+
+
+def test_stats_merge_and_plot(tmp_path):
+    _write_sim_csv(tmp_path / "a.csv", {"a/x": [1, 2]}, "C1")
+    _write_sim_csv(tmp_path / "b.csv", {"a/x": [3, 4]}, "C2")
+    merged = stats_plots.merge([str(tmp_path / "a.csv"), str(tmp_path / "b.csv")])
+    blocks = get_stats.parse_csv_blocks(merged)
+    row = blocks[r"gpu_sim_cycle\s*=\s*(.*)"]["a/x--k0--0"]
+    assert row == {"C1": "1", "C2": "3"}
+    (tmp_path / "m.csv").write_text(merged)
+    files = stats_plots.plot(str(tmp_path / "m.csv"), str(tmp_path / "html"))
+    assert files and "<svg" in open(files[0]).read()

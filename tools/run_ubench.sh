@@ -1,0 +1,13 @@
+#!/bin/bash
+# Run the CDNA4 micro-benchmark suite (bin/ubench/*) on the current GPU and
+# keep each program's output under $1 (default gpurun_out/ubench); every
+# program runs under its own time limit and the script stops at the first
+# failure (GPU-box etiquette: no retries after a fault).
+set -o pipefail
+out=${1:-gpurun_out/ubench}
+mkdir -p "$out"
+for p in ub_config ub_cache_lat ub_alu ub_lds ub_mfma ub_atomic_kernel ub_mem_bw ub_power; do
+  echo "== $p"
+  timeout -k 10 240 ./bin/ubench/$p > "$out/$p.log" 2>&1 || { echo "$p failed rc=$?"; tail -5 "$out/$p.log"; exit 1; }
+  tail -3 "$out/$p.log"
+done
