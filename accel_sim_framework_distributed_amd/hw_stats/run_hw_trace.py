@@ -31,7 +31,7 @@ else:
 
 def to_binary(trace_dir: str) -> int:
     """Convert every kernel-N.traceg listed in kernelslist.g to .asimk."""
-    from .. import _native
+    from accel_sim_framework_distributed_amd import _native
     mod = _native.load()
     kl = os.path.join(trace_dir, "kernelslist.g")
     lines = open(kl).read().splitlines()

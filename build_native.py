@@ -138,7 +138,7 @@ def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
         tracer = os.path.join(ROOT, "csrc", "tracer", "asim_tracer.cc")
         if os.path.exists(tracer) and os.path.isdir(os.path.join(ROCM, "include", "rocprofiler-sdk")):
             t_o = os.path.join(bdir, "tracer.o")
-            lines.append(f"build {t_o}: cxx {tracer}")
+            lines.append(f"build {t_o}: hip {tracer}")
             t_so = os.path.join(ROOT, "bin", "libasim_tracer.so")
             lines.append(f"build {t_so}: link_so {t_o}")
             lines.append(f"  libs = -lrocprofiler-sdk -ldl")

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Full MI355X correlation pipeline on the GPU box:
+#  1. capture asim_trace traces + rocprofv3 timings (tools/gpu_trace_and_time.sh)
+#  2. simulate every trace with the tuned MI355X config (run_simulations via the
+#     local procman, CPU engine), wait with monitor_func_test
+#  3. get_stats (per kernel) + correlator -> cycle MAE vs hardware
+# Only the small outputs are kept (traces are archived if they fit).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+out=$R/gpurun_out/corr
+bash $R/tools/gpu_trace_and_time.sh || exit 1
+export PROCMAN_STATE=$out/procman.json ASIM_JOB_LOGDIR=$out/logs
+JL=$R/util/job_launching
+timeout -k 10 300 python $JL/run_simulations.py -B asim_hip_apps -C MI355X_TUNED -T $out/traces -N corr -l local \
+  -r $out/simrun -c 5 --threads 3 > $out/launch.log 2>&1 || { echo "launch failed"; tail $out/launch.log; exit 1; }
+timeout -k 10 2400 python $JL/monitor_func_test.py -N corr -r $out/simrun -S 10 -T 2300 -K -j procman \
+  > $out/monitor.log 2>&1; mrc=$?
+tail -25 $out/monitor.log
+python $JL/get_stats.py -N corr -r $out/simrun -k -K -I > $out/stats_per_kernel.csv
+python $JL/get_stats.py -N corr -r $out/simrun -I > $out/stats.csv
+python $R/util/plotting/plot-correlation.py -c $out/stats_per_kernel.csv -H $out/hw -B 1 --clock_mhz 2400 \
+  -p mi355x -o $out/correl | tee $out/correl.log
+# keep the simulator outputs, drop the trace links / copies
+find $out/simrun -name traces -type l -delete
+tar czf $out/traces.tgz -C $out traces && rm -rf $out/traces
+sz=$(du -m $out/traces.tgz | cut -f1)
+[ "$sz" -gt 40 ] && rm -f $out/traces.tgz && echo "traces archive too big ($sz MB), dropped"
+du -sh $out
+exit $mrc
