@@ -59,9 +59,14 @@ def _mean(v):
     return float(np.mean(v)) if len(v) else float("nan")
 
 
+def _median(v):
+    return float(np.median(v)) if len(v) else float("nan")
+
+
 CORREL_STATS: List[CorrelStat] = [
+    # median over runs: short kernels on a shared node have a heavy right tail
     CorrelStat("Cycles", r"gpu_sim_cycle\s*=\s*(.*)",
-               lambda hw, mhz: _mean(hw["duration_ns"]) * mhz / 1000.0, "cycles"),
+               lambda hw, mhz: _median(hw["duration_ns"]) * mhz / 1000.0, "cycles"),
     CorrelStat("Instructions (thread)", r"gpu_sim_insn\s*=\s*(.*)",
                lambda hw, mhz: _mean(hw["thread_insts"]) if "thread_insts" in hw else float("nan"), "insn"),
     CorrelStat("L2 read accesses", r"\s+L2_cache_stats_breakdown\[GLOBAL_ACC_R\]\[TOTAL_ACCESS\]\s*=\s*(.*)",
@@ -95,7 +100,11 @@ def load_hw_rocprof(hw_dir: str, burn: int = 0) -> Dict[str, List[Dict[str, List
                             t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
                         except (KeyError, ValueError):
                             continue
-                        rows.append((t0, t1, row.get("Kernel_Name", "")))
+                        name = row.get("Kernel_Name", "")
+                        # runtime-internal blits (hipMemcpy/hipMemset kernels) are not application kernels
+                        if "__amd_rocclr_" in name:
+                            continue
+                        rows.append((t0, t1, name))
             rows.sort()
             counters = _load_counters(r)
             for i, (t0, t1, name) in enumerate(rows):
@@ -203,8 +212,8 @@ def correlate(sim_csv: str, hw: Dict[str, List[Dict[str, List[float]]]], clock_m
                     continue
                 hv = [st.hw_eval(hk[i], clock_mhz) for i in range(n)]
                 sv = [svals[i] * st.sim_scale for i in range(n)]
-                # HW spread check (max-min over runs relative to mean) on cycles
-                spread = [np.ptp(hk[i]["duration_ns"]) / max(1e-9, np.mean(hk[i]["duration_ns"])) * 100
+                # HW variability check (coefficient of variation over runs, %)
+                spread = [np.std(hk[i]["duration_ns"]) / max(1e-9, np.mean(hk[i]["duration_ns"])) * 100
                           for i in range(n) if "duration_ns" in hk[i] and len(hk[i]["duration_ns"]) > 1]
                 noisy = bool(spread) and max(spread) > hw_err_tolerance
                 for i in range(n):

@@ -220,6 +220,7 @@ const OptDef kOptions[] = {
     {"-resume_CTA", 'i', "0", ""},
     {"-checkpoint_CTA_t", 'i', "0", ""},
     {"-checkpoint_insn_Y", 'i', "0", ""},
+    {"-checkpoint_path", 's', "checkpoint_files", "directory of timing-state checkpoints (extension)"},
     // ---- power (AccelWattch) ----
     {"-power_simulation_enabled", 'b', "0", "enable the power model"},
     {"-accelwattch_xml_file", 's', "accelwattch_sass_sim.xml", "power model XML"},
@@ -798,6 +799,11 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
     }
   }
   d.power_report_file = r.gets("-power_report_file");
+  d.checkpoint_option = (int32_t)r.geti("-checkpoint_option");
+  d.checkpoint_kernel = (int32_t)r.geti("-checkpoint_kernel");
+  d.resume_option = (int32_t)r.geti("-resume_option");
+  d.resume_kernel = (int32_t)r.geti("-resume_kernel");
+  d.checkpoint_dir = r.gets("-checkpoint_path");
   {
     auto v = split(strip_ws(r.gets("-gpgpu_runtime_stat")), ':');
     d.stat_sample_freq = v.empty() || v[0].empty() ? 500 : parse_u(v[0], "-gpgpu_runtime_stat");

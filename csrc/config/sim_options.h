@@ -72,6 +72,10 @@ struct DriverOpts {
   double steady_dev_pct = 8;
   uint32_t steady_samples = 4;
   std::string power_report_file;
+  // timing-state checkpoint / resume at kernel boundaries (trace mode)
+  int32_t checkpoint_option = 0, checkpoint_kernel = 1;
+  int32_t resume_option = 0, resume_kernel = 0;
+  std::string checkpoint_dir;
   uint64_t stat_sample_freq = 500;
   std::string engine;             // cpu | gpu
   bool trace_enabled = false;

@@ -80,9 +80,15 @@ double Simulator::wall_seconds() const {
 int Simulator::run() {
   print("Accel-Sim-AMD [MI355X-native trace-driven simulator, engine=%s]\n", eng_->name());
   cmds_ = parse_commandlist(dopt_.trace_file);
-  for (size_t i = 0; i < cmds_.size(); ++i) {
+  size_t first = 0;
+  if (dopt_.resume_option) first = resume_checkpoint();
+  for (size_t i = first; i < cmds_.size(); ++i) {
     run_command(i);
     if (deadlock_) break;
+    if (cmds_[i].type == CMD_KERNEL) {
+      ++kernels_done_;
+      if (dopt_.checkpoint_option && kernels_done_ == (uint32_t)dopt_.checkpoint_kernel) write_checkpoint(i);
+    }
     if (dopt_.max_cycle && (int64_t)tot_cycle_ >= dopt_.max_cycle) {
       print("GPGPU-Sim: ** break due to reaching the maximum cycles (or instructions) **\n");
       break;
@@ -96,6 +102,78 @@ int Simulator::run() {
   print("GPGPU-Sim: *** exit detected ***\n");
   fflush(stdout);
   return deadlock_ ? 1 : 0;
+}
+
+// Checkpoint file: magic, driver counters, previous stat snapshots, engine image.
+namespace {
+struct CkptHeader {
+  uint64_t magic = 0x41534d434b505431ull;  // "ASMCKPT1"
+  uint64_t cmd_index = 0, kernels_done = 0;
+  uint64_t tot_cycle = 0, tot_insn = 0, tot_warp_insn = 0, tot_cta = 0, next_uid = 0;
+  uint64_t n_sm_stats = 0, n_mem_stats = 0, engine_bytes = 0;
+};
+}  // namespace
+
+std::string Simulator::checkpoint_file(uint32_t kernel) const {
+  return dopt_.checkpoint_dir + "/asim_state_kernel" + std::to_string(kernel) + ".ckpt";
+}
+
+void Simulator::write_checkpoint(size_t cmd_index) {
+  std::vector<uint8_t> eng;
+  eng_->save_state(eng);
+  CkptHeader h;
+  h.cmd_index = cmd_index;
+  h.kernels_done = kernels_done_;
+  h.tot_cycle = tot_cycle_;
+  h.tot_insn = tot_insn_;
+  h.tot_warp_insn = tot_warp_insn_;
+  h.tot_cta = tot_cta_;
+  h.next_uid = next_uid_;
+  h.n_sm_stats = prev_sm_.size();
+  h.n_mem_stats = prev_mem_.size();
+  h.engine_bytes = eng.size();
+  std::string cmd = "mkdir -p '" + dopt_.checkpoint_dir + "'";
+  if (system(cmd.c_str()) != 0) throw std::runtime_error("cannot create " + dopt_.checkpoint_dir);
+  const std::string path = checkpoint_file(kernels_done_);
+  FILE* f = fopen(path.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot write checkpoint " + path);
+  bool ok = fwrite(&h, sizeof(h), 1, f) == 1;
+  ok = ok && (!h.n_sm_stats || fwrite(prev_sm_.data(), sizeof(SMStats), h.n_sm_stats, f) == h.n_sm_stats);
+  ok = ok && (!h.n_mem_stats || fwrite(prev_mem_.data(), sizeof(MemStats), h.n_mem_stats, f) == h.n_mem_stats);
+  ok = ok && fwrite(eng.data(), 1, eng.size(), f) == eng.size();
+  ok = fclose(f) == 0 && ok;
+  if (!ok) throw std::runtime_error("short write to checkpoint " + path);
+  print("GPGPU-Sim: checkpoint after kernel %u written to %s\n", kernels_done_, path.c_str());
+}
+
+size_t Simulator::resume_checkpoint() {
+  const std::string path = checkpoint_file((uint32_t)dopt_.resume_kernel);
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("cannot open checkpoint " + path);
+  CkptHeader h, want;
+  bool ok = fread(&h, sizeof(h), 1, f) == 1 && h.magic == want.magic;
+  if (!ok) {
+    fclose(f);
+    throw std::runtime_error("not a checkpoint file: " + path);
+  }
+  prev_sm_.resize(h.n_sm_stats);
+  prev_mem_.resize(h.n_mem_stats);
+  std::vector<uint8_t> eng(h.engine_bytes);
+  ok = (!h.n_sm_stats || fread(prev_sm_.data(), sizeof(SMStats), h.n_sm_stats, f) == h.n_sm_stats) &&
+       (!h.n_mem_stats || fread(prev_mem_.data(), sizeof(MemStats), h.n_mem_stats, f) == h.n_mem_stats) &&
+       fread(eng.data(), 1, eng.size(), f) == eng.size();
+  fclose(f);
+  if (!ok) throw std::runtime_error("truncated checkpoint " + path);
+  eng_->load_state(eng);
+  kernels_done_ = (uint32_t)h.kernels_done;
+  tot_cycle_ = h.tot_cycle;
+  tot_insn_ = h.tot_insn;
+  tot_warp_insn_ = h.tot_warp_insn;
+  tot_cta_ = h.tot_cta;
+  next_uid_ = (uint32_t)h.next_uid;
+  print("GPGPU-Sim: resumed from %s (kernel %u done, cycle %llu)\n", path.c_str(), kernels_done_,
+        (unsigned long long)tot_cycle_);
+  return (size_t)h.cmd_index + 1;
 }
 
 void Simulator::run_command(size_t idx) {

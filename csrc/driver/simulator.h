@@ -86,6 +86,11 @@ class Simulator {
   void do_collective(const Command& c);
   void print_kernel_stats(const KernelResult& r, const std::vector<SMStats>& sm, const std::vector<MemStats>& mem);
   void print_sim_time();
+  // timing-state checkpoint at a kernel boundary / resume from one (returns first command to run)
+  std::string checkpoint_file(uint32_t kernel) const;
+  void write_checkpoint(size_t cmd_index);
+  size_t resume_checkpoint();
+  uint32_t kernels_done_ = 0;
   // run the current kernel in gpu_stat_sample_freq slices, one power sample per slice
   RunResult run_sampled(uint64_t start, const RunLimits& lim, const std::string& kname);
 

@@ -57,6 +57,14 @@ void host_memcpy_fill(ChanState* chs, uint32_t nch, const SimCfg& c, uint64_t ad
   }
 }
 
+void check_state_header(const EngineStateHeader& h, const EngineStateHeader& w) {
+  if (h.magic != w.magic || h.version != w.version) throw std::runtime_error("engine state: not a state image");
+  if (h.n_sm != w.n_sm || h.n_mem != w.n_mem || h.sm_bytes != w.sm_bytes || h.ch_bytes != w.ch_bytes ||
+      h.pub_bytes != w.pub_bytes || h.box_req != w.box_req || h.cnt_req != w.cnt_req || h.box_rep != w.box_rep ||
+      h.cnt_rep != w.cnt_rep)
+    throw std::runtime_error("engine state: image was written for a different configuration or build");
+}
+
 void host_flush_l2(ChanState* chs, uint32_t nch, const SimCfg& c) {
   for (uint32_t i = 0; i < nch; ++i)
     for (uint32_t j = 0; j < c.n_sub_per_mem; ++j)
@@ -198,6 +206,58 @@ class CpuEngine : public Engine {
   void advance(uint64_t cycles) override {
     uint64_t E = c_.icnt_latency;
     cycle_ += (cycles + E - 1) / E * E;
+  }
+
+  EngineStateHeader header() const {
+    EngineStateHeader h;
+    h.n_sm = sms_.size();
+    h.n_mem = chs_.size();
+    h.sm_bytes = sizeof(SMState);
+    h.ch_bytes = sizeof(ChanState);
+    h.pub_bytes = sizeof(EpochPub);
+    h.box_req = box_req_[0].size();
+    h.cnt_req = cnt_req_[0].size();
+    h.box_rep = box_rep_[0].size();
+    h.cnt_rep = cnt_rep_[0].size();
+    h.cycle = cycle_;
+    h.epoch = epoch_;
+    h.ready = ready_;
+    return h;
+  }
+
+  void save_state(std::vector<uint8_t>& out) override {
+    out.clear();
+    StateOut o{out};
+    EngineStateHeader h = header();
+    o.put(&h, sizeof(h));
+    o.put(sms_.data(), sms_.size() * sizeof(SMState));
+    o.put(chs_.data(), chs_.size() * sizeof(ChanState));
+    o.put(pub_.get(), sizeof(EpochPub));
+    for (int p = 0; p < 2; ++p) {
+      o.put(box_req_[p].data(), box_req_[p].size() * sizeof(Pkt));
+      o.put(cnt_req_[p].data(), cnt_req_[p].size() * sizeof(uint32_t));
+      o.put(box_rep_[p].data(), box_rep_[p].size() * sizeof(Pkt));
+      o.put(cnt_rep_[p].data(), cnt_rep_[p].size() * sizeof(uint32_t));
+    }
+  }
+
+  void load_state(const std::vector<uint8_t>& in) override {
+    StateIn r{in};
+    EngineStateHeader h;
+    r.get(&h, sizeof(h));
+    check_state_header(h, header());
+    r.get(sms_.data(), sms_.size() * sizeof(SMState));
+    r.get(chs_.data(), chs_.size() * sizeof(ChanState));
+    r.get(pub_.get(), sizeof(EpochPub));
+    for (int p = 0; p < 2; ++p) {
+      r.get(box_req_[p].data(), box_req_[p].size() * sizeof(Pkt));
+      r.get(cnt_req_[p].data(), cnt_req_[p].size() * sizeof(uint32_t));
+      r.get(box_rep_[p].data(), box_rep_[p].size() * sizeof(Pkt));
+      r.get(cnt_rep_[p].data(), cnt_rep_[p].size() * sizeof(uint32_t));
+    }
+    cycle_ = h.cycle;
+    epoch_ = h.epoch;
+    ready_ = h.ready;
   }
 
  private:

@@ -3,7 +3,9 @@
 // MI355X engine (gpu_engine.hip, one wavefront per SM / memory channel,
 // persistent kernel with one grid barrier per PDES epoch).
 #pragma once
+#include <cstring>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -46,7 +48,45 @@ class Engine {
   virtual void restore(const std::vector<uint8_t>& in) = 0;
   // advance the clock without simulating (collective stalls, idle time)
   virtual void advance(uint64_t cycles) = 0;
+  // complete, engine-independent timing state (SM + channel states, epoch
+  // publication block, both mailbox parities, clocks): a checkpoint written
+  // by one engine resumes on the other (SURVEY §5.4 timing-state snapshot)
+  virtual void save_state(std::vector<uint8_t>& out) = 0;
+  virtual void load_state(const std::vector<uint8_t>& in) = 0;
 };
+
+// layout of save_state(): header, then SMState[n_sm], ChanState[n_mem],
+// EpochPub, and for parity 0/1: req packets, req counts, reply packets,
+// reply counts
+struct EngineStateHeader {
+  uint64_t magic = 0x41534d5354415445ull;  // "ASMSTATE"
+  uint64_t version = 1;
+  uint64_t n_sm = 0, n_mem = 0, sm_bytes = 0, ch_bytes = 0, pub_bytes = 0;
+  uint64_t box_req = 0, cnt_req = 0, box_rep = 0, cnt_rep = 0;  // element counts per parity
+  uint64_t cycle = 0, epoch = 0, ready = 0;
+};
+
+// helpers for the serialisation
+struct StateOut {
+  std::vector<uint8_t>& v;
+  void put(const void* p, size_t n) {
+    const size_t o = v.size();
+    v.resize(o + n);
+    if (n) memcpy(v.data() + o, p, n);
+  }
+};
+struct StateIn {
+  const std::vector<uint8_t>& v;
+  size_t off = 0;
+  const uint8_t* take(size_t n) {
+    if (off + n > v.size()) throw std::runtime_error("engine state: truncated image");
+    const uint8_t* p = v.data() + off;
+    off += n;
+    return p;
+  }
+  void get(void* dst, size_t n) { memcpy(dst, take(n), n); }
+};
+void check_state_header(const EngineStateHeader& h, const EngineStateHeader& want);
 
 std::unique_ptr<Engine> make_cpu_engine();
 // defined in the HIP engine module; returns nullptr when no GPU is usable

@@ -467,6 +467,66 @@ class GpuEngine : public Engine {
   }
   void set_epochs_per_launch(uint32_t n) { epochs_per_launch_ = n ? n : 4096; }
 
+  // same image layout as the CPU engine (engine.h EngineStateHeader), so a
+  // state saved here resumes on either engine
+  EngineStateHeader header() const {
+    EngineStateHeader h;
+    h.n_sm = c_.n_sm;
+    h.n_mem = c_.n_mem;
+    h.sm_bytes = sizeof(SMState);
+    h.ch_bytes = sizeof(ChanState);
+    h.pub_bytes = sizeof(EpochPub);
+    h.box_req = (uint64_t)c_.n_subpart * c_.n_sm * cap_req_;
+    h.cnt_req = (uint64_t)c_.n_subpart * c_.n_sm;
+    h.box_rep = (uint64_t)c_.n_sm * c_.n_subpart * cap_rep_;
+    h.cnt_rep = (uint64_t)c_.n_sm * c_.n_subpart;
+    h.cycle = cycle_;
+    h.epoch = epoch_;
+    h.ready = ready_;
+    return h;
+  }
+  void save_state(std::vector<uint8_t>& out) override {
+    const EngineStateHeader h = header();
+    out.assign(sizeof(h), 0);
+    memcpy(out.data(), &h, sizeof(h));
+    auto dl = [&](const void* d, size_t n) {
+      const size_t o = out.size();
+      out.resize(o + n);
+      if (n) HIPCHECK(hipMemcpy(out.data() + o, d, n, hipMemcpyDeviceToHost));
+    };
+    dl(d_sms_, sizeof(SMState) * c_.n_sm);
+    dl(d_chs_, sizeof(ChanState) * c_.n_mem);
+    dl(d_pub_, sizeof(EpochPub));
+    for (int p = 0; p < 2; ++p) {
+      dl(d_box_req_[p], h.box_req * sizeof(Pkt));
+      dl(d_cnt_req_[p], h.cnt_req * sizeof(uint32_t));
+      dl(d_box_rep_[p], h.box_rep * sizeof(Pkt));
+      dl(d_cnt_rep_[p], h.cnt_rep * sizeof(uint32_t));
+    }
+  }
+  void load_state(const std::vector<uint8_t>& in) override {
+    StateIn r{in};
+    EngineStateHeader h;
+    r.get(&h, sizeof(h));
+    const EngineStateHeader w = header();
+    check_state_header(h, w);
+    auto ul = [&](void* d, size_t n) {
+      if (n) HIPCHECK(hipMemcpy(d, r.take(n), n, hipMemcpyHostToDevice));
+    };
+    ul(d_sms_, sizeof(SMState) * c_.n_sm);
+    ul(d_chs_, sizeof(ChanState) * c_.n_mem);
+    ul(d_pub_, sizeof(EpochPub));
+    for (int p = 0; p < 2; ++p) {
+      ul(d_box_req_[p], w.box_req * sizeof(Pkt));
+      ul(d_cnt_req_[p], w.cnt_req * sizeof(uint32_t));
+      ul(d_box_rep_[p], w.box_rep * sizeof(Pkt));
+      ul(d_cnt_rep_[p], w.cnt_rep * sizeof(uint32_t));
+    }
+    cycle_ = h.cycle;
+    epoch_ = h.epoch;
+    ready_ = h.ready;
+  }
+
  private:
   void upload(void*& d, size_t& cap, const void* h, size_t bytes) {
     if (bytes > cap) {

@@ -73,8 +73,13 @@ int main() {
   const double b = (n * sxy - sx * sy) / (n * sxx - sx * sx), a = (sy - b * sx) / n;
   const double mhz = ub_shader_mhz();
   printf("# launch_us %.3f  per_block_us %.5f  shader_mhz %.0f\n", a, b, mhz);
-  ub_opt("-gpgpu_kernel_launch_latency", (long long)std::max(0.0, a * mhz + 0.5));
-  ub_opt("-gpgpu_TB_launch_latency", (long long)std::max(0.0, b * mhz * cus + 0.5));
+  // launch overhead between back-to-back kernels is host/CP time that a
+  // kernel's own (rocprofv3 start..end) duration does not contain: it is
+  // reported, while the simulated kernel starts issuing at once; the
+  // per-workgroup slope is the dispatcher cost per CTA
+  printf("# kernel_launch_overhead_cycles %.0f\n", a * mhz);
+  ub_opt("-gpgpu_kernel_launch_latency", 0);
+  ub_opt("-gpgpu_TB_launch_latency", (long long)std::max(0.0, b * mhz + 0.5));
   UB_CHECK(hipFree(p));
   UB_CHECK(hipFree(o));
   return 0;
