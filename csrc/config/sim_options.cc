@@ -678,6 +678,8 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.busW = (uint32_t)r.getu("-gpgpu_dram_buswidth");
   c.data_cmd_ratio = std::max<uint32_t>(1, (uint32_t)r.getu("-dram_data_command_freq_ratio"));
   c.dual_bus = (uint32_t)r.getu("-dram_dual_bus_interface");
+  c.perfect_mem = r.getb("-gpgpu_perfect_mem") ? 1u : 0u;
+  c.simple_dram = r.getb("-gpgpu_simple_dram_model") ? 1u : 0u;
   c.bk_index_policy = (uint32_t)r.getu("-dram_bnk_indexing_policy");
   c.bkgrp_index_policy = (uint32_t)r.getu("-dram_bnkgrp_indexing_policy");
   c.atom_size = c.BL * c.busW * (uint32_t)r.getu("-gpgpu_n_mem_per_ctrlr");

@@ -146,6 +146,10 @@ struct SimCfg {
   // ---- misc ----
   uint32_t deadlock_window;
   uint32_t max_cycle_lo, max_cycle_hi;
+  // ---- idealisations (reference -gpgpu_perfect_mem, perfect_memory_interface
+  //      shader.h:2681; -gpgpu_simple_dram_model, l2cache.cc:235-303) ----
+  uint32_t perfect_mem;     // every global/local access hits with L1 latency, no traffic
+  uint32_t simple_dram;     // DRAM = latency pipe + one column per DRAM cycle, no bank timing
 };
 
 // ---- helpers shared by both engines ----

@@ -509,6 +509,30 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
   st.dram_q_occ += ch.q_n;
   if (ch.q_n == 0) return;
   const uint32_t burst = amax<uint32_t>(1, c.BL / (c.data_cmd_ratio ? c.data_cmd_ratio : 1));
+  if (c.simple_dram) {
+    // oldest request, one column access per DRAM cycle, no bank state
+    int o = P::argmin(kDramQ, [&](int i) -> uint64_t { return ch.q_valid[i] ? ch.q_age[i] : ~0ull; });
+    if (o < 0 || t < ch.t_ccd_ok) return;
+    const DramReq r = ch.q[o];
+    if (!r.write) {
+      if (ch.ret_n >= (uint32_t)kDramRet) return;
+      DramRet& d = ch.ret[(ch.ret_head + ch.ret_n) % kDramRet];
+      d.line = r.line;
+      d.sector = r.sector;
+      d.sub = r.sub;
+      d.ready = (t + burst) * c.per_dram;
+      ch.ret_n++;
+      st.dram_rd++;
+    } else {
+      st.dram_wr++;
+    }
+    ch.t_ccd_ok = t + burst;
+    st.dram_busy_cycles += burst;
+    ch.q_valid[o] = 0;
+    ch.q_n--;
+    ch.sp[r.sub].n_l2dram--;
+    return;
+  }
   // banks that have a queued row hit
   uint64_t hitmask = P::vor(kDramQ, [&](int i) -> uint64_t {
     if (!ch.q_valid[i]) return 0;
@@ -518,12 +542,12 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
   });
   // ---- column command ----
   bool col = false;
+  uint64_t oldest_age = ~0ull;
+  if (c.dram_sched == 0) {  // FIFO: only the oldest request may issue (column and row commands)
+    int o = P::argmin(kDramQ, [&](int i) -> uint64_t { return ch.q_valid[i] ? ch.q_age[i] : ~0ull; });
+    oldest_age = o >= 0 ? ch.q_age[o] : ~0ull;
+  }
   {
-    uint64_t oldest_age = ~0ull;
-    if (c.dram_sched == 0) {  // FIFO: only the oldest request may issue
-      int o = P::argmin(kDramQ, [&](int i) -> uint64_t { return ch.q_valid[i] ? ch.q_age[i] : ~0ull; });
-      oldest_age = o >= 0 ? ch.q_age[o] : ~0ull;
-    }
     int pick = P::argmin(kDramQ, [&](int i) -> uint64_t {
       if (!ch.q_valid[i]) return ~0ull;
       if (c.dram_sched == 0 && ch.q_age[i] != oldest_age) return ~0ull;
@@ -566,11 +590,14 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
   if (col && !c.dual_bus) return;
   int act = P::argmin(kDramQ, [&](int i) -> uint64_t {
     if (!ch.q_valid[i]) return ~0ull;
+    if (c.dram_sched == 0 && ch.q_age[i] != oldest_age) return ~0ull;
     const DramReq& r = ch.q[i];
     const DramBank& b = ch.bk[r.bank];
     if (b.open) {
-      // precharge a row only when no queued request still hits it
-      if (b.row == r.row || (hitmask >> r.bank & 1ull) || t < b.t_pre_ok) return ~0ull;
+      // FR-FCFS: precharge a row only when no queued request still hits it
+      // (FIFO serves strictly in order, so the oldest request's row wins)
+      if (b.row == r.row || t < b.t_pre_ok) return ~0ull;
+      if (c.dram_sched != 0 && (hitmask >> r.bank & 1ull)) return ~0ull;
       return ch.q_age[i];
     }
     if (t < b.t_act_ok || t < ch.t_rrd_ok) return ~0ull;

@@ -502,7 +502,13 @@ SIM_HDI void sm_ldst(SMState& s, const SmCtx& x, uint64_t now) {
     const TAcc a = x.acc[in.mem + u.next];
     uint32_t bbit = 1u << (a.bank & 31);
     if (banks_used & bbit) break;  // L1 bank conflict: next cycle
-    if (is_store) {
+    if (c.perfect_mem) {
+      // ideal memory: loads/atomics return after the L1 latency, stores retire at once
+      if (!is_store) {
+        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, u.slot, 0)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+      }
+      s.st.l1[stype][L1O_HIT]++;
+    } else if (is_store) {
       if (!sm_can_send(s, c)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
       sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
       s.w_stores[w]++;
