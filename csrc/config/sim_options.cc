@@ -269,6 +269,7 @@ const OptDef kOptions[] = {
     {"-xgmi_link_bandwidth_gbps", 'f', "153.0", "per-link xGMI bandwidth (GB/s)"},
     {"-xgmi_link_latency_ns", 'f', "1000.0", "collective step latency (ns)"},
     {"-xgmi_links_per_gpu", 'u', "7", "xGMI links per GPU"},
+    {"-sim_event_skip", 'b', "1", "fast-forward quiet SM cycles inside an epoch (results identical)"},
     {"-collective_slice_bytes", 'u', "131072", "packet model: bytes per link packet (RCCL slice)"},
     {"-collective_max_channels", 'u', "16", "packet model: max parallel rings (channels)"},
     {"-collective_reduce_gbps", 'f', "900.0", "packet model: local memory bandwidth for reduce/copy (GB/s)"},
@@ -680,6 +681,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.dual_bus = (uint32_t)r.getu("-dram_dual_bus_interface");
   c.perfect_mem = r.getb("-gpgpu_perfect_mem") ? 1u : 0u;
   c.simple_dram = r.getb("-gpgpu_simple_dram_model") ? 1u : 0u;
+  c.event_skip = r.getb("-sim_event_skip") ? 1u : 0u;
   c.bk_index_policy = (uint32_t)r.getu("-dram_bnk_indexing_policy");
   c.bkgrp_index_policy = (uint32_t)r.getu("-dram_bnkgrp_indexing_policy");
   c.atom_size = c.BL * c.busW * (uint32_t)r.getu("-gpgpu_n_mem_per_ctrlr");

@@ -150,6 +150,7 @@ struct SimCfg {
   //      shader.h:2681; -gpgpu_simple_dram_model, l2cache.cc:235-303) ----
   uint32_t perfect_mem;     // every global/local access hits with L1 latency, no traffic
   uint32_t simple_dram;     // DRAM = latency pipe + one column per DRAM cycle, no bank timing
+  uint32_t event_skip;      // fast-forward provably quiet SM cycles inside an epoch (exact)
 };
 
 // ---- helpers shared by both engines ----

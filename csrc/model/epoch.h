@@ -110,7 +110,18 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& 
   P::prof(15);
   s.epoch_end = t1;
   if (s.n_cta_active || !sm_idle(s)) {
-    for (uint64_t t = t0; t < t1; ++t) sm_cycle<P>(s, x, t);
+    for (uint64_t t = t0; t < t1;) {
+      sm_cycle<P>(s, x, t);
+      ++t;
+      if (t < t1 && c.event_skip) {
+        // fast-forward cycles in which provably nothing happens
+        const uint64_t nx = sm_quiet_until<P>(s, c, t, t1);
+        if (nx > t) {
+          sm_skip<P>(s, c, nx - t);
+          t = nx;
+        }
+      }
+    }
   }
   s.cycle = t1;
   P::prof(16);

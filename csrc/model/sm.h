@@ -201,6 +201,11 @@ struct alignas(16) SMState {
   uint32_t oc_mask;       // occupied operand collectors
   uint32_t oc_read_mask;  // collectors still reading operands
   uint32_t l1_stamp;
+  // occupancy bitmaps of the time-indexed rings (bit = slot holds entries):
+  // the next completion time is a find-first-set instead of a ring scan
+  uint64_t wb_occ[kWbRing / 64];
+  uint64_t hit_occ[kHitRing / 64];
+  uint64_t skipped_cycles;  // quiet cycles fast-forwarded inside epochs (diagnostic)
   // ---- interconnect endpoints ----
   Pkt outq[kOutQ];
   uint32_t outq_head, outq_n;
@@ -322,6 +327,7 @@ SIM_HDI void sm_writeback(SMState& s, const SimCfg& c, uint64_t now) {
   }
   if (n) s.last_progress = now;
   s.wb_cnt[slot] = 0;
+  s.wb_occ[slot >> 6] &= ~(1ull << (slot & 63));
 }
 
 SIM_HDI void sm_load_slot_done(SMState& s, uint32_t w, uint32_t slot, uint64_t now) {
@@ -349,11 +355,13 @@ SIM_HDI void sm_hit_complete(SMState& s, uint64_t now) {
     }
   }
   s.hit_cnt[slot] = 0;
+  s.hit_occ[slot >> 6] &= ~(1ull << (slot & 63));
 }
 
 SIM_HDI bool hit_push(SMState& s, uint64_t when, uint8_t warp, uint8_t slot, uint8_t kind) {
   uint32_t r = (uint32_t)(when % kHitRing);
   if (s.hit_cnt[r] >= kHitSlot) return false;
+  s.hit_occ[r >> 6] |= 1ull << (r & 63);
   HitEnt& e = s.hit[r][s.hit_cnt[r]++];
   e.warp = warp;
   e.slot = slot;
@@ -676,6 +684,7 @@ SIM_HDI void sm_dispatch(SMState& s, const SimCfg& c, uint64_t now) {
     uint32_t slot = (uint32_t)((now + lat) % kWbRing);
     if (s.wb_cnt[slot] >= wbw) { s.st.pipe_stall++; continue; }  // result bus busy
     WbEnt& e = s.wb[slot][s.wb_cnt[slot]++];
+    s.wb_occ[slot >> 6] |= 1ull << (slot & 63);
     e.warp = o.warp;
     e.dst0 = o.inst.dst[0];
     e.dst1 = o.inst.dst[1];
@@ -746,6 +755,26 @@ SIM_HDI void sm_barrier_check(SMState& s, uint32_t cta, const KernelDesc& k) {
   }
 }
 
+// can warp `w` issue its next instruction this cycle (scoreboard, flags,
+// pipeline register and load slot availability)
+SIM_HDI bool warp_can_issue(const SMState& s, const SimCfg& c, int w, uint32_t nsched, uint64_t idoc_busy) {
+  uint8_t f = s.w_flags[w];
+  if (!(f & WF_ACTIVE) || (f & (WF_EXITING | WF_BARRIER | WF_MEMBAR | WF_WAITCNT))) return false;
+  if (s.w_ibuf[w] == 0) return false;
+  const TInst& in = s.w_win[w][s.w_head[w] % kWin];
+  const uint64_t* sb = s.w_sb[w];
+  for (int j = 0; j < 5; ++j)
+    if (sb_test(sb, in.src[j])) return false;
+  if (sb_test(sb, in.dst[0]) || sb_test(sb, in.dst[1])) return false;
+  uint32_t u = unit_of(c, in.cls);
+  uint32_t sc = (uint32_t)w % nsched;
+  if (in.cls == OC_EXIT || in.cls == OC_BARRIER || in.cls == OC_MEMBAR || in.cls == OC_NOP || (in.flags & F_WAITCNT))
+    return true;  // handled at issue, no pipeline register needed
+  if (idoc_busy >> (sc * U_COUNT + u) & 1ull) return false;
+  if (u == U_MEM && in.cls == OC_LOAD && s.w_slot_used[w] == 0xff) return false;
+  return true;
+}
+
 template <class P>
 SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
@@ -754,24 +783,7 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
   const uint64_t idoc_busy = s.idoc_mask;
   // readiness of every warp (lane-parallel)
-  uint64_t ready = P::ballot(nw, [&](int w) -> bool {
-    uint8_t f = s.w_flags[w];
-    if (!(f & WF_ACTIVE) || (f & (WF_EXITING | WF_BARRIER | WF_MEMBAR | WF_WAITCNT))) return false;
-    if (s.w_ibuf[w] == 0) return false;
-    const TInst& in = s.w_win[w][s.w_head[w] % kWin];
-    const uint64_t* sb = s.w_sb[w];
-    for (int j = 0; j < 5; ++j)
-      if (sb_test(sb, in.src[j])) return false;
-    if (sb_test(sb, in.dst[0]) || sb_test(sb, in.dst[1])) return false;
-    uint32_t u = unit_of(c, in.cls);
-    uint32_t sc = (uint32_t)w % nsched;
-    if (in.cls == OC_EXIT || in.cls == OC_BARRIER || in.cls == OC_MEMBAR || in.cls == OC_NOP ||
-        (in.flags & F_WAITCNT))
-      return true;  // handled at issue, no pipeline register needed
-    if (idoc_busy >> (sc * U_COUNT + u) & 1ull) return false;
-    if (u == U_MEM && in.cls == OC_LOAD && s.w_slot_used[w] == 0xff) return false;
-    return true;
-  });
+  uint64_t ready = P::ballot(nw, [&](int w) -> bool { return warp_can_issue(s, c, w, nsched, idoc_busy); });
   uint64_t live = P::ballot(nw, [&](int w) { return (s.w_flags[w] & WF_ACTIVE) != 0; });
   bool issued_any = false;
   for (uint32_t sc = 0; sc < nsched; ++sc) {
@@ -1036,6 +1048,76 @@ SIM_HDI void sm_cycle(SMState& s, const SmCtx& x, uint64_t now) {
 // true if the SM holds no work at all (no CTAs, nothing in flight)
 SIM_HDI bool sm_idle(const SMState& s) {
   return s.n_cta_active == 0 && s.outq_n == 0 && s.outstanding == 0 && !s.ldst.busy;
+}
+
+// first cycle in [from, limit) whose slot of a time-indexed ring is occupied
+SIM_HDI uint64_t ring_next(const uint64_t* occ, uint32_t ring, uint64_t from, uint64_t limit) {
+  const uint32_t nwords = ring / 64;
+  const uint32_t start = (uint32_t)(from % ring);
+  const uint32_t w0 = start >> 6, b0 = start & 63;
+  uint64_t m = occ[w0] >> b0;
+  if (m) return amin<uint64_t>(limit, from + (uint64_t)ffs64(m));
+  uint64_t d = 64 - b0;
+  for (uint32_t j = 1; j <= nwords && from + d < limit; ++j, d += 64) {
+    const uint64_t v = occ[(w0 + j) % nwords];
+    if (v) return amin<uint64_t>(limit, from + d + (uint64_t)ffs64(v));
+  }
+  return limit;
+}
+
+// Exact quiescence test before simulating cycle `t`: if no stage of
+// sm_cycle can change state until some later cycle, return that cycle
+// (capped at `limit`); otherwise return `t`.  Quiet cycles only add the
+// per-cycle statistics (sm_skip).  This is what makes latency-bound phases
+// (every warp waiting on memory) cost one check instead of one cycle each.
+template <class P>
+SIM_HDI uint64_t sm_quiet_until(const SMState& s, const SimCfg& c, uint64_t t, uint64_t limit) {
+  if (s.ldst.busy || s.idoc_mask || s.oc_mask || s.oc_read_mask || s.outq_n) return t;
+  uint64_t nx = ring_next(s.wb_occ, kWbRing, t, limit);
+  if (nx == t) return t;
+  nx = ring_next(s.hit_occ, kHitRing, t, nx);
+  if (nx == t) return t;
+  if (s.inq_n) {
+    const uint64_t at = (s.inq[s.inq_head].t + c.per_core - 1) / c.per_core;
+    if (at <= t) return t;
+    nx = amin<uint64_t>(nx, at);
+  }
+  const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
+  const uint32_t nsched = c.n_sched ? c.n_sched : 1;
+  const uint64_t act = P::ballot(nw, [&](int w) -> bool {
+    const uint8_t f = s.w_flags[w];
+    if (!(f & WF_ACTIVE)) return false;
+    if (!(f & WF_EXITING) && s.w_ibuf[w] == 0 && s.w_next[w] < s.w_end[w]) return true;  // fetch
+    const bool drained = s.w_head[w] >= s.w_end[w] && s.w_ibuf[w] == 0;
+    if (drained && s.w_inflight[w] == 0 && s.w_stores[w] == 0 && s.w_loads[w] == 0) return true;  // retire
+    if ((f & WF_MEMBAR) && s.w_stores[w] == 0) return true;
+    if ((f & WF_WAITCNT) && s.w_stores[w] == 0 && s.w_loads[w] == 0) return true;
+    return warp_can_issue(s, c, w, nsched, s.idoc_mask);  // issue
+  });
+  return act ? t : nx;
+}
+
+// account `k` quiet cycles: exactly what k idle sm_cycle calls would add
+template <class P>
+SIM_HDI void sm_skip(SMState& s, const SimCfg& c, uint64_t k) {
+  const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
+  const uint32_t nsched = c.n_sched ? c.n_sched : 1;
+  const uint64_t live = P::ballot(nw, [&](int w) { return (s.w_flags[w] & WF_ACTIVE) != 0; });
+  uint32_t stalled = 0;
+  for (uint32_t sc = 0; sc < nsched; ++sc) {
+    uint64_t mine = 0;
+    for (int w = (int)sc; w < nw; w += (int)nsched) mine |= 1ull << w;
+    if (live & mine) ++stalled;
+  }
+  P::one([&] {
+    s.st.issue_stall_idle += (uint64_t)stalled * k;
+    if (s.n_cta_active) {
+      s.st.active_cycles += k;
+      s.st.occupancy_acc += (uint64_t)popc64(live) * k;
+    }
+    s.skipped_cycles += k;
+  });
+  P::sync();
 }
 
 }  // namespace asim
