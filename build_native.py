@@ -135,6 +135,19 @@ def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
                     out = os.path.join(ROOT, "bin", "apps", fn[:-4])
                     lines.append(f"build {out}: hipexe {os.path.join(app_dir, fn)} | {hdr}")
                     defaults.append(out)
+        # examples/<name>/main.hip -> bin/examples/<name>
+        ex_dir = os.path.join(ROOT, "examples")
+        if os.path.isdir(ex_dir):
+            hdr = os.path.join(ROOT, "csrc", "tracer", "asim_trace.h")
+            for name in sorted(os.listdir(ex_dir)):
+                src = os.path.join(ex_dir, name, "main.hip")
+                if os.path.exists(src):
+                    out = os.path.join(ROOT, "bin", "examples", name)
+                    lines.append(f"build {out}: hipexe {src} | {hdr}")
+                    first = open(src).readline()
+                    if first.startswith("// UB_LIBS:"):
+                        lines.append(f"  libs = {first.split(':', 1)[1].strip()}")
+                    defaults.append(out)
         tracer = os.path.join(ROOT, "csrc", "tracer", "asim_tracer.cc")
         if os.path.exists(tracer) and os.path.isdir(os.path.join(ROCM, "include", "rocprofiler-sdk")):
             t_o = os.path.join(bdir, "tracer.o")

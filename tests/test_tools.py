@@ -115,3 +115,27 @@ def test_stats_merge_and_plot(tmp_path):
     (tmp_path / "m.csv").write_text(merged)
     files = stats_plots.plot(str(tmp_path / "m.csv"), str(tmp_path / "html"))
     assert files and "<svg" in open(files[0]).read()
+
+
+def test_trace_tools_cli(native, tmp_path, capsys):
+    from accel_sim_framework_distributed_amd.tracegen import cli
+    assert cli.main(["generate", "-o", str(tmp_path), "-a", "bfs-rodinia-2.0-ft"]) == 0
+    kl = [os.path.join(r, f) for r, _, fs in os.walk(tmp_path) for f in fs if f == "kernelslist.g"][0]
+    d = os.path.dirname(kl)
+    assert cli.main(["info", d]) == 0
+    assert cli.main(["occupancy", d]) == 0
+    out = capsys.readouterr().out
+    assert "CTAs/SM, limited by" in out and "#thread insts" in out
+    bbv_path = str(tmp_path / "bbv.json")
+    assert cli.main(["bbv", d, "-o", bbv_path]) == 0
+    bbv = json.load(open(bbv_path))
+    assert len(bbv) >= 2 and all(sum(v.values()) > 0 for v in bbv.values())
+    # every thread instruction lands in exactly one basic block
+    info = {os.path.basename(p): native.kernel_info(p)["thread_insts"] for p in cli.kernel_files(d)}
+    for k, v in bbv.items():
+        assert sum(v.values()) == info[k]
+    before = {k: native.kernel_info(p)["warp_insts"] for k, p in zip(info, cli.kernel_files(d))}
+    assert cli.main(["convert", d, "--to", "text"]) == 0
+    assert cli.main(["convert", d, "--to", "binary"]) == 0
+    after = {os.path.basename(p): native.kernel_info(p)["warp_insts"] for p in cli.kernel_files(d)}
+    assert before == after

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Entry point at the reference's path (util/.../run_hw_trace.py); implementation in
-accel_sim_framework_distributed_amd.hw_stats.run_hw_trace."""
+"""Entry point at the reference's path (util/tracer_nvbit/run_hw_trace.py);
+implementation in accel_sim_framework_distributed_amd.hw_stats.run_hw_trace."""
 import os
 import sys
 
