@@ -803,6 +803,10 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
     }
   }
   d.power_report_file = r.gets("-power_report_file");
+  d.memlatency_stat = (int32_t)r.geti("-gpgpu_memlatency_stat");
+  d.visualizer = r.getb("-visualizer_enabled");
+  d.visualizer_file = r.gets("-visualizer_outputfile");
+  if (d.visualizer_file.empty()) d.visualizer_file = "gpgpusim_visualizer.log";
   d.checkpoint_option = (int32_t)r.geti("-checkpoint_option");
   d.checkpoint_kernel = (int32_t)r.geti("-checkpoint_kernel");
   d.resume_option = (int32_t)r.geti("-resume_option");

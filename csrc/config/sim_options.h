@@ -72,6 +72,9 @@ struct DriverOpts {
   double steady_dev_pct = 8;
   uint32_t steady_samples = 4;
   std::string power_report_file;
+  int32_t memlatency_stat = 0;     // -gpgpu_memlatency_stat: print memory latency statistics
+  bool visualizer = false;         // -visualizer_enabled: per-sample activity log
+  std::string visualizer_file;
   // timing-state checkpoint / resume at kernel boundaries (trace mode)
   int32_t checkpoint_option = 0, checkpoint_kernel = 1;
   int32_t resume_option = 0, resume_kernel = 0;

@@ -45,6 +45,7 @@ Simulator::Simulator(const std::vector<std::string>& args) {
     std::string err;
     if (!power_->load_xml(dopt_.power_xml, &err)) throw std::runtime_error("power model: " + err);
     power_report_.reset(new std::ofstream(dopt_.power_report_file));
+    if (!*power_report_) throw std::runtime_error("cannot write " + dopt_.power_report_file);
     if (dopt_.power_trace) {
       power_trace_.reset(new std::ofstream("accelwattch_power_trace.csv"));
       ptrack_.write_trace_header(*power_trace_);
@@ -54,6 +55,10 @@ Simulator::Simulator(const std::vector<std::string>& args) {
       *power_steady_ << "kernel,start_cycle,end_cycle,samples,avg_power\n";
       ptrack_.set_steady(dopt_.steady_dev_pct, dopt_.steady_samples);
     }
+  }
+  if (dopt_.visualizer) {
+    visualizer_.reset(new std::ofstream(dopt_.visualizer_file));
+    if (!*visualizer_) throw std::runtime_error("cannot write " + dopt_.visualizer_file);
   }
 }
 
@@ -316,9 +321,10 @@ void Simulator::do_kernel(const Command& c) {
   if (dopt_.max_cycle) lim.max_cycle = (uint64_t)dopt_.max_cycle;
   auto ts = std::chrono::steady_clock::now();
   RunResult rr;
-  if (power_) {
+  if (power_ || visualizer_) {
     ptrack_.begin_kernel();
     rr = run_sampled(start, lim, rk.h.name);
+    if (visualizer_) visualizer_->flush();
   } else {
     rr = eng_->run_kernel(start, dopt_.flush_l1, lim);
   }
@@ -389,7 +395,7 @@ void Simulator::do_kernel(const Command& c) {
 
 RunResult Simulator::run_sampled(uint64_t start, const RunLimits& lim0, const std::string& kname) {
   // HW / HYBRID modes take one sample per kernel (the hardware counters are per kernel)
-  const bool hw = dopt_.power_mode == 1 || dopt_.power_mode == 2;
+  const bool hw = power_ && (dopt_.power_mode == 1 || dopt_.power_mode == 2);
   const uint64_t freq = std::max<uint64_t>(dopt_.stat_sample_freq, std::max<uint32_t>(1, cfg_.icnt_latency));
   const double mhz = 1e9 / (double)cfg_.per_core;
   Activity hwa;
@@ -423,15 +429,18 @@ RunResult Simulator::run_sampled(uint64_t start, const RunLimits& lim0, const st
     eng_->stats(sm1, m1);
     stat_delta(sm1, sm0, dsm);
     stat_delta(m1, m0, dm);
-    Activity a = PowerModel::activity_from_stats(dsm, dm, now > t_prev ? now - t_prev : 1);
-    if (hw && have_hw) {
-      bool use_sim[HW_COUNT];
-      for (int i = 0; i < HW_COUNT; ++i) use_sim[i] = dopt_.power_mode == 2 && dopt_.hybrid_use_sim[i];
-      a = PowerModel::merge_hw(a, hwa, use_sim);
+    if (power_) {
+      Activity a = PowerModel::activity_from_stats(dsm, dm, now > t_prev ? now - t_prev : 1);
+      if (hw && have_hw) {
+        bool use_sim[HW_COUNT];
+        for (int i = 0; i < HW_COUNT; ++i) use_sim[i] = dopt_.power_mode == 2 && dopt_.hybrid_use_sim[i];
+        a = PowerModel::merge_hw(a, hwa, use_sim);
+      }
+      PowerReport p = power_->compute(a, mhz, cfg_.n_sm);
+      ptrack_.add_sample(p, a, now);
+      if (power_trace_) ptrack_.write_trace_line(*power_trace_, p, now);
     }
-    PowerReport p = power_->compute(a, mhz, cfg_.n_sm);
-    ptrack_.add_sample(p, a, now);
-    if (power_trace_) ptrack_.write_trace_line(*power_trace_, p, now);
+    if (visualizer_) write_visualizer_sample(kname, now, now > t_prev ? now - t_prev : 1, dsm, dm);
     sm0.swap(sm1);
     m0.swap(m1);
     t_prev = now;
@@ -443,6 +452,38 @@ RunResult Simulator::run_sampled(uint64_t start, const RunLimits& lim0, const st
     if (r.epochs == 0) throw std::runtime_error("power sampling: engine made no progress");
   }
   return tot;
+}
+
+// One line per sample period (reference visualizer_printstat, visualizer.cc:56-84,
+// whose gz log feeds AerialVision): global counters plus per-SM instruction
+// counts, so activity over time can be plotted per core.
+void Simulator::write_visualizer_sample(const std::string& kname, uint64_t now, uint64_t cycles,
+                                        const std::vector<SMStats>& dsm, const std::vector<MemStats>& dm) {
+  uint64_t insn = 0, l1_acc = 0, l1_miss = 0, l2_acc = 0, l2_miss = 0, drd = 0, dwr = 0, busy = 0, dcyc = 0;
+  for (auto& s : dsm) {
+    insn += s.thread_insn;
+    for (int t = 0; t < L1T_COUNT; ++t) {
+      for (int o = 0; o < L1O_COUNT; ++o) l1_acc += s.l1[t][o];
+      l1_miss += s.l1[t][L1O_MISS];
+    }
+  }
+  for (auto& m : dm) {
+    for (int t = 0; t < L2T_COUNT; ++t) {
+      l2_acc += m.l2[t][L2O_HIT] + m.l2[t][L2O_MISS] + m.l2[t][L2O_MSHR_HIT];
+      l2_miss += m.l2[t][L2O_MISS];
+    }
+    drd += m.dram_rd;
+    dwr += m.dram_wr;
+    busy += m.dram_busy_cycles;
+    dcyc += m.dram_cycles;
+  }
+  std::ostream& o = *visualizer_;
+  o << "kernel=" << kname << " cycle=" << now << " period=" << cycles << " insn=" << insn
+    << " ipc=" << (double)insn / (double)cycles << " l1_access=" << l1_acc << " l1_miss=" << l1_miss
+    << " l2_access=" << l2_acc << " l2_miss=" << l2_miss << " dram_rd=" << drd << " dram_wr=" << dwr
+    << " dram_util=" << (dcyc ? (double)busy / (double)dcyc : 0.0) << " sm_insn=";
+  for (size_t i = 0; i < dsm.size(); ++i) o << (i ? "," : "") << dsm[i].warp_insn;
+  o << "\n";
 }
 
 void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMStats>& sm,
@@ -531,6 +572,22 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   }
   print("icnt_total_pkts_mem_to_simt = %llu\n", (unsigned long long)pk_in);
   print("icnt_total_pkts_simt_to_mem = %llu\n", (unsigned long long)pk_out);
+  if (dopt_.memlatency_stat) {
+    // L1 miss round trips, cumulative over the run like the reference's
+    // memory_stats_t::memlatstat_print (prev_sm_ holds the raw counters here)
+    uint64_t n = 0, sum = 0, mx = 0, hist[16] = {};
+    for (auto& s : prev_sm_) {
+      n += s.mf_lat_n;
+      sum += s.mf_lat_sum;
+      mx = std::max<uint64_t>(mx, s.mf_lat_max);
+      for (int i = 0; i < 16; ++i) hist[i] += s.mf_lat_hist[i];
+    }
+    print("maxmflatency = %llu \n", (unsigned long long)mx);
+    print("averagemflatency = %llu \n", (unsigned long long)(n ? sum / n : 0));
+    print("mf_lat_table:");
+    for (int i = 0; i < 16; ++i) print("%llu \t", (unsigned long long)hist[i]);
+    print("\n");
+  }
   if (power_) print("gpu_avg_power = %.4f W\n", r.avg_power_w);
 }
 

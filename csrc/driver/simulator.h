@@ -100,7 +100,9 @@ class Simulator {
   std::unique_ptr<Engine> eng_;
   std::unique_ptr<PowerModel> power_;
   PowerTracker ptrack_;
-  std::unique_ptr<std::ofstream> power_report_, power_trace_, power_steady_;
+  std::unique_ptr<std::ofstream> power_report_, power_trace_, power_steady_, visualizer_;
+  void write_visualizer_sample(const std::string& kname, uint64_t now, uint64_t cycles,
+                               const std::vector<SMStats>& dsm, const std::vector<MemStats>& dm);
   std::vector<Command> cmds_;
   std::string out_;
   bool echo_ = true;

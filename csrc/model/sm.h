@@ -86,7 +86,8 @@ struct L1Mshr {
   uint8_t requested;  // sectors requested from L2
   uint8_t valid;      // entry in use
   uint8_t merges;
-  uint8_t pad[5];
+  uint8_t pad;
+  uint32_t t_issue;   // core cycle (low 32 bits) the miss was sent: memory latency stats
 };
 
 struct L1Pend {  // a load access waiting for sectors of a line
@@ -134,6 +135,10 @@ struct SMStats {
   uint64_t occupancy_acc;      // sum over cycles of live warps
   uint64_t mem_insn;
   uint64_t power_acc[8];       // spare power-model counters
+  // L1 miss round-trip latency (MSHR allocation -> last sector filled), the
+  // reference's mem_latency_stat (mem_latency_stat.h:37, -gpgpu_memlatency_stat)
+  uint64_t mf_lat_sum, mf_lat_n, mf_lat_max;
+  uint64_t mf_lat_hist[16];    // log2 buckets: [2^i, 2^(i+1)) cycles
 };
 
 // per-SM kernel bookkeeping (replicated identically in every SM)
@@ -423,7 +428,14 @@ SIM_HDI void l1_fill(SMState& s, const SmCtx& x, uint64_t line, uint8_t sectors,
   });
   if (mi >= 0) {
     s.mshr[mi].requested &= (uint8_t)~sectors;
-    if (s.mshr[mi].requested == 0) s.mshr[mi].valid = 0;
+    if (s.mshr[mi].requested == 0) {
+      s.mshr[mi].valid = 0;
+      const uint32_t lat = (uint32_t)now - s.mshr[mi].t_issue;
+      s.st.mf_lat_sum += lat;
+      s.st.mf_lat_n++;
+      if (lat > s.st.mf_lat_max) s.st.mf_lat_max = lat;
+      s.st.mf_lat_hist[lat ? amin<int>(15, 31 - __builtin_clz(lat)) : 0]++;
+    }
   }
   // wake waiters whose sectors are now all present (lane-parallel scan)
   const uint32_t np = s.n_pend;
@@ -563,6 +575,7 @@ SIM_HDI void sm_ldst(SMState& s, const SmCtx& x, uint64_t now) {
             s.mshr[mi].line = a.line;
             s.mshr[mi].requested = 0;
             s.mshr[mi].merges = 0;
+            s.mshr[mi].t_issue = (uint32_t)now;
           }
           s.mshr[mi].requested |= need_req;
           sm_send(s, c, P_RD, a.line, need_req, a.bytes, (uint32_t)mi);
