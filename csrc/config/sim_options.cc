@@ -682,6 +682,31 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.perfect_mem = r.getb("-gpgpu_perfect_mem") ? 1u : 0u;
   c.simple_dram = r.getb("-gpgpu_simple_dram_model") ? 1u : 0u;
   c.event_skip = r.getb("-sim_event_skip") ? 1u : 0u;
+  c.trace_mask = 0;
+  if (r.getb("-trace_enabled")) {
+    static const std::pair<const char*, uint32_t> streams[] = {
+        {"WARP_SCHEDULER", TS_WARP_SCHEDULER},
+        {"SCOREBOARD", TS_SCOREBOARD},
+        {"MEMORY_PARTITION_UNIT", TS_MEMORY_PARTITION_UNIT},
+        {"MEMORY_SUBPARTITION_UNIT", TS_MEMORY_SUBPARTITION_UNIT},
+        {"INTERCONNECT", TS_INTERCONNECT},
+        {"LIVENESS", TS_LIVENESS}};
+    for (auto& tok : split(strip_ws(r.gets("-trace_components")), ',')) {
+      if (tok.empty() || tok == "none") continue;
+      bool found = false;
+      for (auto& s : streams)
+        if (tok == s.first || tok == "all") {
+          c.trace_mask |= s.second;
+          found = true;
+        }
+      if (!found) throw OptionError("-trace_components: unknown stream " + tok);
+    }
+  }
+  c.trace_sm = (int32_t)r.geti("-trace_sampling_core");
+  c.trace_mem = (int32_t)r.geti("-trace_sampling_memory_partition");
+  c.trace_cap = 1u << 16;
+  c.trace_ev = nullptr;
+  c.trace_cnt = nullptr;
   c.bk_index_policy = (uint32_t)r.getu("-dram_bnk_indexing_policy");
   c.bkgrp_index_policy = (uint32_t)r.getu("-dram_bnkgrp_indexing_policy");
   c.atom_size = c.BL * c.busW * (uint32_t)r.getu("-gpgpu_n_mem_per_ctrlr");

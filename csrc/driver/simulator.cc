@@ -321,7 +321,7 @@ void Simulator::do_kernel(const Command& c) {
   if (dopt_.max_cycle) lim.max_cycle = (uint64_t)dopt_.max_cycle;
   auto ts = std::chrono::steady_clock::now();
   RunResult rr;
-  if (power_ || visualizer_) {
+  if (power_ || visualizer_ || cfg_.trace_mask) {
     ptrack_.begin_kernel();
     rr = run_sampled(start, lim, rk.h.name);
     if (visualizer_) visualizer_->flush();
@@ -441,6 +441,18 @@ RunResult Simulator::run_sampled(uint64_t start, const RunLimits& lim0, const st
       if (power_trace_) ptrack_.write_trace_line(*power_trace_, p, now);
     }
     if (visualizer_) write_visualizer_sample(kname, now, now > t_prev ? now - t_prev : 1, dsm, dm);
+    if (cfg_.trace_mask) {
+      emit_trace();
+      if (cfg_.trace_mask & TS_LIVENESS) {
+        uint64_t insn = 0;
+        for (auto& s : dsm) insn += s.thread_insn;
+        const double el = std::max(1e-9, wall_seconds());
+        print("GPGPU-Sim uArch: cycles simulated: %llu  inst.: %llu (ipc=%4.1f) sim_rate=%llu (inst/sec)\n",
+              (unsigned long long)now, (unsigned long long)(tot_insn_ + insn),
+              now > t_prev ? (double)insn / (double)(now - t_prev) : 0.0,
+              (unsigned long long)((double)(tot_insn_ + insn) / el));
+      }
+    }
     sm0.swap(sm1);
     m0.swap(m1);
     t_prev = now;
@@ -452,6 +464,61 @@ RunResult Simulator::run_sampled(uint64_t start, const RunLimits& lim0, const st
     if (r.epochs == 0) throw std::runtime_error("power sampling: engine made no progress");
   }
   return tot;
+}
+
+// Drain the engine's debug trace buffers and print them DPRINTF-style
+// (reference trace.h:56-88: "GPGPU-Sim Cycle N: STREAM - ...") in time order.
+void Simulator::emit_trace() {
+  std::vector<TraceEv> ev;
+  uint64_t dropped = 0;
+  eng_->trace_drain(ev, &dropped);
+  auto core_time = [&](const TraceEv& e) -> double {
+    if (e.kind == EV_L2_ACCESS) return (double)e.cycle * (double)cfg_.per_l2 / (double)cfg_.per_core;
+    if (e.kind == EV_DRAM_CMD) return (double)e.cycle * (double)cfg_.per_dram / (double)cfg_.per_core;
+    return (double)e.cycle;
+  };
+  std::vector<size_t> idx(ev.size());
+  for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+  std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
+    const double ta = core_time(ev[a]), tb = core_time(ev[b]);
+    if (ta != tb) return ta < tb;
+    return ev[a].unit < ev[b].unit;
+  });
+  static const char* l2o[] = {"hit", "miss", "mshr-hit", "write-through"};
+  static const char* dcmd[] = {"RD", "WR", "ACT", "PRE"};
+  for (size_t i : idx) {
+    const TraceEv& e = ev[i];
+    const unsigned long long cyc = (unsigned long long)core_time(e);
+    switch (e.kind) {
+      case EV_ISSUE:
+        print("GPGPU-Sim Cycle %llu: WARP_SCHEDULER - core %u issued warp %u pc 0x%llx %s\n", cyc, e.unit, e.a,
+              (unsigned long long)(e.b & 0xffffffffull), opcode_name((uint16_t)(e.b >> 32)).c_str());
+        break;
+      case EV_SB_RELEASE:
+        print("GPGPU-Sim Cycle %llu: SCOREBOARD - core %u warp %u releases register %llu\n", cyc, e.unit, e.a,
+              (unsigned long long)e.b);
+        break;
+      case EV_PKT_SEND:
+        print("GPGPU-Sim Cycle %llu: INTERCONNECT - core %u injects packet to sub-partition %u addr 0x%llx\n", cyc,
+              e.unit, e.a, (unsigned long long)e.b);
+        break;
+      case EV_PKT_RECV:
+        print("GPGPU-Sim Cycle %llu: INTERCONNECT - core %u ejects packet type %u addr 0x%llx\n", cyc, e.unit, e.a,
+              (unsigned long long)e.b);
+        break;
+      case EV_L2_ACCESS:
+        print("GPGPU-Sim Cycle %llu: MEMORY_SUBPARTITION_UNIT - channel %u sub %u L2 %s line 0x%llx\n", cyc,
+              e.unit - cfg_.n_sm, e.a >> 8, l2o[e.a & 3], (unsigned long long)e.b);
+        break;
+      case EV_DRAM_CMD:
+        print("GPGPU-Sim Cycle %llu: MEMORY_PARTITION_UNIT - channel %u DRAM %s bank %llu row %llu\n", cyc,
+              e.unit - cfg_.n_sm, dcmd[e.a & 3], (unsigned long long)(e.b >> 32),
+              (unsigned long long)(e.b & 0xffffffffull));
+        break;
+      default: break;
+    }
+  }
+  if (dropped) print("GPGPU-Sim: WARNING %llu trace events dropped (per-unit buffer full)\n", (unsigned long long)dropped);
 }
 
 // One line per sample period (reference visualizer_printstat, visualizer.cc:56-84,

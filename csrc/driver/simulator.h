@@ -101,6 +101,7 @@ class Simulator {
   std::unique_ptr<PowerModel> power_;
   PowerTracker ptrack_;
   std::unique_ptr<std::ofstream> power_report_, power_trace_, power_steady_, visualizer_;
+  void emit_trace();
   void write_visualizer_sample(const std::string& kname, uint64_t now, uint64_t cycles,
                                const std::vector<SMStats>& dsm, const std::vector<MemStats>& dm);
   std::vector<Command> cmds_;

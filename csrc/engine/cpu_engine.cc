@@ -98,6 +98,23 @@ class CpuEngine : public Engine {
     }
     epoch_ = 0;
     cycle_ = 0;
+    if (c_.trace_mask) {
+      const size_t units = (size_t)c.n_sm + c.n_mem;
+      trace_ev_.assign(units * c_.trace_cap, TraceEv{});
+      trace_cnt_.assign(units, 0);
+      c_.trace_ev = trace_ev_.data();
+      c_.trace_cnt = trace_cnt_.data();
+    }
+  }
+
+  void trace_drain(std::vector<TraceEv>& out, uint64_t* dropped) override {
+    out.clear();
+    for (size_t u = 0; u < trace_cnt_.size(); ++u) {
+      const uint32_t n = trace_cnt_[u], k = std::min(n, c_.trace_cap);
+      out.insert(out.end(), trace_ev_.begin() + (long)(u * c_.trace_cap), trace_ev_.begin() + (long)(u * c_.trace_cap + k));
+      if (dropped) *dropped += n - k;
+      trace_cnt_[u] = 0;
+    }
   }
 
   void load_kernel(const ReadyKernel& k, const KernelDesc& kd) override {
@@ -164,6 +181,8 @@ class CpuEngine : public Engine {
 
   uint64_t now() const override { return cycle_; }
   uint64_t ready_ = 0;  // cycle the current kernel may start issuing CTAs
+  std::vector<TraceEv> trace_ev_;
+  std::vector<uint32_t> trace_cnt_;
 
   void memcpy_fill_l2(uint64_t addr, uint64_t bytes) override {
     host_memcpy_fill(chs_.data(), (uint32_t)chs_.size(), c_, addr, bytes);

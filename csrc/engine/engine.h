@@ -53,6 +53,9 @@ class Engine {
   // by one engine resumes on the other (SURVEY §5.4 timing-state snapshot)
   virtual void save_state(std::vector<uint8_t>& out) = 0;
   virtual void load_state(const std::vector<uint8_t>& in) = 0;
+  // debug trace streams: events recorded since the last drain (per unit, in
+  // program order); `dropped` counts events lost to full per-unit buffers
+  virtual void trace_drain(std::vector<TraceEv>& out, uint64_t* dropped) = 0;
 };
 
 // layout of save_state(): header, then SMState[n_sm], ChanState[n_mem],

@@ -316,6 +316,15 @@ class GpuEngine : public Engine {
       HIPCHECK(hipMemset(d_prof_, 0, sizeof(uint64_t) * nblocks_ * kProfSlots));
     }
     HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (c_.trace_mask) {
+      // debug trace buffers in HBM; the device copy of the config points at them
+      const size_t units = (size_t)c.n_sm + c.n_mem;
+      HIPCHECK(hipMalloc(&d_trace_ev_, units * c_.trace_cap * sizeof(TraceEv)));
+      HIPCHECK(hipMalloc(&d_trace_cnt_, units * sizeof(uint32_t)));
+      HIPCHECK(hipMemset(d_trace_cnt_, 0, units * sizeof(uint32_t)));
+      c_.trace_ev = d_trace_ev_;
+      c_.trace_cnt = d_trace_cnt_;
+    }
     HIPCHECK(hipMalloc(&d_cfg_, sizeof(SimCfg)));
     HIPCHECK(hipMemcpy(d_cfg_, &c_, sizeof(SimCfg), hipMemcpyHostToDevice));
     std::vector<SMState> hs(c.n_sm);
@@ -467,6 +476,23 @@ class GpuEngine : public Engine {
   }
   void set_epochs_per_launch(uint32_t n) { epochs_per_launch_ = n ? n : 4096; }
 
+  void trace_drain(std::vector<TraceEv>& out, uint64_t* dropped) override {
+    out.clear();
+    if (!c_.trace_mask) return;
+    const size_t units = (size_t)c_.n_sm + c_.n_mem;
+    std::vector<uint32_t> cnt(units);
+    HIPCHECK(hipMemcpy(cnt.data(), d_trace_cnt_, units * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (size_t u = 0; u < units; ++u) {
+      const uint32_t k = std::min(cnt[u], c_.trace_cap);
+      if (dropped) *dropped += cnt[u] - k;
+      if (!k) continue;
+      const size_t o = out.size();
+      out.resize(o + k);
+      HIPCHECK(hipMemcpy(out.data() + o, d_trace_ev_ + u * c_.trace_cap, k * sizeof(TraceEv), hipMemcpyDeviceToHost));
+    }
+    HIPCHECK(hipMemset(d_trace_cnt_, 0, units * sizeof(uint32_t)));
+  }
+
   // same image layout as the CPU engine (engine.h EngineStateHeader), so a
   // state saved here resumes on either engine
   EngineStateHeader header() const {
@@ -551,6 +577,8 @@ class GpuEngine : public Engine {
       fr(d_cnt_rep_[p]);
     }
     fr(d_ctl_);
+    fr(d_trace_ev_);
+    fr(d_trace_cnt_);
     fr(d_insts_);
     fr(d_accs_);
     fr(d_streams_);
@@ -573,6 +601,8 @@ class GpuEngine : public Engine {
   uint32_t* d_cnt_rep_[2] = {nullptr, nullptr};
   GpuCtl* d_ctl_ = nullptr;
   GpuCtl* h_ctl_ = nullptr;
+  TraceEv* d_trace_ev_ = nullptr;
+  uint32_t* d_trace_cnt_ = nullptr;
   void* d_insts_ = nullptr;
   void* d_accs_ = nullptr;
   void* d_streams_ = nullptr;

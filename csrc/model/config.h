@@ -67,6 +67,34 @@ struct CacheGeom {
   uint8_t pad;
 };
 
+// Debug trace streams (reference gem5-style DPRINTF streams, trace.h:28-92,
+// trace_streams.tup: -trace_enabled / -trace_components / -trace_sampling_*).
+// Units append fixed-size events to per-unit buffers; the host drains and
+// prints them in (cycle, unit, order) order, identically for both engines.
+enum TraceStream : uint32_t {
+  TS_WARP_SCHEDULER = 1u << 0,
+  TS_SCOREBOARD = 1u << 1,
+  TS_MEMORY_PARTITION_UNIT = 1u << 2,
+  TS_MEMORY_SUBPARTITION_UNIT = 1u << 3,
+  TS_INTERCONNECT = 1u << 4,
+  TS_LIVENESS = 1u << 5,
+};
+enum TraceKind : uint16_t {
+  EV_ISSUE = 1,      // a = warp, b = pc | opcode << 32
+  EV_SB_RELEASE,     // a = warp, b = register
+  EV_PKT_SEND,       // a = destination sub-partition, b = line address
+  EV_PKT_RECV,       // a = packet type, b = line address
+  EV_L2_ACCESS,      // a = sub << 8 | outcome (0 hit, 1 miss, 2 mshr hit, 3 bypass/atomic), b = line
+  EV_DRAM_CMD,       // a = command (0 RD, 1 WR, 2 ACT, 3 PRE), b = bank << 32 | row
+};
+struct TraceEv {
+  uint64_t cycle;  // core cycle (SM events) or DRAM cycle (DRAM commands) / femtoseconds>>10 (L2)
+  uint32_t unit;   // SM id, or n_sm + channel id
+  uint16_t kind;
+  uint16_t a;
+  uint64_t b;
+};
+
 struct SimCfg {
   // ---- topology ----
   uint32_t n_sm;
@@ -151,7 +179,35 @@ struct SimCfg {
   uint32_t perfect_mem;     // every global/local access hits with L1 latency, no traffic
   uint32_t simple_dram;     // DRAM = latency pipe + one column per DRAM cycle, no bank timing
   uint32_t event_skip;      // fast-forward provably quiet SM cycles inside an epoch (exact)
+  // ---- debug trace streams (pointers are set by the engine that owns the buffers) ----
+  uint32_t trace_mask;      // TraceStream bits
+  int32_t trace_sm;         // -trace_sampling_core (-1: all)
+  int32_t trace_mem;        // -trace_sampling_memory_partition (-1: all)
+  uint32_t trace_cap;       // events per unit per drain
+  TraceEv* trace_ev;        // [units][trace_cap]
+  uint32_t* trace_cnt;      // [units]
 };
+
+// append one event for `unit` (call from code that one lane executes, or all
+// lanes redundantly through P::one)
+SIM_HDI void trace_put(const SimCfg& c, uint32_t unit, uint64_t cycle, uint16_t kind, uint16_t a, uint64_t b) {
+  uint32_t n = c.trace_cnt[unit];
+  if (n < c.trace_cap) {
+    TraceEv& e = c.trace_ev[(uint64_t)unit * c.trace_cap + n];
+    e.cycle = cycle;
+    e.unit = unit;
+    e.kind = kind;
+    e.a = a;
+    e.b = b;
+  }
+  c.trace_cnt[unit] = n + 1;
+}
+SIM_HDI bool trace_sm_on(const SimCfg& c, uint32_t stream, uint32_t sm) {
+  return (c.trace_mask & stream) && (c.trace_sm < 0 || (uint32_t)c.trace_sm == sm);
+}
+SIM_HDI bool trace_mem_on(const SimCfg& c, uint32_t stream, uint32_t ch) {
+  return (c.trace_mask & stream) && (c.trace_mem < 0 || (uint32_t)c.trace_mem == ch);
+}
 
 // ---- helpers shared by both engines ----
 SIM_HDI uint32_t unit_of(const SimCfg& c, uint8_t cls) {

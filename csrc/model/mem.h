@@ -245,6 +245,11 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
   const uint32_t set = l2_set(c, p.addr);
   const uint32_t stype = p.type == P_WR ? L2T_WR : (p.type == P_ATOM ? L2T_ATOM : L2T_RD);
   if (sp.rep_n >= (uint32_t)kReplyQ) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
+  // MEMORY_SUBPARTITION_UNIT trace: outcome 0 hit, 1 miss, 2 mshr hit, 3 write-through
+  auto trace = [&](uint16_t outcome) {
+    if (trace_mem_on(c, TS_MEMORY_SUBPARTITION_UNIT, ch.id))
+      P::one([&] { trace_put(c, c.n_sm + ch.id, now_fs / c.per_l2, EV_L2_ACCESS, (uint16_t)(sub << 8 | outcome), p.addr); });
+  };
   int way = g.disabled ? -1 : l2_find<P>(sp, g, set, p.addr);
   if (p.type == P_WR) {
     if (g.disabled || g.wpolicy == WP_WRITE_THROUGH) {
@@ -253,13 +258,16 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
       for (uint32_t s = 0; s < 4; ++s)
         if (p.sectors >> s & 1u) l2dram_push(ch, sp, c, sub, p.addr, s, true, now_fs);
       if (way >= 0) sp.l2[set * g.assoc + way].valid |= p.sectors;
+      trace(3);
     } else {
       if (way < 0) {
         way = l2_alloc<P>(ch, sp, c, sub, set, p.addr, now_fs);
         if (way < 0) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
         sp.st.l2[stype][L2O_MISS]++;
+        trace(1);
       } else {
         sp.st.l2[stype][L2O_HIT]++;
+        trace(0);
       }
       L2Line& L = sp.l2[set * g.assoc + way];
       L.valid |= p.sectors;
@@ -279,6 +287,7 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
     if (p.type == P_ATOM) L.dirty |= p.sectors;
     reply_push(sp, rtype, p, p.sectors);
     sp.st.l2[stype][L2O_HIT]++;
+    trace(0);
     return true;
   }
   if (sp.n_wait >= (uint32_t)kMaxL2Wait) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
@@ -291,6 +300,7 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
     if (sp.mshr[mi].merges >= g.mshr_merge) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
     sp.mshr[mi].merges++;
     sp.st.l2[stype][L2O_MSHR_HIT]++;
+    trace(2);
   } else {
     uint32_t nreq = (uint32_t)popc64(need_req);
     if (!l2dram_can(ch, sp, c, nreq)) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
@@ -306,6 +316,7 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
     for (uint32_t s = 0; s < 4; ++s)
       if (need_req >> s & 1u) l2dram_push(ch, sp, c, sub, p.addr, s, false, now_fs);
     sp.st.l2[stype][L2O_MISS]++;
+    trace(1);
   }
   // waiter entry (first free)
   uint32_t wi = sp.n_wait;
@@ -561,6 +572,8 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
     if (pick >= 0 && !(ch.q[pick].write == 0 && ch.ret_n >= (uint32_t)kDramRet)) {
       const DramReq r = ch.q[pick];
       DramBank& b = ch.bk[r.bank];
+      if (trace_mem_on(c, TS_MEMORY_PARTITION_UNIT, ch.id))
+        P::one([&] { trace_put(c, c.n_sm + ch.id, t, EV_DRAM_CMD, r.write ? 1 : 0, (uint64_t)r.bank << 32 | r.row); });
       if (r.write) {
         b.t_pre_ok = amax<uint64_t>(b.t_pre_ok, t + c.WL + burst + c.tWR);
         ch.t_rd_ok = amax<uint64_t>(ch.t_rd_ok, t + c.WL + burst + c.tCDLR);
@@ -606,6 +619,11 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
   if (act >= 0) {
     const DramReq& r = ch.q[act];
     DramBank& b = ch.bk[r.bank];
+    if (trace_mem_on(c, TS_MEMORY_PARTITION_UNIT, ch.id))
+      P::one([&] {
+        trace_put(c, c.n_sm + ch.id, t, EV_DRAM_CMD, b.open ? 3 : 2,
+                  (uint64_t)r.bank << 32 | (b.open ? b.row : r.row));
+      });
     if (b.open) {
       b.open = 0;
       b.t_act_ok = amax<uint64_t>(b.t_act_ok, t + c.tRP);

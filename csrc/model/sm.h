@@ -305,6 +305,7 @@ SIM_HDI void sm_inject(SMState& s, const SmCtx& x, uint64_t now) {
   if (n >= x.out_cap) return;  // outbox cell full (cannot happen with cap >= epoch)
   s.ocnt[dst] = n + 1;
   p.t = (done + c.icnt_latency) * c.per_core;
+  if (trace_sm_on(c, TS_INTERCONNECT, s.id)) P::one([&] { trace_put(c, s.id, now, EV_PKT_SEND, (uint16_t)dst, p.addr); });
   P::one([&] {
     x.outbox[(uint64_t)slot * x.out_cap + n] = p;
     x.outcnt[slot] = n + 1;
@@ -325,6 +326,11 @@ SIM_HDI void sm_writeback(SMState& s, const SimCfg& c, uint64_t now) {
   uint32_t n = s.wb_cnt[slot];
   for (uint32_t i = 0; i < n; ++i) {
     WbEnt e = s.wb[slot][i];
+    if (trace_sm_on(c, TS_SCOREBOARD, s.id))
+      P::one([&] {
+        if (e.dst0) trace_put(c, s.id, now, EV_SB_RELEASE, e.warp, e.dst0 - 1u);
+        if (e.dst1) trace_put(c, s.id, now, EV_SB_RELEASE, e.warp, e.dst1 - 1u);
+      });
     sb_clr(s.w_sb[e.warp], e.dst0);
     sb_clr(s.w_sb[e.warp], e.dst1);
     s.w_inflight[e.warp]--;
@@ -467,6 +473,7 @@ SIM_HDI void sm_receive(SMState& s, const SmCtx& x, uint64_t now) {
   const Pkt& p = s.inq[s.inq_head];
   if (p.t > now * c.per_core) return;
   Pkt q = p;
+  if (trace_sm_on(c, TS_INTERCONNECT, s.id)) P::one([&] { trace_put(c, s.id, now, EV_PKT_RECV, q.type, q.addr); });
   s.inq_head = (s.inq_head + 1) % kInQ;
   s.inq_n--;
   s.outstanding--;
@@ -836,6 +843,8 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
     const uint32_t w = (uint32_t)pick;
     s.sched_last[sc] = w;
     const TInst in = s.w_win[w][s.w_head[w] % kWin];
+    if (trace_sm_on(c, TS_WARP_SCHEDULER, s.id))
+      P::one([&] { trace_put(c, s.id, now, EV_ISSUE, (uint16_t)w, (uint64_t)in.pc | (uint64_t)in.opcode << 32); });
     s.w_head[w]++;
     s.w_ibuf[w]--;
     issued_any = true;

@@ -57,3 +57,23 @@ def test_state_snapshot_bit_exact(gpu_mod, tmp_path):
     a, b = sg.native.snapshot(), sc.native.snapshot()
     assert len(a) == len(b)
     assert a == b
+
+
+@pytest.mark.parametrize("extra", [
+    {"-trace_enabled": "1", "-trace_sampling_core": "-1", "-gpgpu_perf_sim_memcpy": "0",
+     "-trace_components": "WARP_SCHEDULER,SCOREBOARD,MEMORY_PARTITION_UNIT,MEMORY_SUBPARTITION_UNIT,INTERCONNECT"},
+    {"-gpgpu_perfect_mem": "1"},
+    {"-gpgpu_simple_dram_model": "1", "-gpgpu_dram_scheduler": "0"},
+    {"-sim_event_skip": "0"},
+])
+def test_model_switches_gpu_equals_cpu(gpu_mod, tmp_path, extra):
+    """Debug trace streams (event for event), idealised memory, FIFO DRAM and
+    the no-skip path are identical on both engines."""
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    kl = rodinia.write_app(str(tmp_path / "bfs"), rodinia.bfs(2048, levels=3))
+    g = sim.simulate(kl, "QV100", engine="gpu", extra=extra)
+    c = sim.simulate(kl, "QV100", engine="cpu", extra=extra)
+    assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
+    tl = lambda o: [l for l in o.splitlines() if l.startswith("GPGPU-Sim Cycle ")]
+    assert tl(g.output) == tl(c.output)

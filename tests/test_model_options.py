@@ -42,6 +42,46 @@ def test_dram_scheduler_choice_matters(native, traces):
     assert fr.tot_cycle != ff.tot_cycle
 
 
+TRACE_ALL = {"-trace_enabled": "1", "-trace_sampling_core": "-1", "-gpgpu_perf_sim_memcpy": "0",
+             "-trace_components": "WARP_SCHEDULER,SCOREBOARD,MEMORY_PARTITION_UNIT,MEMORY_SUBPARTITION_UNIT,"
+                                  "INTERCONNECT,LIVENESS"}
+
+
+def _trace_lines(out):
+    return [l for l in out.splitlines() if l.startswith("GPGPU-Sim Cycle ")]
+
+
+def test_debug_trace_streams(native, traces):
+    import re
+    base = _run(native, traces["vadd"], {"-gpgpu_perf_sim_memcpy": "0"})
+    tr = _run(native, traces["vadd"], TRACE_ALL)
+    assert tr.tot_cycle == base.tot_cycle  # tracing never changes timing
+    lines = _trace_lines(tr.output)
+    streams = {re.match(r"GPGPU-Sim Cycle \d+: (\w+) -", l).group(1) for l in lines}
+    assert streams == {"WARP_SCHEDULER", "SCOREBOARD", "MEMORY_PARTITION_UNIT", "MEMORY_SUBPARTITION_UNIT",
+                       "INTERCONNECT"}
+    cycles = [int(l.split()[2].rstrip(":")) for l in lines]
+    assert cycles == sorted(cycles)
+    assert "cycles simulated:" in tr.output
+    # issue events == warp instructions
+    issued = sum(1 for l in lines if "WARP_SCHEDULER" in l)
+    m = re.findall(r"gpgpu_n_tot_w_icount = (\d+)", tr.output)
+    assert issued == int(m[-1])
+    one = _run(native, traces["vadd"], dict(TRACE_ALL, **{"-trace_sampling_core": "3",
+                                                          "-trace_components": "WARP_SCHEDULER"}))
+    assert {l.split("core ")[1].split()[0] for l in _trace_lines(one.output)} == {"3"}
+
+
+def test_memlatency_and_visualizer(native, traces, tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    s = _run(native, traces["vadd"], {"-gpgpu_memlatency_stat": "14", "-visualizer_enabled": "1",
+                                      "-gpgpu_runtime_stat": "500:0", "-gpgpu_perf_sim_memcpy": "0"})
+    assert "averagemflatency = " in s.output and "mf_lat_table:" in s.output
+    log = open(tmp_path / "gpgpusim_visualizer.log").read().splitlines()
+    assert len(log) > 3 and all(l.startswith("kernel=") for l in log)
+    assert sum(int(l.split(" insn=")[1].split()[0]) for l in log) == s.tot_insn
+
+
 def test_max_cycle_cap_breaks(native, traces):
     s = native.Simulator(presets.args_for("QV100", {"-gpgpu_max_cycle": "3000"}) + ["-trace", traces["bfs"]], False)
     assert s.run() == 0
