@@ -306,8 +306,11 @@ def split_config(opts: Dict[str, str]) -> Tuple[Dict[str, str], Dict[str, str]]:
     return gpgpu, trace
 
 
-def write_config(name_or_opts, out_dir: str, extra: Dict[str, str] | None = None) -> Tuple[str, str]:
-    """Write gpgpusim.config + trace.config for a preset; returns both paths."""
+def write_config(name_or_opts, out_dir: str, extra: Dict[str, str] | None = None,
+                 power_preset: str | None = None) -> Tuple[str, str]:
+    """Write gpgpusim.config + trace.config for a preset; returns both paths.
+    ``power_preset`` names the preset whose default AccelWattch XMLs go next
+    to a custom option dict (default: the preset's own)."""
     opts = get_preset(name_or_opts) if isinstance(name_or_opts, str) else dict(name_or_opts)
     if extra:
         opts.update(extra)
@@ -323,7 +326,7 @@ def write_config(name_or_opts, out_dir: str, extra: Dict[str, str] | None = None
     # AccelWattch XMLs next to the configs (SIM / HW / HYBRID modes share the
     # uncalibrated defaults until power.calibrate rewrites them)
     from ..power.xmlcfg import default_params, write_xml
-    pname = name_or_opts if isinstance(name_or_opts, str) else "custom"
+    pname = power_preset or (name_or_opts if isinstance(name_or_opts, str) else "custom")
     for mode in ("sim", "hw", "hybrid"):
         xp = os.path.join(out_dir, f"accelwattch_sass_{mode}.xml")
         if not os.path.exists(xp):

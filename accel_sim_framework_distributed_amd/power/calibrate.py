@@ -82,6 +82,48 @@ def fit_scaling(A: np.ndarray, b: np.ndarray, lower: float | np.ndarray = 0.1, u
     return x
 
 
+# coarse component groups: one scaling factor per group keeps the number of
+# fitted parameters well below the number of validation kernels
+COMPONENT_GROUPS: Dict[str, List[str]] = {
+    "idle": ["CONSTP", "IDLE_COREP"],
+    "static": ["STATICP"],
+    "valu": ["IBP", "ICP", "RFP", "INTP", "FPUP", "DPUP", "INT_MUL24P", "INT_MUL32P", "INT_MULP", "INT_DIVP",
+             "FP_MULP", "FP_DIVP", "DP_DIVP", "SCHEDP", "PIPEP"],
+    "special": ["FP_SQRTP", "FP_LGP", "FP_SINP", "FP_EXP", "DP_MULP", "TENSORP", "TEXP"],
+    "memory": ["DCP", "TCP", "CCP", "SHRDP", "L2CP", "MCP", "NOCP", "DRAMP"],
+}
+
+
+def group_matrix(components: Sequence[str] = COMPONENTS, groups: Dict[str, List[str]] = COMPONENT_GROUPS):
+    """(G x C) 0/1 matrix mapping group factors to component factors."""
+    names = list(groups)
+    M = np.zeros((len(names), len(components)))
+    for gi, g in enumerate(names):
+        for c in groups[g]:
+            if c in components:
+                M[gi, list(components).index(c)] = 1.0
+    return names, M
+
+
+def fit_groups(A: np.ndarray, b: np.ndarray, groups: Dict[str, List[str]] = COMPONENT_GROUPS, **kw) -> np.ndarray:
+    """Per-component factors constrained to be equal within each group."""
+    names, M = group_matrix(groups=groups)
+    xg = fit_scaling(np.asarray(A) @ M.T, b, **kw)
+    x = M.T @ xg
+    x[M.sum(axis=0) == 0] = 1.0
+    return x
+
+
+def leave_one_out_groups(A: np.ndarray, b: np.ndarray, **kw) -> np.ndarray:
+    A = np.asarray(A, np.float64)
+    b = np.asarray(b, np.float64)
+    out = np.zeros(len(b))
+    for i in range(len(b)):
+        keep = np.arange(len(b)) != i
+        out[i] = A[i] @ fit_groups(A[keep], b[keep], **kw)
+    return out
+
+
 def mape(pred: Sequence[float], meas: Sequence[float]) -> Tuple[float, float]:
     """(mean absolute percentage error %, mean absolute error W)."""
     p, m = np.asarray(pred, np.float64), np.asarray(meas, np.float64)

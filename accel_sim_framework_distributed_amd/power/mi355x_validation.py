@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""AccelWattch validation micro-benchmarks on MI355X (BASELINE config #3).
+
+The stress kernels of csrc/ubench/ub_power.hip (idle, fp32 FMA, int32 MAD,
+fp64 FMA, sqrt+exp, bf16 MFMA, LDS read, HBM read) are re-expressed as
+synthetic wave64 CDNA traces with the same instruction mix, occupancy and
+memory pattern (shortened: power is a rate, so a few hundred loop
+iterations reach the kernel's steady state).  Each trace is simulated with
+the tuned MI355X configuration and the power model on; the per-component
+simulated power of every kernel (the rows of the reference's
+quadprog_solver.m design matrix) is fitted to the socket power amd-smi
+measured while the real kernel ran (profiles/ubench_mi355x/ub_power.log).
+
+Outputs the calibrated XML and MAPE -- in-sample and leave-one-out, the
+latter being the honest number for 8 kernels.
+
+    python -m accel_sim_framework_distributed_amd.power.mi355x_validation
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+import sys
+import tempfile
+from typing import Dict, List
+
+import numpy as np
+
+if __package__ in (None, ""):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from accel_sim_framework_distributed_amd import _native  # noqa: E402
+from accel_sim_framework_distributed_amd.power import calibrate, report, xmlcfg  # noqa: E402
+from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder  # noqa: E402
+from accel_sim_framework_distributed_amd.tracegen.format import write_kernel_binary, write_kernelslist  # noqa: E402
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+TUNED = os.path.join(REPO, "configs", "tuned", "AMD_Instinct_MI355X")
+MEASURED = os.path.join(REPO, "profiles", "ubench_mi355x", "ub_power.log")
+
+CUS, BLOCK = 256, 256
+
+
+def _kernel(name: str, body, iters: int, cta_per_cu: int = 8, shmem: int = 0) -> KernelBuilder:
+    k = KernelBuilder(name, (CUS * cta_per_cu, 1, 1), (BLOCK, 1, 1), shmem=shmem, nregs=32, binary_version=950,
+                      warp_size=64)
+    k.op("v_mad_u32_u24", [1], [0])
+    for i in range(iters):
+        body(k, i)
+    k.op("s_endpgm")
+    return k
+
+
+def stress_kernels(iters: int = 48) -> Dict[str, KernelBuilder]:
+    """Trace builders mirroring ub_power.hip's kernels (8 independent chains each)."""
+    hbm_base = 0x7F0000000000
+
+    def fp32(k, i):
+        for c in range(8):
+            k.op("v_fma_f32", [8 + c], [8 + c])
+        k.op("s_add_u32", [], []) if i % 8 == 7 else None
+
+    def int32(k, i):
+        for c in range(8):
+            k.op("v_mul_lo_u32", [8 + c], [8 + c])
+            k.op("v_add_u32", [8 + c], [8 + c])
+
+    def fp64(k, i):
+        for c in range(8):
+            k.op("v_fma_f64", [8 + 2 * c], [8 + 2 * c])
+
+    def sfu(k, i):
+        k.op("v_sqrt_f32", [8], [8])
+        k.op("v_exp_f32", [9], [8])
+        k.op("v_add_f32", [8], [8, 9])
+
+    def mfma(k, i):
+        k.op("v_mfma_f32_32x32x16_bf16", [40], [40, 2, 3])
+        k.op("v_mfma_f32_32x32x16_bf16", [56], [56, 2, 3])
+
+    def lds(k, i):
+        k.op("ds_read_b32", [8 + (i % 8)], [1], base=(i * 256) % 16384, stride=4)
+        k.op("v_add_f32", [7], [7, 8 + (i % 8)])
+
+    def hbm(k, i):
+        g = k.g
+        stride_cta = BLOCK * 16
+        base = hbm_base + (g.cta * stride_cta + g.warp * 64 * 16 + i * (CUS * 8 * stride_cta)) % (1 << 30)
+        k.op("global_load_dwordx4", [8], [1], base=base, stride=16)
+        k.op("s_waitcnt")
+        k.op("v_add_f32", [7], [7, 8])
+
+    ks = {
+        "fp32_fma": _kernel("k_fp32", fp32, iters),
+        "int32_mad": _kernel("k_int", int32, iters),
+        "fp64_fma": _kernel("k_fp64", fp64, iters),
+        "sfu_sqrt_exp": _kernel("k_sfu", sfu, iters * 2),
+        "mfma_bf16": _kernel("k_mfma", mfma, iters),
+        "lds_read": _kernel("k_lds", lds, iters * 2, shmem=16384),
+        "hbm_read": _kernel("k_hbm", hbm, iters // 2),
+    }
+    # idle: one tiny workgroup, the rest of the chip idle
+    idle = KernelBuilder("k_idle", (1, 1, 1), (64, 1, 1), nregs=8, binary_version=950, warp_size=64)
+    idle.op("s_endpgm")
+    ks["idle"] = idle
+    return ks
+
+
+def measured_power(path: str = MEASURED) -> Dict[str, float]:
+    out = {}
+    with open(path) as f:
+        for row in csv.reader(l for l in f if not l.startswith("#")):
+            if len(row) >= 2 and row[0] and row[0] != "":
+                try:
+                    out[row[0]] = float(row[1])
+                except ValueError:
+                    pass
+    return out
+
+
+def simulate_power(work: str, xml: str, kernels: Dict[str, KernelBuilder]) -> Dict[str, Dict]:
+    mod = _native.load()
+    res = {}
+    for name, kb in kernels.items():
+        d = os.path.join(work, name)
+        os.makedirs(d, exist_ok=True)
+        write_kernel_binary(os.path.join(d, "kernel-1.asimk"), kb.build())
+        kl = write_kernelslist(d, ["kernel-1.asimk"])
+        args = ["-config", os.path.join(TUNED, "gpgpusim.config"), "-config", os.path.join(TUNED, "trace.config"),
+                "-trace", kl, "-power_simulation_enabled", "1", "-accelwattch_xml_file", xml,
+                "-power_report_file", os.path.join(d, "accelwattch_power_report.log"), "-gpgpu_runtime_stat", "2000:0"]
+        s = mod.Simulator(args, False)
+        if s.run() != 0:
+            raise RuntimeError(f"{name}: simulation failed\n{s.output[-1000:]}")
+        rep = report.parse_power_report(os.path.join(d, "accelwattch_power_report.log"))[0]
+        res[name] = dict(report=rep, cycles=s.tot_cycle, insn=s.tot_insn)
+    return res
+
+
+def run(work: str, out_xml: str) -> Dict:
+    base_xml = os.path.join(TUNED, "accelwattch_sass_sim.xml")
+    if not os.path.exists(base_xml):
+        xmlcfg.write_xml(base_xml, xmlcfg.default_params("MI355X"))
+    meas = measured_power()
+    ks = stress_kernels()
+    sim = simulate_power(work, base_xml, ks)
+    names = [n for n in ks if n in meas]
+    A = calibrate.design_matrix([sim[n]["report"] for n in names])
+    b = np.array([meas[n] for n in names])
+    before = A.sum(axis=1)
+    # one factor per component group (static / VALU / special units / memory):
+    # 4 parameters for 8 kernels, so leave-one-out is a real prediction
+    x = calibrate.fit_groups(A, b, lower=0.05, upper=50.0)
+    fit = A @ x
+    loo = calibrate.leave_one_out_groups(A, b, lower=0.05, upper=50.0)
+    # the per-component fit (33 free factors) for reference: exact in sample, no predictive power
+    xc = calibrate.fit_scaling(A, b, lower=0.05, upper=50.0)
+    calibrate.apply_factors(base_xml, out_xml, x)
+    names_g, M = calibrate.group_matrix()
+    summary = dict(
+        kernels=names, measured_w=b.tolist(), uncalibrated_w=before.tolist(), calibrated_w=fit.tolist(),
+        loo_w=loo.tolist(),
+        mape_uncalibrated=calibrate.mape(before, b)[0], mape_in_sample=calibrate.mape(fit, b)[0],
+        mape_leave_one_out=calibrate.mape(loo, b)[0], mae_leave_one_out_w=calibrate.mape(loo, b)[1],
+        mape_per_component_in_sample=calibrate.mape(A @ xc, b)[0],
+        group_factors={g: float(x[list(M[i]).index(1.0)]) if M[i].any() else 1.0 for i, g in enumerate(names_g)},
+        xml=out_xml)
+    return summary
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("-o", "--out_xml", default=os.path.join(TUNED, "accelwattch_sass_sim_calibrated.xml"))
+    ap.add_argument("-j", "--json", default=os.path.join(REPO, "profiles", "power_mi355x_validation.json"))
+    ap.add_argument("-w", "--work", default="")
+    o = ap.parse_args(argv)
+    work = o.work or tempfile.mkdtemp(prefix="asim_power_")
+    s = run(work, o.out_xml)
+    with open(o.json, "w") as f:
+        json.dump(s, f, indent=1)
+    print(f"{'kernel':14s} {'measured':>9s} {'uncal':>9s} {'fit':>9s} {'LOO':>9s}")
+    for i, n in enumerate(s["kernels"]):
+        print(f"{n:14s} {s['measured_w'][i]:9.1f} {s['uncalibrated_w'][i]:9.1f} {s['calibrated_w'][i]:9.1f} "
+              f"{s['loo_w'][i]:9.1f}")
+    print(f"MAPE uncalibrated {s['mape_uncalibrated']:.2f}%  in-sample {s['mape_in_sample']:.2f}%  "
+          f"leave-one-out {s['mape_leave_one_out']:.2f}% ({s['mae_leave_one_out_w']:.1f} W)")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -53,8 +53,9 @@ def default_params(preset: str) -> Dict[str, float]:
     power.calibrate to fit them to measured power."""
     p = {a: 1.0 for a in ACTIVITIES}
     if preset.upper() == "MI355X":
-        # 1400 W board; 256 CUs; idle board power ~ 250 W class
-        p.update(constant_power=160.0, idle_core_power=0.35)
+        # 1400 W board, 256 CUs; ~300 W measured with the chip idle
+        # (profiles/ubench_mi355x/ub_power.log): HBM3E stacks, fabric, MALL
+        p.update(constant_power=230.0, idle_core_power=0.3)
         cats = dict(cat1=(120.0, 3.0), cat2=(150.0, 3.5), cat3=(170.0, 4.0), cat4=(155.0, 3.5), cat5=(130.0, 3.0),
                     cat6=(380.0, 0.0), light=(20.0, 0.05))
         p.update(static_shared_flane=90.0, static_l1_flane=100.0, static_l2_flane=60.0)

@@ -62,10 +62,33 @@ SASS = {
 }
 
 
+# CDNA4 (gfx950) mnemonics for native wave64 traces; classes follow the
+# simulator's CDNA decoder (csrc/trace/trace.cc decode_cdna)
+CDNA = {
+    "v_fma_f32": ("SP", "NONE", 0, 0), "v_add_f32": ("SP", "NONE", 0, 0), "v_mul_f32": ("SP", "NONE", 0, 0),
+    "v_mov_b32": ("SP", "NONE", 0, 0), "v_mad_u32_u24": ("SP", "NONE", 0, 0), "v_add_u32": ("SP", "NONE", 0, 0),
+    "v_mul_lo_u32": ("SP", "NONE", 0, 0), "v_lshlrev_b32": ("SP", "NONE", 0, 0), "v_cmp_gt_i32": ("SP", "NONE", 0, 0),
+    "v_fma_f64": ("DP", "NONE", 0, 0), "v_add_f64": ("DP", "NONE", 0, 0),
+    "v_sqrt_f32": ("SFU", "NONE", 0, 0), "v_exp_f32": ("SFU", "NONE", 0, 0), "v_rcp_f32": ("SFU", "NONE", 0, 0),
+    "v_mfma_f32_32x32x16_bf16": ("TENSOR", "NONE", 0, 0),
+    "s_add_u32": ("INTP", "NONE", 0, 0), "s_mul_i32": ("INTP", "NONE", 0, 0), "s_cmp_lt_i32": ("INTP", "NONE", 0, 0),
+    "s_cbranch_scc1": ("BRANCH", "NONE", 0, 0), "s_branch": ("BRANCH", "NONE", 0, 0),
+    "s_waitcnt": ("NOP", "NONE", FLAG["WAITCNT"], 0), "s_barrier": ("BARRIER", "NONE", 0, 0),
+    "s_endpgm": ("EXIT", "NONE", 0, 0), "s_nop": ("NOP", "NONE", 0, 0),
+    "global_load_dword": ("LOAD", "GLOBAL", FLAG["MEM"], 4), "global_load_dwordx2": ("LOAD", "GLOBAL", FLAG["MEM"], 8),
+    "global_load_dwordx4": ("LOAD", "GLOBAL", FLAG["MEM"], 16),
+    "global_store_dword": ("STORE", "GLOBAL", FLAG["MEM"], 4),
+    "global_store_dwordx4": ("STORE", "GLOBAL", FLAG["MEM"], 16),
+    "global_atomic_add": ("LOAD", "GLOBAL", FLAG["MEM"] | FLAG["ATOMIC"] | FLAG["BYPASS_L1"], 4),
+    "ds_read_b32": ("LOAD", "SHARED", FLAG["MEM"], 4), "ds_write_b32": ("STORE", "SHARED", FLAG["MEM"], 4),
+}
+
+
 def op_info(mnemonic: str):
-    if mnemonic not in SASS:
+    table = SASS if mnemonic in SASS else CDNA
+    if mnemonic not in table:
         raise KeyError(f"generator does not know opcode {mnemonic!r}")
-    c, s, f, w = SASS[mnemonic]
+    c, s, f, w = table[mnemonic]
     return OC[c], SPACE[s], f, w
 
 

@@ -98,7 +98,7 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
             applied[k] = v
         cfg[k] = v
     out = os.path.join(out_root, name or device)
-    presets.write_config(cfg, out)
+    presets.write_config(cfg, out, power_preset=base)
     with open(os.path.join(out, "TUNING.md"), "w") as f:
         f.write(f"# Tuned configuration for {device}\n\nBase preset: {base}\n\n")
         f.write("| option | tuned value | preset value |\n|---|---|---|\n")
