@@ -138,12 +138,12 @@ def simulate_power(work: str, xml: str, kernels: Dict[str, KernelBuilder]) -> Di
     return res
 
 
-def run(work: str, out_xml: str) -> Dict:
+def run(work: str, out_xml: str, iters: int = 48) -> Dict:
     base_xml = os.path.join(TUNED, "accelwattch_sass_sim.xml")
     if not os.path.exists(base_xml):
         xmlcfg.write_xml(base_xml, xmlcfg.default_params("MI355X"))
     meas = measured_power()
-    ks = stress_kernels()
+    ks = stress_kernels(iters)
     sim = simulate_power(work, base_xml, ks)
     names = [n for n in ks if n in meas]
     A = calibrate.design_matrix([sim[n]["report"] for n in names])

@@ -105,6 +105,27 @@ def test_calibration_recovers_factors():
     assert xc[a0] <= xc[a1] + 1e-6
 
 
+def test_grouped_fit_shares_factors():
+    rng = np.random.default_rng(3)
+    A = rng.uniform(0, 10, (12, len(report.COMPONENTS)))
+    x_true = calibrate.group_matrix()[1].T @ np.array([1.2, 0.8, 1.5, 0.6, 2.0])
+    x_true[x_true == 0] = 1.0
+    b = A @ x_true
+    x = calibrate.fit_groups(A, b, lower=0.05, upper=50)
+    assert np.allclose(A @ x, b, rtol=1e-6)
+
+
+def test_mi355x_power_validation_pipeline(native, tmp_path):
+    """Synthetic CDNA traces of the ub_power kernels -> simulated component
+    power -> grouped QP fit against the amd-smi measurements."""
+    from accel_sim_framework_distributed_amd.power import mi355x_validation as v
+    s = v.run(str(tmp_path / "w"), str(tmp_path / "cal.xml"), iters=6)
+    assert set(s["kernels"]) == {"idle", "fp32_fma", "int32_mad", "fp64_fma", "sfu_sqrt_exp", "mfma_bf16",
+                                 "lds_read", "hbm_read"}
+    assert s["mape_in_sample"] <= s["mape_uncalibrated"] + 1e-9
+    assert os.path.exists(tmp_path / "cal.xml") and xmlcfg.read_xml(str(tmp_path / "cal.xml"))["constant_power"] > 0
+
+
 def test_apply_factors_rescales_xml(tmp_path):
     src = str(tmp_path / "in.xml")
     xmlcfg.write_xml(src, xmlcfg.default_params("MI355X"))
