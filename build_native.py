@@ -32,6 +32,7 @@ CORE_SRC = [
     "csrc/engine/cpu_engine.cc",
     "csrc/power/power.cc",
     "csrc/driver/simulator.cc",
+    "csrc/driver/dump.cc",
     "csrc/parallel/linksim.cc",
 ]
 HIP_SRC = ["csrc/engine/gpu_engine.hip"]

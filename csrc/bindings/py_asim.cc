@@ -331,6 +331,8 @@ PYBIND11_MODULE(_asim, m) {
       .def("collective_cycles",
            [](Simulator& s, const std::string& line) { return s.collective_cycles(parse_collective_line(line)); })
       .def("link_params", [](Simulator& s) { return link_dict(s.link_params()); })
+      .def("dump_pipeline", &Simulator::dump_pipeline, py::arg("sm") = -1, py::arg("channel") = -1,
+           "pipeline state of an SM / memory channel (-1: all busy SMs / all channels, -2: none)")
       .def_property_readonly("core_period_ps", &Simulator::core_period_ps)
       .def("set_collective_hook",
            [](Simulator& s, py::function f) {

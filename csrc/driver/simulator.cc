@@ -390,6 +390,9 @@ void Simulator::do_kernel(const Command& c) {
     deadlock_ = true;
     print("GPGPU-Sim uArch: ERROR ** deadlock detected: last writeback core %u @ gpu_sim_cycle %llu (+ gpu_tot_sim_cycle %llu)\n",
           0u, (unsigned long long)r.cycles, (unsigned long long)start);
+    // what every stuck unit is waiting for (reference prints the pipeline in debug mode)
+    const std::string d = dump_pipeline(-1, -1);
+    print("%s", d.substr(0, 60000).c_str());
   }
 }
 

@@ -79,6 +79,9 @@ class Simulator {
   LinkParams link_params() const;
   // simulated core clock period in picoseconds
   double core_period_ps() const { return (double)cfg_.per_core / 1000.0; }
+  // pipeline dump of SM `sm` / channel `ch` (-1: every busy SM / every channel,
+  // -2: none), decoded from the engine state image (reference dump_pipeline)
+  std::string dump_pipeline(int sm, int ch);
 
  private:
   void print(const char* fmt, ...);

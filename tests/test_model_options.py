@@ -80,6 +80,19 @@ def test_memlatency_and_visualizer(native, traces, tmp_path, monkeypatch):
     log = open(tmp_path / "gpgpusim_visualizer.log").read().splitlines()
     assert len(log) > 3 and all(l.startswith("kernel=") for l in log)
     assert sum(int(l.split(" insn=")[1].split()[0]) for l in log) == s.tot_insn
+    from accel_sim_framework_distributed_amd.plotting import visualizer
+    rows = visualizer.parse(str(tmp_path / "gpgpusim_visualizer.log"))
+    assert len(rows) == len(log) and len(rows[-1]["sm_insn"]) == 80
+    assert "<svg" in visualizer.render(rows)
+
+
+def test_pipeline_dump(native, traces):
+    s = native.Simulator(presets.args_for("QV100", {"-gpgpu_max_cycle": "9000"}) + ["-trace", traces["bfs"]], False)
+    s.run()
+    d = s.dump_pipeline(-1, 0)
+    assert "=== SM " in d and "scoreboard" in d and "=== memory channel 0" in d
+    assert "=== memory channel 1" not in d
+    assert s.dump_pipeline(-2, -2) == ""
 
 
 def test_max_cycle_cap_breaks(native, traces):
