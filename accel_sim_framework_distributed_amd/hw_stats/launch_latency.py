@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""Fit the simulator's launch latencies to rocprofv3 kernel durations.
+
+Reference: util/tuner/GPU_Microbenchmark/ubench/system/kernel_lat (kernel
+launch latency vs thread-block count) and the QV100 config's
+``-gpgpu_kernel_launch_latency 5000`` / ``-gpgpu_TB_launch_latency``
+(gpu-sim.cc:746-757, applied as ``kernel_launch_latency + n_blocks *
+TB_launch_latency`` cycles before a kernel issues CTAs).
+
+The correlator's hardware cycles are ``rocprofv3 duration x clock``; an empty
+kernel's duration is therefore exactly the fixed cost the simulated kernel
+must carry.  ``bin/ubench/ub_launch`` launches isolated empty kernels of
+1..16384 workgroups; this script runs it under ``rocprofv3 --kernel-trace``
+(or reads an existing run with ``-i``), fits ``duration = a + b * blocks`` on
+the per-grid medians, and prints the two options in the micro-benchmark
+output format the tuner reads:
+
+    launch_latency.py -o gpurun_out/ubench/launch_rocprof   > gpurun_out/ubench/ub_launch_rocprof.log
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import os
+import subprocess
+import sys
+from collections import defaultdict
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+
+
+def read_durations(run_dir: str, name_sub: str = "ub_empty_kernel") -> Dict[int, List[float]]:
+    """{workgroups: [duration ns, ...]} of the empty-kernel dispatches."""
+    per: Dict[int, List[float]] = defaultdict(list)
+    for f in glob.glob(os.path.join(run_dir, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if name_sub not in row.get("Kernel_Name", ""):
+                    continue
+                try:
+                    gx = int(row["Grid_Size_X"]) // max(1, int(row["Workgroup_Size_X"]))
+                    d = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+                except (KeyError, ValueError, ZeroDivisionError):
+                    continue
+                per[gx].append(float(d))
+    return dict(per)
+
+
+def fit(per: Dict[int, List[float]]) -> Tuple[float, float]:
+    """(a ns, b ns/workgroup) of duration = a + b * workgroups on per-grid medians."""
+    xs = np.array(sorted(per), dtype=np.float64)
+    ys = np.array([np.median(per[int(x)]) for x in xs])
+    if len(xs) < 2:
+        return float(ys[0]) if len(ys) else 0.0, 0.0
+    b, a = np.polyfit(xs, ys, 1)
+    return float(a), float(max(0.0, b))
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("-o", "--out", default=os.path.join(REPO, "gpurun_out", "ubench", "launch_rocprof"))
+    ap.add_argument("-i", "--input", default="", help="existing rocprofv3 output directory (skip the run)")
+    ap.add_argument("--mhz", type=float, default=0.0, help="shader clock (default: read from ub_launch)")
+    ap.add_argument("--exe", default=os.path.join(REPO, "bin", "ubench", "ub_launch"))
+    o = ap.parse_args(argv)
+    run_dir = o.input
+    mhz = o.mhz
+    if not run_dir:
+        run_dir = o.out
+        os.makedirs(run_dir, exist_ok=True)
+        cmd = ["timeout", "-k", "10", "180", "rocprofv3", "--kernel-trace", "--output-format", "csv",
+               "-d", run_dir, "-o", "run", "--", o.exe]
+        env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+        p = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        if p.returncode != 0:
+            print(p.stdout[-2000:], file=sys.stderr)
+            return p.returncode
+        for line in p.stdout.splitlines():
+            if line.startswith("# measured_shader_mhz") and not mhz:
+                mhz = float(line.split()[-1])
+    mhz = mhz or 2400.0
+    per = read_durations(run_dir)
+    if not per:
+        print("launch_latency: no ub_empty_kernel dispatches found", file=sys.stderr)
+        return 1
+    for nb in sorted(per):
+        d = per[nb]
+        print(f"empty kernel {nb:6d} workgroups: median {np.median(d):8.0f} ns  min {min(d):8.0f} ns  (n={len(d)})")
+    a, b = fit(per)
+    print(f"# rocprof_launch_ns {a:.1f}")
+    print(f"# rocprof_per_block_ns {b:.4f}")
+    print(f"-gpgpu_kernel_launch_latency {int(round(a * mhz / 1000.0))}")
+    print(f"-gpgpu_TB_launch_latency {int(round(b * mhz / 1000.0))}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

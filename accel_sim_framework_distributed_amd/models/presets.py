@@ -253,6 +253,10 @@ def _mi355x() -> Dict[str, str]:
         "-gpgpu_adaptive_cache_config": "0",
         "-gpgpu_unified_l1d_size": "0",
         "-gpgpu_cache:dl1": "S:64:128:4,L:T:m:L:L,A:256:8,16:0,32",
+        # instruction cache: 64 KB shared by a CU pair -> 32 KB per CU, modelled
+        # (not perfect) because small kernels pay their cold misses
+        "-gpgpu_perfect_inst_const_cache": "0",
+        "-gpgpu_cache:il1": "N:64:128:4,L:R:f:N:L,S:4:64,4",
         "-gpgpu_l1_latency": "120",
         "-gpgpu_smem_latency": "64",
         "-gpgpu_cache:dl2": "S:128:128:8,L:B:m:L:P,A:192:4,32:0,32",

@@ -202,7 +202,7 @@ def correlate(sim_csv: str, hw: Dict[str, List[Dict[str, List[float]]]], clock_m
         per_cfg = OrderedDict()
         for cfg in configs:
             apps = sim[st.sim_stat].get(cfg, {})
-            app_pts, k_pts = [], []
+            app_pts, app_all, k_pts = [], [], []
             for app, svals in apps.items():
                 if app not in hw or any(b.search(app) for b in bl):
                     continue
@@ -220,11 +220,14 @@ def correlate(sim_csv: str, hw: Dict[str, List[Dict[str, List[float]]]], clock_m
                     if math.isfinite(hv[i]) and hv[i] > st.drop_hw_below:
                         k_pts.append((hv[i], sv[i], f"{app}--{i}"))
                 ha, sa = float(np.nansum(hv)), float(np.sum(sv))
+                if math.isfinite(ha) and ha > st.drop_hw_below:
+                    app_all.append((ha, sa, app))
                 if math.isfinite(ha) and ha > st.drop_hw_below and not noisy:
                     if abs(sa - ha) / ha * 100 <= err_threshold:
                         app_pts.append((ha, sa, app))
-            per_cfg[cfg] = dict(apps=app_pts, kernels=k_pts,
+            per_cfg[cfg] = dict(apps=app_pts, kernels=k_pts, apps_all=app_all,
                                 app_metrics=error_metrics([p[0] for p in app_pts], [p[1] for p in app_pts]),
+                                app_all_metrics=error_metrics([p[0] for p in app_all], [p[1] for p in app_all]),
                                 kernel_metrics=error_metrics([p[0] for p in k_pts], [p[1] for p in k_pts]))
         result[st.chart_name] = dict(stat=st, configs=per_cfg)
     return result
@@ -242,7 +245,12 @@ def write_outputs(res: Dict, out_dir: str, plotname: str = "correl") -> List[str
             if m.get("n"):
                 body.append(f"<p><b>{cfg}</b>: {m['n']} apps, MAE {m['mae']:.2f}%, aggregate error "
                             f"{m['agg_err']:.2f}%, correl {m['correl']:.4f}, NRMSE {m['nrmse']:.4f}</p>")
-            summary.setdefault(chart, {})[cfg] = dict(app=v["app_metrics"], kernel=v["kernel_metrics"])
+            summary.setdefault(chart, {})[cfg] = dict(
+                app=v["app_metrics"], kernel=v["kernel_metrics"],
+                # every app, including those whose HW runs vary more than -t (the
+                # reference drops those from its headline, plot-correlation.py:66-90)
+                app_incl_noisy=v.get("app_all_metrics", {}),
+                points={a: {"hw": h, "sim": s_} for h, s_, a in v.get("apps_all", [])})
         body.append(svg.scatter(series, f"{chart}: simulation vs hardware (per app)", f"hardware {chart}",
                                 f"simulated {chart}", log=st.log))
         kseries = {cfg: v["kernels"] for cfg, v in d["configs"].items()}

@@ -52,7 +52,7 @@ def parse_stats(paths: List[str]) -> Tuple[Dict[str, str], Dict[str, str], str]:
                 opts[m.group(1)] = m.group(2)
                 continue
             d = _DEV.match(line)
-            if d:
+            if d and d.group(1).strip():
                 device = d.group(1).strip().replace(" ", "_")
                 continue
             if line.startswith("# "):

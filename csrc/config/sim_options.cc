@@ -467,7 +467,7 @@ void register_sim_options(OptionRegistry& r) {
   }
 }
 
-CacheGeom parse_cache_geom(const std::string& s0) {
+CacheGeom parse_cache_geom(const std::string& s0, bool any_line) {
   CacheGeom g{};
   std::string s = strip_ws(s0);
   if (s == "none" || s.empty()) {
@@ -522,6 +522,11 @@ CacheGeom parse_cache_geom(const std::string& s0) {
   g.mshr_entries = mshr ? mshr : 1;
   g.mshr_merge = merge ? merge : 1;
   g.miss_queue = mq;
+  if (any_line && g.line != 128 && g.line >= 16 && g.line <= 128 && !(g.line & (g.line - 1))) {
+    // read-only caches of smaller lines: same capacity in 128 B lines
+    g.nsets = std::max<uint32_t>(1, g.nsets * g.line / 128);
+    g.line = 128;
+  }
   if (g.line != 128) throw OptionError("only 128-byte cache lines are supported: " + s0);
   if (g.nsets & (g.nsets - 1)) throw OptionError("cache set count must be a power of two: " + s0);
   return g;
@@ -629,6 +634,15 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.adaptive_l1 = r.getb("-gpgpu_adaptive_cache_config") ? 1 : 0;
   c.unified_l1_kb = (uint32_t)r.getu("-gpgpu_unified_l1d_size");
   c.l1_write_ratio = (uint32_t)r.getu("-gpgpu_l1_cache_write_ratio");
+  c.perfect_icache = r.getb("-gpgpu_perfect_inst_const_cache") ? 1u : 0u;
+  c.il1 = parse_cache_geom(r.gets("-gpgpu_cache:il1"), true);
+  if (!c.il1.disabled) {
+    // the tag array lives in LDS next to the SM state: keep the associativity,
+    // cap the set count (kernels' code rarely exceeds 64 KB)
+    while ((uint64_t)c.il1.nsets * c.il1.assoc > (uint64_t)kMaxIL1Lines && c.il1.nsets > 1) c.il1.nsets >>= 1;
+    if ((uint64_t)c.il1.nsets * c.il1.assoc > (uint64_t)kMaxIL1Lines) c.il1.assoc = kMaxIL1Lines;
+    c.il1.mshr_entries = std::min<uint32_t>(std::max<uint32_t>(1, c.il1.mshr_entries), kMaxIL1Mshr);
+  }
   {
     auto v = split(strip_ws(r.gets("-gpgpu_shmem_option")), ',');
     for (auto& x : v) {
@@ -675,6 +689,22 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
     c.dram_ret_queue = (rq <= 0 || rq > kDramRet) ? (uint32_t)kDramRet : (uint32_t)rq;
   }
   parse_dram_timing(c, r.gets("-gpgpu_dram_timing_opt"));
+  c.rw_turnaround = r.getb("-dram_elimnate_rw_turnaround") ? 0u : 1u;
+  c.wq_enable = r.getb("-dram_seperate_write_queue_enable") ? 1u : 0u;
+  {
+    auto v = split(strip_ws(r.gets("-dram_write_queue_size")), ':');
+    if (v.size() != 3) throw OptionError("-dram_write_queue_size expects <size>:<high>:<low>");
+    c.wq_size = parse_u(v[0], "-dram_write_queue_size");
+    c.wq_hi = parse_u(v[1], "-dram_write_queue_size");
+    c.wq_lo = parse_u(v[2], "-dram_write_queue_size");
+    if (c.wq_enable) {
+      // reads and writes share the kDramQ-entry pool
+      c.wq_size = std::max<uint32_t>(1, std::min<uint32_t>(c.wq_size, kDramQ / 2));
+      c.dram_queue = std::min<uint32_t>(c.dram_queue, (uint32_t)kDramQ - c.wq_size);
+      c.wq_hi = std::min(c.wq_hi, c.wq_size);
+      c.wq_lo = std::min(c.wq_lo, c.wq_hi);
+    }
+  }
   c.BL = (uint32_t)r.getu("-gpgpu_dram_burst_length");
   c.busW = (uint32_t)r.getu("-gpgpu_dram_buswidth");
   c.data_cmd_ratio = std::max<uint32_t>(1, (uint32_t)r.getu("-dram_data_command_freq_ratio"));

@@ -22,7 +22,7 @@ void register_sim_options(OptionRegistry& r);
 SimCfg derive_sim_cfg(const OptionRegistry& r);
 
 // cache geometry string  <S|N>:<sets>:<line>:<assoc>,<rep>:<wr>:<alloc>:<wr_alloc>:<idx>,<mshr>:<N>:<merge>,<mq>[:...]
-CacheGeom parse_cache_geom(const std::string& s);
+CacheGeom parse_cache_geom(const std::string& s, bool any_line = false);
 
 struct KernelShape {
   uint32_t threads_per_cta;

@@ -89,7 +89,20 @@ std::string dump_chan_state(const ChanState& ch, const SimCfg& c) {
     for (uint32_t i = 0; i < (uint32_t)kMaxL2Mshr; ++i) mshrs += sp.mshr[i].valid ? 1 : 0;
     o << "  sub-partition " << j << ": icnt->L2 " << sp.inq_n << ", ROP " << sp.rop_n << ", replies " << sp.rep_n
       << ", DRAM->L2 " << sp.fill_n << ", waiting requests " << sp.n_wait << ", L2 MSHRs " << mshrs
-      << ", to DRAM " << sp.n_l2dram << "\n";
+      << ", to DRAM " << sp.n_l2dram << ", input backlog " << sp.ovf_n << "\n";
+    for (uint32_t k = 0; k < sp.rop_n && k < 4; ++k) {
+      const Pkt& p = sp.rop[(sp.rop_head + k) % kRopQ];
+      o << "    ROP[" << k << "] type " << (int)p.type << " line 0x" << std::hex << p.addr << std::dec
+        << " sectors " << (int)p.sectors << " from SM " << p.src << " ready " << p.t / c.per_l2 << "\n";
+    }
+    uint32_t shown = 0;
+    for (uint32_t k = 0; k < sp.n_wait && shown < 4; ++k) {
+      const L2Wait& e = sp.wait[k];
+      if (!e.valid) continue;
+      o << "    waiter line 0x" << std::hex << e.line << std::dec << " need " << (int)e.need << " type "
+        << (int)e.type << " for SM " << e.src << "\n";
+      ++shown;
+    }
   }
   for (uint32_t b = 0; b < c.nbk && b < (uint32_t)kMaxBanksDram; ++b)
     if (ch.bk[b].open) o << "  bank " << b << " open row " << ch.bk[b].row << "\n";
@@ -109,7 +122,14 @@ std::string Simulator::dump_pipeline(int sm, int ch) {
     }
   for (uint32_t i = 0; i < cfg_.n_mem; ++i)
     if (ch == -1 || (ch >= 0 && (uint32_t)ch == i)) {
-      out += dump_chan_state(chs[i], cfg_);
+      const ChanState& cs = chs[i];
+      bool busy = cs.lat_n || cs.q_n || cs.ret_n;
+      for (uint32_t j = 0; j < cfg_.n_sub_per_mem && j < (uint32_t)kMaxSubPerCh; ++j) {
+        const SubPart& sp = cs.sp[j];
+        busy = busy || sp.inq_n || sp.rop_n || sp.rep_n || sp.fill_n || sp.n_wait || sp.n_l2dram;
+      }
+      if (ch == -1 && !busy) continue;  // skip idle channels in "all"
+      out += dump_chan_state(cs, cfg_);
     }
   return out;
 }

@@ -71,7 +71,16 @@ void Simulator::print(const char* fmt, ...) {
   int n = vsnprintf(buf, sizeof(buf), fmt, ap);
   va_end(ap);
   if (n < 0) return;
-  std::string s(buf, std::min<size_t>((size_t)n, sizeof(buf) - 1));
+  std::string s;
+  if ((size_t)n < sizeof(buf)) {
+    s.assign(buf, (size_t)n);
+  } else {  // long message (pipeline dumps): format again into a sized buffer
+    s.resize((size_t)n + 1);
+    va_start(ap, fmt);
+    vsnprintf(&s[0], s.size(), fmt, ap);
+    va_end(ap);
+    s.resize((size_t)n);
+  }
   out_ += s;
   if (echo_) {
     fputs(s.c_str(), stdout);
@@ -390,9 +399,11 @@ void Simulator::do_kernel(const Command& c) {
     deadlock_ = true;
     print("GPGPU-Sim uArch: ERROR ** deadlock detected: last writeback core %u @ gpu_sim_cycle %llu (+ gpu_tot_sim_cycle %llu)\n",
           0u, (unsigned long long)r.cycles, (unsigned long long)start);
-    // what every stuck unit is waiting for (reference prints the pipeline in debug mode)
-    const std::string d = dump_pipeline(-1, -1);
-    print("%s", d.substr(0, 60000).c_str());
+    // what every stuck unit is waiting for (reference prints the pipeline in
+    // debug mode): busy memory channels first, then the SMs
+    std::string d = dump_pipeline(-2, -1) + dump_pipeline(-1, -2);
+    if (d.size() > 60000) d = d.substr(0, 60000) + "\n... (truncated)\n";
+    print("%s", d.c_str());
   }
 }
 
@@ -611,6 +622,18 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   for (int t = 0; t < L1T_COUNT; ++t)
     print("\tTotal_core_cache_fail_stats_breakdown[%s][MSHR_ENRTY_FAIL] = %llu\n", l1t[t],
           (unsigned long long)l1[t][L1O_RES_FAIL]);
+  {
+    // instruction cache, cumulative over the run (reference shader.cc:3051-3074)
+    uint64_t ic[4] = {};
+    for (auto& st : prev_sm_)
+      for (int i = 0; i < 4; ++i) ic[i] += st.il1[i];
+    const uint64_t acc = ic[IL1_HIT] + ic[IL1_MISS] + ic[IL1_MSHR_HIT];
+    print("\tL1I_total_cache_accesses = %llu\n", (unsigned long long)acc);
+    print("\tL1I_total_cache_misses = %llu\n", (unsigned long long)ic[IL1_MISS]);
+    if (acc) print("\tL1I_total_cache_miss_rate = %.4lf\n", (double)ic[IL1_MISS] / (double)acc);
+    print("\tL1I_total_cache_pending_hits = %llu\n", (unsigned long long)ic[IL1_MSHR_HIT]);
+    print("\tL1I_total_cache_reservation_fails = %llu\n", (unsigned long long)ic[IL1_RES_FAIL]);
+  }
   print("gpgpu_n_shmem_bank_access = %llu\n", (unsigned long long)shm);
   print("gpgpu_n_shmem_bkconflict = %llu\n", (unsigned long long)shm_conf);
   static const char* l2t[L2T_COUNT] = {"GLOBAL_ACC_R", "GLOBAL_ACC_W", "GLOBAL_ATOMIC"};
@@ -639,6 +662,16 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   for (auto& s : sm) {
     pk_out += s.pkts_out;
     pk_in += s.pkts_in;
+  }
+  {
+    uint64_t bl = 0, drop = 0;
+    for (auto& m : mem) {
+      bl += m.icnt_backlog;
+      drop += m.icnt_ovf_drop;
+    }
+    print("icnt_mem_input_backlog = %llu\n", (unsigned long long)bl);
+    if (drop) print("GPGPU-Sim uArch: WARNING ** %llu interconnect packets lost to a full backlog ring\n",
+                    (unsigned long long)drop);
   }
   print("icnt_total_pkts_mem_to_simt = %llu\n", (unsigned long long)pk_in);
   print("icnt_total_pkts_simt_to_mem = %llu\n", (unsigned long long)pk_out);

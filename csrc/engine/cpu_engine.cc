@@ -61,7 +61,7 @@ void check_state_header(const EngineStateHeader& h, const EngineStateHeader& w) 
   if (h.magic != w.magic || h.version != w.version) throw std::runtime_error("engine state: not a state image");
   if (h.n_sm != w.n_sm || h.n_mem != w.n_mem || h.sm_bytes != w.sm_bytes || h.ch_bytes != w.ch_bytes ||
       h.pub_bytes != w.pub_bytes || h.box_req != w.box_req || h.cnt_req != w.cnt_req || h.box_rep != w.box_rep ||
-      h.cnt_rep != w.cnt_rep)
+      h.cnt_rep != w.cnt_rep || h.ovf != w.ovf)
     throw std::runtime_error("engine state: image was written for a different configuration or build");
 }
 
@@ -96,6 +96,8 @@ class CpuEngine : public Engine {
       box_rep_[p].assign((size_t)c.n_sm * c.n_subpart * cap_rep_, Pkt{});
       cnt_rep_[p].assign((size_t)c.n_sm * c.n_subpart, 0);
     }
+    ovf_cap_ = backlog_cap(c);
+    ovf_.assign((size_t)c.n_subpart * ovf_cap_, Pkt{});
     epoch_ = 0;
     cycle_ = 0;
     if (c_.trace_mask) {
@@ -238,6 +240,7 @@ class CpuEngine : public Engine {
     h.cnt_req = cnt_req_[0].size();
     h.box_rep = box_rep_[0].size();
     h.cnt_rep = cnt_rep_[0].size();
+    h.ovf = ovf_.size();
     h.cycle = cycle_;
     h.epoch = epoch_;
     h.ready = ready_;
@@ -258,6 +261,7 @@ class CpuEngine : public Engine {
       o.put(box_rep_[p].data(), box_rep_[p].size() * sizeof(Pkt));
       o.put(cnt_rep_[p].data(), cnt_rep_[p].size() * sizeof(uint32_t));
     }
+    o.put(ovf_.data(), ovf_.size() * sizeof(Pkt));
   }
 
   void load_state(const std::vector<uint8_t>& in) override {
@@ -274,6 +278,7 @@ class CpuEngine : public Engine {
       r.get(box_rep_[p].data(), box_rep_[p].size() * sizeof(Pkt));
       r.get(cnt_rep_[p].data(), cnt_rep_[p].size() * sizeof(uint32_t));
     }
+    r.get(ovf_.data(), ovf_.size() * sizeof(Pkt));
     cycle_ = h.cycle;
     epoch_ = h.epoch;
     ready_ = h.ready;
@@ -299,6 +304,8 @@ class CpuEngine : public Engine {
     m.out_cap = cap_rep_;
     m.n_src_sub = c_.n_subpart;
     m.win_end = t1 * c_.per_core;
+    m.ovf = ovf_.data();
+    m.ovf_cap = ovf_cap_;
     return m;
   }
 
@@ -309,6 +316,8 @@ class CpuEngine : public Engine {
   std::vector<Pkt> box_req_[2], box_rep_[2];
   std::vector<uint32_t> cnt_req_[2], cnt_rep_[2];
   uint32_t cap_req_ = 0, cap_rep_ = 0;
+  std::vector<Pkt> ovf_;  // arrival backlog rings [n_subpart][ovf_cap_]
+  uint32_t ovf_cap_ = 0;
   uint64_t epoch_ = 0, cycle_ = 0;
   const ReadyKernel* kern_ = nullptr;
   KernelDesc kd_{};

@@ -61,11 +61,21 @@ class Engine {
 // layout of save_state(): header, then SMState[n_sm], ChanState[n_mem],
 // EpochPub, and for parity 0/1: req packets, req counts, reply packets,
 // reply counts
+// capacity of each sub-partition's arrival backlog ring (packets): every SM
+// can have at most icnt_out_limit packets in flight, so n_sm of them bound
+// what one destination can ever hold back; capped to keep MI355X-sized
+// configurations at a few MB per sub-partition
+inline uint32_t backlog_cap(const SimCfg& c) {
+  uint64_t b = (uint64_t)c.n_sm * c.icnt_out_limit;
+  return (uint32_t)(b < 16384 ? b : 16384);
+}
+
 struct EngineStateHeader {
   uint64_t magic = 0x41534d5354415445ull;  // "ASMSTATE"
-  uint64_t version = 1;
+  uint64_t version = 2;
   uint64_t n_sm = 0, n_mem = 0, sm_bytes = 0, ch_bytes = 0, pub_bytes = 0;
   uint64_t box_req = 0, cnt_req = 0, box_rep = 0, cnt_rep = 0;  // element counts per parity
+  uint64_t ovf = 0;                                              // arrival backlog packets (all sub-partitions)
   uint64_t cycle = 0, epoch = 0, ready = 0;
 };
 

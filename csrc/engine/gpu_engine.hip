@@ -59,6 +59,8 @@ struct GpuArgs {
   Pkt* box_rep[2];
   uint32_t* cnt_rep[2];
   uint32_t cap_req, cap_rep;
+  Pkt* ovf;
+  uint32_t ovf_cap;
   uint64_t epoch0;
   uint64_t cycle0;
   uint64_t ready_cycle;
@@ -185,6 +187,8 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   mx.cfg = &c;
   mx.out_cap = a.cap_rep;
   mx.n_src_sub = c.n_subpart;
+  mx.ovf = a.ovf;
+  mx.ovf_cap = a.ovf_cap;
   if (is_sm && a.init_kernel) {
     sx.outbox = a.box_req[0];
     sx.outcnt = a.cnt_req[0];
@@ -347,6 +351,8 @@ class GpuEngine : public Engine {
       HIPCHECK(hipMalloc(&d_cnt_rep_[p], sizeof(uint32_t) * c.n_sm * c.n_subpart));
       HIPCHECK(hipMemset(d_cnt_rep_[p], 0, sizeof(uint32_t) * c.n_sm * c.n_subpart));
     }
+    ovf_cap_ = backlog_cap(c);
+    HIPCHECK(hipMalloc(&d_ovf_, sizeof(Pkt) * c.n_subpart * (size_t)ovf_cap_));
     HIPCHECK(hipMalloc(&d_ctl_, sizeof(GpuCtl)));
     HIPCHECK(hipHostMalloc(&h_ctl_, sizeof(GpuCtl)));
     epoch_ = 0;
@@ -385,6 +391,8 @@ class GpuEngine : public Engine {
       }
       a.cap_req = cap_req_;
       a.cap_rep = cap_rep_;
+      a.ovf = d_ovf_;
+      a.ovf_cap = ovf_cap_;
       a.epoch0 = epoch_;
       a.cycle0 = cycle_;
       a.ready_cycle = ready;
@@ -506,6 +514,7 @@ class GpuEngine : public Engine {
     h.cnt_req = (uint64_t)c_.n_subpart * c_.n_sm;
     h.box_rep = (uint64_t)c_.n_sm * c_.n_subpart * cap_rep_;
     h.cnt_rep = (uint64_t)c_.n_sm * c_.n_subpart;
+    h.ovf = (uint64_t)c_.n_subpart * ovf_cap_;
     h.cycle = cycle_;
     h.epoch = epoch_;
     h.ready = ready_;
@@ -529,6 +538,7 @@ class GpuEngine : public Engine {
       dl(d_box_rep_[p], h.box_rep * sizeof(Pkt));
       dl(d_cnt_rep_[p], h.cnt_rep * sizeof(uint32_t));
     }
+    dl(d_ovf_, h.ovf * sizeof(Pkt));
   }
   void load_state(const std::vector<uint8_t>& in) override {
     StateIn r{in};
@@ -548,6 +558,7 @@ class GpuEngine : public Engine {
       ul(d_box_rep_[p], w.box_rep * sizeof(Pkt));
       ul(d_cnt_rep_[p], w.cnt_rep * sizeof(uint32_t));
     }
+    ul(d_ovf_, w.ovf * sizeof(Pkt));
     cycle_ = h.cycle;
     epoch_ = h.epoch;
     ready_ = h.ready;
@@ -577,6 +588,7 @@ class GpuEngine : public Engine {
       fr(d_cnt_rep_[p]);
     }
     fr(d_ctl_);
+    fr(d_ovf_);
     fr(d_trace_ev_);
     fr(d_trace_cnt_);
     fr(d_insts_);
@@ -595,6 +607,8 @@ class GpuEngine : public Engine {
   SMState* d_sms_ = nullptr;
   ChanState* d_chs_ = nullptr;
   EpochPub* d_pub_ = nullptr;
+  Pkt* d_ovf_ = nullptr;  // arrival backlog rings [n_subpart][ovf_cap_]
+  uint32_t ovf_cap_ = 0;
   Pkt* d_box_req_[2] = {nullptr, nullptr};
   uint32_t* d_cnt_req_[2] = {nullptr, nullptr};
   Pkt* d_box_rep_[2] = {nullptr, nullptr};

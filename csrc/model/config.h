@@ -22,6 +22,9 @@ constexpr int kWbRing = 512;        // writeback ring (max FU latency 511)
 constexpr int kWbSlot = 8;          // writebacks per cycle (EX_WB width cap)
 constexpr int kMaxL1Lines = 1024;   // 128 KB of 128 B lines
 constexpr int kMaxL1Mshr = 256;
+constexpr int kMaxIL1Lines = 512;  // instruction cache: 64 KB of 128 B lines
+constexpr int kMaxIL1Mshr = 16;
+constexpr uint64_t kProgramMemStart = 0xF0000000ull;  // code address base (reference PROGRAM_MEM_START)
 constexpr int kMaxPend = 1024;      // outstanding (warp,load-slot,line) L1 waiters
 constexpr int kLoadSlots = 8;       // in-flight load instructions per warp
 constexpr int kHitRing = 256;       // L1 / shared-memory completion ring (latency < 222)
@@ -140,6 +143,10 @@ struct SimCfg {
   uint32_t n_shmem_opts;
   uint32_t shmem_opts_kb[8];
   uint32_t l1_write_ratio;
+  // ---- instruction cache (reference m_L1I read_only_cache, shader.cc:918-1020;
+  //      -gpgpu_perfect_inst_const_cache bypasses it, shader.cc:990) ----
+  CacheGeom il1;
+  uint32_t perfect_icache;
   // ---- interconnect ----
   uint32_t icnt_latency;   // core cycles (== epoch length, the PDES lookahead)
   uint32_t flit_size;
@@ -157,6 +164,9 @@ struct SimCfg {
   uint32_t nbk, nbkgrp, tCCD, tRRD, tRCD, tRAS, tRP, tRC, CL, WL, tCDLR, tWR, tCCDL, tRTPL;
   uint32_t BL, busW, data_cmd_ratio, dual_bus, bk_index_policy, bkgrp_index_policy;
   uint32_t atom_size;       // bytes per DRAM column access
+  uint32_t rw_turnaround;   // 0: -dram_elimnate_rw_turnaround (tWTR = tRTW = 0)
+  uint32_t wq_enable;       // -dram_seperate_write_queue_enable
+  uint32_t wq_size, wq_hi, wq_lo;  // -dram_write_queue_size <size>:<high>:<low watermark>
   // ---- address decode ----
   uint64_t addr_mask[AF_COUNT];
   uint8_t mk_hi[AF_COUNT];

@@ -153,7 +153,10 @@ template <class P>
 SIM_HDI void chan_epoch(ChanState& ch, const MemCtx& x, const Pkt* inbox, const uint32_t* incnt,
                         uint32_t in_cap, uint64_t t0_fs) {
   P::prof(20);
-  mem_gather<P>(ch, *x.cfg, inbox, incnt, in_cap, t0_fs);
+  mem_gather<P>(ch, *x.cfg, x, inbox, incnt, in_cap, t0_fs);
+  P::one([&] {
+    for (uint32_t j = 0; j < x.cfg->n_sub_per_mem; ++j) ch.sp[j].st.icnt_backlog += ch.sp[j].ovf_n;
+  });
   P::prof(24);
   mem_window<P>(ch, x);
   P::prof(25);

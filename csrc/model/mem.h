@@ -87,6 +87,8 @@ struct MemStats {
   uint64_t bytes_out;
   uint64_t l2_evict_dirty;
   uint64_t icnt_stall;
+  uint64_t icnt_backlog;       // arrivals that waited in the input backlog (sum over epochs of its length)
+  uint64_t icnt_ovf_drop;      // arrivals lost to a full backlog ring (must stay 0)
 };
 
 struct SubPart {
@@ -102,6 +104,7 @@ struct SubPart {
   uint32_t l2_stamp;
   uint32_t n_wait;
   uint32_t n_l2dram;   // requests of this sub in the L2->DRAM path
+  uint32_t ovf_head, ovf_n;  // arrival backlog ring (MemCtx::ovf) for arrivals that did not fit in inq
   uint32_t pad;
   L2Line l2[kMaxL2Lines];
   L2Mshr mshr[kMaxL2Mshr];
@@ -121,7 +124,9 @@ struct alignas(16) ChanState {
   uint32_t lat_head, lat_n;
   DramReq q[kDramQ];    // scheduler queue (pool; age order via q_age)
   uint32_t q_n;
-  uint32_t pad1;
+  uint16_t qw_n;        // writes among them (separate write queue accounting)
+  uint8_t wmode;        // write-drain mode of the separate write queue
+  uint8_t pad1;
   DramBank bk[kMaxBanksDram];
   uint64_t t_rrd_ok, t_ccd_ok, t_rd_ok, t_wr_ok, bus_free;
   uint64_t t_ccdl_ok[8];
@@ -133,7 +138,7 @@ struct alignas(16) ChanState {
   uint16_t ocnt[kMaxSubPerCh][kMaxSmTot];  // replies put in each (dst SM) cell this epoch
   uint64_t skey[kMemInQ];                  // gather scratch: sort keys
   uint32_t sref[kMemInQ];                  // gather scratch: (src << 16 | k)
-  uint32_t srank[kMemInQ];
+  uint32_t srank[kMemInQ > kMaxSmTot ? kMemInQ : kMaxSmTot];  // gather scratch: ranks / per-source offsets
   SubPart sp[kMaxSubPerCh];
 };
 
@@ -147,6 +152,8 @@ struct MemCtx {
   uint32_t out_cap;
   uint32_t n_src_sub;   // row stride (number of sub-partitions)
   uint64_t win_end;     // fs, exclusive
+  Pkt* ovf;             // per-sub-partition arrival backlog rings [n_subpart][ovf_cap] (global memory)
+  uint32_t ovf_cap;
 };
 
 // ---------------------------------------------------------------------------
@@ -494,9 +501,13 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
   st.dram_cycles++;
   const uint32_t qcap = amin<uint32_t>(c.dram_queue ? c.dram_queue : 1, kDramQ);
   // latency pipe -> scheduler queue
-  while (ch.lat_n && ch.q_n < qcap) {
+  while (ch.lat_n) {
     const DramReq& h = ch.lat[ch.lat_head];
     if (h.ready > now_fs) break;
+    // reads and writes have their own capacity with a separate write queue
+    // (reference dram_t::full, dram.cc:160-175)
+    if (c.wq_enable ? (h.write ? ch.qw_n >= c.wq_size : ch.q_n - ch.qw_n >= qcap) : ch.q_n >= qcap) break;
+    ch.qw_n += h.write ? 1 : 0;
     int f = P::argmin(kDramQ, [&](int i) -> uint64_t { return ch.q_valid[i] ? ~0ull : (uint64_t)i; });
     ch.q[f] = h;
     ch.q_valid[f] = 1;
@@ -541,13 +552,25 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
     st.dram_busy_cycles += burst;
     ch.q_valid[o] = 0;
     ch.q_n--;
+    ch.qw_n -= r.write ? 1 : 0;
     ch.sp[r.sub].n_l2dram--;
     return;
+  }
+  // separate write queue: serve reads until the writes reach the high
+  // watermark, then drain writes down to the low watermark (reference
+  // frfcfs_scheduler::schedule, dram_sched.cc:118-130).  With no read queued
+  // at all the writes are served too, so a kernel's tail cannot strand them.
+  uint32_t only = 2;  // 0 reads only, 1 writes only, 2 both
+  if (c.wq_enable) {
+    if (!ch.wmode && ch.qw_n >= c.wq_hi) ch.wmode = 1;
+    else if (ch.wmode && ch.qw_n < c.wq_lo) ch.wmode = 0;
+    only = ch.wmode ? 1u : (ch.q_n > ch.qw_n ? 0u : 1u);
   }
   // banks that have a queued row hit
   uint64_t hitmask = P::vor(kDramQ, [&](int i) -> uint64_t {
     if (!ch.q_valid[i]) return 0;
     const DramReq& r = ch.q[i];
+    if (only != 2 && r.write != only) return 0;  // requests of the idle queue do not hold rows open
     const DramBank& b = ch.bk[r.bank];
     return (b.open && b.row == r.row) ? (1ull << r.bank) : 0ull;
   });
@@ -555,7 +578,9 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
   bool col = false;
   uint64_t oldest_age = ~0ull;
   if (c.dram_sched == 0) {  // FIFO: only the oldest request may issue (column and row commands)
-    int o = P::argmin(kDramQ, [&](int i) -> uint64_t { return ch.q_valid[i] ? ch.q_age[i] : ~0ull; });
+    int o = P::argmin(kDramQ, [&](int i) -> uint64_t {
+      return (ch.q_valid[i] && (only == 2 || ch.q[i].write == only)) ? ch.q_age[i] : ~0ull;
+    });
     oldest_age = o >= 0 ? ch.q_age[o] : ~0ull;
   }
   {
@@ -563,6 +588,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
       if (!ch.q_valid[i]) return ~0ull;
       if (c.dram_sched == 0 && ch.q_age[i] != oldest_age) return ~0ull;
       const DramReq& r = ch.q[i];
+      if (only != 2 && r.write != only) return ~0ull;
       const DramBank& b = ch.bk[r.bank];
       if (!b.open || b.row != r.row || t < b.t_col_ok || t < ch.t_ccd_ok) return ~0ull;
       if (t < ch.t_ccdl_ok[dram_bkgrp(c, r.bank) & 7]) return ~0ull;
@@ -576,7 +602,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
         P::one([&] { trace_put(c, c.n_sm + ch.id, t, EV_DRAM_CMD, r.write ? 1 : 0, (uint64_t)r.bank << 32 | r.row); });
       if (r.write) {
         b.t_pre_ok = amax<uint64_t>(b.t_pre_ok, t + c.WL + burst + c.tWR);
-        ch.t_rd_ok = amax<uint64_t>(ch.t_rd_ok, t + c.WL + burst + c.tCDLR);
+        if (c.rw_turnaround) ch.t_rd_ok = amax<uint64_t>(ch.t_rd_ok, t + c.WL + burst + c.tCDLR);
         st.dram_wr++;
       } else {
         DramRet& o = ch.ret[(ch.ret_head + ch.ret_n) % kDramRet];
@@ -587,7 +613,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
         ch.ret_n++;
         b.t_pre_ok = amax<uint64_t>(b.t_pre_ok, t + c.tRTPL);
         uint64_t rtw = t + c.CL + burst + 2;
-        ch.t_wr_ok = amax<uint64_t>(ch.t_wr_ok, rtw > c.WL ? rtw - c.WL : 0);
+        if (c.rw_turnaround) ch.t_wr_ok = amax<uint64_t>(ch.t_wr_ok, rtw > c.WL ? rtw - c.WL : 0);
         st.dram_rd++;
       }
       ch.t_ccd_ok = t + amax<uint32_t>(c.tCCD, burst);
@@ -595,6 +621,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
       st.dram_busy_cycles += burst;
       ch.q_valid[pick] = 0;
       ch.q_n--;
+      ch.qw_n -= r.write ? 1 : 0;
       ch.sp[r.sub].n_l2dram--;
       col = true;
     }
@@ -605,6 +632,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
     if (!ch.q_valid[i]) return ~0ull;
     if (c.dram_sched == 0 && ch.q_age[i] != oldest_age) return ~0ull;
     const DramReq& r = ch.q[i];
+    if (only != 2 && r.write != only) return ~0ull;
     const DramBank& b = ch.bk[r.bank];
     if (b.open) {
       // FR-FCFS: precharge a row only when no queued request still hits it
@@ -641,7 +669,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
 }
 
 SIM_HDI bool sub_idle(const SubPart& sp) {
-  return sp.inq_n == 0 && sp.rop_n == 0 && sp.rep_n == 0 && sp.fill_n == 0 && sp.n_wait == 0 && sp.n_l2dram == 0;
+  return sp.inq_n == 0 && sp.ovf_n == 0 && sp.rop_n == 0 && sp.rep_n == 0 && sp.fill_n == 0 && sp.n_wait == 0 && sp.n_l2dram == 0;
 }
 SIM_HDI bool chan_idle(const ChanState& ch, const SimCfg& c) {
   if (ch.lat_n || ch.q_n || ch.ret_n) return false;
@@ -699,56 +727,117 @@ SIM_HDI void mem_window(ChanState& ch, const MemCtx& x) {
 // Gather one epoch of arrivals from the n_src source rows of an outbox cell
 // array ([dst][src][cap], counts [dst][src]) and append them to `q` sorted by
 // (time, source).  Keys are epoch-relative so they fit with the source id.
+//
+// Arrivals that do not fit in `q` are appended, in the same order, to the
+// destination's backlog ring `ovf` (global memory) when one is given; the
+// backlog is older than any new arrival and drains into `q` first on the next
+// gathers.  This is the input buffering of the reference's interconnect
+// (icnt input buffers, local_interconnect.cc:325-358) without a size limit of
+// its own: the senders' outstanding-packet limit bounds it.  Without a
+// backlog (SM side: replies <= outstanding requests <= queue size) nothing
+// can overflow.
+struct Backlog {
+  Pkt* ring;          // nullptr = none
+  uint32_t cap;
+  uint32_t* head;
+  uint32_t* n;
+  uint64_t* drop;     // packets lost because the ring itself was full
+};
+
 template <class P>
 SIM_HDI uint32_t gather_sorted(const Pkt* box, const uint32_t* cnt, uint32_t dst, uint32_t n_src,
                                uint32_t cap, uint64_t t0, Pkt* q, uint32_t qcap, uint32_t& qhead,
                                uint32_t& qn, uint64_t* skey, uint32_t* sref, uint32_t* srank,
-                               uint32_t scap) {
+                               uint32_t scap, const Backlog& bl = Backlog{nullptr, 0, nullptr, nullptr, nullptr}) {
+  // 1. older backlog first (FIFO)
+  if (bl.ring && *bl.n) {
+    const uint32_t m = amin<uint32_t>(*bl.n, qcap - qn);
+    const uint32_t h = *bl.head;
+    P::each((int)m, [&](int i) { q[(qhead + qn + (uint32_t)i) % qcap] = bl.ring[(h + (uint32_t)i) % bl.cap]; });
+    P::sync();
+    qn += m;
+    *bl.head = (h + m) % bl.cap;
+    *bl.n -= m;
+  }
   const uint32_t* row = cnt + (uint64_t)dst * n_src;
   // exclusive scan of the per-source counts -> slot of each packet
-  uint32_t total = P::scan((int)n_src, [&](int s) -> uint32_t { return row[s]; },
-                           [&](int s, uint32_t off) { srank[s] = off; });
+  const uint32_t total = P::scan((int)n_src, [&](int s) -> uint32_t { return row[s]; },
+                                 [&](int s, uint32_t off) { srank[s] = off; });
   P::sync();
   if (total == 0) return 0;
-  if (total > scap) total = scap;  // (capacity sized so this never triggers)
-  P::each((int)n_src, [&](int s) {
-    uint32_t n = row[s], off = srank[s];
-    for (uint32_t k = 0; k < n && off + k < scap; ++k) {
-      const Pkt& p = box[((uint64_t)dst * n_src + s) * cap + k];
-      skey[off + k] = ((p.t - t0) << 16) | (uint64_t)s;
-      sref[off + k] = ((uint32_t)s << 16) | k;
+  const Pkt* cell0 = box + (uint64_t)dst * n_src * cap;
+  const uint32_t room = (bl.ring && *bl.n) ? 0u : qcap - qn;  // a non-empty backlog keeps order
+  const uint32_t n = total < room ? total : room;
+  // place the packet of rank r: queue slot or backlog tail
+  auto place = [&](uint32_t r, const Pkt& p) {
+    if (r < n) {
+      q[(qhead + qn + r) % qcap] = p;
+    } else if (bl.ring) {
+      const uint32_t o = r - n;
+      if (*bl.n + o < bl.cap) bl.ring[(*bl.head + *bl.n + o) % bl.cap] = p;
     }
-  });
-  P::sync();
-  // rank sort (keys are unique: one packet per source per tick)
-  P::each((int)total, [&](int i) {
-    uint64_t k = skey[i];
-    uint32_t r = 0;
-    for (uint32_t j = 0; j < total; ++j) r += skey[j] < k;
-    srank[i] = r;
-  });
-  P::sync();
-  uint32_t room = qcap - qn;
-  uint32_t n = total < room ? total : room;
-  P::each((int)total, [&](int i) {
-    uint32_t r = srank[i];
-    if (r >= n) return;
-    uint32_t s = sref[i] >> 16, k = sref[i] & 0xffff;
-    q[(qhead + qn + r) % qcap] = box[((uint64_t)dst * n_src + s) * cap + k];
-  });
-  P::sync();
+  };
+  if (total <= scap) {
+    P::each((int)n_src, [&](int s) {
+      uint32_t cnt_s = row[s], off = srank[s];
+      for (uint32_t k = 0; k < cnt_s; ++k) {
+        const Pkt& p = cell0[(uint64_t)s * cap + k];
+        skey[off + k] = ((p.t - t0) << 16) | (uint64_t)s;
+        sref[off + k] = ((uint32_t)s << 16) | k;
+      }
+    });
+    P::sync();
+    // rank sort (keys are unique: one packet per source per tick)
+    P::each((int)total, [&](int i) {
+      uint64_t k = skey[i];
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < total; ++j) r += skey[j] < k;
+      srank[i] = r;
+    });
+    P::sync();
+    P::each((int)total, [&](int i) {
+      const uint32_t s = sref[i] >> 16, k = sref[i] & 0xffff;
+      place(srank[i], cell0[(uint64_t)s * cap + k]);
+    });
+    P::sync();
+  } else {
+    // more arrivals than sort scratch (many sources hitting one destination):
+    // rank every packet against the time-ordered source rows directly
+    P::each((int)n_src, [&](int s) {
+      for (uint32_t k = 0; k < row[s]; ++k) {
+        const Pkt& p = cell0[(uint64_t)s * cap + k];
+        const uint64_t key = ((p.t - t0) << 16) | (uint64_t)s;
+        uint32_t r = 0;
+        for (uint32_t s2 = 0; s2 < n_src; ++s2)
+          for (uint32_t k2 = 0; k2 < row[s2]; ++k2) {
+            const uint64_t key2 = ((cell0[(uint64_t)s2 * cap + k2].t - t0) << 16) | (uint64_t)s2;
+            if (key2 >= key) break;  // rows are time ordered
+            ++r;
+          }
+        place(r, p);
+      }
+    });
+    P::sync();
+  }
   qn += n;
+  if (bl.ring && total > n) {
+    const uint32_t extra = total - n, fit = amin<uint32_t>(extra, bl.cap - *bl.n);
+    *bl.n += fit;
+    *bl.drop += extra - fit;
+  }
   return n;
 }
 
 template <class P>
-SIM_HDI void mem_gather(ChanState& ch, const SimCfg& c, const Pkt* box, const uint32_t* cnt,
+SIM_HDI void mem_gather(ChanState& ch, const SimCfg& c, const MemCtx& x, const Pkt* box, const uint32_t* cnt,
                         uint32_t cap, uint64_t t0) {
   for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
     SubPart& sp = ch.sp[j];
     uint32_t gsub = ch.id * c.n_sub_per_mem + j;
+    Backlog bl{x.ovf ? x.ovf + (uint64_t)gsub * x.ovf_cap : nullptr, x.ovf_cap, &sp.ovf_head, &sp.ovf_n,
+               &sp.st.icnt_ovf_drop};
     gather_sorted<P>(box, cnt, gsub, c.n_sm, cap, t0, sp.inq, kMemInQ, sp.inq_head, sp.inq_n, ch.skey,
-                     ch.sref, ch.srank, kMemInQ);
+                     ch.sref, ch.srank, kMemInQ, bl);
   }
 }
 

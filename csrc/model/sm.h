@@ -37,6 +37,7 @@ enum WarpFlags : uint8_t {
   WF_BARRIER = 4,    // waiting at a CTA barrier
   WF_MEMBAR = 8,     // waiting for outstanding stores
   WF_WAITCNT = 16,   // waiting for all outstanding memory (CDNA s_waitcnt)
+  WF_IMISS = 32,     // instruction-cache miss pending (reference imiss_pending)
 };
 
 // hit / shared-memory completion ring entries
@@ -139,7 +140,9 @@ struct SMStats {
   // reference's mem_latency_stat (mem_latency_stat.h:37, -gpgpu_memlatency_stat)
   uint64_t mf_lat_sum, mf_lat_n, mf_lat_max;
   uint64_t mf_lat_hist[16];    // log2 buckets: [2^i, 2^(i+1)) cycles
+  uint64_t il1[4];             // instruction cache: hit, miss, mshr (pending) hit, reservation fail
 };
+enum IL1Out : uint8_t { IL1_HIT = 0, IL1_MISS, IL1_MSHR_HIT, IL1_RES_FAIL };
 
 // per-SM kernel bookkeeping (replicated identically in every SM)
 struct SmKernel {
@@ -202,6 +205,9 @@ struct alignas(16) SMState {
   L1Mshr mshr[kMaxL1Mshr];
   L1Pend pend[kMaxPend];
   uint32_t n_pend;
+  L1Line il1[kMaxIL1Lines];     // instruction cache tags (non-sectored: valid = 0xf)
+  L1Mshr imshr[kMaxIL1Mshr];
+  uint64_t w_iline[kMaxWarps];  // code line a WF_IMISS warp waits for
   uint64_t idoc_mask;     // bit sched*U_COUNT+unit: ID_OC register occupied
   uint32_t oc_mask;       // occupied operand collectors
   uint32_t oc_read_mask;  // collectors still reading operands
@@ -465,6 +471,77 @@ SIM_HDI void l1_fill(SMState& s, const SmCtx& x, uint64_t line, uint8_t sectors,
   while (s.n_pend && !s.pend[s.n_pend - 1].valid) s.n_pend--;
 }
 
+// ---------------------------------------------------------------------------
+// L1 instruction cache (reference read_only_cache m_L1I: fetch probes it with
+// the warp's next PC + PROGRAM_MEM_START, a miss parks the warp in
+// imiss_pending until the line returns from L2, shader.cc:918-1020, 3989)
+template <class P>
+SIM_HDI int il1_find(const SMState& s, const CacheGeom& g, uint32_t set, uint64_t line) {
+  const L1Line* base = &s.il1[set * g.assoc];
+  uint64_t m = P::ballot((int)amin<uint32_t>(g.assoc, 64), [&](int w) { return base[w].valid && base[w].tag == line; });
+  return m ? ffs64(m) : -1;
+}
+
+template <class P>
+SIM_HDI void il1_fill(SMState& s, const SimCfg& c, uint64_t line) {
+  const CacheGeom& g = c.il1;
+  const uint32_t set = cache_set_index(g, line);
+  if (il1_find<P>(s, g, set, line) < 0) {
+    L1Line* base = &s.il1[set * g.assoc];
+    const int v = P::argmin((int)amin<uint32_t>(g.assoc, 64), [&](int w) -> uint64_t {
+      return base[w].valid ? (1ull << 40) | base[w].lru : (uint64_t)w;
+    });
+    base[v].tag = line;
+    base[v].valid = 0xf;
+    base[v].lru = ++s.l1_stamp;
+  }
+  const int mi = P::argmin((int)g.mshr_entries, [&](int i) -> uint64_t {
+    return (s.imshr[i].valid && s.imshr[i].line == line) ? (uint64_t)i : ~0ull;
+  });
+  if (mi >= 0) s.imshr[mi].valid = 0;
+  const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
+  P::each(nw, [&](int w) {
+    if ((s.w_flags[w] & WF_IMISS) && s.w_iline[w] == line) s.w_flags[w] &= (uint8_t)~WF_IMISS;
+  });
+  P::sync();
+}
+
+// probe the instruction cache for warp w's next fetch; true = instructions
+// available this cycle
+template <class P>
+SIM_HDI bool il1_fetch(SMState& s, const SimCfg& c, uint32_t w) {
+  const CacheGeom& g = c.il1;
+  const TInst& in = s.w_win[w][s.w_next[w] % kWin];
+  const uint64_t line = (kProgramMemStart + in.pc) & ~127ull;
+  const uint32_t set = cache_set_index(g, line);
+  const int way = il1_find<P>(s, g, set, line);
+  if (way >= 0) {
+    if (g.repl == REPL_LRU) s.il1[set * g.assoc + way].lru = ++s.l1_stamp;
+    s.st.il1[IL1_HIT]++;
+    return true;
+  }
+  int mi = P::argmin((int)g.mshr_entries, [&](int i) -> uint64_t {
+    return (s.imshr[i].valid && s.imshr[i].line == line) ? (uint64_t)i : ~0ull;
+  });
+  if (mi >= 0) {
+    if (s.imshr[mi].merges >= g.mshr_merge) { s.st.il1[IL1_RES_FAIL]++; return false; }
+    s.imshr[mi].merges++;
+    s.st.il1[IL1_MSHR_HIT]++;
+  } else {
+    mi = P::argmin((int)g.mshr_entries, [&](int i) -> uint64_t { return s.imshr[i].valid ? ~0ull : (uint64_t)i; });
+    if (mi < 0 || !sm_can_send(s, c)) { s.st.il1[IL1_RES_FAIL]++; return false; }
+    s.imshr[mi].valid = 1;
+    s.imshr[mi].line = line;
+    s.imshr[mi].merges = 0;
+    s.imshr[mi].t_issue = 0;
+    sm_send(s, c, P_RD, line, 0xf, 128, 0x40000000u | (uint32_t)mi);
+    s.st.il1[IL1_MISS]++;
+  }
+  s.w_flags[w] |= WF_IMISS;
+  s.w_iline[w] = line;
+  return false;
+}
+
 // consume at most one arrived packet per cycle (response FIFO)
 template <class P>
 SIM_HDI void sm_receive(SMState& s, const SmCtx& x, uint64_t now) {
@@ -483,6 +560,8 @@ SIM_HDI void sm_receive(SMState& s, const SmCtx& x, uint64_t now) {
     uint32_t w = q.tag & 0xff;
     s.w_stores[w]--;
     s.last_progress = now;
+  } else if ((q.tag & 0xc0000000u) == 0x40000000u) {  // instruction-cache fill
+    il1_fill<P>(s, c, q.addr);
   } else if (q.tag & 0x80000000u) {  // direct (bypass / atomic) load access
     uint32_t w = q.tag & 0xff, sl = (q.tag >> 8) & 0xff;
     if (--s.w_slot_pend[w][sl] == 0) sm_load_slot_done(s, w, sl, now);
@@ -925,14 +1004,19 @@ SIM_HDI void sm_fetch(SMState& s, const SimCfg& c) {
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   uint64_t need = P::ballot(nw, [&](int w) {
     uint8_t f = s.w_flags[w];
-    return (f & WF_ACTIVE) && !(f & WF_EXITING) && s.w_ibuf[w] == 0 && s.w_next[w] < s.w_end[w];
+    return (f & WF_ACTIVE) && !(f & (WF_EXITING | WF_IMISS)) && s.w_ibuf[w] == 0 && s.w_next[w] < s.w_end[w];
   });
   uint32_t start = s.fetch_rr % (uint32_t)nw;
   uint64_t r = rotr64(need, start, (unsigned)nw);
+  const bool icache = !c.perfect_icache && !c.il1.disabled;
   for (uint32_t i = 0; i < c.fetch_throughput && r; ++i) {
     int b = ffs64(r);
     r &= r - 1;
     uint32_t w = (uint32_t)(b + start) % (uint32_t)nw;
+    if (icache && !il1_fetch<P>(s, c, w)) {
+      s.fetch_rr = w + 1;  // miss / reservation fail ends this cycle's fetch (shader.cc:997-1010)
+      break;
+    }
     uint32_t avail = s.w_end[w] - s.w_next[w];
     uint32_t n = avail < (uint32_t)kIbuf ? avail : (uint32_t)kIbuf;
     s.w_next[w] += n;
@@ -1109,7 +1193,7 @@ SIM_HDI uint64_t sm_quiet_until(const SMState& s, const SimCfg& c, uint64_t t, u
   const uint64_t act = P::ballot(nw, [&](int w) -> bool {
     const uint8_t f = s.w_flags[w];
     if (!(f & WF_ACTIVE)) return false;
-    if (!(f & WF_EXITING) && s.w_ibuf[w] == 0 && s.w_next[w] < s.w_end[w]) return true;  // fetch
+    if (!(f & (WF_EXITING | WF_IMISS)) && s.w_ibuf[w] == 0 && s.w_next[w] < s.w_end[w]) return true;  // fetch
     const bool drained = s.w_head[w] >= s.w_end[w] && s.w_ibuf[w] == 0;
     if (drained && s.w_inflight[w] == 0 && s.w_stores[w] == 0 && s.w_loads[w] == 0) return true;  // retire
     if ((f & WF_MEMBAR) && s.w_stores[w] == 0) return true;

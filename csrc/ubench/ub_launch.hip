@@ -1,0 +1,37 @@
+// Kernel launch latency as the correlator sees it (reference
+// GPU_Microbenchmark/ubench/system/kernel_lat: kernel_lat_{1..2048}TB).
+//
+// The correlator turns a kernel's rocprofv3 duration (End - Start timestamp)
+// into hardware cycles, so the simulator's -gpgpu_kernel_launch_latency and
+// -gpgpu_TB_launch_latency must be the fixed and per-workgroup parts of THAT
+// duration, not of host-side launch throughput.  This program only launches
+// isolated empty kernels (one per grid size, synchronised, 40 repetitions);
+// run it under `rocprofv3 --kernel-trace` and fit the durations with
+// accel_sim_framework_distributed_amd/hw_stats/launch_latency.py.  Run
+// standalone it prints host-side event timings of the same launches.
+#include "ubench.h"
+
+__global__ void ub_empty_kernel(int* sink) {
+  if (sink && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) sink[0] = 1;
+}
+
+int main() {
+  UbDevice dev;
+  const double mhz = ub_shader_mhz();
+  printf("device %s, %d CUs\n", dev.p.gcnArchName, dev.cus());
+  printf("# measured_shader_mhz %.1f\n", mhz);
+  UbTimer t;
+  const int grids[] = {1, 16, 64, 256, 1024, 4096, 16384};
+  for (int nb : grids) {
+    double best = 1e30;
+    for (int r = 0; r < 40; ++r) {
+      t.start();
+      hipLaunchKernelGGL(ub_empty_kernel, dim3(nb), dim3(64), 0, 0, nullptr);
+      const double us = t.stop_ms() * 1e3;
+      best = std::min(best, us);
+      UB_CHECK(hipDeviceSynchronize());
+    }
+    printf("empty kernel, %5d workgroups: best event time %.2f us\n", nb, best);
+  }
+  return 0;
+}

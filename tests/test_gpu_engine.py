@@ -65,6 +65,8 @@ def test_state_snapshot_bit_exact(gpu_mod, tmp_path):
     {"-gpgpu_perfect_mem": "1"},
     {"-gpgpu_simple_dram_model": "1", "-gpgpu_dram_scheduler": "0"},
     {"-sim_event_skip": "0"},
+    {"-gpgpu_perfect_inst_const_cache": "0"},
+    {"-dram_seperate_write_queue_enable": "1", "-dram_write_queue_size": "16:12:4", "-gpgpu_perf_sim_memcpy": "0"},
 ])
 def test_model_switches_gpu_equals_cpu(gpu_mod, tmp_path, extra):
     """Debug trace streams (event for event), idealised memory, FIFO DRAM and
@@ -77,3 +79,22 @@ def test_model_switches_gpu_equals_cpu(gpu_mod, tmp_path, extra):
     assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
     tl = lambda o: [l for l in o.splitlines() if l.startswith("GPGPU-Sim Cycle ")]
     assert tl(g.output) == tl(c.output)
+
+
+def test_hotspot_backlog_gpu_equals_cpu(gpu_mod, tmp_path):
+    """Arrival backlog (more packets per epoch than a sub-partition's input
+    queue, both gather paths) is bit-identical on the HIP engine."""
+    import numpy as np
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+    k = KernelBuilder("_Z7hotspotPi", (320, 1, 1), (256, 1, 1), nregs=16)
+    for i in range(6):
+        k.op("STG.E", [], [4, 5], base=np.full(k.g.nwarps, 0x7000_0000 + 128 * (i % 2), np.int64), stride=0)
+    k.op("EXIT")
+    kl = rodinia.write_app(str(tmp_path / "hot"), [k.build()])
+    ex = {"-gpgpu_perf_sim_memcpy": "0"}
+    g = sim.simulate(kl, "QV100", engine="gpu", extra=ex)
+    c = sim.simulate(kl, "QV100", engine="cpu", extra=ex)
+    assert not g.deadlock
+    assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)

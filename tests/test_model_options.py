@@ -101,3 +101,71 @@ def test_max_cycle_cap_breaks(native, traces):
     assert "break due to reaching the maximum cycles" in s.output
     full = _run(native, traces["bfs"], {})
     assert s.tot_insn < full.tot_insn
+
+
+def _stat(out, key):
+    import re
+    m = re.findall(rf"{re.escape(key)} = ([0-9.]+)", out)
+    return float(m[-1]) if m else None
+
+
+def test_instruction_cache(native, traces):
+    """-gpgpu_perfect_inst_const_cache 0 routes fetch through the L1I
+    (reference shader.cc:918-1020): cold misses cost cycles, every miss is one
+    L2 request, and the quiet-cycle skipper stays exact with warps parked in
+    imiss_pending."""
+    ic = {"-gpgpu_perfect_inst_const_cache": "0"}
+    base = _run(native, traces["bfs"], {})
+    cold = _run(native, traces["bfs"], ic)
+    assert cold.tot_insn == base.tot_insn
+    assert cold.tot_cycle > base.tot_cycle
+    assert _stat(base.output, "L1I_total_cache_accesses") == 0
+    acc = _stat(cold.output, "L1I_total_cache_accesses")
+    miss = _stat(cold.output, "L1I_total_cache_misses")
+    assert acc > 0 and 0 < miss < acc
+    # each SM misses every code line at most once per kernel while it stays resident
+    noskip = _run(native, traces["bfs"], dict(ic, **{"-sim_event_skip": "0"}))
+    assert (noskip.tot_cycle, noskip.tot_insn) == (cold.tot_cycle, cold.tot_insn)
+    # a one-line, one-way cache thrashes
+    tiny = _run(native, traces["bfs"], dict(ic, **{"-gpgpu_cache:il1": "N:1:128:1,L:R:f:N:L,S:2:48,4"}))
+    assert _stat(tiny.output, "L1I_total_cache_misses") > miss
+
+
+def test_dram_write_queue_and_turnaround(native, traces):
+    """-dram_seperate_write_queue_enable with <size>:<high>:<low> watermarks
+    (reference dram_sched.cc:118-130) and -dram_elimnate_rw_turnaround
+    (gpu-sim.h:247-253) change DRAM timing, never the work done.  A small
+    write-back L2 makes the kernel evict dirty lines while it streams."""
+    small = {"-gpgpu_perf_sim_memcpy": "0", "-gpgpu_cache:dl2": "S:8:128:4,L:B:m:L:P,A:192:4,32:0,32"}
+    base = _run(native, traces["vadd"], small)
+    assert _stat(base.output, "total dram writes") > 0
+    runs = [_run(native, traces["vadd"], dict(small, **x)) for x in (
+        {"-dram_seperate_write_queue_enable": "1", "-dram_write_queue_size": "32:28:16"},
+        {"-dram_seperate_write_queue_enable": "1", "-dram_write_queue_size": "8:6:2"},
+        {"-dram_seperate_write_queue_enable": "1", "-dram_write_queue_size": "8:6:2", "-gpgpu_dram_scheduler": "0"},
+        {"-dram_elimnate_rw_turnaround": "1"})]
+    for r in runs:
+        assert not r.deadlock and r.tot_insn == base.tot_insn
+        assert _stat(r.output, "total dram reads") == _stat(base.output, "total dram reads")
+    assert runs[1].tot_cycle != base.tot_cycle
+    assert runs[3].tot_cycle <= base.tot_cycle
+
+
+def test_hotspot_backlog_no_loss(native, tmp_path):
+    """Every warp of an 80-SM grid stores into the same few lines: one L2
+    sub-partition receives far more packets per epoch than its input queue
+    holds.  Arrivals wait in the destination's backlog (nothing is dropped,
+    no deadlock) and the quiet-cycle skipper stays exact."""
+    import numpy as np
+    from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+    k = KernelBuilder("_Z7hotspotPi", (320, 1, 1), (256, 1, 1), nregs=16)
+    for i in range(6):
+        k.op("STG.E", [], [4, 5], base=np.full(k.g.nwarps, 0x7000_0000 + 128 * (i % 2), np.int64), stride=0)
+    k.op("EXIT")
+    kl = rodinia.write_app(str(tmp_path / "hot"), [k.build()])
+    a = _run(native, kl, {"-gpgpu_perf_sim_memcpy": "0"})
+    b = _run(native, kl, {"-gpgpu_perf_sim_memcpy": "0", "-sim_event_skip": "0"})
+    assert not a.deadlock
+    assert _stat(a.output, "icnt_mem_input_backlog") > 0
+    assert "lost to a full backlog ring" not in a.output
+    assert (a.tot_cycle, a.tot_insn) == (b.tot_cycle, b.tot_insn)

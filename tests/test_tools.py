@@ -102,7 +102,7 @@ def test_run_hw_dry_run(capsys):
     from accel_sim_framework_distributed_amd.hw_stats import run_hw
     assert run_hw.main(["-B", "asim_hip_apps", "-R", "2", "-n", "-o", "/tmp/x"]) == 0
     out = capsys.readouterr().out
-    assert out.count("rocprofv3 --kernel-trace") == 10 and "bin/apps/vectoradd 262144" in out
+    assert out.count("rocprofv3 --kernel-trace") == 20 and "bin/apps/vectoradd 262144" in out  # 10 app inputs x 2 runs
 
 
 def test_stats_merge_and_plot(tmp_path):

@@ -1,5 +1,7 @@
 #!/bin/bash
 # Full MI355X correlation pipeline on the GPU box:
+#  0. micro-benchmarks (incl. rocprofv3-fitted launch latency) -> tuner ->
+#     configs/tuned/AMD_Instinct_MI355X (copied to gpurun_out/corr/tuned)
 #  1. capture asim_trace traces + rocprofv3 timings (tools/gpu_trace_and_time.sh)
 #  2. simulate every trace with the tuned MI355X config (run_simulations via the
 #     local procman, CPU engine), wait with monitor_func_test
@@ -8,12 +10,18 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 out=$R/gpurun_out/corr
+mkdir -p $out
+UBENCH_PROGS="ub_config ub_cache_lat ub_alu ub_lds ub_mfma ub_atomic_kernel ub_launch ub_mem_bw" \
+  bash $R/tools/run_ubench.sh $R/gpurun_out/ubench > $out/ubench.log 2>&1 || { echo "ubench failed"; tail $out/ubench.log; exit 1; }
+python $R/util/tuner/tuner.py -s $R/gpurun_out/ubench -b MI355X -o $R/configs/tuned > $out/tuner.log 2>&1 \
+  || { echo "tuner failed"; tail $out/tuner.log; exit 1; }
+cp -r $R/configs/tuned/AMD_Instinct_MI355X $out/tuned
 bash $R/tools/gpu_trace_and_time.sh || exit 1
 export PROCMAN_STATE=$out/procman.json ASIM_JOB_LOGDIR=$out/logs
 JL=$R/util/job_launching
 timeout -k 10 300 python $JL/run_simulations.py -B asim_hip_apps -C MI355X_TUNED -T $out/traces -N corr -l local \
-  -r $out/simrun -c 5 --threads 3 > $out/launch.log 2>&1 || { echo "launch failed"; tail $out/launch.log; exit 1; }
-timeout -k 10 2400 python $JL/monitor_func_test.py -N corr -r $out/simrun -S 10 -T 2300 -K -j procman \
+  -r $out/simrun -c 10 --threads 2 > $out/launch.log 2>&1 || { echo "launch failed"; tail $out/launch.log; exit 1; }
+timeout -k 10 700 python $JL/monitor_func_test.py -N corr -r $out/simrun -S 10 -T 650 -K -j procman \
   > $out/monitor.log 2>&1; mrc=$?
 tail -25 $out/monitor.log
 python $JL/get_stats.py -N corr -r $out/simrun -k -K -I > $out/stats_per_kernel.csv

@@ -1,5 +1,5 @@
 #!/bin/bash
-# On the MI355X box: refresh the micro-benchmarks the tuner reads, capture
+# On the MI355X box: capture
 # asim_trace traces of the HIP app suite, and time the plain builds under
 # rocprofv3 (4 runs each).  Every GPU step has its own time limit and the
 # script stops at the first failure.
@@ -7,10 +7,7 @@ set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 out=$R/gpurun_out/corr
-mkdir -p $out $R/gpurun_out/ubench
-for p in ub_config ub_lds ub_mem_bw; do
-  timeout -k 10 240 $R/bin/ubench/$p > $R/gpurun_out/ubench/$p.log 2>&1 || { echo "$p failed"; exit 1; }
-done
+mkdir -p $out
 timeout -k 10 900 python $R/accel_sim_framework_distributed_amd/hw_stats/run_hw_trace.py -B asim_hip_apps -b \
   -o $out/traces > $out/trace.log 2>&1 || { echo "tracing failed"; tail -20 $out/trace.log; exit 1; }
 timeout -k 10 900 python $R/accel_sim_framework_distributed_amd/hw_stats/run_hw.py -B asim_hip_apps -R 4 \

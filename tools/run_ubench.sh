@@ -6,8 +6,12 @@
 set -o pipefail
 out=${1:-gpurun_out/ubench}
 mkdir -p "$out"
-for p in ub_config ub_cache_lat ub_alu ub_lds ub_mfma ub_atomic_kernel ub_mem_bw ub_power; do
+for p in ${UBENCH_PROGS:-ub_config ub_cache_lat ub_alu ub_lds ub_mfma ub_atomic_kernel ub_launch ub_mem_bw ub_power}; do
   echo "== $p"
   timeout -k 10 240 ./bin/ubench/$p > "$out/$p.log" 2>&1 || { echo "$p failed rc=$?"; tail -5 "$out/$p.log"; exit 1; }
   tail -3 "$out/$p.log"
 done
+echo "== launch latency (rocprofv3 durations of empty kernels)"
+timeout -k 10 240 python accel_sim_framework_distributed_amd/hw_stats/launch_latency.py -o "$out/launch_rocprof" \
+  > "$out/ub_launch_rocprof.log" 2>&1 || { echo "launch_latency failed"; tail -5 "$out/ub_launch_rocprof.log"; exit 1; }
+tail -4 "$out/ub_launch_rocprof.log"
