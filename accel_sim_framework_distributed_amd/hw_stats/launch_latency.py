@@ -9,7 +9,7 @@ TB_launch_latency`` cycles before a kernel issues CTAs).
 
 The correlator's hardware cycles are ``rocprofv3 duration x clock``; an empty
 kernel's duration is therefore exactly the fixed cost the simulated kernel
-must carry.  ``bin/ubench/ub_launch`` launches isolated empty kernels of
+must carry.  ``bin/ubench/ub_launch`` launches empty kernels (each right behind a ~20 us busy kernel, then synchronised) of
 1..16384 workgroups; this script runs it under ``rocprofv3 --kernel-trace``
 (or reads an existing run with ``-i``), fits ``duration = a + b * blocks`` on
 the per-grid medians, and prints the two options in the micro-benchmark

@@ -43,6 +43,18 @@ def _parse():
     return ap.parse_args()
 
 
+def _cycle_mae():
+    """Latest committed MI355X cycle correlation (HIP app suite vs rocprofv3),
+    produced by tools/gpu_correlate.sh / tools/local_correlate.py."""
+    p = os.path.join(ROOT, "profiles", "correlation", "mi355x_local_resim.json")
+    try:
+        d = json.load(open(p))
+        return {"mae_pct": round(d["mae_pct"], 2), "apps": len(d["apps"]), "gpu": "MI355X",
+                "source": os.path.relpath(p, ROOT)}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def main() -> int:
     a = _parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -139,7 +151,7 @@ def main() -> int:
                 "sim_insn_per_step_per_rank": int(insn / max(1, a.steps)),
                 "sim_cycles_per_step_per_rank": int(cycles / max(1, a.steps)),
             },
-            "cycle_mae_vs_hw": None,
+            "cycle_mae_vs_hw": _cycle_mae(),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -28,6 +28,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 CORE_SRC = [
     "csrc/config/options.cc",
     "csrc/config/sim_options.cc",
+    "csrc/config/icnt_config.cc",
     "csrc/trace/trace.cc",
     "csrc/engine/cpu_engine.cc",
     "csrc/power/power.cc",

@@ -1,0 +1,129 @@
+// -network_mode 1: read a Booksim-format .icnt file and turn it into the
+// per-pair latency model of the epoch engine (model/config.h icnt_pkt_lat_fs).
+//
+// What is kept from the reference's intersim2 network (interconnect_interface
+// .cpp, networks/*, routers/iq_router.cpp): the topology (fly, mesh, torus,
+// cmesh, fattree/tree4/qtree, flatfly/dragonfly), the node numbering (shader
+// clusters first, then memory sub-partitions: icnt_wrapper.cc), the router
+// pipeline depth (routing + VC allocation + switch allocation + traversal)
+// and channel latency per hop, and the flit size used for serialisation.
+// Contention is modelled at the injection and ejection ports of every node
+// (as for the local crossbar); link-level contention inside multi-hop
+// topologies and virtual-channel flow control are not -- the tested configs
+// all use a single-stage `fly` (a crossbar) where the two coincide.
+#include "icnt_config.h"
+
+#include <algorithm>
+#include <cctype>
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
+
+#include "options.h"
+
+namespace asim {
+
+std::map<std::string, std::string> parse_booksim_config(const std::string& text0) {
+  // strip comments
+  std::string t;
+  t.reserve(text0.size());
+  for (size_t i = 0; i < text0.size();) {
+    if (text0.compare(i, 2, "//") == 0) {
+      while (i < text0.size() && text0[i] != '\n') ++i;
+    } else if (text0.compare(i, 2, "/*") == 0) {
+      size_t e = text0.find("*/", i + 2);
+      i = e == std::string::npos ? text0.size() : e + 2;
+    } else {
+      t += text0[i++];
+    }
+  }
+  std::map<std::string, std::string> kv;
+  size_t i = 0;
+  while (i < t.size()) {
+    size_t eq = t.find('=', i);
+    if (eq == std::string::npos) break;
+    std::string key = t.substr(i, eq - i);
+    // value runs to the ';' at brace depth 0
+    size_t j = eq + 1;
+    int depth = 0;
+    while (j < t.size() && !(t[j] == ';' && depth == 0)) {
+      if (t[j] == '{') ++depth;
+      if (t[j] == '}') --depth;
+      ++j;
+    }
+    std::string val = t.substr(eq + 1, j - eq - 1);
+    auto trim = [](std::string s) {
+      size_t a = 0, b = s.size();
+      while (a < b && isspace((unsigned char)s[a])) ++a;
+      while (b > a && isspace((unsigned char)s[b - 1])) --b;
+      return s.substr(a, b - a);
+    };
+    key = trim(key);
+    if (!key.empty()) kv[key] = trim(val);
+    i = j + 1;
+  }
+  return kv;
+}
+
+static long geti(const std::map<std::string, std::string>& kv, const char* k, long dflt) {
+  auto it = kv.find(k);
+  if (it == kv.end() || it->second.empty()) return dflt;
+  char* end = nullptr;
+  double v = strtod(it->second.c_str(), &end);
+  if (end == it->second.c_str()) throw OptionError(std::string("interconnect config: bad value for ") + k);
+  return (long)v;
+}
+
+void apply_intersim_config(SimCfg& c, const std::string& path) {
+  std::ifstream f(path);
+  if (!f.good()) throw OptionError("cannot open interconnect config file '" + path + "'");
+  std::stringstream ss;
+  ss << f.rdbuf();
+  auto kv = parse_booksim_config(ss.str());
+  std::string topo = kv.count("topology") ? kv["topology"] : "mesh";
+  const long k = geti(kv, "k", 8), n = geti(kv, "n", 2);
+  if (k < 1 || n < 1 || k > 65535 || n > 255) throw OptionError("interconnect config: k/n out of range");
+  c.topo_k = (uint16_t)k;
+  c.topo_n = (uint8_t)n;
+  c.topo_conc = (uint16_t)std::max<long>(1, geti(kv, "c", 1));
+  uint64_t nodes = 1;
+  for (long d = 0; d < n; ++d) nodes *= (uint64_t)k;
+  if (topo == "fly") {
+    c.topo = TOPO_FLY;
+  } else if (topo == "mesh") {
+    c.topo = TOPO_MESH;
+  } else if (topo == "torus" || topo == "kncube") {
+    c.topo = TOPO_TORUS;
+  } else if (topo == "cmesh") {
+    c.topo = TOPO_CMESH;
+    nodes *= c.topo_conc;
+  } else if (topo == "fattree" || topo == "tree4" || topo == "qtree") {
+    c.topo = TOPO_FATTREE;
+    if (topo == "tree4") c.topo_k = 4;
+  } else if (topo == "flatfly" || topo == "dragonfly") {
+    c.topo = TOPO_FLATFLY;  // one hop per differing dimension (minimal routing)
+  } else {
+    throw OptionError("interconnect config: unsupported topology '" + topo + "' (anynet needs a network file)");
+  }
+  const uint64_t need = (uint64_t)c.n_clusters + c.n_subpart;
+  if (c.topo != TOPO_FLATFLY && nodes < need)
+    throw OptionError("interconnect config: topology has " + std::to_string(nodes) + " nodes, need " +
+                      std::to_string(need) + " (clusters + memory sub-partitions)");
+  // iq_router pipeline: routing, VC allocation, switch allocation, traversal
+  const long hop = geti(kv, "routing_delay", 0) + geti(kv, "vc_alloc_delay", 1) + geti(kv, "sw_alloc_delay", 1) + 1;
+  c.hop_icnt = (uint16_t)std::max<long>(1, hop);
+  c.chan_icnt = (uint16_t)std::max<long>(1, geti(kv, "channel_latency", 1));
+  if (kv.count("flit_size")) c.flit_size = (uint32_t)std::max<long>(8, geti(kv, "flit_size", 32));
+  c.icnt_mode = 1;
+  // lookahead = smallest pair latency in whole core cycles (>= 1, <= kWin - kIbuf)
+  uint64_t lo = ~0ull;
+  c.icnt_latency = 1;  // icnt_pkt_lat_fs clamps to it; 1 core cycle is the floor
+  for (uint32_t s = 0; s < c.n_sm; s += (c.cores_per_cluster ? c.cores_per_cluster : 1))
+    for (uint32_t d = 0; d < c.n_subpart; ++d) lo = std::min(lo, icnt_pkt_lat_fs(c, s, d));
+  uint64_t e = lo / c.per_core;
+  if (e < 1) e = 1;
+  if (e > (uint64_t)(kWin - kIbuf)) e = (uint64_t)(kWin - kIbuf);
+  c.icnt_latency = (uint32_t)e;
+}
+
+}  // namespace asim

@@ -279,6 +279,10 @@ void OptionRegistry::parse_file(const std::string& path) {
   std::ifstream f(path);
   if (!f.good()) throw OptionError("Cannot open config file '" + path + "'");
   if (++include_depth_ > 32) throw OptionError("-config include depth exceeded at '" + path + "'");
+  {
+    const size_t sl = path.find_last_of('/');
+    config_dirs_.push_back(sl == std::string::npos ? std::string(".") : path.substr(0, sl));
+  }
   std::string line, buf;
   while (std::getline(f, line)) {
     size_t h = line.find('#');

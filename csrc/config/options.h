@@ -65,6 +65,9 @@ class OptionRegistry {
   // argv[0] is skipped like a program name
   void parse_cmdline(const std::vector<std::string>& argv, bool skip_first = true);
   void parse_file(const std::string& path);
+  // directories of the -config files read so far (relative file options such
+  // as -inter_config_file are looked up there, like run directories expect)
+  const std::vector<std::string>& config_dirs() const { return config_dirs_; }
   // parse a string of tokens; characters in `delims` act as whitespace
   void parse_string(const std::string& s, const std::string& delims = " ;");
   void set(const std::string& name, const std::string& value);
@@ -81,6 +84,7 @@ class OptionRegistry {
   std::vector<std::unique_ptr<Opt>> opts_;
   std::map<std::string, Opt*> map_;
   int include_depth_ = 0;
+  std::vector<std::string> config_dirs_;
 };
 
 // split helpers shared by config derivation

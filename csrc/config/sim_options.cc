@@ -1,5 +1,9 @@
 #include "sim_options.h"
 
+#include <unistd.h>
+
+#include "icnt_config.h"
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -532,6 +536,17 @@ CacheGeom parse_cache_geom(const std::string& s0, bool any_line) {
   return g;
 }
 
+// a relative file named by an option: as given if readable, else next to the
+// -config files (most recent first), like a run directory's copies
+static std::string resolve_cfg_path(const OptionRegistry& r, const std::string& f) {
+  auto exists = [](const std::string& p) { return access(p.c_str(), R_OK) == 0; };
+  if (f.empty() || f[0] == '/' || exists(f)) return f;
+  const auto& dirs = r.config_dirs();
+  for (auto it = dirs.rbegin(); it != dirs.rend(); ++it)
+    if (exists(*it + "/" + f)) return *it + "/" + f;
+  return f;
+}
+
 SimCfg derive_sim_cfg(const OptionRegistry& r) {
   SimCfg c;
   memset(&c, 0, sizeof(c));
@@ -675,7 +690,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
     uint32_t v[4] = {8, 8, 8, 8};
     for (size_t i = 0; i < q.size() && i < 4; ++i) v[i] = parse_u(q[i], "-gpgpu_dram_partition_queues");
     c.q_icnt_l2 = std::max<uint32_t>(1, v[0]);
-    c.q_l2_dram = std::max<uint32_t>(4, std::min<uint32_t>(v[1], kDramQ));
+    c.q_l2_dram = std::max<uint32_t>(4, v[1]);
     c.q_dram_l2 = std::max<uint32_t>(1, std::min<uint32_t>(v[2], 64));
     c.q_l2_icnt = std::max<uint32_t>(1, v[3]);
   }
@@ -687,6 +702,15 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
     c.dram_queue = (q <= 0 || q > kDramQ) ? (uint32_t)kDramQ : (uint32_t)q;
     long long rq = r.geti("-gpgpu_dram_return_queue_size");
     c.dram_ret_queue = (rq <= 0 || rq > kDramRet) ? (uint32_t)kDramRet : (uint32_t)rq;
+  }
+  {
+    // shared credit pool of the reference's L2->DRAM arbitration: scheduler
+    // queue + return queue (0 = unlimited -> the pipe size)
+    long long q = r.geti("-gpgpu_frfcfs_dram_sched_queue_size"), rq = r.geti("-gpgpu_dram_return_queue_size");
+    uint64_t cr = (q <= 0 || rq <= 0) ? (uint64_t)kDramLat : (uint64_t)q + (uint64_t)rq;
+    c.dram_credits = (uint32_t)std::min<uint64_t>(cr, kDramLat);
+    // the per-sub-partition L2->DRAM queue plus its share of the pool
+    c.q_l2_dram = std::min<uint32_t>(c.q_l2_dram + c.dram_credits / std::max<uint32_t>(1, c.n_sub_per_mem), kDramLat);
   }
   parse_dram_timing(c, r.gets("-gpgpu_dram_timing_opt"));
   c.rw_turnaround = r.getb("-dram_elimnate_rw_turnaround") ? 0u : 1u;
@@ -766,6 +790,13 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.kernel_launch_latency = (uint32_t)std::max<long long>(0, r.geti("-gpgpu_kernel_launch_latency"));
   c.tb_launch_latency = (uint32_t)std::max<long long>(0, r.geti("-gpgpu_TB_launch_latency"));
   c.deadlock_window = r.getb("-gpgpu_deadlock_detect") ? 50000 : 0;
+  // interconnect model
+  c.icnt_mode = 2;
+  if (r.geti("-network_mode") == 1) {
+    apply_intersim_config(c, resolve_cfg_path(r, r.gets("-inter_config_file")));
+  } else if (r.geti("-network_mode") != 2) {
+    throw OptionError("-network_mode must be 1 (intersim topology) or 2 (local crossbar)");
+  }
   return c;
 }
 
@@ -839,6 +870,13 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.max_concurrent_kernel = (int32_t)r.geti("-gpgpu_max_concurrent_kernel");
   d.power_enabled = r.getb("-power_simulation_enabled");
   d.power_xml = r.gets("-accelwattch_xml_file");
+  {
+    // legacy GPUWattch configs (SM2_GTX480) name their XML with -gpuwattch_xml_file
+    const OptionRegistry::Opt* aw = r.find("-accelwattch_xml_file");
+    const OptionRegistry::Opt* gw = r.find("-gpuwattch_xml_file");
+    if (gw && gw->parsed && !(aw && aw->parsed)) d.power_xml = r.gets("-gpuwattch_xml_file");
+    d.power_xml = resolve_cfg_path(r, d.power_xml);
+  }
   d.power_mode = (int32_t)r.geti("-power_simulation_mode");
   d.hw_perf_file = r.gets("-hw_perf_file_name");
   d.hw_perf_bench = r.gets("-hw_perf_bench_name");

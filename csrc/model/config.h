@@ -40,6 +40,7 @@ constexpr int kRopQ = 256;
 constexpr int kMemInQ = 256;        // arrivals per epoch per sub-partition
 constexpr int kReplyQ = 128;
 constexpr int kDramQ = 128;         // per channel FR-FCFS queue
+constexpr int kDramLat = 512;       // per channel L2->DRAM latency pipe (in flight >= dram_latency x 1/cycle)
 constexpr int kDramRet = 256;
 constexpr int kMaxBanksDram = 32;
 constexpr int kMaxSubPerCh = 2;
@@ -151,6 +152,18 @@ struct SimCfg {
   uint32_t icnt_latency;   // core cycles (== epoch length, the PDES lookahead)
   uint32_t flit_size;
   uint32_t icnt_out_limit; // per-SM outstanding packets before injection stalls
+  // -network_mode 1 (intersim2 / Booksim topologies, reference
+  // icnt_wrapper.cc:35-45 + intersim2/networks/*): per-pair latency from the
+  // topology's hop count and the router pipeline; icnt_latency above is then
+  // the minimum over all SM<->sub-partition pairs (the PDES lookahead)
+  uint32_t icnt_mode;       // 1 topology (intersim), 2 local crossbar (fixed latency)
+  uint8_t topo;             // IcntTopo
+  uint8_t topo_n;           // dimensions / stages / tree levels
+  uint16_t topo_k;          // radix
+  uint16_t topo_conc;       // nodes per router (cmesh concentration)
+  uint16_t hop_icnt;        // icnt cycles per router traversal (routing + VA + SA + ST)
+  uint16_t chan_icnt;       // icnt cycles per channel
+  uint16_t pad_icnt;
   // ---- memory partition ----
   CacheGeom l2;
   uint32_t rop_latency;
@@ -161,6 +174,7 @@ struct SimCfg {
   uint32_t dram_sched;      // 0 FIFO, 1 FR-FCFS
   uint32_t dram_queue;
   uint32_t dram_ret_queue;
+  uint32_t dram_credits;    // L2->DRAM in-flight limit per channel (latency pipe + scheduler queue)
   uint32_t nbk, nbkgrp, tCCD, tRRD, tRCD, tRAS, tRP, tRC, CL, WL, tCDLR, tWR, tCCDL, tRTPL;
   uint32_t BL, busW, data_cmd_ratio, dual_bus, bk_index_policy, bkgrp_index_policy;
   uint32_t atom_size;       // bytes per DRAM column access
@@ -212,6 +226,67 @@ SIM_HDI void trace_put(const SimCfg& c, uint32_t unit, uint64_t cycle, uint16_t 
   }
   c.trace_cnt[unit] = n + 1;
 }
+enum IcntTopo : uint8_t { TOPO_FLY = 0, TOPO_MESH, TOPO_TORUS, TOPO_CMESH, TOPO_FATTREE, TOPO_FLATFLY };
+
+// routers a packet traverses between interconnect nodes a and b
+SIM_HDI uint32_t icnt_routers(const SimCfg& c, uint32_t a, uint32_t b) {
+  const uint32_t k = c.topo_k ? c.topo_k : 2, n = c.topo_n ? c.topo_n : 1;
+  switch (c.topo) {
+    case TOPO_FLY:  // k-ary n-fly: every route crosses all n stages
+      return n;
+    case TOPO_CMESH:
+      a /= (c.topo_conc ? c.topo_conc : 1);
+      b /= (c.topo_conc ? c.topo_conc : 1);
+      [[fallthrough]];
+    case TOPO_MESH:
+    case TOPO_TORUS: {  // k-ary n-cube, dimension-order routing
+      uint32_t h = 0;
+      for (uint32_t d = 0; d < n; ++d) {
+        const uint32_t x = a % k, y = b % k;
+        uint32_t dd = x > y ? x - y : y - x;
+        if (c.topo == TOPO_TORUS && k - dd < dd) dd = k - dd;
+        h += dd;
+        a /= k;
+        b /= k;
+      }
+      return h + 1;
+    }
+    case TOPO_FATTREE: {  // k-ary n-tree: up to the lowest common ancestor and down
+      uint32_t lvl = 1;
+      a /= k;
+      b /= k;
+      while (a != b && lvl < n) {
+        a /= k;
+        b /= k;
+        ++lvl;
+      }
+      return 2 * lvl - 1;
+    }
+    default: {  // flattened butterfly: one hop per differing dimension
+      uint32_t h = 0;
+      for (uint32_t d = 0; d < n; ++d) {
+        h += (a % k) != (b % k);
+        a /= k;
+        b /= k;
+      }
+      return h + 1;
+    }
+  }
+}
+
+// femtoseconds from injection complete to arrival: SM `sm` -> sub-partition `sub`
+// (either direction; the topologies are symmetric)
+SIM_HDI uint64_t icnt_pkt_lat_fs(const SimCfg& c, uint32_t sm, uint32_t sub) {
+  if (c.icnt_mode != 1) return (uint64_t)c.icnt_latency * c.per_core;
+  const uint32_t a = sm / (c.cores_per_cluster ? c.cores_per_cluster : 1);  // one node per cluster
+  const uint32_t b = c.n_clusters + sub;                                  // then the sub-partitions
+  const uint32_t r = icnt_routers(c, a, b);
+  const uint64_t cyc = (uint64_t)r * c.hop_icnt + (uint64_t)(r + 1) * c.chan_icnt;
+  const uint64_t fs = cyc * c.per_icnt;
+  const uint64_t lo = (uint64_t)c.icnt_latency * c.per_core;  // never below the lookahead
+  return fs > lo ? fs : lo;
+}
+
 SIM_HDI bool trace_sm_on(const SimCfg& c, uint32_t stream, uint32_t sm) {
   return (c.trace_mask & stream) && (c.trace_sm < 0 || (uint32_t)c.trace_sm == sm);
 }

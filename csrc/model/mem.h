@@ -120,7 +120,7 @@ struct alignas(16) ChanState {
   uint64_t t_dram;
   uint64_t dcycle;    // dram cycle counter
   // DRAM
-  DramReq lat[kDramQ];  // L2 -> DRAM latency pipe (FIFO)
+  DramReq lat[kDramLat];  // L2 -> DRAM latency pipe (FIFO)
   uint32_t lat_head, lat_n;
   DramReq q[kDramQ];    // scheduler queue (pool; age order via q_age)
   uint32_t q_n;
@@ -165,13 +165,19 @@ SIM_HDI uint32_t dram_bkgrp(const SimCfg& c, uint32_t bank) {
   return (bank / per) % ng;
 }
 
+// Requests between the L2 and the DRAM data return hold channel credits
+// (reference memory_partition_unit arbitration: a private credit per
+// sub-partition + a shared pool of sched_queue + return_queue entries,
+// l2cache.cc:120-140, borrowed when a request enters the DRAM latency queue);
+// the per-sub-partition share also bounds what one L2 slice can queue.
 SIM_HDI bool l2dram_can(const ChanState& ch, const SubPart& sp, const SimCfg& c, uint32_t n) {
-  return sp.n_l2dram + n <= c.q_l2_dram && ch.lat_n + n <= (uint32_t)kDramQ;
+  return sp.n_l2dram + n <= c.q_l2_dram && ch.lat_n + ch.q_n + n <= c.dram_credits &&
+         ch.lat_n + n <= (uint32_t)kDramLat;
 }
 
 SIM_HDI void l2dram_push(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, uint64_t line,
                          uint32_t sector, bool write, uint64_t now_fs) {
-  DramReq& r = ch.lat[(ch.lat_head + ch.lat_n) % kDramQ];
+  DramReq& r = ch.lat[(ch.lat_head + ch.lat_n) % kDramLat];
   AddrTlx t = addr_decode(c, line + sector * 32ull);
   r.line = line;
   r.ready = now_fs + (uint64_t)c.dram_latency * c.per_l2;
@@ -471,7 +477,7 @@ SIM_HDI void mem_icnt_cycle(ChanState& ch, SubPart& sp, const SimCfg& c, const M
       // per-destination counter kept in the reply's own slot count array
       uint32_t n = sp_out_count(ch, sub, r.dst);
       if (n < x.out_cap) {
-        r.t = done + (uint64_t)c.icnt_latency * c.per_core;
+        r.t = done + icnt_pkt_lat_fs(c, r.dst, gsub);
         P::one([&] { x.outbox[(uint64_t)cell * x.out_cap + n] = r; });
         sp_out_count_inc(ch, sub, r.dst);
         sp.rep_head = (sp.rep_head + 1) % kReplyQ;
@@ -513,7 +519,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
     ch.q_valid[f] = 1;
     ch.q_age[f] = ch.q_seq++;
     ch.q_n++;
-    ch.lat_head = (ch.lat_head + 1) % kDramQ;
+    ch.lat_head = (ch.lat_head + 1) % kDramLat;
     ch.lat_n--;
   }
   // data returns -> DRAM->L2 queues

@@ -310,7 +310,7 @@ SIM_HDI void sm_inject(SMState& s, const SmCtx& x, uint64_t now) {
   uint32_t n = s.ocnt[dst];
   if (n >= x.out_cap) return;  // outbox cell full (cannot happen with cap >= epoch)
   s.ocnt[dst] = n + 1;
-  p.t = (done + c.icnt_latency) * c.per_core;
+  p.t = done * c.per_core + icnt_pkt_lat_fs(c, s.id, dst);
   if (trace_sm_on(c, TS_INTERCONNECT, s.id)) P::one([&] { trace_put(c, s.id, now, EV_PKT_SEND, (uint16_t)dst, p.addr); });
   P::one([&] {
     x.outbox[(uint64_t)slot * x.out_cap + n] = p;

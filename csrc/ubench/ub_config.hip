@@ -23,10 +23,11 @@ int main() {
   ub_opt("-gpgpu_shmem_size", (long long)p.sharedMemPerMultiprocessor);
   ub_opt("-gpgpu_shmem_per_block", (long long)p.sharedMemPerBlock);
   ub_opt("-gpgpu_shader_cta", (long long)std::min(32, p.maxThreadsPerMultiProcessor / 64));
-  // HBM3E: 8 stacks x 16 pseudo-channel pairs; one simulated channel per 128-bit slice
-  const int channels = std::max(1, p.memoryBusWidth / 128);
+  // HBM3E: 8 stacks x 16 channels of 64 bits; one simulated channel (with
+  // one L2 slice) per 64-bit channel
+  const int channels = std::max(1, p.memoryBusWidth / 64);
   ub_opt("-gpgpu_n_mem", channels);
-  ub_opt("-gpgpu_n_sub_partition_per_mchannel", 2);
+  ub_opt("-gpgpu_n_sub_partition_per_mchannel", 1);
   const double mem_mhz = p.memoryClockRate / 1000.0;
   // -gpgpu_dram_buswidth comes from ub_mem_bw (sized to the measured bandwidth)
   char clk[128];
@@ -37,7 +38,7 @@ int main() {
   // simulator's memory-side L2 gets the chip total, split across the
   // memory sub-partitions (16-way, 128B lines)
   const long long l2_bytes = (long long)p.l2CacheSize * 8;
-  const long long per_sub = std::max<long long>(128 * 16, l2_bytes / (2LL * channels));
+  const long long per_sub = std::max<long long>(128 * 16, l2_bytes / channels);
   const long long sets = std::max<long long>(1, per_sub / (128 * 16));
   ub_opt("-gpgpu_cache:dl2", "S:" + std::to_string(sets) + ":128:16,L:B:m:L:P,A:192:4,32:0,32");
   printf("# measured_shader_mhz %.1f\n", mhz);

@@ -75,7 +75,7 @@ int main() {
   // bytes per DRAM clock per channel (DDR) such that the simulated channels,
   // running at the ~80 % bus efficiency a streaming read reaches, deliver the
   // measured read bandwidth; rounded up to a power of two
-  const int channels = std::max(1, d.p.memoryBusWidth / 128);
+  const int channels = std::max(1, d.p.memoryBusWidth / 64);
   const double mem_mhz = d.p.memoryClockRate / 1000.0;
   const double need = rd * 1e9 / (0.8 * channels * 2.0 * mem_mhz * 1e6);
   int width = 1;

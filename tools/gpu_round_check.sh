@@ -1,3 +1,6 @@
+#!/bin/bash
+# GPU-box round check: GPU tests (one process), smoke, 1-GPU bench; each step
+# has its own time limit and the chain stops at the first failure.
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
