@@ -221,6 +221,204 @@ def _rtx3070() -> Dict[str, str]:
     return c
 
 
+# ---- interconnect files for -network_mode 1 (Booksim/intersim2 format) ----
+# Every tested pre-Volta config uses a single-stage butterfly (a crossbar with
+# iSLIP allocation) sized to clusters + memory sub-partitions (reference
+# configs/tested-cfgs/*/config_*_islip.icnt); the generator below writes the
+# same parameter set for any node count / topology.
+def icnt_params(k: int, topology: str = "fly", n: int = 1, flit_size: int = 40, **over) -> Dict[str, str]:
+    p = {
+        "use_map": "0", "flit_size": str(flit_size), "network_count": "2",
+        "topology": topology, "k": str(k), "n": str(n), "routing_function": "dest_tag",
+        "num_vcs": "1", "vc_buf_size": "64", "input_buffer_size": "256", "ejection_buffer_size": "64",
+        "boundary_buffer_size": "64", "wait_for_tail_credit": "0", "vc_allocator": "islip",
+        "sw_allocator": "islip", "alloc_iters": "1", "credit_delay": "0", "routing_delay": "0",
+        "vc_alloc_delay": "1", "sw_alloc_delay": "1", "input_speedup": "1", "output_speedup": "1",
+        "internal_speedup": "2.0", "traffic": "uniform", "sim_type": "gpgpusim", "injection_rate": "0.1",
+        "subnets": "2", "read_request_subnet": "0", "read_reply_subnet": "1", "write_request_subnet": "0",
+        "write_reply_subnet": "1",
+    }
+    p.update({kk: str(v) for kk, v in over.items()})
+    return p
+
+
+def render_icnt(params: Dict[str, str], title: str = "") -> str:
+    lines = [f"// {title}" if title else "// generated by accel_sim_framework_distributed_amd.models.presets"]
+    lines += [f"{k} = {v};" for k, v in params.items()]
+    return "\n".join(lines) + "\n"
+
+
+# preset -> (file name, booksim parameters)
+ICNT_FILES: Dict[str, Tuple[str, Dict[str, str]]] = {
+    "GTX480": ("config_fermi_islip.icnt", icnt_params(27)),
+    "KEPLER_TITAN": ("config_kepler_islip.icnt", icnt_params(38)),
+    "TITANX": ("config_pascal_islip.icnt", icnt_params(52)),
+}
+
+
+def _pre_volta_common() -> Dict[str, str]:
+    """Fermi/Kepler/Pascal-era settings shared by the tested pre-Volta configs
+    (SM2_GTX480, SM3_KEPLER_TITAN, SM6_TITANX gpgpusim.config)."""
+    c = _volta_common()
+    for k in [k for k in c if k.startswith("-specialized_unit_") or "_spec_op_" in k]:
+        del c[k]
+    c.update({
+        "-gpgpu_ignore_resources_limitation": "1",
+        "-gpgpu_kernel_launch_latency": "0",
+        "-gpgpu_tensor_core_avail": "0",
+        "-gpgpu_num_tensor_core_units": "0",
+        "-gpgpu_num_int_units": "0",
+        "-gpgpu_num_dp_units": "0",
+        "-gpgpu_sub_core_model": "0",
+        "-gpgpu_adaptive_cache_config": "0",
+        "-gpgpu_unified_l1d_size": "0",
+        "-gpgpu_shmem_option": "0",
+        "-gpgpu_l1_banks": "1",
+        "-gpgpu_l1_cache_write_ratio": "0",
+        "-gpgpu_gmem_skip_L1D": "1",
+        "-gpgpu_scheduler": "gto",
+        "-gpgpu_max_insn_issue_per_warp": "2",
+        "-gpgpu_dual_issue_diff_exec_units": "1",
+        "-gpgpu_memory_partition_indexing": "0",
+        "-gpgpu_perfect_inst_const_cache": "0",
+        "-gpgpu_cache:il1": "N:8:128:4,L:R:f:N:L,S:2:48,4",
+        "-gpgpu_inst_fetch_throughput": "8",
+        "-gpgpu_tex_cache:l1": "N:16:128:24,L:R:m:N:L,T:128:4,128:2",
+        "-gpgpu_const_cache:l1": "N:128:64:2,L:R:f:N:L,S:2:64,4",
+        "-gpgpu_dram_partition_queues": "32:32:32:32",
+        "-gpgpu_l2_rop_latency": "120",
+        "-dram_latency": "100",
+        "-gpgpu_frfcfs_dram_sched_queue_size": "64",
+        "-gpgpu_dram_return_queue_size": "64",
+        "-gpgpu_dram_buswidth": "4",
+        "-gpgpu_dram_burst_length": "8",
+        "-dram_data_command_freq_ratio": "4",
+        "-dram_dual_bus_interface": "0",
+        "-gpgpu_mem_addr_mapping": "dramid@8;00000000.00000000.00000000.00000000.0000RRRR.RRRRRRRR.RBBBCCCC.BCCSSSSS",
+        "-gpgpu_dram_timing_opt": '"nbk=16:CCD=2:RRD=8:RCD=16:RAS=37:RP=16:RC=52:CL=16:WL=6:CDLR=7:WR=16:nbkgrp=4:CCDL=4:RTPL=3"',
+        "-network_mode": "1",
+        "-icnt_flit_size": "40",
+        "-gpgpu_n_cluster_ejection_buffer_size": "32",
+        "-gpgpu_flush_l1_cache": "1",
+        "-gpgpu_l1_latency": "82",
+        "-gpgpu_smem_latency": "24",
+        "-trace_opcode_latency_initiation_int": "4,1",
+        "-trace_opcode_latency_initiation_sp": "4,1",
+        "-trace_opcode_latency_initiation_dp": "20,8",
+        "-trace_opcode_latency_initiation_sfu": "20,4",
+        "-trace_opcode_latency_initiation_tensor": "4,1",
+    })
+    return c
+
+
+def _titanx() -> Dict[str, str]:
+    """Pascal TITAN X (SM6_TITANX): 28 SMs, 12 GDDR5X channels x 2, fly(52) icnt."""
+    c = _pre_volta_common()
+    c.update({
+        "-gpgpu_compute_capability_major": "6", "-gpgpu_compute_capability_minor": "1",
+        "-gpgpu_ptx_force_max_capability": "61", "-gpgpu_occupancy_sm_number": "62",
+        "-gpgpu_n_clusters": "28", "-gpgpu_n_mem": "12", "-gpgpu_n_sub_partition_per_mchannel": "2",
+        "-gpgpu_clock_domains": "1417.0:1417.0:1417.0:2500.0",
+        "-gpgpu_pipeline_widths": "4,0,0,4,4,4,0,0,4,4,8",
+        "-gpgpu_num_sp_units": "4", "-gpgpu_num_sfu_units": "4",
+        "-gpgpu_coalesce_arch": "61", "-gpgpu_l1_banks": "2",
+        "-gpgpu_cache:dl1": "S:4:128:96,L:L:s:N:L,A:256:8,16:0,32",
+        "-gpgpu_shmem_size": "98304", "-gpgpu_shmem_sizeDefault": "98304", "-gpgpu_shmem_per_block": "49152",
+        "-gpgpu_cache:dl2": "S:64:128:16,L:B:m:L:P,A:256:64,16:0,32",
+        "-gpgpu_memory_partition_indexing": "4",
+        "-gpgpu_perfect_inst_const_cache": "1",
+        "-gpgpu_kernel_launch_latency": "5000",
+        "-gpgpu_mem_addr_mapping": "dramid@8;00000000.00000000.00000000.00000000.0000RRRR.RRRRRRRR.RBBBCCCC.BCCSSSSS",
+        "-inter_config_file": "config_pascal_islip.icnt",
+    })
+    return c
+
+
+def _kepler_titan() -> Dict[str, str]:
+    """Kepler GTX TITAN (SM3_KEPLER_TITAN): 14 SMX, 12 channels x 2, fly(38) icnt."""
+    c = _pre_volta_common()
+    c.update({
+        "-gpgpu_compute_capability_major": "3", "-gpgpu_compute_capability_minor": "5",
+        "-gpgpu_ptx_force_max_capability": "35", "-gpgpu_occupancy_sm_number": "62",
+        "-gpgpu_n_clusters": "14", "-gpgpu_n_mem": "12", "-gpgpu_n_sub_partition_per_mchannel": "2",
+        "-gpgpu_clock_domains": "837.0:837.0:837.0:1502.0",
+        "-gpgpu_shader_cta": "16",
+        "-gpgpu_pipeline_widths": "6,4,0,2,1,6,4,0,2,1,12",
+        "-gpgpu_num_sp_units": "6", "-gpgpu_num_sfu_units": "2", "-gpgpu_num_dp_units": "4",
+        "-gpgpu_enable_specialized_operand_collector": "1",
+        "-gpgpu_operand_collector_num_units_sp": "12", "-gpgpu_operand_collector_num_units_sfu": "6",
+        "-gpgpu_operand_collector_num_units_mem": "8", "-gpgpu_operand_collector_num_units_dp": "6",
+        "-gpgpu_operand_collector_num_units_gen": "0",
+        "-gpgpu_coalesce_arch": "35", "-gpgpu_dual_issue_diff_exec_units": "0",
+        "-gpgpu_cache:dl1": "S:4:128:32,L:L:s:N:L,A:256:8,16:0,32",
+        "-gpgpu_shmem_size": "49152", "-gpgpu_shmem_sizeDefault": "49152", "-gpgpu_shmem_per_block": "49152",
+        "-gpgpu_cache:dl2": "S:32:128:16,L:B:m:L:P,A:256:64,16:0,32",
+        "-gpgpu_clock_gated_lanes": "0",
+        "-inter_config_file": "config_kepler_islip.icnt",
+        "-trace_opcode_latency_initiation_dp": "20,2",
+        "-trace_opcode_latency_initiation_sfu": "200,2",
+    })
+    return c
+
+
+def _gtx480() -> Dict[str, str]:
+    """Fermi GTX 480 (SM2_GTX480): 15 SMs, 6 GDDR5 channels x 2, fly(27) icnt."""
+    c = _pre_volta_common()
+    c.update({
+        "-gpgpu_compute_capability_major": "2", "-gpgpu_compute_capability_minor": "0",
+        "-gpgpu_ptx_force_max_capability": "20", "-gpgpu_occupancy_sm_number": "20",
+        "-gpgpu_n_clusters": "15", "-gpgpu_n_mem": "6", "-gpgpu_n_sub_partition_per_mchannel": "2",
+        "-gpgpu_clock_domains": "700.0:700.0:700.0:924.0",
+        "-gpgpu_shader_registers": "32768", "-gpgpu_registers_per_block": "32768",
+        "-gpgpu_shader_core_pipeline": "1536:32", "-gpgpu_shader_cta": "8",
+        "-gpgpu_pipeline_widths": "2,0,0,1,1,2,0,0,1,1,2",
+        "-gpgpu_num_sp_units": "2", "-gpgpu_num_sfu_units": "1",
+        "-gpgpu_num_sched_per_core": "2", "-gpgpu_max_insn_issue_per_warp": "1",
+        "-gpgpu_enable_specialized_operand_collector": "1",
+        "-gpgpu_operand_collector_num_units_sp": "6", "-gpgpu_operand_collector_num_units_sfu": "8",
+        "-gpgpu_operand_collector_num_units_mem": "2", "-gpgpu_operand_collector_num_units_gen": "0",
+        "-gpgpu_coalesce_arch": "20", "-gpgpu_ignore_resources_limitation": "0",
+        "-gpgpu_cache:dl1": "N:32:128:4,L:L:m:N:H,S:64:8,8",
+        "-gpgpu_gmem_skip_L1D": "0", "-gpgpu_l1_latency": "35", "-gpgpu_smem_latency": "26",
+        "-gpgpu_shmem_size": "49152", "-gpgpu_shmem_sizeDefault": "49152", "-gpgpu_shmem_per_block": "49152",
+        "-gpgpu_cache:dl2": "S:64:128:8,L:B:m:L:L,A:256:4,4:0,32",
+        "-gpgpu_cache:il1": "N:4:128:4,L:R:f:N:L,S:2:32,4",
+        "-gpgpu_const_cache:l1": "N:64:64:2,L:R:f:N:L,S:2:32,4",
+        "-gpgpu_dram_partition_queues": "64:64:64:64",
+        "-gpgpu_dram_return_queue_size": "116",
+        "-gpgpu_n_mem_per_ctrlr": "2",
+        "-gpgpu_mem_addr_mapping": "dramid@8;00000000.00000000.00000000.00000000.0000RRRR.RRRRRRRR.BBBCCCCB.CCSSSSSS",
+        "-gpgpu_dram_timing_opt": '"nbk=16:CCD=2:RRD=6:RCD=12:RAS=28:RP=12:RC=40:CL=12:WL=4:CDLR=5:WR=12:nbkgrp=4:CCDL=3:RTPL=2"',
+        "-gpgpu_clock_gated_lanes": "0",
+        "-inter_config_file": "config_fermi_islip.icnt",
+    })
+    return c
+
+
+def _rtx2060_s() -> Dict[str, str]:
+    """RTX 2060 SUPER (SM75_RTX2060_S): 34 SMs at 1905 MHz, 16 GDDR6 channels."""
+    c = _rtx2060()
+    c.update({
+        "-gpgpu_n_clusters": "34", "-gpgpu_n_mem": "16",
+        "-gpgpu_clock_domains": "1905.0:1905.0:1905.0:3500.0",
+        "-gpgpu_shader_cta": "32", "-gpgpu_num_reg_banks": "16",
+        "-gpgpu_pipeline_widths": "4,0,4,4,4,4,0,4,4,4,8,4,4",
+        "-gpgpu_adaptive_cache_config": "0",
+        "-gpgpu_cache:dl1": "S:1:128:512,L:L:s:N:L,A:256:8,16:0,32",
+        "-gpgpu_shmem_per_block": "65536",
+        "-gpgpu_l1_latency": "20", "-gpgpu_smem_latency": "20", "-gpgpu_l2_rop_latency": "160",
+        "-dram_latency": "100",
+        "-trace_opcode_latency_initiation_int": "2,2", "-trace_opcode_latency_initiation_sp": "2,2",
+        "-trace_opcode_latency_initiation_dp": "64,64", "-trace_opcode_latency_initiation_sfu": "21,8",
+        "-trace_opcode_latency_initiation_tensor": "16,16",
+        "-specialized_unit_3": "1,4,16,4,4,TENSOR",
+        "-trace_opcode_latency_initiation_spec_op_3": "16,16",
+        "-specialized_unit_4": "1,4,4,4,4,UDP",
+        "-trace_opcode_latency_initiation_spec_op_4": "4,1",
+    })
+    return c
+
+
 def _mi355x() -> Dict[str, str]:
     """CDNA4 / MI355X model: 256 CUs (8 XCDs x 32), wave64, 4 SIMD32 per CU.
 
@@ -281,6 +479,10 @@ def _mi355x() -> Dict[str, str]:
 
 
 PRESETS = {
+    "GTX480": _gtx480,
+    "KEPLER_TITAN": _kepler_titan,
+    "TITANX": _titanx,
+    "RTX2060_S": _rtx2060_s,
     "QV100": _qv100,
     "GV100": _gv100,
     "TITANV": _titanv,
@@ -291,7 +493,9 @@ PRESETS = {
 
 
 def get_preset(name: str) -> Dict[str, str]:
-    key = name.upper().replace("-SASS", "").replace("SM7_", "").replace("SM75_", "").replace("SM86_", "")
+    key = name.upper().replace("-SASS", "")
+    for pre in ("SM7_", "SM75_", "SM86_", "SM6_", "SM3_", "SM2_"):
+        key = key.replace(pre, "")
     if key not in PRESETS:
         raise KeyError(f"unknown GPU preset {name!r}; known: {sorted(PRESETS)}")
     return copy.deepcopy(PRESETS[key]())
@@ -330,6 +534,13 @@ def write_config(name_or_opts, out_dir: str, extra: Dict[str, str] | None = None
         f.write(render(gp, sorted(gp)))
     with open(p2, "w") as f:
         f.write(render(tr, sorted(tr)))
+    # -network_mode 1: the Booksim interconnect file next to the configs
+    if opts.get("-network_mode", "2").strip() == "1":
+        fn = opts.get("-inter_config_file", "").strip()
+        spec = _icnt_spec(name_or_opts, fn)
+        if spec and not os.path.isabs(fn):
+            with open(os.path.join(out_dir, spec[0]), "w") as f:
+                f.write(render_icnt(spec[1], f"{spec[0]} ({spec[1]['topology']}, k={spec[1]['k']}, n={spec[1]['n']})"))
     # AccelWattch XMLs next to the configs (SIM / HW / HYBRID modes share the
     # uncalibrated defaults until power.calibrate rewrites them)
     from ..power.xmlcfg import default_params, write_xml
@@ -341,11 +552,51 @@ def write_config(name_or_opts, out_dir: str, extra: Dict[str, str] | None = None
     return p1, p2
 
 
+def _icnt_spec(name_or_opts, fn: str):
+    """(file name, params) of the interconnect file a preset / option dict names."""
+    if isinstance(name_or_opts, str):
+        try:
+            key = next(k for k in PRESETS if get_preset(name_or_opts)["-inter_config_file"] == ICNT_FILES.get(k, ("",))[0])
+        except (StopIteration, KeyError):
+            key = None
+        if key in ICNT_FILES:
+            return ICNT_FILES[key]
+    for f, p in ICNT_FILES.values():
+        if f == os.path.basename(fn):
+            return f, p
+    return None
+
+
+def _materialise_icnt(opts: Dict[str, str], name_or_opts) -> None:
+    """argv use: point -inter_config_file at a generated file in a cache dir."""
+    if opts.get("-network_mode", "2").strip() != "1":
+        return
+    fn = opts.get("-inter_config_file", "").strip()
+    if os.path.isabs(fn) or os.path.exists(fn):
+        return
+    spec = _icnt_spec(name_or_opts, fn)
+    if not spec:
+        return
+    import hashlib
+    import tempfile
+    text = render_icnt(spec[1], spec[0])
+    d = os.path.join(tempfile.gettempdir(), f"asim_icnt_{os.getuid()}")
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, hashlib.sha1(text.encode()).hexdigest()[:12] + "_" + spec[0])
+    if not os.path.exists(path):
+        tmp = path + f".{os.getpid()}"
+        with open(tmp, "w") as f:
+            f.write(text)
+        os.replace(tmp, path)
+    opts["-inter_config_file"] = path
+
+
 def args_for(name_or_opts, extra: Dict[str, str] | None = None) -> list:
     """Flat argv list (no files) for a preset, for in-process simulators."""
     opts = get_preset(name_or_opts) if isinstance(name_or_opts, str) else dict(name_or_opts)
     if extra:
         opts.update(extra)
+    _materialise_icnt(opts, name_or_opts)
     argv = []
     for k, v in opts.items():
         if len(v) >= 2 and v[0] == '"' and v[-1] == '"':

@@ -5,6 +5,7 @@
 
 #include <cstring>
 
+#include "../config/icnt_config.h"
 #include "../driver/simulator.h"
 
 namespace py = pybind11;
@@ -172,6 +173,14 @@ PYBIND11_MODULE(_asim, m) {
     d["sub"] = t.sub;
     return d;
   });
+  m.def("icnt_latency", [](const std::vector<std::string>& args, uint32_t sm, uint32_t sub) {
+    // (packet latency SM sm <-> sub-partition sub in core cycles, lookahead in core cycles, routers)
+    SimCfg c = cfg_from_args(args);
+    const uint32_t node = sm / (c.cores_per_cluster ? c.cores_per_cluster : 1);
+    return py::make_tuple((double)icnt_pkt_lat_fs(c, sm, sub) / (double)c.per_core, c.icnt_latency,
+                          c.icnt_mode == 1 ? icnt_routers(c, node, c.n_clusters + sub) : 1u);
+  }, "interconnect latency model (-network_mode 1 topology or local crossbar)");
+  m.def("parse_booksim_config", [](const std::string& text) { return parse_booksim_config(text); });
   m.def("ipoly_hash", &ipoly_hash);
   m.def("cache_set_index", [](const std::string& geom, uint64_t addr) {
     return cache_set_index(parse_cache_geom(geom), addr);

@@ -98,3 +98,15 @@ def test_hotspot_backlog_gpu_equals_cpu(gpu_mod, tmp_path):
     c = sim.simulate(kl, "QV100", engine="cpu", extra=ex)
     assert not g.deadlock
     assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
+
+
+@pytest.mark.parametrize("preset", ["TITANX", "GTX480"])
+def test_intersim_presets_gpu_equals_cpu(gpu_mod, tmp_path, preset):
+    """-network_mode 1 (topology latency per SM/sub-partition pair, lookahead
+    from the .icnt router pipeline) is bit-identical on the HIP engine."""
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    kl = rodinia.write_app(str(tmp_path / "bfs"), rodinia.bfs(2048, levels=3))
+    g = sim.simulate(kl, preset, engine="gpu")
+    c = sim.simulate(kl, preset, engine="cpu")
+    assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)

@@ -1,0 +1,95 @@
+"""-network_mode 1: Booksim/intersim2 .icnt files, topology latency model
+(reference gpu-simulator/gpgpu-sim/src/intersim2: networks/*, routers/
+iq_router pipeline; icnt_wrapper.cc node numbering) and the pre-Volta presets
+that use it."""
+import glob
+import os
+import subprocess
+
+import pytest
+
+from conftest import REFERENCE
+from accel_sim_framework_distributed_amd.models import presets
+from accel_sim_framework_distributed_amd.tracegen import rodinia
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_booksim_grammar(native):
+    kv = native.parse_booksim_config("""
+        // a comment
+        topology = mesh; /* block
+        comment */ k = 4 ;
+        n=2;
+        packet_size ={{1,2,3,4},{10,20}};  // list value keeps its braces
+        routing_function = dim_order;""")
+    assert kv["topology"] == "mesh" and kv["k"] == "4" and kv["n"] == "2"
+    assert kv["packet_size"] == "{{1,2,3,4},{10,20}}"
+    assert kv["routing_function"] == "dim_order"
+
+
+@pytest.mark.skipif(not os.path.isdir(REFERENCE), reason="reference tree not mounted")
+def test_reference_icnt_files_parse(native):
+    files = glob.glob(os.path.join(REFERENCE, "gpu-simulator/gpgpu-sim/configs/tested-cfgs/*/*.icnt"))
+    assert files
+    for f in files:
+        kv = native.parse_booksim_config(open(f).read())
+        assert kv["topology"] == "fly" and kv["n"] == "1" and int(kv["k"]) >= 27, f
+
+
+def _icnt_args(tmp_path, name, **kw):
+    p = tmp_path / f"{name}.icnt"
+    p.write_text(presets.render_icnt(presets.icnt_params(**kw)))
+    # 16 clusters + 16 sub-partitions = 32 nodes
+    return presets.args_for("QV100", {"-gpgpu_n_clusters": "16", "-gpgpu_n_mem": "8",
+                                      "-network_mode": "1", "-inter_config_file": str(p)})
+
+
+def test_topology_latencies(native, tmp_path):
+    fly = _icnt_args(tmp_path, "fly", k=32, n=1)
+    lat, look, routers = native.icnt_latency(fly, 0, 0)
+    assert routers == 1 and look == int(lat) and lat == 5  # 1 router x (0+1+1+1) + 2 channels
+    mesh = _icnt_args(tmp_path, "mesh", k=8, n=2, topology="mesh")
+    # node 0 (SM 0) -> node 16 + 15 = 31: (7, 3) in an 8x8 mesh: 7 + 3 hops, 11 routers
+    assert native.icnt_latency(mesh, 0, 15)[2] == 11
+    torus = _icnt_args(tmp_path, "torus", k=8, n=2, topology="torus")
+    assert native.icnt_latency(torus, 0, 15)[2] == 1 + 1 + 3  # wrap-around in x
+    ft = _icnt_args(tmp_path, "ft", k=4, n=3, topology="fattree")
+    assert native.icnt_latency(ft, 0, 0)[2] == 5   # leaves 0 and 16 share only the root level
+    # lookahead = the smallest pair latency in core cycles
+    assert native.icnt_latency(mesh, 0, 0)[1] <= min(native.icnt_latency(mesh, s, d)[0]
+                                                    for s in range(16) for d in range(16))
+
+
+def test_too_small_topology_rejected(native, tmp_path):
+    small = _icnt_args(tmp_path, "small", k=8, n=1)
+    with pytest.raises(Exception):
+        native.parse_config(small)
+
+
+def test_mesh_slower_than_crossbar(native, tmp_path):
+    kl = rodinia.write_app(str(tmp_path / "bfs"), rodinia.bfs(2048, levels=2))
+    runs = {}
+    for name, kw in (("fly", dict(k=32, n=1)), ("mesh", dict(k=8, n=2, topology="mesh"))):
+        s = native.Simulator(_icnt_args(tmp_path, name, **kw) + ["-trace", kl], False)
+        assert s.run() == 0 and not s.deadlock
+        runs[name] = s
+    assert runs["fly"].tot_insn == runs["mesh"].tot_insn
+    assert runs["mesh"].tot_cycle > runs["fly"].tot_cycle
+
+
+@pytest.mark.parametrize("preset", ["GTX480", "KEPLER_TITAN", "TITANX", "RTX2060_S"])
+def test_pre_volta_presets(native, tmp_path, preset):
+    kl = rodinia.write_app(str(tmp_path / "vadd"), [rodinia.vectoradd(20000, block=256)])
+    s = native.Simulator(presets.args_for(preset) + ["-trace", kl], False)
+    q = native.Simulator(presets.args_for("QV100") + ["-trace", kl], False)
+    assert s.run() == 0 and q.run() == 0
+    assert s.tot_insn == q.tot_insn and s.tot_cycle > 0 and not s.deadlock
+    # written run directories carry the interconnect file and run from anywhere
+    d = tmp_path / "cfg"
+    presets.write_config(preset, str(d))
+    args = [os.path.join(ROOT, "bin", "accel-sim.out"), "-config", str(d / "gpgpusim.config"),
+            "-config", str(d / "trace.config"), "-trace", kl]
+    p = subprocess.run(args, cwd="/", capture_output=True, text=True)
+    assert p.returncode == 0, p.stdout[-500:] + p.stderr[-500:]
+    assert "gpu_tot_sim_cycle" in p.stdout
