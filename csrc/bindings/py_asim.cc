@@ -128,6 +128,7 @@ py::dict kernel_dict(const KernelResult& k) {
   d["wall_s"] = k.wall_s;
   d["deadlock"] = k.deadlock;
   d["avg_power_w"] = k.avg_power_w;
+  d["epochs"] = k.epochs;
   return d;
 }
 
@@ -137,6 +138,7 @@ PYBIND11_MODULE(_asim, m) {
   m.doc() = "MI355X-native trace-driven GPU simulator (native core)";
   m.attr("sizeof_SMState") = sizeof(SMState);
   m.attr("sizeof_ChanState") = sizeof(ChanState);
+  m.attr("offsetof_SMState_skipped") = offsetof(SMState, skipped_cycles);
   m.attr("sizeof_TInst") = sizeof(TInst);
 
   m.def("gpu_available", &gpu_engine_available, "True if a HIP device is usable by the GPU engine");

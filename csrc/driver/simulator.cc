@@ -376,6 +376,7 @@ void Simulator::do_kernel(const Command& c) {
   }
   r.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   r.deadlock = rr.deadlock;
+  r.epochs = rr.epochs;
   tot_cycle_ = eng_->now();
   tot_insn_ += r.insn;
   tot_warp_insn_ += r.warp_insn;

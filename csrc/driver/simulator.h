@@ -30,6 +30,7 @@ struct KernelResult {
   double wall_s = 0;        // wall time spent simulating this kernel
   bool deadlock = false;
   double avg_power_w = 0;
+  uint64_t epochs = 0;      // PDES epochs simulated (one grid barrier each on the GPU engine)
 };
 
 struct CollectiveResult {

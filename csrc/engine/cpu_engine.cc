@@ -160,7 +160,7 @@ class CpuEngine : public Engine {
         }
       }
       const uint32_t next_done = pub_->next_cta[cur] >= kd_.n_cta ? 1u : 0u;
-      EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, ready, next_done, epoch_);
+      EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, ready, next_done, epoch_, lim.max_cycle);
       ++epoch_;
       ++res.epochs;
       cycle_ = d.next_start;

@@ -35,9 +35,9 @@ namespace asim {
   } while (0)
 
 struct GpuCtl {
-  uint32_t arrive[8][32];     // per-XCD-group arrival counters (padded to 128 B)
-  uint32_t top[32];           // group leaders' counter
-  uint32_t gen[32];           // generation word
+  uint32_t arrive[8][64];     // per-group arrival counters (one 256-B line each)
+  uint32_t gen[8][64];        // per-group generation words: each group polls its own line
+  uint32_t top[64];           // group leaders' counter
   uint32_t error;             // barrier timeout / fault code
   uint32_t done;
   uint32_t deadlock;
@@ -76,8 +76,11 @@ struct GpuArgs {
 // ---------------------------------------------------------------------------
 // grid barrier: blocks are grouped by blockIdx % 8 (which shares an XCD under
 // the observed round-robin placement: a speed hint only, correctness does not
-// depend on it).  Monotonic counters, relaxed polls with s_sleep, one agent
-// release before arriving and one agent acquire after leaving.
+// depend on it).  Monotonic counters; the last arriver of a group forwards to
+// the top counter, the last group leader bumps every group's generation word,
+// and each block polls only its own group's word (relaxed, with s_sleep), so
+// no single line is hammered by every block while the arrivals queue behind
+// it.  One agent release before arriving and one agent acquire after leaving.
 __device__ __forceinline__ bool grid_barrier(GpuCtl* ctl, uint32_t nblocks, uint32_t epoch_in_launch) {
   const uint32_t b = blockIdx.x;
   const uint32_t grp = b & 7u;
@@ -94,17 +97,19 @@ __device__ __forceinline__ bool grid_barrier(GpuCtl* ctl, uint32_t nblocks, uint
     if (prev + 1u == target * in_grp) {
       // last of its group: forward to the top counter
       uint32_t t = __hip_atomic_fetch_add(&ctl->top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t + 1u == target * ngrp) __hip_atomic_store(&ctl->gen[0], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1u == target * ngrp)
+        for (uint32_t g = 0; g < ngrp; ++g)
+          __hip_atomic_store(&ctl->gen[g][0], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     uint64_t spins = 0;
-    while (__hip_atomic_load(&ctl->gen[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1ull << 26)) {  // ~seconds: give up, report, let every block exit
+    while (__hip_atomic_load(&ctl->gen[grp][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1ull << 25)) {  // ~seconds: give up, report, let every block exit
         __hip_atomic_store(&ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = false;
         break;
       }
-      if (__hip_atomic_load(&ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      if ((spins & 15) == 0 && __hip_atomic_load(&ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         ok = false;
         break;
       }
@@ -218,7 +223,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     if (!grid_barrier(a.ctl, a.nblocks, n - 1)) break;
     P::prof(27);  // decision
     const uint32_t next_done = a.pub->next_cta[cur] >= kd.n_cta ? 1u : 0u;
-    EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, a.ready_cycle, next_done, epoch);
+    EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, a.ready_cycle, next_done, epoch, a.max_cycle);
     P::prof(28);
     ++epoch;
     cycle = d.next_start;
@@ -645,11 +650,25 @@ class GpuEngine : public Engine {
         if (b < c_.n_sm) { sm[k] += v / c_.n_sm; smt += v / c_.n_sm; }
         else { mc[k] += v / c_.n_mem; mct += v / c_.n_mem; }
       }
-    fprintf(stderr, "[asim gpu profile] shader-clock cycles per block (mean), share of block time\n");
-    for (int k = 0; k < kProfSlots; ++k)
+    // the critical block: most time outside the barrier wait
+    uint32_t crit = 0;
+    double crit_work = -1;
+    for (uint32_t b = 0; b < nblocks_; ++b) {
+      double w = 0;
+      for (int k = 0; k < kProfSlots; ++k)
+        if (k != 26) w += (double)h[(size_t)b * kProfSlots + k];
+      if (w > crit_work) { crit_work = w; crit = b; }
+    }
+    fprintf(stderr, "[asim gpu profile] shader-clock cycles per block (mean), share of block time; "
+                    "CRIT = block %u (%s), the one with the least barrier wait\n", crit, crit < c_.n_sm ? "SM" : "MEM");
+    double ct = 0;
+    for (int k = 0; k < kProfSlots; ++k) ct += (double)h[(size_t)crit * kProfSlots + k];
+    for (int k = 0; k < kProfSlots; ++k) {
+      const double cv = (double)h[(size_t)crit * kProfSlots + k];
       if (sm[k] + mc[k] > 0)
-        fprintf(stderr, "  %-18s SM %14.0f (%5.1f%%)   MEM %14.0f (%5.1f%%)\n", names[k], sm[k], 100 * sm[k] / smt, mc[k],
-                100 * mc[k] / mct);
+        fprintf(stderr, "  %-18s SM %14.0f (%5.1f%%)   MEM %14.0f (%5.1f%%)   CRIT %14.0f (%5.1f%%)\n", names[k], sm[k],
+                100 * sm[k] / smt, mc[k], 100 * mc[k] / mct, cv, 100 * cv / ct);
+    }
   }
 
  private:

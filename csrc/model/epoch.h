@@ -27,7 +27,15 @@ struct EpochPub {
   uint32_t ch_idle[2][kMaxChTot];
   uint32_t next_cta[2];              // replicated dispatch cursor (published by SM 0)
   uint32_t pad[2];
+  // next-event times (fs, ~0 = none) for whole-epoch fast-forward: the first
+  // instant a unit can change state, or one of the packets it injected this
+  // epoch arrives (-sim_event_skip)
+  uint64_t sm_next[2][kMaxSmTot];
+  uint64_t ch_next[2][kMaxChTot];
 };
+
+// upper bound of one SM's quiet-cycle look-ahead at an epoch boundary
+constexpr uint64_t kSkipHorizon = 1ull << 16;
 
 // decision every participant derives after the barrier
 struct EpochDecision {
@@ -95,6 +103,10 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& 
                       uint64_t t0, uint64_t t1, const Pkt* inbox, const uint32_t* incnt, uint32_t in_cap,
                       uint32_t n_sub, uint64_t epoch_idx) {
   const SimCfg& c = *x.cfg;
+  // 0. cycles [s.cycle, t0) were fast-forwarded by epoch_decide (nothing could
+  //    happen in them): account them exactly like quiet cycles
+  if (t0 > s.cycle && (s.n_cta_active || !sm_idle(s))) sm_skip<P>(s, c, t0 - s.cycle);
+  s.min_emit = ~0ull;
   // 1. arrivals (replies injected by the memory side last epoch)
   P::prof(12);
   gather_sorted<P>(inbox, incnt, s.id, n_sub, in_cap, t0 * c.per_core, s.inq, kInQ, s.inq_head, s.inq_n,
@@ -102,7 +114,9 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& 
   // 2. CTA dispatch (state published at the previous boundary)
   P::prof(13);
   if (t0 >= ks.ready_cycle)
-    cta_dispatch<P>(s, x, ks, pub.sm_req[prev], c.n_sm, (uint32_t)(epoch_idx % c.n_sm));
+    // rotation by simulated time (t0 / epoch length), not by the epoch counter,
+    // so fast-forwarded epochs leave the CTA -> SM assignment unchanged
+    cta_dispatch<P>(s, x, ks, pub.sm_req[prev], c.n_sm, (uint32_t)((t0 / c.icnt_latency) % c.n_sm));
   // 3. trace window refill
   P::prof(14);
   sm_refill_window<P>(s, c, *x.k);
@@ -139,7 +153,12 @@ SIM_HDI void sm_publish(SMState& s, const SmCtx& x, const SmKernel& ks, EpochPub
   const bool ready_for_cta = ks.next_cta < x.k->n_cta;
   const uint32_t req = ready_for_cta ? sm_free_slots(s) : 0u;
   const uint32_t idle = (ks.next_cta >= x.k->n_cta && sm_idle(s)) ? 1u : 0u;
+  uint64_t nx = ~0ull;
+  if (c.event_skip && (s.n_cta_active || !sm_idle(s)))
+    nx = sm_quiet_until<P>(s, c, s.cycle, s.cycle + kSkipHorizon) * c.per_core;
+  nx = amin(nx, s.min_emit);
   P::one([&] {
+    pub.sm_next[cur][s.id] = nx;
     pub.sm_req[cur][s.id] = req;
     pub.sm_idle[cur][s.id] = idle;
     pub.sm_drained[cur][s.id] = sm_idle(s) ? 1u : 0u;
@@ -153,6 +172,7 @@ template <class P>
 SIM_HDI void chan_epoch(ChanState& ch, const MemCtx& x, const Pkt* inbox, const uint32_t* incnt,
                         uint32_t in_cap, uint64_t t0_fs) {
   P::prof(20);
+  ch.min_emit = ~0ull;
   mem_gather<P>(ch, *x.cfg, x, inbox, incnt, in_cap, t0_fs);
   P::one([&] {
     for (uint32_t j = 0; j < x.cfg->n_sub_per_mem; ++j) ch.sp[j].st.icnt_backlog += ch.sp[j].ovf_n;
@@ -166,13 +186,20 @@ template <class P>
 SIM_HDI void chan_publish(ChanState& ch, const MemCtx& x, EpochPub& pub, uint32_t cur) {
   mem_publish<P>(ch, *x.cfg, x.outcnt);
   uint32_t idle = chan_idle(ch, *x.cfg) ? 1u : 0u;
-  P::one([&] { pub.ch_idle[cur][ch.id] = idle; });
+  uint64_t nx = ~0ull;
+  if (x.cfg->event_skip) nx = chan_next_event(ch, *x.cfg, amin(ch.t_dram, amin(ch.t_l2, ch.t_icnt)));
+  nx = amin(nx, ch.min_emit);
+  P::one([&] {
+    pub.ch_idle[cur][ch.id] = idle;
+    pub.ch_next[cur][ch.id] = nx;
+  });
 }
 
 // every participant computes the same decision from the published state
 template <class P>
 SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_t cur, uint64_t t1,
-                                   uint64_t ready_cycle, uint32_t next_cta_done, uint64_t epoch_idx) {
+                                   uint64_t ready_cycle, uint32_t next_cta_done, uint64_t epoch_idx,
+                                   uint64_t max_cycle) {
   EpochDecision d;
   uint32_t nbusy = P::sum((int)c.n_sm, [&](int j) -> uint32_t { return pub.sm_idle[cur][j] ? 0u : 1u; });
   uint32_t cbusy = P::sum((int)c.n_mem, [&](int j) -> uint32_t { return pub.ch_idle[cur][j] ? 0u : 1u; });
@@ -190,7 +217,29 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
       d.next_start = t1 + skip;
     }
   }
-  if (c.deadlock_window && nbusy && (epoch_idx & 63) == 0) {
+  // Whole-epoch fast-forward (conservative PDES with exact next-event times):
+  // the earliest instant any SM or channel can change state, any packet in
+  // flight arrives, or the next CTA can be dispatched bounds how far every
+  // participant can jump; epochs wholly before it are skipped.  With no
+  // pending event at all (a deadlock) nothing is skipped.
+  if (c.event_skip && !d.done) {
+    const int js = P::argmin((int)c.n_sm, [&](int j) -> uint64_t { return pub.sm_next[cur][j]; });
+    const int jc = P::argmin((int)c.n_mem, [&](int j) -> uint64_t { return pub.ch_next[cur][j]; });
+    uint64_t ev = js >= 0 ? pub.sm_next[cur][js] : ~0ull;
+    if (jc >= 0) ev = amin(ev, pub.ch_next[cur][jc]);
+    if (!next_cta_done && P::sum((int)c.n_sm, [&](int j) -> uint32_t { return pub.sm_req[cur][j] ? 1u : 0u; }))
+      ev = amin(ev, amax(t1, ready_cycle) * c.per_core);
+    if (ev != ~0ull) {
+      const uint64_t E = c.icnt_latency;
+      const uint64_t tc = ev / c.per_core;  // the next epoch may start no later than this
+      if (tc >= t1 + E) {
+        uint64_t s = t1 + (tc - t1) / E * E;
+        if (max_cycle && s > max_cycle) s = max_cycle > t1 ? t1 + (max_cycle - t1 + E - 1) / E * E : t1;
+        if (s > d.next_start) d.next_start = s;
+      }
+    }
+  }
+  if (c.deadlock_window && nbusy && ((t1 / c.icnt_latency) & 63) == 0) {
     // newest progress stamp over all SMs (progress stamps are < 2^56)
     int jm = P::argmin((int)c.n_sm, [&](int j) -> uint64_t { return ~pub.sm_prog[cur][j] & ((1ull << 56) - 1); });
     uint64_t last = jm >= 0 ? pub.sm_prog[cur][jm] : 0;

@@ -119,6 +119,7 @@ struct alignas(16) ChanState {
   uint64_t t_l2;
   uint64_t t_dram;
   uint64_t dcycle;    // dram cycle counter
+  uint64_t min_emit;  // earliest arrival time (fs) of the replies injected this epoch
   // DRAM
   DramReq lat[kDramLat];  // L2 -> DRAM latency pipe (FIFO)
   uint32_t lat_head, lat_n;
@@ -478,6 +479,7 @@ SIM_HDI void mem_icnt_cycle(ChanState& ch, SubPart& sp, const SimCfg& c, const M
       uint32_t n = sp_out_count(ch, sub, r.dst);
       if (n < x.out_cap) {
         r.t = done + icnt_pkt_lat_fs(c, r.dst, gsub);
+        ch.min_emit = amin(ch.min_emit, r.t);
         P::one([&] { x.outbox[(uint64_t)cell * x.out_cap + n] = r; });
         sp_out_count_inc(ch, sub, r.dst);
         sp.rep_head = (sp.rep_head + 1) % kReplyQ;
@@ -691,6 +693,49 @@ SIM_HDI uint64_t next_tick(uint64_t t, uint64_t per, uint64_t t1) {
   return t + k * per;
 }
 
+// Earliest time (fs) at which a tick of this channel can do more than add its
+// per-tick statistics; `now` when something may happen right away.  A
+// request that is ready but blocked (full queue, no credit) also counts as
+// "now", so only pure waiting is skipped: requests riding the ROP delay
+// queue, the L2->DRAM latency pipe or the DRAM data return, and arrivals not
+// yet due.  Busy DRAM scheduler queues are never skipped (bank timing
+// changes every cycle).  ~0 = nothing pending at all.
+SIM_HDI uint64_t chan_next_event(const ChanState& ch, const SimCfg& c, uint64_t now) {
+  if (ch.q_n) return now;
+  uint64_t nx = ~0ull;
+  if (ch.lat_n) nx = amin(nx, ch.lat[ch.lat_head].ready);
+  if (ch.ret_n) nx = amin(nx, ch.ret[ch.ret_head].ready);
+  for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
+    const SubPart& sp = ch.sp[j];
+    if (sp.rep_n || sp.ovf_n) return now;
+    if (sp.fill_n) nx = amin(nx, sp.fill[sp.fill_head].ready);
+    if (sp.rop_n) nx = amin(nx, sp.rop[sp.rop_head].t);
+    if (sp.inq_n && sp.rop_n < (uint32_t)kRopQ && sp.rop_n < c.q_icnt_l2 + c.rop_latency)
+      nx = amin(nx, sp.inq[sp.inq_head].t);
+  }
+  return nx > now ? nx : now;
+}
+
+// advance every clock domain of a quiet channel to its first tick >= target,
+// adding exactly the statistics those ticks would have added (l2_cycle /
+// dram_cycle with nothing ready)
+SIM_HDI void chan_quiet_advance(ChanState& ch, const SimCfg& c, uint64_t target) {
+  const uint64_t nd = next_tick(ch.t_dram, c.per_dram, target);
+  const uint64_t kd = (nd - ch.t_dram) / c.per_dram;
+  ch.sp[0].st.dram_cycles += kd;
+  ch.sp[0].st.dram_q_occ += (uint64_t)ch.q_n * kd;
+  ch.dcycle += kd;
+  ch.t_dram = nd;
+  const uint64_t nl = next_tick(ch.t_l2, c.per_l2, target);
+  const uint64_t kl = (nl - ch.t_l2) / c.per_l2;
+  for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
+    ch.sp[j].st.l2_cycles += kl;
+    ch.sp[j].st.rop_occ += (uint64_t)ch.sp[j].rop_n * kl;
+  }
+  ch.t_l2 = nl;
+  ch.t_icnt = next_tick(ch.t_icnt, c.per_icnt, target);
+}
+
 // simulate all memory-side clock ticks in [.., x.win_end)
 template <class P>
 SIM_HDI void mem_window(ChanState& ch, const MemCtx& x) {
@@ -711,6 +756,14 @@ SIM_HDI void mem_window(ChanState& ch, const MemCtx& x) {
   for (;;) {
     uint64_t tm = amin(ch.t_dram, amin(ch.t_l2, ch.t_icnt));
     if (tm >= t1) break;
+    if (c.event_skip) {
+      // fast-forward ticks in which provably nothing but statistics happens
+      const uint64_t nx = chan_next_event(ch, c, tm);
+      if (nx > tm) {
+        chan_quiet_advance(ch, c, amin(nx, t1));
+        continue;
+      }
+    }
     if (ch.t_dram == tm) {
       P::prof(21);
       dram_cycle<P>(ch, c, tm);

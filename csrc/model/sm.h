@@ -217,6 +217,7 @@ struct alignas(16) SMState {
   uint64_t wb_occ[kWbRing / 64];
   uint64_t hit_occ[kHitRing / 64];
   uint64_t skipped_cycles;  // quiet cycles fast-forwarded inside epochs (diagnostic)
+  uint64_t min_emit;        // earliest arrival time (fs) of the packets injected this epoch
   // ---- interconnect endpoints ----
   Pkt outq[kOutQ];
   uint32_t outq_head, outq_n;
@@ -311,6 +312,7 @@ SIM_HDI void sm_inject(SMState& s, const SmCtx& x, uint64_t now) {
   if (n >= x.out_cap) return;  // outbox cell full (cannot happen with cap >= epoch)
   s.ocnt[dst] = n + 1;
   p.t = done * c.per_core + icnt_pkt_lat_fs(c, s.id, dst);
+  s.min_emit = amin(s.min_emit, p.t);
   if (trace_sm_on(c, TS_INTERCONNECT, s.id)) P::one([&] { trace_put(c, s.id, now, EV_PKT_SEND, (uint16_t)dst, p.addr); });
   P::one([&] {
     x.outbox[(uint64_t)slot * x.out_cap + n] = p;

@@ -20,16 +20,18 @@ def main():
     from accel_sim_framework_distributed_amd import sim
     from accel_sim_framework_distributed_amd.tracegen import rodinia
     d = tempfile.mkdtemp()
-    gen = {"hotspot": lambda: rodinia.hotspot(256, 2, 6), "heartwall": lambda: rodinia.heartwall(51, scale=2.0),
-           "backprop": lambda: rodinia.backprop(4096), "bfs": lambda: rodinia.bfs(4096),
-           "vadd": lambda: [rodinia.vectoradd()]}[a.app]
+    gen = {"vadd": lambda: [rodinia.vectoradd()]}
+    for name, (_, g) in rodinia.SUITE.items():
+        gen[name.split("-")[0]] = g
+    gen = gen[a.app]
     kl = rodinia.write_app(os.path.join(d, a.app), gen())
     s = sim.Simulator("QV100", kl, engine=a.engine, torch_runtime=True)
     t = time.perf_counter()
     r = s.run()
     dt = time.perf_counter() - t
     print(f"{a.app}: insn={r.tot_insn} cycles={r.tot_cycle} wall={dt:.3f}s sim={r.sim_s:.3f}s "
-          f"KIPS={r.tot_insn / dt / 1e3:.1f} kernels={len(r.kernels)}", flush=True)
+          f"KIPS={r.tot_insn / dt / 1e3:.1f} kernels={len(r.kernels)} "
+          f"epochs={sum(k.get('epochs', 0) for k in r.kernels)}", flush=True)
     del s
 
 
