@@ -69,7 +69,7 @@ class DistributedSuite:
                 if os.path.exists(kl):
                     self.apps.append((app, kl))
         self.max_concurrency = None
-        self.weights: Dict[str, int] = {}
+        self.weights: Dict[str, float] = {}  # last wall time per app (LPT order)
         ar = os.path.join(root, "all-reduce", "kernelslist.g")
         self.allreduce = ar if os.path.exists(ar) else None
         self.sync = PacketCollective() if collective_model == "packet" else CollectiveSync(world)
@@ -90,11 +90,14 @@ class DistributedSuite:
         return max(1, cus // per) if cus else 1
 
     def _run_app(self, app_kl):
+        import time
         app, kl = app_kl
+        t0 = time.perf_counter()
         s = self._sim(kl)
         rc = s.run()
         if rc != 0:
             raise RuntimeError(f"{app}: simulation failed (deadlock={s.deadlock})\n{s.output[-1500:]}")
+        self.weights[app] = time.perf_counter() - t0
         return app, s.tot_insn, s.tot_cycle
 
     def step(self) -> Dict:
@@ -105,15 +108,14 @@ class DistributedSuite:
             results = [self._run_app(x) for x in self.apps]
         else:
             from concurrent.futures import ThreadPoolExecutor
-            # longest first keeps both CU groups busy
-            order = sorted(self.apps, key=lambda x: -self.weights.get(x[0], 0))
+            # longest (by last measured wall time) first: greedy LPT over the CU groups
+            order = sorted(self.apps, key=lambda x: -self.weights.get(x[0], 0.0))
             with ThreadPoolExecutor(max_workers=conc) as ex:
                 results = list(ex.map(self._run_app, order))
         for app, i, c in results:
             insn += i
             cycles += c
-            per_app[app] = dict(insn=i, cycles=c)
-            self.weights[app] = i
+            per_app[app] = dict(insn=i, cycles=c, wall_s=self.weights.get(app, 0.0))
         if self.allreduce:
             s = self._sim(self.allreduce)
             s.set_collective_hook(lambda d, now, s=s: self.sync(s, d, now))

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "grid_barrier.h"
 #include "wave_par.h"
 
 namespace asim {
@@ -34,21 +35,9 @@ namespace asim {
       throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x);    \
   } while (0)
 
-struct GpuCtl {
-  uint32_t arrive[8][64];     // per-group arrival counters (one 256-B line each)
-  uint32_t gen[8][64];        // per-group generation words: each group polls its own line
-  uint32_t top[64];           // group leaders' counter
-  uint32_t error;             // barrier timeout / fault code
-  uint32_t done;
-  uint32_t deadlock;
-  uint32_t pad;
-  uint64_t end_cycle;
-  uint64_t end_epoch;
-  uint64_t epochs_run;
-};
-
 struct GpuArgs {
-  const SimCfg* cfg;
+  SimCfg cfg;          // by value: kernel-argument (constant) memory, read with scalar loads
+  const SimCfg* cfg_g; // device copy (host-side bookkeeping only)
   KernelDesc kd;
   const TAcc* acc;
   SMState* sms;
@@ -73,54 +62,6 @@ struct GpuArgs {
   uint64_t* prof;  // [nblocks][kProfSlots] shader-clock cycles per stage (profiling build)
 };
 
-// ---------------------------------------------------------------------------
-// grid barrier: blocks are grouped by blockIdx % 8 (which shares an XCD under
-// the observed round-robin placement: a speed hint only, correctness does not
-// depend on it).  Monotonic counters; the last arriver of a group forwards to
-// the top counter, the last group leader bumps every group's generation word,
-// and each block polls only its own group's word (relaxed, with s_sleep), so
-// no single line is hammered by every block while the arrivals queue behind
-// it.  One agent release before arriving and one agent acquire after leaving.
-__device__ __forceinline__ bool grid_barrier(GpuCtl* ctl, uint32_t nblocks, uint32_t epoch_in_launch) {
-  const uint32_t b = blockIdx.x;
-  const uint32_t grp = b & 7u;
-  const uint32_t ngrp = nblocks < 8 ? nblocks : 8u;
-  const uint32_t in_grp = (nblocks - grp + 7u) / 8u;  // members of this group
-  const uint32_t target = epoch_in_launch + 1u;
-  bool ok = true;
-  // every lane's stores must be complete and visible at agent scope
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0) {
-    uint32_t prev = __hip_atomic_fetch_add(&ctl->arrive[grp][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev + 1u == target * in_grp) {
-      // last of its group: forward to the top counter
-      uint32_t t = __hip_atomic_fetch_add(&ctl->top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t + 1u == target * ngrp)
-        for (uint32_t g = 0; g < ngrp; ++g)
-          __hip_atomic_store(&ctl->gen[g][0], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    uint64_t spins = 0;
-    while (__hip_atomic_load(&ctl->gen[grp][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1ull << 25)) {  // ~seconds: give up, report, let every block exit
-        __hip_atomic_store(&ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = false;
-        break;
-      }
-      if ((spins & 15) == 0 && __hip_atomic_load(&ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        ok = false;
-        break;
-      }
-    }
-  }
-  ok = __shfl(ok ? 1 : 0, 0, 64) != 0;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  return ok;
-}
-
 template <class T>
 __device__ __forceinline__ void copy_state(T* dst, const T* src) {
   static_assert(sizeof(T) % 16 == 0, "state must be 16-byte granular");
@@ -133,7 +74,8 @@ __device__ __forceinline__ void copy_state(T* dst, const T* src) {
 
 extern __shared__ __attribute__((aligned(16))) char g_lds[];
 constexpr size_t kStateLds = ((sizeof(SMState) > sizeof(ChanState) ? sizeof(SMState) : sizeof(ChanState)) + 15) / 16 * 16;
-constexpr size_t kProfOff = kStateLds + (sizeof(KernelDesc) + 15) / 16 * 16;
+constexpr size_t kCfgOff = kStateLds + (sizeof(KernelDesc) + 15) / 16 * 16;
+constexpr size_t kProfOff = kCfgOff + (sizeof(SimCfg) + 15) / 16 * 16;
 constexpr int kProfSlots = 32;
 struct ProfLds {
   uint64_t last;
@@ -157,12 +99,22 @@ struct WaveParProf : WavePar {
     }
     __builtin_amdgcn_wave_barrier();
   }
+  // event counters in the spare slots (not time): P::tick(k) adds one
+  static __device__ __forceinline__ void tick(int k) {
+    ProfLds* p = reinterpret_cast<ProfLds*>(g_lds + kProfOff);
+    if ((threadIdx.x & 63) == 0) p->acc[k] += 1;
+    __builtin_amdgcn_wave_barrier();
+  }
 };
 
 template <class P>
 __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   const uint32_t b = blockIdx.x;
-  const SimCfg& c = *a.cfg;  // read-only, scalar-cached
+  // The configuration is read all over the model.  As a by-value kernel
+  // argument it lives in constant memory: every field is a scalar load into
+  // an SGPR (uniform, invariant across the epoch fences), not a vector load
+  // behind each acquire or an LDS round trip into a VGPR.
+  const SimCfg& c = a.cfg;
   const bool is_sm = b < c.n_sm;
   const uint64_t E = c.icnt_latency;
   SMState* s = reinterpret_cast<SMState*>(g_lds);
@@ -226,9 +178,9 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, a.ready_cycle, next_done, epoch, a.max_cycle);
     P::prof(28);
     ++epoch;
-    cycle = d.next_start;
-    if (d.done) { done = 1; break; }
-    if (d.deadlock) { dead = 1; break; }
+    cycle = P::uni(d.next_start);
+    if (P::uni(d.done)) { done = 1; break; }
+    if (P::uni(d.deadlock)) { dead = 1; break; }
     if (a.max_cycle && cycle >= a.max_cycle) break;
   }
   P::prof(kProfSlots - 1);
@@ -382,7 +334,8 @@ class GpuEngine : public Engine {
     bool first = !lim.resume;
     for (;;) {
       GpuArgs a{};
-      a.cfg = d_cfg_;
+      a.cfg = c_;
+      a.cfg_g = d_cfg_;
       a.kd = kd_;
       a.acc = reinterpret_cast<const TAcc*>(d_accs_);
       a.sms = d_sms_;
@@ -641,28 +594,44 @@ class GpuEngine : public Engine {
     static const char* names[kProfSlots] = {
         "sm.receive", "sm.writeback", "sm.hit_complete", "sm.ldst", "sm.dispatch", "sm.read_operands",
         "sm.alloc_oc", "sm.issue", "sm.fetch", "sm.retire", "sm.inject", "sm.occupancy", "sm.gather",
-        "sm.cta_dispatch", "sm.refill", "sm.cycle_loop", "sm.publish", "-", "-", "-", "mem.gather", "mem.dram",
+        "sm.cta_dispatch", "sm.refill", "sm.cycle_loop", "sm.publish", "#sm_cycles", "#quiet_checks", "#epochs_busy", "mem.gather", "mem.dram",
         "mem.l2", "mem.icnt", "mem.window_other", "mem.publish", "barrier", "decide", "post", "-", "-", "launch_rest"};
     double sm[kProfSlots] = {}, mc[kProfSlots] = {}, smt = 0, mct = 0;
     for (uint32_t b = 0; b < nblocks_; ++b)
       for (int k = 0; k < kProfSlots; ++k) {
         double v = (double)h[(size_t)b * kProfSlots + k];
-        if (b < c_.n_sm) { sm[k] += v / c_.n_sm; smt += v / c_.n_sm; }
-        else { mc[k] += v / c_.n_mem; mct += v / c_.n_mem; }
+        const bool counter = k >= 17 && k <= 19;
+        if (b < c_.n_sm) { sm[k] += v / c_.n_sm; smt += counter ? 0 : v / c_.n_sm; }
+        else { mc[k] += v / c_.n_mem; mct += counter ? 0 : v / c_.n_mem; }
       }
+    // per simulated SM cycle: the SM-cycle stages (slots 0..11) over all SM blocks
+    {
+      double cyc_clk = 0, n_cyc = 0, n_q = 0, n_ep = 0, q_clk = 0;
+      for (uint32_t b = 0; b < c_.n_sm; ++b) {
+        for (int k = 0; k <= 11; ++k) cyc_clk += (double)h[(size_t)b * kProfSlots + k];
+        q_clk += (double)h[(size_t)b * kProfSlots + 15];
+        n_cyc += (double)h[(size_t)b * kProfSlots + 17];
+        n_q += (double)h[(size_t)b * kProfSlots + 18];
+        n_ep += (double)h[(size_t)b * kProfSlots + 19];
+      }
+      fprintf(stderr, "[asim gpu profile] SM cycles simulated %.0f (%.0f clocks each), quiet checks %.0f "
+                      "(cycle_loop %.0f clocks each), busy SM-epochs %.0f\n",
+              n_cyc, n_cyc ? cyc_clk / n_cyc : 0, n_q, n_q ? q_clk / n_q : 0, n_ep);
+    }
     // the critical block: most time outside the barrier wait
     uint32_t crit = 0;
     double crit_work = -1;
     for (uint32_t b = 0; b < nblocks_; ++b) {
       double w = 0;
       for (int k = 0; k < kProfSlots; ++k)
-        if (k != 26) w += (double)h[(size_t)b * kProfSlots + k];
+        if (k != 26 && !(k >= 17 && k <= 19)) w += (double)h[(size_t)b * kProfSlots + k];
       if (w > crit_work) { crit_work = w; crit = b; }
     }
     fprintf(stderr, "[asim gpu profile] shader-clock cycles per block (mean), share of block time; "
                     "CRIT = block %u (%s), the one with the least barrier wait\n", crit, crit < c_.n_sm ? "SM" : "MEM");
     double ct = 0;
-    for (int k = 0; k < kProfSlots; ++k) ct += (double)h[(size_t)crit * kProfSlots + k];
+    for (int k = 0; k < kProfSlots; ++k)
+      if (!(k >= 17 && k <= 19)) ct += (double)h[(size_t)crit * kProfSlots + k];
     for (int k = 0; k < kProfSlots; ++k) {
       const double cv = (double)h[(size_t)crit * kProfSlots + k];
       if (sm[k] + mc[k] > 0)

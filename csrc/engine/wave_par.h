@@ -30,45 +30,109 @@ struct WavePar {
     if (lane() == 0) f();
   }
   static __device__ __forceinline__ void prof(int) {}
+  static __device__ __forceinline__ void tick(int) {}
+  // Values read from LDS state land in VGPRs (the compiler cannot know that
+  // every lane read the same word), so all arithmetic and control flow
+  // derived from them runs as 64-lane VALU code with exec masking.
+  // readfirstlane makes the value -- and what is computed from it -- scalar.
+  template <class T>
+  static __device__ __forceinline__ T uni(T v) {
+    static_assert(sizeof(T) <= 4 || sizeof(T) % 4 == 0, "uni: 1/2/4-byte or word-multiple types");
+    if constexpr (sizeof(T) <= 4) {
+      uint32_t u = 0;
+      __builtin_memcpy(&u, &v, sizeof(T));
+      u = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
+      T r;
+      __builtin_memcpy(&r, &u, sizeof(T));
+      return r;
+    } else {
+      uint32_t w[sizeof(T) / 4];
+      __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+      for (int i = 0; i < (int)(sizeof(T) / 4); ++i) w[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)w[i]);
+      T r;
+      __builtin_memcpy(&r, w, sizeof(T));
+      return r;
+    }
+  }
+
   static __device__ __forceinline__ void sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
-  static __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-    lo = __shfl_xor(lo, m, 64);
-    hi = __shfl_xor(hi, m, 64);
-    return ((uint64_t)hi << 32) | lo;
+  // ---- cross-lane reductions on DPP row operations (no LDS traffic) ----
+  // Every reduction runs in wave-uniform control flow with all 64 lanes
+  // active.  Within a 16-lane row: quad_perm xor 1 / xor 2, row_half_mirror,
+  // row_mirror (each a register-to-register v_mov_dpp); across the 4 rows:
+  // v_readlane into SGPRs.  A __shfl_xor reduction compiles to ds_bpermute,
+  // an LDS round trip per step (~6 dependent LDS latencies per reduction).
+  template <int Ctrl>
+  static __device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, Ctrl, 0xf, 0xf, false);
+  }
+  static __device__ __forceinline__ uint32_t rdl(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+  }
+  template <class Op>
+  static __device__ __forceinline__ uint32_t row_reduce(uint32_t v, Op op) {
+    v = op(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = op(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = op(v, dpp<0x141>(v));  // row_half_mirror
+    v = op(v, dpp<0x140>(v));  // row_mirror
+    return v;
+  }
+  template <class Op>
+  static __device__ __forceinline__ uint32_t wave_reduce(uint32_t v, Op op) {
+    v = row_reduce(v, op);
+    return op(op(rdl(v, 0), rdl(v, 16)), op(rdl(v, 32), rdl(v, 48)));
+  }
+  // (key, index) pair: smaller key wins, ties to the smaller index
+  static __device__ __forceinline__ bool kless(uint32_t ah, uint32_t al, uint32_t ai, uint32_t bh, uint32_t bl,
+                                               uint32_t bi) {
+    return ah < bh || (ah == bh && (al < bl || (al == bl && ai < bi)));
+  }
+  template <int Ctrl>
+  static __device__ __forceinline__ void kstep(uint32_t& h, uint32_t& l, uint32_t& i) {
+    const uint32_t oh = dpp<Ctrl>(h), ol = dpp<Ctrl>(l), oi = dpp<Ctrl>(i);
+    if (kless(oh, ol, oi, h, l, i)) {
+      h = oh;
+      l = ol;
+      i = oi;
+    }
   }
   template <class F>
   static __device__ __forceinline__ int argmin(int n, F&& key) {
     uint64_t best = ~0ull;
-    int bi = 0x7fffffff;
+    uint32_t bi = 0x7fffffffu;
     for (int i = lane(); i < n; i += 64) {
       uint64_t k = key(i);
-      if (k != ~0ull && (k < best || (k == best && i < bi))) {
+      if (k != ~0ull && (k < best || (k == best && (uint32_t)i < bi))) {
         best = k;
-        bi = i;
+        bi = (uint32_t)i;
       }
     }
+    uint32_t h = (uint32_t)(best >> 32), l = (uint32_t)best;
+    kstep<0xB1>(h, l, bi);
+    kstep<0x4E>(h, l, bi);
+    kstep<0x141>(h, l, bi);
+    kstep<0x140>(h, l, bi);
+    uint32_t rh = rdl(h, 0), rl = rdl(l, 0), ri = rdl(bi, 0);
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      uint64_t ob = shfl_xor64(best, m);
-      int oi = __shfl_xor(bi, m, 64);
-      if (ob < best || (ob == best && oi < bi)) {
-        best = ob;
-        bi = oi;
+    for (int r = 16; r < 64; r += 16) {
+      const uint32_t oh = rdl(h, r), ol = rdl(l, r), oi = rdl(bi, r);
+      if (kless(oh, ol, oi, rh, rl, ri)) {
+        rh = oh;
+        rl = ol;
+        ri = oi;
       }
     }
-    return best == ~0ull ? -1 : bi;
+    return (rh == ~0u && rl == ~0u) ? -1 : (int)ri;
   }
   template <class F>
   static __device__ __forceinline__ uint32_t sum(int n, F&& f) {
     uint32_t s = 0;
     for (int i = lane(); i < n; i += 64) s += f(i);
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
-    return s;
+    return wave_reduce(s, [](uint32_t a, uint32_t b) { return a + b; });
   }
   template <class F>
   static __device__ __forceinline__ uint32_t vmax(int n, F&& f) {
@@ -77,21 +141,18 @@ struct WavePar {
       uint32_t v = f(i);
       s = v > s ? v : s;
     }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      uint32_t o = __shfl_xor(s, m, 64);
-      s = o > s ? o : s;
-    }
-    return s;
+    return wave_reduce(s, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
   }
   template <class F>
   static __device__ __forceinline__ uint64_t vor(int n, F&& f) {
     uint64_t s = 0;
     for (int i = lane(); i < n; i += 64) s |= f(i);
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) s |= shfl_xor64(s, m);
-    return s;
+    auto o = [](uint32_t a, uint32_t b) { return a | b; };
+    const uint32_t lo = wave_reduce((uint32_t)s, o), hi = wave_reduce((uint32_t)(s >> 32), o);
+    return ((uint64_t)hi << 32) | lo;
   }
+  // exclusive scan: within-row Hillis-Steele on row_shr:1/2/4/8 (lanes
+  // shifted in from outside the row read 0), then the row totals via readlane
   template <class F, class G>
   static __device__ __forceinline__ uint32_t scan(int n, F&& val, G&& out) {
     uint32_t carry = 0;
@@ -100,13 +161,15 @@ struct WavePar {
       const int i = b + l;
       uint32_t v = i < n ? val(i) : 0u;
       uint32_t inc = v;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        uint32_t o = __shfl_up(inc, d, 64);
-        if (l >= d) inc += o;
-      }
+      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x111, 0xf, 0xf, false);  // row_shr:1
+      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x112, 0xf, 0xf, false);  // row_shr:2
+      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x114, 0xf, 0xf, false);  // row_shr:4
+      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x118, 0xf, 0xf, false);  // row_shr:8
+      const uint32_t t0 = rdl(inc, 15), t1 = rdl(inc, 31), t2 = rdl(inc, 47), t3 = rdl(inc, 63);
+      const int row = l >> 4;
+      inc += row == 0 ? 0u : row == 1 ? t0 : row == 2 ? t0 + t1 : t0 + t1 + t2;
       if (i < n) out(i, carry + inc - v);
-      carry += __shfl(inc, 63, 64);
+      carry += t0 + t1 + t2 + t3;
     }
     return carry;
   }

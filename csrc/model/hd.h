@@ -63,6 +63,11 @@ struct SeqPar {
   // stage profiling stamp (no-op on the CPU; the GPU profiling build records
   // s_memtime deltas per stage)
   static SIM_HDI void prof(int) {}
+  static SIM_HDI void tick(int) {}
+  // wave-uniform value hint (identity here; readfirstlane on the GPU so that
+  // the compiler keeps the value and everything derived from it in SGPRs)
+  template <class T>
+  static SIM_HDI T uni(T v) { return v; }
   // index i < n minimising key(i) (ties -> lowest i); key == ~0ull means
   // "not a candidate".  Returns -1 if there is no candidate.
   template <class F>

@@ -300,15 +300,15 @@ SIM_HDI void sm_send(SMState& s, const SimCfg& c, uint8_t type, uint64_t line, u
 template <class P>
 SIM_HDI void sm_inject(SMState& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
-  if (s.outq_n == 0) return;
-  if (now < s.out_port_free) return;
-  Pkt p = s.outq[s.outq_head];
+  if (P::uni(s.outq_n) == 0) return;
+  if (now < P::uni(s.out_port_free)) return;
+  Pkt p = P::uni(s.outq[P::uni(s.outq_head)]);
   uint32_t nflits = (p.size + c.flit_size - 1) / c.flit_size;
   uint64_t done = now + nflits - 1;
   if (done >= s.epoch_end) return;  // completes next epoch
   uint32_t dst = p.dst;
   uint32_t slot = dst * x.n_src_sm + s.id;
-  uint32_t n = s.ocnt[dst];
+  uint32_t n = P::uni(s.ocnt[dst]);
   if (n >= x.out_cap) return;  // outbox cell full (cannot happen with cap >= epoch)
   s.ocnt[dst] = n + 1;
   p.t = done * c.per_core + icnt_pkt_lat_fs(c, s.id, dst);
@@ -331,9 +331,9 @@ SIM_HDI void sm_inject(SMState& s, const SmCtx& x, uint64_t now) {
 template <class P>
 SIM_HDI void sm_writeback(SMState& s, const SimCfg& c, uint64_t now) {
   uint32_t slot = (uint32_t)(now % kWbRing);
-  uint32_t n = s.wb_cnt[slot];
+  uint32_t n = P::uni(s.wb_cnt[slot]);
   for (uint32_t i = 0; i < n; ++i) {
-    WbEnt e = s.wb[slot][i];
+    WbEnt e = P::uni(s.wb[slot][i]);
     if (trace_sm_on(c, TS_SCOREBOARD, s.id))
       P::one([&] {
         if (e.dst0) trace_put(c, s.id, now, EV_SB_RELEASE, e.warp, e.dst0 - 1u);
@@ -363,9 +363,9 @@ SIM_HDI void sm_load_slot_done(SMState& s, uint32_t w, uint32_t slot, uint64_t n
 template <class P>
 SIM_HDI void sm_hit_complete(SMState& s, uint64_t now) {
   uint32_t slot = (uint32_t)(now % kHitRing);
-  uint32_t n = s.hit_cnt[slot];
+  uint32_t n = P::uni(s.hit_cnt[slot]);
   for (uint32_t i = 0; i < n; ++i) {
-    HitEnt e = s.hit[slot][i];
+    HitEnt e = P::uni(s.hit[slot][i]);
     if (e.kind == 0) {
       if (--s.w_slot_pend[e.warp][e.slot] == 0) sm_load_slot_done(s, e.warp, e.slot, now);
     } else {
@@ -548,10 +548,9 @@ SIM_HDI bool il1_fetch(SMState& s, const SimCfg& c, uint32_t w) {
 template <class P>
 SIM_HDI void sm_receive(SMState& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
-  if (s.inq_n == 0) return;
-  const Pkt& p = s.inq[s.inq_head];
-  if (p.t > now * c.per_core) return;
-  Pkt q = p;
+  if (P::uni(s.inq_n) == 0) return;
+  const Pkt q = P::uni(s.inq[P::uni(s.inq_head)]);
+  if (q.t > now * c.per_core) return;
   if (trace_sm_on(c, TS_INTERCONNECT, s.id)) P::one([&] { trace_put(c, s.id, now, EV_PKT_RECV, q.type, q.addr); });
   s.inq_head = (s.inq_head + 1) % kInQ;
   s.inq_n--;
@@ -584,15 +583,15 @@ template <class P>
 SIM_HDI void sm_ldst(SMState& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
   LdstState& u = s.ldst;
-  if (!u.busy) return;
-  const TInst& in = u.inst;
-  const uint32_t w = u.warp;
+  if (!P::uni(u.busy)) return;
+  const TInst in = P::uni(u.inst);
+  const uint32_t w = P::uni(u.warp);
   if (in.space == S_SHARED) {
     // bank-conflict serialisation: nacc == conflict degree (precomputed)
     uint32_t deg = in.width ? in.width : 1;
-    if ((uint32_t)(now - u.start) + 1 < deg) return;
+    if ((uint32_t)(now - P::uni(u.start)) + 1 < deg) return;
     uint8_t kind = (in.cls == OC_STORE) ? 1 : 0;
-    if (!hit_push(s, now + c.smem_latency, (uint8_t)w, u.slot, kind)) return;
+    if (!hit_push(s, now + c.smem_latency, (uint8_t)w, P::uni(u.slot), kind)) return;
     s.st.shmem_acc++;
     s.st.shmem_conflict_cycles += deg - 1;
     u.busy = 0;
@@ -606,14 +605,16 @@ SIM_HDI void sm_ldst(SMState& s, const SmCtx& x, uint64_t now) {
   const uint32_t stype = l1_stat_type(in.space, is_store, atomic);
   uint32_t banks_used = 0;
   uint32_t processed = 0;
-  while (u.next < nacc && processed < c.l1_banks) {
-    const TAcc a = x.acc[in.mem + u.next];
+  uint32_t unext = P::uni(u.next);
+  const uint8_t uslot = P::uni(u.slot);
+  while (unext < nacc && processed < c.l1_banks) {
+    const TAcc a = P::uni(x.acc[in.mem + unext]);
     uint32_t bbit = 1u << (a.bank & 31);
     if (banks_used & bbit) break;  // L1 bank conflict: next cycle
     if (c.perfect_mem) {
       // ideal memory: loads/atomics return after the L1 latency, stores retire at once
       if (!is_store) {
-        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, u.slot, 0)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, uslot, 0)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
       }
       s.st.l1[stype][L1O_HIT]++;
     } else if (is_store) {
@@ -628,7 +629,7 @@ SIM_HDI void sm_ldst(SMState& s, const SmCtx& x, uint64_t now) {
       s.st.l1[stype][bypass ? L1O_BYPASS : L1O_MISS]++;
     } else if (bypass) {
       if (!sm_can_send(s, c)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
-      uint32_t tag = 0x80000000u | (u.slot << 8) | w;
+      uint32_t tag = 0x80000000u | ((uint32_t)uslot << 8) | w;
       sm_send(s, c, atomic ? P_ATOM : P_RD, a.line, a.sectors, a.bytes, tag);
       s.st.l1[stype][L1O_BYPASS]++;
     } else {
@@ -637,7 +638,7 @@ SIM_HDI void sm_ldst(SMState& s, const SmCtx& x, uint64_t now) {
       uint8_t have = way >= 0 ? s.l1[set * g.assoc + way].valid : 0;
       uint8_t miss = a.sectors & (uint8_t)~have;
       if (miss == 0) {
-        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, u.slot, 0)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, uslot, 0)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
         if (g.repl == REPL_LRU) s.l1[set * g.assoc + way].lru = ++s.l1_stamp;
         s.st.l1[stype][L1O_HIT]++;
       } else {
@@ -680,16 +681,17 @@ SIM_HDI void sm_ldst(SMState& s, const SmCtx& x, uint64_t now) {
         e.line = a.line;
         e.need = miss;
         e.warp = (uint8_t)w;
-        e.slot = u.slot;
+        e.slot = uslot;
         e.valid = 1;
         if (pi == s.n_pend) s.n_pend++;
       }
     }
     banks_used |= bbit;
-    u.next++;
+    unext++;
+    u.next = (uint8_t)unext;
     processed++;
   }
-  if (u.next >= nacc) {
+  if (unext >= nacc) {
     if (is_store) {
       s.w_inflight[w]--;  // store instruction leaves the pipeline; acks tracked in w_stores
       s.last_progress = now;
@@ -710,11 +712,12 @@ SIM_HDI uint32_t reg_bank(const SimCfg& c, uint32_t sched, uint32_t warp, uint32
 template <class P>
 SIM_HDI void sm_read_operands(SMState& s, const SimCfg& c) {
   // each register bank serves reg_port_tp reads per cycle, oldest collector first
-  if (!s.oc_read_mask) return;
+  uint32_t rmask = P::uni(s.oc_read_mask);
+  if (!rmask) return;
   const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
-  for (uint32_t round = 0; round < c.reg_port_tp && s.oc_read_mask; ++round) {
+  for (uint32_t round = 0; round < c.reg_port_tp && rmask; ++round) {
     uint32_t bank_busy = 0;
-    const uint32_t want = s.oc_read_mask;
+    const uint32_t want = rmask;
     for (int k = 0; k < noc; ++k) {
       // visit collectors oldest-first
       int best = P::argmin(noc, [&](int i) -> uint64_t {
@@ -728,11 +731,16 @@ SIM_HDI void sm_read_operands(SMState& s, const SimCfg& c) {
       if (best < 0) break;
       OCUnit& o = s.oc[best];
       for (int j = 0; j < 5; ++j) {
-        if (o.banks[j] != 0xff && !(bank_busy >> o.banks[j] & 1u)) {
-          bank_busy |= 1u << o.banks[j];
+        const uint32_t bj = P::uni(o.banks[j]);
+        if (bj != 0xff && !(bank_busy >> bj & 1u)) {
+          bank_busy |= 1u << bj;
           o.banks[j] = 0xff;
-          o.nread--;
-          if (o.nread == 0) s.oc_read_mask &= ~(1u << best);
+          const uint8_t nr = (uint8_t)(P::uni(o.nread) - 1);
+          o.nread = nr;
+          if (nr == 0) {
+            rmask &= ~(1u << best);
+            s.oc_read_mask = rmask;
+          }
           s.st.rf_reads++;
           break;  // one operand per collector per round
         }
@@ -746,7 +754,7 @@ SIM_HDI void sm_dispatch(SMState& s, const SimCfg& c, uint64_t now) {
   const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
   const uint32_t wbw = wb_width(c);
   // oldest-first over ready collectors (valid, all operands read)
-  const uint32_t ready = s.oc_mask & ~s.oc_read_mask;
+  const uint32_t ready = P::uni(s.oc_mask & ~s.oc_read_mask);
   if (!ready) return;
   uint32_t tried = 0;
   for (int k = 0; k < noc; ++k) {
@@ -759,10 +767,10 @@ SIM_HDI void sm_dispatch(SMState& s, const SimCfg& c, uint64_t now) {
     if (best < 0) break;
     tried |= 1u << best;
     OCUnit& o = s.oc[best];
-    const uint32_t u = o.unit;
+    const uint32_t u = P::uni(o.unit);
     if (u == U_MEM) {
-      if (s.ldst.busy) continue;
-      const TInst& in = o.inst;
+      if (P::uni(s.ldst.busy)) continue;
+      const TInst in = P::uni(o.inst);
       // loads need a slot: allocated at issue (slot id carried in pad of OC)
       s.ldst.inst = in;
       s.ldst.busy = 1;
@@ -776,21 +784,24 @@ SIM_HDI void sm_dispatch(SMState& s, const SimCfg& c, uint64_t now) {
       continue;
     }
     uint32_t cnt = c.unit_count[u] ? c.unit_count[u] : 1;
-    uint32_t phys = o.sched % cnt;
+    uint32_t phys = P::uni(o.sched) % cnt;
     if (phys >= (uint32_t)kMaxSched) phys %= kMaxSched;
-    uint32_t nf = s.fu_next[u][phys];
+    uint32_t nf = P::uni(s.fu_next[u][phys]);
     if ((int32_t)(nf - (uint32_t)now) > 0) continue;  // initiation interval
-    uint32_t lat = o.inst.lat ? o.inst.lat : 1;
+    const TInst oi = P::uni(o.inst);
+    uint32_t lat = oi.lat ? oi.lat : 1;
     if (lat >= (uint32_t)kWbRing) lat = kWbRing - 1;
     uint32_t slot = (uint32_t)((now + lat) % kWbRing);
-    if (s.wb_cnt[slot] >= wbw) { s.st.pipe_stall++; continue; }  // result bus busy
-    WbEnt& e = s.wb[slot][s.wb_cnt[slot]++];
+    const uint32_t nwb = P::uni(s.wb_cnt[slot]);
+    if (nwb >= wbw) { s.st.pipe_stall++; continue; }  // result bus busy
+    s.wb_cnt[slot] = (uint8_t)(nwb + 1);
+    WbEnt& e = s.wb[slot][nwb];
     s.wb_occ[slot >> 6] |= 1ull << (slot & 63);
-    e.warp = o.warp;
-    e.dst0 = o.inst.dst[0];
-    e.dst1 = o.inst.dst[1];
+    e.warp = P::uni(o.warp);
+    e.dst0 = oi.dst[0];
+    e.dst1 = oi.dst[1];
     e.pad = 0;
-    s.fu_next[u][phys] = (uint32_t)now + (o.inst.ii ? o.inst.ii : 1);
+    s.fu_next[u][phys] = (uint32_t)now + (oi.ii ? oi.ii : 1);
     o.valid = 0;
     s.oc_mask &= ~(1u << best);
   }
@@ -802,7 +813,8 @@ SIM_HDI void sm_alloc_collectors(SMState& s, const SimCfg& c) {
   const uint32_t nsched = c.n_sched;
   const uint32_t per = (c.sub_core && nsched) ? (noc / nsched ? noc / nsched : 1) : (uint32_t)noc;
   // visit pending pipeline registers in (scheduler, unit) order via the mask
-  uint64_t pend = s.idoc_mask;
+  uint64_t pend = P::uni(s.idoc_mask);
+  uint32_t ocm = P::uni(s.oc_mask);
   while (pend) {
     const int bit = ffs64(pend);
     pend &= pend - 1;
@@ -814,29 +826,33 @@ SIM_HDI void sm_alloc_collectors(SMState& s, const SimCfg& c) {
       uint32_t hi = c.sub_core ? lo + per : (uint32_t)noc;
       if (hi > (uint32_t)noc) hi = noc;
       const uint32_t grp = ((hi >= 32 ? 0xffffffffu : ((1u << hi) - 1)) & ~((1u << lo) - 1));
-      const uint32_t freem = grp & ~s.oc_mask;
+      const uint32_t freem = grp & ~ocm;
       if (!freem) continue;
       const int f = ffs64(freem);
       OCUnit& o = s.oc[f];
-      s.oc_mask |= 1u << f;
-      o.inst = r.inst;
+      ocm |= 1u << f;
+      s.oc_mask = ocm;
+      const TInst rin = P::uni(r.inst);
+      const uint32_t rw = P::uni(r.warp);
+      o.inst = rin;
       o.valid = 1;
-      o.warp = r.warp;
+      o.warp = (uint8_t)rw;
       o.sched = (uint8_t)sc;
       o.unit = (uint8_t)u;
       o.pad[0] = r.pad[0];  // load slot
       o.age = r.widx;
-      o.nread = 0;
+      uint32_t nread = 0;
       for (int j = 0; j < 5; ++j) {
-        uint8_t reg = r.inst.src[j];
+        uint8_t reg = rin.src[j];
         if (reg) {
-          o.banks[j] = (uint8_t)reg_bank(c, sc, r.warp, reg - 1);
-          o.nread++;
+          o.banks[j] = (uint8_t)reg_bank(c, sc, rw, reg - 1);
+          nread++;
         } else {
           o.banks[j] = 0xff;
         }
       }
-      if (o.nread) s.oc_read_mask |= 1u << f;
+      o.nread = (uint8_t)nread;
+      if (nread) s.oc_read_mask |= 1u << f;
       r.valid = 0;
       s.idoc_mask &= ~(1ull << bit);
     }
@@ -882,7 +898,7 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
   const KernelDesc& k = *x.k;
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
-  const uint64_t idoc_busy = s.idoc_mask;
+  const uint64_t idoc_busy = P::uni(s.idoc_mask);
   // readiness of every warp (lane-parallel)
   uint64_t ready = P::ballot(nw, [&](int w) -> bool { return warp_can_issue(s, c, w, nsched, idoc_busy); });
   uint64_t live = P::ballot(nw, [&](int w) { return (s.w_flags[w] & WF_ACTIVE) != 0; });
@@ -897,7 +913,7 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
       continue;
     }
     int pick = -1;
-    uint32_t last = s.sched_last[sc];
+    uint32_t last = P::uni(s.sched_last[sc]);
     switch (c.sched_policy) {
       case SCHED_GTO:
       case SCHED_TWO_LEVEL:
@@ -921,13 +937,14 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
         break;
       }
     }
-    const uint32_t w = (uint32_t)pick;
+    const uint32_t w = P::uni((uint32_t)pick);
     s.sched_last[sc] = w;
-    const TInst in = s.w_win[w][s.w_head[w] % kWin];
+    const uint32_t head = P::uni(s.w_head[w]);
+    const TInst in = P::uni(s.w_win[w][head % kWin]);
     if (trace_sm_on(c, TS_WARP_SCHEDULER, s.id))
       P::one([&] { trace_put(c, s.id, now, EV_ISSUE, (uint16_t)w, (uint64_t)in.pc | (uint64_t)in.opcode << 32); });
-    s.w_head[w]++;
-    s.w_ibuf[w]--;
+    s.w_head[w] = head + 1;
+    s.w_ibuf[w] = (uint8_t)(P::uni(s.w_ibuf[w]) - 1);
     issued_any = true;
     // stats: instruction counts at issue (reference counts active threads,
     // shader.cc:1911)
@@ -935,11 +952,11 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
     s.st.thread_insn += (uint64_t)popc64(in.mask);
     s.st.cls_insn[in.cls < OC_COUNT ? in.cls : OC_ALU]++;
     s.last_progress = now;
-    uint32_t cta = s.w_cta[w];
+    uint32_t cta = P::uni(s.w_cta[w]);
     if (in.cls == OC_EXIT) {
       // lanes retire; the warp ends only when EXIT is its last instruction
       // (reference checkExecutionStatusAndUpdate, trace_driven.cc:588-606)
-      if (s.w_head[w] >= s.w_end[w]) {
+      if (head + 1 >= P::uni(s.w_end[w])) {
         s.w_flags[w] |= WF_EXITING;
         s.cta_nexit[cta]++;
         sm_barrier_check<P>(s, cta, k);
@@ -972,7 +989,7 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
     s.w_inflight[w]++;
     if (in.cls == OC_LOAD) {
       // allocate a load slot; scoreboard reserves destination registers
-      uint8_t used = s.w_slot_used[w];
+      uint8_t used = P::uni(s.w_slot_used[w]);
       uint32_t sl = (uint32_t)ffs64((uint64_t)(uint8_t)~used);
       s.w_slot_used[w] = (uint8_t)(used | (1u << sl));
       s.w_loads[w]++;
@@ -1008,7 +1025,7 @@ SIM_HDI void sm_fetch(SMState& s, const SimCfg& c) {
     uint8_t f = s.w_flags[w];
     return (f & WF_ACTIVE) && !(f & (WF_EXITING | WF_IMISS)) && s.w_ibuf[w] == 0 && s.w_next[w] < s.w_end[w];
   });
-  uint32_t start = s.fetch_rr % (uint32_t)nw;
+  uint32_t start = P::uni(s.fetch_rr) % (uint32_t)nw;
   uint64_t r = rotr64(need, start, (unsigned)nw);
   const bool icache = !c.perfect_icache && !c.il1.disabled;
   for (uint32_t i = 0; i < c.fetch_throughput && r; ++i) {
@@ -1019,9 +1036,10 @@ SIM_HDI void sm_fetch(SMState& s, const SimCfg& c) {
       s.fetch_rr = w + 1;  // miss / reservation fail ends this cycle's fetch (shader.cc:997-1010)
       break;
     }
-    uint32_t avail = s.w_end[w] - s.w_next[w];
+    const uint32_t wnext = P::uni(s.w_next[w]);
+    uint32_t avail = P::uni(s.w_end[w]) - wnext;
     uint32_t n = avail < (uint32_t)kIbuf ? avail : (uint32_t)kIbuf;
-    s.w_next[w] += n;
+    s.w_next[w] = wnext + n;
     s.w_ibuf[w] = (uint8_t)n;
     s.fetch_rr = w + 1;
   }
@@ -1146,7 +1164,7 @@ SIM_HDI void sm_cycle(SMState& s, const SmCtx& x, uint64_t now) {
   P::prof(10);
   sm_inject<P>(s, x, now);
   P::prof(11);
-  if (s.n_cta_active) {
+  if (P::uni(s.n_cta_active)) {
     s.st.active_cycles++;
     s.st.occupancy_acc += P::sum((int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps),
                                  [&](int w) -> uint32_t { return (s.w_flags[w] & WF_ACTIVE) ? 1u : 0u; });
@@ -1180,13 +1198,13 @@ SIM_HDI uint64_t ring_next(const uint64_t* occ, uint32_t ring, uint64_t from, ui
 // (every warp waiting on memory) cost one check instead of one cycle each.
 template <class P>
 SIM_HDI uint64_t sm_quiet_until(const SMState& s, const SimCfg& c, uint64_t t, uint64_t limit) {
-  if (s.ldst.busy || s.idoc_mask || s.oc_mask || s.oc_read_mask || s.outq_n) return t;
+  if (P::uni(s.ldst.busy) || P::uni(s.idoc_mask) || P::uni(s.oc_mask | s.oc_read_mask) || P::uni(s.outq_n)) return t;
   uint64_t nx = ring_next(s.wb_occ, kWbRing, t, limit);
   if (nx == t) return t;
   nx = ring_next(s.hit_occ, kHitRing, t, nx);
   if (nx == t) return t;
-  if (s.inq_n) {
-    const uint64_t at = (s.inq[s.inq_head].t + c.per_core - 1) / c.per_core;
+  if (P::uni(s.inq_n)) {
+    const uint64_t at = (P::uni(s.inq[P::uni(s.inq_head)].t) + c.per_core - 1) / c.per_core;
     if (at <= t) return t;
     nx = amin<uint64_t>(nx, at);
   }
