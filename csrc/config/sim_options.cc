@@ -575,6 +575,10 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.shmem_per_block = (uint32_t)r.getu("-gpgpu_shmem_per_block");
   c.n_sched = (uint32_t)std::max<long long>(1, r.geti("-gpgpu_num_sched_per_core"));
   if (c.n_sched > (uint32_t)kMaxSched) throw OptionError("at most 4 schedulers per SM");
+  for (uint32_t sc = 0; sc < (uint32_t)kMaxSched; ++sc) {
+    c.sched_mask[sc] = 0;
+    for (uint32_t w = sc; w < c.max_warps_per_sm && sc < c.n_sched; w += c.n_sched) c.sched_mask[sc] |= 1ull << w;
+  }
   c.sched_policy = sched_of(r.gets("-gpgpu_scheduler"));
   c.sub_core = r.getb("-gpgpu_sub_core_model") ? 1 : 0;
   c.fetch_throughput = (uint32_t)std::max<long long>(1, r.geti("-gpgpu_inst_fetch_throughput"));

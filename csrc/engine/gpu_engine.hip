@@ -595,7 +595,7 @@ class GpuEngine : public Engine {
         "sm.receive", "sm.writeback", "sm.hit_complete", "sm.ldst", "sm.dispatch", "sm.read_operands",
         "sm.alloc_oc", "sm.issue", "sm.fetch", "sm.retire", "sm.inject", "sm.occupancy", "sm.gather",
         "sm.cta_dispatch", "sm.refill", "sm.cycle_loop", "sm.publish", "#sm_cycles", "#quiet_checks", "#epochs_busy", "mem.gather", "mem.dram",
-        "mem.l2", "mem.icnt", "mem.window_other", "mem.publish", "barrier", "decide", "post", "-", "-", "launch_rest"};
+        "mem.l2", "mem.icnt", "mem.window_other", "mem.publish", "barrier", "decide", "post", "sm.issue_sched", "-", "launch_rest"};
     double sm[kProfSlots] = {}, mc[kProfSlots] = {}, smt = 0, mct = 0;
     for (uint32_t b = 0; b < nblocks_; ++b)
       for (int k = 0; k < kProfSlots; ++k) {

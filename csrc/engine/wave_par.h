@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../model/hd.h"
+#include "sm_view.h"
 
 namespace asim {
 
@@ -38,6 +39,7 @@ struct WavePar {
   template <class T>
   static __device__ __forceinline__ T uni(T v) {
     static_assert(sizeof(T) <= 4 || sizeof(T) % 4 == 0, "uni: 1/2/4-byte or word-multiple types");
+    static_assert(std::is_trivially_copyable<T>::value, "uni: values only (cast proxies first)");
     if constexpr (sizeof(T) <= 4) {
       uint32_t u = 0;
       __builtin_memcpy(&u, &v, sizeof(T));
@@ -59,6 +61,15 @@ struct WavePar {
   static __device__ __forceinline__ void sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+  }
+  // the cycle loop runs on a register-resident view of the LDS state
+  template <class S, class F>
+  static __device__ __forceinline__ void view(S& s, F&& f) {
+    sync();
+    SmView<S> v(s);
+    f(v);
+    v.flush();
+    sync();
   }
   // ---- cross-lane reductions on DPP row operations (no LDS traffic) ----
   // Every reduction runs in wave-uniform control flow with all 64 lanes

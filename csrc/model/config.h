@@ -118,6 +118,7 @@ struct SimCfg {
   // ---- front end / issue ----
   uint32_t n_sched;
   uint32_t sched_policy;
+  uint64_t sched_mask[kMaxSched];  // warps (lanes) supervised by each scheduler: w % n_sched == sc
   uint32_t sub_core;
   uint32_t fetch_throughput;
   uint32_t max_issue_per_warp;

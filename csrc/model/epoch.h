@@ -125,20 +125,22 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& 
   s.epoch_end = t1;
   if (P::uni(s.n_cta_active) || !sm_idle(s)) {
     P::tick(19);
-    for (uint64_t t = t0; t < t1;) {
-      P::tick(17);
-      sm_cycle<P>(s, x, t);
-      ++t;
-      if (t < t1 && c.event_skip) {
-        // fast-forward cycles in which provably nothing happens
-        P::tick(18);
-        const uint64_t nx = P::uni(sm_quiet_until<P>(s, c, t, t1));
-        if (nx > t) {
-          sm_skip<P>(s, c, nx - t);
-          t = nx;
+    P::view(s, [&](auto& v) {
+      for (uint64_t t = t0; t < t1;) {
+        P::tick(17);
+        sm_cycle<P>(v, x, t);
+        ++t;
+        if (t < t1 && c.event_skip) {
+          // fast-forward cycles in which provably nothing happens
+          P::tick(18);
+          const uint64_t nx = P::uni(sm_quiet_until<P>(v, c, t, t1));
+          if (nx > t) {
+            sm_skip<P>(v, c, nx - t);
+            t = nx;
+          }
         }
       }
-    }
+    });
   }
   s.cycle = t1;
   P::prof(16);

@@ -68,6 +68,10 @@ struct SeqPar {
   // the compiler keeps the value and everything derived from it in SGPRs)
   template <class T>
   static SIM_HDI T uni(T v) { return v; }
+  // run f on the SM state for an epoch's cycle loop (the GPU policy hands f
+  // a register-resident view of the same state, csrc/engine/sm_view.h)
+  template <class S, class F>
+  static SIM_HDI void view(S& s, F&& f) { f(s); }
   // index i < n minimising key(i) (ties -> lowest i); key == ~0ull means
   // "not a candidate".  Returns -1 if there is no candidate.
   template <class F>

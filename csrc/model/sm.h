@@ -188,6 +188,8 @@ struct alignas(16) SMState {
   uint8_t cta_bar[kMaxCta];      // warps arrived at barrier
   uint8_t cta_nexit[kMaxCta];    // warps exited (excluded from barrier count)
   uint32_t n_cta_active;
+  uint32_t n_warps_live;         // warps with WF_ACTIVE (occupancy statistic)
+  uint32_t n_wait_flags;         // warps parked in WF_MEMBAR / WF_WAITCNT
   // ---- front end ----
   uint32_t fetch_rr;
   uint32_t sched_last[kMaxSched];
@@ -261,8 +263,8 @@ SIM_HDI void sb_clr(uint64_t* sb, uint8_t r) {
 // ---------------------------------------------------------------------------
 // reset an SM for a new kernel (state persists across kernels otherwise:
 // L1 may be flushed by -gpgpu_flush_l1_cache)
-template <class P>
-SIM_HDI void sm_reset(SMState& s, uint32_t id) {
+template <class P, class S>
+SIM_HDI void sm_reset(S& s, uint32_t id) {
   // caller zero-fills the struct; set identity
   s.id = id;
 }
@@ -277,10 +279,12 @@ SIM_HDI CacheGeom l1_geom(const SimCfg& c, const KernelDesc& k) {
 
 // ---------------------------------------------------------------------------
 // injection: enqueue a packet towards the interconnect
-SIM_HDI bool sm_can_send(const SMState& s, const SimCfg& c) {
+template <class S>
+SIM_HDI bool sm_can_send(const S& s, const SimCfg& c) {
   return s.outq_n < (uint32_t)kOutQ && s.outstanding + s.outq_n < c.icnt_out_limit;
 }
-SIM_HDI void sm_send(SMState& s, const SimCfg& c, uint8_t type, uint64_t line, uint8_t sectors,
+template <class S>
+SIM_HDI void sm_send(S& s, const SimCfg& c, uint8_t type, uint64_t line, uint8_t sectors,
                      uint16_t bytes, uint32_t tag) {
   AddrTlx t = addr_decode(c, line);
   Pkt& p = s.outq[(s.outq_head + s.outq_n) % kOutQ];
@@ -297,8 +301,8 @@ SIM_HDI void sm_send(SMState& s, const SimCfg& c, uint8_t type, uint64_t line, u
 }
 
 // move packets whose injection completes inside the epoch into the outbox
-template <class P>
-SIM_HDI void sm_inject(SMState& s, const SmCtx& x, uint64_t now) {
+template <class P, class S>
+SIM_HDI void sm_inject(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
   if (P::uni(s.outq_n) == 0) return;
   if (now < P::uni(s.out_port_free)) return;
@@ -328,8 +332,8 @@ SIM_HDI void sm_inject(SMState& s, const SmCtx& x, uint64_t now) {
 
 // ---------------------------------------------------------------------------
 // writeback of ALU results due this cycle
-template <class P>
-SIM_HDI void sm_writeback(SMState& s, const SimCfg& c, uint64_t now) {
+template <class P, class S>
+SIM_HDI void sm_writeback(S& s, const SimCfg& c, uint64_t now) {
   uint32_t slot = (uint32_t)(now % kWbRing);
   uint32_t n = P::uni(s.wb_cnt[slot]);
   for (uint32_t i = 0; i < n; ++i) {
@@ -349,7 +353,8 @@ SIM_HDI void sm_writeback(SMState& s, const SimCfg& c, uint64_t now) {
   s.wb_occ[slot >> 6] &= ~(1ull << (slot & 63));
 }
 
-SIM_HDI void sm_load_slot_done(SMState& s, uint32_t w, uint32_t slot, uint64_t now) {
+template <class S>
+SIM_HDI void sm_load_slot_done(S& s, uint32_t w, uint32_t slot, uint64_t now) {
   sb_clr(s.w_sb[w], s.w_slot_dst[w][slot][0]);
   sb_clr(s.w_sb[w], s.w_slot_dst[w][slot][1]);
   s.st.rf_writes += (s.w_slot_dst[w][slot][0] != 0) + (s.w_slot_dst[w][slot][1] != 0);
@@ -360,8 +365,8 @@ SIM_HDI void sm_load_slot_done(SMState& s, uint32_t w, uint32_t slot, uint64_t n
 }
 
 // L1-hit / shared-memory completions due this cycle
-template <class P>
-SIM_HDI void sm_hit_complete(SMState& s, uint64_t now) {
+template <class P, class S>
+SIM_HDI void sm_hit_complete(S& s, uint64_t now) {
   uint32_t slot = (uint32_t)(now % kHitRing);
   uint32_t n = P::uni(s.hit_cnt[slot]);
   for (uint32_t i = 0; i < n; ++i) {
@@ -377,7 +382,8 @@ SIM_HDI void sm_hit_complete(SMState& s, uint64_t now) {
   s.hit_occ[slot >> 6] &= ~(1ull << (slot & 63));
 }
 
-SIM_HDI bool hit_push(SMState& s, uint64_t when, uint8_t warp, uint8_t slot, uint8_t kind) {
+template <class S>
+SIM_HDI bool hit_push(S& s, uint64_t when, uint8_t warp, uint8_t slot, uint8_t kind) {
   uint32_t r = (uint32_t)(when % kHitRing);
   if (s.hit_cnt[r] >= kHitSlot) return false;
   s.hit_occ[r >> 6] |= 1ull << (r & 63);
@@ -391,8 +397,8 @@ SIM_HDI bool hit_push(SMState& s, uint64_t when, uint8_t warp, uint8_t slot, uin
 
 // ---------------------------------------------------------------------------
 // L1 data cache (sectored, lane-parallel probe over the ways of a set)
-template <class P>
-SIM_HDI int l1_find(const SMState& s, const CacheGeom& g, uint32_t set, uint64_t line) {
+template <class P, class S>
+SIM_HDI int l1_find(const S& s, const CacheGeom& g, uint32_t set, uint64_t line) {
   const L1Line* base = &s.l1[set * g.assoc];
   const int assoc = (int)g.assoc;
   if (assoc <= 64) {
@@ -407,8 +413,8 @@ SIM_HDI int l1_find(const SMState& s, const CacheGeom& g, uint32_t set, uint64_t
   return -1;
 }
 
-template <class P>
-SIM_HDI int l1_victim(const SMState& s, const CacheGeom& g, uint32_t set) {
+template <class P, class S>
+SIM_HDI int l1_victim(const S& s, const CacheGeom& g, uint32_t set) {
   const L1Line* base = &s.l1[set * g.assoc];
   // invalid way first (lowest index), else smallest stamp (LRU or FIFO)
   int v = P::argmin((int)g.assoc, [&](int w) -> uint64_t {
@@ -418,8 +424,8 @@ SIM_HDI int l1_victim(const SMState& s, const CacheGeom& g, uint32_t set) {
 }
 
 // fill sectors of a line into L1 (allocate-on-fill) and wake waiters
-template <class P>
-SIM_HDI void l1_fill(SMState& s, const SmCtx& x, uint64_t line, uint8_t sectors, uint64_t now) {
+template <class P, class S>
+SIM_HDI void l1_fill(S& s, const SmCtx& x, uint64_t line, uint8_t sectors, uint64_t now) {
   const SimCfg& c = *x.cfg;
   const CacheGeom g = l1_geom(c, *x.k);
   if (!g.disabled) {
@@ -477,15 +483,15 @@ SIM_HDI void l1_fill(SMState& s, const SmCtx& x, uint64_t line, uint8_t sectors,
 // L1 instruction cache (reference read_only_cache m_L1I: fetch probes it with
 // the warp's next PC + PROGRAM_MEM_START, a miss parks the warp in
 // imiss_pending until the line returns from L2, shader.cc:918-1020, 3989)
-template <class P>
-SIM_HDI int il1_find(const SMState& s, const CacheGeom& g, uint32_t set, uint64_t line) {
+template <class P, class S>
+SIM_HDI int il1_find(const S& s, const CacheGeom& g, uint32_t set, uint64_t line) {
   const L1Line* base = &s.il1[set * g.assoc];
   uint64_t m = P::ballot((int)amin<uint32_t>(g.assoc, 64), [&](int w) { return base[w].valid && base[w].tag == line; });
   return m ? ffs64(m) : -1;
 }
 
-template <class P>
-SIM_HDI void il1_fill(SMState& s, const SimCfg& c, uint64_t line) {
+template <class P, class S>
+SIM_HDI void il1_fill(S& s, const SimCfg& c, uint64_t line) {
   const CacheGeom& g = c.il1;
   const uint32_t set = cache_set_index(g, line);
   if (il1_find<P>(s, g, set, line) < 0) {
@@ -510,8 +516,8 @@ SIM_HDI void il1_fill(SMState& s, const SimCfg& c, uint64_t line) {
 
 // probe the instruction cache for warp w's next fetch; true = instructions
 // available this cycle
-template <class P>
-SIM_HDI bool il1_fetch(SMState& s, const SimCfg& c, uint32_t w) {
+template <class P, class S>
+SIM_HDI bool il1_fetch(S& s, const SimCfg& c, uint32_t w) {
   const CacheGeom& g = c.il1;
   const TInst& in = s.w_win[w][s.w_next[w] % kWin];
   const uint64_t line = (kProgramMemStart + in.pc) & ~127ull;
@@ -545,8 +551,8 @@ SIM_HDI bool il1_fetch(SMState& s, const SimCfg& c, uint32_t w) {
 }
 
 // consume at most one arrived packet per cycle (response FIFO)
-template <class P>
-SIM_HDI void sm_receive(SMState& s, const SmCtx& x, uint64_t now) {
+template <class P, class S>
+SIM_HDI void sm_receive(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
   if (P::uni(s.inq_n) == 0) return;
   const Pkt q = P::uni(s.inq[P::uni(s.inq_head)]);
@@ -579,8 +585,8 @@ SIM_HDI uint32_t l1_stat_type(uint8_t space, bool write, bool atomic) {
   return write ? L1T_GLOBAL_W : L1T_GLOBAL_R;
 }
 
-template <class P>
-SIM_HDI void sm_ldst(SMState& s, const SmCtx& x, uint64_t now) {
+template <class P, class S>
+SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
   LdstState& u = s.ldst;
   if (!P::uni(u.busy)) return;
@@ -709,8 +715,8 @@ SIM_HDI uint32_t reg_bank(const SimCfg& c, uint32_t sched, uint32_t warp, uint32
   return base + (reg + warp) % per;
 }
 
-template <class P>
-SIM_HDI void sm_read_operands(SMState& s, const SimCfg& c) {
+template <class P, class S>
+SIM_HDI void sm_read_operands(S& s, const SimCfg& c) {
   // each register bank serves reg_port_tp reads per cycle, oldest collector first
   uint32_t rmask = P::uni(s.oc_read_mask);
   if (!rmask) return;
@@ -749,8 +755,8 @@ SIM_HDI void sm_read_operands(SMState& s, const SimCfg& c) {
   }
 }
 
-template <class P>
-SIM_HDI void sm_dispatch(SMState& s, const SimCfg& c, uint64_t now) {
+template <class P, class S>
+SIM_HDI void sm_dispatch(S& s, const SimCfg& c, uint64_t now) {
   const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
   const uint32_t wbw = wb_width(c);
   // oldest-first over ready collectors (valid, all operands read)
@@ -807,8 +813,8 @@ SIM_HDI void sm_dispatch(SMState& s, const SimCfg& c, uint64_t now) {
   }
 }
 
-template <class P>
-SIM_HDI void sm_alloc_collectors(SMState& s, const SimCfg& c) {
+template <class P, class S>
+SIM_HDI void sm_alloc_collectors(S& s, const SimCfg& c) {
   const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
   const uint32_t nsched = c.n_sched;
   const uint32_t per = (c.sub_core && nsched) ? (noc / nsched ? noc / nsched : 1) : (uint32_t)noc;
@@ -861,8 +867,8 @@ SIM_HDI void sm_alloc_collectors(SMState& s, const SimCfg& c) {
 
 // ---------------------------------------------------------------------------
 // issue
-template <class P>
-SIM_HDI void sm_barrier_check(SMState& s, uint32_t cta, const KernelDesc& k) {
+template <class P, class S>
+SIM_HDI void sm_barrier_check(S& s, uint32_t cta, const KernelDesc& k) {
   uint32_t live = s.cta_live[cta] - s.cta_nexit[cta];
   if (s.cta_bar[cta] > 0 && s.cta_bar[cta] >= live) {
     uint32_t base = cta * k.warps_per_cta;
@@ -874,7 +880,8 @@ SIM_HDI void sm_barrier_check(SMState& s, uint32_t cta, const KernelDesc& k) {
 
 // can warp `w` issue its next instruction this cycle (scoreboard, flags,
 // pipeline register and load slot availability)
-SIM_HDI bool warp_can_issue(const SMState& s, const SimCfg& c, int w, uint32_t nsched, uint64_t idoc_busy) {
+template <class S>
+SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, int w, uint32_t nsched, uint64_t idoc_busy) {
   uint8_t f = s.w_flags[w];
   if (!(f & WF_ACTIVE) || (f & (WF_EXITING | WF_BARRIER | WF_MEMBAR | WF_WAITCNT))) return false;
   if (s.w_ibuf[w] == 0) return false;
@@ -892,8 +899,8 @@ SIM_HDI bool warp_can_issue(const SMState& s, const SimCfg& c, int w, uint32_t n
   return true;
 }
 
-template <class P>
-SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
+template <class P, class S>
+SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
   const KernelDesc& k = *x.k;
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
@@ -902,11 +909,11 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
   // readiness of every warp (lane-parallel)
   uint64_t ready = P::ballot(nw, [&](int w) -> bool { return warp_can_issue(s, c, w, nsched, idoc_busy); });
   uint64_t live = P::ballot(nw, [&](int w) { return (s.w_flags[w] & WF_ACTIVE) != 0; });
+  P::prof(29);
   bool issued_any = false;
   for (uint32_t sc = 0; sc < nsched; ++sc) {
     // warps of this scheduler
-    uint64_t mine = 0;
-    for (int w = (int)sc; w < nw; w += (int)nsched) mine |= 1ull << w;
+    const uint64_t mine = c.sched_mask[sc];
     uint64_t cand = ready & mine;
     if (!cand) {
       if (live & mine) s.st.issue_stall_idle++;
@@ -939,12 +946,12 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
     }
     const uint32_t w = P::uni((uint32_t)pick);
     s.sched_last[sc] = w;
-    const uint32_t head = P::uni(s.w_head[w]);
+    const uint32_t head = P::uni((uint32_t)s.w_head[w]);
     const TInst in = P::uni(s.w_win[w][head % kWin]);
     if (trace_sm_on(c, TS_WARP_SCHEDULER, s.id))
       P::one([&] { trace_put(c, s.id, now, EV_ISSUE, (uint16_t)w, (uint64_t)in.pc | (uint64_t)in.opcode << 32); });
     s.w_head[w] = head + 1;
-    s.w_ibuf[w] = (uint8_t)(P::uni(s.w_ibuf[w]) - 1);
+    s.w_ibuf[w] = (uint8_t)(P::uni((uint8_t)s.w_ibuf[w]) - 1);
     issued_any = true;
     // stats: instruction counts at issue (reference counts active threads,
     // shader.cc:1911)
@@ -952,11 +959,11 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
     s.st.thread_insn += (uint64_t)popc64(in.mask);
     s.st.cls_insn[in.cls < OC_COUNT ? in.cls : OC_ALU]++;
     s.last_progress = now;
-    uint32_t cta = P::uni(s.w_cta[w]);
+    uint32_t cta = P::uni((uint8_t)s.w_cta[w]);
     if (in.cls == OC_EXIT) {
       // lanes retire; the warp ends only when EXIT is its last instruction
       // (reference checkExecutionStatusAndUpdate, trace_driven.cc:588-606)
-      if (head + 1 >= P::uni(s.w_end[w])) {
+      if (head + 1 >= P::uni((uint32_t)s.w_end[w])) {
         s.w_flags[w] |= WF_EXITING;
         s.cta_nexit[cta]++;
         sm_barrier_check<P>(s, cta, k);
@@ -970,11 +977,17 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
       continue;
     }
     if (in.cls == OC_MEMBAR) {
-      if (s.w_stores[w]) s.w_flags[w] |= WF_MEMBAR;
+      if (s.w_stores[w]) {
+        s.w_flags[w] |= WF_MEMBAR;
+        s.n_wait_flags++;
+      }
       continue;
     }
     if (in.flags & F_WAITCNT) {
-      if (s.w_stores[w] || s.w_loads[w]) s.w_flags[w] |= WF_WAITCNT;
+      if (s.w_stores[w] || s.w_loads[w]) {
+        s.w_flags[w] |= WF_WAITCNT;
+        s.n_wait_flags++;
+      }
       continue;
     }
     if (in.cls == OC_NOP) continue;
@@ -989,7 +1002,7 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
     s.w_inflight[w]++;
     if (in.cls == OC_LOAD) {
       // allocate a load slot; scoreboard reserves destination registers
-      uint8_t used = P::uni(s.w_slot_used[w]);
+      uint8_t used = P::uni((uint8_t)s.w_slot_used[w]);
       uint32_t sl = (uint32_t)ffs64((uint64_t)(uint8_t)~used);
       s.w_slot_used[w] = (uint8_t)(used | (1u << sl));
       s.w_loads[w]++;
@@ -1018,8 +1031,8 @@ SIM_HDI void sm_issue(SMState& s, const SmCtx& x, uint64_t now) {
 // ---------------------------------------------------------------------------
 // fetch/decode: refill the instruction buffer of up to fetch_throughput
 // warps whose buffer is empty (round-robin), perfect instruction cache
-template <class P>
-SIM_HDI void sm_fetch(SMState& s, const SimCfg& c) {
+template <class P, class S>
+SIM_HDI void sm_fetch(S& s, const SimCfg& c) {
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   uint64_t need = P::ballot(nw, [&](int w) {
     uint8_t f = s.w_flags[w];
@@ -1036,8 +1049,8 @@ SIM_HDI void sm_fetch(SMState& s, const SimCfg& c) {
       s.fetch_rr = w + 1;  // miss / reservation fail ends this cycle's fetch (shader.cc:997-1010)
       break;
     }
-    const uint32_t wnext = P::uni(s.w_next[w]);
-    uint32_t avail = P::uni(s.w_end[w]) - wnext;
+    const uint32_t wnext = P::uni((uint32_t)s.w_next[w]);
+    uint32_t avail = P::uni((uint32_t)s.w_end[w]) - wnext;
     uint32_t n = avail < (uint32_t)kIbuf ? avail : (uint32_t)kIbuf;
     s.w_next[w] = wnext + n;
     s.w_ibuf[w] = (uint8_t)n;
@@ -1047,8 +1060,8 @@ SIM_HDI void sm_fetch(SMState& s, const SimCfg& c) {
 
 // stream exhausted without explicit EXIT -> treat as exit
 // warp retirement and CTA completion
-template <class P>
-SIM_HDI void sm_retire(SMState& s, const SmCtx& x, uint64_t now) {
+template <class P, class S>
+SIM_HDI void sm_retire(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
   const KernelDesc& k = *x.k;
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
@@ -1059,19 +1072,25 @@ SIM_HDI void sm_retire(SMState& s, const SmCtx& x, uint64_t now) {
     return drained && s.w_inflight[w] == 0 && s.w_stores[w] == 0 && s.w_loads[w] == 0;
   });
   // release membar / waitcnt waits
-  P::each(nw, [&](int w) {
-    uint8_t f = s.w_flags[w];
-    if ((f & WF_MEMBAR) && s.w_stores[w] == 0) s.w_flags[w] = f & (uint8_t)~WF_MEMBAR;
-    f = s.w_flags[w];
-    if ((f & WF_WAITCNT) && s.w_stores[w] == 0 && s.w_loads[w] == 0) s.w_flags[w] = f & (uint8_t)~WF_WAITCNT;
-  });
-  P::sync();
+  if (P::uni(s.n_wait_flags)) {
+    const uint32_t released = P::sum(nw, [&](int w) -> uint32_t {
+      uint8_t f = s.w_flags[w];
+      uint32_t r = 0;
+      if ((f & WF_MEMBAR) && s.w_stores[w] == 0) { f = f & (uint8_t)~WF_MEMBAR; ++r; }
+      if ((f & WF_WAITCNT) && s.w_stores[w] == 0 && s.w_loads[w] == 0) { f = f & (uint8_t)~WF_WAITCNT; ++r; }
+      if (r) s.w_flags[w] = f;
+      return r;
+    });
+    s.n_wait_flags = P::uni(s.n_wait_flags) - released;
+    P::sync();
+  }
   while (done) {
     int w = ffs64(done);
     done &= done - 1;
     uint32_t cta = s.w_cta[w];
     if (!(s.w_flags[w] & WF_EXITING)) s.cta_nexit[cta]++;  // implicit exit at stream end
     s.w_flags[w] = 0;
+    s.n_warps_live--;
     s.st.warps_done++;
     s.cta_live[cta]--;
     s.cta_nexit[cta]--;
@@ -1088,8 +1107,8 @@ SIM_HDI void sm_retire(SMState& s, const SmCtx& x, uint64_t now) {
 
 // ---------------------------------------------------------------------------
 // launch a CTA into slot `slot`
-template <class P>
-SIM_HDI void sm_launch_cta(SMState& s, const SmCtx& x, uint32_t slot, uint32_t cta_id) {
+template <class P, class S>
+SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id) {
   const KernelDesc& k = *x.k;
   const uint32_t wpc = k.warps_per_cta;
   const uint32_t base = slot * wpc;
@@ -1099,6 +1118,7 @@ SIM_HDI void sm_launch_cta(SMState& s, const SmCtx& x, uint32_t slot, uint32_t c
   s.cta_bar[slot] = 0;
   s.cta_nexit[slot] = 0;
   s.n_cta_active++;
+  s.n_warps_live += wpc;
   uint32_t age0 = s.age_ctr;
   s.age_ctr += wpc;
   P::each((int)wpc, [&](int i) {
@@ -1124,8 +1144,8 @@ SIM_HDI void sm_launch_cta(SMState& s, const SmCtx& x, uint32_t slot, uint32_t c
 // refill the per-warp instruction windows from the kernel trace (HBM).
 // Done once per epoch: a warp can consume at most `epoch` instructions per
 // epoch, so kWin >= epoch + kIbuf guarantees the window never runs dry.
-template <class P>
-SIM_HDI void sm_refill_window(SMState& s, const SimCfg& c, const KernelDesc& k) {
+template <class P, class S>
+SIM_HDI void sm_refill_window(S& s, const SimCfg& c, const KernelDesc& k) {
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   P::each(nw, [&](int w) {
     if (!(s.w_flags[w] & WF_ACTIVE)) return;
@@ -1138,8 +1158,8 @@ SIM_HDI void sm_refill_window(SMState& s, const SimCfg& c, const KernelDesc& k) 
 }
 
 // one simulated core cycle
-template <class P>
-SIM_HDI void sm_cycle(SMState& s, const SmCtx& x, uint64_t now) {
+template <class P, class S>
+SIM_HDI void sm_cycle(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
   P::prof(0);
   sm_receive<P>(s, x, now);
@@ -1166,13 +1186,13 @@ SIM_HDI void sm_cycle(SMState& s, const SmCtx& x, uint64_t now) {
   P::prof(11);
   if (P::uni(s.n_cta_active)) {
     s.st.active_cycles++;
-    s.st.occupancy_acc += P::sum((int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps),
-                                 [&](int w) -> uint32_t { return (s.w_flags[w] & WF_ACTIVE) ? 1u : 0u; });
+    s.st.occupancy_acc += P::uni(s.n_warps_live);
   }
 }
 
 // true if the SM holds no work at all (no CTAs, nothing in flight)
-SIM_HDI bool sm_idle(const SMState& s) {
+template <class S>
+SIM_HDI bool sm_idle(const S& s) {
   return s.n_cta_active == 0 && s.outq_n == 0 && s.outstanding == 0 && !s.ldst.busy;
 }
 
@@ -1196,8 +1216,8 @@ SIM_HDI uint64_t ring_next(const uint64_t* occ, uint32_t ring, uint64_t from, ui
 // (capped at `limit`); otherwise return `t`.  Quiet cycles only add the
 // per-cycle statistics (sm_skip).  This is what makes latency-bound phases
 // (every warp waiting on memory) cost one check instead of one cycle each.
-template <class P>
-SIM_HDI uint64_t sm_quiet_until(const SMState& s, const SimCfg& c, uint64_t t, uint64_t limit) {
+template <class P, class S>
+SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, uint64_t t, uint64_t limit) {
   if (P::uni(s.ldst.busy) || P::uni(s.idoc_mask) || P::uni(s.oc_mask | s.oc_read_mask) || P::uni(s.outq_n)) return t;
   uint64_t nx = ring_next(s.wb_occ, kWbRing, t, limit);
   if (nx == t) return t;
@@ -1224,25 +1244,23 @@ SIM_HDI uint64_t sm_quiet_until(const SMState& s, const SimCfg& c, uint64_t t, u
 }
 
 // account `k` quiet cycles: exactly what k idle sm_cycle calls would add
-template <class P>
-SIM_HDI void sm_skip(SMState& s, const SimCfg& c, uint64_t k) {
+template <class P, class S>
+SIM_HDI void sm_skip(S& s, const SimCfg& c, uint64_t k) {
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
   const uint64_t live = P::ballot(nw, [&](int w) { return (s.w_flags[w] & WF_ACTIVE) != 0; });
   uint32_t stalled = 0;
   for (uint32_t sc = 0; sc < nsched; ++sc) {
-    uint64_t mine = 0;
-    for (int w = (int)sc; w < nw; w += (int)nsched) mine |= 1ull << w;
-    if (live & mine) ++stalled;
+    if (live & c.sched_mask[sc]) ++stalled;
   }
-  P::one([&] {
-    s.st.issue_stall_idle += (uint64_t)stalled * k;
-    if (s.n_cta_active) {
-      s.st.active_cycles += k;
-      s.st.occupancy_acc += (uint64_t)popc64(live) * k;
-    }
-    s.skipped_cycles += k;
-  });
+  // uniform update by every lane (not P::one: on the GPU these fields may be
+  // registers of a view, which a one-lane write would leave divergent)
+  s.st.issue_stall_idle += (uint64_t)stalled * k;
+  if (P::uni(s.n_cta_active)) {
+    s.st.active_cycles += k;
+    s.st.occupancy_acc += (uint64_t)popc64(live) * k;
+  }
+  s.skipped_cycles += k;
   P::sync();
 }
 
