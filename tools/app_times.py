@@ -9,7 +9,7 @@ import sys
 import tempfile
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.environ.get("ASIM_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
