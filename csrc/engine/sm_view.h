@@ -10,7 +10,8 @@
 // (templated on the state type), but
 //   * per-warp fields the ballots read every cycle live in one VGPR each
 //     (lane w holds warp w: WarpReg<T>),
-//   * the scalar bookkeeping fields and scalar statistics live in registers,
+//   * the scalar bookkeeping fields live in registers (the statistics stay in
+//     LDS: promoting them too measured ~1 % slower, SGPR spills),
 //   * everything else (instruction windows, caches, rings, queues) stays a
 //     reference into the LDS state.
 // The view is loaded when an SM's cycle loop starts and flushed back before
@@ -222,7 +223,7 @@ struct SmView {
   SV_REF(sref);
   SV_REF(srank);
   SV_REF(ks);
-  SmStatsView<decltype(B::st)> st;
+  decltype(B::st)& st;  // statistics stay in LDS (SGPR pressure)
 
 #define SV_SCALARS(X)                                                                                   \
   X(id) X(kernel_cta_slots) X(last_progress) X(epoch_end) X(out_port_free) X(age_ctr) X(n_cta_active)    \
@@ -261,7 +262,6 @@ struct SmView {
     SV_WARPS(SV_STW)
 #undef SV_STW
     base.ldst = ldst;
-    st.flush(base.st);
   }
 #undef SV_SCALARS
 #undef SV_WARPS
