@@ -59,7 +59,7 @@ class DistributedSuite:
         self.collective_model = collective_model
         self.apps = []
         for app in sorted(os.listdir(root)):
-            if app == "all-reduce" or app.startswith("."):
+            if app.startswith("all-reduce") or app.startswith("."):
                 continue
             if apps and app not in apps:
                 continue
@@ -70,9 +70,28 @@ class DistributedSuite:
                     self.apps.append((app, kl))
         self.max_concurrency = None
         self.weights: Dict[str, float] = {}  # last wall time per app (LPT order)
-        ar = os.path.join(root, "all-reduce", "kernelslist.g")
+        # the all-reduce example traced for this rank count (all-reduce-<N>),
+        # or the single-rank one
+        ar = os.path.join(root, f"all-reduce-{world}", "kernelslist.g")
+        if not os.path.exists(ar):
+            ar = os.path.join(root, "all-reduce", "kernelslist.g")
         self.allreduce = ar if os.path.exists(ar) else None
         self.sync = PacketCollective() if collective_model == "packet" else CollectiveSync(world)
+        # HIP's current device is per host thread: worker threads start on
+        # device 0, so every thread this suite creates binds this rank's GPU
+        # first (else all ranks of a node would simulate on GPU 0)
+        self.device_index = None
+        try:
+            import torch
+            if torch.cuda.is_available():
+                self.device_index = torch.cuda.current_device()
+        except Exception:  # pragma: no cover - torch is optional for the CPU engine
+            pass
+
+    def _bind_device(self):
+        if self.device_index is not None:
+            import torch
+            torch.cuda.set_device(self.device_index)
 
     def _sim(self, kl: str):
         extra = {"-collective_model": self.collective_model}
@@ -100,6 +119,13 @@ class DistributedSuite:
         self.weights[app] = time.perf_counter() - t0
         return app, s.tot_insn, s.tot_cycle
 
+    def _run_allreduce(self):
+        s = self._sim(self.allreduce)
+        s.set_collective_hook(lambda d, now, s=s: self.sync(s, d, now))
+        if s.run() != 0:
+            raise RuntimeError("all-reduce example failed\n" + s.output[-1500:])
+        return "all-reduce", s.tot_insn, s.tot_cycle
+
     def step(self) -> Dict:
         insn = cycles = 0
         per_app = {}
@@ -110,18 +136,16 @@ class DistributedSuite:
             from concurrent.futures import ThreadPoolExecutor
             # longest (by last measured wall time) first: greedy LPT over the CU groups
             order = sorted(self.apps, key=lambda x: -self.weights.get(x[0], 0.0))
-            with ThreadPoolExecutor(max_workers=conc) as ex:
+            with ThreadPoolExecutor(max_workers=conc, initializer=self._bind_device) as ex:
                 results = list(ex.map(self._run_app, order))
+        # The all-reduce example closes the step on the main thread.  (Packing
+        # it into the suite's thread pool, or running it beside the pool,
+        # measured 3-15 % slower per step on one MI355X: its two kernels then
+        # compete with the suite for the CU pool.)
+        if self.allreduce:
+            results.append(self._run_allreduce())
         for app, i, c in results:
             insn += i
             cycles += c
             per_app[app] = dict(insn=i, cycles=c, wall_s=self.weights.get(app, 0.0))
-        if self.allreduce:
-            s = self._sim(self.allreduce)
-            s.set_collective_hook(lambda d, now, s=s: self.sync(s, d, now))
-            if s.run() != 0:
-                raise RuntimeError("all-reduce example failed\n" + s.output[-1500:])
-            insn += s.tot_insn
-            cycles += s.tot_cycle
-            per_app["all-reduce"] = dict(insn=s.tot_insn, cycles=s.tot_cycle)
         return dict(insn=insn, cycles=cycles, apps=per_app)

@@ -85,14 +85,26 @@ def main() -> int:
     tdir = a.trace_dir or os.path.join(tempfile.gettempdir(), f"asim_bench_rodinia_{os.getuid()}")
     apps = None if a.apps == "all" else a.apps.split(",")
     # every rank generates (or reuses) the deterministic synthetic traces
-    marker = os.path.join(tdir, ".complete")
-    if rank == 0 and not os.path.exists(marker):
-        rodinia.generate_suite(tdir, apps)
-        rodinia.write_allreduce_example(os.path.join(tdir, "all-reduce"), nranks=max(1, world))
-        open(marker, "w").write("ok")
+    # a generated subset never stands in for the full suite (and vice versa is fine)
+    full_marker = os.path.join(tdir, ".complete-all")
+    marker = full_marker if apps is None else os.path.join(tdir, ".complete-" + "+".join(sorted(apps))[:200])
+    if apps is not None and os.path.exists(full_marker):
+        marker = full_marker
+    # the all-reduce example is traced per rank count, so a cached suite from a
+    # run with another GPU count never hands this run a collective of the
+    # wrong size (which the simulator would then emulate locally)
+    ar_dir = os.path.join(tdir, f"all-reduce-{max(1, world)}")
+    ar_marker = os.path.join(ar_dir, ".complete")
+    if rank == 0:
+        if not os.path.exists(marker):
+            rodinia.generate_suite(tdir, apps)
+            open(marker, "w").write("ok")
+        if not os.path.exists(ar_marker):
+            rodinia.write_allreduce_example(ar_dir, nranks=max(1, world))
+            open(ar_marker, "w").write("ok")
     if world > 1:
         dist.barrier()
-    while not os.path.exists(marker):
+    while not (os.path.exists(marker) and os.path.exists(ar_marker)):
         time.sleep(0.1)
 
     suite = DistributedSuite(tdir, config=a.config, engine=engine, rank=rank, world=world, apps=apps,
