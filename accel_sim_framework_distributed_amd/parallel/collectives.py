@@ -4,14 +4,25 @@ Each rank runs the native ``LinkSim`` of its simulated GPU (csrc/parallel/
 linksim.h): the collective is cut into RCCL-style channel/step/slice packets
 on point-to-point links.  Ranks advance in lock-step epochs no longer than
 the link latency (conservative PDES lookahead) and after every epoch
-exchange the packets they put on the wire with ``all_to_all_single`` -- RCCL
-over xGMI on MI355X (backend "nccl"), gloo on CPU.  Per epoch:
+exchange the packets they put on the wire with ONE fixed-size
+``all_to_all_single`` -- RCCL over xGMI on MI355X (backend "nccl"), gloo on
+CPU.  Per epoch:
 
 1. ``emit``: every packet whose send starts in [t, t+E) gets its arrival time;
-2. header all-to-all: per-destination packet counts and each rank's total;
-3. payload all-to-all (skipped when no rank sent anything): 32-byte packets;
-4. ``receive`` and one all-reduce of (next event, not-done) to pick the next
-   epoch start -- idle stretches are skipped, deterministically on all ranks.
+2. one all-to-all of a fixed slot per destination: a header (packets for you,
+   my largest per-destination count, my next event and not-done flag as of
+   the previous epoch, the earliest arrival among the packets I send now)
+   followed by up to K packets; only if some rank had more than K for one
+   destination (every rank sees that in the headers) a second, variable-size
+   all-to-all carries the rest;
+3. ``receive``, sources in rank order, each in emission order.
+
+The next epoch starts at max(t+E, G), G = the minimum over ranks of the
+previous next events and of this epoch's earliest arrivals: every event a
+rank can have after this epoch is one of its earlier pending sends or is
+caused by a packet exchanged now, so nothing happens before G.  The flags
+and next events travel one epoch late, so the ranks stop one epoch after the
+last is done; there is no separate all-reduce and no extra host sync.
 
 The result is bit-identical to ``_asim.linksim_run_local`` with the same
 arrival times, which runs every rank in one process (tests check this over
@@ -57,43 +68,73 @@ class PacketExchange:
         self.stats["exchanges"] += 1
         return dst.cpu().numpy()
 
+    K = 8       # packet slots per destination in the fixed exchange
+    HDR = 8     # header words per destination slot
+
     def run(self, params: Dict, kind: str, nbytes: int, root: int, start_ps: int) -> Dict:
         mod = _native.load(prefer_torch_runtime=True)
-        W, R = self.world, self.rank
+        W, R, K, H = self.world, self.rank, self.K, self.HDR
         ls = mod.LinkSim(params, kind, int(nbytes), int(root), R, W, int(start_ps))
         t_dev = self.torch.tensor([min(int(start_ps), _I64_MAX)], dtype=self.torch.int64, device=self.device)
         self.dist.all_reduce(t_dev, op=self.dist.ReduceOp.MIN, group=self.group)
         t = int(t_dev.item())
         E = int(ls.epoch_ps)
+        slot = H + 4 * K
+        # state announced in the next exchange: as of the end of the previous epoch
+        ann_next = min(int(ls.next_event()), _I64_MAX)
+        ann_busy = 0 if ls.done() else 1
         while True:
             t_end = t + E
             out = np.frombuffer(ls.emit(t_end), dtype=np.int64).reshape(-1, 4)
             dst = (out[:, 0] >> 32).astype(np.int64) if len(out) else np.zeros(0, np.int64)
             order = np.argsort(dst, kind="stable")
             counts = np.bincount(dst, minlength=W).astype(np.int64)
-            # header: [packets for you, my total]
-            hdr = np.stack([counts, np.full(W, len(out), np.int64)], axis=1).reshape(-1)
-            rh = self._a2a(hdr, [2] * W, [2] * W).reshape(W, 2)
-            in_counts = rh[:, 0].tolist()
-            if int(rh[:, 1].sum()) > 0:
-                payload = out[order].reshape(-1)
-                inc = self._a2a(payload, (counts * 4).tolist(), [c * 4 for c in in_counts])
-                if len(inc):
-                    ls.receive(inc.astype(np.int64).tobytes())
-                self.stats["packets"] += len(out)
-            ne = ls.next_event()
-            st = self.torch.tensor([min(ne, _I64_MAX), 0 if ls.done() else 1], dtype=self.torch.int64,
-                                   device=self.device)
-            # one all-reduce: MIN next event, MAX not-done (negated into a MIN)
-            st[1] = -st[1]
-            self.dist.all_reduce(st, op=self.dist.ReduceOp.MIN, group=self.group)
-            gne, not_done = int(st[0].item()), -int(st[1].item())
+            sorted_out = out[order]
+            starts = np.concatenate([[0], np.cumsum(counts)])
+            # earliest arrival among this epoch's packets (arrive_ps: word 3)
+            min_arr = int(out[:, 3].min()) if len(out) else _I64_MAX
+            send = np.zeros((W, slot), np.int64)
+            send[:, 0] = counts
+            send[:, 1] = int(counts.max()) if W else 0
+            send[:, 2] = ann_next
+            send[:, 3] = ann_busy
+            send[:, 4] = min(min_arr, _I64_MAX)
+            for d in range(W):
+                n = min(int(counts[d]), K)
+                if n:
+                    send[d, H:H + 4 * n] = sorted_out[starts[d]:starts[d] + n].reshape(-1)
+            recv = self._a2a(send.reshape(-1), [slot] * W, [slot] * W).reshape(W, slot)
+            in_counts = recv[:, 0]
+            per_src = [recv[s, H:H + 4 * min(int(in_counts[s]), K)] for s in range(W)]
+            if int(recv[:, 1].max()) > K:
+                # some rank sent more than K packets to one destination: the rest
+                extra_out = [max(0, int(counts[d]) - K) for d in range(W)]
+                extra_in = [max(0, int(in_counts[s]) - K) for s in range(W)]
+                payload = np.concatenate([sorted_out[starts[d] + K:starts[d + 1]].reshape(-1)
+                                          for d in range(W)]) if sum(extra_out) else np.zeros(0, np.int64)
+                inc = self._a2a(payload, [4 * c for c in extra_out], [4 * c for c in extra_in])
+                off = 0
+                for s_ in range(W):
+                    n = 4 * extra_in[s_]
+                    if n:
+                        per_src[s_] = np.concatenate([per_src[s_], inc[off:off + n]])
+                        off += n
+            inc_all = np.concatenate(per_src) if per_src else np.zeros(0, np.int64)
+            if len(inc_all):
+                ls.receive(inc_all.astype(np.int64).tobytes())
+            self.stats["packets"] += len(out)
             self.stats["epochs"] += 1
-            if not not_done:
+            any_busy = int(recv[:, 3].max())
+            if not any_busy:
+                # every rank was done before this epoch: nothing was sent in it
                 break
-            if gne >= _I64_MAX:
+            g = int(min(recv[:, 2].min(), recv[:, 4].min()))
+            ann_next = min(int(ls.next_event()), _I64_MAX)
+            ann_busy = 0 if ls.done() else 1
+            if g >= _I64_MAX:
+                # no pending send anywhere and nothing on the wire, yet a rank is not done
                 raise RuntimeError("packet collective deadlocked (no rank has pending work)")
-            t = max(t_end, gne)
+            t = max(t_end, g)
         return dict(finish_ps=int(ls.finish_ps), channels=int(ls.channels), packets_sent=int(ls.packets_sent))
 
 

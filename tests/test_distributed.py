@@ -112,3 +112,33 @@ def test_distributed_allreduce_example(native, tmp_path):
     assert sim.run() == 0
     assert sim.collectives[0]["cycles"] == ev0[0]["cycles"]
     assert res[0][1]["insn"] == res[1][1]["insn"]
+
+
+def _worker_params(rank, world, port, params, cases, q):
+    import torch.distributed as dist
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ex = collectives.PacketExchange()
+        out = [ex.run(params, kind, nbytes, 0, starts[rank])["finish_ps"] for kind, nbytes, starts in cases]
+        q.put((rank, out, ex.stats))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_packet_exchange_four_ranks_overflow(native):
+    """World size 4 with 2 KB slices: many packets per destination per epoch,
+    so the fixed-slot exchange spills into its second all-to-all; results
+    must still equal the single-process emulation exactly."""
+    params = dict(PARAMS, slice_bytes=2048)
+    cases = [("AllReduce", 1 << 20, [0, 0, 0, 0]), ("AllGather", 1 << 19, [0, 2_000_000, 0, 500_000]),
+             ("ReduceScatter", 1 << 20, [0, 0, 0, 0]), ("AllToAll", 1 << 19, [0, 0, 7, 0]),
+             ("Broadcast", 1 << 19, [0, 0, 0, 0])]
+    res = _spawn(_worker_params, 4, params, cases)
+    for i, (kind, nbytes, starts) in enumerate(cases):
+        ref = collectives.emulate(params, kind, nbytes, starts)["finish_ps"]
+        got = [res[r][1][i] for r in range(4)]
+        assert got == ref, (kind, got, ref)
+    st = res[0][2]
+    # one fixed exchange per epoch, plus the spill exchanges
+    assert st["exchanges"] > st["epochs"] > 0
