@@ -156,6 +156,20 @@ PYBIND11_MODULE(_asim, m) {
     m.attr("limits") = lim;
   }
   m.def("gpu_cu_count", &gpu_cu_count, "compute units of the current HIP device");
+  m.def("gpu_engine_kernel_info", []() {
+    const EngineKernelInfo k = gpu_engine_kernel_info();
+    py::dict d;
+    if (!k.valid) return d;
+    d["vgprs_per_lane"] = k.num_regs;
+    d["scratch_bytes_per_lane"] = k.local_bytes;
+    d["lds_static"] = k.shared_static;
+    d["lds_dynamic"] = k.lds_dynamic;
+    d["max_threads_per_block"] = k.max_threads;
+    d["binary_version"] = k.binary_version;
+    d["sm_state_bytes"] = k.sm_state_bytes;
+    d["chan_state_bytes"] = k.chan_state_bytes;
+    return d;
+  }, "compiled resources of the persistent HIP engine kernel (needs a GPU)");
   m.def("option_names", []() {
     OptionRegistry r;
     register_sim_options(r);

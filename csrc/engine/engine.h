@@ -106,6 +106,14 @@ std::unique_ptr<Engine> make_cpu_engine();
 std::unique_ptr<Engine> make_gpu_engine();
 bool gpu_engine_available();
 int gpu_cu_count();  // compute units of the current HIP device (0 if none)
+// compiled resources of the persistent engine kernel (empty if no HIP build):
+// registers, scratch, static LDS, plus the dynamic LDS the engine requests
+struct EngineKernelInfo {
+  int num_regs = 0, local_bytes = 0, shared_static = 0, max_threads = 0, binary_version = 0;
+  size_t lds_dynamic = 0, sm_state_bytes = 0, chan_state_bytes = 0;
+  bool valid = false;
+};
+EngineKernelInfo gpu_engine_kernel_info();
 
 // helpers shared by both engines
 uint32_t reply_cap(const SimCfg& c);

@@ -669,3 +669,21 @@ int gpu_cu_count() {
   return p.multiProcessorCount;
 }
 }  // namespace asim
+
+namespace asim {
+EngineKernelInfo gpu_engine_kernel_info() {
+  EngineKernelInfo k;
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, (const void*)engine_kernel<WavePar>) != hipSuccess) return k;
+  k.num_regs = fa.numRegs;
+  k.local_bytes = (int)fa.localSizeBytes;
+  k.shared_static = (int)fa.sharedSizeBytes;
+  k.max_threads = fa.maxThreadsPerBlock;
+  k.binary_version = fa.binaryVersion;
+  k.lds_dynamic = kLdsBytes;
+  k.sm_state_bytes = sizeof(SMState);
+  k.chan_state_bytes = sizeof(ChanState);
+  k.valid = true;
+  return k;
+}
+}  // namespace asim

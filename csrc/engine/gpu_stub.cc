@@ -8,4 +8,5 @@ bool gpu_engine_available() { return false; }
 
 namespace asim {
 int gpu_cu_count() { return 0; }
+EngineKernelInfo gpu_engine_kernel_info() { return EngineKernelInfo{}; }
 }  // namespace asim

@@ -110,3 +110,15 @@ def test_intersim_presets_gpu_equals_cpu(gpu_mod, tmp_path, preset):
     g = sim.simulate(kl, preset, engine="gpu")
     c = sim.simulate(kl, preset, engine="cpu")
     assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
+
+
+def test_engine_kernel_resources(gpu_mod):
+    """The persistent engine kernel fits its one-block-per-CU design: the
+    dynamic LDS holds the largest unit state, no large scratch, one wavefront."""
+    from accel_sim_framework_distributed_amd.ops import engine
+    k = engine.kernel_info()
+    assert k and k["max_threads_per_block"] >= 64
+    assert max(k["sm_state_bytes"], k["chan_state_bytes"]) < k["lds_dynamic"] <= 160 * 1024
+    assert k["scratch_bytes_per_lane"] <= 1024
+    f = engine.footprint("QV100")
+    assert f["blocks"] == 112 and f["concurrent_simulations"] >= 2

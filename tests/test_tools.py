@@ -139,3 +139,10 @@ def test_trace_tools_cli(native, tmp_path, capsys):
     assert cli.main(["convert", d, "--to", "binary"]) == 0
     after = {os.path.basename(p): native.kernel_info(p)["warp_insts"] for p in cli.kernel_files(d)}
     assert before == after
+
+
+def test_ubench_output_parser():
+    from accel_sim_framework_distributed_amd.ops import ubench
+    log = open(os.path.join(UBENCH, "ub_cache_lat.log")).read()
+    r = ubench.parse(log)
+    assert r["options"]["-gpgpu_l1_latency"] and float(r["measurements"]["xcd_l2_hit_latency"]) > 0
