@@ -34,7 +34,8 @@ class CollectiveSync:
         import torch.distributed as dist
         arrive = now
         if self.world > 1 and dist.is_available() and dist.is_initialized():
-            dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+            on_dev = torch.cuda.is_available() and dist.get_backend() == "nccl"
+            dev = torch.device("cuda", torch.cuda.current_device()) if on_dev else torch.device("cpu")
             t = torch.tensor([float(now)], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             arrive = int(t.item())
@@ -106,7 +107,17 @@ class DistributedSuite:
         cus = int(self.mod.gpu_cu_count())
         cfg = self.mod.parse_config(build_args(self.config, None, "cpu"))
         per = cfg["n_sm"] + cfg["n_mem"]
-        return max(1, cus // per) if cus else 1
+        return max(1, cus // per // self.ranks_per_gpu()) if cus else 1
+
+    @staticmethod
+    def ranks_per_gpu() -> int:
+        """Ranks of this node that share one GPU (1 in production: one rank per
+        MI355X).  Each rank's simulations must all stay co-resident with the
+        other ranks' on a shared card, so the CU groups are split between them."""
+        import torch
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+        ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
+        return max(1, -(-local_world // ndev)) if ndev else 1
 
     def _run_app(self, app_kl):
         import time

@@ -92,6 +92,11 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
             opts["-gpgpu_cache:dl2"] = ":".join(f) + "," + rest
             notes.append(f"L2 per sub-partition clamped from {sets}x{assoc} to {new_sets}x{assoc} lines "
                          f"(simulator limit {max_lines} lines)")
+    for key, pol in _write_policies(meas).items():
+        cur = opts.get(key, cfg.get(key))
+        if cur:
+            opts[key] = _set_write_policy(cur, *pol)
+            notes.append(f"{key} write policy {pol[0]}, write-allocate {pol[1]} from ub_cache_policy")
     applied = {}
     for k, v in opts.items():
         if cfg.get(k) != v:
@@ -112,6 +117,34 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
             for k in sorted(meas):
                 f.write(f"- {k}: {meas[k]}\n")
     return out, applied
+
+
+def _write_policies(meas: Dict[str, str]) -> Dict[str, Tuple[str, str]]:
+    """gpgpusim (write policy, write-allocate policy) letters of L1 and L2 from
+    ub_cache_policy's measurements (reference write_policy_mb programs):
+    a store hit that drops the line is write-evict 'E' (else write-through 'T'
+    for L1, write-back 'B' for L2); whole-line stores allocating while partial
+    ones miss is lazy-fetch-on-read 'L', both allocating 'W', neither 'N'."""
+    def flag(k):
+        return int(float(meas[k])) if k in meas else None
+    out = {}
+    l1_wa, l1_pa, l1_keep = flag("l1_write_allocate"), flag("l1_partial_write_allocate"), flag("l1_store_keeps_line")
+    if None not in (l1_wa, l1_pa, l1_keep):
+        out["-gpgpu_cache:dl1"] = ("T" if l1_keep else "E", "W" if l1_pa else ("L" if l1_wa else "N"))
+    l2_wa, l2_lazy, l2_keep = flag("l2_write_allocate"), flag("l2_lazy_fetch_on_read"), flag("l2_store_hit_keeps_line")
+    if None not in (l2_wa, l2_lazy, l2_keep):
+        out["-gpgpu_cache:dl2"] = ("B" if l2_keep else "E", ("L" if l2_lazy else "W") if l2_wa else "N")
+    return out
+
+
+def _set_write_policy(spec: str, wp: str, wa: str) -> str:
+    """Replace the write-policy / write-allocate letters of a cache spec
+    `<kind>:<sets>:<line>:<assoc>,<rep>:<wp>:<alloc>:<wa>:<index>,...`."""
+    groups = spec.split(",")
+    f = groups[1].split(":")
+    f[1], f[3] = wp, wa
+    groups[1] = ":".join(f)
+    return ",".join(groups)
 
 
 # --- search over the parameters the micro-benchmarks cannot demystify --------

@@ -40,6 +40,9 @@ def _parse():
     ap.add_argument("--apps", default="all")
     ap.add_argument("--trace-dir", default=None)
     ap.add_argument("--verbose", action="store_true")
+    # "nccl" (RCCL over xGMI) is the production path; "gloo" lets several ranks
+    # share one card to rehearse the multi-rank GPU-engine path on a 1-GPU box
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
     return ap.parse_args()
 
 
@@ -55,6 +58,16 @@ def _cycle_mae():
         return None
 
 
+def _resolve_app(rodinia, name: str) -> str:
+    """Full suite name for `name` ("nw" -> "nw-rodinia-2.0-ft"); unknown names fail."""
+    if name in rodinia.SUITE:
+        return name
+    hit = [k for k in rodinia.SUITE if k.split("-rodinia")[0] == name]
+    if not hit:
+        raise SystemExit(f"bench.py: unknown app {name!r}; known: {', '.join(rodinia.SUITE)}")
+    return hit[0]
+
+
 def main() -> int:
     a = _parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -68,8 +81,11 @@ def main() -> int:
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl" if use_cuda else "gloo")
-    dev = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
+        backend = a.dist_backend if a.dist_backend != "auto" else ("nccl" if use_cuda else "gloo")
+        dist.init_process_group(backend)
+    # collective operands live where the backend reads them
+    on_dev = use_cuda and (world == 1 or dist.get_backend() == "nccl")
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_dev else torch.device("cpu")
 
     from accel_sim_framework_distributed_amd import _native
     mod = _native.load(prefer_torch_runtime=True)
@@ -83,7 +99,7 @@ def main() -> int:
     from accel_sim_framework_distributed_amd.tracegen import rodinia
 
     tdir = a.trace_dir or os.path.join(tempfile.gettempdir(), f"asim_bench_rodinia_{os.getuid()}")
-    apps = None if a.apps == "all" else a.apps.split(",")
+    apps = None if a.apps == "all" else [_resolve_app(rodinia, x) for x in a.apps.split(",")]
     # every rank generates (or reuses) the deterministic synthetic traces
     # a generated subset never stands in for the full suite (and vice versa is fine)
     full_marker = os.path.join(tdir, ".complete-all")
@@ -96,6 +112,7 @@ def main() -> int:
     ar_dir = os.path.join(tdir, f"all-reduce-{max(1, world)}")
     ar_marker = os.path.join(ar_dir, ".complete")
     if rank == 0:
+        os.makedirs(tdir, exist_ok=True)
         if not os.path.exists(marker):
             rodinia.generate_suite(tdir, apps)
             open(marker, "w").write("ok")
