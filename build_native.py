@@ -31,6 +31,7 @@ CORE_SRC = [
     "csrc/config/icnt_config.cc",
     "csrc/trace/trace.cc",
     "csrc/engine/cpu_engine.cc",
+    "csrc/engine/check_engine.cc",
     "csrc/power/power.cc",
     "csrc/driver/simulator.cc",
     "csrc/driver/dump.cc",

@@ -267,7 +267,10 @@ const OptDef kOptions[] = {
     // ---- extensions of this simulator ----
     {"-icnt_latency", 'u', "8", "interconnect traversal latency in core cycles (= PDES epoch)"},
     {"-sim_max_outstanding_pkts", 'u', "128", "per-SM packets in flight before injection stalls"},
-    {"-sim_engine", 's', "cpu", "cpu | gpu cycle engine"},
+    {"-sim_engine", 's', "cpu", "cpu | gpu | check (gpu and cpu in lock step, states compared) cycle engine"},
+    {"-sim_check_interval", 'u', "4096", "-sim_engine check: cycles between state comparisons"},
+    {"-sim_check_primary", 's', "gpu", "-sim_engine check: engine checked against the cpu engine (gpu | cpu)"},
+    {"-sim_check_corrupt_at", 'u', "0", "-sim_engine check: perturb the reference state from this cycle (checker self-test)"},
     {"-sim_epochs_per_launch", 'u', "4096", "GPU engine epochs per persistent launch"},
     {"-collective_model", 's', "const", "const | ring | tree | packet collective timing"},
     {"-xgmi_link_bandwidth_gbps", 'f', "153.0", "per-link xGMI bandwidth (GB/s)"},
@@ -914,6 +917,9 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
     d.stat_sample_freq = v.empty() || v[0].empty() ? 500 : parse_u(v[0], "-gpgpu_runtime_stat");
   }
   d.engine = r.gets("-sim_engine");
+  d.check_interval = r.getu("-sim_check_interval");
+  d.check_primary = r.gets("-sim_check_primary");
+  d.check_corrupt_at = r.getu("-sim_check_corrupt_at");
   d.trace_enabled = r.getb("-trace_enabled");
   d.trace_components = r.gets("-trace_components");
   d.trace_sampling_core = (int32_t)r.geti("-trace_sampling_core");

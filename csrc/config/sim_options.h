@@ -80,7 +80,10 @@ struct DriverOpts {
   int32_t resume_option = 0, resume_kernel = 0;
   std::string checkpoint_dir;
   uint64_t stat_sample_freq = 500;
-  std::string engine;             // cpu | gpu
+  std::string engine;             // cpu | gpu | check
+  uint64_t check_interval = 4096;  // -sim_engine check
+  std::string check_primary = "gpu";
+  uint64_t check_corrupt_at = 0;
   bool trace_enabled = false;
   std::string trace_components;
   int32_t trace_sampling_core = 0;

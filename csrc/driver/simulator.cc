@@ -36,8 +36,19 @@ Simulator::Simulator(const std::vector<std::string>& args) {
     if (!eng_) throw std::runtime_error("-sim_engine gpu requested but the HIP engine is unavailable");
   } else if (dopt_.engine == "cpu") {
     eng_ = make_cpu_engine();
+  } else if (dopt_.engine == "check") {
+    std::unique_ptr<Engine> primary;
+    if (dopt_.check_primary == "gpu") {
+      primary = make_gpu_engine();
+      if (!primary) throw std::runtime_error("-sim_engine check: the HIP engine is unavailable");
+    } else if (dopt_.check_primary == "cpu") {
+      primary = make_cpu_engine();
+    } else {
+      throw OptionError("-sim_check_primary must be cpu or gpu");
+    }
+    eng_ = make_check_engine(std::move(primary), make_cpu_engine(), dopt_.check_interval, dopt_.check_corrupt_at);
   } else {
-    throw OptionError("-sim_engine must be cpu or gpu");
+    throw OptionError("-sim_engine must be cpu, gpu or check");
   }
   eng_->init(cfg_);
   if (dopt_.power_enabled) {

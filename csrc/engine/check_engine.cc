@@ -1,0 +1,132 @@
+// Lock-step engine checker (`-sim_engine check`).
+//
+// the reference has no race detection; its determinism rests on
+// a single host thread.  Here the cycle model runs as hundreds of concurrent
+// wavefronts (csrc/engine/gpu_engine.hip) or OpenMP threads
+// (cpu_engine.cc), made race-free by the two-phase epoch design
+// (csrc/model/epoch.h).  This engine drives the GPU engine and the CPU engine
+// side by side over the same kernel, stops both every `-sim_check_interval`
+// cycles and compares their complete timing-state images (save_state: every
+// SM and channel state, the epoch publication block, both mailbox parities,
+// the clocks) byte for byte.  The first divergence aborts the run with the
+// cycle and the state offset, which `-sim_check_interval 1` narrows to one
+// epoch.
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+#include "engine.h"
+
+namespace asim {
+namespace {
+
+class CheckEngine final : public Engine {
+ public:
+  CheckEngine(std::unique_ptr<Engine> a, std::unique_ptr<Engine> b, uint64_t every, uint64_t corrupt_at)
+      : a_(std::move(a)), b_(std::move(b)), every_(every ? every : 1), corrupt_at_(corrupt_at) {}
+  const char* name() const override { return "check"; }
+  void init(const SimCfg& c) override {
+    a_->init(c);
+    b_->init(c);
+  }
+  void load_kernel(const ReadyKernel& k, const KernelDesc& kd) override {
+    a_->load_kernel(k, kd);
+    b_->load_kernel(k, kd);
+  }
+  RunResult run_kernel(uint64_t start, bool flush_l1, const RunLimits& lim) override {
+    RunResult total;
+    bool resume = lim.resume;
+    for (;;) {
+      uint64_t cap = (resume ? a_->now() : start) + every_;
+      const bool final_cap = lim.max_cycle && lim.max_cycle <= cap;
+      if (final_cap) cap = lim.max_cycle;
+      RunLimits l{cap, lim.max_epochs, resume};
+      const RunResult ra = a_->run_kernel(start, flush_l1, l);
+      const RunResult rb = b_->run_kernel(start, flush_l1, l);
+      total.epochs += ra.epochs;
+      compare(ra, rb);
+      if (ra.done || ra.deadlock || !ra.hit_limit || final_cap) {
+        total.end_cycle = ra.end_cycle;
+        total.done = ra.done;
+        total.deadlock = ra.deadlock;
+        total.hit_limit = ra.hit_limit;
+        return total;
+      }
+      resume = true;
+    }
+  }
+  uint64_t now() const override { return a_->now(); }
+  void memcpy_fill_l2(uint64_t addr, uint64_t bytes) override {
+    a_->memcpy_fill_l2(addr, bytes);
+    b_->memcpy_fill_l2(addr, bytes);
+  }
+  void flush_l2() override {
+    a_->flush_l2();
+    b_->flush_l2();
+  }
+  void stats(std::vector<SMStats>& sm, std::vector<MemStats>& mem) override { a_->stats(sm, mem); }
+  void snapshot(std::vector<uint8_t>& out) override { a_->snapshot(out); }
+  void restore(const std::vector<uint8_t>& in) override {
+    a_->restore(in);
+    b_->restore(in);
+  }
+  void advance(uint64_t cycles) override {
+    a_->advance(cycles);
+    b_->advance(cycles);
+  }
+  void save_state(std::vector<uint8_t>& out) override { a_->save_state(out); }
+  void load_state(const std::vector<uint8_t>& in) override {
+    a_->load_state(in);
+    b_->load_state(in);
+  }
+  void trace_drain(std::vector<TraceEv>& out, uint64_t* dropped) override {
+    a_->trace_drain(out, dropped);
+    std::vector<TraceEv> discard;
+    uint64_t d = 0;
+    b_->trace_drain(discard, &d);
+  }
+
+ private:
+  void compare(const RunResult& ra, const RunResult& rb) {
+    ++checks_;
+    const uint64_t cyc = a_->now();
+    if (ra.end_cycle != rb.end_cycle || ra.done != rb.done || ra.deadlock != rb.deadlock ||
+        ra.hit_limit != rb.hit_limit || cyc != b_->now())
+      fail(cyc, "run results differ: " + std::string(a_->name()) + " end " + std::to_string(ra.end_cycle) +
+                    " done " + std::to_string(ra.done) + ", " + b_->name() + " end " + std::to_string(rb.end_cycle) +
+                    " done " + std::to_string(rb.done));
+    a_->save_state(ia_);
+    b_->save_state(ib_);
+    // fault injection for the checker's own test: perturb the reference image
+    if (corrupt_at_ && cyc >= corrupt_at_ && !ib_.empty()) ib_[ib_.size() / 2] ^= 0x5a;
+    if (ia_.size() != ib_.size())
+      fail(cyc, "state images differ in size (" + std::to_string(ia_.size()) + " vs " + std::to_string(ib_.size()) + ")");
+    for (size_t i = 0; i < ia_.size(); ++i)
+      if (ia_[i] != ib_[i])
+        fail(cyc, "state images diverge at byte " + std::to_string(i) + " of " + std::to_string(ia_.size()) + " (" +
+                      a_->name() + " 0x" + hex(ia_[i]) + ", " + b_->name() + " 0x" + hex(ib_[i]) + ")");
+  }
+  static std::string hex(uint8_t v) {
+    char b[4];
+    snprintf(b, sizeof(b), "%02x", v);
+    return b;
+  }
+  [[noreturn]] void fail(uint64_t cyc, const std::string& what) {
+    throw std::runtime_error("engine check failed at cycle " + std::to_string(cyc) + " (check point " +
+                             std::to_string(checks_) + "): " + what);
+  }
+
+  std::unique_ptr<Engine> a_, b_;
+  uint64_t every_, corrupt_at_;
+  uint64_t checks_ = 0;
+  std::vector<uint8_t> ia_, ib_;
+};
+
+}  // namespace
+
+std::unique_ptr<Engine> make_check_engine(std::unique_ptr<Engine> primary, std::unique_ptr<Engine> reference,
+                                          uint64_t interval, uint64_t corrupt_at) {
+  return std::unique_ptr<Engine>(new CheckEngine(std::move(primary), std::move(reference), interval, corrupt_at));
+}
+
+}  // namespace asim

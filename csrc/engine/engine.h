@@ -105,6 +105,12 @@ std::unique_ptr<Engine> make_cpu_engine();
 // defined in the HIP engine module; returns nullptr when no GPU is usable
 std::unique_ptr<Engine> make_gpu_engine();
 bool gpu_engine_available();
+// lock-step checker: runs `primary` and `reference` side by side and compares
+// their timing-state images every `interval` cycles (check_engine.cc);
+// `corrupt_at` (0 = off) perturbs the reference image from that cycle on, to
+// test the checker itself
+std::unique_ptr<Engine> make_check_engine(std::unique_ptr<Engine> primary, std::unique_ptr<Engine> reference,
+                                          uint64_t interval, uint64_t corrupt_at = 0);
 int gpu_cu_count();  // compute units of the current HIP device (0 if none)
 // compiled resources of the persistent engine kernel (empty if no HIP build):
 // registers, scratch, static LDS, plus the dynamic LDS the engine requests

@@ -122,3 +122,14 @@ def test_engine_kernel_resources(gpu_mod):
     assert k["scratch_bytes_per_lane"] <= 1024
     f = engine.footprint("QV100")
     assert f["blocks"] == 112 and f["concurrent_simulations"] >= 2
+
+
+def test_check_engine_gpu_vs_cpu_lockstep(gpu_mod, tmp_path):
+    """-sim_engine check: GPU and CPU engines run side by side, timing states
+    compared byte for byte every 512 cycles (SURVEY §5.2 --check mode)."""
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    kl = rodinia.generate_suite(str(tmp_path), ["nw-rodinia-2.0-ft"])["nw-rodinia-2.0-ft"]
+    c = sim.simulate(kl, "QV100", engine="cpu")
+    k = sim.simulate(kl, "QV100", engine="check", extra={"-sim_check_interval": "512"})
+    assert (k.tot_cycle, k.tot_insn) == (c.tot_cycle, c.tot_insn)
