@@ -9,8 +9,11 @@
 // cycles and compares their complete timing-state images (save_state: every
 // SM and channel state, the epoch publication block, both mailbox parities,
 // the clocks) byte for byte.  The first divergence aborts the run with the
-// cycle and the state offset, which `-sim_check_interval 1` narrows to one
-// epoch.
+// cycle and the unit whose state differs, which `-sim_check_interval 1`
+// narrows to one epoch.  Compared: the header, every SMState and ChanState and
+// the epoch publication block.  Mailbox packet slots are not: slots past a
+// mailbox's count are stale on one engine and zero on the other, and a packet
+// still in flight that differed reaches a unit state by the next check point.
 #include <cstdio>
 #include <stdexcept>
 #include <string>
@@ -26,6 +29,8 @@ class CheckEngine final : public Engine {
       : a_(std::move(a)), b_(std::move(b)), every_(every ? every : 1), corrupt_at_(corrupt_at) {}
   const char* name() const override { return "check"; }
   void init(const SimCfg& c) override {
+    n_sm_ = c.n_sm;
+    n_mem_ = c.n_mem;
     a_->init(c);
     b_->init(c);
   }
@@ -98,13 +103,23 @@ class CheckEngine final : public Engine {
     a_->save_state(ia_);
     b_->save_state(ib_);
     // fault injection for the checker's own test: perturb the reference image
-    if (corrupt_at_ && cyc >= corrupt_at_ && !ib_.empty()) ib_[ib_.size() / 2] ^= 0x5a;
-    if (ia_.size() != ib_.size())
+    if (corrupt_at_ && cyc >= corrupt_at_ && ib_.size() > sizeof(EngineStateHeader) + 64)
+      ib_[sizeof(EngineStateHeader) + 64] ^= 0x5a;
+    const size_t head = sizeof(EngineStateHeader), sm_end = head + (size_t)n_sm_ * sizeof(SMState),
+                 ch_end = sm_end + (size_t)n_mem_ * sizeof(ChanState), pub_end = ch_end + sizeof(EpochPub);
+    if (ia_.size() != ib_.size() || ia_.size() < pub_end)
       fail(cyc, "state images differ in size (" + std::to_string(ia_.size()) + " vs " + std::to_string(ib_.size()) + ")");
-    for (size_t i = 0; i < ia_.size(); ++i)
-      if (ia_[i] != ib_[i])
-        fail(cyc, "state images diverge at byte " + std::to_string(i) + " of " + std::to_string(ia_.size()) + " (" +
-                      a_->name() + " 0x" + hex(ia_[i]) + ", " + b_->name() + " 0x" + hex(ib_[i]) + ")");
+    for (size_t i = 0; i < pub_end; ++i)
+      if (ia_[i] != ib_[i]) {
+        std::string where = i < head     ? "header"
+                            : i < sm_end ? "SM " + std::to_string((i - head) / sizeof(SMState)) + " +" +
+                                               std::to_string((i - head) % sizeof(SMState))
+                            : i < ch_end ? "channel " + std::to_string((i - sm_end) / sizeof(ChanState)) + " +" +
+                                               std::to_string((i - sm_end) % sizeof(ChanState))
+                                         : "epoch block +" + std::to_string(i - ch_end);
+        fail(cyc, "states diverge in " + where + " (" + a_->name() + " 0x" + hex(ia_[i]) + ", " + b_->name() +
+                      " 0x" + hex(ib_[i]) + ")");
+      }
   }
   static std::string hex(uint8_t v) {
     char b[4];
@@ -119,6 +134,7 @@ class CheckEngine final : public Engine {
   std::unique_ptr<Engine> a_, b_;
   uint64_t every_, corrupt_at_;
   uint64_t checks_ = 0;
+  uint32_t n_sm_ = 0, n_mem_ = 0;
   std::vector<uint8_t> ia_, ib_;
 };
 
