@@ -100,24 +100,55 @@ class DistributedSuite:
         return self.mod.Simulator(args, self.verbose)
 
     def concurrency(self) -> int:
-        """Simulations that fit on this GPU at once (each needs one CU per
-        simulated SM and per memory channel, all co-resident)."""
+        """Simulations that run at once.  GPU engine: as many as fit on this
+        GPU (each needs all its unit blocks co-resident).  CPU engine: job
+        level parallelism, one single-threaded simulation per host core
+        (``ASIM_CPU_JOBS`` overrides the core count)."""
         if self.engine != "gpu":
-            return 1
+            n = int(os.environ.get("ASIM_CPU_JOBS", "0") or 0)
+            if n <= 0:
+                try:
+                    n = len(os.sched_getaffinity(0))
+                except AttributeError:  # pragma: no cover - non-Linux
+                    n = os.cpu_count() or 1
+            return max(1, min(len(self.apps) or 1, n))
         cus = int(self.mod.gpu_cu_count())
         cfg = self.mod.parse_config(build_args(self.config, None, "cpu"))
-        per = cfg["n_sm"] + cfg["n_mem"]
+        per = self.mod.gpu_cus_per_sim(cfg["n_sm"], cfg["n_mem"]) if hasattr(self.mod, "gpu_cus_per_sim") \
+            else cfg["n_sm"] + cfg["n_mem"]
         return max(1, cus // per // self.ranks_per_gpu()) if cus else 1
 
-    @staticmethod
-    def ranks_per_gpu() -> int:
-        """Ranks of this node that share one GPU (1 in production: one rank per
-        MI355X).  Each rank's simulations must all stay co-resident with the
-        other ranks' on a shared card, so the CU groups are split between them."""
-        import torch
-        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
-        ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
-        return max(1, -(-local_world // ndev)) if ndev else 1
+    _rpg_cache: Optional[int] = None
+
+    @classmethod
+    def ranks_per_gpu(cls) -> int:
+        """Ranks of this node that share one physical GPU (1 in production:
+        one rank per MI355X).  Co-resident simulations of ranks sharing a card
+        must split its CUs.  Decided from the devices' identities (host name +
+        PCI bus id, gathered over the process group), never from how many
+        devices a rank can see: with HIP_VISIBLE_DEVICES every rank sees one.
+        ``ASIM_RANKS_PER_GPU`` overrides."""
+        env = os.environ.get("ASIM_RANKS_PER_GPU")
+        if env:
+            return max(1, int(env))
+        if cls._rpg_cache is not None:
+            return cls._rpg_cache
+        n = 1
+        try:
+            import socket
+            import torch
+            import torch.distributed as dist
+            if torch.cuda.is_available() and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+                p = torch.cuda.get_device_properties(torch.cuda.current_device())
+                ident = getattr(p, "uuid", None) or getattr(p, "pci_bus_id", None)
+                me = (socket.gethostname(), str(ident), getattr(p, "pci_bus_id", -1), getattr(p, "pci_domain_id", -1))
+                allids = [None] * dist.get_world_size()
+                dist.all_gather_object(allids, me)
+                n = max(1, sum(1 for x in allids if x == me))
+        except Exception:  # pragma: no cover - identity unavailable: assume one rank per GPU
+            n = 1
+        cls._rpg_cache = n
+        return n
 
     def _run_app(self, app_kl):
         import time

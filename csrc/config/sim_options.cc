@@ -3,6 +3,7 @@
 #include <unistd.h>
 
 #include "icnt_config.h"
+#include "../model/addrdec.h"
 
 #include <algorithm>
 #include <cmath>
@@ -271,12 +272,15 @@ const OptDef kOptions[] = {
     {"-sim_check_interval", 'u', "4096", "-sim_engine check: cycles between state comparisons"},
     {"-sim_check_primary", 's', "gpu", "-sim_engine check: engine checked against the cpu engine (gpu | cpu)"},
     {"-sim_check_corrupt_at", 'u', "0", "-sim_engine check: perturb the reference state from this cycle (checker self-test)"},
+    {"-sim_check_corrupt_mailbox", 'u', "0", "-sim_engine check self-test: perturb a request-mailbox count instead of a unit state"},
     {"-sim_epochs_per_launch", 'u', "4096", "GPU engine epochs per persistent launch"},
     {"-collective_model", 's', "const", "const | ring | tree | packet collective timing"},
     {"-xgmi_link_bandwidth_gbps", 'f', "153.0", "per-link xGMI bandwidth (GB/s)"},
     {"-xgmi_link_latency_ns", 'f', "1000.0", "collective step latency (ns)"},
     {"-xgmi_links_per_gpu", 'u', "7", "xGMI links per GPU"},
     {"-sim_event_skip", 'b', "1", "fast-forward quiet SM cycles inside an epoch (results identical)"},
+    {"-sim_cpu_threads", 'u', "1", "CPU engine: OpenMP threads over the units of one epoch (1 = serial; "
+                                  "run simulations job-parallel instead)"},
     {"-collective_slice_bytes", 'u', "131072", "packet model: bytes per link packet (RCCL slice)"},
     {"-collective_max_channels", 'u', "16", "packet model: max parallel rings (channels)"},
     {"-collective_reduce_gbps", 'f', "900.0", "packet model: local memory bandwidth for reduce/copy (GB/s)"},
@@ -403,6 +407,8 @@ void setup_addrdec(SimCfg& c, const std::string& mapping, int mask_mode) {
         ++pos;
       }
   }
+  for (int f = 0; f < AF_COUNT; ++f) c.addr_runs[f] = make_runs(c.addr_mask[f], c.mk_hi[f], c.mk_lo[f]);
+  c.part_runs = make_runs(c.gap ? ~c.sub_id_mask : ~(c.addr_mask[AF_CHIP] | c.sub_id_mask), 64, 0);
 }
 
 void parse_dram_timing(SimCfg& c, const std::string& s0) {
@@ -743,6 +749,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.perfect_mem = r.getb("-gpgpu_perfect_mem") ? 1u : 0u;
   c.simple_dram = r.getb("-gpgpu_simple_dram_model") ? 1u : 0u;
   c.event_skip = r.getb("-sim_event_skip") ? 1u : 0u;
+  c.cpu_threads = r.getu("-sim_cpu_threads");
   c.trace_mask = 0;
   if (r.getb("-trace_enabled")) {
     static const std::pair<const char*, uint32_t> streams[] = {
@@ -920,6 +927,7 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.check_interval = r.getu("-sim_check_interval");
   d.check_primary = r.gets("-sim_check_primary");
   d.check_corrupt_at = r.getu("-sim_check_corrupt_at");
+  d.check_corrupt_mailbox = r.getu("-sim_check_corrupt_mailbox");
   d.trace_enabled = r.getb("-trace_enabled");
   d.trace_components = r.gets("-trace_components");
   d.trace_sampling_core = (int32_t)r.geti("-trace_sampling_core");

@@ -84,6 +84,7 @@ struct DriverOpts {
   uint64_t check_interval = 4096;  // -sim_engine check
   std::string check_primary = "gpu";
   uint64_t check_corrupt_at = 0;
+  uint32_t check_corrupt_mailbox = 0;
   bool trace_enabled = false;
   std::string trace_components;
   int32_t trace_sampling_core = 0;

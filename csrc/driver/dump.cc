@@ -49,17 +49,18 @@ std::string dump_sm_state(const SMState& s, const SimCfg& c) {
   bool any = false;
   for (uint32_t sc = 0; sc < (uint32_t)kMaxSched; ++sc)
     for (uint32_t u = 0; u < (uint32_t)U_COUNT; ++u)
-      if (s.idoc[sc][u].valid) {
-        o << " [sched " << sc << " unit " << u << " warp " << (int)s.idoc[sc][u].warp << " "
-          << opcode_name(s.idoc[sc][u].inst.opcode) << "]";
+      if (s.idoc_mask >> (sc * U_COUNT + u) & 1ull) {
+        const uint32_t k = sc * U_COUNT + u;
+        o << " [sched " << sc << " unit " << u << " warp " << (int)(s.idoc_meta[k] & 0xff) << " "
+          << opcode_name(s.idoc_inst[k].opcode) << "]";
         any = true;
       }
   o << (any ? "\n" : " empty\n") << "  operand collectors:";
   any = false;
   for (uint32_t i = 0; i < (uint32_t)kMaxOC; ++i)
-    if (s.oc[i].valid) {
-      o << " [oc " << i << " warp " << (int)s.oc[i].warp << " " << opcode_name(s.oc[i].inst.opcode) << " reads-left "
-        << (int)s.oc[i].nread << "]";
+    if (s.oc_mask >> i & 1u) {
+      o << " [oc " << i << " warp " << (int)(s.oc_info[i] & 0xff) << " " << opcode_name(s.oc_inst[i].opcode)
+        << " reads-left " << (int)((s.oc_banks[i] >> 40) & 0xff) << "]";
       any = true;
     }
   o << (any ? "\n" : " empty\n");

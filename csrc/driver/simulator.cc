@@ -46,7 +46,8 @@ Simulator::Simulator(const std::vector<std::string>& args) {
     } else {
       throw OptionError("-sim_check_primary must be cpu or gpu");
     }
-    eng_ = make_check_engine(std::move(primary), make_cpu_engine(), dopt_.check_interval, dopt_.check_corrupt_at);
+    eng_ = make_check_engine(std::move(primary), make_cpu_engine(), dopt_.check_interval, dopt_.check_corrupt_at,
+                             dopt_.check_corrupt_mailbox != 0);
   } else {
     throw OptionError("-sim_engine must be cpu, gpu or check");
   }

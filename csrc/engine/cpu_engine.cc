@@ -144,7 +144,11 @@ class CpuEngine : public Engine {
       const uint32_t cur = (uint32_t)(epoch_ & 1), prev = cur ^ 1u;
       const uint64_t t0 = cycle_, t1 = t0 + E;
       const int nsm = (int)sms_.size(), nch = (int)chs_.size();
-#pragma omp parallel for schedule(dynamic, 1)
+      // serial by default: at 8-cycle epochs the parallel region costs more
+      // than it saves (8 threads measured 8.1k vs 10.8k KIPS serial); whole
+      // simulations run job-parallel instead (parallel/multi_gpu.py)
+      const int nthr = c.cpu_threads > 1 ? (int)c.cpu_threads : 1;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthr) if (nthr > 1)
       for (int i = 0; i < nsm + nch; ++i) {
         if (i < nsm) {
           SMState& s = sms_[i];

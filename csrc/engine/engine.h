@@ -108,9 +108,10 @@ bool gpu_engine_available();
 // lock-step checker: runs `primary` and `reference` side by side and compares
 // their timing-state images every `interval` cycles (check_engine.cc);
 // `corrupt_at` (0 = off) perturbs the reference image from that cycle on, to
-// test the checker itself
+// test the checker itself (a unit state byte, or with `corrupt_mailbox` the
+// first request-mailbox count)
 std::unique_ptr<Engine> make_check_engine(std::unique_ptr<Engine> primary, std::unique_ptr<Engine> reference,
-                                          uint64_t interval, uint64_t corrupt_at = 0);
+                                          uint64_t interval, uint64_t corrupt_at = 0, bool corrupt_mailbox = false);
 int gpu_cu_count();  // compute units of the current HIP device (0 if none)
 // compiled resources of the persistent engine kernel (empty if no HIP build):
 // registers, scratch, static LDS, plus the dynamic LDS the engine requests

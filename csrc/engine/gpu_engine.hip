@@ -60,6 +60,7 @@ struct GpuArgs {
   uint32_t nblocks;
   GpuCtl* ctl;
   uint64_t* prof;  // [nblocks][kProfSlots] shader-clock cycles per stage (profiling build)
+  uint32_t* ework; // [nblocks] work clocks of the last epoch (profiling build)
 };
 
 template <class T>
@@ -76,7 +77,7 @@ extern __shared__ __attribute__((aligned(16))) char g_lds[];
 constexpr size_t kStateLds = ((sizeof(SMState) > sizeof(ChanState) ? sizeof(SMState) : sizeof(ChanState)) + 15) / 16 * 16;
 constexpr size_t kCfgOff = kStateLds + (sizeof(KernelDesc) + 15) / 16 * 16;
 constexpr size_t kProfOff = kCfgOff + (sizeof(SimCfg) + 15) / 16 * 16;
-constexpr int kProfSlots = 32;
+constexpr int kProfSlots = 36;
 struct ProfLds {
   uint64_t last;
   uint32_t slot;
@@ -129,7 +130,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   if ((threadIdx.x & 63) == 0) {
     *kdl = a.kd;
     pl->last = __builtin_amdgcn_s_memtime();
-    pl->slot = kProfSlots - 1;
+    pl->slot = 31;
     for (int i = 0; i < kProfSlots; ++i) pl->acc[i] = 0;
   }
   __syncthreads();
@@ -152,6 +153,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     sm_kernel_init<P>(*s, sx, s->ks, a.cycle0, a.flush_l1);
   }
   uint64_t epoch = a.epoch0, cycle = a.cycle0;
+  uint64_t t_work0 = a.ework ? __builtin_amdgcn_s_memtime() : 0;
   uint32_t done = 0, dead = 0;
   uint32_t n = 0;
   for (; n < a.max_epochs;) {
@@ -172,8 +174,26 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     }
     ++n;
     P::prof(26);  // barrier
-    if (!grid_barrier(a.ctl, a.nblocks, n - 1)) break;
+    uint64_t t_arrive = 0;
+    if (a.ework) {
+      t_arrive = __builtin_amdgcn_s_memtime();
+      if ((threadIdx.x & 63) == 0) a.ework[b] = (uint32_t)(t_arrive - t_work0);
+    }
+    uint32_t was_last = 0;
+    if (!grid_barrier(a.ctl, a.nblocks, n - 1, &was_last)) break;
     P::prof(27);  // decision
+    if (a.ework) {
+      const uint64_t t_exit = __builtin_amdgcn_s_memtime();
+      if ((threadIdx.x & 63) == 0 && was_last) { pl->acc[34] += t_exit - t_arrive; pl->acc[35] += 1; }
+      if (b == 0) {
+        // slowest block's work this epoch (critical path) and the epoch count
+        uint32_t m = 0;
+        for (uint32_t j = threadIdx.x & 63; j < a.nblocks; j += 64) m = a.ework[j] > m ? a.ework[j] : m;
+        m = WavePar::wave_reduce(m, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
+        if ((threadIdx.x & 63) == 0) { pl->acc[32] += m; pl->acc[33] += 1; }
+      }
+      t_work0 = t_exit;
+    }
     const uint32_t next_done = a.pub->next_cta[cur] >= kd.n_cta ? 1u : 0u;
     EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, a.ready_cycle, next_done, epoch, a.max_cycle);
     P::prof(28);
@@ -183,7 +203,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     if (P::uni(d.deadlock)) { dead = 1; break; }
     if (a.max_cycle && cycle >= a.max_cycle) break;
   }
-  P::prof(kProfSlots - 1);
+  P::prof(31);  // launch_rest
   // write state back
   if (is_sm)
     copy_state(&a.sms[b], s);
@@ -249,6 +269,7 @@ class GpuEngine : public Engine {
     } catch (...) {
     }
     if (d_prof_) (void)hipFree(d_prof_);
+    if (d_ework_) (void)hipFree(d_ework_);
     release();
   }
   const char* name() const override { return "gpu"; }
@@ -275,6 +296,7 @@ class GpuEngine : public Engine {
     if (profiling_) {
       HIPCHECK(hipMalloc(&d_prof_, sizeof(uint64_t) * nblocks_ * kProfSlots));
       HIPCHECK(hipMemset(d_prof_, 0, sizeof(uint64_t) * nblocks_ * kProfSlots));
+      HIPCHECK(hipMalloc(&d_ework_, sizeof(uint32_t) * nblocks_));
     }
     HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     if (c_.trace_mask) {
@@ -301,15 +323,20 @@ class GpuEngine : public Engine {
     cap_req_ = c.icnt_latency;
     cap_rep_ = reply_cap(c);
     for (int p = 0; p < 2; ++p) {
+      // mailboxes start zeroed (like the CPU engine's) so state images and
+      // checkpoints never carry uninitialised device memory
       HIPCHECK(hipMalloc(&d_box_req_[p], sizeof(Pkt) * c.n_subpart * c.n_sm * cap_req_));
+      HIPCHECK(hipMemset(d_box_req_[p], 0, sizeof(Pkt) * c.n_subpart * c.n_sm * cap_req_));
       HIPCHECK(hipMalloc(&d_cnt_req_[p], sizeof(uint32_t) * c.n_subpart * c.n_sm));
       HIPCHECK(hipMemset(d_cnt_req_[p], 0, sizeof(uint32_t) * c.n_subpart * c.n_sm));
       HIPCHECK(hipMalloc(&d_box_rep_[p], sizeof(Pkt) * c.n_sm * c.n_subpart * cap_rep_));
+      HIPCHECK(hipMemset(d_box_rep_[p], 0, sizeof(Pkt) * c.n_sm * c.n_subpart * cap_rep_));
       HIPCHECK(hipMalloc(&d_cnt_rep_[p], sizeof(uint32_t) * c.n_sm * c.n_subpart));
       HIPCHECK(hipMemset(d_cnt_rep_[p], 0, sizeof(uint32_t) * c.n_sm * c.n_subpart));
     }
     ovf_cap_ = backlog_cap(c);
     HIPCHECK(hipMalloc(&d_ovf_, sizeof(Pkt) * c.n_subpart * (size_t)ovf_cap_));
+    HIPCHECK(hipMemset(d_ovf_, 0, sizeof(Pkt) * c.n_subpart * (size_t)ovf_cap_));
     HIPCHECK(hipMalloc(&d_ctl_, sizeof(GpuCtl)));
     HIPCHECK(hipHostMalloc(&h_ctl_, sizeof(GpuCtl)));
     epoch_ = 0;
@@ -362,6 +389,7 @@ class GpuEngine : public Engine {
       a.ctl = d_ctl_;
       HIPCHECK(hipMemsetAsync(d_ctl_, 0, sizeof(GpuCtl), stream_));
       a.prof = d_prof_;
+      a.ework = d_ework_;
       CuPool::get().acquire((int)nblocks_);
       hipError_t le;
       if (profiling_)
@@ -584,6 +612,7 @@ class GpuEngine : public Engine {
   uint32_t epochs_per_launch_ = 4096;
   bool profiling_ = false;
   uint64_t* d_prof_ = nullptr;
+  uint32_t* d_ework_ = nullptr;
 
  public:
   // per-stage shader-clock totals: [0] = mean over SM blocks, [1] = mean over channel blocks
@@ -595,12 +624,13 @@ class GpuEngine : public Engine {
         "sm.receive", "sm.writeback", "sm.hit_complete", "sm.ldst", "sm.dispatch", "sm.read_operands",
         "sm.alloc_oc", "sm.issue", "sm.fetch", "sm.retire", "sm.inject", "sm.occupancy", "sm.gather",
         "sm.cta_dispatch", "sm.refill", "sm.cycle_loop", "sm.publish", "#sm_cycles", "#quiet_checks", "#epochs_busy", "mem.gather", "mem.dram",
-        "mem.l2", "mem.icnt", "mem.window_other", "mem.publish", "barrier", "decide", "post", "sm.issue_sched", "-", "launch_rest"};
+        "mem.l2", "mem.icnt", "mem.window_other", "mem.publish", "barrier", "decide", "post", "sm.issue_sched", "-", "launch_rest",
+        "#max_work/epoch", "#epochs(b0)", "#last_arriver_wait", "#last_arrivals"};
     double sm[kProfSlots] = {}, mc[kProfSlots] = {}, smt = 0, mct = 0;
     for (uint32_t b = 0; b < nblocks_; ++b)
       for (int k = 0; k < kProfSlots; ++k) {
         double v = (double)h[(size_t)b * kProfSlots + k];
-        const bool counter = k >= 17 && k <= 19;
+        const bool counter = (k >= 17 && k <= 19) || k >= 32;
         if (b < c_.n_sm) { sm[k] += v / c_.n_sm; smt += counter ? 0 : v / c_.n_sm; }
         else { mc[k] += v / c_.n_mem; mct += counter ? 0 : v / c_.n_mem; }
       }
@@ -618,20 +648,32 @@ class GpuEngine : public Engine {
                       "(cycle_loop %.0f clocks each), busy SM-epochs %.0f\n",
               n_cyc, n_cyc ? cyc_clk / n_cyc : 0, n_q, n_q ? q_clk / n_q : 0, n_ep);
     }
+    {
+      double mx = 0, ne = 0, lw = 0, nl = 0;
+      for (uint32_t b = 0; b < nblocks_; ++b) {
+        mx += (double)h[(size_t)b * kProfSlots + 32];
+        ne += (double)h[(size_t)b * kProfSlots + 33];
+        lw += (double)h[(size_t)b * kProfSlots + 34];
+        nl += (double)h[(size_t)b * kProfSlots + 35];
+      }
+      fprintf(stderr, "[asim gpu profile] epochs %.0f: slowest block's work %.0f clocks/epoch; last arriver's "
+                      "barrier wait %.0f clocks/epoch (pure barrier latency)\n",
+              ne, ne ? mx / ne : 0, nl ? lw / nl : 0);
+    }
     // the critical block: most time outside the barrier wait
     uint32_t crit = 0;
     double crit_work = -1;
     for (uint32_t b = 0; b < nblocks_; ++b) {
       double w = 0;
       for (int k = 0; k < kProfSlots; ++k)
-        if (k != 26 && !(k >= 17 && k <= 19)) w += (double)h[(size_t)b * kProfSlots + k];
+        if (k != 26 && !(k >= 17 && k <= 19) && k < 32) w += (double)h[(size_t)b * kProfSlots + k];
       if (w > crit_work) { crit_work = w; crit = b; }
     }
     fprintf(stderr, "[asim gpu profile] shader-clock cycles per block (mean), share of block time; "
                     "CRIT = block %u (%s), the one with the least barrier wait\n", crit, crit < c_.n_sm ? "SM" : "MEM");
     double ct = 0;
     for (int k = 0; k < kProfSlots; ++k)
-      if (!(k >= 17 && k <= 19)) ct += (double)h[(size_t)crit * kProfSlots + k];
+      if (!(k >= 17 && k <= 19) && k < 32) ct += (double)h[(size_t)crit * kProfSlots + k];
     for (int k = 0; k < kProfSlots; ++k) {
       const double cv = (double)h[(size_t)crit * kProfSlots + k];
       if (sm[k] + mc[k] > 0)

@@ -30,13 +30,15 @@ struct GpuCtl {  // zeroed by hipMemsetAsync before every launch
 // no single line is hammered by every block while the arrivals queue behind
 // it.  One agent release before arriving and one agent acquire after leaving.
 template <bool kFence = true>
-__device__ __forceinline__ bool grid_barrier(GpuCtl* ctl, uint32_t nblocks, uint32_t epoch_in_launch) {
+__device__ __forceinline__ bool grid_barrier(GpuCtl* ctl, uint32_t nblocks, uint32_t epoch_in_launch,
+                                             uint32_t* was_last = nullptr) {
   const uint32_t b = blockIdx.x;
   const uint32_t grp = b & 7u;
   const uint32_t ngrp = nblocks < 8 ? nblocks : 8u;
   const uint32_t in_grp = (nblocks - grp + 7u) / 8u;  // members of this group
   const uint32_t target = epoch_in_launch + 1u;
   bool ok = true;
+  uint32_t last = 0;
   // every lane's stores must be complete and visible at agent scope
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (kFence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -46,6 +48,7 @@ __device__ __forceinline__ bool grid_barrier(GpuCtl* ctl, uint32_t nblocks, uint
     if (prev + 1u == target * in_grp) {
       // last of its group: forward to the top counter
       uint32_t t = __hip_atomic_fetch_add(&ctl->top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1u == target * ngrp) last = 1;
       if (t + 1u == target * ngrp)
         for (uint32_t g = 0; g < ngrp; ++g)
           __hip_atomic_store(&ctl->gen[g][0], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -65,6 +68,7 @@ __device__ __forceinline__ bool grid_barrier(GpuCtl* ctl, uint32_t nblocks, uint
     }
   }
   ok = __builtin_amdgcn_readlane(ok ? 1 : 0, 0) != 0;
+  if (was_last) *was_last = (uint32_t)__builtin_amdgcn_readlane((int)last, 0);
   if (kFence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   return ok;

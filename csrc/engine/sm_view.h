@@ -50,8 +50,16 @@ struct WarpReg {
   T v;
   __device__ __forceinline__ T get(int w) const {
     const int w0 = __builtin_amdgcn_readfirstlane(w);
-    if (__builtin_amdgcn_ballot_w64(w != w0) == 0)
-      return (T)__builtin_amdgcn_readlane((int)(uint32_t)v, w0);
+    if (__builtin_amdgcn_ballot_w64(w != w0) == 0) {
+      if constexpr (sizeof(T) == 8) {
+        const uint64_t u = (uint64_t)v;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, w0);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), w0);
+        return (T)(((uint64_t)hi << 32) | lo);
+      } else {
+        return (T)__builtin_amdgcn_readlane((int)(uint32_t)v, w0);
+      }
+    }
     return v;
   }
   __device__ __forceinline__ void put(int w, T x) {
@@ -88,69 +96,73 @@ struct WarpReg {
   };
   __device__ __forceinline__ Ref operator[](int w) { return Ref{this, w}; }
   __device__ __forceinline__ T operator[](int w) const { return get(w); }
+  // arrays shorter than the wave: lanes past the end hold 0 and store nothing
   template <class A>
   __device__ __forceinline__ void load(const A& arr) {
-    v = arr[sv_lane()];
+    constexpr int n = (int)std::extent<A>::value;
+    if constexpr (n >= 64) {
+      v = arr[sv_lane()];
+    } else {
+      v = sv_lane() < n ? arr[sv_lane() < n ? sv_lane() : 0] : (T)0;
+    }
   }
   template <class A>
   __device__ __forceinline__ void store(A& arr) const {
-    arr[sv_lane()] = v;
+    constexpr int n = (int)std::extent<A>::value;
+    if (n >= 64 || sv_lane() < n) arr[sv_lane() < n ? sv_lane() : 0] = v;
   }
 };
+
+// the scoreboard of this lane's warp: four 64-bit register words per lane
+// (csrc/model/sm.h sbt/sbs/sbc/sbz are overloaded for it below)
+struct WarpSb {
+  uint64_t v[4];
+  __device__ __forceinline__ uint64_t word(uint32_t k) const {
+    return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3];
+  }
+  template <class A>
+  __device__ __forceinline__ void load(const A& arr) {
+    const int l = sv_lane();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = arr[l][k];
+  }
+  template <class A>
+  __device__ __forceinline__ void store(A& arr) const {
+    const int l = sv_lane();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) arr[l][k] = v[k];
+  }
+};
+__device__ __forceinline__ bool sbt(const WarpSb& sb, uint32_t w, uint8_t r) {
+  if (!r) return false;
+  const uint32_t k = (uint32_t)r >> 6;
+  uint64_t m = sb.word(k);
+  const int w0 = __builtin_amdgcn_readfirstlane((int)w);
+  if (__builtin_amdgcn_ballot_w64((int)w != w0) == 0) {  // wave-uniform (warp, register)
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, w0);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), w0);
+    m = ((uint64_t)hi << 32) | lo;
+  }
+  return (m >> (r & 63)) & 1ull;
+}
+__device__ __forceinline__ void sb_upd(WarpSb& sb, uint32_t w, uint8_t r, bool set) {
+  if (!r) return;
+  const uint32_t k = (uint32_t)r >> 6;
+  const uint64_t bit = 1ull << (r & 63);
+  const bool me = sv_lane() == (int)w;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j)
+    if (me && j == k) sb.v[j] = set ? (sb.v[j] | bit) : (sb.v[j] & ~bit);
+}
+__device__ __forceinline__ void sbs(WarpSb& sb, uint32_t w, uint8_t r) { sb_upd(sb, w, r, true); }
+__device__ __forceinline__ void sbc(WarpSb& sb, uint32_t w, uint8_t r) { sb_upd(sb, w, r, false); }
+__device__ __forceinline__ void sbz(WarpSb& sb, uint32_t w) {
+  if (sv_lane() == (int)w) sb.v[0] = sb.v[1] = sb.v[2] = sb.v[3] = 0;
+}
 
 #define SV_REF(m) decltype(B::m)& m
 #define SV_VAL(m) decltype(B::m) m
 #define SV_WARP(m) WarpReg<typename std::remove_extent<decltype(B::m)>::type> m
-
-// statistics: scalars in registers, arrays by reference
-template <class B>
-struct SmStatsView {
-  SV_VAL(thread_insn);
-  SV_VAL(warp_insn);
-  SV_REF(cls_insn);
-  SV_VAL(active_cycles);
-  SV_VAL(busy_cycles);
-  SV_VAL(issue_stall_idle);
-  SV_VAL(sb_stall);
-  SV_VAL(pipe_stall);
-  SV_REF(l1);
-  SV_VAL(shmem_acc);
-  SV_VAL(shmem_conflict_cycles);
-  SV_VAL(pkts_out);
-  SV_VAL(pkts_in);
-  SV_VAL(bytes_out);
-  SV_VAL(bytes_in);
-  SV_VAL(rf_reads);
-  SV_VAL(rf_writes);
-  SV_VAL(oc_bank_conflicts);
-  SV_VAL(ctas_done);
-  SV_VAL(warps_done);
-  SV_VAL(occupancy_acc);
-  SV_VAL(mem_insn);
-  SV_REF(power_acc);
-  SV_VAL(mf_lat_sum);
-  SV_VAL(mf_lat_n);
-  SV_VAL(mf_lat_max);
-  SV_REF(mf_lat_hist);
-  SV_REF(il1);
-#define SV_SCALARS(X)                                                                                    \
-  X(thread_insn) X(warp_insn) X(active_cycles) X(busy_cycles) X(issue_stall_idle) X(sb_stall) X(pipe_stall) \
-  X(shmem_acc) X(shmem_conflict_cycles) X(pkts_out) X(pkts_in) X(bytes_out) X(bytes_in) X(rf_reads)         \
-  X(rf_writes) X(oc_bank_conflicts) X(ctas_done) X(warps_done) X(occupancy_acc) X(mem_insn) X(mf_lat_sum)   \
-  X(mf_lat_n) X(mf_lat_max)
-  __device__ __forceinline__ explicit SmStatsView(B& b)
-      : cls_insn(b.cls_insn), l1(b.l1), power_acc(b.power_acc), mf_lat_hist(b.mf_lat_hist), il1(b.il1) {
-#define SV_LD(m) m = sv_uni(b.m);
-    SV_SCALARS(SV_LD)
-#undef SV_LD
-  }
-  __device__ __forceinline__ void flush(B& b) const {
-#define SV_ST(m) b.m = m;
-    SV_SCALARS(SV_ST)
-#undef SV_ST
-  }
-#undef SV_SCALARS
-};
 
 template <class B>
 struct SmView {
@@ -173,24 +185,28 @@ struct SmView {
   SV_WARP(w_inflight);
   SV_WARP(w_stores);
   SV_WARP(w_loads);
-  SV_REF(w_sb);
+  WarpSb w_sb;
   SV_WARP(w_slot_used);
   SV_REF(w_slot_pend);
   SV_REF(w_slot_dst);
   SV_REF(w_win);
   SV_REF(cta_id);
-  SV_REF(cta_valid);
-  SV_REF(cta_live);
-  SV_REF(cta_bar);
-  SV_REF(cta_nexit);
+  SV_WARP(cta_valid);
+  SV_WARP(cta_live);
+  SV_WARP(cta_bar);
+  SV_WARP(cta_nexit);
   SV_VAL(n_cta_active);
   SV_VAL(n_warps_live);
   SV_VAL(n_wait_flags);
   SV_VAL(fetch_rr);
-  SV_REF(sched_last);
-  SV_REF(idoc);
-  SV_REF(oc);
-  SV_REF(fu_next);
+  SV_WARP(sched_last);
+  SV_REF(idoc_inst);
+  SV_WARP(idoc_meta);
+  SV_REF(oc_inst);
+  SV_WARP(oc_info);
+  SV_WARP(oc_banks);
+  SV_WARP(oc_age);
+  SV_WARP(fu_next);
   SV_REF(wb_cnt);
   SV_REF(wb);
   SV_VAL(ldst);
@@ -202,13 +218,13 @@ struct SmView {
   SV_VAL(n_pend);
   SV_REF(il1);
   SV_REF(imshr);
-  SV_REF(w_iline);
+  SV_WARP(w_iline);
   SV_VAL(idoc_mask);
   SV_VAL(oc_mask);
   SV_VAL(oc_read_mask);
   SV_VAL(l1_stamp);
-  SV_REF(wb_occ);
-  SV_REF(hit_occ);
+  SV_WARP(wb_occ);
+  SV_WARP(hit_occ);
   SV_VAL(skipped_cycles);
   SV_VAL(min_emit);
   SV_REF(outq);
@@ -223,28 +239,57 @@ struct SmView {
   SV_REF(sref);
   SV_REF(srank);
   SV_REF(ks);
-  decltype(B::st)& st;  // statistics stay in LDS (SGPR pressure)
+  // statistics: counter word k lives in lane (k & 63) of stv[k >> 6], so an
+  // update is one masked VALU add instead of an LDS read-modify-write
+  uint64_t stv[2];
+  __device__ __forceinline__ void sadd(uint32_t k, uint64_t d) {
+    if (sv_lane() == (int)(k & 63u)) {
+      if (k < 64u) stv[0] += d;
+      else stv[1] += d;
+    }
+  }
+  __device__ __forceinline__ uint64_t sget(uint32_t k) const {
+    const uint64_t m = k < 64u ? stv[0] : stv[1];
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, (int)(k & 63u));
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), (int)(k & 63u));
+    return ((uint64_t)hi << 32) | lo;
+  }
+  __device__ __forceinline__ void sset(uint32_t k, uint64_t v) {
+    if (sv_lane() == (int)(k & 63u)) {
+      if (k < 64u) stv[0] = v;
+      else stv[1] = v;
+    }
+  }
 
 #define SV_SCALARS(X)                                                                                   \
   X(id) X(kernel_cta_slots) X(last_progress) X(epoch_end) X(out_port_free) X(age_ctr) X(n_cta_active)    \
   X(n_warps_live) X(n_wait_flags) X(fetch_rr) X(n_pend) X(idoc_mask) X(oc_mask) X(oc_read_mask)         \
   X(l1_stamp) X(skipped_cycles) X(min_emit) X(outq_head) X(outq_n) X(outstanding) X(inq_head) X(inq_n)
 #define SV_WARPS(X) \
-  X(w_next) X(w_end) X(w_head) X(w_age) X(w_flags) X(w_ibuf) X(w_cta) X(w_inflight) X(w_stores) X(w_loads) X(w_slot_used)
+  X(w_next) X(w_end) X(w_head) X(w_age) X(w_flags) X(w_ibuf) X(w_cta) X(w_inflight) X(w_stores) X(w_loads) X(w_slot_used) \
+  X(idoc_meta) X(oc_info) X(oc_banks) X(oc_age) X(fu_next) X(wb_occ) X(hit_occ) X(cta_valid) X(cta_live) X(cta_bar) \
+  X(cta_nexit) X(sched_last) X(w_iline)
 
   __device__ __forceinline__ explicit SmView(B& b)
-      : base(b), cycle(b.cycle), w_wfill(b.w_wfill), w_sb(b.w_sb), w_slot_pend(b.w_slot_pend),
-        w_slot_dst(b.w_slot_dst), w_win(b.w_win), cta_id(b.cta_id), cta_valid(b.cta_valid), cta_live(b.cta_live),
-        cta_bar(b.cta_bar), cta_nexit(b.cta_nexit), sched_last(b.sched_last), idoc(b.idoc), oc(b.oc),
-        fu_next(b.fu_next), wb_cnt(b.wb_cnt), wb(b.wb), hit_cnt(b.hit_cnt), hit(b.hit), l1(b.l1), mshr(b.mshr),
-        pend(b.pend), il1(b.il1), imshr(b.imshr), w_iline(b.w_iline), wb_occ(b.wb_occ), hit_occ(b.hit_occ),
-        outq(b.outq), ocnt(b.ocnt), inq(b.inq), skey(b.skey), sref(b.sref), srank(b.srank), ks(b.ks), st(b.st) {
+      : base(b), cycle(b.cycle), w_wfill(b.w_wfill), w_slot_pend(b.w_slot_pend),
+        w_slot_dst(b.w_slot_dst), w_win(b.w_win), cta_id(b.cta_id),
+        idoc_inst(b.idoc_inst), oc_inst(b.oc_inst),
+        wb_cnt(b.wb_cnt), wb(b.wb), hit_cnt(b.hit_cnt), hit(b.hit), l1(b.l1), mshr(b.mshr),
+        pend(b.pend), il1(b.il1), imshr(b.imshr),
+        outq(b.outq), ocnt(b.ocnt), inq(b.inq), skey(b.skey), sref(b.sref), srank(b.srank), ks(b.ks) {
 #define SV_LD(m) m = sv_uni(b.m);
     SV_SCALARS(SV_LD)
 #undef SV_LD
 #define SV_LDW(m) m.load(b.m);
     SV_WARPS(SV_LDW)
 #undef SV_LDW
+    w_sb.load(b.w_sb);
+    {
+      const uint64_t* sw = reinterpret_cast<const uint64_t*>(&b.st);
+      const int l = sv_lane();
+      stv[0] = l < kStatWords ? sw[l] : 0ull;
+      stv[1] = l + 64 < kStatWords ? sw[l + 64 < kStatWords ? l + 64 : 0] : 0ull;
+    }
     {  // LdstState: 16-byte words through readfirstlane
       uint32_t w[sizeof(ldst) / 4];
       __builtin_memcpy(w, &b.ldst, sizeof(ldst));
@@ -261,6 +306,13 @@ struct SmView {
 #define SV_STW(m) m.store(base.m);
     SV_WARPS(SV_STW)
 #undef SV_STW
+    w_sb.store(base.w_sb);
+    {
+      uint64_t* sw = reinterpret_cast<uint64_t*>(&base.st);
+      const int l = sv_lane();
+      if (l < kStatWords) sw[l] = stv[0];
+      if (l + 64 < kStatWords) sw[l + 64] = stv[1];
+    }
     base.ldst = ldst;
   }
 #undef SV_SCALARS

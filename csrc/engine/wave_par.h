@@ -139,6 +139,70 @@ struct WavePar {
     }
     return (rh == ~0u && rl == ~0u) ? -1 : (int)ri;
   }
+  // per-lane values (hd.h SeqPar::lanes): computed once per lane, handed to
+  // uniform code with one v_readlane per 32-bit word
+  template <class T>
+  struct LaneVal {
+    T v;
+    __device__ __forceinline__ T self(int) const { return v; }
+    __device__ __forceinline__ T at(int i) const {
+      static_assert(sizeof(T) % 4 == 0, "LaneVal: word-multiple types");
+      uint32_t w[sizeof(T) / 4];
+      __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(T) / 4); ++k) w[k] = rdl(w[k], i);
+      T r;
+      __builtin_memcpy(&r, w, sizeof(T));
+      return r;
+    }
+  };
+  template <class T, class F>
+  static __device__ __forceinline__ LaneVal<T> lanes(int n, F&& f) {
+    LaneVal<T> r;
+    if (lane() < n) r.v = f(lane());
+    else __builtin_memset(&r.v, 0, sizeof(T));
+    return r;
+  }
+  // members of `mask` (n <= 16) by ascending key, 4 bits per rank (hd.h
+  // SeqPar::order16): lane i ranks itself against every member (readlane
+  // loop over the mask in SGPRs), then one OR-reduction packs the order
+  template <class F>
+  static __device__ __forceinline__ uint64_t order16(int n, uint32_t mask, F&& key) {
+    const int l = lane();
+    const bool mine = l < n && (mask >> l & 1u);
+    const uint32_t k = mine ? (uint32_t)key(l) : 0u;
+    uint32_t r = 0;
+    for (uint32_t m = mask; m;) {
+      const int j = __builtin_ctz(m);
+      m &= m - 1;
+      const uint32_t kj = rdl(k, j);
+      r += (j != l && (kj < k || (kj == k && j < l))) ? 1u : 0u;
+    }
+    const uint64_t v = mine ? ((uint64_t)(uint32_t)l << (4 * r)) : 0ull;
+    auto o = [](uint32_t a, uint32_t b) { return a | b; };
+    const uint32_t lo = wave_reduce((uint32_t)v, o), hi = wave_reduce((uint32_t)(v >> 32), o);
+    return ((uint64_t)hi << 32) | lo;
+  }
+  // smallest i < n with pred(i): four 64-lane chunks are evaluated (their
+  // loads in flight together) before the first hit is picked by ballot + ffs
+  template <class F>
+  static __device__ __forceinline__ int find_first(int n, F&& pred) {
+    const int l = lane();
+    for (int b = 0; b < n; b += 256) {
+      bool p0 = false, p1 = false, p2 = false, p3 = false;
+      if (b + l < n) p0 = pred(b + l);
+      if (b + 64 < n && b + 64 + l < n) p1 = pred(b + 64 + l);
+      if (b + 128 < n && b + 128 + l < n) p2 = pred(b + 128 + l);
+      if (b + 192 < n && b + 192 + l < n) p3 = pred(b + 192 + l);
+      const uint64_t m0 = (uint64_t)__ballot(p0), m1 = (uint64_t)__ballot(p1), m2 = (uint64_t)__ballot(p2),
+                     m3 = (uint64_t)__ballot(p3);
+      if (m0) return b + __builtin_ctzll(m0);
+      if (m1) return b + 64 + __builtin_ctzll(m1);
+      if (m2) return b + 128 + __builtin_ctzll(m2);
+      if (m3) return b + 192 + __builtin_ctzll(m3);
+    }
+    return -1;
+  }
   template <class F>
   static __device__ __forceinline__ uint32_t sum(int n, F&& f) {
     uint32_t s = 0;

@@ -41,17 +41,51 @@ SIM_HDI uint64_t pack_bits(uint64_t mask, uint64_t val, int high, int low) {
 
 SIM_HDI int ilog2u(uint64_t x) { return x ? 63 - __builtin_clzll(x) : 0; }
 
+// runs of a gather mask restricted to bit positions [low, high) (host side,
+// once per configuration): the decoder then costs a few shifts per run
+// instead of a loop over every mask bit
+SIM_HDI BitRuns make_runs(uint64_t mask, int high, int low) {
+  BitRuns r{};
+  if (high < 64) mask &= (1ull << high) - 1;
+  if (low > 0) mask &= ~((1ull << low) - 1);
+  int pos = 0;
+  while (mask) {
+    const int sh = __builtin_ctzll(mask);
+    const uint64_t m = mask >> sh;
+    const int w = (~m == 0) ? 64 - sh : __builtin_ctzll(~m);
+    if (r.n == 8) { r.n = 0xff; return r; }
+    r.sh[r.n] = (uint8_t)sh;
+    r.w[r.n] = (uint8_t)w;
+    r.out[r.n] = (uint8_t)pos;
+    ++r.n;
+    pos += w;
+    mask = (w + sh >= 64) ? 0 : (mask & ~(((w >= 64) ? ~0ull : ((1ull << w) - 1)) << sh));
+  }
+  return r;
+}
+SIM_HDI uint64_t run_gather(const BitRuns& r, uint64_t v) {
+  uint64_t o = 0;
+  for (int i = 0; i < (int)r.n && i < 8; ++i) {
+    const uint64_t m = r.w[i] >= 64 ? ~0ull : ((1ull << r.w[i]) - 1);
+    o |= ((v >> r.sh[i]) & m) << r.out[i];
+  }
+  return o;
+}
+
 // GF(2): (h * x^n) mod P, P given with its x^n term (bit n set).
 SIM_HDI uint32_t gf2_mulxn_mod(uint64_t h, int n, uint32_t poly) {
-  // process bits of h from the top: r = r*x + bit, reduced, then * x^n
-  uint32_t r = 0;
-  for (int i = 63; i >= 0; --i) {
-    r = (r << 1) | (uint32_t)((h >> i) & 1ull);
-    if (r >> n & 1u) r ^= poly;
-  }
+  // linear in h: XOR over the set bits i of h of x^(i+n) mod P, walking the
+  // powers of x only as far as h's highest set bit
+  uint32_t xp = 1;
   for (int i = 0; i < n; ++i) {
-    r <<= 1;
-    if (r >> n & 1u) r ^= poly;
+    xp <<= 1;
+    if (xp >> n & 1u) xp ^= poly;
+  }
+  uint32_t r = 0;
+  for (; h; h >>= 1) {
+    if (h & 1ull) r ^= xp;
+    xp <<= 1;
+    if (xp >> n & 1u) xp ^= poly;
   }
   return r;
 }
@@ -102,22 +136,26 @@ SIM_HDI AddrTlx addr_decode(const SimCfg& c, uint64_t addr) {
   AddrTlx t;
   uint64_t rest_high;
   const uint32_t nsub = c.n_sub_per_mem;
+  auto field = [&](int f, uint64_t v) -> uint32_t {
+    return c.addr_runs[f].n != 0xff ? (uint32_t)run_gather(c.addr_runs[f], v)
+                                    : (uint32_t)pack_bits(c.addr_mask[f], v, c.mk_hi[f], c.mk_lo[f]);
+  };
   if (!c.gap) {
-    t.chip = (uint32_t)pack_bits(c.addr_mask[AF_CHIP], addr, c.mk_hi[AF_CHIP], c.mk_lo[AF_CHIP]);
-    t.bk = (uint32_t)pack_bits(c.addr_mask[AF_BK], addr, c.mk_hi[AF_BK], c.mk_lo[AF_BK]);
-    t.row = (uint32_t)pack_bits(c.addr_mask[AF_ROW], addr, c.mk_hi[AF_ROW], c.mk_lo[AF_ROW]);
-    t.col = (uint32_t)pack_bits(c.addr_mask[AF_COL], addr, c.mk_hi[AF_COL], c.mk_lo[AF_COL]);
-    t.burst = (uint32_t)pack_bits(c.addr_mask[AF_BURST], addr, c.mk_hi[AF_BURST], c.mk_lo[AF_BURST]);
+    t.chip = field(AF_CHIP, addr);
+    t.bk = field(AF_BK, addr);
+    t.row = field(AF_ROW, addr);
+    t.col = field(AF_COL, addr);
+    t.burst = field(AF_BURST, addr);
     rest_high = addr >> (c.addr_chip_s + c.log2ch + c.log2sub);
   } else {
     uint64_t hi = addr >> c.addr_chip_s;
     uint64_t rest = ((hi / c.n_mem) << c.addr_chip_s) | (addr & ((1ull << c.addr_chip_s) - 1));
     rest_high = hi / c.n_mem;
     t.chip = (uint32_t)(hi % c.n_mem);
-    t.bk = (uint32_t)pack_bits(c.addr_mask[AF_BK], rest, c.mk_hi[AF_BK], c.mk_lo[AF_BK]);
-    t.row = (uint32_t)pack_bits(c.addr_mask[AF_ROW], rest, c.mk_hi[AF_ROW], c.mk_lo[AF_ROW]);
-    t.col = (uint32_t)pack_bits(c.addr_mask[AF_COL], rest, c.mk_hi[AF_COL], c.mk_lo[AF_COL]);
-    t.burst = (uint32_t)pack_bits(c.addr_mask[AF_BURST], rest, c.mk_hi[AF_BURST], c.mk_lo[AF_BURST]);
+    t.bk = field(AF_BK, rest);
+    t.row = field(AF_ROW, rest);
+    t.col = field(AF_COL, rest);
+    t.burst = field(AF_BURST, rest);
   }
   switch (c.part_index) {
     case PIDX_BITWISE:
@@ -125,17 +163,17 @@ SIM_HDI AddrTlx addr_decode(const SimCfg& c, uint64_t addr) {
       break;
     case PIDX_IPOLY:
     case PIDX_PAE: {  // PAE has no decoder case in the reference (defect D11): use IPOLY
-      uint32_t sp = t.chip * nsub + (t.bk & (nsub - 1));
+      uint32_t sp = (t.chip << c.log2sub) + (t.bk & (nsub - 1));
       sp = ipoly_hash(rest_high, sp, c.n_ch_pow2 * nsub);
       if (c.gap) sp = sp % (c.n_mem * nsub);
-      t.chip = sp / nsub;
+      t.chip = sp >> c.log2sub;  // sub-partitions per channel: a power of two
       t.sub = sp;
       return t;
     }
     case PIDX_RANDOM: {
       uint64_t ca = addr >> (c.addr_chip_s - c.log2sub);
       uint32_t id = (uint32_t)(splitmix64(ca) % (c.n_mem * nsub));
-      t.chip = id / nsub;
+      t.chip = id >> c.log2sub;
       t.sub = id;
       return t;
     }
@@ -143,17 +181,19 @@ SIM_HDI AddrTlx addr_decode(const SimCfg& c, uint64_t addr) {
       break;
   }
   if (t.chip >= c.n_mem) t.chip %= c.n_mem;
-  t.sub = t.chip * nsub + (t.bk & (nsub - 1));
+  t.sub = (t.chip << c.log2sub) + (t.bk & (nsub - 1));
   return t;
 }
 
 // address with the channel / sub-partition selection bits squeezed out
 // (used for L2 set indexing, reference partition_address addrdec.cc:78-93)
 SIM_HDI uint64_t partition_address(const SimCfg& c, uint64_t addr) {
-  if (!c.gap) return pack_bits(~(c.addr_mask[AF_CHIP] | c.sub_id_mask), addr, 64, 0);
+  if (!c.gap)
+    return c.part_runs.n != 0xff ? run_gather(c.part_runs, addr)
+                                 : pack_bits(~(c.addr_mask[AF_CHIP] | c.sub_id_mask), addr, 64, 0);
   uint64_t pa = ((addr >> c.addr_chip_s) / c.n_mem) << c.addr_chip_s;
   pa |= addr & ((1ull << c.addr_chip_s) - 1);
-  return pack_bits(~c.sub_id_mask, pa, 64, 0);
+  return c.part_runs.n != 0xff ? run_gather(c.part_runs, pa) : pack_bits(~c.sub_id_mask, pa, 64, 0);
 }
 
 SIM_HDI uint32_t cache_set_index(const CacheGeom& g, uint64_t addr) {

@@ -54,6 +54,16 @@ enum SetIndexFn : uint8_t { SIDX_LINEAR = 0, SIDX_FERMI, SIDX_HASH_IPOLY, SIDX_B
 enum PartIndex : uint8_t { PIDX_CONSECUTIVE = 0, PIDX_BITWISE = 1, PIDX_IPOLY = 2, PIDX_PAE = 3, PIDX_RANDOM = 4, PIDX_CUSTOM = 5 };
 enum AddrField : uint8_t { AF_CHIP = 0, AF_BK, AF_ROW, AF_COL, AF_BURST, AF_COUNT };
 
+// a bit-gather mask as contiguous runs: field = OR_i ((v >> sh[i]) & (2^w[i]-1)) << out[i]
+// (n = 0xff: more than 8 runs, gather bit by bit)
+struct BitRuns {
+  uint8_t n;
+  uint8_t sh[8];
+  uint8_t w[8];
+  uint8_t out[8];
+  uint8_t pad[7];
+};
+
 struct CacheGeom {
   uint32_t nsets;
   uint32_t assoc;
@@ -191,6 +201,8 @@ struct SimCfg {
   int32_t addr_chip_s;
   uint32_t log2ch, log2sub, n_ch_pow2;
   uint64_t sub_id_mask;
+  BitRuns addr_runs[AF_COUNT];  // addr_mask[f] restricted to [mk_lo, mk_hi), as runs
+  BitRuns part_runs;            // partition_address gather mask as runs
   // ---- clocks (femtoseconds per cycle) ----
   uint64_t per_core, per_icnt, per_l2, per_dram;
   // ---- kernel scheduling ----
@@ -204,6 +216,7 @@ struct SimCfg {
   uint32_t perfect_mem;     // every global/local access hits with L1 latency, no traffic
   uint32_t simple_dram;     // DRAM = latency pipe + one column per DRAM cycle, no bank timing
   uint32_t event_skip;      // fast-forward provably quiet SM cycles inside an epoch (exact)
+  uint32_t cpu_threads;     // CPU engine only: OpenMP threads per epoch (host option)
   // ---- debug trace streams (pointers are set by the engine that owns the buffers) ----
   uint32_t trace_mask;      // TraceStream bits
   int32_t trace_sm;         // -trace_sampling_core (-1: all)

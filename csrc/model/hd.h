@@ -87,6 +87,14 @@ struct SeqPar {
     }
     return bi;
   }
+  // smallest i < n with pred(i), -1 if none (the argmin of "key = i if
+  // candidate" searches: MSHR / free-slot lookups)
+  template <class F>
+  static SIM_HDI int find_first(int n, F&& pred) {
+    for (int i = 0; i < n; ++i)
+      if (pred(i)) return i;
+    return -1;
+  }
   template <class F>
   static SIM_HDI uint32_t sum(int n, F&& f) {
     uint32_t s = 0;
@@ -101,6 +109,20 @@ struct SeqPar {
       s = v > s ? v : s;
     }
     return s;
+  }
+  // per-lane values: lanes<T>(n, f) evaluates f(i) for the lanes i < n; the
+  // result gives a lane's own value back (self(i) inside lane-parallel code)
+  // and any one lane's value to wave-uniform code (at(i)).  On the CPU it is a
+  // lazy re-evaluation; on the GPU a register per lane read by v_readlane.
+  template <class T, class F>
+  struct Lanes {
+    F f;
+    SIM_HDI T self(int i) const { return f(i); }
+    SIM_HDI T at(int i) const { return f(i); }
+  };
+  template <class T, class F>
+  static SIM_HDI Lanes<T, F> lanes(int, F f) {
+    return Lanes<T, F>{f};
   }
   // exclusive prefix sum: out(i, sum_{j<i} val(j)); returns the total
   template <class F, class G>
@@ -118,6 +140,25 @@ struct SeqPar {
     uint64_t s = 0;
     for (int i = 0; i < n; ++i) s |= f(i);
     return s;
+  }
+  // the members of `mask` (indices < n <= 16) sorted by key ascending (ties
+  // to the lower index), packed 4 bits per entry: entry r = (ord >> 4r) & 15.
+  // Replaces repeated "oldest remaining" argmin scans with one ranking.
+  template <class F>
+  static SIM_HDI uint64_t order16(int n, uint32_t mask, F&& key) {
+    uint64_t ord = 0;
+    for (int i = 0; i < n; ++i) {
+      if (!(mask >> i & 1u)) continue;
+      const uint32_t ki = key(i);
+      uint32_t r = 0;
+      for (int j = 0; j < n; ++j)
+        if ((mask >> j & 1u) && j != i) {
+          const uint32_t kj = key(j);
+          r += (kj < ki || (kj == ki && j < i)) ? 1u : 0u;
+        }
+      ord |= (uint64_t)i << (4 * r);
+    }
+    return ord;
   }
 };
 

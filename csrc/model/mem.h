@@ -306,9 +306,7 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
   }
   if (sp.n_wait >= (uint32_t)kMaxL2Wait) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
   const int nm = (int)amin<uint32_t>(g.mshr_entries, kMaxL2Mshr);
-  int mi = P::argmin(nm, [&](int i) -> uint64_t {
-    return (sp.mshr[i].valid && sp.mshr[i].line == p.addr) ? (uint64_t)i : ~0ull;
-  });
+  int mi = P::find_first(nm, [&](int i) -> bool { return sp.mshr[i].valid && sp.mshr[i].line == p.addr; });
   uint8_t need_req = mi >= 0 ? (uint8_t)(miss & ~sp.mshr[mi].requested) : miss;
   if (need_req == 0) {
     if (sp.mshr[mi].merges >= g.mshr_merge) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
@@ -319,7 +317,7 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
     uint32_t nreq = (uint32_t)popc64(need_req);
     if (!l2dram_can(ch, sp, c, nreq)) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
     if (mi < 0) {
-      mi = P::argmin(nm, [&](int i) -> uint64_t { return sp.mshr[i].valid ? ~0ull : (uint64_t)i; });
+      mi = P::find_first(nm, [&](int i) -> bool { return !sp.mshr[i].valid; });
       if (mi < 0) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
       sp.mshr[mi].valid = 1;
       sp.mshr[mi].line = p.addr;
@@ -380,9 +378,7 @@ SIM_HDI bool l2_fill(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, 
     if (g.repl == REPL_LRU) L.lru = ++sp.l2_stamp;
   }
   const int nm = (int)amin<uint32_t>(g.mshr_entries, kMaxL2Mshr);
-  int mi = P::argmin(nm, [&](int i) -> uint64_t {
-    return (sp.mshr[i].valid && sp.mshr[i].line == r.line) ? (uint64_t)i : ~0ull;
-  });
+  int mi = P::find_first(nm, [&](int i) -> bool { return sp.mshr[i].valid && sp.mshr[i].line == r.line; });
   if (mi >= 0) {
     sp.mshr[mi].requested &= (uint8_t)~sbit;
     if (!sp.mshr[mi].requested) sp.mshr[mi].valid = 0;
@@ -516,7 +512,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
     // (reference dram_t::full, dram.cc:160-175)
     if (c.wq_enable ? (h.write ? ch.qw_n >= c.wq_size : ch.q_n - ch.qw_n >= qcap) : ch.q_n >= qcap) break;
     ch.qw_n += h.write ? 1 : 0;
-    int f = P::argmin(kDramQ, [&](int i) -> uint64_t { return ch.q_valid[i] ? ~0ull : (uint64_t)i; });
+    int f = P::find_first(kDramQ, [&](int i) -> bool { return !ch.q_valid[i]; });
     ch.q[f] = h;
     ch.q_valid[f] = 1;
     ch.q_age[f] = ch.q_seq++;

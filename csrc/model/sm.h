@@ -11,6 +11,8 @@
 // MSHR waiters live in a flat associative table instead of linked lists
 // (mshr_table, gpu-cache.h:1019).
 #pragma once
+#include <stddef.h>
+
 #include "addrdec.h"
 
 namespace asim {
@@ -55,25 +57,19 @@ struct WbEnt {
   uint8_t pad;
 };
 
-struct IdOc {  // ID_OC pipeline register (one per scheduler per unit type)
-  TInst inst;
-  uint8_t valid;
-  uint8_t warp;
-  uint8_t pad[2];
-  uint32_t widx;  // warp-local instruction sequence (for age)
-};
-
-struct OCUnit {
-  TInst inst;
-  uint8_t valid;
-  uint8_t warp;
-  uint8_t sched;
-  uint8_t unit;
-  uint8_t nread;      // remaining operand reads
-  uint8_t banks[5];   // bank of each pending read (0xff = done)
-  uint8_t pad[2];
-  uint32_t age;
-};
+// ID_OC pipeline registers (one per scheduler per unit type, index
+// sched * U_COUNT + unit == its idoc_mask bit) and operand collector units
+// are kept as SoA columns: the instruction copies stay in memory, the small
+// per-entry fields are single words that the GPU engine's register view holds
+// one entry per lane (csrc/engine/sm_view.h).
+//   idoc_meta: warp | load slot << 8 | age << 32
+//   oc_info:   warp | sched << 8 | unit << 16 | load slot << 24 | lat << 32 | ii << 48
+//   oc_banks:  bytes 0-4 bank of each pending operand read (0xff = none),
+//              byte 5 reads left, byte 6 dst0, byte 7 dst1
+constexpr int kIdOc = kMaxSched * U_COUNT;
+SIM_HDI uint64_t idoc_pack(uint32_t warp, uint32_t slot, uint32_t age) {
+  return (uint64_t)warp | (uint64_t)slot << 8 | (uint64_t)age << 32;
+}
 
 struct L1Line {
   uint64_t tag;      // line address
@@ -194,9 +190,13 @@ struct alignas(16) SMState {
   uint32_t fetch_rr;
   uint32_t sched_last[kMaxSched];
   // ---- pipeline registers / operand collectors / FUs ----
-  IdOc idoc[kMaxSched][U_COUNT];
-  OCUnit oc[kMaxOC];
-  uint32_t fu_next[U_COUNT][kMaxSched];  // cycle (low 32) a unit can accept again
+  TInst idoc_inst[kIdOc];
+  uint64_t idoc_meta[kIdOc];
+  TInst oc_inst[kMaxOC];
+  uint64_t oc_info[kMaxOC];
+  uint64_t oc_banks[kMaxOC];
+  uint32_t oc_age[kMaxOC];
+  uint32_t fu_next[U_COUNT * kMaxSched];  // [unit * kMaxSched + phys]: cycle (low 32) the unit can accept again
   uint8_t wb_cnt[kWbRing];
   WbEnt wb[kWbRing][kWbSlot];
   // ---- LD/ST + L1 ----
@@ -233,7 +233,15 @@ struct alignas(16) SMState {
   uint32_t srank[kInQ > kMaxSubTot ? kInQ : kMaxSubTot];
   SmKernel ks;               // replicated kernel dispatch state
   SMStats st;
+  // statistics by word index (SK below); the GPU engine's register view keeps
+  // the counters in lanes during the cycle loop (csrc/engine/sm_view.h)
+  SIM_HDI void sadd(uint32_t k, uint64_t d) { reinterpret_cast<uint64_t*>(&st)[k] += d; }
+  SIM_HDI uint64_t sget(uint32_t k) const { return reinterpret_cast<const uint64_t*>(&st)[k]; }
+  SIM_HDI void sset(uint32_t k, uint64_t v) { reinterpret_cast<uint64_t*>(&st)[k] = v; }
 };
+#define SK(f) ((uint32_t)(offsetof(::asim::SMStats, f) / 8))
+constexpr int kStatWords = (int)(sizeof(SMStats) / 8);
+static_assert(kStatWords <= 128, "SM statistics must fit two register words per lane");
 SIM_HDI uint64_t* s_scratch_key(SMState& s) { return s.skey; }
 SIM_HDI uint32_t* s_scratch_ref(SMState& s) { return s.sref; }
 SIM_HDI uint32_t* s_scratch_rank(SMState& s) { return s.srank; }
@@ -259,6 +267,16 @@ SIM_HDI void sb_set(uint64_t* sb, uint8_t r) {
 SIM_HDI void sb_clr(uint64_t* sb, uint8_t r) {
   if (r) sb[r >> 6] &= ~(1ull << (r & 63));
 }
+// scoreboard by (warp, register): the GPU engine's register view overloads
+// these for its per-lane scoreboard words (csrc/engine/sm_view.h)
+template <size_t N>
+SIM_HDI bool sbt(const uint64_t (&sb)[N][4], uint32_t w, uint8_t r) { return sb_test(sb[w], r); }
+template <size_t N>
+SIM_HDI void sbs(uint64_t (&sb)[N][4], uint32_t w, uint8_t r) { sb_set(sb[w], r); }
+template <size_t N>
+SIM_HDI void sbc(uint64_t (&sb)[N][4], uint32_t w, uint8_t r) { sb_clr(sb[w], r); }
+template <size_t N>
+SIM_HDI void sbz(uint64_t (&sb)[N][4], uint32_t w) { sb[w][0] = sb[w][1] = sb[w][2] = sb[w][3] = 0; }
 
 // ---------------------------------------------------------------------------
 // reset an SM for a new kernel (state persists across kernels otherwise:
@@ -326,8 +344,8 @@ SIM_HDI void sm_inject(S& s, const SmCtx& x, uint64_t now) {
   s.outq_n--;
   s.out_port_free = now + nflits;
   s.outstanding++;
-  s.st.pkts_out++;
-  s.st.bytes_out += p.size;
+  s.sadd(SK(pkts_out), 1);
+  s.sadd(SK(bytes_out), p.size);
 }
 
 // ---------------------------------------------------------------------------
@@ -343,10 +361,10 @@ SIM_HDI void sm_writeback(S& s, const SimCfg& c, uint64_t now) {
         if (e.dst0) trace_put(c, s.id, now, EV_SB_RELEASE, e.warp, e.dst0 - 1u);
         if (e.dst1) trace_put(c, s.id, now, EV_SB_RELEASE, e.warp, e.dst1 - 1u);
       });
-    sb_clr(s.w_sb[e.warp], e.dst0);
-    sb_clr(s.w_sb[e.warp], e.dst1);
+    sbc(s.w_sb, e.warp, e.dst0);
+    sbc(s.w_sb, e.warp, e.dst1);
     s.w_inflight[e.warp]--;
-    s.st.rf_writes += (e.dst0 != 0) + (e.dst1 != 0);
+    s.sadd(SK(rf_writes), (e.dst0 != 0) + (e.dst1 != 0));
   }
   if (n) s.last_progress = now;
   s.wb_cnt[slot] = 0;
@@ -355,9 +373,9 @@ SIM_HDI void sm_writeback(S& s, const SimCfg& c, uint64_t now) {
 
 template <class S>
 SIM_HDI void sm_load_slot_done(S& s, uint32_t w, uint32_t slot, uint64_t now) {
-  sb_clr(s.w_sb[w], s.w_slot_dst[w][slot][0]);
-  sb_clr(s.w_sb[w], s.w_slot_dst[w][slot][1]);
-  s.st.rf_writes += (s.w_slot_dst[w][slot][0] != 0) + (s.w_slot_dst[w][slot][1] != 0);
+  sbc(s.w_sb, w, s.w_slot_dst[w][slot][0]);
+  sbc(s.w_sb, w, s.w_slot_dst[w][slot][1]);
+  s.sadd(SK(rf_writes), (s.w_slot_dst[w][slot][0] != 0) + (s.w_slot_dst[w][slot][1] != 0));
   s.w_slot_used[w] &= (uint8_t)~(1u << slot);
   s.w_loads[w]--;
   s.w_inflight[w]--;
@@ -443,18 +461,16 @@ SIM_HDI void l1_fill(S& s, const SmCtx& x, uint64_t line, uint8_t sectors, uint6
     if (g.repl == REPL_LRU) L.lru = ++s.l1_stamp;
   }
   // mshr bookkeeping
-  int mi = P::argmin((int)c.l1.mshr_entries, [&](int i) -> uint64_t {
-    return (s.mshr[i].valid && s.mshr[i].line == line) ? (uint64_t)i : ~0ull;
-  });
+  int mi = P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return s.mshr[i].valid && s.mshr[i].line == line; });
   if (mi >= 0) {
     s.mshr[mi].requested &= (uint8_t)~sectors;
     if (s.mshr[mi].requested == 0) {
       s.mshr[mi].valid = 0;
       const uint32_t lat = (uint32_t)now - s.mshr[mi].t_issue;
-      s.st.mf_lat_sum += lat;
-      s.st.mf_lat_n++;
-      if (lat > s.st.mf_lat_max) s.st.mf_lat_max = lat;
-      s.st.mf_lat_hist[lat ? amin<int>(15, 31 - __builtin_clz(lat)) : 0]++;
+      s.sadd(SK(mf_lat_sum), lat);
+      s.sadd(SK(mf_lat_n), 1);
+      if (lat > s.sget(SK(mf_lat_max))) s.sset(SK(mf_lat_max), lat);
+      s.sadd(SK(mf_lat_hist) + (lat ? amin<int>(15, 31 - __builtin_clz(lat)) : 0), 1);
     }
   }
   // wake waiters whose sectors are now all present (lane-parallel scan)
@@ -503,9 +519,7 @@ SIM_HDI void il1_fill(S& s, const SimCfg& c, uint64_t line) {
     base[v].valid = 0xf;
     base[v].lru = ++s.l1_stamp;
   }
-  const int mi = P::argmin((int)g.mshr_entries, [&](int i) -> uint64_t {
-    return (s.imshr[i].valid && s.imshr[i].line == line) ? (uint64_t)i : ~0ull;
-  });
+  const int mi = P::find_first((int)g.mshr_entries, [&](int i) -> bool { return s.imshr[i].valid && s.imshr[i].line == line; });
   if (mi >= 0) s.imshr[mi].valid = 0;
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   P::each(nw, [&](int w) {
@@ -525,25 +539,23 @@ SIM_HDI bool il1_fetch(S& s, const SimCfg& c, uint32_t w) {
   const int way = il1_find<P>(s, g, set, line);
   if (way >= 0) {
     if (g.repl == REPL_LRU) s.il1[set * g.assoc + way].lru = ++s.l1_stamp;
-    s.st.il1[IL1_HIT]++;
+    s.sadd(SK(il1) + (IL1_HIT), 1);
     return true;
   }
-  int mi = P::argmin((int)g.mshr_entries, [&](int i) -> uint64_t {
-    return (s.imshr[i].valid && s.imshr[i].line == line) ? (uint64_t)i : ~0ull;
-  });
+  int mi = P::find_first((int)g.mshr_entries, [&](int i) -> bool { return s.imshr[i].valid && s.imshr[i].line == line; });
   if (mi >= 0) {
-    if (s.imshr[mi].merges >= g.mshr_merge) { s.st.il1[IL1_RES_FAIL]++; return false; }
+    if (s.imshr[mi].merges >= g.mshr_merge) { s.sadd(SK(il1) + (IL1_RES_FAIL), 1); return false; }
     s.imshr[mi].merges++;
-    s.st.il1[IL1_MSHR_HIT]++;
+    s.sadd(SK(il1) + (IL1_MSHR_HIT), 1);
   } else {
-    mi = P::argmin((int)g.mshr_entries, [&](int i) -> uint64_t { return s.imshr[i].valid ? ~0ull : (uint64_t)i; });
-    if (mi < 0 || !sm_can_send(s, c)) { s.st.il1[IL1_RES_FAIL]++; return false; }
+    mi = P::find_first((int)g.mshr_entries, [&](int i) -> bool { return !s.imshr[i].valid; });
+    if (mi < 0 || !sm_can_send(s, c)) { s.sadd(SK(il1) + (IL1_RES_FAIL), 1); return false; }
     s.imshr[mi].valid = 1;
     s.imshr[mi].line = line;
     s.imshr[mi].merges = 0;
     s.imshr[mi].t_issue = 0;
     sm_send(s, c, P_RD, line, 0xf, 128, 0x40000000u | (uint32_t)mi);
-    s.st.il1[IL1_MISS]++;
+    s.sadd(SK(il1) + (IL1_MISS), 1);
   }
   s.w_flags[w] |= WF_IMISS;
   s.w_iline[w] = line;
@@ -561,8 +573,8 @@ SIM_HDI void sm_receive(S& s, const SmCtx& x, uint64_t now) {
   s.inq_head = (s.inq_head + 1) % kInQ;
   s.inq_n--;
   s.outstanding--;
-  s.st.pkts_in++;
-  s.st.bytes_in += q.size;
+  s.sadd(SK(pkts_in), 1);
+  s.sadd(SK(bytes_in), q.size);
   if (q.type == P_WR_ACK) {
     uint32_t w = q.tag & 0xff;
     s.w_stores[w]--;
@@ -598,8 +610,8 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
     if ((uint32_t)(now - P::uni(u.start)) + 1 < deg) return;
     uint8_t kind = (in.cls == OC_STORE) ? 1 : 0;
     if (!hit_push(s, now + c.smem_latency, (uint8_t)w, P::uni(u.slot), kind)) return;
-    s.st.shmem_acc++;
-    s.st.shmem_conflict_cycles += deg - 1;
+    s.sadd(SK(shmem_acc), 1);
+    s.sadd(SK(shmem_conflict_cycles), deg - 1);
     u.busy = 0;
     return;
   }
@@ -620,11 +632,11 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
     if (c.perfect_mem) {
       // ideal memory: loads/atomics return after the L1 latency, stores retire at once
       if (!is_store) {
-        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, uslot, 0)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, uslot, 0)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
       }
-      s.st.l1[stype][L1O_HIT]++;
+      s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_HIT), 1);
     } else if (is_store) {
-      if (!sm_can_send(s, c)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+      if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
       sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
       s.w_stores[w]++;
       if (!bypass && g.wpolicy == WP_WRITE_EVICT) {
@@ -632,40 +644,36 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
         int way = l1_find<P>(s, g, set, a.line);
         if (way >= 0) s.l1[set * g.assoc + way].valid &= (uint8_t)~a.sectors;
       }
-      s.st.l1[stype][bypass ? L1O_BYPASS : L1O_MISS]++;
+      s.sadd(SK(l1) + (stype) * L1O_COUNT + (bypass ? L1O_BYPASS : L1O_MISS), 1);
     } else if (bypass) {
-      if (!sm_can_send(s, c)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+      if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
       uint32_t tag = 0x80000000u | ((uint32_t)uslot << 8) | w;
       sm_send(s, c, atomic ? P_ATOM : P_RD, a.line, a.sectors, a.bytes, tag);
-      s.st.l1[stype][L1O_BYPASS]++;
+      s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_BYPASS), 1);
     } else {
       uint32_t set = cache_set_index(g, a.line);
       int way = l1_find<P>(s, g, set, a.line);
       uint8_t have = way >= 0 ? s.l1[set * g.assoc + way].valid : 0;
       uint8_t miss = a.sectors & (uint8_t)~have;
       if (miss == 0) {
-        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, uslot, 0)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, uslot, 0)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
         if (g.repl == REPL_LRU) s.l1[set * g.assoc + way].lru = ++s.l1_stamp;
-        s.st.l1[stype][L1O_HIT]++;
+        s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_HIT), 1);
       } else {
-        if (s.n_pend >= (uint32_t)kMaxPend) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
-        int mi = P::argmin((int)c.l1.mshr_entries, [&](int i) -> uint64_t {
-          return (s.mshr[i].valid && s.mshr[i].line == a.line) ? (uint64_t)i : ~0ull;
-        });
+        if (s.n_pend >= (uint32_t)kMaxPend) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+        int mi = P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return s.mshr[i].valid && s.mshr[i].line == a.line; });
         uint8_t need_req = miss;
         if (mi >= 0) need_req = miss & (uint8_t)~s.mshr[mi].requested;
         bool merged = (mi >= 0 && need_req == 0);
         if (merged) {
-          if (s.mshr[mi].merges >= c.l1.mshr_merge) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+          if (s.mshr[mi].merges >= c.l1.mshr_merge) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
           s.mshr[mi].merges++;
-          s.st.l1[stype][L1O_MSHR_HIT]++;
+          s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_MSHR_HIT), 1);
         } else {
-          if (!sm_can_send(s, c)) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+          if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
           if (mi < 0) {
-            mi = P::argmin((int)c.l1.mshr_entries, [&](int i) -> uint64_t {
-              return s.mshr[i].valid ? ~0ull : (uint64_t)i;
-            });
-            if (mi < 0) { s.st.l1[stype][L1O_RES_FAIL]++; break; }
+            mi = P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return !s.mshr[i].valid; });
+            if (mi < 0) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
             s.mshr[mi].valid = 1;
             s.mshr[mi].line = a.line;
             s.mshr[mi].requested = 0;
@@ -674,7 +682,7 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
           }
           s.mshr[mi].requested |= need_req;
           sm_send(s, c, P_RD, a.line, need_req, a.bytes, (uint32_t)mi);
-          s.st.l1[stype][L1O_MISS]++;
+          s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_MISS), 1);
         }
         // register the waiter (first free entry)
         uint32_t pi = s.n_pend;
@@ -712,103 +720,104 @@ SIM_HDI uint32_t reg_bank(const SimCfg& c, uint32_t sched, uint32_t warp, uint32
   uint32_t nb = c.reg_banks ? c.reg_banks : 1;
   uint32_t per = (c.sub_core && c.n_sched) ? (nb / c.n_sched ? nb / c.n_sched : 1) : nb;
   uint32_t base = (c.sub_core && c.n_sched) ? (sched * per) % nb : 0;
+  // power-of-two bank groups (every tested config) avoid integer division
+  if ((per & (per - 1)) == 0) return base + ((reg + warp) & (per - 1));
   return base + (reg + warp) % per;
 }
 
+// operand reads: each register bank serves one read per round, up to
+// reg_port_tp rounds per cycle, oldest collector first.  The reference's
+// arbiter (opndcoll_rfu_t::allocate_reads, shader.cc:3650-3733) is replaced by
+// the equivalent greedy pass: the oldest collector with a grantable operand
+// keeps winning until it has none left (banks only become busy within a
+// round), so the round visits collectors once in age order, each taking its
+// operands on free banks in operand order, at most `noc` grants per round.
 template <class P, class S>
 SIM_HDI void sm_read_operands(S& s, const SimCfg& c) {
-  // each register bank serves reg_port_tp reads per cycle, oldest collector first
   uint32_t rmask = P::uni(s.oc_read_mask);
   if (!rmask) return;
   const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
   for (uint32_t round = 0; round < c.reg_port_tp && rmask; ++round) {
-    uint32_t bank_busy = 0;
     const uint32_t want = rmask;
-    for (int k = 0; k < noc; ++k) {
-      // visit collectors oldest-first
-      int best = P::argmin(noc, [&](int i) -> uint64_t {
-        if (!(want >> i & 1u)) return ~0ull;
-        const OCUnit& o = s.oc[i];
-        bool ready = false;
-        for (int j = 0; j < 5; ++j)
-          if (o.banks[j] != 0xff && !(bank_busy >> o.banks[j] & 1u)) ready = true;
-        return ready ? (uint64_t)o.age : ~0ull;
-      });
-      if (best < 0) break;
-      OCUnit& o = s.oc[best];
-      for (int j = 0; j < 5; ++j) {
-        const uint32_t bj = P::uni(o.banks[j]);
-        if (bj != 0xff && !(bank_busy >> bj & 1u)) {
+    const int nwant = popc64(want);
+    const uint64_t ord = nwant == 1 ? (uint64_t)ffs64(want)
+                                    : P::order16(noc, want, [&](int i) -> uint32_t { return s.oc_age[i]; });
+    uint32_t bank_busy = 0, grants = 0;
+    for (int r = 0; r < nwant && grants < (uint32_t)noc; ++r) {
+      const int i = (int)((ord >> (4 * r)) & 15u);
+      uint64_t b = P::uni((uint64_t)s.oc_banks[i]);
+      uint32_t nr = (uint32_t)(b >> 40) & 0xffu;
+      uint32_t got = 0;
+      for (int j = 0; j < 5 && grants < (uint32_t)noc; ++j) {
+        const uint32_t bj = (uint32_t)(b >> (8 * j)) & 0xffu;
+        if (bj != 0xffu && !(bank_busy >> bj & 1u)) {
           bank_busy |= 1u << bj;
-          o.banks[j] = 0xff;
-          const uint8_t nr = (uint8_t)(P::uni(o.nread) - 1);
-          o.nread = nr;
-          if (nr == 0) {
-            rmask &= ~(1u << best);
-            s.oc_read_mask = rmask;
-          }
-          s.st.rf_reads++;
-          break;  // one operand per collector per round
+          b |= 0xffull << (8 * j);
+          ++got;
+          ++grants;
         }
       }
+      if (got) {
+        nr -= got;
+        b = (b & ~(0xffull << 40)) | ((uint64_t)nr << 40);
+        s.oc_banks[i] = b;
+        s.sadd(SK(rf_reads), got);
+        if (nr == 0) rmask &= ~(1u << i);
+      }
     }
+    s.oc_read_mask = rmask;
   }
 }
 
+// collectors whose operands are all read go to their unit, oldest first
 template <class P, class S>
 SIM_HDI void sm_dispatch(S& s, const SimCfg& c, uint64_t now) {
   const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
   const uint32_t wbw = wb_width(c);
-  // oldest-first over ready collectors (valid, all operands read)
   const uint32_t ready = P::uni(s.oc_mask & ~s.oc_read_mask);
   if (!ready) return;
-  uint32_t tried = 0;
-  for (int k = 0; k < noc; ++k) {
-    const uint32_t cand = ready & ~tried;
-    if (!cand) break;
-    int best = (cand & (cand - 1)) == 0 ? ffs64(cand) : P::argmin(noc, [&](int i) -> uint64_t {
-      if (!(cand >> i & 1u)) return ~0ull;
-      return (uint64_t)s.oc[i].age;
-    });
-    if (best < 0) break;
-    tried |= 1u << best;
-    OCUnit& o = s.oc[best];
-    const uint32_t u = P::uni(o.unit);
+  const int n = popc64(ready);
+  const uint64_t ord =
+      n == 1 ? (uint64_t)ffs64(ready) : P::order16(noc, ready, [&](int i) -> uint32_t { return s.oc_age[i]; });
+  for (int r = 0; r < n; ++r) {
+    const int best = (int)((ord >> (4 * r)) & 15u);
+    const uint64_t info = P::uni((uint64_t)s.oc_info[best]);
+    const uint32_t u = (uint32_t)(info >> 16) & 0xffu;
     if (u == U_MEM) {
       if (P::uni(s.ldst.busy)) continue;
-      const TInst in = P::uni(o.inst);
-      // loads need a slot: allocated at issue (slot id carried in pad of OC)
-      s.ldst.inst = in;
+      s.ldst.inst = P::uni(s.oc_inst[best]);
       s.ldst.busy = 1;
-      s.ldst.warp = o.warp;
-      s.ldst.slot = o.pad[0];
+      s.ldst.warp = (uint8_t)(info & 0xffu);
+      s.ldst.slot = (uint8_t)((info >> 24) & 0xffu);  // load slot allocated at issue
       s.ldst.next = 0;
       s.ldst.start = (uint32_t)now;
-      s.st.mem_insn++;
-      o.valid = 0;
+      s.sadd(SK(mem_insn), 1);
       s.oc_mask &= ~(1u << best);
       continue;
     }
-    uint32_t cnt = c.unit_count[u] ? c.unit_count[u] : 1;
-    uint32_t phys = P::uni(o.sched) % cnt;
+    const uint32_t sched = (uint32_t)(info >> 8) & 0xffu;
+    const uint32_t cnt = c.unit_count[u] ? c.unit_count[u] : 1;
+    uint32_t phys = sched < cnt ? sched : sched % cnt;
     if (phys >= (uint32_t)kMaxSched) phys %= kMaxSched;
-    uint32_t nf = P::uni(s.fu_next[u][phys]);
+    const uint32_t fi = u * (uint32_t)kMaxSched + phys;
+    const uint32_t nf = P::uni((uint32_t)s.fu_next[fi]);
     if ((int32_t)(nf - (uint32_t)now) > 0) continue;  // initiation interval
-    const TInst oi = P::uni(o.inst);
-    uint32_t lat = oi.lat ? oi.lat : 1;
+    uint32_t lat = (uint32_t)(info >> 32) & 0xffffu;
+    if (!lat) lat = 1;
     if (lat >= (uint32_t)kWbRing) lat = kWbRing - 1;
-    uint32_t slot = (uint32_t)((now + lat) % kWbRing);
+    const uint32_t slot = (uint32_t)((now + lat) % kWbRing);
     const uint32_t nwb = P::uni(s.wb_cnt[slot]);
-    if (nwb >= wbw) { s.st.pipe_stall++; continue; }  // result bus busy
+    if (nwb >= wbw) { s.sadd(SK(pipe_stall), 1); continue; }  // result bus busy
     s.wb_cnt[slot] = (uint8_t)(nwb + 1);
+    const uint64_t bk = P::uni((uint64_t)s.oc_banks[best]);
     WbEnt& e = s.wb[slot][nwb];
     s.wb_occ[slot >> 6] |= 1ull << (slot & 63);
-    e.warp = P::uni(o.warp);
-    e.dst0 = oi.dst[0];
-    e.dst1 = oi.dst[1];
+    e.warp = (uint8_t)(info & 0xffu);
+    e.dst0 = (uint8_t)(bk >> 48);
+    e.dst1 = (uint8_t)(bk >> 56);
     e.pad = 0;
-    s.fu_next[u][phys] = (uint32_t)now + (oi.ii ? oi.ii : 1);
-    o.valid = 0;
+    const uint32_t ii = (uint32_t)(info >> 48) & 0xffu;
+    s.fu_next[fi] = (uint32_t)now + (ii ? ii : 1);
     s.oc_mask &= ~(1u << best);
   }
 }
@@ -825,43 +834,35 @@ SIM_HDI void sm_alloc_collectors(S& s, const SimCfg& c) {
     const int bit = ffs64(pend);
     pend &= pend - 1;
     const uint32_t sc = (uint32_t)bit / U_COUNT, u = (uint32_t)bit % U_COUNT;
-    {
-      IdOc& r = s.idoc[sc][u];
-      // free collector in this scheduler's group
-      uint32_t lo = c.sub_core ? (sc * per) % noc : 0;
-      uint32_t hi = c.sub_core ? lo + per : (uint32_t)noc;
-      if (hi > (uint32_t)noc) hi = noc;
-      const uint32_t grp = ((hi >= 32 ? 0xffffffffu : ((1u << hi) - 1)) & ~((1u << lo) - 1));
-      const uint32_t freem = grp & ~ocm;
-      if (!freem) continue;
-      const int f = ffs64(freem);
-      OCUnit& o = s.oc[f];
-      ocm |= 1u << f;
-      s.oc_mask = ocm;
-      const TInst rin = P::uni(r.inst);
-      const uint32_t rw = P::uni(r.warp);
-      o.inst = rin;
-      o.valid = 1;
-      o.warp = (uint8_t)rw;
-      o.sched = (uint8_t)sc;
-      o.unit = (uint8_t)u;
-      o.pad[0] = r.pad[0];  // load slot
-      o.age = r.widx;
-      uint32_t nread = 0;
-      for (int j = 0; j < 5; ++j) {
-        uint8_t reg = rin.src[j];
-        if (reg) {
-          o.banks[j] = (uint8_t)reg_bank(c, sc, rw, reg - 1);
-          nread++;
-        } else {
-          o.banks[j] = 0xff;
-        }
-      }
-      o.nread = (uint8_t)nread;
-      if (nread) s.oc_read_mask |= 1u << f;
-      r.valid = 0;
-      s.idoc_mask &= ~(1ull << bit);
+    // free collector in this scheduler's group
+    uint32_t lo = c.sub_core ? (sc * per) % noc : 0;
+    uint32_t hi = c.sub_core ? lo + per : (uint32_t)noc;
+    if (hi > (uint32_t)noc) hi = noc;
+    const uint32_t grp = ((hi >= 32 ? 0xffffffffu : ((1u << hi) - 1)) & ~((1u << lo) - 1));
+    const uint32_t freem = grp & ~ocm;
+    if (!freem) continue;
+    const int f = ffs64(freem);
+    ocm |= 1u << f;
+    s.oc_mask = ocm;
+    const uint64_t meta = P::uni((uint64_t)s.idoc_meta[bit]);
+    const TInst rin = P::uni(s.idoc_inst[bit]);
+    const uint32_t rw = (uint32_t)(meta & 0xffu);
+    s.oc_inst[f] = rin;
+    uint64_t bk = 0;
+    uint32_t nread = 0;
+    for (int j = 0; j < 5; ++j) {
+      const uint8_t reg = rin.src[j];
+      const uint32_t bank = reg ? reg_bank(c, sc, rw, reg - 1u) : 0xffu;
+      bk |= (uint64_t)(bank & 0xffu) << (8 * j);
+      nread += reg ? 1u : 0u;
     }
+    bk |= (uint64_t)nread << 40 | (uint64_t)rin.dst[0] << 48 | (uint64_t)rin.dst[1] << 56;
+    s.oc_banks[f] = bk;
+    s.oc_info[f] = (uint64_t)rw | (uint64_t)sc << 8 | (uint64_t)u << 16 | ((meta >> 8) & 0xffull) << 24 |
+                   (uint64_t)rin.lat << 32 | (uint64_t)rin.ii << 48;
+    s.oc_age[f] = (uint32_t)(meta >> 32);
+    if (nread) s.oc_read_mask |= 1u << f;
+    s.idoc_mask &= ~(1ull << bit);
   }
 }
 
@@ -881,15 +882,14 @@ SIM_HDI void sm_barrier_check(S& s, uint32_t cta, const KernelDesc& k) {
 // can warp `w` issue its next instruction this cycle (scoreboard, flags,
 // pipeline register and load slot availability)
 template <class S>
-SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, int w, uint32_t nsched, uint64_t idoc_busy) {
+SIM_HDI bool warp_can_issue_i(const S& s, const SimCfg& c, int w, const TInst& in, uint32_t nsched,
+                              uint64_t idoc_busy) {
   uint8_t f = s.w_flags[w];
   if (!(f & WF_ACTIVE) || (f & (WF_EXITING | WF_BARRIER | WF_MEMBAR | WF_WAITCNT))) return false;
   if (s.w_ibuf[w] == 0) return false;
-  const TInst& in = s.w_win[w][s.w_head[w] % kWin];
-  const uint64_t* sb = s.w_sb[w];
   for (int j = 0; j < 5; ++j)
-    if (sb_test(sb, in.src[j])) return false;
-  if (sb_test(sb, in.dst[0]) || sb_test(sb, in.dst[1])) return false;
+    if (sbt(s.w_sb, w, in.src[j])) return false;
+  if (sbt(s.w_sb, w, in.dst[0]) || sbt(s.w_sb, w, in.dst[1])) return false;
   uint32_t u = unit_of(c, in.cls);
   uint32_t sc = (uint32_t)w % nsched;
   if (in.cls == OC_EXIT || in.cls == OC_BARRIER || in.cls == OC_MEMBAR || in.cls == OC_NOP || (in.flags & F_WAITCNT))
@@ -897,6 +897,12 @@ SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, int w, uint32_t nsched,
   if (idoc_busy >> (sc * U_COUNT + u) & 1ull) return false;
   if (u == U_MEM && in.cls == OC_LOAD && s.w_slot_used[w] == 0xff) return false;
   return true;
+}
+template <class S>
+SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, int w, uint32_t nsched, uint64_t idoc_busy) {
+  if (!(s.w_flags[w] & WF_ACTIVE) || s.w_ibuf[w] == 0) return false;
+  const TInst in = s.w_win[w][s.w_head[w] % kWin];
+  return warp_can_issue_i(s, c, w, in, nsched, idoc_busy);
 }
 
 template <class P, class S>
@@ -906,8 +912,10 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
   const uint64_t idoc_busy = P::uni(s.idoc_mask);
+  // every warp's next instruction, read once (a register per lane on the GPU)
+  const auto head = P::template lanes<TInst>(nw, [&](int w) -> TInst { return s.w_win[w][s.w_head[w] % kWin]; });
   // readiness of every warp (lane-parallel)
-  uint64_t ready = P::ballot(nw, [&](int w) -> bool { return warp_can_issue(s, c, w, nsched, idoc_busy); });
+  uint64_t ready = P::ballot(nw, [&](int w) -> bool { return warp_can_issue_i(s, c, w, head.self(w), nsched, idoc_busy); });
   uint64_t live = P::ballot(nw, [&](int w) { return (s.w_flags[w] & WF_ACTIVE) != 0; });
   P::prof(29);
   bool issued_any = false;
@@ -916,11 +924,11 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
     const uint64_t mine = c.sched_mask[sc];
     uint64_t cand = ready & mine;
     if (!cand) {
-      if (live & mine) s.st.issue_stall_idle++;
+      if (live & mine) s.sadd(SK(issue_stall_idle), 1);
       continue;
     }
     int pick = -1;
-    uint32_t last = P::uni(s.sched_last[sc]);
+    uint32_t last = P::uni((uint32_t)s.sched_last[sc]);
     switch (c.sched_policy) {
       case SCHED_GTO:
       case SCHED_TWO_LEVEL:
@@ -946,24 +954,24 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
     }
     const uint32_t w = P::uni((uint32_t)pick);
     s.sched_last[sc] = w;
-    const uint32_t head = P::uni((uint32_t)s.w_head[w]);
-    const TInst in = P::uni(s.w_win[w][head % kWin]);
+    const uint32_t hidx = P::uni((uint32_t)s.w_head[w]);
+    const TInst in = head.at((int)w);
     if (trace_sm_on(c, TS_WARP_SCHEDULER, s.id))
       P::one([&] { trace_put(c, s.id, now, EV_ISSUE, (uint16_t)w, (uint64_t)in.pc | (uint64_t)in.opcode << 32); });
-    s.w_head[w] = head + 1;
+    s.w_head[w] = hidx + 1;
     s.w_ibuf[w] = (uint8_t)(P::uni((uint8_t)s.w_ibuf[w]) - 1);
     issued_any = true;
     // stats: instruction counts at issue (reference counts active threads,
     // shader.cc:1911)
-    s.st.warp_insn++;
-    s.st.thread_insn += (uint64_t)popc64(in.mask);
-    s.st.cls_insn[in.cls < OC_COUNT ? in.cls : OC_ALU]++;
+    s.sadd(SK(warp_insn), 1);
+    s.sadd(SK(thread_insn), (uint64_t)popc64(in.mask));
+    s.sadd(SK(cls_insn) + (in.cls < OC_COUNT ? in.cls : OC_ALU), 1);
     s.last_progress = now;
     uint32_t cta = P::uni((uint8_t)s.w_cta[w]);
     if (in.cls == OC_EXIT) {
       // lanes retire; the warp ends only when EXIT is its last instruction
       // (reference checkExecutionStatusAndUpdate, trace_driven.cc:588-606)
-      if (head + 1 >= P::uni((uint32_t)s.w_end[w])) {
+      if (hidx + 1 >= P::uni((uint32_t)s.w_end[w])) {
         s.w_flags[w] |= WF_EXITING;
         s.cta_nexit[cta]++;
         sm_barrier_check<P>(s, cta, k);
@@ -992,13 +1000,9 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
     }
     if (in.cls == OC_NOP) continue;
     const uint32_t u = unit_of(c, in.cls);
-    IdOc& r = s.idoc[sc][u];
-    r.inst = in;
-    r.valid = 1;
-    s.idoc_mask |= 1ull << (sc * U_COUNT + u);
-    r.warp = (uint8_t)w;
-    r.widx = ++s.age_ctr;
-    r.pad[0] = 0xff;
+    const uint32_t k = sc * U_COUNT + u;
+    TInst ri = in;
+    uint32_t lslot = 0xff;
     s.w_inflight[w]++;
     if (in.cls == OC_LOAD) {
       // allocate a load slot; scoreboard reserves destination registers
@@ -1011,21 +1015,24 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
       s.w_slot_pend[w][sl] = (uint16_t)nacc;
       s.w_slot_dst[w][sl][0] = in.dst[0];
       s.w_slot_dst[w][sl][1] = in.dst[1];
-      r.pad[0] = (uint8_t)sl;
+      lslot = sl;
       if (in.space != S_SHARED && in.width == 0) {
         // memory instruction without any active access: completes via ring
         s.w_slot_pend[w][sl] = 1;
-        r.inst.space = S_SHARED;
-        r.inst.width = 1;
+        ri.space = S_SHARED;
+        ri.width = 1;
       }
     } else if (in.cls == OC_STORE && in.space != S_SHARED && in.width == 0) {
-      r.inst.space = S_SHARED;
-      r.inst.width = 1;
+      ri.space = S_SHARED;
+      ri.width = 1;
     }
-    sb_set(s.w_sb[w], in.dst[0]);
-    sb_set(s.w_sb[w], in.dst[1]);
+    s.idoc_inst[k] = ri;
+    s.idoc_meta[k] = idoc_pack(w, lslot, ++s.age_ctr);
+    s.idoc_mask |= 1ull << k;
+    sbs(s.w_sb, w, in.dst[0]);
+    sbs(s.w_sb, w, in.dst[1]);
   }
-  if (issued_any) s.st.busy_cycles++;
+  if (issued_any) s.sadd(SK(busy_cycles), 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1091,13 +1098,13 @@ SIM_HDI void sm_retire(S& s, const SmCtx& x, uint64_t now) {
     if (!(s.w_flags[w] & WF_EXITING)) s.cta_nexit[cta]++;  // implicit exit at stream end
     s.w_flags[w] = 0;
     s.n_warps_live--;
-    s.st.warps_done++;
+    s.sadd(SK(warps_done), 1);
     s.cta_live[cta]--;
     s.cta_nexit[cta]--;
     if (s.cta_live[cta] == 0) {
       s.cta_valid[cta] = 0;
       s.n_cta_active--;
-      s.st.ctas_done++;
+      s.sadd(SK(ctas_done), 1);
     } else {
       sm_barrier_check<P>(s, cta, k);
     }
@@ -1136,7 +1143,7 @@ SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id)
     s.w_stores[w] = 0;
     s.w_loads[w] = 0;
     s.w_slot_used[w] = 0;
-    s.w_sb[w][0] = s.w_sb[w][1] = s.w_sb[w][2] = s.w_sb[w][3] = 0;
+    sbz(s.w_sb, w);
   });
   P::sync();
 }
@@ -1185,8 +1192,8 @@ SIM_HDI void sm_cycle(S& s, const SmCtx& x, uint64_t now) {
   sm_inject<P>(s, x, now);
   P::prof(11);
   if (P::uni(s.n_cta_active)) {
-    s.st.active_cycles++;
-    s.st.occupancy_acc += P::uni(s.n_warps_live);
+    s.sadd(SK(active_cycles), 1);
+    s.sadd(SK(occupancy_acc), P::uni(s.n_warps_live));
   }
 }
 
@@ -1196,19 +1203,25 @@ SIM_HDI bool sm_idle(const S& s) {
   return s.n_cta_active == 0 && s.outq_n == 0 && s.outstanding == 0 && !s.ldst.busy;
 }
 
-// first cycle in [from, limit) whose slot of a time-indexed ring is occupied
-SIM_HDI uint64_t ring_next(const uint64_t* occ, uint32_t ring, uint64_t from, uint64_t limit) {
+// first cycle in [from, limit) whose slot of a time-indexed ring is occupied:
+// the occupied slot at the smallest circular distance from `from` (one
+// candidate per 64-slot word, lane-parallel; the GPU view keeps the words in
+// registers)
+template <class P, class A>
+SIM_HDI uint64_t ring_next(const A& occ, uint32_t ring, uint64_t from, uint64_t limit) {
   const uint32_t nwords = ring / 64;
   const uint32_t start = (uint32_t)(from % ring);
   const uint32_t w0 = start >> 6, b0 = start & 63;
-  uint64_t m = occ[w0] >> b0;
-  if (m) return amin<uint64_t>(limit, from + (uint64_t)ffs64(m));
-  uint64_t d = 64 - b0;
-  for (uint32_t j = 1; j <= nwords && from + d < limit; ++j, d += 64) {
-    const uint64_t v = occ[(w0 + j) % nwords];
-    if (v) return amin<uint64_t>(limit, from + d + (uint64_t)ffs64(v));
-  }
-  return limit;
+  auto dist = [&](int i) -> uint64_t {
+    const uint64_t m = occ[i];
+    if (!m) return ~0ull;
+    const uint64_t mh = (uint32_t)i == w0 ? (m & (~0ull << b0)) : m;
+    const uint32_t p = (uint32_t)i * 64u + (uint32_t)ffs64(mh ? mh : m);
+    return (uint64_t)((p + ring - start) & (ring - 1));
+  };
+  const int j = P::argmin((int)nwords, dist);
+  if (j < 0) return limit;
+  return amin<uint64_t>(limit, from + P::uni(dist(j)));
 }
 
 // Exact quiescence test before simulating cycle `t`: if no stage of
@@ -1219,9 +1232,9 @@ SIM_HDI uint64_t ring_next(const uint64_t* occ, uint32_t ring, uint64_t from, ui
 template <class P, class S>
 SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, uint64_t t, uint64_t limit) {
   if (P::uni(s.ldst.busy) || P::uni(s.idoc_mask) || P::uni(s.oc_mask | s.oc_read_mask) || P::uni(s.outq_n)) return t;
-  uint64_t nx = ring_next(s.wb_occ, kWbRing, t, limit);
+  uint64_t nx = ring_next<P>(s.wb_occ, kWbRing, t, limit);
   if (nx == t) return t;
-  nx = ring_next(s.hit_occ, kHitRing, t, nx);
+  nx = ring_next<P>(s.hit_occ, kHitRing, t, nx);
   if (nx == t) return t;
   if (P::uni(s.inq_n)) {
     const uint64_t at = (P::uni(s.inq[P::uni(s.inq_head)].t) + c.per_core - 1) / c.per_core;
@@ -1255,10 +1268,10 @@ SIM_HDI void sm_skip(S& s, const SimCfg& c, uint64_t k) {
   }
   // uniform update by every lane (not P::one: on the GPU these fields may be
   // registers of a view, which a one-lane write would leave divergent)
-  s.st.issue_stall_idle += (uint64_t)stalled * k;
+  s.sadd(SK(issue_stall_idle), (uint64_t)stalled * k);
   if (P::uni(s.n_cta_active)) {
-    s.st.active_cycles += k;
-    s.st.occupancy_acc += (uint64_t)popc64(live) * k;
+    s.sadd(SK(active_cycles), k);
+    s.sadd(SK(occupancy_acc), (uint64_t)popc64(live) * k);
   }
   s.skipped_cycles += k;
   P::sync();

@@ -24,3 +24,12 @@ def test_check_engine_reports_divergence(native, nw):
     with pytest.raises(Exception, match="engine check failed at cycle"):
         sim.simulate(nw, "QV100", engine="check",
                      extra={"-sim_check_primary": "cpu", "-sim_check_interval": "300", "-sim_check_corrupt_at": "1000"})
+
+
+def test_check_engine_reports_mailbox_divergence(native, nw):
+    # a wrong mailbox count is caught at the check point where it happens and
+    # named as a mailbox, not blamed on the unit that later receives it
+    with pytest.raises(Exception, match="mailbox count diverges"):
+        sim.simulate(nw, "QV100", engine="check",
+                     extra={"-sim_check_primary": "cpu", "-sim_check_interval": "300", "-sim_check_corrupt_at": "1000",
+                            "-sim_check_corrupt_mailbox": "1"})
