@@ -146,11 +146,12 @@ def _volta_common() -> Dict[str, str]:
         "-enable_ptx_file_line_stats": "1",
         "-visualizer_enabled": "0",
         # trace frontend
-        "-trace_opcode_latency_initiation_int": "4,2",
-        "-trace_opcode_latency_initiation_sp": "4,2",
+        # SM7_QV100/trace.config:1-5
+        "-trace_opcode_latency_initiation_int": "2,2",
+        "-trace_opcode_latency_initiation_sp": "2,2",
         "-trace_opcode_latency_initiation_dp": "8,4",
         "-trace_opcode_latency_initiation_sfu": "20,8",
-        "-trace_opcode_latency_initiation_tensor": "8,4",
+        "-trace_opcode_latency_initiation_tensor": "2,2",
         "-specialized_unit_1": "1,4,4,4,4,BRA",
         "-trace_opcode_latency_initiation_spec_op_1": "4,4",
         "-specialized_unit_2": "1,4,200,4,4,TEX",
@@ -174,6 +175,15 @@ def _titanv() -> Dict[str, str]:
     c = _volta_common()
     c["-gpgpu_n_mem"] = "24"
     c["-gpgpu_clock_domains"] = "1200.0:1200.0:1200.0:850.0"
+    # SM7_TITANV/gpgpusim.config + trace.config
+    c.update({
+        "-gpgpu_n_clusters": "40", "-gpgpu_n_cores_per_cluster": "2",
+        "-ptx_opcode_latency_int": "4,13,4,5,145,32", "-gpgpu_num_reg_banks": "8", "-gpgpu_coalesce_arch": "60",
+        "-dram_bnk_indexing_policy": "1", "-dram_seperate_write_queue_enable": "1",
+        "-dram_write_queue_size": "128:108:32",
+        "-trace_opcode_latency_initiation_tensor": "8,4", "-trace_opcode_latency_initiation_spec_op_3": "8,4",
+        "-gpgpu_kernel_launch_latency": "0",  # not set in SM7_TITANV/gpgpusim.config: the option default
+    })
     return c
 
 
@@ -200,6 +210,21 @@ def _rtx2060() -> Dict[str, str]:
         "-gpgpu_mem_addr_mapping": "dramid@8;00000000.00000000.00000000.00000000.0000RRRR.RRRRRRRR.RBBBCCCC.BCCSSSSS",
         "-gpgpu_dram_timing_opt": '"nbk=16:CCD=4:RRD=10:RCD=20:RAS=50:RP=20:RC=62:CL=20:WL=8:CDLR=9:WR=20:nbkgrp=4:CCDL=4:RTPL=4"',
     })
+    # SM75_RTX2060/gpgpusim.config + trace.config
+    c.update({
+        "-gpgpu_clock_domains": "1365:1365:1365:3500.5", "-gpgpu_occupancy_sm_number": "75",
+        "-ptx_opcode_latency_int": "4,4,4,4,21", "-ptx_opcode_initiation_int": "2,2,2,2,2",
+        "-ptx_opcode_latency_fp": "4,4,4,4,39", "-ptx_opcode_latency_dp": "64,64,64,64,330",
+        "-ptx_opcode_initiation_dp": "64,64,64,64,130", "-ptx_opcode_latency_sfu": "21",
+        "-gpgpu_num_reg_banks": "8", "-gpgpu_cache:dl1": "S:4:128:64,L:T:m:L:L,A:256:32,16:0,32",
+        "-gpgpu_l1_latency": "32", "-gpgpu_shmem_per_block": "49152", "-gpgpu_smem_latency": "30",
+        "-gpgpu_coalesce_arch": "75", "-gpgpu_l2_rop_latency": "194", "-dram_latency": "96",
+        "-gpgpu_dram_timing_opt": '"nbk=16:CCD=4:RRD=12:RCD=24:RAS=55:RP=24:RC=78:CL=24:WL=8:CDLR=10:WR=24:nbkgrp=4:CCDL=6:RTPL=4"',
+        "-trace_opcode_latency_initiation_dp": "64,64", "-trace_opcode_latency_initiation_sfu": "21,8",
+        "-trace_opcode_latency_initiation_tensor": "16,16", "-specialized_unit_3": "1,4,16,4,4,TENSOR",
+        "-trace_opcode_latency_initiation_spec_op_3": "16,16", "-specialized_unit_4": "1,4,4,4,4,UDP",
+        "-trace_opcode_latency_initiation_spec_op_4": "4,1",
+    })
     return c
 
 
@@ -217,6 +242,16 @@ def _rtx3070() -> Dict[str, str]:
         "-gpgpu_shmem_option": "0,8,16,32,64,100",
         "-gpgpu_shmem_size": "102400",
         "-gpgpu_shmem_sizeDefault": "102400",
+    })
+    # SM86_RTX3070/gpgpusim.config + trace.config
+    c.update({
+        "-gpgpu_clock_domains": "1132:1132:1132:3500.5", "-gpgpu_occupancy_sm_number": "86",
+        "-gpgpu_shader_cta": "32", "-ptx_opcode_initiation_fp": "1,1,1,1,2",
+        "-gpgpu_cache:dl1": "S:4:128:256,L:T:m:L:L,A:384:48,16:0,32", "-gpgpu_l1_latency": "39",
+        "-gpgpu_smem_latency": "29", "-gpgpu_coalesce_arch": "86", "-gpgpu_memory_partition_indexing": "2",
+        "-gpgpu_l2_rop_latency": "187", "-dram_latency": "254",
+        "-trace_opcode_latency_initiation_sp": "2,1", "-trace_opcode_latency_initiation_tensor": "32,32",
+        "-specialized_unit_3": "1,4,32,4,4,TENSOR", "-trace_opcode_latency_initiation_spec_op_3": "32,32",
     })
     return c
 
@@ -331,6 +366,16 @@ def _titanx() -> Dict[str, str]:
         "-gpgpu_mem_addr_mapping": "dramid@8;00000000.00000000.00000000.00000000.0000RRRR.RRRRRRRR.RBBBCCCC.BCCSSSSS",
         "-inter_config_file": "config_pascal_islip.icnt",
     })
+    # SM6_TITANX/gpgpusim.config
+    c.update({
+        "-ptx_opcode_latency_int": "4,13,4,5,145,32", "-ptx_opcode_initiation_int": "1,1,1,1,4,4",
+        "-ptx_opcode_latency_fp": "4,13,4,4,39", "-ptx_opcode_initiation_fp": "1,2,1,1,4",
+        "-ptx_opcode_initiation_dp": "8,8,8,8,130", "-ptx_opcode_initiation_sfu": "4", "-ptx_opcode_latency_sfu": "20",
+        "-gpgpu_sub_core_model": "1",
+        "-gpgpu_cache:dl1PrefL1": "S:4:128:96,L:L:s:N:L,A:256:8,16:0,32",
+        "-gpgpu_cache:dl1PrefShared": "S:4:128:96,L:L:s:N:L,A:256:8,16:0,32",
+        "-gpgpu_shmem_size_PrefL1": "98304", "-gpgpu_shmem_size_PrefShared": "98304",
+    })
     return c
 
 
@@ -357,6 +402,19 @@ def _kepler_titan() -> Dict[str, str]:
         "-inter_config_file": "config_kepler_islip.icnt",
         "-trace_opcode_latency_initiation_dp": "20,2",
         "-trace_opcode_latency_initiation_sfu": "200,2",
+    })
+    # SM3_KEPLER_TITAN/gpgpusim.config
+    c.update({
+        "-ptx_opcode_latency_int": "4,13,4,5,145,32", "-ptx_opcode_initiation_int": "1,1,1,1,4,4",
+        "-ptx_opcode_initiation_fp": "1,2,1,1,4", "-ptx_opcode_initiation_dp": "2,8,8,8,130",
+        "-ptx_opcode_initiation_sfu": "2", "-ptx_opcode_latency_sfu": "200",
+        "-gpgpu_operand_collector_num_in_ports_sp": "2", "-gpgpu_operand_collector_num_out_ports_sp": "2",
+        "-gpgpu_operand_collector_num_in_ports_sfu": "2", "-gpgpu_operand_collector_num_out_ports_sfu": "2",
+        "-gpgpu_operand_collector_num_in_ports_mem": "1", "-gpgpu_operand_collector_num_out_ports_mem": "1",
+        "-gpgpu_operand_collector_num_in_ports_dp": "1", "-gpgpu_operand_collector_num_out_ports_dp": "1",
+        "-gpgpu_cache:dl1PrefL1": "S:4:128:96,L:L:s:N:L,A:256:8,16:0,32",
+        "-gpgpu_cache:dl1PrefShared": "S:4:128:32,L:L:s:N:L,A:256:8,16:0,32",
+        "-gpgpu_shmem_size_PrefL1": "16384", "-gpgpu_shmem_size_PrefShared": "49152", "-smem_latency": "24",
     })
     return c
 
@@ -392,6 +450,18 @@ def _gtx480() -> Dict[str, str]:
         "-gpgpu_clock_gated_lanes": "0",
         "-inter_config_file": "config_fermi_islip.icnt",
     })
+    # SM2_GTX480/gpgpusim.config
+    c.update({
+        "-ptx_opcode_latency_int": "4,13,4,5,145,32", "-ptx_opcode_initiation_int": "1,2,2,1,8,4",
+        "-ptx_opcode_initiation_fp": "1,2,1,1,4", "-ptx_opcode_initiation_dp": "8,16,8,8,130",
+        "-gpgpu_tex_cache:l1": "N:4:128:24,L:R:m:N:L,T:128:4,128:2",
+        "-gpgpu_operand_collector_num_in_ports_sp": "2", "-gpgpu_operand_collector_num_out_ports_sp": "2",
+        # no trace.config for SM2_GTX480 and no fetch throughput line: option defaults
+        "-gpgpu_inst_fetch_throughput": "1",
+        "-trace_opcode_latency_initiation_int": "4,1", "-trace_opcode_latency_initiation_sp": "4,1",
+        "-trace_opcode_latency_initiation_dp": "4,1", "-trace_opcode_latency_initiation_sfu": "4,1",
+        "-trace_opcode_latency_initiation_tensor": "4,1",
+    })
     return c
 
 
@@ -415,6 +485,14 @@ def _rtx2060_s() -> Dict[str, str]:
         "-trace_opcode_latency_initiation_spec_op_3": "16,16",
         "-specialized_unit_4": "1,4,4,4,4,UDP",
         "-trace_opcode_latency_initiation_spec_op_4": "4,1",
+    })
+    # SM75_RTX2060_S/gpgpusim.config: the Volta-style FU latencies
+    c.update({
+        "-gpgpu_occupancy_sm_number": "75", "-gpgpu_coalesce_arch": "75", "-gpgpu_num_dp_units": "0",
+        "-ptx_opcode_latency_int": "4,13,4,5,145,32", "-ptx_opcode_initiation_int": "2,2,2,2,8,4",
+        "-ptx_opcode_latency_fp": "4,13,4,5,39", "-ptx_opcode_latency_dp": "8,19,8,8,330",
+        "-ptx_opcode_initiation_dp": "4,4,4,4,130", "-ptx_opcode_latency_sfu": "100",
+        "-gpgpu_dram_timing_opt": '"nbk=16:CCD=4:RRD=10:RCD=20:RAS=50:RP=20:RC=62:CL=20:WL=8:CDLR=9:WR=20:nbkgrp=4:CCDL=4:RTPL=4"',
     })
     return c
 

@@ -71,6 +71,8 @@ class DistributedSuite:
                     self.apps.append((app, kl))
         self.max_concurrency = None
         self.weights: Dict[str, float] = {}  # last wall time per app (LPT order)
+        self.times: Dict = {}                # (app, engine) -> last wall time
+        self.assignment: Dict[str, str] = {}
         # the all-reduce example traced for this rank count (all-reduce-<N>),
         # or the single-rank one
         ar = os.path.join(root, f"all-reduce-{world}", "kernelslist.g")
@@ -94,9 +96,10 @@ class DistributedSuite:
             import torch
             torch.cuda.set_device(self.device_index)
 
-    def _sim(self, kl: str):
+    def _sim(self, kl: str, engine: Optional[str] = None):
         extra = {"-collective_model": self.collective_model}
-        args = build_args(self.config, kl, self.engine, extra)
+        eng = engine or ("gpu" if self.engine == "node" else self.engine)
+        args = build_args(self.config, kl, eng, extra)
         return self.mod.Simulator(args, self.verbose)
 
     def concurrency(self) -> int:
@@ -104,19 +107,28 @@ class DistributedSuite:
         GPU (each needs all its unit blocks co-resident).  CPU engine: job
         level parallelism, one single-threaded simulation per host core
         (``ASIM_CPU_JOBS`` overrides the core count)."""
-        if self.engine != "gpu":
-            n = int(os.environ.get("ASIM_CPU_JOBS", "0") or 0)
-            if n <= 0:
-                try:
-                    n = len(os.sched_getaffinity(0))
-                except AttributeError:  # pragma: no cover - non-Linux
-                    n = os.cpu_count() or 1
+        if self.engine == "cpu":
+            n = self.cpu_slots()
             return max(1, min(len(self.apps) or 1, n))
         cus = int(self.mod.gpu_cu_count())
         cfg = self.mod.parse_config(build_args(self.config, None, "cpu"))
         per = self.mod.gpu_cus_per_sim(cfg["n_sm"], cfg["n_mem"]) if hasattr(self.mod, "gpu_cus_per_sim") \
             else cfg["n_sm"] + cfg["n_mem"]
         return max(1, cus // per // self.ranks_per_gpu()) if cus else 1
+
+    def cpu_slots(self, reserve: int = 0) -> int:
+        """Host cores this rank may use for CPU-engine simulations: its share
+        of the node's cores (ranks of one node split them), less `reserve`
+        (the host threads driving GPU-engine simulations).  ``ASIM_CPU_JOBS``
+        overrides."""
+        n = int(os.environ.get("ASIM_CPU_JOBS", "0") or 0)
+        if n <= 0:
+            try:
+                n = len(os.sched_getaffinity(0))
+            except AttributeError:  # pragma: no cover - non-Linux
+                n = os.cpu_count() or 1
+            n //= max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+        return max(1, n - reserve)
 
     _rpg_cache: Optional[int] = None
 
@@ -150,16 +162,84 @@ class DistributedSuite:
         cls._rpg_cache = n
         return n
 
-    def _run_app(self, app_kl):
+    def _run_app(self, app_kl, engine: Optional[str] = None):
         import time
         app, kl = app_kl
         t0 = time.perf_counter()
-        s = self._sim(kl)
+        s = self._sim(kl, engine)
         rc = s.run()
         if rc != 0:
             raise RuntimeError(f"{app}: simulation failed (deadlock={s.deadlock})\n{s.output[-1500:]}")
-        self.weights[app] = time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        self.weights[app] = dt
+        self.times[(app, engine or ("gpu" if self.engine == "node" else self.engine))] = dt
         return app, s.tot_insn, s.tot_cycle
+
+    # ---- whole-node mode: GPU-engine slots and CPU-engine cores together ----
+    # A cycle-level simulation is a long chain of dependent epochs.  The HIP
+    # engine wins where an epoch carries much parallel work (many busy SMs:
+    # hotspot, heartwall, backprop); a latency-bound application (few warps,
+    # many short kernels: bfs, nw, streamcluster) runs about as fast on one
+    # host core.  The node schedule gives every application the engine that
+    # minimises the step's makespan, like the reference's job-level
+    # parallelism (procman over a node's cores) plus the GPU.
+    def calibrate(self) -> Dict[str, Dict[str, float]]:
+        """Time every application on both engines (GPU slots and CPU cores
+        side by side), so plan() can place them."""
+        from concurrent.futures import ThreadPoolExecutor
+        gslots = max(1, self.concurrency())
+        cslots = self.cpu_slots(reserve=gslots)
+        with ThreadPoolExecutor(max_workers=gslots, initializer=self._bind_device) as gx, \
+                ThreadPoolExecutor(max_workers=cslots) as cx:
+            fg = [gx.submit(self._run_app, a, "gpu") for a in self.apps]
+            fc = [cx.submit(self._run_app, a, "cpu") for a in self.apps]
+            for f in fg + fc:
+                f.result()
+        return {a: {"gpu": self.times[(a, "gpu")], "cpu": self.times[(a, "cpu")]} for a, _ in self.apps}
+
+    @staticmethod
+    def _lpt(ts: List[float], slots: int) -> float:
+        load = [0.0] * max(1, slots)
+        for t in sorted(ts, reverse=True):
+            i = min(range(len(load)), key=load.__getitem__)
+            load[i] += t
+        return max(load) if ts else 0.0
+
+    def plan(self):
+        """Engine per application minimising the predicted makespan
+        (exhaustive over the subsets sent to the GPU; LPT inside each pool)."""
+        gslots = max(1, self.concurrency())
+        cslots = self.cpu_slots(reserve=gslots)
+        names = [a for a, _ in self.apps]
+        tg = [self.times.get((a, "gpu"), 1.0) for a in names]
+        tc = [self.times.get((a, "cpu"), 1.0) for a in names]
+        n = len(names)
+        best = (float("inf"), 0)
+        for m in range(1 << n) if n <= 16 else [(1 << n) - 1]:
+            g = [tg[i] for i in range(n) if m >> i & 1]
+            c = [tc[i] for i in range(n) if not m >> i & 1]
+            span = max(self._lpt(g, gslots), self._lpt(c, cslots))
+            if span < best[0]:
+                best = (span, m)
+        self.assignment = {names[i]: ("gpu" if best[1] >> i & 1 else "cpu") for i in range(n)}
+        self.predicted_span = best[0]
+        return self.assignment
+
+    def _step_node(self):
+        from concurrent.futures import ThreadPoolExecutor
+        if not getattr(self, "assignment", None):
+            if not all((a, e) in self.times for a, _ in self.apps for e in ("gpu", "cpu")):
+                self.calibrate()
+            self.plan()
+        gslots = max(1, self.concurrency())
+        cslots = self.cpu_slots(reserve=gslots)
+        ga = sorted([x for x in self.apps if self.assignment[x[0]] == "gpu"], key=lambda x: -self.times[(x[0], "gpu")])
+        ca = sorted([x for x in self.apps if self.assignment[x[0]] == "cpu"], key=lambda x: -self.times[(x[0], "cpu")])
+        with ThreadPoolExecutor(max_workers=gslots, initializer=self._bind_device) as gx, \
+                ThreadPoolExecutor(max_workers=max(1, min(cslots, len(ca) or 1))) as cx:
+            fg = [gx.submit(self._run_app, a, "gpu") for a in ga]
+            fc = [cx.submit(self._run_app, a, "cpu") for a in ca]
+            return [f.result() for f in fg + fc]
 
     def _run_allreduce(self):
         s = self._sim(self.allreduce)
@@ -172,7 +252,9 @@ class DistributedSuite:
         insn = cycles = 0
         per_app = {}
         conc = self.concurrency() if self.max_concurrency is None else self.max_concurrency
-        if conc <= 1:
+        if self.engine == "node":
+            results = self._step_node()
+        elif conc <= 1:
             results = [self._run_app(x) for x in self.apps]
         else:
             from concurrent.futures import ThreadPoolExecutor

@@ -1,13 +1,22 @@
 #!/usr/bin/env python3
 """Headline benchmark: simulator throughput (sim KIPS, whole node) on the
-Rodinia-2.0-ft suite (synthetic traces of the suite's shape) with the QV100
-config, one simulated GPU per MI355X.
+Rodinia-2.0-ft suite (synthetic traces of the suite's shape) with the GV100
+config (BASELINE.json config #2: SM7_GV100 = the SM7_QV100 gpgpusim.config at
+1447 MHz, plus the SM7_QV100 trace.config), one simulated GPU per MI355X.
 
 One "step" = every application of the suite simulated end to end (trace load
-+ coalescing + cycle simulation + stats) on the GPU engine, followed -- when
-N > 1 -- by the suite's closing all-reduce (examples/all-reduce) whose
-completion is synchronised across the N simulated GPUs over RCCL.  Weak
-scaling: every rank simulates its own GPU running the full suite.
++ coalescing + cycle simulation + stats), followed -- when N > 1 -- by the
+suite's closing all-reduce (examples/all-reduce) whose completion is
+synchronised across the N simulated GPUs over RCCL.  Weak scaling: every rank
+simulates its own GPU running the full suite.
+
+Engines: ``node`` (default with a GPU) runs each application on the engine that
+minimises the step's makespan -- the HIP cycle engine on the MI355X for
+applications with much parallel work per epoch, the CPU engine on the rank's
+share of host cores for latency-bound ones (placement measured during warmup,
+parallel/multi_gpu.py DistributedSuite.plan).  ``gpu`` / ``cpu`` force one
+engine (``cpu``: one single-threaded simulation per core, the reference's
+job-level parallelism).
 
     python bench.py --gpus N --steps K --warmup W
 Rank 0 prints ONE JSON line.  KIPS = simulated thread instructions (the
@@ -35,8 +44,8 @@ def _parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="QV100")
-    ap.add_argument("--engine", default="auto", choices=["auto", "gpu", "cpu"])
+    ap.add_argument("--config", default="GV100")
+    ap.add_argument("--engine", default="auto", choices=["auto", "node", "gpu", "cpu"])
     ap.add_argument("--apps", default="all")
     ap.add_argument("--trace-dir", default=None)
     ap.add_argument("--verbose", action="store_true")
@@ -47,15 +56,22 @@ def _parse():
 
 
 def _cycle_mae():
-    """Latest committed MI355X cycle correlation (HIP app suite vs rocprofv3),
-    produced by tools/gpu_correlate.sh / tools/local_correlate.py."""
+    """The latest committed MI355X cycle correlation, labelled as what it is:
+    an offline run (tools/gpu_correlate.sh: HIP apps timed with rocprofv3,
+    re-simulated), NOT measured by this bench run."""
     p = os.path.join(ROOT, "profiles", "correlation", "mi355x_local_resim.json")
     try:
         d = json.load(open(p))
         return {"mae_pct": round(d["mae_pct"], 2), "apps": len(d["apps"]), "gpu": "MI355X",
-                "source": os.path.relpath(p, ROOT)}
+                "measured": "offline, not in this run", "engine": d.get("engine", "cpu"),
+                "run": d.get("run_id", os.path.basename(p)), "source": os.path.relpath(p, ROOT)}
     except (OSError, ValueError, KeyError):
         return None
+
+
+def _cfg_desc(name: str) -> str:
+    return {"GV100": "SM7_GV100 gpgpusim.config = SM7_QV100 at 1447 MHz, + SM7_QV100 trace.config",
+            "QV100": "SM7_QV100 gpgpusim.config + trace.config"}.get(name, "preset " + name)
 
 
 def _resolve_app(rodinia, name: str) -> str:
@@ -91,9 +107,9 @@ def main() -> int:
     mod = _native.load(prefer_torch_runtime=True)
     engine = a.engine
     if engine == "auto":
-        engine = "gpu" if mod.gpu_available() else "cpu"
-    if engine == "gpu" and not mod.gpu_available():
-        raise SystemExit("bench.py: --engine gpu requested but no HIP device is usable")
+        engine = "node" if mod.gpu_available() else "cpu"
+    if engine in ("gpu", "node") and not mod.gpu_available():
+        raise SystemExit(f"bench.py: --engine {engine} requested but no HIP device is usable")
 
     from accel_sim_framework_distributed_amd.parallel.multi_gpu import DistributedSuite
     from accel_sim_framework_distributed_amd.tracegen import rodinia
@@ -133,6 +149,10 @@ def main() -> int:
         if world > 1:
             dist.barrier()
 
+    if engine == "node":
+        # untimed: time every application on both engines, then place them
+        suite.calibrate()
+        suite.plan()
     for _ in range(a.warmup):
         suite.step()
     sync()
@@ -171,11 +191,12 @@ def main() -> int:
             "dtype": "n/a (integer cycle-level model)",
             "data": "synthetic (seeded Rodinia-2.0-ft-shaped SASS traces; no recorded traces available)",
             "config": {
-                "model": f"{a.config} (SM7_QV100 gpgpusim.config + trace.config) simulating rodinia_2.0-ft",
+                "model": f"{a.config} ({_cfg_desc(a.config)}) simulating rodinia_2.0-ft",
                 "global_batch": world,
                 "seq_len": None,
                 "parallelism": f"one simulated GPU per MI355X rank (dp{world}), RCCL-synchronised collectives",
                 "engine": engine,
+                **({"node_assignment": suite.assignment} if engine == "node" else {}),
                 "apps": len(suite.apps),
                 "sim_insn_per_step_per_rank": int(insn / max(1, a.steps)),
                 "sim_cycles_per_step_per_rank": int(cycles / max(1, a.steps)),

@@ -77,3 +77,25 @@ def test_reference_tested_configs_load(native):
         assert c["n_sm"] > 0
         n += 1
     assert n >= 5
+
+
+@pytest.mark.skipif(not os.path.isdir(REFERENCE), reason="reference tree not mounted")
+@pytest.mark.parametrize("preset,gdir,tdir", [("GV100", "SM7_GV100", "SM7_QV100"), ("QV100", "SM7_QV100", "SM7_QV100"),
+                                              ("TITANV", "SM7_TITANV", "SM7_TITANV"),
+                                              ("RTX2060", "SM75_RTX2060", "SM75_RTX2060"),
+                                              ("RTX2060_S", "SM75_RTX2060_S", "SM75_RTX2060_S"),
+                                              ("RTX3070", "SM86_RTX3070", "SM86_RTX3070"),
+                                              ("TITANX", "SM6_TITANX", "SM6_TITANX"),
+                                              ("KEPLER_TITAN", "SM3_KEPLER_TITAN", "SM3_KEPLER_TITAN"),
+                                              ("GTX480", "SM2_GTX480", None)])
+def test_presets_equal_reference_files(native, preset, gdir, tdir):
+    """Every preset derives exactly the configuration of the reference's own
+    files (gpgpusim.config + trace.config; the bench's GV100 takes the
+    SM7_QV100 trace.config, as no SM7_GV100 one exists)."""
+    from accel_sim_framework_distributed_amd.models import presets
+    gp = os.path.join(REFERENCE, "gpu-simulator/gpgpu-sim/configs/tested-cfgs", gdir, "gpgpusim.config")
+    tr = os.path.join(REFERENCE, "gpu-simulator/configs/tested-cfgs", tdir or "-", "trace.config")
+    ref = native.parse_config(["-config", gp] + (["-config", tr] if os.path.exists(tr) else []))
+    mine = native.parse_config(presets.args_for(preset))
+    diff = {k: (ref[k], mine.get(k)) for k in ref if ref[k] != mine.get(k)}
+    assert not diff, diff

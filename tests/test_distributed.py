@@ -142,3 +142,22 @@ def test_packet_exchange_four_ranks_overflow(native):
     st = res[0][2]
     # one fixed exchange per epoch, plus the spill exchanges
     assert st["exchanges"] > st["epochs"] > 0
+
+
+def test_node_plan_places_apps_by_makespan(native, tmp_path, monkeypatch):
+    """Whole-node mode: every application goes to the engine that minimises
+    the step's makespan (GPU slots vs CPU cores, LPT inside each pool)."""
+    from accel_sim_framework_distributed_amd.parallel.multi_gpu import DistributedSuite
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    apps = ["nn-rodinia-2.0-ft", "pathfinder-rodinia-2.0-ft", "backprop-rodinia-2.0-ft"]
+    rodinia.generate_suite(str(tmp_path), apps)
+    monkeypatch.setenv("ASIM_CPU_JOBS", "3")  # 1 GPU slot (no GPU here) + 2 CPU cores
+    s = DistributedSuite(str(tmp_path), engine="node")
+    t = {"nn-rodinia-2.0-ft": (0.1, 1.0), "pathfinder-rodinia-2.0-ft": (0.9, 0.5),
+         "backprop-rodinia-2.0-ft": (0.2, 2.0)}  # (gpu, cpu) seconds
+    for a, (g, c) in t.items():
+        s.times[(a, "gpu")] = g
+        s.times[(a, "cpu")] = c
+    plan = s.plan()
+    assert plan == {"nn-rodinia-2.0-ft": "gpu", "backprop-rodinia-2.0-ft": "gpu", "pathfinder-rodinia-2.0-ft": "cpu"}
+    assert abs(s.predicted_span - 0.5) < 1e-9
