@@ -115,14 +115,14 @@ void apply_intersim_config(SimCfg& c, const std::string& path) {
   c.chan_icnt = (uint16_t)std::max<long>(1, geti(kv, "channel_latency", 1));
   if (kv.count("flit_size")) c.flit_size = (uint32_t)std::max<long>(8, geti(kv, "flit_size", 32));
   c.icnt_mode = 1;
-  // lookahead = smallest pair latency in whole core cycles (>= 1, <= kWin - kIbuf)
+  // lookahead = smallest pair latency in whole core cycles (>= 1, <= kMaxEpoch)
   uint64_t lo = ~0ull;
   c.icnt_latency = 1;  // icnt_pkt_lat_fs clamps to it; 1 core cycle is the floor
   for (uint32_t s = 0; s < c.n_sm; s += (c.cores_per_cluster ? c.cores_per_cluster : 1))
     for (uint32_t d = 0; d < c.n_subpart; ++d) lo = std::min(lo, icnt_pkt_lat_fs(c, s, d));
   uint64_t e = lo / c.per_core;
   if (e < 1) e = 1;
-  if (e > (uint64_t)(kWin - kIbuf)) e = (uint64_t)(kWin - kIbuf);
+  if (e > (uint64_t)kMaxEpoch) e = (uint64_t)kMaxEpoch;
   c.icnt_latency = (uint32_t)e;
 }
 

@@ -686,8 +686,8 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.l1.mshr_entries = std::min<uint32_t>(c.l1.mshr_entries, kMaxL1Mshr);
   // interconnect
   c.icnt_latency = (uint32_t)r.getu("-icnt_latency");
-  if (c.icnt_latency < 1 || c.icnt_latency + kIbuf > (uint32_t)kWin)
-    throw OptionError("-icnt_latency must be in 1..14 (epoch length)");
+  if (c.icnt_latency < 1 || c.icnt_latency > (uint32_t)kMaxEpoch)
+    throw OptionError("-icnt_latency must be in 1.." + std::to_string(kMaxEpoch) + " (epoch length)");
   c.flit_size = std::max<uint32_t>(8, (uint32_t)r.getu("-icnt_flit_size"));
   c.icnt_out_limit = std::min<uint32_t>((uint32_t)r.getu("-sim_max_outstanding_pkts"), kInQ);
   if (c.icnt_out_limit == 0) c.icnt_out_limit = 1;

@@ -21,7 +21,7 @@ static void sb_regs(std::ostringstream& o, const uint64_t* sb) {
   if (!any) o << "-";
 }
 
-std::string dump_sm_state(const SMState& s, const SimCfg& c) {
+std::string dump_sm_state(const SMState& s, const SimCfg& c, const TInst* insts) {
   std::ostringstream o;
   o << "=== SM " << s.id << " @ cycle " << s.cycle << ": " << s.n_cta_active << " CTAs, "
     << s.outstanding << " packets in flight, outq " << s.outq_n << ", inq " << s.inq_n << ", L1 waiters " << s.n_pend
@@ -39,8 +39,8 @@ std::string dump_sm_state(const SMState& s, const SimCfg& c) {
     if (f & WF_WAITCNT) o << " WAITCNT";
     o << " scoreboard ";
     sb_regs(o, s.w_sb[w]);
-    if (s.w_ibuf[w]) {
-      const TInst& in = s.w_win[w][s.w_head[w] % kWin];
+    if (s.w_ibuf[w] && insts) {
+      const TInst& in = insts[s.w_head[w]];
       o << " next " << opcode_name(in.opcode) << " pc 0x" << std::hex << in.pc << std::dec;
     }
     o << "\n";
@@ -119,7 +119,7 @@ std::string Simulator::dump_pipeline(int sm, int ch) {
   for (uint32_t i = 0; i < cfg_.n_sm; ++i)
     if (sm == -1 || (sm >= 0 && (uint32_t)sm == i)) {
       if (sm == -1 && sms[i].n_cta_active == 0 && sms[i].outstanding == 0) continue;  // skip idle SMs in "all"
-      out += dump_sm_state(sms[i], cfg_);
+      out += dump_sm_state(sms[i], cfg_, cur_kernel_ && !cur_kernel_->insts.empty() ? cur_kernel_->insts.data() : nullptr);
     }
   for (uint32_t i = 0; i < cfg_.n_mem; ++i)
     if (ch == -1 || (ch >= 0 && (uint32_t)ch == i)) {

@@ -72,7 +72,7 @@ inline uint32_t backlog_cap(const SimCfg& c) {
 
 struct EngineStateHeader {
   uint64_t magic = 0x41534d5354415445ull;  // "ASMSTATE"
-  uint64_t version = 2;
+  uint64_t version = 3;  // 3: UnitPub records, no instruction window
   uint64_t n_sm = 0, n_mem = 0, sm_bytes = 0, ch_bytes = 0, pub_bytes = 0;
   uint64_t box_req = 0, cnt_req = 0, box_rep = 0, cnt_rep = 0;  // element counts per parity
   uint64_t ovf = 0;                                              // arrival backlog packets (all sub-partitions)

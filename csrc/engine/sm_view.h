@@ -177,7 +177,6 @@ struct SmView {
   SV_WARP(w_next);
   SV_WARP(w_end);
   SV_WARP(w_head);
-  SV_REF(w_wfill);
   SV_WARP(w_age);
   SV_WARP(w_flags);
   SV_WARP(w_ibuf);
@@ -189,7 +188,6 @@ struct SmView {
   SV_WARP(w_slot_used);
   SV_REF(w_slot_pend);
   SV_REF(w_slot_dst);
-  SV_REF(w_win);
   SV_REF(cta_id);
   SV_WARP(cta_valid);
   SV_WARP(cta_live);
@@ -197,6 +195,7 @@ struct SmView {
   SV_WARP(cta_nexit);
   SV_VAL(n_cta_active);
   SV_VAL(n_warps_live);
+  SV_VAL(live_mask);
   SV_VAL(n_wait_flags);
   SV_VAL(fetch_rr);
   SV_WARP(sched_last);
@@ -263,7 +262,7 @@ struct SmView {
 
 #define SV_SCALARS(X)                                                                                   \
   X(id) X(kernel_cta_slots) X(last_progress) X(epoch_end) X(out_port_free) X(age_ctr) X(n_cta_active)    \
-  X(n_warps_live) X(n_wait_flags) X(fetch_rr) X(n_pend) X(idoc_mask) X(oc_mask) X(oc_read_mask)         \
+  X(n_warps_live) X(live_mask) X(n_wait_flags) X(fetch_rr) X(n_pend) X(idoc_mask) X(oc_mask) X(oc_read_mask)         \
   X(l1_stamp) X(skipped_cycles) X(min_emit) X(outq_head) X(outq_n) X(outstanding) X(inq_head) X(inq_n)
 #define SV_WARPS(X) \
   X(w_next) X(w_end) X(w_head) X(w_age) X(w_flags) X(w_ibuf) X(w_cta) X(w_inflight) X(w_stores) X(w_loads) X(w_slot_used) \
@@ -271,8 +270,8 @@ struct SmView {
   X(cta_nexit) X(sched_last) X(w_iline)
 
   __device__ __forceinline__ explicit SmView(B& b)
-      : base(b), cycle(b.cycle), w_wfill(b.w_wfill), w_slot_pend(b.w_slot_pend),
-        w_slot_dst(b.w_slot_dst), w_win(b.w_win), cta_id(b.cta_id),
+      : base(b), cycle(b.cycle), w_slot_pend(b.w_slot_pend),
+        w_slot_dst(b.w_slot_dst), cta_id(b.cta_id),
         idoc_inst(b.idoc_inst), oc_inst(b.oc_inst),
         wb_cnt(b.wb_cnt), wb(b.wb), hit_cnt(b.hit_cnt), hit(b.hit), l1(b.l1), mshr(b.mshr),
         pend(b.pend), il1(b.il1), imshr(b.imshr),

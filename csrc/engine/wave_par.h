@@ -23,6 +23,47 @@ struct WavePar {
     return (uint64_t)__ballot(p);
   }
   template <class F>
+  static __device__ __forceinline__ void lane_loop(int n, F&& f) {
+    for (int i = lane(); i < n; i += 64) f(i);
+  }
+  static __device__ __forceinline__ uint32_t red_sum(uint32_t v) {
+    return wave_reduce(v, [](uint32_t a, uint32_t b) { return a + b; });
+  }
+  template <bool kMax>
+  static __device__ __forceinline__ uint64_t red64(uint64_t v) {
+    uint32_t h = (uint32_t)(v >> 32), l = (uint32_t)v;
+    auto step = [&](uint32_t oh, uint32_t ol) {
+      const bool take = kMax ? (oh > h || (oh == h && ol > l)) : (oh < h || (oh == h && ol < l));
+      if (take) { h = oh; l = ol; }
+    };
+    step(dpp<0xB1>(h), dpp<0xB1>(l));
+    step(dpp<0x4E>(h), dpp<0x4E>(l));
+    step(dpp<0x141>(h), dpp<0x141>(l));
+    step(dpp<0x140>(h), dpp<0x140>(l));
+    uint32_t rh = rdl(h, 0), rl = rdl(l, 0);
+#pragma unroll
+    for (int r = 16; r < 64; r += 16) {
+      const uint32_t oh = rdl(h, r), ol = rdl(l, r);
+      const bool take = kMax ? (oh > rh || (oh == rh && ol > rl)) : (oh < rh || (oh == rh && ol < rl));
+      if (take) { rh = oh; rl = ol; }
+    }
+    return ((uint64_t)rh << 32) | rl;
+  }
+  static __device__ __forceinline__ uint64_t red_min64(uint64_t v) { return red64<false>(v); }
+  static __device__ __forceinline__ uint64_t red_max64(uint64_t v) { return red64<true>(v); }
+  template <class F>
+  static __device__ __forceinline__ uint64_t ballot_m(uint64_t mask, F&& f) {
+    const int l = lane();
+    bool p = false;
+    if ((mask >> l) & 1ull) p = f(l);
+    return (uint64_t)__ballot(p);
+  }
+  template <class F>
+  static __device__ __forceinline__ void each_m(uint64_t mask, F&& f) {
+    const int l = lane();
+    if ((mask >> l) & 1ull) f(l);
+  }
+  template <class F>
   static __device__ __forceinline__ void each(int n, F&& f) {
     for (int i = lane(); i < n; i += 64) f(i);
   }

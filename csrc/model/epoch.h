@@ -18,20 +18,24 @@ namespace asim {
 
 constexpr int kMaxChTot = 128;
 
+// one unit's epoch-boundary publication: one 32-byte record, written by one
+// store and read by one load per unit (the decision pass reads every unit)
+struct UnitPub {
+  uint64_t next;     // next-event time (fs, ~0 = none) for whole-epoch fast-forward:
+                     // the first instant the unit can change state, or one of the
+                     // packets it injected this epoch arrives (-sim_event_skip)
+  uint64_t prog;     // SM: last progress cycle
+  uint32_t req;      // SM: CTA slots it can accept next epoch
+  uint32_t idle;     // SM: drained and kernel fully dispatched; channel: idle
+  uint32_t drained;  // SM: holds no work (launch latency may be pending)
+  uint32_t pad;
+};
 // epoch-boundary publications, double buffered by epoch parity
 struct EpochPub {
-  uint32_t sm_req[2][kMaxSmTot];     // CTA slots an SM can accept next epoch
-  uint32_t sm_idle[2][kMaxSmTot];    // SM drained and kernel fully dispatched
-  uint32_t sm_drained[2][kMaxSmTot]; // SM holds no work (launch latency may be pending)
-  uint64_t sm_prog[2][kMaxSmTot];    // last progress cycle
-  uint32_t ch_idle[2][kMaxChTot];
-  uint32_t next_cta[2];              // replicated dispatch cursor (published by SM 0)
+  UnitPub sm[2][kMaxSmTot];
+  UnitPub ch[2][kMaxChTot];
+  uint32_t next_cta[2];  // replicated dispatch cursor (published by SM 0)
   uint32_t pad[2];
-  // next-event times (fs, ~0 = none) for whole-epoch fast-forward: the first
-  // instant a unit can change state, or one of the packets it injected this
-  // epoch arrives (-sim_event_skip)
-  uint64_t sm_next[2][kMaxSmTot];
-  uint64_t ch_next[2][kMaxChTot];
 };
 
 // upper bound of one SM's quiet-cycle look-ahead at an epoch boundary
@@ -49,20 +53,21 @@ struct EpochDecision {
 // ---------------------------------------------------------------------------
 // CTA dispatch: round-robin rounds over requesting SMs, rotated by epoch.
 template <class P>
-SIM_HDI void cta_dispatch(SMState& s, const SmCtx& x, SmKernel& ks, const uint32_t* req, uint32_t n_sm,
+SIM_HDI void cta_dispatch(SMState& s, const SmCtx& x, SmKernel& ks, const UnitPub* pubs, uint32_t n_sm,
                           uint32_t rot) {
   const KernelDesc& k = *x.k;
   if (ks.next_cta >= k.n_cta) return;
   const uint32_t me = s.id;
-  const uint32_t my_q = req[me];
+  auto req = [&](int j) -> uint32_t { return pubs[j].req; };
+  const uint32_t my_q = req((int)me);
   const uint32_t my_rank = (me + n_sm - rot) % n_sm;
   uint32_t base = ks.next_cta;
   for (uint32_t r = 0; r < (uint32_t)kMaxCta && base < k.n_cta; ++r) {
-    uint32_t pr = P::sum((int)n_sm, [&](int j) -> uint32_t { return req[j] > r ? 1u : 0u; });
+    uint32_t pr = P::sum((int)n_sm, [&](int j) -> uint32_t { return req(j) > r ? 1u : 0u; });
     if (pr == 0) break;
     if (my_q > r) {
       uint32_t pos = P::sum((int)n_sm, [&](int j) -> uint32_t {
-        return (req[j] > r && ((uint32_t)j + n_sm - rot) % n_sm < my_rank) ? 1u : 0u;
+        return (req(j) > r && ((uint32_t)j + n_sm - rot) % n_sm < my_rank) ? 1u : 0u;
       });
       uint32_t cta = base + pos;
       if (cta < k.n_cta) {
@@ -116,10 +121,9 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& 
   if (t0 >= ks.ready_cycle)
     // rotation by simulated time (t0 / epoch length), not by the epoch counter,
     // so fast-forwarded epochs leave the CTA -> SM assignment unchanged
-    cta_dispatch<P>(s, x, ks, pub.sm_req[prev], c.n_sm, (uint32_t)((t0 / c.icnt_latency) % c.n_sm));
-  // 3. trace window refill
+    cta_dispatch<P>(s, x, ks, pub.sm[prev], c.n_sm, (uint32_t)((t0 / c.icnt_latency) % c.n_sm));
+  // 3. (instructions are read from the kernel trace directly)
   P::prof(14);
-  sm_refill_window<P>(s, c, *x.k);
   // 4. cycles
   P::prof(15);
   s.epoch_end = t1;
@@ -133,7 +137,7 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& 
         if (t < t1 && c.event_skip) {
           // fast-forward cycles in which provably nothing happens
           P::tick(18);
-          const uint64_t nx = P::uni(sm_quiet_until<P>(v, c, t, t1));
+          const uint64_t nx = P::uni(sm_quiet_until<P>(v, c, x.k->insts, t, t1));
           if (nx > t) {
             sm_skip<P>(v, c, nx - t);
             t = nx;
@@ -160,14 +164,17 @@ SIM_HDI void sm_publish(SMState& s, const SmCtx& x, const SmKernel& ks, EpochPub
   const uint32_t idle = (ks.next_cta >= x.k->n_cta && sm_idle(s)) ? 1u : 0u;
   uint64_t nx = ~0ull;
   if (c.event_skip && (s.n_cta_active || !sm_idle(s)))
-    nx = sm_quiet_until<P>(s, c, s.cycle, s.cycle + kSkipHorizon) * c.per_core;
+    nx = sm_quiet_until<P>(s, c, x.k->insts, s.cycle, s.cycle + kSkipHorizon) * c.per_core;
   nx = amin(nx, s.min_emit);
+  UnitPub u;
+  u.next = nx;
+  u.prog = s.last_progress;
+  u.req = req;
+  u.idle = idle;
+  u.drained = sm_idle(s) ? 1u : 0u;
+  u.pad = 0;
   P::one([&] {
-    pub.sm_next[cur][s.id] = nx;
-    pub.sm_req[cur][s.id] = req;
-    pub.sm_idle[cur][s.id] = idle;
-    pub.sm_drained[cur][s.id] = sm_idle(s) ? 1u : 0u;
-    pub.sm_prog[cur][s.id] = s.last_progress;
+    pub.sm[cur][s.id] = u;
     if (s.id == 0) pub.next_cta[cur] = ks.next_cta;
   });
 }
@@ -194,10 +201,14 @@ SIM_HDI void chan_publish(ChanState& ch, const MemCtx& x, EpochPub& pub, uint32_
   uint64_t nx = ~0ull;
   if (x.cfg->event_skip) nx = chan_next_event(ch, *x.cfg, amin(ch.t_dram, amin(ch.t_l2, ch.t_icnt)));
   nx = amin(nx, ch.min_emit);
-  P::one([&] {
-    pub.ch_idle[cur][ch.id] = idle;
-    pub.ch_next[cur][ch.id] = nx;
-  });
+  UnitPub u;
+  u.next = nx;
+  u.prog = 0;
+  u.req = 0;
+  u.idle = idle;
+  u.drained = idle;
+  u.pad = 0;
+  P::one([&] { pub.ch[cur][ch.id] = u; });
 }
 
 // every participant computes the same decision from the published state
@@ -206,21 +217,39 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
                                    uint64_t ready_cycle, uint32_t next_cta_done, uint64_t epoch_idx,
                                    uint64_t max_cycle) {
   EpochDecision d;
-  uint32_t nbusy = P::sum((int)c.n_sm, [&](int j) -> uint32_t { return pub.sm_idle[cur][j] ? 0u : 1u; });
-  uint32_t cbusy = P::sum((int)c.n_mem, [&](int j) -> uint32_t { return pub.ch_idle[cur][j] ? 0u : 1u; });
+  // one pass over every unit's record (one load per unit), then reductions
+  uint32_t nbusy = 0, undrained = 0, nreq = 0, cbusy = 0;
+  uint64_t sm_next = ~0ull, ch_next = ~0ull, prog = 0;
+  P::lane_loop((int)c.n_sm, [&](int j) {
+    const UnitPub u = pub.sm[cur][j];
+    nbusy += u.idle ? 0u : 1u;
+    undrained += u.drained ? 0u : 1u;
+    nreq += u.req ? 1u : 0u;
+    sm_next = amin<uint64_t>(sm_next, u.next);
+    prog = amax<uint64_t>(prog, u.prog & ((1ull << 56) - 1));  // progress stamps are < 2^56
+  });
+  P::lane_loop((int)c.n_mem, [&](int j) {
+    const UnitPub u = pub.ch[cur][j];
+    cbusy += u.idle ? 0u : 1u;
+    ch_next = amin<uint64_t>(ch_next, u.next);
+  });
+  nbusy = P::uni(P::red_sum(nbusy));
+  undrained = P::uni(P::red_sum(undrained));
+  nreq = P::uni(P::red_sum(nreq));
+  cbusy = P::uni(P::red_sum(cbusy));
+  sm_next = P::uni(P::red_min64(sm_next));
+  ch_next = P::uni(P::red_min64(ch_next));
+  prog = P::uni(P::red_max64(prog));
   d.done = (nbusy == 0) ? 1u : 0u;
   d.all_idle = (nbusy == 0 && cbusy == 0) ? 1u : 0u;
   d.next_start = t1;
   d.deadlock = 0;
   d.pad = 0;
   // fast-forward over the kernel launch latency when nothing is in flight
-  if (!next_cta_done && cbusy == 0 && t1 < ready_cycle) {
-    uint32_t undrained = P::sum((int)c.n_sm, [&](int j) -> uint32_t { return pub.sm_drained[cur][j] ? 0u : 1u; });
-    if (undrained == 0) {
-      uint64_t E = c.icnt_latency;
-      uint64_t skip = (ready_cycle - t1) / E * E;
-      d.next_start = t1 + skip;
-    }
+  if (!next_cta_done && cbusy == 0 && t1 < ready_cycle && undrained == 0) {
+    uint64_t E = c.icnt_latency;
+    uint64_t skip = (ready_cycle - t1) / E * E;
+    d.next_start = t1 + skip;
   }
   // Whole-epoch fast-forward (conservative PDES with exact next-event times):
   // the earliest instant any SM or channel can change state, any packet in
@@ -228,12 +257,8 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   // participant can jump; epochs wholly before it are skipped.  With no
   // pending event at all (a deadlock) nothing is skipped.
   if (c.event_skip && !d.done) {
-    const int js = P::argmin((int)c.n_sm, [&](int j) -> uint64_t { return pub.sm_next[cur][j]; });
-    const int jc = P::argmin((int)c.n_mem, [&](int j) -> uint64_t { return pub.ch_next[cur][j]; });
-    uint64_t ev = js >= 0 ? pub.sm_next[cur][js] : ~0ull;
-    if (jc >= 0) ev = amin(ev, pub.ch_next[cur][jc]);
-    if (!next_cta_done && P::sum((int)c.n_sm, [&](int j) -> uint32_t { return pub.sm_req[cur][j] ? 1u : 0u; }))
-      ev = amin(ev, amax(t1, ready_cycle) * c.per_core);
+    uint64_t ev = amin(sm_next, ch_next);
+    if (!next_cta_done && nreq) ev = amin(ev, amax(t1, ready_cycle) * c.per_core);
     if (ev != ~0ull) {
       const uint64_t E = c.icnt_latency;
       const uint64_t tc = ev / c.per_core;  // the next epoch may start no later than this
@@ -245,9 +270,8 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
     }
   }
   if (c.deadlock_window && nbusy && ((t1 / c.icnt_latency) & 63) == 0) {
-    // newest progress stamp over all SMs (progress stamps are < 2^56)
-    int jm = P::argmin((int)c.n_sm, [&](int j) -> uint64_t { return ~pub.sm_prog[cur][j] & ((1ull << 56) - 1); });
-    uint64_t last = jm >= 0 ? pub.sm_prog[cur][jm] : 0;
+    // newest progress stamp over all SMs
+    const uint64_t last = prog;
     if (t1 > last + c.deadlock_window && t1 > ready_cycle + c.deadlock_window) d.deadlock = 1;
   }
   return d;

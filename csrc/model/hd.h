@@ -51,6 +51,30 @@ struct SeqPar {
       if (f(i)) m |= 1ull << i;
     return m;
   }
+  // one pass over n elements split across lanes (here: all of them), then
+  // reductions of the per-lane partials (here: identity)
+  template <class F>
+  static SIM_HDI void lane_loop(int n, F&& f) {
+    for (int i = 0; i < n; ++i) f(i);
+  }
+  static SIM_HDI uint32_t red_sum(uint32_t v) { return v; }
+  static SIM_HDI uint64_t red_min64(uint64_t v) { return v; }
+  static SIM_HDI uint64_t red_max64(uint64_t v) { return v; }
+  // ballot restricted to the lanes of `mask` (bit i = f(i) && mask bit i):
+  // the CPU engine visits only those lanes (e.g. the live warps)
+  template <class F>
+  static SIM_HDI uint64_t ballot_m(uint64_t mask, F&& f) {
+    uint64_t m = 0;
+    for (uint64_t r = mask; r; r &= r - 1) {
+      const int i = __builtin_ctzll(r);
+      if (f(i)) m |= 1ull << i;
+    }
+    return m;
+  }
+  template <class F>
+  static SIM_HDI void each_m(uint64_t mask, F&& f) {
+    for (uint64_t r = mask; r; r &= r - 1) f(__builtin_ctzll(r));
+  }
   // run f(i) for every i < n (independent iterations only)
   template <class F>
   static SIM_HDI void each(int n, F&& f) {

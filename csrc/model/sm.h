@@ -29,9 +29,8 @@ struct TAcc {
 };
 static_assert(sizeof(TAcc) == 16, "TAcc must stay 16 bytes");
 
-// instruction window per warp (prefetched trace records, ring indexed by
-// instruction index modulo kWin)
-// (kWin is defined in config.h)
+// Warps read their instructions straight from the kernel's decoded trace
+// (KernelDesc::insts, HBM on the GPU): w_next / w_head / w_end index it.
 
 enum WarpFlags : uint8_t {
   WF_ACTIVE = 1,
@@ -163,7 +162,6 @@ struct alignas(16) SMState {
   uint32_t w_next[kMaxWarps];   // next trace index to fetch into ibuf
   uint32_t w_end[kMaxWarps];    // end of stream
   uint32_t w_head[kMaxWarps];   // next trace index to issue
-  uint32_t w_wfill[kMaxWarps];  // window filled up to (exclusive)
   uint32_t w_age[kMaxWarps];    // dynamic warp id (oldest first)
   uint8_t w_flags[kMaxWarps];
   uint8_t w_ibuf[kMaxWarps];    // decoded instructions available
@@ -176,7 +174,6 @@ struct alignas(16) SMState {
   uint8_t w_pad[kMaxWarps][3];
   uint16_t w_slot_pend[kMaxWarps][kLoadSlots];
   uint8_t w_slot_dst[kMaxWarps][kLoadSlots][2];
-  TInst w_win[kMaxWarps][kWin];
   // ---- CTAs ----
   uint32_t cta_id[kMaxCta];
   uint8_t cta_valid[kMaxCta];
@@ -185,6 +182,7 @@ struct alignas(16) SMState {
   uint8_t cta_nexit[kMaxCta];    // warps exited (excluded from barrier count)
   uint32_t n_cta_active;
   uint32_t n_warps_live;         // warps with WF_ACTIVE (occupancy statistic)
+  uint64_t live_mask;            // bit w: warp w has WF_ACTIVE
   uint32_t n_wait_flags;         // warps parked in WF_MEMBAR / WF_WAITCNT
   // ---- front end ----
   uint32_t fetch_rr;
@@ -531,10 +529,10 @@ SIM_HDI void il1_fill(S& s, const SimCfg& c, uint64_t line) {
 // probe the instruction cache for warp w's next fetch; true = instructions
 // available this cycle
 template <class P, class S>
-SIM_HDI bool il1_fetch(S& s, const SimCfg& c, uint32_t w) {
+SIM_HDI bool il1_fetch(S& s, const SimCfg& c, const TInst* insts, uint32_t w) {
   const CacheGeom& g = c.il1;
-  const TInst& in = s.w_win[w][s.w_next[w] % kWin];
-  const uint64_t line = (kProgramMemStart + in.pc) & ~127ull;
+  const uint32_t pc = P::uni(insts[P::uni((uint32_t)s.w_next[w])].pc);
+  const uint64_t line = (kProgramMemStart + pc) & ~127ull;
   const uint32_t set = cache_set_index(g, line);
   const int way = il1_find<P>(s, g, set, line);
   if (way >= 0) {
@@ -899,9 +897,10 @@ SIM_HDI bool warp_can_issue_i(const S& s, const SimCfg& c, int w, const TInst& i
   return true;
 }
 template <class S>
-SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, int w, uint32_t nsched, uint64_t idoc_busy) {
+SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, const TInst* insts, int w, uint32_t nsched,
+                            uint64_t idoc_busy) {
   if (!(s.w_flags[w] & WF_ACTIVE) || s.w_ibuf[w] == 0) return false;
-  const TInst in = s.w_win[w][s.w_head[w] % kWin];
+  const TInst in = insts[s.w_head[w]];  // ibuf > 0: the head is inside the warp's stream
   return warp_can_issue_i(s, c, w, in, nsched, idoc_busy);
 }
 
@@ -913,10 +912,14 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
   const uint64_t idoc_busy = P::uni(s.idoc_mask);
   // every warp's next instruction, read once (a register per lane on the GPU)
-  const auto head = P::template lanes<TInst>(nw, [&](int w) -> TInst { return s.w_win[w][s.w_head[w] % kWin]; });
+  // (read straight from the kernel's trace in HBM: an L2-resident stream)
+  const auto head = P::template lanes<TInst>(nw, [&](int w) -> TInst {
+    const uint32_t h = s.w_head[w];
+    return h < s.w_end[w] ? k.insts[h] : TInst{};
+  });
   // readiness of every warp (lane-parallel)
-  uint64_t ready = P::ballot(nw, [&](int w) -> bool { return warp_can_issue_i(s, c, w, head.self(w), nsched, idoc_busy); });
-  uint64_t live = P::ballot(nw, [&](int w) { return (s.w_flags[w] & WF_ACTIVE) != 0; });
+  const uint64_t live = P::uni(s.live_mask);
+  uint64_t ready = P::ballot_m(live, [&](int w) -> bool { return warp_can_issue_i(s, c, w, head.self(w), nsched, idoc_busy); });
   P::prof(29);
   bool issued_any = false;
   for (uint32_t sc = 0; sc < nsched; ++sc) {
@@ -1039,9 +1042,9 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
 // fetch/decode: refill the instruction buffer of up to fetch_throughput
 // warps whose buffer is empty (round-robin), perfect instruction cache
 template <class P, class S>
-SIM_HDI void sm_fetch(S& s, const SimCfg& c) {
+SIM_HDI void sm_fetch(S& s, const SimCfg& c, const TInst* insts) {
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
-  uint64_t need = P::ballot(nw, [&](int w) {
+  uint64_t need = P::ballot_m(P::uni(s.live_mask), [&](int w) {
     uint8_t f = s.w_flags[w];
     return (f & WF_ACTIVE) && !(f & (WF_EXITING | WF_IMISS)) && s.w_ibuf[w] == 0 && s.w_next[w] < s.w_end[w];
   });
@@ -1052,7 +1055,7 @@ SIM_HDI void sm_fetch(S& s, const SimCfg& c) {
     int b = ffs64(r);
     r &= r - 1;
     uint32_t w = (uint32_t)(b + start) % (uint32_t)nw;
-    if (icache && !il1_fetch<P>(s, c, w)) {
+    if (icache && !il1_fetch<P>(s, c, insts, w)) {
       s.fetch_rr = w + 1;  // miss / reservation fail ends this cycle's fetch (shader.cc:997-1010)
       break;
     }
@@ -1072,7 +1075,8 @@ SIM_HDI void sm_retire(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
   const KernelDesc& k = *x.k;
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
-  uint64_t done = P::ballot(nw, [&](int w) {
+  const uint64_t live = P::uni(s.live_mask);
+  uint64_t done = P::ballot_m(live, [&](int w) {
     uint8_t f = s.w_flags[w];
     if (!(f & WF_ACTIVE)) return false;
     bool drained = s.w_head[w] >= s.w_end[w] && s.w_ibuf[w] == 0;
@@ -1080,14 +1084,17 @@ SIM_HDI void sm_retire(S& s, const SmCtx& x, uint64_t now) {
   });
   // release membar / waitcnt waits
   if (P::uni(s.n_wait_flags)) {
-    const uint32_t released = P::sum(nw, [&](int w) -> uint32_t {
+    uint32_t released = 0;
+    const uint64_t rel = P::ballot_m(live, [&](int w) {
       uint8_t f = s.w_flags[w];
       uint32_t r = 0;
       if ((f & WF_MEMBAR) && s.w_stores[w] == 0) { f = f & (uint8_t)~WF_MEMBAR; ++r; }
       if ((f & WF_WAITCNT) && s.w_stores[w] == 0 && s.w_loads[w] == 0) { f = f & (uint8_t)~WF_WAITCNT; ++r; }
       if (r) s.w_flags[w] = f;
-      return r;
+      return r != 0;
     });
+    // a warp waits on at most one of the two flags at a time
+    released = (uint32_t)popc64(rel);
     s.n_wait_flags = P::uni(s.n_wait_flags) - released;
     P::sync();
   }
@@ -1097,6 +1104,7 @@ SIM_HDI void sm_retire(S& s, const SmCtx& x, uint64_t now) {
     uint32_t cta = s.w_cta[w];
     if (!(s.w_flags[w] & WF_EXITING)) s.cta_nexit[cta]++;  // implicit exit at stream end
     s.w_flags[w] = 0;
+    s.live_mask &= ~(1ull << w);
     s.n_warps_live--;
     s.sadd(SK(warps_done), 1);
     s.cta_live[cta]--;
@@ -1126,6 +1134,7 @@ SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id)
   s.cta_nexit[slot] = 0;
   s.n_cta_active++;
   s.n_warps_live += wpc;
+  s.live_mask |= (wpc >= 64 ? ~0ull : ((1ull << wpc) - 1)) << base;
   uint32_t age0 = s.age_ctr;
   s.age_ctr += wpc;
   P::each((int)wpc, [&](int i) {
@@ -1133,7 +1142,6 @@ SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id)
     WStream ws = k.streams[(uint64_t)cta_id * wpc + (uint32_t)i];
     s.w_next[w] = ws.begin;
     s.w_head[w] = ws.begin;
-    s.w_wfill[w] = ws.begin;
     s.w_end[w] = ws.begin + ws.count;
     s.w_age[w] = age0 + (uint32_t)i;
     s.w_flags[w] = WF_ACTIVE;
@@ -1144,22 +1152,6 @@ SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id)
     s.w_loads[w] = 0;
     s.w_slot_used[w] = 0;
     sbz(s.w_sb, w);
-  });
-  P::sync();
-}
-
-// refill the per-warp instruction windows from the kernel trace (HBM).
-// Done once per epoch: a warp can consume at most `epoch` instructions per
-// epoch, so kWin >= epoch + kIbuf guarantees the window never runs dry.
-template <class P, class S>
-SIM_HDI void sm_refill_window(S& s, const SimCfg& c, const KernelDesc& k) {
-  const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
-  P::each(nw, [&](int w) {
-    if (!(s.w_flags[w] & WF_ACTIVE)) return;
-    uint32_t lim = s.w_head[w] + kWin;
-    if (lim > s.w_end[w]) lim = s.w_end[w];
-    for (uint32_t i = s.w_wfill[w]; i < lim; ++i) s.w_win[w][i % kWin] = k.insts[i];
-    if (lim > s.w_wfill[w]) s.w_wfill[w] = lim;
   });
   P::sync();
 }
@@ -1185,7 +1177,7 @@ SIM_HDI void sm_cycle(S& s, const SmCtx& x, uint64_t now) {
   P::prof(7);
   sm_issue<P>(s, x, now);
   P::prof(8);
-  sm_fetch<P>(s, c);
+  sm_fetch<P>(s, c, x.k->insts);
   P::prof(9);
   sm_retire<P>(s, x, now);
   P::prof(10);
@@ -1230,7 +1222,7 @@ SIM_HDI uint64_t ring_next(const A& occ, uint32_t ring, uint64_t from, uint64_t 
 // per-cycle statistics (sm_skip).  This is what makes latency-bound phases
 // (every warp waiting on memory) cost one check instead of one cycle each.
 template <class P, class S>
-SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, uint64_t t, uint64_t limit) {
+SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, const TInst* insts, uint64_t t, uint64_t limit) {
   if (P::uni(s.ldst.busy) || P::uni(s.idoc_mask) || P::uni(s.oc_mask | s.oc_read_mask) || P::uni(s.outq_n)) return t;
   uint64_t nx = ring_next<P>(s.wb_occ, kWbRing, t, limit);
   if (nx == t) return t;
@@ -1243,7 +1235,7 @@ SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, uint64_t t, uint64_
   }
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
-  const uint64_t act = P::ballot(nw, [&](int w) -> bool {
+  const uint64_t act = P::ballot_m(P::uni(s.live_mask), [&](int w) -> bool {
     const uint8_t f = s.w_flags[w];
     if (!(f & WF_ACTIVE)) return false;
     if (!(f & (WF_EXITING | WF_IMISS)) && s.w_ibuf[w] == 0 && s.w_next[w] < s.w_end[w]) return true;  // fetch
@@ -1251,7 +1243,7 @@ SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, uint64_t t, uint64_
     if (drained && s.w_inflight[w] == 0 && s.w_stores[w] == 0 && s.w_loads[w] == 0) return true;  // retire
     if ((f & WF_MEMBAR) && s.w_stores[w] == 0) return true;
     if ((f & WF_WAITCNT) && s.w_stores[w] == 0 && s.w_loads[w] == 0) return true;
-    return warp_can_issue(s, c, w, nsched, s.idoc_mask);  // issue
+    return warp_can_issue(s, c, insts, w, nsched, s.idoc_mask);  // issue
   });
   return act ? t : nx;
 }
@@ -1261,7 +1253,7 @@ template <class P, class S>
 SIM_HDI void sm_skip(S& s, const SimCfg& c, uint64_t k) {
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
-  const uint64_t live = P::ballot(nw, [&](int w) { return (s.w_flags[w] & WF_ACTIVE) != 0; });
+  const uint64_t live = P::uni(s.live_mask);
   uint32_t stalled = 0;
   for (uint32_t sc = 0; sc < nsched; ++sc) {
     if (live & c.sched_mask[sc]) ++stalled;
