@@ -52,7 +52,7 @@ SASS = {
     "LDG.E.128": ("LOAD", "GLOBAL", FLAG["MEM"], 16),
     "LDG.E.CONSTANT": ("LOAD", "GLOBAL", FLAG["MEM"], 4),
     "STG.E": ("STORE", "GLOBAL", FLAG["MEM"], 4), "STG.E.64": ("STORE", "GLOBAL", FLAG["MEM"], 8),
-    "STG.E.128": ("STORE", "GLOBAL", FLAG["MEM"], 16),
+    "STG.E.128": ("STORE", "GLOBAL", FLAG["MEM"], 16), "STG.E.U16": ("STORE", "GLOBAL", FLAG["MEM"], 2),
     "LDL": ("LOAD", "LOCAL", FLAG["MEM"], 4), "STL": ("STORE", "LOCAL", FLAG["MEM"], 4),
     "LDS": ("LOAD", "SHARED", FLAG["MEM"], 4), "LDS.64": ("LOAD", "SHARED", FLAG["MEM"], 8),
     "STS": ("STORE", "SHARED", FLAG["MEM"], 4), "STS.64": ("STORE", "SHARED", FLAG["MEM"], 8),

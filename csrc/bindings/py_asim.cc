@@ -56,6 +56,9 @@ py::dict cfg_dict(const SimCfg& c) {
   d["max_cta_per_sm"] = c.max_cta_per_sm;
   d["n_sched"] = c.n_sched;
   d["sched_policy"] = c.sched_policy;
+  d["sched_param"] = c.sched_param;
+  d["max_issue_per_warp"] = c.max_issue_per_warp;
+  d["dual_issue_diff"] = c.dual_issue_diff;
   d["fetch_throughput"] = c.fetch_throughput;
   d["ex_wb_width"] = c.ex_wb_width;
   d["oc_units"] = c.oc_units;

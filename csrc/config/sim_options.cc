@@ -452,7 +452,7 @@ uint8_t sched_of(const std::string& s) {
   if (s.rfind("old", 0) == 0) return SCHED_OLDEST;
   if (s.rfind("rrr", 0) == 0) return SCHED_RRR;
   if (s.rfind("two_level_active", 0) == 0) return SCHED_TWO_LEVEL;
-  if (s.rfind("warp_limiting", 0) == 0) return SCHED_GTO;
+  if (s.rfind("warp_limiting", 0) == 0) return SCHED_WARP_LIMITING;
   throw OptionError("unknown scheduler '" + s + "'");
 }
 
@@ -592,6 +592,21 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.sub_core = r.getb("-gpgpu_sub_core_model") ? 1 : 0;
   c.fetch_throughput = (uint32_t)std::max<long long>(1, r.geti("-gpgpu_inst_fetch_throughput"));
   c.max_issue_per_warp = (uint32_t)std::max<long long>(1, r.geti("-gpgpu_max_insn_issue_per_warp"));
+  c.dual_issue_diff = r.getb("-gpgpu_dual_issue_diff_exec_units") ? 1u : 0u;
+  {
+    // scheduler parameters: two_level_active:<max_active>:<inner>:<outer>,
+    // warp_limiting:<prioritization>:<warps to limit>
+    const std::string sp = r.gets("-gpgpu_scheduler");
+    const auto f = split(sp, ':');
+    c.sched_param = 0;
+    if (c.sched_policy == SCHED_TWO_LEVEL) c.sched_param = f.size() > 1 ? parse_u(f[1], "-gpgpu_scheduler") : 6;
+    if (c.sched_policy == SCHED_WARP_LIMITING) {
+      if (f.size() < 3) throw OptionError("warp_limiting needs warp_limiting:<prio>:<warps>");
+      c.sched_param = parse_u(f[2], "-gpgpu_scheduler");
+    }
+    if ((c.sched_policy == SCHED_TWO_LEVEL || c.sched_policy == SCHED_WARP_LIMITING) && c.sched_param == 0)
+      throw OptionError("scheduler limit must be >= 1: " + sp);
+  }
   // execution units
   c.unit_count[U_SP] = (uint32_t)r.getu("-gpgpu_num_sp_units");
   c.unit_count[U_DP] = (uint32_t)r.getu("-gpgpu_num_dp_units");

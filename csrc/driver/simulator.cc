@@ -671,6 +671,78 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   print("total dram activates = %llu\n", (unsigned long long)dram_act);
   print("dram_bw_util = %.4f\n", dram_cyc ? (double)dram_busy / dram_cyc : 0.0);
   print("gpgpu_n_tot_w_icount = %llu\n", (unsigned long long)tot_warp_insn_);
+  {
+    // further gpu_print_stat / shader_core_stats lines (reference
+    // gpu-sim.cc:1355-1541, shader.cc:3012-3170): instruction mix, issue
+    // stalls, register-bank conflicts, dual issue, L1 write-backs; memory
+    // partition, DRAM queue and interconnect stalls
+    uint64_t cls[OC_COUNT] = {}, stall_idle = 0, sb = 0, pipe = 0, bankc = 0, dual = 0, l1wb = 0, l1wbl = 0,
+             act = 0, busyc = 0, occ = 0, rfr = 0, rfw = 0, ctas = 0, warps = 0, memi = 0;
+    for (auto& st : sm) {
+      for (int i = 0; i < OC_COUNT; ++i) cls[i] += st.cls_insn[i];
+      stall_idle += st.issue_stall_idle;
+      sb += st.sb_stall;
+      pipe += st.pipe_stall;
+      bankc += st.oc_bank_conflicts;
+      dual += st.dual_issued;
+      l1wb += st.l1_wb;
+      l1wbl += st.l1_wb_lost;
+      act += st.active_cycles;
+      busyc += st.busy_cycles;
+      occ += st.occupancy_acc;
+      rfr += st.rf_reads;
+      rfw += st.rf_writes;
+      ctas += st.ctas_done;
+      warps += st.warps_done;
+      memi += st.mem_insn;
+    }
+    print("gpgpu_n_load_insn = %llu\n", (unsigned long long)cls[OC_LOAD]);
+    print("gpgpu_n_store_insn = %llu\n", (unsigned long long)cls[OC_STORE]);
+    print("gpgpu_n_mem_insn_dispatched = %llu\n", (unsigned long long)memi);
+    print("gpgpu_n_branch_insn = %llu\n", (unsigned long long)cls[OC_BRANCH]);
+    print("gpgpu_n_sfu_insn = %llu\n", (unsigned long long)cls[OC_SFU]);
+    print("gpgpu_n_dp_insn = %llu\n", (unsigned long long)cls[OC_DP]);
+    print("gpgpu_n_tensor_insn = %llu\n", (unsigned long long)cls[OC_TENSOR]);
+    print("gpgpu_n_barrier_insn = %llu\n", (unsigned long long)cls[OC_BARRIER]);
+    print("gpgpu_n_dual_issue = %llu\n", (unsigned long long)dual);
+    print("gpu_stall_shd_idle_sched = %llu\n", (unsigned long long)stall_idle);
+    print("gpgpu_n_stall_shd_mem = %llu\n",
+          (unsigned long long)(l1[L1T_GLOBAL_R][L1O_RES_FAIL] + l1[L1T_GLOBAL_W][L1O_RES_FAIL] +
+                               l1[L1T_LOCAL_R][L1O_RES_FAIL] + l1[L1T_LOCAL_W][L1O_RES_FAIL] +
+                               l1[L1T_ATOMIC][L1O_RES_FAIL]));
+    print("gpu_stall_result_bus = %llu\n", (unsigned long long)pipe);
+    print("gpu_reg_bank_conflict_stalls = %llu\n", (unsigned long long)bankc);
+    print("gpgpu_n_l1_writebacks = %llu\n", (unsigned long long)l1wb);
+    if (l1wbl) print("GPGPU-Sim uArch: WARNING ** %llu L1 write-backs lost to a full injection queue\n",
+                     (unsigned long long)l1wbl);
+    print("gpgpu_n_regfile_reads = %llu\n", (unsigned long long)rfr);
+    print("gpgpu_n_regfile_writes = %llu\n", (unsigned long long)rfw);
+    print("gpgpu_n_completed_cta = %llu\n", (unsigned long long)ctas);
+    print("gpgpu_n_completed_warps = %llu\n", (unsigned long long)warps);
+    print("gpgpu_sm_active_cycles = %llu\n", (unsigned long long)act);
+    print("gpgpu_sm_issue_busy_cycles = %llu\n", (unsigned long long)busyc);
+    print("gpgpu_avg_active_warps = %.4f\n", act ? (double)occ / (double)act : 0.0);
+    uint64_t l2cyc = 0, l2busy = 0, rop = 0, qocc = 0, icst = 0, pre = 0, evd = 0;
+    for (auto& m : mem) {
+      l2cyc += m.l2_cycles;
+      l2busy += m.l2_busy;
+      rop += m.rop_occ;
+      qocc += m.dram_q_occ;
+      icst += m.icnt_stall;
+      pre += m.dram_pre;
+      evd += m.l2_evict_dirty;
+    }
+    print("gpu_stall_dramfull = %llu\n", (unsigned long long)(l2[L2T_RD][L2O_RES_FAIL] + l2[L2T_WR][L2O_RES_FAIL] +
+                                                              l2[L2T_ATOM][L2O_RES_FAIL]));
+    print("gpu_stall_icnt2sh = %llu\n", (unsigned long long)icst);
+    print("L2_cache_dirty_evictions = %llu\n", (unsigned long long)evd);
+    print("L2_busy_rate = %.4f\n", l2cyc ? (double)l2busy / (double)l2cyc : 0.0);
+    print("avg_rop_queue_occupancy = %.4f\n", l2cyc ? (double)rop / (double)l2cyc : 0.0);
+    print("avg_dram_sched_queue_occupancy = %.4f\n", dram_cyc ? (double)qocc / (double)dram_cyc : 0.0);
+    print("total dram precharges = %llu\n", (unsigned long long)pre);
+    print("dram_row_buffer_locality = %.4f\n",
+          (dram_rd + dram_wr) ? 1.0 - (double)dram_act / (double)(dram_rd + dram_wr) : 0.0);
+  }
   uint64_t pk_out = 0, pk_in = 0;
   for (auto& s : sm) {
     pk_out += s.pkts_out;

@@ -47,7 +47,7 @@ constexpr int kMaxSubPerCh = 2;
 constexpr int kMaxSubTot = 128;    // L2 sub-partitions (interconnect destinations)
 constexpr int kMaxSmTot = 512;     // simulated SMs
 
-enum SchedPolicy : uint8_t { SCHED_LRR = 0, SCHED_GTO, SCHED_OLDEST, SCHED_RRR, SCHED_TWO_LEVEL };
+enum SchedPolicy : uint8_t { SCHED_LRR = 0, SCHED_GTO, SCHED_OLDEST, SCHED_RRR, SCHED_TWO_LEVEL, SCHED_WARP_LIMITING };
 enum ReplPolicy : uint8_t { REPL_LRU = 0, REPL_FIFO };
 enum WritePolicy : uint8_t { WP_READ_ONLY = 0, WP_WRITE_BACK, WP_WRITE_THROUGH, WP_WRITE_EVICT, WP_LOCAL_WB_GLOBAL_WT };
 enum SetIndexFn : uint8_t { SIDX_LINEAR = 0, SIDX_FERMI, SIDX_HASH_IPOLY, SIDX_BITWISE_XOR, SIDX_CUSTOM };
@@ -132,6 +132,8 @@ struct SimCfg {
   uint32_t sub_core;
   uint32_t fetch_throughput;
   uint32_t max_issue_per_warp;
+  uint32_t dual_issue_diff;      // -gpgpu_dual_issue_diff_exec_units
+  uint32_t sched_param;          // two_level_active:<max active>, warp_limiting:<prio>:<warps>
   // ---- execution ----
   uint32_t unit_count[U_COUNT];   // total units of each type per SM (0 = absent)
   uint32_t id_oc_width[U_COUNT];  // ID_OC pipeline register slots per type

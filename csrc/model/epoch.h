@@ -97,7 +97,10 @@ SIM_HDI void sm_kernel_init(SMState& s, const SmCtx& x, SmKernel& ks, uint64_t s
   ks.ready_cycle = start + x.cfg->kernel_launch_latency + (uint64_t)x.cfg->tb_launch_latency * k.n_cta;
   s.kernel_cta_slots = k.cta_per_sm;
   if (flush_l1) {
-    P::each(kMaxL1Lines, [&](int i) { s.l1[i].valid = 0; });
+    P::each(kMaxL1Lines, [&](int i) {
+      s.l1[i].valid = 0;
+      s.l1[i].dirty = 0;
+    });
     P::sync();
   }
 }

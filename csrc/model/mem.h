@@ -274,19 +274,65 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
       if (way >= 0) sp.l2[set * g.assoc + way].valid |= p.sectors;
       trace(3);
     } else {
+      // write-back L2 (reference data_cache wr_hit_wb / wr_miss_*,
+      // gpu-cache.cc:1229-1599): a hit, or any write-allocate miss, makes
+      // the sectors dirty; only whole-sector writes are readable at once
+      // (lazy fetch on read); 'N' sends a miss to DRAM without allocating
+      const uint8_t have = way >= 0 ? sp.l2[set * g.assoc + way].valid : (uint8_t)0;
+      const bool hit = way >= 0 && (have & p.sectors) == p.sectors;
+      const uint32_t bytes = p.size > 8 ? p.size - 8u : 0u;
+      const bool full = bytes >= 32u * (uint32_t)popc64(p.sectors);
+      const uint8_t wa = g.walloc;
+      if (!hit && wa == 'N') {
+        const uint32_t n = (uint32_t)popc64(p.sectors);
+        if (!l2dram_can(ch, sp, c, n)) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
+        for (uint32_t s2 = 0; s2 < 4; ++s2)
+          if (p.sectors >> s2 & 1u) l2dram_push(ch, sp, c, sub, p.addr, s2, true, now_fs);
+        sp.st.l2[stype][L2O_MISS]++;
+        trace(1);
+        reply_push(sp, P_WR_ACK, p, p.sectors);
+        return true;
+      }
+      // fetch-on-write ('F', partial sectors) and naive ('W') read the
+      // written sectors that are not yet readable
+      const bool fetch = !hit && (wa == 'W' || (wa == 'F' && !full));
+      int mi = -1, mfree = 0;
+      uint8_t rd = 0;
+      const int nm = (int)amin<uint32_t>(g.mshr_entries, kMaxL2Mshr);
+      if (fetch) {
+        mi = P::find_first(nm, [&](int i) -> bool { return sp.mshr[i].valid && sp.mshr[i].line == p.addr; });
+        if (mi < 0) mfree = P::find_first(nm, [&](int i) -> bool { return !sp.mshr[i].valid; });
+        rd = p.sectors & (uint8_t)~have;
+        if (mi >= 0) rd &= (uint8_t)~sp.mshr[mi].requested;
+        if (mfree < 0 || !l2dram_can(ch, sp, c, (uint32_t)popc64(rd))) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
+      }
       if (way < 0) {
         way = l2_alloc<P>(ch, sp, c, sub, set, p.addr, now_fs);
         if (way < 0) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
-        sp.st.l2[stype][L2O_MISS]++;
-        trace(1);
-      } else {
+      }
+      if (hit) {
         sp.st.l2[stype][L2O_HIT]++;
         trace(0);
+      } else {
+        sp.st.l2[stype][L2O_MISS]++;
+        trace(1);
       }
       L2Line& L = sp.l2[set * g.assoc + way];
-      L.valid |= p.sectors;
+      if (full && !fetch) L.valid |= p.sectors;
       L.dirty |= p.sectors;
       if (g.repl == REPL_LRU) L.lru = ++sp.l2_stamp;
+      if (fetch && rd) {
+        if (mi < 0) {
+          mi = mfree;
+          sp.mshr[mi].valid = 1;
+          sp.mshr[mi].line = p.addr;
+          sp.mshr[mi].requested = 0;
+          sp.mshr[mi].merges = 0;
+        }
+        sp.mshr[mi].requested |= rd;
+        for (uint32_t s2 = 0; s2 < 4; ++s2)
+          if (rd >> s2 & 1u) l2dram_push(ch, sp, c, sub, p.addr, s2, false, now_fs);
+      }
     }
     reply_push(sp, P_WR_ACK, p, p.sectors);
     return true;

@@ -73,8 +73,9 @@ SIM_HDI uint64_t idoc_pack(uint32_t warp, uint32_t slot, uint32_t age) {
 struct L1Line {
   uint64_t tag;      // line address
   uint32_t lru;      // last-use / insertion stamp
-  uint8_t valid;     // sector mask
-  uint8_t pad[3];
+  uint8_t valid;     // sector mask (readable sectors)
+  uint8_t dirty;     // sector mask (write-back data not yet written below)
+  uint8_t pad[2];
 };
 
 struct L1Mshr {
@@ -136,6 +137,9 @@ struct SMStats {
   uint64_t mf_lat_sum, mf_lat_n, mf_lat_max;
   uint64_t mf_lat_hist[16];    // log2 buckets: [2^i, 2^(i+1)) cycles
   uint64_t il1[4];             // instruction cache: hit, miss, mshr (pending) hit, reservation fail
+  uint64_t dual_issued;        // second instructions issued in the same cycle by one warp
+  uint64_t l1_wb;              // dirty L1 lines written back on eviction
+  uint64_t l1_wb_lost;         // write-backs dropped with the injection queue full (must stay 0)
 };
 enum IL1Out : uint8_t { IL1_HIT = 0, IL1_MISS, IL1_MSHR_HIT, IL1_RES_FAIL };
 
@@ -300,6 +304,13 @@ SIM_HDI bool sm_can_send(const S& s, const SimCfg& c) {
   return s.outq_n < (uint32_t)kOutQ && s.outstanding + s.outq_n < c.icnt_out_limit;
 }
 template <class S>
+SIM_HDI bool sm_can_send_n(const S& s, const SimCfg& c, uint32_t n) {
+  return s.outq_n + n <= (uint32_t)kOutQ && s.outstanding + s.outq_n + n <= c.icnt_out_limit;
+}
+// write-back packets of evicted dirty L1 sectors carry this tag: their
+// acknowledgement retires no warp store
+constexpr uint32_t kTagL1Writeback = 0x20000000u;
+template <class S>
 SIM_HDI void sm_send(S& s, const SimCfg& c, uint8_t type, uint64_t line, uint8_t sectors,
                      uint16_t bytes, uint32_t tag) {
   AddrTlx t = addr_decode(c, line);
@@ -439,6 +450,27 @@ SIM_HDI int l1_victim(const S& s, const CacheGeom& g, uint32_t set) {
   return v;
 }
 
+// evict L1 line `idx`: dirty (write-back) sectors go below (reference
+// data_cache eviction write-back, gpu-cache.cc:1372-1386).  With the
+// injection queue full the write-back is counted as lost instead.
+template <class P, class S>
+SIM_HDI void l1_evict(S& s, const SimCfg& c, uint32_t idx) {
+  L1Line& V = s.l1[idx];
+  const uint8_t d = P::uni(V.dirty);
+  if (V.valid | d) {
+    if (d) {
+      if (s.outq_n < (uint32_t)kOutQ) {
+        sm_send(s, c, P_WR, P::uni(V.tag), d, (uint16_t)(32 * popc64(d)), kTagL1Writeback);
+        s.sadd(SK(l1_wb), 1);
+      } else {
+        s.sadd(SK(l1_wb_lost), 1);
+      }
+    }
+  }
+  V.valid = 0;
+  V.dirty = 0;
+}
+
 // fill sectors of a line into L1 (allocate-on-fill) and wake waiters
 template <class P, class S>
 SIM_HDI void l1_fill(S& s, const SmCtx& x, uint64_t line, uint8_t sectors, uint64_t now) {
@@ -449,9 +481,11 @@ SIM_HDI void l1_fill(S& s, const SmCtx& x, uint64_t line, uint8_t sectors, uint6
     int w = l1_find<P>(s, g, set, line);
     if (w < 0) {
       w = l1_victim<P>(s, g, set);
+      l1_evict<P>(s, c, set * g.assoc + w);
       L1Line& L = s.l1[set * g.assoc + w];
       L.tag = line;
       L.valid = 0;
+      L.dirty = 0;
       L.lru = ++s.l1_stamp;
     }
     L1Line& L = s.l1[set * g.assoc + w];
@@ -574,8 +608,10 @@ SIM_HDI void sm_receive(S& s, const SmCtx& x, uint64_t now) {
   s.sadd(SK(pkts_in), 1);
   s.sadd(SK(bytes_in), q.size);
   if (q.type == P_WR_ACK) {
-    uint32_t w = q.tag & 0xff;
-    s.w_stores[w]--;
+    if (!(q.tag & kTagL1Writeback)) {
+      uint32_t w = q.tag & 0xff;
+      s.w_stores[w]--;
+    }
     s.last_progress = now;
   } else if ((q.tag & 0xc0000000u) == 0x40000000u) {  // instruction-cache fill
     il1_fill<P>(s, c, q.addr);
@@ -634,15 +670,95 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
       }
       s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_HIT), 1);
     } else if (is_store) {
-      if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
-      sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
-      s.w_stores[w]++;
-      if (!bypass && g.wpolicy == WP_WRITE_EVICT) {
-        uint32_t set = cache_set_index(g, a.line);
+      // write policy (reference data_cache wr_hit_* / wr_miss_*,
+      // gpu-cache.cc:1229-1599); 'L' = write-back for local, write-evict for
+      // global data (wr_hit_global_we_local_wb)
+      uint8_t pol = g.wpolicy;
+      if (pol == WP_LOCAL_WB_GLOBAL_WT) pol = in.space == S_LOCAL ? WP_WRITE_BACK : WP_WRITE_EVICT;
+      if (bypass || pol == WP_READ_ONLY) {
+        if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+        sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
+        s.w_stores[w]++;
+        s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_BYPASS), 1);
+      } else {
+        const uint32_t set = cache_set_index(g, a.line);
         int way = l1_find<P>(s, g, set, a.line);
-        if (way >= 0) s.l1[set * g.assoc + way].valid &= (uint8_t)~a.sectors;
+        const uint8_t have = way >= 0 ? P::uni(s.l1[set * g.assoc + way].valid) : (uint8_t)0;
+        const bool hit = way >= 0 && (have & a.sectors) == a.sectors;
+        // a write covering whole sectors leaves them readable (lazy / fetch-on-write)
+        const bool full = g.sectored ? a.bytes >= 32u * (uint32_t)popc64(a.sectors) : a.bytes >= g.line;
+        const bool wb = pol == WP_WRITE_BACK;
+        const uint8_t wa = g.walloc;
+        if (hit) {
+          if (wb) {
+            // write-back hit: the line absorbs the store, nothing goes below
+            L1Line& L = s.l1[set * g.assoc + way];
+            L.dirty |= a.sectors;
+            if (g.repl == REPL_LRU) L.lru = ++s.l1_stamp;
+          } else {
+            if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+            sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
+            s.w_stores[w]++;
+            L1Line& L = s.l1[set * g.assoc + way];
+            if (pol == WP_WRITE_EVICT) L.valid &= (uint8_t)~a.sectors;
+            else if (g.repl == REPL_LRU) L.lru = ++s.l1_stamp;
+          }
+          s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_HIT), 1);
+        } else if (wa == 'N' || pol == WP_WRITE_EVICT) {
+          // no write-allocate: straight to the L2
+          if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+          sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
+          s.w_stores[w]++;
+          if (way >= 0 && pol == WP_WRITE_EVICT) s.l1[set * g.assoc + way].valid &= (uint8_t)~a.sectors;
+          s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_MISS), 1);
+        } else {
+          // write-allocate: lazy fetch on read ('L'), fetch-on-write ('F'),
+          // naive ('W': write and read the line)
+          const bool fetch = wa == 'W' || (wa == 'F' && !full);
+          const bool send_wr = !wb || wa == 'W';
+          int mi = -1;
+          if (fetch) mi = P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return s.mshr[i].valid && s.mshr[i].line == a.line; });
+          const int mfree = fetch && mi < 0 ? P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return !s.mshr[i].valid; }) : 0;
+          const uint32_t need = (send_wr ? 1u : 0u) + (fetch ? 1u : 0u) + 1u;  // + a possible dirty victim
+          if (!sm_can_send_n(s, c, need) || mfree < 0) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+          if (send_wr) {
+            sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
+            s.w_stores[w]++;
+          }
+          if (way < 0) {
+            way = l1_victim<P>(s, g, set);
+            l1_evict<P>(s, c, set * g.assoc + way);
+            L1Line& L = s.l1[set * g.assoc + way];
+            L.tag = a.line;
+            L.valid = 0;
+            L.dirty = 0;
+            L.lru = ++s.l1_stamp;
+          }
+          L1Line& L = s.l1[set * g.assoc + way];
+          if (full && !fetch) L.valid |= a.sectors;
+          if (wb) L.dirty |= a.sectors;
+          if (g.repl == REPL_LRU) L.lru = ++s.l1_stamp;
+          if (fetch) {
+            // read the written line's missing sectors (no waiter: the fill
+            // only makes them readable)
+            const uint8_t want = a.sectors & (uint8_t)~P::uni(L.valid);
+            if (mi < 0) {
+              mi = mfree;
+              s.mshr[mi].valid = 1;
+              s.mshr[mi].line = a.line;
+              s.mshr[mi].requested = 0;
+              s.mshr[mi].merges = 0;
+              s.mshr[mi].t_issue = (uint32_t)now;
+            }
+            const uint8_t req = want & (uint8_t)~P::uni(s.mshr[mi].requested);
+            if (req) {
+              s.mshr[mi].requested |= req;
+              sm_send(s, c, P_RD, a.line, req, (uint16_t)(32 * popc64(req)), (uint32_t)mi);
+            }
+          }
+          s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_MISS), 1);
+        }
       }
-      s.sadd(SK(l1) + (stype) * L1O_COUNT + (bypass ? L1O_BYPASS : L1O_MISS), 1);
     } else if (bypass) {
       if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
       uint32_t tag = 0x80000000u | ((uint32_t)uslot << 8) | w;
@@ -762,6 +878,7 @@ SIM_HDI void sm_read_operands(S& s, const SimCfg& c) {
         s.sadd(SK(rf_reads), got);
         if (nr == 0) rmask &= ~(1u << i);
       }
+      if (nr) s.sadd(SK(oc_bank_conflicts), nr);  // reads left waiting on a busy bank this round
     }
     s.oc_read_mask = rmask;
   }
@@ -904,6 +1021,108 @@ SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, const TInst* insts, int
   return warp_can_issue_i(s, c, w, in, nsched, idoc_busy);
 }
 
+// issue one instruction `in` (trace index hidx) of warp w from scheduler sc;
+// returns its execution unit, or -1 for the kinds handled at issue (EXIT,
+// barrier, fence, waitcnt, NOP)
+template <class P, class S>
+SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32_t w, const TInst& in,
+                         uint32_t hidx) {
+  const SimCfg& c = *x.cfg;
+  const KernelDesc& k = *x.k;
+  if (trace_sm_on(c, TS_WARP_SCHEDULER, s.id))
+    P::one([&] { trace_put(c, s.id, now, EV_ISSUE, (uint16_t)w, (uint64_t)in.pc | (uint64_t)in.opcode << 32); });
+  s.w_head[w] = hidx + 1;
+  s.w_ibuf[w] = (uint8_t)(P::uni((uint8_t)s.w_ibuf[w]) - 1);
+  // stats: instruction counts at issue (reference counts active threads,
+  // shader.cc:1911)
+  s.sadd(SK(warp_insn), 1);
+  s.sadd(SK(thread_insn), (uint64_t)popc64(in.mask));
+  s.sadd(SK(cls_insn) + (in.cls < OC_COUNT ? in.cls : OC_ALU), 1);
+  s.last_progress = now;
+  const uint32_t cta = P::uni((uint8_t)s.w_cta[w]);
+  if (in.cls == OC_EXIT) {
+    // lanes retire; the warp ends only when EXIT is its last instruction
+    // (reference checkExecutionStatusAndUpdate, trace_driven.cc:588-606)
+    if (hidx + 1 >= P::uni((uint32_t)s.w_end[w])) {
+      s.w_flags[w] |= WF_EXITING;
+      s.cta_nexit[cta]++;
+      sm_barrier_check<P>(s, cta, k);
+    }
+    return -1;
+  }
+  if (in.cls == OC_BARRIER) {
+    s.w_flags[w] |= WF_BARRIER;
+    s.cta_bar[cta]++;
+    sm_barrier_check<P>(s, cta, k);
+    return -1;
+  }
+  if (in.cls == OC_MEMBAR) {
+    if (s.w_stores[w]) {
+      s.w_flags[w] |= WF_MEMBAR;
+      s.n_wait_flags++;
+    }
+    return -1;
+  }
+  if (in.flags & F_WAITCNT) {
+    if (s.w_stores[w] || s.w_loads[w]) {
+      s.w_flags[w] |= WF_WAITCNT;
+      s.n_wait_flags++;
+    }
+    return -1;
+  }
+  if (in.cls == OC_NOP) return -1;
+  const uint32_t u = unit_of(c, in.cls);
+  const uint32_t kk = sc * U_COUNT + u;
+  TInst ri = in;
+  uint32_t lslot = 0xff;
+  s.w_inflight[w]++;
+  if (in.cls == OC_LOAD) {
+    // allocate a load slot; scoreboard reserves destination registers
+    uint8_t used = P::uni((uint8_t)s.w_slot_used[w]);
+    uint32_t sl = (uint32_t)ffs64((uint64_t)(uint8_t)~used);
+    s.w_slot_used[w] = (uint8_t)(used | (1u << sl));
+    s.w_loads[w]++;
+    uint32_t nacc = (in.space == S_SHARED) ? 1u : (uint32_t)in.width;
+    if (nacc == 0) nacc = 1;
+    s.w_slot_pend[w][sl] = (uint16_t)nacc;
+    s.w_slot_dst[w][sl][0] = in.dst[0];
+    s.w_slot_dst[w][sl][1] = in.dst[1];
+    lslot = sl;
+    if (in.space != S_SHARED && in.width == 0) {
+      // memory instruction without any active access: completes via ring
+      s.w_slot_pend[w][sl] = 1;
+      ri.space = S_SHARED;
+      ri.width = 1;
+    }
+  } else if (in.cls == OC_STORE && in.space != S_SHARED && in.width == 0) {
+    ri.space = S_SHARED;
+    ri.width = 1;
+  }
+  s.idoc_inst[kk] = ri;
+  s.idoc_meta[kk] = idoc_pack(w, lslot, ++s.age_ctr);
+  s.idoc_mask |= 1ull << kk;
+  sbs(s.w_sb, w, in.dst[0]);
+  sbs(s.w_sb, w, in.dst[1]);
+  return (int)u;
+}
+
+// does `in` read a register that an in-flight load of warp w will write (the
+// reference scoreboard's long-operation test, Scoreboard::islongop)
+template <class S>
+SIM_HDI bool waits_long_op(const S& s, int w, const TInst& in) {
+  const uint8_t used = s.w_slot_used[w];
+  for (int sl = 0; sl < kLoadSlots; ++sl) {
+    if (!(used >> sl & 1u)) continue;
+    for (int d = 0; d < 2; ++d) {
+      const uint8_t r = s.w_slot_dst[w][sl][d];
+      if (!r) continue;
+      for (int j = 0; j < 5; ++j)
+        if (in.src[j] == r) return true;
+    }
+  }
+  return false;
+}
+
 template <class P, class S>
 SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
@@ -920,21 +1139,57 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   // readiness of every warp (lane-parallel)
   const uint64_t live = P::uni(s.live_mask);
   uint64_t ready = P::ballot_m(live, [&](int w) -> bool { return warp_can_issue_i(s, c, w, head.self(w), nsched, idoc_busy); });
+  // warps parked at a barrier / fence / exit (the reference's waiting()),
+  // plus for the two-level scheduler those whose next instruction waits on
+  // a long (memory) operation
+  uint64_t waiting = 0;
+  if (c.sched_policy == SCHED_WARP_LIMITING || c.sched_policy == SCHED_TWO_LEVEL)
+    waiting = P::ballot_m(live, [&](int w) -> bool {
+      const uint8_t f = s.w_flags[w];
+      if (f & (WF_EXITING | WF_BARRIER | WF_MEMBAR | WF_WAITCNT)) return true;
+      return c.sched_policy == SCHED_TWO_LEVEL && s.w_ibuf[w] && waits_long_op(s, w, head.self(w));
+    });
   P::prof(29);
   bool issued_any = false;
   for (uint32_t sc = 0; sc < nsched; ++sc) {
     // warps of this scheduler
     const uint64_t mine = c.sched_mask[sc];
     uint64_t cand = ready & mine;
+    const uint32_t last = P::uni((uint32_t)s.sched_last[sc]);
+    if (c.sched_policy == SCHED_WARP_LIMITING && cand) {
+      // swl_scheduler::order_warps (shader.cc:1686-1700): only the
+      // sched_param oldest non-waiting warps (and the greedy one) compete
+      uint64_t pool = live & mine & ~waiting, lim = 0;
+      for (uint32_t i = 0; i < c.sched_param && pool; ++i) {
+        const int o = P::argmin(nw, [&](int w) -> uint64_t {
+          return (pool >> w & 1ull) ? ((uint64_t)s.w_age[w] << 8 | (uint64_t)w) : ~0ull;
+        });
+        if (o < 0) break;
+        lim |= 1ull << o;
+        pool &= ~(1ull << o);
+      }
+      if (last < (uint32_t)nw) lim |= 1ull << last;
+      cand &= lim;
+    } else if (c.sched_policy == SCHED_TWO_LEVEL && cand) {
+      // two_level_active_scheduler (shader.cc:1599-1660): warps waiting on
+      // long operations are demoted; the active set holds at most
+      // sched_param warps, refilled in warp order; LRR inside it
+      uint64_t pool = live & mine & ~waiting, act = 0;
+      for (uint32_t i = 0; i < c.sched_param && pool; ++i) {
+        const uint64_t b = pool & (~pool + 1);
+        act |= b;
+        pool &= ~b;
+      }
+      cand &= act;
+    }
     if (!cand) {
       if (live & mine) s.sadd(SK(issue_stall_idle), 1);
       continue;
     }
     int pick = -1;
-    uint32_t last = P::uni((uint32_t)s.sched_last[sc]);
     switch (c.sched_policy) {
       case SCHED_GTO:
-      case SCHED_TWO_LEVEL:
+      case SCHED_WARP_LIMITING:
         if (last < (uint32_t)nw && (cand >> last & 1ull)) { pick = (int)last; break; }
         [[fallthrough]];
       case SCHED_OLDEST:
@@ -948,7 +1203,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
         pick = (int)((ffs64(r) + start) % (uint32_t)nw);
         break;
       }
-      default: {  // LRR: first ready warp after the last issued one
+      default: {  // LRR (and the two-level inner level): first ready warp after the last issued one
         uint32_t start = (last + 1) % (uint32_t)nw;
         uint64_t r = rotr64(cand, start, (unsigned)nw);
         pick = (int)((ffs64(r) + start) % (uint32_t)nw);
@@ -958,82 +1213,21 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
     const uint32_t w = P::uni((uint32_t)pick);
     s.sched_last[sc] = w;
     const uint32_t hidx = P::uni((uint32_t)s.w_head[w]);
-    const TInst in = head.at((int)w);
-    if (trace_sm_on(c, TS_WARP_SCHEDULER, s.id))
-      P::one([&] { trace_put(c, s.id, now, EV_ISSUE, (uint16_t)w, (uint64_t)in.pc | (uint64_t)in.opcode << 32); });
-    s.w_head[w] = hidx + 1;
-    s.w_ibuf[w] = (uint8_t)(P::uni((uint8_t)s.w_ibuf[w]) - 1);
+    const int u1 = sm_issue_one<P>(s, x, now, sc, w, head.at((int)w), hidx);
     issued_any = true;
-    // stats: instruction counts at issue (reference counts active threads,
-    // shader.cc:1911)
-    s.sadd(SK(warp_insn), 1);
-    s.sadd(SK(thread_insn), (uint64_t)popc64(in.mask));
-    s.sadd(SK(cls_insn) + (in.cls < OC_COUNT ? in.cls : OC_ALU), 1);
-    s.last_progress = now;
-    uint32_t cta = P::uni((uint8_t)s.w_cta[w]);
-    if (in.cls == OC_EXIT) {
-      // lanes retire; the warp ends only when EXIT is its last instruction
-      // (reference checkExecutionStatusAndUpdate, trace_driven.cc:588-606)
-      if (hidx + 1 >= P::uni((uint32_t)s.w_end[w])) {
-        s.w_flags[w] |= WF_EXITING;
-        s.cta_nexit[cta]++;
-        sm_barrier_check<P>(s, cta, k);
+    // dual issue (reference scheduler_unit::cycle, shader.cc:1249-1556): the
+    // warp's next buffered instruction issues in the same cycle if it is
+    // ready and, with -gpgpu_dual_issue_diff_exec_units, uses another unit
+    if (c.max_issue_per_warp > 1 && u1 >= 0 && P::uni((uint8_t)s.w_ibuf[w])) {
+      const TInst in2 = P::uni(k.insts[hidx + 1]);
+      const bool special = in2.cls == OC_EXIT || in2.cls == OC_BARRIER || in2.cls == OC_MEMBAR ||
+                           in2.cls == OC_NOP || (in2.flags & F_WAITCNT);
+      if (!special && (!c.dual_issue_diff || unit_of(c, in2.cls) != (uint32_t)u1) &&
+          warp_can_issue_i(s, c, (int)w, in2, nsched, P::uni(s.idoc_mask))) {
+        sm_issue_one<P>(s, x, now, sc, w, in2, hidx + 1);
+        s.sadd(SK(dual_issued), 1);
       }
-      continue;
     }
-    if (in.cls == OC_BARRIER) {
-      s.w_flags[w] |= WF_BARRIER;
-      s.cta_bar[cta]++;
-      sm_barrier_check<P>(s, cta, k);
-      continue;
-    }
-    if (in.cls == OC_MEMBAR) {
-      if (s.w_stores[w]) {
-        s.w_flags[w] |= WF_MEMBAR;
-        s.n_wait_flags++;
-      }
-      continue;
-    }
-    if (in.flags & F_WAITCNT) {
-      if (s.w_stores[w] || s.w_loads[w]) {
-        s.w_flags[w] |= WF_WAITCNT;
-        s.n_wait_flags++;
-      }
-      continue;
-    }
-    if (in.cls == OC_NOP) continue;
-    const uint32_t u = unit_of(c, in.cls);
-    const uint32_t k = sc * U_COUNT + u;
-    TInst ri = in;
-    uint32_t lslot = 0xff;
-    s.w_inflight[w]++;
-    if (in.cls == OC_LOAD) {
-      // allocate a load slot; scoreboard reserves destination registers
-      uint8_t used = P::uni((uint8_t)s.w_slot_used[w]);
-      uint32_t sl = (uint32_t)ffs64((uint64_t)(uint8_t)~used);
-      s.w_slot_used[w] = (uint8_t)(used | (1u << sl));
-      s.w_loads[w]++;
-      uint32_t nacc = (in.space == S_SHARED) ? 1u : (uint32_t)in.width;
-      if (nacc == 0) nacc = 1;
-      s.w_slot_pend[w][sl] = (uint16_t)nacc;
-      s.w_slot_dst[w][sl][0] = in.dst[0];
-      s.w_slot_dst[w][sl][1] = in.dst[1];
-      lslot = sl;
-      if (in.space != S_SHARED && in.width == 0) {
-        // memory instruction without any active access: completes via ring
-        s.w_slot_pend[w][sl] = 1;
-        ri.space = S_SHARED;
-        ri.width = 1;
-      }
-    } else if (in.cls == OC_STORE && in.space != S_SHARED && in.width == 0) {
-      ri.space = S_SHARED;
-      ri.width = 1;
-    }
-    s.idoc_inst[k] = ri;
-    s.idoc_meta[k] = idoc_pack(w, lslot, ++s.age_ctr);
-    s.idoc_mask |= 1ull << k;
-    sbs(s.w_sb, w, in.dst[0]);
-    sbs(s.w_sb, w, in.dst[1]);
   }
   if (issued_any) s.sadd(SK(busy_cycles), 1);
 }
