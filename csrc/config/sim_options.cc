@@ -819,6 +819,8 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.kernel_launch_latency = (uint32_t)std::max<long long>(0, r.geti("-gpgpu_kernel_launch_latency"));
   c.tb_launch_latency = (uint32_t)std::max<long long>(0, r.geti("-gpgpu_TB_launch_latency"));
   c.deadlock_window = r.getb("-gpgpu_deadlock_detect") ? 50000 : 0;
+  c.max_insn = (uint64_t)std::max<long long>(0, r.geti("-gpgpu_max_insn"));
+  c.max_completed_cta = (uint32_t)std::max<long long>(0, r.geti("-gpgpu_max_completed_cta"));
   // interconnect model
   c.icnt_mode = 2;
   if (r.geti("-network_mode") == 1) {

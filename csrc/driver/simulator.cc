@@ -119,7 +119,7 @@ int Simulator::run() {
       print("GPGPU-Sim: ** break due to reaching the maximum cycles (or instructions) **\n");
       break;
     }
-    if (dopt_.max_insn && (int64_t)tot_insn_ >= dopt_.max_insn) {
+    if ((dopt_.max_insn && (int64_t)tot_insn_ >= dopt_.max_insn) || cap_hit_) {
       print("GPGPU-Sim: ** break due to reaching the maximum cycles (or instructions) **\n");
       break;
     }
@@ -319,6 +319,16 @@ void Simulator::do_kernel(const Command& c) {
   KernelDesc kd{};
   kd.uid = next_uid_++;
   kd.n_cta = rk.n_cta;
+  kd.stop_when_issued = 0;
+  if (dopt_.max_cta > 0) {
+    // -gpgpu_max_cta: CTAs past the cap are never issued, and the run ends as
+    // soon as the cap is reached (reference gpgpu_sim::active, gpu-sim.cc:1086)
+    const uint64_t left = (uint64_t)dopt_.max_cta > tot_cta_ ? (uint64_t)dopt_.max_cta - tot_cta_ : 0;
+    if (left <= kd.n_cta) {
+      kd.n_cta = (uint32_t)left;
+      kd.stop_when_issued = 1;
+    }
+  }
   kd.warps_per_cta = rk.warps_per_cta;
   kd.threads_per_cta = ks.threads_per_cta;
   kd.shmem_per_cta = rk.h.shmem;
@@ -389,6 +399,7 @@ void Simulator::do_kernel(const Command& c) {
   r.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   r.deadlock = rr.deadlock;
   r.epochs = rr.epochs;
+  if (rr.cap) cap_hit_ = true;
   tot_cycle_ = eng_->now();
   tot_insn_ += r.insn;
   tot_warp_insn_ += r.warp_insn;
@@ -452,6 +463,8 @@ RunResult Simulator::run_sampled(uint64_t start, const RunLimits& lim0, const st
     tot.end_cycle = r.end_cycle;
     tot.done = r.done;
     tot.deadlock = r.deadlock;
+    tot.cap = r.cap;
+    tot.hit_limit = r.cap;
     const uint64_t now = eng_->now();
     eng_->stats(sm1, m1);
     stat_delta(sm1, sm0, dsm);
@@ -483,7 +496,7 @@ RunResult Simulator::run_sampled(uint64_t start, const RunLimits& lim0, const st
     sm0.swap(sm1);
     m0.swap(m1);
     t_prev = now;
-    if (r.done || r.deadlock) break;
+    if (r.done || r.deadlock || r.cap) break;
     if (lim0.max_cycle && now >= lim0.max_cycle) {
       tot.hit_limit = true;
       break;

@@ -124,6 +124,7 @@ class Simulator {
   uint32_t next_uid_ = 1;
   // currently loaded kernel (kept alive for the engine)
   std::unique_ptr<ReadyKernel> cur_kernel_;
+  bool cap_hit_ = false;  // a run cap (-gpgpu_max_insn / _max_cta / _max_completed_cta) stopped a kernel
 };
 
 }  // namespace asim

@@ -56,11 +56,12 @@ class CheckEngine final : public Engine {
       const RunResult rb = b_->run_kernel(start, flush_l1, l);
       total.epochs += ra.epochs;
       compare(ra, rb);
-      if (ra.done || ra.deadlock || !ra.hit_limit || final_cap) {
+      if (ra.done || ra.deadlock || !ra.hit_limit || final_cap || ra.cap) {
         total.end_cycle = ra.end_cycle;
         total.done = ra.done;
         total.deadlock = ra.deadlock;
         total.hit_limit = ra.hit_limit;
+        total.cap = ra.cap;
         return total;
       }
       resume = true;

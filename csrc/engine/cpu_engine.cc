@@ -164,7 +164,8 @@ class CpuEngine : public Engine {
         }
       }
       const uint32_t next_done = pub_->next_cta[cur] >= kd_.n_cta ? 1u : 0u;
-      EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, ready, next_done, epoch_, lim.max_cycle);
+      EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, ready, next_done, epoch_, lim.max_cycle,
+                                                kd_.stop_when_issued);
       ++epoch_;
       ++res.epochs;
       cycle_ = d.next_start;
@@ -174,6 +175,11 @@ class CpuEngine : public Engine {
       }
       if (d.deadlock) {
         res.deadlock = true;
+        break;
+      }
+      if (d.limit) {
+        res.hit_limit = true;
+        res.cap = true;
         break;
       }
       if ((lim.max_cycle && cycle_ >= lim.max_cycle) || (lim.max_epochs && res.epochs >= lim.max_epochs)) {

@@ -26,6 +26,7 @@ struct RunResult {
   bool done = false;
   bool deadlock = false;
   bool hit_limit = false;
+  bool cap = false;  // stopped by -gpgpu_max_insn / -gpgpu_max_cta / -gpgpu_max_completed_cta
 };
 
 class Engine {

@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   }
   uint64_t epoch = a.epoch0, cycle = a.cycle0;
   uint64_t t_work0 = a.ework ? __builtin_amdgcn_s_memtime() : 0;
-  uint32_t done = 0, dead = 0;
+  uint32_t done = 0, dead = 0, capped = 0;
   uint32_t n = 0;
   for (; n < a.max_epochs;) {
     const uint32_t cur = (uint32_t)(epoch & 1), prev = cur ^ 1u;
@@ -195,12 +195,14 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
       t_work0 = t_exit;
     }
     const uint32_t next_done = a.pub->next_cta[cur] >= kd.n_cta ? 1u : 0u;
-    EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, a.ready_cycle, next_done, epoch, a.max_cycle);
+    EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, a.ready_cycle, next_done, epoch, a.max_cycle,
+                                      kd.stop_when_issued);
     P::prof(28);
     ++epoch;
     cycle = P::uni(d.next_start);
     if (P::uni(d.done)) { done = 1; break; }
     if (P::uni(d.deadlock)) { dead = 1; break; }
+    if (P::uni(d.limit)) { capped = 1; break; }
     if (a.max_cycle && cycle >= a.max_cycle) break;
   }
   P::prof(31);  // launch_rest
@@ -213,6 +215,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   if (b == 0 && (threadIdx.x & 63) == 0) {
     a.ctl->done = done;
     a.ctl->deadlock = dead;
+    a.ctl->cap = capped;
     a.ctl->end_cycle = cycle;
     a.ctl->end_epoch = epoch;
     a.ctl->epochs_run = n;
@@ -410,6 +413,7 @@ class GpuEngine : public Engine {
       res.epochs += h_ctl_->epochs_run;
       if (h_ctl_->done) { res.done = true; break; }
       if (h_ctl_->deadlock) { res.deadlock = true; break; }
+      if (h_ctl_->cap) { res.hit_limit = true; res.cap = true; break; }
       if ((lim.max_cycle && cycle_ >= lim.max_cycle) || (lim.max_epochs && res.epochs >= lim.max_epochs)) {
         res.hit_limit = true;
         break;

@@ -16,7 +16,7 @@ struct GpuCtl {  // zeroed by hipMemsetAsync before every launch
   uint32_t error;             // barrier timeout / fault code
   uint32_t done;
   uint32_t deadlock;
-  uint32_t pad;
+  uint32_t cap;  // a run cap (-gpgpu_max_insn / _max_cta / _max_completed_cta) ended the launch
   uint64_t end_cycle;
   uint64_t end_epoch;
   uint64_t epochs_run;

@@ -29,6 +29,17 @@ struct WavePar {
   static __device__ __forceinline__ uint32_t red_sum(uint32_t v) {
     return wave_reduce(v, [](uint32_t a, uint32_t b) { return a + b; });
   }
+  static __device__ __forceinline__ uint64_t red_sum64(uint64_t v) {
+    // lane partials of 64-bit sums: reduce the two halves as 32-bit sums of
+    // 16-bit limbs so no carry is lost (64 lanes x 2^16 fits in 32 bits)
+    uint64_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t limb = (uint32_t)(v >> (16 * k)) & 0xffffu;
+      r += (uint64_t)wave_reduce(limb, [](uint32_t a, uint32_t b) { return a + b; }) << (16 * k);
+    }
+    return r;
+  }
   template <bool kMax>
   static __device__ __forceinline__ uint64_t red64(uint64_t v) {
     uint32_t h = (uint32_t)(v >> 32), l = (uint32_t)v;

@@ -212,6 +212,10 @@ struct SimCfg {
   uint32_t tb_launch_latency;
   // ---- misc ----
   uint32_t deadlock_window;
+  // run caps checked every epoch (-gpgpu_max_insn, -gpgpu_max_completed_cta)
+  uint64_t max_insn;
+  uint32_t max_completed_cta;
+  uint32_t pad_caps;
   uint32_t max_cycle_lo, max_cycle_hi;
   // ---- idealisations (reference -gpgpu_perfect_mem, perfect_memory_interface
   //      shader.h:2681; -gpgpu_simple_dram_model, l2cache.cc:235-303) ----

@@ -25,11 +25,14 @@ struct UnitPub {
                      // the first instant the unit can change state, or one of the
                      // packets it injected this epoch arrives (-sim_event_skip)
   uint64_t prog;     // SM: last progress cycle
+  uint64_t insn;     // SM: thread instructions issued so far (-gpgpu_max_insn)
   uint32_t req;      // SM: CTA slots it can accept next epoch
   uint32_t idle;     // SM: drained and kernel fully dispatched; channel: idle
   uint32_t drained;  // SM: holds no work (launch latency may be pending)
-  uint32_t pad;
+  uint32_t ctas;     // SM: CTAs completed so far (-gpgpu_max_completed_cta)
+  uint64_t pad;
 };
+static_assert(sizeof(UnitPub) == 48, "UnitPub layout");
 // epoch-boundary publications, double buffered by epoch parity
 struct EpochPub {
   UnitPub sm[2][kMaxSmTot];
@@ -46,7 +49,7 @@ struct EpochDecision {
   uint32_t done;        // kernel complete (all SMs idle)
   uint32_t all_idle;    // SMs and memory idle
   uint32_t deadlock;
-  uint32_t pad;
+  uint32_t limit;       // -gpgpu_max_insn / _max_completed_cta / _max_cta reached: stop
   uint64_t next_start;  // start cycle of the next epoch (after fast-forward)
 };
 
@@ -172,9 +175,11 @@ SIM_HDI void sm_publish(SMState& s, const SmCtx& x, const SmKernel& ks, EpochPub
   UnitPub u;
   u.next = nx;
   u.prog = s.last_progress;
+  u.insn = s.sget(SK(thread_insn));
   u.req = req;
   u.idle = idle;
   u.drained = sm_idle(s) ? 1u : 0u;
+  u.ctas = (uint32_t)s.sget(SK(ctas_done));
   u.pad = 0;
   P::one([&] {
     pub.sm[cur][s.id] = u;
@@ -207,9 +212,11 @@ SIM_HDI void chan_publish(ChanState& ch, const MemCtx& x, EpochPub& pub, uint32_
   UnitPub u;
   u.next = nx;
   u.prog = 0;
+  u.insn = 0;
   u.req = 0;
   u.idle = idle;
   u.drained = idle;
+  u.ctas = 0;
   u.pad = 0;
   P::one([&] { pub.ch[cur][ch.id] = u; });
 }
@@ -218,13 +225,15 @@ SIM_HDI void chan_publish(ChanState& ch, const MemCtx& x, EpochPub& pub, uint32_
 template <class P>
 SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_t cur, uint64_t t1,
                                    uint64_t ready_cycle, uint32_t next_cta_done, uint64_t epoch_idx,
-                                   uint64_t max_cycle) {
+                                   uint64_t max_cycle, uint32_t stop_when_issued = 0) {
   EpochDecision d;
   // one pass over every unit's record (one load per unit), then reductions
-  uint32_t nbusy = 0, undrained = 0, nreq = 0, cbusy = 0;
-  uint64_t sm_next = ~0ull, ch_next = ~0ull, prog = 0;
+  uint32_t nbusy = 0, undrained = 0, nreq = 0, cbusy = 0, ctas = 0;
+  uint64_t sm_next = ~0ull, ch_next = ~0ull, prog = 0, insn = 0;
   P::lane_loop((int)c.n_sm, [&](int j) {
     const UnitPub u = pub.sm[cur][j];
+    insn += u.insn;
+    ctas += u.ctas;
     nbusy += u.idle ? 0u : 1u;
     undrained += u.drained ? 0u : 1u;
     nreq += u.req ? 1u : 0u;
@@ -247,7 +256,12 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   d.all_idle = (nbusy == 0 && cbusy == 0) ? 1u : 0u;
   d.next_start = t1;
   d.deadlock = 0;
-  d.pad = 0;
+  // run caps checked while the kernel runs (reference gpgpu_sim::active,
+  // gpu-sim.cc:1071-1094): instructions, completed CTAs, issued CTAs
+  d.limit = 0;
+  if (c.max_insn && P::uni(P::red_sum64(insn)) >= c.max_insn) d.limit = 1;
+  if (c.max_completed_cta && P::uni(P::red_sum(ctas)) >= c.max_completed_cta) d.limit = 1;
+  if (stop_when_issued && next_cta_done) d.limit = 1;
   // fast-forward over the kernel launch latency when nothing is in flight
   if (!next_cta_done && cbusy == 0 && t1 < ready_cycle && undrained == 0) {
     uint64_t E = c.icnt_latency;

@@ -131,7 +131,7 @@ struct SMStats {
   uint64_t warps_done;
   uint64_t occupancy_acc;      // sum over cycles of live warps
   uint64_t mem_insn;
-  uint64_t power_acc[8];       // spare power-model counters
+  uint64_t power_acc[8];       // power-model counters (PwrCounter)
   // L1 miss round-trip latency (MSHR allocation -> last sector filled), the
   // reference's mem_latency_stat (mem_latency_stat.h:37, -gpgpu_memlatency_stat)
   uint64_t mf_lat_sum, mf_lat_n, mf_lat_max;
@@ -142,6 +142,8 @@ struct SMStats {
   uint64_t l1_wb_lost;         // write-backs dropped with the injection queue full (must stay 0)
 };
 enum IL1Out : uint8_t { IL1_HIT = 0, IL1_MISS, IL1_MSHR_HIT, IL1_RES_FAIL };
+// SMStats::power_acc slots
+enum PwrCounter : uint8_t { PWR_CONST_OPERAND = 0 };
 
 // per-SM kernel bookkeeping (replicated identically in every SM)
 struct SmKernel {
@@ -1038,6 +1040,9 @@ SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32
   s.sadd(SK(warp_insn), 1);
   s.sadd(SK(thread_insn), (uint64_t)popc64(in.mask));
   s.sadd(SK(cls_insn) + (in.cls < OC_COUNT ? in.cls : OC_ALU), 1);
+  // LDC / s_load: an ALU-timed instruction with a constant-cache operand
+  // (reference trace_driven.cc:255-261 keeps LDC an ALU op; shader.cc:3287)
+  if (in.space == S_CONST) s.sadd(SK(power_acc) + PWR_CONST_OPERAND, 1);
   s.last_progress = now;
   const uint32_t cta = P::uni((uint8_t)s.w_cta[w]);
   if (in.cls == OC_EXIT) {

@@ -140,6 +140,8 @@ struct KernelDesc {
   uint32_t block[3];
   uint32_t stream;
   uint32_t l1_sets, l1_assoc;  // adaptive L1 geometry chosen for this kernel
+  uint32_t stop_when_issued;   // cut to the -gpgpu_max_cta remainder: the run ends once all CTAs issued
+  uint32_t pad_k;
   uint64_t shmem_base;
   uint64_t local_base;
   uint64_t n_insts;

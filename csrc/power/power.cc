@@ -263,6 +263,9 @@ Activity PowerModel::activity_from_stats(const std::vector<SMStats>& dsm, const 
                      s.l1[L1T_LOCAL_R][L1O_MSHR_HIT] + s.l1[L1T_GLOBAL_R][L1O_BYPASS];
     a.a[PA_DC_WM] += s.l1[L1T_GLOBAL_W][L1O_MISS] + s.l1[L1T_LOCAL_W][L1O_MISS] + s.l1[L1T_GLOBAL_W][L1O_BYPASS] +
                      s.l1[L1T_ATOMIC][L1O_BYPASS];
+    a.a[PA_DC_WH] += s.l1[L1T_GLOBAL_W][L1O_HIT] + s.l1[L1T_LOCAL_W][L1O_HIT];
+    // constant-cache operand accesses (reference shader.cc:3287 inc_const_accesses)
+    a.a[PA_CC_H] += s.power_acc[PWR_CONST_OPERAND];
     a.a[PA_SHRD_ACC] += s.shmem_acc;
     a.a[PA_REG_RD] += s.rf_reads;
     a.a[PA_REG_WR] += s.rf_writes;

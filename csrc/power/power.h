@@ -9,8 +9,7 @@
 // (csrc/power/power.cc), so a power sample is a small linear model:
 //   P = constant + idle_sm * n_idle + static(category, lanes)
 //       + sum_i  base_nJ[i] * scale[i] * accesses[i] / t
-// which the GPU engine evaluates for all SMs x samples as one matrix
-// product (counters x coefficients) and the host evaluates per kernel.
+// evaluated on the host per sample from the engines' activity counters.
 #pragma once
 #include <map>
 #include <ostream>

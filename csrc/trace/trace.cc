@@ -124,7 +124,10 @@ OpInfo decode_sass(const std::string& op, uint32_t bv) {
   o.half_ii = 0;
   // memory semantics (reference trace_driven.cc:254-378)
   if (m == "LDC") {
-    o.cls = OC_ALU;  // constant cache is perfect in the tested configs
+    // timed as an ALU op with a constant-cache operand, like the reference
+    // (volta_opcode.h:108 maps LDC to ALU_OP; trace_driven.cc:255-261 only
+    // marks const_cache_operand, counted for power at shader.cc:3287)
+    o.cls = OC_ALU;
     o.space = S_CONST;
   } else if (m == "LDG" || m == "LDL" || m == "LD") {
     o.cls = OC_LOAD;

@@ -133,3 +133,30 @@ def test_check_engine_gpu_vs_cpu_lockstep(gpu_mod, tmp_path):
     c = sim.simulate(kl, "QV100", engine="cpu")
     k = sim.simulate(kl, "QV100", engine="check", extra={"-sim_check_interval": "512"})
     assert (k.tot_cycle, k.tot_insn) == (c.tot_cycle, c.tot_insn)
+
+
+# model features added in round 2, each bit-exact on both engines
+_FEATURES = {
+    "l1_write_back": {"-gpgpu_cache:dl1": "S:4:128:64,L:B:m:L:L,A:512:8,16:0,32"},
+    "l1_fetch_on_write": {"-gpgpu_cache:dl1": "S:4:128:64,L:T:m:F:L,A:512:8,16:0,32"},
+    "l2_no_write_alloc": {"-gpgpu_cache:dl2": "S:32:128:24,L:B:m:N:P,A:192:4,32:0,32"},
+    "dual_issue": {"-gpgpu_max_insn_issue_per_warp": "2"},
+    "warp_limiting": {"-gpgpu_scheduler": "warp_limiting:2:2"},
+    "two_level": {"-gpgpu_scheduler": "two_level_active:4:0:1"},
+    "max_insn_cap": {"-gpgpu_max_insn": "150000"},
+    "max_cta_cap": {"-gpgpu_max_cta": "30"},
+    "long_epoch": {"-icnt_latency": "32"},
+}
+
+
+@pytest.mark.parametrize("feature", sorted(_FEATURES))
+def test_round2_features_gpu_equals_cpu(gpu_mod, tmp_path, feature):
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    kl = rodinia.write_app(str(tmp_path / "bp"), rodinia.backprop(1024))
+    extra = _FEATURES[feature]
+    g = sim.simulate(kl, "QV100", engine="gpu", extra=extra)
+    c = sim.simulate(kl, "QV100", engine="cpu", extra=extra)
+    assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
+    strip = lambda s: {k: v for k, v in s.items() if "rate" not in k and "slowdown" not in k and "time" not in k}
+    assert strip(g.stats) == strip(c.stats)

@@ -169,3 +169,26 @@ def test_hotspot_backlog_no_loss(native, tmp_path):
     assert _stat(a.output, "icnt_mem_input_backlog") > 0
     assert "lost to a full backlog ring" not in a.output
     assert (a.tot_cycle, a.tot_insn) == (b.tot_cycle, b.tot_insn)
+
+
+def test_max_insn_stops_mid_kernel(native, traces):
+    """-gpgpu_max_insn is checked every epoch, not only between kernels
+    (reference gpgpu_sim::active, gpu-sim.cc:1071-1094): a one-kernel run
+    stops within one epoch's worth of issue after the cap."""
+    full = _run(native, traces["vadd"], {})
+    cap = full.tot_insn // 3
+    s = _run(native, traces["vadd"], {"-gpgpu_max_insn": str(cap)})
+    assert cap <= s.tot_insn < full.tot_insn
+    assert s.tot_cycle < full.tot_cycle
+    assert "break due to reaching the maximum" in s.output
+
+
+def test_max_cta_and_completed_cta_caps(native, traces):
+    full = _run(native, traces["vadd"], {})
+    n_cta = int(_stat(full.output, "gpu_tot_issued_cta"))
+    s = _run(native, traces["vadd"], {"-gpgpu_max_cta": "40"})
+    assert int(_stat(s.output, "gpu_tot_issued_cta")) == 40 < n_cta
+    assert s.tot_insn < full.tot_insn
+    c = _run(native, traces["vadd"], {"-gpgpu_max_completed_cta": "20"})
+    assert 20 <= int(_stat(c.output, "gpgpu_n_completed_cta")) < n_cta
+    assert c.tot_insn < full.tot_insn
