@@ -37,7 +37,7 @@ namespace asim {
 
 struct GpuArgs {
   SimCfg cfg;          // by value: kernel-argument (constant) memory, read with scalar loads
-  const SimCfg* cfg_g; // device copy (host-side bookkeeping only)
+  const SimCfg* __restrict__ cfg_g;  // device copy: read-only, uniform addresses -> scalar loads
   KernelDesc kd;
   const TAcc* acc;
   SMState* sms;
@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   // argument it lives in constant memory: every field is a scalar load into
   // an SGPR (uniform, invariant across the epoch fences), not a vector load
   // behind each acquire or an LDS round trip into a VGPR.
-  const SimCfg& c = a.cfg;
+  const SimCfg& c = *a.cfg_g;
   const bool is_sm = b < c.n_sm;
   const uint64_t E = c.icnt_latency;
   SMState* s = reinterpret_cast<SMState*>(g_lds);
