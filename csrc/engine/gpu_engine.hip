@@ -73,6 +73,44 @@ __device__ __forceinline__ void copy_state(T* dst, const T* src) {
   __syncthreads();
 }
 
+// HBM -> LDS state swap-in for time-sliced units: LDS-DMA (global_load_lds,
+// 16 B per lane, lane-linear LDS image) issues the whole state back to back
+// with no VGPR staging, then one wait.
+template <class T>
+__device__ __forceinline__ void swap_in(T* lds, const T* src) {
+  static_assert(sizeof(T) % 16 == 0, "state must be 16-byte granular");
+  typedef __attribute__((address_space(1))) const uint4 g4;
+  typedef __attribute__((address_space(3))) uint4 l4;
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(lds);
+  const int n = (int)(sizeof(T) / 16);
+  const int lane = (int)(threadIdx.x & 63);
+  for (int i = 0; i < n; i += 64)
+    if (i + lane < n) __builtin_amdgcn_global_load_lds((g4*)(s + i + lane), (l4*)(d + i), 16, 0, 0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+}
+// LDS -> HBM swap-out: eight 16-byte LDS reads in flight per lane, then the
+// stores (completion is awaited by the epoch barrier's release fence)
+template <class T>
+__device__ __forceinline__ void swap_out(T* dst, const T* lds) {
+  const uint4* s = reinterpret_cast<const uint4*>(lds);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  const int n = (int)(sizeof(T) / 16);
+  const int lane = (int)(threadIdx.x & 63);
+  int i = 0;
+  for (; i + 4 * 64 <= n; i += 4 * 64) {
+    uint4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = s[i + j * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[i + j * 64 + lane] = v[j];
+  }
+  for (; i < n; i += 64)
+    if (i + lane < n) d[i + lane] = s[i + lane];
+  __syncthreads();
+}
+
 extern __shared__ __attribute__((aligned(16))) char g_lds[];
 constexpr size_t kStateLds = ((sizeof(SMState) > sizeof(ChanState) ? sizeof(SMState) : sizeof(ChanState)) + 15) / 16 * 16;
 constexpr size_t kCfgOff = kStateLds + (sizeof(KernelDesc) + 15) / 16 * 16;
@@ -108,7 +146,7 @@ struct WaveParProf : WavePar {
   }
 };
 
-template <class P>
+template <class P, bool kSliced>
 __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   const uint32_t b = blockIdx.x;
   // The configuration is read all over the model.  As a by-value kernel
@@ -116,11 +154,29 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   // an SGPR (uniform, invariant across the epoch fences), not a vector load
   // behind each acquire or an LDS round trip into a VGPR.
   const SimCfg& c = *a.cfg_g;
-  const bool is_sm = b < c.n_sm;
   const uint64_t E = c.icnt_latency;
   SMState* s = reinterpret_cast<SMState*>(g_lds);
   ChanState* ch = reinterpret_cast<ChanState*>(g_lds);
-  if (is_sm)
+  // Units (SMs 0..n_sm-1, then channels) map to blocks round-robin: unit
+  // b + k * nblocks.  With no more units than blocks each block owns one
+  // unit whose state stays in LDS for the whole launch; otherwise (configs
+  // larger than the CU count, e.g. the 384-unit MI355X preset) a block
+  // time-slices its units every epoch, swapping states through HBM and
+  // keeping the last one resident into the next epoch.
+  const uint32_t nunits = c.n_sm + c.n_mem;
+  const uint32_t nmine = kSliced ? (nunits - 1 - b) / a.nblocks + 1 : 1;
+  const bool sliced = kSliced && nmine > 1;
+  uint32_t loaded = b;  // unit whose state is in LDS
+  auto unit_k = [&](uint32_t k) { return b + k * a.nblocks; };
+  auto swap_to = [&](uint32_t u) {
+    if (!kSliced || u == loaded) return;
+    if (loaded < c.n_sm) swap_out(&a.sms[loaded], s);
+    else swap_out(&a.chs[loaded - c.n_sm], ch);
+    if (u < c.n_sm) swap_in(s, &a.sms[u]);
+    else swap_in(ch, &a.chs[u - c.n_sm]);
+    loaded = u;
+  };
+  if (b < c.n_sm)
     copy_state(s, &a.sms[b]);
   else
     copy_state(ch, &a.chs[b - c.n_sm]);
@@ -147,10 +203,15 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   mx.n_src_sub = c.n_subpart;
   mx.ovf = a.ovf;
   mx.ovf_cap = a.ovf_cap;
-  if (is_sm && a.init_kernel) {
+  if (a.init_kernel) {
     sx.outbox = a.box_req[0];
     sx.outcnt = a.cnt_req[0];
-    sm_kernel_init<P>(*s, sx, s->ks, a.cycle0, a.flush_l1);
+    for (uint32_t k = 0; k < nmine; ++k) {
+      const uint32_t u = unit_k(sliced ? nmine - 1 - k : k);  // end with unit b resident
+      if (u >= c.n_sm) continue;
+      swap_to(u);
+      sm_kernel_init<P>(*s, sx, s->ks, a.cycle0, a.flush_l1);
+    }
   }
   uint64_t epoch = a.epoch0, cycle = a.cycle0;
   uint64_t t_work0 = a.ework ? __builtin_amdgcn_s_memtime() : 0;
@@ -159,18 +220,27 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   for (; n < a.max_epochs;) {
     const uint32_t cur = (uint32_t)(epoch & 1), prev = cur ^ 1u;
     const uint64_t t0 = cycle, t1 = t0 + E;
-    if (is_sm) {
-      sx.outbox = a.box_req[cur];
-      sx.outcnt = a.cnt_req[cur];
-      sm_epoch<P>(*s, sx, s->ks, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep,
-                  c.n_subpart, epoch);
-      sm_publish<P>(*s, sx, s->ks, *a.pub, cur);
-    } else {
-      mx.outbox = a.box_rep[cur];
-      mx.outcnt = a.cnt_rep[cur];
-      mx.win_end = t1 * c.per_core;
-      chan_epoch<P>(*ch, mx, a.box_req[prev], a.cnt_req[prev], a.cap_req, t0 * c.per_core);
-      chan_publish<P>(*ch, mx, *a.pub, cur);
+    // the resident unit first, then the others (units are independent
+    // within an epoch: they read only the previous epoch's mailboxes)
+    uint32_t first_k = 0;
+    for (uint32_t k = 0; k < nmine; ++k)
+      if (unit_k(k) == loaded) first_k = k;
+    for (uint32_t j = 0; j < nmine; ++j) {
+      const uint32_t u = unit_k((first_k + j) % nmine);
+      swap_to(u);
+      if (u < c.n_sm) {
+        sx.outbox = a.box_req[cur];
+        sx.outcnt = a.cnt_req[cur];
+        sm_epoch<P>(*s, sx, s->ks, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep,
+                    c.n_subpart, epoch);
+        sm_publish<P>(*s, sx, s->ks, *a.pub, cur);
+      } else {
+        mx.outbox = a.box_rep[cur];
+        mx.outcnt = a.cnt_rep[cur];
+        mx.win_end = t1 * c.per_core;
+        chan_epoch<P>(*ch, mx, a.box_req[prev], a.cnt_req[prev], a.cap_req, t0 * c.per_core);
+        chan_publish<P>(*ch, mx, *a.pub, cur);
+      }
     }
     ++n;
     P::prof(26);  // barrier
@@ -206,11 +276,11 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     if (a.max_cycle && cycle >= a.max_cycle) break;
   }
   P::prof(31);  // launch_rest
-  // write state back
-  if (is_sm)
-    copy_state(&a.sms[b], s);
+  // write the resident state back
+  if (loaded < c.n_sm)
+    copy_state(&a.sms[loaded], s);
   else
-    copy_state(&a.chs[b - c.n_sm], ch);
+    copy_state(&a.chs[loaded - c.n_sm], ch);
   if (a.prof && (threadIdx.x & 63) < kProfSlots) a.prof[(size_t)b * kProfSlots + (threadIdx.x & 63)] += pl->acc[threadIdx.x & 63];
   if (b == 0 && (threadIdx.x & 63) == 0) {
     a.ctl->done = done;
@@ -285,15 +355,18 @@ class GpuEngine : public Engine {
     HIPCHECK(hipGetDeviceProperties(&prop, dev));
     n_cu_ = prop.multiProcessorCount;
     CuPool::get().init(n_cu_);
+    // one block per unit while the units fit the CUs; larger configs (or a
+    // smaller ASIM_GPU_BLOCKS cap) time-slice several units per block
     nblocks_ = c.n_sm + c.n_mem;
+    uint32_t cap = (uint32_t)n_cu_;
+    if (const char* eb = getenv("ASIM_GPU_BLOCKS"))
+      if (atoi(eb) > 0) cap = std::min<uint32_t>(cap, (uint32_t)atoi(eb));
+    if (nblocks_ > cap) nblocks_ = cap;
     lds_ = kLdsBytes;
-    if ((int)nblocks_ > n_cu_)
-      throw std::runtime_error("GPU engine needs one CU per simulated SM/channel: " + std::to_string(nblocks_) +
-                               " blocks > " + std::to_string(n_cu_) + " CUs");
-    HIPCHECK(hipFuncSetAttribute((const void*)engine_kernel<WavePar>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)lds_));
-    HIPCHECK(hipFuncSetAttribute((const void*)engine_kernel<WaveParProf>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_));
+    sliced_ = nblocks_ < c.n_sm + c.n_mem;
+    for (const void* f : {(const void*)engine_kernel<WavePar, false>, (const void*)engine_kernel<WaveParProf, false>,
+                          (const void*)engine_kernel<WavePar, true>, (const void*)engine_kernel<WaveParProf, true>})
+      HIPCHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_));
     const char* pe = getenv("ASIM_GPU_PROFILE");
     profiling_ = pe && *pe && *pe != '0';
     if (profiling_) {
@@ -395,10 +468,14 @@ class GpuEngine : public Engine {
       a.ework = d_ework_;
       CuPool::get().acquire((int)nblocks_);
       hipError_t le;
-      if (profiling_)
-        hipLaunchKernelGGL(engine_kernel<WaveParProf>, dim3(nblocks_), dim3(64), lds_, stream_, a);
+      if (profiling_ && sliced_)
+        hipLaunchKernelGGL((engine_kernel<WaveParProf, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      else if (profiling_)
+        hipLaunchKernelGGL((engine_kernel<WaveParProf, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      else if (sliced_)
+        hipLaunchKernelGGL((engine_kernel<WavePar, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else
-        hipLaunchKernelGGL(engine_kernel<WavePar>, dim3(nblocks_), dim3(64), lds_, stream_, a);
+        hipLaunchKernelGGL((engine_kernel<WavePar, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       le = hipGetLastError();
       hipError_t ce = hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_);
       hipError_t se = hipStreamSynchronize(stream_);
@@ -615,6 +692,7 @@ class GpuEngine : public Engine {
   uint64_t epoch_ = 0, cycle_ = 0;
   uint32_t epochs_per_launch_ = 4096;
   bool profiling_ = false;
+  bool sliced_ = false;  // more units than blocks: the time-slicing kernel
   uint64_t* d_prof_ = nullptr;
   uint32_t* d_ework_ = nullptr;
 
@@ -720,7 +798,7 @@ namespace asim {
 EngineKernelInfo gpu_engine_kernel_info() {
   EngineKernelInfo k;
   hipFuncAttributes fa;
-  if (hipFuncGetAttributes(&fa, (const void*)engine_kernel<WavePar>) != hipSuccess) return k;
+  if (hipFuncGetAttributes(&fa, (const void*)engine_kernel<WavePar, false>) != hipSuccess) return k;
   k.num_regs = fa.numRegs;
   k.local_bytes = (int)fa.localSizeBytes;
   k.shared_static = (int)fa.sharedSizeBytes;
