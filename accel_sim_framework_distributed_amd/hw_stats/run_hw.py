@@ -5,10 +5,12 @@ Reference: util/hw_stats/run_hw.py:52-183 (runs every app of the selected
 suites under nvprof/nsight N times, one output directory per app/args).  Here
 each run is ``rocprofv3 --kernel-trace --output-format csv`` (timestamps ->
 cycles in the correlator); ``-c`` adds a separate counter pass
-(``--pmc ...``) -- counters are never combined with system/runtime tracing.
+(``--pmc ...``) per counter group (``-c`` repeatable, ``--counter_groups``
+for the correlator's set) -- counters are never combined with system/runtime
+tracing, and each group stays within one pass's hardware counter limits.
 
 Layout: ``<out>/<app>/<argfolder>/run_<i>/...kernel_trace.csv`` (and
-``counters_<i>/`` for ``-c``), consumed by plotting/correlate.py.
+``ctr<g>_<i>/`` per counter group), consumed by plotting/correlate.py.
 
     run_hw.py -B asim_hip_apps -R 4 -o hw_run/rocprof/MI355X
 """
@@ -24,8 +26,10 @@ from typing import List
 if __package__ in (None, ""):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
     from accel_sim_framework_distributed_amd.job_launching import common  # noqa: E402
+    from accel_sim_framework_distributed_amd.plotting.correlate import COUNTER_GROUPS  # noqa: E402
 else:
     from ..job_launching import common
+    from ..plotting.correlate import COUNTER_GROUPS
 
 
 def rocprof_cmd(out_dir: str, exe: List[str], counters: str = "") -> List[str]:
@@ -41,13 +45,19 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("-B", "--benchmark_list", required=True)
     ap.add_argument("-R", "--repeat", type=int, default=4, help="runs per app (the correlator burns the first)")
-    ap.add_argument("-c", "--counters", default="", help="comma separated PMC counters for an extra pass")
+    ap.add_argument("-c", "--counters", action="append", default=[],
+                    help="comma separated PMC counters for an extra pass (repeatable: one pass each)")
+    ap.add_argument("--counter_groups", action="store_true",
+                    help="add the correlator's counter passes (plotting/correlate.py COUNTER_GROUPS)")
     ap.add_argument("-o", "--out", default=os.path.join(common.REPO_ROOT, "hw_run", "rocprof", "MI355X"))
     ap.add_argument("-t", "--timeout", type=int, default=300, help="seconds per run")
     ap.add_argument("-n", "--dry_run", action="store_true")
     o = ap.parse_args(argv)
     reg = common.Registry()
     out = os.path.abspath(o.out)
+    groups = list(o.counters)
+    if o.counter_groups:
+        groups += COUNTER_GROUPS
     env = dict(os.environ)
     env.pop("ASIM_TRACE_DIR", None)  # time the plain build, never the traced one
     env.setdefault("TMPDIR", "/tmp")
@@ -59,7 +69,7 @@ def main(argv=None) -> int:
             args = a.get("args")
             argv_app = [exe_path] + (shlex.split(str(args)) if args else [])
             base = os.path.join(out, app, common.argfoldername(args))
-            passes = [("run", "")] + ([("counters", o.counters)] if o.counters else [])
+            passes = [("run", "")] + [(f"ctr{g}", c) for g, c in enumerate(groups)]
             for tag, ctr in passes:
                 for r in range(o.repeat):
                     d = os.path.join(base, f"{tag}_{r}")

@@ -53,6 +53,11 @@ class CorrelStat:
     drop_hw_below: float = 0.0
     log: bool = True
     sim_scale: float = 1.0
+    # derived simulator value: sim_eval({stat regex: per-kernel value}) over
+    # sim_stats (sim_stat is then only the chart's key)
+    sim_stats: Sequence[str] = ()
+    sim_eval: Optional[Callable[[Dict[str, float]], float]] = None
+    ratio: bool = False                            # a rate: per-app value is the mean over kernels, not the sum
 
 
 def _mean(v):
@@ -63,14 +68,111 @@ def _median(v):
     return float(np.median(v)) if len(v) else float("nan")
 
 
+def _hw(*cols: str) -> Callable[[Dict[str, List[float]], float], float]:
+    """Sum of the run-mean of rocprofv3 counter columns (NaN if one is absent)."""
+    def f(hw, mhz):
+        if any(c not in hw for c in cols):
+            return float("nan")
+        return float(sum(_mean(hw[c]) for c in cols))
+    return f
+
+
+def _hw_ratio(num: Sequence[str], den: Sequence[str], one_minus: bool = False):
+    def f(hw, mhz):
+        n, d = _hw(*num)(hw, mhz), _hw(*den)(hw, mhz)
+        if not (d > 0) or not math.isfinite(n):
+            return float("nan")
+        r = n / d
+        return 1.0 - r if one_minus else r
+    return f
+
+
+def _cycles(hw, mhz):
+    return _median(hw["duration_ns"]) * mhz / 1000.0 if "duration_ns" in hw else float("nan")
+
+
+# simulator stat regexes (they must be listed in job_launching/stats/example_stats.yml)
+S_CYC = r"gpu_sim_cycle\s*=\s*(.*)"
+S_WINSN = r"gpgpu_n_tot_w_icount\s*=\s*(.*)"
+S_LOAD = r"gpgpu_n_load_insn\s*=\s*(.*)"
+S_STORE = r"gpgpu_n_store_insn\s*=\s*(.*)"
+S_L1 = r"\s+Total_core_cache_stats_breakdown\[%s\]\[%s\]\s*=\s*(.*)"
+S_L2 = r"\s+L2_cache_stats_breakdown\[%s\]\[%s\]\s*=\s*(.*)"
+_VMEM = ("SQ_INSTS_VMEM_RD_sum", "SQ_INSTS_VMEM_WR_sum")
+_WAVE_INSTS = ("SQ_INSTS_VALU_sum", "SQ_INSTS_SALU_sum", "SQ_INSTS_SMEM_sum", "SQ_INSTS_LDS_sum",
+               "SQ_INSTS_BRANCH_sum") + _VMEM
+
+
+def _ipc(d):
+    return d[S_WINSN] / d[S_CYC] if d.get(S_CYC) else float("nan")
+
+
+def _l1_hit_rate(d):
+    tot = d[S_L1 % ("GLOBAL_ACC_R", "TOTAL_ACCESS")]
+    return d[S_L1 % ("GLOBAL_ACC_R", "HIT")] / tot if tot else float("nan")
+
+
+def _l2_hit_rate(d):
+    h = d[S_L2 % ("GLOBAL_ACC_R", "HIT")] + d[S_L2 % ("GLOBAL_ACC_W", "HIT")]
+    m = d[r"L2_total_cache_misses\s*=\s*(.*)"]
+    return h / (h + m) if h + m else float("nan")
+
+
+# Sim statistic <-> MI355X rocprofv3 counter mappings (the reference's
+# correl_mappings.py:5-23 maps GPGPU-Sim stats to nvprof/nsight metrics; these
+# map the same simulator stats to gfx950 SQ / TCP (L1) / TCC (L2) / EA (HBM)
+# counters collected by hw_stats/run_hw.py --counter_groups).
 CORREL_STATS: List[CorrelStat] = [
     # median over runs: short kernels on a shared node have a heavy right tail
-    CorrelStat("Cycles", r"gpu_sim_cycle\s*=\s*(.*)",
-               lambda hw, mhz: _median(hw["duration_ns"]) * mhz / 1000.0, "cycles"),
+    CorrelStat("Cycles", S_CYC, _cycles, "cycles"),
     CorrelStat("Instructions (thread)", r"gpu_sim_insn\s*=\s*(.*)",
                lambda hw, mhz: _mean(hw["thread_insts"]) if "thread_insts" in hw else float("nan"), "insn"),
-    CorrelStat("L2 read accesses", r"\s+L2_cache_stats_breakdown\[GLOBAL_ACC_R\]\[TOTAL_ACCESS\]\s*=\s*(.*)",
-               lambda hw, mhz: _mean(hw["TCC_REQ_sum"]) if "TCC_REQ_sum" in hw else float("nan"), "l2-reads"),
+    CorrelStat("Warp instructions", S_WINSN, _hw(*_WAVE_INSTS), "warp-insn"),
+    CorrelStat("Warp IPC", "warp_ipc", lambda hw, mhz: _hw(*_WAVE_INSTS)(hw, mhz) / _cycles(hw, mhz),
+               "warp-ipc", sim_stats=(S_WINSN, S_CYC), sim_eval=_ipc, ratio=True, log=False),
+    CorrelStat("Memory instructions (VMEM + LDS)", "mem_insn", _hw(*(_VMEM + ("SQ_INSTS_LDS_sum",))), "mem-insn",
+               sim_stats=(S_LOAD, S_STORE), sim_eval=lambda d: d[S_LOAD] + d[S_STORE]),
+    CorrelStat("Waves launched", r"gpgpu_n_completed_warps\s*=\s*(.*)", _hw("SQ_WAVES_sum"), "waves"),
+    CorrelStat("Branch instructions", r"gpgpu_n_branch_insn\s*=\s*(.*)", _hw("SQ_INSTS_BRANCH_sum"), "branch"),
+    CorrelStat("MFMA instructions", r"gpgpu_n_tensor_insn\s*=\s*(.*)", _hw("SQ_INSTS_MFMA_sum"), "mfma"),
+    CorrelStat("LDS bank conflict cycles", r"gpgpu_n_shmem_bkconflict\s*=\s*(.*)", _hw("SQ_LDS_BANK_CONFLICT_sum"),
+               "lds-conflict"),
+    CorrelStat("L1 accesses", "l1_acc", _hw("TCP_TOTAL_CACHE_ACCESSES_sum"), "l1-acc",
+               sim_stats=(S_L1 % ("GLOBAL_ACC_R", "TOTAL_ACCESS"), S_L1 % ("GLOBAL_ACC_W", "TOTAL_ACCESS")),
+               sim_eval=lambda d: sum(d.values())),
+    CorrelStat("L1 read misses (L1->L2 reads)", S_L1 % ("GLOBAL_ACC_R", "MISS"), _hw("TCP_TCC_READ_REQ_sum"),
+               "l1-read-miss"),
+    CorrelStat("L1->L2 write requests", S_L1 % ("GLOBAL_ACC_W", "TOTAL_ACCESS"), _hw("TCP_TCC_WRITE_REQ_sum"),
+               "l1-writes"),
+    CorrelStat("L1 read hit rate", "l1_hit_rate",
+               _hw_ratio(("TCP_TCC_READ_REQ_sum",), ("TCP_TOTAL_CACHE_ACCESSES_sum",), one_minus=True),
+               "l1-hit-rate", sim_stats=(S_L1 % ("GLOBAL_ACC_R", "HIT"), S_L1 % ("GLOBAL_ACC_R", "TOTAL_ACCESS")),
+               sim_eval=_l1_hit_rate, ratio=True, log=False),
+    CorrelStat("L2 read accesses", S_L2 % ("GLOBAL_ACC_R", "TOTAL_ACCESS"), _hw("TCC_READ_sum"), "l2-reads"),
+    CorrelStat("L2 write accesses", S_L2 % ("GLOBAL_ACC_W", "TOTAL_ACCESS"), _hw("TCC_WRITE_sum"), "l2-writes"),
+    CorrelStat("L2 atomic accesses", S_L2 % ("GLOBAL_ATOMIC", "TOTAL_ACCESS"), _hw("TCC_ATOMIC_sum"), "l2-atomics"),
+    CorrelStat("L2 hits", "l2_hits", _hw("TCC_HIT_sum"), "l2-hits",
+               sim_stats=(S_L2 % ("GLOBAL_ACC_R", "HIT"), S_L2 % ("GLOBAL_ACC_W", "HIT")),
+               sim_eval=lambda d: sum(d.values())),
+    CorrelStat("L2 misses", r"L2_total_cache_misses\s*=\s*(.*)", _hw("TCC_MISS_sum"), "l2-misses"),
+    CorrelStat("L2 hit rate", "l2_hit_rate", _hw_ratio(("TCC_HIT_sum",), ("TCC_HIT_sum", "TCC_MISS_sum")),
+               "l2-hit-rate", sim_stats=(S_L2 % ("GLOBAL_ACC_R", "HIT"), S_L2 % ("GLOBAL_ACC_W", "HIT"),
+                                          r"L2_total_cache_misses\s*=\s*(.*)"),
+               sim_eval=_l2_hit_rate, ratio=True, log=False),
+    CorrelStat("DRAM read requests", r"total dram reads\s*=\s*(.*)", _hw("TCC_EA0_RDREQ_sum"), "dram-reads"),
+    CorrelStat("DRAM write requests", r"total dram writes\s*=\s*(.*)", _hw("TCC_EA0_WRREQ_sum"), "dram-writes"),
+    CorrelStat("Interconnect packets SM->memory", r"icnt_total_pkts_simt_to_mem\s*=\s*(.*)",
+               _hw("TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum", "TCP_TCC_ATOMIC_WITH_RET_REQ_sum"), "icnt-pkts"),
+]
+
+# rocprofv3 counter passes covering CORREL_STATS within one pass's hardware
+# limits (<= 8 SQ, <= 4 TCC, <= 4 TCP counters per run)
+COUNTER_GROUPS: List[str] = [
+    "SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_SMEM,SQ_INSTS_LDS,SQ_INSTS_BRANCH,SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR",
+    "SQ_INSTS_MFMA,SQ_LDS_BANK_CONFLICT,TCP_TOTAL_CACHE_ACCESSES,TCP_TCC_READ_REQ,TCP_TCC_WRITE_REQ,"
+    "TCP_TCC_ATOMIC_WITH_RET_REQ,TCC_HIT,TCC_MISS",
+    "TCC_READ,TCC_WRITE,TCC_ATOMIC,TCC_EA0_RDREQ",
+    "TCC_EA0_WRREQ",
 ]
 
 
@@ -114,17 +216,30 @@ def load_hw_rocprof(hw_dir: str, burn: int = 0) -> Dict[str, List[Dict[str, List
                 kernels[i]["name"] = [_norm_kernel(name)]  # type: ignore[list-item]
                 for k, v in (counters[i] if i < len(counters) else {}).items():
                     kernels[i][k].append(v)
+        # separate counter passes (run_hw.py -c / --counter_groups): one
+        # directory per (group, repeat), kernels matched by dispatch order
+        for cdir in sorted(glob.glob(os.path.join(args_dir, "*"))):
+            if not re.fullmatch(r"(counters|ctr\d+)_\d+", os.path.basename(cdir)):
+                continue
+            for i, cv in enumerate(_load_counters(cdir)):
+                while len(kernels) <= i:
+                    kernels.append(defaultdict(list))
+                for k, v in cv.items():
+                    kernels[i][k].append(v)
         if kernels:
             out[app] = [dict(k) for k in kernels]
     return out
 
 
 def _load_counters(run_dir: str) -> List[Dict[str, float]]:
-    """Per-dispatch counter values from rocprofv3 ``*counter_collection.csv``."""
+    """Per-dispatch counter values from rocprofv3 ``*counter_collection.csv``
+    (dimension instances summed; runtime blit kernels skipped)."""
     per: Dict[int, Dict[str, float]] = {}
     for f in glob.glob(os.path.join(run_dir, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
+                if "__amd_rocclr_" in row.get("Kernel_Name", ""):
+                    continue
                 try:
                     d = int(row["Dispatch_Id"])
                     per.setdefault(d, {})[row["Counter_Name"] + "_sum"] = \
@@ -190,6 +305,32 @@ def error_metrics(hw: Sequence[float], sim: Sequence[float]) -> Dict[str, float]
     return r
 
 
+def _finite_mean(v) -> float:
+    f = [x for x in v if math.isfinite(x)]
+    return float(np.mean(f)) if f else float("nan")
+
+
+def _sim_series(sim, st: CorrelStat, cfg: str) -> Dict[str, List[float]]:
+    """{app: per-kernel simulator values} of one stat (derived stats evaluated
+    kernel by kernel from their input stats)."""
+    if st.sim_eval is None:
+        return sim[st.sim_stat].get(cfg, {})
+    per = [sim[s].get(cfg, {}) for s in st.sim_stats]
+    out: Dict[str, List[float]] = {}
+    for app in per[0]:
+        if not all(app in p for p in per):
+            continue
+        n = min(len(p[app]) for p in per)
+        vals = []
+        for i in range(n):
+            try:
+                vals.append(float(st.sim_eval({s: p[app][i] for s, p in zip(st.sim_stats, per)})))
+            except ZeroDivisionError:
+                vals.append(float("nan"))
+        out[app] = vals
+    return out
+
+
 def correlate(sim_csv: str, hw: Dict[str, List[Dict[str, List[float]]]], clock_mhz: float,
               stats: Sequence[CorrelStat] = CORREL_STATS, blacklist: Sequence[str] = (),
               hw_err_tolerance: float = 30.0, err_threshold: float = 9e9) -> Dict:
@@ -197,11 +338,14 @@ def correlate(sim_csv: str, hw: Dict[str, List[Dict[str, List[float]]]], clock_m
     bl = [re.compile(b) for b in blacklist if b.strip()]
     result = OrderedDict()
     for st in stats:
-        if st.sim_stat not in sim:
+        if st.sim_eval is None and st.sim_stat not in sim:
             continue
+        if st.sim_eval is not None and any(s not in sim for s in st.sim_stats):
+            continue
+        agg = _finite_mean if st.ratio else (lambda v: float(np.nansum(v)))
         per_cfg = OrderedDict()
         for cfg in configs:
-            apps = sim[st.sim_stat].get(cfg, {})
+            apps = _sim_series(sim, st, cfg)
             app_pts, app_all, k_pts = [], [], []
             for app, svals in apps.items():
                 if app not in hw or any(b.search(app) for b in bl):
@@ -219,7 +363,7 @@ def correlate(sim_csv: str, hw: Dict[str, List[Dict[str, List[float]]]], clock_m
                 for i in range(n):
                     if math.isfinite(hv[i]) and hv[i] > st.drop_hw_below:
                         k_pts.append((hv[i], sv[i], f"{app}--{i}"))
-                ha, sa = float(np.nansum(hv)), float(np.sum(sv))
+                ha, sa = agg(hv), agg(sv)
                 if math.isfinite(ha) and ha > st.drop_hw_below:
                     app_all.append((ha, sa, app))
                 if math.isfinite(ha) and ha > st.drop_hw_below and not noisy:

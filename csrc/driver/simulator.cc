@@ -608,13 +608,21 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   print("gpu_tot_occupancy = %.4f%% \n", r.occupancy);
   uint64_t l2_bytes = 0, dram_rd = 0, dram_wr = 0, dram_act = 0, dram_busy = 0, dram_cyc = 0;
   uint64_t l2[L2T_COUNT][L2O_COUNT] = {};
+  // Rates (bandwidths, utilisation) are this kernel's; event counts are
+  // cumulative over the run like the reference's (gpu-sim.cc:1355-1541 print
+  // the never-reset shader / cache / DRAM counters; get_stats.py differences
+  // them per kernel as collect_aggregate).
+  const std::vector<SMStats>& csm = prev_sm_;
+  const std::vector<MemStats>& cmem = prev_mem_;
   for (auto& m : mem) {
     l2_bytes += m.bytes_in + m.bytes_out;
+    dram_busy += m.dram_busy_cycles;
+    dram_cyc += m.dram_cycles;
+  }
+  for (auto& m : cmem) {
     dram_rd += m.dram_rd;
     dram_wr += m.dram_wr;
     dram_act += m.dram_act;
-    dram_busy += m.dram_busy_cycles;
-    dram_cyc += m.dram_cycles;
     for (int t = 0; t < L2T_COUNT; ++t)
       for (int o = 0; o < L2O_COUNT; ++o) l2[t][o] += m.l2[t][o];
   }
@@ -627,7 +635,7 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   static const char* l1t[L1T_COUNT] = {"GLOBAL_ACC_R", "GLOBAL_ACC_W", "LOCAL_ACC_R", "LOCAL_ACC_W", "GLOBAL_ATOMIC"};
   uint64_t l1[L1T_COUNT][L1O_COUNT] = {};
   uint64_t shm = 0, shm_conf = 0;
-  for (auto& s : sm) {
+  for (auto& s : csm) {
     for (int t = 0; t < L1T_COUNT; ++t)
       for (int o = 0; o < L1O_COUNT; ++o) l1[t][o] += s.l1[t][o];
     shm += s.shmem_acc;
@@ -691,7 +699,7 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
     // partition, DRAM queue and interconnect stalls
     uint64_t cls[OC_COUNT] = {}, stall_idle = 0, sb = 0, pipe = 0, bankc = 0, dual = 0, l1wb = 0, l1wbl = 0,
              act = 0, busyc = 0, occ = 0, rfr = 0, rfw = 0, ctas = 0, warps = 0, memi = 0;
-    for (auto& st : sm) {
+    for (auto& st : csm) {
       for (int i = 0; i < OC_COUNT; ++i) cls[i] += st.cls_insn[i];
       stall_idle += st.issue_stall_idle;
       sb += st.sb_stall;
@@ -735,8 +743,9 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
     print("gpgpu_sm_active_cycles = %llu\n", (unsigned long long)act);
     print("gpgpu_sm_issue_busy_cycles = %llu\n", (unsigned long long)busyc);
     print("gpgpu_avg_active_warps = %.4f\n", act ? (double)occ / (double)act : 0.0);
-    uint64_t l2cyc = 0, l2busy = 0, rop = 0, qocc = 0, icst = 0, pre = 0, evd = 0;
-    for (auto& m : mem) {
+    uint64_t l2cyc = 0, l2busy = 0, rop = 0, qocc = 0, icst = 0, pre = 0, evd = 0, cdc = 0;
+    for (auto& m : cmem) {
+      cdc += m.dram_cycles;
       l2cyc += m.l2_cycles;
       l2busy += m.l2_busy;
       rop += m.rop_occ;
@@ -751,19 +760,19 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
     print("L2_cache_dirty_evictions = %llu\n", (unsigned long long)evd);
     print("L2_busy_rate = %.4f\n", l2cyc ? (double)l2busy / (double)l2cyc : 0.0);
     print("avg_rop_queue_occupancy = %.4f\n", l2cyc ? (double)rop / (double)l2cyc : 0.0);
-    print("avg_dram_sched_queue_occupancy = %.4f\n", dram_cyc ? (double)qocc / (double)dram_cyc : 0.0);
+    print("avg_dram_sched_queue_occupancy = %.4f\n", cdc ? (double)qocc / (double)cdc : 0.0);
     print("total dram precharges = %llu\n", (unsigned long long)pre);
     print("dram_row_buffer_locality = %.4f\n",
           (dram_rd + dram_wr) ? 1.0 - (double)dram_act / (double)(dram_rd + dram_wr) : 0.0);
   }
   uint64_t pk_out = 0, pk_in = 0;
-  for (auto& s : sm) {
+  for (auto& s : csm) {
     pk_out += s.pkts_out;
     pk_in += s.pkts_in;
   }
   {
     uint64_t bl = 0, drop = 0;
-    for (auto& m : mem) {
+    for (auto& m : cmem) {
       bl += m.icnt_backlog;
       drop += m.icnt_ovf_drop;
     }

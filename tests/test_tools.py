@@ -150,3 +150,70 @@ def test_ubench_output_parser():
     log = open(os.path.join(UBENCH, "ub_cache_lat.log")).read()
     r = ubench.parse(log)
     assert r["options"]["-gpgpu_l1_latency"] and float(r["measurements"]["xcd_l2_hit_latency"]) > 0
+
+
+def test_correlator_stat_breadth_matches_simulator_output(tmp_path):
+    """>= 15 CorrelStats, and every simulator regex they use is in the stats
+    yml and matches a line of a real simulator run (per kernel)."""
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    assert len(correlate.CORREL_STATS) >= 15
+    spec = get_stats.load_stats_yml("")
+    listed = set(spec["collect_aggregate"] + spec["collect_abs"] + spec["collect_rates"])
+    kl = rodinia.write_app(str(tmp_path / "bp"), rodinia.backprop(1024))
+    out = sim.simulate(kl, "QV100", engine="cpu").output
+    per, order = get_stats.parse_output(out, spec, per_kernel=True, kernel_instance=True)
+    assert len(order) == 2
+    for st in correlate.CORREL_STATS:
+        for rx in (st.sim_stats or (st.sim_stat,)):
+            assert rx in listed, rx
+            assert all(rx in per[k] for k in order), rx
+    # cumulative counters are differenced back to per-kernel values
+    l2r = r"\s+L2_cache_stats_breakdown\[GLOBAL_ACC_R\]\[TOTAL_ACCESS\]\s*=\s*(.*)"
+    vals = [int(per[k][l2r]) for k in order]
+    raw = [int(l.split("=")[1]) for l in out.splitlines() if "L2_cache_stats_breakdown[GLOBAL_ACC_R][TOTAL_ACCESS]" in l]
+    assert raw[1] >= raw[0] and vals == [raw[0], raw[1] - raw[0]]
+
+
+def test_correlator_counter_passes_and_derived_stats(tmp_path):
+    """Counter-pass directories (ctr<g>_<i>) merge into the kernel records and
+    derived stats (IPC, hit rates) are evaluated kernel by kernel."""
+    S = correlate
+    t = get_stats.StatTable()
+    stats = {S.S_CYC: [1000, 2000], S.S_WINSN: [500, 3000],
+             S.S_L2 % ("GLOBAL_ACC_R", "HIT"): [60, 10], S.S_L2 % ("GLOBAL_ACC_W", "HIT"): [20, 10],
+             r"L2_total_cache_misses\s*=\s*(.*)": [20, 80]}
+    t.stats = list(stats)
+    for s, ks in stats.items():
+        for i, v in enumerate(ks):
+            t.set("app/x", f"k{i}--0", "MI355X", s, str(v))
+    (tmp_path / "s.csv").write_text(get_stats.render_csv(t))
+    d = tmp_path / "hw" / "app" / "x"
+    for r in range(2):
+        rd = d / f"run_{r}"
+        rd.mkdir(parents=True)
+        with open(rd / "k_kernel_trace.csv", "w") as f:
+            w = csv.writer(f)
+            w.writerow(["Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+            w.writerow([1, "k0", 0, 500])      # 1000 cycles at 2000 MHz
+            w.writerow([2, "k1", 1000, 2000])  # 2000 cycles
+    cd = d / "ctr0_0"
+    cd.mkdir()
+    with open(cd / "c_counter_collection.csv", "w") as f:
+        w = csv.writer(f)
+        w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writerow([7, "__amd_rocclr_fillBuffer", "TCC_HIT", 999])
+        for disp, hit, miss in ((8, 40, 10), (9, 30, 30)):
+            w.writerow([disp, "k", "TCC_HIT", hit / 2])   # two dimension instances
+            w.writerow([disp, "k", "TCC_HIT", hit / 2])
+            w.writerow([disp, "k", "TCC_MISS", miss])
+            w.writerow([disp, "k", "SQ_INSTS_VALU", 250 if disp == 8 else 1000])
+    hw = S.load_hw_rocprof(str(tmp_path / "hw"), burn=0)
+    k = hw["app/x"]
+    assert k[0]["TCC_HIT_sum"] == [40.0] and k[1]["TCC_MISS_sum"] == [30.0]
+    res = S.correlate(str(tmp_path / "s.csv"), hw, 2000.0)
+    hr = res["L2 hit rate"]["configs"]["MI355X"]
+    # per kernel: sim 0.8 / 0.2, hw 0.8 / 0.5 -> per-app means 0.5 vs 0.65
+    (hwv, simv, _), = hr["apps"]
+    assert simv == pytest.approx(0.5) and hwv == pytest.approx(0.65)
+    assert res["Cycles"]["configs"]["MI355X"]["app_metrics"]["mae"] == pytest.approx(0.0)
