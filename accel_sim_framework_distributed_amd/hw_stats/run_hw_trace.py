@@ -4,8 +4,9 @@ util/tracer_nvbit/run_hw_trace.py:51-121: per benchmark create
 ``<out>/<app>/<args>/traces``, run the app with the tracer injected,
 post-process).
 
-Applications built with asim_trace annotations (csrc/apps, csrc/tracer/
-asim_trace.h) write ``kernel-N.traceg`` + ``kernelslist.g`` themselves when
+Plain HIP applications are traced through their automatically instrumented
+twins (``bin/isatrace/<app>``, built by isatrace/build.py from the same
+source), which write ``kernel-N.traceg`` + ``kernelslist.g`` when
 ``ASIM_TRACE_DIR`` is set; this driver runs them, then (``--binary``)
 converts each text trace to the simulator's binary ``.asimk`` format and
 rewrites the kernelslist -- the post-processing step.  ``-l`` injects the
@@ -59,12 +60,18 @@ def main(argv=None) -> int:
     ap.add_argument("-l", "--rocprof_tool", action="store_true", help="also inject bin/libasim_tracer.so")
     ap.add_argument("-t", "--timeout", type=int, default=600)
     ap.add_argument("-n", "--dry_run", action="store_true")
+    ap.add_argument("--no_isa", dest="isa", action="store_false",
+                    help="run bin/apps/<app> itself instead of its isatrace twin bin/isatrace/<app>")
     o = ap.parse_args(argv)
     reg = common.Registry()
     for exec_dir, data_dir, app, args_list in reg.benchmarks(o.benchmark_list.split(",")):
         exe_path = os.path.join(os.path.expandvars(exec_dir) or ".", app)
         if not os.path.isabs(exe_path):
             exe_path = os.path.join(common.REPO_ROOT, exe_path)
+        # the automatically instrumented twin of a plain HIP app (isatrace)
+        twin = os.path.join(common.REPO_ROOT, "bin", "isatrace", app)
+        if o.isa and os.path.exists(twin) and os.path.exists(twin + ".asimisa"):
+            exe_path = twin
         for a in args_list:
             args = a.get("args")
             tdir = os.path.abspath(os.path.join(o.out, app, common.argfoldername(args), "traces"))

@@ -86,6 +86,9 @@ def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
         "  description = LINK $out",
         "rule hipexe",
         f"  command = {hipcc} $hipflags $in -o $out $libs",
+        "rule isatrace",
+        f"  command = {sys.executable} {os.path.join(PKG, 'isatrace', 'build.py')} $in -o $out \"--libs=$libs\" -- "
+        f"-munsafe-fp-atomics -fPIC -I{os.path.join(ROOT, 'csrc')}",
         "  description = HIPEXE $out",
     ]
     objs = []
@@ -129,28 +132,39 @@ def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
                     if first.startswith("// UB_LIBS:"):
                         lines.append(f"  libs = {first.split(':', 1)[1].strip()}")
                     defaults.append(out)
-        # HIP applications with asim_trace annotations (trace capture + HW timing)
+        # plain HIP applications: bin/apps/<app> (HW timing / counters) and the
+        # automatically instrumented twin bin/isatrace/<app> (+ .asimisa map)
+        # built from the same source with the same device flags
         app_dir = os.path.join(ROOT, "csrc", "apps")
         if os.path.isdir(app_dir):
-            hdr = os.path.join(ROOT, "csrc", "tracer", "asim_trace.h")
+            hdr = os.path.join(app_dir, "app_common.h")
+            isa_deps = " ".join(os.path.join(ROOT, p) for p in (
+                "accel_sim_framework_distributed_amd/isatrace/rewrite.py",
+                "accel_sim_framework_distributed_amd/isatrace/build.py", "csrc/tracer/isa_runtime.cc"))
             for fn in sorted(os.listdir(app_dir)):
                 if fn.endswith(".hip"):
                     out = os.path.join(ROOT, "bin", "apps", fn[:-4])
                     lines.append(f"build {out}: hipexe {os.path.join(app_dir, fn)} | {hdr}")
                     defaults.append(out)
+                    tout = os.path.join(ROOT, "bin", "isatrace", fn[:-4])
+                    lines.append(f"build {tout}: isatrace {os.path.join(app_dir, fn)} | {hdr} {isa_deps}")
+                    defaults.append(tout)
         # examples/<name>/main.hip -> bin/examples/<name>
         ex_dir = os.path.join(ROOT, "examples")
         if os.path.isdir(ex_dir):
-            hdr = os.path.join(ROOT, "csrc", "tracer", "asim_trace.h")
+            hdr = os.path.join(ROOT, "csrc", "apps", "app_common.h")
             for name in sorted(os.listdir(ex_dir)):
                 src = os.path.join(ex_dir, name, "main.hip")
                 if os.path.exists(src):
                     out = os.path.join(ROOT, "bin", "examples", name)
-                    lines.append(f"build {out}: hipexe {src} | {hdr}")
+                    tout = os.path.join(ROOT, "bin", "isatrace", name)
                     first = open(src).readline()
-                    if first.startswith("// UB_LIBS:"):
-                        lines.append(f"  libs = {first.split(':', 1)[1].strip()}")
-                    defaults.append(out)
+                    libs = first.split(':', 1)[1].strip() if first.startswith("// UB_LIBS:") else ""
+                    lines.append(f"build {out}: hipexe {src} | {hdr}")
+                    lines.append(f"  libs = {libs}")
+                    lines.append(f"build {tout}: isatrace {src} | {hdr} {isa_deps}")
+                    lines.append(f"  libs = {libs}")
+                    defaults += [out, tout]
         tracer = os.path.join(ROOT, "csrc", "tracer", "asim_tracer.cc")
         if os.path.exists(tracer) and os.path.isdir(os.path.join(ROCM, "include", "rocprofiler-sdk")):
             t_o = os.path.join(bdir, "tracer.o")

@@ -1,49 +1,25 @@
 // pathfinder-shaped dynamic programming (Rodinia pathfinder: minimum-cost
 // path down a 2-D wall, one row per step, the previous row staged in shared
-// memory with a one-column halo), HIP + asim_trace annotations.
+// memory with a one-column halo), plain HIP.
+#include <algorithm>
 #include <cmath>
 
-#include "../tracer/asim_trace.h"
-
-using namespace asim_trace;
+#include "app_common.h"
 
 constexpr int B = 256;
 
-template <class TR>
-__global__ void dynproc(TR tr, const int* wall_row, const int* src, int* dst, int cols) {
+__global__ void dynproc_kernel(const int* wall_row, const int* src, int* dst, int cols) {
   __shared__ int prev[B + 2];
-  auto w = tr.wave();
   const int x = blockIdx.x * B + threadIdx.x;
-  ASIM_VALU(w, V_MAD_U32_U24, 1, 0);
-  ASIM_VALU(w, V_CMP_GT_I32, 0, 1);
-  int v = 0x3fffffff;
-  if (x < cols) v = ASIM_LD(w, GLOBAL_LOAD_DWORD, src + x, 2, 1);
-  ASIM_VALU(w, S_WAITCNT, 0, 0);
-  ASIM_ST(w, DS_WRITE_B32, &prev[threadIdx.x + 1], v, 2, 3);
-  if (threadIdx.x == 0) {
-    int h = 0x3fffffff;
-    if (x > 0) h = ASIM_LD(w, GLOBAL_LOAD_DWORD, src + x - 1, 4, 1);
-    ASIM_ST(w, DS_WRITE_B32, &prev[0], h, 4, 3);
-  }
-  if (threadIdx.x == B - 1) {
-    int h = 0x3fffffff;
-    if (x + 1 < cols) h = ASIM_LD(w, GLOBAL_LOAD_DWORD, src + x + 1, 4, 1);
-    ASIM_ST(w, DS_WRITE_B32, &prev[B + 1], h, 4, 3);
-  }
-  ASIM_BARRIER(w);
+  prev[threadIdx.x + 1] = x < cols ? src[x] : 0x3fffffff;
+  if (threadIdx.x == 0) prev[0] = x > 0 ? src[x - 1] : 0x3fffffff;
+  if (threadIdx.x == B - 1) prev[B + 1] = x + 1 < cols ? src[x + 1] : 0x3fffffff;
+  __syncthreads();
   if (x < cols) {
-    const int l = ASIM_LD(w, DS_READ_B32, &prev[threadIdx.x], 5, 3);
-    const int u = ASIM_LD(w, DS_READ_B32, &prev[threadIdx.x + 1], 6, 3);
-    const int r = ASIM_LD(w, DS_READ_B32, &prev[threadIdx.x + 2], 7, 3);
-    const int wv = ASIM_LD(w, GLOBAL_LOAD_DWORD, wall_row + x, 8, 1);
-    ASIM_VALU(w, S_WAITCNT, 0, 0);
-    ASIM_VALU(w, V_MIN_F32, 9, 5, 6);
-    ASIM_VALU(w, V_MIN_F32, 9, 9, 7);
-    ASIM_VALU(w, V_ADD_U32, 10, 9, 8);
+    const int l = prev[threadIdx.x], u = prev[threadIdx.x + 1], r = prev[threadIdx.x + 2];
     const int m = l < u ? (l < r ? l : r) : (u < r ? u : r);
-    ASIM_ST(w, GLOBAL_STORE_DWORD, dst + x, wv + m, 10, 1);
+    dst[x] = wall_row[x] + m;
   }
-  w.exit();
 }
 
 int main(int argc, char** argv) {
@@ -55,18 +31,17 @@ int main(int argc, char** argv) {
     v = (int)((s >> 16) % 10);
   }
   int *dwall, *r0, *r1;
-  ASIM_HIP(hipMalloc(&dwall, wall.size() * 4));
-  ASIM_HIP(hipMalloc(&r0, cols * 4));
-  ASIM_HIP(hipMalloc(&r1, cols * 4));
-  memcpy_htod(dwall, wall.data(), wall.size() * 4);
-  memcpy_htod(r0, wall.data(), cols * 4);
+  APP_HIP(hipMalloc(&dwall, wall.size() * 4));
+  APP_HIP(hipMalloc(&r0, cols * 4));
+  APP_HIP(hipMalloc(&r1, cols * 4));
+  APP_HIP(hipMemcpy(dwall, wall.data(), wall.size() * 4, hipMemcpyHostToDevice));
+  APP_HIP(hipMemcpy(r0, wall.data(), cols * 4, hipMemcpyHostToDevice));
   const dim3 grid((cols + B - 1) / B), blk(B);
   for (int t = 1; t < rows; ++t)
-    launch("_Z14dynproc_kerneliPiS_S_iiii", dynproc<On>, dynproc<Off>, grid, blk, 0, 0,
-           (const int*)(dwall + (size_t)t * cols), (const int*)(t % 2 ? r0 : r1), t % 2 ? r1 : r0, cols);
-  ASIM_HIP(hipDeviceSynchronize());
+    dynproc_kernel<<<grid, blk>>>(dwall + (size_t)t * cols, t % 2 ? r0 : r1, t % 2 ? r1 : r0, cols);
+  APP_HIP(hipDeviceSynchronize());
   std::vector<int> out(cols);
-  ASIM_HIP(hipMemcpy(out.data(), (rows - 1) % 2 ? r1 : r0, cols * 4, hipMemcpyDeviceToHost));
+  APP_HIP(hipMemcpy(out.data(), (rows - 1) % 2 ? r1 : r0, cols * 4, hipMemcpyDeviceToHost));
   // host check of the DP
   std::vector<int> a(wall.begin(), wall.begin() + cols), b(cols);
   for (int t = 1; t < rows; ++t) {
@@ -80,8 +55,8 @@ int main(int argc, char** argv) {
   }
   const bool ok = a == out;
   printf("pathfinder cols=%d rows=%d: %s\n", cols, rows, ok ? "PASSED" : "FAILED");
-  ASIM_HIP(hipFree(dwall));
-  ASIM_HIP(hipFree(r0));
-  ASIM_HIP(hipFree(r1));
+  APP_HIP(hipFree(dwall));
+  APP_HIP(hipFree(r0));
+  APP_HIP(hipFree(r1));
   return ok ? 0 : 1;
 }

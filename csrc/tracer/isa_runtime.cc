@@ -1,0 +1,409 @@
+// Host runtime of the automatic gfx950 ISA tracer (linked into executables
+// built by accel_sim_framework_distributed_amd/isatrace/build.py).
+//
+// Reference: the host half of the NVBit tracer -- nvbit_at_cuda_event
+// (util/tracer_nvbit/tracer_tool/tracer_tool.cu:380-506) resets the device
+// channel per launch, waits for the kernel, and the receiver thread
+// (:508-700) turns the pushed records into the kernel-N.traceg text format
+// (PC, active mask, registers, opcode, addresses), plus kernelslist.g with
+// MemcpyHtoD lines (:369-378).
+//
+// Here the instrumented code object (isatrace/rewrite.py) appends per-wave
+// record streams to 64 KB chunks of one device buffer.  This runtime
+//  * interposes __hipRegisterFatBinary / __hipRegisterFunction to register
+//    the probes' control block (device global __asim_tctl) and learn kernel
+//    names, and hipLaunchKernel to arm the buffer, launch, wait and decode;
+//  * expands each wave's segment / memory records with the static map
+//    (<exe>.asimisa: every segment's instructions with real byte offsets,
+//    registers and memory widths) into trace lines;
+//  * writes kernel-N.traceg (format v4, wavefront size 64, binary version
+//    950), kernelslist.g (+ MemcpyHtoD lines from hipMemcpy) and stats.csv.
+// Environment: ASIM_TRACE_DIR (enables tracing), ASIM_TRACE_KERNEL_START/END
+// (1-based launch range), ASIM_TRACE_BUF_MB (device buffer, default 4096),
+// ASIM_ISA_MAP (map path, default <exe>.asimisa).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+constexpr uint32_t kTagMem = 0x80000000u, kTagChunk = 0xC0000000u;
+// 16-byte units per chunk: from the map header (isatrace/rewrite.py CHUNK_UNITS)
+uint32_t kChunkUnits = 512;
+
+struct Ctl {  // must match the probes (isatrace/rewrite.py): buf @0, next_chunk @8, n_chunks @12
+  uint64_t buf;
+  uint32_t next_chunk;
+  uint32_t n_chunks;
+  uint64_t pad[2];
+};
+static_assert(sizeof(Ctl) == 32, "control block layout");
+
+struct SInst {
+  uint32_t pc;
+  int32_t mem;
+  std::string text;  // "<ndst> <dsts> <mnemonic> <nsrc> <srcs>" (trace line middle)
+  int width;
+};
+struct KMap {
+  std::vector<std::vector<SInst>> segs;  // seg id - 1
+  uint32_t lds = 0, vgprs = 32;
+};
+
+#define RT_HIP(x)                                                                                    \
+  do {                                                                                               \
+    hipError_t e_ = (x);                                                                             \
+    if (e_ != hipSuccess) {                                                                          \
+      fprintf(stderr, "asim isa tracer: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, \
+              __LINE__);                                                                             \
+      exit(3);                                                                                       \
+    }                                                                                                \
+  } while (0)
+
+struct Tracer {
+  bool enabled = false;
+  std::string dir;
+  long kstart = 1, kend = 1L << 40;
+  long next_id = 0;
+  size_t buf_bytes = 4096ull << 20;
+  struct DevBuf {
+    uint8_t* ptr = nullptr;
+    uint32_t last_used = 0;  // chunks written by the previous traced launch (re-zeroed)
+  };
+  std::unordered_map<int, DevBuf> bufs;  // one trace buffer per device (launch device's HBM)
+  std::mutex mu;
+  std::unordered_map<std::string, KMap> maps;
+  std::unordered_map<const void*, std::string> names;
+  std::vector<Ctl*> shadows;  // one device __asim_tctl per registered code object
+
+  Tracer() {
+    const char* d = getenv("ASIM_TRACE_DIR");
+    if (!d || !*d) return;
+    enabled = true;
+    dir = d;
+    std::string cmd = "mkdir -p '" + dir + "'";
+    if (system(cmd.c_str()) != 0) fprintf(stderr, "asim isa tracer: cannot create %s\n", d);
+    fclose(fopen((dir + "/kernelslist.g").c_str(), "w"));
+    FILE* f = fopen((dir + "/stats.csv").c_str(), "w");
+    if (f) {
+      fprintf(f, "kernel id, kernel name, grid_dim, block_dim, #warp insts, #thread insts\n");
+      fclose(f);
+    }
+    if (const char* s = getenv("ASIM_TRACE_KERNEL_START")) kstart = atol(s);
+    if (const char* s = getenv("ASIM_TRACE_KERNEL_END")) kend = atol(s);
+    if (const char* s = getenv("ASIM_TRACE_BUF_MB")) buf_bytes = (size_t)atol(s) << 20;
+    std::string mp;
+    if (const char* s = getenv("ASIM_ISA_MAP")) {
+      mp = s;
+    } else {
+      char exe[4096];
+      ssize_t n = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+      if (n > 0) {
+        exe[n] = 0;
+        mp = std::string(exe) + ".asimisa";
+      }
+    }
+    load_map(mp);
+  }
+
+  void load_map(const std::string& path) {
+    std::ifstream in(path);
+    if (!in) {
+      fprintf(stderr, "asim isa tracer: no instruction map %s (tracing disabled)\n", path.c_str());
+      enabled = false;
+      return;
+    }
+    std::string line;
+    KMap* k = nullptr;
+    std::vector<SInst>* seg = nullptr;
+    while (std::getline(in, line)) {
+      if (line.rfind("ASIMISA", 0) == 0) {
+        std::istringstream hs(line);
+        std::string tag;
+        int ver = 0;
+        uint32_t cu = 0;
+        hs >> tag >> ver >> cu;
+        if (cu) kChunkUnits = cu;
+        continue;
+      }
+      if (line.empty()) continue;
+      std::istringstream ss(line);
+      if (line[0] == 'K' && line[1] == ' ') {
+        std::string tag, name;
+        size_t nseg = 0, nmem = 0;
+        ss >> tag >> name >> nseg >> nmem;
+        k = &maps[name];
+        k->segs.assign(nseg, {});
+        ss >> k->lds >> k->vgprs;
+        seg = nullptr;
+      } else if (line[0] == 'S' && line[1] == ' ') {
+        std::string tag;
+        size_t id = 0, n = 0;
+        ss >> tag >> id >> n;
+        if (k && id >= 1 && id <= k->segs.size()) seg = &k->segs[id - 1];
+      } else if (seg) {
+        SInst si;
+        std::string pc;
+        ss >> pc >> si.mem;
+        si.pc = (uint32_t)strtoul(pc.c_str(), nullptr, 16);
+        // rest of the line: ndst dsts mnemonic nsrc srcs width
+        std::string rest;
+        std::getline(ss, rest);
+        size_t b = rest.find_first_not_of(' ');
+        rest = b == std::string::npos ? "" : rest.substr(b);
+        size_t e = rest.find_last_of(' ');
+        si.width = atoi(rest.c_str() + e + 1);
+        si.text = rest.substr(0, e);
+        seg->push_back(si);
+      }
+    }
+  }
+
+  bool traced(long id) const { return enabled && id >= kstart && id <= kend; }
+
+  void append(const std::string& file, const std::string& s) {
+    FILE* f = fopen((dir + "/" + file).c_str(), "a");
+    if (f) {
+      fprintf(f, "%s\n", s.c_str());
+      fclose(f);
+    }
+  }
+};
+
+Tracer& T() {
+  static Tracer t;
+  return t;
+}
+
+struct Wave {
+  std::vector<std::pair<uint32_t, uint32_t>> chunks;  // (seq, chunk index)
+};
+
+void write_kernel(Tracer& t, long id, const std::string& name, const KMap& km, dim3 g, dim3 b, size_t shmem,
+                  const std::vector<uint8_t>& host, uint32_t used) {
+  // group chunks by wave: (wg z, wg y, wg x, packed tid of the first lane)
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, Wave> waves;
+  const size_t cb = (size_t)kChunkUnits * 16;
+  for (uint32_t c = 0; c < used; ++c) {
+    const uint32_t* u = reinterpret_cast<const uint32_t*>(host.data() + c * cb);
+    if ((u[0] & kTagChunk) != kTagChunk) continue;
+    waves[std::make_tuple(u[3], u[2], u[1], u[4])].chunks.push_back({u[0] & ~kTagChunk, c});
+  }
+  const std::string fn = "kernel-" + std::to_string(id) + ".traceg";
+  FILE* f = fopen((t.dir + "/" + fn).c_str(), "w");
+  if (!f) {
+    fprintf(stderr, "asim isa tracer: cannot write %s\n", fn.c_str());
+    exit(3);
+  }
+  fprintf(f, "-kernel name = %s\n-kernel id = %ld\n-grid dim = (%u,%u,%u)\n-block dim = (%u,%u,%u)\n", name.c_str(),
+          id, g.x, g.y, g.z, b.x, b.y, b.z);
+  fprintf(f, "-shmem = %zu\n-nregs = %u\n-binary version = 950\n-wavefront size = 64\n-hip stream id = 0\n",
+          shmem + km.lds, km.vgprs);
+  fprintf(f, "-shmem base_addr = 0x0\n-local mem base_addr = 0x0\n-rocprofiler version = asim_isa_tracer\n");
+  fprintf(f, "-accelsim tracer version = 4\n\n");
+  fprintf(f, "#traces format = PC mask dest_num reg_dests opcode src_num reg_srcs mem_width mem_addresses\n\n");
+  uint64_t winsts = 0, tinsts = 0;
+  long bad = 0;
+  std::vector<std::string> lines;
+  auto it = waves.begin();
+  while (it != waves.end()) {
+    const uint32_t cz = std::get<0>(it->first), cy = std::get<1>(it->first), cx = std::get<2>(it->first);
+    fprintf(f, "#BEGIN_TB\n\nthread block = %u,%u,%u\n\n", cx, cy, cz);
+    // waves of this CTA in wave-index order
+    std::vector<std::pair<uint32_t, Wave*>> ws;
+    for (; it != waves.end() && std::get<0>(it->first) == cz && std::get<1>(it->first) == cy &&
+           std::get<2>(it->first) == cx;
+         ++it) {
+      const uint32_t p = std::get<3>(it->first);
+      const uint32_t tx = p & 0x3ff, ty = (p >> 10) & 0x3ff, tz = (p >> 20) & 0x3ff;
+      const uint32_t flat = tx + ty * b.x + tz * b.x * b.y;
+      ws.push_back({flat / 64, &it->second});
+    }
+    std::sort(ws.begin(), ws.end(), [](auto& x, auto& y) { return x.first < y.first; });
+    for (auto& w : ws) {
+      std::sort(w.second->chunks.begin(), w.second->chunks.end());
+      lines.clear();
+      // flatten the wave's records
+      std::vector<const uint32_t*> recs;
+      for (auto& ch : w.second->chunks) {
+        const uint32_t* base = reinterpret_cast<const uint32_t*>(host.data() + ch.second * cb);
+        uint32_t u = 2;
+        while (u < kChunkUnits) {
+          const uint32_t* r = base + u * 4;
+          if (r[0] == 0) break;
+          recs.push_back(r);
+          u += (r[0] & kTagMem) ? 33 : 1;
+        }
+      }
+      size_t ri = 0;
+      char buf[160];
+      while (ri < recs.size()) {
+        const uint32_t* r = recs[ri++];
+        if (r[0] & kTagMem) {  // a memory record outside its segment: stream out of sync
+          ++bad;
+          continue;
+        }
+        const uint32_t sid = r[0];
+        if (sid == 0 || sid > km.segs.size()) {
+          ++bad;
+          continue;
+        }
+        const uint64_t exec = (uint64_t)r[2] | (uint64_t)r[3] << 32;
+        for (const SInst& si : km.segs[sid - 1]) {
+          uint64_t m = exec;
+          const uint64_t* addrs = nullptr;
+          if (si.mem >= 0) {
+            if (ri < recs.size() && recs[ri][0] == (kTagMem | (uint32_t)si.mem)) {
+              const uint32_t* mr = recs[ri++];
+              m = (uint64_t)mr[2] | (uint64_t)mr[3] << 32;
+              addrs = reinterpret_cast<const uint64_t*>(mr + 4);
+            } else {
+              ++bad;
+            }
+          }
+          std::string ln;
+          snprintf(buf, sizeof(buf), "%04x %016llx ", si.pc, (unsigned long long)m);
+          ln = buf;
+          ln += si.text;
+          if (si.mem >= 0 && si.width) {
+            snprintf(buf, sizeof(buf), " %d 0", si.width);
+            ln += buf;
+            if (addrs)
+              for (int l = 0; l < 64; ++l)
+                if ((m >> l) & 1ull) {
+                  snprintf(buf, sizeof(buf), " 0x%llx", (unsigned long long)addrs[l]);
+                  ln += buf;
+                }
+          } else {
+            ln += " 0";
+          }
+          lines.push_back(ln);
+          tinsts += (uint64_t)__builtin_popcountll(m);
+        }
+      }
+      winsts += lines.size();
+      fprintf(f, "warp = %u\ninsts = %zu\n", w.first, lines.size());
+      for (auto& l : lines) fprintf(f, "%s\n", l.c_str());
+    }
+    fprintf(f, "\n#END_TB\n\n");
+  }
+  fclose(f);
+  if (bad) fprintf(stderr, "asim isa tracer: kernel %ld (%s): %ld records out of sequence\n", id, name.c_str(), bad);
+  t.append("kernelslist.g", fn);
+  char s[512];
+  snprintf(s, sizeof(s), "kernel-%ld, %s, (%u,%u,%u), (%u,%u,%u), %llu, %llu", id, name.c_str(), g.x, g.y, g.z, b.x,
+           b.y, b.z, (unsigned long long)winsts, (unsigned long long)tinsts);
+  t.append("stats.csv", s);
+}
+
+}  // namespace
+
+extern "C" {
+
+void** __hipRegisterFatBinary(const void* data) {
+  using F = void** (*)(const void*);
+  static F real = (F)dlsym(RTLD_NEXT, "__hipRegisterFatBinary");
+  void** h = real(data);
+  Tracer& t = T();
+  using RV = void (*)(void**, void*, char*, char*, int, size_t, int, int);
+  static RV regvar = (RV)dlsym(RTLD_NEXT, "__hipRegisterVar");
+  // the probes' control block: one per code object, registered like a
+  // compiler-emitted __device__ variable
+  Ctl* shadow = new Ctl();
+  static char nm[] = "__asim_tctl";
+  regvar(h, shadow, nm, nm, 0, sizeof(Ctl), 0, 0);
+  std::lock_guard<std::mutex> g(t.mu);
+  t.shadows.push_back(shadow);
+  return h;
+}
+
+void __hipRegisterFunction(void** modules, const void* hostFunction, char* deviceFunction, const char* deviceName,
+                           unsigned int threadLimit, uint3* tid, uint3* bid, dim3* blockDim, dim3* gridDim,
+                           int* wSize) {
+  using F = void (*)(void**, const void*, char*, const char*, unsigned int, uint3*, uint3*, dim3*, dim3*, int*);
+  static F real = (F)dlsym(RTLD_NEXT, "__hipRegisterFunction");
+  {
+    Tracer& t = T();
+    std::lock_guard<std::mutex> g(t.mu);
+    t.names[hostFunction] = deviceName ? deviceName : deviceFunction;
+  }
+  real(modules, hostFunction, deviceFunction, deviceName, threadLimit, tid, bid, blockDim, gridDim, wSize);
+}
+
+hipError_t hipMemcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  using F = hipError_t (*)(void*, const void*, size_t, hipMemcpyKind);
+  static F real = (F)dlsym(RTLD_NEXT, "hipMemcpy");
+  hipError_t e = real(dst, src, bytes, kind);
+  Tracer& t = T();
+  if (t.enabled && kind == hipMemcpyHostToDevice) {
+    char s[96];
+    snprintf(s, sizeof(s), "MemcpyHtoD,0x%016llx,%zu", (unsigned long long)(uintptr_t)dst, bytes);
+    std::lock_guard<std::mutex> g(t.mu);
+    t.append("kernelslist.g", s);
+  }
+  return e;
+}
+
+hipError_t hipLaunchKernel(const void* f, dim3 g, dim3 b, void** args, size_t shmem, hipStream_t st) {
+  using F = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t);
+  static F real = (F)dlsym(RTLD_NEXT, "hipLaunchKernel");
+  Tracer& t = T();
+  if (!t.enabled) return real(f, g, b, args, shmem, st);
+  std::lock_guard<std::mutex> lk(t.mu);
+  const long id = ++t.next_id;
+  auto nit = t.names.find(f);
+  const std::string name = nit == t.names.end() ? "" : nit->second;
+  auto mit = t.maps.find(name);
+  if (!t.traced(id) || mit == t.maps.end()) {
+    if (t.traced(id)) fprintf(stderr, "asim isa tracer: kernel %s has no instrumentation map\n", name.c_str());
+    return real(f, g, b, args, shmem, st);
+  }
+  int dev = 0;
+  RT_HIP(hipGetDevice(&dev));
+  Tracer::DevBuf& db = t.bufs[dev];
+  if (!db.ptr) {
+    RT_HIP(hipMalloc(&db.ptr, t.buf_bytes));
+    RT_HIP(hipMemset(db.ptr, 0, t.buf_bytes));
+  } else if (db.last_used) {
+    RT_HIP(hipMemset(db.ptr, 0, (size_t)db.last_used * kChunkUnits * 16));
+  }
+  Ctl c{};
+  c.buf = (uint64_t)(uintptr_t)db.ptr;
+  c.n_chunks = (uint32_t)(t.buf_bytes / ((size_t)kChunkUnits * 16));
+  for (Ctl* sh : t.shadows) RT_HIP(hipMemcpyToSymbol((const void*)sh, &c, sizeof(c), 0, hipMemcpyHostToDevice));  // the shadow itself, not the template overload (&sh)
+  hipError_t e = real(f, g, b, args, shmem, st);
+  if (e != hipSuccess) return e;
+  RT_HIP(hipStreamSynchronize(st));
+  uint32_t used = 0;
+  for (Ctl* sh : t.shadows) {
+    Ctl r{};
+    RT_HIP(hipMemcpyFromSymbol(&r, (const void*)sh, sizeof(r), 0, hipMemcpyDeviceToHost));
+    used = std::max(used, r.next_chunk);
+  }
+  if (used > c.n_chunks) {
+    fprintf(stderr, "asim isa tracer: kernel %s needs %u chunks of %u KB, buffer holds %u; raise ASIM_TRACE_BUF_MB\n",
+            name.c_str(), used, kChunkUnits / 64, c.n_chunks);
+    exit(4);
+  }
+  db.last_used = used;
+  std::vector<uint8_t> host((size_t)used * kChunkUnits * 16);
+  if (used) RT_HIP(hipMemcpy(host.data(), db.ptr, host.size(), hipMemcpyDeviceToHost));
+  write_kernel(t, id, name, mit->second, g, b, shmem, host, used);
+  return e;
+}
+
+}  // extern "C"
