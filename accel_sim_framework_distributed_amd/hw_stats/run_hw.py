@@ -47,6 +47,7 @@ def main(argv=None) -> int:
     ap.add_argument("-R", "--repeat", type=int, default=4, help="runs per app (the correlator burns the first)")
     ap.add_argument("-c", "--counters", action="append", default=[],
                     help="comma separated PMC counters for an extra pass (repeatable: one pass each)")
+    ap.add_argument("--counter_repeat", type=int, default=1, help="runs per counter pass (counts are deterministic)")
     ap.add_argument("--counter_groups", action="store_true",
                     help="add the correlator's counter passes (plotting/correlate.py COUNTER_GROUPS)")
     ap.add_argument("-o", "--out", default=os.path.join(common.REPO_ROOT, "hw_run", "rocprof", "MI355X"))
@@ -71,7 +72,7 @@ def main(argv=None) -> int:
             base = os.path.join(out, app, common.argfoldername(args))
             passes = [("run", "")] + [(f"ctr{g}", c) for g, c in enumerate(groups)]
             for tag, ctr in passes:
-                for r in range(o.repeat):
+                for r in range(o.repeat if not ctr else o.counter_repeat):
                     d = os.path.join(base, f"{tag}_{r}")
                     cmd = ["timeout", "-k", "10", str(o.timeout)] + rocprof_cmd(d, argv_app, ctr)
                     print(" ".join(shlex.quote(c) for c in cmd), flush=True)

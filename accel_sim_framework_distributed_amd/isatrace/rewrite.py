@@ -300,22 +300,23 @@ class Probe:
         return out
 
     def guarded(self, n: int, need: int, body: List[str], stubs: List[str]) -> List[str]:
-        """SCC save, space check (out-of-line chunk allocation), body, SCC restore."""
+        """SCC save, space check, chunk allocation (in line, jumped over when
+        the chunk has room: every probe branch stays short however large the
+        kernel), body, SCC restore."""
         out = [f"s_cselect_b32 {self.scc}, 1, 0",
                f"s_add_u32 {self.t}, {self.cur}, {need}",
                f"s_cmp_gt_u32 {self.t}, {self.end}",
-               f"s_cbranch_scc1 .Lasim{self.tag}_alloc_{n}",
-               f".Lasim{self.tag}_ret_{n}:"]
+               f"s_cbranch_scc0 .Lasim{self.tag}_ret_{n}"]
+        out += self.alloc_stub(n)
+        out += [f".Lasim{self.tag}_ret_{n}:"]
         out += body
         out += [f".Lasim{self.tag}_skip_{n}:",
                 f"s_cmp_lg_u32 {self.scc}, 0"]
-        stubs += self.alloc_stub(n)
         return out
 
     def alloc_stub(self, n: int) -> List[str]:
         h = self.h
-        out = [f".Lasim{self.tag}_alloc_{n}:",
-               f"s_mov_b64 {self.tx}, exec",
+        out = [f"s_mov_b64 {self.tx}, exec",
                "s_mov_b64 exec, 1",
                f"v_mov_b32_e32 {h[0]}, 1",
                f"v_mov_b32_e32 {self.off}, 8",
@@ -675,6 +676,24 @@ def assign_pcs(maps: Sequence[KernelMap], disasm: str) -> None:
                 ins.pc = 4 * i
 
 
+def trace_mnemonic(ins: Inst) -> str:
+    """Trace opcode of an instruction: the mnemonic, with s_waitcnt's counts
+    attached ('s_waitcnt.vm1.lgkm0'; a counter it does not name is not
+    waited for) so the simulator can model count-based waits."""
+    if ins.mnem != "s_waitcnt":
+        return ins.mnem
+    vm = re.search(r"vmcnt\((\d+)\)", ins.text)
+    lg = re.search(r"lgkmcnt\((\d+)\)", ins.text)
+    name = "s_waitcnt"
+    if vm:
+        name += f".vm{vm.group(1)}"
+    if lg:
+        name += f".lgkm{lg.group(1)}"
+    if not vm and not lg:
+        name += ".vm255.lgkm255" if "expcnt" in ins.text else ""
+    return name
+
+
 def write_map(maps: Sequence[KernelMap]) -> str:
     """Text map read by csrc/tracer/isa_runtime.cc."""
     out = [f"ASIMISA 1 {CHUNK_UNITS}"]
@@ -686,6 +705,6 @@ def write_map(maps: Sequence[KernelMap]) -> str:
                 ins = km.insts[i]
                 dst, src = reg_operands(ins)
                 w = mem_width(ins.mnem) if ins.mem_id >= 0 else 0
-                body = " ".join([str(len(dst))] + dst + [ins.mnem, str(len(src))] + src)
+                body = " ".join([str(len(dst))] + dst + [trace_mnemonic(ins), str(len(src))] + src)
                 out.append(f"{ins.pc:x} {ins.mem_id} {body} {w}")
     return "\n".join(out) + "\n"

@@ -101,6 +101,8 @@ const OptDef kOptions[] = {
     {"-gpgpu_scheduler", 's', "gto", "warp scheduler policy lrr|gto|two_level_active|old|rrr|warp_limiting"},
     {"-gpgpu_concurrent_kernel_sm", 'b', "0", "concurrent kernels per SM"},
     {"-gpgpu_perfect_inst_const_cache", 'b', "0", "perfect instruction/constant cache"},
+    {"-gpgpu_inst_prefetch_lines", 'u', "0",
+     "sequential instruction prefetch: code lines fetched ahead on an L1I miss or on entering a line (0 = off)"},
     {"-gpgpu_inst_fetch_throughput", 'i', "1", "fetch throughput"},
     {"-gpgpu_reg_file_port_throughput", 'i', "1", "register file port throughput"},
     {"-gpgpu_simd_model", 'i', "1", "SIMD model"},
@@ -678,6 +680,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.unified_l1_kb = (uint32_t)r.getu("-gpgpu_unified_l1d_size");
   c.l1_write_ratio = (uint32_t)r.getu("-gpgpu_l1_cache_write_ratio");
   c.perfect_icache = r.getb("-gpgpu_perfect_inst_const_cache") ? 1u : 0u;
+  c.inst_prefetch = (uint32_t)std::min<uint64_t>(r.getu("-gpgpu_inst_prefetch_lines"), kMaxIL1Mshr);
   c.il1 = parse_cache_geom(r.gets("-gpgpu_cache:il1"), true);
   if (!c.il1.disabled) {
     // the tag array lives in LDS next to the SM state: keep the associativity,

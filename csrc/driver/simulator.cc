@@ -667,6 +667,9 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
     if (acc) print("\tL1I_total_cache_miss_rate = %.4lf\n", (double)ic[IL1_MISS] / (double)acc);
     print("\tL1I_total_cache_pending_hits = %llu\n", (unsigned long long)ic[IL1_MSHR_HIT]);
     print("\tL1I_total_cache_reservation_fails = %llu\n", (unsigned long long)ic[IL1_RES_FAIL]);
+    uint64_t pf = 0;
+    for (auto& st : prev_sm_) pf += st.il1_prefetch;
+    if (cfg_.inst_prefetch) print("\tL1I_total_cache_prefetches = %llu\n", (unsigned long long)pf);
   }
   print("gpgpu_n_shmem_bank_access = %llu\n", (unsigned long long)shm);
   print("gpgpu_n_shmem_bkconflict = %llu\n", (unsigned long long)shm_conf);

@@ -184,6 +184,9 @@ struct SmView {
   SV_WARP(w_inflight);
   SV_WARP(w_stores);
   SV_WARP(w_loads);
+  SV_REF(w_wait);
+  SV_REF(w_slot_lds);
+  SV_REF(w_lds_st);
   WarpSb w_sb;
   SV_WARP(w_slot_used);
   SV_REF(w_slot_pend);
@@ -270,7 +273,8 @@ struct SmView {
   X(cta_nexit) X(sched_last) X(w_iline)
 
   __device__ __forceinline__ explicit SmView(B& b)
-      : base(b), cycle(b.cycle), w_slot_pend(b.w_slot_pend),
+      : base(b), cycle(b.cycle), w_wait(b.w_wait), w_slot_lds(b.w_slot_lds), w_lds_st(b.w_lds_st),
+        w_slot_pend(b.w_slot_pend),
         w_slot_dst(b.w_slot_dst), cta_id(b.cta_id),
         idoc_inst(b.idoc_inst), oc_inst(b.oc_inst),
         wb_cnt(b.wb_cnt), wb(b.wb), hit_cnt(b.hit_cnt), hit(b.hit), l1(b.l1), mshr(b.mshr),

@@ -161,6 +161,7 @@ struct SimCfg {
   //      -gpgpu_perfect_inst_const_cache bypasses it, shader.cc:990) ----
   CacheGeom il1;
   uint32_t perfect_icache;
+  uint32_t inst_prefetch;   // L1I sequential prefetch depth in lines (CDNA SQC fetches ahead)
   // ---- interconnect ----
   uint32_t icnt_latency;   // core cycles (== epoch length, the PDES lookahead)
   uint32_t flit_size;

@@ -137,6 +137,7 @@ struct SMStats {
   uint64_t mf_lat_sum, mf_lat_n, mf_lat_max;
   uint64_t mf_lat_hist[16];    // log2 buckets: [2^i, 2^(i+1)) cycles
   uint64_t il1[4];             // instruction cache: hit, miss, mshr (pending) hit, reservation fail
+  uint64_t il1_prefetch;       // code lines requested by the sequential prefetcher
   uint64_t dual_issued;        // second instructions issued in the same cycle by one warp
   uint64_t l1_wb;              // dirty L1 lines written back on eviction
   uint64_t l1_wb_lost;         // write-backs dropped with the injection queue full (must stay 0)
@@ -175,9 +176,12 @@ struct alignas(16) SMState {
   uint8_t w_inflight[kMaxWarps];
   uint16_t w_stores[kMaxWarps];  // outstanding store acks
   uint16_t w_loads[kMaxWarps];   // outstanding load slots in use
+  uint16_t w_wait[kMaxWarps];    // counts of the pending s_waitcnt: vm | lgkm << 8 (0xff: not waited for)
   uint64_t w_sb[kMaxWarps][4];   // scoreboard: pending destination registers
   uint8_t w_slot_used[kMaxWarps];  // bitmask of used load slots
-  uint8_t w_pad[kMaxWarps][3];
+  uint8_t w_slot_lds[kMaxWarps];   // load slots holding an LDS load (lgkmcnt, not vmcnt)
+  uint8_t w_lds_st[kMaxWarps];     // LDS stores in flight (lgkmcnt)
+  uint8_t w_pad[kMaxWarps];
   uint16_t w_slot_pend[kMaxWarps][kLoadSlots];
   uint8_t w_slot_dst[kMaxWarps][kLoadSlots][2];
   // ---- CTAs ----
@@ -388,9 +392,24 @@ SIM_HDI void sm_load_slot_done(S& s, uint32_t w, uint32_t slot, uint64_t now) {
   sbc(s.w_sb, w, s.w_slot_dst[w][slot][1]);
   s.sadd(SK(rf_writes), (s.w_slot_dst[w][slot][0] != 0) + (s.w_slot_dst[w][slot][1] != 0));
   s.w_slot_used[w] &= (uint8_t)~(1u << slot);
+  s.w_slot_lds[w] &= (uint8_t)~(1u << slot);
   s.w_loads[w]--;
   s.w_inflight[w]--;
   s.last_progress = now;
+}
+
+// CDNA s_waitcnt: the wave may go on once at most vm vector-memory operations
+// (global/local loads and store acknowledgements) and at most lgkm LDS
+// operations are outstanding.  The hardware counters retire in issue order;
+// here completions may come back out of order, so a younger fast access can
+// release a count-based wait early.
+template <class S>
+SIM_HDI bool waitcnt_met(S& s, uint32_t w) {
+  const uint32_t wt = s.w_wait[w];
+  const uint32_t lds_ld = (uint32_t)__builtin_popcount((uint32_t)s.w_slot_lds[w]);
+  const uint32_t vm = (uint32_t)s.w_loads[w] - lds_ld + (uint32_t)s.w_stores[w];
+  const uint32_t lgkm = lds_ld + (uint32_t)s.w_lds_st[w];
+  return vm <= (wt & 0xffu) && lgkm <= (wt >> 8);
 }
 
 // L1-hit / shared-memory completions due this cycle
@@ -404,6 +423,7 @@ SIM_HDI void sm_hit_complete(S& s, uint64_t now) {
       if (--s.w_slot_pend[e.warp][e.slot] == 0) sm_load_slot_done(s, e.warp, e.slot, now);
     } else {
       s.w_inflight[e.warp]--;
+      s.w_lds_st[e.warp]--;
       s.last_progress = now;
     }
   }
@@ -564,6 +584,28 @@ SIM_HDI void il1_fill(S& s, const SimCfg& c, uint64_t line) {
 
 // probe the instruction cache for warp w's next fetch; true = instructions
 // available this cycle
+// sequential instruction prefetch: request the next inst_prefetch code lines
+// that are neither cached nor pending (no waiter; the fill path is the demand
+// one), as far as free MSHRs and the injection port allow
+template <class P, class S>
+SIM_HDI void il1_prefetch(S& s, const SimCfg& c, uint64_t line) {
+  const CacheGeom& g = c.il1;
+  for (uint32_t k = 1; k <= c.inst_prefetch; ++k) {
+    const uint64_t l = line + 128ull * k;
+    if (il1_find<P>(s, g, cache_set_index(g, l), l) >= 0) continue;
+    if (P::find_first((int)g.mshr_entries, [&](int i) -> bool { return s.imshr[i].valid && s.imshr[i].line == l; }) >= 0)
+      continue;
+    const int mi = P::find_first((int)g.mshr_entries, [&](int i) -> bool { return !s.imshr[i].valid; });
+    if (mi < 0 || !sm_can_send(s, c)) return;
+    s.imshr[mi].valid = 1;
+    s.imshr[mi].line = l;
+    s.imshr[mi].merges = 0;
+    s.imshr[mi].t_issue = 0;
+    sm_send(s, c, P_RD, l, 0xf, 128, 0x40000000u | (uint32_t)mi);
+    s.sadd(SK(il1_prefetch), 1);
+  }
+}
+
 template <class P, class S>
 SIM_HDI bool il1_fetch(S& s, const SimCfg& c, const TInst* insts, uint32_t w) {
   const CacheGeom& g = c.il1;
@@ -574,6 +616,7 @@ SIM_HDI bool il1_fetch(S& s, const SimCfg& c, const TInst* insts, uint32_t w) {
   if (way >= 0) {
     if (g.repl == REPL_LRU) s.il1[set * g.assoc + way].lru = ++s.l1_stamp;
     s.sadd(SK(il1) + (IL1_HIT), 1);
+    if (c.inst_prefetch && ((kProgramMemStart + pc) & 127u) < 8u) il1_prefetch<P>(s, c, line);  // entering a line
     return true;
   }
   int mi = P::find_first((int)g.mshr_entries, [&](int i) -> bool { return s.imshr[i].valid && s.imshr[i].line == line; });
@@ -590,6 +633,7 @@ SIM_HDI bool il1_fetch(S& s, const SimCfg& c, const TInst* insts, uint32_t w) {
     s.imshr[mi].t_issue = 0;
     sm_send(s, c, P_RD, line, 0xf, 128, 0x40000000u | (uint32_t)mi);
     s.sadd(SK(il1) + (IL1_MISS), 1);
+    if (c.inst_prefetch) il1_prefetch<P>(s, c, line);
   }
   s.w_flags[w] |= WF_IMISS;
   s.w_iline[w] = line;
@@ -1069,7 +1113,8 @@ SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32
     return -1;
   }
   if (in.flags & F_WAITCNT) {
-    if (s.w_stores[w] || s.w_loads[w]) {
+    s.w_wait[w] = in.lat;
+    if (!waitcnt_met(s, w)) {
       s.w_flags[w] |= WF_WAITCNT;
       s.n_wait_flags++;
     }
@@ -1099,10 +1144,12 @@ SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32
       ri.space = S_SHARED;
       ri.width = 1;
     }
+    if (ri.space == S_SHARED) s.w_slot_lds[w] = (uint8_t)(s.w_slot_lds[w] | (1u << sl));
   } else if (in.cls == OC_STORE && in.space != S_SHARED && in.width == 0) {
     ri.space = S_SHARED;
     ri.width = 1;
   }
+  if (in.cls == OC_STORE && ri.space == S_SHARED) s.w_lds_st[w]++;
   s.idoc_inst[kk] = ri;
   s.idoc_meta[kk] = idoc_pack(w, lslot, ++s.age_ctr);
   s.idoc_mask |= 1ull << kk;
@@ -1288,7 +1335,7 @@ SIM_HDI void sm_retire(S& s, const SmCtx& x, uint64_t now) {
       uint8_t f = s.w_flags[w];
       uint32_t r = 0;
       if ((f & WF_MEMBAR) && s.w_stores[w] == 0) { f = f & (uint8_t)~WF_MEMBAR; ++r; }
-      if ((f & WF_WAITCNT) && s.w_stores[w] == 0 && s.w_loads[w] == 0) { f = f & (uint8_t)~WF_WAITCNT; ++r; }
+      if ((f & WF_WAITCNT) && waitcnt_met(s, w)) { f = f & (uint8_t)~WF_WAITCNT; ++r; }
       if (r) s.w_flags[w] = f;
       return r != 0;
     });
@@ -1350,6 +1397,9 @@ SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id)
     s.w_stores[w] = 0;
     s.w_loads[w] = 0;
     s.w_slot_used[w] = 0;
+    s.w_slot_lds[w] = 0;
+    s.w_lds_st[w] = 0;
+    s.w_wait[w] = 0;
     sbz(s.w_sb, w);
   });
   P::sync();
@@ -1441,7 +1491,7 @@ SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, const TInst* insts,
     const bool drained = s.w_head[w] >= s.w_end[w] && s.w_ibuf[w] == 0;
     if (drained && s.w_inflight[w] == 0 && s.w_stores[w] == 0 && s.w_loads[w] == 0) return true;  // retire
     if ((f & WF_MEMBAR) && s.w_stores[w] == 0) return true;
-    if ((f & WF_WAITCNT) && s.w_stores[w] == 0 && s.w_loads[w] == 0) return true;
+    if ((f & WF_WAITCNT) && waitcnt_met(s, w)) return true;
     return warp_can_issue(s, c, insts, w, nsched, s.idoc_mask);  // issue
   });
   return act ? t : nx;

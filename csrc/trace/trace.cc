@@ -242,7 +242,9 @@ OpInfo decode_cdna(const std::string& op0) {
   } else if (starts(m, "s_nop") || starts(m, "s_sleep") || starts(m, "s_setprio") || starts(m, "s_sched")) {
     o.cls = OC_NOP;
   } else if (starts(m, "s_")) {
-    o.cls = OC_INTP;  // scalar ALU
+    // scalar ALU: its own pipe (the CU's scalar unit), specialized unit 8 of
+    // the config (-specialized_unit_8 ... SALU); on the SP pipe without one
+    o.cls = OC_SPEC8;
   } else if (starts(m, "v_exp") || starts(m, "v_log") || starts(m, "v_rcp") || starts(m, "v_rsq") ||
              starts(m, "v_sqrt") || starts(m, "v_sin") || starts(m, "v_cos")) {
     o.cls = OC_SFU;
@@ -287,6 +289,35 @@ struct Tok {
     return true;
   }
 };
+
+// CDNA register files share the scoreboard's 255 ids without aliasing each
+// other: v0-v127 -> 1..128, a0-a31 -> 129..160, s0-s93 -> 161..254
+// (higher numbers fold modulo each range)
+uint8_t reg_of_cdna(const std::string& t) {
+  if (t.size() < 2 || !(t[1] >= '0' && t[1] <= '9')) return 0;
+  const long r = atol(t.c_str() + 1);
+  if (r < 0) return 0;
+  switch (t[0]) {
+    case 'v': return (uint8_t)(1 + r % 128);
+    case 'a': return (uint8_t)(129 + r % 32);
+    case 's': return (uint8_t)(161 + r % 94);
+    default: return 0;
+  }
+}
+
+// s_waitcnt counts carried in the mnemonic by the ISA tracer
+// ("s_waitcnt.vm<N>.lgkm<M>", a missing counter is not waited for; a bare
+// s_waitcnt waits for everything): packed as vm | lgkm << 8 into TInst::lat
+uint16_t waitcnt_counts(const std::string& op) {
+  const size_t d = op.find('.');
+  if (d == std::string::npos) return 0;
+  uint32_t vm = 0xff, lgkm = 0xff;
+  size_t p = op.find(".vm", d);
+  if (p != std::string::npos) vm = (uint32_t)std::min(254L, atol(op.c_str() + p + 3));
+  p = op.find(".lgkm", d);
+  if (p != std::string::npos) lgkm = (uint32_t)std::min(254L, atol(op.c_str() + p + 5));
+  return (uint16_t)(vm | lgkm << 8);
+}
 
 uint8_t reg_of(const std::string& t) {
   // R12 / v12 / s3 / a7 -> 13 ; RZ / R255 -> 0 (no dependency)
@@ -535,6 +566,7 @@ HostKernel load_kernel_text(const std::string& path) {
     if (h.trace_version && h.trace_version < 3) {
       for (int i = 0; i < 4; ++i) t.dec(dv);
     }
+    const bool cdna = h.binary_version >= 900;
     uint64_t pc = 0, mask = 0;
     t.hex(pc);
     t.hex(mask);
@@ -546,7 +578,7 @@ HostKernel load_kernel_text(const std::string& path) {
     t.dec(nd);
     for (long long i = 0; i < nd; ++i) {
       t.next(tok);
-      if (i < 2) in.dst[i] = reg_of(tok);
+      if (i < 2) in.dst[i] = cdna ? reg_of_cdna(tok) : reg_of(tok);
     }
     std::string opstr;
     t.next(opstr);
@@ -554,7 +586,7 @@ HostKernel load_kernel_text(const std::string& path) {
     t.dec(ns);
     for (long long i = 0; i < ns; ++i) {
       t.next(tok);
-      if (i < 5) in.src[i] = reg_of(tok);
+      if (i < 5) in.src[i] = cdna ? reg_of_cdna(tok) : reg_of(tok);
     }
     long long mw = 0;
     t.dec(mw);
@@ -625,6 +657,7 @@ HostKernel load_kernel_text(const std::string& path) {
     (void)ii;
     if (oi.half_ii) in.flags |= 0;  // applied by coalesce_kernel from the config
     in.lat = oi.half_ii ? 0x8000 : 0;  // marker consumed by coalesce_kernel
+    if (oi.flags & F_WAITCNT) in.lat = waitcnt_counts(opstr);
     k.insts.push_back(in);
     k.thread_insts += (uint64_t)__builtin_popcountll(mask);
     ++got;
@@ -879,6 +912,7 @@ ReadyKernel coalesce_kernel(const HostKernel& k, const SimCfg& c) {
   std::vector<uint32_t> bytes;
   for (auto& in : r.insts) {
     // latency / initiation interval from the config (per op class)
+    if (in.flags & F_WAITCNT) continue;  // lat holds the s_waitcnt counts
     const bool half = (in.lat & 0x8000) != 0;
     uint32_t cls = in.cls < OC_COUNT ? in.cls : OC_ALU;
     in.lat = c.lat[cls];

@@ -69,8 +69,43 @@ static void measure(const char* name, const char* flag, T seed, T y) {
   UB_CHECK(hipFree(sink));
 }
 
+// scalar ALU (the CU's scalar unit): a dependent s_add_u32 chain of one wave
+__global__ void salu_lat_kernel(uint32_t seed, uint32_t y, int iters, uint64_t* out, uint32_t* sink) {
+  uint32_t x = seed;
+  uint64_t t0 = ub_clock();
+  for (int i = 0; i < iters; i += 16) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) asm volatile("s_add_u32 %0, %0, %1" : "+s"(x) : "s"(y) : "scc");
+  }
+  uint64_t t1 = ub_clock();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  if (x == 0xdeadbeefu) sink[0] = x;
+}
+
+static void measure_salu() {
+  uint64_t* o;
+  uint32_t* sink;
+  UB_CHECK(hipMalloc(&o, 16));
+  UB_CHECK(hipMalloc(&sink, 16));
+  const int iters = 1 << 14;
+  uint64_t h = 0;
+  hipLaunchKernelGGL(salu_lat_kernel, dim3(1), dim3(64), 0, 0, 3u, 1664525u, iters, o, sink);
+  UB_CHECK(hipMemcpy(&h, o, 8, hipMemcpyDeviceToHost));
+  const double lat = (double)h / iters;
+  printf("%-6s latency %6.2f cycles (dependent chain, one wave)\n", "salu", lat);
+  char v[64];
+  const int l = std::max(1, (int)(lat + 0.5));
+  snprintf(v, sizeof(v), "%d,%d", l, 1);
+  ub_opt("-trace_opcode_latency_initiation_spec_op_8", v);
+  snprintf(v, sizeof(v), "1,4,%d,4,4,SALU", l);
+  ub_opt("-specialized_unit_8", v);
+  UB_CHECK(hipFree(o));
+  UB_CHECK(hipFree(sink));
+}
+
 int main() {
   UbDevice d;
+  measure_salu();
   measure<0, float>("fp32", "-trace_opcode_latency_initiation_sp", 1.0001f, 0.9999f);
   measure<1, double>("fp64", "-trace_opcode_latency_initiation_dp", 1.0001, 0.9999);
   measure<2, uint32_t>("int32", "-trace_opcode_latency_initiation_int", 3u, 1664525u);

@@ -28,13 +28,16 @@ int main(int argc, char** argv) {
   const double l1 = at(8), l2 = at(1024), mall = at(65536), hbm = at(4194304);
   printf("# l1 %.0f  l2 %.0f  mall %.0f  hbm %.0f cycles\n", l1, l2, mall, hbm);
   ub_opt("-gpgpu_l1_latency", (long long)(l1 + 0.5));
-  // The simulator's memory-side L2 (one slice per memory sub-partition) is
-  // mapped onto MI355X's memory-side Infinity Cache (MALL): freshly copied
-  // data lives there, and an "L2 hit" costs the MALL latency.  gpgpu-sim
-  // splits that into icnt + ROP delay; the ROP term is what is left after the
-  // L1 miss path and two icnt traversals.  The per-XCD L2 is reported only.
-  ub_opt("-gpgpu_l2_rop_latency", (long long)std::max(1.0, mall - l1 - 16));
-  ub_opt("-dram_latency", (long long)std::max(1.0, hbm - mall));
+  // The simulator's L2 stands for the per-XCD L2 that a kernel's re-used
+  // lines hit (its hit costs the XCD-L2 latency, split as gpgpu-sim does into
+  // the L1 miss path, two icnt traversals and the ROP delay), and an L2 miss
+  // for the memory-side Infinity Cache (MALL) that holds freshly copied data
+  // (hipMemcpy'd inputs of ordinary working sets sit there), so the DRAM
+  // latency is the MALL-over-L2 step.  Streams beyond the 256 MB MALL pay the
+  // HBM latency on hardware; that step is reported only.
+  ub_opt("-gpgpu_l2_rop_latency", (long long)std::max(1.0, l2 - l1 - 16));
+  ub_opt("-dram_latency", (long long)std::max(1.0, mall - l2));
+  printf("# hbm_over_mall_latency %.0f\n", hbm - mall);
   printf("# mall_hit_latency %.0f\n# xcd_l2_hit_latency %.0f\n", mall, l2);
   return 0;
 }

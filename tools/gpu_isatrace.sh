@@ -25,4 +25,5 @@ for spec in $APPS; do
     || { echo "$app verify failed"; exit 1; }
   cat $out/$app.verify.txt
   du -sh $out/$app
+  [ -n "$ISAT_KEEP" ] || rm -rf $out/$app $out/$app.pmc  # traces are large; keep the verdicts
 done
