@@ -57,15 +57,20 @@ def _parse():
 
 def _cycle_mae():
     """The latest committed MI355X cycle correlation, labelled as what it is:
-    an offline run (tools/gpu_correlate.sh: HIP apps timed with rocprofv3,
-    re-simulated), NOT measured by this bench run."""
-    p = os.path.join(ROOT, "profiles", "correlation", "mi355x_local_resim.json")
+    an offline run, NOT measured by this bench run (tools/gpu_correlate.sh:
+    the Rodinia-2.0-ft HIP suite traced by the automatic ISA tracer, timed
+    with rocprofv3, simulated by the MI355X cycle engine with the tuned
+    MI355X config; correlator semantics of plot-correlation.py)."""
+    p = os.path.join(ROOT, "profiles", "correlation", "rodinia_hip_isatrace_r2.json")
     try:
-        d = json.load(open(p))
-        return {"mae_pct": round(d["mae_pct"], 2), "apps": len(d["apps"]), "gpu": "MI355X",
-                "measured": "offline, not in this run", "engine": d.get("engine", "cpu"),
-                "run": d.get("run_id", os.path.basename(p)), "source": os.path.relpath(p, ROOT)}
-    except (OSError, ValueError, KeyError):
+        d = json.load(open(p))["Cycles"]
+        cfg, v = next(iter(d.items()))
+        return {"mae_pct": round(v["app_incl_noisy"]["mae"], 2), "apps": v["app_incl_noisy"]["n"],
+                "mae_pct_stable_apps": round(v["app"]["mae"], 2), "stable_apps": v["app"]["n"],
+                "pearson": round(v["app_incl_noisy"]["correl"], 4), "gpu": "MI355X", "config": cfg,
+                "traces": "automatic gfx950 ISA traces (isatrace)", "measured": "offline, not in this run",
+                "engine": "gpu", "source": os.path.relpath(p, ROOT)}
+    except (OSError, ValueError, KeyError, StopIteration):
         return None
 
 
