@@ -94,6 +94,22 @@ COMPONENT_GROUPS: Dict[str, List[str]] = {
 }
 
 
+# finer groups for the 24-kernel validation suite (csrc/apps/power_suite.hip):
+# 9 factors, each exercised by several kernels (a factor only one kernel
+# drives cannot be predicted leave-one-out)
+FINE_GROUPS: Dict[str, List[str]] = {
+    "idle_static": ["CONSTP", "IDLE_COREP", "STATICP"],
+    "frontend": ["IBP", "ICP", "SCHEDP", "PIPEP", "RFP"],
+    "valu": ["FPUP", "FP_MULP", "FP_DIVP", "INTP", "INT_MUL24P", "INT_MUL32P", "INT_MULP", "INT_DIVP"],
+    "fp64": ["DPUP", "DP_MULP", "DP_DIVP"],
+    "sfu": ["FP_SQRTP", "FP_LGP", "FP_SINP", "FP_EXP"],
+    "tensor": ["TENSORP", "TEXP"],
+    "lds": ["SHRDP"],
+    "cache": ["DCP", "TCP", "CCP", "L2CP", "NOCP"],
+    "dram": ["DRAMP", "MCP"],
+}
+
+
 def group_matrix(components: Sequence[str] = COMPONENTS, groups: Dict[str, List[str]] = COMPONENT_GROUPS):
     """(G x C) 0/1 matrix mapping group factors to component factors."""
     names = list(groups)
@@ -122,6 +138,11 @@ def leave_one_out_groups(A: np.ndarray, b: np.ndarray, **kw) -> np.ndarray:
         keep = np.arange(len(b)) != i
         out[i] = A[i] @ fit_groups(A[keep], b[keep], **kw)
     return out
+
+
+def group_factors(x: Sequence[float], groups: Dict[str, List[str]] = COMPONENT_GROUPS) -> Dict[str, float]:
+    names, M = group_matrix(groups=groups)
+    return {g: float(np.asarray(x)[list(M[i]).index(1.0)]) if M[i].any() else 1.0 for i, g in enumerate(names)}
 
 
 def mape(pred: Sequence[float], meas: Sequence[float]) -> Tuple[float, float]:

@@ -169,14 +169,87 @@ def run(work: str, out_xml: str, iters: int = 48) -> Dict:
     return summary
 
 
+def simulate_trace_power(kernelslist: str, xml: str, work: str, config_dir: str = TUNED,
+                         engine: str = "cpu") -> List[Dict]:
+    """Per-kernel power reports of one simulation of a captured trace list.
+    The traced kernels are short versions of the measured loops and power is
+    a rate, so the fixed kernel-launch latency (idle time) is left out."""
+    mod = _native.load()
+    os.makedirs(work, exist_ok=True)
+    rep_path = os.path.join(work, "accelwattch_power_report.log")
+    args = ["-config", os.path.join(config_dir, "gpgpusim.config"), "-config", os.path.join(config_dir, "trace.config"),
+            "-trace", kernelslist, "-power_simulation_enabled", "1", "-accelwattch_xml_file", xml,
+            "-power_report_file", rep_path, "-gpgpu_runtime_stat", "2000:0", "-sim_engine", engine,
+            "-gpgpu_kernel_launch_latency", "0"]
+    s = mod.Simulator(args, False)
+    import threading
+    import time
+    done = threading.Event()
+
+    def beat():  # progress line while a large trace list parses and runs
+        t0 = time.time()
+        while not done.wait(30):
+            print(f"[power validation] simulating {kernelslist}: {time.time() - t0:.0f} s", file=sys.stderr,
+                  flush=True)
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        rc = s.run()
+    finally:
+        done.set()
+    if rc != 0:
+        raise RuntimeError(f"simulation failed\n{s.output[-1000:]}")
+    return report.parse_power_report(rep_path)
+
+
+def run_traces(kernelslist: str, measured_csv: str, work: str, out_xml: str, config_dir: str = TUNED,
+               bound: float = 20.0, engine: str = "cpu") -> Dict:
+    """Validation on automatically traced kernels (bin/isatrace/power_suite
+    trace) against their measured socket power (power_suite measure): the
+    per-kernel component powers are fitted with one factor per FINE_GROUPS
+    group, bounded to [1/bound, bound]; leave-one-out MAPE is the headline."""
+    base_xml = os.path.join(config_dir, "accelwattch_sass_sim.xml")
+    if not os.path.exists(base_xml):
+        xmlcfg.write_xml(base_xml, xmlcfg.default_params("MI355X"))
+    meas = measured_power(measured_csv)
+    reps = simulate_trace_power(kernelslist, base_xml, work, config_dir, engine)
+    order = list(meas)  # measure mode prints the kernels in launch order
+    if len(reps) != len(order):
+        raise RuntimeError(f"{len(reps)} simulated kernels vs {len(order)} measured")
+    A = calibrate.design_matrix(reps)
+    b = np.array([meas[n] for n in order])
+    before = A.sum(axis=1)
+    kw = dict(groups=calibrate.FINE_GROUPS, lower=1.0 / bound, upper=bound)
+    x = calibrate.fit_groups(A, b, **kw)
+    loo = calibrate.leave_one_out_groups(A, b, **kw)
+    fit = A @ x
+    gf = calibrate.group_factors(x, calibrate.FINE_GROUPS)
+    at_bound = [g for g, v in gf.items() if v <= 1.0 / bound * 1.001 or v >= bound * 0.999]
+    calibrate.apply_factors(base_xml, out_xml, x)
+    return dict(kernels=order, measured_w=b.tolist(), uncalibrated_w=before.tolist(), calibrated_w=fit.tolist(),
+                loo_w=loo.tolist(), mape_uncalibrated=calibrate.mape(before, b)[0],
+                mape_in_sample=calibrate.mape(fit, b)[0], mape_leave_one_out=calibrate.mape(loo, b)[0],
+                mae_leave_one_out_w=calibrate.mape(loo, b)[1], group_factors=gf, factors_at_bound=at_bound,
+                sim_cycles=[r.get("gpu_sim_cycle", 0.0) for r in reps], traces="automatic ISA traces (isatrace)",
+                components=list(calibrate.COMPONENTS), components_w=A.tolist(), bounds=[1.0 / bound, bound],
+                xml=out_xml)
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("-o", "--out_xml", default=os.path.join(TUNED, "accelwattch_sass_sim_calibrated.xml"))
     ap.add_argument("-j", "--json", default=os.path.join(REPO, "profiles", "power_mi355x_validation.json"))
     ap.add_argument("-w", "--work", default="")
+    ap.add_argument("-t", "--traces", default="", help="kernelslist.g of bin/isatrace/power_suite trace")
+    ap.add_argument("-m", "--measured", default="", help="CSV of power_suite measure")
+    ap.add_argument("-c", "--config_dir", default=TUNED)
+    ap.add_argument("-e", "--engine", default="cpu", help="cpu | gpu (the MI355X cycle engine)")
     o = ap.parse_args(argv)
     work = o.work or tempfile.mkdtemp(prefix="asim_power_")
-    s = run(work, o.out_xml)
+    if o.traces:
+        s = run_traces(o.traces, o.measured or MEASURED, work, o.out_xml, o.config_dir, engine=o.engine)
+    else:
+        s = run(work, o.out_xml)
     with open(o.json, "w") as f:
         json.dump(s, f, indent=1)
     print(f"{'kernel':14s} {'measured':>9s} {'uncal':>9s} {'fit':>9s} {'LOO':>9s}")
@@ -185,6 +258,8 @@ def main(argv=None) -> int:
               f"{s['loo_w'][i]:9.1f}")
     print(f"MAPE uncalibrated {s['mape_uncalibrated']:.2f}%  in-sample {s['mape_in_sample']:.2f}%  "
           f"leave-one-out {s['mape_leave_one_out']:.2f}% ({s['mae_leave_one_out_w']:.1f} W)")
+    print("group factors:", {g: round(v, 3) for g, v in s["group_factors"].items()},
+          "at bound:", s.get("factors_at_bound"))
     return 0
 
 

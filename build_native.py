@@ -144,10 +144,14 @@ def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
             for fn in sorted(os.listdir(app_dir)):
                 if fn.endswith(".hip"):
                     out = os.path.join(ROOT, "bin", "apps", fn[:-4])
+                    first = open(os.path.join(app_dir, fn)).readline()
+                    libs = first.split(':', 1)[1].strip() if first.startswith("// UB_LIBS:") else ""
                     lines.append(f"build {out}: hipexe {os.path.join(app_dir, fn)} | {hdr}")
+                    lines.append(f"  libs = {libs}")
                     defaults.append(out)
                     tout = os.path.join(ROOT, "bin", "isatrace", fn[:-4])
                     lines.append(f"build {tout}: isatrace {os.path.join(app_dir, fn)} | {hdr} {isa_deps}")
+                    lines.append(f"  libs = {libs}")
                     defaults.append(tout)
         # examples/<name>/main.hip -> bin/examples/<name>
         ex_dir = os.path.join(ROOT, "examples")

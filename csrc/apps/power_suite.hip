@@ -1,0 +1,355 @@
+// UB_LIBS: -lamd_smi -lpthread
+// Power validation suite (reference util/accelwattch: the AccelWattch
+// validation micro-benchmarks + accelwattch_hw_profiler/measureGpuPower.cpp
+// and hw_power_validation_volta.csv): 24 kernels spanning VALU fp32 / int /
+// fp64, transcendental, MFMA, LDS, L1-, L2- and HBM-resident traffic, atomics,
+// mixes of them and four occupancy levels, plus idle.
+//
+//   power_suite measure [seconds]   every kernel back to back for `seconds`
+//                                   while a host thread samples socket power
+//                                   through amd-smi every 10 ms; prints the CSV
+//                                   ",mean HW_power,st_dev,var,#samples"
+//   power_suite trace               every kernel once, at the same grid with a
+//                                   short loop (power is a rate), for the
+//                                   automatic ISA tracer (bin/isatrace/power_suite)
+#include <amd_smi/amdsmi.h>
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <thread>
+
+#include "app_common.h"
+
+__global__ void k_idle() {}
+
+__global__ void k_fp32(float* sink, int iters) {
+  float x[8];
+  for (int k = 0; k < 8; ++k) x[k] = threadIdx.x + k;
+  for (int i = 0; i < iters; ++i)
+    for (int k = 0; k < 8; ++k) x[k] = __builtin_fmaf(x[k], 1.000001f, 0.25f);
+  float s = 0;
+  for (int k = 0; k < 8; ++k) s += x[k];
+  if (s == -1.f) sink[0] = s;
+}
+
+__global__ void k_int(float* sink, int iters) {
+  unsigned x[8];
+  for (int k = 0; k < 8; ++k) x[k] = threadIdx.x * 7 + k;
+  for (int i = 0; i < iters; ++i)
+    for (int k = 0; k < 8; ++k) x[k] = x[k] * 1664525u + 1013904223u;
+  unsigned s = 0;
+  for (int k = 0; k < 8; ++k) s ^= x[k];
+  if (s == 7u) sink[0] = (float)s;
+}
+
+__global__ void k_fp64(float* sink, int iters) {
+  double x[8];
+  for (int k = 0; k < 8; ++k) x[k] = threadIdx.x + k;
+  for (int i = 0; i < iters; ++i)
+    for (int k = 0; k < 8; ++k) x[k] = __builtin_fma(x[k], 1.000001, 0.25);
+  double s = 0;
+  for (int k = 0; k < 8; ++k) s += x[k];
+  if (s == -1.0) sink[0] = (float)s;
+}
+
+__global__ void k_sfu(float* sink, int iters) {
+  float x = threadIdx.x + 1.5f;
+  for (int i = 0; i < iters; ++i) x = __builtin_sqrtf(x) + __expf(-x) + 1.0f;
+  if (x == -1.f) sink[0] = x;
+}
+
+typedef __attribute__((__vector_size__(8 * sizeof(__bf16)))) __bf16 bf16x8;
+typedef __attribute__((__vector_size__(16 * sizeof(float)))) float f32x16;
+
+__global__ void k_mfma(float* sink, int iters) {
+  bf16x8 a, b;
+  for (int i = 0; i < 8; ++i) {
+    a[i] = (__bf16)(0.001f * (threadIdx.x + i));
+    b[i] = (__bf16)0.5f;
+  }
+  f32x16 c0 = {}, c1 = {};
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c1, 0, 0, 0);
+  }
+  float s = 0;
+  for (int i = 0; i < 16; ++i) s += c0[i] + c1[i];
+  if (s == -1.f) sink[0] = s;
+}
+
+// MFMA interleaved with fp32 VALU work (the filler slots between MFMAs)
+__global__ void k_mfma_valu(float* sink, int iters) {
+  bf16x8 a, b;
+  for (int i = 0; i < 8; ++i) {
+    a[i] = (__bf16)(0.002f * (threadIdx.x + i));
+    b[i] = (__bf16)0.25f;
+  }
+  f32x16 c0 = {};
+  float x[4] = {1.f, 2.f, 3.f, 4.f};
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    for (int k = 0; k < 4; ++k) x[k] = __builtin_fmaf(x[k], 0.999f, 0.5f);
+  }
+  float s = x[0] + x[1] + x[2] + x[3];
+  for (int i = 0; i < 16; ++i) s += c0[i];
+  if (s == -1.f) sink[0] = s;
+}
+
+__global__ void k_lds_read(float* sink, int iters) {
+  __shared__ float s[4096];
+  for (int i = threadIdx.x; i < 4096; i += blockDim.x) s[i] = (float)i;
+  __syncthreads();
+  float acc = 0;
+  unsigned idx = threadIdx.x;
+  for (int i = 0; i < iters; ++i) {
+    acc += s[idx & 4095];
+    idx += 64;
+  }
+  if (acc == -1.f) sink[0] = acc;
+}
+
+__global__ void k_lds_write(float* sink, int iters) {
+  __shared__ float s[4096];
+  unsigned idx = threadIdx.x;
+  for (int i = 0; i < iters; ++i) {
+    s[idx & 4095] = (float)i;
+    idx += 64;
+  }
+  __syncthreads();
+  if (s[threadIdx.x] == -1.f) sink[0] = 1.f;
+}
+
+__global__ void k_lds_fp32(float* sink, int iters) {
+  __shared__ float s[4096];
+  for (int i = threadIdx.x; i < 4096; i += blockDim.x) s[i] = (float)i;
+  __syncthreads();
+  float acc = 0, x = threadIdx.x;
+  unsigned idx = threadIdx.x;
+  for (int i = 0; i < iters; ++i) {
+    acc += s[idx & 4095];
+    x = __builtin_fmaf(x, 1.0001f, acc);
+    x = __builtin_fmaf(x, 0.9999f, 0.5f);
+    idx += 64;
+  }
+  if (acc + x == -1.f) sink[0] = acc;
+}
+
+// streaming reads / writes / copy over a buffer of `n` float4 (grid-stride,
+// `reps` sweeps): HBM-resident for a large buffer, L2- / L1-resident for small
+__global__ void k_read(const float4* __restrict__ a, size_t n, int reps, float* sink) {
+  float4 acc = make_float4(0, 0, 0, 0);
+  for (int r = 0; r < reps; ++r)
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+      const float4 v = a[i];
+      acc.x += v.x;
+      acc.w += v.w;
+    }
+  if (acc.x + acc.w == 1234.5f) sink[0] = acc.x;
+}
+
+__global__ void k_write(float4* __restrict__ a, size_t n, int reps) {
+  for (int r = 0; r < reps; ++r)
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+      a[i] = make_float4((float)r, 1.f, 2.f, 3.f);
+}
+
+__global__ void k_copy(const float4* __restrict__ a, float4* __restrict__ b, size_t n, int reps) {
+  for (int r = 0; r < reps; ++r)
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+      b[i] = a[i];
+}
+
+// per-block private slice read repeatedly: stays in the CU's L1
+__global__ void k_l1_read(const float4* __restrict__ a, int reps, float* sink) {
+  const float4* p = a + (size_t)(blockIdx.x % 64) * 1024;  // 16 KB per slice
+  float4 acc = make_float4(0, 0, 0, 0);
+  for (int r = 0; r < reps; ++r)
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+      const float4 v = p[i];
+      acc.x += v.x;
+      acc.y += v.y;
+    }
+  if (acc.x + acc.y == 1234.5f) sink[0] = acc.x;
+}
+
+__global__ void k_fp32_read(const float4* __restrict__ a, size_t n, int iters, float* sink) {
+  float x = threadIdx.x, acc = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    acc += a[i].y;
+    for (int k = 0; k < iters; ++k) x = __builtin_fmaf(x, 1.00001f, acc);
+  }
+  if (x == -1.f) sink[0] = x;
+}
+
+__global__ void k_fp64_read(const float4* __restrict__ a, size_t n, int iters, float* sink) {
+  double x = threadIdx.x, acc = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    acc += a[i].z;
+    for (int k = 0; k < iters; ++k) x = __builtin_fma(x, 1.00001, acc);
+  }
+  if (x == -1.0) sink[0] = (float)x;
+}
+
+__global__ void k_atomic(unsigned* ctr, int iters) {
+  for (int i = 0; i < iters; ++i) atomicAdd(&ctr[(threadIdx.x + i * 64) & 4095], 1u);
+}
+
+__global__ void k_int_lds(float* sink, int iters) {
+  __shared__ unsigned s[4096];
+  for (int i = threadIdx.x; i < 4096; i += blockDim.x) s[i] = i;
+  __syncthreads();
+  unsigned x = threadIdx.x;
+  for (int i = 0; i < iters; ++i) x = x * 1664525u + s[(x >> 7) & 4095];
+  if (x == 7u) sink[0] = (float)x;
+}
+
+struct Sampler {
+  amdsmi_processor_handle h = nullptr;
+  bool ok = false;
+  explicit Sampler(int hip_dev) {
+    if (amdsmi_init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return;
+    char bus[64] = {};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), hip_dev) != hipSuccess) return;
+    unsigned dom = 0, b = 0, dv = 0, fn = 0;
+    sscanf(bus, "%x:%x:%x.%x", &dom, &b, &dv, &fn);
+    uint32_t ns = 0;
+    amdsmi_get_socket_handles(&ns, nullptr);
+    std::vector<amdsmi_socket_handle> socks(ns);
+    amdsmi_get_socket_handles(&ns, socks.data());
+    for (auto s : socks) {
+      uint32_t np = 0;
+      amdsmi_get_processor_handles(s, &np, nullptr);
+      std::vector<amdsmi_processor_handle> ps(np);
+      amdsmi_get_processor_handles(s, &np, ps.data());
+      for (auto p : ps) {
+        amdsmi_bdf_t bdf;
+        if (amdsmi_get_gpu_device_bdf(p, &bdf) != AMDSMI_STATUS_SUCCESS) continue;
+        if (bdf.bus_number == b && bdf.device_number == dv && bdf.function_number == fn) {
+          h = p;
+          ok = true;
+        }
+      }
+    }
+  }
+  double watts() const {
+    amdsmi_power_info_t pi;
+    if (!ok || amdsmi_get_power_info(h, &pi) != AMDSMI_STATUS_SUCCESS) return NAN;
+    if (pi.current_socket_power != UINT32_MAX && pi.current_socket_power) return pi.current_socket_power;
+    if (pi.average_socket_power != UINT32_MAX && pi.average_socket_power) return pi.average_socket_power;
+    return (double)pi.socket_power;
+  }
+  ~Sampler() {
+    if (ok) amdsmi_shut_down();
+  }
+};
+
+int main(int argc, char** argv) {
+  const bool trace = argc > 1 && !strcmp(argv[1], "trace");
+  const double secs = argc > 2 ? atof(argv[2]) : 1.5;
+  int dev = 0;
+  APP_HIP(hipGetDevice(&dev));
+  hipDeviceProp_t prop;
+  APP_HIP(hipGetDeviceProperties(&prop, dev));
+  const int cus = prop.multiProcessorCount;
+  float* sink;
+  unsigned* ctr;
+  APP_HIP(hipMalloc(&sink, 64));
+  APP_HIP(hipMalloc(&ctr, 4096 * 4));
+  APP_HIP(hipMemset(ctr, 0, 4096 * 4));
+  const size_t big = (size_t)1 << 30, l2 = (size_t)2 << 20;  // 1 GB (HBM), 2 MB (L2-resident)
+  float4 *buf, *buf2;
+  APP_HIP(hipMalloc(&buf, big));
+  APP_HIP(hipMalloc(&buf2, big));
+  APP_HIP(hipMemset(buf, 0, big));
+  APP_HIP(hipMemset(buf2, 0, big));
+  // the same grids in both modes; `trace` shortens loops (steady-state rate)
+  // measure: every kernel runs ~0.5-2 ms, so the launch overhead between the
+  // back-to-back launches does not dilute the steady-state power
+  const int sc = trace ? 1 : 2048;  // loop scale
+  const size_t nbig = trace ? (size_t)2 << 20 : big / 16;  // trace: 32 MB sweep
+  const dim3 b(256);
+  auto g = [&](int per_cu) { return dim3(cus * per_cu); };
+  struct K {
+    const char* name;
+    std::function<void()> launch;
+  };
+  std::vector<K> ks = {
+      {"idle", [&] { k_idle<<<1, 64>>>(); }},
+      {"fp32_fma_occ1", [&] { k_fp32<<<g(1), b>>>(sink, 8 * sc); }},
+      {"fp32_fma_occ2", [&] { k_fp32<<<g(2), b>>>(sink, 8 * sc); }},
+      {"fp32_fma_occ4", [&] { k_fp32<<<g(4), b>>>(sink, 8 * sc); }},
+      {"fp32_fma", [&] { k_fp32<<<g(8), b>>>(sink, 8 * sc); }},
+      {"int32_mad", [&] { k_int<<<g(8), b>>>(sink, 8 * sc); }},
+      {"fp64_fma", [&] { k_fp64<<<g(8), b>>>(sink, 4 * sc); }},
+      {"sfu_sqrt_exp", [&] { k_sfu<<<g(8), b>>>(sink, 8 * sc); }},
+      {"mfma_bf16", [&] { k_mfma<<<g(8), b>>>(sink, 2 * sc); }},
+      {"mfma_bf16_occ2", [&] { k_mfma<<<g(2), b>>>(sink, 2 * sc); }},
+      {"mfma_valu", [&] { k_mfma_valu<<<g(8), b>>>(sink, 2 * sc); }},
+      {"lds_read", [&] { k_lds_read<<<g(8), b>>>(sink, 16 * sc); }},
+      {"lds_write", [&] { k_lds_write<<<g(8), b>>>(sink, 16 * sc); }},
+      {"lds_fp32", [&] { k_lds_fp32<<<g(8), b>>>(sink, 8 * sc); }},
+      {"int_lds", [&] { k_int_lds<<<g(8), b>>>(sink, 8 * sc); }},
+      {"hbm_read", [&] { k_read<<<g(16), b>>>(buf, nbig, trace ? 1 : 4, sink); }},
+      {"hbm_write", [&] { k_write<<<g(16), b>>>(buf, nbig, trace ? 1 : 4); }},
+      {"hbm_copy", [&] { k_copy<<<g(16), b>>>(buf, buf2, nbig / 2, trace ? 1 : 4); }},
+      {"l2_read", [&] { k_read<<<g(8), b>>>(buf, l2 / 16, trace ? 2 : 2 * sc, sink); }},
+      {"l1_read", [&] { k_l1_read<<<g(8), b>>>(buf, trace ? 2 : sc / 4, sink); }},
+      {"fp32_hbm_mix", [&] { k_fp32_read<<<g(16), b>>>(buf, nbig, 8, sink); }},
+      {"fp64_hbm_mix", [&] { k_fp64_read<<<g(16), b>>>(buf, nbig, 4, sink); }},
+      {"atomic_l2", [&] { k_atomic<<<g(4), b>>>(ctr, trace ? 2 : sc / 8); }},
+      {"fp32_fma_light", [&] { k_fp32<<<g(8), b>>>(sink, sc); }},
+  };
+  if (trace) {
+    for (auto& k : ks) {
+      k.launch();
+      APP_HIP(hipGetLastError());
+      APP_HIP(hipDeviceSynchronize());
+    }
+    printf("power_suite trace: %zu kernels PASSED\n", ks.size());
+  } else {
+    Sampler smi(dev);
+    if (!smi.ok) {
+      printf("# amd-smi power sampling unavailable on this node; nothing measured\n");
+      return 0;
+    }
+    printf(",mean HW_power,st_dev,var,#samples\n");
+    for (auto& k : ks) {
+      k.launch();
+      APP_HIP(hipDeviceSynchronize());
+      std::atomic<bool> stop{false};
+      std::vector<double> samples;
+      std::thread th([&] {
+        while (!stop.load()) {
+          const double w = smi.watts();
+          if (!std::isnan(w)) samples.push_back(w);
+          std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        }
+      });
+      const auto t0 = std::chrono::steady_clock::now();
+      while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < secs) {
+        for (int r = 0; r < 4; ++r) k.launch();
+        APP_HIP(hipDeviceSynchronize());
+      }
+      stop = true;
+      th.join();
+      const size_t skip = samples.size() / 4;  // ramp-up
+      double m = 0, v = 0;
+      const size_t n = samples.size() - skip;
+      for (size_t i = skip; i < samples.size(); ++i) m += samples[i];
+      m = n ? m / n : NAN;
+      for (size_t i = skip; i < samples.size(); ++i) v += (samples[i] - m) * (samples[i] - m);
+      v = n > 1 ? v / (n - 1) : 0;
+      printf("%s,%.4f,%.4f,%.4f,%zu\n", k.name, m, std::sqrt(v), v, n);
+      fflush(stdout);
+    }
+  }
+  APP_HIP(hipFree(buf));
+  APP_HIP(hipFree(buf2));
+  APP_HIP(hipFree(sink));
+  APP_HIP(hipFree(ctr));
+  return 0;
+}

@@ -422,7 +422,7 @@ class GpuEngine : public Engine {
   void load_kernel(const ReadyKernel& k, const KernelDesc& kd) override {
     kd_ = kd;
     upload(d_insts_, cap_insts_, k.insts.data(), k.insts.size() * sizeof(TInst));
-    upload(d_accs_, cap_accs_, k.accs.data(), std::max<size_t>(16, k.accs.size() * sizeof(TAcc)));
+    upload(d_accs_, cap_accs_, k.accs.data(), k.accs.size() * sizeof(TAcc));  // may be empty (no memory ops)
     upload(d_streams_, cap_streams_, k.streams.data(), k.streams.size() * sizeof(WStream));
     kd_.insts = reinterpret_cast<const TInst*>(d_insts_);
     kd_.streams = reinterpret_cast<const WStream*>(d_streams_);
@@ -633,12 +633,12 @@ class GpuEngine : public Engine {
 
  private:
   void upload(void*& d, size_t& cap, const void* h, size_t bytes) {
-    if (bytes > cap) {
+    if (bytes > cap || !d) {
       if (d) HIPCHECK(hipFree(d));
       cap = bytes + bytes / 4 + 4096;
       HIPCHECK(hipMalloc(&d, cap));
     }
-    if (bytes) HIPCHECK(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice));
+    if (bytes && h) HIPCHECK(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice));
   }
   void release() {
     auto fr = [](void* p) {

@@ -211,3 +211,18 @@ def test_time_sliced_units_gpu_equals_cpu(gpu_mod, tmp_path, monkeypatch, blocks
     g = sim.simulate(kl, "QV100", engine="gpu")
     assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
     assert [k["cycles"] for k in g.kernels] == [k["cycles"] for k in c.kernels]
+
+
+def test_kernel_without_memory_ops_gpu_equals_cpu(gpu_mod, tmp_path):
+    """A kernel with no memory instruction at all (empty access table) runs on
+    the HIP engine (regression: the empty table upload used a null host pointer)."""
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+    k = KernelBuilder("k_alu", (512, 1, 1), (256, 1, 1), nregs=16, binary_version=950, warp_size=64)
+    k.alu("v_fma_f32", 16, regs=(4, 5, 6))
+    k.op("s_endpgm")
+    kl = rodinia.write_app(str(tmp_path / "alu"), [k.build()], memcpy=False)
+    g = sim.simulate(kl, "MI355X", engine="gpu")
+    c = sim.simulate(kl, "MI355X", engine="cpu")
+    assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
