@@ -514,7 +514,7 @@ SIM_HDI void mem_icnt_cycle(ChanState& ch, SubPart& sp, const SimCfg& c, const M
     Pkt r = sp.reply[sp.rep_head];
     uint32_t nflits = (r.size + c.flit_size - 1) / c.flit_size;
     uint64_t done = now_fs + (uint64_t)(nflits - 1) * c.per_icnt;
-    if (done < x.win_end) {
+    {  // serialisation may run past the window end (see sm_inject)
       uint32_t gsub = ch.id * c.n_sub_per_mem + sub;
       uint32_t cell = (uint32_t)r.dst * x.n_src_sub + gsub;
       // per-destination counter kept in the reply's own slot count array

@@ -333,7 +333,11 @@ SIM_HDI void sm_send(S& s, const SimCfg& c, uint8_t type, uint64_t line, uint8_t
   s.outq_n++;
 }
 
-// move packets whose injection completes inside the epoch into the outbox
+// move the head packet into the outbox once the injection port is free.  A
+// multi-flit packet may finish serialising after the epoch ends (port_free
+// carries over); its arrival time is still beyond the lookahead, so the
+// epoch length does not gate injection (it did: with epochs shorter than a
+// packet's flit count nothing could ever be sent)
 template <class P, class S>
 SIM_HDI void sm_inject(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
@@ -342,7 +346,6 @@ SIM_HDI void sm_inject(S& s, const SmCtx& x, uint64_t now) {
   Pkt p = P::uni(s.outq[P::uni(s.outq_head)]);
   uint32_t nflits = (p.size + c.flit_size - 1) / c.flit_size;
   uint64_t done = now + nflits - 1;
-  if (done >= s.epoch_end) return;  // completes next epoch
   uint32_t dst = p.dst;
   uint32_t slot = dst * x.n_src_sm + s.id;
   uint32_t n = P::uni(s.ocnt[dst]);

@@ -93,3 +93,20 @@ def test_pre_volta_presets(native, tmp_path, preset):
     p = subprocess.run(args, cwd="/", capture_output=True, text=True)
     assert p.returncode == 0, p.stdout[-500:] + p.stderr[-500:]
     assert "gpu_tot_sim_cycle" in p.stdout
+
+
+def test_epoch_length_sensitivity_is_smooth(tmp_path):
+    """-icnt_latency is both the crossbar latency and the PDES lookahead: short
+    epochs must still simulate (multi-flit packets serialise across epoch
+    boundaries) and cycles must grow smoothly with the latency, not jump."""
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    kls = rodinia.generate_suite(str(tmp_path), ["nn-rodinia-2.0-ft", "backprop-rodinia-2.0-ft"])
+    for app, kl in kls.items():
+        cyc = []
+        for L in (1, 2, 8):
+            r = sim.simulate(kl, "GV100", engine="cpu", extra={"-icnt_latency": str(L)})
+            assert not r.deadlock, (app, L)
+            cyc.append(r.tot_cycle)
+        assert cyc[0] <= cyc[1] * 1.01 and cyc[1] <= cyc[2] * 1.01, (app, cyc)
+        assert cyc[2] <= cyc[0] * 1.10, (app, cyc)  # 7 extra cycles per hop cost < 10 %
