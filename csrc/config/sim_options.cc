@@ -581,6 +581,9 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
     if (c.max_warps_per_sm > (uint32_t)kMaxWarps) throw OptionError("more than 64 warps per SM");
   }
   c.max_cta_per_sm = std::min<uint32_t>((uint32_t)r.getu("-gpgpu_shader_cta"), kMaxCta);
+  c.concurrent_kernel_sm = r.getb("-gpgpu_concurrent_kernel_sm") ? 1u : 0u;
+  c.max_concurrent_kernel =
+      (uint32_t)std::max<long long>(1, std::min<long long>(kMaxConc, r.geti("-gpgpu_max_concurrent_kernel")));
   c.regs_per_sm = (uint32_t)r.getu("-gpgpu_shader_registers");
   c.shmem_per_sm = (uint32_t)r.getu("-gpgpu_shmem_size");
   c.shmem_per_block = (uint32_t)r.getu("-gpgpu_shmem_per_block");

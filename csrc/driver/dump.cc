@@ -21,7 +21,7 @@ static void sb_regs(std::ostringstream& o, const uint64_t* sb) {
   if (!any) o << "-";
 }
 
-std::string dump_sm_state(const SMState& s, const SimCfg& c, const TInst* insts) {
+std::string dump_sm_state(const SMState& s, const SimCfg& c, const TInst* const* slot_insts) {
   std::ostringstream o;
   o << "=== SM " << s.id << " @ cycle " << s.cycle << ": " << s.n_cta_active << " CTAs, "
     << s.outstanding << " packets in flight, outq " << s.outq_n << ", inq " << s.inq_n << ", L1 waiters " << s.n_pend
@@ -39,8 +39,9 @@ std::string dump_sm_state(const SMState& s, const SimCfg& c, const TInst* insts)
     if (f & WF_WAITCNT) o << " WAITCNT";
     o << " scoreboard ";
     sb_regs(o, s.w_sb[w]);
+    const TInst* insts = slot_insts[s.w_head[w] >> kSlotShift];
     if (s.w_ibuf[w] && insts) {
-      const TInst& in = insts[s.w_head[w]];
+      const TInst& in = insts[s.w_head[w] & kIdxMask];
       o << " next " << opcode_name(in.opcode) << " pc 0x" << std::hex << in.pc << std::dec;
     }
     o << "\n";
@@ -116,10 +117,13 @@ std::string Simulator::dump_pipeline(int sm, int ch) {
   const SMState* sms = reinterpret_cast<const SMState*>(img.data());
   const ChanState* chs = reinterpret_cast<const ChanState*>(img.data() + sizeof(SMState) * cfg_.n_sm);
   std::string out;
+  const TInst* slot_insts[kMaxConc] = {};
+  for (int k = 0; k < kMaxConc; ++k)
+    if (slot_op_[k] && slot_op_[k]->rk && !slot_op_[k]->rk->insts.empty()) slot_insts[k] = slot_op_[k]->rk->insts.data();
   for (uint32_t i = 0; i < cfg_.n_sm; ++i)
     if (sm == -1 || (sm >= 0 && (uint32_t)sm == i)) {
       if (sm == -1 && sms[i].n_cta_active == 0 && sms[i].outstanding == 0) continue;  // skip idle SMs in "all"
-      out += dump_sm_state(sms[i], cfg_, cur_kernel_ && !cur_kernel_->insts.empty() ? cur_kernel_->insts.data() : nullptr);
+      out += dump_sm_state(sms[i], cfg_, slot_insts);
     }
   for (uint32_t i = 0; i < cfg_.n_mem; ++i)
     if (ch == -1 || (ch >= 0 && (uint32_t)ch == i)) {

@@ -103,31 +103,77 @@ double Simulator::wall_seconds() const {
   return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start_).count();
 }
 
+// The command loop (reference gpu-simulator/main.cc:74-197): commands enter
+// a window in trace order -- up to -gpgpu_max_concurrent_kernel kernels /
+// collectives with -gpgpu_concurrent_kernel_sm, else one -- memcpys are
+// applied as they are reached, and a windowed operation starts once every
+// earlier operation of its stream has finished (stream order; kernels also
+// need a free engine slot).  The engine then runs until the next kernel or
+// collective completes.
 int Simulator::run() {
   print("Accel-Sim-AMD [MI355X-native trace-driven simulator, engine=%s]\n", eng_->name());
   cmds_ = parse_commandlist(dopt_.trace_file);
-  size_t first = 0;
-  if (dopt_.resume_option) first = resume_checkpoint();
-  for (size_t i = first; i < cmds_.size(); ++i) {
-    run_command(i);
-    if (deadlock_) break;
-    if (cmds_[i].type == CMD_KERNEL) {
-      ++kernels_done_;
-      if (dopt_.checkpoint_option && kernels_done_ == (uint32_t)dopt_.checkpoint_kernel) write_checkpoint(i);
-    }
-    if (dopt_.max_cycle && (int64_t)tot_cycle_ >= dopt_.max_cycle) {
-      print("GPGPU-Sim: ** break due to reaching the maximum cycles (or instructions) **\n");
-      break;
-    }
-    if ((dopt_.max_insn && (int64_t)tot_insn_ >= dopt_.max_insn) || cap_hit_) {
-      print("GPGPU-Sim: ** break due to reaching the maximum cycles (or instructions) **\n");
-      break;
-    }
+  next_cmd_ = 0;
+  if (dopt_.resume_option) next_cmd_ = resume_checkpoint();
+  while (!stop_ && (next_cmd_ < cmds_.size() || !win_.empty())) {
+    admit(cmds_.size());
+    step();
   }
   print("GPGPU-Sim: *** simulation thread exiting ***\n");
   print("GPGPU-Sim: *** exit detected ***\n");
   fflush(stdout);
   return deadlock_ ? 1 : 0;
+}
+
+size_t Simulator::window_size() const {
+  return dopt_.concurrent_kernel_sm ? std::max<uint32_t>(1, cfg_.max_concurrent_kernel) : 1;
+}
+
+void Simulator::admit(size_t end) {
+  while (next_cmd_ < end && win_.size() < window_size()) {
+    const size_t i = next_cmd_++;
+    const Command& c = cmds_[i];
+    if (c.type == CMD_KERNEL) {
+      admit_kernel(i);
+    } else if (c.type == CMD_COLLECTIVE) {
+      std::unique_ptr<StreamOp> op(new StreamOp());
+      op->cmd = i;
+      op->coll = true;
+      op->stream = c.stream;
+      win_.push_back(std::move(op));
+    } else {
+      run_now(c);
+    }
+  }
+}
+
+void Simulator::run_now(const Command& c) {
+  switch (c.type) {
+    case CMD_MEMCPY_HTOD:
+      print("launching memcpy command : %s\n", c.text.c_str());
+      if (cfg_.perf_memcpy) eng_->memcpy_fill_l2(c.addr, c.bytes);
+      break;
+    case CMD_COLL_INIT:
+    case CMD_COLL_DESTROY:
+    case CMD_GROUP_START:
+    case CMD_GROUP_END:
+      print("%s was run!\n", c.text.c_str());
+      break;
+    default:
+      break;
+  }
+}
+
+// step API: run the command list up to and including command `idx` (the
+// window drains, so every admitted kernel / collective completes)
+void Simulator::run_command(size_t idx) {
+  if (cmds_.empty()) cmds_ = parse_commandlist(dopt_.trace_file);
+  if (next_cmd_ < idx) next_cmd_ = idx;
+  const size_t end = std::min(idx + 1, cmds_.size());
+  while (!stop_ && (next_cmd_ < end || !win_.empty())) {
+    admit(end);
+    if (!win_.empty()) step();
+  }
 }
 
 // Checkpoint file: magic, driver counters, previous stat snapshots, engine image.
@@ -202,31 +248,6 @@ size_t Simulator::resume_checkpoint() {
   return (size_t)h.cmd_index + 1;
 }
 
-void Simulator::run_command(size_t idx) {
-  if (cmds_.empty()) cmds_ = parse_commandlist(dopt_.trace_file);
-  const Command& c = cmds_.at(idx);
-  switch (c.type) {
-    case CMD_MEMCPY_HTOD:
-      print("launching memcpy command : %s\n", c.text.c_str());
-      if (cfg_.perf_memcpy) eng_->memcpy_fill_l2(c.addr, c.bytes);
-      break;
-    case CMD_KERNEL:
-      do_kernel(c);
-      break;
-    case CMD_COLLECTIVE:
-      do_collective(c);
-      break;
-    case CMD_COLL_INIT:
-    case CMD_COLL_DESTROY:
-    case CMD_GROUP_START:
-    case CMD_GROUP_END:
-      print("%s was run!\n", c.text.c_str());
-      break;
-    default:
-      break;
-  }
-}
-
 uint64_t Simulator::collective_cycles(const Command& c) const {
   const std::string& m = dopt_.collective_model;
   if (m == "const") return c.coll == "AllReduce" ? (uint64_t)std::max(0, dopt_.nccl_allreduce_latency) : 0;
@@ -287,36 +308,26 @@ LinkParams Simulator::link_params() const {
   return p;
 }
 
-void Simulator::do_collective(const Command& c) {
-  uint64_t cyc = coll_hook_ ? coll_hook_(c, eng_->now()) : collective_cycles(c);
-  if (c.coll == "AllReduce")
-    print("ncclAllReduce was run! Latency: %llu cycles.\n", (unsigned long long)cyc);
-  else
-    print("%s was run! Latency: %llu cycles.\n", c.text.c_str(), (unsigned long long)cyc);
-  if (cyc) eng_->advance(cyc);
-  tot_cycle_ = eng_->now();
-  CollectiveResult r;
-  r.op = c.coll;
-  r.bytes = c.bytes;
-  r.nranks = c.nranks;
-  r.cycles = cyc;
-  colls_.push_back(r);
-}
-
-void Simulator::do_kernel(const Command& c) {
-  auto t0 = std::chrono::steady_clock::now();
+// header, trace and occupancy of a kernel entering the window (reference
+// main.cc:94-99 parse_kernel_info + create_kernel_info)
+void Simulator::admit_kernel(size_t idx) {
+  const Command& c = cmds_[idx];
+  std::unique_ptr<StreamOp> op(new StreamOp());
+  op->cmd = idx;
+  op->t_admit = std::chrono::steady_clock::now();
   HostKernel hk = load_kernel(c.text);
   print("Processing kernel %s\n", c.text.c_str());
   if (hk.h.warp_size != cfg_.warp_size)
     throw std::runtime_error("trace warp size does not match -gpgpu_shader_core_pipeline");
-  cur_kernel_.reset(new ReadyKernel(coalesce_kernel(hk, cfg_)));
-  const ReadyKernel& rk = *cur_kernel_;
+  op->rk.reset(new ReadyKernel(coalesce_kernel(hk, cfg_)));
+  const ReadyKernel& rk = *op->rk;
   KernelShape ks{rk.h.block[0] * rk.h.block[1] * rk.h.block[2], rk.h.shmem, rk.h.nregs, rk.n_cta};
   Occupancy occ = compute_occupancy(cfg_, ks);
   if ((uint64_t)occ.cta_per_sm * rk.warps_per_cta > (uint64_t)std::min<uint32_t>(cfg_.max_warps_per_sm, kMaxWarps))
     occ.cta_per_sm = std::max<uint32_t>(1, std::min<uint32_t>(cfg_.max_warps_per_sm, kMaxWarps) / rk.warps_per_cta);
   if (rk.warps_per_cta > (uint32_t)kMaxWarps) throw std::runtime_error("CTA larger than 64 warps");
-  KernelDesc kd{};
+  KernelDesc& kd = op->kd;
+  kd = KernelDesc{};
   kd.uid = next_uid_++;
   kd.n_cta = rk.n_cta;
   kd.stop_when_issued = 0;
@@ -341,26 +352,149 @@ void Simulator::do_kernel(const Command& c) {
   kd.stream = (uint32_t)rk.h.stream;
   kd.l1_sets = occ.l1_sets;
   kd.l1_assoc = occ.l1_assoc;
+  kd.flush_l1 = dopt_.flush_l1 ? 1u : 0u;
+  // per-CTA resources for SMs shared by concurrent kernels (the same limits
+  // compute_occupancy applies to one kernel)
+  const uint32_t padded = (ks.threads_per_cta + cfg_.warp_size - 1) / cfg_.warp_size * cfg_.warp_size;
+  kd.thr_cta = padded;
+  kd.regs_cta = rk.h.nregs ? padded * ((rk.h.nregs + 3) & ~3u) : 0;
+  kd.shmem_cap = occ.shmem_kb ? occ.shmem_kb * 1024u : cfg_.shmem_per_sm;
   kd.shmem_base = rk.h.shmem_base;
   kd.local_base = rk.h.local_base;
   kd.n_insts = rk.insts.size();
-  print("launching kernel name: %s uid: %u\n", rk.h.name.c_str(), kd.uid);
-  print("GPGPU-Sim uArch: CTA/core = %u, limited by: %s\n", kd.cta_per_sm, occ.limiter);
-  eng_->load_kernel(rk, kd);
-  const uint64_t start = eng_->now();
+  op->occ_limiter = occ.limiter;
+  op->stream = rk.h.stream;
+  tot_cta_ += kd.n_cta;
+  win_.push_back(std::move(op));
+}
+
+// start every windowed operation whose stream has no earlier unfinished
+// operation (reference main.cc:102-115: busy_streams), kernels in a free slot
+void Simulator::launch_ready() {
+  std::vector<uint64_t> busy;
+  for (auto& up : win_) {
+    StreamOp& op = *up;
+    const bool stream_busy = std::find(busy.begin(), busy.end(), op.stream) != busy.end();
+    busy.push_back(op.stream);
+    if (op.launched || stream_busy) continue;
+    if (op.coll) {
+      launch_collective(op);
+      continue;
+    }
+    int slot = -1;
+    for (uint32_t k = 0; k < (uint32_t)std::min<uint32_t>(kMaxConc, (uint32_t)window_size()); ++k)
+      if (!slot_op_[k]) {
+        slot = (int)k;
+        break;
+      }
+    if (slot < 0) continue;
+    if (!eng_->running()) ptrack_.begin_kernel();  // power samples of a busy period
+    const uint64_t now = eng_->now();
+    op.kd.ready_cycle = now + cfg_.kernel_launch_latency + (uint64_t)cfg_.tb_launch_latency * op.kd.n_cta;
+    op.start = now;
+    op.slot = slot;
+    op.launched = true;
+    slot_op_[slot] = &op;
+    print("launching kernel name: %s uid: %u\n", op.rk->h.name.c_str(), op.kd.uid);
+    print("GPGPU-Sim uArch: CTA/core = %u, limited by: %s\n", op.kd.cta_per_sm, op.occ_limiter);
+    eng_->launch((uint32_t)slot, *op.rk, op.kd);
+  }
+}
+
+void Simulator::launch_collective(StreamOp& op) {
+  const Command& c = cmds_[op.cmd];
+  const uint64_t now = eng_->now();
+  uint64_t cyc = coll_hook_ ? coll_hook_(c, now) : collective_cycles(c);
+  if (c.coll == "AllReduce")
+    print("ncclAllReduce was run! Latency: %llu cycles.\n", (unsigned long long)cyc);
+  else
+    print("%s was run! Latency: %llu cycles.\n", c.text.c_str(), (unsigned long long)cyc);
+  op.launched = true;
+  op.start = now;
+  op.end = now + cyc;
+  op.coll_cycles = cyc;
+}
+
+// advance to the next completion in the window and retire what completed
+void Simulator::step() {
+  launch_ready();
+  uint64_t coll_end = ~0ull;
+  for (auto& up : win_)
+    if (up->coll && up->launched) coll_end = std::min(coll_end, up->end);
+  if (!eng_->running()) {
+    if (coll_end == ~0ull) {
+      if (!win_.empty()) throw std::runtime_error("command window stalled: nothing can start");
+      return;
+    }
+    // only collectives in flight: the clock jumps to the first one's end
+    const uint64_t now = eng_->now();
+    if (coll_end > now) eng_->advance(coll_end - now);
+    tot_cycle_ = eng_->now();
+    retire_collectives();
+    check_limits();
+    return;
+  }
   RunLimits lim;
   if (dopt_.max_cycle) lim.max_cycle = (uint64_t)dopt_.max_cycle;
+  if (coll_end != ~0ull) lim.max_cycle = lim.max_cycle ? std::min(lim.max_cycle, coll_end) : coll_end;
   auto ts = std::chrono::steady_clock::now();
-  RunResult rr;
-  if (power_ || visualizer_ || cfg_.trace_mask) {
-    ptrack_.begin_kernel();
-    rr = run_sampled(start, lim, rk.h.name);
-    if (visualizer_) visualizer_->flush();
-  } else {
-    rr = eng_->run_kernel(start, dopt_.flush_l1, lim);
+  RunResult rr = (power_ || visualizer_ || cfg_.trace_mask) ? run_sampled(lim) : eng_->run(lim);
+  sim_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
+  for (auto* op : slot_op_)
+    if (op) op->epochs += rr.epochs;
+  tot_cycle_ = eng_->now();
+  retire_collectives();
+  const bool at_max_cycle = dopt_.max_cycle && eng_->now() >= (uint64_t)dopt_.max_cycle;
+  if (rr.cap) cap_hit_ = true;
+  if (rr.deadlock) deadlock_ = true;
+  // kernels end when they complete, or all together when the run stops
+  uint32_t fin = rr.done_mask;
+  if (rr.deadlock || rr.cap || at_max_cycle) fin = eng_->running() | rr.done_mask;
+  for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k)
+    if ((fin >> k & 1u) && slot_op_[k]) finish_kernel(k, rr);
+  check_limits();
+}
+
+void Simulator::retire_collectives() {
+  const uint64_t now = eng_->now();
+  for (auto it = win_.begin(); it != win_.end();) {
+    StreamOp& op = **it;
+    if (op.coll && op.launched && op.end <= now) {
+      const Command& c = cmds_[op.cmd];
+      CollectiveResult r;
+      r.op = c.coll;
+      r.bytes = c.bytes;
+      r.nranks = c.nranks;
+      r.cycles = op.coll_cycles;
+      colls_.push_back(r);
+      it = win_.erase(it);
+    } else {
+      ++it;
+    }
   }
-  auto te = std::chrono::steady_clock::now();
-  sim_s_ += std::chrono::duration<double>(te - ts).count();
+}
+
+void Simulator::check_limits() {
+  if (deadlock_) {
+    stop_ = true;
+    return;
+  }
+  if (dopt_.max_cycle && (int64_t)tot_cycle_ >= dopt_.max_cycle) {
+    print("GPGPU-Sim: ** break due to reaching the maximum cycles (or instructions) **\n");
+    stop_ = true;
+  } else if ((dopt_.max_insn && (int64_t)tot_insn_ >= dopt_.max_insn) || cap_hit_) {
+    print("GPGPU-Sim: ** break due to reaching the maximum cycles (or instructions) **\n");
+    stop_ = true;
+  }
+}
+
+// statistics of a completed kernel (reference main.cc:163-184: print_stats
+// when finished_kernel() names it); counters are the deltas since the last
+// kernel completed
+void Simulator::finish_kernel(uint32_t slot, const RunResult& rr) {
+  StreamOp& op = *slot_op_[slot];
+  const ReadyKernel& rk = *op.rk;
+  const KernelDesc& kd = op.kd;
   if (dopt_.flush_l2) eng_->flush_l2();
   std::vector<SMStats> sm;
   std::vector<MemStats> mem;
@@ -369,7 +503,6 @@ void Simulator::do_kernel(const Command& c) {
     prev_sm_.assign(sm.size(), SMStats{});
     prev_mem_.assign(mem.size(), MemStats{});
   }
-  // per-kernel deltas
   std::vector<SMStats> dsm(sm.size());
   std::vector<MemStats> dmem(mem.size());
   stat_delta(sm, prev_sm_, dsm);
@@ -379,8 +512,8 @@ void Simulator::do_kernel(const Command& c) {
   KernelResult r;
   r.name = rk.h.name;
   r.uid = kd.uid;
-  r.start_cycle = start;
-  r.cycles = rr.end_cycle - start;
+  r.start_cycle = op.start;
+  r.cycles = rr.end_cycle - op.start;
   for (auto& s : dsm) {
     r.insn += s.thread_insn;
     r.warp_insn += s.warp_insn;
@@ -396,14 +529,11 @@ void Simulator::do_kernel(const Command& c) {
     }
     r.occupancy = act > 0 ? 100.0 * occ_acc / (act * cfg_.max_warps_per_sm) : 0;
   }
-  r.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  r.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - op.t_admit).count();
   r.deadlock = rr.deadlock;
-  r.epochs = rr.epochs;
-  if (rr.cap) cap_hit_ = true;
-  tot_cycle_ = eng_->now();
+  r.epochs = op.epochs;
   tot_insn_ += r.insn;
   tot_warp_insn_ += r.warp_insn;
-  tot_cta_ += kd.n_cta;
   if (power_) {
     r.avg_power_w = ptrack_.kernel_avg_power();
     char hdr[512];
@@ -415,27 +545,51 @@ void Simulator::do_kernel(const Command& c) {
       power_steady_->flush();
     }
     if (power_trace_) power_trace_->flush();
+    ptrack_.begin_kernel();
   }
+  if (visualizer_) visualizer_->flush();
   results_.push_back(r);
   print_kernel_stats(r, dsm, dmem);
   print_sim_time();
   if (rr.deadlock) {
-    deadlock_ = true;
     print("GPGPU-Sim uArch: ERROR ** deadlock detected: last writeback core %u @ gpu_sim_cycle %llu (+ gpu_tot_sim_cycle %llu)\n",
-          0u, (unsigned long long)r.cycles, (unsigned long long)start);
+          0u, (unsigned long long)r.cycles, (unsigned long long)op.start);
     // what every stuck unit is waiting for (reference prints the pipeline in
     // debug mode): busy memory channels first, then the SMs
     std::string d = dump_pipeline(-2, -1) + dump_pipeline(-1, -2);
     if (d.size() > 60000) d = d.substr(0, 60000) + "\n... (truncated)\n";
     print("%s", d.c_str());
   }
+  // the slot is free again; the operation leaves the window
+  slot_op_[slot] = nullptr;
+  for (auto it = win_.begin(); it != win_.end(); ++it)
+    if (it->get() == &op) {
+      win_.erase(it);
+      break;
+    }
+  ++kernels_done_;
+  if (dopt_.checkpoint_option && kernels_done_ == (uint32_t)dopt_.checkpoint_kernel) ckpt_pending_ = true;
+  if (ckpt_pending_ && win_.empty() && !eng_->running()) {
+    write_checkpoint(next_cmd_ - 1);
+    ckpt_pending_ = false;
+  }
 }
 
-RunResult Simulator::run_sampled(uint64_t start, const RunLimits& lim0, const std::string& kname) {
+// Run in gpu_stat_sample_freq slices, one power / visualizer / trace sample
+// per slice, until a kernel completes (or a limit stops the run)
+RunResult Simulator::run_sampled(const RunLimits& lim0) {
   // HW / HYBRID modes take one sample per kernel (the hardware counters are per kernel)
   const bool hw = power_ && (dopt_.power_mode == 1 || dopt_.power_mode == 2);
   const uint64_t freq = std::max<uint64_t>(dopt_.stat_sample_freq, std::max<uint32_t>(1, cfg_.icnt_latency));
   const double mhz = 1e9 / (double)cfg_.per_core;
+  // samples are named after the oldest running kernel
+  std::string kname;
+  uint32_t best = ~0u;
+  for (auto* op : slot_op_)
+    if (op && op->kd.uid < best) {
+      best = op->kd.uid;
+      kname = op->rk->h.name;
+    }
   Activity hwa;
   bool have_hw = false;
   if (hw) {
@@ -448,20 +602,18 @@ RunResult Simulator::run_sampled(uint64_t start, const RunLimits& lim0, const st
   std::vector<MemStats> m0, m1, dm;
   eng_->stats(sm0, m0);
   RunResult tot;
-  bool resume = false;
-  uint64_t t_prev = std::max(start, eng_->now());
+  uint64_t t_prev = eng_->now();
   for (;;) {
     RunLimits l = lim0;
-    l.resume = resume;
-    resume = true;
     if (!hw) {
       const uint64_t nxt = t_prev + freq;
       l.max_cycle = lim0.max_cycle ? std::min<uint64_t>(lim0.max_cycle, nxt) : nxt;
     }
-    RunResult r = eng_->run_kernel(start, dopt_.flush_l1, l);
+    RunResult r = eng_->run(l);
     tot.epochs += r.epochs;
     tot.end_cycle = r.end_cycle;
     tot.done = r.done;
+    tot.done_mask = r.done_mask;
     tot.deadlock = r.deadlock;
     tot.cap = r.cap;
     tot.hit_limit = r.cap;

@@ -2,6 +2,7 @@
 // loop (gpu-simulator/main.cc:55-206) re-built around the epoch engines.
 #pragma once
 #include <chrono>
+#include <deque>
 #include <fstream>
 #include <functional>
 #include <map>
@@ -45,6 +46,23 @@ struct CollectiveResult {
 // the other simulated GPUs over RCCL).  When unset the analytic model is used.
 using CollectiveHook = std::function<uint64_t(const Command&, uint64_t now_cycle)>;
 
+// one kernel or collective in the command window (reference main.cc
+// kernels_info + the busy_streams bookkeeping)
+struct StreamOp {
+  size_t cmd = 0;             // command index
+  bool coll = false;          // collective (else kernel)
+  uint64_t stream = 0;
+  bool launched = false;
+  int slot = -1;              // kernel: engine slot while running
+  uint64_t start = 0, end = 0;  // launch cycle; collective: completion cycle
+  uint64_t coll_cycles = 0;
+  uint64_t epochs = 0;        // engine epochs simulated while the kernel ran
+  std::unique_ptr<ReadyKernel> rk;
+  KernelDesc kd{};
+  const char* occ_limiter = "";
+  std::chrono::steady_clock::time_point t_admit;
+};
+
 class Simulator {
  public:
   // args: accel-sim.out style argument vector (without argv[0])
@@ -86,8 +104,17 @@ class Simulator {
 
  private:
   void print(const char* fmt, ...);
-  void do_kernel(const Command& c);
-  void do_collective(const Command& c);
+  // stream window (main.cc:74-197)
+  size_t window_size() const;
+  void admit(size_t end);                 // move commands [next_cmd_, end) into the window
+  void run_now(const Command& c);         // memcpy / communicator bookkeeping
+  void admit_kernel(size_t idx);
+  void launch_ready();
+  void launch_collective(StreamOp& op);
+  void step();                            // run to the next kernel / collective completion
+  void retire_collectives();
+  void finish_kernel(uint32_t slot, const RunResult& rr);
+  void check_limits();
   void print_kernel_stats(const KernelResult& r, const std::vector<SMStats>& sm, const std::vector<MemStats>& mem);
   void print_sim_time();
   // timing-state checkpoint at a kernel boundary / resume from one (returns first command to run)
@@ -95,8 +122,8 @@ class Simulator {
   void write_checkpoint(size_t cmd_index);
   size_t resume_checkpoint();
   uint32_t kernels_done_ = 0;
-  // run the current kernel in gpu_stat_sample_freq slices, one power sample per slice
-  RunResult run_sampled(uint64_t start, const RunLimits& lim, const std::string& kname);
+  // run in gpu_stat_sample_freq slices, one power sample per slice
+  RunResult run_sampled(const RunLimits& lim);
 
   OptionRegistry reg_;
   SimCfg cfg_{};
@@ -122,8 +149,12 @@ class Simulator {
   double sim_s_ = 0;
   bool deadlock_ = false;
   uint32_t next_uid_ = 1;
-  // currently loaded kernel (kept alive for the engine)
-  std::unique_ptr<ReadyKernel> cur_kernel_;
+  // command window: kernels / collectives admitted and not yet completed
+  std::deque<std::unique_ptr<StreamOp>> win_;
+  StreamOp* slot_op_[kMaxConc] = {};  // running kernel per engine slot
+  size_t next_cmd_ = 0;
+  bool stop_ = false;
+  bool ckpt_pending_ = false;
   bool cap_hit_ = false;  // a run cap (-gpgpu_max_insn / _max_cta / _max_completed_cta) stopped a kernel
 };
 

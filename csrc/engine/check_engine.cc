@@ -40,31 +40,31 @@ class CheckEngine final : public Engine {
     a_->init(c);
     b_->init(c);
   }
-  void load_kernel(const ReadyKernel& k, const KernelDesc& kd) override {
-    a_->load_kernel(k, kd);
-    b_->load_kernel(k, kd);
+  void launch(uint32_t slot, const ReadyKernel& k, const KernelDesc& kd) override {
+    a_->launch(slot, k, kd);
+    b_->launch(slot, k, kd);
   }
-  RunResult run_kernel(uint64_t start, bool flush_l1, const RunLimits& lim) override {
+  uint32_t running() const override { return a_->running(); }
+  RunResult run(const RunLimits& lim) override {
     RunResult total;
-    bool resume = lim.resume;
     for (;;) {
-      uint64_t cap = (resume ? a_->now() : start) + every_;
+      uint64_t cap = a_->now() + every_;
       const bool final_cap = lim.max_cycle && lim.max_cycle <= cap;
       if (final_cap) cap = lim.max_cycle;
-      RunLimits l{cap, lim.max_epochs, resume};
-      const RunResult ra = a_->run_kernel(start, flush_l1, l);
-      const RunResult rb = b_->run_kernel(start, flush_l1, l);
+      RunLimits l{cap, lim.max_epochs};
+      const RunResult ra = a_->run(l);
+      const RunResult rb = b_->run(l);
       total.epochs += ra.epochs;
       compare(ra, rb);
       if (ra.done || ra.deadlock || !ra.hit_limit || final_cap || ra.cap) {
         total.end_cycle = ra.end_cycle;
         total.done = ra.done;
+        total.done_mask = ra.done_mask;
         total.deadlock = ra.deadlock;
         total.hit_limit = ra.hit_limit;
         total.cap = ra.cap;
         return total;
       }
-      resume = true;
     }
   }
   uint64_t now() const override { return a_->now(); }
@@ -102,7 +102,7 @@ class CheckEngine final : public Engine {
   void compare(const RunResult& ra, const RunResult& rb) {
     ++checks_;
     const uint64_t cyc = a_->now();
-    if (ra.end_cycle != rb.end_cycle || ra.done != rb.done || ra.deadlock != rb.deadlock ||
+    if (ra.end_cycle != rb.end_cycle || ra.done_mask != rb.done_mask || ra.deadlock != rb.deadlock ||
         ra.hit_limit != rb.hit_limit || cyc != b_->now())
       fail(cyc, "run results differ: " + std::string(a_->name()) + " end " + std::to_string(ra.end_cycle) +
                     " done " + std::to_string(ra.done) + ", " + b_->name() + " end " + std::to_string(rb.end_cycle) +

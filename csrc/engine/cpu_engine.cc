@@ -100,6 +100,8 @@ class CpuEngine : public Engine {
     ovf_.assign((size_t)c.n_subpart * ovf_cap_, Pkt{});
     epoch_ = 0;
     cycle_ = 0;
+    kt_ = KernelTab{};
+    kt_.mix = c.concurrent_kernel_sm;
     if (c_.trace_mask) {
       const size_t units = (size_t)c.n_sm + c.n_mem;
       trace_ev_.assign(units * c_.trace_cap, TraceEv{});
@@ -119,27 +121,26 @@ class CpuEngine : public Engine {
     }
   }
 
-  void load_kernel(const ReadyKernel& k, const KernelDesc& kd) override {
-    kern_ = &k;
-    kd_ = kd;
-    kd_.insts = k.insts.data();
-    kd_.streams = k.streams.data();
-    accs_ = k.accs.data();
+  void launch(uint32_t slot, const ReadyKernel& k, const KernelDesc& kd) override {
+    if (slot >= (uint32_t)kMaxConc || (kt_.active >> slot & 1u)) throw std::runtime_error("launch: kernel slot busy");
+    if (k.insts.size() > kIdxMask) throw std::runtime_error("kernel trace exceeds 2^29 warp instructions");
+    KernelDesc& d = kt_.k[slot];
+    d = kd;
+    d.insts = k.insts.data();
+    d.accs = k.accs.data();
+    d.streams = k.streams.data();
+    kt_.active |= 1u << slot;
   }
+  uint32_t running() const override { return kt_.active; }
 
-  RunResult run_kernel(uint64_t start, bool flush_l1, const RunLimits& lim) override {
+  RunResult run(const RunLimits& lim) override {
     RunResult res;
-    if (start > cycle_) cycle_ = start;
     const SimCfg& c = c_;
     const uint64_t E = c.icnt_latency;
-    if (!lim.resume) {
-      for (auto& s : sms_) {
-        SmCtx x = ctx_sm(0);
-        sm_kernel_init<SeqPar>(s, x, s.ks, cycle_, flush_l1 ? 1u : 0u);
-      }
-      ready_ = sms_.empty() ? 0 : sms_[0].ks.ready_cycle;
+    if (!kt_.active) {
+      res.end_cycle = cycle_;
+      return res;
     }
-    const uint64_t ready = ready_;
     for (;;) {
       const uint32_t cur = (uint32_t)(epoch_ & 1), prev = cur ^ 1u;
       const uint64_t t0 = cycle_, t1 = t0 + E;
@@ -153,9 +154,9 @@ class CpuEngine : public Engine {
         if (i < nsm) {
           SMState& s = sms_[i];
           SmCtx x = ctx_sm(cur);
-          sm_epoch<SeqPar>(s, x, s.ks, *pub_, prev, t0, t1, box_rep_[prev].data(), cnt_rep_[prev].data(), cap_rep_,
+          sm_epoch<SeqPar>(s, x, *pub_, prev, t0, t1, box_rep_[prev].data(), cnt_rep_[prev].data(), cap_rep_,
                            c.n_subpart, epoch_);
-          sm_publish<SeqPar>(s, x, s.ks, *pub_, cur);
+          sm_publish<SeqPar>(s, x, *pub_, cur);
         } else {
           ChanState& ch = chs_[i - nsm];
           MemCtx m = ctx_mem(cur, t1);
@@ -163,14 +164,14 @@ class CpuEngine : public Engine {
           chan_publish<SeqPar>(ch, m, *pub_, cur);
         }
       }
-      const uint32_t next_done = pub_->next_cta[cur] >= kd_.n_cta ? 1u : 0u;
-      EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, ready, next_done, epoch_, lim.max_cycle,
-                                                kd_.stop_when_issued);
+      EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, kt_, epoch_, lim.max_cycle);
       ++epoch_;
       ++res.epochs;
       cycle_ = d.next_start;
       if (d.done) {
         res.done = true;
+        res.done_mask = d.done;
+        kt_.active &= ~d.done;
         break;
       }
       if (d.deadlock) {
@@ -192,7 +193,6 @@ class CpuEngine : public Engine {
   }
 
   uint64_t now() const override { return cycle_; }
-  uint64_t ready_ = 0;  // cycle the current kernel may start issuing CTAs
   std::vector<TraceEv> trace_ev_;
   std::vector<uint32_t> trace_cnt_;
 
@@ -253,7 +253,7 @@ class CpuEngine : public Engine {
     h.ovf = ovf_.size();
     h.cycle = cycle_;
     h.epoch = epoch_;
-    h.ready = ready_;
+    h.ready = kt_.active;
     return h;
   }
 
@@ -291,15 +291,14 @@ class CpuEngine : public Engine {
     r.get(ovf_.data(), ovf_.size() * sizeof(Pkt));
     cycle_ = h.cycle;
     epoch_ = h.epoch;
-    ready_ = h.ready;
+    if (h.ready) throw std::runtime_error("engine state: image taken with kernels running");
   }
 
  private:
   SmCtx ctx_sm(uint32_t cur) {
     SmCtx x;
     x.cfg = &c_;
-    x.k = &kd_;
-    x.acc = accs_;
+    x.kt = &kt_;
     x.outbox = box_req_[cur].data();
     x.outcnt = cnt_req_[cur].data();
     x.out_cap = cap_req_;
@@ -329,9 +328,7 @@ class CpuEngine : public Engine {
   std::vector<Pkt> ovf_;  // arrival backlog rings [n_subpart][ovf_cap_]
   uint32_t ovf_cap_ = 0;
   uint64_t epoch_ = 0, cycle_ = 0;
-  const ReadyKernel* kern_ = nullptr;
-  KernelDesc kd_{};
-  const TAcc* accs_ = nullptr;
+  KernelTab kt_{};
 };
 
 }  // namespace

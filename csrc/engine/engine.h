@@ -17,13 +17,13 @@ namespace asim {
 struct RunLimits {
   uint64_t max_cycle = 0;   // absolute cycle cap (0 = none)
   uint64_t max_epochs = 0;  // safety cap (0 = none)
-  bool resume = false;      // continue the current kernel after a hit_limit stop (no re-init)
 };
 
 struct RunResult {
   uint64_t end_cycle = 0;
   uint64_t epochs = 0;
-  bool done = false;
+  bool done = false;        // at least one kernel completed (done_mask)
+  uint32_t done_mask = 0;   // bit k: the kernel in slot k completed at end_cycle
   bool deadlock = false;
   bool hit_limit = false;
   bool cap = false;  // stopped by -gpgpu_max_insn / -gpgpu_max_cta / -gpgpu_max_completed_cta
@@ -34,10 +34,15 @@ class Engine {
   virtual ~Engine() = default;
   virtual const char* name() const = 0;
   virtual void init(const SimCfg& c) = 0;
-  // make `k` the current kernel (uploads its trace)
-  virtual void load_kernel(const ReadyKernel& k, const KernelDesc& kd) = 0;
-  // simulate the current kernel from `start` until it completes
-  virtual RunResult run_kernel(uint64_t start, bool flush_l1, const RunLimits& lim) = 0;
+  // start kernel `k` in free slot `slot` (< kMaxConc; uploads its trace): its
+  // CTAs dispatch from kd.ready_cycle on.  `k` must stay alive until the
+  // kernel completes.
+  virtual void launch(uint32_t slot, const ReadyKernel& k, const KernelDesc& kd) = 0;
+  // simulate the running kernels until one (or more, same epoch) completes,
+  // a limit is hit, or deadlock; completed slots are free again afterwards
+  virtual RunResult run(const RunLimits& lim) = 0;
+  // bit k: slot k holds a running kernel
+  virtual uint32_t running() const = 0;
   // cycle at which the next epoch would start
   virtual uint64_t now() const = 0;
   // L2 pre-fill for MemcpyHtoD (reference perf_memcpy_to_gpu, gpu-sim.cc:2116-2136)
@@ -73,7 +78,7 @@ inline uint32_t backlog_cap(const SimCfg& c) {
 
 struct EngineStateHeader {
   uint64_t magic = 0x41534d5354415445ull;  // "ASMSTATE"
-  uint64_t version = 3;  // 3: UnitPub records, no instruction window
+  uint64_t version = 4;  // 4: kernel slots (concurrent kernels)
   uint64_t n_sm = 0, n_mem = 0, sm_bytes = 0, ch_bytes = 0, pub_bytes = 0;
   uint64_t box_req = 0, cnt_req = 0, box_rep = 0, cnt_rep = 0;  // element counts per parity
   uint64_t ovf = 0;                                              // arrival backlog packets (all sub-partitions)

@@ -38,8 +38,7 @@ namespace asim {
 struct GpuArgs {
   SimCfg cfg;          // by value: kernel-argument (constant) memory, read with scalar loads
   const SimCfg* __restrict__ cfg_g;  // device copy: read-only, uniform addresses -> scalar loads
-  KernelDesc kd;
-  const TAcc* acc;
+  const KernelTab* kt;               // running kernels (copied into LDS at launch)
   SMState* sms;
   ChanState* chs;
   EpochPub* pub;
@@ -52,11 +51,8 @@ struct GpuArgs {
   uint32_t ovf_cap;
   uint64_t epoch0;
   uint64_t cycle0;
-  uint64_t ready_cycle;
   uint64_t max_cycle;
   uint32_t max_epochs;
-  uint32_t init_kernel;
-  uint32_t flush_l1;
   uint32_t nblocks;
   GpuCtl* ctl;
   uint64_t* prof;  // [nblocks][kProfSlots] shader-clock cycles per stage (profiling build)
@@ -113,7 +109,7 @@ __device__ __forceinline__ void swap_out(T* dst, const T* lds) {
 
 extern __shared__ __attribute__((aligned(16))) char g_lds[];
 constexpr size_t kStateLds = ((sizeof(SMState) > sizeof(ChanState) ? sizeof(SMState) : sizeof(ChanState)) + 15) / 16 * 16;
-constexpr size_t kCfgOff = kStateLds + (sizeof(KernelDesc) + 15) / 16 * 16;
+constexpr size_t kCfgOff = kStateLds + (sizeof(KernelTab) + 15) / 16 * 16;
 constexpr size_t kProfOff = kCfgOff + (sizeof(SimCfg) + 15) / 16 * 16;
 constexpr int kProfSlots = 36;
 struct ProfLds {
@@ -180,21 +176,25 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     copy_state(s, &a.sms[b]);
   else
     copy_state(ch, &a.chs[b - c.n_sm]);
-  // kernel descriptor lives in LDS behind the state (never in scratch)
-  KernelDesc* kdl = reinterpret_cast<KernelDesc*>(g_lds + kStateLds);
+  // kernel table lives in LDS behind the state (never in scratch)
+  KernelTab* ktl = reinterpret_cast<KernelTab*>(g_lds + kStateLds);
+  {
+    static_assert(sizeof(KernelTab) % 16 == 0, "kernel table must be 16-byte granular");
+    const uint4* src = reinterpret_cast<const uint4*>(a.kt);
+    uint4* dst = reinterpret_cast<uint4*>(ktl);
+    for (int i = (int)(threadIdx.x & 63); i < (int)(sizeof(KernelTab) / 16); i += 64) dst[i] = src[i];
+  }
   ProfLds* pl = reinterpret_cast<ProfLds*>(g_lds + kProfOff);
   if ((threadIdx.x & 63) == 0) {
-    *kdl = a.kd;
     pl->last = __builtin_amdgcn_s_memtime();
     pl->slot = 31;
     for (int i = 0; i < kProfSlots; ++i) pl->acc[i] = 0;
   }
   __syncthreads();
-  const KernelDesc& kd = *kdl;
+  const KernelTab& kt = *ktl;
   SmCtx sx;
   sx.cfg = &c;
-  sx.k = &kd;
-  sx.acc = a.acc;
+  sx.kt = &kt;
   sx.out_cap = a.cap_req;
   sx.n_src_sm = c.n_sm;
   MemCtx mx;
@@ -203,16 +203,6 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   mx.n_src_sub = c.n_subpart;
   mx.ovf = a.ovf;
   mx.ovf_cap = a.ovf_cap;
-  if (a.init_kernel) {
-    sx.outbox = a.box_req[0];
-    sx.outcnt = a.cnt_req[0];
-    for (uint32_t k = 0; k < nmine; ++k) {
-      const uint32_t u = unit_k(sliced ? nmine - 1 - k : k);  // end with unit b resident
-      if (u >= c.n_sm) continue;
-      swap_to(u);
-      sm_kernel_init<P>(*s, sx, s->ks, a.cycle0, a.flush_l1);
-    }
-  }
   uint64_t epoch = a.epoch0, cycle = a.cycle0;
   uint64_t t_work0 = a.ework ? __builtin_amdgcn_s_memtime() : 0;
   uint32_t done = 0, dead = 0, capped = 0;
@@ -231,9 +221,9 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
       if (u < c.n_sm) {
         sx.outbox = a.box_req[cur];
         sx.outcnt = a.cnt_req[cur];
-        sm_epoch<P>(*s, sx, s->ks, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep,
+        sm_epoch<P>(*s, sx, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep,
                     c.n_subpart, epoch);
-        sm_publish<P>(*s, sx, s->ks, *a.pub, cur);
+        sm_publish<P>(*s, sx, *a.pub, cur);
       } else {
         mx.outbox = a.box_rep[cur];
         mx.outcnt = a.cnt_rep[cur];
@@ -264,13 +254,11 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
       }
       t_work0 = t_exit;
     }
-    const uint32_t next_done = a.pub->next_cta[cur] >= kd.n_cta ? 1u : 0u;
-    EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, a.ready_cycle, next_done, epoch, a.max_cycle,
-                                      kd.stop_when_issued);
+    EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, kt, epoch, a.max_cycle);
     P::prof(28);
     ++epoch;
     cycle = P::uni(d.next_start);
-    if (P::uni(d.done)) { done = 1; break; }
+    if (P::uni(d.done)) { done = P::uni(d.done); break; }
     if (P::uni(d.deadlock)) { dead = 1; break; }
     if (P::uni(d.limit)) { capped = 1; break; }
     if (a.max_cycle && cycle >= a.max_cycle) break;
@@ -415,32 +403,41 @@ class GpuEngine : public Engine {
     HIPCHECK(hipMemset(d_ovf_, 0, sizeof(Pkt) * c.n_subpart * (size_t)ovf_cap_));
     HIPCHECK(hipMalloc(&d_ctl_, sizeof(GpuCtl)));
     HIPCHECK(hipHostMalloc(&h_ctl_, sizeof(GpuCtl)));
+    HIPCHECK(hipMalloc(&d_kt_, sizeof(KernelTab)));
+    kt_ = KernelTab{};
+    kt_.mix = c.concurrent_kernel_sm;
     epoch_ = 0;
     cycle_ = 0;
   }
 
-  void load_kernel(const ReadyKernel& k, const KernelDesc& kd) override {
-    kd_ = kd;
-    upload(d_insts_, cap_insts_, k.insts.data(), k.insts.size() * sizeof(TInst));
-    upload(d_accs_, cap_accs_, k.accs.data(), k.accs.size() * sizeof(TAcc));  // may be empty (no memory ops)
-    upload(d_streams_, cap_streams_, k.streams.data(), k.streams.size() * sizeof(WStream));
-    kd_.insts = reinterpret_cast<const TInst*>(d_insts_);
-    kd_.streams = reinterpret_cast<const WStream*>(d_streams_);
-    fresh_kernel_ = true;
+  void launch(uint32_t slot, const ReadyKernel& k, const KernelDesc& kd) override {
+    if (slot >= (uint32_t)kMaxConc || (kt_.active >> slot & 1u)) throw std::runtime_error("launch: kernel slot busy");
+    if (k.insts.size() > kIdxMask) throw std::runtime_error("kernel trace exceeds 2^29 warp instructions");
+    SlotBufs& sb = bufs_[slot];
+    upload(sb.insts, sb.cap_insts, k.insts.data(), k.insts.size() * sizeof(TInst));
+    upload(sb.accs, sb.cap_accs, k.accs.data(), k.accs.size() * sizeof(TAcc));  // may be empty (no memory ops)
+    upload(sb.streams, sb.cap_streams, k.streams.data(), k.streams.size() * sizeof(WStream));
+    KernelDesc& d = kt_.k[slot];
+    d = kd;
+    d.insts = reinterpret_cast<const TInst*>(sb.insts);
+    d.accs = reinterpret_cast<const TAcc*>(sb.accs);
+    d.streams = reinterpret_cast<const WStream*>(sb.streams);
+    kt_.active |= 1u << slot;
   }
+  uint32_t running() const override { return kt_.active; }
 
-  RunResult run_kernel(uint64_t start, bool flush_l1, const RunLimits& lim) override {
+  RunResult run(const RunLimits& lim) override {
     RunResult res;
-    if (start > cycle_) cycle_ = start;
-    if (!lim.resume) ready_ = cycle_ + c_.kernel_launch_latency + (uint64_t)c_.tb_launch_latency * kd_.n_cta;
-    const uint64_t ready = ready_;
-    bool first = !lim.resume;
+    if (!kt_.active) {
+      res.end_cycle = cycle_;
+      return res;
+    }
+    HIPCHECK(hipMemcpy(d_kt_, &kt_, sizeof(KernelTab), hipMemcpyHostToDevice));
     for (;;) {
       GpuArgs a{};
       a.cfg = c_;
       a.cfg_g = d_cfg_;
-      a.kd = kd_;
-      a.acc = reinterpret_cast<const TAcc*>(d_accs_);
+      a.kt = d_kt_;
       a.sms = d_sms_;
       a.chs = d_chs_;
       a.pub = d_pub_;
@@ -456,11 +453,8 @@ class GpuEngine : public Engine {
       a.ovf_cap = ovf_cap_;
       a.epoch0 = epoch_;
       a.cycle0 = cycle_;
-      a.ready_cycle = ready;
       a.max_cycle = lim.max_cycle;
       a.max_epochs = epochs_per_launch_;
-      a.init_kernel = first ? 1u : 0u;
-      a.flush_l1 = flush_l1 ? 1u : 0u;
       a.nblocks = nblocks_;
       a.ctl = d_ctl_;
       HIPCHECK(hipMemsetAsync(d_ctl_, 0, sizeof(GpuCtl), stream_));
@@ -483,12 +477,16 @@ class GpuEngine : public Engine {
       HIPCHECK(le);
       HIPCHECK(ce);
       HIPCHECK(se);
-      first = false;
       if (h_ctl_->error) throw std::runtime_error("GPU engine: grid barrier timed out (blocks not co-resident?)");
       epoch_ = h_ctl_->end_epoch;
       cycle_ = h_ctl_->end_cycle;
       res.epochs += h_ctl_->epochs_run;
-      if (h_ctl_->done) { res.done = true; break; }
+      if (h_ctl_->done) {
+        res.done = true;
+        res.done_mask = h_ctl_->done;
+        kt_.active &= ~h_ctl_->done;
+        break;
+      }
       if (h_ctl_->deadlock) { res.deadlock = true; break; }
       if (h_ctl_->cap) { res.hit_limit = true; res.cap = true; break; }
       if ((lim.max_cycle && cycle_ >= lim.max_cycle) || (lim.max_epochs && res.epochs >= lim.max_epochs)) {
@@ -502,7 +500,6 @@ class GpuEngine : public Engine {
   }
 
   uint64_t now() const override { return cycle_; }
-  uint64_t ready_ = 0;
 
   void memcpy_fill_l2(uint64_t addr, uint64_t bytes) override {
     std::vector<ChanState> hc(c_.n_mem);
@@ -584,7 +581,7 @@ class GpuEngine : public Engine {
     h.ovf = (uint64_t)c_.n_subpart * ovf_cap_;
     h.cycle = cycle_;
     h.epoch = epoch_;
-    h.ready = ready_;
+    h.ready = kt_.active;
     return h;
   }
   void save_state(std::vector<uint8_t>& out) override {
@@ -628,7 +625,7 @@ class GpuEngine : public Engine {
     ul(d_ovf_, w.ovf * sizeof(Pkt));
     cycle_ = h.cycle;
     epoch_ = h.epoch;
-    ready_ = h.ready;
+    if (h.ready) throw std::runtime_error("engine state: image taken with kernels running");
   }
 
  private:
@@ -658,9 +655,12 @@ class GpuEngine : public Engine {
     fr(d_ovf_);
     fr(d_trace_ev_);
     fr(d_trace_cnt_);
-    fr(d_insts_);
-    fr(d_accs_);
-    fr(d_streams_);
+    for (SlotBufs& b : bufs_) {
+      fr(b.insts);
+      fr(b.accs);
+      fr(b.streams);
+    }
+    fr(d_kt_);
     if (h_ctl_) (void)hipHostFree(h_ctl_);
     if (stream_) (void)hipStreamDestroy(stream_);
   }
@@ -684,10 +684,15 @@ class GpuEngine : public Engine {
   GpuCtl* h_ctl_ = nullptr;
   TraceEv* d_trace_ev_ = nullptr;
   uint32_t* d_trace_cnt_ = nullptr;
-  void* d_insts_ = nullptr;
-  void* d_accs_ = nullptr;
-  void* d_streams_ = nullptr;
-  size_t cap_insts_ = 0, cap_accs_ = 0, cap_streams_ = 0;
+  struct SlotBufs {  // device copies of one kernel slot's trace
+    void* insts = nullptr;
+    void* accs = nullptr;
+    void* streams = nullptr;
+    size_t cap_insts = 0, cap_accs = 0, cap_streams = 0;
+  };
+  SlotBufs bufs_[kMaxConc];
+  KernelTab kt_{};
+  KernelTab* d_kt_ = nullptr;
   uint32_t cap_req_ = 0, cap_rep_ = 0;
   uint64_t epoch_ = 0, cycle_ = 0;
   uint32_t epochs_per_launch_ = 4096;
@@ -764,9 +769,6 @@ class GpuEngine : public Engine {
     }
   }
 
- private:
-  KernelDesc kd_{};
-  bool fresh_kernel_ = false;
 };
 
 }  // namespace

@@ -168,7 +168,8 @@ template <class B>
 struct SmView {
   B& base;
   SV_VAL(id);
-  SV_VAL(kernel_cta_slots);
+  SV_REF(l1_sets);
+  SV_REF(l1_assoc);
   SV_REF(cycle);
   SV_VAL(last_progress);
   SV_VAL(epoch_end);
@@ -196,6 +197,14 @@ struct SmView {
   SV_WARP(cta_live);
   SV_WARP(cta_bar);
   SV_WARP(cta_nexit);
+  SV_REF(cta_ks);
+  SV_REF(cta_wbase);
+  SV_REF(cta_nw);
+  SV_REF(n_cta_k);
+  SV_REF(cta_wmask);
+  SV_REF(used_thr);
+  SV_REF(used_regs);
+  SV_REF(used_shmem);
   SV_VAL(n_cta_active);
   SV_VAL(n_warps_live);
   SV_VAL(live_mask);
@@ -240,7 +249,6 @@ struct SmView {
   SV_REF(skey);
   SV_REF(sref);
   SV_REF(srank);
-  SV_REF(ks);
   // statistics: counter word k lives in lane (k & 63) of stv[k >> 6], so an
   // update is one masked VALU add instead of an LDS read-modify-write
   uint64_t stv[2];
@@ -264,7 +272,7 @@ struct SmView {
   }
 
 #define SV_SCALARS(X)                                                                                   \
-  X(id) X(kernel_cta_slots) X(last_progress) X(epoch_end) X(out_port_free) X(age_ctr) X(n_cta_active)    \
+  X(id) X(last_progress) X(epoch_end) X(out_port_free) X(age_ctr) X(n_cta_active)    \
   X(n_warps_live) X(live_mask) X(n_wait_flags) X(fetch_rr) X(n_pend) X(idoc_mask) X(oc_mask) X(oc_read_mask)         \
   X(l1_stamp) X(skipped_cycles) X(min_emit) X(outq_head) X(outq_n) X(outstanding) X(inq_head) X(inq_n)
 #define SV_WARPS(X) \
@@ -273,13 +281,15 @@ struct SmView {
   X(cta_nexit) X(sched_last) X(w_iline)
 
   __device__ __forceinline__ explicit SmView(B& b)
-      : base(b), cycle(b.cycle), w_wait(b.w_wait), w_slot_lds(b.w_slot_lds), w_lds_st(b.w_lds_st),
+      : base(b), l1_sets(b.l1_sets), l1_assoc(b.l1_assoc), cycle(b.cycle), w_wait(b.w_wait), w_slot_lds(b.w_slot_lds), w_lds_st(b.w_lds_st),
         w_slot_pend(b.w_slot_pend),
-        w_slot_dst(b.w_slot_dst), cta_id(b.cta_id),
+        w_slot_dst(b.w_slot_dst), cta_id(b.cta_id), cta_ks(b.cta_ks), cta_wbase(b.cta_wbase), cta_nw(b.cta_nw),
+        n_cta_k(b.n_cta_k), cta_wmask(b.cta_wmask), used_thr(b.used_thr), used_regs(b.used_regs),
+        used_shmem(b.used_shmem),
         idoc_inst(b.idoc_inst), oc_inst(b.oc_inst),
         wb_cnt(b.wb_cnt), wb(b.wb), hit_cnt(b.hit_cnt), hit(b.hit), l1(b.l1), mshr(b.mshr),
         pend(b.pend), il1(b.il1), imshr(b.imshr),
-        outq(b.outq), ocnt(b.ocnt), inq(b.inq), skey(b.skey), sref(b.sref), srank(b.srank), ks(b.ks) {
+        outq(b.outq), ocnt(b.ocnt), inq(b.inq), skey(b.skey), sref(b.sref), srank(b.srank) {
 #define SV_LD(m) m = sv_uni(b.m);
     SV_SCALARS(SV_LD)
 #undef SV_LD

@@ -29,6 +29,9 @@ struct WavePar {
   static __device__ __forceinline__ uint32_t red_sum(uint32_t v) {
     return wave_reduce(v, [](uint32_t a, uint32_t b) { return a + b; });
   }
+  static __device__ __forceinline__ uint32_t red_or(uint32_t v) {
+    return wave_reduce(v, [](uint32_t a, uint32_t b) { return a | b; });
+  }
   static __device__ __forceinline__ uint64_t red_sum64(uint64_t v) {
     // lane partials of 64-bit sums: reduce the two halves as 32-bit sums of
     // 16-bit limbs so no carry is lost (64 lanes x 2^16 fits in 32 bits)

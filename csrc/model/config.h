@@ -125,6 +125,8 @@ struct SimCfg {
   uint32_t regs_per_sm;
   uint32_t shmem_per_sm;
   uint32_t shmem_per_block;
+  uint32_t concurrent_kernel_sm;  // -gpgpu_concurrent_kernel_sm: CTAs of several kernels share an SM
+  uint32_t max_concurrent_kernel; // running kernels (<= kMaxConc)
   // ---- front end / issue ----
   uint32_t n_sched;
   uint32_t sched_policy;

@@ -26,19 +26,20 @@ struct UnitPub {
                      // packets it injected this epoch arrives (-sim_event_skip)
   uint64_t prog;     // SM: last progress cycle
   uint64_t insn;     // SM: thread instructions issued so far (-gpgpu_max_insn)
-  uint32_t req;      // SM: CTA slots it can accept next epoch
-  uint32_t idle;     // SM: drained and kernel fully dispatched; channel: idle
+  uint32_t req;      // SM: bit k: it requests CTAs of the kernel in slot k next epoch
+  uint16_t idle;     // SM: drained and every kernel fully dispatched; channel: idle
+  uint8_t kbusy;     // SM: bit k: it holds CTAs of the kernel in slot k
+  uint8_t pad8;
   uint32_t drained;  // SM: holds no work (launch latency may be pending)
   uint32_t ctas;     // SM: CTAs completed so far (-gpgpu_max_completed_cta)
-  uint64_t pad;
+  uint64_t reqk;     // SM: byte k: CTAs of slot k it can accept next epoch
 };
 static_assert(sizeof(UnitPub) == 48, "UnitPub layout");
 // epoch-boundary publications, double buffered by epoch parity
 struct EpochPub {
   UnitPub sm[2][kMaxSmTot];
   UnitPub ch[2][kMaxChTot];
-  uint32_t next_cta[2];  // replicated dispatch cursor (published by SM 0)
-  uint32_t pad[2];
+  uint32_t next_cta[2][kMaxConc];  // replicated dispatch cursors per kernel slot (published by SM 0)
 };
 
 // upper bound of one SM's quiet-cycle look-ahead at an epoch boundary
@@ -46,7 +47,7 @@ constexpr uint64_t kSkipHorizon = 1ull << 16;
 
 // decision every participant derives after the barrier
 struct EpochDecision {
-  uint32_t done;        // kernel complete (all SMs idle)
+  uint32_t done;        // bit k: the kernel in slot k completed
   uint32_t all_idle;    // SMs and memory idle
   uint32_t deadlock;
   uint32_t limit;       // -gpgpu_max_insn / _max_completed_cta / _max_cta reached: stop
@@ -54,17 +55,20 @@ struct EpochDecision {
 };
 
 // ---------------------------------------------------------------------------
-// CTA dispatch: round-robin rounds over requesting SMs, rotated by epoch.
+// CTA dispatch (reference gpgpu_sim::issue_block2core, gpu-sim.cc and
+// simt_core_cluster::issue_block2core, shader.cc:4502-4535): round-robin
+// rounds over the SMs requesting CTAs of one kernel, rotated by epoch.
 template <class P>
-SIM_HDI void cta_dispatch(SMState& s, const SmCtx& x, SmKernel& ks, const UnitPub* pubs, uint32_t n_sm,
+SIM_HDI void cta_dispatch(SMState& s, const SmCtx& x, uint32_t ks, const UnitPub* pubs, uint32_t n_sm,
                           uint32_t rot) {
-  const KernelDesc& k = *x.k;
-  if (ks.next_cta >= k.n_cta) return;
+  const KernelDesc& k = x.kt->k[ks];
+  if (s.next_cta[ks] >= k.n_cta) return;
   const uint32_t me = s.id;
-  auto req = [&](int j) -> uint32_t { return pubs[j].req; };
+  const uint32_t sh = ks * 8;
+  auto req = [&](int j) -> uint32_t { return (uint32_t)(pubs[j].reqk >> sh) & 0xffu; };
   const uint32_t my_q = req((int)me);
   const uint32_t my_rank = (me + n_sm - rot) % n_sm;
-  uint32_t base = ks.next_cta;
+  uint32_t base = s.next_cta[ks];
   for (uint32_t r = 0; r < (uint32_t)kMaxCta && base < k.n_cta; ++r) {
     uint32_t pr = P::sum((int)n_sm, [&](int j) -> uint32_t { return req(j) > r ? 1u : 0u; });
     if (pr == 0) break;
@@ -76,44 +80,85 @@ SIM_HDI void cta_dispatch(SMState& s, const SmCtx& x, SmKernel& ks, const UnitPu
       if (cta < k.n_cta) {
         // lowest free slot
         int slot = -1;
-        for (uint32_t i = 0; i < s.kernel_cta_slots; ++i)
+        for (uint32_t i = 0; i < (uint32_t)kMaxCta; ++i)
           if (!s.cta_valid[i]) { slot = (int)i; break; }
-        if (slot >= 0) sm_launch_cta<P>(s, x, (uint32_t)slot, cta);
+        if (slot >= 0) sm_launch_cta<P>(s, x, (uint32_t)slot, cta, ks);
       }
     }
     base += pr;
   }
-  ks.next_cta = base < k.n_cta ? base : k.n_cta;
+  s.next_cta[ks] = base < k.n_cta ? base : k.n_cta;
 }
 
-SIM_HDI uint32_t sm_free_slots(const SMState& s) {
-  return s.kernel_cta_slots > s.n_cta_active ? s.kernel_cta_slots - s.n_cta_active : 0;
+// kernel slots in launch (uid) order: older kernels are served first
+SIM_HDI uint32_t slot_order(const KernelTab& kt, uint8_t* order) {
+  uint32_t n = 0;
+  for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k) {
+    if (!(kt.active >> k & 1u)) continue;
+    uint32_t i = n++;
+    while (i > 0 && kt.k[order[i - 1]].uid > kt.k[k].uid) {
+      order[i] = order[i - 1];
+      --i;
+    }
+    order[i] = (uint8_t)k;
+  }
+  return n;
 }
 
-// kernel (re)initialisation of an SM: first epoch of a new kernel
+// CTAs of kernel slot `ks` this SM can accept on top of what it holds and of
+// `held` warps / `thr` threads / ... already promised to older kernels
+// (shader_core_ctx::can_issue_1block / occupy_shader_resource_1block):
+// per-kernel CTA limit, CTA slots, threads, registers, shared memory, and a
+// contiguous run of free warps per CTA
+struct SmRes {
+  uint64_t wmask;
+  uint32_t ctas, thr, regs, shmem;
+};
+SIM_HDI uint32_t sm_cta_fit(const SMState& s, const SimCfg& c, const KernelDesc& k, uint32_t ks, SmRes& r) {
+  const uint32_t nwm = amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
+  const uint32_t max_cta = amin<uint32_t>(c.max_cta_per_sm, kMaxCta);
+  uint32_t n = 0;
+  while (n < (uint32_t)kMaxCta) {
+    if ((uint32_t)s.n_cta_k[ks] + n >= k.cta_per_sm || r.ctas >= max_cta) break;
+    if (r.thr + k.thr_cta > c.max_threads_per_sm || r.regs + k.regs_cta > c.regs_per_sm) break;
+    if (k.shmem_per_cta && r.shmem + k.shmem_per_cta > k.shmem_cap) break;
+    const int b = warp_run_fit(r.wmask, k.warps_per_cta, nwm);
+    if (b < 0) break;
+    r.wmask |= (k.warps_per_cta >= 64 ? ~0ull : ((1ull << k.warps_per_cta) - 1)) << b;
+    r.ctas++;
+    r.thr += k.thr_cta;
+    r.regs += k.regs_cta;
+    r.shmem += k.shmem_per_cta;
+    ++n;
+  }
+  return n;
+}
+
+// kernel slot (re)initialisation of an SM: first epoch after a launch
 template <class P>
-SIM_HDI void sm_kernel_init(SMState& s, const SmCtx& x, SmKernel& ks, uint64_t start, uint32_t flush_l1) {
-  const KernelDesc& k = *x.k;
-  ks.uid = k.uid;
-  ks.next_cta = 0;
-  ks.start_cycle = start;
-  ks.ready_cycle = start + x.cfg->kernel_launch_latency + (uint64_t)x.cfg->tb_launch_latency * k.n_cta;
-  s.kernel_cta_slots = k.cta_per_sm;
-  if (flush_l1) {
-    P::each(kMaxL1Lines, [&](int i) {
-      s.l1[i].valid = 0;
-      s.l1[i].dirty = 0;
-    });
-    P::sync();
+SIM_HDI void sm_kernels_init(SMState& s, const SmCtx& x) {
+  const KernelTab& kt = *x.kt;
+  for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k) {
+    if (!(kt.active >> k & 1u) || s.k_uid[k] == kt.k[k].uid) continue;
+    s.k_uid[k] = kt.k[k].uid;
+    s.next_cta[k] = 0;
+    if (kt.k[k].flush_l1) {
+      P::each(kMaxL1Lines, [&](int i) {
+        s.l1[i].valid = 0;
+        s.l1[i].dirty = 0;
+      });
+      P::sync();
+    }
   }
 }
 
 // one epoch of one SM: [t0, t1) core cycles
 template <class P>
-SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& pub, uint32_t prev,
+SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t prev,
                       uint64_t t0, uint64_t t1, const Pkt* inbox, const uint32_t* incnt, uint32_t in_cap,
                       uint32_t n_sub, uint64_t epoch_idx) {
   const SimCfg& c = *x.cfg;
+  sm_kernels_init<P>(s, x);
   // 0. cycles [s.cycle, t0) were fast-forwarded by epoch_decide (nothing could
   //    happen in them): account them exactly like quiet cycles
   if (t0 > s.cycle && (s.n_cta_active || !sm_idle(s))) sm_skip<P>(s, c, t0 - s.cycle);
@@ -124,10 +169,16 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& 
                    s_scratch_key(s), s_scratch_ref(s), s_scratch_rank(s), kInQ);
   // 2. CTA dispatch (state published at the previous boundary)
   P::prof(13);
-  if (t0 >= ks.ready_cycle)
+  {
     // rotation by simulated time (t0 / epoch length), not by the epoch counter,
     // so fast-forwarded epochs leave the CTA -> SM assignment unchanged
-    cta_dispatch<P>(s, x, ks, pub.sm[prev], c.n_sm, (uint32_t)((t0 / c.icnt_latency) % c.n_sm));
+    const KernelTab& kt = *x.kt;
+    uint8_t order[kMaxConc];
+    const uint32_t nk = slot_order(kt, order);
+    for (uint32_t i = 0; i < nk; ++i)
+      if (t0 >= kt.k[order[i]].ready_cycle)
+        cta_dispatch<P>(s, x, order[i], pub.sm[prev], c.n_sm, (uint32_t)((t0 / c.icnt_latency) % c.n_sm));
+  }
   // 3. (instructions are read from the kernel trace directly)
   P::prof(14);
   // 4. cycles
@@ -143,7 +194,7 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& 
         if (t < t1 && c.event_skip) {
           // fast-forward cycles in which provably nothing happens
           P::tick(18);
-          const uint64_t nx = P::uni(sm_quiet_until<P>(v, c, x.k->insts, t, t1));
+          const uint64_t nx = P::uni(sm_quiet_until<P>(v, c, *x.kt, t, t1));
           if (nx > t) {
             sm_skip<P>(v, c, nx - t);
             t = nx;
@@ -158,32 +209,61 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, SmKernel& ks, const EpochPub& 
 
 // publish SM outbox counts + boundary state
 template <class P>
-SIM_HDI void sm_publish(SMState& s, const SmCtx& x, const SmKernel& ks, EpochPub& pub, uint32_t cur) {
+SIM_HDI void sm_publish(SMState& s, const SmCtx& x, EpochPub& pub, uint32_t cur) {
   const SimCfg& c = *x.cfg;
   P::each((int)c.n_subpart, [&](int d) {
     x.outcnt[(uint64_t)d * x.n_src_sm + s.id] = s.ocnt[d];
     s.ocnt[d] = 0;
   });
   P::sync();
-  const bool ready_for_cta = ks.next_cta < x.k->n_cta;
-  const uint32_t req = ready_for_cta ? sm_free_slots(s) : 0u;
-  const uint32_t idle = (ks.next_cta >= x.k->n_cta && sm_idle(s)) ? 1u : 0u;
+  // CTA requests per kernel, oldest kernel first: each kernel asks for what
+  // is left after the older ones' requests (a request the dispatch does not
+  // fill is simply renewed at the next boundary)
+  const KernelTab& kt = *x.kt;
+  uint8_t order[kMaxConc];
+  const uint32_t nk = slot_order(kt, order);
+  SmRes r{s.cta_wmask, s.n_cta_active, s.used_thr, s.used_regs, s.used_shmem};
+  uint32_t req = 0, kbusy = 0;
+  uint64_t reqk = 0;
+  bool all_dispatched = true;
+  uint32_t other = 0;  // kernels holding (or promised) this SM's resources
+  for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k)
+    if (s.n_cta_k[k]) kbusy |= 1u << k;
+  other = kbusy;
+  for (uint32_t i = 0; i < nk; ++i) {
+    const uint32_t k = order[i];
+    const KernelDesc& kd = kt.k[k];
+    if (s.next_cta[k] >= kd.n_cta) continue;
+    all_dispatched = false;
+    // without -gpgpu_concurrent_kernel_sm an SM runs one kernel at a time
+    if (!kt.mix && (other & ~(1u << k))) continue;
+    const uint32_t n = sm_cta_fit(s, c, kd, k, r);
+    if (n) {
+      req |= 1u << k;
+      reqk |= (uint64_t)n << (8 * k);
+      other |= 1u << k;
+    }
+  }
+  const uint32_t idle = (all_dispatched && sm_idle(s)) ? 1u : 0u;
   uint64_t nx = ~0ull;
   if (c.event_skip && (s.n_cta_active || !sm_idle(s)))
-    nx = sm_quiet_until<P>(s, c, x.k->insts, s.cycle, s.cycle + kSkipHorizon) * c.per_core;
+    nx = sm_quiet_until<P>(s, c, kt, s.cycle, s.cycle + kSkipHorizon) * c.per_core;
   nx = amin(nx, s.min_emit);
   UnitPub u;
   u.next = nx;
   u.prog = s.last_progress;
   u.insn = s.sget(SK(thread_insn));
   u.req = req;
-  u.idle = idle;
+  u.idle = (uint16_t)idle;
+  u.kbusy = (uint8_t)kbusy;
+  u.pad8 = 0;
   u.drained = sm_idle(s) ? 1u : 0u;
   u.ctas = (uint32_t)s.sget(SK(ctas_done));
-  u.pad = 0;
+  u.reqk = reqk;
   P::one([&] {
     pub.sm[cur][s.id] = u;
-    if (s.id == 0) pub.next_cta[cur] = ks.next_cta;
+    if (s.id == 0)
+      for (int k = 0; k < kMaxConc; ++k) pub.next_cta[cur][k] = s.next_cta[k];
   });
 }
 
@@ -214,21 +294,22 @@ SIM_HDI void chan_publish(ChanState& ch, const MemCtx& x, EpochPub& pub, uint32_
   u.prog = 0;
   u.insn = 0;
   u.req = 0;
-  u.idle = idle;
+  u.idle = (uint16_t)idle;
+  u.kbusy = 0;
+  u.pad8 = 0;
   u.drained = idle;
   u.ctas = 0;
-  u.pad = 0;
+  u.reqk = 0;
   P::one([&] { pub.ch[cur][ch.id] = u; });
 }
 
 // every participant computes the same decision from the published state
 template <class P>
 SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_t cur, uint64_t t1,
-                                   uint64_t ready_cycle, uint32_t next_cta_done, uint64_t epoch_idx,
-                                   uint64_t max_cycle, uint32_t stop_when_issued = 0) {
+                                   const KernelTab& kt, uint64_t epoch_idx, uint64_t max_cycle) {
   EpochDecision d;
   // one pass over every unit's record (one load per unit), then reductions
-  uint32_t nbusy = 0, undrained = 0, nreq = 0, cbusy = 0, ctas = 0;
+  uint32_t nbusy = 0, undrained = 0, cbusy = 0, ctas = 0, reqs = 0, kbusy = 0;
   uint64_t sm_next = ~0ull, ch_next = ~0ull, prog = 0, insn = 0;
   P::lane_loop((int)c.n_sm, [&](int j) {
     const UnitPub u = pub.sm[cur][j];
@@ -236,7 +317,8 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
     ctas += u.ctas;
     nbusy += u.idle ? 0u : 1u;
     undrained += u.drained ? 0u : 1u;
-    nreq += u.req ? 1u : 0u;
+    reqs |= u.req;
+    kbusy |= u.kbusy;
     sm_next = amin<uint64_t>(sm_next, u.next);
     prog = amax<uint64_t>(prog, u.prog & ((1ull << 56) - 1));  // progress stamps are < 2^56
   });
@@ -247,25 +329,47 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   });
   nbusy = P::uni(P::red_sum(nbusy));
   undrained = P::uni(P::red_sum(undrained));
-  nreq = P::uni(P::red_sum(nreq));
+  reqs = P::uni(P::red_or(reqs));
+  kbusy = P::uni(P::red_or(kbusy));
   cbusy = P::uni(P::red_sum(cbusy));
   sm_next = P::uni(P::red_min64(sm_next));
   ch_next = P::uni(P::red_min64(ch_next));
   prog = P::uni(P::red_max64(prog));
-  d.done = (nbusy == 0) ? 1u : 0u;
+  // per kernel slot: fully dispatched, launch latency, completion
+  const uint32_t active = kt.active;
+  uint32_t undisp = 0, cut = 0;
+  uint64_t ready_min = ~0ull, ready_req = ~0ull, ready_max = 0;
+  for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k) {
+    if (!(active >> k & 1u)) continue;
+    const KernelDesc& kd = kt.k[k];
+    ready_max = amax<uint64_t>(ready_max, kd.ready_cycle);
+    if (pub.next_cta[cur][k] < kd.n_cta) {
+      undisp |= 1u << k;
+      ready_min = amin<uint64_t>(ready_min, kd.ready_cycle);
+      if (reqs >> k & 1u) ready_req = amin<uint64_t>(ready_req, amax<uint64_t>(t1, kd.ready_cycle));
+    } else if (kd.stop_when_issued) {
+      cut = 1;
+    }
+  }
+  // a kernel completes when all its CTAs were dispatched and have finished;
+  // the last running kernel also waits for the SMs to drain (write-backs,
+  // instruction fetches), as the whole GPU going idle ends a serial kernel
+  uint32_t done = active & ~undisp & ~kbusy;
+  if (done == active && nbusy != 0) done = 0;
+  d.done = done;
   d.all_idle = (nbusy == 0 && cbusy == 0) ? 1u : 0u;
   d.next_start = t1;
   d.deadlock = 0;
-  // run caps checked while the kernel runs (reference gpgpu_sim::active,
+  // run caps checked while kernels run (reference gpgpu_sim::active,
   // gpu-sim.cc:1071-1094): instructions, completed CTAs, issued CTAs
   d.limit = 0;
   if (c.max_insn && P::uni(P::red_sum64(insn)) >= c.max_insn) d.limit = 1;
   if (c.max_completed_cta && P::uni(P::red_sum(ctas)) >= c.max_completed_cta) d.limit = 1;
-  if (stop_when_issued && next_cta_done) d.limit = 1;
+  if (cut) d.limit = 1;
   // fast-forward over the kernel launch latency when nothing is in flight
-  if (!next_cta_done && cbusy == 0 && t1 < ready_cycle && undrained == 0) {
+  if (undisp && cbusy == 0 && t1 < ready_min && undrained == 0) {
     uint64_t E = c.icnt_latency;
-    uint64_t skip = (ready_cycle - t1) / E * E;
+    uint64_t skip = (ready_min - t1) / E * E;
     d.next_start = t1 + skip;
   }
   // Whole-epoch fast-forward (conservative PDES with exact next-event times):
@@ -275,7 +379,7 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   // pending event at all (a deadlock) nothing is skipped.
   if (c.event_skip && !d.done) {
     uint64_t ev = amin(sm_next, ch_next);
-    if (!next_cta_done && nreq) ev = amin(ev, amax(t1, ready_cycle) * c.per_core);
+    if (ready_req != ~0ull) ev = amin(ev, ready_req * c.per_core);
     if (ev != ~0ull) {
       const uint64_t E = c.icnt_latency;
       const uint64_t tc = ev / c.per_core;  // the next epoch may start no later than this
@@ -289,8 +393,9 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   if (c.deadlock_window && nbusy && ((t1 / c.icnt_latency) & 63) == 0) {
     // newest progress stamp over all SMs
     const uint64_t last = prog;
-    if (t1 > last + c.deadlock_window && t1 > ready_cycle + c.deadlock_window) d.deadlock = 1;
+    if (t1 > last + c.deadlock_window && t1 > ready_max + c.deadlock_window) d.deadlock = 1;
   }
+  (void)epoch_idx;
   return d;
 }
 

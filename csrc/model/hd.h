@@ -58,6 +58,7 @@ struct SeqPar {
     for (int i = 0; i < n; ++i) f(i);
   }
   static SIM_HDI uint32_t red_sum(uint32_t v) { return v; }
+  static SIM_HDI uint32_t red_or(uint32_t v) { return v; }
   static SIM_HDI uint64_t red_sum64(uint64_t v) { return v; }
   static SIM_HDI uint64_t red_min64(uint64_t v) { return v; }
   static SIM_HDI uint64_t red_max64(uint64_t v) { return v; }

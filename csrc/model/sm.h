@@ -17,20 +17,10 @@
 
 namespace asim {
 
-// ---- per-access record produced by the trace-ingest coalescer ----
-// line (128B aligned) | sector mask (bits 0..3) | (bytes/4-1) in bits 4..6 is
-// NOT packed: keep it simple and 16-byte aligned.
-struct TAcc {
-  uint64_t line;     // 128B-aligned line address
-  uint16_t bytes;    // bytes touched (write packet size)
-  uint8_t sectors;   // 32B sector mask
-  uint8_t bank;      // L1 bank (precomputed)
-  uint32_t pad;
-};
-static_assert(sizeof(TAcc) == 16, "TAcc must stay 16 bytes");
 
 // Warps read their instructions straight from the kernel's decoded trace
-// (KernelDesc::insts, HBM on the GPU): w_next / w_head / w_end index it.
+// (KernelDesc::insts, HBM on the GPU): w_next / w_head / w_end index it, with
+// the kernel slot in the top bits (inst_at, types.h).
 
 enum WarpFlags : uint8_t {
   WF_ACTIVE = 1,
@@ -146,19 +136,12 @@ enum IL1Out : uint8_t { IL1_HIT = 0, IL1_MISS, IL1_MSHR_HIT, IL1_RES_FAIL };
 // SMStats::power_acc slots
 enum PwrCounter : uint8_t { PWR_CONST_OPERAND = 0 };
 
-// per-SM kernel bookkeeping (replicated identically in every SM)
-struct SmKernel {
-  uint32_t uid;
-  uint32_t next_cta;
-  uint64_t ready_cycle;  // kernel launch latency expires
-  uint64_t start_cycle;
-};
 
 // Complete state of one SM.  On the GPU it lives in LDS for the duration of
 // a launch (copied in/out of HBM), on the CPU it is a plain struct.
 struct alignas(16) SMState {
   uint32_t id;
-  uint32_t kernel_cta_slots;  // CTA slots for the current kernel
+  uint16_t l1_sets, l1_assoc; // L1 geometry of the kernel that last found the SM empty (adaptive carve-out)
   uint64_t cycle;             // next core cycle to simulate
   uint64_t last_progress;     // last cycle an instruction completed (deadlock)
   uint64_t epoch_end;         // current epoch end cycle (exclusive)
@@ -190,6 +173,12 @@ struct alignas(16) SMState {
   uint8_t cta_live[kMaxCta];     // warps not yet completed
   uint8_t cta_bar[kMaxCta];      // warps arrived at barrier
   uint8_t cta_nexit[kMaxCta];    // warps exited (excluded from barrier count)
+  uint8_t cta_ks[kMaxCta];       // kernel slot of the CTA
+  uint8_t cta_wbase[kMaxCta];    // first warp of the CTA (its warps are contiguous)
+  uint8_t cta_nw[kMaxCta];       // warps of the CTA
+  uint8_t n_cta_k[kMaxConc];     // CTAs resident per kernel slot
+  uint64_t cta_wmask;            // warps owned by resident CTAs
+  uint32_t used_thr, used_regs, used_shmem;  // resources held by resident CTAs
   uint32_t n_cta_active;
   uint32_t n_warps_live;         // warps with WF_ACTIVE (occupancy statistic)
   uint64_t live_mask;            // bit w: warp w has WF_ACTIVE
@@ -239,7 +228,10 @@ struct alignas(16) SMState {
   uint64_t skey[kInQ];       // gather scratch
   uint32_t sref[kInQ];
   uint32_t srank[kInQ > kMaxSubTot ? kInQ : kMaxSubTot];
-  SmKernel ks;               // replicated kernel dispatch state
+  // replicated kernel dispatch state (identical in every SM): per slot, the
+  // uid the SM initialised it for and the next CTA to hand out
+  uint32_t k_uid[kMaxConc];
+  uint32_t next_cta[kMaxConc];
   SMStats st;
   // statistics by word index (SK below); the GPU engine's register view keeps
   // the counters in lanes during the cycle loop (csrc/engine/sm_view.h)
@@ -258,8 +250,7 @@ SIM_HDI uint32_t* s_scratch_rank(SMState& s) { return s.srank; }
 // context passed to every SM step
 struct SmCtx {
   const SimCfg* cfg;
-  const KernelDesc* k;
-  const TAcc* acc;       // coalesced access table of the kernel
+  const KernelTab* kt;   // running kernels (instructions, access tables, CTA streams)
   Pkt* outbox;           // this epoch's outbox base: [dst][src][cap]
   uint32_t* outcnt;      // [dst][src]
   uint32_t out_cap;      // per (dst,src) capacity (>= epoch length)
@@ -295,11 +286,16 @@ SIM_HDI void sm_reset(S& s, uint32_t id) {
   s.id = id;
 }
 
-// L1 geometry in use (adaptive per kernel)
-SIM_HDI CacheGeom l1_geom(const SimCfg& c, const KernelDesc& k) {
+// L1 geometry in use (adaptive per kernel: set when a CTA launches into an
+// empty SM, shader_core_ctx::issue_block2core's cache reconfiguration)
+template <class S>
+SIM_HDI CacheGeom l1_geom(const SimCfg& c, const S& s) {
   CacheGeom g = c.l1;
-  g.nsets = k.l1_sets;
-  g.assoc = k.l1_assoc;
+  const uint32_t sets = s.l1_sets;
+  if (sets) {
+    g.nsets = sets;
+    g.assoc = s.l1_assoc;
+  }
   return g;
 }
 
@@ -500,7 +496,7 @@ SIM_HDI void l1_evict(S& s, const SimCfg& c, uint32_t idx) {
 template <class P, class S>
 SIM_HDI void l1_fill(S& s, const SmCtx& x, uint64_t line, uint8_t sectors, uint64_t now) {
   const SimCfg& c = *x.cfg;
-  const CacheGeom g = l1_geom(c, *x.k);
+  const CacheGeom g = l1_geom(c, s);
   if (!g.disabled) {
     uint32_t set = cache_set_index(g, line);
     int w = l1_find<P>(s, g, set, line);
@@ -610,9 +606,9 @@ SIM_HDI void il1_prefetch(S& s, const SimCfg& c, uint64_t line) {
 }
 
 template <class P, class S>
-SIM_HDI bool il1_fetch(S& s, const SimCfg& c, const TInst* insts, uint32_t w) {
+SIM_HDI bool il1_fetch(S& s, const SimCfg& c, const KernelTab& kt, uint32_t w) {
   const CacheGeom& g = c.il1;
-  const uint32_t pc = P::uni(insts[P::uni((uint32_t)s.w_next[w])].pc);
+  const uint32_t pc = P::uni(inst_at(kt, P::uni((uint32_t)s.w_next[w])).pc);
   const uint64_t line = (kProgramMemStart + pc) & ~127ull;
   const uint32_t set = cache_set_index(g, line);
   const int way = il1_find<P>(s, g, set, line);
@@ -700,7 +696,7 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
   }
   const bool is_store = in.cls == OC_STORE;
   const bool atomic = (in.flags & F_ATOMIC) != 0;
-  const CacheGeom g = l1_geom(c, *x.k);
+  const CacheGeom g = l1_geom(c, s);
   const bool bypass = atomic || (in.flags & F_BYPASS_L1) || c.gmem_skip_l1 || g.disabled;
   const uint32_t nacc = in.width;
   const uint32_t stype = l1_stat_type(in.space, is_store, atomic);
@@ -708,8 +704,10 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
   uint32_t processed = 0;
   uint32_t unext = P::uni(u.next);
   const uint8_t uslot = P::uni(u.slot);
+  // access table of the warp's kernel (slot in the top bits of its stream index)
+  const TAcc* accs = x.kt->k[P::uni((uint32_t)s.w_end[w]) >> kSlotShift].accs;
   while (unext < nacc && processed < c.l1_banks) {
-    const TAcc a = P::uni(x.acc[in.mem + unext]);
+    const TAcc a = P::uni(accs[in.mem + unext]);
     uint32_t bbit = 1u << (a.bank & 31);
     if (banks_used & bbit) break;  // L1 bank conflict: next cycle
     if (c.perfect_mem) {
@@ -1033,11 +1031,11 @@ SIM_HDI void sm_alloc_collectors(S& s, const SimCfg& c) {
 // ---------------------------------------------------------------------------
 // issue
 template <class P, class S>
-SIM_HDI void sm_barrier_check(S& s, uint32_t cta, const KernelDesc& k) {
+SIM_HDI void sm_barrier_check(S& s, uint32_t cta) {
   uint32_t live = s.cta_live[cta] - s.cta_nexit[cta];
   if (s.cta_bar[cta] > 0 && s.cta_bar[cta] >= live) {
-    uint32_t base = cta * k.warps_per_cta;
-    for (uint32_t w = base; w < base + k.warps_per_cta && w < (uint32_t)kMaxWarps; ++w)
+    const uint32_t base = s.cta_wbase[cta], nw = s.cta_nw[cta];
+    for (uint32_t w = base; w < base + nw && w < (uint32_t)kMaxWarps; ++w)
       s.w_flags[w] &= (uint8_t)~WF_BARRIER;
     s.cta_bar[cta] = 0;
   }
@@ -1063,10 +1061,10 @@ SIM_HDI bool warp_can_issue_i(const S& s, const SimCfg& c, int w, const TInst& i
   return true;
 }
 template <class S>
-SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, const TInst* insts, int w, uint32_t nsched,
+SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, const KernelTab& kt, int w, uint32_t nsched,
                             uint64_t idoc_busy) {
   if (!(s.w_flags[w] & WF_ACTIVE) || s.w_ibuf[w] == 0) return false;
-  const TInst in = insts[s.w_head[w]];  // ibuf > 0: the head is inside the warp's stream
+  const TInst in = inst_at(kt, s.w_head[w]);  // ibuf > 0: the head is inside the warp's stream
   return warp_can_issue_i(s, c, w, in, nsched, idoc_busy);
 }
 
@@ -1077,7 +1075,6 @@ template <class P, class S>
 SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32_t w, const TInst& in,
                          uint32_t hidx) {
   const SimCfg& c = *x.cfg;
-  const KernelDesc& k = *x.k;
   if (trace_sm_on(c, TS_WARP_SCHEDULER, s.id))
     P::one([&] { trace_put(c, s.id, now, EV_ISSUE, (uint16_t)w, (uint64_t)in.pc | (uint64_t)in.opcode << 32); });
   s.w_head[w] = hidx + 1;
@@ -1098,14 +1095,14 @@ SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32
     if (hidx + 1 >= P::uni((uint32_t)s.w_end[w])) {
       s.w_flags[w] |= WF_EXITING;
       s.cta_nexit[cta]++;
-      sm_barrier_check<P>(s, cta, k);
+      sm_barrier_check<P>(s, cta);
     }
     return -1;
   }
   if (in.cls == OC_BARRIER) {
     s.w_flags[w] |= WF_BARRIER;
     s.cta_bar[cta]++;
-    sm_barrier_check<P>(s, cta, k);
+    sm_barrier_check<P>(s, cta);
     return -1;
   }
   if (in.cls == OC_MEMBAR) {
@@ -1181,7 +1178,7 @@ SIM_HDI bool waits_long_op(const S& s, int w, const TInst& in) {
 template <class P, class S>
 SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
-  const KernelDesc& k = *x.k;
+  const KernelTab& kt = *x.kt;
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
   const uint64_t idoc_busy = P::uni(s.idoc_mask);
@@ -1189,7 +1186,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   // (read straight from the kernel's trace in HBM: an L2-resident stream)
   const auto head = P::template lanes<TInst>(nw, [&](int w) -> TInst {
     const uint32_t h = s.w_head[w];
-    return h < s.w_end[w] ? k.insts[h] : TInst{};
+    return h < s.w_end[w] ? inst_at(kt, h) : TInst{};
   });
   // readiness of every warp (lane-parallel)
   const uint64_t live = P::uni(s.live_mask);
@@ -1274,7 +1271,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
     // warp's next buffered instruction issues in the same cycle if it is
     // ready and, with -gpgpu_dual_issue_diff_exec_units, uses another unit
     if (c.max_issue_per_warp > 1 && u1 >= 0 && P::uni((uint8_t)s.w_ibuf[w])) {
-      const TInst in2 = P::uni(k.insts[hidx + 1]);
+      const TInst in2 = P::uni(inst_at(kt, hidx + 1));
       const bool special = in2.cls == OC_EXIT || in2.cls == OC_BARRIER || in2.cls == OC_MEMBAR ||
                            in2.cls == OC_NOP || (in2.flags & F_WAITCNT);
       if (!special && (!c.dual_issue_diff || unit_of(c, in2.cls) != (uint32_t)u1) &&
@@ -1291,7 +1288,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
 // fetch/decode: refill the instruction buffer of up to fetch_throughput
 // warps whose buffer is empty (round-robin), perfect instruction cache
 template <class P, class S>
-SIM_HDI void sm_fetch(S& s, const SimCfg& c, const TInst* insts) {
+SIM_HDI void sm_fetch(S& s, const SimCfg& c, const KernelTab& kt) {
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   uint64_t need = P::ballot_m(P::uni(s.live_mask), [&](int w) {
     uint8_t f = s.w_flags[w];
@@ -1304,7 +1301,7 @@ SIM_HDI void sm_fetch(S& s, const SimCfg& c, const TInst* insts) {
     int b = ffs64(r);
     r &= r - 1;
     uint32_t w = (uint32_t)(b + start) % (uint32_t)nw;
-    if (icache && !il1_fetch<P>(s, c, insts, w)) {
+    if (icache && !il1_fetch<P>(s, c, kt, w)) {
       s.fetch_rr = w + 1;  // miss / reservation fail ends this cycle's fetch (shader.cc:997-1010)
       break;
     }
@@ -1317,12 +1314,34 @@ SIM_HDI void sm_fetch(S& s, const SimCfg& c, const TInst* insts) {
   }
 }
 
+// first warp of a free contiguous run of n warps among the first nw, or -1
+// (shader_core_ctx::find_available_hwtid: a CTA's hardware threads are contiguous)
+SIM_HDI int warp_run_fit(uint64_t used, uint32_t n, uint32_t nw) {
+  if (n == 0 || n > nw) return -1;
+  const uint64_t need = n >= 64 ? ~0ull : ((1ull << n) - 1);
+  for (uint32_t b = 0; b + n <= nw; ++b)
+    if (!((used >> b) & need)) return (int)b;
+  return -1;
+}
+
+// resources a resident CTA gives back when it completes
+template <class S>
+SIM_HDI void sm_cta_release(S& s, const KernelTab& kt, uint32_t cta) {
+  const uint32_t ks = s.cta_ks[cta];
+  const KernelDesc& k = kt.k[ks];
+  const uint32_t nw = s.cta_nw[cta];
+  s.cta_wmask = s.cta_wmask & ~((nw >= 64 ? ~0ull : ((1ull << nw) - 1)) << s.cta_wbase[cta]);
+  s.n_cta_k[ks] = (uint8_t)(s.n_cta_k[ks] - 1);
+  s.used_thr = s.used_thr - k.thr_cta;
+  s.used_regs = s.used_regs - k.regs_cta;
+  s.used_shmem = s.used_shmem - k.shmem_per_cta;
+}
+
 // stream exhausted without explicit EXIT -> treat as exit
 // warp retirement and CTA completion
 template <class P, class S>
 SIM_HDI void sm_retire(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
-  const KernelDesc& k = *x.k;
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint64_t live = P::uni(s.live_mask);
   uint64_t done = P::ballot_m(live, [&](int w) {
@@ -1361,37 +1380,56 @@ SIM_HDI void sm_retire(S& s, const SmCtx& x, uint64_t now) {
     if (s.cta_live[cta] == 0) {
       s.cta_valid[cta] = 0;
       s.n_cta_active--;
+      sm_cta_release(s, *x.kt, cta);
       s.sadd(SK(ctas_done), 1);
     } else {
-      sm_barrier_check<P>(s, cta, k);
+      sm_barrier_check<P>(s, cta);
     }
     s.last_progress = now;
   }
 }
 
 // ---------------------------------------------------------------------------
-// launch a CTA into slot `slot`
+// launch CTA `cta_id` of the kernel in slot `ks` into CTA slot `slot`, on the
+// first contiguous run of free warps
 template <class P, class S>
-SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id) {
-  const KernelDesc& k = *x.k;
+SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id, uint32_t ks) {
+  const KernelDesc& k = x.kt->k[ks];
+  const SimCfg& c = *x.cfg;
   const uint32_t wpc = k.warps_per_cta;
-  const uint32_t base = slot * wpc;
+  const uint32_t nwm = amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
+  const uint32_t base = (uint32_t)warp_run_fit(s.cta_wmask, wpc, nwm);  // checked by sm_cta_fit
+  const uint64_t wm = (wpc >= 64 ? ~0ull : ((1ull << wpc) - 1)) << base;
+  if (s.n_cta_active == 0) {
+    // an empty SM takes the kernel's L1 / shared-memory carve-out
+    s.l1_sets = (uint16_t)k.l1_sets;
+    s.l1_assoc = (uint16_t)k.l1_assoc;
+  }
   s.cta_valid[slot] = 1;
   s.cta_id[slot] = cta_id;
   s.cta_live[slot] = (uint8_t)wpc;
   s.cta_bar[slot] = 0;
   s.cta_nexit[slot] = 0;
+  s.cta_ks[slot] = (uint8_t)ks;
+  s.cta_wbase[slot] = (uint8_t)base;
+  s.cta_nw[slot] = (uint8_t)wpc;
+  s.cta_wmask |= wm;
+  s.n_cta_k[ks]++;
+  s.used_thr += k.thr_cta;
+  s.used_regs += k.regs_cta;
+  s.used_shmem += k.shmem_per_cta;
   s.n_cta_active++;
   s.n_warps_live += wpc;
-  s.live_mask |= (wpc >= 64 ? ~0ull : ((1ull << wpc) - 1)) << base;
+  s.live_mask |= wm;
   uint32_t age0 = s.age_ctr;
   s.age_ctr += wpc;
+  const uint32_t tag = ks << kSlotShift;
   P::each((int)wpc, [&](int i) {
     uint32_t w = base + (uint32_t)i;
     WStream ws = k.streams[(uint64_t)cta_id * wpc + (uint32_t)i];
-    s.w_next[w] = ws.begin;
-    s.w_head[w] = ws.begin;
-    s.w_end[w] = ws.begin + ws.count;
+    s.w_next[w] = tag | ws.begin;
+    s.w_head[w] = tag | ws.begin;
+    s.w_end[w] = tag | (ws.begin + ws.count);
     s.w_age[w] = age0 + (uint32_t)i;
     s.w_flags[w] = WF_ACTIVE;
     s.w_ibuf[w] = 0;
@@ -1429,7 +1467,7 @@ SIM_HDI void sm_cycle(S& s, const SmCtx& x, uint64_t now) {
   P::prof(7);
   sm_issue<P>(s, x, now);
   P::prof(8);
-  sm_fetch<P>(s, c, x.k->insts);
+  sm_fetch<P>(s, c, *x.kt);
   P::prof(9);
   sm_retire<P>(s, x, now);
   P::prof(10);
@@ -1474,7 +1512,7 @@ SIM_HDI uint64_t ring_next(const A& occ, uint32_t ring, uint64_t from, uint64_t 
 // per-cycle statistics (sm_skip).  This is what makes latency-bound phases
 // (every warp waiting on memory) cost one check instead of one cycle each.
 template <class P, class S>
-SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, const TInst* insts, uint64_t t, uint64_t limit) {
+SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, const KernelTab& kt, uint64_t t, uint64_t limit) {
   if (P::uni(s.ldst.busy) || P::uni(s.idoc_mask) || P::uni(s.oc_mask | s.oc_read_mask) || P::uni(s.outq_n)) return t;
   uint64_t nx = ring_next<P>(s.wb_occ, kWbRing, t, limit);
   if (nx == t) return t;
@@ -1495,7 +1533,7 @@ SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, const TInst* insts,
     if (drained && s.w_inflight[w] == 0 && s.w_stores[w] == 0 && s.w_loads[w] == 0) return true;  // retire
     if ((f & WF_MEMBAR) && s.w_stores[w] == 0) return true;
     if ((f & WF_WAITCNT) && waitcnt_met(s, w)) return true;
-    return warp_can_issue(s, c, insts, w, nsched, s.idoc_mask);  // issue
+    return warp_can_issue(s, c, kt, w, nsched, s.idoc_mask);  // issue
   });
   return act ? t : nx;
 }

@@ -103,6 +103,18 @@ struct WStream {
   uint32_t count;
 };
 
+// ---- per-access record produced by the trace-ingest coalescer ----
+// line (128B aligned) | sector mask (bits 0..3) | (bytes/4-1) in bits 4..6 is
+// NOT packed: keep it simple and 16-byte aligned.
+struct TAcc {
+  uint64_t line;     // 128B-aligned line address
+  uint16_t bytes;    // bytes touched (write packet size)
+  uint8_t sectors;   // 32B sector mask
+  uint8_t bank;      // L1 bank (precomputed)
+  uint32_t pad;
+};
+static_assert(sizeof(TAcc) == 16, "TAcc must stay 16 bytes");
+
 // Interconnect packet (32 B).  Time stamps are femtoseconds so that the
 // four clock domains (core/icnt/L2/DRAM, reference gpu-sim.cc:1047-1062) are
 // exact integers.
@@ -141,14 +153,35 @@ struct KernelDesc {
   uint32_t stream;
   uint32_t l1_sets, l1_assoc;  // adaptive L1 geometry chosen for this kernel
   uint32_t stop_when_issued;   // cut to the -gpgpu_max_cta remainder: the run ends once all CTAs issued
-  uint32_t pad_k;
+  uint32_t flush_l1;           // -gpgpu_flush_l1_cache: SMs drop their L1 when the kernel starts
+  // per-CTA SM resources (shader_core_ctx::occupy_shader_resource_1block):
+  // warp-padded threads, registers, and the shared-memory capacity of the
+  // carve-out chosen for this kernel
+  uint32_t thr_cta, regs_cta, shmem_cap, pad_k;
+  uint64_t ready_cycle;        // launch + kernel/CTA launch latency: first CTA dispatch
   uint64_t shmem_base;
   uint64_t local_base;
   uint64_t n_insts;
   const TInst* insts;
-  const TMem* mems;
-  const uint64_t* addrs;
+  const TAcc* accs;        // coalesced access table (inst.mem indexes it)
   const WStream* streams;  // [n_cta * warps_per_cta]
+  uint64_t pad_p;
 };
+
+// Concurrent kernels (reference gpgpu_sim::m_running_kernels, gpu-sim.cc:805-900,
+// and the stream window of gpu-simulator/main.cc:74-115).  A warp's
+// instruction indices (w_next / w_head / w_end) carry the kernel slot in
+// their top bits, so the fetch / issue paths index one merged instruction
+// space with no per-warp kernel lookup beyond the slot's base pointer.
+constexpr int kMaxConc = 8;
+constexpr uint32_t kSlotShift = 29;
+constexpr uint32_t kIdxMask = (1u << kSlotShift) - 1;
+struct KernelTab {
+  KernelDesc k[kMaxConc];
+  uint32_t active;  // bit k: slot k holds a launched kernel that has not completed
+  uint32_t mix;     // -gpgpu_concurrent_kernel_sm: one SM may hold CTAs of several kernels
+  uint64_t pad[3];
+};
+SIM_HDI const TInst& inst_at(const KernelTab& kt, uint32_t gi) { return kt.k[gi >> kSlotShift].insts[gi & kIdxMask]; }
 
 }  // namespace asim

@@ -1,0 +1,139 @@
+"""Concurrent kernels and the stream window (reference gpu-simulator/main.cc:74-115
+window of -gpgpu_max_concurrent_kernel commands with stream-busy gating, and
+shader.cc:4502-4535 -gpgpu_concurrent_kernel_sm CTA mixing on one SM), plus
+collectives on their own stream overlapping compute."""
+
+import pytest
+
+from accel_sim_framework_distributed_amd.models import presets
+from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+from accel_sim_framework_distributed_amd.tracegen.format import write_kernel_binary, write_kernelslist
+
+BASE = 0x7100_0000
+
+
+def _kernel(kid, stream, ctas=2, threads=64, alu=200, shmem=0, loads=4):
+    """`ctas` CTAs of a dependent FFMA chain with a few global loads."""
+    k = KernelBuilder(f"_Z2k{kid}Pf", (ctas, 1, 1), (threads, 1, 1), nregs=16, kid=kid, shmem=shmem)
+    k.header["stream"] = stream
+    g = k.g
+    for i in range(loads):
+        k.op("LDG.E", [8], [2], base=BASE + kid * (1 << 22) + g.gtid0 * 4 + i * (1 << 16), stride=4)
+        k.op("FFMA", [4], [4, 8])
+    for _ in range(alu):
+        k.op("FFMA", [4], [4, 5])
+    k.op("STG.E", [], [2, 4], base=BASE + kid * (1 << 22) + g.gtid0 * 4, stride=4)
+    k.op("EXIT")
+    return k.build()
+
+
+def _app(tmp_path, name, kernels, extra_cmds=()):
+    d = tmp_path / name
+    d.mkdir()
+    cmds = []
+    for i, k in enumerate(kernels, 1):
+        write_kernel_binary(str(d / f"kernel-{i}.asimk"), k)
+        cmds.append(f"kernel-{i}.asimk")
+    for pos, line in extra_cmds:
+        cmds.insert(pos, line)
+    return write_kernelslist(str(d), cmds)
+
+
+def _run(native, kl, conc, extra=None, engine="cpu"):
+    over = {"-gpgpu_concurrent_kernel_sm": "1" if conc else "0", "-gpgpu_perf_sim_memcpy": "0",
+            "-sim_engine": engine}
+    over.update(extra or {})
+    s = native.Simulator(presets.args_for("QV100", over) + ["-trace", kl], False)
+    assert s.run() == 0
+    return s
+
+
+def test_independent_streams_overlap(native, tmp_path):
+    kl = _app(tmp_path, "two", [_kernel(1, 1), _kernel(2, 2)])
+    ser = _run(native, kl, False)
+    con = _run(native, kl, True)
+    ks, kc = ser.kernels, con.kernels
+    assert [k["uid"] for k in ks] == [1, 2] and len(kc) == 2
+    # serial: kernel 2 starts after kernel 1 ends; concurrent: both start at once
+    assert ks[1]["start_cycle"] >= ks[0]["start_cycle"] + ks[0]["cycles"]
+    assert kc[0]["start_cycle"] == kc[1]["start_cycle"] == 0
+    assert con.tot_cycle < 0.75 * ser.tot_cycle
+    assert con.tot_cycle >= max(k["cycles"] for k in ks) * 0.9
+    assert con.tot_insn == ser.tot_insn
+    assert "launching kernel name: _Z2k2Pf uid: 2" in con.output
+
+
+def test_same_stream_stays_ordered(native, tmp_path):
+    kl = _app(tmp_path, "same", [_kernel(1, 3), _kernel(2, 3)])
+    ser = _run(native, kl, False)
+    con = _run(native, kl, True)
+    # the window holds both, but stream order serialises them exactly
+    assert con.tot_cycle == ser.tot_cycle
+    assert [k["cycles"] for k in con.kernels] == [k["cycles"] for k in ser.kernels]
+
+
+def test_kernels_share_one_sm(native, tmp_path):
+    # a single SM: with -gpgpu_concurrent_kernel_sm the two kernels' CTAs
+    # co-reside (warps / CTA slots permit); the SM then interleaves them
+    one = {"-gpgpu_n_clusters": "1"}
+    kl = _app(tmp_path, "one_sm", [_kernel(1, 1, ctas=2), _kernel(2, 2, ctas=2)])
+    ser = _run(native, kl, False, one)
+    con = _run(native, kl, True, one)
+    assert con.tot_cycle < 0.8 * ser.tot_cycle
+    assert con.tot_insn == ser.tot_insn
+
+
+def test_shared_memory_limits_mixing(native, tmp_path):
+    # each CTA takes 64 KB of the 96 KB shared memory: CTAs of the second
+    # kernel cannot join an SM holding one of the first, so one SM runs them
+    # back to back even with concurrent kernels enabled
+    one = {"-gpgpu_n_clusters": "1", "-gpgpu_shmem_size": "98304", "-gpgpu_adaptive_cache_config": "0",
+           "-gpgpu_kernel_launch_latency": "0"}
+    kl = _app(tmp_path, "shm", [_kernel(1, 1, ctas=1, shmem=65536), _kernel(2, 2, ctas=1, shmem=65536)])
+    ser = _run(native, kl, False, one)
+    con = _run(native, kl, True, one)
+    k1, k2 = con.kernels
+    assert k2["start_cycle"] == 0  # launched at once, but its CTA waits for the SM's shared memory
+    assert con.tot_cycle >= 0.95 * ser.tot_cycle
+    small = _app(tmp_path, "shm_small", [_kernel(1, 1, ctas=1, shmem=32768), _kernel(2, 2, ctas=1, shmem=32768)])
+    assert _run(native, small, True, one).tot_cycle < 0.7 * _run(native, small, False, one).tot_cycle
+
+
+def test_collective_overlaps_compute_on_its_stream(native, tmp_path):
+    # kernel on stream 1, an all-reduce on stream 2, a kernel after it on stream 2
+    coll = "ncclAllReduce,count=8388608,dtype=ncclFloat,op=ncclSum,nranks=8,stream=2"
+    kl = _app(tmp_path, "coll", [_kernel(1, 1, ctas=8, alu=400), _kernel(2, 2, ctas=8, alu=100)],
+              extra_cmds=[(1, coll)])
+    extra = {"-collective_model": "ring"}
+    ser = _run(native, kl, False, extra)
+    con = _run(native, kl, True, extra)
+    c = ser.collectives[0]["cycles"]
+    assert c > 0 and con.collectives[0]["cycles"] == c
+    k1s, k2s = ser.kernels
+    k1c, k2c = con.kernels
+    # serial: kernel, collective, kernel; concurrent: the collective runs under kernel 1
+    assert ser.tot_cycle >= k1s["cycles"] + c
+    assert k2c["start_cycle"] >= c and k2c["start_cycle"] < k1s["cycles"] + c
+    assert con.tot_cycle < ser.tot_cycle - min(c, k1s["cycles"]) // 2
+
+
+def test_window_size_bounds_running_kernels(native, tmp_path):
+    ks = [_kernel(i, i, ctas=1, alu=100) for i in range(1, 5)]
+    kl = _app(tmp_path, "win", ks)
+    con2 = _run(native, kl, True, {"-gpgpu_max_concurrent_kernel": "2"})
+    starts = sorted(k["start_cycle"] for k in con2.kernels)
+    assert starts[0] == starts[1] == 0 and starts[2] > 0
+    con4 = _run(native, kl, True, {"-gpgpu_max_concurrent_kernel": "4"})
+    assert all(k["start_cycle"] == 0 for k in con4.kernels)
+    assert con4.tot_cycle < con2.tot_cycle
+
+
+@pytest.mark.gpu
+def test_concurrent_gpu_matches_cpu(native, tmp_path):
+    kl = _app(tmp_path, "gpu", [_kernel(1, 1, ctas=40, alu=150), _kernel(2, 2, ctas=60, alu=80),
+                                _kernel(3, 1, ctas=20, alu=50)])
+    cpu = _run(native, kl, True)
+    gpu = _run(native, kl, True, engine="gpu")
+    assert gpu.tot_cycle == cpu.tot_cycle
+    assert [(k["uid"], k["start_cycle"], k["cycles"], k["insn"]) for k in gpu.kernels] == \
+        [(k["uid"], k["start_cycle"], k["cycles"], k["insn"]) for k in cpu.kernels]
