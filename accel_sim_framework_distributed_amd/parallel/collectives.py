@@ -169,6 +169,46 @@ class PacketCollective:
         return cyc
 
 
+class LocalRanks:
+    """All ranks in ONE process (threads), coupled like the distributed path:
+    ``hook(r)`` is rank r's collective hook.  At each collective every rank
+    deposits its start time and waits for the others; the packet link model
+    then runs once over all ranks' start times (``linksim_run_local``) and
+    each rank is charged its own finish - start.  This is the oracle the
+    RCCL / gloo path (PacketCollective over PacketExchange) must match bit
+    for bit, collectives overlapping compute included.  Usage:
+    ``sim_r.set_collective_hook(ranks.hook(r, sim_r))``."""
+
+    def __init__(self, nranks: int):
+        import threading
+        self.n = nranks
+        self.lock = threading.Lock()
+        self.barrier = threading.Barrier(nranks, timeout=600)
+        self.starts: List[int] = [0] * nranks
+        self.result: Optional[Dict] = None
+        self.events: List[List[Dict]] = [[] for _ in range(nranks)]
+
+    def hook(self, rank: int, sim):
+        def call(desc: Dict, now: int) -> int:
+            period = float(sim.core_period_ps)
+            start = int(round(now * period))
+            n = max(1, int(desc.get("nranks", 1)))
+            if n != self.n:
+                raise RuntimeError(f"collective over {n} ranks in a {self.n}-rank emulation")
+            kind, nbytes, root = desc["op"], int(desc["bytes"]), max(0, int(desc.get("root", 0)))
+            self.starts[rank] = start
+            if self.barrier.wait() == 0:
+                mod = _native.load()
+                self.result = mod.linksim_run_local(sim.link_params(), kind, nbytes, root, list(self.starts))
+            self.barrier.wait()
+            fin = int(self.result["finish_ps"][rank])
+            cyc = int(np.ceil((fin - start) / period))
+            self.events[rank].append(dict(op=kind, bytes=nbytes, nranks=n, now=now, cycles=cyc, mode="local-ranks"))
+            self.barrier.wait()  # every rank read the result before the next collective overwrites it
+            return cyc
+        return call
+
+
 def emulate(params: Dict, kind: str, nbytes: int, starts_ps: List[int], root: int = 0) -> Dict:
     """All ranks in-process (reference for the distributed path)."""
     mod = _native.load()

@@ -60,7 +60,7 @@ class DistributedSuite:
         self.collective_model = collective_model
         self.apps = []
         for app in sorted(os.listdir(root)):
-            if app.startswith("all-reduce") or app.startswith("."):
+            if app.startswith("all-reduce") or app.startswith("dp-step") or app.startswith("."):
                 continue
             if apps and app not in apps:
                 continue
@@ -79,6 +79,16 @@ class DistributedSuite:
         if not os.path.exists(ar):
             ar = os.path.join(root, "all-reduce", "kernelslist.g")
         self.allreduce = ar if os.path.exists(ar) else None
+        # one data-parallel training step per rank (tracegen/training.py):
+        # per-layer gradient all-reduces on a communication stream overlapping
+        # the backward pass; it replaces the all-reduce example when present
+        dp = os.path.join(root, f"dp-step-{world}", f"rank{rank}", "kernelslist.g")
+        self.dp_step = dp if os.path.exists(dp) and (not apps or "dp-step" in apps) else None
+        self.dp_last: Dict = {}
+        if self.dp_step:
+            # scheduled like any application (node placement, LPT order)
+            self.apps.append(("dp-step", self.dp_step))
+        self._calibrating = False
         self.sync = PacketCollective() if collective_model == "packet" else CollectiveSync(world)
         # HIP's current device is per host thread: worker threads start on
         # device 0, so every thread this suite creates binds this rank's GPU
@@ -166,6 +176,12 @@ class DistributedSuite:
         import time
         app, kl = app_kl
         t0 = time.perf_counter()
+        if app == "dp-step":
+            r = self._run_dp_step(engine, coupled=not self._calibrating)
+            dt = time.perf_counter() - t0
+            self.weights[app] = dt
+            self.times[(app, engine or ("gpu" if self.engine == "node" else self.engine))] = dt
+            return r
         s = self._sim(kl, engine)
         rc = s.run()
         if rc != 0:
@@ -189,12 +205,18 @@ class DistributedSuite:
         from concurrent.futures import ThreadPoolExecutor
         gslots = max(1, self.concurrency())
         cslots = self.cpu_slots(reserve=gslots)
-        with ThreadPoolExecutor(max_workers=gslots, initializer=self._bind_device) as gx, \
-                ThreadPoolExecutor(max_workers=cslots) as cx:
-            fg = [gx.submit(self._run_app, a, "gpu") for a in self.apps]
-            fc = [cx.submit(self._run_app, a, "cpu") for a in self.apps]
-            for f in fg + fc:
-                f.result()
+        # the DDP step is timed uncoupled (its collectives emulated locally):
+        # two engines running it at once must not both talk to the other ranks
+        self._calibrating = True
+        try:
+            with ThreadPoolExecutor(max_workers=gslots, initializer=self._bind_device) as gx, \
+                    ThreadPoolExecutor(max_workers=cslots) as cx:
+                fg = [gx.submit(self._run_app, a, "gpu") for a in self.apps]
+                fc = [cx.submit(self._run_app, a, "cpu") for a in self.apps]
+                for f in fg + fc:
+                    f.result()
+        finally:
+            self._calibrating = False
         return {a: {"gpu": self.times[(a, "gpu")], "cpu": self.times[(a, "cpu")]} for a, _ in self.apps}
 
     @staticmethod
@@ -248,6 +270,30 @@ class DistributedSuite:
             raise RuntimeError("all-reduce example failed\n" + s.output[-1500:])
         return "all-reduce", s.tot_insn, s.tot_cycle
 
+    def _run_dp_step(self, engine: Optional[str] = None, coupled: bool = True):
+        """The rank's DDP step with concurrent kernels: its all-reduces start
+        when the layer's gradient is ready and couple this rank's simulated
+        clock to the others' mid-step (packet link model over RCCL).
+        Uncoupled (calibration), the simulator emulates all ranks locally."""
+        self._bind_device()
+        extra = {"-collective_model": self.collective_model, "-gpgpu_concurrent_kernel_sm": "1"}
+        eng = engine or ("gpu" if self.engine == "node" else self.engine)
+        s = self.mod.Simulator(build_args(self.config, self.dp_step, eng, extra), self.verbose)
+        n0 = len(getattr(self.sync, "events", []))
+        if coupled:
+            s.set_collective_hook(lambda d, now, s=s: self.sync(s, d, now))
+        if s.run() != 0:
+            raise RuntimeError("dp step failed\n" + s.output[-1500:])
+        ev = getattr(self.sync, "events", [])[n0:] if coupled else []
+        if not coupled:
+            return "dp-step", s.tot_insn, s.tot_cycle
+        ks = s.kernels
+        comp = sum(k["cycles"] for k in ks)
+        self.dp_last = dict(cycles=int(s.tot_cycle), kernels=len(ks), collectives=len(s.collectives),
+                            comm_cycles=int(sum(c["cycles"] for c in s.collectives)), kernel_cycles=int(comp),
+                            modes=sorted({e.get("mode", "") for e in ev}))
+        return "dp-step", s.tot_insn, s.tot_cycle
+
     def step(self) -> Dict:
         insn = cycles = 0
         per_app = {}
@@ -266,7 +312,7 @@ class DistributedSuite:
         # it into the suite's thread pool, or running it beside the pool,
         # measured 3-15 % slower per step on one MI355X: its two kernels then
         # compete with the suite for the CU pool.)
-        if self.allreduce:
+        if self.allreduce and not self.dp_step:
             results.append(self._run_allreduce())
         for app, i, c in results:
             insn += i

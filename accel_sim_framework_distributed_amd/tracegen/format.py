@@ -44,7 +44,8 @@ SASS = {
     "DFMA": ("DP", "NONE", 0, 0), "DADD": ("DP", "NONE", 0, 0), "DMUL": ("DP", "NONE", 0, 0),
     "MUFU.RCP": ("SFU", "NONE", 0, 0), "MUFU.SQRT": ("SFU", "NONE", 0, 0), "MUFU.EX2": ("SFU", "NONE", 0, 0),
     "MUFU.LG2": ("SFU", "NONE", 0, 0), "MUFU.RSQ": ("SFU", "NONE", 0, 0),
-    "HMMA.1688.F32": ("SPEC3", "NONE", 0, 0),
+    "HMMA.1688.F32": ("SPEC3", "NONE", 0, 0), "HMMA.884.F32.F32.STEP0": ("SPEC3", "NONE", 0, 0),
+    "HMMA.884.F32.F32.STEP1": ("SPEC3", "NONE", 0, 0),
     "BRA": ("SPEC1", "NONE", 0, 0), "BSSY": ("SPEC1", "NONE", 0, 0), "BSYNC": ("SPEC1", "NONE", 0, 0),
     "BAR.SYNC": ("BARRIER", "NONE", 0, 0), "MEMBAR.GL": ("MEMBAR", "NONE", 0, 0),
     "EXIT": ("EXIT", "NONE", 0, 0), "NOP": ("NOP", "NONE", 0, 0),
@@ -56,6 +57,7 @@ SASS = {
     "LDL": ("LOAD", "LOCAL", FLAG["MEM"], 4), "STL": ("STORE", "LOCAL", FLAG["MEM"], 4),
     "LDS": ("LOAD", "SHARED", FLAG["MEM"], 4), "LDS.64": ("LOAD", "SHARED", FLAG["MEM"], 8),
     "STS": ("STORE", "SHARED", FLAG["MEM"], 4), "STS.64": ("STORE", "SHARED", FLAG["MEM"], 8),
+    "LDS.128": ("LOAD", "SHARED", FLAG["MEM"], 16), "STS.128": ("STORE", "SHARED", FLAG["MEM"], 16),
     "ATOMG.E.ADD.STRONG.GPU": ("LOAD", "GLOBAL", FLAG["MEM"] | FLAG["ATOMIC"] | FLAG["BYPASS_L1"], 4),
     "RED.E.ADD.STRONG.GPU": ("LOAD", "GLOBAL", FLAG["MEM"] | FLAG["ATOMIC"] | FLAG["BYPASS_L1"], 4),
     "ATOMS.ADD": ("LOAD", "SHARED", FLAG["MEM"], 4),

@@ -132,6 +132,11 @@ def main() -> int:
     # wrong size (which the simulator would then emulate locally)
     ar_dir = os.path.join(tdir, f"all-reduce-{max(1, world)}")
     ar_marker = os.path.join(ar_dir, ".complete")
+    # the step's data-parallel training trace, one per rank (unequal shards:
+    # rank r computes 1 + 0.25 r/(N-1) of the base batch, so the per-layer
+    # gradient all-reduces couple the ranks' simulated clocks)
+    dp_dir = os.path.join(tdir, f"dp-step-{max(1, world)}")
+    dp_marker = os.path.join(dp_dir, ".complete")
     if rank == 0:
         os.makedirs(tdir, exist_ok=True)
         if not os.path.exists(marker):
@@ -140,9 +145,13 @@ def main() -> int:
         if not os.path.exists(ar_marker):
             rodinia.write_allreduce_example(ar_dir, nranks=max(1, world))
             open(ar_marker, "w").write("ok")
+        if not os.path.exists(dp_marker):
+            from accel_sim_framework_distributed_amd.tracegen import training
+            training.write_dp_ranks(dp_dir, max(1, world), straggle=0.25)
+            open(dp_marker, "w").write("ok")
     if world > 1:
         dist.barrier()
-    while not (os.path.exists(marker) and os.path.exists(ar_marker)):
+    while not (os.path.exists(marker) and os.path.exists(ar_marker) and os.path.exists(dp_marker)):
         time.sleep(0.1)
 
     suite = DistributedSuite(tdir, config=a.config, engine=engine, rank=rank, world=world, apps=apps,
@@ -170,16 +179,18 @@ def main() -> int:
         cycles += r["cycles"]
     sync()
     dt = time.perf_counter() - t0
-    # max wall time over ranks, total instructions over ranks
-    t = torch.tensor([dt, float(insn), float(cycles)], dtype=torch.float64, device=dev)
+    # max wall time over ranks, total instructions over ranks; the DDP step's
+    # simulated cycles: max over ranks (the step ends with the slowest rank)
+    dpl = suite.dp_last or {}
+    t = torch.tensor([dt, float(insn), float(cycles), float(dpl.get("cycles", 0))], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        dt, insn_all, cyc_all = float(tmax[0]), float(tsum[1]), float(tsum[2])
+        dt, insn_all, cyc_all, dp_max = float(tmax[0]), float(tsum[1]), float(tsum[2]), float(tmax[3])
     else:
-        insn_all, cyc_all = float(insn), float(cycles)
+        insn_all, cyc_all, dp_max = float(insn), float(cycles), float(dpl.get("cycles", 0))
     kips = insn_all / dt / 1e3
     if rank == 0:
         out = {
@@ -207,6 +218,12 @@ def main() -> int:
                 "sim_cycles_per_step_per_rank": int(cycles / max(1, a.steps)),
             },
             "cycle_mae_vs_hw": _cycle_mae(),
+            "dp_step": ({"ranks": world, "simulated_cycles_max_rank": int(dp_max),
+                         "rank0_kernels": dpl.get("kernels"), "rank0_collectives": dpl.get("collectives"),
+                         "rank0_comm_cycles": dpl.get("comm_cycles"),
+                         "collective_coupling": dpl.get("modes"),
+                         "streams": "per-layer gradient all-reduce on stream 2 overlapping backward on stream 1"}
+                        if dpl else None),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -129,17 +129,42 @@ size_t Simulator::window_size() const {
   return dopt_.concurrent_kernel_sm ? std::max<uint32_t>(1, cfg_.max_concurrent_kernel) : 1;
 }
 
+size_t Simulator::kernels_in_window() const {
+  size_t n = 0;
+  for (auto& op : win_) n += op->kind == OP_KERNEL ? 1 : 0;
+  return n;
+}
+
+// Serially (no -gpgpu_concurrent_kernel_sm) the window holds one operation of
+// any kind; with concurrent kernels it bounds the kernels, and collectives /
+// events ride along in trace order.
 void Simulator::admit(size_t end) {
-  while (next_cmd_ < end && win_.size() < window_size()) {
+  while (next_cmd_ < end) {
+    const Command& c = cmds_[next_cmd_];
+    const bool windowed = c.type == CMD_KERNEL || c.type == CMD_COLLECTIVE || c.type == CMD_EVENT_RECORD ||
+                          c.type == CMD_EVENT_WAIT;
+    if (windowed) {
+      const bool full = dopt_.concurrent_kernel_sm ? (c.type == CMD_KERNEL && kernels_in_window() >= window_size())
+                                                   : win_.size() >= window_size();
+      if (full) break;
+    }
     const size_t i = next_cmd_++;
-    const Command& c = cmds_[i];
     if (c.type == CMD_KERNEL) {
       admit_kernel(i);
-    } else if (c.type == CMD_COLLECTIVE) {
+    } else if (windowed) {
       std::unique_ptr<StreamOp> op(new StreamOp());
       op->cmd = i;
-      op->coll = true;
       op->stream = c.stream;
+      op->event = c.event;
+      if (c.type == CMD_COLLECTIVE) {
+        op->kind = OP_COLL;
+      } else if (c.type == CMD_EVENT_RECORD) {
+        op->kind = OP_RECORD;
+        ev_admitted_[c.event]++;
+      } else {
+        op->kind = OP_WAIT;
+        op->wait_for = ev_admitted_[c.event];  // the latest record issued before the wait
+      }
       win_.push_back(std::move(op));
     } else {
       run_now(c);
@@ -369,35 +394,62 @@ void Simulator::admit_kernel(size_t idx) {
 }
 
 // start every windowed operation whose stream has no earlier unfinished
-// operation (reference main.cc:102-115: busy_streams), kernels in a free slot
+// operation (reference main.cc:102-115: busy_streams), kernels in a free
+// slot; event records fire at once, event waits end when their record fired
+// (repeated until nothing changes: a fired record may release a wait, which
+// frees its stream)
 void Simulator::launch_ready() {
-  std::vector<uint64_t> busy;
-  for (auto& up : win_) {
-    StreamOp& op = *up;
-    const bool stream_busy = std::find(busy.begin(), busy.end(), op.stream) != busy.end();
-    busy.push_back(op.stream);
-    if (op.launched || stream_busy) continue;
-    if (op.coll) {
-      launch_collective(op);
-      continue;
-    }
-    int slot = -1;
-    for (uint32_t k = 0; k < (uint32_t)std::min<uint32_t>(kMaxConc, (uint32_t)window_size()); ++k)
-      if (!slot_op_[k]) {
-        slot = (int)k;
-        break;
+  for (bool changed = true; changed;) {
+    changed = false;
+    std::vector<uint64_t> busy;
+    for (auto it = win_.begin(); it != win_.end();) {
+      StreamOp& op = **it;
+      const bool stream_busy = std::find(busy.begin(), busy.end(), op.stream) != busy.end();
+      if (op.launched || stream_busy) {
+        busy.push_back(op.stream);
+        ++it;
+        continue;
       }
-    if (slot < 0) continue;
-    if (!eng_->running()) ptrack_.begin_kernel();  // power samples of a busy period
-    const uint64_t now = eng_->now();
-    op.kd.ready_cycle = now + cfg_.kernel_launch_latency + (uint64_t)cfg_.tb_launch_latency * op.kd.n_cta;
-    op.start = now;
-    op.slot = slot;
-    op.launched = true;
-    slot_op_[slot] = &op;
-    print("launching kernel name: %s uid: %u\n", op.rk->h.name.c_str(), op.kd.uid);
-    print("GPGPU-Sim uArch: CTA/core = %u, limited by: %s\n", op.kd.cta_per_sm, op.occ_limiter);
-    eng_->launch((uint32_t)slot, *op.rk, op.kd);
+      if (op.kind == OP_RECORD || (op.kind == OP_WAIT && ev_fired_[op.event] >= op.wait_for)) {
+        if (op.kind == OP_RECORD) ev_fired_[op.event]++;
+        it = win_.erase(it);
+        changed = true;
+        continue;
+      }
+      busy.push_back(op.stream);
+      if (op.kind == OP_WAIT) {
+        ++it;
+        continue;
+      }
+      if (op.kind == OP_COLL) {
+        launch_collective(op);
+        changed = true;
+        ++it;
+        continue;
+      }
+      int slot = -1;
+      for (uint32_t k = 0; k < (uint32_t)std::min<uint32_t>(kMaxConc, (uint32_t)window_size()); ++k)
+        if (!slot_op_[k]) {
+          slot = (int)k;
+          break;
+        }
+      if (slot < 0) {
+        ++it;
+        continue;
+      }
+      if (!eng_->running()) ptrack_.begin_kernel();  // power samples of a busy period
+      const uint64_t now = eng_->now();
+      op.kd.ready_cycle = now + cfg_.kernel_launch_latency + (uint64_t)cfg_.tb_launch_latency * op.kd.n_cta;
+      op.start = now;
+      op.slot = slot;
+      op.launched = true;
+      slot_op_[slot] = &op;
+      print("launching kernel name: %s uid: %u\n", op.rk->h.name.c_str(), op.kd.uid);
+      print("GPGPU-Sim uArch: CTA/core = %u, limited by: %s\n", op.kd.cta_per_sm, op.occ_limiter);
+      eng_->launch((uint32_t)slot, *op.rk, op.kd);
+      changed = true;
+      ++it;
+    }
   }
 }
 
@@ -420,7 +472,7 @@ void Simulator::step() {
   launch_ready();
   uint64_t coll_end = ~0ull;
   for (auto& up : win_)
-    if (up->coll && up->launched) coll_end = std::min(coll_end, up->end);
+    if (up->kind == OP_COLL && up->launched) coll_end = std::min(coll_end, up->end);
   if (!eng_->running()) {
     if (coll_end == ~0ull) {
       if (!win_.empty()) throw std::runtime_error("command window stalled: nothing can start");
@@ -459,7 +511,7 @@ void Simulator::retire_collectives() {
   const uint64_t now = eng_->now();
   for (auto it = win_.begin(); it != win_.end();) {
     StreamOp& op = **it;
-    if (op.coll && op.launched && op.end <= now) {
+    if (op.kind == OP_COLL && op.launched && op.end <= now) {
       const Command& c = cmds_[op.cmd];
       CollectiveResult r;
       r.op = c.coll;

@@ -48,10 +48,12 @@ using CollectiveHook = std::function<uint64_t(const Command&, uint64_t now_cycle
 
 // one kernel or collective in the command window (reference main.cc
 // kernels_info + the busy_streams bookkeeping)
+enum OpKind : uint8_t { OP_KERNEL = 0, OP_COLL, OP_RECORD, OP_WAIT };
 struct StreamOp {
   size_t cmd = 0;             // command index
-  bool coll = false;          // collective (else kernel)
+  OpKind kind = OP_KERNEL;
   uint64_t stream = 0;
+  uint64_t event = 0, wait_for = 0;  // event ops: id; wait: records of it that must have fired
   bool launched = false;
   int slot = -1;              // kernel: engine slot while running
   uint64_t start = 0, end = 0;  // launch cycle; collective: completion cycle
@@ -151,6 +153,8 @@ class Simulator {
   uint32_t next_uid_ = 1;
   // command window: kernels / collectives admitted and not yet completed
   std::deque<std::unique_ptr<StreamOp>> win_;
+  size_t kernels_in_window() const;
+  std::map<uint64_t, uint64_t> ev_admitted_, ev_fired_;  // per event: records admitted / fired
   StreamOp* slot_op_[kMaxConc] = {};  // running kernel per engine slot
   size_t next_cmd_ = 0;
   bool stop_ = false;

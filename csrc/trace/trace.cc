@@ -454,6 +454,19 @@ std::vector<Command> parse_commandlist(const std::string& path) {
       c.text = line[0] == '/' ? line : dir + "/" + line;
     } else if (line.rfind("nccl", 0) == 0 || line.rfind("rccl", 0) == 0) {
       c = parse_collective_line(line);
+    } else if (line.rfind("hipEventRecord", 0) == 0 || line.rfind("cudaEventRecord", 0) == 0 ||
+               line.rfind("hipStreamWaitEvent", 0) == 0 || line.rfind("cudaStreamWaitEvent", 0) == 0) {
+      // cross-stream dependencies (a DDP gradient all-reduce waits for its
+      // layer's backward kernel; the optimizer waits for the all-reduces)
+      c.type = line.find("WaitEvent") != std::string::npos ? CMD_EVENT_WAIT : CMD_EVENT_RECORD;
+      c.text = line;
+      for (const std::string& part : split_commas(line)) {
+        const auto eq = part.find('=');
+        if (eq == std::string::npos) continue;
+        const std::string k = trim_copy(part.substr(0, eq)), v = trim_copy(part.substr(eq + 1));
+        if (k == "event") c.event = strtoull(v.c_str(), nullptr, 0);
+        else if (k == "stream") c.stream = strtoull(v.c_str(), nullptr, 0);
+      }
     } else {
       continue;  // unknown commands are skipped
     }

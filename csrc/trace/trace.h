@@ -23,6 +23,8 @@ enum CmdType : uint8_t {
   CMD_GROUP_START,    // ncclGroupStart
   CMD_GROUP_END,      // ncclGroupEnd
   CMD_COLLECTIVE,     // ncclAllReduce / AllGather / ReduceScatter / Broadcast / AllToAll ...
+  CMD_EVENT_RECORD,   // hipEventRecord,event=E,stream=S: fires when S's earlier work is done
+  CMD_EVENT_WAIT,     // hipStreamWaitEvent,stream=S,event=E: S waits for the latest earlier record of E
 };
 
 struct Command {
@@ -38,6 +40,7 @@ struct Command {
   int32_t root = -1;
   int32_t nranks = 1;
   uint64_t stream = 0;
+  uint64_t event = 0;  // event record / wait
 };
 
 // Parse a kernelslist(.g) file.  Kernel paths are resolved relative to it.

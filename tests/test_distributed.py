@@ -161,3 +161,69 @@ def test_node_plan_places_apps_by_makespan(native, tmp_path, monkeypatch):
     plan = s.plan()
     assert plan == {"nn-rodinia-2.0-ft": "gpu", "backprop-rodinia-2.0-ft": "gpu", "pathfinder-rodinia-2.0-ft": "cpu"}
     assert abs(s.predicted_span - 0.5) < 1e-9
+
+
+# ---- data-parallel training step: collectives overlapping compute ----------
+DP_KW = dict(layers=2, ctas=8, k_tiles=1, grad_mb=0.0625, straggle=0.6)
+DP_EXTRA = {"-gpgpu_concurrent_kernel_sm": "1", "-collective_model": "packet", "-gpgpu_n_clusters": "16"}
+
+
+def _dp_result(s):
+    return (int(s.tot_cycle), [(k["uid"], k["start_cycle"], k["cycles"]) for k in s.kernels],
+            [c["cycles"] for c in s.collectives])
+
+
+def _dp_worker(rank, world, port, root, q):
+    import torch.distributed as dist
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        from accel_sim_framework_distributed_amd import _native
+        from accel_sim_framework_distributed_amd.sim import build_args
+        kl = os.path.join(root, f"rank{rank}", "kernelslist.g")
+        s = _native.load().Simulator(build_args("QV100", kl, "cpu", DP_EXTRA), False)
+        hook = collectives.PacketCollective()
+        s.set_collective_hook(lambda d, now: hook(s, d, now))
+        assert s.run() == 0
+        q.put((rank, _dp_result(s), [e["mode"] for e in hook.events]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_step_eight_ranks_match_in_process_emulation(native, tmp_path):
+    """Eight gloo processes, one simulated GPU each, run unequal shards of a
+    DDP step whose per-layer all-reduces (stream 2) overlap the backward pass
+    (stream 1): every rank's kernel and collective timing equals the
+    in-process emulation of all eight ranks (threads + linksim_run_local)
+    exactly, and the collectives couple the ranks' clocks."""
+    import threading
+    from accel_sim_framework_distributed_amd.sim import build_args
+    from accel_sim_framework_distributed_amd.tracegen import training
+    W = 8
+    root = str(tmp_path / "dp")
+    kls = training.write_dp_ranks(root, W, **DP_KW)
+    res = _spawn(_dp_worker, W, root)
+    assert all(m == ["rccl"] * DP_KW["layers"] for _, _, m in res)
+    # oracle: all ranks in this process
+    loc = collectives.LocalRanks(W)
+    out = [None] * W
+
+    def run(r):
+        s = native.Simulator(build_args("QV100", kls[r], "cpu", DP_EXTRA), False)
+        s.set_collective_hook(loc.hook(r, s))
+        assert s.run() == 0
+        out[r] = _dp_result(s)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert [r[1] for r in res] == out
+    # coupling: the fastest rank's first all-reduce waits for the slowest rank
+    # (its collective lasts longer than the slowest rank's own)
+    first = [r[1][2][0] for r in res]
+    assert first[0] > first[-1]
+    # overlap: backward kernels run back to back while the all-reduces proceed
+    bwd = [k for k in res[0][1][1] if k[0] in (3, 4)]
+    assert bwd[1][1] == bwd[0][1] + bwd[0][2]
