@@ -81,7 +81,7 @@ def optimizer_kernel(kid: int, params: int) -> KernelArrays:
 
 
 def write_dp_step(out_dir: str, rank: int = 0, nranks: int = 1, layers: int = 4, ctas: int = 80,
-                  k_tiles: int = 4, grad_mb: float = 0.25, straggle: float = 0.0) -> str:
+                  k_tiles: int = 2, grad_mb: float = 0.25, straggle: float = 0.0) -> str:
     """Write rank `rank`'s trace of one DDP step; returns its kernelslist.g.
 
     ``grad_mb``: gradient bucket per layer (MB, fp32) all-reduced over

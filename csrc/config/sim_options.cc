@@ -710,6 +710,14 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   if (c.icnt_latency < 1 || c.icnt_latency > (uint32_t)kMaxEpoch)
     throw OptionError("-icnt_latency must be in 1.." + std::to_string(kMaxEpoch) + " (epoch length)");
   c.flit_size = std::max<uint32_t>(8, (uint32_t)r.getu("-icnt_flit_size"));
+  c.icnt_arbiter = r.getu("-icnt_arbiter_algo") ? 1u : 0u;
+  c.icnt_grant_cycles = std::max<uint32_t>(1, (uint32_t)r.getu("-icnt_grant_cycles"));
+  {
+    // the injection buffer holds -icnt_in_buffer_limit flits; a packet is at
+    // most a 128-byte line plus its header (reference mem_fetch sizes)
+    const uint32_t max_flits = (136 + c.flit_size - 1) / c.flit_size;
+    c.icnt_in_pkts = std::max<uint32_t>(1, std::min<uint32_t>(kOutQ, (uint32_t)r.getu("-icnt_in_buffer_limit") / max_flits));
+  }
   c.icnt_out_limit = std::min<uint32_t>((uint32_t)r.getu("-sim_max_outstanding_pkts"), kInQ);
   if (c.icnt_out_limit == 0) c.icnt_out_limit = 1;
   // memory partition

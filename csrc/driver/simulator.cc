@@ -900,6 +900,32 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   print("dram_bw_util = %.4f\n", dram_cyc ? (double)dram_busy / dram_cyc : 0.0);
   print("gpgpu_n_tot_w_icount = %llu\n", (unsigned long long)tot_warp_insn_);
   {
+    // crossbar subnets (reference LocalInterconnect::DisplayStats,
+    // local_interconnect.cc:360-420): request net = SM -> L2 ports, reply
+    // net = L2 -> SM ports; conflicts = ready inputs a port did not grant
+    uint64_t rq_pk = 0, rq_cf = 0, rq_ac = 0, rq_q = 0, rp_pk = 0, rp_cf = 0, rp_q = 0;
+    for (auto& m : cmem) {
+      rq_pk += m.pkts_in;
+      rq_cf += m.icnt_conflicts;
+      rq_ac += m.icnt_arb_cycles;
+      rq_q += m.icnt_queue_cycles;
+    }
+    for (auto& st : csm) {
+      rp_pk += st.pkts_in;
+      rp_cf += st.icnt_reply_conflicts;
+      rp_q += st.icnt_reply_queue_cycles;
+    }
+    print("Req_Network_injected_packets_num = %llu\n", (unsigned long long)rq_pk);
+    print("Req_Network_conflicts = %llu\n", (unsigned long long)rq_cf);
+    print("Req_Network_conflicts_per_cycle_util = %.4f\n", rq_ac ? (double)rq_cf / (double)rq_ac : 0.0);
+    print("Req_Network_queueing_cycles = %llu\n", (unsigned long long)rq_q);
+    print("Req_Network_avg_queueing_cycles = %.4f\n", rq_pk ? (double)rq_q / (double)rq_pk : 0.0);
+    print("Reply_Network_injected_packets_num = %llu\n", (unsigned long long)rp_pk);
+    print("Reply_Network_conflicts = %llu\n", (unsigned long long)rp_cf);
+    print("Reply_Network_queueing_cycles = %llu\n", (unsigned long long)rp_q);
+    print("Reply_Network_avg_queueing_cycles = %.4f\n", rp_pk ? (double)rp_q / (double)rp_pk : 0.0);
+  }
+  {
     // further gpu_print_stat / shader_core_stats lines (reference
     // gpu-sim.cc:1355-1541, shader.cc:3012-3170): instruction mix, issue
     // stalls, register-bank conflicts, dual issue, L1 write-backs; memory

@@ -175,6 +175,8 @@ struct SmView {
   SV_VAL(epoch_end);
   SV_VAL(out_port_free);
   SV_VAL(age_ctr);
+  SV_REF(arb_next);
+  SV_REF(arb_cnt);
   SV_WARP(w_next);
   SV_WARP(w_end);
   SV_WARP(w_head);
@@ -281,7 +283,8 @@ struct SmView {
   X(cta_nexit) X(sched_last) X(w_iline)
 
   __device__ __forceinline__ explicit SmView(B& b)
-      : base(b), l1_sets(b.l1_sets), l1_assoc(b.l1_assoc), cycle(b.cycle), w_wait(b.w_wait), w_slot_lds(b.w_slot_lds), w_lds_st(b.w_lds_st),
+      : base(b), l1_sets(b.l1_sets), l1_assoc(b.l1_assoc), cycle(b.cycle), arb_next(b.arb_next),
+        arb_cnt(b.arb_cnt), w_wait(b.w_wait), w_slot_lds(b.w_slot_lds), w_lds_st(b.w_lds_st),
         w_slot_pend(b.w_slot_pend),
         w_slot_dst(b.w_slot_dst), cta_id(b.cta_id), cta_ks(b.cta_ks), cta_wbase(b.cta_wbase), cta_nw(b.cta_nw),
         n_cta_k(b.n_cta_k), cta_wmask(b.cta_wmask), used_thr(b.used_thr), used_regs(b.used_regs),

@@ -167,6 +167,11 @@ struct SimCfg {
   // ---- interconnect ----
   uint32_t icnt_latency;   // core cycles (== epoch length, the PDES lookahead)
   uint32_t flit_size;
+  // crossbar output-port arbitration (local_interconnect.cc:123-270):
+  // 0 = round robin with a rotating global pointer, 1 = iSLIP (per-output
+  // pointer advanced past the granted input every icnt_grant_cycles grants)
+  uint32_t icnt_arbiter, icnt_grant_cycles;
+  uint32_t icnt_in_pkts;  // SM injection buffer (-icnt_in_buffer_limit flits) in max-size packets
   uint32_t icnt_out_limit; // per-SM outstanding packets before injection stalls
   // -network_mode 1 (intersim2 / Booksim topologies, reference
   // icnt_wrapper.cc:35-45 + intersim2/networks/*): per-pair latency from the

@@ -89,6 +89,9 @@ struct MemStats {
   uint64_t icnt_stall;
   uint64_t icnt_backlog;       // arrivals that waited in the input backlog (sum over epochs of its length)
   uint64_t icnt_ovf_drop;      // arrivals lost to a full backlog ring (must stay 0)
+  uint64_t icnt_conflicts;     // request net: ready inputs not granted by this output port (per cycle)
+  uint64_t icnt_queue_cycles;  // request net: icnt cycles granted packets waited at this output port
+  uint64_t icnt_arb_cycles;    // request net: icnt cycles with at least one input ready
 };
 
 struct SubPart {
@@ -105,7 +108,7 @@ struct SubPart {
   uint32_t n_wait;
   uint32_t n_l2dram;   // requests of this sub in the L2->DRAM path
   uint32_t ovf_head, ovf_n;  // arrival backlog ring (MemCtx::ovf) for arrivals that did not fit in inq
-  uint32_t pad;
+  uint16_t arb_next, arb_cnt;  // crossbar output-port arbiter: next input, grants left at the pointer
   L2Line l2[kMaxL2Lines];
   L2Mshr mshr[kMaxL2Mshr];
   L2Wait wait[kMaxL2Wait];
@@ -497,15 +500,19 @@ SIM_HDI void l2_cycle(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub,
 template <class P>
 SIM_HDI void mem_icnt_cycle(ChanState& ch, SubPart& sp, const SimCfg& c, const MemCtx& x,
                             uint32_t sub, uint64_t now_fs) {
-  if (sp.inq_n && sp.rop_n < (uint32_t)kRopQ && sp.rop_n < c.q_icnt_l2 + c.rop_latency) {
-    const Pkt& a = sp.inq[sp.inq_head];
-    if (a.t <= now_fs) {
-      Pkt p = a;
+  if (sp.inq_n && sp.rop_n < (uint32_t)kRopQ && sp.rop_n < c.q_icnt_l2 + c.rop_latency &&
+      sp.inq[sp.inq_head].t <= now_fs) {
+    // the output port grants one ready input per cycle
+    XbarGrant g = xbar_pick<P>(sp.inq, sp.inq_head, sp.inq_n, kMemInQ, now_fs, c, now_fs / c.per_icnt,
+                               sp.arb_next, sp.arb_cnt, c.n_sm);
+    sp.st.icnt_arb_cycles++;
+    sp.st.icnt_conflicts += g.ready - 1;
+    {
+      Pkt p = xbar_take(sp.inq, sp.inq_head, sp.inq_n, kMemInQ, g.off);
+      sp.st.icnt_queue_cycles += (now_fs - p.t) / c.per_icnt;
       p.t = now_fs + (uint64_t)c.rop_latency * c.per_l2;
       sp.rop[(sp.rop_head + sp.rop_n) % kRopQ] = p;
       sp.rop_n++;
-      sp.inq_head = (sp.inq_head + 1) % kMemInQ;
-      sp.inq_n--;
       sp.st.pkts_in++;
       sp.st.bytes_in += p.size;
     }

@@ -131,6 +131,8 @@ struct SMStats {
   uint64_t dual_issued;        // second instructions issued in the same cycle by one warp
   uint64_t l1_wb;              // dirty L1 lines written back on eviction
   uint64_t l1_wb_lost;         // write-backs dropped with the injection queue full (must stay 0)
+  uint64_t icnt_reply_conflicts;     // reply net: ready inputs not granted by this SM's ejection port
+  uint64_t icnt_reply_queue_cycles;  // reply net: icnt cycles granted replies waited at the port
 };
 enum IL1Out : uint8_t { IL1_HIT = 0, IL1_MISS, IL1_MSHR_HIT, IL1_RES_FAIL };
 // SMStats::power_acc slots
@@ -147,7 +149,7 @@ struct alignas(16) SMState {
   uint64_t epoch_end;         // current epoch end cycle (exclusive)
   uint64_t out_port_free;     // cycle the injection port frees
   uint32_t age_ctr;
-  uint32_t pad_a;
+  uint16_t arb_next, arb_cnt;  // reply-network output-port arbiter (xbar_pick)
   // ---- warps (SoA) ----
   uint32_t w_next[kMaxWarps];   // next trace index to fetch into ibuf
   uint32_t w_end[kMaxWarps];    // end of stream
@@ -303,11 +305,11 @@ SIM_HDI CacheGeom l1_geom(const SimCfg& c, const S& s) {
 // injection: enqueue a packet towards the interconnect
 template <class S>
 SIM_HDI bool sm_can_send(const S& s, const SimCfg& c) {
-  return s.outq_n < (uint32_t)kOutQ && s.outstanding + s.outq_n < c.icnt_out_limit;
+  return s.outq_n < c.icnt_in_pkts && s.outstanding + s.outq_n < c.icnt_out_limit;
 }
 template <class S>
 SIM_HDI bool sm_can_send_n(const S& s, const SimCfg& c, uint32_t n) {
-  return s.outq_n + n <= (uint32_t)kOutQ && s.outstanding + s.outq_n + n <= c.icnt_out_limit;
+  return s.outq_n + n <= c.icnt_in_pkts && s.outstanding + s.outq_n + n <= c.icnt_out_limit;
 }
 // write-back packets of evicted dirty L1 sectors carry this tag: their
 // acknowledgement retires no warp store
@@ -639,16 +641,78 @@ SIM_HDI bool il1_fetch(S& s, const SimCfg& c, const KernelTab& kt, uint32_t w) {
   return false;
 }
 
-// consume at most one arrived packet per cycle (response FIFO)
+// ---------------------------------------------------------------------------
+// Crossbar output port (reference xbar_router::RR_Advance / iSLIP_Advance,
+// local_interconnect.cc:123-270).  Arrivals reach a destination's port in
+// time order (the sorted input queue); each cycle the port grants ONE of the
+// inputs whose packet has arrived, in round-robin order from the arbiter's
+// pointer -- the rotating global pointer (RR) or the per-output pointer moved
+// past the granted input (iSLIP).  Input-side virtual output queues: a packet
+// waiting for one busy output never blocks its input's packets to others
+// (the sender's injection port already serialises one flit per cycle).
+// Arbitration looks at the 64 oldest arrivals.
+struct XbarGrant {
+  uint32_t off;    // offset of the granted packet from the queue head
+  uint32_t ready;  // inputs' packets ready at the port this cycle (>= 1)
+};
+template <class P>
+SIM_HDI XbarGrant xbar_pick(const Pkt* q, uint32_t head, uint32_t n, uint32_t cap, uint64_t now_fs,
+                            const SimCfg& c, uint64_t icnt_cycle, uint16_t& arb_next, uint16_t& arb_cnt,
+                            uint32_t nsrc) {
+  const uint32_t m = n < 64u ? n : 64u;
+  const uint32_t ptr = c.icnt_arbiter ? (uint32_t)arb_next % nsrc : (uint32_t)(icnt_cycle % nsrc);
+  uint32_t ready = 0;
+  const int o = P::argmin((int)m, [&](int i) -> uint64_t {
+    const Pkt& p = q[(head + (uint32_t)i) % cap];
+    if (p.t > now_fs) return ~0ull;
+    const uint32_t d = ((uint32_t)p.src + nsrc - ptr) % nsrc;
+    return (uint64_t)d << 8 | (uint64_t)i;
+  });
+  ready = (uint32_t)popc64(P::ballot((int)m, [&](int i) { return q[(head + (uint32_t)i) % cap].t <= now_fs; }));
+  const uint32_t off = o < 0 ? 0u : (uint32_t)o;
+  if (c.icnt_arbiter) {
+    if (arb_cnt <= 1) {
+      arb_next = (uint16_t)(((uint32_t)P::uni(q[(head + off) % cap].src) + 1) % nsrc);
+      arb_cnt = (uint16_t)c.icnt_grant_cycles;
+    } else {
+      arb_cnt = (uint16_t)(arb_cnt - 1);
+    }
+  }
+  return XbarGrant{off, ready ? ready : 1u};
+}
+// remove the packet at `off` from the head of a time-ordered ring (the
+// packets before it move up one slot, keeping their order)
+template <class Q>
+SIM_HDI Pkt xbar_take(Q& q, uint32_t& head, uint32_t& n, uint32_t cap, uint32_t off) {
+  const Pkt p = q[(head + off) % cap];
+  for (uint32_t j = off; j > 0; --j) q[(head + j) % cap] = q[(head + j - 1) % cap];
+  head = (head + 1) % cap;
+  n--;
+  return p;
+}
+
+// consume at most one arrived packet per cycle (response FIFO; the SM is the
+// reply network's output port)
 template <class P, class S>
 SIM_HDI void sm_receive(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
   if (P::uni(s.inq_n) == 0) return;
-  const Pkt q = P::uni(s.inq[P::uni(s.inq_head)]);
-  if (q.t > now * c.per_core) return;
+  if (P::uni(s.inq[P::uni(s.inq_head)].t) > now * c.per_core) return;
+  Pkt q;
+  {
+    uint32_t head = P::uni(s.inq_head), n = P::uni(s.inq_n);
+    uint16_t an = s.arb_next, ac = s.arb_cnt;
+    const XbarGrant g = xbar_pick<P>(s.inq, head, n, kInQ, now * c.per_core, c, now * c.per_core / c.per_icnt,
+                                     an, ac, c.n_subpart);
+    s.arb_next = an;
+    s.arb_cnt = ac;
+    s.sadd(SK(icnt_reply_conflicts), g.ready - 1);
+    q = P::uni(xbar_take(s.inq, head, n, kInQ, g.off));
+    s.sadd(SK(icnt_reply_queue_cycles), (now * c.per_core - q.t) / c.per_icnt);
+    s.inq_head = head;
+    s.inq_n = n;
+  }
   if (trace_sm_on(c, TS_INTERCONNECT, s.id)) P::one([&] { trace_put(c, s.id, now, EV_PKT_RECV, q.type, q.addr); });
-  s.inq_head = (s.inq_head + 1) % kInQ;
-  s.inq_n--;
   s.outstanding--;
   s.sadd(SK(pkts_in), 1);
   s.sadd(SK(bytes_in), q.size);

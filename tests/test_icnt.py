@@ -110,3 +110,60 @@ def test_epoch_length_sensitivity_is_smooth(tmp_path):
             cyc.append(r.tot_cycle)
         assert cyc[0] <= cyc[1] * 1.01 and cyc[1] <= cyc[2] * 1.01, (app, cyc)
         assert cyc[2] <= cyc[0] * 1.10, (app, cyc)  # 7 extra cycles per hop cost < 10 %
+
+
+# ---- crossbar output-port arbitration (local_interconnect.cc:123-270) -------
+def _hotspot_app(tmp_path, name, same_line):
+    """80 single-warp CTAs; each warp issues 16 independent loads.  same_line:
+    every SM reads the same lines, whose requests all meet at ONE L2
+    sub-partition's port (a hotspot); else each SM reads its own lines,
+    spread over all sub-partitions."""
+    from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+    import numpy as np
+    k = KernelBuilder("_Z7hotspotPf", (80, 1, 1), (32, 1, 1), nregs=32)
+    g = k.g
+    for i in range(16):
+        if same_line:
+            base = np.full(g.nwarps, 0x7000_0000 + i * 0x40000, np.int64)
+            k.op("LDG.E", [8 + i], [2], base=base, stride=0)
+        else:
+            k.op("LDG.E", [8 + i], [2], base=0x7000_0000 + g.cta * 0x100000 + i * 128, stride=4)
+    for i in range(16):
+        k.op("FADD", [5], [8 + i, 5])
+    k.op("EXIT")
+    return rodinia.write_app(str(tmp_path / name), [k.build()], memcpy=False)
+
+
+def _stat(out, key):
+    import re
+    m = re.findall(rf"^{re.escape(key)} = ([0-9.]+)", out, re.M)
+    return float(m[-1])
+
+
+@pytest.mark.parametrize("algo", ["0", "1"])
+def test_crossbar_hotspot_queues_at_one_port(native, tmp_path, algo):
+    outs = {}
+    for hot in (True, False):
+        kl = _hotspot_app(tmp_path, f"h{int(hot)}_{algo}", hot)
+        s = native.Simulator(presets.args_for("QV100", {"-icnt_arbiter_algo": algo, "-gpgpu_perf_sim_memcpy": "0"})
+                             + ["-trace", kl], False)
+        assert s.run() == 0
+        outs[hot] = s.output
+    hot, spread = outs[True], outs[False]
+    # every SM's miss for the same line meets at one port: conflicts and queueing
+    assert _stat(hot, "Req_Network_conflicts") > 100
+    assert _stat(hot, "Req_Network_avg_queueing_cycles") > 5 * max(0.5, _stat(spread, "Req_Network_avg_queueing_cycles"))
+    assert _stat(hot, "Req_Network_injected_packets_num") == _stat(spread, "Req_Network_injected_packets_num") == 80 * 16
+
+
+@pytest.mark.gpu
+def test_crossbar_hotspot_gpu_matches_cpu(native, tmp_path):
+    kl = _hotspot_app(tmp_path, "hg", True)
+    res = []
+    for eng in ("cpu", "gpu"):
+        s = native.Simulator(presets.args_for("QV100", {"-gpgpu_perf_sim_memcpy": "0", "-sim_engine": eng})
+                             + ["-trace", kl], False)
+        assert s.run() == 0
+        res.append([_stat(s.output, k) for k in ("gpu_sim_cycle", "Req_Network_conflicts",
+                                                  "Req_Network_queueing_cycles", "Reply_Network_queueing_cycles")])
+    assert res[0] == res[1] and res[0][1] > 100
