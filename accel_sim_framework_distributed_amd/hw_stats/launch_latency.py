@@ -96,6 +96,20 @@ def main(argv=None) -> int:
     print(f"# rocprof_per_block_ns {b:.4f}")
     print(f"-gpgpu_kernel_launch_latency {int(round(a * mhz / 1000.0))}")
     print(f"-gpgpu_TB_launch_latency {int(round(b * mhz / 1000.0))}")
+    # back-to-back launches (no event / sync between): the queued cost
+    q = read_durations(run_dir, "ub_empty_queued")
+    if q:
+        for nb in sorted(q):
+            d = q[nb]
+            print(f"queued empty kernel {nb:6d} workgroups: median {np.median(d):8.0f} ns  min {min(d):8.0f} ns  (n={len(d)})")
+        qa, _ = fit(q)
+        # reported, not applied: under rocprofv3 a queued dispatch's duration
+        # also covers its wait behind the previous one (start stamps overlap
+        # the previous end), so it is no per-kernel launch cost; measured on
+        # MI355X: 4.7 us queued vs 3.7 us isolated vs ~2 us for a host-bound
+        # launch into an idle queue (pathfinder), see profiles/ubench_mi355x
+        print(f"# rocprof_queued_launch_ns {qa:.1f}")
+        print(f"# queued_launch_cycles {int(round(qa * mhz / 1000.0))}  (-gpgpu_kernel_launch_latency_queued)")
     return 0
 
 

@@ -167,7 +167,10 @@ const OptDef kOptions[] = {
     // ---- clocks / kernel ----
     {"-gpgpu_clock_domains", 's', "500.0:2000.0:2000.0:2000.0", "core:icnt:L2:DRAM MHz"},
     {"-gpgpu_max_concurrent_kernel", 'i', "32", ""},
+    {"-trace_prefetch", 'b', "1", "parse + coalesce the next kernel's trace on a host thread while the engine runs"},
     {"-gpgpu_kernel_launch_latency", 'i', "0", "kernel launch latency (cycles)"},
+    {"-gpgpu_kernel_launch_latency_queued", 'i', "-1",
+     "launch latency of a kernel queued right behind the previous one (no memcpy / sync between); -1 = as -gpgpu_kernel_launch_latency"},
     {"-gpgpu_TB_launch_latency", 'i', "0", "thread block launch latency"},
     {"-gpgpu_cdp_enabled", 'b', "0", ""},
     {"-gpgpu_max_cycle", 'I', "0", "stop after cycles"},
@@ -831,6 +834,10 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
     c.per_dram = (uint64_t)llround(1e9 / f[3]);
   }
   c.kernel_launch_latency = (uint32_t)std::max<long long>(0, r.geti("-gpgpu_kernel_launch_latency"));
+  {
+    const long long q = r.geti("-gpgpu_kernel_launch_latency_queued");
+    c.kernel_launch_latency_queued = q < 0 ? c.kernel_launch_latency : (uint32_t)q;
+  }
   c.tb_launch_latency = (uint32_t)std::max<long long>(0, r.geti("-gpgpu_TB_launch_latency"));
   c.deadlock_window = r.getb("-gpgpu_deadlock_detect") ? 50000 : 0;
   c.max_insn = (uint64_t)std::max<long long>(0, r.geti("-gpgpu_max_insn"));
@@ -913,6 +920,7 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.coll_reduce_gbps = r.getd("-collective_reduce_gbps");
   d.concurrent_kernel_sm = r.getb("-gpgpu_concurrent_kernel_sm") ? 1 : 0;
   d.max_concurrent_kernel = (int32_t)r.geti("-gpgpu_max_concurrent_kernel");
+  d.trace_prefetch = r.getb("-trace_prefetch");
   d.power_enabled = r.getb("-power_simulation_enabled");
   d.power_xml = r.gets("-accelwattch_xml_file");
   {

@@ -151,6 +151,8 @@ void Simulator::admit(size_t end) {
     const size_t i = next_cmd_++;
     if (c.type == CMD_KERNEL) {
       admit_kernel(i);
+      win_.back()->queued = last_cmd_kernel_;
+      last_cmd_kernel_ = true;
     } else if (windowed) {
       std::unique_ptr<StreamOp> op(new StreamOp());
       op->cmd = i;
@@ -167,6 +169,7 @@ void Simulator::admit(size_t end) {
       }
       win_.push_back(std::move(op));
     } else {
+      if (c.type == CMD_MEMCPY_HTOD || c.type == CMD_MEMCPY_DTOH) last_cmd_kernel_ = false;  // host sync
       run_now(c);
     }
   }
@@ -340,11 +343,10 @@ void Simulator::admit_kernel(size_t idx) {
   std::unique_ptr<StreamOp> op(new StreamOp());
   op->cmd = idx;
   op->t_admit = std::chrono::steady_clock::now();
-  HostKernel hk = load_kernel(c.text);
+  op->rk = take_kernel(idx);
   print("Processing kernel %s\n", c.text.c_str());
-  if (hk.h.warp_size != cfg_.warp_size)
+  if (op->rk->h.warp_size != cfg_.warp_size)
     throw std::runtime_error("trace warp size does not match -gpgpu_shader_core_pipeline");
-  op->rk.reset(new ReadyKernel(coalesce_kernel(hk, cfg_)));
   const ReadyKernel& rk = *op->rk;
   KernelShape ks{rk.h.block[0] * rk.h.block[1] * rk.h.block[2], rk.h.shmem, rk.h.nregs, rk.n_cta};
   Occupancy occ = compute_occupancy(cfg_, ks);
@@ -393,6 +395,29 @@ void Simulator::admit_kernel(size_t idx) {
   win_.push_back(std::move(op));
 }
 
+std::unique_ptr<ReadyKernel> Simulator::take_kernel(size_t idx) {
+  auto it = pf_.find(idx);
+  if (it != pf_.end()) {
+    std::unique_ptr<ReadyKernel> k = it->second.get();  // rethrows a loader error
+    pf_.erase(it);
+    return k;
+  }
+  return std::unique_ptr<ReadyKernel>(new ReadyKernel(coalesce_kernel(load_kernel(cmds_[idx].text), cfg_)));
+}
+
+void Simulator::prefetch_next() {
+  if (!dopt_.trace_prefetch || !pf_.empty()) return;
+  for (size_t i = next_cmd_; i < cmds_.size(); ++i) {
+    if (cmds_[i].type != CMD_KERNEL) continue;
+    const std::string path = cmds_[i].text;
+    const SimCfg cfg = cfg_;
+    pf_[i] = std::async(std::launch::async, [path, cfg]() {
+      return std::unique_ptr<ReadyKernel>(new ReadyKernel(coalesce_kernel(load_kernel(path), cfg)));
+    });
+    return;
+  }
+}
+
 // start every windowed operation whose stream has no earlier unfinished
 // operation (reference main.cc:102-115: busy_streams), kernels in a free
 // slot; event records fire at once, event waits end when their record fired
@@ -439,7 +464,8 @@ void Simulator::launch_ready() {
       }
       if (!eng_->running()) ptrack_.begin_kernel();  // power samples of a busy period
       const uint64_t now = eng_->now();
-      op.kd.ready_cycle = now + cfg_.kernel_launch_latency + (uint64_t)cfg_.tb_launch_latency * op.kd.n_cta;
+      const uint64_t lat = op.queued ? cfg_.kernel_launch_latency_queued : cfg_.kernel_launch_latency;
+      op.kd.ready_cycle = now + lat + (uint64_t)cfg_.tb_launch_latency * op.kd.n_cta;
       op.start = now;
       op.slot = slot;
       op.launched = true;
@@ -470,6 +496,7 @@ void Simulator::launch_collective(StreamOp& op) {
 // advance to the next completion in the window and retire what completed
 void Simulator::step() {
   launch_ready();
+  prefetch_next();
   uint64_t coll_end = ~0ull;
   for (auto& up : win_)
     if (up->kind == OP_COLL && up->launched) coll_end = std::min(coll_end, up->end);

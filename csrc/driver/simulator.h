@@ -5,6 +5,7 @@
 #include <deque>
 #include <fstream>
 #include <functional>
+#include <future>
 #include <map>
 #include <memory>
 #include <string>
@@ -54,6 +55,7 @@ struct StreamOp {
   OpKind kind = OP_KERNEL;
   uint64_t stream = 0;
   uint64_t event = 0, wait_for = 0;  // event ops: id; wait: records of it that must have fired
+  bool queued = false;        // kernel: right behind another kernel (no host sync between)
   bool launched = false;
   int slot = -1;              // kernel: engine slot while running
   uint64_t start = 0, end = 0;  // launch cycle; collective: completion cycle
@@ -117,6 +119,12 @@ class Simulator {
   void retire_collectives();
   void finish_kernel(uint32_t slot, const RunResult& rr);
   void check_limits();
+  // host trace prefetch (the reference's TODO, AS/main.cc:25-44): the next
+  // kernel's trace is parsed and coalesced on a worker thread while the
+  // engine simulates
+  void prefetch_next();
+  std::unique_ptr<ReadyKernel> take_kernel(size_t idx);
+  std::map<size_t, std::future<std::unique_ptr<ReadyKernel>>> pf_;
   void print_kernel_stats(const KernelResult& r, const std::vector<SMStats>& sm, const std::vector<MemStats>& mem);
   void print_sim_time();
   // timing-state checkpoint at a kernel boundary / resume from one (returns first command to run)
@@ -159,6 +167,7 @@ class Simulator {
   size_t next_cmd_ = 0;
   bool stop_ = false;
   bool ckpt_pending_ = false;
+  bool last_cmd_kernel_ = false;  // the previous admitted command was a kernel launch
   bool cap_hit_ = false;  // a run cap (-gpgpu_max_insn / _max_cta / _max_completed_cta) stopped a kernel
 };
 

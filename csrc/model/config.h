@@ -25,6 +25,7 @@ constexpr int kMaxL1Mshr = 256;
 constexpr int kMaxIL1Lines = 512;  // instruction cache: 64 KB of 128 B lines
 constexpr int kMaxIL1Mshr = 16;
 constexpr uint64_t kProgramMemStart = 0xF0000000ull;  // code address base (reference PROGRAM_MEM_START)
+constexpr uint64_t kScalarBase = 0x7FFE00000000ull;   // data addresses keyed to CDNA scalar loads (coalesce_kernel)
 constexpr int kMaxPend = 1024;      // outstanding (warp,load-slot,line) L1 waiters
 constexpr int kLoadSlots = 8;       // in-flight load instructions per warp
 constexpr int kHitRing = 256;       // L1 / shared-memory completion ring (latency < 222)
@@ -217,6 +218,7 @@ struct SimCfg {
   uint64_t per_core, per_icnt, per_l2, per_dram;
   // ---- kernel scheduling ----
   uint32_t kernel_launch_latency;
+  uint32_t kernel_launch_latency_queued;  // a kernel right behind the previous one (driver)
   uint32_t tb_launch_latency;
   // ---- misc ----
   uint32_t deadlock_window;

@@ -761,7 +761,8 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
   const bool is_store = in.cls == OC_STORE;
   const bool atomic = (in.flags & F_ATOMIC) != 0;
   const CacheGeom g = l1_geom(c, s);
-  const bool bypass = atomic || (in.flags & F_BYPASS_L1) || c.gmem_skip_l1 || g.disabled;
+  // scalar loads always use the (scalar) cache, -gpgpu_gmem_skip_L1D aside
+  const bool bypass = atomic || (in.flags & F_BYPASS_L1) || (c.gmem_skip_l1 && in.space != S_CONST) || g.disabled;
   const uint32_t nacc = in.width;
   const uint32_t stype = l1_stat_type(in.space, is_store, atomic);
   uint32_t banks_used = 0;
@@ -1208,7 +1209,8 @@ SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32
       ri.space = S_SHARED;
       ri.width = 1;
     }
-    if (ri.space == S_SHARED) s.w_slot_lds[w] = (uint8_t)(s.w_slot_lds[w] | (1u << sl));
+    // slots lgkmcnt counts: LDS and scalar (SMEM) loads
+    if (ri.space == S_SHARED || ri.space == S_CONST) s.w_slot_lds[w] = (uint8_t)(s.w_slot_lds[w] | (1u << sl));
   } else if (in.cls == OC_STORE && in.space != S_SHARED && in.width == 0) {
     ri.space = S_SHARED;
     ri.width = 1;

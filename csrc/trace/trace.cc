@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <sstream>
@@ -226,8 +227,13 @@ OpInfo decode_cdna(const std::string& op0) {
     o.space = S_SHARED;
     o.flags = F_MEM;
     o.width = cdna_width(m);
-  } else if (starts(m, "s_load") || starts(m, "s_buffer_load") || starts(m, "s_memtime") ||
-             starts(m, "s_memrealtime")) {
+  } else if (starts(m, "s_load") || starts(m, "s_buffer_load")) {
+    // scalar memory load (SMEM): through the CU's scalar data cache, counted
+    // by lgkmcnt; the trace carries no address (coalesce_kernel keys it)
+    o.cls = OC_LOAD;
+    o.space = S_CONST;
+    o.width = cdna_width(m);
+  } else if (starts(m, "s_memtime") || starts(m, "s_memrealtime")) {
     o.cls = OC_ALU;
     o.space = S_CONST;
   } else if (m == "s_waitcnt" || starts(m, "s_waitcnt")) {
@@ -448,7 +454,8 @@ std::vector<Command> parse_commandlist(const std::string& path) {
         c.addr = strtoull(p[1].c_str(), nullptr, 16);
         c.bytes = strtoull(p[2].c_str(), nullptr, 10);
       }
-      if (c.type == CMD_MEMCPY_DTOH) continue;  // ignored like the reference
+      // DtoH copies move no simulated work (ignored like the reference) but
+      // are host synchronisation points: the next kernel launches from idle
     } else if (line.rfind("kernel", 0) == 0) {
       c.type = CMD_KERNEL;
       c.text = line[0] == '/' ? line : dir + "/" + line;
@@ -784,13 +791,16 @@ HostKernel load_kernel_binary(const std::string& path) {
   uint32_t nu = 0;
   f.read(reinterpret_cast<char*>(&nu), 4);
   std::unordered_map<uint16_t, uint16_t> remap;
+  std::unordered_map<uint16_t, OpInfo> smem;  // CDNA scalar loads (classified by the current decoder)
   for (uint32_t i = 0; i < nu; ++i) {
     uint16_t id, len;
     f.read(reinterpret_cast<char*>(&id), 2);
     f.read(reinterpret_cast<char*>(&len), 2);
     std::string n(len, '\0');
     f.read(&n[0], len);
-    remap[id] = decode_opcode(n, h.binary_version).opcode;
+    const OpInfo oi = decode_opcode(n, h.binary_version);
+    remap[id] = oi.opcode;
+    if (h.binary_version >= 900 && oi.cls == OC_LOAD && oi.space == S_CONST) smem[id] = oi;
   }
   rd(f, k.insts, h.n_insts);
   rd(f, k.mems, h.n_mems);
@@ -798,6 +808,13 @@ HostKernel load_kernel_binary(const std::string& path) {
   rd(f, k.streams, h.n_streams);
   if (!f) throw std::runtime_error("truncated .asimk file: " + path);
   for (auto& in : k.insts) {
+    auto sm = smem.find(in.opcode);
+    if (sm != smem.end() && in.mem == kNoMem) {
+      // traces written before scalar loads became SMEM accesses kept them ALU
+      in.cls = OC_LOAD;
+      in.space = S_CONST;
+      in.width = sm->second.width;
+    }
     auto it = remap.find(in.opcode);
     if (it != remap.end()) in.opcode = it->second;
   }
@@ -921,6 +938,7 @@ ReadyKernel coalesce_kernel(const HostKernel& k, const SimCfg& c) {
   r.accs.reserve(k.mems.size() * 2);
   const uint32_t ws = k.h.warp_size ? k.h.warp_size : 32;
   std::vector<uint64_t> lane(64);
+  const uint64_t name_hash = std::hash<std::string>{}(k.h.name);
   std::vector<std::pair<uint64_t, uint8_t>> lines;
   std::vector<uint32_t> bytes;
   for (auto& in : r.insts) {
@@ -932,6 +950,23 @@ ReadyKernel coalesce_kernel(const HostKernel& k, const SimCfg& c) {
     uint32_t ii = c.ii[cls];
     if (half) ii = std::max<uint32_t>(1, ii / 2);
     in.ii = (uint8_t)std::min<uint32_t>(ii, 255);
+    if (in.mem == kNoMem && in.cls == OC_LOAD && in.space == S_CONST) {
+      // CDNA scalar load: one wave-uniform access.  Its address is not in the
+      // trace (the ISA tracer records vector addresses), so the scalar cache
+      // is keyed by kernel and code offset: the kernel-argument / constant
+      // loads every wave repeats hit after the first touch on a CU, nearby
+      // loads share lines (code offset / 8 -> data offset)
+      const uint64_t addr = kScalarBase + (name_hash & 0xfffffull) * 4096 + (uint64_t)(std::min<uint32_t>(in.pc, 32767) / 8);
+      TAcc a{};
+      a.line = addr & ~127ull;
+      a.sectors = (uint8_t)(1u << ((addr >> 5) & 3));
+      a.bytes = (uint16_t)std::max<uint32_t>(4, in.width);
+      a.bank = (uint8_t)((a.line >> 7) % std::max<uint32_t>(1, c.l1_banks));
+      in.mem = (uint32_t)r.accs.size();
+      r.accs.push_back(a);
+      in.width = 1;
+      continue;
+    }
     if (in.mem == kNoMem) {
       if ((in.cls == OC_LOAD || in.cls == OC_STORE) && in.space != S_SHARED) {
         // no active address: completes like a 1-cycle shared access

@@ -349,9 +349,14 @@ hipError_t hipMemcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind kin
   static F real = (F)dlsym(RTLD_NEXT, "hipMemcpy");
   hipError_t e = real(dst, src, bytes, kind);
   Tracer& t = T();
-  if (t.enabled && kind == hipMemcpyHostToDevice) {
+  if (t.enabled && (kind == hipMemcpyHostToDevice || kind == hipMemcpyDeviceToHost)) {
+    // DtoH copies carry no simulated work but mark a host synchronisation
+    // (the next kernel is launched from an idle queue)
     char s[96];
-    snprintf(s, sizeof(s), "MemcpyHtoD,0x%016llx,%zu", (unsigned long long)(uintptr_t)dst, bytes);
+    if (kind == hipMemcpyHostToDevice)
+      snprintf(s, sizeof(s), "MemcpyHtoD,0x%016llx,%zu", (unsigned long long)(uintptr_t)dst, bytes);
+    else
+      snprintf(s, sizeof(s), "MemcpyDtoH,0x%016llx,%zu", (unsigned long long)(uintptr_t)src, bytes);
     std::lock_guard<std::mutex> g(t.mu);
     t.append("kernelslist.g", s);
   }
@@ -401,7 +406,8 @@ hipError_t hipLaunchKernel(const void* f, dim3 g, dim3 b, void** args, size_t sh
   }
   db.last_used = used;
   std::vector<uint8_t> host((size_t)used * kChunkUnits * 16);
-  if (used) RT_HIP(hipMemcpy(host.data(), db.ptr, host.size(), hipMemcpyDeviceToHost));
+  // the tracer's own read-back is not an application copy (no trace line)
+  if (used) RT_HIP(hipMemcpyDtoH(host.data(), db.ptr, host.size()));
   write_kernel(t, id, name, mit->second, g, b, shmem, host, used);
   return e;
 }

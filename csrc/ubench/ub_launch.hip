@@ -15,6 +15,10 @@ __global__ void ub_empty_kernel(int* sink) {
   if (sink && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) sink[0] = 1;
 }
 
+__global__ void ub_empty_queued(int* sink) {
+  if (sink && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) sink[0] = 2;
+}
+
 // keeps the GPU busy (and its clocks up) for ~20 us before each measured launch,
 // like the kernel a real application launched just before
 __global__ void ub_warm_kernel(int spin, float* sink) {
@@ -41,6 +45,18 @@ int main() {
       UB_CHECK(hipDeviceSynchronize());
     }
     printf("empty kernel, %5d workgroups: best event time %.2f us\n", nb, best);
+  }
+  // queued launches: empty kernels issued back to back behind a busy kernel,
+  // with no event or synchronisation in between -- how an application's
+  // consecutive kernels reach the GPU (rocprofv3 durations of these give the
+  // per-kernel cost of a queued launch, -gpgpu_kernel_launch_latency_queued)
+  for (int nb : {1, 64, 1024}) {
+    for (int r = 0; r < 10; ++r) {
+      hipLaunchKernelGGL(ub_warm_kernel, dim3(256), dim3(64), 0, 0, 20000, nullptr);
+      for (int q = 0; q < 8; ++q) hipLaunchKernelGGL(ub_empty_queued, dim3(nb), dim3(64), 0, 0, nullptr);
+      UB_CHECK(hipDeviceSynchronize());
+    }
+    printf("queued empty kernels, %5d workgroups: launched\n", nb);
   }
   return 0;
 }

@@ -29,8 +29,8 @@ sys.path.insert(0, ROOT)
 from accel_sim_framework_distributed_amd.plotting import correlate  # noqa: E402
 
 
-def sim_one(kl: str, cfg_dir: str, extra: str) -> list:
-    args = [os.path.join(ROOT, "bin", "accel-sim.out"), "-config", os.path.join(cfg_dir, "gpgpusim.config")]
+def sim_one(kl: str, cfg_dir: str, extra: str, exe: str = "") -> list:
+    args = [exe or os.path.join(ROOT, "bin", "accel-sim.out"), "-config", os.path.join(cfg_dir, "gpgpusim.config")]
     tc = os.path.join(cfg_dir, "trace.config")
     if os.path.exists(tc):
         args += ["-config", tc]
@@ -49,6 +49,7 @@ def main(argv=None) -> int:
     ap.add_argument("--mhz", type=float, default=0.0, help="HW clock (default: the config's core clock)")
     ap.add_argument("-j", "--jobs", type=int, default=4)
     ap.add_argument("-o", "--json", default="")
+    ap.add_argument("--bin", default="", help="simulator executable (default bin/accel-sim.out)")
     o = ap.parse_args(argv)
     mhz = o.mhz
     if not mhz:
@@ -58,7 +59,7 @@ def main(argv=None) -> int:
     apps = sorted(a for a in hw if os.path.exists(os.path.join(o.traces, a, "traces", "kernelslist.g")))
     with ThreadPoolExecutor(o.jobs) as ex:
         sims = dict(zip(apps, ex.map(lambda a: sim_one(os.path.join(o.traces, a, "traces", "kernelslist.g"),
-                                                        o.config, o.extra), apps)))
+                                                        o.config, o.extra, o.bin), apps)))
     rows, errs = [], []
     for a in apps:
         ks = hw[a]
