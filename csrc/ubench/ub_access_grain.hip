@@ -46,25 +46,27 @@ int main() {
   const int trials = 32, offs[] = {4, 16, 32, 64, 96, 124};
   int *lines, *evict;
   uint64_t* o;
-  const size_t nlines = (size_t)trials * 2 * 8;  // fresh lines for every (offset, level) trial
+  const size_t nlines = (size_t)trials * 2 * 10;  // fresh lines for every (offset, level) trial
   UB_CHECK(hipMalloc(&lines, nlines * 4096 * sizeof(int)));
   UB_CHECK(hipMemset(lines, 0, nlines * 4096 * sizeof(int)));
   const int evict_n = 2 * 64 * 1024 / 4;  // 2x a 64 KB L1 in ints (one load per 128 B)
   UB_CHECK(hipMalloc(&evict, (size_t)evict_n * sizeof(int)));
   UB_CHECK(hipMemset(evict, 0, (size_t)evict_n * sizeof(int)));
   UB_CHECK(hipMalloc(&o, 16));
-  const double l1 = ub_chase_latency(8 * 1024, 128, 4096);
-  const double l2 = ub_chase_latency(512 * 1024, 128, 4096);
-  printf("# l1_hit_latency %.1f\n# l2_hit_latency %.1f\n", l1, l2);
   size_t slot = 0;
+  auto next = [&]() { return lines + (slot++) * 4096 * trials; };
+  // references in the same kernel shape (the stamps' own cost included):
+  // the same word again (an L1 hit) and the same word after the L1 sweep
+  // (an L2 hit); a word of another sector / line is classified against them
+  const double hit = probe(next(), evict, 0, 0, trials, o);
+  const double l2hit = probe(next(), evict, evict_n, 0, trials, o);
+  printf("# timed_l1_hit %.0f\n# timed_l2_hit %.0f\n", hit, l2hit);
   int l1_grain = 128, l2_grain = 128;
   bool l1_done = false, l2_done = false;
   for (int off : offs) {
-    const double a = probe(lines + slot * 4096 * trials, evict, 0, off, trials, o);
-    ++slot;
-    const double b = probe(lines + slot * 4096 * trials, evict, evict_n, off, trials, o);
-    ++slot;
-    const bool l1_hit = a < 0.5 * (l1 + l2), l2_hit = b < 2.0 * l2;
+    const double a = probe(next(), evict, 0, off, trials, o);
+    const double b = probe(next(), evict, evict_n, off, trials, o);
+    const bool l1_hit = a < 0.5 * (hit + l2hit), l2_hit = b < l2hit + 0.5 * (l2hit - hit) + 50;
     printf("second load at +%3d B: %6.0f cycles (%s in L1), after L1 eviction %6.0f cycles (%s in L2)\n", off, a,
            l1_hit ? "hit" : "miss", b, l2_hit ? "hit" : "miss");
     if (!l1_hit && !l1_done) { l1_grain = off < 32 ? 32 : (off / 32) * 32; l1_done = true; }

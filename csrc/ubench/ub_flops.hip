@@ -11,11 +11,11 @@ template <class T>
 __device__ __forceinline__ T fma_op(T a, T b, T c) { return a * b + c; }
 
 template <class T, int ITERS>
-__global__ void ub_flops_kernel(T seed, T* sink) {
+__global__ void ub_flops_kernel(T seed, T m, T c, T* sink) {
+  // m, c are kernel arguments: the compiler cannot fold the FMA chains
   T a[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) a[k] = seed + (T)(threadIdx.x + k);
-  const T m = (T)1.0001f, c = (T)0.5f;
   for (int i = 0; i < ITERS; ++i) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) a[k] = fma_op(a[k], m, c);
@@ -28,11 +28,11 @@ __global__ void ub_flops_kernel(T seed, T* sink) {
 
 // packed fp16: v_pk_fma_f16 does two half FMAs per lane
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-__global__ void ub_flops_half2(float seed, h2* sink) {
+__global__ void ub_flops_half2(float seed, float mf, float cf, h2* sink) {
   h2 a[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) a[k] = h2{(_Float16)(seed + k), (_Float16)(threadIdx.x + k)};
-  const h2 m = h2{(_Float16)1.0001f, (_Float16)1.0001f}, c = h2{(_Float16)0.5f, (_Float16)0.5f};
+  const h2 m = h2{(_Float16)mf, (_Float16)mf}, c = h2{(_Float16)cf, (_Float16)cf};
   for (int i = 0; i < 4096; ++i) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) a[k] = a[k] * m + c;
@@ -65,16 +65,16 @@ int main() {
   struct Row { const char* name; double ms; double ops_per_lane; };
   std::vector<Row> rows;
   rows.push_back({"fp64 (v_fma_f64)", timed_ms([&] {
-                    hipLaunchKernelGGL((ub_flops_kernel<double, 2048>), grid, block, 0, 0, 1.0, (double*)sink); }),
+                    hipLaunchKernelGGL((ub_flops_kernel<double, 2048>), grid, block, 0, 0, 1.0, 1.0001, 0.5, (double*)sink); }),
                   2.0 * 8 * 2048});
   rows.push_back({"fp32 (v_fma_f32)", timed_ms([&] {
-                    hipLaunchKernelGGL((ub_flops_kernel<float, 4096>), grid, block, 0, 0, 1.f, (float*)sink); }),
+                    hipLaunchKernelGGL((ub_flops_kernel<float, 4096>), grid, block, 0, 0, 1.f, 1.0001f, 0.5f, (float*)sink); }),
                   2.0 * 8 * 4096});
   rows.push_back({"fp16x2 (v_pk_fma_f16)", timed_ms([&] {
-                    hipLaunchKernelGGL(ub_flops_half2, grid, block, 0, 0, 1.f, (h2*)sink); }),
+                    hipLaunchKernelGGL(ub_flops_half2, grid, block, 0, 0, 1.f, 1.0001f, 0.5f, (h2*)sink); }),
                   4.0 * 8 * 4096});
   rows.push_back({"int32 (v_mad_u32)", timed_ms([&] {
-                    hipLaunchKernelGGL((ub_flops_kernel<uint32_t, 4096>), grid, block, 0, 0, 1u, (uint32_t*)sink); }),
+                    hipLaunchKernelGGL((ub_flops_kernel<uint32_t, 4096>), grid, block, 0, 0, 1u, 3u, 7u, (uint32_t*)sink); }),
                   2.0 * 8 * 4096});
   for (const Row& r : rows) {
     const double ops = lanes * r.ops_per_lane;
