@@ -117,21 +117,35 @@ struct SmRes {
 SIM_HDI uint32_t sm_cta_fit(const SMState& s, const SimCfg& c, const KernelDesc& k, uint32_t ks, SmRes& r) {
   const uint32_t nwm = amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t max_cta = amin<uint32_t>(c.max_cta_per_sm, kMaxCta);
-  uint32_t n = 0;
-  while (n < (uint32_t)kMaxCta) {
-    if ((uint32_t)s.n_cta_k[ks] + n >= k.cta_per_sm || r.ctas >= max_cta) break;
-    if (r.thr + k.thr_cta > c.max_threads_per_sm || r.regs + k.regs_cta > c.regs_per_sm) break;
-    if (k.shmem_per_cta && r.shmem + k.shmem_per_cta > k.shmem_cap) break;
-    const int b = warp_run_fit(r.wmask, k.warps_per_cta, nwm);
-    if (b < 0) break;
-    r.wmask |= (k.warps_per_cta >= 64 ? ~0ull : ((1ull << k.warps_per_cta) - 1)) << b;
-    r.ctas++;
-    r.thr += k.thr_cta;
-    r.regs += k.regs_cta;
-    r.shmem += k.shmem_per_cta;
-    ++n;
+  // counted resources: closed form
+  uint32_t n = k.cta_per_sm > s.n_cta_k[ks] ? k.cta_per_sm - s.n_cta_k[ks] : 0u;
+  n = amin<uint32_t>(n, max_cta > r.ctas ? max_cta - r.ctas : 0u);
+  if (k.thr_cta) n = amin<uint32_t>(n, c.max_threads_per_sm > r.thr ? (c.max_threads_per_sm - r.thr) / k.thr_cta : 0u);
+  if (k.regs_cta) n = amin<uint32_t>(n, c.regs_per_sm > r.regs ? (c.regs_per_sm - r.regs) / k.regs_cta : 0u);
+  if (k.shmem_per_cta) n = amin<uint32_t>(n, k.shmem_cap > r.shmem ? (k.shmem_cap - r.shmem) / k.shmem_per_cta : 0u);
+  // warps: first-fit placement of equal CTAs = as many as fit in each free
+  // run, lowest run first (one pass over the runs of the free mask)
+  const uint32_t wpc = k.warps_per_cta;
+  uint32_t placed = 0;
+  if (n && wpc && wpc <= nwm) {
+    uint64_t freem = ~r.wmask & (nwm >= 64 ? ~0ull : ((1ull << nwm) - 1));
+    const uint64_t one = wpc >= 64 ? ~0ull : ((1ull << wpc) - 1);
+    while (freem && placed < n) {
+      const uint32_t b0 = (uint32_t)ffs64(freem);
+      const uint64_t rest = b0 ? (freem >> b0) : freem;
+      const uint32_t len = ~rest ? (uint32_t)ffs64(~rest) : 64u - b0;
+      uint32_t fit = len / wpc;
+      if (fit > n - placed) fit = n - placed;
+      for (uint32_t j = 0; j < fit; ++j) r.wmask |= one << (b0 + j * wpc);
+      placed += fit;
+      freem = (b0 + len >= 64) ? 0ull : (freem & (~0ull << (b0 + len)));
+    }
   }
-  return n;
+  r.ctas += placed;
+  r.thr += placed * k.thr_cta;
+  r.regs += placed * k.regs_cta;
+  r.shmem += placed * k.shmem_per_cta;
+  return placed;
 }
 
 // kernel slot (re)initialisation of an SM: first epoch after a launch
