@@ -661,15 +661,20 @@ SIM_HDI XbarGrant xbar_pick(const Pkt* q, uint32_t head, uint32_t n, uint32_t ca
                             uint32_t nsrc) {
   const uint32_t m = n < 64u ? n : 64u;
   const uint32_t ptr = c.icnt_arbiter ? (uint32_t)arb_next % nsrc : (uint32_t)(icnt_cycle % nsrc);
-  uint32_t ready = 0;
-  const int o = P::argmin((int)m, [&](int i) -> uint64_t {
-    const Pkt& p = q[(head + (uint32_t)i) % cap];
-    if (p.t > now_fs) return ~0ull;
-    const uint32_t d = ((uint32_t)p.src + nsrc - ptr) % nsrc;
-    return (uint64_t)d << 8 | (uint64_t)i;
-  });
-  ready = (uint32_t)popc64(P::ballot((int)m, [&](int i) { return q[(head + (uint32_t)i) % cap].t <= now_fs; }));
-  const uint32_t off = o < 0 ? 0u : (uint32_t)o;
+  // packets that reached the port (arrival order is only nearly time order:
+  // serialised multi-flit packets can arrive after later-injected ones)
+  const uint64_t rmask = P::ballot((int)m, [&](int i) { return q[(head + (uint32_t)i) % cap].t <= now_fs; });
+  const uint32_t ready = (uint32_t)popc64(rmask);
+  uint32_t off = rmask ? (uint32_t)ffs64(rmask) : 0u;
+  if (ready > 1) {
+    const int o = P::argmin((int)m, [&](int i) -> uint64_t {
+      if (!(rmask >> i & 1ull)) return ~0ull;
+      const Pkt& p = q[(head + (uint32_t)i) % cap];
+      const uint32_t d = ((uint32_t)p.src + nsrc - ptr) % nsrc;
+      return (uint64_t)d << 8 | (uint64_t)i;
+    });
+    off = o < 0 ? 0u : (uint32_t)o;
+  }
   if (c.icnt_arbiter) {
     if (arb_cnt <= 1) {
       arb_next = (uint16_t)(((uint32_t)P::uni(q[(head + off) % cap].src) + 1) % nsrc);
