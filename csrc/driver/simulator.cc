@@ -925,6 +925,45 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   print("total dram writes = %llu\n", (unsigned long long)dram_wr);
   print("total dram activates = %llu\n", (unsigned long long)dram_act);
   print("dram_bw_util = %.4f\n", dram_cyc ? (double)dram_busy / dram_cyc : 0.0);
+  {
+    // per memory channel and per L2 bank (reference dram_t::print and the
+    // L2_cache_bank lines of gpgpu_sim::print_stats, cumulative counters;
+    // utilisation over this kernel)
+    const uint32_t per = std::max<uint32_t>(1, cfg_.n_sub_per_mem);
+    uint64_t icnt_stall = 0, dram_full = 0;
+    for (size_t ch = 0; ch * per < cmem.size(); ++ch) {
+      uint64_t rd = 0, wr = 0, act = 0, pre = 0, busy = 0, cyc = 0;
+      for (uint32_t j = 0; j < per && ch * per + j < cmem.size(); ++j) {
+        const MemStats& m = cmem[ch * per + j];
+        rd += m.dram_rd;
+        wr += m.dram_wr;
+        act += m.dram_act;
+        pre += m.dram_pre;
+        if (ch * per + j < mem.size()) {
+          busy += mem[ch * per + j].dram_busy_cycles;
+          cyc += mem[ch * per + j].dram_cycles;
+        }
+      }
+      print("DRAM[%zu]: n_act=%llu n_pre=%llu n_rd=%llu n_write=%llu bw_util=%.4f\n", ch, (unsigned long long)act,
+            (unsigned long long)pre, (unsigned long long)rd, (unsigned long long)wr, cyc ? (double)busy / cyc : 0.0);
+    }
+    for (size_t b = 0; b < cmem.size(); ++b) {
+      const MemStats& m = cmem[b];
+      uint64_t acc = 0, miss = 0;
+      for (int t = 0; t < L2T_COUNT; ++t) {
+        acc += m.l2[t][L2O_HIT] + m.l2[t][L2O_MISS] + m.l2[t][L2O_MSHR_HIT];
+        miss += m.l2[t][L2O_MISS];
+      }
+      print("L2_cache_bank[%zu]: Access = %llu, Miss = %llu, Miss_rate = %.3f, Pending_hits = %llu, Reservation_fails = %llu\n",
+            b, (unsigned long long)acc, (unsigned long long)miss, acc ? (double)miss / acc : 0.0,
+            (unsigned long long)(m.l2[L2T_RD][L2O_MSHR_HIT] + m.l2[L2T_WR][L2O_MSHR_HIT] + m.l2[L2T_ATOM][L2O_MSHR_HIT]),
+            (unsigned long long)(m.l2[L2T_RD][L2O_RES_FAIL] + m.l2[L2T_WR][L2O_RES_FAIL] + m.l2[L2T_ATOM][L2O_RES_FAIL]));
+      icnt_stall += m.icnt_stall;
+      dram_full += m.l2[L2T_RD][L2O_RES_FAIL] + m.l2[L2T_WR][L2O_RES_FAIL] + m.l2[L2T_ATOM][L2O_RES_FAIL];
+    }
+    print("gpu_stall_dramfull = %llu\n", (unsigned long long)dram_full);
+    print("gpu_stall_icnt2sh    = %llu\n", (unsigned long long)icnt_stall);
+  }
   print("gpgpu_n_tot_w_icount = %llu\n", (unsigned long long)tot_warp_insn_);
   {
     // crossbar subnets (reference LocalInterconnect::DisplayStats,
