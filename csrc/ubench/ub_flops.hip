@@ -1,6 +1,5 @@
 // Peak arithmetic throughput per data type and the register-file bandwidth
-// it implies (reference GPU_Microbenchmark core/MaxFlops_{double,float,half,
-// int32}, core/config_{dpu,fpu,int} and core/regfile_bw): every CU runs 8
+// it implies (reference GPU_Microbenchmark core/MaxFlops_{double,float,int32}, core/config_{dpu,fpu,int} and core/regfile_bw): every CU runs 8
 // waves of independent FMA chains (8 accumulators per lane, no dependency
 // between consecutive instructions), timed with hipEvents over the grid.
 // Prints TFLOP/s (TOP/s for int32), operations per CU per shader cycle, and
@@ -24,23 +23,6 @@ __global__ void ub_flops_kernel(T seed, T m, T c, T* sink) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) s += a[k];
   if (s == (T)-12345) sink[0] = s;  // keeps the chains alive
-}
-
-// packed fp16: v_pk_fma_f16 does two half FMAs per lane
-typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-__global__ void ub_flops_half2(float seed, float mf, float cf, h2* sink) {
-  h2 a[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) a[k] = h2{(_Float16)(seed + k), (_Float16)(threadIdx.x + k)};
-  const h2 m = h2{(_Float16)mf, (_Float16)mf}, c = h2{(_Float16)cf, (_Float16)cf};
-  for (int i = 0; i < 4096; ++i) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] = a[k] * m + c;
-  }
-  h2 s = a[0];
-#pragma unroll
-  for (int k = 1; k < 8; ++k) s = s + a[k];
-  if ((float)s.x == -12345.f) sink[0] = s;
 }
 
 template <class F>
@@ -70,9 +52,6 @@ int main() {
   rows.push_back({"fp32 (v_fma_f32)", timed_ms([&] {
                     hipLaunchKernelGGL((ub_flops_kernel<float, 4096>), grid, block, 0, 0, 1.f, 1.0001f, 0.5f, (float*)sink); }),
                   2.0 * 8 * 4096});
-  rows.push_back({"fp16x2 (v_pk_fma_f16)", timed_ms([&] {
-                    hipLaunchKernelGGL(ub_flops_half2, grid, block, 0, 0, 1.f, 1.0001f, 0.5f, (h2*)sink); }),
-                  4.0 * 8 * 4096});
   rows.push_back({"int32 (v_mad_u32)", timed_ms([&] {
                     hipLaunchKernelGGL((ub_flops_kernel<uint32_t, 4096>), grid, block, 0, 0, 1u, 3u, 7u, (uint32_t*)sink); }),
                   2.0 * 8 * 4096});
