@@ -76,6 +76,7 @@ CDNA = {
     "s_add_u32": ("INTP", "NONE", 0, 0), "s_mul_i32": ("INTP", "NONE", 0, 0), "s_cmp_lt_i32": ("INTP", "NONE", 0, 0),
     "s_cbranch_scc1": ("BRANCH", "NONE", 0, 0), "s_branch": ("BRANCH", "NONE", 0, 0),
     "s_waitcnt": ("NOP", "NONE", FLAG["WAITCNT"], 0), "s_barrier": ("BARRIER", "NONE", 0, 0),
+    "s_load_dwordx2": ("LOAD", "CONST", 0, 8), "s_load_dwordx4": ("LOAD", "CONST", 0, 16),
     "s_endpgm": ("EXIT", "NONE", 0, 0), "s_nop": ("NOP", "NONE", 0, 0),
     "global_load_dword": ("LOAD", "GLOBAL", FLAG["MEM"], 4), "global_load_dwordx2": ("LOAD", "GLOBAL", FLAG["MEM"], 8),
     "global_load_dwordx4": ("LOAD", "GLOBAL", FLAG["MEM"], 16),

@@ -137,3 +137,27 @@ def test_concurrent_gpu_matches_cpu(native, tmp_path):
     assert gpu.tot_cycle == cpu.tot_cycle
     assert [(k["uid"], k["start_cycle"], k["cycles"], k["insn"]) for k in gpu.kernels] == \
         [(k["uid"], k["start_cycle"], k["cycles"], k["insn"]) for k in cpu.kernels]
+
+
+def test_event_orders_streams(native, tmp_path):
+    """hipStreamWaitEvent: a kernel on stream 2 that waits for an event
+    recorded on stream 1 after kernel 1 starts only when kernel 1 is done."""
+    ks = [_kernel(1, 1, ctas=4, alu=200), _kernel(2, 2, ctas=4, alu=100)]
+    free = _app(tmp_path, "free", ks)
+    dep = _app(tmp_path, "dep", ks, extra_cmds=[(1, "hipEventRecord,event=7,stream=1"),
+                                              (2, "hipStreamWaitEvent,stream=2,event=7")])
+    a = _run(native, free, True).kernels
+    b = _run(native, dep, True).kernels
+    assert a[1]["start_cycle"] == 0
+    assert b[1]["start_cycle"] >= b[0]["start_cycle"] + b[0]["cycles"]
+    # a wait for an event recorded later in the trace does not wait for it
+    late = _app(tmp_path, "late", ks, extra_cmds=[(0, "hipStreamWaitEvent,stream=2,event=9"),
+                                                 (2, "hipEventRecord,event=9,stream=1")])
+    assert _run(native, late, True).kernels[1]["start_cycle"] == 0
+
+
+def test_trace_prefetch_does_not_change_results(native, tmp_path):
+    kl = _app(tmp_path, "pf", [_kernel(i, 1, ctas=3, alu=50) for i in range(1, 5)])
+    on = _run(native, kl, False, {"-trace_prefetch": "1"})
+    off = _run(native, kl, False, {"-trace_prefetch": "0"})
+    assert on.tot_cycle == off.tot_cycle and on.tot_insn == off.tot_insn

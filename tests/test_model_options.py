@@ -192,3 +192,43 @@ def test_max_cta_and_completed_cta_caps(native, traces):
     c = _run(native, traces["vadd"], {"-gpgpu_max_completed_cta": "20"})
     assert 20 <= int(_stat(c.output, "gpgpu_n_completed_cta")) < n_cta
     assert c.tot_insn < full.tot_insn
+
+
+def test_cdna_scalar_loads_use_the_scalar_cache(native, tmp_path):
+    """CDNA s_load: an lgkmcnt-counted load through the cache, keyed by kernel
+    and code offset (trace.cc coalesce_kernel); the first wave on a CU misses,
+    later waves of the same load hit."""
+    import re
+    from accel_sim_framework_distributed_amd.models import presets
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+
+    def run(smem, ctas, extra):
+        k = KernelBuilder("_Z4kargPf", (ctas, 1, 1), (256, 1, 1), nregs=32, binary_version=950, warp_size=64)
+        for i in range(8):  # a dependent chain: load, wait, use
+            k.op("s_load_dwordx2" if smem else "s_add_u32", [170], [171])
+            k.op("s_waitcnt")
+            k.op("s_add_u32", [171], [170, 171])
+        k.op("v_add_u32", [4], [171, 4])
+        k.op("s_endpgm")
+        kl = rodinia.write_app(str(tmp_path / f"k{int(smem)}_{ctas}"), [k.build()], memcpy=False)
+        s = native.Simulator(presets.args_for("MI355X", dict({"-gpgpu_perf_sim_memcpy": "0"}, **extra))
+                             + ["-trace", kl], False)
+        assert s.run() == 0
+        return s.output
+
+    def stat(out, key):
+        return int(re.findall(rf"^{re.escape(key)} = (\d+)", out, re.M)[-1])
+
+    full = run(True, 256, {})
+    assert stat(full, "gpgpu_n_load_insn") == 256 * 4 * 8
+    # nearby loads share a line (code offset / 8): the chain's 8 loads touch
+    # two 32-byte sectors, one miss each per CU (256 CUs, one CTA each); the
+    # other accesses hit or merge into them
+    l1 = [stat(full, f"\tTotal_core_cache_stats_breakdown[GLOBAL_ACC_R][{k}]") for k in ("HIT", "MISS", "MSHR_HIT")]
+    assert l1[1] == 2 * 256 and sum(l1) == 256 * 4 * 8
+    # latency: eight dependent round trips through the cache on one CU
+    quiet = {"-gpgpu_kernel_launch_latency": "0", "-gpgpu_inst_prefetch_lines": "0"}
+    ld, alu = run(True, 1, quiet), run(False, 1, quiet)
+    assert stat(alu, "gpgpu_n_load_insn") == 0
+    assert stat(ld, "gpu_sim_cycle") > stat(alu, "gpu_sim_cycle") + 8 * 100
