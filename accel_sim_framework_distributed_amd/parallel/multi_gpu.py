@@ -124,6 +124,10 @@ class DistributedSuite:
         cfg = self.mod.parse_config(build_args(self.config, None, "cpu"))
         per = self.mod.gpu_cus_per_sim(cfg["n_sm"], cfg["n_mem"]) if hasattr(self.mod, "gpu_cus_per_sim") \
             else cfg["n_sm"] + cfg["n_mem"]
+        # ASIM_GPU_BLOCKS caps a simulation's blocks (units time-slice over them)
+        cap = int(os.environ.get("ASIM_GPU_BLOCKS", "0") or 0)
+        if cap > 0:
+            per = min(per, cap)
         return max(1, cus // per // self.ranks_per_gpu()) if cus else 1
 
     def cpu_slots(self, reserve: int = 0) -> int:

@@ -169,6 +169,58 @@ def run(work: str, out_xml: str, iters: int = 48) -> Dict:
     return summary
 
 
+def simulate_trace_power_split(kernelslist: str, xml: str, work: str, config_dir: str = TUNED,
+                               jobs: int = 16) -> List[Dict]:
+    """simulate_trace_power with every kernel as its own CPU-engine simulation
+    (bin/accel-sim.out), `jobs` at a time: the kernels are independent power
+    samples, and one process per host core finishes a multi-GB trace list in
+    a fraction of one sequential run."""
+    import subprocess
+    import threading
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+    exe = os.path.join(REPO, "bin", "accel-sim.out")
+    d = os.path.dirname(os.path.abspath(kernelslist))
+    kernels = [l.strip() for l in open(kernelslist) if l.strip().startswith("kernel")]
+    os.makedirs(work, exist_ok=True)
+
+    def one(i_k):
+        i, k = i_k
+        wd = os.path.join(work, f"k{i:03d}")
+        os.makedirs(wd, exist_ok=True)
+        kl = os.path.join(wd, "kernelslist.g")
+        with open(kl, "w") as f:
+            f.write(os.path.join(d, k) + "\n")
+        rep = os.path.join(wd, "accelwattch_power_report.log")
+        args = [exe, "-config", os.path.join(config_dir, "gpgpusim.config"), "-config",
+                os.path.join(config_dir, "trace.config"), "-trace", kl, "-power_simulation_enabled", "1",
+                "-accelwattch_xml_file", xml, "-power_report_file", rep, "-gpgpu_runtime_stat", "1000000000:0",
+                "-sim_engine", "cpu", "-gpgpu_kernel_launch_latency", "0"]
+        r = subprocess.run(args, cwd=wd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                           env=dict(os.environ, OMP_NUM_THREADS="1"))
+        if r.returncode != 0:
+            raise RuntimeError(f"kernel {k}: simulation failed\n{r.stderr[-800:]}")
+        reps = report.parse_power_report(rep)
+        if len(reps) != 1:
+            raise RuntimeError(f"kernel {k}: {len(reps)} power reports")
+        return reps[0]
+
+    done = threading.Event()
+
+    def beat():
+        t0 = time.time()
+        while not done.wait(30):
+            print(f"[power validation] {len(kernels)} kernels on {jobs} cores: {time.time() - t0:.0f} s",
+                  file=sys.stderr, flush=True)
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            return list(ex.map(one, enumerate(kernels)))
+    finally:
+        done.set()
+
+
 def simulate_trace_power(kernelslist: str, xml: str, work: str, config_dir: str = TUNED,
                          engine: str = "cpu") -> List[Dict]:
     """Per-kernel power reports of one simulation of a captured trace list.
@@ -212,7 +264,11 @@ def run_traces(kernelslist: str, measured_csv: str, work: str, out_xml: str, con
     if not os.path.exists(base_xml):
         xmlcfg.write_xml(base_xml, xmlcfg.default_params("MI355X"))
     meas = measured_power(measured_csv)
-    reps = simulate_trace_power(kernelslist, base_xml, work, config_dir, engine)
+    if engine == "cpu-split":
+        reps = simulate_trace_power_split(kernelslist, base_xml, work, config_dir,
+                                          int(os.environ.get("MAX_JOBS", "16") or 16))
+    else:
+        reps = simulate_trace_power(kernelslist, base_xml, work, config_dir, engine)
     order = list(meas)  # measure mode prints the kernels in launch order
     if len(reps) != len(order):
         raise RuntimeError(f"{len(reps)} simulated kernels vs {len(order)} measured")

@@ -619,6 +619,7 @@ void Simulator::finish_kernel(uint32_t slot, const RunResult& rr) {
     snprintf(hdr, sizeof(hdr), "kernel_name = %s\nkernel_launch_uid = %u\ngpu_sim_cycle = %llu", r.name.c_str(), r.uid,
              (unsigned long long)r.cycles);
     ptrack_.write_kernel(*power_report_, hdr);
+    power_report_->flush();  // the CLI may exit without destroying the simulator
     if (power_steady_) {
       ptrack_.write_steady(*power_steady_, r.name);
       power_steady_->flush();

@@ -456,7 +456,9 @@ std::vector<Command> parse_commandlist(const std::string& path) {
       }
       // DtoH copies move no simulated work (ignored like the reference) but
       // are host synchronisation points: the next kernel launches from idle
-    } else if (line.rfind("kernel", 0) == 0) {
+    } else if (line.rfind("kernel", 0) == 0 ||
+               (line[0] == '/' && line.substr(line.rfind('/') + 1).rfind("kernel", 0) == 0)) {
+      // kernel-N.traceg / .asimk, relative to the list or an absolute path
       c.type = CMD_KERNEL;
       c.text = line[0] == '/' ? line : dir + "/" + line;
     } else if (line.rfind("nccl", 0) == 0 || line.rfind("rccl", 0) == 0) {

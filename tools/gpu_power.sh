@@ -18,8 +18,9 @@ ASIM_TRACE_DIR=/tmp/pwr_traces timeout -k 10 300 $R/bin/isatrace/power_suite tra
   || { echo "trace failed"; tail $out/trace.log; exit 1; }
 tail -1 $out/trace.log
 du -sh /tmp/pwr_traces
-timeout -k 10 600 python3 $R/accel_sim_framework_distributed_amd/power/mi355x_validation.py -t /tmp/pwr_traces/kernelslist.g \
-  -m $out/measured.csv -c $R/configs/tuned/AMD_Instinct_MI355X -e ${PWR_ENGINE:-gpu} -w /tmp/pwr_work \
+# cpu-split: every kernel is its own CPU-engine simulation, one per host core
+timeout -k 10 ${PWR_SIM_SECS:-800} python3 $R/accel_sim_framework_distributed_amd/power/mi355x_validation.py -t /tmp/pwr_traces/kernelslist.g \
+  -m $out/measured.csv -c $R/configs/tuned/AMD_Instinct_MI355X -e ${PWR_ENGINE:-cpu-split} -w /tmp/pwr_work \
   -j $out/validation.json -o $out/accelwattch_sass_sim_calibrated.xml > $out/validation.log 2>&1; e=$?
 cat $out/validation.log | tail -32
 rm -rf /tmp/pwr_traces /tmp/pwr_work
