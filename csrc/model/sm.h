@@ -163,6 +163,8 @@ struct alignas(16) SMState {
   uint16_t w_loads[kMaxWarps];   // outstanding load slots in use
   uint16_t w_wait[kMaxWarps];    // counts of the pending s_waitcnt: vm | lgkm << 8 (0xff: not waited for)
   uint64_t w_sb[kMaxWarps][4];   // scoreboard: pending destination registers
+  TInst w_hin[kMaxWarps];        // the instruction at w_head (TInst{} past the stream end): read every cycle
+                                 // by the scheduler from here instead of from the trace in HBM
   uint8_t w_slot_used[kMaxWarps];  // bitmask of used load slots
   uint8_t w_slot_lds[kMaxWarps];   // load slots holding an LDS load (lgkmcnt, not vmcnt)
   uint8_t w_lds_st[kMaxWarps];     // LDS stores in flight (lgkmcnt)
@@ -1134,7 +1136,7 @@ template <class S>
 SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, const KernelTab& kt, int w, uint32_t nsched,
                             uint64_t idoc_busy) {
   if (!(s.w_flags[w] & WF_ACTIVE) || s.w_ibuf[w] == 0) return false;
-  const TInst in = inst_at(kt, s.w_head[w]);  // ibuf > 0: the head is inside the warp's stream
+  const TInst in = s.w_hin[w];  // ibuf > 0: the head is inside the warp's stream
   return warp_can_issue_i(s, c, w, in, nsched, idoc_busy);
 }
 
@@ -1148,6 +1150,10 @@ SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32
   if (trace_sm_on(c, TS_WARP_SCHEDULER, s.id))
     P::one([&] { trace_put(c, s.id, now, EV_ISSUE, (uint16_t)w, (uint64_t)in.pc | (uint64_t)in.opcode << 32); });
   s.w_head[w] = hidx + 1;
+  {
+    const TInst nx = hidx + 1 < P::uni((uint32_t)s.w_end[w]) ? inst_at(*x.kt, hidx + 1) : TInst{};
+    P::one([&] { s.w_hin[w] = nx; });
+  }
   s.w_ibuf[w] = (uint8_t)(P::uni((uint8_t)s.w_ibuf[w]) - 1);
   // stats: instruction counts at issue (reference counts active threads,
   // shader.cc:1911)
@@ -1255,10 +1261,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   const uint64_t idoc_busy = P::uni(s.idoc_mask);
   // every warp's next instruction, read once (a register per lane on the GPU)
   // (read straight from the kernel's trace in HBM: an L2-resident stream)
-  const auto head = P::template lanes<TInst>(nw, [&](int w) -> TInst {
-    const uint32_t h = s.w_head[w];
-    return h < s.w_end[w] ? inst_at(kt, h) : TInst{};
-  });
+  const auto head = P::template lanes<TInst>(nw, [&](int w) -> TInst { return s.w_hin[w]; });
   // readiness of every warp (lane-parallel)
   const uint64_t live = P::uni(s.live_mask);
   uint64_t ready = P::ballot_m(live, [&](int w) -> bool { return warp_can_issue_i(s, c, w, head.self(w), nsched, idoc_busy); });
@@ -1342,7 +1345,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
     // warp's next buffered instruction issues in the same cycle if it is
     // ready and, with -gpgpu_dual_issue_diff_exec_units, uses another unit
     if (c.max_issue_per_warp > 1 && u1 >= 0 && P::uni((uint8_t)s.w_ibuf[w])) {
-      const TInst in2 = P::uni(inst_at(kt, hidx + 1));
+      const TInst in2 = P::uni(s.w_hin[w]);  // refreshed by the first issue
       const bool special = in2.cls == OC_EXIT || in2.cls == OC_BARRIER || in2.cls == OC_MEMBAR ||
                            in2.cls == OC_NOP || (in2.flags & F_WAITCNT);
       if (!special && (!c.dual_issue_diff || unit_of(c, in2.cls) != (uint32_t)u1) &&
@@ -1501,6 +1504,7 @@ SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id,
     s.w_next[w] = tag | ws.begin;
     s.w_head[w] = tag | ws.begin;
     s.w_end[w] = tag | (ws.begin + ws.count);
+    s.w_hin[w] = ws.count ? k.insts[ws.begin] : TInst{};
     s.w_age[w] = age0 + (uint32_t)i;
     s.w_flags[w] = WF_ACTIVE;
     s.w_ibuf[w] = 0;
