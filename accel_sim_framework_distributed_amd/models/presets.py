@@ -522,6 +522,8 @@ def _mi355x() -> Dict[str, str]:
         "-gpgpu_registers_per_block": "131072",
         "-gpgpu_shader_cta": "32",
         "-gpgpu_num_sched_per_core": "4",
+        # one wave issues an instruction every ~5.5 cycles (ub_wave_issue)
+        "-gpgpu_warp_issue_interval": "5",
         "-gpgpu_scheduler": "gto",
         "-gpgpu_shmem_num_banks": "64",
         "-gpgpu_shmem_size": "163840",

@@ -88,6 +88,8 @@ const OptDef kOptions[] = {
     {"-gpgpu_coalesce_arch", 'i', "13", "coalescing architecture (compute capability)"},
     {"-gpgpu_num_sched_per_core", 'i', "1", "warp schedulers per SM"},
     {"-gpgpu_max_insn_issue_per_warp", 'i', "2", "max instructions issued per warp per cycle"},
+    {"-gpgpu_warp_issue_interval", 'u', "1",
+     "minimum cycles between two issue cycles of one warp (1 = every cycle; CDNA: the sequencer visits a SIMD's waves every few cycles)"},
     {"-gpgpu_dual_issue_diff_exec_units", 'b', "1", "dual issue to different units only"},
     {"-gpgpu_simt_core_sim_order", 'i', "1", "core simulation order"},
     {"-gpgpu_pipeline_widths", 's', "1,1,1,1,1,1,1,1,1,1,1,1,1", "pipeline register widths"},
@@ -600,6 +602,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.sub_core = r.getb("-gpgpu_sub_core_model") ? 1 : 0;
   c.fetch_throughput = (uint32_t)std::max<long long>(1, r.geti("-gpgpu_inst_fetch_throughput"));
   c.max_issue_per_warp = (uint32_t)std::max<long long>(1, r.geti("-gpgpu_max_insn_issue_per_warp"));
+  c.warp_issue_interval = std::max<uint32_t>(1, (uint32_t)r.getu("-gpgpu_warp_issue_interval"));
   c.dual_issue_diff = r.getb("-gpgpu_dual_issue_diff_exec_units") ? 1u : 0u;
   {
     // scheduler parameters: two_level_active:<max_active>:<inner>:<outer>,

@@ -191,6 +191,7 @@ struct SmView {
   SV_REF(w_slot_lds);
   SV_REF(w_lds_st);
   WarpSb w_sb;
+  SV_REF(w_issue_ok);
   SV_REF(w_hin);
   SV_WARP(w_slot_used);
   SV_REF(w_slot_pend);
@@ -285,7 +286,7 @@ struct SmView {
 
   __device__ __forceinline__ explicit SmView(B& b)
       : base(b), l1_sets(b.l1_sets), l1_assoc(b.l1_assoc), cycle(b.cycle), arb_next(b.arb_next),
-        arb_cnt(b.arb_cnt), w_wait(b.w_wait), w_slot_lds(b.w_slot_lds), w_lds_st(b.w_lds_st), w_hin(b.w_hin),
+        arb_cnt(b.arb_cnt), w_wait(b.w_wait), w_slot_lds(b.w_slot_lds), w_lds_st(b.w_lds_st), w_issue_ok(b.w_issue_ok), w_hin(b.w_hin),
         w_slot_pend(b.w_slot_pend),
         w_slot_dst(b.w_slot_dst), cta_id(b.cta_id), cta_ks(b.cta_ks), cta_wbase(b.cta_wbase), cta_nw(b.cta_nw),
         n_cta_k(b.n_cta_k), cta_wmask(b.cta_wmask), used_thr(b.used_thr), used_regs(b.used_regs),

@@ -135,6 +135,7 @@ struct SimCfg {
   uint32_t sub_core;
   uint32_t fetch_throughput;
   uint32_t max_issue_per_warp;
+  uint32_t warp_issue_interval;   // cycles between two issue cycles of one warp (CDNA: a wave issues once per SIMD visit)
   uint32_t dual_issue_diff;      // -gpgpu_dual_issue_diff_exec_units
   uint32_t sched_param;          // two_level_active:<max active>, warp_limiting:<prio>:<warps>
   // ---- execution ----

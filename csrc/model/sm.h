@@ -163,6 +163,7 @@ struct alignas(16) SMState {
   uint16_t w_loads[kMaxWarps];   // outstanding load slots in use
   uint16_t w_wait[kMaxWarps];    // counts of the pending s_waitcnt: vm | lgkm << 8 (0xff: not waited for)
   uint64_t w_sb[kMaxWarps][4];   // scoreboard: pending destination registers
+  uint64_t w_issue_ok[kMaxWarps];  // first cycle the warp may issue again (-gpgpu_warp_issue_interval)
   TInst w_hin[kMaxWarps];        // the instruction at w_head (TInst{} past the stream end): read every cycle
                                  // by the scheduler from here instead of from the trace in HBM
   uint8_t w_slot_used[kMaxWarps];  // bitmask of used load slots
@@ -1140,6 +1141,12 @@ SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, const KernelTab& kt, in
   return warp_can_issue_i(s, c, w, in, nsched, idoc_busy);
 }
 
+// -gpgpu_warp_issue_interval: has the warp's issue interval elapsed at `now`
+template <class S>
+SIM_HDI bool warp_issue_due(const S& s, const SimCfg& c, int w, uint64_t now) {
+  return c.warp_issue_interval <= 1 || now >= s.w_issue_ok[w];
+}
+
 // issue one instruction `in` (trace index hidx) of warp w from scheduler sc;
 // returns its execution unit, or -1 for the kinds handled at issue (EXIT,
 // barrier, fence, waitcnt, NOP)
@@ -1264,7 +1271,9 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   const auto head = P::template lanes<TInst>(nw, [&](int w) -> TInst { return s.w_hin[w]; });
   // readiness of every warp (lane-parallel)
   const uint64_t live = P::uni(s.live_mask);
-  uint64_t ready = P::ballot_m(live, [&](int w) -> bool { return warp_can_issue_i(s, c, w, head.self(w), nsched, idoc_busy); });
+  uint64_t ready = P::ballot_m(live, [&](int w) -> bool {
+    return warp_can_issue_i(s, c, w, head.self(w), nsched, idoc_busy) && warp_issue_due(s, c, w, now);
+  });
   // warps parked at a barrier / fence / exit (the reference's waiting()),
   // plus for the two-level scheduler those whose next instruction waits on
   // a long (memory) operation
@@ -1338,6 +1347,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
     }
     const uint32_t w = P::uni((uint32_t)pick);
     s.sched_last[sc] = w;
+    if (c.warp_issue_interval > 1) P::one([&] { s.w_issue_ok[w] = now + c.warp_issue_interval; });
     const uint32_t hidx = P::uni((uint32_t)s.w_head[w]);
     const int u1 = sm_issue_one<P>(s, x, now, sc, w, head.at((int)w), hidx);
     issued_any = true;
@@ -1505,6 +1515,7 @@ SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id,
     s.w_head[w] = tag | ws.begin;
     s.w_end[w] = tag | (ws.begin + ws.count);
     s.w_hin[w] = ws.count ? k.insts[ws.begin] : TInst{};
+    s.w_issue_ok[w] = 0;
     s.w_age[w] = age0 + (uint32_t)i;
     s.w_flags[w] = WF_ACTIVE;
     s.w_ibuf[w] = 0;
@@ -1608,9 +1619,19 @@ SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, const KernelTab& kt
     if (drained && s.w_inflight[w] == 0 && s.w_stores[w] == 0 && s.w_loads[w] == 0) return true;  // retire
     if ((f & WF_MEMBAR) && s.w_stores[w] == 0) return true;
     if ((f & WF_WAITCNT) && waitcnt_met(s, w)) return true;
-    return warp_can_issue(s, c, kt, w, nsched, s.idoc_mask);  // issue
+    return warp_can_issue(s, c, kt, w, nsched, s.idoc_mask) && warp_issue_due(s, c, w, t);  // issue
   });
-  return act ? t : nx;
+  if (act) return t;
+  if (c.warp_issue_interval > 1) {
+    // warps held only by their issue interval wake when it ends
+    const int o = P::argmin(nw, [&](int w) -> uint64_t {
+      if (!(P::uni(s.live_mask) >> w & 1ull)) return ~0ull;
+      return warp_can_issue(s, c, kt, w, nsched, s.idoc_mask) && !warp_issue_due(s, c, w, t) ? s.w_issue_ok[w]
+                                                                                                : ~0ull;
+    });
+    if (o >= 0) nx = amin<uint64_t>(nx, P::uni((uint64_t)s.w_issue_ok[o]));
+  }
+  return nx;
 }
 
 // account `k` quiet cycles: exactly what k idle sm_cycle calls would add

@@ -232,3 +232,25 @@ def test_cdna_scalar_loads_use_the_scalar_cache(native, tmp_path):
     ld, alu = run(True, 1, quiet), run(False, 1, quiet)
     assert stat(alu, "gpgpu_n_load_insn") == 0
     assert stat(ld, "gpu_sim_cycle") > stat(alu, "gpu_sim_cycle") + 8 * 100
+
+
+def test_warp_issue_interval(native, tmp_path):
+    """-gpgpu_warp_issue_interval: one warp's independent instructions issue
+    at most once per interval (measured on MI355X by ub_wave_issue: ~5.5)."""
+    import re
+    from accel_sim_framework_distributed_amd.models import presets
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+    k = KernelBuilder("_Z3ilpPf", (1, 1, 1), (32, 1, 1), nregs=32)
+    for i in range(256):
+        k.op("FFMA", [8 + i % 8], [8 + i % 8, 4])
+    k.op("EXIT")
+    kl = rodinia.write_app(str(tmp_path / "ilp"), [k.build()], memcpy=False)
+    cyc = {}
+    for iv in (1, 4):
+        s = native.Simulator(presets.args_for("QV100", {"-gpgpu_warp_issue_interval": str(iv),
+                                                        "-gpgpu_kernel_launch_latency": "0"}) + ["-trace", kl], False)
+        assert s.run() == 0
+        cyc[iv] = int(re.findall(r"^gpu_sim_cycle = (\d+)", s.output, re.M)[-1])
+    # 256 independent instructions: ~3 extra cycles each
+    assert cyc[4] - cyc[1] >= 256 * 2
