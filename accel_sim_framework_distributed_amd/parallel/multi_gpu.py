@@ -85,6 +85,8 @@ class DistributedSuite:
         dp = os.path.join(root, f"dp-step-{world}", f"rank{rank}", "kernelslist.g")
         self.dp_step = dp if os.path.exists(dp) and (not apps or "dp-step" in apps) else None
         self.dp_last: Dict = {}
+        self.calibration: Dict = {}
+        self.predicted_span = 0.0
         if self.dp_step:
             # scheduled like any application (node placement, LPT order)
             self.apps.append(("dp-step", self.dp_step))
@@ -203,25 +205,35 @@ class DistributedSuite:
     # host core.  The node schedule gives every application the engine that
     # minimises the step's makespan, like the reference's job-level
     # parallelism (procman over a node's cores) plus the GPU.
-    def calibrate(self) -> Dict[str, Dict[str, float]]:
+    def calibrate(self, rounds: int = 2) -> Dict[str, Dict[str, float]]:
         """Time every application on both engines (GPU slots and CPU cores
-        side by side), so plan() can place them."""
+        side by side), so plan() can place them.  Each (application, engine)
+        keeps its fastest of `rounds` timings: one sample taken under the
+        whole node's load is noisy enough to flip a placement."""
         from concurrent.futures import ThreadPoolExecutor
         gslots = max(1, self.concurrency())
         cslots = self.cpu_slots(reserve=gslots)
+        best: Dict = {}
         # the DDP step is timed uncoupled (its collectives emulated locally):
         # two engines running it at once must not both talk to the other ranks
         self._calibrating = True
         try:
-            with ThreadPoolExecutor(max_workers=gslots, initializer=self._bind_device) as gx, \
-                    ThreadPoolExecutor(max_workers=cslots) as cx:
-                fg = [gx.submit(self._run_app, a, "gpu") for a in self.apps]
-                fc = [cx.submit(self._run_app, a, "cpu") for a in self.apps]
-                for f in fg + fc:
-                    f.result()
+            for _ in range(max(1, rounds)):
+                with ThreadPoolExecutor(max_workers=gslots, initializer=self._bind_device) as gx, \
+                        ThreadPoolExecutor(max_workers=cslots) as cx:
+                    fg = [gx.submit(self._run_app, a, "gpu") for a in self.apps]
+                    fc = [cx.submit(self._run_app, a, "cpu") for a in self.apps]
+                    for f in fg + fc:
+                        f.result()
+                for a, _ in self.apps:
+                    for e in ("gpu", "cpu"):
+                        best[(a, e)] = min(best.get((a, e), float("inf")), self.times[(a, e)])
         finally:
             self._calibrating = False
-        return {a: {"gpu": self.times[(a, "gpu")], "cpu": self.times[(a, "cpu")]} for a, _ in self.apps}
+        self.times.update(best)
+        self.calibration = {a: {"gpu": round(self.times[(a, "gpu")], 4), "cpu": round(self.times[(a, "cpu")], 4)}
+                            for a, _ in self.apps}
+        return self.calibration
 
     @staticmethod
     def _lpt(ts: List[float], slots: int) -> float:

@@ -212,7 +212,9 @@ def main() -> int:
                 "seq_len": None,
                 "parallelism": f"one simulated GPU per MI355X rank (dp{world}), RCCL-synchronised collectives",
                 "engine": engine,
-                **({"node_assignment": suite.assignment} if engine == "node" else {}),
+                **({"node_assignment": suite.assignment,
+                    "node_calibration_s": suite.calibration,
+                    "node_predicted_step_ms": round(suite.predicted_span * 1e3, 1)} if engine == "node" else {}),
                 "apps": len(suite.apps),
                 "sim_insn_per_step_per_rank": int(insn / max(1, a.steps)),
                 "sim_cycles_per_step_per_rank": int(cycles / max(1, a.steps)),
