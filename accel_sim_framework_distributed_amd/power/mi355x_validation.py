@@ -274,21 +274,54 @@ def run_traces(kernelslist: str, measured_csv: str, work: str, out_xml: str, con
         raise RuntimeError(f"{len(reps)} simulated kernels vs {len(order)} measured")
     A = calibrate.design_matrix(reps)
     b = np.array([meas[n] for n in order])
+    s = fit_report(A, b, order, bound)
+    calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
+    s.update(sim_cycles=[r.get("gpu_sim_cycle", 0.0) for r in reps], traces="automatic ISA traces (isatrace)",
+             xml=out_xml)
+    return s
+
+
+def fit_report(A: np.ndarray, b: np.ndarray, order: List[str], bound: float = 20.0) -> Dict:
+    """Fit the FINE_GROUPS factors plus the package power cap to measured
+    power (rows of A: per-kernel simulated component powers with no cap in
+    the XML) and score it in-sample and leave-one-out.  The uncapped linear
+    fit is reported alongside for comparison."""
     before = A.sum(axis=1)
     kw = dict(groups=calibrate.FINE_GROUPS, lower=1.0 / bound, upper=bound)
-    x = calibrate.fit_groups(A, b, **kw)
-    loo = calibrate.leave_one_out_groups(A, b, **kw)
-    fit = A @ x
+    x, cap = calibrate.fit_groups_capped(A, b, **kw)
+    loo = calibrate.leave_one_out_capped(A, b, **kw)
+    fit = calibrate.predict_capped(A, x, cap)
+    x_lin = calibrate.fit_groups(A, b, **kw)
+    loo_lin = calibrate.leave_one_out_groups(A, b, **kw)
     gf = calibrate.group_factors(x, calibrate.FINE_GROUPS)
     at_bound = [g for g, v in gf.items() if v <= 1.0 / bound * 1.001 or v >= bound * 0.999]
-    calibrate.apply_factors(base_xml, out_xml, x)
-    return dict(kernels=order, measured_w=b.tolist(), uncalibrated_w=before.tolist(), calibrated_w=fit.tolist(),
+    return dict(kernels=list(order), measured_w=b.tolist(), uncalibrated_w=before.tolist(), calibrated_w=fit.tolist(),
                 loo_w=loo.tolist(), mape_uncalibrated=calibrate.mape(before, b)[0],
                 mape_in_sample=calibrate.mape(fit, b)[0], mape_leave_one_out=calibrate.mape(loo, b)[0],
                 mae_leave_one_out_w=calibrate.mape(loo, b)[1], group_factors=gf, factors_at_bound=at_bound,
-                sim_cycles=[r.get("gpu_sim_cycle", 0.0) for r in reps], traces="automatic ISA traces (isatrace)",
-                components=list(calibrate.COMPONENTS), components_w=A.tolist(), bounds=[1.0 / bound, bound],
-                xml=out_xml)
+                power_cap_w=cap, capped_kernels=[n for n, v in zip(order, A @ x) if v > cap],
+                linear_no_cap=dict(mape_in_sample=calibrate.mape(A @ x_lin, b)[0],
+                                   mape_leave_one_out=calibrate.mape(loo_lin, b)[0],
+                                   group_factors=calibrate.group_factors(x_lin, calibrate.FINE_GROUPS)),
+                components=list(calibrate.COMPONENTS), components_w=np.asarray(A).tolist(), bounds=[1.0 / bound, bound],
+                _x=x)
+
+
+def refit(json_path: str, out_xml: str, config_dir: str = TUNED, bound: float = 20.0) -> Dict:
+    """Re-run the fit on a saved validation record (its per-kernel component
+    powers and measured watts) without re-simulating."""
+    with open(json_path) as f:
+        old = json.load(f)
+    A = np.asarray(old["components_w"], np.float64)
+    b = np.asarray(old["measured_w"], np.float64)
+    s = fit_report(A, b, old["kernels"], bound)
+    base_xml = os.path.join(config_dir, "accelwattch_sass_sim.xml")
+    calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
+    for k in ("sim_cycles", "traces", "note"):
+        if k in old:
+            s[k] = old[k]
+    s["xml"] = os.path.relpath(out_xml, REPO) if out_xml.startswith(REPO) else out_xml
+    return s
 
 
 def main(argv=None) -> int:
@@ -300,9 +333,12 @@ def main(argv=None) -> int:
     ap.add_argument("-m", "--measured", default="", help="CSV of power_suite measure")
     ap.add_argument("-c", "--config_dir", default=TUNED)
     ap.add_argument("-e", "--engine", default="cpu", help="cpu | gpu (the MI355X cycle engine)")
+    ap.add_argument("--refit", default="", help="re-fit a saved validation JSON (no simulation)")
     o = ap.parse_args(argv)
     work = o.work or tempfile.mkdtemp(prefix="asim_power_")
-    if o.traces:
+    if o.refit:
+        s = refit(o.refit, o.out_xml, o.config_dir)
+    elif o.traces:
         s = run_traces(o.traces, o.measured or MEASURED, work, o.out_xml, o.config_dir, engine=o.engine)
     else:
         s = run(work, o.out_xml)
@@ -315,7 +351,7 @@ def main(argv=None) -> int:
     print(f"MAPE uncalibrated {s['mape_uncalibrated']:.2f}%  in-sample {s['mape_in_sample']:.2f}%  "
           f"leave-one-out {s['mape_leave_one_out']:.2f}% ({s['mae_leave_one_out_w']:.1f} W)")
     print("group factors:", {g: round(v, 3) for g, v in s["group_factors"].items()},
-          "at bound:", s.get("factors_at_bound"))
+          "at bound:", s.get("factors_at_bound"), "power cap:", s.get("power_cap_w"))
     return 0
 
 

@@ -137,6 +137,19 @@ PowerReport PowerModel::compute(const Activity& a, double core_mhz, uint32_t n_s
   r.cmp[PC_IDLE_CORE] = r.idle;
   r.cmp[PC_CONST] = r.constant;
   r.cmp[PC_STATIC] = r.static_w;
+  r.uncapped = r.total;
+  const double cap = param("power_cap", 0);
+  if (cap > 0 && r.total > cap) {
+    const double f = cap / r.total;
+    for (int i = 0; i < PA_COUNT; ++i) r.dynamic_w[i] *= f;
+    for (int i = 0; i < PC_COUNT; ++i) r.cmp[i] *= f;
+    r.dynamic *= f;
+    r.static_w *= f;
+    r.constant *= f;
+    r.idle *= f;
+    r.total = cap;
+    r.capped = true;
+  }
   return r;
 }
 

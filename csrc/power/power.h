@@ -10,6 +10,11 @@
 //   P = constant + idle_sm * n_idle + static(category, lanes)
 //       + sum_i  base_nJ[i] * scale[i] * accesses[i] / t
 // evaluated on the host per sample from the engines' activity counters.
+// An optional `power_cap` parameter models the package power limit: the
+// MI355X's power management holds socket power at its limit by lowering the
+// clocks (every compute-saturating validation kernel measures 1280-1330 W),
+// so a sample whose unconstrained estimate exceeds the cap reports the cap,
+// with every component scaled by cap / estimate (DVFS lowers all of them).
 #pragma once
 #include <map>
 #include <ostream>
@@ -63,6 +68,8 @@ struct PowerReport {
   double constant = 0;
   double idle = 0;
   double total = 0;
+  double uncapped = 0;  // estimate before the package power cap
+  bool capped = false;
   std::string static_category;
 };
 

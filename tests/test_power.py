@@ -138,3 +138,46 @@ def test_apply_factors_rescales_xml(tmp_path):
     assert p1["MEM_RD"] == pytest.approx(2 * p0["MEM_RD"]) and p1["MEM_WR"] == pytest.approx(2 * p0["MEM_WR"])
     assert p1["static_cat2_flane"] == pytest.approx(0.5 * p0["static_cat2_flane"])
     assert p1["INT_ACC"] == pytest.approx(p0["INT_ACC"])
+
+
+def test_capped_fit_recovers_power_cap():
+    # synthetic suite: linear model with known group factors, clipped at a cap
+    rng = np.random.RandomState(3)
+    comps = list(calibrate.COMPONENTS)
+    A = np.zeros((24, len(comps)))
+    A[:, comps.index("CONSTP")] = 300.0
+    A[:, comps.index("FPUP")] = rng.uniform(0, 400, 24)
+    A[:, comps.index("DRAMP")] = rng.uniform(0, 150, 24)
+    A[:, comps.index("TENSORP")] = rng.uniform(0, 100, 24) * (rng.rand(24) < 0.4)
+    x_true = np.ones(len(comps))
+    x_true[comps.index("FPUP")] = 2.5
+    x_true[comps.index("DRAMP")] = 3.0
+    x_true[comps.index("TENSORP")] = 6.0
+    b = np.minimum(A @ x_true, 1200.0)
+    assert (A @ x_true > 1200.0).sum() >= 3  # some kernels really are capped
+    x, cap = calibrate.fit_groups_capped(A, b)
+    assert cap == pytest.approx(1200.0, rel=5e-3)
+    assert calibrate.mape(calibrate.predict_capped(A, x, cap), b)[0] < 0.5
+    loo = calibrate.leave_one_out_capped(A, b)
+    assert calibrate.mape(loo, b)[0] < 2.0
+
+
+def test_power_cap_clamps_samples(native, tmp_path):
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    p = xmlcfg.default_params("QV100")
+    free_xml = str(tmp_path / "free.xml")
+    xmlcfg.write_xml(free_xml, p)
+    ks = [rodinia.vectoradd(300000)]
+    opts = {"-power_simulation_enabled": "1", "-gpgpu_runtime_stat": "300:0"}
+    _, d0 = _run(native, tmp_path, "free", dict(opts, **{"-accelwattch_xml_file": free_xml}), ks)
+    free = report.parse_power_report(str(d0 / "accelwattch_power_report.log"))[0]
+    cap = 0.5 * (free["kernel_max_power"] + free["kernel_min_power"])
+    assert free["kernel_max_power"] > cap > p["constant_power"]
+    capped_xml = str(tmp_path / "capped.xml")
+    xmlcfg.write_xml(capped_xml, dict(p, power_cap=cap))
+    _, d1 = _run(native, tmp_path, "capped", dict(opts, **{"-accelwattch_xml_file": capped_xml}), ks)
+    k = report.parse_power_report(str(d1 / "accelwattch_power_report.log"))[0]
+    assert k["kernel_max_power"] == pytest.approx(cap, rel=1e-6)
+    assert k["kernel_avg_power"] < free["kernel_avg_power"]
+    # components are scaled with the total, so they still add up
+    assert abs(sum(k["avg"].values()) - k["kernel_avg_power"]) < 1e-4 * k["kernel_avg_power"]
