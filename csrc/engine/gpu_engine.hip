@@ -145,11 +145,21 @@ struct WaveParProf : WavePar {
 template <class P, bool kSliced>
 __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   const uint32_t b = blockIdx.x;
-  // The configuration is read all over the model.  As a by-value kernel
-  // argument it lives in constant memory: every field is a scalar load into
-  // an SGPR (uniform, invariant across the epoch fences), not a vector load
-  // behind each acquire or an LDS round trip into a VGPR.
-  const SimCfg& c = *a.cfg_g;
+  // The configuration is read all over the model, much of it at lane-varying
+  // indices (address-decoder bit runs, per-unit counts, cache geometries
+  // selected per warp) that cannot be scalar loads: from HBM each is a vector
+  // load that misses the vector L1 after every epoch's acquire fence.  The
+  // block copies the configuration into LDS once and reads it from there
+  // (static global loads in this kernel 1031 -> 58; bfs engine time -3 %,
+  // profiles/pmc_sq_engine_bfs_r2.json).
+  {
+    static_assert(sizeof(SimCfg) % 8 == 0, "SimCfg must be 8-byte granular");
+    const uint2* src = reinterpret_cast<const uint2*>(a.cfg_g);
+    uint2* dst = reinterpret_cast<uint2*>(g_lds + kCfgOff);
+    for (int i = (int)(threadIdx.x & 63); i < (int)(sizeof(SimCfg) / 8); i += 64) dst[i] = src[i];
+    __syncthreads();
+  }
+  const SimCfg& c = *reinterpret_cast<const SimCfg*>(g_lds + kCfgOff);
   const uint64_t E = c.icnt_latency;
   SMState* s = reinterpret_cast<SMState*>(g_lds);
   ChanState* ch = reinterpret_cast<ChanState*>(g_lds);
