@@ -898,23 +898,44 @@ static void lane_addresses(const HostKernel& k, const TInst& in, uint64_t* out, 
 
 uint32_t smem_conflict_degree(const uint64_t* addr, uint64_t mask, uint32_t width, const SimCfg& c,
                               uint32_t ws) {
+  // Conflict degree of one shared-memory access: per part of the warp, the
+  // largest number of distinct 4-byte words that fall into one bank.  Called
+  // for every LDS instruction at ingest, so it works on fixed stack arrays:
+  // the part's words (<= 64 lanes x 4 words of a 16-byte access) are sorted
+  // and deduplicated, then counted per bank.
   const uint32_t nb = c.smem_banks ? c.smem_banks : 32;
   const uint32_t parts = c.smem_warp_parts ? c.smem_warp_parts : 1;
   const uint32_t per = (ws + parts - 1) / parts;
+  const uint64_t wb = width ? width : 4;
+  constexpr uint32_t kMaxBanks = 256, kMaxWords = 64 * 8;
   uint32_t total = 0;
   for (uint32_t p = 0; p < parts; ++p) {
-    // distinct 4-byte words per bank in this part of the warp
-    std::vector<std::vector<uint64_t>> words(nb);
-    for (uint32_t l = p * per; l < (p + 1) * per && l < ws; ++l) {
+    uint64_t words[kMaxWords];
+    uint32_t nw = 0;
+    bool fits = nb <= kMaxBanks;
+    for (uint32_t l = p * per; fits && l < (p + 1) * per && l < ws; ++l) {
       if (!(mask >> l & 1ull)) continue;
-      uint64_t w0 = addr[l] >> 2, w1 = (addr[l] + (width ? width : 4) - 1) >> 2;
-      for (uint64_t w = w0; w <= w1; ++w) {
-        auto& v = words[w % nb];
-        if (std::find(v.begin(), v.end(), w) == v.end()) v.push_back(w);
-      }
+      const uint64_t w0 = addr[l] >> 2, w1 = (addr[l] + wb - 1) >> 2;
+      if (w1 - w0 >= 8 || nw + (w1 - w0 + 1) > kMaxWords) { fits = false; break; }
+      for (uint64_t w = w0; w <= w1; ++w) words[nw++] = w;
     }
     uint32_t deg = 0;
-    for (auto& v : words) deg = std::max<uint32_t>(deg, (uint32_t)v.size());
+    if (fits) {
+      std::sort(words, words + nw);
+      const uint32_t nu = (uint32_t)(std::unique(words, words + nw) - words);
+      uint32_t cnt[kMaxBanks] = {};
+      for (uint32_t i = 0; i < nu; ++i) deg = std::max(deg, ++cnt[words[i] % nb]);
+    } else {  // very wide accesses or bank counts: the general path
+      std::vector<std::vector<uint64_t>> bw(nb);
+      for (uint32_t l = p * per; l < (p + 1) * per && l < ws; ++l) {
+        if (!(mask >> l & 1ull)) continue;
+        for (uint64_t w = addr[l] >> 2; w <= (addr[l] + wb - 1) >> 2; ++w) {
+          auto& v = bw[w % nb];
+          if (std::find(v.begin(), v.end(), w) == v.end()) v.push_back(w);
+        }
+      }
+      for (auto& v : bw) deg = std::max<uint32_t>(deg, (uint32_t)v.size());
+    }
     if (c.smem_limited_bcast) {
       // limited broadcast: duplicated words in a bank also serialize
       uint32_t lanes_max = 0;
@@ -943,6 +964,7 @@ ReadyKernel coalesce_kernel(const HostKernel& k, const SimCfg& c) {
   const uint64_t name_hash = std::hash<std::string>{}(k.h.name);
   std::vector<std::pair<uint64_t, uint8_t>> lines;
   std::vector<uint32_t> bytes;
+  std::vector<uint32_t> ord;
   for (auto& in : r.insts) {
     // latency / initiation interval from the config (per op class)
     if (in.flags & F_WAITCNT) continue;  // lat holds the s_waitcnt counts
@@ -1012,9 +1034,9 @@ ReadyKernel coalesce_kernel(const HostKernel& k, const SimCfg& c) {
         a = lend;
       }
     }
-    std::vector<size_t> ord(lines.size());
-    for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
-    std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return lines[x].first < lines[y].first; });
+    ord.resize(lines.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (uint32_t)i;
+    std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return lines[x].first < lines[y].first; });
     in.mem = (uint32_t)r.accs.size();
     uint32_t n = 0;
     for (size_t oi = 0; oi < ord.size() && n < (uint32_t)kMaxAccess; ++oi) {

@@ -80,6 +80,26 @@ def test_shared_bank_conflicts(native, qv100_args):
     assert native.smem_conflict_degree(col, full, 4, qv100_args) == 32
 
 
+def test_shared_bank_conflicts_random(native, qv100_args):
+    """The stack-array fast path agrees with the definition (max distinct
+    4-byte words per bank over the active lanes) on random patterns,
+    including multi-word accesses and partial masks."""
+    import random
+    rng = random.Random(7)
+    for _ in range(300):
+        width = rng.choice([1, 2, 4, 8, 16])
+        span = rng.choice([64, 256, 4096])
+        addr = [rng.randrange(0, span) * rng.choice([1, 4]) for _ in range(32)]
+        mask = rng.getrandbits(32) | 1
+        banks = {}
+        for l in range(32):
+            if mask >> l & 1:
+                for w in range(addr[l] >> 2, ((addr[l] + width - 1) >> 2) + 1):
+                    banks.setdefault(w % 32, set()).add(w)
+        want = max(len(v) for v in banks.values())
+        assert native.smem_conflict_degree(addr, mask, width, qv100_args) == want
+
+
 def test_coalescing(native, tmp_path, qv100_args):
     k = rodinia.vectoradd(n=64, block=64)
     p = str(tmp_path / "k.asimk")
