@@ -623,16 +623,9 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
     else if (ch.wmode && ch.qw_n < c.wq_lo) ch.wmode = 0;
     only = ch.wmode ? 1u : (ch.q_n > ch.qw_n ? 0u : 1u);
   }
-  // banks that have a queued row hit
-  uint64_t hitmask = P::vor(kDramQ, [&](int i) -> uint64_t {
-    if (!ch.q_valid[i]) return 0;
-    const DramReq& r = ch.q[i];
-    if (only != 2 && r.write != only) return 0;  // requests of the idle queue do not hold rows open
-    const DramBank& b = ch.bk[r.bank];
-    return (b.open && b.row == r.row) ? (1ull << r.bank) : 0ull;
-  });
   // ---- column command ----
   bool col = false;
+  uint32_t col_bank = 0;
   uint64_t oldest_age = ~0ull;
   if (c.dram_sched == 0) {  // FIFO: only the oldest request may issue (column and row commands)
     int o = P::argmin(kDramQ, [&](int i) -> uint64_t {
@@ -640,7 +633,8 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
     });
     oldest_age = o >= 0 ? ch.q_age[o] : ~0ull;
   }
-  {
+  // no column command can issue before tCCD has elapsed: skip the scan
+  if (t >= ch.t_ccd_ok) {
     int pick = P::argmin(kDramQ, [&](int i) -> uint64_t {
       if (!ch.q_valid[i]) return ~0ull;
       if (c.dram_sched == 0 && ch.q_age[i] != oldest_age) return ~0ull;
@@ -681,10 +675,21 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
       ch.qw_n -= r.write ? 1 : 0;
       ch.sp[r.sub].n_l2dram--;
       col = true;
+      col_bank = r.bank;
     }
   }
   // ---- row command (dual bus: in the same cycle) ----
   if (col && !c.dual_bus) return;
+  // banks that had a queued row hit at the start of the cycle (only FR-FCFS
+  // consults them): the column command above removed one row-hit request and
+  // changed no bank's open row, so its bank is added back
+  const uint64_t hitmask = c.dram_sched == 0 ? 0ull : (P::vor(kDramQ, [&](int i) -> uint64_t {
+    if (!ch.q_valid[i]) return 0;
+    const DramReq& r = ch.q[i];
+    if (only != 2 && r.write != only) return 0;  // requests of the idle queue do not hold rows open
+    const DramBank& b = ch.bk[r.bank];
+    return (b.open && b.row == r.row) ? (1ull << r.bank) : 0ull;
+  }) | (col ? 1ull << col_bank : 0ull));
   int act = P::argmin(kDramQ, [&](int i) -> uint64_t {
     if (!ch.q_valid[i]) return ~0ull;
     if (c.dram_sched == 0 && ch.q_age[i] != oldest_age) return ~0ull;
