@@ -920,12 +920,29 @@ uint32_t smem_conflict_degree(const uint64_t* addr, uint64_t mask, uint32_t widt
       for (uint64_t w = w0; w <= w1; ++w) words[nw++] = w;
     }
     uint32_t deg = 0;
+    if (fits && nw > 0 && nb <= 64) {
+      // common patterns first: every word in its own bank, or one word
+      // broadcast to every lane -- degree 1 with no sort
+      uint64_t seen = 0;
+      bool distinct = true, same = true;
+      for (uint32_t i = 0; i < nw; ++i) {
+        const uint64_t bit = 1ull << (words[i] % nb);
+        distinct = distinct && !(seen & bit);
+        seen |= bit;
+        same = same && words[i] == words[0];
+      }
+      if (distinct || same) {
+        deg = 1;
+        fits = false;  // done: skip the sort below
+        nw = 0;
+      }
+    }
     if (fits) {
       std::sort(words, words + nw);
       const uint32_t nu = (uint32_t)(std::unique(words, words + nw) - words);
       uint32_t cnt[kMaxBanks] = {};
       for (uint32_t i = 0; i < nu; ++i) deg = std::max(deg, ++cnt[words[i] % nb]);
-    } else {  // very wide accesses or bank counts: the general path
+    } else if (deg == 0) {  // very wide accesses or bank counts: the general path
       std::vector<std::vector<uint64_t>> bw(nb);
       for (uint32_t l = p * per; l < (p + 1) * per && l < ws; ++l) {
         if (!(mask >> l & 1ull)) continue;
