@@ -297,6 +297,9 @@ def _pre_volta_common() -> Dict[str, str]:
     c = _volta_common()
     for k in [k for k in c if k.startswith("-specialized_unit_") or "_spec_op_" in k]:
         del c[k]
+    # the pre-Volta tested configs leave the crossbar buffers at their defaults
+    for k in ("-icnt_in_buffer_limit", "-icnt_out_buffer_limit"):
+        c.pop(k, None)
     c.update({
         "-gpgpu_ignore_resources_limitation": "1",
         "-gpgpu_kernel_launch_latency": "0",

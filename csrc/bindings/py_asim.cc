@@ -106,6 +106,10 @@ py::dict cfg_dict(const SimCfg& c) {
   for (int i = 0; i < U_COUNT; ++i) units.append(c.unit_count[i]);
   d["unit_count"] = units;
   d["kernel_launch_latency"] = c.kernel_launch_latency;
+  d["eject_buf"] = c.eject_buf;
+  d["ldst_resp_buf"] = c.ldst_resp_buf;
+  d["icnt_in_pkts"] = c.icnt_in_pkts;
+  d["icnt_out_limit"] = c.icnt_out_limit;
   return d;
 }
 
@@ -178,6 +182,12 @@ PYBIND11_MODULE(_asim, m) {
     register_sim_options(r);
     return r.names();
   });
+  m.def("unmodelled_option_warnings", [](const std::vector<std::string>& args) {
+    OptionRegistry r;
+    register_sim_options(r);
+    r.parse_cmdline(args, false);
+    return unmodelled_option_warnings(r);
+  }, "warnings for options that are accepted but have no effect");
   m.def("parse_config", [](const std::vector<std::string>& args) { return cfg_dict(cfg_from_args(args)); },
         "derive the model configuration from accel-sim style arguments");
   m.def("addr_decode", [](const std::vector<std::string>& args, uint64_t addr) {

@@ -563,6 +563,76 @@ static std::string resolve_cfg_path(const OptionRegistry& r, const std::string& 
   return f;
 }
 
+namespace {
+// why an accepted option has no effect here
+struct Unmodelled {
+  const char* name;  // exact name, or a prefix ending in '*'
+  const char* why;
+  const char* same;  // a value that leaves the modelled behaviour unchanged (no message), or null
+};
+const char* const kPtxOnly = "PTX (execution-driven) mode only; this is a trace-driven simulator";
+const char* const kNotModelled = "accepted for config compatibility, not modelled";
+const char* const kPtxLat = "PTX-mode latencies; trace mode times instructions with -trace_opcode_latency_initiation_*";
+const char* const kCoalesce = "the trace-ingest coalescer always applies the sectored (sm_70+) rules";
+const Unmodelled kUnmodelled[] = {
+    {"-gpgpu_ptx_*", kPtxOnly}, {"-save_embedded_ptx", kPtxOnly}, {"-keep", kPtxOnly},
+    {"-enable_ptx_file_line_stats", kPtxOnly}, {"-ptx_line_stats_filename", kPtxOnly},
+    {"-gpgpu_experimental_lib_support", kPtxOnly}, {"-gpgpu_cdp_enabled", kPtxOnly}, {"-cdp_latency", kPtxOnly},
+    {"-gpgpu_compute_capability_major", kPtxOnly}, {"-gpgpu_compute_capability_minor", kPtxOnly},
+    {"-gpgpu_stack_size_limit", kPtxOnly}, {"-gpgpu_heap_size_limit", kPtxOnly},
+    {"-gpgpu_runtime_sync_depth_limit", kPtxOnly}, {"-gpgpu_runtime_pending_launch_count_limit", kPtxOnly},
+    {"-checkpoint_CTA", kPtxOnly}, {"-resume_CTA", kPtxOnly}, {"-checkpoint_CTA_t", kPtxOnly},
+    {"-checkpoint_insn_Y", kPtxOnly}, {"-gpgpu_occupancy_sm_number", kPtxOnly},
+    {"-ptx_opcode_latency_*", kPtxLat}, {"-ptx_opcode_initiation_*", kPtxLat},
+    {"-gpgpu_coalesce_arch", kCoalesce},
+    {"-gpgpu_simd_model", kNotModelled},
+    {"-gpgpu_reg_bank_use_warp_id", "the reference ignores it too: register banks always include the warp id (shader.cc:4141-4144)"},
+    {"-gpgpu_mem_unit_ports", kNotModelled}, {"-gpgpu_num_mem_units", "one LD/ST unit per SM"},
+    {"-gpgpu_operand_collector_num_in_ports_*", "collector ports are not a separate resource here"},
+    {"-gpgpu_operand_collector_num_out_ports_*", "collector ports are not a separate resource here"},
+    {"-gpgpu_tex_cache:l1", "texture path not modelled (no texture instructions in CDNA traces)"},
+    {"-gpgpu_const_cache:l1", "constant loads go through the L1D / scalar-cache path"},
+    {"-gpgpu_l1_banks_byte_interleaving", kNotModelled}, {"-gpgpu_l1_banks_hashing_function", kNotModelled},
+    {"-gpgpu_cache:dl2_texture_only", kNotModelled, "0"}, {"-l2_ideal", kNotModelled},
+    {"-icnt_out_buffer_limit", kNotModelled}, {"-icnt_subnets", "the crossbar always has separate request / reply subnets"},
+    {"-icnt_verbose", kNotModelled}, {"-gpgpu_clock_gated_reg_file", kNotModelled},
+    {"-gpgpu_clock_gated_lanes", kNotModelled}, {"-n_regfile_gating_group", kNotModelled},
+    {"-gpgpu_registers_per_block", kPtxOnly}, {"-gpgpu_ignore_resources_limitation", kNotModelled},
+    {"-gpgpu_num_cta_barriers", kNotModelled}, {"-gpgpu_shmem_sizeDefault", kNotModelled},
+    {"-gpgpu_shmem_size_PrefL1", kNotModelled}, {"-gpgpu_shmem_size_PrefShared", kNotModelled},
+    {"-gpgpu_cache:dl1PrefL1", kNotModelled}, {"-gpgpu_cache:dl1PrefShared", kNotModelled},
+    {"-gpgpu_warpdistro_shader", kNotModelled}, {"-gpgpu_warp_issue_shader", kNotModelled},
+    {"-gpgpu_local_mem_map", kNotModelled}, {"-gpgpu_simt_core_sim_order", kNotModelled},
+    {"-power_per_cycle_dump", kNotModelled}, {"-aggregate_power_stats", kNotModelled},
+    {"-power_trace_zlevel", kNotModelled}, {"-visualizer_zlevel", kNotModelled}, {"-gpgpu_cflog_interval", kNotModelled},
+    {"-liveness_message_freq", kNotModelled}, {"-gpgpu_mem_addr_test", kNotModelled},
+};
+bool unmodelled_match(const char* pat, const std::string& name) {
+  const size_t n = strlen(pat);
+  if (n && pat[n - 1] == '*') return name.compare(0, n - 1, pat, n - 1) == 0;
+  return name == pat;
+}
+}  // namespace
+
+std::vector<std::string> unmodelled_option_warnings(const OptionRegistry& r) {
+  std::vector<std::string> out;
+  for (const auto& kv : r.user_values()) {
+    const OptionRegistry::Opt* o = r.find(kv.first);
+    if (!o || o->value == o->deflt) continue;
+    // the default carve-out only differs from -gpgpu_shmem_size when set apart
+    if (kv.first == "-gpgpu_shmem_sizeDefault" && r.getu(kv.first) == r.getu("-gpgpu_shmem_size")) continue;
+    for (const Unmodelled& u : kUnmodelled)
+      if (unmodelled_match(u.name, kv.first)) {
+        if (u.same && kv.second == u.same) break;
+        const bool note = u.why == kPtxOnly || u.why == kPtxLat || u.why == kCoalesce;
+        out.push_back(std::string(note ? "note: option " : "WARNING option ") + kv.first + " " + kv.second + ": " +
+                      u.why);
+        break;
+      }
+  }
+  return out;
+}
+
 SimCfg derive_sim_cfg(const OptionRegistry& r) {
   SimCfg c;
   memset(&c, 0, sizeof(c));
@@ -726,6 +796,8 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   }
   c.icnt_out_limit = std::min<uint32_t>((uint32_t)r.getu("-sim_max_outstanding_pkts"), kInQ);
   if (c.icnt_out_limit == 0) c.icnt_out_limit = 1;
+  c.eject_buf = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)r.getu("-gpgpu_n_cluster_ejection_buffer_size"), kEjectQ));
+  c.ldst_resp_buf = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)r.getu("-gpgpu_n_ldst_response_buffer_size"), kLdstRespQ));
   // memory partition
   c.l2 = parse_cache_geom(r.gets("-gpgpu_cache:dl2"));
   if (!c.l2.disabled && (uint64_t)c.l2.nsets * c.l2.assoc > (uint64_t)kMaxL2Lines)

@@ -17,6 +17,12 @@ namespace asim {
 // accepted and ignored, as tested configs still carry them.
 void register_sim_options(OptionRegistry& r);
 
+// Options that are accepted for config-file compatibility but change nothing
+// in this simulator, set by the user to a value other than their default: one
+// message per option, naming why (PTX-mode only, not modelled, ...).  The
+// driver prints them as warnings so a config never silently loses an effect.
+std::vector<std::string> unmodelled_option_warnings(const OptionRegistry& r);
+
 // Derive the model configuration.  Throws OptionError on malformed composite
 // strings or configurations beyond the compiled capacity caps.
 SimCfg derive_sim_cfg(const OptionRegistry& r);

@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstring>
+#include <filesystem>
 #include <stdexcept>
 
 namespace asim {
@@ -31,6 +32,7 @@ Simulator::Simulator(const std::vector<std::string>& args) {
   reg_.parse_cmdline(args, false);
   cfg_ = derive_sim_cfg(reg_);
   dopt_ = derive_driver_opts(reg_);
+  for (const std::string& w : unmodelled_option_warnings(reg_)) print("GPGPU-Sim: %s\n", w.c_str());
   if (dopt_.engine == "gpu") {
     eng_ = make_gpu_engine();
     if (!eng_) throw std::runtime_error("-sim_engine gpu requested but the HIP engine is unavailable");
@@ -139,6 +141,7 @@ size_t Simulator::kernels_in_window() const {
 // any kind; with concurrent kernels it bounds the kernels, and collectives /
 // events ride along in trace order.
 void Simulator::admit(size_t end) {
+  bool admitted = false;  // a windowed operation entered the window in this pass
   while (next_cmd_ < end) {
     const Command& c = cmds_[next_cmd_];
     const bool windowed = c.type == CMD_KERNEL || c.type == CMD_COLLECTIVE || c.type == CMD_EVENT_RECORD ||
@@ -147,8 +150,17 @@ void Simulator::admit(size_t end) {
       const bool full = dopt_.concurrent_kernel_sm ? (c.type == CMD_KERNEL && kernels_in_window() >= window_size())
                                                    : win_.size() >= window_size();
       if (full) break;
+    } else if (c.type == CMD_MEMCPY_HTOD || c.type == CMD_MEMCPY_DTOH) {
+      // A memcpy behind a kernel is reached only after the engine has run
+      // (reference main.cc:83-161: each pass of the command loop admits one
+      // group, then simulates until a kernel completes): serially it waits
+      // for the window to drain, with concurrent kernels for the next
+      // completion.  Applying it earlier would pre-fill the L2 under a kernel
+      // that has not been simulated yet.
+      if (dopt_.concurrent_kernel_sm ? admitted : !win_.empty()) break;
     }
     const size_t i = next_cmd_++;
+    if (windowed) admitted = true;
     if (c.type == CMD_KERNEL) {
       admit_kernel(i);
       win_.back()->queued = last_cmd_kernel_;
@@ -232,8 +244,11 @@ void Simulator::write_checkpoint(size_t cmd_index) {
   h.n_sm_stats = prev_sm_.size();
   h.n_mem_stats = prev_mem_.size();
   h.engine_bytes = eng.size();
-  std::string cmd = "mkdir -p '" + dopt_.checkpoint_dir + "'";
-  if (system(cmd.c_str()) != 0) throw std::runtime_error("cannot create " + dopt_.checkpoint_dir);
+  {
+    std::error_code ec;
+    std::filesystem::create_directories(dopt_.checkpoint_dir, ec);
+    if (ec) throw std::runtime_error("cannot create " + dopt_.checkpoint_dir + ": " + ec.message());
+  }
   const std::string path = checkpoint_file(kernels_done_);
   FILE* f = fopen(path.c_str(), "wb");
   if (!f) throw std::runtime_error("cannot write checkpoint " + path);
@@ -1054,9 +1069,7 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
       pre += m.dram_pre;
       evd += m.l2_evict_dirty;
     }
-    print("gpu_stall_dramfull = %llu\n", (unsigned long long)(l2[L2T_RD][L2O_RES_FAIL] + l2[L2T_WR][L2O_RES_FAIL] +
-                                                              l2[L2T_ATOM][L2O_RES_FAIL]));
-    print("gpu_stall_icnt2sh = %llu\n", (unsigned long long)icst);
+    (void)icst;  // gpu_stall_dramfull / gpu_stall_icnt2sh are printed once, with the L2 bank lines
     print("L2_cache_dirty_evictions = %llu\n", (unsigned long long)evd);
     print("L2_busy_rate = %.4f\n", l2cyc ? (double)l2busy / (double)l2cyc : 0.0);
     print("avg_rop_queue_occupancy = %.4f\n", l2cyc ? (double)rop / (double)l2cyc : 0.0);

@@ -250,6 +250,12 @@ struct SmView {
   SV_REF(inq);
   SV_VAL(inq_head);
   SV_VAL(inq_n);
+  SV_REF(rsp_cl);
+  SV_REF(rsp_ld);
+  SV_VAL(cl_head);
+  SV_VAL(cl_n);
+  SV_VAL(ld_head);
+  SV_VAL(ld_n);
   SV_REF(skey);
   SV_REF(sref);
   SV_REF(srank);
@@ -278,7 +284,7 @@ struct SmView {
 #define SV_SCALARS(X)                                                                                   \
   X(id) X(last_progress) X(epoch_end) X(out_port_free) X(age_ctr) X(n_cta_active)    \
   X(n_warps_live) X(live_mask) X(n_wait_flags) X(fetch_rr) X(n_pend) X(idoc_mask) X(oc_mask) X(oc_read_mask)         \
-  X(l1_stamp) X(skipped_cycles) X(min_emit) X(outq_head) X(outq_n) X(outstanding) X(inq_head) X(inq_n)
+  X(l1_stamp) X(skipped_cycles) X(min_emit) X(outq_head) X(outq_n) X(outstanding) X(inq_head) X(inq_n) X(cl_head) X(cl_n) X(ld_head) X(ld_n)
 #define SV_WARPS(X) \
   X(w_next) X(w_end) X(w_head) X(w_age) X(w_flags) X(w_ibuf) X(w_cta) X(w_inflight) X(w_stores) X(w_loads) X(w_slot_used) \
   X(idoc_meta) X(oc_info) X(oc_banks) X(oc_age) X(fu_next) X(wb_occ) X(hit_occ) X(cta_valid) X(cta_live) X(cta_bar) \
@@ -294,7 +300,7 @@ struct SmView {
         idoc_inst(b.idoc_inst), oc_inst(b.oc_inst),
         wb_cnt(b.wb_cnt), wb(b.wb), hit_cnt(b.hit_cnt), hit(b.hit), l1(b.l1), mshr(b.mshr),
         pend(b.pend), il1(b.il1), imshr(b.imshr),
-        outq(b.outq), ocnt(b.ocnt), inq(b.inq), skey(b.skey), sref(b.sref), srank(b.srank) {
+        outq(b.outq), ocnt(b.ocnt), inq(b.inq), rsp_cl(b.rsp_cl), rsp_ld(b.rsp_ld), skey(b.skey), sref(b.sref), srank(b.srank) {
 #define SV_LD(m) m = sv_uni(b.m);
     SV_SCALARS(SV_LD)
 #undef SV_LD

@@ -32,6 +32,8 @@ constexpr int kHitRing = 256;       // L1 / shared-memory completion ring (laten
 constexpr int kHitSlot = 8;
 constexpr int kOutQ = 64;           // SM -> icnt injection queue
 constexpr int kInQ = 128;           // icnt -> SM arrivals per epoch
+constexpr int kEjectQ = 32;         // cluster ejection buffer (-gpgpu_n_cluster_ejection_buffer_size cap)
+constexpr int kLdstRespQ = 8;       // LD/ST response FIFO (-gpgpu_n_ldst_response_buffer_size cap)
 constexpr int kMaxAccess = 64;      // coalesced accesses of one instruction
 // memory side (per sub-partition)
 constexpr int kMaxL2Lines = 1024;   // per sub-partition
@@ -175,6 +177,12 @@ struct SimCfg {
   uint32_t icnt_arbiter, icnt_grant_cycles;
   uint32_t icnt_in_pkts;  // SM injection buffer (-icnt_in_buffer_limit flits) in max-size packets
   uint32_t icnt_out_limit; // per-SM outstanding packets before injection stalls
+  // reply path into the SM (reference simt_core_cluster::icnt_cycle and
+  // ldst_unit::cycle, shader.cc:4623-4660, 2302-2309, 2810-2857): packets
+  // leave the crossbar into the cluster's ejection buffer, move to the LD/ST
+  // unit's response FIFO, and are consumed there one per cycle
+  uint32_t eject_buf;      // -gpgpu_n_cluster_ejection_buffer_size (packets)
+  uint32_t ldst_resp_buf;  // -gpgpu_n_ldst_response_buffer_size (packets)
   // -network_mode 1 (intersim2 / Booksim topologies, reference
   // icnt_wrapper.cc:35-45 + intersim2/networks/*): per-pair latency from the
   // topology's hop count and the router pipeline; icnt_latency above is then

@@ -12,6 +12,10 @@
 // (mshr_table, gpu-cache.h:1019).
 #pragma once
 #include <stddef.h>
+#if !defined(__HIP_DEVICE_COMPILE__)
+#include <stdexcept>
+#include <stdio.h>
+#endif
 
 #include "addrdec.h"
 
@@ -230,6 +234,10 @@ struct alignas(16) SMState {
   uint32_t ocnt[kMaxSubTot]; // packets put into each destination's outbox cell this epoch
   Pkt inq[kInQ];
   uint32_t inq_head, inq_n;
+  // reply path: cluster ejection buffer -> LD/ST response FIFO (sm_receive)
+  Pkt rsp_cl[kEjectQ];
+  Pkt rsp_ld[kLdstRespQ];
+  uint32_t cl_head, cl_n, ld_head, ld_n;
   uint64_t skey[kInQ];       // gather scratch
   uint32_t sref[kInQ];
   uint32_t srank[kInQ > kMaxSubTot ? kInQ : kMaxSubTot];
@@ -699,15 +707,44 @@ SIM_HDI Pkt xbar_take(Q& q, uint32_t& head, uint32_t& n, uint32_t cap, uint32_t 
   return p;
 }
 
-// consume at most one arrived packet per cycle (response FIFO; the SM is the
-// reply network's output port)
+// The reply path into the SM, one step per core cycle in the reference's
+// order (simt_core_cluster::icnt_cycle runs before the core, shader.cc:4623-4660;
+// ldst_unit::cycle consumes its response FIFO, shader.cc:2810-2857):
+//   1. the head of the cluster ejection buffer moves to the LD/ST response
+//      FIFO if that has room (an instruction-cache fill goes to the fetch
+//      unit at once: accept_fetch_response);
+//   2. one packet that reached the SM's crossbar output port is ejected into
+//      the cluster buffer if it is not full (otherwise it waits in the port);
+//   3. the LD/ST unit consumes the head of its response FIFO: store ack,
+//      bypass / atomic load completion, or L1 fill.  A fill may evict a dirty
+//      line whose write-back needs an injection-queue entry: with that queue
+//      full the fill waits (like the reference's fill-port reservation)
+//      instead of dropping the write-back.
 template <class P, class S>
 SIM_HDI void sm_receive(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
-  if (P::uni(s.inq_n) == 0) return;
-  if (P::uni(s.inq[P::uni(s.inq_head)].t) > now * c.per_core) return;
-  Pkt q;
-  {
+  // 1. cluster buffer -> LD/ST response FIFO
+  if (P::uni(s.cl_n)) {
+    const uint32_t ch = P::uni(s.cl_head);
+    const Pkt& h = s.rsp_cl[ch];
+    const bool ifill = (P::uni(h.tag) & 0xc0000000u) == 0x40000000u && P::uni(h.type) != P_WR_ACK;
+    if (ifill) {
+      il1_fill<P>(s, c, P::uni(h.addr));
+      s.cl_head = (ch + 1) % kEjectQ;
+      s.cl_n = P::uni(s.cl_n) - 1;
+    } else if (P::uni(s.ld_n) < c.ldst_resp_buf) {
+      const uint32_t li = (P::uni(s.ld_head) + P::uni(s.ld_n)) % kLdstRespQ;
+      const Pkt v = P::uni(h);
+      P::one([&] { s.rsp_ld[li] = v; });
+      s.ld_n = P::uni(s.ld_n) + 1;
+      s.cl_head = (ch + 1) % kEjectQ;
+      s.cl_n = P::uni(s.cl_n) - 1;
+    }
+  }
+  // 2. crossbar output port -> cluster ejection buffer
+  if (P::uni(s.inq_n) && P::uni(s.cl_n) < c.eject_buf &&
+      P::uni(s.inq[P::uni(s.inq_head)].t) <= now * c.per_core) {
+    Pkt q;
     uint32_t head = P::uni(s.inq_head), n = P::uni(s.inq_n);
     uint16_t an = s.arb_next, ac = s.arb_cnt;
     const XbarGrant g = xbar_pick<P>(s.inq, head, n, kInQ, now * c.per_core, c, now * c.per_core / c.per_icnt,
@@ -719,19 +756,27 @@ SIM_HDI void sm_receive(S& s, const SmCtx& x, uint64_t now) {
     s.sadd(SK(icnt_reply_queue_cycles), (now * c.per_core - q.t) / c.per_icnt);
     s.inq_head = head;
     s.inq_n = n;
+    if (trace_sm_on(c, TS_INTERCONNECT, s.id)) P::one([&] { trace_put(c, s.id, now, EV_PKT_RECV, q.type, q.addr); });
+    s.outstanding--;
+    s.sadd(SK(pkts_in), 1);
+    s.sadd(SK(bytes_in), q.size);
+    const uint32_t ci = (P::uni(s.cl_head) + P::uni(s.cl_n)) % kEjectQ;
+    P::one([&] { s.rsp_cl[ci] = q; });
+    s.cl_n = P::uni(s.cl_n) + 1;
   }
-  if (trace_sm_on(c, TS_INTERCONNECT, s.id)) P::one([&] { trace_put(c, s.id, now, EV_PKT_RECV, q.type, q.addr); });
-  s.outstanding--;
-  s.sadd(SK(pkts_in), 1);
-  s.sadd(SK(bytes_in), q.size);
+  // 3. the LD/ST unit consumes one response
+  if (!P::uni(s.ld_n)) return;
+  if (P::uni(s.outq_n) >= (uint32_t)kOutQ) return;
+  const uint32_t lh = P::uni(s.ld_head);
+  const Pkt q = P::uni(s.rsp_ld[lh]);
+  s.ld_head = (lh + 1) % kLdstRespQ;
+  s.ld_n = P::uni(s.ld_n) - 1;
   if (q.type == P_WR_ACK) {
     if (!(q.tag & kTagL1Writeback)) {
       uint32_t w = q.tag & 0xff;
       s.w_stores[w]--;
     }
     s.last_progress = now;
-  } else if ((q.tag & 0xc0000000u) == 0x40000000u) {  // instruction-cache fill
-    il1_fill<P>(s, c, q.addr);
   } else if (q.tag & 0x80000000u) {  // direct (bypass / atomic) load access
     uint32_t w = q.tag & 0xff, sl = (q.tag >> 8) & 0xff;
     if (--s.w_slot_pend[w][sl] == 0) sm_load_slot_done(s, w, sl, now);
@@ -1398,6 +1443,14 @@ SIM_HDI void sm_fetch(S& s, const SimCfg& c, const KernelTab& kt) {
   }
 }
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+[[noreturn]] inline void throw_cta_fit_error(uint32_t sm, uint32_t cta) {
+  char b[128];
+  snprintf(b, sizeof(b), "SM %u: no contiguous warp run for CTA %u (dispatch plan out of date)", sm, cta);
+  throw std::logic_error(b);
+}
+#endif
+
 // first warp of a free contiguous run of n warps among the first nw, or -1
 // (shader_core_ctx::find_available_hwtid: a CTA's hardware threads are contiguous)
 SIM_HDI int warp_run_fit(uint64_t used, uint32_t n, uint32_t nw) {
@@ -1482,7 +1535,16 @@ SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id,
   const SimCfg& c = *x.cfg;
   const uint32_t wpc = k.warps_per_cta;
   const uint32_t nwm = amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
-  const uint32_t base = (uint32_t)warp_run_fit(s.cta_wmask, wpc, nwm);  // checked by sm_cta_fit
+  const int fit = warp_run_fit(s.cta_wmask, wpc, nwm);  // planned by sm_cta_fit at the last boundary
+  if (fit < 0) {
+    // the plan no longer matches the SM (cannot happen while the kernel table
+    // and the SM state evolve together); never index warps with -1
+#if !defined(__HIP_DEVICE_COMPILE__)
+    throw_cta_fit_error(s.id, cta_id);
+#endif
+    return;
+  }
+  const uint32_t base = (uint32_t)fit;
   const uint64_t wm = (wpc >= 64 ? ~0ull : ((1ull << wpc) - 1)) << base;
   if (s.n_cta_active == 0) {
     // an empty SM takes the kernel's L1 / shared-memory carve-out
@@ -1568,7 +1630,7 @@ SIM_HDI void sm_cycle(S& s, const SmCtx& x, uint64_t now) {
 // true if the SM holds no work at all (no CTAs, nothing in flight)
 template <class S>
 SIM_HDI bool sm_idle(const S& s) {
-  return s.n_cta_active == 0 && s.outq_n == 0 && s.outstanding == 0 && !s.ldst.busy;
+  return s.n_cta_active == 0 && s.outq_n == 0 && s.outstanding == 0 && !s.ldst.busy && s.cl_n == 0 && s.ld_n == 0;
 }
 
 // first cycle in [from, limit) whose slot of a time-indexed ring is occupied:
@@ -1599,7 +1661,9 @@ SIM_HDI uint64_t ring_next(const A& occ, uint32_t ring, uint64_t from, uint64_t 
 // (every warp waiting on memory) cost one check instead of one cycle each.
 template <class P, class S>
 SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, const KernelTab& kt, uint64_t t, uint64_t limit) {
-  if (P::uni(s.ldst.busy) || P::uni(s.idoc_mask) || P::uni(s.oc_mask | s.oc_read_mask) || P::uni(s.outq_n)) return t;
+  if (P::uni(s.ldst.busy) || P::uni(s.idoc_mask) || P::uni(s.oc_mask | s.oc_read_mask) || P::uni(s.outq_n) ||
+      P::uni(s.cl_n | s.ld_n))
+    return t;
   uint64_t nx = ring_next<P>(s.wb_occ, kWbRing, t, limit);
   if (nx == t) return t;
   nx = ring_next<P>(s.hit_occ, kHitRing, t, nx);

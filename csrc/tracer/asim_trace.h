@@ -28,6 +28,7 @@
 // version 950) plus kernelslist.g, ready for the simulator or for
 // conversion to the binary .asimk format.
 #pragma once
+#include <filesystem>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -227,8 +228,11 @@ struct Session {
     if (d && *d) {
       dir = d;
       enabled = true;
-      std::string cmd = "mkdir -p '" + dir + "'";
-      if (system(cmd.c_str()) != 0) fprintf(stderr, "asim_trace: cannot create %s\n", d);
+      {
+        std::error_code ec;
+        std::filesystem::create_directories(dir, ec);
+        if (ec) fprintf(stderr, "asim_trace: cannot create %s\n", d);
+      }
       FILE* f = fopen((dir + "/kernelslist.g").c_str(), "w");
       if (f) fclose(f);
       f = fopen((dir + "/stats.csv").c_str(), "w");

@@ -15,6 +15,7 @@
 //    kernel-N.traceg files plus MemcpyHtoD lines in kernelslist.g;
 //  * kernel-range filtering (ASIM_TRACE_KERNEL_START/END) and a device filter
 //    (ASIM_TRACE_GPU = agent node id).
+#include <filesystem>
 #include <dlfcn.h>
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
@@ -232,8 +233,11 @@ extern "C" rocprofiler_tool_configure_result_t* rocprofiler_configure(uint32_t, 
   if (const char* s = getenv("ASIM_TRACE_TOOL_LIST")) g_tool->full_list = atoi(s) != 0;
   if (const char* s = getenv("ASIM_TRACE_KERNEL_START")) g_tool->kstart = atol(s);
   if (const char* s = getenv("ASIM_TRACE_KERNEL_END")) g_tool->kend = atol(s);
-  std::string cmd = "mkdir -p '" + g_tool->dir + "'";
-  if (system(cmd.c_str()) != 0) fprintf(stderr, "asim_tracer: cannot create %s\n", g_tool->dir.c_str());
+  {
+    std::error_code ec;
+    std::filesystem::create_directories(g_tool->dir, ec);
+    if (ec) fprintf(stderr, "asim_tracer: cannot create %s\n", g_tool->dir.c_str());
+  }
   g_tool->line("dispatches.csv", "id,kernel,grid_x,grid_y,grid_z,wg_x,wg_y,wg_z,lds,scratch,vgpr,agpr,sgpr,dispatch_id");
   static rocprofiler_tool_configure_result_t cfg{sizeof(rocprofiler_tool_configure_result_t), &tool_init, &tool_fini,
                                                  nullptr};

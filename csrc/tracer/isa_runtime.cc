@@ -21,6 +21,7 @@
 // Environment: ASIM_TRACE_DIR (enables tracing), ASIM_TRACE_KERNEL_START/END
 // (1-based launch range), ASIM_TRACE_BUF_MB (device buffer, default 4096),
 // ASIM_ISA_MAP (map path, default <exe>.asimisa).
+#include <filesystem>
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <unistd.h>
@@ -95,9 +96,16 @@ struct Tracer {
     if (!d || !*d) return;
     enabled = true;
     dir = d;
-    std::string cmd = "mkdir -p '" + dir + "'";
-    if (system(cmd.c_str()) != 0) fprintf(stderr, "asim isa tracer: cannot create %s\n", d);
-    fclose(fopen((dir + "/kernelslist.g").c_str(), "w"));
+    std::error_code ec;
+    std::filesystem::create_directories(dir, ec);
+    FILE* kl = fopen((dir + "/kernelslist.g").c_str(), "w");
+    if (!kl) {
+      fprintf(stderr, "asim isa tracer: cannot write %s/kernelslist.g (%s); tracing disabled\n", d,
+              ec ? ec.message().c_str() : "open failed");
+      enabled = false;
+      return;
+    }
+    fclose(kl);
     FILE* f = fopen((dir + "/stats.csv").c_str(), "w");
     if (f) {
       fprintf(f, "kernel id, kernel name, grid_dim, block_dim, #warp insts, #thread insts\n");

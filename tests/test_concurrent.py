@@ -161,3 +161,30 @@ def test_trace_prefetch_does_not_change_results(native, tmp_path):
     on = _run(native, kl, False, {"-trace_prefetch": "1"})
     off = _run(native, kl, False, {"-trace_prefetch": "0"})
     assert on.tot_cycle == off.tot_cycle and on.tot_insn == off.tot_insn
+
+
+def _first_stat(out, key):
+    import re
+    m = re.findall(rf"{re.escape(key)} = ([0-9.]+)", out)
+    return float(m[0]) if m else None
+
+
+def test_memcpy_behind_kernel_waits_for_it(native, tmp_path):
+    """A MemcpyHtoD that follows a kernel in the command list pre-fills the L2
+    only after that kernel has been simulated (reference main.cc:83-161 reaches
+    the memcpy on the next pass of the command loop).  Kernel 1 reads region R
+    cold; the memcpy of R behind it must not turn those reads into L2 hits."""
+    region = BASE + 1 * (1 << 22)
+    memcpy = f"MemcpyHtoD,0x{region:016x},{1 << 20}"
+    kl = _app(tmp_path, "km", [_kernel(1, 0, ctas=4, alu=20), _kernel(2, 0, ctas=4, alu=20)],
+              extra_cmds=[(1, memcpy)])
+    # reference: the same two kernels with no memcpy at all -> kernel 1 cold
+    kl0 = _app(tmp_path, "k0", [_kernel(1, 0, ctas=4, alu=20), _kernel(2, 0, ctas=4, alu=20)])
+    for conc in (False, True):
+        with_cp = _run(native, kl, conc, {"-gpgpu_perf_sim_memcpy": "1"})
+        without = _run(native, kl0, conc, {"-gpgpu_perf_sim_memcpy": "1"})
+        key = "L2_cache_stats_breakdown[GLOBAL_ACC_R][HIT]"
+        assert _first_stat(with_cp.output, key) == _first_stat(without.output, key)
+        assert with_cp.kernels[0]["cycles"] == without.kernels[0]["cycles"]
+        # the memcpy lands before kernel 2: its reads of R now hit in the L2
+        assert "launching memcpy command" in with_cp.output

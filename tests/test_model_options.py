@@ -254,3 +254,34 @@ def test_warp_issue_interval(native, tmp_path):
         cyc[iv] = int(re.findall(r"^gpu_sim_cycle = (\d+)", s.output, re.M)[-1])
     # 256 independent instructions: ~3 extra cycles each
     assert cyc[4] - cyc[1] >= 256 * 2
+
+
+def test_reply_path_buffers(native, traces):
+    """Cluster ejection buffer and LD/ST response FIFO (reference
+    simt_core_cluster::icnt_cycle, shader.cc:4623-4660; ldst_unit response
+    FIFO, shader.cc:2302-2309,2810-2857): the flags size the two queues every
+    reply passes (one extra cycle between the crossbar port and the L1 fill,
+    as in the reference's icnt_cycle -> ldst_unit::cycle order); with room for
+    one packet each the path still moves one reply per cycle."""
+    cfg = native.parse_config(presets.args_for("QV100", {"-gpgpu_n_cluster_ejection_buffer_size": "3",
+                                                          "-gpgpu_n_ldst_response_buffer_size": "1"}))
+    assert (cfg["eject_buf"], cfg["ldst_resp_buf"]) == (3, 1)
+    base = _run(native, traces["vadd"], {})
+    tight = _run(native, traces["vadd"], {"-gpgpu_n_cluster_ejection_buffer_size": "1",
+                                          "-gpgpu_n_ldst_response_buffer_size": "1"})
+    assert tight.tot_insn == base.tot_insn
+    assert abs(tight.tot_cycle - base.tot_cycle) <= 0.02 * base.tot_cycle
+    # no L1 write-back is ever dropped by a full injection queue
+    for r in (base, tight):
+        assert "write-backs lost" not in r.output
+
+
+def test_unmodelled_options_warn(native, traces):
+    """Options accepted only for config compatibility never change a run
+    silently: a non-default value prints why it has no effect."""
+    s = _run(native, traces["vadd"], {"-gpgpu_mem_unit_ports": "2"})
+    assert "GPGPU-Sim: WARNING option -gpgpu_mem_unit_ports 2: accepted for config compatibility, not modelled" \
+        in s.output
+    w = native.unmodelled_option_warnings(presets.args_for("QV100", {}))
+    assert not any("ejection_buffer" in x or "response_buffer" in x for x in w)  # both modelled now
+    assert any(x.startswith("note: option -gpgpu_ptx_force_max_capability") for x in w)
