@@ -32,7 +32,6 @@ Simulator::Simulator(const std::vector<std::string>& args) {
   reg_.parse_cmdline(args, false);
   cfg_ = derive_sim_cfg(reg_);
   dopt_ = derive_driver_opts(reg_);
-  for (const std::string& w : unmodelled_option_warnings(reg_)) print("GPGPU-Sim: %s\n", w.c_str());
   if (dopt_.engine == "gpu") {
     eng_ = make_gpu_engine();
     if (!eng_) throw std::runtime_error("-sim_engine gpu requested but the HIP engine is unavailable");
@@ -114,6 +113,7 @@ double Simulator::wall_seconds() const {
 // collective completes.
 int Simulator::run() {
   print("Accel-Sim-AMD [MI355X-native trace-driven simulator, engine=%s]\n", eng_->name());
+  for (const std::string& w : unmodelled_option_warnings(reg_)) print("GPGPU-Sim: %s\n", w.c_str());
   cmds_ = parse_commandlist(dopt_.trace_file);
   next_cmd_ = 0;
   if (dopt_.resume_option) next_cmd_ = resume_checkpoint();

@@ -192,7 +192,7 @@ struct SmView {
   SV_REF(w_lds_st);
   WarpSb w_sb;
   SV_REF(w_issue_ok);
-  SV_REF(w_hin);
+  SV_REF(w_win);
   SV_WARP(w_slot_used);
   SV_REF(w_slot_pend);
   SV_REF(w_slot_dst);
@@ -225,6 +225,7 @@ struct SmView {
   SV_REF(wb_cnt);
   SV_REF(wb);
   SV_VAL(ldst);
+  SV_REF(ldst_acc);
   SV_REF(hit_cnt);
   SV_REF(hit);
   SV_REF(l1);
@@ -292,13 +293,13 @@ struct SmView {
 
   __device__ __forceinline__ explicit SmView(B& b)
       : base(b), l1_sets(b.l1_sets), l1_assoc(b.l1_assoc), cycle(b.cycle), arb_next(b.arb_next),
-        arb_cnt(b.arb_cnt), w_wait(b.w_wait), w_slot_lds(b.w_slot_lds), w_lds_st(b.w_lds_st), w_issue_ok(b.w_issue_ok), w_hin(b.w_hin),
+        arb_cnt(b.arb_cnt), w_wait(b.w_wait), w_slot_lds(b.w_slot_lds), w_lds_st(b.w_lds_st), w_issue_ok(b.w_issue_ok), w_win(b.w_win),
         w_slot_pend(b.w_slot_pend),
         w_slot_dst(b.w_slot_dst), cta_id(b.cta_id), cta_ks(b.cta_ks), cta_wbase(b.cta_wbase), cta_nw(b.cta_nw),
         n_cta_k(b.n_cta_k), cta_wmask(b.cta_wmask), used_thr(b.used_thr), used_regs(b.used_regs),
         used_shmem(b.used_shmem),
         idoc_inst(b.idoc_inst), oc_inst(b.oc_inst),
-        wb_cnt(b.wb_cnt), wb(b.wb), hit_cnt(b.hit_cnt), hit(b.hit), l1(b.l1), mshr(b.mshr),
+        wb_cnt(b.wb_cnt), wb(b.wb), ldst_acc(b.ldst_acc), hit_cnt(b.hit_cnt), hit(b.hit), l1(b.l1), mshr(b.mshr),
         pend(b.pend), il1(b.il1), imshr(b.imshr),
         outq(b.outq), ocnt(b.ocnt), inq(b.inq), rsp_cl(b.rsp_cl), rsp_ld(b.rsp_ld), skey(b.skey), sref(b.sref), srank(b.srank) {
 #define SV_LD(m) m = sv_uni(b.m);

@@ -85,6 +85,20 @@ struct WavePar {
   static __device__ __forceinline__ void one(F&& f) {
     if (lane() == 0) f();
   }
+  // trace records HBM -> LDS without VGPR staging: lane i moves 16 bytes
+  // (global_load_lds, lane-linear LDS image at a wave-uniform base); the
+  // copy completes asynchronously, fetch_wait() is the reader's wait
+  template <class T>
+  static __device__ __forceinline__ void fetch_copy(T* dst, const T* src, int n) {
+    static_assert(sizeof(T) % 16 == 0, "fetch_copy: 16-byte granular records");
+    typedef __attribute__((address_space(1))) const uint4 g4;
+    typedef __attribute__((address_space(3))) uint4 l4;
+    const int chunks = n * (int)(sizeof(T) / 16);
+    const int l = lane();
+    if (l < chunks)
+      __builtin_amdgcn_global_load_lds((g4*)(reinterpret_cast<const uint4*>(src) + l), (l4*)dst, 16, 0, 0);
+  }
+  static __device__ __forceinline__ void fetch_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
   static __device__ __forceinline__ void prof(int) {}
   static __device__ __forceinline__ void tick(int) {}
   // Values read from LDS state land in VGPRs (the compiler cannot know that

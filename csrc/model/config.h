@@ -15,6 +15,7 @@ constexpr int kMaxWarps = 64;       // warps per SM (lanes of one wavefront)
 constexpr int kMaxCta = 32;         // CTA slots per SM
 constexpr int kMaxSched = 4;        // schedulers / sub-cores per SM
 constexpr int kIbuf = 2;            // instruction buffer entries per warp
+constexpr int kWin = 4;             // per-warp decoded-instruction window [w_head, w_next] (>= kIbuf + 1, power of 2)
 constexpr int kMaxEpoch = 256;     // longest PDES epoch (interconnect lookahead), core cycles
 constexpr int kMaxOC = 16;          // operand collector units per SM
 constexpr int kMaxBanks = 32;       // register file banks per SM

@@ -85,6 +85,15 @@ struct SeqPar {
   // side effect executed once per wave (global-memory stores of uniform data)
   template <class F>
   static SIM_HDI void one(F&& f) { f(); }
+  // copy n trace records (instructions / access records, 16-byte multiples,
+  // at most 1 KB) from the kernel trace into the unit's state.  The GPU policy
+  // issues them as asynchronous LDS DMA and the reader calls fetch_wait()
+  // first; here it is a plain copy.
+  template <class T>
+  static SIM_HDI void fetch_copy(T* dst, const T* src, int n) {
+    for (int i = 0; i < n; ++i) dst[i] = src[i];
+  }
+  static SIM_HDI void fetch_wait() {}
   static SIM_HDI void sync() {}
   // stage profiling stamp (no-op on the CPU; the GPU profiling build records
   // s_memtime deltas per stage)

@@ -168,8 +168,11 @@ struct alignas(16) SMState {
   uint16_t w_wait[kMaxWarps];    // counts of the pending s_waitcnt: vm | lgkm << 8 (0xff: not waited for)
   uint64_t w_sb[kMaxWarps][4];   // scoreboard: pending destination registers
   uint64_t w_issue_ok[kMaxWarps];  // first cycle the warp may issue again (-gpgpu_warp_issue_interval)
-  TInst w_hin[kMaxWarps];        // the instruction at w_head (TInst{} past the stream end): read every cycle
-                                 // by the scheduler from here instead of from the trace in HBM
+  // decoded instructions [w_head, w_next] of each warp (slot = index & (kWin-1)):
+  // the fetched-not-issued ones plus the next fetch's target (its PC feeds the
+  // instruction cache).  Filled from the trace at fetch / CTA launch (LDS DMA
+  // on the GPU), so the issue path never waits on HBM.
+  TInst w_win[kMaxWarps][kWin];
   uint8_t w_slot_used[kMaxWarps];  // bitmask of used load slots
   uint8_t w_slot_lds[kMaxWarps];   // load slots holding an LDS load (lgkmcnt, not vmcnt)
   uint8_t w_lds_st[kMaxWarps];     // LDS stores in flight (lgkmcnt)
@@ -207,6 +210,7 @@ struct alignas(16) SMState {
   WbEnt wb[kWbRing][kWbSlot];
   // ---- LD/ST + L1 ----
   LdstState ldst;
+  TAcc ldst_acc[kMaxAccess];     // access records of the instruction in the LD/ST unit (loaded at dispatch)
   uint8_t hit_cnt[kHitRing];
   HitEnt hit[kHitRing][kHitSlot];
   L1Line l1[kMaxL1Lines];
@@ -621,7 +625,7 @@ SIM_HDI void il1_prefetch(S& s, const SimCfg& c, uint64_t line) {
 template <class P, class S>
 SIM_HDI bool il1_fetch(S& s, const SimCfg& c, const KernelTab& kt, uint32_t w) {
   const CacheGeom& g = c.il1;
-  const uint32_t pc = P::uni(inst_at(kt, P::uni((uint32_t)s.w_next[w])).pc);
+  const uint32_t pc = P::uni(s.w_win[w][P::uni((uint32_t)s.w_next[w]) & (kWin - 1)].pc);
   const uint64_t line = (kProgramMemStart + pc) & ~127ull;
   const uint32_t set = cache_set_index(g, line);
   const int way = il1_find<P>(s, g, set, line);
@@ -822,10 +826,10 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
   uint32_t processed = 0;
   uint32_t unext = P::uni(u.next);
   const uint8_t uslot = P::uni(u.slot);
-  // access table of the warp's kernel (slot in the top bits of its stream index)
-  const TAcc* accs = x.kt->k[P::uni((uint32_t)s.w_end[w]) >> kSlotShift].accs;
+  // access records were brought into the unit at dispatch
+  P::fetch_wait();
   while (unext < nacc && processed < c.l1_banks) {
-    const TAcc a = P::uni(accs[in.mem + unext]);
+    const TAcc a = P::uni(s.ldst_acc[unext]);
     uint32_t bbit = 1u << (a.bank & 31);
     if (banks_used & bbit) break;  // L1 bank conflict: next cycle
     if (c.perfect_mem) {
@@ -1051,7 +1055,9 @@ SIM_HDI void sm_read_operands(S& s, const SimCfg& c) {
 
 // collectors whose operands are all read go to their unit, oldest first
 template <class P, class S>
-SIM_HDI void sm_dispatch(S& s, const SimCfg& c, uint64_t now) {
+SIM_HDI void sm_dispatch(S& s, const SmCtx& x, uint64_t now) {
+  const SimCfg& c = *x.cfg;
+  const KernelTab* x_kt = x.kt;
   const int noc = (int)amin<uint32_t>(c.oc_units, kMaxOC);
   const uint32_t wbw = wb_width(c);
   const uint32_t ready = P::uni(s.oc_mask & ~s.oc_read_mask);
@@ -1065,9 +1071,15 @@ SIM_HDI void sm_dispatch(S& s, const SimCfg& c, uint64_t now) {
     const uint32_t u = (uint32_t)(info >> 16) & 0xffu;
     if (u == U_MEM) {
       if (P::uni(s.ldst.busy)) continue;
-      s.ldst.inst = P::uni(s.oc_inst[best]);
+      const TInst li = P::uni(s.oc_inst[best]);
+      s.ldst.inst = li;
       s.ldst.busy = 1;
       s.ldst.warp = (uint8_t)(info & 0xffu);
+      if (li.space != S_SHARED && li.width && li.mem != kNoMem) {
+        // the warp's kernel's access table (slot in the top bits of its stream index)
+        const TAcc* accs = x_kt->k[P::uni((uint32_t)s.w_end[info & 0xffu]) >> kSlotShift].accs;
+        P::fetch_copy(&s.ldst_acc[0], &accs[li.mem], (int)amin<uint32_t>(li.width, kMaxAccess));
+      }
       s.ldst.slot = (uint8_t)((info >> 24) & 0xffu);  // load slot allocated at issue
       s.ldst.next = 0;
       s.ldst.start = (uint32_t)now;
@@ -1182,7 +1194,7 @@ template <class S>
 SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, const KernelTab& kt, int w, uint32_t nsched,
                             uint64_t idoc_busy) {
   if (!(s.w_flags[w] & WF_ACTIVE) || s.w_ibuf[w] == 0) return false;
-  const TInst in = s.w_hin[w];  // ibuf > 0: the head is inside the warp's stream
+  const TInst in = s.w_win[w][s.w_head[w] & (kWin - 1)];  // ibuf > 0: the head is in the window
   return warp_can_issue_i(s, c, w, in, nsched, idoc_busy);
 }
 
@@ -1202,10 +1214,6 @@ SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32
   if (trace_sm_on(c, TS_WARP_SCHEDULER, s.id))
     P::one([&] { trace_put(c, s.id, now, EV_ISSUE, (uint16_t)w, (uint64_t)in.pc | (uint64_t)in.opcode << 32); });
   s.w_head[w] = hidx + 1;
-  {
-    const TInst nx = hidx + 1 < P::uni((uint32_t)s.w_end[w]) ? inst_at(*x.kt, hidx + 1) : TInst{};
-    P::one([&] { s.w_hin[w] = nx; });
-  }
   s.w_ibuf[w] = (uint8_t)(P::uni((uint8_t)s.w_ibuf[w]) - 1);
   // stats: instruction counts at issue (reference counts active threads,
   // shader.cc:1911)
@@ -1313,7 +1321,8 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   const uint64_t idoc_busy = P::uni(s.idoc_mask);
   // every warp's next instruction, read once (a register per lane on the GPU)
   // (read straight from the kernel's trace in HBM: an L2-resident stream)
-  const auto head = P::template lanes<TInst>(nw, [&](int w) -> TInst { return s.w_hin[w]; });
+  P::fetch_wait();  // window entries DMA'd by earlier fetches
+  const auto head = P::template lanes<TInst>(nw, [&](int w) -> TInst { return s.w_win[w][s.w_head[w] & (kWin - 1)]; });
   // readiness of every warp (lane-parallel)
   const uint64_t live = P::uni(s.live_mask);
   uint64_t ready = P::ballot_m(live, [&](int w) -> bool {
@@ -1400,7 +1409,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
     // warp's next buffered instruction issues in the same cycle if it is
     // ready and, with -gpgpu_dual_issue_diff_exec_units, uses another unit
     if (c.max_issue_per_warp > 1 && u1 >= 0 && P::uni((uint8_t)s.w_ibuf[w])) {
-      const TInst in2 = P::uni(s.w_hin[w]);  // refreshed by the first issue
+      const TInst in2 = P::uni(s.w_win[w][(hidx + 1) & (kWin - 1)]);  // the warp's next buffered instruction
       const bool special = in2.cls == OC_EXIT || in2.cls == OC_BARRIER || in2.cls == OC_MEMBAR ||
                            in2.cls == OC_NOP || (in2.flags & F_WAITCNT);
       if (!special && (!c.dual_issue_diff || unit_of(c, in2.cls) != (uint32_t)u1) &&
@@ -1419,6 +1428,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
 template <class P, class S>
 SIM_HDI void sm_fetch(S& s, const SimCfg& c, const KernelTab& kt) {
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
+  P::fetch_wait();
   uint64_t need = P::ballot_m(P::uni(s.live_mask), [&](int w) {
     uint8_t f = s.w_flags[w];
     return (f & WF_ACTIVE) && !(f & (WF_EXITING | WF_IMISS)) && s.w_ibuf[w] == 0 && s.w_next[w] < s.w_end[w];
@@ -1435,8 +1445,13 @@ SIM_HDI void sm_fetch(S& s, const SimCfg& c, const KernelTab& kt) {
       break;
     }
     const uint32_t wnext = P::uni((uint32_t)s.w_next[w]);
-    uint32_t avail = P::uni((uint32_t)s.w_end[w]) - wnext;
+    const uint32_t wend = P::uni((uint32_t)s.w_end[w]);
+    uint32_t avail = wend - wnext;
     uint32_t n = avail < (uint32_t)kIbuf ? avail : (uint32_t)kIbuf;
+    // window: [wnext] is already there (launch / previous fetch); bring in the
+    // rest of this fetch and the next fetch's target
+    for (uint32_t j = 1; j <= n && wnext + j < wend; ++j)
+      P::fetch_copy(&s.w_win[w][(wnext + j) & (kWin - 1)], &inst_at(kt, wnext + j), 1);
     s.w_next[w] = wnext + n;
     s.w_ibuf[w] = (uint8_t)n;
     s.fetch_rr = w + 1;
@@ -1576,7 +1591,7 @@ SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id,
     s.w_next[w] = tag | ws.begin;
     s.w_head[w] = tag | ws.begin;
     s.w_end[w] = tag | (ws.begin + ws.count);
-    s.w_hin[w] = ws.count ? k.insts[ws.begin] : TInst{};
+    if (ws.count) s.w_win[w][ws.begin & (kWin - 1)] = k.insts[ws.begin];  // the first fetch's target
     s.w_issue_ok[w] = 0;
     s.w_age[w] = age0 + (uint32_t)i;
     s.w_flags[w] = WF_ACTIVE;
@@ -1607,7 +1622,7 @@ SIM_HDI void sm_cycle(S& s, const SmCtx& x, uint64_t now) {
   P::prof(3);
   sm_ldst<P>(s, x, now);
   P::prof(4);
-  sm_dispatch<P>(s, c, now);
+  sm_dispatch<P>(s, x, now);
   P::prof(5);
   sm_read_operands<P>(s, c);
   P::prof(6);
