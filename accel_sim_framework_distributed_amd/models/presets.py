@@ -564,6 +564,16 @@ def _mi355x() -> Dict[str, str]:
         "-trace_opcode_latency_initiation_spec_op_8": "2,1",
         # the SQC instruction cache fetches sequential code lines ahead
         "-gpgpu_inst_prefetch_lines": "8",
+        # CDNA4 memory hierarchy: 8 XCDs with private L2s (16 slices each;
+        # workgroups round-robin over the XCDs), and the 256 MB Infinity Cache
+        # (MALL) as a memory-side cache in front of the 128 HBM channels
+        # (2 MB = 1024 sets x 16 ways of 128 B per channel); -dram_latency is
+        # the L2-miss path to the MALL (ub_cache_lat: MALL 535 - L2 201
+        # cycles), a MALL miss adds the HBM path on top (HBM 889 - MALL 535,
+        # less the DRAM timing the channel model adds itself)
+        "-sim_xcd": "8",
+        "-sim_mall": "1024:16",
+        "-sim_mall_miss_latency": "250",
     })
     return c
 

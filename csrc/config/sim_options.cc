@@ -286,6 +286,11 @@ const OptDef kOptions[] = {
     {"-xgmi_link_latency_ns", 'f', "1000.0", "collective step latency (ns)"},
     {"-xgmi_links_per_gpu", 'u', "7", "xGMI links per GPU"},
     {"-sim_event_skip", 'b', "1", "fast-forward quiet SM cycles inside an epoch (results identical)"},
+    {"-sim_xcd", 'u', "0",
+     "XCDs with private L2s (0 = one shared L2): SM s belongs to XCD s % N and uses the n_subpart/N slices of its XCD"},
+    {"-sim_mall", 's', "none",
+     "memory-attached last-level cache (Infinity Cache) per DRAM channel: <sets>:<assoc> of 128 B sectored lines, or none"},
+    {"-sim_mall_miss_latency", 'u', "0", "extra core cycles of an HBM access over a MALL hit"},
     {"-sim_cpu_threads", 'u', "1", "CPU engine: OpenMP threads over the units of one epoch (1 = serial; "
                                   "run simulations job-parallel instead)"},
     {"-collective_slice_bytes", 'u', "131072", "packet model: bytes per link packet (RCCL slice)"},
@@ -856,6 +861,30 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.perfect_mem = r.getb("-gpgpu_perfect_mem") ? 1u : 0u;
   c.simple_dram = r.getb("-gpgpu_simple_dram_model") ? 1u : 0u;
   c.event_skip = r.getb("-sim_event_skip") ? 1u : 0u;
+  {
+    // CDNA4 memory hierarchy
+    c.n_xcd = (uint32_t)r.getu("-sim_xcd");
+    c.log2_spx = 0;
+    if (c.n_xcd > 1) {
+      if (c.n_subpart % c.n_xcd) throw OptionError("-sim_xcd must divide the number of L2 sub-partitions");
+      const uint32_t spx = c.n_subpart / c.n_xcd;
+      if (spx & (spx - 1)) throw OptionError("-sim_xcd: sub-partitions per XCD must be a power of two");
+      while ((1u << c.log2_spx) < spx) ++c.log2_spx;
+    } else {
+      c.n_xcd = 0;
+    }
+    c.mall_sets = c.mall_assoc = 0;
+    const std::string m = strip_ws(r.gets("-sim_mall"));
+    if (!m.empty() && m != "none" && m != "0") {
+      auto v = split(m, ':');
+      if (v.size() != 2) throw OptionError("-sim_mall expects <sets>:<assoc>");
+      c.mall_sets = parse_u(v[0], "-sim_mall");
+      c.mall_assoc = parse_u(v[1], "-sim_mall");
+      if (!c.mall_sets || (c.mall_sets & (c.mall_sets - 1)) || !c.mall_assoc || c.mall_assoc > 64)
+        throw OptionError("-sim_mall: sets must be a power of two and 1 <= assoc <= 64");
+    }
+    c.mall_miss_fs = (uint64_t)r.getu("-sim_mall_miss_latency");  // cycles; fs once the clocks are known
+  }
   c.cpu_threads = r.getu("-sim_cpu_threads");
   c.trace_mask = 0;
   if (r.getb("-trace_enabled")) {
@@ -908,6 +937,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
     c.per_l2 = (uint64_t)llround(1e9 / f[2]);
     c.per_dram = (uint64_t)llround(1e9 / f[3]);
   }
+  c.mall_miss_fs *= c.per_core;
   c.kernel_launch_latency = (uint32_t)std::max<long long>(0, r.geti("-gpgpu_kernel_launch_latency"));
   {
     const long long q = r.geti("-gpgpu_kernel_launch_latency_queued");

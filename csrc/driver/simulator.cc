@@ -940,6 +940,29 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   print("total dram reads = %llu\n", (unsigned long long)dram_rd);
   print("total dram writes = %llu\n", (unsigned long long)dram_wr);
   print("total dram activates = %llu\n", (unsigned long long)dram_act);
+  {
+    // traffic leaving the L2 for memory (Infinity Fabric on CDNA4: what
+    // rocprofv3 counts as TCC_EA0_RDREQ / WRREQ) and the MALL in front of DRAM
+    uint64_t mrd = 0, mwr = 0, mh = 0, mm = 0, mw = 0, mwb = 0;
+    for (auto& m : cmem) {
+      mrd += m.l2_mem_rd;
+      mwr += m.l2_mem_wr;
+      mh += m.mall_rd_hit;
+      mm += m.mall_rd_miss;
+      mw += m.mall_wr;
+      mwb += m.mall_wb;
+    }
+    print("L2_to_mem_read_sectors = %llu\n", (unsigned long long)mrd);
+    print("L2_to_mem_write_sectors = %llu\n", (unsigned long long)mwr);
+    if (cfg_.mall_sets) {
+      print("MALL_read_hits = %llu\n", (unsigned long long)mh);
+      print("MALL_read_misses = %llu\n", (unsigned long long)mm);
+      print("MALL_read_hit_rate = %.4f\n", mh + mm ? (double)mh / (double)(mh + mm) : 0.0);
+      print("MALL_writes = %llu\n", (unsigned long long)mw);
+      print("MALL_writebacks = %llu\n", (unsigned long long)mwb);
+    }
+    if (cfg_.n_xcd) print("XCDs = %u (private L2 slices per XCD = %u)\n", cfg_.n_xcd, 1u << cfg_.log2_spx);
+  }
   print("dram_bw_util = %.4f\n", dram_cyc ? (double)dram_busy / dram_cyc : 0.0);
   {
     // per memory channel and per L2 bank (reference dram_t::print and the

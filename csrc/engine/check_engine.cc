@@ -149,7 +149,7 @@ class CheckEngine final : public Engine {
     memcpy(&h, ia_.data(), sizeof(h));
     const uint64_t cap_req = h.cnt_req ? h.box_req / h.cnt_req : 0, cap_rep = h.cnt_rep ? h.box_rep / h.cnt_rep : 0;
     const size_t need = off + 2 * ((h.box_req + h.box_rep) * sizeof(Pkt) + (h.cnt_req + h.cnt_rep) * 4) +
-                        h.ovf * sizeof(Pkt);
+                        h.ovf * sizeof(Pkt) + h.mall * sizeof(L2Line);
     if (ia_.size() < need) fail(cyc, "state image truncated before the mailboxes");
     auto cells = [&](const char* what, int parity, uint64_t nbox, uint64_t ncnt, uint64_t cap) {
       const size_t box = off, cnt = off + nbox * sizeof(Pkt);
@@ -195,6 +195,13 @@ class CheckEngine final : public Engine {
                     ia_[i], ib_[i]);
       }
     }
+    // MALL lines: all of them are state
+    const size_t mall0 = off + h.ovf * sizeof(Pkt);
+    for (size_t i = mall0; i < mall0 + h.mall * sizeof(L2Line); ++i)
+      if (ia_[i] != ib_[i])
+        diverge(cyc, "MALL line " + std::to_string((i - mall0) / sizeof(L2Line)) + " +" +
+                         std::to_string((i - mall0) % sizeof(L2Line)),
+                ia_[i], ib_[i]);
   }
   [[noreturn]] void diverge(uint64_t cyc, const std::string& where, uint8_t va, uint8_t vb) {
     fail(cyc, "states diverge in " + where + " (" + a_->name() + " 0x" + hex(va) + ", " + b_->name() + " 0x" + hex(vb) + ")");

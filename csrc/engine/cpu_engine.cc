@@ -29,7 +29,8 @@ void init_chan_state(ChanState& ch, uint32_t id, const SimCfg& c) {
 }
 
 void host_memcpy_fill(ChanState* chs, uint32_t nch, const SimCfg& c, uint64_t addr, uint64_t bytes) {
-  if (c.l2.disabled) return;
+  // with XCD-private L2s a host copy (SDMA) lands in memory, not in any XCD's L2
+  if (c.l2.disabled || c.n_xcd) return;
   const uint64_t first = addr & ~127ull;
   const uint64_t last = (addr + bytes + 127) & ~127ull;
   // only the tail that can still be resident matters
@@ -61,7 +62,7 @@ void check_state_header(const EngineStateHeader& h, const EngineStateHeader& w) 
   if (h.magic != w.magic || h.version != w.version) throw std::runtime_error("engine state: not a state image");
   if (h.n_sm != w.n_sm || h.n_mem != w.n_mem || h.sm_bytes != w.sm_bytes || h.ch_bytes != w.ch_bytes ||
       h.pub_bytes != w.pub_bytes || h.box_req != w.box_req || h.cnt_req != w.cnt_req || h.box_rep != w.box_rep ||
-      h.cnt_rep != w.cnt_rep || h.ovf != w.ovf)
+      h.cnt_rep != w.cnt_rep || h.ovf != w.ovf || h.mall != w.mall)
     throw std::runtime_error("engine state: image was written for a different configuration or build");
 }
 
@@ -98,6 +99,7 @@ class CpuEngine : public Engine {
     }
     ovf_cap_ = backlog_cap(c);
     ovf_.assign((size_t)c.n_subpart * ovf_cap_, Pkt{});
+    mall_.assign((size_t)(c.n_mem * mall_lines(c)), L2Line{});
     epoch_ = 0;
     cycle_ = 0;
     kt_ = KernelTab{};
@@ -160,6 +162,7 @@ class CpuEngine : public Engine {
         } else {
           ChanState& ch = chs_[i - nsm];
           MemCtx m = ctx_mem(cur, t1);
+          m.mall = mall_.empty() ? nullptr : mall_.data() + (size_t)(i - nsm) * mall_lines(c);
           chan_epoch<SeqPar>(ch, m, box_req_[prev].data(), cnt_req_[prev].data(), cap_req_, t0 * c.per_core);
           chan_publish<SeqPar>(ch, m, *pub_, cur);
         }
@@ -210,7 +213,7 @@ class CpuEngine : public Engine {
   }
 
   void snapshot(std::vector<uint8_t>& out) override {
-    out.resize(sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState));
+    out.resize(sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState) + mall_.size() * sizeof(L2Line));
     uint8_t* p = out.data();
     for (auto& s : sms_) {
       memcpy(p, &s, sizeof(SMState));
@@ -220,9 +223,10 @@ class CpuEngine : public Engine {
       memcpy(p, &ch, sizeof(ChanState));
       p += sizeof(ChanState);
     }
+    if (!mall_.empty()) memcpy(p, mall_.data(), mall_.size() * sizeof(L2Line));
   }
   void restore(const std::vector<uint8_t>& in) override {
-    if (in.size() != sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState))
+    if (in.size() != sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState) + mall_.size() * sizeof(L2Line))
       throw std::runtime_error("snapshot size mismatch");
     const uint8_t* p = in.data();
     for (auto& s : sms_) {
@@ -233,6 +237,7 @@ class CpuEngine : public Engine {
       memcpy(&ch, p, sizeof(ChanState));
       p += sizeof(ChanState);
     }
+    if (!mall_.empty()) memcpy(mall_.data(), p, mall_.size() * sizeof(L2Line));
   }
   void advance(uint64_t cycles) override {
     uint64_t E = c_.icnt_latency;
@@ -251,6 +256,7 @@ class CpuEngine : public Engine {
     h.box_rep = box_rep_[0].size();
     h.cnt_rep = cnt_rep_[0].size();
     h.ovf = ovf_.size();
+    h.mall = mall_.size();
     h.cycle = cycle_;
     h.epoch = epoch_;
     h.ready = kt_.active;
@@ -272,6 +278,7 @@ class CpuEngine : public Engine {
       o.put(cnt_rep_[p].data(), cnt_rep_[p].size() * sizeof(uint32_t));
     }
     o.put(ovf_.data(), ovf_.size() * sizeof(Pkt));
+    o.put(mall_.data(), mall_.size() * sizeof(L2Line));
   }
 
   void load_state(const std::vector<uint8_t>& in) override {
@@ -289,6 +296,7 @@ class CpuEngine : public Engine {
       r.get(cnt_rep_[p].data(), cnt_rep_[p].size() * sizeof(uint32_t));
     }
     r.get(ovf_.data(), ovf_.size() * sizeof(Pkt));
+    r.get(mall_.data(), mall_.size() * sizeof(L2Line));
     cycle_ = h.cycle;
     epoch_ = h.epoch;
     if (h.ready) throw std::runtime_error("engine state: image taken with kernels running");
@@ -315,6 +323,7 @@ class CpuEngine : public Engine {
     m.win_end = t1 * c_.per_core;
     m.ovf = ovf_.data();
     m.ovf_cap = ovf_cap_;
+    m.mall = nullptr;
     return m;
   }
 
@@ -326,6 +335,7 @@ class CpuEngine : public Engine {
   std::vector<uint32_t> cnt_req_[2], cnt_rep_[2];
   uint32_t cap_req_ = 0, cap_rep_ = 0;
   std::vector<Pkt> ovf_;  // arrival backlog rings [n_subpart][ovf_cap_]
+  std::vector<L2Line> mall_;  // MALL lines [n_mem][mall_sets * mall_assoc]
   uint32_t ovf_cap_ = 0;
   uint64_t epoch_ = 0, cycle_ = 0;
   KernelTab kt_{};

@@ -78,10 +78,11 @@ inline uint32_t backlog_cap(const SimCfg& c) {
 
 struct EngineStateHeader {
   uint64_t magic = 0x41534d5354415445ull;  // "ASMSTATE"
-  uint64_t version = 4;  // 4: kernel slots (concurrent kernels)
+  uint64_t version = 5;  // 4: kernel slots (concurrent kernels); 5: MALL lines
   uint64_t n_sm = 0, n_mem = 0, sm_bytes = 0, ch_bytes = 0, pub_bytes = 0;
   uint64_t box_req = 0, cnt_req = 0, box_rep = 0, cnt_rep = 0;  // element counts per parity
   uint64_t ovf = 0;                                              // arrival backlog packets (all sub-partitions)
+  uint64_t mall = 0;                                             // MALL lines (all channels), after the backlog
   uint64_t cycle = 0, epoch = 0, ready = 0;
 };
 
@@ -127,6 +128,9 @@ struct EngineKernelInfo {
   bool valid = false;
 };
 EngineKernelInfo gpu_engine_kernel_info();
+
+// MALL lines of one channel (0 without a MALL)
+inline uint64_t mall_lines(const SimCfg& c) { return (uint64_t)c.mall_sets * c.mall_assoc; }
 
 // helpers shared by both engines
 uint32_t reply_cap(const SimCfg& c);

@@ -49,6 +49,7 @@ struct GpuArgs {
   uint32_t cap_req, cap_rep;
   Pkt* ovf;
   uint32_t ovf_cap;
+  L2Line* mall;  // [n_mem][mall_sets * mall_assoc] or nullptr
   uint64_t epoch0;
   uint64_t cycle0;
   uint64_t max_cycle;
@@ -213,6 +214,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   mx.n_src_sub = c.n_subpart;
   mx.ovf = a.ovf;
   mx.ovf_cap = a.ovf_cap;
+  mx.mall = nullptr;
   uint64_t epoch = a.epoch0, cycle = a.cycle0;
   uint64_t t_work0 = a.ework ? __builtin_amdgcn_s_memtime() : 0;
   uint32_t done = 0, dead = 0, capped = 0;
@@ -237,6 +239,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
       } else {
         mx.outbox = a.box_rep[cur];
         mx.outcnt = a.cnt_rep[cur];
+        mx.mall = a.mall ? a.mall + (size_t)(u - c.n_sm) * ((size_t)c.mall_sets * c.mall_assoc) : nullptr;
         mx.win_end = t1 * c.per_core;
         chan_epoch<P>(*ch, mx, a.box_req[prev], a.cnt_req[prev], a.cap_req, t0 * c.per_core);
         chan_publish<P>(*ch, mx, *a.pub, cur);
@@ -411,6 +414,11 @@ class GpuEngine : public Engine {
     ovf_cap_ = backlog_cap(c);
     HIPCHECK(hipMalloc(&d_ovf_, sizeof(Pkt) * c.n_subpart * (size_t)ovf_cap_));
     HIPCHECK(hipMemset(d_ovf_, 0, sizeof(Pkt) * c.n_subpart * (size_t)ovf_cap_));
+    n_mall_ = (size_t)c.n_mem * mall_lines(c);
+    if (n_mall_) {
+      HIPCHECK(hipMalloc(&d_mall_, sizeof(L2Line) * n_mall_));
+      HIPCHECK(hipMemset(d_mall_, 0, sizeof(L2Line) * n_mall_));
+    }
     HIPCHECK(hipMalloc(&d_ctl_, sizeof(GpuCtl)));
     HIPCHECK(hipHostMalloc(&h_ctl_, sizeof(GpuCtl)));
     HIPCHECK(hipMalloc(&d_kt_, sizeof(KernelTab)));
@@ -461,6 +469,7 @@ class GpuEngine : public Engine {
       a.cap_rep = cap_rep_;
       a.ovf = d_ovf_;
       a.ovf_cap = ovf_cap_;
+      a.mall = d_mall_;
       a.epoch0 = epoch_;
       a.cycle0 = cycle_;
       a.max_cycle = lim.max_cycle;
@@ -540,17 +549,20 @@ class GpuEngine : public Engine {
   }
 
   void snapshot(std::vector<uint8_t>& out) override {
-    out.resize(sizeof(SMState) * c_.n_sm + sizeof(ChanState) * c_.n_mem);
+    const size_t units = sizeof(SMState) * c_.n_sm + sizeof(ChanState) * c_.n_mem;
+    out.resize(units + sizeof(L2Line) * n_mall_);
     HIPCHECK(hipMemcpy(out.data(), d_sms_, sizeof(SMState) * c_.n_sm, hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(out.data() + sizeof(SMState) * c_.n_sm, d_chs_, sizeof(ChanState) * c_.n_mem,
                        hipMemcpyDeviceToHost));
+    if (n_mall_) HIPCHECK(hipMemcpy(out.data() + units, d_mall_, sizeof(L2Line) * n_mall_, hipMemcpyDeviceToHost));
   }
   void restore(const std::vector<uint8_t>& in) override {
-    if (in.size() != sizeof(SMState) * c_.n_sm + sizeof(ChanState) * c_.n_mem)
-      throw std::runtime_error("snapshot size mismatch");
+    const size_t units = sizeof(SMState) * c_.n_sm + sizeof(ChanState) * c_.n_mem;
+    if (in.size() != units + sizeof(L2Line) * n_mall_) throw std::runtime_error("snapshot size mismatch");
     HIPCHECK(hipMemcpy(d_sms_, in.data(), sizeof(SMState) * c_.n_sm, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(d_chs_, in.data() + sizeof(SMState) * c_.n_sm, sizeof(ChanState) * c_.n_mem,
                        hipMemcpyHostToDevice));
+    if (n_mall_) HIPCHECK(hipMemcpy(d_mall_, in.data() + units, sizeof(L2Line) * n_mall_, hipMemcpyHostToDevice));
   }
   void advance(uint64_t cycles) override {
     uint64_t E = c_.icnt_latency;
@@ -589,6 +601,7 @@ class GpuEngine : public Engine {
     h.box_rep = (uint64_t)c_.n_sm * c_.n_subpart * cap_rep_;
     h.cnt_rep = (uint64_t)c_.n_sm * c_.n_subpart;
     h.ovf = (uint64_t)c_.n_subpart * ovf_cap_;
+    h.mall = n_mall_;
     h.cycle = cycle_;
     h.epoch = epoch_;
     h.ready = kt_.active;
@@ -613,6 +626,7 @@ class GpuEngine : public Engine {
       dl(d_cnt_rep_[p], h.cnt_rep * sizeof(uint32_t));
     }
     dl(d_ovf_, h.ovf * sizeof(Pkt));
+    dl(d_mall_, h.mall * sizeof(L2Line));
   }
   void load_state(const std::vector<uint8_t>& in) override {
     StateIn r{in};
@@ -633,6 +647,7 @@ class GpuEngine : public Engine {
       ul(d_cnt_rep_[p], w.cnt_rep * sizeof(uint32_t));
     }
     ul(d_ovf_, w.ovf * sizeof(Pkt));
+    ul(d_mall_, w.mall * sizeof(L2Line));
     cycle_ = h.cycle;
     epoch_ = h.epoch;
     if (h.ready) throw std::runtime_error("engine state: image taken with kernels running");
@@ -663,6 +678,7 @@ class GpuEngine : public Engine {
     }
     fr(d_ctl_);
     fr(d_ovf_);
+    fr(d_mall_);
     fr(d_trace_ev_);
     fr(d_trace_cnt_);
     for (SlotBufs& b : bufs_) {
@@ -685,6 +701,8 @@ class GpuEngine : public Engine {
   ChanState* d_chs_ = nullptr;
   EpochPub* d_pub_ = nullptr;
   Pkt* d_ovf_ = nullptr;  // arrival backlog rings [n_subpart][ovf_cap_]
+  L2Line* d_mall_ = nullptr;  // MALL lines [n_mem][mall_sets * mall_assoc]
+  size_t n_mall_ = 0;
   uint32_t ovf_cap_ = 0;
   Pkt* d_box_req_[2] = {nullptr, nullptr};
   uint32_t* d_cnt_req_[2] = {nullptr, nullptr};

@@ -196,6 +196,20 @@ SIM_HDI uint64_t partition_address(const SimCfg& c, uint64_t addr) {
   return c.part_runs.n != 0xff ? run_gather(c.part_runs, pa) : pack_bits(~c.sub_id_mask, pa, 64, 0);
 }
 
+// XCD-private L2s (SimCfg::n_xcd): the destination sub-partition of a request
+// from SM `sm` whose address decodes to the global sub-partition `gsub`: the
+// slice of the SM's own XCD picked by the address's low slice bits
+SIM_HDI uint32_t l2_slice_of(const SimCfg& c, uint32_t sm, uint32_t gsub) {
+  if (!c.n_xcd) return gsub;
+  return ((sm % c.n_xcd) << c.log2_spx) | (gsub & ((1u << c.log2_spx) - 1u));
+}
+// set-index address of an XCD slice (and of the MALL behind it): the
+// slice-select bits squeezed out of the channel field
+SIM_HDI uint64_t xcd_partition_address(const SimCfg& c, uint64_t a) {
+  const uint32_t lo = (uint32_t)c.addr_chip_s, k = c.log2_spx;
+  return ((a >> (lo + k)) << lo) | (a & ((1ull << lo) - 1));
+}
+
 SIM_HDI uint32_t cache_set_index(const CacheGeom& g, uint64_t addr) {
   const int lb = ilog2u(g.line);
   const int sb = ilog2u(g.nsets);

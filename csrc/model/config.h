@@ -46,6 +46,7 @@ constexpr int kReplyQ = 128;
 constexpr int kDramQ = 128;         // per channel FR-FCFS queue
 constexpr int kDramLat = 512;       // per channel L2->DRAM latency pipe (in flight >= dram_latency x 1/cycle)
 constexpr int kDramRet = 256;
+constexpr int kMallRet = 64;        // MALL read hits waiting to return to the L2 (per channel)
 constexpr int kMaxBanksDram = 32;
 constexpr int kMaxSubPerCh = 2;
 constexpr int kMaxSubTot = 128;    // L2 sub-partitions (interconnect destinations)
@@ -242,6 +243,21 @@ struct SimCfg {
   uint32_t perfect_mem;     // every global/local access hits with L1 latency, no traffic
   uint32_t simple_dram;     // DRAM = latency pipe + one column per DRAM cycle, no bank timing
   uint32_t event_skip;      // fast-forward provably quiet SM cycles inside an epoch (exact)
+  // ---- CDNA4 memory hierarchy (MI355X-native extension; 0 = the reference's
+  //      single address-interleaved L2, l2cache.cc:463-595) ----
+  // -sim_xcd N: the SMs form N XCDs (SM s -> XCD s % N, the workgroup
+  // round-robin of the hardware dispatcher) with PRIVATE L2s: XCD x owns
+  // sub-partitions [x*spx, (x+1)*spx), spx = n_subpart / N, and an SM's
+  // request goes to the slice of its own XCD selected by the address.  Data
+  // read by several XCDs is cached (and missed) in each of them.
+  uint32_t n_xcd;
+  uint32_t log2_spx;        // log2(sub-partitions per XCD)
+  // -sim_mall <sets>:<assoc>: the memory-attached last-level cache (AMD
+  // Infinity Cache / MALL) in front of every DRAM channel, sectored like the
+  // L2, write-back; L2 misses that hit it return without a DRAM access, HBM
+  // accesses pay -sim_mall_miss_latency on top of the DRAM timing
+  uint32_t mall_sets, mall_assoc;
+  uint64_t mall_miss_fs;    // extra latency of a MALL miss (fs)
   uint32_t cpu_threads;     // CPU engine only: OpenMP threads per epoch (host option)
   // ---- debug trace streams (pointers are set by the engine that owns the buffers) ----
   uint32_t trace_mask;      // TraceStream bits

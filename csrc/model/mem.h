@@ -92,6 +92,11 @@ struct MemStats {
   uint64_t icnt_conflicts;     // request net: ready inputs not granted by this output port (per cycle)
   uint64_t icnt_queue_cycles;  // request net: icnt cycles granted packets waited at this output port
   uint64_t icnt_arb_cycles;    // request net: icnt cycles with at least one input ready
+  // below the L2 (per 32 B sector): what leaves the L2 for memory (the
+  // Infinity Fabric traffic rocprofv3 counts as TCC_EA0_RDREQ / WRREQ), and
+  // how the memory-attached cache (MALL) in front of DRAM served it
+  uint64_t l2_mem_rd, l2_mem_wr;
+  uint64_t mall_rd_hit, mall_rd_miss, mall_wr, mall_wb;
 };
 
 struct SubPart {
@@ -137,6 +142,10 @@ struct alignas(16) ChanState {
   DramRet ret[kDramRet];
   uint32_t ret_head, ret_n;
   uint64_t q_seq;        // arrival sequence for FR-FCFS age order
+  // MALL: read hits on their way back to the L2 (DRAM returns use ret[])
+  DramRet mret[kMallRet];
+  uint32_t mret_head, mret_n;
+  uint32_t mall_stamp, pad_m;
   uint64_t q_age[kDramQ];
   uint8_t q_valid[kDramQ];
   uint16_t ocnt[kMaxSubPerCh][kMaxSmTot];  // replies put in each (dst SM) cell this epoch
@@ -158,6 +167,7 @@ struct MemCtx {
   uint64_t win_end;     // fs, exclusive
   Pkt* ovf;             // per-sub-partition arrival backlog rings [n_subpart][ovf_cap] (global memory)
   uint32_t ovf_cap;
+  L2Line* mall;         // this channel's MALL lines [mall_sets][mall_assoc] (global memory), nullptr = no MALL
 };
 
 // ---------------------------------------------------------------------------
@@ -192,6 +202,93 @@ SIM_HDI void l2dram_push(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t s
   r.sub = (uint8_t)sub;
   ch.lat_n++;
   sp.n_l2dram++;
+  if (write) sp.st.l2_mem_wr++;
+  else sp.st.l2_mem_rd++;
+}
+
+// ---- MALL (memory-attached last-level cache) -------------------------------
+constexpr uint8_t kSubNone = 0xff;  // DramReq::sub of a MALL write-back (holds no L2 credit)
+SIM_HDI uint32_t mall_set(const SimCfg& c, uint64_t line) {
+  const uint64_t a = c.n_xcd ? xcd_partition_address(c, line) : partition_address(c, line);
+  return (uint32_t)((a >> 7) & (c.mall_sets - 1));
+}
+template <class P>
+SIM_HDI int mall_find(const L2Line* b, uint32_t assoc, uint64_t line) {
+  const uint64_t m = P::ballot((int)assoc, [&](int w) { return b[w].valid && b[w].tag == line; });
+  return m ? ffs64(m) : -1;
+}
+template <class P>
+SIM_HDI int mall_victim(const L2Line* b, uint32_t assoc) {
+  return P::argmin((int)assoc, [&](int w) -> uint64_t { return b[w].valid ? ((1ull << 40) | b[w].lru) : (uint64_t)w; });
+}
+// a MALL line lives in global memory: one lane stores it, the fence orders it
+// before the wave's next probe
+template <class P>
+SIM_HDI void mall_put(L2Line* b, int w, const L2Line& v) {
+  P::one([&] { b[w] = v; });
+  P::sync();
+}
+// room in the DRAM scheduler for n more requests of one kind
+SIM_HDI bool dram_room(const ChanState& ch, const SimCfg& c, bool write, uint32_t n) {
+  const uint32_t qcap = amin<uint32_t>(c.dram_queue ? c.dram_queue : 1, kDramQ);
+  if (ch.q_n + n > (uint32_t)kDramQ) return false;
+  if (!c.wq_enable) return ch.q_n + n <= qcap;
+  return write ? ch.qw_n + n <= c.wq_size : ch.q_n - ch.qw_n + n <= qcap;
+}
+template <class P>
+SIM_HDI void dram_enqueue(ChanState& ch, const DramReq& h) {
+  ch.qw_n += h.write ? 1 : 0;
+  const int f = P::find_first(kDramQ, [&](int i) -> bool { return !ch.q_valid[i]; });
+  ch.q[f] = h;
+  ch.q_valid[f] = 1;
+  ch.q_age[f] = ch.q_seq++;
+  ch.q_n++;
+}
+// dirty sectors of a MALL victim go to DRAM (false: no room, nothing changed)
+template <class P>
+SIM_HDI bool mall_writeback(ChanState& ch, const SimCfg& c, const L2Line& v, uint64_t now_fs) {
+  if (!(v.valid && v.dirty)) return true;
+  const uint32_t n = (uint32_t)popc64(v.dirty);
+  if (!dram_room(ch, c, true, n)) return false;
+  for (uint32_t s = 0; s < 4; ++s) {
+    if (!(v.dirty >> s & 1u)) continue;
+    DramReq r;
+    const AddrTlx t = addr_decode(c, v.tag + s * 32ull);
+    r.line = v.tag;
+    r.ready = now_fs;
+    r.row = t.row;
+    r.bank = (uint16_t)dram_bank_of(c, t);
+    r.sector = (uint8_t)s;
+    r.write = 1;
+    r.sub = kSubNone;
+    dram_enqueue<P>(ch, r);
+  }
+  ch.sp[0].st.mall_wb += n;
+  return true;
+}
+// install sector `sec` of `line` (a DRAM read returning or a write absorbed);
+// false: the victim's write-back found no room (the caller decides)
+template <class P>
+SIM_HDI bool mall_install(ChanState& ch, const SimCfg& c, L2Line* b, uint64_t line, uint32_t sec, bool dirty,
+                          uint64_t now_fs) {
+  int w = mall_find<P>(b, c.mall_assoc, line);
+  L2Line v;
+  if (w < 0) {
+    w = mall_victim<P>(b, c.mall_assoc);
+    const L2Line old = P::uni(b[w]);
+    if (!mall_writeback<P>(ch, c, old, now_fs)) return false;
+    v.tag = line;
+    v.valid = 0;
+    v.dirty = 0;
+    v.pad[0] = v.pad[1] = 0;
+  } else {
+    v = P::uni(b[w]);
+  }
+  v.valid |= (uint8_t)(1u << sec);
+  if (dirty) v.dirty |= (uint8_t)(1u << sec);
+  v.lru = ++ch.mall_stamp;
+  mall_put<P>(b, w, v);
+  return true;
 }
 
 // ---- L2 tag array (lane-parallel over ways) ----
@@ -213,7 +310,7 @@ SIM_HDI int l2_victim(const SubPart& sp, const CacheGeom& g, uint32_t set) {
   });
 }
 SIM_HDI uint32_t l2_set(const SimCfg& c, uint64_t line) {
-  return cache_set_index(c.l2, partition_address(c, line));
+  return cache_set_index(c.l2, c.n_xcd ? xcd_partition_address(c, line) : partition_address(c, line));
 }
 
 // allocate a line for `line` (evicting, writing back dirty sectors);
@@ -552,34 +649,75 @@ namespace asim {
 // per-bank ACT/PRE state machines and HBM-style dual command bus
 // (reference dram_t::cycle dram.cc:289-552, frfcfs dram_sched.cc:109-258).
 template <class P>
-SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
+SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, const MemCtx& x, uint64_t now_fs) {
   MemStats& st = ch.sp[0].st;
   const uint64_t t = ch.dcycle++;
   st.dram_cycles++;
-  const uint32_t qcap = amin<uint32_t>(c.dram_queue ? c.dram_queue : 1, kDramQ);
-  // latency pipe -> scheduler queue
+  // latency pipe -> (MALL) -> scheduler queue
   while (ch.lat_n) {
-    const DramReq& h = ch.lat[ch.lat_head];
+    const DramReq h = ch.lat[ch.lat_head];
     if (h.ready > now_fs) break;
+    if (x.mall) {
+      L2Line* b = x.mall + (uint64_t)mall_set(c, h.line) * c.mall_assoc;
+      if (h.write) {
+        // write-back, write-allocate: the MALL absorbs the sector
+        if (!mall_install<P>(ch, c, b, h.line, h.sector, true, now_fs)) break;
+        st.mall_wr++;
+        ch.sp[h.sub].n_l2dram--;
+        ch.lat_head = (ch.lat_head + 1) % kDramLat;
+        ch.lat_n--;
+        continue;
+      }
+      const int w = mall_find<P>(b, c.mall_assoc, h.line);
+      if (w >= 0 && (P::uni(b[w].valid) >> h.sector & 1u)) {
+        if (ch.mret_n >= (uint32_t)kMallRet) break;
+        DramRet& o = ch.mret[(ch.mret_head + ch.mret_n) % kMallRet];
+        o.line = h.line;
+        o.sector = h.sector;
+        o.sub = h.sub;
+        o.ready = now_fs;
+        ch.mret_n++;
+        L2Line v = P::uni(b[w]);
+        v.lru = ++ch.mall_stamp;
+        mall_put<P>(b, w, v);
+        st.mall_rd_hit++;
+        ch.sp[h.sub].n_l2dram--;
+        ch.lat_head = (ch.lat_head + 1) % kDramLat;
+        ch.lat_n--;
+        continue;
+      }
+    }
     // reads and writes have their own capacity with a separate write queue
     // (reference dram_t::full, dram.cc:160-175)
-    if (c.wq_enable ? (h.write ? ch.qw_n >= c.wq_size : ch.q_n - ch.qw_n >= qcap) : ch.q_n >= qcap) break;
-    ch.qw_n += h.write ? 1 : 0;
-    int f = P::find_first(kDramQ, [&](int i) -> bool { return !ch.q_valid[i]; });
-    ch.q[f] = h;
-    ch.q_valid[f] = 1;
-    ch.q_age[f] = ch.q_seq++;
-    ch.q_n++;
+    if (!dram_room(ch, c, h.write != 0, 1)) break;
+    if (x.mall) st.mall_rd_miss++;
+    dram_enqueue<P>(ch, h);
     ch.lat_head = (ch.lat_head + 1) % kDramLat;
     ch.lat_n--;
   }
-  // data returns -> DRAM->L2 queues
+  // MALL hits, then DRAM data returns -> DRAM->L2 queues
+  const uint32_t fcap = amin<uint32_t>(c.q_dram_l2 ? c.q_dram_l2 : 1, 64);
+  while (ch.mret_n) {
+    const DramRet& r = ch.mret[ch.mret_head];
+    if (r.ready > now_fs) break;
+    SubPart& sp = ch.sp[r.sub];
+    if (sp.fill_n >= fcap) break;
+    sp.fill[(sp.fill_head + sp.fill_n) % 64] = r;
+    sp.fill_n++;
+    ch.mret_head = (ch.mret_head + 1) % kMallRet;
+    ch.mret_n--;
+  }
   while (ch.ret_n) {
     const DramRet& r = ch.ret[ch.ret_head];
     if (r.ready > now_fs) break;
     SubPart& sp = ch.sp[r.sub];
-    uint32_t cap = amin<uint32_t>(c.q_dram_l2 ? c.q_dram_l2 : 1, 64);
-    if (sp.fill_n >= cap) break;
+    if (sp.fill_n >= fcap) break;
+    // a read that missed the MALL allocates there on its way back (a dirty
+    // victim without DRAM queue room leaves the line uncached instead)
+    if (x.mall) {
+      L2Line* b = x.mall + (uint64_t)mall_set(c, r.line) * c.mall_assoc;
+      (void)mall_install<P>(ch, c, b, r.line, r.sector, false, now_fs);
+    }
     sp.fill[(sp.fill_head + sp.fill_n) % 64] = r;
     sp.fill_n++;
     ch.ret_head = (ch.ret_head + 1) % kDramRet;
@@ -599,7 +737,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
       d.line = r.line;
       d.sector = r.sector;
       d.sub = r.sub;
-      d.ready = (t + burst) * c.per_dram;
+      d.ready = (t + burst) * c.per_dram + (x.mall ? c.mall_miss_fs : 0);
       ch.ret_n++;
       st.dram_rd++;
     } else {
@@ -610,7 +748,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
     ch.q_valid[o] = 0;
     ch.q_n--;
     ch.qw_n -= r.write ? 1 : 0;
-    ch.sp[r.sub].n_l2dram--;
+    if (r.sub != kSubNone) ch.sp[r.sub].n_l2dram--;
     return;
   }
   // separate write queue: serve reads until the writes reach the high
@@ -660,7 +798,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
         o.line = r.line;
         o.sector = r.sector;
         o.sub = r.sub;
-        o.ready = (t + c.CL + burst) * c.per_dram;
+        o.ready = (t + c.CL + burst) * c.per_dram + (x.mall ? c.mall_miss_fs : 0);
         ch.ret_n++;
         b.t_pre_ok = amax<uint64_t>(b.t_pre_ok, t + c.tRTPL);
         uint64_t rtw = t + c.CL + burst + 2;
@@ -673,7 +811,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, uint64_t now_fs) {
       ch.q_valid[pick] = 0;
       ch.q_n--;
       ch.qw_n -= r.write ? 1 : 0;
-      ch.sp[r.sub].n_l2dram--;
+      if (r.sub != kSubNone) ch.sp[r.sub].n_l2dram--;
       col = true;
       col_bank = r.bank;
     }
@@ -734,7 +872,7 @@ SIM_HDI bool sub_idle(const SubPart& sp) {
   return sp.inq_n == 0 && sp.ovf_n == 0 && sp.rop_n == 0 && sp.rep_n == 0 && sp.fill_n == 0 && sp.n_wait == 0 && sp.n_l2dram == 0;
 }
 SIM_HDI bool chan_idle(const ChanState& ch, const SimCfg& c) {
-  if (ch.lat_n || ch.q_n || ch.ret_n) return false;
+  if (ch.lat_n || ch.q_n || ch.ret_n || ch.mret_n) return false;
   for (uint32_t j = 0; j < c.n_sub_per_mem; ++j)
     if (!sub_idle(ch.sp[j])) return false;
   return true;
@@ -759,6 +897,7 @@ SIM_HDI uint64_t chan_next_event(const ChanState& ch, const SimCfg& c, uint64_t 
   uint64_t nx = ~0ull;
   if (ch.lat_n) nx = amin(nx, ch.lat[ch.lat_head].ready);
   if (ch.ret_n) nx = amin(nx, ch.ret[ch.ret_head].ready);
+  if (ch.mret_n) nx = amin(nx, ch.mret[ch.mret_head].ready);
   for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
     const SubPart& sp = ch.sp[j];
     if (sp.rep_n || sp.ovf_n) return now;
@@ -820,7 +959,7 @@ SIM_HDI void mem_window(ChanState& ch, const MemCtx& x) {
     }
     if (ch.t_dram == tm) {
       P::prof(21);
-      dram_cycle<P>(ch, c, tm);
+      dram_cycle<P>(ch, c, x, tm);
       ch.t_dram += c.per_dram;
     }
     if (ch.t_l2 == tm) {

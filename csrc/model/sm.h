@@ -338,7 +338,7 @@ SIM_HDI void sm_send(S& s, const SimCfg& c, uint8_t type, uint64_t line, uint8_t
   p.t = 0;
   p.tag = tag;
   p.src = (uint16_t)s.id;
-  p.dst = (uint16_t)t.sub;
+  p.dst = (uint16_t)l2_slice_of(c, s.id, t.sub);
   p.type = type;
   p.sectors = sectors;
   p.size = (type == P_WR) ? (uint16_t)(8 + bytes) : (uint16_t)8;

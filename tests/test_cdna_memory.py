@@ -1,0 +1,127 @@
+"""CDNA4 memory hierarchy (MI355X-native extension of the reference's single
+address-interleaved L2, l2cache.cc:463-595 / gpu-cache.h:1694): XCD-private L2
+slices (-sim_xcd) and the memory-attached Infinity Cache / MALL in front of
+every DRAM channel (-sim_mall, -sim_mall_miss_latency)."""
+import re
+
+import pytest
+
+from accel_sim_framework_distributed_amd.models import presets
+from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+from accel_sim_framework_distributed_amd.tracegen.format import write_kernel_binary, write_kernelslist
+
+BUF = 0x7200_0000
+REGION = 32 * 1024          # bytes read by one load instruction over all warps
+LOADS = 4                   # load instructions per warp: 128 KB footprint
+
+
+def _reader(kid, ctas=64):
+    """Every warp reads one 128 B line per load; all CTAs sweep the same buffer."""
+    k = KernelBuilder(f"_Z4readPf{kid}", (ctas, 1, 1), (128, 1, 1), nregs=16, kid=kid)
+    g = k.g
+    for i in range(LOADS):
+        k.op("LDG.E", [8 + i], [2], base=BUF + i * REGION + (g.gtid0 * 4) % REGION, stride=4)
+    for i in range(LOADS):
+        k.op("FFMA", [4], [4, 8 + i])
+    k.op("EXIT")
+    return k.build()
+
+
+def _shared_reader(kid, ctas=64, loads=16):
+    """Every CTA reads the same lines: warp w of any CTA reads line (load, w)."""
+    k = KernelBuilder(f"_Z6sharedPf{kid}", (ctas, 1, 1), (128, 1, 1), nregs=16, kid=kid)
+    g = k.g
+    for i in range(loads):
+        k.op("LDG.E", [8], [2], base=BUF + i * 4096 + g.warp * 128, stride=4)
+        k.op("FFMA", [4], [4, 8])
+    k.op("EXIT")
+    return k.build()
+
+
+def _app(tmp_path, name, nk=1, gen=None):
+    d = tmp_path / name
+    d.mkdir()
+    cmds = []
+    for i in range(1, nk + 1):
+        write_kernel_binary(str(d / f"kernel-{i}.asimk"), (gen or _reader)(i))
+        cmds.append(f"kernel-{i}.asimk")
+    return write_kernelslist(str(d), cmds)
+
+
+def _stat(out, key, first=False):
+    m = re.findall(rf"{re.escape(key)} = ([0-9.]+)", out)
+    return float(m[0] if first else m[-1]) if m else None
+
+
+def _run(native, kl, extra, engine="cpu"):
+    over = {"-gpgpu_perf_sim_memcpy": "0", "-sim_engine": engine}
+    over.update(extra)
+    s = native.Simulator(presets.args_for("QV100", over) + ["-trace", kl], False)
+    assert s.run() == 0
+    return s
+
+
+def test_config_validation(native):
+    cfg = native.parse_config(presets.args_for("QV100", {"-sim_xcd": "8", "-sim_mall": "256:16"}))
+    assert cfg["n_sm"] == 80
+    with pytest.raises(Exception, match="sim_xcd"):
+        native.parse_config(presets.args_for("QV100", {"-sim_xcd": "3"}))
+    with pytest.raises(Exception, match="sim_mall"):
+        native.parse_config(presets.args_for("QV100", {"-sim_mall": "100:16"}))
+
+
+def test_xcd_private_l2_replicates_shared_data(native, tmp_path):
+    kl = _app(tmp_path, "one", gen=_shared_reader)
+    shared = _run(native, kl, {})
+    xcd = _run(native, kl, {"-sim_xcd": "8"})
+    assert xcd.tot_insn == shared.tot_insn
+    lines = 16 * 4
+    rd_shared = _stat(shared.output, "L2_to_mem_read_sectors")
+    rd_xcd = _stat(xcd.output, "L2_to_mem_read_sectors")
+    # one shared L2 fetches every sector once; eight private ones each fetch it
+    assert rd_shared == pytest.approx(4 * lines, rel=0.02)
+    assert rd_xcd == pytest.approx(8 * 4 * lines, rel=0.05)
+    assert "XCDs = 8 (private L2 slices per XCD = 8)" in xcd.output
+
+
+def test_mall_serves_rereads_after_l2_flush(native, tmp_path):
+    kl = _app(tmp_path, "two", nk=2)
+    flush = {"-gpgpu_flush_l2_cache": "1", "-sim_mall_miss_latency": "300"}
+    no_mall = _run(native, kl, flush)
+    mall = _run(native, kl, dict(flush, **{"-sim_mall": "512:16"}))
+    sectors = LOADS * REGION // 32
+    # kernel 2 re-reads everything: without the MALL from DRAM again
+    assert _stat(no_mall.output, "total dram reads") == pytest.approx(2 * sectors, rel=0.02)
+    assert _stat(mall.output, "total dram reads") == pytest.approx(sectors, rel=0.02)
+    assert _stat(mall.output, "MALL_read_hits") == pytest.approx(sectors, rel=0.02)
+    assert _stat(mall.output, "L2_to_mem_read_sectors") == _stat(no_mall.output, "L2_to_mem_read_sectors")
+    # the second kernel's misses return at MALL latency: faster than the first
+    k1, k2 = mall.kernels
+    assert k2["cycles"] < k1["cycles"]
+
+
+def test_mall_absorbs_writes(native, tmp_path):
+    """Stores write back into the MALL (write-allocate): DRAM sees only its
+    dirty evictions, and a later reader of the data hits there."""
+    k = KernelBuilder("_Z5writePf", (64, 1, 1), (128, 1, 1), nregs=16, kid=1)
+    g = k.g
+    for i in range(LOADS):
+        k.op("STG.E", [], [2, 4], base=BUF + i * REGION + (g.gtid0 * 4) % REGION, stride=4)
+    k.op("EXIT")
+    d = tmp_path / "w"
+    d.mkdir()
+    write_kernel_binary(str(d / "kernel-1.asimk"), k.build())
+    write_kernel_binary(str(d / "kernel-2.asimk"), _reader(2))
+    kl = write_kernelslist(str(d), ["kernel-1.asimk", "kernel-2.asimk"])
+    # a write-through L2 sends every store below it; the flush makes the
+    # reader miss in the L2
+    wt = {"-gpgpu_cache:dl2": "S:32:128:24,L:T:m:L:P,A:192:4,32:0,32", "-gpgpu_flush_l2_cache": "1"}
+    base = _run(native, kl, wt)
+    mall = _run(native, kl, dict(wt, **{"-sim_mall": "512:16"}))
+    sectors = LOADS * REGION // 32
+    assert _stat(base.output, "total dram writes") > 0
+    assert _stat(base.output, "total dram reads") == pytest.approx(sectors, rel=0.02)
+    assert _stat(mall.output, "total dram writes") == 0
+    assert _stat(mall.output, "MALL_writes") == _stat(mall.output, "L2_to_mem_write_sectors") > 0
+    assert _stat(mall.output, "total dram reads") == 0
+    assert _stat(mall.output, "MALL_read_hits") == pytest.approx(sectors, rel=0.02)

@@ -45,13 +45,15 @@ def test_rodinia_app_gpu_equals_cpu(gpu_mod, tmp_path, app):
     assert [k["cycles"] for k in g.kernels] == [k["cycles"] for k in c.kernels]
 
 
-def test_state_snapshot_bit_exact(gpu_mod, tmp_path):
-    """Full architectural state (every SM and channel) is byte-identical."""
+@pytest.mark.parametrize("extra", [{}, {"-sim_xcd": "8", "-sim_mall": "256:16"}], ids=["shared_l2", "xcd_mall"])
+def test_state_snapshot_bit_exact(gpu_mod, tmp_path, extra):
+    """Full architectural state (every SM and channel, and the MALL lines) is
+    byte-identical."""
     from accel_sim_framework_distributed_amd import sim
     from accel_sim_framework_distributed_amd.tracegen import rodinia
     kl = rodinia.write_app(str(tmp_path / "hs"), rodinia.hotspot(64, 2, 2))
-    sg = sim.Simulator("QV100", kl, engine="gpu", torch_runtime=True)
-    sc = sim.Simulator("QV100", kl, engine="cpu")
+    sg = sim.Simulator("QV100", kl, engine="gpu", torch_runtime=True, extra=extra)
+    sc = sim.Simulator("QV100", kl, engine="cpu", extra=extra)
     sg.run()
     sc.run()
     a, b = sg.native.snapshot(), sc.native.snapshot()
@@ -146,6 +148,10 @@ _FEATURES = {
     "max_insn_cap": {"-gpgpu_max_insn": "150000"},
     "max_cta_cap": {"-gpgpu_max_cta": "30"},
     "long_epoch": {"-icnt_latency": "32"},
+    # round 3: CDNA4 memory hierarchy and the SM reply-path buffers
+    "xcd_mall": {"-sim_xcd": "8", "-sim_mall": "256:16", "-sim_mall_miss_latency": "200",
+                 "-gpgpu_flush_l2_cache": "1"},
+    "reply_buffers": {"-gpgpu_n_cluster_ejection_buffer_size": "1", "-gpgpu_n_ldst_response_buffer_size": "1"},
 }
 
 
