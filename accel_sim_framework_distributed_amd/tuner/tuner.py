@@ -92,6 +92,20 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
             opts["-gpgpu_cache:dl2"] = ":".join(f) + "," + rest
             notes.append(f"L2 per sub-partition clamped from {sets}x{assoc} to {new_sets}x{assoc} lines "
                          f"(simulator limit {max_lines} lines)")
+    # MALL: the extra latency of an HBM access over a Infinity Cache hit,
+    # less the DRAM service time the channel model adds by itself (row miss:
+    # tRCD + CL + a burst, at the DRAM clock, in core cycles)
+    if "hbm_over_mall_latency" in meas and cfg.get("-sim_mall", "none") != "none":
+        try:
+            hbm = float(meas["hbm_over_mall_latency"])
+            clk = [float(x) for x in cfg["-gpgpu_clock_domains"].split(":")]
+            tim = dict(kv.split("=") for kv in cfg.get("-gpgpu_dram_timing_opt", "").replace(" ", "").split(":")
+                       if "=" in kv)
+            svc = (int(tim.get("RCD", 12)) + int(tim.get("CL", 12)) + 2) * clk[0] / clk[3]
+            opts["-sim_mall_miss_latency"] = str(max(0, int(round(hbm - svc))))
+            notes.append(f"-sim_mall_miss_latency = HBM over MALL {hbm:.0f} - modelled DRAM service {svc:.0f} cycles")
+        except (KeyError, ValueError, IndexError):
+            pass
     for key, pol in _write_policies(meas).items():
         cur = opts.get(key, cfg.get(key))
         if cur:
