@@ -98,9 +98,25 @@ S_LOAD = r"gpgpu_n_load_insn\s*=\s*(.*)"
 S_STORE = r"gpgpu_n_store_insn\s*=\s*(.*)"
 S_L1 = r"\s+Total_core_cache_stats_breakdown\[%s\]\[%s\]\s*=\s*(.*)"
 S_L2 = r"\s+L2_cache_stats_breakdown\[%s\]\[%s\]\s*=\s*(.*)"
+S_VALU = r"gpgpu_n_valu_insn\s*=\s*(.*)"
+S_SALU = r"gpgpu_n_salu_insn\s*=\s*(.*)"
+S_SMEM = r"gpgpu_n_smem_insn\s*=\s*(.*)"
+S_VMRD = r"gpgpu_n_vmem_rd_insn\s*=\s*(.*)"
+S_VMWR = r"gpgpu_n_vmem_wr_insn\s*=\s*(.*)"
+S_LDSI = r"gpgpu_n_lds_insn\s*=\s*(.*)"
+S_SQBR = r"gpgpu_n_sq_branch_insn\s*=\s*(.*)"
+
+
+def _ea_rd_sectors(hw, mhz):
+    """TCC->EA read requests in 32 B sectors (requests are 32, 64 or 128 B)."""
+    return (_hw("TCC_EA0_RDREQ_32B_sum")(hw, mhz) + 2 * _hw("TCC_EA0_RDREQ_64B_sum")(hw, mhz) +
+            4 * _hw("TCC_EA0_RDREQ_128B_sum")(hw, mhz))
 _VMEM = ("SQ_INSTS_VMEM_RD_sum", "SQ_INSTS_VMEM_WR_sum")
 _WAVE_INSTS = ("SQ_INSTS_VALU_sum", "SQ_INSTS_SALU_sum", "SQ_INSTS_SMEM_sum", "SQ_INSTS_LDS_sum",
                "SQ_INSTS_BRANCH_sum") + _VMEM
+
+
+_SQ_STATS = (S_VALU, S_SALU, S_SMEM, S_VMRD, S_VMWR, S_LDSI, S_SQBR)
 
 
 def _ipc(d):
@@ -127,11 +143,16 @@ CORREL_STATS: List[CorrelStat] = [
     CorrelStat("Cycles", S_CYC, _cycles, "cycles"),
     CorrelStat("Instructions (thread)", r"gpu_sim_insn\s*=\s*(.*)",
                lambda hw, mhz: _mean(hw["thread_insts"]) if "thread_insts" in hw else float("nan"), "insn"),
-    CorrelStat("Warp instructions", S_WINSN, _hw(*_WAVE_INSTS), "warp-insn"),
+    # the SQ_INSTS_* classes exclude s_waitcnt / s_nop / s_barrier / s_endpgm:
+    # the simulator side sums its instructions of the same classes
+    CorrelStat("Warp instructions", "warp_insn", _hw(*_WAVE_INSTS), "warp-insn",
+               sim_stats=_SQ_STATS, sim_eval=lambda d: sum(d.values())),
     CorrelStat("Warp IPC", "warp_ipc", lambda hw, mhz: _hw(*_WAVE_INSTS)(hw, mhz) / _cycles(hw, mhz),
-               "warp-ipc", sim_stats=(S_WINSN, S_CYC), sim_eval=_ipc, ratio=True, log=False),
+               "warp-ipc", sim_stats=_SQ_STATS + (S_CYC,),
+               sim_eval=lambda d: sum(v for k, v in d.items() if k != S_CYC) / d[S_CYC] if d.get(S_CYC) else float("nan"),
+               ratio=True, log=False),
     CorrelStat("Memory instructions (VMEM + LDS)", "mem_insn", _hw(*(_VMEM + ("SQ_INSTS_LDS_sum",))), "mem-insn",
-               sim_stats=(S_LOAD, S_STORE), sim_eval=lambda d: d[S_LOAD] + d[S_STORE]),
+               sim_stats=(S_VMRD, S_VMWR, S_LDSI), sim_eval=lambda d: sum(d.values())),
     CorrelStat("Waves launched", r"gpgpu_n_completed_warps\s*=\s*(.*)", _hw("SQ_WAVES_sum"), "waves"),
     CorrelStat("Branch instructions", r"gpgpu_n_branch_insn\s*=\s*(.*)", _hw("SQ_INSTS_BRANCH_sum"), "branch"),
     CorrelStat("MFMA instructions", r"gpgpu_n_tensor_insn\s*=\s*(.*)", _hw("SQ_INSTS_MFMA_sum"), "mfma"),
@@ -163,6 +184,32 @@ CORREL_STATS: List[CorrelStat] = [
     CorrelStat("DRAM write requests", r"total dram writes\s*=\s*(.*)", _hw("TCC_EA0_WRREQ_sum"), "dram-writes"),
     CorrelStat("Interconnect packets SM->memory", r"icnt_total_pkts_simt_to_mem\s*=\s*(.*)",
                _hw("TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum", "TCP_TCC_ATOMIC_WITH_RET_REQ_sum"), "icnt-pkts"),
+    # ---- round 3: instruction mix by the sequencer's own classes (the
+    # simulator classifies each issued instruction like SQ_INSTS_*, see
+    # csrc/model/sm.h sq_class / isatrace/verify.py classify) ----
+    CorrelStat("VALU instructions (incl. MFMA)", S_VALU, _hw("SQ_INSTS_VALU_sum"), "valu"),
+    CorrelStat("SALU instructions", S_SALU, _hw("SQ_INSTS_SALU_sum"), "salu"),
+    CorrelStat("SMEM instructions", S_SMEM, _hw("SQ_INSTS_SMEM_sum"), "smem"),
+    CorrelStat("VMEM read instructions", S_VMRD, _hw("SQ_INSTS_VMEM_RD_sum"), "vmem-rd"),
+    CorrelStat("VMEM write instructions", S_VMWR, _hw("SQ_INSTS_VMEM_WR_sum"), "vmem-wr"),
+    CorrelStat("LDS instructions", S_LDSI, _hw("SQ_INSTS_LDS_sum"), "lds-insn"),
+    # ---- below the L2: Infinity Fabric traffic in 32 B sectors (TCC->EA
+    # requests are 32/64/128 B), L2 dirty write-backs, L2 requests ----
+    CorrelStat("L2->memory read sectors", r"L2_to_mem_read_sectors\s*=\s*(.*)", _ea_rd_sectors, "l2-mem-rd"),
+    CorrelStat("L2->memory write sectors", r"L2_to_mem_write_sectors\s*=\s*(.*)",
+               _hw("TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"), "l2-mem-wr"),
+    CorrelStat("L2 dirty write-backs", r"L2_cache_dirty_evictions\s*=\s*(.*)", _hw("TCC_WRITEBACK_sum"),
+               "l2-writebacks"),
+    CorrelStat("L2 requests", r"L2_total_cache_accesses\s*=\s*(.*)", _hw("TCC_REQ_sum"), "l2-req"),
+    # mean L1-miss round trip (TCP->TCC read latency), shader cycles
+    CorrelStat("Mean L1 miss latency", r"L1_miss_avg_latency\s*=\s*(.*)",
+               _hw_ratio(("TCP_TCC_READ_REQ_LATENCY_sum",), ("TCP_TCC_READ_REQ_sum",)), "l1-miss-lat",
+               ratio=True, log=False),
+    # instruction cache (SQC, shared by a CU pair on CDNA4)
+    CorrelStat("Instruction cache misses", r"\s+L1I_total_cache_misses\s*=\s*(.*)", _hw("SQC_ICACHE_MISSES_sum"),
+               "icache-miss"),
+    CorrelStat("Instruction cache accesses", r"\s+L1I_total_cache_accesses\s*=\s*(.*)",
+               _hw("SQC_ICACHE_HITS_sum", "SQC_ICACHE_MISSES_sum"), "icache-acc"),
 ]
 
 # rocprofv3 counter passes covering CORREL_STATS within one pass's hardware
@@ -172,7 +219,9 @@ COUNTER_GROUPS: List[str] = [
     "SQ_INSTS_MFMA,SQ_LDS_BANK_CONFLICT,TCP_TOTAL_CACHE_ACCESSES,TCP_TCC_READ_REQ,TCP_TCC_WRITE_REQ,"
     "TCP_TCC_ATOMIC_WITH_RET_REQ,TCC_HIT,TCC_MISS",
     "TCC_READ,TCC_WRITE,TCC_ATOMIC,TCC_EA0_RDREQ",
-    "TCC_EA0_WRREQ",
+    "TCC_EA0_WRREQ,TCC_EA0_WRREQ_64B,TCC_WRITEBACK,TCC_REQ,TCP_TCC_READ_REQ_LATENCY",
+    "TCC_EA0_RDREQ_32B,TCC_EA0_RDREQ_64B,TCC_EA0_RDREQ_128B",
+    "SQC_ICACHE_HITS,SQC_ICACHE_MISSES",
 ]
 
 

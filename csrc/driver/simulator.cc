@@ -853,6 +853,15 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   print("gpu_tot_issued_cta = %llu\n", (unsigned long long)tot_cta_);
   print("gpu_occupancy = %.4f%% \n", r.occupancy);
   print("gpu_tot_occupancy = %.4f%% \n", r.occupancy);
+  {
+    // this kernel's mean L1-miss round trip (MSHR allocation -> last sector), core cycles
+    uint64_t n = 0, sum = 0;
+    for (auto& st : sm) {
+      n += st.mf_lat_n;
+      sum += st.mf_lat_sum;
+    }
+    print("L1_miss_avg_latency = %.2f\n", n ? (double)sum / (double)n : 0.0);
+  }
   uint64_t l2_bytes = 0, dram_rd = 0, dram_wr = 0, dram_act = 0, dram_busy = 0, dram_cyc = 0;
   uint64_t l2[L2T_COUNT][L2O_COUNT] = {};
   // Rates (bandwidths, utilisation) are this kernel's; event counts are
@@ -1063,6 +1072,14 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
     print("gpgpu_n_dp_insn = %llu\n", (unsigned long long)cls[OC_DP]);
     print("gpgpu_n_tensor_insn = %llu\n", (unsigned long long)cls[OC_TENSOR]);
     print("gpgpu_n_barrier_insn = %llu\n", (unsigned long long)cls[OC_BARRIER]);
+    {
+      // wave instructions by the CDNA sequencer counter classes (SQ_INSTS_*)
+      uint64_t sq[8] = {};
+      for (auto& st : csm)
+        for (int i = 0; i < 8; ++i) sq[i] += st.sq_insn[i];
+      static const char* sqn[8] = {"valu", "salu", "smem", "vmem_rd", "vmem_wr", "lds", "sq_branch", "other"};
+      for (int i = 0; i < 8; ++i) print("gpgpu_n_%s_insn = %llu\n", sqn[i], (unsigned long long)sq[i]);
+    }
     print("gpgpu_n_dual_issue = %llu\n", (unsigned long long)dual);
     print("gpu_stall_shd_idle_sched = %llu\n", (unsigned long long)stall_idle);
     print("gpgpu_n_stall_shd_mem = %llu\n",

@@ -262,20 +262,30 @@ struct SmView {
   SV_REF(srank);
   // statistics: counter word k lives in lane (k & 63) of stv[k >> 6], so an
   // update is one masked VALU add instead of an LDS read-modify-write
+  // (words 128.. are rarer histograms: they stay in the LDS state)
   uint64_t stv[2];
   __device__ __forceinline__ void sadd(uint32_t k, uint64_t d) {
+    if (k >= 128u) {
+      reinterpret_cast<uint64_t*>(&base.st)[k] += d;
+      return;
+    }
     if (sv_lane() == (int)(k & 63u)) {
       if (k < 64u) stv[0] += d;
       else stv[1] += d;
     }
   }
   __device__ __forceinline__ uint64_t sget(uint32_t k) const {
+    if (k >= 128u) return reinterpret_cast<const uint64_t*>(&base.st)[k];
     const uint64_t m = k < 64u ? stv[0] : stv[1];
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, (int)(k & 63u));
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), (int)(k & 63u));
     return ((uint64_t)hi << 32) | lo;
   }
   __device__ __forceinline__ void sset(uint32_t k, uint64_t v) {
+    if (k >= 128u) {
+      reinterpret_cast<uint64_t*>(&base.st)[k] = v;
+      return;
+    }
     if (sv_lane() == (int)(k & 63u)) {
       if (k < 64u) stv[0] = v;
       else stv[1] = v;
@@ -313,7 +323,7 @@ struct SmView {
       const uint64_t* sw = reinterpret_cast<const uint64_t*>(&b.st);
       const int l = sv_lane();
       stv[0] = l < kStatWords ? sw[l] : 0ull;
-      stv[1] = l + 64 < kStatWords ? sw[l + 64 < kStatWords ? l + 64 : 0] : 0ull;
+      stv[1] = l + 64 < kStatWords ? sw[l + 64 < kStatWords ? l + 64 : 0] : 0ull;  // words < 128
     }
     {  // LdstState: 16-byte words through readfirstlane
       uint32_t w[sizeof(ldst) / 4];

@@ -12,6 +12,7 @@ namespace asim {
 // compile-time capacity caps of the fixed-size state (checked by the host
 // when a config is loaded; configs beyond them are rejected loudly)
 constexpr int kMaxWarps = 64;       // warps per SM (lanes of one wavefront)
+constexpr int kMaxWarpLanes = 64;   // threads per warp (wave64)
 constexpr int kMaxCta = 32;         // CTA slots per SM
 constexpr int kMaxSched = 4;        // schedulers / sub-cores per SM
 constexpr int kIbuf = 2;            // instruction buffer entries per warp

@@ -175,7 +175,7 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t 
   sm_kernels_init<P>(s, x);
   // 0. cycles [s.cycle, t0) were fast-forwarded by epoch_decide (nothing could
   //    happen in them): account them exactly like quiet cycles
-  if (t0 > s.cycle && (s.n_cta_active || !sm_idle(s))) sm_skip<P>(s, c, t0 - s.cycle);
+  if (t0 > s.cycle && (s.n_cta_active || !sm_idle(s))) sm_skip<P>(s, c, t0 - s.cycle, s.cycle);
   s.min_emit = ~0ull;
   // 1. arrivals (replies injected by the memory side last epoch)
   P::prof(12);
@@ -210,7 +210,7 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t 
           P::tick(18);
           const uint64_t nx = P::uni(sm_quiet_until<P>(v, c, *x.kt, t, t1));
           if (nx > t) {
-            sm_skip<P>(v, c, nx - t);
+            sm_skip<P>(v, c, nx - t, t);
             t = nx;
           }
         }

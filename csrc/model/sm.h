@@ -137,8 +137,37 @@ struct SMStats {
   uint64_t l1_wb_lost;         // write-backs dropped with the injection queue full (must stay 0)
   uint64_t icnt_reply_conflicts;     // reply net: ready inputs not granted by this SM's ejection port
   uint64_t icnt_reply_queue_cycles;  // reply net: icnt cycles granted replies waited at the port
+  uint64_t sq_insn[8];               // issued wave instructions by the CDNA SQ counter classes (SqClass)
+  // ---- words from 128 on stay in LDS on the GPU engine (sm_view.h) ----
+  // reference shader_core_stats::shader_cycle_distro (shader.cc:724-730,
+  // 1045, 1547-1555), per scheduler and cycle: [0] W0_Idle (no warp with a
+  // valid instruction), [1] W0_Scoreboard (valid instructions all wait on the
+  // scoreboard), [2] Stall (ready, but the pipeline did not take it), and
+  // [2 + k] one instruction issued with k active threads (k = 1..64)
+  uint64_t issue_distro[3 + kMaxWarpLanes];
+  uint64_t single_issue[kMaxSched];  // scheduler cycles that issued one instruction
+  uint64_t dual_issue[kMaxSched];    // ... two
 };
 enum IL1Out : uint8_t { IL1_HIT = 0, IL1_MISS, IL1_MSHR_HIT, IL1_RES_FAIL };
+// Instruction classes of the CDNA sequencer's counters (rocprofv3
+// SQ_INSTS_VALU / _SALU / _SMEM / _VMEM_RD / _VMEM_WR / _LDS / _BRANCH; VALU
+// includes MFMA), derived from the decoded class and memory space; OTHER =
+// s_waitcnt / s_nop / s_barrier / s_endpgm and friends, which no SQ_INSTS_*
+// class counts (isatrace/verify.py classify() is the mnemonic-level twin)
+enum SqClass : uint8_t { SQ_VALU = 0, SQ_SALU, SQ_SMEM, SQ_VMEM_RD, SQ_VMEM_WR, SQ_LDS, SQ_BRANCH, SQ_OTHER };
+SIM_HDI uint32_t sq_class(const TInst& in) {
+  switch (in.cls) {
+    case OC_LOAD: return in.space == S_SHARED ? SQ_LDS : in.space == S_CONST ? SQ_SMEM : SQ_VMEM_RD;
+    case OC_STORE: return in.space == S_SHARED ? SQ_LDS : in.space == S_CONST ? SQ_SMEM : SQ_VMEM_WR;
+    case OC_BRANCH: return SQ_BRANCH;
+    case OC_SPEC8: return SQ_SALU;  // CDNA traces put the scalar ALU on specialized unit 8
+    case OC_BARRIER:
+    case OC_MEMBAR:
+    case OC_EXIT:
+    case OC_NOP: return SQ_OTHER;
+    default: return in.space == S_CONST ? SQ_SMEM : SQ_VALU;  // s_memtime is an SMEM op
+  }
+}
 // SMStats::power_acc slots
 enum PwrCounter : uint8_t { PWR_CONST_OPERAND = 0 };
 
@@ -258,7 +287,7 @@ struct alignas(16) SMState {
 };
 #define SK(f) ((uint32_t)(offsetof(::asim::SMStats, f) / 8))
 constexpr int kStatWords = (int)(sizeof(SMStats) / 8);
-static_assert(kStatWords <= 128, "SM statistics must fit two register words per lane");
+static_assert(kStatWords <= 256, "SM statistics: words 0..127 in registers, the rest in LDS on the GPU engine");
 SIM_HDI uint64_t* s_scratch_key(SMState& s) { return s.skey; }
 SIM_HDI uint32_t* s_scratch_ref(SMState& s) { return s.sref; }
 SIM_HDI uint32_t* s_scratch_rank(SMState& s) { return s.srank; }
@@ -1220,6 +1249,7 @@ SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32
   s.sadd(SK(warp_insn), 1);
   s.sadd(SK(thread_insn), (uint64_t)popc64(in.mask));
   s.sadd(SK(cls_insn) + (in.cls < OC_COUNT ? in.cls : OC_ALU), 1);
+  s.sadd(SK(sq_insn) + sq_class(in), 1);
   // LDC / s_load: an ALU-timed instruction with a constant-cache operand
   // (reference trace_driven.cc:255-261 keeps LDC an ALU op; shader.cc:3287)
   if (in.space == S_CONST) s.sadd(SK(power_acc) + PWR_CONST_OPERAND, 1);
@@ -1312,6 +1342,29 @@ SIM_HDI bool waits_long_op(const S& s, int w, const TInst& in) {
   return false;
 }
 
+// warps with a valid instruction (buffered, not parked, issue interval
+// elapsed) and, among them, those whose operands are ready (the reference
+// scheduler_unit::cycle's valid_inst / ready_inst, shader.cc:1547-1555)
+template <class P, class S>
+SIM_HDI void sm_stall_masks(const S& s, const SimCfg& c, uint64_t now, uint64_t live, uint64_t& valid_m,
+                            uint64_t& sbok_m) {
+  valid_m = P::ballot_m(live, [&](int w) -> bool {
+    const uint8_t f = s.w_flags[w];
+    return (f & WF_ACTIVE) && !(f & (WF_EXITING | WF_BARRIER | WF_MEMBAR | WF_WAITCNT)) && s.w_ibuf[w] != 0 &&
+           warp_issue_due(s, c, w, now);
+  });
+  sbok_m = P::ballot_m(valid_m, [&](int w) -> bool {
+    const TInst& in = s.w_win[w][s.w_head[w] & (kWin - 1)];
+    for (int j = 0; j < 5; ++j)
+      if (sbt(s.w_sb, w, in.src[j])) return false;
+    return !sbt(s.w_sb, w, in.dst[0]) && !sbt(s.w_sb, w, in.dst[1]);
+  });
+}
+// stall class of one scheduler without an issue (issue_distro index 0..2)
+SIM_HDI uint32_t stall_class(uint64_t mine, uint64_t valid_m, uint64_t sbok_m) {
+  return !(valid_m & mine) ? 0u : !(sbok_m & mine) ? 1u : 2u;
+}
+
 template <class P, class S>
 SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
@@ -1340,6 +1393,15 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
     });
   P::prof(29);
   bool issued_any = false;
+  // issue-stall classification for the warp occupancy distribution, computed
+  // only when a scheduler with live warps has nothing to issue
+  uint64_t valid_m = 0, sbok_m = 0;
+  bool classified = false;
+  auto classify = [&]() {
+    if (classified) return;
+    classified = true;
+    sm_stall_masks<P>(s, c, now, live, valid_m, sbok_m);
+  };
   for (uint32_t sc = 0; sc < nsched; ++sc) {
     // warps of this scheduler
     const uint64_t mine = c.sched_mask[sc];
@@ -1372,7 +1434,11 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
       cand &= act;
     }
     if (!cand) {
-      if (live & mine) s.sadd(SK(issue_stall_idle), 1);
+      if (live & mine) {
+        s.sadd(SK(issue_stall_idle), 1);
+        classify();
+        s.sadd(SK(issue_distro) + stall_class(mine, valid_m, sbok_m), 1);
+      }
       continue;
     }
     int pick = -1;
@@ -1403,8 +1469,11 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
     s.sched_last[sc] = w;
     if (c.warp_issue_interval > 1) P::one([&] { s.w_issue_ok[w] = now + c.warp_issue_interval; });
     const uint32_t hidx = P::uni((uint32_t)s.w_head[w]);
-    const int u1 = sm_issue_one<P>(s, x, now, sc, w, head.at((int)w), hidx);
+    const TInst in1 = head.at((int)w);
+    const int u1 = sm_issue_one<P>(s, x, now, sc, w, in1, hidx);
     issued_any = true;
+    s.sadd(SK(issue_distro) + 2u + (uint32_t)amin<int>(popc64(in1.mask), kMaxWarpLanes), 1);
+    bool dual = false;
     // dual issue (reference scheduler_unit::cycle, shader.cc:1249-1556): the
     // warp's next buffered instruction issues in the same cycle if it is
     // ready and, with -gpgpu_dual_issue_diff_exec_units, uses another unit
@@ -1416,8 +1485,11 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
           warp_can_issue_i(s, c, (int)w, in2, nsched, P::uni(s.idoc_mask))) {
         sm_issue_one<P>(s, x, now, sc, w, in2, hidx + 1);
         s.sadd(SK(dual_issued), 1);
+        s.sadd(SK(issue_distro) + 2u + (uint32_t)amin<int>(popc64(in2.mask), kMaxWarpLanes), 1);
+        dual = true;
       }
     }
+    s.sadd((dual ? SK(dual_issue) : SK(single_issue)) + sc, 1);
   }
   if (issued_any) s.sadd(SK(busy_cycles), 1);
 }
@@ -1715,13 +1787,18 @@ SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, const KernelTab& kt
 
 // account `k` quiet cycles: exactly what k idle sm_cycle calls would add
 template <class P, class S>
-SIM_HDI void sm_skip(S& s, const SimCfg& c, uint64_t k) {
+SIM_HDI void sm_skip(S& s, const SimCfg& c, uint64_t k, uint64_t t) {
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
   const uint64_t live = P::uni(s.live_mask);
   uint32_t stalled = 0;
+  uint64_t valid_m = 0, sbok_m = 0;
+  if (live) sm_stall_masks<P>(s, c, t, live, valid_m, sbok_m);  // constant over the quiet cycles
   for (uint32_t sc = 0; sc < nsched; ++sc) {
-    if (live & c.sched_mask[sc]) ++stalled;
+    if (live & c.sched_mask[sc]) {
+      ++stalled;
+      s.sadd(SK(issue_distro) + stall_class(c.sched_mask[sc], valid_m, sbok_m), k);
+    }
   }
   // uniform update by every lane (not P::one: on the GPU these fields may be
   // registers of a view, which a one-lane write would leave divergent)

@@ -227,13 +227,19 @@ OpInfo decode_cdna(const std::string& op0) {
     o.space = S_SHARED;
     o.flags = F_MEM;
     o.width = cdna_width(m);
+  } else if (starts(m, "ds_")) {
+    // every other LDS op (min/max/and/or/cmpst/append ...) reads and returns
+    o.cls = OC_LOAD;
+    o.space = S_SHARED;
+    o.flags = F_MEM;
+    o.width = cdna_width(m);
   } else if (starts(m, "s_load") || starts(m, "s_buffer_load")) {
     // scalar memory load (SMEM): through the CU's scalar data cache, counted
     // by lgkmcnt; the trace carries no address (coalesce_kernel keys it)
     o.cls = OC_LOAD;
     o.space = S_CONST;
     o.width = cdna_width(m);
-  } else if (starts(m, "s_memtime") || starts(m, "s_memrealtime")) {
+  } else if (starts(m, "s_memtime") || starts(m, "s_memrealtime") || starts(m, "s_dcache")) {
     o.cls = OC_ALU;
     o.space = S_CONST;
   } else if (m == "s_waitcnt" || starts(m, "s_waitcnt")) {
