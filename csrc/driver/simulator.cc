@@ -1081,6 +1081,29 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
       for (int i = 0; i < 8; ++i) print("gpgpu_n_%s_insn = %llu\n", sqn[i], (unsigned long long)sq[i]);
     }
     print("gpgpu_n_dual_issue = %llu\n", (unsigned long long)dual);
+    {
+      // reference shader_core_stats::print (shader.cc:724-740), cumulative
+      uint64_t dist[3 + kMaxWarpLanes] = {}, si[kMaxSched] = {}, di[kMaxSched] = {};
+      for (auto& st : csm) {
+        for (int i = 0; i < 3 + kMaxWarpLanes; ++i) dist[i] += st.issue_distro[i];
+        for (int i = 0; i < kMaxSched; ++i) {
+          si[i] += st.single_issue[i];
+          di[i] += st.dual_issue[i];
+        }
+      }
+      std::string l = "Stall:" + std::to_string(dist[2]) + "\tW0_Idle:" + std::to_string(dist[0]) +
+                      "\tW0_Scoreboard:" + std::to_string(dist[1]);
+      const uint32_t ws = std::min<uint32_t>(cfg_.warp_size, kMaxWarpLanes);
+      for (uint32_t i = 1; i <= ws; ++i) l += "\tW" + std::to_string(i) + ":" + std::to_string(dist[2 + i]);
+      print("Warp Occupancy Distribution:\n%s\n", l.c_str());
+      std::string a = "single_issue_nums: ", b = "dual_issue_nums: ";
+      const uint32_t ns = std::max<uint32_t>(1, std::min<uint32_t>(cfg_.n_sched, kMaxSched));
+      for (uint32_t i = 0; i < ns; ++i) {
+        a += "WS" + std::to_string(i) + ":" + std::to_string(si[i]) + "\t";
+        b += "WS" + std::to_string(i) + ":" + std::to_string(di[i]) + "\t";
+      }
+      print("%s\n%s\n", a.c_str(), b.c_str());
+    }
     print("gpu_stall_shd_idle_sched = %llu\n", (unsigned long long)stall_idle);
     print("gpgpu_n_stall_shd_mem = %llu\n",
           (unsigned long long)(l1[L1T_GLOBAL_R][L1O_RES_FAIL] + l1[L1T_GLOBAL_W][L1O_RES_FAIL] +

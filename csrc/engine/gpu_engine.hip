@@ -15,9 +15,18 @@
 // reference engine.
 #include <hip/hip_runtime.h>
 
+#include <cerrno>
+#include <csignal>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
+#include <string>
+
+#include <fcntl.h>
+#include <sys/file.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <condition_variable>
 #include <mutex>
 #include <vector>
@@ -298,10 +307,81 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
 
 namespace {
 
+// Machine-wide CU reservation between PROCESSES sharing one GPU (job-level
+// parallelism: several accel-sim.out / bench ranks per card).  A table of
+// (pid, CUs) holders per device in a file under /tmp, guarded by flock; a
+// launch waits until the CUs it needs are free, holders that died are pruned.
+class DeviceCuTable {
+ public:
+  struct Ent {
+    int32_t pid;
+    int32_t cus;
+  };
+  static constexpr int kMax = 256;
+  explicit DeviceCuTable(int dev) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) snprintf(bus, sizeof(bus), "dev%d", dev);
+    for (char* q = bus; *q; ++q)
+      if (*q == ':' || *q == '.') *q = '_';
+    path_ = std::string("/tmp/asim_gpu_cus_") + bus + ".lock";
+    fd_ = open(path_.c_str(), O_RDWR | O_CREAT, 0666);
+    if (fd_ >= 0) (void)fchmod(fd_, 0666);
+  }
+  ~DeviceCuTable() {
+    if (fd_ >= 0) close(fd_);
+  }
+  void acquire(int n, int cap) {
+    if (fd_ < 0) return;  // no shared table: only the in-process pool applies
+    for (int spin = 0;; ++spin) {
+      if (flock(fd_, LOCK_EX) != 0) return;
+      std::vector<Ent> e = load();
+      int used = 0;
+      for (const Ent& x : e) used += x.cus;
+      if (used + n <= cap || e.empty()) {
+        e.push_back(Ent{(int32_t)getpid(), (int32_t)n});
+        store(e);
+        flock(fd_, LOCK_UN);
+        return;
+      }
+      flock(fd_, LOCK_UN);
+      usleep(spin < 100 ? 200 : 2000);
+    }
+  }
+  void release(int n) {
+    if (fd_ < 0 || flock(fd_, LOCK_EX) != 0) return;
+    std::vector<Ent> e = load();
+    for (size_t i = 0; i < e.size(); ++i)
+      if (e[i].pid == (int32_t)getpid() && e[i].cus == n) {
+        e.erase(e.begin() + (long)i);
+        break;
+      }
+    store(e);
+    flock(fd_, LOCK_UN);
+  }
+
+ private:
+  std::vector<Ent> load() {
+    std::vector<Ent> e(kMax);
+    const ssize_t r = pread(fd_, e.data(), sizeof(Ent) * kMax, 0);
+    e.resize(r > 0 ? (size_t)r / sizeof(Ent) : 0);
+    std::vector<Ent> live;
+    for (const Ent& x : e)  // drop holders that no longer exist
+      if (x.pid > 0 && x.cus > 0 && (kill(x.pid, 0) == 0 || errno == EPERM)) live.push_back(x);
+    return live;
+  }
+  void store(const std::vector<Ent>& e) {
+    if (ftruncate(fd_, 0) != 0) return;
+    if (!e.empty()) (void)pwrite(fd_, e.data(), sizeof(Ent) * e.size(), 0);
+  }
+  std::string path_;
+  int fd_ = -1;
+};
+
 // Process-wide CU reservation.  Every simulation needs ALL its blocks
 // co-resident (grid barrier) and each block takes one CU (LDS-bound), so
 // concurrent simulations in one process (job-level parallelism on one GPU)
-// must never oversubscribe the CUs: a launch waits until its CUs are free.
+// must never oversubscribe the CUs: a launch waits until its CUs are free,
+// first in this process, then in the machine-wide table of the device.
 class CuPool {
  public:
   static CuPool& get() {
@@ -310,14 +390,22 @@ class CuPool {
   }
   void init(int cus) {
     std::lock_guard<std::mutex> g(mu_);
-    if (cap_ == 0) cap_ = free_ = cus;
+    if (cap_ == 0) {
+      cap_ = free_ = cus;
+      int dev = 0;
+      if (hipGetDevice(&dev) == hipSuccess) table_.reset(new DeviceCuTable(dev));
+    }
   }
   void acquire(int n) {
-    std::unique_lock<std::mutex> g(mu_);
-    cv_.wait(g, [&] { return free_ >= n; });
-    free_ -= n;
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      cv_.wait(g, [&] { return free_ >= n; });
+      free_ -= n;
+    }
+    if (table_) table_->acquire(n, cap_);
   }
   void release(int n) {
+    if (table_) table_->release(n);
     {
       std::lock_guard<std::mutex> g(mu_);
       free_ += n;
@@ -333,6 +421,7 @@ class CuPool {
   std::mutex mu_;
   std::condition_variable cv_;
   int cap_ = 0, free_ = 0;
+  std::unique_ptr<DeviceCuTable> table_;
 };
 
 class GpuEngine : public Engine {

@@ -22,7 +22,9 @@ bash $R/tools/gpu_trace_and_time.sh || exit 1
 SUITE=${SUITE:-rodinia_2.0-ft-hip}
 export SUITE
 if [ "${ENG:-GPU}" = GPU ]; then CFG=MI355X_TUNED-GPU; SLOTS="-g 1 -c 8"; else CFG=MI355X_TUNED; SLOTS="-c 10 --threads 2"; fi
-export PROCMAN_STATE=$out/procman.json ASIM_JOB_LOGDIR=$out/logs
+# one GPU-engine simulation per GPU at a time: an MI355X-config simulation
+# occupies all 256 CUs (the engine also serialises launches across processes)
+export PROCMAN_STATE=$out/procman.json ASIM_JOB_LOGDIR=$out/logs PROCMAN_PER_GPU=1
 JL=$R/util/job_launching
 timeout -k 10 300 python $JL/run_simulations.py -B $SUITE -C $CFG -T $out/traces -N corr -l local \
   -r $out/simrun $SLOTS > $out/launch.log 2>&1 || { echo "launch failed"; tail $out/launch.log; exit 1; }
