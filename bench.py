@@ -204,6 +204,12 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(kips / BASELINE_KIPS, 3),
+            # not like-for-like: the baseline is GPGPU-Sim on one CPU core on
+            # recorded QV100 heartwall traces (util/job_launching/README.md:77);
+            # this run is this simulator on synthetic suite-shaped traces
+            "vs_baseline_note": "not like-for-like: reference = GPGPU-Sim, 1 CPU core, recorded heartwall "
+                                "traces (349 KIPS); this = MI355X-native simulator, synthetic Rodinia-2.0-ft-"
+                                "shaped traces, engine placement in config.engine",
             "dtype": "n/a (integer cycle-level model)",
             "data": "synthetic (seeded Rodinia-2.0-ft-shaped SASS traces; no recorded traces available)",
             "config": {
