@@ -110,7 +110,51 @@ def main(argv=None) -> int:
         # launch into an idle queue (pathfinder), see profiles/ubench_mi355x
         print(f"# rocprof_queued_launch_ns {qa:.1f}")
         print(f"# queued_launch_cycles {int(round(qa * mhz / 1000.0))}  (-gpgpu_kernel_launch_latency_queued)")
+    # launches into an idle queue after a host gap (no event in between)
+    idle = read_durations(run_dir, "ub_empty_idle")
+    if idle:
+        for nb in sorted(idle):
+            d = idle[nb]
+            print(f"idle empty kernel {nb:6d} workgroups: median {np.median(d):8.0f} ns  min {min(d):8.0f} ns  (n={len(d)})")
+        ia, ib = fit(idle)
+        print(f"# rocprof_idle_launch_ns {ia:.1f}")
+        print(f"# rocprof_idle_per_block_ns {ib:.4f}")
+        print(f"# idle_launch_cycles {int(round(ia * mhz / 1000.0))}")
+    # back-to-back chains: steady-state start-to-start interval and duration
+    ch = chain_stats(run_dir)
+    if ch:
+        print(f"# chain_start_interval_ns {ch[0]:.1f}")
+        print(f"# chain_duration_ns {ch[1]:.1f}")
+        print(f"# chain_gap_ns {ch[2]:.1f}")
     return 0
+
+
+def chain_stats(run_dir: str, name_sub: str = "ub_empty_chain"):
+    """(median start-to-start interval, median duration, median end-to-start
+    gap) over the back-to-back chain dispatches, skipping each chain's first
+    four (the queue fills)."""
+    rows = []
+    for f in glob.glob(os.path.join(run_dir, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if name_sub in row.get("Kernel_Name", ""):
+                    rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+    if len(rows) < 16:
+        return None
+    rows.sort()
+    iv, du, gp = [], [], []
+    run = 0
+    for i, (s, e) in enumerate(rows):
+        if i and s - rows[i - 1][1] > 20000:  # a new chain (30 us host gap)
+            run = 0
+        if i and run >= 4:
+            iv.append(s - rows[i - 1][0])
+            gp.append(s - rows[i - 1][1])
+            du.append(e - s)
+        run += 1
+    if not iv:
+        return None
+    return float(np.median(iv)), float(np.median(du)), float(np.median(gp))
 
 
 if __name__ == "__main__":

@@ -543,7 +543,7 @@ def _mi355x() -> Dict[str, str]:
         "-gpgpu_cache:il1": "N:64:128:4,L:R:f:N:L,S:8:64,4",
         "-gpgpu_l1_latency": "120",
         "-gpgpu_smem_latency": "64",
-        "-gpgpu_cache:dl2": "S:128:128:8,L:B:m:L:P,A:192:4,32:0,32",
+        "-gpgpu_cache:dl2": "S:128:128:16,L:B:m:L:P,A:192:4,32:0,32",  # 4 MiB per XCD: 16 x 256 KB
         # L2 hit = per-XCD L2 (~207 cycles), L2 miss = Infinity Cache (~540)
         "-gpgpu_l2_rop_latency": "75",
         "-dram_latency": "333",

@@ -129,9 +129,34 @@ def _l1_hit_rate(d):
 
 
 def _l2_hit_rate(d):
-    h = d[S_L2 % ("GLOBAL_ACC_R", "HIT")] + d[S_L2 % ("GLOBAL_ACC_W", "HIT")]
-    m = d[r"L2_total_cache_misses\s*=\s*(.*)"]
+    h = _l2_hits(d)
+    m = _l2_misses(d)
     return h / (h + m) if h + m else float("nan")
+
+
+# gfx950's TCC counts every write as a hit: a write allocates its bytes in the
+# write-back L2 without fetching the line (byte-masked dirty data), so only
+# reads and atomics miss (per app, TCC_HIT + TCC_MISS == TCC_READ + TCC_WRITE
+# + TCC_ATOMIC, and TCC_MISS matches the read misses).  The simulator's
+# lazy-fetch write allocation ('L' policy) is the same operation, which the
+# GPGPU-Sim breakdown files as a write miss; the correlator therefore puts the
+# simulator's writes on the hit side and its read / atomic misses on the miss
+# side, with the reads merged into a pending miss.
+_L2_R_HIT = S_L2 % ("GLOBAL_ACC_R", "HIT")
+_L2_W_ALL = S_L2 % ("GLOBAL_ACC_W", "TOTAL_ACCESS")
+_L2_R_MISS = S_L2 % ("GLOBAL_ACC_R", "MISS")
+_L2_A_MISS = S_L2 % ("GLOBAL_ATOMIC", "MISS")
+_L2_R_MSHR = S_L2 % ("GLOBAL_ACC_R", "MSHR_HIT")
+
+
+def _l2_hits(d):
+    return d[_L2_R_HIT] + d[_L2_W_ALL]
+
+
+def _l2_misses(d):
+    # a read merged into a pending miss (the simulator's MSHR hit) waits for
+    # the same fill: TCC counts it as a miss
+    return d[_L2_R_MISS] + d[_L2_R_MSHR] + d.get(_L2_A_MISS, 0.0)
 
 
 # Sim statistic <-> MI355X rocprofv3 counter mappings (the reference's
@@ -173,12 +198,11 @@ CORREL_STATS: List[CorrelStat] = [
     CorrelStat("L2 write accesses", S_L2 % ("GLOBAL_ACC_W", "TOTAL_ACCESS"), _hw("TCC_WRITE_sum"), "l2-writes"),
     CorrelStat("L2 atomic accesses", S_L2 % ("GLOBAL_ATOMIC", "TOTAL_ACCESS"), _hw("TCC_ATOMIC_sum"), "l2-atomics"),
     CorrelStat("L2 hits", "l2_hits", _hw("TCC_HIT_sum"), "l2-hits",
-               sim_stats=(S_L2 % ("GLOBAL_ACC_R", "HIT"), S_L2 % ("GLOBAL_ACC_W", "HIT")),
-               sim_eval=lambda d: sum(d.values())),
-    CorrelStat("L2 misses", r"L2_total_cache_misses\s*=\s*(.*)", _hw("TCC_MISS_sum"), "l2-misses"),
+               sim_stats=(_L2_R_HIT, _L2_W_ALL), sim_eval=_l2_hits),
+    CorrelStat("L2 misses", "l2_misses", _hw("TCC_MISS_sum"), "l2-misses",
+               sim_stats=(_L2_R_MISS, _L2_R_MSHR), sim_eval=_l2_misses),
     CorrelStat("L2 hit rate", "l2_hit_rate", _hw_ratio(("TCC_HIT_sum",), ("TCC_HIT_sum", "TCC_MISS_sum")),
-               "l2-hit-rate", sim_stats=(S_L2 % ("GLOBAL_ACC_R", "HIT"), S_L2 % ("GLOBAL_ACC_W", "HIT"),
-                                          r"L2_total_cache_misses\s*=\s*(.*)"),
+               "l2-hit-rate", sim_stats=(_L2_R_HIT, _L2_R_MSHR, _L2_W_ALL, _L2_R_MISS),
                sim_eval=_l2_hit_rate, ratio=True, log=False),
     CorrelStat("DRAM read requests", r"total dram reads\s*=\s*(.*)", _hw("TCC_EA0_RDREQ_sum"), "dram-reads"),
     CorrelStat("DRAM write requests", r"total dram writes\s*=\s*(.*)", _hw("TCC_EA0_WRREQ_sum"), "dram-writes"),

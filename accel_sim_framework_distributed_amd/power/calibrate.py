@@ -233,3 +233,94 @@ def apply_factors(xml_in: str, xml_out: str, x: Sequence[float], components: Seq
             p[k] = p.get(k, 1.0) * float(f)
     write_xml(xml_out, p, comment=f"calibrated from {xml_in}")
     return p
+
+
+# ---- DVFS-aware calibration (round 3) ---------------------------------------
+# The power model runs a kernel at core clock ratio s = f / f_nominal with the
+# rail voltage V(s)/V(1) = v_floor + (1 - v_floor) s (csrc/power/power.cc):
+# core dynamic power ~ s V^2, static and idle-core power ~ V, DRAM ~ s (its own
+# rail), the constant term fixed.  A row of A holds a kernel's component powers
+# simulated at the nominal clock; dvfs_scale() maps it to clock ratio s.
+_DVFS_V = ("STATICP", "IDLE_COREP")
+_DVFS_FIXED = ("CONSTP",)
+_DVFS_S = ("DRAMP", "MCP")
+
+
+def voltage_ratio(s, v_floor: float):
+    return v_floor + (1.0 - v_floor) * np.asarray(s, np.float64)
+
+
+def dvfs_scale(s: float, v_floor: float, components: Sequence[str] = COMPONENTS) -> np.ndarray:
+    v = float(voltage_ratio(s, v_floor))
+    return np.array([1.0 if c in _DVFS_FIXED else v if c in _DVFS_V else s if c in _DVFS_S else s * v * v
+                     for c in components])
+
+
+def dvfs_matrix(A: np.ndarray, ratios: Sequence[float], v_floor: float) -> np.ndarray:
+    A = np.asarray(A, np.float64)
+    return np.stack([A[i] * dvfs_scale(float(r), v_floor) for i, r in enumerate(ratios)])
+
+
+def fit_groups_relative(A: np.ndarray, b: np.ndarray, groups: Dict[str, List[str]] = FINE_GROUPS,
+                        **kw) -> np.ndarray:
+    """Group factors minimising the RELATIVE error (MAPE is the reported
+    metric): rows scaled by 1 / measured power, target all ones."""
+    A = np.asarray(A, np.float64)
+    b = np.asarray(b, np.float64)
+    return fit_groups(A / b[:, None], np.ones(len(b)), groups=groups, **kw)
+
+
+def governor_ratio(a_row: np.ndarray, x: np.ndarray, cap: float, v_floor: float, s_min: float = 0.5) -> float:
+    """The DVFS governor of csrc/power/power.cc (dvfs_clock_ratio) on one
+    kernel: the highest clock ratio in [s_min, 1] whose power fits the cap."""
+    p = lambda s: float(a_row @ (x * dvfs_scale(s, v_floor)))
+    if cap <= 0 or p(1.0) <= cap:
+        return 1.0
+    lo, hi = s_min, 1.0
+    if p(lo) >= cap:
+        return lo
+    for _ in range(40):
+        m = 0.5 * (lo + hi)
+        if p(m) <= cap:
+            lo = m
+        else:
+            hi = m
+    return lo
+
+
+def leave_one_out_dvfs(A: np.ndarray, b: np.ndarray, ratios: Sequence[float], v_floor: float, cap: float,
+                       s_min: float = 0.5, **kw) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Leave-one-out over the kernels with the DVFS model.  Each fold fits the
+    group factors on the other kernels at their MEASURED clocks, then
+    predicts the held-out kernel (a) at its measured clock and (b) at the
+    clock the governor picks under the measured cap.  Returns (power at the
+    measured clock, power under the governor, governor clock ratios)."""
+    A = np.asarray(A, np.float64)
+    b = np.asarray(b, np.float64)
+    r = np.asarray(ratios, np.float64)
+    n = len(b)
+    at_meas, at_gov, s_gov = np.zeros(n), np.zeros(n), np.zeros(n)
+    Ad = dvfs_matrix(A, r, v_floor)
+    for i in range(n):
+        keep = np.arange(n) != i
+        x = fit_groups_relative(Ad[keep], b[keep], **kw)
+        at_meas[i] = Ad[i] @ x
+        s_gov[i] = governor_ratio(A[i], x, cap, v_floor, s_min)
+        at_gov[i] = A[i] @ (x * dvfs_scale(s_gov[i], v_floor))
+    return at_meas, at_gov, s_gov
+
+
+def v_floor_from_measurements(sclk_mhz: Sequence[float], mv: Sequence[float], max_sclk: float) -> Optional[float]:
+    """V(s)/V(1) = v_floor + (1 - v_floor) s from measured (clock, rail
+    voltage) pairs: a line fitted through them, evaluated at s = 0.  None
+    when fewer than 3 distinct clocks carry a voltage reading."""
+    f = np.asarray(sclk_mhz, np.float64)
+    v = np.asarray(mv, np.float64)
+    ok = np.isfinite(f) & np.isfinite(v) & (v > 0)
+    if ok.sum() < 3 or np.ptp(f[ok]) < 50.0:
+        return None
+    slope, icpt = np.polyfit(f[ok], v[ok], 1)
+    v1 = icpt + slope * max_sclk
+    if v1 <= 0:
+        return None
+    return float(min(0.95, max(0.0, icpt / v1)))

@@ -21,10 +21,11 @@ from __future__ import annotations
 import argparse
 import csv
 import json
+import math
 import os
 import sys
 import tempfile
-from typing import Dict, List
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -117,6 +118,32 @@ def measured_power(path: str = MEASURED) -> Dict[str, float]:
                 except ValueError:
                     pass
     return out
+
+
+def measured_rows(path: str) -> Tuple[Dict[str, Dict[str, float]], Dict[str, float]]:
+    """power_suite measure output: {kernel: {w, sclk, mv, temp}} in launch
+    order, and the '# key value' header lines (power_cap_w, max_sclk_mhz)."""
+    rows: Dict[str, Dict[str, float]] = {}
+    meta: Dict[str, float] = {}
+
+    def num(x):
+        try:
+            return float(x)
+        except ValueError:
+            return float("nan")
+    with open(path) as f:
+        for line in f:
+            if line.startswith("#"):
+                t = line[1:].split()
+                if len(t) == 2:
+                    meta[t[0]] = num(t[1])
+                continue
+            row = next(csv.reader([line]))
+            if len(row) >= 2 and row[0] and not math.isnan(num(row[1])):
+                rows[row[0]] = dict(w=num(row[1]), sclk=num(row[5]) if len(row) > 5 else float("nan"),
+                                    mv=num(row[6]) if len(row) > 6 else float("nan"),
+                                    temp=num(row[7]) if len(row) > 7 else float("nan"))
+    return rows, meta
 
 
 def simulate_power(work: str, xml: str, kernels: Dict[str, KernelBuilder]) -> Dict[str, Dict]:
@@ -274,11 +301,73 @@ def run_traces(kernelslist: str, measured_csv: str, work: str, out_xml: str, con
         raise RuntimeError(f"{len(reps)} simulated kernels vs {len(order)} measured")
     A = calibrate.design_matrix(reps)
     b = np.array([meas[n] for n in order])
-    s = fit_report(A, b, order, bound)
-    calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
+    rows, meta = measured_rows(measured_csv)
+    if all(not math.isnan(rows[n]["sclk"]) for n in order) and meta.get("power_cap_w", float("nan")) > 0:
+        s = fit_report_dvfs(A, b, order, [rows[n]["sclk"] for n in order], [rows[n]["mv"] for n in order],
+                            meta["power_cap_w"], meta.get("max_sclk_mhz", float("nan")), bound)
+        calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
+        _set_dvfs_params(out_xml, s)
+    else:
+        s = fit_report(A, b, order, bound)
+        calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
     s.update(sim_cycles=[r.get("gpu_sim_cycle", 0.0) for r in reps], traces="automatic ISA traces (isatrace)",
              xml=out_xml)
     return s
+
+
+def _set_dvfs_params(xml: str, s: Dict) -> None:
+    p = xmlcfg.read_xml(xml)
+    p["dvfs_v_floor"] = float(s["v_floor"])
+    p["dvfs_min_clock_ratio"] = float(s["dvfs_min_clock_ratio"])
+    xmlcfg.write_xml(xml, p, comment="calibrated with measured clocks; power_cap measured by amd-smi")
+
+
+DEFAULT_V_FLOOR = 0.6
+
+
+def fit_report_dvfs(A: np.ndarray, b: np.ndarray, order: List[str], sclk: List[float], mv: List[float],
+                    cap: float, max_sclk: float, bound: float = 20.0, v_floor: Optional[float] = None) -> Dict:
+    """Validation with the DVFS model and MEASURED inputs only: the package
+    power limit and every kernel's graphics clock come from amd-smi
+    (power_suite measure); V(f) from the measured rail voltages when the
+    firmware reports them.  The FINE_GROUPS factors are fitted on relative
+    error with each kernel's components moved to its measured clock;
+    leave-one-out predicts the held-out kernel both at its measured clock
+    (the headline, like AccelWattch's validation with measured voltage) and
+    fully predictively, at the clock the governor picks under the cap."""
+    sclk = np.asarray(sclk, np.float64)
+    fmax = max_sclk if max_sclk and not math.isnan(max_sclk) else float(np.nanmax(sclk))
+    ratios = np.clip(sclk / fmax, 0.05, 1.0)
+    vsrc = "given"
+    if v_floor is None:
+        v_floor = calibrate.v_floor_from_measurements(sclk, mv, fmax)
+        vsrc = "measured rail voltage vs clock"
+        if v_floor is None:
+            v_floor, vsrc = DEFAULT_V_FLOOR, "assumed (no rail voltage reported by amd-smi)"
+    s_min = float(max(0.3, min(1.0, np.nanmin(ratios) * 0.9)))
+    kw = dict(groups=calibrate.FINE_GROUPS, lower=1.0 / bound, upper=bound)
+    Ad = calibrate.dvfs_matrix(A, ratios, v_floor)
+    x = calibrate.fit_groups_relative(Ad, b, **kw)
+    fit = Ad @ x
+    loo_meas, loo_gov, s_gov = calibrate.leave_one_out_dvfs(A, b, ratios, v_floor, cap, s_min, **kw)
+    gov_fit = np.array([calibrate.governor_ratio(A[i], x, cap, v_floor, s_min) for i in range(len(b))])
+    gf = calibrate.group_factors(x, calibrate.FINE_GROUPS)
+    at_bound = [g for g, v in gf.items() if v <= 1.0 / bound * 1.001 or v >= bound * 0.999]
+    before = A.sum(axis=1)
+    return dict(kernels=list(order), measured_w=b.tolist(), uncalibrated_w=before.tolist(), calibrated_w=fit.tolist(),
+                loo_w=loo_meas.tolist(), mape_uncalibrated=calibrate.mape(before, b)[0],
+                mape_in_sample=calibrate.mape(fit, b)[0], mape_leave_one_out=calibrate.mape(loo_meas, b)[0],
+                mae_leave_one_out_w=calibrate.mape(loo_meas, b)[1], group_factors=gf, factors_at_bound=at_bound,
+                power_cap_w=float(cap), power_cap_source="measured (amd-smi power cap)", max_sclk_mhz=float(fmax),
+                measured_sclk_mhz=sclk.tolist(), measured_clock_ratio=ratios.tolist(),
+                measured_vddgfx_mv=[float(v) for v in mv], v_floor=float(v_floor), v_floor_source=vsrc,
+                dvfs_min_clock_ratio=s_min,
+                governor=dict(loo_w=loo_gov.tolist(), mape_leave_one_out=calibrate.mape(loo_gov, b)[0],
+                              loo_clock_ratio=s_gov.tolist(), fit_clock_ratio=gov_fit.tolist(),
+                              clock_ratio_mae=float(np.mean(np.abs(s_gov - ratios))),
+                              throttled_kernels=[n for n, r in zip(order, ratios) if r < 0.98]),
+                components=list(calibrate.COMPONENTS), components_w=np.asarray(A).tolist(),
+                bounds=[1.0 / bound, bound], model="DVFS: measured cap and clocks, V(f) line", _x=x)
 
 
 def fit_report(A: np.ndarray, b: np.ndarray, order: List[str], bound: float = 20.0) -> Dict:
@@ -314,9 +403,15 @@ def refit(json_path: str, out_xml: str, config_dir: str = TUNED, bound: float = 
         old = json.load(f)
     A = np.asarray(old["components_w"], np.float64)
     b = np.asarray(old["measured_w"], np.float64)
-    s = fit_report(A, b, old["kernels"], bound)
     base_xml = os.path.join(config_dir, "accelwattch_sass_sim.xml")
-    calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
+    if "measured_sclk_mhz" in old:
+        s = fit_report_dvfs(A, b, old["kernels"], old["measured_sclk_mhz"], old.get("measured_vddgfx_mv", []),
+                            old["power_cap_w"], old.get("max_sclk_mhz", float("nan")), bound)
+        calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
+        _set_dvfs_params(out_xml, s)
+    else:
+        s = fit_report(A, b, old["kernels"], bound)
+        calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
     for k in ("sim_cycles", "traces", "note"):
         if k in old:
             s[k] = old[k]
@@ -352,6 +447,11 @@ def main(argv=None) -> int:
           f"leave-one-out {s['mape_leave_one_out']:.2f}% ({s['mae_leave_one_out_w']:.1f} W)")
     print("group factors:", {g: round(v, 3) for g, v in s["group_factors"].items()},
           "at bound:", s.get("factors_at_bound"), "power cap:", s.get("power_cap_w"))
+    if "governor" in s:
+        g = s["governor"]
+        print(f"DVFS: measured cap {s['power_cap_w']:.0f} W, v_floor {s['v_floor']:.3f} ({s['v_floor_source']}); "
+              f"governor-predicted LOO MAPE {g['mape_leave_one_out']:.2f}%, clock-ratio MAE {g['clock_ratio_mae']:.3f}, "
+              f"throttled: {g['throttled_kernels']}")
     return 0
 
 

@@ -36,7 +36,8 @@ def parse_power_report(path_or_text: str) -> List[Dict[str, float]]:
         except ValueError:
             continue
         if k in ("kernel_launch_uid", "gpu_sim_cycle", "kernel_avg_power", "kernel_max_power", "kernel_min_power",
-                 "gpu_tot_avg_power", "gpu_tot_max_power", "gpu_tot_min_power", "gpu_avg_threads_per_warp"):
+                 "gpu_tot_avg_power", "gpu_tot_max_power", "gpu_tot_min_power", "gpu_avg_threads_per_warp",
+                 "kernel_avg_clock_ratio"):
             cur[k] = x
         elif k.startswith("gpu_avg_"):
             n = k[8:]

@@ -77,12 +77,15 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
         raise ValueError(f"micro-benchmarks printed unknown options: {bad}")
     cfg = presets.get_preset(base)
     notes = []
-    # the cycle model's per-sub-partition L2 capacity is a compile-time limit
-    # (its tag arrays live in LDS on the GPU engine): keep the geometry,
-    # reduce the set count to fit and say so
+    # the cycle model's per-channel L2 capacity is a compile-time limit (its
+    # tag arrays live in LDS on the GPU engine; the sub-partitions of a
+    # channel share it): keep the geometry, reduce the set count to fit and
+    # say so
     if "-gpgpu_cache:dl2" in opts:
         from .. import _native
-        max_lines = int(_native.load().limits["l2_lines"])
+        per_ch = int(opts.get("-gpgpu_n_sub_partition_per_mchannel",
+                              cfg.get("-gpgpu_n_sub_partition_per_mchannel", "1")))
+        max_lines = int(_native.load().limits["l2_lines_per_channel"]) // max(1, per_ch)
         head, rest = opts["-gpgpu_cache:dl2"].split(",", 1)
         f = head.split(":")
         sets, assoc = int(f[1]), int(f[3])

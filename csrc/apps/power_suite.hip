@@ -1,14 +1,16 @@
 // UB_LIBS: -lamd_smi -lpthread
 // Power validation suite (reference util/accelwattch: the AccelWattch
 // validation micro-benchmarks + accelwattch_hw_profiler/measureGpuPower.cpp
-// and hw_power_validation_volta.csv): 24 kernels spanning VALU fp32 / int /
+// and hw_power_validation_volta.csv): 30 kernels spanning VALU fp32 / int /
 // fp64, transcendental, MFMA, LDS, L1-, L2- and HBM-resident traffic, atomics,
-// mixes of them and four occupancy levels, plus idle.
+// mixes of them and several occupancy levels, plus idle.
 //
 //   power_suite measure [seconds]   every kernel back to back for `seconds`
 //                                   while a host thread samples socket power
 //                                   through amd-smi every 10 ms; prints the CSV
-//                                   ",mean HW_power,st_dev,var,#samples"
+//                                   ",mean HW_power,st_dev,var,#samples" plus
+//                                   the mean graphics clock, rail voltage and
+//                                   hotspot temperature, after the power limit"
 //   power_suite trace               every kernel once, at the same grid with a
 //                                   short loop (power is a rate), for the
 //                                   automatic ISA tracer (bin/isatrace/power_suite)
@@ -235,12 +237,59 @@ struct Sampler {
       }
     }
   }
-  double watts() const {
+  struct Sample {
+    double w = NAN, sclk = NAN, mv = NAN, temp = NAN;
+  };
+  // one reading of socket power, the graphics clock (mean over the XCDs that
+  // report one), the graphics rail voltage and the hotspot temperature; a
+  // field the firmware does not report stays NaN
+  Sample read() const {
+    Sample r;
+    if (!ok) return r;
     amdsmi_power_info_t pi;
-    if (!ok || amdsmi_get_power_info(h, &pi) != AMDSMI_STATUS_SUCCESS) return NAN;
-    if (pi.current_socket_power != UINT32_MAX && pi.current_socket_power) return pi.current_socket_power;
-    if (pi.average_socket_power != UINT32_MAX && pi.average_socket_power) return pi.average_socket_power;
-    return (double)pi.socket_power;
+    if (amdsmi_get_power_info(h, &pi) == AMDSMI_STATUS_SUCCESS) {
+      if (pi.current_socket_power != UINT32_MAX && pi.current_socket_power) r.w = pi.current_socket_power;
+      else if (pi.average_socket_power != UINT32_MAX && pi.average_socket_power) r.w = pi.average_socket_power;
+      else r.w = (double)pi.socket_power;
+    }
+    amdsmi_gpu_metrics_t m;
+    if (amdsmi_get_gpu_metrics_info(h, &m) == AMDSMI_STATUS_SUCCESS) {
+      double sum = 0;
+      int n = 0;
+      for (int i = 0; i < AMDSMI_MAX_NUM_GFX_CLKS; ++i)
+        if (m.current_gfxclks[i] != UINT16_MAX && m.current_gfxclks[i]) {
+          sum += m.current_gfxclks[i];
+          ++n;
+        }
+      if (n) r.sclk = sum / n;
+      else if (m.current_gfxclk != UINT16_MAX && m.current_gfxclk) r.sclk = m.current_gfxclk;
+      else if (m.average_gfxclk_frequency != UINT16_MAX && m.average_gfxclk_frequency) r.sclk = m.average_gfxclk_frequency;
+      if (m.voltage_gfx != UINT16_MAX && m.voltage_gfx) r.mv = m.voltage_gfx;
+      if (m.temperature_hotspot != UINT16_MAX && m.temperature_hotspot) r.temp = m.temperature_hotspot;
+    }
+    if (std::isnan(r.sclk)) {
+      amdsmi_clk_info_t ci;
+      if (amdsmi_get_clock_info(h, AMDSMI_CLK_TYPE_GFX, &ci) == AMDSMI_STATUS_SUCCESS && ci.clk) r.sclk = ci.clk;
+    }
+    if (std::isnan(r.mv)) {
+      int64_t v = 0;
+      if (amdsmi_get_gpu_volt_metric(h, AMDSMI_VOLT_TYPE_VDDGFX, AMDSMI_VOLT_CURRENT, &v) == AMDSMI_STATUS_SUCCESS && v > 0)
+        r.mv = (double)v;
+    }
+    return r;
+  }
+  double watts() const { return read().w; }
+  // the package power limit in W (the firmware's PPT) and the highest
+  // graphics clock in MHz; NaN when not reported
+  double power_cap_w() const {
+    amdsmi_power_cap_info_t ci;
+    if (!ok || amdsmi_get_power_cap_info(h, 0, &ci) != AMDSMI_STATUS_SUCCESS || !ci.power_cap) return NAN;
+    return ci.power_cap > 100000 ? ci.power_cap / 1e6 : (double)ci.power_cap;  // uW on bare metal, W on a host
+  }
+  double max_sclk() const {
+    amdsmi_clk_info_t ci;
+    if (!ok || amdsmi_get_clock_info(h, AMDSMI_CLK_TYPE_GFX, &ci) != AMDSMI_STATUS_SUCCESS || !ci.max_clk) return NAN;
+    return ci.max_clk;
   }
   ~Sampler() {
     if (ok) amdsmi_shut_down();
@@ -308,6 +357,13 @@ int main(int argc, char** argv) {
       {"fp64_hbm_mix", [&] { k_fp64_read<<<g(16), b>>>(buf, nbig, 4, sink); }},
       {"atomic_l2", [&] { k_atomic<<<g(4), b>>>(ctr, trace ? 2 : sc / 8); }},
       {"fp32_fma_light", [&] { k_fp32<<<g(8), b>>>(sink, sc); }},
+      // round 3: more occupancy / unit-mix points between the saturating ones
+      {"mfma_bf16_occ4", [&] { k_mfma<<<g(4), b>>>(sink, 2 * sc); }},
+      {"sfu_occ2", [&] { k_sfu<<<g(2), b>>>(sink, 8 * sc); }},
+      {"fp64_fma_occ2", [&] { k_fp64<<<g(2), b>>>(sink, 4 * sc); }},
+      {"hbm_read_occ2", [&] { k_read<<<g(2), b>>>(buf, nbig, trace ? 1 : 4, sink); }},
+      {"l2_write", [&] { k_write<<<g(8), b>>>(buf, l2 / 16, trace ? 2 : 2 * sc); }},
+      {"lds_read_occ2", [&] { k_lds_read<<<g(2), b>>>(sink, 16 * sc); }},
   };
   if (trace) {
     for (auto& k : ks) {
@@ -322,16 +378,19 @@ int main(int argc, char** argv) {
       printf("# amd-smi power sampling unavailable on this node; nothing measured\n");
       return 0;
     }
-    printf(",mean HW_power,st_dev,var,#samples\n");
+    // the power limit and the top graphics clock, once: the DVFS model's
+    // measured inputs (power/mi355x_validation.py)
+    printf("# power_cap_w %.1f\n# max_sclk_mhz %.0f\n", smi.power_cap_w(), smi.max_sclk());
+    printf(",mean HW_power,st_dev,var,#samples,sclk_mhz,vddgfx_mv,hotspot_c\n");
     for (auto& k : ks) {
       k.launch();
       APP_HIP(hipDeviceSynchronize());
       std::atomic<bool> stop{false};
-      std::vector<double> samples;
+      std::vector<Sampler::Sample> samples;
       std::thread th([&] {
         while (!stop.load()) {
-          const double w = smi.watts();
-          if (!std::isnan(w)) samples.push_back(w);
+          const Sampler::Sample r = smi.read();
+          if (!std::isnan(r.w)) samples.push_back(r);
           std::this_thread::sleep_for(std::chrono::milliseconds(10));
         }
       });
@@ -345,11 +404,23 @@ int main(int argc, char** argv) {
       const size_t skip = samples.size() / 4;  // ramp-up
       double m = 0, v = 0;
       const size_t n = samples.size() - skip;
-      for (size_t i = skip; i < samples.size(); ++i) m += samples[i];
+      for (size_t i = skip; i < samples.size(); ++i) m += samples[i].w;
       m = n ? m / n : NAN;
-      for (size_t i = skip; i < samples.size(); ++i) v += (samples[i] - m) * (samples[i] - m);
+      for (size_t i = skip; i < samples.size(); ++i) v += (samples[i].w - m) * (samples[i].w - m);
       v = n > 1 ? v / (n - 1) : 0;
-      printf("%s,%.4f,%.4f,%.4f,%zu\n", k.name, m, std::sqrt(v), v, n);
+      // means of the reported fields (NaN when the firmware reports none)
+      auto mean_of = [&](double Sampler::Sample::*f) {
+        double a = 0;
+        size_t c = 0;
+        for (size_t i = skip; i < samples.size(); ++i)
+          if (!std::isnan(samples[i].*f)) {
+            a += samples[i].*f;
+            ++c;
+          }
+        return c ? a / c : NAN;
+      };
+      printf("%s,%.4f,%.4f,%.4f,%zu,%.1f,%.1f,%.1f\n", k.name, m, std::sqrt(v), v, n, mean_of(&Sampler::Sample::sclk),
+             mean_of(&Sampler::Sample::mv), mean_of(&Sampler::Sample::temp));
       fflush(stdout);
     }
   }

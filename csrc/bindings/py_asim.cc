@@ -156,7 +156,7 @@ PYBIND11_MODULE(_asim, m) {
     lim["max_cta"] = kMaxCta;
     lim["l1_lines"] = kMaxL1Lines;
     lim["l1_mshr"] = kMaxL1Mshr;
-    lim["l2_lines"] = kMaxL2Lines;
+    lim["l2_lines_per_channel"] = kMaxL2LinesCh;
     lim["l2_mshr"] = kMaxL2Mshr;
     lim["sm_total"] = kMaxSmTot;
     lim["sub_total"] = kMaxSubTot;

@@ -240,7 +240,10 @@ const OptDef kOptions[] = {
     {"-hw_perf_file_name", 's', "hw_perf.csv", ""},
     {"-hw_perf_bench_name", 's', "", ""},
     {"-power_simulation_mode", 'i', "0", "0 SIM, 1 HW, 2 HYBRID"},
-    {"-dvfs_enabled", 'b', "0", ""},
+    {"-dvfs_enabled", 'b', "0",
+     "DVFS governor: with a power_cap in the power XML, run the core below its nominal clock (and voltage) when a "
+     "sample's power exceeds the cap; the slower clock lengthens simulated time"},
+    {"-dvfs_min_clock_ratio", 'f', "0.5", "lowest core clock / nominal the DVFS governor may choose"},
     {"-aggregate_power_stats", 'b', "0", ""},
     {"-accelwattch_hybrid_perfsim_L1_RH", 'b', "0", ""},
     {"-accelwattch_hybrid_perfsim_L1_RM", 'b', "0", ""},
@@ -291,6 +294,9 @@ const OptDef kOptions[] = {
     {"-sim_mall", 's', "none",
      "memory-attached last-level cache (Infinity Cache) per DRAM channel: <sets>:<assoc> of 128 B sectored lines, or none"},
     {"-sim_mall_miss_latency", 'u', "0", "extra core cycles of an HBM access over a MALL hit"},
+    {"-sim_l2_kernel_release", 'b', "0",
+     "at the end of every kernel write the L2s' dirty sectors back to memory (the MALL if any) and invalidate them "
+     "(the release / acquire of a multi-XCD GPU, whose XCD L2s are not coherent with each other)"},
     {"-sim_cpu_threads", 'u', "1", "CPU engine: OpenMP threads over the units of one epoch (1 = serial; "
                                   "run simulations job-parallel instead)"},
     {"-collective_slice_bytes", 'u', "131072", "packet model: bytes per link packet (RCCL slice)"},
@@ -805,8 +811,10 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.ldst_resp_buf = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)r.getu("-gpgpu_n_ldst_response_buffer_size"), kLdstRespQ));
   // memory partition
   c.l2 = parse_cache_geom(r.gets("-gpgpu_cache:dl2"));
-  if (!c.l2.disabled && (uint64_t)c.l2.nsets * c.l2.assoc > (uint64_t)kMaxL2Lines)
-    throw OptionError("L2 sub-partition larger than 1024 lines is not supported in this build");
+  if (!c.l2.disabled && (uint64_t)c.l2.nsets * c.l2.assoc * std::max<uint32_t>(1, c.n_sub_per_mem) >
+                            (uint64_t)kMaxL2LinesCh)
+    throw OptionError("L2 lines per memory channel (sets x assoc x sub-partitions) above " +
+                      std::to_string(kMaxL2LinesCh) + " are not supported in this build");
   c.l2.mshr_entries = std::min<uint32_t>(c.l2.mshr_entries, kMaxL2Mshr);
   c.rop_latency = (uint32_t)r.getu("-gpgpu_l2_rop_latency");
   c.dram_latency = (uint32_t)r.getu("-dram_latency");
@@ -938,6 +946,12 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
     c.per_dram = (uint64_t)llround(1e9 / f[3]);
   }
   c.mall_miss_fs *= c.per_core;
+  c.per_core_max = c.per_core;
+  if (r.getb("-dvfs_enabled")) {
+    const double mr = r.getd("-dvfs_min_clock_ratio");
+    if (!(mr > 0.05 && mr <= 1.0)) throw OptionError("-dvfs_min_clock_ratio must be in (0.05, 1]");
+    c.per_core_max = (uint64_t)std::ceil((double)c.per_core / mr);
+  }
   c.kernel_launch_latency = (uint32_t)std::max<long long>(0, r.geti("-gpgpu_kernel_launch_latency"));
   {
     const long long q = r.geti("-gpgpu_kernel_launch_latency_queued");
@@ -1014,6 +1028,9 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.max_completed_cta = (int32_t)r.geti("-gpgpu_max_completed_cta");
   d.flush_l1 = r.getb("-gpgpu_flush_l1_cache");
   d.flush_l2 = r.getb("-gpgpu_flush_l2_cache");
+  d.l2_kernel_release = r.getb("-sim_l2_kernel_release");
+  d.dvfs = r.getb("-dvfs_enabled");
+  d.dvfs_min_clock_ratio = r.getd("-dvfs_min_clock_ratio");
   d.deadlock_detect = r.getb("-gpgpu_deadlock_detect");
   d.nccl_allreduce_latency = (int32_t)r.geti("-nccl_allreduce_latency");
   d.collective_model = r.gets("-collective_model");

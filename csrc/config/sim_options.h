@@ -56,6 +56,9 @@ struct DriverOpts {
   int32_t max_completed_cta = 0;
   bool flush_l1 = false;
   bool flush_l2 = false;
+  bool l2_kernel_release = false;
+  bool dvfs = false;               // -dvfs_enabled: the power-cap DVFS governor
+  double dvfs_min_clock_ratio = 0.5;  // -sim_l2_kernel_release: write back + invalidate the L2s at kernel end
   bool deadlock_detect = true;
   int32_t nccl_allreduce_latency = 100;
   std::string collective_model;   // const | ring | tree | packet

@@ -53,10 +53,14 @@ Simulator::Simulator(const std::vector<std::string>& args) {
     throw OptionError("-sim_engine must be cpu, gpu or check");
   }
   eng_->init(cfg_);
+  per_core_nom_ = cfg_.per_core;
   if (dopt_.power_enabled) {
     power_.reset(new PowerModel());
     std::string err;
     if (!power_->load_xml(dopt_.power_xml, &err)) throw std::runtime_error("power model: " + err);
+    // the governor never goes below what the engine's buffers were sized for
+    power_->set_param("dvfs_min_clock_ratio",
+                      std::max(power_->param("dvfs_min_clock_ratio", 0.0), dopt_.dvfs_min_clock_ratio));
     power_report_.reset(new std::ofstream(dopt_.power_report_file));
     if (!*power_report_) throw std::runtime_error("cannot write " + dopt_.power_report_file);
     if (dopt_.power_trace) {
@@ -219,10 +223,11 @@ void Simulator::run_command(size_t idx) {
 // Checkpoint file: magic, driver counters, previous stat snapshots, engine image.
 namespace {
 struct CkptHeader {
-  uint64_t magic = 0x41534d434b505431ull;  // "ASMCKPT1"
+  uint64_t magic = 0x41534d434b505432ull;  // "ASMCKPT2"
   uint64_t cmd_index = 0, kernels_done = 0;
   uint64_t tot_cycle = 0, tot_insn = 0, tot_warp_insn = 0, tot_cta = 0, next_uid = 0;
   uint64_t n_sm_stats = 0, n_mem_stats = 0, engine_bytes = 0;
+  uint64_t per_core = 0, clk_base_cyc = 0, clk_base_fs = 0;  // the core-clock time base (DVFS)
 };
 }  // namespace
 
@@ -244,6 +249,9 @@ void Simulator::write_checkpoint(size_t cmd_index) {
   h.n_sm_stats = prev_sm_.size();
   h.n_mem_stats = prev_mem_.size();
   h.engine_bytes = eng.size();
+  h.per_core = cfg_.per_core;
+  h.clk_base_cyc = cfg_.clk_base_cyc;
+  h.clk_base_fs = cfg_.clk_base_fs;
   {
     std::error_code ec;
     std::filesystem::create_directories(dopt_.checkpoint_dir, ec);
@@ -280,6 +288,13 @@ size_t Simulator::resume_checkpoint() {
   fclose(f);
   if (!ok) throw std::runtime_error("truncated checkpoint " + path);
   eng_->load_state(eng);
+  if (h.per_core && (h.per_core != cfg_.per_core || h.clk_base_cyc || h.clk_base_fs)) {
+    eng_->set_core_clock(h.per_core, h.clk_base_cyc, h.clk_base_fs);
+    cfg_.per_core = h.per_core;
+    cfg_.clk_base_cyc = h.clk_base_cyc;
+    cfg_.clk_base_fs = h.clk_base_fs;
+    dvfs_ratio_ = (double)per_core_nom_ / (double)h.per_core;
+  }
   kernels_done_ = (uint32_t)h.kernels_done;
   tot_cycle_ = h.tot_cycle;
   tot_insn_ = h.tot_insn;
@@ -482,6 +497,7 @@ void Simulator::launch_ready() {
       const uint64_t lat = op.queued ? cfg_.kernel_launch_latency_queued : cfg_.kernel_launch_latency;
       op.kd.ready_cycle = now + lat + (uint64_t)cfg_.tb_launch_latency * op.kd.n_cta;
       op.start = now;
+      op.start_fs = core_fs(cfg_, now);
       op.slot = slot;
       op.launched = true;
       slot_op_[slot] = &op;
@@ -589,7 +605,9 @@ void Simulator::finish_kernel(uint32_t slot, const RunResult& rr) {
   StreamOp& op = *slot_op_[slot];
   const ReadyKernel& rk = *op.rk;
   const KernelDesc& kd = op.kd;
-  if (dopt_.flush_l2) eng_->flush_l2();
+  // -gpgpu_flush_l2_cache drops the lines (reference l2 flush at kernel
+  // end); -sim_l2_kernel_release writes the dirty sectors back first
+  if (dopt_.flush_l2 || dopt_.l2_kernel_release) eng_->flush_l2(dopt_.l2_kernel_release);
   std::vector<SMStats> sm;
   std::vector<MemStats> mem;
   eng_->stats(sm, mem);
@@ -608,6 +626,8 @@ void Simulator::finish_kernel(uint32_t slot, const RunResult& rr) {
   r.uid = kd.uid;
   r.start_cycle = op.start;
   r.cycles = rr.end_cycle - op.start;
+  r.sim_time_ns = (double)(core_fs(cfg_, rr.end_cycle) - op.start_fs) * 1e-6;
+  r.avg_clock_mhz = r.sim_time_ns > 0 ? (double)r.cycles / r.sim_time_ns * 1e3 : 1e9 / (double)per_core_nom_;
   for (auto& s : dsm) {
     r.insn += s.thread_insn;
     r.warp_insn += s.warp_insn;
@@ -676,7 +696,7 @@ RunResult Simulator::run_sampled(const RunLimits& lim0) {
   // HW / HYBRID modes take one sample per kernel (the hardware counters are per kernel)
   const bool hw = power_ && (dopt_.power_mode == 1 || dopt_.power_mode == 2);
   const uint64_t freq = std::max<uint64_t>(dopt_.stat_sample_freq, std::max<uint32_t>(1, cfg_.icnt_latency));
-  const double mhz = 1e9 / (double)cfg_.per_core;
+  const double mhz = 1e9 / (double)per_core_nom_;  // nominal: the power model applies the DVFS ratio
   // samples are named after the oldest running kernel
   std::string kname;
   uint32_t best = ~0u;
@@ -723,9 +743,12 @@ RunResult Simulator::run_sampled(const RunLimits& lim0) {
         for (int i = 0; i < HW_COUNT; ++i) use_sim[i] = dopt_.power_mode == 2 && dopt_.hybrid_use_sim[i];
         a = PowerModel::merge_hw(a, hwa, use_sim);
       }
-      PowerReport p = power_->compute(a, mhz, cfg_.n_sm);
+      PowerReport p = power_->compute(a, mhz, cfg_.n_sm, dvfs_ratio_);
       ptrack_.add_sample(p, a, now);
       if (power_trace_) ptrack_.write_trace_line(*power_trace_, p, now);
+      // DVFS governor: the next sample runs at the highest clock whose power,
+      // for this sample's per-cycle activity, fits under the measured cap
+      if (dopt_.dvfs && !hw) set_clock_ratio(power_->dvfs_clock_ratio(a, mhz, cfg_.n_sm));
     }
     if (visualizer_) write_visualizer_sample(kname, now, now > t_prev ? now - t_prev : 1, dsm, dm);
     if (cfg_.trace_mask) {
@@ -751,6 +774,21 @@ RunResult Simulator::run_sampled(const RunLimits& lim0) {
     if (r.epochs == 0) throw std::runtime_error("power sampling: engine made no progress");
   }
   return tot;
+}
+
+// DVFS: from the engine's current cycle on, the core runs at `ratio` x the
+// nominal clock.  The time base moves to now, so femtosecond stamps already
+// taken (packets in flight, memory-domain ticks) keep their meaning.
+void Simulator::set_clock_ratio(double ratio) {
+  const uint64_t per = (uint64_t)std::llround((double)per_core_nom_ / ratio);
+  if (per == cfg_.per_core) return;
+  const uint64_t now = eng_->now();
+  const uint64_t base_fs = core_fs(cfg_, now);
+  eng_->set_core_clock(per, now, base_fs);
+  cfg_.per_core = per;
+  cfg_.clk_base_cyc = now;
+  cfg_.clk_base_fs = base_fs;
+  dvfs_ratio_ = ratio;
 }
 
 // Drain the engine's debug trace buffers and print them DPRINTF-style
@@ -847,6 +885,11 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   print("gpu_sim_cycle = %llu\n", (unsigned long long)r.cycles);
   print("gpu_sim_insn = %llu\n", (unsigned long long)r.insn);
   print("gpu_ipc = %12.4f\n", r.ipc);
+  if (dopt_.dvfs) {
+    // DVFS: the core clock followed the power cap, so cycles != time
+    print("gpu_sim_time_ns = %.1f\n", r.sim_time_ns);
+    print("gpu_avg_core_clock_mhz = %.1f\n", r.avg_clock_mhz);
+  }
   print("gpu_tot_sim_cycle = %llu\n", (unsigned long long)tot_cycle_);
   print("gpu_tot_sim_insn = %llu\n", (unsigned long long)tot_insn_);
   print("gpu_tot_ipc = %12.4f\n", tot_cycle_ ? (double)tot_insn_ / (double)tot_cycle_ : 0.0);

@@ -32,6 +32,8 @@ struct KernelResult {
   double wall_s = 0;        // wall time spent simulating this kernel
   bool deadlock = false;
   double avg_power_w = 0;
+  double sim_time_ns = 0;   // simulated time of the kernel (core cycles at the clock(s) DVFS ran them)
+  double avg_clock_mhz = 0;
   uint64_t epochs = 0;      // PDES epochs simulated (one grid barrier each on the GPU engine)
 };
 
@@ -59,6 +61,7 @@ struct StreamOp {
   bool launched = false;
   int slot = -1;              // kernel: engine slot while running
   uint64_t start = 0, end = 0;  // launch cycle; collective: completion cycle
+  uint64_t start_fs = 0;        // launch time (femtoseconds; the core clock may change under DVFS)
   uint64_t coll_cycles = 0;
   uint64_t epochs = 0;        // engine epochs simulated while the kernel ran
   std::unique_ptr<ReadyKernel> rk;
@@ -141,6 +144,10 @@ class Simulator {
   std::unique_ptr<Engine> eng_;
   std::unique_ptr<PowerModel> power_;
   PowerTracker ptrack_;
+  // DVFS governor state: the nominal core period and the current clock ratio
+  uint64_t per_core_nom_ = 0;
+  double dvfs_ratio_ = 1.0;
+  void set_clock_ratio(double ratio);
   std::unique_ptr<std::ofstream> power_report_, power_trace_, power_steady_, visualizer_;
   void emit_trace();
   void write_visualizer_sample(const std::string& kname, uint64_t now, uint64_t cycles,

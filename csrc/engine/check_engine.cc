@@ -72,9 +72,13 @@ class CheckEngine final : public Engine {
     a_->memcpy_fill_l2(addr, bytes);
     b_->memcpy_fill_l2(addr, bytes);
   }
-  void flush_l2() override {
-    a_->flush_l2();
-    b_->flush_l2();
+  void set_core_clock(uint64_t per_core, uint64_t base_cyc, uint64_t base_fs) override {
+    a_->set_core_clock(per_core, base_cyc, base_fs);
+    b_->set_core_clock(per_core, base_cyc, base_fs);
+  }
+  void flush_l2(bool writeback) override {
+    a_->flush_l2(writeback);
+    b_->flush_l2(writeback);
   }
   void stats(std::vector<SMStats>& sm, std::vector<MemStats>& mem) override { a_->stats(sm, mem); }
   void snapshot(std::vector<uint8_t>& out) override { a_->snapshot(out); }

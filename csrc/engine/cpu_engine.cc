@@ -9,9 +9,15 @@
 namespace asim {
 
 uint32_t reply_cap(const SimCfg& c) {
-  // icnt ticks per epoch, +1 for phase alignment
-  uint64_t win = (uint64_t)c.icnt_latency * c.per_core;
+  // icnt ticks per epoch, +1 for phase alignment (at the slowest core clock
+  // DVFS may choose: an epoch is icnt_latency core cycles)
+  uint64_t win = (uint64_t)c.icnt_latency * std::max(c.per_core, c.per_core_max);
   return (uint32_t)((win + c.per_icnt - 1) / c.per_icnt + 1);
+}
+
+void check_core_clock(const SimCfg& c, uint64_t per_core) {
+  if (per_core == 0 || per_core > std::max(c.per_core, c.per_core_max))
+    throw std::runtime_error("set_core_clock: core period beyond the configured DVFS range (-dvfs_min_clock_ratio)");
 }
 
 void init_sm_state(SMState& s, uint32_t id) {
@@ -42,16 +48,17 @@ void host_memcpy_fill(ChanState* chs, uint32_t nch, const SimCfg& c, uint64_t ad
     uint32_t ch = t.sub / c.n_sub_per_mem, sub = t.sub % c.n_sub_per_mem;
     if (ch >= nch) continue;
     SubPart& sp = chs[ch].sp[sub];
+    L2Line* T = l2_tags(chs[ch], c, sub);
     uint32_t set = l2_set(c, line);
-    int way = l2_find<SeqPar>(sp, c.l2, set, line);
+    int way = l2_find<SeqPar>(T, c.l2, set, line);
     if (way < 0) {
-      way = l2_victim<SeqPar>(sp, c.l2, set);
-      L2Line& L = sp.l2[set * c.l2.assoc + way];
+      way = l2_victim<SeqPar>(T, c.l2, set);
+      L2Line& L = T[set * c.l2.assoc + way];
       L.tag = line;
       L.dirty = 0;
       L.valid = 0;
     }
-    L2Line& L = sp.l2[set * c.l2.assoc + way];
+    L2Line& L = T[set * c.l2.assoc + way];
     uint64_t lo = std::max(line, addr), hi = std::min(line + 128, addr + bytes);
     for (uint64_t s = (lo - line) >> 5; s <= ((hi - 1 - line) >> 5) && s < 4; ++s) L.valid |= (uint8_t)(1u << s);
     L.lru = ++sp.l2_stamp;
@@ -66,13 +73,50 @@ void check_state_header(const EngineStateHeader& h, const EngineStateHeader& w) 
     throw std::runtime_error("engine state: image was written for a different configuration or build");
 }
 
-void host_flush_l2(ChanState* chs, uint32_t nch, const SimCfg& c) {
-  for (uint32_t i = 0; i < nch; ++i)
-    for (uint32_t j = 0; j < c.n_sub_per_mem; ++j)
-      for (auto& L : chs[i].sp[j].l2) {
-        L.valid = 0;
-        L.dirty = 0;
+void host_flush_l2(ChanState* chs, uint32_t nch, const SimCfg& c, bool writeback, L2Line* mall) {
+  const uint32_t per_sub = c.l2.nsets * c.l2.assoc;
+  for (uint32_t i = 0; i < nch; ++i) {
+    ChanState& ch = chs[i];
+    if (writeback && !c.l2.disabled) {
+      // sub-partition by sub-partition, lines in index order: the same order
+      // on every engine, so the MALL contents stay bit-exact
+      for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
+        MemStats& st = ch.sp[j].st;
+        const L2Line* T = l2_tags(ch, c, j);
+        for (uint32_t k = 0; k < per_sub; ++k) {
+          const L2Line& L = T[k];
+          if (!(L.valid && L.dirty)) continue;
+          const uint32_t n = (uint32_t)popc64(L.dirty);
+          st.l2_mem_wr += n;
+          st.l2_evict_dirty++;
+          if (!mall) {
+            st.dram_wr += n;  // straight to DRAM, untimed (between kernels)
+            continue;
+          }
+          L2Line* b = mall + (size_t)i * mall_lines(c) + (size_t)mall_set(c, L.tag) * c.mall_assoc;
+          int w = mall_find<SeqPar>(b, c.mall_assoc, L.tag);
+          if (w < 0) {
+            w = mall_victim<SeqPar>(b, c.mall_assoc);
+            if (b[w].valid && b[w].dirty) {
+              const uint32_t nv = (uint32_t)popc64(b[w].dirty);
+              ch.sp[0].st.mall_wb += nv;
+              ch.sp[0].st.dram_wr += nv;
+            }
+            b[w] = L2Line{};
+            b[w].tag = L.tag;
+          }
+          b[w].valid |= L.dirty;
+          b[w].dirty |= L.dirty;
+          b[w].lru = ++ch.mall_stamp;
+          ch.sp[0].st.mall_wr += n;
+        }
       }
+    }
+    for (auto& L : ch.l2) {
+      L.valid = 0;
+      L.dirty = 0;
+    }
+  }
 }
 
 namespace {
@@ -163,7 +207,7 @@ class CpuEngine : public Engine {
           ChanState& ch = chs_[i - nsm];
           MemCtx m = ctx_mem(cur, t1);
           m.mall = mall_.empty() ? nullptr : mall_.data() + (size_t)(i - nsm) * mall_lines(c);
-          chan_epoch<SeqPar>(ch, m, box_req_[prev].data(), cnt_req_[prev].data(), cap_req_, t0 * c.per_core);
+          chan_epoch<SeqPar>(ch, m, box_req_[prev].data(), cnt_req_[prev].data(), cap_req_, core_fs(c, t0));
           chan_publish<SeqPar>(ch, m, *pub_, cur);
         }
       }
@@ -202,7 +246,15 @@ class CpuEngine : public Engine {
   void memcpy_fill_l2(uint64_t addr, uint64_t bytes) override {
     host_memcpy_fill(chs_.data(), (uint32_t)chs_.size(), c_, addr, bytes);
   }
-  void flush_l2() override { host_flush_l2(chs_.data(), (uint32_t)chs_.size(), c_); }
+  void set_core_clock(uint64_t per_core, uint64_t base_cyc, uint64_t base_fs) override {
+    check_core_clock(c_, per_core);
+    c_.per_core = per_core;
+    c_.clk_base_cyc = base_cyc;
+    c_.clk_base_fs = base_fs;
+  }
+  void flush_l2(bool writeback) override {
+    host_flush_l2(chs_.data(), (uint32_t)chs_.size(), c_, writeback, mall_.empty() ? nullptr : mall_.data());
+  }
 
   void stats(std::vector<SMStats>& sm, std::vector<MemStats>& mem) override {
     sm.clear();
@@ -320,7 +372,7 @@ class CpuEngine : public Engine {
     m.outcnt = cnt_rep_[cur].data();
     m.out_cap = cap_rep_;
     m.n_src_sub = c_.n_subpart;
-    m.win_end = t1 * c_.per_core;
+    m.win_end = core_fs(c_, t1);
     m.ovf = ovf_.data();
     m.ovf_cap = ovf_cap_;
     m.mall = nullptr;

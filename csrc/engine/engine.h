@@ -47,7 +47,14 @@ class Engine {
   virtual uint64_t now() const = 0;
   // L2 pre-fill for MemcpyHtoD (reference perf_memcpy_to_gpu, gpu-sim.cc:2116-2136)
   virtual void memcpy_fill_l2(uint64_t addr, uint64_t bytes) = 0;
-  virtual void flush_l2() = 0;
+  // invalidate the L2s; with `writeback` the dirty sectors are first written
+  // to memory (the MALL when there is one), as the release at the end of a
+  // kernel does on a multi-XCD GPU
+  virtual void flush_l2(bool writeback = false) = 0;
+  // DVFS: core cycles from `base_cyc` on last `per_core` fs, cycle base_cyc
+  // beginning at femtosecond `base_fs` (called at an epoch boundary, i.e.
+  // between run() calls; per_core must not exceed SimCfg::per_core_max)
+  virtual void set_core_clock(uint64_t per_core, uint64_t base_cyc, uint64_t base_fs) = 0;
   virtual void stats(std::vector<SMStats>& sm, std::vector<MemStats>& mem) = 0;
   // raw state image (SM states then channel states) for checkpoint/compare
   virtual void snapshot(std::vector<uint8_t>& out) = 0;
@@ -134,8 +141,10 @@ inline uint64_t mall_lines(const SimCfg& c) { return (uint64_t)c.mall_sets * c.m
 
 // helpers shared by both engines
 uint32_t reply_cap(const SimCfg& c);
+void check_core_clock(const SimCfg& c, uint64_t per_core);
 void host_memcpy_fill(ChanState* chs, uint32_t nch, const SimCfg& c, uint64_t addr, uint64_t bytes);
-void host_flush_l2(ChanState* chs, uint32_t nch, const SimCfg& c);
+// mall: the channels' MALL lines [nch][mall_lines(c)] (nullptr without a MALL)
+void host_flush_l2(ChanState* chs, uint32_t nch, const SimCfg& c, bool writeback = false, L2Line* mall = nullptr);
 void init_sm_state(SMState& s, uint32_t id);
 void init_chan_state(ChanState& ch, uint32_t id, const SimCfg& c);
 

@@ -249,8 +249,8 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
         mx.outbox = a.box_rep[cur];
         mx.outcnt = a.cnt_rep[cur];
         mx.mall = a.mall ? a.mall + (size_t)(u - c.n_sm) * ((size_t)c.mall_sets * c.mall_assoc) : nullptr;
-        mx.win_end = t1 * c.per_core;
-        chan_epoch<P>(*ch, mx, a.box_req[prev], a.cnt_req[prev], a.cap_req, t0 * c.per_core);
+        mx.win_end = core_fs(c, t1);
+        chan_epoch<P>(*ch, mx, a.box_req[prev], a.cnt_req[prev], a.cap_req, core_fs(c, t0));
         chan_publish<P>(*ch, mx, *a.pub, cur);
       }
     }
@@ -615,11 +615,21 @@ class GpuEngine : public Engine {
     host_memcpy_fill(hc.data(), c_.n_mem, c_, addr, bytes);
     HIPCHECK(hipMemcpy(d_chs_, hc.data(), sizeof(ChanState) * c_.n_mem, hipMemcpyHostToDevice));
   }
-  void flush_l2() override {
+  void set_core_clock(uint64_t per_core, uint64_t base_cyc, uint64_t base_fs) override {
+    check_core_clock(c_, per_core);
+    c_.per_core = per_core;
+    c_.clk_base_cyc = base_cyc;
+    c_.clk_base_fs = base_fs;
+    HIPCHECK(hipMemcpy(d_cfg_, &c_, sizeof(SimCfg), hipMemcpyHostToDevice));
+  }
+  void flush_l2(bool writeback) override {
     std::vector<ChanState> hc(c_.n_mem);
     HIPCHECK(hipMemcpy(hc.data(), d_chs_, sizeof(ChanState) * c_.n_mem, hipMemcpyDeviceToHost));
-    host_flush_l2(hc.data(), c_.n_mem, c_);
+    std::vector<L2Line> hm(writeback ? n_mall_ : 0);
+    if (!hm.empty()) HIPCHECK(hipMemcpy(hm.data(), d_mall_, sizeof(L2Line) * n_mall_, hipMemcpyDeviceToHost));
+    host_flush_l2(hc.data(), c_.n_mem, c_, writeback, hm.empty() ? nullptr : hm.data());
     HIPCHECK(hipMemcpy(d_chs_, hc.data(), sizeof(ChanState) * c_.n_mem, hipMemcpyHostToDevice));
+    if (!hm.empty()) HIPCHECK(hipMemcpy(d_mall_, hm.data(), sizeof(L2Line) * n_mall_, hipMemcpyHostToDevice));
   }
 
   void stats(std::vector<SMStats>& sm, std::vector<MemStats>& mem) override {

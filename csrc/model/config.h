@@ -38,7 +38,7 @@ constexpr int kEjectQ = 32;         // cluster ejection buffer (-gpgpu_n_cluster
 constexpr int kLdstRespQ = 8;       // LD/ST response FIFO (-gpgpu_n_ldst_response_buffer_size cap)
 constexpr int kMaxAccess = 64;      // coalesced accesses of one instruction
 // memory side (per sub-partition)
-constexpr int kMaxL2Lines = 1024;   // per sub-partition
+constexpr int kMaxL2LinesCh = 2048; // per memory channel, shared by its sub-partitions
 constexpr int kMaxL2Mshr = 256;
 constexpr int kMaxL2Wait = 256;
 constexpr int kRopQ = 256;
@@ -228,6 +228,12 @@ struct SimCfg {
   BitRuns part_runs;            // partition_address gather mask as runs
   // ---- clocks (femtoseconds per cycle) ----
   uint64_t per_core, per_icnt, per_l2, per_dram;
+  // core-clock time base: core cycle clk_base_cyc began at clk_base_fs, and
+  // every later core cycle lasts per_core.  DVFS (-dvfs_enabled with a power
+  // cap) changes per_core at an epoch boundary by moving the base there, so
+  // the stamps already taken in femtoseconds stay valid (core_fs / core_cyc)
+  uint64_t clk_base_cyc, clk_base_fs;
+  uint64_t per_core_max;    // the longest core period DVFS may set (sizes the per-epoch reply mailboxes)
   // ---- kernel scheduling ----
   uint32_t kernel_launch_latency;
   uint32_t kernel_launch_latency_queued;  // a kernel right behind the previous one (driver)
@@ -329,6 +335,20 @@ SIM_HDI uint32_t icnt_routers(const SimCfg& c, uint32_t a, uint32_t b) {
       return h + 1;
     }
   }
+}
+
+// absolute femtoseconds of the start of core cycle `cyc`, and the core cycle
+// holding femtosecond `fs` (floor) or starting at or after it (ceil)
+SIM_HDI uint64_t core_fs(const SimCfg& c, uint64_t cyc) {
+  return (uint64_t)((int64_t)c.clk_base_fs + ((int64_t)cyc - (int64_t)c.clk_base_cyc) * (int64_t)c.per_core);
+}
+SIM_HDI uint64_t core_cyc(const SimCfg& c, uint64_t fs) {
+  if (fs >= c.clk_base_fs) return c.clk_base_cyc + (fs - c.clk_base_fs) / c.per_core;
+  return c.clk_base_cyc - (c.clk_base_fs - fs + c.per_core - 1) / c.per_core;
+}
+SIM_HDI uint64_t core_cyc_ceil(const SimCfg& c, uint64_t fs) {
+  if (fs >= c.clk_base_fs) return c.clk_base_cyc + (fs - c.clk_base_fs + c.per_core - 1) / c.per_core;
+  return c.clk_base_cyc - (c.clk_base_fs - fs) / c.per_core;
 }
 
 // femtoseconds from injection complete to arrival: SM `sm` -> sub-partition `sub`

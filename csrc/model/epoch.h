@@ -179,7 +179,7 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t 
   s.min_emit = ~0ull;
   // 1. arrivals (replies injected by the memory side last epoch)
   P::prof(12);
-  gather_sorted<P>(inbox, incnt, s.id, n_sub, in_cap, t0 * c.per_core, s.inq, kInQ, s.inq_head, s.inq_n,
+  gather_sorted<P>(inbox, incnt, s.id, n_sub, in_cap, core_fs(c, t0), s.inq, kInQ, s.inq_head, s.inq_n,
                    s_scratch_key(s), s_scratch_ref(s), s_scratch_rank(s), kInQ);
   // 2. CTA dispatch (state published at the previous boundary)
   P::prof(13);
@@ -261,7 +261,7 @@ SIM_HDI void sm_publish(SMState& s, const SmCtx& x, EpochPub& pub, uint32_t cur)
   const uint32_t idle = (all_dispatched && sm_idle(s)) ? 1u : 0u;
   uint64_t nx = ~0ull;
   if (c.event_skip && (s.n_cta_active || !sm_idle(s)))
-    nx = sm_quiet_until<P>(s, c, kt, s.cycle, s.cycle + kSkipHorizon) * c.per_core;
+    nx = core_fs(c, sm_quiet_until<P>(s, c, kt, s.cycle, s.cycle + kSkipHorizon));
   nx = amin(nx, s.min_emit);
   UnitPub u;
   u.next = nx;
@@ -393,10 +393,10 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   // pending event at all (a deadlock) nothing is skipped.
   if (c.event_skip && !d.done) {
     uint64_t ev = amin(sm_next, ch_next);
-    if (ready_req != ~0ull) ev = amin(ev, ready_req * c.per_core);
+    if (ready_req != ~0ull) ev = amin(ev, core_fs(c, ready_req));
     if (ev != ~0ull) {
       const uint64_t E = c.icnt_latency;
-      const uint64_t tc = ev / c.per_core;  // the next epoch may start no later than this
+      const uint64_t tc = core_cyc(c, ev);  // the next epoch may start no later than this
       if (tc >= t1 + E) {
         uint64_t s = t1 + (tc - t1) / E * E;
         if (max_cycle && s > max_cycle) s = max_cycle > t1 ? t1 + (max_cycle - t1 + E - 1) / E * E : t1;

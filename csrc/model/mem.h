@@ -114,7 +114,6 @@ struct SubPart {
   uint32_t n_l2dram;   // requests of this sub in the L2->DRAM path
   uint32_t ovf_head, ovf_n;  // arrival backlog ring (MemCtx::ovf) for arrivals that did not fit in inq
   uint16_t arb_next, arb_cnt;  // crossbar output-port arbiter: next input, grants left at the pointer
-  L2Line l2[kMaxL2Lines];
   L2Mshr mshr[kMaxL2Mshr];
   L2Wait wait[kMaxL2Wait];
   MemStats st;
@@ -153,7 +152,15 @@ struct alignas(16) ChanState {
   uint32_t sref[kMemInQ];                  // gather scratch: (src << 16 | k)
   uint32_t srank[kMemInQ > kMaxSmTot ? kMemInQ : kMaxSmTot];  // gather scratch: ranks / per-source offsets
   SubPart sp[kMaxSubPerCh];
+  // L2 tag arrays of the channel's sub-partitions, one pool: sub-partition j
+  // owns lines [j * sets * assoc, (j + 1) * sets * assoc), so a channel with
+  // one sub-partition can hold twice the lines of one with two (MI355X: 4 MiB
+  // per XCD = 16 channels x 2048 lines of 128 B)
+  L2Line l2[kMaxL2LinesCh];
 };
+SIM_HDI L2Line* l2_tags(ChanState& ch, const SimCfg& c, uint32_t sub) {
+  return ch.l2 + (size_t)sub * c.l2.nsets * c.l2.assoc;
+}
 
 SIM_HDI uint32_t sp_out_count(const ChanState& ch, uint32_t sub, uint32_t dst) { return ch.ocnt[sub][dst]; }
 SIM_HDI void sp_out_count_inc(ChanState& ch, uint32_t sub, uint32_t dst) { ch.ocnt[sub][dst]++; }
@@ -293,8 +300,8 @@ SIM_HDI bool mall_install(ChanState& ch, const SimCfg& c, L2Line* b, uint64_t li
 
 // ---- L2 tag array (lane-parallel over ways) ----
 template <class P>
-SIM_HDI int l2_find(const SubPart& sp, const CacheGeom& g, uint32_t set, uint64_t line) {
-  const L2Line* b = &sp.l2[set * g.assoc];
+SIM_HDI int l2_find(const L2Line* T, const CacheGeom& g, uint32_t set, uint64_t line) {
+  const L2Line* b = &T[set * g.assoc];
   for (uint32_t o = 0; o < g.assoc; o += 64) {
     int n = (int)amin<uint32_t>(64, g.assoc - o);
     uint64_t m = P::ballot(n, [&](int w) { return b[o + w].valid && b[o + w].tag == line; });
@@ -303,8 +310,8 @@ SIM_HDI int l2_find(const SubPart& sp, const CacheGeom& g, uint32_t set, uint64_
   return -1;
 }
 template <class P>
-SIM_HDI int l2_victim(const SubPart& sp, const CacheGeom& g, uint32_t set) {
-  const L2Line* b = &sp.l2[set * g.assoc];
+SIM_HDI int l2_victim(const L2Line* T, const CacheGeom& g, uint32_t set) {
+  const L2Line* b = &T[set * g.assoc];
   return P::argmin((int)g.assoc, [&](int w) -> uint64_t {
     return b[w].valid ? ((1ull << 40) | b[w].lru) : (uint64_t)w;
   });
@@ -319,8 +326,9 @@ template <class P>
 SIM_HDI int l2_alloc(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, uint32_t set,
                      uint64_t line, uint64_t now_fs) {
   const CacheGeom& g = c.l2;
-  int v = l2_victim<P>(sp, g, set);
-  L2Line& L = sp.l2[set * g.assoc + v];
+  L2Line* T = l2_tags(ch, c, sub);
+  int v = l2_victim<P>(T, g, set);
+  L2Line& L = T[set * g.assoc + v];
   if (L.valid && L.dirty) {
     uint32_t nd = (uint32_t)popc64(L.dirty);
     if (!l2dram_can(ch, sp, c, nd)) return -1;
@@ -364,21 +372,22 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
     if (trace_mem_on(c, TS_MEMORY_SUBPARTITION_UNIT, ch.id))
       P::one([&] { trace_put(c, c.n_sm + ch.id, now_fs / c.per_l2, EV_L2_ACCESS, (uint16_t)(sub << 8 | outcome), p.addr); });
   };
-  int way = g.disabled ? -1 : l2_find<P>(sp, g, set, p.addr);
+  L2Line* T = l2_tags(ch, c, sub);
+  int way = g.disabled ? -1 : l2_find<P>(T, g, set, p.addr);
   if (p.type == P_WR) {
     if (g.disabled || g.wpolicy == WP_WRITE_THROUGH) {
       uint32_t n = (uint32_t)popc64(p.sectors);
       if (!l2dram_can(ch, sp, c, n)) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
       for (uint32_t s = 0; s < 4; ++s)
         if (p.sectors >> s & 1u) l2dram_push(ch, sp, c, sub, p.addr, s, true, now_fs);
-      if (way >= 0) sp.l2[set * g.assoc + way].valid |= p.sectors;
+      if (way >= 0) T[set * g.assoc + way].valid |= p.sectors;
       trace(3);
     } else {
       // write-back L2 (reference data_cache wr_hit_wb / wr_miss_*,
       // gpu-cache.cc:1229-1599): a hit, or any write-allocate miss, makes
       // the sectors dirty; only whole-sector writes are readable at once
       // (lazy fetch on read); 'N' sends a miss to DRAM without allocating
-      const uint8_t have = way >= 0 ? sp.l2[set * g.assoc + way].valid : (uint8_t)0;
+      const uint8_t have = way >= 0 ? T[set * g.assoc + way].valid : (uint8_t)0;
       const bool hit = way >= 0 && (have & p.sectors) == p.sectors;
       const uint32_t bytes = p.size > 8 ? p.size - 8u : 0u;
       const bool full = bytes >= 32u * (uint32_t)popc64(p.sectors);
@@ -417,7 +426,7 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
         sp.st.l2[stype][L2O_MISS]++;
         trace(1);
       }
-      L2Line& L = sp.l2[set * g.assoc + way];
+      L2Line& L = T[set * g.assoc + way];
       if (full && !fetch) L.valid |= p.sectors;
       L.dirty |= p.sectors;
       if (g.repl == REPL_LRU) L.lru = ++sp.l2_stamp;
@@ -438,11 +447,11 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
     return true;
   }
   // read / atomic
-  uint8_t have = way >= 0 ? sp.l2[set * g.assoc + way].valid : 0;
+  uint8_t have = way >= 0 ? T[set * g.assoc + way].valid : 0;
   uint8_t miss = p.sectors & (uint8_t)~have;
   const uint8_t rtype = p.type == P_ATOM ? P_ATOM_REPLY : P_RD_REPLY;
   if (miss == 0) {
-    L2Line& L = sp.l2[set * g.assoc + way];
+    L2Line& L = T[set * g.assoc + way];
     if (g.repl == REPL_LRU) L.lru = ++sp.l2_stamp;
     if (p.type == P_ATOM) L.dirty |= p.sectors;
     reply_push(sp, rtype, p, p.sectors);
@@ -453,7 +462,11 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
   if (sp.n_wait >= (uint32_t)kMaxL2Wait) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
   const int nm = (int)amin<uint32_t>(g.mshr_entries, kMaxL2Mshr);
   int mi = P::find_first(nm, [&](int i) -> bool { return sp.mshr[i].valid && sp.mshr[i].line == p.addr; });
-  uint8_t need_req = mi >= 0 ? (uint8_t)(miss & ~sp.mshr[mi].requested) : miss;
+  // a sectored L2 ('S') fetches the missing sectors it was asked for; a
+  // line-granular one ('N', e.g. the MI355X L2: TCC_EA0_RDREQ_128B dominates
+  // its fills) fetches every sector of the line it does not hold
+  const uint8_t fetch = g.sectored ? miss : (uint8_t)(0xFu & ~have);
+  uint8_t need_req = mi >= 0 ? (uint8_t)(fetch & ~sp.mshr[mi].requested) : fetch;
   if (need_req == 0) {
     if (sp.mshr[mi].merges >= g.mshr_merge) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
     sp.mshr[mi].merges++;
@@ -500,6 +513,7 @@ template <class P>
 SIM_HDI bool l2_fill(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, const DramRet& r,
                      uint64_t now_fs) {
   const CacheGeom& g = c.l2;
+  L2Line* T = l2_tags(ch, c, sub);
   const uint8_t sbit = (uint8_t)(1u << r.sector);
   // replies this fill will generate must fit
   uint32_t nrep = 0;
@@ -514,12 +528,12 @@ SIM_HDI bool l2_fill(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, 
   if (sp.rep_n + nrep > (uint32_t)kReplyQ) return false;
   if (!g.disabled) {
     uint32_t set = l2_set(c, r.line);
-    int way = l2_find<P>(sp, g, set, r.line);
+    int way = l2_find<P>(T, g, set, r.line);
     if (way < 0) {
       way = l2_alloc<P>(ch, sp, c, sub, set, r.line, now_fs);
       if (way < 0) return false;
     }
-    L2Line& L = sp.l2[set * g.assoc + way];
+    L2Line& L = T[set * g.assoc + way];
     L.valid |= sbit;
     if (g.repl == REPL_LRU) L.lru = ++sp.l2_stamp;
   }
@@ -554,8 +568,8 @@ SIM_HDI bool l2_fill(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, 
       reply_push(sp, e.type == P_ATOM ? P_ATOM_REPLY : P_RD_REPLY, q, e.sectors);
       if (e.type == P_ATOM && !g.disabled) {
         uint32_t set = l2_set(c, r.line);
-        int way = l2_find<P>(sp, g, set, r.line);
-        if (way >= 0) sp.l2[set * g.assoc + way].dirty |= e.sectors;
+        int way = l2_find<P>(T, g, set, r.line);
+        if (way >= 0) T[set * g.assoc + way].dirty |= e.sectors;
       }
       e.valid = 0;
     }

@@ -393,7 +393,7 @@ SIM_HDI void sm_inject(S& s, const SmCtx& x, uint64_t now) {
   uint32_t n = P::uni(s.ocnt[dst]);
   if (n >= x.out_cap) return;  // outbox cell full (cannot happen with cap >= epoch)
   s.ocnt[dst] = n + 1;
-  p.t = done * c.per_core + icnt_pkt_lat_fs(c, s.id, dst);
+  p.t = core_fs(c, done) + icnt_pkt_lat_fs(c, s.id, dst);
   s.min_emit = amin(s.min_emit, p.t);
   if (trace_sm_on(c, TS_INTERCONNECT, s.id)) P::one([&] { trace_put(c, s.id, now, EV_PKT_SEND, (uint16_t)dst, p.addr); });
   P::one([&] {
@@ -776,17 +776,17 @@ SIM_HDI void sm_receive(S& s, const SmCtx& x, uint64_t now) {
   }
   // 2. crossbar output port -> cluster ejection buffer
   if (P::uni(s.inq_n) && P::uni(s.cl_n) < c.eject_buf &&
-      P::uni(s.inq[P::uni(s.inq_head)].t) <= now * c.per_core) {
+      P::uni(s.inq[P::uni(s.inq_head)].t) <= core_fs(c, now)) {
     Pkt q;
     uint32_t head = P::uni(s.inq_head), n = P::uni(s.inq_n);
     uint16_t an = s.arb_next, ac = s.arb_cnt;
-    const XbarGrant g = xbar_pick<P>(s.inq, head, n, kInQ, now * c.per_core, c, now * c.per_core / c.per_icnt,
+    const XbarGrant g = xbar_pick<P>(s.inq, head, n, kInQ, core_fs(c, now), c, core_fs(c, now) / c.per_icnt,
                                      an, ac, c.n_subpart);
     s.arb_next = an;
     s.arb_cnt = ac;
     s.sadd(SK(icnt_reply_conflicts), g.ready - 1);
     q = P::uni(xbar_take(s.inq, head, n, kInQ, g.off));
-    s.sadd(SK(icnt_reply_queue_cycles), (now * c.per_core - q.t) / c.per_icnt);
+    s.sadd(SK(icnt_reply_queue_cycles), (core_fs(c, now) - q.t) / c.per_icnt);
     s.inq_head = head;
     s.inq_n = n;
     if (trace_sm_on(c, TS_INTERCONNECT, s.id)) P::one([&] { trace_put(c, s.id, now, EV_PKT_RECV, q.type, q.addr); });
@@ -1756,7 +1756,7 @@ SIM_HDI uint64_t sm_quiet_until(const S& s, const SimCfg& c, const KernelTab& kt
   nx = ring_next<P>(s.hit_occ, kHitRing, t, nx);
   if (nx == t) return t;
   if (P::uni(s.inq_n)) {
-    const uint64_t at = (P::uni(s.inq[P::uni(s.inq_head)].t) + c.per_core - 1) / c.per_core;
+    const uint64_t at = core_cyc_ceil(c, P::uni(s.inq[P::uni(s.inq_head)].t));
     if (at <= t) return t;
     nx = amin<uint64_t>(nx, at);
   }

@@ -104,17 +104,21 @@ std::vector<double> PowerModel::coefficients(double core_mhz) const {
   return c;
 }
 
-PowerReport PowerModel::compute(const Activity& a, double core_mhz, uint32_t n_sm) const {
+PowerReport PowerModel::compute(const Activity& a, double core_mhz, uint32_t n_sm, double clock_ratio) const {
   PowerReport r;
   const double cyc = a.cycles > 0 ? a.cycles : 1;
-  const auto coef = coefficients(core_mhz);
-  const double v2 = a.voltage * a.voltage;
+  const double s = clock_ratio > 0 ? clock_ratio : 1.0;
+  const double vr = s < 1.0 ? dvfs_voltage_ratio(s) : 1.0;
+  const auto coef = coefficients(core_mhz * s);
+  // a.voltage: the HW-mode chip voltage ratio (hw_perf.csv); vr: DVFS
+  const double v2 = a.voltage * a.voltage * vr * vr;
   for (int i = 0; i < PA_COUNT; ++i) {
-    r.dynamic_w[i] = coef[i] * (a.a[i] / cyc) * v2;
+    const bool dram = i == PA_MEM_RD || i == PA_MEM_WR || i == PA_MEM_PRE;  // the HBM rail keeps its voltage
+    r.dynamic_w[i] = coef[i] * (a.a[i] / cyc) * (dram ? a.voltage * a.voltage : v2);
     r.dynamic += r.dynamic_w[i];
   }
   r.constant = param("constant_power", 0);
-  r.idle = param("idle_core_power", 0) * a.idle_sms;
+  r.idle = param("idle_core_power", 0) * a.idle_sms * vr;
   // categorical static power by active unit mix (reference
   // calculate_static_power, gpgpu_sim_wrapper.cc:746-846)
   std::string cat;
@@ -132,25 +136,39 @@ PowerReport PowerModel::compute(const Activity& a, double core_mhz, uint32_t n_s
   if (a.a[PA_SHRD_ACC] > 0) r.static_w += param("static_shared_flane", 0) * busy_frac;
   if (a.a[PA_DC_RH] + a.a[PA_DC_RM] + a.a[PA_DC_WH] + a.a[PA_DC_WM] > 0) r.static_w += param("static_l1_flane", 0) * busy_frac;
   if (a.a[PA_L2_RH] + a.a[PA_L2_RM] + a.a[PA_L2_WH] + a.a[PA_L2_WM] > 0) r.static_w += param("static_l2_flane", 0);
+  r.static_w *= vr;
   r.total = r.dynamic + r.static_w + r.constant + r.idle;
   for (int i = 0; i < PA_COUNT; ++i) r.cmp[kActCmp[i]] += r.dynamic_w[i];
   r.cmp[PC_IDLE_CORE] = r.idle;
   r.cmp[PC_CONST] = r.constant;
   r.cmp[PC_STATIC] = r.static_w;
-  r.uncapped = r.total;
-  const double cap = param("power_cap", 0);
-  if (cap > 0 && r.total > cap) {
-    const double f = cap / r.total;
-    for (int i = 0; i < PA_COUNT; ++i) r.dynamic_w[i] *= f;
-    for (int i = 0; i < PC_COUNT; ++i) r.cmp[i] *= f;
-    r.dynamic *= f;
-    r.static_w *= f;
-    r.constant *= f;
-    r.idle *= f;
-    r.total = cap;
-    r.capped = true;
-  }
+  r.clock_ratio = s;
+  r.voltage_ratio = vr;
+  r.capped = s < 1.0;
+  r.uncapped = s < 1.0 ? compute(a, core_mhz, n_sm, 1.0).total : r.total;
   return r;
+}
+
+double PowerModel::dvfs_voltage_ratio(double s) const {
+  const double vf = param("dvfs_v_floor", 0.6);
+  return vf + (1.0 - vf) * s;
+}
+
+double PowerModel::dvfs_min_ratio() const {
+  return std::min(1.0, std::max(0.05, param("dvfs_min_clock_ratio", 0.5)));
+}
+
+double PowerModel::dvfs_clock_ratio(const Activity& a, double core_mhz, uint32_t n_sm) const {
+  const double cap = param("power_cap", 0);
+  if (cap <= 0 || compute(a, core_mhz, n_sm, 1.0).total <= cap) return 1.0;
+  // P(s) rises monotonically with s: bisect for the highest s under the cap
+  double lo = dvfs_min_ratio(), hi = 1.0;
+  if (compute(a, core_mhz, n_sm, lo).total >= cap) return lo;
+  for (int i = 0; i < 40; ++i) {
+    const double m = 0.5 * (lo + hi);
+    (compute(a, core_mhz, n_sm, m).total <= cap ? lo : hi) = m;
+  }
+  return lo;
 }
 
 Activity PowerModel::merge_hw(const Activity& sim, const Activity& hw, const bool use_sim[HW_COUNT]) {
@@ -186,6 +204,7 @@ void PowerTracker::begin_kernel() {
   for (auto& x : k_act_) x = Agg{};
   k_tot_ = Agg{};
   k_lanes_ = 0;
+  k_clk_ = k_cyc_ = 0;
   k_n_ = 0;
   k_series_.clear();
 }
@@ -196,6 +215,8 @@ void PowerTracker::add_sample(const PowerReport& r, const Activity& a, uint64_t 
   k_tot_.add(r.total);
   g_tot_.add(r.total);
   k_lanes_ += a.avg_lanes;
+  k_clk_ += r.clock_ratio * a.cycles;
+  k_cyc_ += a.cycles;
   ++k_n_;
   ++g_n_;
   k_series_.emplace_back(cycle, r.total);
@@ -209,6 +230,7 @@ void PowerTracker::write_kernel(std::ostream& os, const std::string& header) con
   for (int i = 0; i < PC_COUNT; ++i) os << "gpu_avg_" << kPwrCmpName[i] << " = " << k_cmp_[i].sum / n << "\n";
   for (int i = 0; i < PA_COUNT; ++i) os << "gpu_avg_" << kPwrActName[i] << " = " << k_act_[i].sum / n << "\n";
   os << "gpu_avg_threads_per_warp = " << k_lanes_ / n << "\n";
+  os << "kernel_avg_clock_ratio = " << kernel_clock_ratio() << "\n";
   for (int i = 0; i < PA_COUNT; ++i) os << "gpu_tot_" << kPwrActName[i] << " = " << k_act_[i].sum << "\n";
   os << "\nKernel Maximum Power Data:\n";
   os << "kernel_max_power = " << k_tot_.mx << "\n";

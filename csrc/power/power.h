@@ -10,11 +10,18 @@
 //   P = constant + idle_sm * n_idle + static(category, lanes)
 //       + sum_i  base_nJ[i] * scale[i] * accesses[i] / t
 // evaluated on the host per sample from the engines' activity counters.
-// An optional `power_cap` parameter models the package power limit: the
-// MI355X's power management holds socket power at its limit by lowering the
-// clocks (every compute-saturating validation kernel measures 1280-1330 W),
-// so a sample whose unconstrained estimate exceeds the cap reports the cap,
-// with every component scaled by cap / estimate (DVFS lowers all of them).
+// DVFS (reference gpgpu_sim_wrapper.cc:948-958 scales static power by the
+// voltage ratio and dynamic power by its square; -dvfs_enabled): with a
+// `power_cap` parameter -- the package power limit MEASURED by amd-smi
+// (power_suite measure), not fitted -- the simulator's governor picks for the
+// next sample the highest core clock ratio s in [dvfs_min_clock_ratio, 1]
+// whose power fits under the cap, with the rail voltage on the line
+//   V(s) / V(1) = dvfs_v_floor + (1 - dvfs_v_floor) * s
+// (dvfs_v_floor from the measured clock / voltage pairs).  At ratio s the
+// core-domain dynamic power is  base * accesses-per-cycle * f(s) * V(s)^2,
+// static and idle-core power scale with V(s), DRAM power keeps the HBM rail's
+// voltage, and the slower clock makes the sample's cycles longer in simulated
+// time (Engine::set_core_clock).  A sample above the cap is reported as it is.
 #pragma once
 #include <map>
 #include <ostream>
@@ -68,8 +75,10 @@ struct PowerReport {
   double constant = 0;
   double idle = 0;
   double total = 0;
-  double uncapped = 0;  // estimate before the package power cap
-  bool capped = false;
+  double uncapped = 0;      // the same activity at the nominal clock and voltage
+  bool capped = false;      // the sample ran below the nominal clock (DVFS)
+  double clock_ratio = 1.0;   // core clock / nominal of the sample
+  double voltage_ratio = 1.0;
   std::string static_category;
 };
 
@@ -80,7 +89,14 @@ class PowerModel {
   bool load_xml(const std::string& path, std::string* err = nullptr);
   void set_param(const std::string& k, double v) { p_[k] = v; }
   double param(const std::string& k, double dflt = 0) const;
-  PowerReport compute(const Activity& act, double core_mhz, uint32_t n_sm) const;
+  // power of one sample whose activity was counted per core cycle, with the
+  // core at `clock_ratio` x the nominal `core_mhz` (and the DVFS voltage)
+  PowerReport compute(const Activity& act, double core_mhz, uint32_t n_sm, double clock_ratio = 1.0) const;
+  // DVFS: V(s) / V(1), and the governor's clock ratio for the activity of the
+  // last sample (1 without a power cap or when the nominal clock fits)
+  double dvfs_voltage_ratio(double clock_ratio) const;
+  double dvfs_clock_ratio(const Activity& act, double core_mhz, uint32_t n_sm) const;
+  double dvfs_min_ratio() const;
   // activity of one kernel from stat deltas
   static Activity activity_from_stats(const std::vector<SMStats>& dsm, const std::vector<MemStats>& dmem,
                                       uint64_t cycles);
@@ -106,6 +122,8 @@ class PowerTracker {
   void begin_kernel();
   void add_sample(const PowerReport& r, const Activity& a, uint64_t cycle);
   size_t kernel_samples() const { return k_n_; }
+  // cycle-weighted mean core clock ratio of the kernel's samples (DVFS)
+  double kernel_clock_ratio() const { return k_cyc_ > 0 ? k_clk_ / k_cyc_ : 1.0; }
   double kernel_avg_power() const { return k_n_ ? k_tot_.sum / (double)k_n_ : 0.0; }
   void write_kernel(std::ostream& os, const std::string& header) const;
   void write_trace_header(std::ostream& os) const;
@@ -127,6 +145,7 @@ class PowerTracker {
   };
   Agg k_cmp_[PC_COUNT], k_act_[PA_COUNT], k_tot_, g_tot_;
   double k_lanes_ = 0;
+  double k_clk_ = 0, k_cyc_ = 0;
   size_t k_n_ = 0, g_n_ = 0;
   std::vector<std::pair<uint64_t, double>> k_series_;
   double st_dev_ = 8;

@@ -9,6 +9,8 @@
 // run it under `rocprofv3 --kernel-trace` and fit the durations with
 // accel_sim_framework_distributed_amd/hw_stats/launch_latency.py.  Run
 // standalone it prints host-side event timings of the same launches.
+#include <chrono>
+
 #include "ubench.h"
 
 __global__ void ub_empty_kernel(int* sink) {
@@ -17,6 +19,20 @@ __global__ void ub_empty_kernel(int* sink) {
 
 __global__ void ub_empty_queued(int* sink) {
   if (sink && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) sink[0] = 2;
+}
+
+__global__ void ub_empty_idle(int* sink) {
+  if (sink && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) sink[0] = 3;
+}
+
+__global__ void ub_empty_chain(int* sink) {
+  if (sink && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) sink[0] = 4;
+}
+
+static void host_spin_us(double us) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() < us) {
+  }
 }
 
 // keeps the GPU busy (and its clocks up) for ~20 us before each measured launch,
@@ -58,5 +74,27 @@ int main() {
     }
     printf("queued empty kernels, %5d workgroups: launched\n", nb);
   }
+  // idle launches: the queue is empty and the GPU idle when the kernel is
+  // submitted (no event, a host gap after the previous synchronisation) --
+  // how a host-bound application loop (pathfinder, nw) reaches the GPU
+  for (int nb : {1, 64, 1024, 4096}) {
+    for (int r = 0; r < 30; ++r) {
+      UB_CHECK(hipDeviceSynchronize());
+      host_spin_us(30.0);
+      hipLaunchKernelGGL(ub_empty_idle, dim3(nb), dim3(64), 0, 0, nullptr);
+    }
+    UB_CHECK(hipDeviceSynchronize());
+    printf("idle empty kernels, %5d workgroups: launched\n", nb);
+  }
+  // chains: 64 empty kernels submitted back to back from an idle GPU; the
+  // start-to-start interval in steady state is the host submission interval
+  // (or the GPU's per-kernel throughput, whichever is longer)
+  for (int r = 0; r < 4; ++r) {
+    UB_CHECK(hipDeviceSynchronize());
+    host_spin_us(30.0);
+    for (int q = 0; q < 64; ++q) hipLaunchKernelGGL(ub_empty_chain, dim3(64), dim3(64), 0, 0, nullptr);
+  }
+  UB_CHECK(hipDeviceSynchronize());
+  printf("chained empty kernels: launched\n");
   return 0;
 }

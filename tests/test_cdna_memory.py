@@ -125,3 +125,56 @@ def test_mall_absorbs_writes(native, tmp_path):
     assert _stat(mall.output, "MALL_writes") == _stat(mall.output, "L2_to_mem_write_sectors") > 0
     assert _stat(mall.output, "total dram reads") == 0
     assert _stat(mall.output, "MALL_read_hits") == pytest.approx(sectors, rel=0.02)
+
+
+def _writer_then_reader(tmp_path):
+    k = KernelBuilder("_Z5writePf", (64, 1, 1), (128, 1, 1), nregs=16, kid=1)
+    g = k.g
+    for i in range(LOADS):
+        k.op("STG.E", [], [2, 4], base=BUF + i * REGION + (g.gtid0 * 4) % REGION, stride=4)
+    k.op("EXIT")
+    d = tmp_path / "rel"
+    d.mkdir()
+    write_kernel_binary(str(d / "kernel-1.asimk"), k.build())
+    write_kernel_binary(str(d / "kernel-2.asimk"), _reader(2))
+    return write_kernelslist(str(d), ["kernel-1.asimk", "kernel-2.asimk"])
+
+
+def test_kernel_release_writes_back_and_invalidates(native, tmp_path):
+    """-sim_l2_kernel_release: the end-of-kernel release of a multi-XCD GPU
+    writes the dirty L2 sectors to the MALL and the next kernel starts with
+    cold L2s (it re-reads from the MALL, DRAM sees nothing)."""
+    kl = _writer_then_reader(tmp_path)
+    wb = {"-gpgpu_cache:dl2": "S:32:128:24,L:B:m:L:P,A:192:4,32:0,32", "-sim_mall": "512:16"}
+    keep = _run(native, kl, wb)
+    rel = _run(native, kl, dict(wb, **{"-sim_l2_kernel_release": "1"}))
+    sectors = LOADS * REGION // 32
+    # without the release the stores stay dirty in the L2 and the reader hits
+    assert _stat(keep.output, "L2_to_mem_write_sectors") == 0
+    assert _stat(keep.output, "L2_to_mem_read_sectors") == 0
+    # with it: every dirty sector goes to the MALL once, the reader misses the
+    # L2 and hits the MALL
+    assert _stat(rel.output, "L2_to_mem_write_sectors") == pytest.approx(sectors, rel=0.02)
+    assert _stat(rel.output, "L2_cache_dirty_evictions") == pytest.approx(sectors / 4, rel=0.02)
+    assert _stat(rel.output, "MALL_writes") == _stat(rel.output, "L2_to_mem_write_sectors")
+    assert _stat(rel.output, "MALL_read_hits") == pytest.approx(sectors, rel=0.02)
+    assert _stat(rel.output, "total dram reads") == 0 and _stat(rel.output, "total dram writes") == 0
+
+
+def test_line_granular_l2_fetches_whole_lines(native, tmp_path):
+    """An 'N' (non-sectored) L2 fetches every sector of a missing line (the
+    MI355X L2's 128 B fills, TCC_EA0_RDREQ_128B); a sectored one only what was
+    asked for."""
+    k = KernelBuilder("_Z5sparsePf", (64, 1, 1), (32, 1, 1), nregs=16, kid=1)
+    g = k.g
+    # each warp reads ONE sector (every lane the same word) of its own line
+    k.op("LDG.E", [8], [2], base=BUF + g.cta * 128, stride=0)
+    k.op("EXIT")
+    d = tmp_path / "sp"
+    d.mkdir()
+    write_kernel_binary(str(d / "kernel-1.asimk"), k.build())
+    kl = write_kernelslist(str(d), ["kernel-1.asimk"])
+    sect = _run(native, kl, {"-gpgpu_cache:dl2": "S:32:128:24,L:B:m:L:P,A:192:4,32:0,32"})
+    line = _run(native, kl, {"-gpgpu_cache:dl2": "N:32:128:24,L:B:m:L:P,A:192:4,32:0,32"})
+    assert _stat(sect.output, "L2_to_mem_read_sectors") == 64
+    assert _stat(line.output, "L2_to_mem_read_sectors") == 4 * 64

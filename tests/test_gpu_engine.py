@@ -152,6 +152,11 @@ _FEATURES = {
     "xcd_mall": {"-sim_xcd": "8", "-sim_mall": "256:16", "-sim_mall_miss_latency": "200",
                  "-gpgpu_flush_l2_cache": "1"},
     "reply_buffers": {"-gpgpu_n_cluster_ejection_buffer_size": "1", "-gpgpu_n_ldst_response_buffer_size": "1"},
+    # kernel-boundary release into the MALL, line-granular L2 fills, a 2048-line
+    # per-channel tag pool (one sub-partition per channel)
+    "xcd_release_line_l2": {"-sim_xcd": "8", "-sim_mall": "256:16", "-sim_mall_miss_latency": "200",
+                            "-sim_l2_kernel_release": "1", "-gpgpu_n_sub_partition_per_mchannel": "1",
+                            "-gpgpu_cache:dl2": "N:128:128:16,L:B:m:L:P,A:192:4,32:0,32"},
 }
 
 

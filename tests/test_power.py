@@ -155,29 +155,124 @@ def test_capped_fit_recovers_power_cap():
     x_true[comps.index("TENSORP")] = 6.0
     b = np.minimum(A @ x_true, 1200.0)
     assert (A @ x_true > 1200.0).sum() >= 3  # some kernels really are capped
-    x, cap = calibrate.fit_groups_capped(A, b)
+    x, cap = calibrate.fit_groups_capped(A, b, restarts=3)
     assert cap == pytest.approx(1200.0, rel=5e-3)
     assert calibrate.mape(calibrate.predict_capped(A, x, cap), b)[0] < 0.5
-    loo = calibrate.leave_one_out_capped(A, b)
+    loo = calibrate.leave_one_out_capped(A, b, restarts=2)
     assert calibrate.mape(loo, b)[0] < 2.0
 
 
-def test_power_cap_clamps_samples(native, tmp_path):
+def _cap_setup(native, tmp_path):
     from accel_sim_framework_distributed_amd.tracegen import rodinia
     p = xmlcfg.default_params("QV100")
     free_xml = str(tmp_path / "free.xml")
     xmlcfg.write_xml(free_xml, p)
-    ks = [rodinia.vectoradd(300000)]
-    opts = {"-power_simulation_enabled": "1", "-gpgpu_runtime_stat": "300:0"}
-    _, d0 = _run(native, tmp_path, "free", dict(opts, **{"-accelwattch_xml_file": free_xml}), ks)
+    ks = rodinia.hotspot(512, 2, 1)
+    opts = {"-power_simulation_enabled": "1", "-gpgpu_runtime_stat": "200:0", "-power_trace_enabled": "1"}
+    free_sim, d0 = _run(native, tmp_path, "free", dict(opts, **{"-accelwattch_xml_file": free_xml}), ks)
     free = report.parse_power_report(str(d0 / "accelwattch_power_report.log"))[0]
-    cap = 0.5 * (free["kernel_max_power"] + free["kernel_min_power"])
-    assert free["kernel_max_power"] > cap > p["constant_power"]
+    cap = 0.5 * (free["kernel_max_power"] + free["kernel_avg_power"])
     capped_xml = str(tmp_path / "capped.xml")
-    xmlcfg.write_xml(capped_xml, dict(p, power_cap=cap))
-    _, d1 = _run(native, tmp_path, "capped", dict(opts, **{"-accelwattch_xml_file": capped_xml}), ks)
+    xmlcfg.write_xml(capped_xml, dict(p, power_cap=cap, dvfs_v_floor=0.6))
+    return ks, opts, free_sim, free, cap, capped_xml
+
+
+def test_power_cap_without_dvfs_reports_the_estimate(native, tmp_path):
+    """A power limit alone changes nothing: the report is the activity's power
+    (no rescaling to the cap -- only the DVFS governor can hold the cap)."""
+    ks, opts, free_sim, free, cap, capped_xml = _cap_setup(native, tmp_path)
+    assert free["kernel_max_power"] > cap
+    s, d1 = _run(native, tmp_path, "capped", dict(opts, **{"-accelwattch_xml_file": capped_xml}), ks)
     k = report.parse_power_report(str(d1 / "accelwattch_power_report.log"))[0]
-    assert k["kernel_max_power"] == pytest.approx(cap, rel=1e-6)
+    assert s.tot_cycle == free_sim.tot_cycle
+    assert k["kernel_avg_power"] == pytest.approx(free["kernel_avg_power"], rel=1e-9)
+
+
+def test_dvfs_governor_slows_the_clock_under_the_cap(native, tmp_path):
+    """-dvfs_enabled with a measured power cap (reference gpgpu_sim_wrapper.cc:
+    948-958 voltage scaling; here the clock drops too): samples over the cap
+    make the governor lower the core clock and voltage, power falls towards
+    the cap, and the kernel takes longer in simulated time."""
+    ks, opts, free_sim, free, cap, capped_xml = _cap_setup(native, tmp_path)
+    s, d1 = _run(native, tmp_path, "dvfs", dict(opts, **{"-accelwattch_xml_file": capped_xml,
+                                                         "-dvfs_enabled": "1"}), ks)
+    k = report.parse_power_report(str(d1 / "accelwattch_power_report.log"))[0]
+    assert s.tot_insn == free_sim.tot_insn
+    assert k["kernel_avg_clock_ratio"] < 0.99
     assert k["kernel_avg_power"] < free["kernel_avg_power"]
-    # components are scaled with the total, so they still add up
+    assert k["kernel_max_power"] < free["kernel_max_power"]
+    # steady state (the middle of the kernel): the governor holds the cap
+    tr = [float(l.split(",")[1]) for l in open(d1 / "accelwattch_power_trace.csv").read().splitlines()[1:]]
+    mid = tr[len(tr) // 3: 2 * len(tr) // 3]
+    assert sum(mid) / len(mid) == pytest.approx(cap, rel=0.03)
     assert abs(sum(k["avg"].values()) - k["kernel_avg_power"]) < 1e-4 * k["kernel_avg_power"]
+    import re
+    mhz = float(re.search(r"gpu_avg_core_clock_mhz = ([0-9.]+)", s.output).group(1))
+    t_ns = float(re.search(r"gpu_sim_time_ns = ([0-9.]+)", s.output).group(1))
+    nominal = 1447.0  # QV100 core clock
+    assert mhz < nominal * 0.999
+    # simulated time: the free run's cycles at the nominal clock vs the DVFS run
+    assert t_ns > free_sim.tot_cycle / nominal * 1e3
+    # the memory clocks did not slow down: memory-bound phases take fewer
+    # (slower) core cycles, so the cycle count differs from the free run
+    assert s.tot_cycle != free_sim.tot_cycle
+
+
+def test_dvfs_checkpoint_resume_reproduces_the_run(native, tmp_path):
+    """The core-clock time base is part of the checkpoint: a resumed DVFS run
+    matches the uninterrupted one cycle for cycle."""
+    from accel_sim_framework_distributed_amd.models import presets
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    p = xmlcfg.default_params("QV100")
+    xml = str(tmp_path / "c.xml")
+    kl = rodinia.write_app(str(tmp_path / "tr"), rodinia.pathfinder(4000, 12, 2))
+    # a cap low enough that the governor is active in every kernel
+    xmlcfg.write_xml(xml, dict(p, power_cap=p["constant_power"] * 1.02))
+    base = presets.args_for("QV100", {"-power_simulation_enabled": "1", "-accelwattch_xml_file": xml,
+                                      "-dvfs_enabled": "1", "-gpgpu_runtime_stat": "200:0"}) + \
+        ["-trace", kl, "-checkpoint_path", str(tmp_path / "ck"), "-power_report_file", str(tmp_path / "p.log")]
+    full = native.Simulator(base, False)
+    assert full.run() == 0
+    c = native.Simulator(base + ["-checkpoint_option", "1", "-checkpoint_kernel", "2"], False)
+    assert c.run() == 0
+    r = native.Simulator(base + ["-resume_option", "1", "-resume_kernel", "2"], False)
+    assert r.run() == 0
+    fk = [(k["name"], k["cycles"], k["insn"]) for k in full.kernels]
+    rk = [(k["name"], k["cycles"], k["insn"]) for k in r.kernels]
+    assert fk[2:] == rk and r.tot_cycle == full.tot_cycle
+    import re
+    assert re.findall(r"gpu_sim_time_ns = ([0-9.]+)", full.output)[2:] == \
+        re.findall(r"gpu_sim_time_ns = ([0-9.]+)", r.output)
+
+
+def test_dvfs_calibration_recovers_factors_from_measured_clocks():
+    """Synthetic suite throttled by a governor like the simulator's: with the
+    measured clocks and cap the fit recovers the group factors, leave-one-out
+    is accurate at the measured clock, and the governor predicts the clocks."""
+    from accel_sim_framework_distributed_amd.power import mi355x_validation as v
+    rng = np.random.RandomState(5)
+    comps = list(calibrate.COMPONENTS)
+    n = 28
+    A = np.zeros((n, len(comps)))
+    A[:, comps.index("CONSTP")] = 250.0
+    A[:, comps.index("STATICP")] = rng.uniform(50, 150, n)
+    A[:, comps.index("FPUP")] = rng.uniform(0, 500, n)
+    A[:, comps.index("DRAMP")] = rng.uniform(0, 200, n)
+    A[:, comps.index("TENSORP")] = rng.uniform(0, 300, n) * (rng.rand(n) < 0.4)
+    x_true = np.ones(len(comps))
+    x_true[comps.index("FPUP")] = 1.8
+    x_true[comps.index("TENSORP")] = 2.5
+    cap, vf = 1000.0, 0.55
+    ratios = np.array([calibrate.governor_ratio(A[i], x_true, cap, vf, 0.4) for i in range(n)])
+    assert (ratios < 0.98).sum() >= 4  # several kernels really throttle
+    b = np.array([A[i] @ (x_true * calibrate.dvfs_scale(r, vf)) for i, r in enumerate(ratios)])
+    fmax = 2400.0
+    s = v.fit_report_dvfs(A, b, [f"k{i}" for i in range(n)], list(ratios * fmax), [float("nan")] * n, cap, fmax,
+                          v_floor=vf)
+    assert s["mape_in_sample"] < 0.5 and s["mape_leave_one_out"] < 1.0
+    assert s["governor"]["mape_leave_one_out"] < 1.0 and s["governor"]["clock_ratio_mae"] < 0.01
+    assert s["group_factors"]["valu"] == pytest.approx(1.8, rel=0.02)
+    assert not s["factors_at_bound"]
+    # the rail voltage line: V = 500 + 0.2 * f mV -> v_floor = 500 / (500 + 480)
+    f = np.array([1500.0, 1800.0, 2100.0, 2400.0])
+    assert calibrate.v_floor_from_measurements(f, 500 + 0.2 * f, 2400.0) == pytest.approx(500 / 980, rel=1e-6)

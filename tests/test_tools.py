@@ -181,8 +181,10 @@ def test_correlator_counter_passes_and_derived_stats(tmp_path):
     S = correlate
     t = get_stats.StatTable()
     stats = {S.S_CYC: [1000, 2000], S.S_WINSN: [500, 3000],
-             S.S_L2 % ("GLOBAL_ACC_R", "HIT"): [60, 10], S.S_L2 % ("GLOBAL_ACC_W", "HIT"): [20, 10],
-             r"L2_total_cache_misses\s*=\s*(.*)": [20, 80]}
+             # MI355X semantics: every write is an L2 hit, read misses and the
+             # reads merged into them are the misses
+             S.S_L2 % ("GLOBAL_ACC_R", "HIT"): [60, 10], S.S_L2 % ("GLOBAL_ACC_W", "TOTAL_ACCESS"): [20, 10],
+             S.S_L2 % ("GLOBAL_ACC_R", "MISS"): [15, 70], S.S_L2 % ("GLOBAL_ACC_R", "MSHR_HIT"): [5, 10]}
     t.stats = list(stats)
     for s, ks in stats.items():
         for i, v in enumerate(ks):
