@@ -94,8 +94,10 @@ def main(argv=None) -> int:
     a, b = fit(per)
     print(f"# rocprof_launch_ns {a:.1f}")
     print(f"# rocprof_per_block_ns {b:.4f}")
-    print(f"-gpgpu_kernel_launch_latency {int(round(a * mhz / 1000.0))}")
-    print(f"-gpgpu_TB_launch_latency {int(round(b * mhz / 1000.0))}")
+    have_idle = bool(read_durations(run_dir, "ub_empty_idle"))
+    if not have_idle:  # older ub_launch: the isolated (after-event) launch is the only one
+        print(f"-gpgpu_kernel_launch_latency {int(round(a * mhz / 1000.0))}")
+        print(f"-gpgpu_TB_launch_latency {int(round(b * mhz / 1000.0))}")
     # back-to-back launches (no event / sync between): the queued cost
     q = read_durations(run_dir, "ub_empty_queued")
     if q:
@@ -109,7 +111,11 @@ def main(argv=None) -> int:
         # MI355X: 4.7 us queued vs 3.7 us isolated vs ~2 us for a host-bound
         # launch into an idle queue (pathfinder), see profiles/ubench_mi355x
         print(f"# rocprof_queued_launch_ns {qa:.1f}")
-        print(f"# queued_launch_cycles {int(round(qa * mhz / 1000.0))}  (-gpgpu_kernel_launch_latency_queued)")
+        print(f"# queued_launch_cycles {int(round(qa * mhz / 1000.0))}")
+        # a dependent kernel dispatched right behind another occupies the
+        # command processor at least this long (its start stamp is the
+        # previous kernel's end): the simulator's minimum queued duration
+        print(f"-sim_kernel_min_cycles_queued {int(round(qa * mhz / 1000.0))}")
     # launches into an idle queue after a host gap (no event in between)
     idle = read_durations(run_dir, "ub_empty_idle")
     if idle:
@@ -120,6 +126,20 @@ def main(argv=None) -> int:
         print(f"# rocprof_idle_launch_ns {ia:.1f}")
         print(f"# rocprof_idle_per_block_ns {ib:.4f}")
         print(f"# idle_launch_cycles {int(round(ia * mhz / 1000.0))}")
+        # the model's launch latency (to the first workgroup) is the idle
+        # launch; a queued kernel pays the same plus the minimum duration above
+        print(f"-gpgpu_kernel_launch_latency {int(round(ia * mhz / 1000.0))}")
+        print(f"-gpgpu_kernel_launch_latency_queued {int(round(ia * mhz / 1000.0))}")
+        print(f"-gpgpu_TB_launch_latency {int(round(ib * mhz / 1000.0))}")
+    # the first kernel after a host-to-device copy vs the same kernel re-run
+    ac = read_durations(run_dir, "ub_touch_after_copy")
+    ag = read_durations(run_dir, "ub_touch_again")
+    if ac and ag:
+        a_med = float(np.median([x for v in ac.values() for x in v]))
+        g_med = float(np.median([x for v in ag.values() for x in v]))
+        print(f"# after_copy_kernel_ns {a_med:.1f}\n# same_kernel_again_ns {g_med:.1f}")
+        print(f"# after_copy_extra_cycles {int(round((a_med - g_med) * mhz / 1000.0))}")
+        print(f"-sim_first_kernel_latency {max(0, int(round((a_med - g_med) * mhz / 1000.0)))}")
     # back-to-back chains: steady-state start-to-start interval and duration
     ch = chain_stats(run_dir)
     if ch:

@@ -543,7 +543,9 @@ def _mi355x() -> Dict[str, str]:
         "-gpgpu_cache:il1": "N:64:128:4,L:R:f:N:L,S:8:64,4",
         "-gpgpu_l1_latency": "120",
         "-gpgpu_smem_latency": "64",
-        "-gpgpu_cache:dl2": "S:128:128:16,L:B:m:L:P,A:192:4,32:0,32",  # 4 MiB per XCD: 16 x 256 KB
+        # 4 MiB per XCD (16 x 256 KB), 128 B line fills (TCC_EA0_RDREQ_128B),
+        # write-back with byte-masked write allocation ('L')
+        "-gpgpu_cache:dl2": "N:128:128:16,L:B:m:L:P,A:192:4,32:0,32",
         # L2 hit = per-XCD L2 (~207 cycles), L2 miss = Infinity Cache (~540)
         "-gpgpu_l2_rop_latency": "75",
         "-dram_latency": "333",
@@ -574,6 +576,22 @@ def _mi355x() -> Dict[str, str]:
         "-sim_xcd": "8",
         "-sim_mall": "1024:16",
         "-sim_mall_miss_latency": "250",
+        # the XCD L2s are not coherent with each other: every kernel ends with
+        # a release that writes their dirty lines back (to the MALL) and the
+        # next one starts with them invalidated
+        "-sim_l2_kernel_release": "1",
+        # kernel launch as rocprofv3 durations see it (ub_launch +
+        # hw_stats/launch_latency.py): 1.5 us from an idle queue to the first
+        # workgroup; a kernel queued behind another lasts >= 4.7 us (the
+        # command processor's dependent back-to-back dispatch); the run's first
+        # kernel pays a cold start.  The host submits a kernel every ~5 us
+        # (fitted on the Rodinia suite: pathfinder's host-bound launches vs the
+        # back-to-back ones of lud / hotspot / nw, profiles/correlation)
+        "-gpgpu_kernel_launch_latency": "3563",
+        "-gpgpu_kernel_launch_latency_queued": "3563",
+        "-sim_kernel_min_cycles_queued": "11251",
+        "-sim_host_launch_interval": "12000",
+        "-sim_first_kernel_latency": "5000",
     })
     return c
 

@@ -294,6 +294,15 @@ const OptDef kOptions[] = {
     {"-sim_mall", 's', "none",
      "memory-attached last-level cache (Infinity Cache) per DRAM channel: <sets>:<assoc> of 128 B sectored lines, or none"},
     {"-sim_mall_miss_latency", 'u', "0", "extra core cycles of an HBM access over a MALL hit"},
+    {"-sim_host_launch_interval", 'u', "0",
+     "host model: core cycles between the host's kernel submissions after a sync (0 = a host that is never the "
+     "bottleneck); a kernel submitted after the previous one ended launches into an idle GPU"},
+    {"-sim_kernel_min_cycles_queued", 'u', "0",
+     "a kernel queued right behind another lasts at least this many core cycles (the command processor's "
+     "back-to-back dispatch interval of dependent kernels; 0 = off)"},
+    {"-sim_first_kernel_latency", 'u', "0",
+     "extra launch cycles of the run's first kernel behind the initial host copies (cold start: the copies' "
+     "completion and the first touch of their pages; ub_launch after-copy)"},
     {"-sim_l2_kernel_release", 'b', "0",
      "at the end of every kernel write the L2s' dirty sectors back to memory (the MALL if any) and invalidate them "
      "(the release / acquire of a multi-XCD GPU, whose XCD L2s are not coherent with each other)"},
@@ -1029,6 +1038,9 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.flush_l1 = r.getb("-gpgpu_flush_l1_cache");
   d.flush_l2 = r.getb("-gpgpu_flush_l2_cache");
   d.l2_kernel_release = r.getb("-sim_l2_kernel_release");
+  d.host_launch_interval = r.getu("-sim_host_launch_interval");
+  d.first_kernel_latency = r.getu("-sim_first_kernel_latency");
+  d.kernel_min_cycles_queued = r.getu("-sim_kernel_min_cycles_queued");
   d.dvfs = r.getb("-dvfs_enabled");
   d.dvfs_min_clock_ratio = r.getd("-dvfs_min_clock_ratio");
   d.deadlock_detect = r.getb("-gpgpu_deadlock_detect");

@@ -57,6 +57,9 @@ struct DriverOpts {
   bool flush_l1 = false;
   bool flush_l2 = false;
   bool l2_kernel_release = false;
+  uint64_t host_launch_interval = 0;      // -sim_host_launch_interval (cycles)
+  uint64_t first_kernel_latency = 0;      // -sim_first_kernel_latency (cycles)
+  uint64_t kernel_min_cycles_queued = 0;  // -sim_kernel_min_cycles_queued
   bool dvfs = false;               // -dvfs_enabled: the power-cap DVFS governor
   double dvfs_min_clock_ratio = 0.5;  // -sim_l2_kernel_release: write back + invalidate the L2s at kernel end
   bool deadlock_detect = true;

@@ -168,6 +168,13 @@ void Simulator::admit(size_t end) {
     if (c.type == CMD_KERNEL) {
       admit_kernel(i);
       win_.back()->queued = last_cmd_kernel_;
+      // host model: launches leave the host -sim_host_launch_interval cycles
+      // apart (the host resumes at the engine's clock after a sync)
+      win_.back()->submit = host_t_;
+      host_t_ += dopt_.host_launch_interval;
+      win_.back()->after_copy = copy_since_kernel_ && !any_kernel_admitted_;
+      copy_since_kernel_ = false;
+      any_kernel_admitted_ = true;
       last_cmd_kernel_ = true;
     } else if (windowed) {
       std::unique_ptr<StreamOp> op(new StreamOp());
@@ -185,7 +192,11 @@ void Simulator::admit(size_t end) {
       }
       win_.push_back(std::move(op));
     } else {
-      if (c.type == CMD_MEMCPY_HTOD || c.type == CMD_MEMCPY_DTOH) last_cmd_kernel_ = false;  // host sync
+      if (c.type == CMD_MEMCPY_HTOD || c.type == CMD_MEMCPY_DTOH) {
+        last_cmd_kernel_ = false;  // host sync
+        copy_since_kernel_ = true;
+        host_t_ = std::max(host_t_, eng_->now());
+      }
       run_now(c);
     }
   }
@@ -493,8 +504,20 @@ void Simulator::launch_ready() {
         continue;
       }
       if (!eng_->running()) ptrack_.begin_kernel();  // power samples of a busy period
-      const uint64_t now = eng_->now();
-      const uint64_t lat = op.queued ? cfg_.kernel_launch_latency_queued : cfg_.kernel_launch_latency;
+      uint64_t now = eng_->now();
+      if (dopt_.host_launch_interval && !dopt_.concurrent_kernel_sm) {
+        // host-bound launch: the GPU idles until the host submits the kernel,
+        // which then launches into an idle queue; one submitted while the
+        // previous kernel still ran is queued behind it
+        op.queued = op.submit < now;
+        if (op.submit > now && !eng_->running()) {
+          eng_->advance(op.submit - now);
+          now = eng_->now();
+          tot_cycle_ = now;
+        }
+      }
+      const uint64_t lat = (op.queued ? cfg_.kernel_launch_latency_queued : cfg_.kernel_launch_latency) +
+                           (op.after_copy ? dopt_.first_kernel_latency : 0);
       op.kd.ready_cycle = now + lat + (uint64_t)cfg_.tb_launch_latency * op.kd.n_cta;
       op.start = now;
       op.start_fs = core_fs(cfg_, now);
@@ -560,8 +583,20 @@ void Simulator::step() {
   // kernels end when they complete, or all together when the run stops
   uint32_t fin = rr.done_mask;
   if (rr.deadlock || rr.cap || at_max_cycle) fin = eng_->running() | rr.done_mask;
+  // a queued kernel occupies the command processor at least
+  // -sim_kernel_min_cycles_queued (back-to-back dispatch of dependent kernels)
+  RunResult rf = rr;
+  if (dopt_.kernel_min_cycles_queued && !dopt_.concurrent_kernel_sm && fin == rr.done_mask && !eng_->running()) {
+    for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k)
+      if ((fin >> k & 1u) && slot_op_[k] && slot_op_[k]->queued) {
+        const uint64_t until = slot_op_[k]->start + (uint64_t)dopt_.kernel_min_cycles_queued;
+        if (eng_->now() < until) eng_->advance(until - eng_->now());
+      }
+    rf.end_cycle = eng_->now();
+    tot_cycle_ = eng_->now();
+  }
   for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k)
-    if ((fin >> k & 1u) && slot_op_[k]) finish_kernel(k, rr);
+    if ((fin >> k & 1u) && slot_op_[k]) finish_kernel(k, rf);
   check_limits();
 }
 

@@ -58,6 +58,8 @@ struct StreamOp {
   uint64_t stream = 0;
   uint64_t event = 0, wait_for = 0;  // event ops: id; wait: records of it that must have fired
   bool queued = false;        // kernel: right behind another kernel (no host sync between)
+  uint64_t submit = 0;        // kernel: cycle the host submits it (-sim_host_launch_interval)
+  bool after_copy = false;    // kernel: the run's first, behind the initial host copies
   bool launched = false;
   int slot = -1;              // kernel: engine slot while running
   uint64_t start = 0, end = 0;  // launch cycle; collective: completion cycle
@@ -175,6 +177,9 @@ class Simulator {
   bool stop_ = false;
   bool ckpt_pending_ = false;
   bool last_cmd_kernel_ = false;  // the previous admitted command was a kernel launch
+  uint64_t host_t_ = 0;           // host model: cycle of the host's next kernel submission
+  bool copy_since_kernel_ = false;  // a host memcpy ran since the last kernel was admitted
+  bool any_kernel_admitted_ = false;
   bool cap_hit_ = false;  // a run cap (-gpgpu_max_insn / _max_cta / _max_completed_cta) stopped a kernel
 };
 

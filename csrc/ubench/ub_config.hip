@@ -36,11 +36,13 @@ int main() {
   ub_opt("-gpgpu_clock_domains", clk);
   // L2: hipDeviceProp reports one XCD's L2; the chip has 8 XCDs.  The
   // simulator's memory-side L2 gets the chip total, split across the
-  // memory sub-partitions (16-way, 128B lines)
+  // memory sub-partitions (16-way, 128B lines).  Line-granular ('N'): an
+  // L2 miss fills the whole 128 B line (rocprofv3 TCC_EA0_RDREQ_128B carries
+  // almost all of the fill traffic of the Rodinia suite, profiles/correlation)
   const long long l2_bytes = (long long)p.l2CacheSize * 8;
   const long long per_sub = std::max<long long>(128 * 16, l2_bytes / channels);
   const long long sets = std::max<long long>(1, per_sub / (128 * 16));
-  ub_opt("-gpgpu_cache:dl2", "S:" + std::to_string(sets) + ":128:16,L:B:m:L:P,A:192:4,32:0,32");
+  ub_opt("-gpgpu_cache:dl2", "N:" + std::to_string(sets) + ":128:16,L:B:m:L:P,A:192:4,32:0,32");
   printf("# measured_shader_mhz %.1f\n", mhz);
   return 0;
 }

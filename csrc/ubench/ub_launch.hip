@@ -29,6 +29,20 @@ __global__ void ub_empty_chain(int* sink) {
   if (sink && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) sink[0] = 4;
 }
 
+// reads one word per 4 KB page of a buffer the host just copied in
+__global__ void ub_touch_after_copy(const int* __restrict__ buf, size_t pages, int* sink) {
+  int acc = 0;
+  for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < pages; p += (size_t)gridDim.x * blockDim.x)
+    acc += buf[p * 1024];
+  if (acc == 0x7fffffff) sink[0] = acc;
+}
+__global__ void ub_touch_again(const int* __restrict__ buf, size_t pages, int* sink) {
+  int acc = 0;
+  for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < pages; p += (size_t)gridDim.x * blockDim.x)
+    acc += buf[p * 1024];
+  if (acc == 0x7fffffff) sink[0] = acc + 1;
+}
+
 static void host_spin_us(double us) {
   const auto t0 = std::chrono::steady_clock::now();
   while (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() < us) {
@@ -96,5 +110,23 @@ int main() {
   }
   UB_CHECK(hipDeviceSynchronize());
   printf("chained empty kernels: launched\n");
+  // first kernel after a host-to-device copy vs the same kernel again: what
+  // the copy (and the first touch of its pages) adds to a kernel's duration
+  {
+    const size_t bytes = size_t(8) << 20, pages = bytes / 4096;
+    std::vector<int> h(bytes / 4, 1);
+    int* d = nullptr;
+    UB_CHECK(hipMalloc(&d, bytes));
+    for (int r = 0; r < 20; ++r) {
+      UB_CHECK(hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice));
+      hipLaunchKernelGGL(ub_touch_after_copy, dim3(64), dim3(64), 0, 0, d, pages, nullptr);
+      UB_CHECK(hipDeviceSynchronize());
+      host_spin_us(30.0);
+      hipLaunchKernelGGL(ub_touch_again, dim3(64), dim3(64), 0, 0, d, pages, nullptr);
+      UB_CHECK(hipDeviceSynchronize());
+    }
+    UB_CHECK(hipFree(d));
+    printf("after-copy kernels: launched\n");
+  }
   return 0;
 }

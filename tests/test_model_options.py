@@ -285,3 +285,28 @@ def test_unmodelled_options_warn(native, traces):
     w = native.unmodelled_option_warnings(presets.args_for("QV100", {}))
     assert not any("ejection_buffer" in x or "response_buffer" in x for x in w)  # both modelled now
     assert any(x.startswith("note: option -gpgpu_ptx_force_max_capability") for x in w)
+
+
+def test_kernel_launch_model(native, tmp_path):
+    """Launch overheads as rocprofv3 sees them on MI355X (ub_launch): a kernel
+    queued behind another lasts at least -sim_kernel_min_cycles_queued; with
+    a host that submits every -sim_host_launch_interval cycles, kernels that
+    arrive after the GPU went idle launch unqueued; the run's first kernel
+    pays -sim_first_kernel_latency."""
+    kl = rodinia.write_app(str(tmp_path / "p"), rodinia.pathfinder(4000, 12, 2))
+    base = _run(native, kl, {})
+    ks = [k["cycles"] for k in base.kernels]
+    assert len(ks) >= 3
+    q = max(ks) * 3
+    queued = _run(native, kl, {"-sim_kernel_min_cycles_queued": str(q)})
+    kq = [k["cycles"] for k in queued.kernels]
+    assert kq[0] == ks[0] and all(c == q for c in kq[1:])
+    # a slow host: every kernel finds the GPU idle -> no minimum applies, the
+    # gaps are idle time between kernels
+    h = q * 4
+    slow = _run(native, kl, {"-sim_kernel_min_cycles_queued": str(q), "-sim_host_launch_interval": str(h)})
+    assert [k["cycles"] for k in slow.kernels] == ks
+    assert slow.tot_cycle >= (len(ks) - 1) * h
+    first = _run(native, kl, {"-sim_first_kernel_latency": "777"})
+    # (+ at most an epoch: the first CTA dispatch lands on an epoch boundary)
+    assert 777 <= first.kernels[0]["cycles"] - ks[0] <= 777 + 32
