@@ -196,6 +196,34 @@ def run(work: str, out_xml: str, iters: int = 48) -> Dict:
     return summary
 
 
+SAMPLE = 250  # power sample period (core cycles) of the validation runs
+
+
+def steady_components(trace_csv: str, lo: float = 0.25, hi: float = 0.75) -> Optional[Dict[str, float]]:
+    """Per-component power averaged over the samples in the middle of the
+    kernel (by sample index, [lo, hi)): the traced kernels are short versions
+    of loops the hardware measured at steady state, so their wave-launch
+    ramp and drain tail are left out.  None without enough samples."""
+    if not os.path.exists(trace_csv):
+        return None
+    with open(trace_csv) as f:
+        rows = list(csv.reader(f))
+    if len(rows) < 3:
+        return None
+    head, data = rows[0], rows[1:]
+    # the last sample is usually a partial period: drop it when there are several
+    if len(data) > 3:
+        data = data[:-1]
+    a, b = int(len(data) * lo), max(int(len(data) * lo) + 1, int(round(len(data) * hi)))
+    mid = data[a:b]
+    out = {}
+    for j, name in enumerate(head):
+        if j < 2:
+            continue
+        out[name] = float(np.mean([float(r[j]) for r in mid]))
+    return out
+
+
 def simulate_trace_power_split(kernelslist: str, xml: str, work: str, config_dir: str = TUNED,
                                jobs: int = 16) -> List[Dict]:
     """simulate_trace_power with every kernel as its own CPU-engine simulation
@@ -221,8 +249,10 @@ def simulate_trace_power_split(kernelslist: str, xml: str, work: str, config_dir
         rep = os.path.join(wd, "accelwattch_power_report.log")
         args = [exe, "-config", os.path.join(config_dir, "gpgpusim.config"), "-config",
                 os.path.join(config_dir, "trace.config"), "-trace", kl, "-power_simulation_enabled", "1",
-                "-accelwattch_xml_file", xml, "-power_report_file", rep, "-gpgpu_runtime_stat", "1000000000:0",
-                "-sim_engine", "cpu", "-gpgpu_kernel_launch_latency", "0"]
+                "-accelwattch_xml_file", xml, "-power_report_file", rep, "-gpgpu_runtime_stat", f"{SAMPLE}:0",
+                "-power_trace_enabled", "1", "-sim_engine", "cpu", "-gpgpu_kernel_launch_latency", "0",
+                "-sim_first_kernel_latency", "0", "-sim_host_launch_interval", "0",
+                "-sim_kernel_min_cycles_queued", "0"]
         r = subprocess.run(args, cwd=wd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
                            env=dict(os.environ, OMP_NUM_THREADS="1"))
         if r.returncode != 0:
@@ -230,7 +260,12 @@ def simulate_trace_power_split(kernelslist: str, xml: str, work: str, config_dir
         reps = report.parse_power_report(rep)
         if len(reps) != 1:
             raise RuntimeError(f"kernel {k}: {len(reps)} power reports")
-        return reps[0]
+        r0 = reps[0]
+        st = steady_components(os.path.join(wd, "accelwattch_power_trace.csv"))
+        if st:
+            r0["avg_kernel"] = r0["avg"]
+            r0["avg"] = st
+        return r0
 
     done = threading.Event()
 

@@ -303,6 +303,9 @@ const OptDef kOptions[] = {
     {"-sim_first_kernel_latency", 'u', "0",
      "extra launch cycles of the run's first kernel behind the initial host copies (cold start: the copies' "
      "completion and the first touch of their pages; ub_launch after-copy)"},
+    {"-collective_mem_traffic", 'b', "0",
+     "run every collective's local memory traffic (send-buffer reads, receive-buffer writes) as an RCCL-style copy "
+     "kernel that loads the simulated L2/MALL/HBM and contends with overlapping kernels"},
     {"-sim_l2_kernel_release", 'b', "0",
      "at the end of every kernel write the L2s' dirty sectors back to memory (the MALL if any) and invalidate them "
      "(the release / acquire of a multi-XCD GPU, whose XCD L2s are not coherent with each other)"},
@@ -1038,6 +1041,7 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.flush_l1 = r.getb("-gpgpu_flush_l1_cache");
   d.flush_l2 = r.getb("-gpgpu_flush_l2_cache");
   d.l2_kernel_release = r.getb("-sim_l2_kernel_release");
+  d.coll_mem_traffic = r.getb("-collective_mem_traffic");
   d.host_launch_interval = r.getu("-sim_host_launch_interval");
   d.first_kernel_latency = r.getu("-sim_first_kernel_latency");
   d.kernel_min_cycles_queued = r.getu("-sim_kernel_min_cycles_queued");

@@ -57,6 +57,7 @@ struct DriverOpts {
   bool flush_l1 = false;
   bool flush_l2 = false;
   bool l2_kernel_release = false;
+  bool coll_mem_traffic = false;   // -collective_mem_traffic: collectives run a copy kernel
   uint64_t host_launch_interval = 0;      // -sim_host_launch_interval (cycles)
   uint64_t first_kernel_latency = 0;      // -sim_first_kernel_latency (cycles)
   uint64_t kernel_min_cycles_queued = 0;  // -sim_kernel_min_cycles_queued

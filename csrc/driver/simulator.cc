@@ -386,6 +386,13 @@ void Simulator::admit_kernel(size_t idx) {
   op->t_admit = std::chrono::steady_clock::now();
   op->rk = take_kernel(idx);
   print("Processing kernel %s\n", c.text.c_str());
+  setup_kernel_op(*op, true);
+  win_.push_back(std::move(op));
+}
+
+// occupancy, resources and descriptor of a kernel operation whose ReadyKernel is set
+void Simulator::setup_kernel_op(StreamOp& o, bool apply_cta_cap) {
+  StreamOp* op = &o;
   if (op->rk->h.warp_size != cfg_.warp_size)
     throw std::runtime_error("trace warp size does not match -gpgpu_shader_core_pipeline");
   const ReadyKernel& rk = *op->rk;
@@ -399,7 +406,7 @@ void Simulator::admit_kernel(size_t idx) {
   kd.uid = next_uid_++;
   kd.n_cta = rk.n_cta;
   kd.stop_when_issued = 0;
-  if (dopt_.max_cta > 0) {
+  if (apply_cta_cap && dopt_.max_cta > 0) {
     // -gpgpu_max_cta: CTAs past the cap are never issued, and the run ends as
     // soon as the cap is reached (reference gpgpu_sim::active, gpu-sim.cc:1086)
     const uint64_t left = (uint64_t)dopt_.max_cta > tot_cta_ ? (uint64_t)dopt_.max_cta - tot_cta_ : 0;
@@ -433,7 +440,6 @@ void Simulator::admit_kernel(size_t idx) {
   op->occ_limiter = occ.limiter;
   op->stream = rk.h.stream;
   tot_cta_ += kd.n_cta;
-  win_.push_back(std::move(op));
 }
 
 std::unique_ptr<ReadyKernel> Simulator::take_kernel(size_t idx) {
@@ -545,6 +551,66 @@ void Simulator::launch_collective(StreamOp& op) {
   op.start = now;
   op.end = now + cyc;
   op.coll_cycles = cyc;
+  if (dopt_.coll_mem_traffic) launch_collective_dma(op);
+}
+
+// -collective_mem_traffic: the collective's reads of the local send buffer
+// and writes of the receive buffer run as an RCCL-style copy kernel in a free
+// engine slot (RCCL collectives ARE kernels on the GPU: -collective_max_channels
+// workgroups of 256 threads), so they load the simulated L2s, MALL and HBM
+// and contend with the compute kernels that overlap them.  The collective
+// completes when both the link model's time and the copy kernel are done.
+// Per-rank volumes of the ring algorithms: all-reduce 2(n-1)/n x S each way
+// (reduce-scatter + all-gather), all-gather / reduce-scatter / all-to-all
+// (n-1)/n x S, broadcast / reduce / send-recv S.
+void Simulator::launch_collective_dma(StreamOp& op) {
+  const Command& c = cmds_[op.cmd];
+  const double n = std::max(1, c.nranks);
+  if (n <= 1 || c.bytes == 0) return;
+  double f = 1.0;
+  if (c.coll == "AllReduce") f = 2.0 * (n - 1) / n;
+  else if (c.coll == "AllGather" || c.coll == "ReduceScatter" || c.coll == "AllToAll") f = (n - 1) / n;
+  const uint64_t bytes = (uint64_t)std::ceil(f * (double)c.bytes);
+  int slot = -1;
+  for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k)
+    if (!slot_op_[k]) {
+      slot = (int)k;
+      break;
+    }
+  if (slot < 0) {
+    print("GPGPU-Sim: WARNING no free kernel slot for the memory traffic of %s: link model only\n", c.text.c_str());
+    return;
+  }
+  const uint64_t now = eng_->now();
+  // synthetic buffers: one 4 GiB region per collective command, send half
+  // then receive half (the RCCL interposer does not record buffer addresses)
+  const uint64_t base = 0x7D0000000000ull + ((uint64_t)op.cmd << 32);
+  const uint32_t warps = std::max<uint32_t>(1, 256 / std::max<uint32_t>(1, cfg_.warp_size));
+  const uint32_t bv = cfg_.warp_size >= 64 ? 950 : 70;
+  std::unique_ptr<StreamOp> d(new StreamOp());
+  d->kind = OP_KERNEL;
+  d->cmd = op.cmd;
+  d->parent = &op;
+  d->t_admit = std::chrono::steady_clock::now();
+  d->rk.reset(new ReadyKernel(coalesce_kernel(
+      make_copy_kernel("rccl_" + c.coll + "_copy", bv, cfg_.warp_size, std::max<uint32_t>(1, dopt_.coll_max_channels),
+                       warps, base, bytes, base + (1ull << 31), bytes, op.stream),
+      cfg_)));
+  setup_kernel_op(*d, false);
+  // copy kernels number apart from the trace's kernels (uids stay stable)
+  --next_uid_;
+  d->kd.uid = 0x40000000u + (uint32_t)(dma_count_++);
+  d->kd.ready_cycle = now;  // starts with the collective
+  d->start = now;
+  d->start_fs = core_fs(cfg_, now);
+  d->slot = slot;
+  d->launched = true;
+  slot_op_[slot] = d.get();
+  print("launching kernel name: %s uid: %u (memory traffic of %s, %llu B each way)\n", d->rk->h.name.c_str(),
+        d->kd.uid, c.text.c_str(), (unsigned long long)bytes);
+  eng_->launch((uint32_t)slot, *d->rk, d->kd);
+  op.dma = std::move(d);
+  op.dma_pending = true;
 }
 
 // advance to the next completion in the window and retire what completed
@@ -553,7 +619,8 @@ void Simulator::step() {
   prefetch_next();
   uint64_t coll_end = ~0ull;
   for (auto& up : win_)
-    if (up->kind == OP_COLL && up->launched) coll_end = std::min(coll_end, up->end);
+    if (up->kind == OP_COLL && up->launched && !(up->dma_pending && up->end <= eng_->now()))
+      coll_end = std::min(coll_end, up->end);
   if (!eng_->running()) {
     if (coll_end == ~0ull) {
       if (!win_.empty()) throw std::runtime_error("command window stalled: nothing can start");
@@ -604,13 +671,13 @@ void Simulator::retire_collectives() {
   const uint64_t now = eng_->now();
   for (auto it = win_.begin(); it != win_.end();) {
     StreamOp& op = **it;
-    if (op.kind == OP_COLL && op.launched && op.end <= now) {
+    if (op.kind == OP_COLL && op.launched && op.end <= now && !op.dma_pending) {
       const Command& c = cmds_[op.cmd];
       CollectiveResult r;
       r.op = c.coll;
       r.bytes = c.bytes;
       r.nranks = c.nranks;
-      r.cycles = op.coll_cycles;
+      r.cycles = op.dma ? std::max<uint64_t>(op.coll_cycles, op.dma_end - op.start) : op.coll_cycles;
       colls_.push_back(r);
       it = win_.erase(it);
     } else {
@@ -710,8 +777,14 @@ void Simulator::finish_kernel(uint32_t slot, const RunResult& rr) {
     if (d.size() > 60000) d = d.substr(0, 60000) + "\n... (truncated)\n";
     print("%s", d.c_str());
   }
-  // the slot is free again; the operation leaves the window
+  // the slot is free again; the operation leaves the window (a collective's
+  // copy kernel instead releases its collective)
   slot_op_[slot] = nullptr;
+  if (op.parent) {
+    op.parent->dma_pending = false;
+    op.parent->dma_end = rr.end_cycle;
+    return;
+  }
   for (auto it = win_.begin(); it != win_.end(); ++it)
     if (it->get() == &op) {
       win_.erase(it);

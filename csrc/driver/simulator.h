@@ -68,6 +68,13 @@ struct StreamOp {
   uint64_t epochs = 0;        // engine epochs simulated while the kernel ran
   std::unique_ptr<ReadyKernel> rk;
   KernelDesc kd{};
+  // collective with -collective_mem_traffic: the RCCL-style copy kernel that
+  // carries its memory traffic (it runs in an engine slot, outside the
+  // window) and whether it is still running; the copy kernel's parent
+  std::unique_ptr<StreamOp> dma;
+  bool dma_pending = false;
+  uint64_t dma_end = 0;
+  StreamOp* parent = nullptr;
   const char* occ_limiter = "";
   std::chrono::steady_clock::time_point t_admit;
 };
@@ -118,6 +125,8 @@ class Simulator {
   void admit(size_t end);                 // move commands [next_cmd_, end) into the window
   void run_now(const Command& c);         // memcpy / communicator bookkeeping
   void admit_kernel(size_t idx);
+  void setup_kernel_op(StreamOp& op, bool apply_cta_cap);
+  void launch_collective_dma(StreamOp& coll);
   void launch_ready();
   void launch_collective(StreamOp& op);
   void step();                            // run to the next kernel / collective completion
@@ -180,6 +189,7 @@ class Simulator {
   uint64_t host_t_ = 0;           // host model: cycle of the host's next kernel submission
   bool copy_since_kernel_ = false;  // a host memcpy ran since the last kernel was admitted
   bool any_kernel_admitted_ = false;
+  uint64_t dma_count_ = 0;        // collective copy kernels launched
   bool cap_hit_ = false;  // a run cap (-gpgpu_max_insn / _max_cta / _max_completed_cta) stopped a kernel
 };
 

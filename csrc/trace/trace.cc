@@ -695,6 +695,88 @@ HostKernel load_kernel_text(const std::string& path) {
 }
 
 // ---------------------------------------------------------------------------
+HostKernel make_copy_kernel(const std::string& name, uint32_t binary_version, uint32_t warp_size, uint32_t n_cta,
+                            uint32_t warps, uint64_t src, uint64_t rd_bytes, uint64_t dst, uint64_t wr_bytes,
+                            uint64_t stream) {
+  const bool cdna = binary_version >= 900;
+  HostKernel k;
+  k.h.name = name;
+  k.h.grid[0] = std::max<uint32_t>(1, n_cta);
+  k.h.block[0] = std::max<uint32_t>(1, warps) * warp_size;
+  k.h.nregs = 32;
+  k.h.stream = stream;
+  k.h.binary_version = binary_version;
+  k.h.trace_version = 5;
+  k.h.warp_size = warp_size;
+  k.warps_per_cta = std::max<uint32_t>(1, warps);
+  k.n_cta = k.h.grid[0];
+  const OpInfo ld = decode_opcode(cdna ? "global_load_dwordx4" : "LDG.E.128", binary_version);
+  const OpInfo st = decode_opcode(cdna ? "global_store_dwordx4" : "STG.E.128", binary_version);
+  const OpInfo wt = decode_opcode("s_waitcnt", binary_version);
+  const OpInfo ex = decode_opcode(cdna ? "s_endpgm" : "EXIT", binary_version);
+  const uint64_t mask = warp_size >= 64 ? ~0ull : ((1ull << warp_size) - 1);
+  const uint64_t wave_bytes = (uint64_t)warp_size * 16;
+  const uint64_t n_waves = (uint64_t)k.n_cta * k.warps_per_cta;
+  // wave-wide accesses per wave, rounded up so that every byte moves
+  const uint64_t nrd = (rd_bytes + wave_bytes * n_waves - 1) / (wave_bytes * n_waves);
+  const uint64_t nwr = (wr_bytes + wave_bytes * n_waves - 1) / (wave_bytes * n_waves);
+  auto mem_inst = [&](const OpInfo& oi, uint64_t addr, uint8_t reg, bool load) {
+    TInst in{};
+    in.pc = (uint32_t)(k.insts.size() * 8);
+    in.mask = mask;
+    in.opcode = oi.opcode;
+    in.cls = oi.cls;
+    in.space = S_GLOBAL;
+    in.flags = oi.flags;
+    in.width = 16;
+    if (load) {
+      in.dst[0] = reg;
+      in.src[0] = 1;  // the address register
+    } else {
+      in.src[0] = 1;
+      in.src[1] = reg;
+    }
+    TMem m{};
+    m.base = addr;
+    m.stride = 16;
+    m.list = kNoMem;
+    in.mem = (uint32_t)k.mems.size();
+    k.mems.push_back(m);
+    k.insts.push_back(in);
+  };
+  auto plain = [&](const OpInfo& oi, bool waitcnt) {
+    TInst in{};
+    in.pc = (uint32_t)(k.insts.size() * 8);
+    in.mask = mask;
+    in.mem = kNoMem;
+    in.opcode = oi.opcode;
+    in.cls = oi.cls;
+    in.space = oi.space;
+    in.flags = oi.flags;
+    in.lat = waitcnt ? waitcnt_counts("s_waitcnt") : 0;
+    k.insts.push_back(in);
+  };
+  for (uint64_t w = 0; w < n_waves; ++w) {
+    const uint32_t begin = (uint32_t)k.insts.size();
+    // wave w owns accesses w, w + n_waves, ... (a grid-stride loop)
+    const uint64_t n = std::max(nrd, nwr);
+    for (uint64_t i = 0; i < n; i += 4) {
+      const uint64_t j = std::min<uint64_t>(4, n - i);
+      for (uint64_t q = 0; q < j; ++q)
+        if (i + q < nrd) mem_inst(ld, src + ((i + q) * n_waves + w) * wave_bytes, (uint8_t)(5 + 4 * q), true);
+      if (cdna) plain(wt, true);
+      for (uint64_t q = 0; q < j; ++q)
+        if (i + q < nwr) mem_inst(st, dst + ((i + q) * n_waves + w) * wave_bytes, (uint8_t)(5 + 4 * q), false);
+    }
+    plain(ex, false);
+    k.streams.push_back(WStream{begin, (uint32_t)k.insts.size() - begin});
+  }
+  k.warp_insts = k.insts.size();
+  k.thread_insts = k.warp_insts * (uint64_t)__builtin_popcountll(mask);
+  return k;
+}
+
+// ---------------------------------------------------------------------------
 // binary format
 namespace {
 const char kMagic[8] = {'A', 'S', 'I', 'M', 'K', '0', '0', '1'};

@@ -91,6 +91,16 @@ struct ReadyKernel {
   uint64_t warp_insts = 0;
 };
 
+// Synthetic streaming-copy kernel: the memory traffic of a collective on one
+// GPU (RCCL runs collectives as kernels that read the local send buffer and
+// write the receive buffer while the link moves the data).  n_cta workgroups
+// of `warps` waves; every wave loads its share of [src, src + rd_bytes) and
+// stores its share of [dst, dst + wr_bytes) in wave-wide 16 B-per-lane
+// accesses, four loads in flight before the stores that forward them.
+HostKernel make_copy_kernel(const std::string& name, uint32_t binary_version, uint32_t warp_size, uint32_t n_cta,
+                            uint32_t warps, uint64_t src, uint64_t rd_bytes, uint64_t dst, uint64_t wr_bytes,
+                            uint64_t stream);
+
 // header only (cheap); used by the command loop before the body is needed
 KernelHeader read_kernel_header(const std::string& path);
 HostKernel load_kernel(const std::string& path);  // text (.traceg/.trace) or binary (.asimk)

@@ -188,3 +188,56 @@ def test_memcpy_behind_kernel_waits_for_it(native, tmp_path):
         assert with_cp.kernels[0]["cycles"] == without.kernels[0]["cycles"]
         # the memcpy lands before kernel 2: its reads of R now hit in the L2
         assert "launching memcpy command" in with_cp.output
+
+
+def _mem_kernel(kid, stream, ctas=80, loads=24):
+    """A memory-bound kernel: every warp streams through its own lines."""
+    k = KernelBuilder(f"_Z3mem{kid}Pf", (ctas, 1, 1), (128, 1, 1), nregs=16, kid=kid)
+    k.header["stream"] = stream
+    g = k.g
+    for i in range(loads):
+        k.op("LDG.E", [8 + i % 4], [2], base=BASE + kid * (1 << 26) + i * ctas * 512 + g.gtid0 * 4, stride=4)
+    for i in range(4):
+        k.op("FFMA", [4], [4, 8 + i])
+    k.op("EXIT")
+    return k.build()
+
+
+def test_collective_memory_traffic_contends_with_compute(native, tmp_path):
+    """-collective_mem_traffic: the all-reduce's send/receive
+    buffer traffic runs as an RCCL-style copy kernel through the simulated
+    L2 and DRAM.  It adds the ring's 2(n-1)/n x S of reads and writes, and
+    slows a memory-bound kernel it overlaps; without overlap the collective
+    still completes no earlier than the link model says."""
+    coll = "ncclAllReduce,count=2097152,dtype=ncclFloat,op=ncclSum,nranks=8,stream=2"
+    kl = _app(tmp_path, "cmem", [_mem_kernel(1, 1)], extra_cmds=[(0, coll)])
+    extra = {"-collective_model": "ring"}
+    off = _run(native, kl, True, extra)
+    on = _run(native, kl, True, dict(extra, **{"-collective_mem_traffic": "1"}))
+    assert [k["name"] for k in off.kernels] == ["_Z3mem1Pf"]
+    names = [k["name"] for k in on.kernels]
+    assert "rccl_AllReduce_copy" in names and "_Z3mem1Pf" in names
+    import re
+
+    def tot(out, key):
+        return sum(float(x) for x in re.findall(rf"^{re.escape(key)} = ([0-9.]+)", out, re.M)[-1:])
+    # 2 (n-1)/n x 8 MiB each way, in 32 B sectors, on top of the kernel's own reads
+    moved = 2 * 7 / 8 * 2097152 * 4 / 32
+    assert tot(on.output, "L2_to_mem_read_sectors") - tot(off.output, "L2_to_mem_read_sectors") > 0.9 * moved
+    comp_off = [k for k in off.kernels if k["name"] == "_Z3mem1Pf"][0]["cycles"]
+    comp_on = [k for k in on.kernels if k["name"] == "_Z3mem1Pf"][0]["cycles"]
+    assert comp_on > comp_off * 1.05
+    assert on.collectives[0]["cycles"] >= off.collectives[0]["cycles"]
+
+
+@pytest.mark.gpu
+def test_collective_memory_traffic_gpu_engine_matches_cpu(native, tmp_path):
+    if not native.gpu_available():
+        pytest.fail("GPU engine not available on a GPU test run")
+    coll = "ncclAllReduce,count=262144,dtype=ncclFloat,op=ncclSum,nranks=4,stream=2"
+    kl = _app(tmp_path, "cmemg", [_mem_kernel(1, 1, ctas=16, loads=8)], extra_cmds=[(0, coll)])
+    extra = {"-collective_model": "ring", "-collective_mem_traffic": "1"}
+    c = _run(native, kl, True, extra)
+    g = _run(native, kl, True, extra, engine="gpu")
+    assert [(k["name"], k["cycles"]) for k in g.kernels] == [(k["name"], k["cycles"]) for k in c.kernels]
+    assert g.tot_cycle == c.tot_cycle

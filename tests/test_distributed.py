@@ -181,7 +181,9 @@ def _dp_worker(rank, world, port, root, q):
         from accel_sim_framework_distributed_amd import _native
         from accel_sim_framework_distributed_amd.sim import build_args
         kl = os.path.join(root, f"rank{rank}", "kernelslist.g")
-        s = _native.load().Simulator(build_args("QV100", kl, "cpu", DP_EXTRA), False)
+        import json
+        extra = json.load(open(os.path.join(root, "extra.json")))
+        s = _native.load().Simulator(build_args("QV100", kl, "cpu", extra), False)
         hook = collectives.PacketCollective()
         s.set_collective_hook(lambda d, now: hook(s, d, now))
         assert s.run() == 0
@@ -190,18 +192,25 @@ def _dp_worker(rank, world, port, root, q):
         dist.destroy_process_group()
 
 
-def test_dp_step_eight_ranks_match_in_process_emulation(native, tmp_path):
+@pytest.mark.parametrize("traffic", ["link_only", "mem_traffic"])
+def test_dp_step_eight_ranks_match_in_process_emulation(native, tmp_path, traffic):
     """Eight gloo processes, one simulated GPU each, run unequal shards of a
     DDP step whose per-layer all-reduces (stream 2) overlap the backward pass
     (stream 1): every rank's kernel and collective timing equals the
     in-process emulation of all eight ranks (threads + linksim_run_local)
-    exactly, and the collectives couple the ranks' clocks."""
+    exactly, and the collectives couple the ranks' clocks.  With
+    -collective_mem_traffic the all-reduces' buffer traffic also runs through
+    each rank's simulated memory system (RCCL copy kernels)."""
+    import json
     import threading
     from accel_sim_framework_distributed_amd.sim import build_args
     from accel_sim_framework_distributed_amd.tracegen import training
     W = 8
     root = str(tmp_path / "dp")
     kls = training.write_dp_ranks(root, W, **DP_KW)
+    extra = dict(DP_EXTRA, **({"-collective_mem_traffic": "1"} if traffic == "mem_traffic" else {}))
+    with open(os.path.join(root, "extra.json"), "w") as f:
+        json.dump(extra, f)
     res = _spawn(_dp_worker, W, root)
     assert all(m == ["rccl"] * DP_KW["layers"] for _, _, m in res)
     # oracle: all ranks in this process
@@ -209,7 +218,7 @@ def test_dp_step_eight_ranks_match_in_process_emulation(native, tmp_path):
     out = [None] * W
 
     def run(r):
-        s = native.Simulator(build_args("QV100", kls[r], "cpu", DP_EXTRA), False)
+        s = native.Simulator(build_args("QV100", kls[r], "cpu", extra), False)
         s.set_collective_hook(loc.hook(r, s))
         assert s.run() == 0
         out[r] = _dp_result(s)
@@ -227,3 +236,5 @@ def test_dp_step_eight_ranks_match_in_process_emulation(native, tmp_path):
     # overlap: backward kernels run back to back while the all-reduces proceed
     bwd = [k for k in res[0][1][1] if k[0] in (3, 4)]
     assert bwd[1][1] == bwd[0][1] + bwd[0][2]
+    copies = [k for k in res[0][1][1] if k[0] >= 0x40000000]
+    assert len(copies) == (DP_KW["layers"] if traffic == "mem_traffic" else 0)
