@@ -28,7 +28,18 @@ COMPONENT_PARAMS: Dict[str, List[str]] = {
     "TENSORP": ["TENSOR_ACC"], "TEXP": ["TEX_ACC"], "SCHEDP": ["FP_INT"], "L2CP": ["L2_RH", "L2_RM", "L2_WH", "L2_WM"],
     "MCP": ["MEM_PRE"], "NOCP": ["NOC_A"], "DRAMP": ["MEM_RD", "MEM_WR"], "PIPEP": ["PIPE_A"],
     "IDLE_COREP": ["idle_core_power"], "CONSTP": ["constant_power"], "STATICP": None,  # None: every static_* param
+    # calibration-only column: the LDS / L1 / L2 "unit in use" part of STATICP
+    # (power trace column STATIC_MEMP); with it, STATICP is the core part
+    "STATIC_MEMP": ["static_shared_flane", "static_l1_flane", "static_l2_flane"],
 }
+# the components of the DVFS-aware calibration: the report's, with STATICP
+# split into core and memory-unit static power
+CAL_COMPONENTS: List[str] = list(COMPONENTS) + ["STATIC_MEMP"]
+
+
+def _comps(n: int) -> List[str]:
+    """The component list a row / factor vector of length n refers to."""
+    return CAL_COMPONENTS if n == len(CAL_COMPONENTS) else list(COMPONENTS)
 
 
 def design_matrix(kernels: Sequence[Dict], components: Sequence[str] = COMPONENTS) -> np.ndarray:
@@ -123,7 +134,7 @@ def group_matrix(components: Sequence[str] = COMPONENTS, groups: Dict[str, List[
 
 def fit_groups(A: np.ndarray, b: np.ndarray, groups: Dict[str, List[str]] = COMPONENT_GROUPS, **kw) -> np.ndarray:
     """Per-component factors constrained to be equal within each group."""
-    names, M = group_matrix(groups=groups)
+    names, M = group_matrix(components=_comps(np.asarray(A).shape[1]), groups=groups)
     xg = fit_scaling(np.asarray(A) @ M.T, b, **kw)
     x = M.T @ xg
     x[M.sum(axis=0) == 0] = 1.0
@@ -141,7 +152,7 @@ def leave_one_out_groups(A: np.ndarray, b: np.ndarray, **kw) -> np.ndarray:
 
 
 def group_factors(x: Sequence[float], groups: Dict[str, List[str]] = COMPONENT_GROUPS) -> Dict[str, float]:
-    names, M = group_matrix(groups=groups)
+    names, M = group_matrix(components=_comps(len(x)), groups=groups)
     return {g: float(np.asarray(x)[list(M[i]).index(1.0)]) if M[i].any() else 1.0 for i, g in enumerate(names)}
 
 
@@ -218,17 +229,19 @@ def leave_one_out(A: np.ndarray, b: np.ndarray, **kw) -> np.ndarray:
     return out
 
 
-def apply_factors(xml_in: str, xml_out: str, x: Sequence[float], components: Sequence[str] = COMPONENTS,
+def apply_factors(xml_in: str, xml_out: str, x: Sequence[float], components: Optional[Sequence[str]] = None,
                   power_cap: Optional[float] = None) -> Dict:
     """Multiply the XML parameters behind every component by its factor
     (and set the package ``power_cap`` when one was fitted)."""
     p = read_xml(xml_in)
     if power_cap:
         p["power_cap"] = float(power_cap)
+    components = list(components) if components is not None else _comps(len(x))
+    split = "STATIC_MEMP" in components
     for c, f in zip(components, x):
         keys = COMPONENT_PARAMS.get(c)
         if keys is None:
-            keys = [k for k in p if k.startswith("static_")]
+            keys = [k for k in p if k.startswith("static_") and not (split and k in COMPONENT_PARAMS["STATIC_MEMP"])]
         for k in keys:
             p[k] = p.get(k, 1.0) * float(f)
     write_xml(xml_out, p, comment=f"calibrated from {xml_in}")
@@ -241,7 +254,7 @@ def apply_factors(xml_in: str, xml_out: str, x: Sequence[float], components: Seq
 # core dynamic power ~ s V^2, static and idle-core power ~ V, DRAM ~ s (its own
 # rail), the constant term fixed.  A row of A holds a kernel's component powers
 # simulated at the nominal clock; dvfs_scale() maps it to clock ratio s.
-_DVFS_V = ("STATICP", "IDLE_COREP")
+_DVFS_V = ("STATICP", "IDLE_COREP", "STATIC_MEMP")
 _DVFS_FIXED = ("CONSTP",)
 _DVFS_S = ("DRAMP", "MCP")
 
@@ -250,15 +263,30 @@ def voltage_ratio(s, v_floor: float):
     return v_floor + (1.0 - v_floor) * np.asarray(s, np.float64)
 
 
-def dvfs_scale(s: float, v_floor: float, components: Sequence[str] = COMPONENTS) -> np.ndarray:
+def dvfs_scale(s: float, v_floor: float, components: Optional[Sequence[str]] = None, n: int = 0) -> np.ndarray:
     v = float(voltage_ratio(s, v_floor))
+    components = components if components is not None else _comps(n or len(COMPONENTS))
     return np.array([1.0 if c in _DVFS_FIXED else v if c in _DVFS_V else s if c in _DVFS_S else s * v * v
                      for c in components])
 
 
 def dvfs_matrix(A: np.ndarray, ratios: Sequence[float], v_floor: float) -> np.ndarray:
     A = np.asarray(A, np.float64)
-    return np.stack([A[i] * dvfs_scale(float(r), v_floor) for i, r in enumerate(ratios)])
+    return np.stack([A[i] * dvfs_scale(float(r), v_floor, n=A.shape[1]) for i, r in enumerate(ratios)])
+
+
+# groups of the DVFS-aware MI355X calibration: one factor per pipe the
+# validation kernels exercise separately -- the always-on part, the VALU pipe
+# (instruction issue, fp32 / int / fp64 / transcendental work), the matrix
+# cores, the memory pipeline on the CU and in the L2 (LDS, L1, L2, NoC and the
+# static power of those units when in use), and the HBM side
+POWER_GROUPS: Dict[str, List[str]] = {
+    "idle_static": ["CONSTP", "IDLE_COREP", "STATICP"],
+    "valu": FINE_GROUPS["frontend"] + FINE_GROUPS["valu"] + FINE_GROUPS["sfu"] + FINE_GROUPS["fp64"],
+    "tensor": FINE_GROUPS["tensor"],
+    "memory": FINE_GROUPS["lds"] + FINE_GROUPS["cache"] + ["STATIC_MEMP"],
+    "dram": FINE_GROUPS["dram"],
+}
 
 
 def fit_groups_relative(A: np.ndarray, b: np.ndarray, groups: Dict[str, List[str]] = FINE_GROUPS,
@@ -273,7 +301,7 @@ def fit_groups_relative(A: np.ndarray, b: np.ndarray, groups: Dict[str, List[str
 def governor_ratio(a_row: np.ndarray, x: np.ndarray, cap: float, v_floor: float, s_min: float = 0.5) -> float:
     """The DVFS governor of csrc/power/power.cc (dvfs_clock_ratio) on one
     kernel: the highest clock ratio in [s_min, 1] whose power fits the cap."""
-    p = lambda s: float(a_row @ (x * dvfs_scale(s, v_floor)))
+    p = lambda s: float(a_row @ (x * dvfs_scale(s, v_floor, n=len(x))))
     if cap <= 0 or p(1.0) <= cap:
         return 1.0
     lo, hi = s_min, 1.0
@@ -306,7 +334,7 @@ def leave_one_out_dvfs(A: np.ndarray, b: np.ndarray, ratios: Sequence[float], v_
         x = fit_groups_relative(Ad[keep], b[keep], **kw)
         at_meas[i] = Ad[i] @ x
         s_gov[i] = governor_ratio(A[i], x, cap, v_floor, s_min)
-        at_gov[i] = A[i] @ (x * dvfs_scale(s_gov[i], v_floor))
+        at_gov[i] = A[i] @ (x * dvfs_scale(s_gov[i], v_floor, n=A.shape[1]))
     return at_meas, at_gov, s_gov
 
 

@@ -221,6 +221,8 @@ def steady_components(trace_csv: str, lo: float = 0.25, hi: float = 0.75) -> Opt
         if j < 2:
             continue
         out[name] = float(np.mean([float(r[j]) for r in mid]))
+    if "STATIC_MEMP" in out:  # STATICP keeps its core (unit-mix category) part
+        out["STATICP"] -= out["STATIC_MEMP"]
     return out
 
 
@@ -334,7 +336,7 @@ def run_traces(kernelslist: str, measured_csv: str, work: str, out_xml: str, con
     order = list(meas)  # measure mode prints the kernels in launch order
     if len(reps) != len(order):
         raise RuntimeError(f"{len(reps)} simulated kernels vs {len(order)} measured")
-    A = calibrate.design_matrix(reps)
+    A = calibrate.design_matrix(reps, calibrate.CAL_COMPONENTS)
     b = np.array([meas[n] for n in order])
     rows, meta = measured_rows(measured_csv)
     if all(not math.isnan(rows[n]["sclk"]) for n in order) and meta.get("power_cap_w", float("nan")) > 0:
@@ -343,6 +345,7 @@ def run_traces(kernelslist: str, measured_csv: str, work: str, out_xml: str, con
         calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
         _set_dvfs_params(out_xml, s)
     else:
+        A = calibrate.design_matrix(reps)
         s = fit_report(A, b, order, bound)
         calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
     s.update(sim_cycles=[r.get("gpu_sim_cycle", 0.0) for r in reps], traces="automatic ISA traces (isatrace)",
@@ -380,13 +383,14 @@ def fit_report_dvfs(A: np.ndarray, b: np.ndarray, order: List[str], sclk: List[f
         if v_floor is None:
             v_floor, vsrc = DEFAULT_V_FLOOR, "assumed (no rail voltage reported by amd-smi)"
     s_min = float(max(0.3, min(1.0, np.nanmin(ratios) * 0.9)))
-    kw = dict(groups=calibrate.FINE_GROUPS, lower=1.0 / bound, upper=bound)
+    groups = calibrate.POWER_GROUPS if A.shape[1] == len(calibrate.CAL_COMPONENTS) else calibrate.FINE_GROUPS
+    kw = dict(groups=groups, lower=1.0 / bound, upper=bound)
     Ad = calibrate.dvfs_matrix(A, ratios, v_floor)
     x = calibrate.fit_groups_relative(Ad, b, **kw)
     fit = Ad @ x
     loo_meas, loo_gov, s_gov = calibrate.leave_one_out_dvfs(A, b, ratios, v_floor, cap, s_min, **kw)
     gov_fit = np.array([calibrate.governor_ratio(A[i], x, cap, v_floor, s_min) for i in range(len(b))])
-    gf = calibrate.group_factors(x, calibrate.FINE_GROUPS)
+    gf = calibrate.group_factors(x, groups)
     at_bound = [g for g, v in gf.items() if v <= 1.0 / bound * 1.001 or v >= bound * 0.999]
     before = A.sum(axis=1)
     return dict(kernels=list(order), measured_w=b.tolist(), uncalibrated_w=before.tolist(), calibrated_w=fit.tolist(),
@@ -401,7 +405,8 @@ def fit_report_dvfs(A: np.ndarray, b: np.ndarray, order: List[str], sclk: List[f
                               loo_clock_ratio=s_gov.tolist(), fit_clock_ratio=gov_fit.tolist(),
                               clock_ratio_mae=float(np.mean(np.abs(s_gov - ratios))),
                               throttled_kernels=[n for n, r in zip(order, ratios) if r < 0.98]),
-                components=list(calibrate.COMPONENTS), components_w=np.asarray(A).tolist(),
+                components=list(calibrate.CAL_COMPONENTS if A.shape[1] == len(calibrate.CAL_COMPONENTS)
+                                else calibrate.COMPONENTS), components_w=np.asarray(A).tolist(), groups=groups,
                 bounds=[1.0 / bound, bound], model="DVFS: measured cap and clocks, V(f) line", _x=x)
 
 

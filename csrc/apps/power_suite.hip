@@ -325,6 +325,12 @@ int main(int argc, char** argv) {
   // occupancy VALU rate while the measured socket power is 0.55x (the
   // single-wave issue rate and the ~1.3 kW power cap are not modelled)
   const int sc = trace ? 1 : 2048;  // loop scale
+  // register-only kernels (VALU / SFU / MFMA) are traced 8x longer: their
+  // traces hold only the basic-block records, and the simulated power is
+  // read from the steady-state samples in the middle of the kernel
+  // (power/mi355x_validation.py steady_components), which the wave-launch
+  // ramp of a 1x loop barely reaches
+  const int scv = trace ? 8 : sc;
   const size_t nbig = trace ? (size_t)2 << 20 : big / 16;  // trace: 32 MB sweep
   const dim3 b(256);
   auto g = [&](int per_cu) { return dim3(cus * per_cu); };
@@ -334,16 +340,16 @@ int main(int argc, char** argv) {
   };
   std::vector<K> ks = {
       {"idle", [&] { k_idle<<<1, 64>>>(); }},
-      {"fp32_fma_occ1", [&] { k_fp32<<<g(1), b>>>(sink, 8 * sc); }},
-      {"fp32_fma_occ2", [&] { k_fp32<<<g(2), b>>>(sink, 8 * sc); }},
-      {"fp32_fma_occ4", [&] { k_fp32<<<g(4), b>>>(sink, 8 * sc); }},
-      {"fp32_fma", [&] { k_fp32<<<g(8), b>>>(sink, 8 * sc); }},
-      {"int32_mad", [&] { k_int<<<g(8), b>>>(sink, 8 * sc); }},
-      {"fp64_fma", [&] { k_fp64<<<g(8), b>>>(sink, 4 * sc); }},
-      {"sfu_sqrt_exp", [&] { k_sfu<<<g(8), b>>>(sink, 8 * sc); }},
-      {"mfma_bf16", [&] { k_mfma<<<g(8), b>>>(sink, 2 * sc); }},
-      {"mfma_bf16_occ2", [&] { k_mfma<<<g(2), b>>>(sink, 2 * sc); }},
-      {"mfma_valu", [&] { k_mfma_valu<<<g(8), b>>>(sink, 2 * sc); }},
+      {"fp32_fma_occ1", [&] { k_fp32<<<g(1), b>>>(sink, 8 * scv); }},
+      {"fp32_fma_occ2", [&] { k_fp32<<<g(2), b>>>(sink, 8 * scv); }},
+      {"fp32_fma_occ4", [&] { k_fp32<<<g(4), b>>>(sink, 8 * scv); }},
+      {"fp32_fma", [&] { k_fp32<<<g(8), b>>>(sink, 8 * scv); }},
+      {"int32_mad", [&] { k_int<<<g(8), b>>>(sink, 8 * scv); }},
+      {"fp64_fma", [&] { k_fp64<<<g(8), b>>>(sink, 4 * scv); }},
+      {"sfu_sqrt_exp", [&] { k_sfu<<<g(8), b>>>(sink, 8 * scv); }},
+      {"mfma_bf16", [&] { k_mfma<<<g(8), b>>>(sink, 2 * scv); }},
+      {"mfma_bf16_occ2", [&] { k_mfma<<<g(2), b>>>(sink, 2 * scv); }},
+      {"mfma_valu", [&] { k_mfma_valu<<<g(8), b>>>(sink, 2 * scv); }},
       {"lds_read", [&] { k_lds_read<<<g(8), b>>>(sink, 16 * sc); }},
       {"lds_write", [&] { k_lds_write<<<g(8), b>>>(sink, 16 * sc); }},
       {"lds_fp32", [&] { k_lds_fp32<<<g(8), b>>>(sink, 8 * sc); }},
@@ -358,9 +364,9 @@ int main(int argc, char** argv) {
       {"atomic_l2", [&] { k_atomic<<<g(4), b>>>(ctr, trace ? 2 : sc / 8); }},
       {"fp32_fma_light", [&] { k_fp32<<<g(8), b>>>(sink, sc); }},
       // round 3: more occupancy / unit-mix points between the saturating ones
-      {"mfma_bf16_occ4", [&] { k_mfma<<<g(4), b>>>(sink, 2 * sc); }},
-      {"sfu_occ2", [&] { k_sfu<<<g(2), b>>>(sink, 8 * sc); }},
-      {"fp64_fma_occ2", [&] { k_fp64<<<g(2), b>>>(sink, 4 * sc); }},
+      {"mfma_bf16_occ4", [&] { k_mfma<<<g(4), b>>>(sink, 2 * scv); }},
+      {"sfu_occ2", [&] { k_sfu<<<g(2), b>>>(sink, 8 * scv); }},
+      {"fp64_fma_occ2", [&] { k_fp64<<<g(2), b>>>(sink, 4 * scv); }},
       {"hbm_read_occ2", [&] { k_read<<<g(2), b>>>(buf, nbig, trace ? 1 : 4, sink); }},
       {"l2_write", [&] { k_write<<<g(8), b>>>(buf, l2 / 16, trace ? 2 : 2 * sc); }},
       {"lds_read_occ2", [&] { k_lds_read<<<g(2), b>>>(sink, 16 * sc); }},

@@ -133,10 +133,12 @@ PowerReport PowerModel::compute(const Activity& a, double core_mhz, uint32_t n_s
   double lanes = a.avg_lanes > 1 ? a.avg_lanes : 1;
   double busy_frac = n_sm ? std::max(0.0, 1.0 - a.idle_sms / n_sm) : 1.0;
   r.static_w = (param("static_" + cat + "_flane", 0) + param("static_" + cat + "_addlane", 0) * (lanes - 1)) * busy_frac;
-  if (a.a[PA_SHRD_ACC] > 0) r.static_w += param("static_shared_flane", 0) * busy_frac;
-  if (a.a[PA_DC_RH] + a.a[PA_DC_RM] + a.a[PA_DC_WH] + a.a[PA_DC_WM] > 0) r.static_w += param("static_l1_flane", 0) * busy_frac;
-  if (a.a[PA_L2_RH] + a.a[PA_L2_RM] + a.a[PA_L2_WH] + a.a[PA_L2_WM] > 0) r.static_w += param("static_l2_flane", 0);
-  r.static_w *= vr;
+  double smem = 0;
+  if (a.a[PA_SHRD_ACC] > 0) smem += param("static_shared_flane", 0) * busy_frac;
+  if (a.a[PA_DC_RH] + a.a[PA_DC_RM] + a.a[PA_DC_WH] + a.a[PA_DC_WM] > 0) smem += param("static_l1_flane", 0) * busy_frac;
+  if (a.a[PA_L2_RH] + a.a[PA_L2_RM] + a.a[PA_L2_WH] + a.a[PA_L2_WM] > 0) smem += param("static_l2_flane", 0);
+  r.static_w = (r.static_w + smem) * vr;
+  r.static_mem = smem * vr;
   r.total = r.dynamic + r.static_w + r.constant + r.idle;
   for (int i = 0; i < PA_COUNT; ++i) r.cmp[kActCmp[i]] += r.dynamic_w[i];
   r.cmp[PC_IDLE_CORE] = r.idle;
@@ -250,13 +252,14 @@ void PowerTracker::write_kernel(std::ostream& os, const std::string& header) con
 void PowerTracker::write_trace_header(std::ostream& os) const {
   os << "cycle,total_power";
   for (int i = 0; i < PC_COUNT; ++i) os << "," << kPwrCmpName[i];
-  os << "\n";
+  // the memory-unit share of STATICP (calibration splits the static factor)
+  os << ",STATIC_MEMP\n";
 }
 
 void PowerTracker::write_trace_line(std::ostream& os, const PowerReport& r, uint64_t cycle) const {
   os << cycle << "," << r.total;
   for (int i = 0; i < PC_COUNT; ++i) os << "," << r.cmp[i];
-  os << "\n";
+  os << "," << r.static_mem << "\n";
 }
 
 void PowerTracker::write_steady(std::ostream& os, const std::string& kernel) const {

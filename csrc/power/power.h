@@ -72,6 +72,7 @@ struct PowerReport {
   double dynamic_w[PA_COUNT] = {};
   double dynamic = 0;
   double static_w = 0;
+  double static_mem = 0;    // the part of static_w from the LDS / L1 / L2 "unit in use" terms
   double constant = 0;
   double idle = 0;
   double total = 0;
