@@ -127,9 +127,11 @@ def main(argv=None) -> int:
         print(f"# rocprof_idle_per_block_ns {ib:.4f}")
         print(f"# idle_launch_cycles {int(round(ia * mhz / 1000.0))}")
         # the model's launch latency (to the first workgroup) is the idle
-        # launch; a queued kernel pays the same plus the minimum duration above
-        print(f"-gpgpu_kernel_launch_latency {int(round(ia * mhz / 1000.0))}")
-        print(f"-gpgpu_kernel_launch_latency_queued {int(round(ia * mhz / 1000.0))}")
+        # launch; a queued kernel pays the same plus the minimum duration
+        # above.  Reported, not applied: the idle launch measured 1.5 us and
+        # 2.1 us on two boxes of the same round, and the preset keeps the
+        # values that the suite's correlation supports (models/presets.py)
+        print(f"# suggested -gpgpu_kernel_launch_latency {int(round(ia * mhz / 1000.0))}")
         print(f"-gpgpu_TB_launch_latency {int(round(ib * mhz / 1000.0))}")
     # the first kernel after a host-to-device copy vs the same kernel re-run
     ac = read_durations(run_dir, "ub_touch_after_copy")
@@ -139,7 +141,7 @@ def main(argv=None) -> int:
         g_med = float(np.median([x for v in ag.values() for x in v]))
         print(f"# after_copy_kernel_ns {a_med:.1f}\n# same_kernel_again_ns {g_med:.1f}")
         print(f"# after_copy_extra_cycles {int(round((a_med - g_med) * mhz / 1000.0))}")
-        print(f"-sim_first_kernel_latency {max(0, int(round((a_med - g_med) * mhz / 1000.0)))}")
+        print(f"# suggested -sim_first_kernel_latency {max(0, int(round((a_med - g_med) * mhz / 1000.0)))}")
     # back-to-back chains: steady-state start-to-start interval and duration
     ch = chain_stats(run_dir)
     if ch:

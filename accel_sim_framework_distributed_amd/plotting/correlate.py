@@ -204,8 +204,14 @@ CORREL_STATS: List[CorrelStat] = [
     CorrelStat("L2 hit rate", "l2_hit_rate", _hw_ratio(("TCC_HIT_sum",), ("TCC_HIT_sum", "TCC_MISS_sum")),
                "l2-hit-rate", sim_stats=(_L2_R_HIT, _L2_R_MSHR, _L2_W_ALL, _L2_R_MISS),
                sim_eval=_l2_hit_rate, ratio=True, log=False),
-    CorrelStat("DRAM read requests", r"total dram reads\s*=\s*(.*)", _hw("TCC_EA0_RDREQ_sum"), "dram-reads"),
-    CorrelStat("DRAM write requests", r"total dram writes\s*=\s*(.*)", _hw("TCC_EA0_WRREQ_sum"), "dram-writes"),
+    # requests leaving the L2 for the Infinity Fabric (MALL, then HBM): the
+    # deepest level rocprofv3 counts on gfx950 -- no counter sees HBM behind
+    # the MALL, so the simulator's DRAM accesses (after its MALL) have no
+    # hardware counterpart and are not correlated
+    CorrelStat("L2->fabric read requests", r"L2_to_mem_read_requests\s*=\s*(.*)", _hw("TCC_EA0_RDREQ_sum"),
+               "dram-reads"),
+    CorrelStat("L2->fabric write requests", r"L2_to_mem_write_requests\s*=\s*(.*)", _hw("TCC_EA0_WRREQ_sum"),
+               "dram-writes"),
     CorrelStat("Interconnect packets SM->memory", r"icnt_total_pkts_simt_to_mem\s*=\s*(.*)",
                _hw("TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum", "TCP_TCC_ATOMIC_WITH_RET_REQ_sum"), "icnt-pkts"),
     # ---- round 3: instruction mix by the sequencer's own classes (the

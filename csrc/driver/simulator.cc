@@ -1103,10 +1103,12 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   {
     // traffic leaving the L2 for memory (Infinity Fabric on CDNA4: what
     // rocprofv3 counts as TCC_EA0_RDREQ / WRREQ) and the MALL in front of DRAM
-    uint64_t mrd = 0, mwr = 0, mh = 0, mm = 0, mw = 0, mwb = 0;
+    uint64_t mrd = 0, mwr = 0, mh = 0, mm = 0, mw = 0, mwb = 0, mrq = 0, mwq = 0;
     for (auto& m : cmem) {
       mrd += m.l2_mem_rd;
       mwr += m.l2_mem_wr;
+      mrq += m.l2_mem_rd_req;
+      mwq += m.l2_mem_wr_req;
       mh += m.mall_rd_hit;
       mm += m.mall_rd_miss;
       mw += m.mall_wr;
@@ -1114,6 +1116,8 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
     }
     print("L2_to_mem_read_sectors = %llu\n", (unsigned long long)mrd);
     print("L2_to_mem_write_sectors = %llu\n", (unsigned long long)mwr);
+    print("L2_to_mem_read_requests = %llu\n", (unsigned long long)mrq);
+    print("L2_to_mem_write_requests = %llu\n", (unsigned long long)mwq);
     if (cfg_.mall_sets) {
       print("MALL_read_hits = %llu\n", (unsigned long long)mh);
       print("MALL_read_misses = %llu\n", (unsigned long long)mm);

@@ -88,6 +88,7 @@ void host_flush_l2(ChanState* chs, uint32_t nch, const SimCfg& c, bool writeback
           if (!(L.valid && L.dirty)) continue;
           const uint32_t n = (uint32_t)popc64(L.dirty);
           st.l2_mem_wr += n;
+          st.l2_mem_wr_req += wr_requests(L.dirty);
           st.l2_evict_dirty++;
           if (!mall) {
             st.dram_wr += n;  // straight to DRAM, untimed (between kernels)

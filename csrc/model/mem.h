@@ -96,6 +96,9 @@ struct MemStats {
   // Infinity Fabric traffic rocprofv3 counts as TCC_EA0_RDREQ / WRREQ), and
   // how the memory-attached cache (MALL) in front of DRAM served it
   uint64_t l2_mem_rd, l2_mem_wr;
+  // the same traffic in requests (a line fill, a write packet or a line
+  // write-back is one request, of 32-128 B): rocprofv3 TCC_EA0_RDREQ / WRREQ
+  uint64_t l2_mem_rd_req, l2_mem_wr_req;
   uint64_t mall_rd_hit, mall_rd_miss, mall_wr, mall_wb;
 };
 
@@ -195,6 +198,9 @@ SIM_HDI bool l2dram_can(const ChanState& ch, const SubPart& sp, const SimCfg& c,
   return sp.n_l2dram + n <= c.q_l2_dram && ch.lat_n + ch.q_n + n <= c.dram_credits &&
          ch.lat_n + n <= (uint32_t)kDramLat;
 }
+
+// write requests to the fabric are at most 64 B: one per half line with data
+SIM_HDI uint32_t wr_requests(uint32_t sectors) { return ((sectors & 3u) ? 1u : 0u) + ((sectors & 12u) ? 1u : 0u); }
 
 SIM_HDI void l2dram_push(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, uint64_t line,
                          uint32_t sector, bool write, uint64_t now_fs) {
@@ -335,6 +341,7 @@ SIM_HDI int l2_alloc(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub, 
     for (uint32_t s = 0; s < 4; ++s)
       if (L.dirty >> s & 1u) l2dram_push(ch, sp, c, sub, L.tag, s, true, now_fs);
     sp.st.l2_evict_dirty++;
+    sp.st.l2_mem_wr_req += wr_requests(L.dirty);
   }
   L.tag = line;
   L.valid = 0;
@@ -380,6 +387,7 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
       if (!l2dram_can(ch, sp, c, n)) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
       for (uint32_t s = 0; s < 4; ++s)
         if (p.sectors >> s & 1u) l2dram_push(ch, sp, c, sub, p.addr, s, true, now_fs);
+      sp.st.l2_mem_wr_req += wr_requests(p.sectors);
       if (way >= 0) T[set * g.assoc + way].valid |= p.sectors;
       trace(3);
     } else {
@@ -397,6 +405,7 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
         if (!l2dram_can(ch, sp, c, n)) { sp.st.l2[stype][L2O_RES_FAIL]++; return false; }
         for (uint32_t s2 = 0; s2 < 4; ++s2)
           if (p.sectors >> s2 & 1u) l2dram_push(ch, sp, c, sub, p.addr, s2, true, now_fs);
+        sp.st.l2_mem_wr_req += wr_requests(p.sectors);
         sp.st.l2[stype][L2O_MISS]++;
         trace(1);
         reply_push(sp, P_WR_ACK, p, p.sectors);
@@ -441,6 +450,7 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
         sp.mshr[mi].requested |= rd;
         for (uint32_t s2 = 0; s2 < 4; ++s2)
           if (rd >> s2 & 1u) l2dram_push(ch, sp, c, sub, p.addr, s2, false, now_fs);
+        sp.st.l2_mem_rd_req++;
       }
     }
     reply_push(sp, P_WR_ACK, p, p.sectors);
@@ -486,6 +496,7 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
     sp.mshr[mi].requested |= need_req;
     for (uint32_t s = 0; s < 4; ++s)
       if (need_req >> s & 1u) l2dram_push(ch, sp, c, sub, p.addr, s, false, now_fs);
+    sp.st.l2_mem_rd_req++;
     sp.st.l2[stype][L2O_MISS]++;
     trace(1);
   }

@@ -12,6 +12,12 @@
 // A next-kernel walk at the same-kernel latency means the L2 kept the lines;
 // one at the MALL latency means the kernel boundary wrote back and
 // invalidated them (the multi-XCD release / acquire).
+// Measured on MI355X: read lines kept, written lines dropped in this minimal
+// two-kernel case; the Rodinia suite's L2 -> fabric read traffic
+// (TCC_EA0_RDREQ) matches invalidating every line within 1.7 % and keeping
+// clean lines undercounts it by up to 67 % (profiles/correlation), so the
+// simulator invalidates all lines; the option line follows the written-line
+// result.
 #include "ubench.h"
 
 __global__ void __launch_bounds__(64) rel_walk(const uint32_t* __restrict__ next, int n, int warm, uint64_t* out) {
@@ -107,7 +113,7 @@ int main() {
   printf("# l2_same_kernel_latency %.1f\n# l2_next_kernel_read_latency %.1f\n# l2_next_kernel_write_latency %.1f\n",
          s, r, w);
   printf("# l2_cold_latency %.1f\n# l2_kept_across_kernels %d\n", c, (kept_read && kept_write) ? 1 : 0);
-  ub_opt("-sim_l2_kernel_release", (kept_read && kept_write) ? 0 : 1);
+  ub_opt("-sim_l2_kernel_release", kept_write ? 0 : 1);
   UB_CHECK(hipFree(d_next));
   UB_CHECK(hipFree(d_src));
   UB_CHECK(hipFree(d_out));

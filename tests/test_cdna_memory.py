@@ -178,3 +178,4 @@ def test_line_granular_l2_fetches_whole_lines(native, tmp_path):
     line = _run(native, kl, {"-gpgpu_cache:dl2": "N:32:128:24,L:B:m:L:P,A:192:4,32:0,32"})
     assert _stat(sect.output, "L2_to_mem_read_sectors") == 64
     assert _stat(line.output, "L2_to_mem_read_sectors") == 4 * 64
+
