@@ -37,6 +37,9 @@ def apps(tmp_path_factory):
 def _run(native, kl, extra):
     s = native.Simulator(presets.args_for("QV100", extra) + ["-trace", kl, "-gpgpu_perf_sim_memcpy", "0"], False)
     assert s.run() == 0
+    # a write-back L1 never drops a dirty victim: the LD/ST unit consumes a
+    # fill reply only when the injection queue has room for its write-back
+    assert "L1 write-backs lost" not in s.output
     return s.output
 
 
