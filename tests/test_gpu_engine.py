@@ -237,3 +237,28 @@ def test_kernel_without_memory_ops_gpu_equals_cpu(gpu_mod, tmp_path):
     g = sim.simulate(kl, "MI355X", engine="gpu")
     c = sim.simulate(kl, "MI355X", engine="cpu")
     assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
+
+
+def test_power_report_and_dvfs_gpu_equals_cpu(gpu_mod, tmp_path):
+    """Power sampling on the MI355X engine: the per-kernel AccelWattch report
+    (every component's avg / max / min) and the DVFS governor's clock choices
+    are identical to the CPU engine's, sample by sample."""
+    from accel_sim_framework_distributed_amd.models import presets
+    from accel_sim_framework_distributed_amd.power import report, xmlcfg
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    kl = rodinia.write_app(str(tmp_path / "hs"), rodinia.hotspot(512, 2, 1))
+    p = xmlcfg.default_params("QV100")
+    xml = str(tmp_path / "aw.xml")
+    xmlcfg.write_xml(xml, dict(p, power_cap=150.0, dvfs_v_floor=0.6))
+    out = {}
+    for eng in ("cpu", "gpu"):
+        rep = str(tmp_path / f"p_{eng}.log")
+        args = presets.args_for("QV100", {"-power_simulation_enabled": "1", "-accelwattch_xml_file": xml,
+                                          "-gpgpu_runtime_stat": "200:0", "-dvfs_enabled": "1",
+                                          "-power_report_file": rep, "-sim_engine": eng}) + ["-trace", kl]
+        s = gpu_mod.Simulator(args, False)
+        assert s.run() == 0
+        out[eng] = (s.tot_cycle, report.parse_power_report(rep),
+                    [l for l in s.output.splitlines() if l.startswith(("gpu_sim_time_ns", "gpu_avg_core_clock"))])
+    assert out["gpu"] == out["cpu"]
+    assert out["cpu"][1][0]["kernel_avg_clock_ratio"] < 1.0  # the governor did act
