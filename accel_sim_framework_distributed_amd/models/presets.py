@@ -580,6 +580,9 @@ def _mi355x() -> Dict[str, str]:
         # a release that writes their dirty lines back (to the MALL) and the
         # next one starts with them invalidated
         "-sim_l2_kernel_release": "1",
+        # TCP -> TCC writes are at most 64 B (TCC_WRITE counts two requests
+        # for a store covering a whole 128 B line)
+        "-sim_l1_write_request_bytes": "64",
         # kernel launch as rocprofv3 durations see it (ub_launch +
         # hw_stats/launch_latency.py): 1.5 us from an idle queue to the first
         # workgroup; a kernel queued behind another lasts >= 4.7 us (the

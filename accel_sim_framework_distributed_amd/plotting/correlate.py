@@ -188,7 +188,9 @@ CORREL_STATS: List[CorrelStat] = [
                sim_eval=lambda d: sum(d.values())),
     CorrelStat("L1 read misses (L1->L2 reads)", S_L1 % ("GLOBAL_ACC_R", "MISS"), _hw("TCP_TCC_READ_REQ_sum"),
                "l1-read-miss"),
-    CorrelStat("L1->L2 write requests", S_L1 % ("GLOBAL_ACC_W", "TOTAL_ACCESS"), _hw("TCP_TCC_WRITE_REQ_sum"),
+    # the write requests the L1 sends (a store may be split into 64 B
+    # requests, -sim_l1_write_request_bytes): what arrives at the L2
+    CorrelStat("L1->L2 write requests", S_L2 % ("GLOBAL_ACC_W", "TOTAL_ACCESS"), _hw("TCP_TCC_WRITE_REQ_sum"),
                "l1-writes"),
     CorrelStat("L1 read hit rate", "l1_hit_rate",
                _hw_ratio(("TCP_TCC_READ_REQ_sum",), ("TCP_TOTAL_CACHE_ACCESSES_sum",), one_minus=True),

@@ -38,6 +38,7 @@ constexpr int kEjectQ = 32;         // cluster ejection buffer (-gpgpu_n_cluster
 constexpr int kLdstRespQ = 8;       // LD/ST response FIFO (-gpgpu_n_ldst_response_buffer_size cap)
 constexpr int kMaxAccess = 64;      // coalesced accesses of one instruction
 // memory side (per sub-partition)
+constexpr int kMaxXcd = 16;        // XCDs (-sim_xcd)
 constexpr int kMaxL2LinesCh = 2048; // per memory channel, shared by its sub-partitions
 constexpr int kMaxL2Mshr = 256;
 constexpr int kMaxL2Wait = 256;
@@ -258,6 +259,7 @@ struct SimCfg {
   // request goes to the slice of its own XCD selected by the address.  Data
   // read by several XCDs is cached (and missed) in each of them.
   uint32_t n_xcd;
+  uint32_t l1_wr_req_bytes;  // -sim_l1_write_request_bytes: 64 = a store is one request per 64 B half line
   uint32_t log2_spx;        // log2(sub-partitions per XCD)
   // -sim_mall <sets>:<assoc>: the memory-attached last-level cache (AMD
   // Infinity Cache / MALL) in front of every DRAM channel, sectored like the

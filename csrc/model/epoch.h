@@ -90,6 +90,50 @@ SIM_HDI void cta_dispatch(SMState& s, const SmCtx& x, uint32_t ks, const UnitPub
   s.next_cta[ks] = base < k.n_cta ? base : k.n_cta;
 }
 
+// -sim_xcd: the hardware hands workgroup i to XCD i % n_xcd (round robin
+// over the XCDs at every dispatch), so the CTAs of residue x go to the SMs of
+// XCD x (SM s belongs to XCD s % n_xcd), in the same rounds as above within
+// each XCD.  Every SM advances every XCD's cursor (the state is replicated).
+template <class P>
+SIM_HDI void cta_dispatch_xcd(SMState& s, const SmCtx& x, uint32_t ks, const UnitPub* pubs, uint32_t n_sm,
+                              uint32_t rot) {
+  const KernelDesc& k = x.kt->k[ks];
+  if (s.next_cta[ks] >= k.n_cta) return;
+  const uint32_t nx = x.cfg->n_xcd;
+  const uint32_t me = s.id;
+  const uint32_t sh = ks * 8;
+  auto req = [&](int j) -> uint32_t { return (uint32_t)(pubs[j].reqk >> sh) & 0xffu; };
+  const uint32_t my_q = req((int)me);
+  const uint32_t my_rank = (me + n_sm - rot) % n_sm;
+  uint32_t total = 0;
+  for (uint32_t xi = 0; xi < nx; ++xi) {
+    const uint32_t ncx = k.n_cta > xi ? (k.n_cta - xi + nx - 1) / nx : 0u;
+    uint32_t base = s.next_ctax[ks][xi];
+    for (uint32_t r = 0; r < (uint32_t)kMaxCta && base < ncx; ++r) {
+      const uint32_t pr = P::sum((int)n_sm, [&](int j) -> uint32_t {
+        return ((uint32_t)j % nx == xi && req(j) > r) ? 1u : 0u;
+      });
+      if (pr == 0) break;
+      if (me % nx == xi && my_q > r) {
+        const uint32_t pos = P::sum((int)n_sm, [&](int j) -> uint32_t {
+          return ((uint32_t)j % nx == xi && req(j) > r && ((uint32_t)j + n_sm - rot) % n_sm < my_rank) ? 1u : 0u;
+        });
+        const uint32_t j = base + pos;
+        if (j < ncx) {
+          int slot = -1;
+          for (uint32_t i = 0; i < (uint32_t)kMaxCta; ++i)
+            if (!s.cta_valid[i]) { slot = (int)i; break; }
+          if (slot >= 0) sm_launch_cta<P>(s, x, (uint32_t)slot, xi + nx * j, ks);
+        }
+      }
+      base += pr;
+    }
+    s.next_ctax[ks][xi] = base < ncx ? base : ncx;
+    total += s.next_ctax[ks][xi];
+  }
+  s.next_cta[ks] = total;
+}
+
 // kernel slots in launch (uid) order: older kernels are served first
 SIM_HDI uint32_t slot_order(const KernelTab& kt, uint8_t* order) {
   uint32_t n = 0;
@@ -156,6 +200,7 @@ SIM_HDI void sm_kernels_init(SMState& s, const SmCtx& x) {
     if (!(kt.active >> k & 1u) || s.k_uid[k] == kt.k[k].uid) continue;
     s.k_uid[k] = kt.k[k].uid;
     s.next_cta[k] = 0;
+    for (int xi = 0; xi < kMaxXcd; ++xi) s.next_ctax[k][xi] = 0;
     if (kt.k[k].flush_l1) {
       P::each(kMaxL1Lines, [&](int i) {
         s.l1[i].valid = 0;
@@ -190,8 +235,11 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t 
     uint8_t order[kMaxConc];
     const uint32_t nk = slot_order(kt, order);
     for (uint32_t i = 0; i < nk; ++i)
-      if (t0 >= kt.k[order[i]].ready_cycle)
-        cta_dispatch<P>(s, x, order[i], pub.sm[prev], c.n_sm, (uint32_t)((t0 / c.icnt_latency) % c.n_sm));
+      if (t0 >= kt.k[order[i]].ready_cycle) {
+        const uint32_t rot = (uint32_t)((t0 / c.icnt_latency) % c.n_sm);
+        if (c.n_xcd > 1) cta_dispatch_xcd<P>(s, x, order[i], pub.sm[prev], c.n_sm, rot);
+        else cta_dispatch<P>(s, x, order[i], pub.sm[prev], c.n_sm, rot);
+      }
   }
   // 3. (instructions are read from the kernel trace directly)
   P::prof(14);

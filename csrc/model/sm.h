@@ -278,6 +278,10 @@ struct alignas(16) SMState {
   // uid the SM initialised it for and the next CTA to hand out
   uint32_t k_uid[kMaxConc];
   uint32_t next_cta[kMaxConc];
+  // -sim_xcd: CTAs go round-robin over the XCDs (CTA i to an SM of XCD
+  // i % n_xcd, the hardware's workgroup dispatch); per XCD the CTAs of its
+  // residue handed out so far (next_cta is then their sum)
+  uint32_t next_ctax[kMaxConc][kMaxXcd];
   SMStats st;
   // statistics by word index (SK below); the GPU engine's register view keeps
   // the counters in lanes during the cycle loop (csrc/engine/sm_view.h)
@@ -373,6 +377,29 @@ SIM_HDI void sm_send(S& s, const SimCfg& c, uint8_t type, uint64_t line, uint8_t
   p.size = (type == P_WR) ? (uint16_t)(8 + bytes) : (uint16_t)8;
   p.aux = 0;
   s.outq_n++;
+}
+
+// -sim_l1_write_request_bytes 64: the L1 sends a store as one request per
+// 64 B half line it touches (gfx950's TCP -> TCC writes are at most 64 B:
+// TCC_WRITE counts two requests for a 128 B store); 128 keeps one per line.
+// Returns the number of packets (each is acknowledged).
+template <class S>
+SIM_HDI uint32_t wr_packets(const SimCfg& c, uint8_t sectors) {
+  if (c.l1_wr_req_bytes != 64) return 1u;
+  return ((sectors & 3u) && (sectors & 12u)) ? 2u : 1u;
+}
+template <class S>
+SIM_HDI uint32_t sm_send_write(S& s, const SimCfg& c, uint64_t line, uint8_t sectors, uint16_t bytes, uint32_t tag) {
+  if (wr_packets<S>(c, sectors) == 1) {
+    sm_send(s, c, P_WR, line, sectors, bytes, tag);
+    return 1;
+  }
+  const uint8_t lo = sectors & 3u, hi = sectors & 12u;
+  const uint32_t n = (uint32_t)popc64(sectors);
+  const uint16_t blo = (uint16_t)((uint32_t)bytes * (uint32_t)popc64(lo) / n);
+  sm_send(s, c, P_WR, line, lo, blo, tag);
+  sm_send(s, c, P_WR, line, hi, (uint16_t)(bytes - blo), tag);
+  return 2;
 }
 
 // move the head packet into the outbox once the injection port is free.  A
@@ -874,9 +901,8 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
       uint8_t pol = g.wpolicy;
       if (pol == WP_LOCAL_WB_GLOBAL_WT) pol = in.space == S_LOCAL ? WP_WRITE_BACK : WP_WRITE_EVICT;
       if (bypass || pol == WP_READ_ONLY) {
-        if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
-        sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
-        s.w_stores[w]++;
+        if (!sm_can_send_n(s, c, wr_packets<S>(c, a.sectors))) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+        s.w_stores[w] += sm_send_write(s, c, a.line, a.sectors, a.bytes, w);
         s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_BYPASS), 1);
       } else {
         const uint32_t set = cache_set_index(g, a.line);
@@ -894,9 +920,8 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
             L.dirty |= a.sectors;
             if (g.repl == REPL_LRU) L.lru = ++s.l1_stamp;
           } else {
-            if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
-            sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
-            s.w_stores[w]++;
+            if (!sm_can_send_n(s, c, wr_packets<S>(c, a.sectors))) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+            s.w_stores[w] += sm_send_write(s, c, a.line, a.sectors, a.bytes, w);
             L1Line& L = s.l1[set * g.assoc + way];
             if (pol == WP_WRITE_EVICT) L.valid &= (uint8_t)~a.sectors;
             else if (g.repl == REPL_LRU) L.lru = ++s.l1_stamp;
@@ -904,9 +929,8 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
           s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_HIT), 1);
         } else if (wa == 'N' || pol == WP_WRITE_EVICT) {
           // no write-allocate: straight to the L2
-          if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
-          sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
-          s.w_stores[w]++;
+          if (!sm_can_send_n(s, c, wr_packets<S>(c, a.sectors))) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+          s.w_stores[w] += sm_send_write(s, c, a.line, a.sectors, a.bytes, w);
           if (way >= 0 && pol == WP_WRITE_EVICT) s.l1[set * g.assoc + way].valid &= (uint8_t)~a.sectors;
           s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_MISS), 1);
         } else {
@@ -917,12 +941,9 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
           int mi = -1;
           if (fetch) mi = P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return s.mshr[i].valid && s.mshr[i].line == a.line; });
           const int mfree = fetch && mi < 0 ? P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return !s.mshr[i].valid; }) : 0;
-          const uint32_t need = (send_wr ? 1u : 0u) + (fetch ? 1u : 0u) + 1u;  // + a possible dirty victim
+          const uint32_t need = (send_wr ? wr_packets<S>(c, a.sectors) : 0u) + (fetch ? 1u : 0u) + 1u;  // + a possible dirty victim
           if (!sm_can_send_n(s, c, need) || mfree < 0) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
-          if (send_wr) {
-            sm_send(s, c, P_WR, a.line, a.sectors, a.bytes, w);
-            s.w_stores[w]++;
-          }
+          if (send_wr) s.w_stores[w] += sm_send_write(s, c, a.line, a.sectors, a.bytes, w);
           if (way < 0) {
             way = l1_victim<P>(s, g, set);
             l1_evict<P>(s, c, set * g.assoc + way);

@@ -179,3 +179,28 @@ def test_line_granular_l2_fetches_whole_lines(native, tmp_path):
     assert _stat(sect.output, "L2_to_mem_read_sectors") == 64
     assert _stat(line.output, "L2_to_mem_read_sectors") == 4 * 64
 
+
+
+def test_xcd_round_robin_cta_dispatch_and_64b_stores(native, tmp_path):
+    """-sim_xcd: CTA i runs on an SM of XCD i % n_xcd (the hardware's
+    workgroup round robin), so a CTA's lines stay in one XCD's L2 however the
+    SMs free up; -sim_l1_write_request_bytes 64 sends a full-line store as two
+    L2 write requests."""
+    k = KernelBuilder("_Z5storePf", (64, 1, 1), (128, 1, 1), nregs=16, kid=1)
+    g = k.g
+    # each warp stores one whole 128 B line
+    k.op("STG.E", [], [2, 4], base=BUF + g.gtid0 * 4, stride=4)
+    k.op("EXIT")
+    d = tmp_path / "st"
+    d.mkdir()
+    write_kernel_binary(str(d / "kernel-1.asimk"), k.build())
+    kl = write_kernelslist(str(d), ["kernel-1.asimk"])
+    base = {"-sim_xcd": "8"}
+    one = _run(native, kl, base)
+    two = _run(native, kl, dict(base, **{"-sim_l1_write_request_bytes": "64"}))
+    w1 = _stat(one.output, "L2_cache_stats_breakdown[GLOBAL_ACC_W][TOTAL_ACCESS]")
+    w2 = _stat(two.output, "L2_cache_stats_breakdown[GLOBAL_ACC_W][TOTAL_ACCESS]")
+    assert w1 == 64 * 4 and w2 == 2 * w1
+    assert one.tot_insn == two.tot_insn
+    with pytest.raises(Exception, match="sim_xcd"):
+        native.parse_config(presets.args_for("QV100", {"-sim_xcd": "32", "-gpgpu_n_clusters": "8"}))
