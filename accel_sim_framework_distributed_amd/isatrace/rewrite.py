@@ -18,10 +18,25 @@ assembled (``hipcc -S --cuda-device-only``):
   ``{0x80000000 | memory-op id, 0, exec}`` plus 64 per-lane 8-byte addresses
   computed from the instruction's own operands (global/flat/scratch/buffer/
   ds addressing modes);
-* records go to 8 KB chunks of one device buffer; a wave claims a chunk with
-  one atomic and tags it ``{0xC0000000 | chunk seq, wg x, wg y, wg z}`` +
-  ``{packed thread id of the first lane}``, so the host regroups chunks by
-  wave without any ordering between waves.
+* records go to 8 KB chunks; a wave claims a chunk with one atomic (a
+  ticket) and tags it ``{0xC0000000 | chunk seq, wg x, wg y, wg z}`` +
+  ``{packed thread id of the first lane, 0, 0, slot generation}``, so the host
+  regroups chunks by wave without any ordering between waves;
+* streaming (the default, ``ctl.mask != 0``): the chunks form a ring of
+  ``mask + 1`` slots in coherent host memory.  Ticket ``t`` owns slot
+  ``t & mask`` once the host has drained that slot's previous occupant
+  (the slot's generation word reads ``t >> shift``; the wave polls it with
+  system-scope loads, ``s_sleep`` between polls, and after ``SPIN_LIMIT``
+  polls gives up and stops recording rather than hang).  A wave leaving a
+  full chunk writes a close marker into the chunk's last unit after its
+  records have drained (``s_waitcnt vmcnt(0)``); the host's drain thread
+  copies closed chunks out during the kernel and frees their slots, so no
+  buffer bounds the trace of one kernel (reference: the NVBit channel,
+  util/tracer_nvbit/nvbit_release/core/utils/channel.hpp:56-116,161-253,
+  whose device side waits for the host to flush a full buffer).  Every probe
+  store is system scope (``sc0 sc1``: written through the XCD L2);
+* device-buffer mode (``mask == 0``): tickets index one device buffer of
+  ``n_chunks`` chunks; a ticket past its end stops the wave's recording.
 
 Probes use only registers above the kernel's own allocation (16 SGPRs, 8
 VGPRs; the descriptor's counts are raised), save and restore SCC and EXEC,
@@ -45,6 +60,9 @@ from typing import Dict, List, Optional, Sequence, Tuple
 CHUNK_UNITS = 512           # 16-byte units per chunk (8 KB; recorded in the map header)
 TAG_MEM = 0x80000000
 TAG_CHUNK = 0xC0000000
+TAG_CLOSE = 0xE0000000      # last unit of a chunk a wave has left (streaming)
+SPIN_LIMIT = 1 << 18        # generation polls before a wave stops recording
+ST = "sc0 sc1"              # probe stores: system scope (the host reads them)
 N_PROBE_SGPR = 16
 N_PROBE_VGPR = 8
 MAX_SGPR = 102
@@ -278,7 +296,7 @@ class Probe:
         if unit_off:
             out.append(f"s_add_u32 {self.t}, {self.t}, {unit_off * 16}")
         out += [f"v_mov_b32_e32 {self.off}, {self.t}",
-                f"global_store_dwordx4 {self.off}, {self.hdr}, {self.buf}",
+                f"global_store_dwordx4 {self.off}, {self.hdr}, {self.buf} {ST}",
                 f"s_mov_b64 exec, {self.tx}"]
         return out
 
@@ -315,8 +333,32 @@ class Probe:
         return out
 
     def alloc_stub(self, n: int) -> List[str]:
+        """claim the next chunk (a ticket); streaming mode closes the chunk
+        being left and waits for the ticket's ring slot (module docstring)."""
         h = self.h
-        out = [f"s_mov_b64 {self.tx}, exec",
+        L = f".Lasim{self.tag}"
+        out = [f"s_bitcmp1_b32 {self.seq}, 29",          # gave up on the ring
+               f"s_cbranch_scc1 {L}_full_{n}",
+               f"s_load_dword {self.t2}, {self.ctl}, 0x10",  # ring mask (0: device buffer)
+               "s_waitcnt lgkmcnt(0)",
+               f"s_cmp_eq_u32 {self.t2}, 0",
+               f"s_cbranch_scc1 {L}_take_{n}",
+               f"s_cmp_eq_u32 {self.end}, 0",
+               f"s_cbranch_scc1 {L}_take_{n}",
+               # close the chunk being left: its records first, then the marker
+               "s_waitcnt vmcnt(0)",
+               f"s_mov_b64 {self.tx}, exec",
+               "s_mov_b64 exec, 1",
+               f"v_mov_b32_e32 {h[0]}, {TAG_CLOSE:#x}",
+               f"v_mov_b32_e32 {h[1]}, 0",
+               f"v_mov_b32_e32 {h[2]}, 0",
+               f"v_mov_b32_e32 {h[3]}, 0",
+               f"s_lshl_b32 {self.t}, {self.end}, 4",
+               f"v_mov_b32_e32 {self.off}, {self.t}",
+               f"global_store_dwordx4 {self.off}, {self.hdr}, {self.buf} {ST}",
+               f"s_mov_b64 exec, {self.tx}",
+               f"{L}_take_{n}:",
+               f"s_mov_b64 {self.tx}, exec",
                "s_mov_b64 exec, 1",
                f"v_mov_b32_e32 {h[0]}, 1",
                f"v_mov_b32_e32 {self.off}, 8",
@@ -325,39 +367,98 @@ class Probe:
                f"v_readfirstlane_b32 {self.t}, {h[1]}",
                f"s_mov_b64 exec, {self.tx}",
                "s_nop 4",
+               f"s_cmp_eq_u32 {self.t2}, 0",
+               f"s_cbranch_scc1 {L}_dev_{n}",
+               # ring: slot = ticket & mask, generation = ticket >> shift
+               f"s_and_b32 {self.end}, {self.t}, {self.t2}",
+               f"s_load_dword {self.t2}, {self.ctl}, 0x14",
+               "s_waitcnt lgkmcnt(0)",
+               f"s_lshr_b32 {self.t2}, {self.t}, {self.t2}",
+               f"s_mul_i32 {self.cur}, {self.end}, {CHUNK_UNITS}",
+               f"s_mov_b32 {self.end}, {SPIN_LIMIT}",
+               f"s_mov_b64 {self.tx}, exec",
+               "s_mov_b64 exec, 1",
+               f"{L}_spin_{n}:",
+               f"s_lshl_b32 {self.t}, {self.cur}, 4",
+               f"s_add_u32 {self.t}, {self.t}, 28",           # unit 1, word 3
+               f"v_mov_b32_e32 {self.off}, {self.t}",
+               f"global_load_dword {h[1]}, {self.off}, {self.buf} sc0 sc1",
+               "s_waitcnt vmcnt(0)",
+               f"v_readfirstlane_b32 {self.t}, {h[1]}",
+               f"s_cmp_eq_u32 {self.t}, {self.t2}",
+               f"s_cbranch_scc1 {L}_got_{n}",
+               f"s_sub_u32 {self.end}, {self.end}, 1",
+               f"s_cmp_eq_u32 {self.end}, 0",
+               f"s_cbranch_scc1 {L}_drop_{n}",
+               "s_sleep 2",
+               f"s_branch {L}_spin_{n}",
+               f"{L}_drop_{n}:",
+               f"s_mov_b64 exec, {self.tx}",
+               f"s_bitset1_b32 {self.seq}, 29",
+               f"s_branch {L}_full_{n}",
+               f"{L}_got_{n}:",
+               f"s_mov_b64 exec, {self.tx}",
+               f"s_add_u32 {self.end}, {self.cur}, {CHUNK_UNITS - 1}",   # last unit: close marker
+               f"s_branch {L}_hdr_{n}",
+               f"{L}_dev_{n}:",
                f"s_load_dword {self.t2}, {self.ctl}, 0xc",
                "s_waitcnt lgkmcnt(0)",
                f"s_cmp_ge_u32 {self.t}, {self.t2}",
-               f"s_cbranch_scc1 .Lasim{self.tag}_full_{n}",
+               f"s_cbranch_scc1 {L}_full_{n}",
                f"s_mul_i32 {self.cur}, {self.t}, {CHUNK_UNITS}",
                f"s_add_u32 {self.end}, {self.cur}, {CHUNK_UNITS}",
-               f"s_or_b32 {self.t2}, {self.seq}, {TAG_CHUNK:#x}"]
-        # header unit 0: {TAG_CHUNK|seq, wg x, wg y, wg z}; unit 1: {ptid, 0, 0, 0}
+               f"{L}_hdr_{n}:"]
+        # header unit 1: {ptid, 0, 0, generation (ring) | n_chunks}; unit 0:
+        # {TAG_CHUNK|seq, wg x, wg y, wg z}, written last
         out += [f"s_mov_b64 {self.tx}, exec",
                 "s_mov_b64 exec, 1",
+                f"v_mov_b32_e32 {h[0]}, {self.ptid}",
+                f"v_mov_b32_e32 {h[1]}, 0",
+                f"v_mov_b32_e32 {h[2]}, 0",
+                f"v_mov_b32_e32 {h[3]}, {self.t2}",
+                f"s_lshl_b32 {self.t}, {self.cur}, 4",
+                f"s_add_u32 {self.t}, {self.t}, 16",
+                f"v_mov_b32_e32 {self.off}, {self.t}",
+                f"global_store_dwordx4 {self.off}, {self.hdr}, {self.buf} {ST}",
+                f"s_or_b32 {self.t2}, {self.seq}, {TAG_CHUNK:#x}",
                 f"v_mov_b32_e32 {h[0]}, {self.t2}",
                 f"v_mov_b32_e32 {h[1]}, {self.wg[0]}",
                 f"v_mov_b32_e32 {h[2]}, {self.wg[1]}",
                 f"v_mov_b32_e32 {h[3]}, {self.wg[2]}",
-                f"s_lshl_b32 {self.t}, {self.cur}, 4",
+                f"s_sub_u32 {self.t}, {self.t}, 16",
                 f"v_mov_b32_e32 {self.off}, {self.t}",
-                f"global_store_dwordx4 {self.off}, {self.hdr}, {self.buf}",
-                f"v_mov_b32_e32 {h[0]}, {self.ptid}",
-                f"v_mov_b32_e32 {h[1]}, 0",
-                f"v_mov_b32_e32 {h[2]}, 0",
-                f"v_mov_b32_e32 {h[3]}, 0",
-                f"s_add_u32 {self.t}, {self.t}, 16",
-                f"v_mov_b32_e32 {self.off}, {self.t}",
-                f"global_store_dwordx4 {self.off}, {self.hdr}, {self.buf}",
+                f"global_store_dwordx4 {self.off}, {self.hdr}, {self.buf} {ST}",
                 f"s_mov_b64 exec, {self.tx}",
                 f"s_add_u32 {self.seq}, {self.seq}, 1",
                 f"s_add_u32 {self.cur}, {self.cur}, 2",
-                f"s_branch .Lasim{self.tag}_ret_{n}",
-                f".Lasim{self.tag}_full_{n}:",
+                f"s_branch {L}_ret_{n}",
+                f"{L}_full_{n}:",
                 f"s_mov_b32 {self.cur}, 0",
                 f"s_mov_b32 {self.end}, 0",
-                f"s_branch .Lasim{self.tag}_skip_{n}"]
+                f"s_branch {L}_skip_{n}"]
         return out
+
+    def close_at_end(self, n: int) -> List[str]:
+        """before s_endpgm (streaming): close the wave's last chunk so its
+        slot can be drained while the kernel still runs"""
+        h = self.h
+        L = f".Lasim{self.tag}"
+        return [f"s_load_dword {self.t2}, {self.ctl}, 0x10",
+                "s_waitcnt lgkmcnt(0)",
+                f"s_cmp_eq_u32 {self.t2}, 0",
+                f"s_cbranch_scc1 {L}_endc_{n}",
+                f"s_cmp_eq_u32 {self.end}, 0",
+                f"s_cbranch_scc1 {L}_endc_{n}",
+                "s_waitcnt vmcnt(0)",
+                "s_mov_b64 exec, 1",
+                f"v_mov_b32_e32 {h[0]}, {TAG_CLOSE:#x}",
+                f"v_mov_b32_e32 {h[1]}, 0",
+                f"v_mov_b32_e32 {h[2]}, 0",
+                f"v_mov_b32_e32 {h[3]}, 0",
+                f"s_lshl_b32 {self.t}, {self.end}, 4",
+                f"v_mov_b32_e32 {self.off}, {self.t}",
+                f"global_store_dwordx4 {self.off}, {self.hdr}, {self.buf} {ST}",
+                f"{L}_endc_{n}:"]
 
     def segment(self, n: int, seg_id: int, stubs: List[str]) -> List[str]:
         body = self._store_unit(str(seg_id)) + [f"s_add_u32 {self.cur}, {self.cur}, 1"]
@@ -476,7 +577,7 @@ class Probe:
                  f"s_lshl_b32 {self.t}, {self.cur}, 4",
                  f"s_add_u32 {self.t}, {self.t}, 16",
                  f"v_add_u32_e32 {self.off}, {self.t}, {self.off}",
-                 f"global_store_dwordx2 {self.off}, {self.va}, {self.buf}"]
+                 f"global_store_dwordx2 {self.off}, {self.va}, {self.buf} {ST}"]
         body += self._store_unit(f"{TAG_MEM | ins.mem_id:#x}")
         body += [f"s_add_u32 {self.cur}, {self.cur}, 33"]
         return self.guarded(n, 33, body, stubs)
@@ -580,6 +681,9 @@ def instrument(asm: str) -> Tuple[str, List[KernelMap]]:
                     n += 1
                 if ins.mem_id >= 0:
                     out += ["\t" + x if not x.endswith(":") else x for x in pr.memory(n, ins, stubs)]
+                    n += 1
+                if ins.mnem == "s_endpgm":
+                    out += ["\t" + x if not x.endswith(":") else x for x in pr.close_at_end(n)]
                     n += 1
             out.append(ln)
         out += ["\t" + x if not x.endswith(":") else x for x in stubs]

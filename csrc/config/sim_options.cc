@@ -289,6 +289,9 @@ const OptDef kOptions[] = {
     {"-xgmi_link_latency_ns", 'f', "1000.0", "collective step latency (ns)"},
     {"-xgmi_links_per_gpu", 'u', "7", "xGMI links per GPU"},
     {"-sim_event_skip", 'b', "1", "fast-forward quiet SM cycles inside an epoch (results identical)"},
+    {"-gpu_trace_window", 'i', "4",
+     "GPU engine: kernel trace resident in HBM per kernel, in multiples of its resident-CTA capacity; CTAs "
+     "stream in as they dispatch (0 = whole kernel; results identical)"},
     {"-sim_xcd", 'u', "0",
      "XCDs with private L2s (0 = one shared L2): SM s belongs to XCD s % N and uses the n_subpart/N slices of its XCD"},
     {"-sim_mall", 's', "none",
@@ -884,6 +887,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.perfect_mem = r.getb("-gpgpu_perfect_mem") ? 1u : 0u;
   c.simple_dram = r.getb("-gpgpu_simple_dram_model") ? 1u : 0u;
   c.event_skip = r.getb("-sim_event_skip") ? 1u : 0u;
+  c.trace_window = (uint32_t)std::max<long long>(0, r.geti("-gpu_trace_window"));
   {
     // CDNA4 memory hierarchy
     c.l1_wr_req_bytes = (uint32_t)r.getu("-sim_l1_write_request_bytes");

@@ -45,6 +45,9 @@ class CheckEngine final : public Engine {
     b_->launch(slot, k, kd);
   }
   uint32_t running() const override { return a_->running(); }
+  void trace_residency(uint64_t* peak_bytes, uint64_t* refills) const override {
+    b_->trace_residency(peak_bytes, refills);
+  }
   RunResult run(const RunLimits& lim) override {
     RunResult total;
     for (;;) {

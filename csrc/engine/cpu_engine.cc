@@ -176,6 +176,8 @@ class CpuEngine : public Engine {
     d.insts = k.insts.data();
     d.accs = k.accs.data();
     d.streams = k.streams.data();
+    d.imask = d.amask = d.cmask = ~0u;  // the whole trace is resident
+    d.cta_avail = d.n_cta;
     kt_.active |= 1u << slot;
   }
   uint32_t running() const override { return kt_.active; }

@@ -69,6 +69,13 @@ class Engine {
   // debug trace streams: events recorded since the last drain (per unit, in
   // program order); `dropped` counts events lost to full per-unit buffers
   virtual void trace_drain(std::vector<TraceEv>& out, uint64_t* dropped) = 0;
+  // kernel-trace residency: peak bytes of trace held by the engine's compute
+  // device at once, and how often a window was refilled (GPU engine streaming;
+  // host engines report 0)
+  virtual void trace_residency(uint64_t* peak_bytes, uint64_t* refills) const {
+    *peak_bytes = 0;
+    *refills = 0;
+  }
 };
 
 // layout of save_state(): header, then SMState[n_sm], ChanState[n_mem],

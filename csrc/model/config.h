@@ -244,7 +244,10 @@ struct SimCfg {
   // run caps checked every epoch (-gpgpu_max_insn, -gpgpu_max_completed_cta)
   uint64_t max_insn;
   uint32_t max_completed_cta;
-  uint32_t pad_caps;
+  // -gpu_trace_window W (GPU engine): keep only a window of about W x the
+  // resident-CTA capacity of a kernel's trace in HBM, streamed in as CTAs
+  // dispatch (0 = the whole kernel); the host engines ignore it
+  uint32_t trace_window;
   uint32_t max_cycle_lo, max_cycle_hi;
   // ---- idealisations (reference -gpgpu_perfect_mem, perfect_memory_interface
   //      shader.h:2681; -gpgpu_simple_dram_model, l2cache.cc:235-303) ----

@@ -40,6 +40,7 @@ struct EpochPub {
   UnitPub sm[2][kMaxSmTot];
   UnitPub ch[2][kMaxChTot];
   uint32_t next_cta[2][kMaxConc];  // replicated dispatch cursors per kernel slot (published by SM 0)
+  uint32_t next_ctax[2][kMaxConc][kMaxXcd];  // -sim_xcd: the per-XCD cursors behind next_cta
 };
 
 // upper bound of one SM's quiet-cycle look-ahead at an epoch boundary
@@ -51,6 +52,7 @@ struct EpochDecision {
   uint32_t all_idle;    // SMs and memory idle
   uint32_t deadlock;
   uint32_t limit;       // -gpgpu_max_insn / _max_completed_cta / _max_cta reached: stop
+  uint32_t refill;      // the next epoch's dispatch could need a CTA whose trace is not resident
   uint64_t next_start;  // start cycle of the next epoch (after fast-forward)
 };
 
@@ -132,6 +134,22 @@ SIM_HDI void cta_dispatch_xcd(SMState& s, const SmCtx& x, uint32_t ks, const Uni
     total += s.next_ctax[ks][xi];
   }
   s.next_cta[ks] = total;
+}
+
+// Highest CTA id the next epoch's dispatch can hand out (an upper bound: every
+// SM takes at most cta_per_sm CTAs per epoch; with -sim_xcd CTA xi + nx * j
+// comes from XCD xi's cursor j).  The GPU engine keeps the traces of CTAs up
+// to this bound resident (-gpu_trace_window); host and device use this one
+// formula.
+SIM_HDI uint64_t dispatch_bound(const SimCfg& c, const KernelDesc& k, uint32_t next, const uint32_t* nextx) {
+  const uint64_t cpc = amin<uint32_t>(k.cta_per_sm, kMaxCta);
+  if (c.n_xcd > 1) {
+    const uint64_t nx = c.n_xcd;
+    uint32_t mb = 0;
+    for (uint32_t xi = 0; xi < c.n_xcd; ++xi) mb = amax<uint32_t>(mb, nextx[xi]);
+    return (nx - 1) + nx * ((uint64_t)mb + (c.n_sm + nx - 1) / nx * cpc);
+  }
+  return (uint64_t)next + (uint64_t)c.n_sm * cpc;
 }
 
 // kernel slots in launch (uid) order: older kernels are served first
@@ -325,7 +343,10 @@ SIM_HDI void sm_publish(SMState& s, const SmCtx& x, EpochPub& pub, uint32_t cur)
   P::one([&] {
     pub.sm[cur][s.id] = u;
     if (s.id == 0)
-      for (int k = 0; k < kMaxConc; ++k) pub.next_cta[cur][k] = s.next_cta[k];
+      for (int k = 0; k < kMaxConc; ++k) {
+        pub.next_cta[cur][k] = s.next_cta[k];
+        for (int xi = 0; xi < kMaxXcd; ++xi) pub.next_ctax[cur][k][xi] = s.next_ctax[k][xi];
+      }
   });
 }
 
@@ -399,7 +420,7 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   prog = P::uni(P::red_max64(prog));
   // per kernel slot: fully dispatched, launch latency, completion
   const uint32_t active = kt.active;
-  uint32_t undisp = 0, cut = 0;
+  uint32_t undisp = 0, cut = 0, refill = 0;
   uint64_t ready_min = ~0ull, ready_req = ~0ull, ready_max = 0;
   for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k) {
     if (!(active >> k & 1u)) continue;
@@ -407,6 +428,8 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
     ready_max = amax<uint64_t>(ready_max, kd.ready_cycle);
     if (pub.next_cta[cur][k] < kd.n_cta) {
       undisp |= 1u << k;
+      if (kd.cta_avail < kd.n_cta && dispatch_bound(c, kd, pub.next_cta[cur][k], pub.next_ctax[cur][k]) >= kd.cta_avail)
+        refill = 1;
       ready_min = amin<uint64_t>(ready_min, kd.ready_cycle);
       if (reqs >> k & 1u) ready_req = amin<uint64_t>(ready_req, amax<uint64_t>(t1, kd.ready_cycle));
     } else if (kd.stop_when_issued) {
@@ -425,6 +448,7 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   // run caps checked while kernels run (reference gpgpu_sim::active,
   // gpu-sim.cc:1071-1094): instructions, completed CTAs, issued CTAs
   d.limit = 0;
+  d.refill = refill;
   if (c.max_insn && P::uni(P::red_sum64(insn)) >= c.max_insn) d.limit = 1;
   if (c.max_completed_cta && P::uni(P::red_sum(ctas)) >= c.max_completed_cta) d.limit = 1;
   if (cut) d.limit = 1;

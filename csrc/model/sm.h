@@ -1127,8 +1127,9 @@ SIM_HDI void sm_dispatch(S& s, const SmCtx& x, uint64_t now) {
       s.ldst.warp = (uint8_t)(info & 0xffu);
       if (li.space != S_SHARED && li.width && li.mem != kNoMem) {
         // the warp's kernel's access table (slot in the top bits of its stream index)
-        const TAcc* accs = x_kt->k[P::uni((uint32_t)s.w_end[info & 0xffu]) >> kSlotShift].accs;
-        P::fetch_copy(&s.ldst_acc[0], &accs[li.mem], (int)amin<uint32_t>(li.width, kMaxAccess));
+        const KernelDesc& kacc = x_kt->k[P::uni((uint32_t)s.w_end[info & 0xffu]) >> kSlotShift];
+        const TAcc* accs = kacc.accs;
+        P::fetch_copy(&s.ldst_acc[0], &accs[li.mem & kacc.amask], (int)amin<uint32_t>(li.width, kMaxAccess));
       }
       s.ldst.slot = (uint8_t)((info >> 24) & 0xffu);  // load slot allocated at issue
       s.ldst.next = 0;
@@ -1680,11 +1681,11 @@ SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id,
   const uint32_t tag = ks << kSlotShift;
   P::each((int)wpc, [&](int i) {
     uint32_t w = base + (uint32_t)i;
-    WStream ws = k.streams[(uint64_t)cta_id * wpc + (uint32_t)i];
+    WStream ws = k.streams[(uint64_t)(cta_id & k.cmask) * wpc + (uint32_t)i];
     s.w_next[w] = tag | ws.begin;
     s.w_head[w] = tag | ws.begin;
     s.w_end[w] = tag | (ws.begin + ws.count);
-    if (ws.count) s.w_win[w][ws.begin & (kWin - 1)] = k.insts[ws.begin];  // the first fetch's target
+    if (ws.count) s.w_win[w][ws.begin & (kWin - 1)] = k.insts[ws.begin & k.imask];  // the first fetch's target
     s.w_issue_ok[w] = 0;
     s.w_age[w] = age0 + (uint32_t)i;
     s.w_flags[w] = WF_ACTIVE;

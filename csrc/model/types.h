@@ -158,6 +158,11 @@ struct KernelDesc {
   // warp-padded threads, registers, and the shared-memory capacity of the
   // carve-out chosen for this kernel
   uint32_t thr_cta, regs_cta, shmem_cap, pad_k;
+  // trace residency (GPU engine, -gpu_trace_window): instruction, access and
+  // CTA-stream indices are taken modulo ring capacities (masks: all ones when
+  // the whole kernel is resident) and CTAs >= cta_avail are not uploaded yet
+  // (epoch_decide ends the launch before a dispatch could need one)
+  uint32_t imask, amask, cmask, cta_avail;
   uint64_t ready_cycle;        // launch + kernel/CTA launch latency: first CTA dispatch
   uint64_t shmem_base;
   uint64_t local_base;
@@ -182,6 +187,9 @@ struct KernelTab {
   uint32_t mix;     // -gpgpu_concurrent_kernel_sm: one SM may hold CTAs of several kernels
   uint64_t pad[3];
 };
-SIM_HDI const TInst& inst_at(const KernelTab& kt, uint32_t gi) { return kt.k[gi >> kSlotShift].insts[gi & kIdxMask]; }
+SIM_HDI const TInst& inst_at(const KernelTab& kt, uint32_t gi) {
+  const KernelDesc& k = kt.k[gi >> kSlotShift];
+  return k.insts[gi & kIdxMask & k.imask];
+}
 
 }  // namespace asim

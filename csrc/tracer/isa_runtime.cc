@@ -9,7 +9,15 @@
 // MemcpyHtoD lines (:369-378).
 //
 // Here the instrumented code object (isatrace/rewrite.py) appends per-wave
-// record streams to 64 KB chunks of one device buffer.  This runtime
+// record streams to 8 KB chunks.  By default the chunks form a ring in
+// coherent host memory that a drain thread empties while the kernel runs
+// (closed chunks are spilled to a file next to the trace and their slots
+// handed back), so the trace of one kernel is bounded by disk, not by a
+// buffer -- the reference's device channel + receiver thread
+// (util/tracer_nvbit/nvbit_release/core/utils/channel.hpp:56-116,161-253).
+// ASIM_TRACE_BUF_MB selects the older one-device-buffer mode instead (faster
+// for small kernels; a kernel that outgrows it is reported and skipped).
+// This runtime
 //  * interposes __hipRegisterFatBinary / __hipRegisterFunction to register
 //    the probes' control block (device global __asim_tctl) and learn kernel
 //    names, and hipLaunchKernel to arm the buffer, launch, wait and decode;
@@ -19,14 +27,19 @@
 //  * writes kernel-N.traceg (format v4, wavefront size 64, binary version
 //    950), kernelslist.g (+ MemcpyHtoD lines from hipMemcpy) and stats.csv.
 // Environment: ASIM_TRACE_DIR (enables tracing), ASIM_TRACE_KERNEL_START/END
-// (1-based launch range), ASIM_TRACE_BUF_MB (device buffer, default 4096),
-// ASIM_ISA_MAP (map path, default <exe>.asimisa).
+// (1-based launch range), ASIM_TRACE_RING_MB (host ring, default 256, rounded
+// down to a power-of-two number of chunks), ASIM_TRACE_BUF_MB (device-buffer
+// mode instead of the ring), ASIM_ISA_MAP (map path, default <exe>.asimisa).
 #include <filesystem>
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -36,21 +49,24 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <unordered_map>
 #include <vector>
 
 namespace {
 
-constexpr uint32_t kTagMem = 0x80000000u, kTagChunk = 0xC0000000u;
+constexpr uint32_t kTagMem = 0x80000000u, kTagChunk = 0xC0000000u, kTagClose = 0xE0000000u;
 // 16-byte units per chunk: from the map header (isatrace/rewrite.py CHUNK_UNITS)
 uint32_t kChunkUnits = 512;
 
-struct Ctl {  // must match the probes (isatrace/rewrite.py): buf @0, next_chunk @8, n_chunks @12
-  uint64_t buf;
-  uint32_t next_chunk;
-  uint32_t n_chunks;
-  uint64_t pad[2];
+struct Ctl {  // must match the probes (isatrace/rewrite.py)
+  uint64_t buf;         // @0  ring (device view of the host ring) or device buffer
+  uint32_t next_chunk;  // @8  tickets handed out
+  uint32_t n_chunks;    // @12 device-buffer mode: chunks in the buffer
+  uint32_t mask;        // @16 ring mode: slots - 1 (0 = device-buffer mode)
+  uint32_t shift;       // @20 ring mode: log2(slots)
+  uint64_t pad;
 };
 static_assert(sizeof(Ctl) == 32, "control block layout");
 
@@ -80,7 +96,14 @@ struct Tracer {
   std::string dir;
   long kstart = 1, kend = 1L << 40;
   long next_id = 0;
-  size_t buf_bytes = 4096ull << 20;
+  size_t buf_bytes = 0;           // device-buffer mode when set
+  size_t ring_bytes = 256ull << 20;
+  struct Ring {
+    uint8_t* host = nullptr;  // coherent host memory
+    uint8_t* dev = nullptr;   // the same memory as the GPU addresses it
+    uint32_t slots = 0, shift = 0;
+  };
+  std::unordered_map<int, Ring> rings;  // one ring per device
   struct DevBuf {
     uint8_t* ptr = nullptr;
     uint32_t last_used = 0;  // chunks written by the previous traced launch (re-zeroed)
@@ -114,6 +137,7 @@ struct Tracer {
     if (const char* s = getenv("ASIM_TRACE_KERNEL_START")) kstart = atol(s);
     if (const char* s = getenv("ASIM_TRACE_KERNEL_END")) kend = atol(s);
     if (const char* s = getenv("ASIM_TRACE_BUF_MB")) buf_bytes = (size_t)atol(s) << 20;
+    if (const char* s = getenv("ASIM_TRACE_RING_MB")) ring_bytes = (size_t)atol(s) << 20;
     std::string mp;
     if (const char* s = getenv("ASIM_ISA_MAP")) {
       mp = s;
@@ -202,12 +226,12 @@ struct Wave {
 };
 
 void write_kernel(Tracer& t, long id, const std::string& name, const KMap& km, dim3 g, dim3 b, size_t shmem,
-                  const std::vector<uint8_t>& host, uint32_t used) {
+                  const uint8_t* host, uint32_t used) {
   // group chunks by wave: (wg z, wg y, wg x, packed tid of the first lane)
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, Wave> waves;
   const size_t cb = (size_t)kChunkUnits * 16;
   for (uint32_t c = 0; c < used; ++c) {
-    const uint32_t* u = reinterpret_cast<const uint32_t*>(host.data() + c * cb);
+    const uint32_t* u = reinterpret_cast<const uint32_t*>(host + c * cb);
     if ((u[0] & kTagChunk) != kTagChunk) continue;
     waves[std::make_tuple(u[3], u[2], u[1], u[4])].chunks.push_back({u[0] & ~kTagChunk, c});
   }
@@ -248,7 +272,7 @@ void write_kernel(Tracer& t, long id, const std::string& name, const KMap& km, d
       // flatten the wave's records
       std::vector<const uint32_t*> recs;
       for (auto& ch : w.second->chunks) {
-        const uint32_t* base = reinterpret_cast<const uint32_t*>(host.data() + ch.second * cb);
+        const uint32_t* base = reinterpret_cast<const uint32_t*>(host + ch.second * cb);
         uint32_t u = 2;
         while (u < kChunkUnits) {
           const uint32_t* r = base + u * 4;
@@ -316,6 +340,140 @@ void write_kernel(Tracer& t, long id, const std::string& name, const KMap& km, d
   snprintf(s, sizeof(s), "kernel-%ld, %s, (%u,%u,%u), (%u,%u,%u), %llu, %llu", id, name.c_str(), g.x, g.y, g.z, b.x,
            b.y, b.z, (unsigned long long)winsts, (unsigned long long)tinsts);
   t.append("stats.csv", s);
+}
+
+// ---- streaming ring (isatrace/rewrite.py module docstring: the protocol)
+struct Spill {
+  FILE* f = nullptr;
+  uint32_t chunks = 0;
+  std::vector<uint8_t> tmp;
+};
+
+// copy one chunk out (the close marker cleared: record parsing stops at a
+// zero unit)
+void spill_chunk(const uint8_t* slot, size_t cb, Spill& sp) {
+  sp.tmp.assign(slot, slot + cb);
+  memset(sp.tmp.data() + cb - 16, 0, 16);
+  if (fwrite(sp.tmp.data(), 1, cb, sp.f) != cb) {
+    fprintf(stderr, "asim isa tracer: spill write failed\n");
+    exit(3);
+  }
+  ++sp.chunks;
+}
+
+// one pass of the drain thread over the ring: every chunk its wave has
+// closed is copied out, zeroed and handed to the slot's next generation
+size_t drain_closed(const Tracer::Ring& r, Spill& sp) {
+  const size_t cb = (size_t)kChunkUnits * 16;
+  size_t n = 0;
+  for (uint32_t s = 0; s < r.slots; ++s) {
+    uint8_t* p = r.host + (size_t)s * cb;
+    if (*reinterpret_cast<volatile const uint32_t*>(p + cb - 16) != kTagClose) continue;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    volatile uint32_t* gen = reinterpret_cast<volatile uint32_t*>(p + 28);  // unit 1, word 3
+    const uint32_t g = *gen;
+    spill_chunk(p, cb, sp);
+    memset(p, 0, 28);
+    memset(p + 32, 0, cb - 32);
+    std::atomic_thread_fence(std::memory_order_release);
+    *gen = g + 1;
+    ++n;
+  }
+  return n;
+}
+
+// after the kernel: every chunk still holding records (closed or not), then
+// all touched slots back to generation 0 for the next launch
+void drain_final(const Tracer::Ring& r, uint32_t tickets, Spill& sp) {
+  const size_t cb = (size_t)kChunkUnits * 16;
+  const uint32_t touched = tickets >= r.slots ? r.slots : tickets;
+  for (uint32_t s = 0; s < touched; ++s) {
+    uint8_t* p = r.host + (size_t)s * cb;
+    if ((reinterpret_cast<const uint32_t*>(p)[0] & kTagChunk) == kTagChunk) spill_chunk(p, cb, sp);
+    memset(p, 0, cb);
+  }
+}
+
+Tracer::Ring& ring_for(Tracer& t, int dev) {
+  Tracer::Ring& r = t.rings[dev];
+  if (r.host) return r;
+  const size_t cb = (size_t)kChunkUnits * 16;
+  r.slots = 64;
+  while ((size_t)r.slots * 2 * cb <= t.ring_bytes) r.slots *= 2;
+  r.shift = (uint32_t)__builtin_ctz(r.slots);
+  RT_HIP(hipHostMalloc((void**)&r.host, (size_t)r.slots * cb, hipHostMallocCoherent | hipHostMallocMapped));
+  memset(r.host, 0, (size_t)r.slots * cb);
+  RT_HIP(hipHostGetDevicePointer((void**)&r.dev, r.host, 0));
+  return r;
+}
+
+uint32_t tickets_issued(Tracer& t) {
+  uint32_t used = 0;
+  for (Ctl* sh : t.shadows) {
+    Ctl r{};
+    RT_HIP(hipMemcpyFromSymbol(&r, (const void*)sh, sizeof(r), 0, hipMemcpyDeviceToHost));
+    used = std::max(used, r.next_chunk);
+  }
+  return used;
+}
+
+// the ring path of a traced launch: drain during the kernel, spill, decode
+hipError_t launch_streamed(Tracer& t, long id, const std::string& name, const KMap& km,
+                           hipError_t (*real)(const void*, dim3, dim3, void**, size_t, hipStream_t), const void* f,
+                           dim3 g, dim3 b, void** args, size_t shmem, hipStream_t st, int dev) {
+  Tracer::Ring& r = ring_for(t, dev);
+  Ctl c{};
+  c.buf = (uint64_t)(uintptr_t)r.dev;
+  c.n_chunks = r.slots;
+  c.mask = r.slots - 1;
+  c.shift = r.shift;
+  for (Ctl* sh : t.shadows) RT_HIP(hipMemcpyToSymbol((const void*)sh, &c, sizeof(c), 0, hipMemcpyHostToDevice));
+  const std::string spath = t.dir + "/.kernel-" + std::to_string(id) + ".chunks";
+  Spill sp;
+  sp.f = fopen(spath.c_str(), "w+b");
+  if (!sp.f) {
+    fprintf(stderr, "asim isa tracer: cannot write %s\n", spath.c_str());
+    exit(3);
+  }
+  hipError_t e = real(f, g, b, args, shmem, st);
+  if (e != hipSuccess) {
+    fclose(sp.f);
+    unlink(spath.c_str());
+    return e;
+  }
+  std::atomic<bool> stop{false};
+  std::thread drain([&] {
+    while (!stop.load(std::memory_order_relaxed))
+      if (!drain_closed(r, sp)) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  });
+  const hipError_t se = hipStreamSynchronize(st);
+  stop = true;
+  drain.join();
+  RT_HIP(se);
+  const uint32_t tickets = tickets_issued(t);
+  drain_final(r, tickets, sp);
+  if (tickets > sp.chunks)
+    fprintf(stderr,
+            "asim isa tracer: kernel %ld (%s): %u of %u chunks dropped (a wave waited too long for a ring slot); "
+            "raise ASIM_TRACE_RING_MB\n",
+            id, name.c_str(), tickets - sp.chunks, tickets);
+  fflush(sp.f);
+  const size_t bytes = (size_t)sp.chunks * kChunkUnits * 16;
+  const uint8_t* data = nullptr;
+  void* m = MAP_FAILED;
+  if (bytes) {
+    m = mmap(nullptr, bytes, PROT_READ, MAP_PRIVATE, fileno(sp.f), 0);
+    if (m == MAP_FAILED) {
+      fprintf(stderr, "asim isa tracer: cannot map %s\n", spath.c_str());
+      exit(3);
+    }
+    data = static_cast<const uint8_t*>(m);
+  }
+  write_kernel(t, id, name, km, g, b, shmem, data, sp.chunks);
+  if (m != MAP_FAILED) munmap(m, bytes);
+  fclose(sp.f);
+  unlink(spath.c_str());
+  return e;
 }
 
 }  // namespace
@@ -387,6 +545,7 @@ hipError_t hipLaunchKernel(const void* f, dim3 g, dim3 b, void** args, size_t sh
   }
   int dev = 0;
   RT_HIP(hipGetDevice(&dev));
+  if (!t.buf_bytes) return launch_streamed(t, id, name, mit->second, real, f, g, b, args, shmem, st, dev);
   Tracer::DevBuf& db = t.bufs[dev];
   if (!db.ptr) {
     RT_HIP(hipMalloc(&db.ptr, t.buf_bytes));
@@ -401,22 +560,20 @@ hipError_t hipLaunchKernel(const void* f, dim3 g, dim3 b, void** args, size_t sh
   hipError_t e = real(f, g, b, args, shmem, st);
   if (e != hipSuccess) return e;
   RT_HIP(hipStreamSynchronize(st));
-  uint32_t used = 0;
-  for (Ctl* sh : t.shadows) {
-    Ctl r{};
-    RT_HIP(hipMemcpyFromSymbol(&r, (const void*)sh, sizeof(r), 0, hipMemcpyDeviceToHost));
-    used = std::max(used, r.next_chunk);
-  }
+  uint32_t used = tickets_issued(t);
+  db.last_used = std::min(used, c.n_chunks);
   if (used > c.n_chunks) {
-    fprintf(stderr, "asim isa tracer: kernel %s needs %u chunks of %u KB, buffer holds %u; raise ASIM_TRACE_BUF_MB\n",
-            name.c_str(), used, kChunkUnits / 64, c.n_chunks);
-    exit(4);
+    // the waves past the end stopped recording: no usable trace of this kernel
+    fprintf(stderr,
+            "asim isa tracer: kernel %ld (%s) needs %u chunks of %u KB, the device buffer holds %u: not written "
+            "(unset ASIM_TRACE_BUF_MB to stream through the host ring)\n",
+            id, name.c_str(), used, kChunkUnits / 64, c.n_chunks);
+    return e;
   }
-  db.last_used = used;
   std::vector<uint8_t> host((size_t)used * kChunkUnits * 16);
   // the tracer's own read-back is not an application copy (no trace line)
   if (used) RT_HIP(hipMemcpyDtoH(host.data(), db.ptr, host.size()));
-  write_kernel(t, id, name, mit->second, g, b, shmem, host, used);
+  write_kernel(t, id, name, mit->second, g, b, shmem, host.data(), used);
   return e;
 }
 

@@ -265,3 +265,32 @@ def test_power_report_and_dvfs_gpu_equals_cpu(gpu_mod, tmp_path):
                     [l for l in s.output.splitlines() if l.startswith(("gpu_sim_time_ns", "gpu_avg_core_clock"))])
     assert out["gpu"] == out["cpu"]
     assert out["cpu"][1][0]["kernel_avg_clock_ratio"] < 1.0  # the governor did act
+
+
+@pytest.mark.parametrize("extra", [{}, {"-sim_xcd": "8", "-sim_mall": "256:16"}], ids=["shared_l2", "xcd_mall"])
+def test_trace_window_streaming_gpu_equals_cpu(gpu_mod, tmp_path, extra):
+    """-gpu_trace_window: only a window of the kernel's trace (about one
+    resident-CTA capacity here) sits in HBM; CTAs stream in as the dispatch
+    cursor advances.  Cycles and statistics equal the whole-kernel upload and
+    the CPU engine, and the resident trace is a fraction of the kernel's."""
+    import numpy as np
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+    k = KernelBuilder("k_many", (6000, 1, 1), (256, 1, 1), nregs=16)
+    base = k.g.gtid0.astype(np.int64) * 4
+    k.op("LDG.E", [4], [2], base=0x7000_0000 + base, stride=4)
+    k.alu("FFMA", 3, regs=(4, 5, 6))
+    k.op("STG.E", [], [2, 4], base=0x9000_0000 + base, stride=4)
+    k.op("EXIT")
+    kl = rodinia.write_app(str(tmp_path / "many"), [k.build()])
+    win = sim.simulate(kl, "QV100", engine="gpu", extra=dict(extra, **{"-gpu_trace_window": "1"}))
+    whole = sim.simulate(kl, "QV100", engine="gpu", extra=dict(extra, **{"-gpu_trace_window": "0"}))
+    cpu = sim.simulate(kl, "QV100", engine="cpu", extra=extra)
+    assert (win.tot_cycle, win.tot_insn) == (cpu.tot_cycle, cpu.tot_insn) == (whole.tot_cycle, whole.tot_insn)
+    skip = ("rate", "slowdown", "time", "gpu_trace")
+    strip = lambda s: {a: v for a, v in s.items() if not any(x in a for x in skip)}
+    assert strip(win.stats) == strip(cpu.stats)
+    pw, pf = win.stats["gpu_trace_resident_peak_bytes"], whole.stats["gpu_trace_resident_peak_bytes"]
+    assert win.stats["gpu_trace_window_fills"] > 3
+    assert pw * 4 < pf, (pw, pf)

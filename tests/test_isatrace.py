@@ -94,7 +94,8 @@ def test_instrumented_asm_keeps_program_and_reserves_registers():
     # the probes' control block is a protected device global
     assert "__asim_tctl:" in new and ".protected\t__asim_tctl" in new
     # address of the saddr global load: v0 + s[4:5] + 16
-    blk = new[new.index("global_load_dword v1") - 1400:new.index("global_load_dword v1")]
+    at = new.index("global_load_dword v1, v0")
+    blk = new[new.rindex("_ret_", 0, at):at]
     assert "v_add_co_u32_e64 v8, s[14:15], s4, v8" in blk and "s_mov_b32 s17, 0x10" in blk
     # map: segment/instruction lines in trace order (ndst dsts mnemonic nsrc srcs width)
     m = rewrite.write_map(maps)
@@ -149,3 +150,66 @@ def test_isatrace_capture_matches_simulation(tmp_path):
     s = sim.simulate(str(kl), "MI355X", engine="gpu")
     assert s.stats["gpgpu_n_tot_w_icount"] == sum(v for k, v in c.items() if k != "WAVES")
     assert s.tot_insn == 16384 * (sum(v for k, v in c.items() if k != "WAVES") // 256)
+
+
+def _trace_body(path):
+    """kernel-N.traceg without the header lines (the per-CTA / per-wave part),
+    each line's lane addresses as offsets from its first lane's (the two
+    captures run as separate processes, whose allocations may sit at
+    different addresses)"""
+    txt = open(path).read()
+    out = []
+    for ln in txt[txt.index("#BEGIN_TB"):].split("\n"):
+        toks = ln.split()
+        addrs = [int(t, 16) for t in toks if t.startswith("0x")]
+        if addrs:
+            ln = " ".join(t for t in toks if not t.startswith("0x")) + " " + " ".join(str(a - addrs[0]) for a in addrs)
+        out.append(ln)
+    return "\n".join(out)
+
+
+@pytest.mark.gpu
+def test_isatrace_ring_streams_a_trace_larger_than_the_ring(tmp_path):
+    """Streaming capture: vectoradd's 4096 waves need 4096 chunks (32 MB of
+    records) and go through a 1 MB host ring (128 slots) drained while the
+    kernel runs; the trace equals the one captured into a device buffer that
+    holds it whole, nothing is dropped, and it simulates."""
+    exe = os.path.join(ROOT, "bin", "isatrace", "vectoradd")
+    assert os.path.exists(exe), "build_native.py builds bin/isatrace/*"
+    n = 1 << 18
+    ring, whole = tmp_path / "ring", tmp_path / "whole"
+    env = {k: v for k, v in os.environ.items() if not k.startswith("ASIM_TRACE")}
+    r = subprocess.run([exe, str(n)], env=dict(env, ASIM_TRACE_DIR=str(ring), ASIM_TRACE_RING_MB="1"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stderr
+    assert "dropped" not in r.stderr and "out of sequence" not in r.stderr, r.stderr
+    r = subprocess.run([exe, str(n)], env=dict(env, ASIM_TRACE_DIR=str(whole), ASIM_TRACE_BUF_MB="256"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stderr
+    c = verify.trace_counts(str(ring / "kernel-1.traceg"))
+    assert c["WAVES"] == n // 64 and c["VMEM_WR"] == n // 64
+    assert _trace_body(ring / "kernel-1.traceg") == _trace_body(whole / "kernel-1.traceg")
+    # spill files are removed once the kernel's trace is written
+    assert not [p for p in os.listdir(ring) if p.endswith(".chunks")]
+    from accel_sim_framework_distributed_amd import sim
+    s = sim.simulate(str(ring / "kernelslist.g"), "MI355X", engine="gpu")
+    assert s.stats["gpgpu_n_tot_w_icount"] == sum(v for k, v in c.items() if k != "WAVES")
+
+
+@pytest.mark.gpu
+def test_isatrace_ring_with_barriers_matches_device_buffer(tmp_path):
+    """hotspot (workgroup barriers, several kernels) streamed through the
+    default ring gives the same traces as the device-buffer mode."""
+    exe = os.path.join(ROOT, "bin", "isatrace", "hotspot")
+    assert os.path.exists(exe)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("ASIM_TRACE")}
+    outs = []
+    for tag, extra in (("ring", {}), ("buf", {"ASIM_TRACE_BUF_MB": "1024"})):
+        d = tmp_path / tag
+        r = subprocess.run([exe, "128", "2"], env=dict(env, ASIM_TRACE_DIR=str(d), **extra), capture_output=True,
+                           text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert "dropped" not in r.stderr, r.stderr
+        ks = sorted(p for p in os.listdir(d) if p.endswith(".traceg"))
+        outs.append({k: _trace_body(d / k) for k in ks})
+    assert outs[0] and outs[0] == outs[1]

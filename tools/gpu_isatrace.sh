@@ -15,7 +15,8 @@ cd /tmp
 for spec in $APPS; do
   app=${spec%%:*}; args=$(echo ${spec#*:} | tr ',' ' ')
   echo "== $app $args"
-  ASIM_TRACE_DIR=$out/$app ASIM_TRACE_BUF_MB=${ISAT_BUF_MB:-2048} timeout -k 10 120 $R/bin/isatrace/$app $args \
+  # streamed through the host ring unless ISAT_BUF_MB asks for a device buffer
+  env ASIM_TRACE_DIR=$out/$app ${ISAT_BUF_MB:+ASIM_TRACE_BUF_MB=$ISAT_BUF_MB} timeout -k 10 120 $R/bin/isatrace/$app $args \
     > $out/$app.run.log 2>&1 || { echo "$app traced run failed"; tail -5 $out/$app.run.log; exit 1; }
   tail -2 $out/$app.run.log
   timeout -k 10 120 $R/bin/apps/$app $args > $out/$app.plain.log 2>&1 || { echo "$app plain run failed"; exit 1; }
