@@ -14,3 +14,7 @@ timeout -k 10 500 python -u -m pytest tests/test_gpu_engine.py tests/test_cdna_m
   --timeout-method thread > $out/gputest.log 2>&1 || { tail -30 $out/gputest.log; exit 1; }
 tail -3 $out/gputest.log
 bash tools/gpu_correlate.sh
+# the round-3 micro-benchmarks (each under its own limit)
+cd $R
+UBENCH_PROGS="ub_kernel_lat_tb ub_l1_adaptive ub_shared_bw ub_atomic_bw ub_dram_atom ub_mem_lat ub_copy_engine ub_regfile" \
+  bash tools/run_ubench.sh gpurun_out/ubench_r3new

@@ -6,7 +6,7 @@
 set -o pipefail
 out=${1:-gpurun_out/ubench}
 mkdir -p "$out"
-for p in ${UBENCH_PROGS:-ub_config ub_cache_lat ub_cache_policy ub_cache_geom ub_l1_assoc ub_alu ub_lds ub_mfma ub_mfma_shapes ub_bw_widths ub_icache ub_atomic_kernel ub_launch ub_mem_bw ub_l2_release ub_power}; do
+for p in ${UBENCH_PROGS:-ub_config ub_cache_lat ub_cache_policy ub_cache_geom ub_l1_assoc ub_alu ub_lds ub_mfma ub_mfma_shapes ub_bw_widths ub_icache ub_atomic_kernel ub_launch ub_mem_bw ub_l2_release ub_kernel_lat_tb ub_l1_adaptive ub_shared_bw ub_atomic_bw ub_dram_atom ub_mem_lat ub_copy_engine ub_regfile ub_power}; do
   echo "== $p"
   timeout -k 10 240 ./bin/ubench/$p > "$out/$p.log" 2>&1 || { echo "$p failed rc=$?"; tail -5 "$out/$p.log"; exit 1; }
   tail -3 "$out/$p.log"
