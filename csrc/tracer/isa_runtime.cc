@@ -29,7 +29,13 @@
 // Environment: ASIM_TRACE_DIR (enables tracing), ASIM_TRACE_KERNEL_START/END
 // (1-based launch range), ASIM_TRACE_RING_MB (host ring, default 256, rounded
 // down to a power-of-two number of chunks), ASIM_TRACE_BUF_MB (device-buffer
-// mode instead of the ring), ASIM_ISA_MAP (map path, default <exe>.asimisa).
+// mode instead of the ring), ASIM_ISA_MAP (map path, default <exe>.asimisa),
+// ASIM_TRACE_GPU_ID / GPU_TRACE_ID (trace only the launches on that HIP
+// device, files kernel-<id>_<gpu>.traceg: the reference's per-device filter
+// and naming, tracer_tool.cu:115-116,303-316,442-445).  "{rank}" in
+// ASIM_TRACE_DIR becomes the process's rank (RANK, OMPI_COMM_WORLD_RANK,
+// SLURM_PROCID or LOCAL_RANK), so every rank of a multi-process job writes
+// its own trace directory.
 #include <filesystem>
 #include <dlfcn.h>
 #include <fcntl.h>
@@ -95,6 +101,7 @@ struct Tracer {
   bool enabled = false;
   std::string dir;
   long kstart = 1, kend = 1L << 40;
+  int gpu_id = -1;  // -1: every device
   long next_id = 0;
   size_t buf_bytes = 0;           // device-buffer mode when set
   size_t ring_bytes = 256ull << 20;
@@ -119,11 +126,19 @@ struct Tracer {
     if (!d || !*d) return;
     enabled = true;
     dir = d;
+    for (size_t at; (at = dir.find("{rank}")) != std::string::npos;) {
+      const char* r = nullptr;
+      for (const char* v : {"RANK", "OMPI_COMM_WORLD_RANK", "SLURM_PROCID", "LOCAL_RANK"})
+        if ((r = getenv(v)) && *r) break;
+      dir.replace(at, 6, r && *r ? r : "0");
+    }
+    if (const char* s = getenv("ASIM_TRACE_GPU_ID")) gpu_id = atoi(s);
+    else if (const char* s2 = getenv("GPU_TRACE_ID")) gpu_id = atoi(s2);
     std::error_code ec;
     std::filesystem::create_directories(dir, ec);
     FILE* kl = fopen((dir + "/kernelslist.g").c_str(), "w");
     if (!kl) {
-      fprintf(stderr, "asim isa tracer: cannot write %s/kernelslist.g (%s); tracing disabled\n", d,
+      fprintf(stderr, "asim isa tracer: cannot write %s/kernelslist.g (%s); tracing disabled\n", dir.c_str(),
               ec ? ec.message().c_str() : "open failed");
       enabled = false;
       return;
@@ -206,6 +221,15 @@ struct Tracer {
   }
 
   bool traced(long id) const { return enabled && id >= kstart && id <= kend; }
+  // the launch / copy happens on a device this process traces
+  bool on_traced_device() const {
+    if (gpu_id < 0) return true;
+    int dev = 0;
+    return hipGetDevice(&dev) == hipSuccess && dev == gpu_id;
+  }
+  std::string kernel_file(long id) const {
+    return "kernel-" + std::to_string(id) + (gpu_id >= 0 ? "_" + std::to_string(gpu_id) : std::string()) + ".traceg";
+  }
 
   void append(const std::string& file, const std::string& s) {
     FILE* f = fopen((dir + "/" + file).c_str(), "a");
@@ -235,7 +259,7 @@ void write_kernel(Tracer& t, long id, const std::string& name, const KMap& km, d
     if ((u[0] & kTagChunk) != kTagChunk) continue;
     waves[std::make_tuple(u[3], u[2], u[1], u[4])].chunks.push_back({u[0] & ~kTagChunk, c});
   }
-  const std::string fn = "kernel-" + std::to_string(id) + ".traceg";
+  const std::string fn = t.kernel_file(id);
   FILE* f = fopen((t.dir + "/" + fn).c_str(), "w");
   if (!f) {
     fprintf(stderr, "asim isa tracer: cannot write %s\n", fn.c_str());
@@ -515,7 +539,7 @@ hipError_t hipMemcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind kin
   static F real = (F)dlsym(RTLD_NEXT, "hipMemcpy");
   hipError_t e = real(dst, src, bytes, kind);
   Tracer& t = T();
-  if (t.enabled && (kind == hipMemcpyHostToDevice || kind == hipMemcpyDeviceToHost)) {
+  if (t.enabled && (kind == hipMemcpyHostToDevice || kind == hipMemcpyDeviceToHost) && t.on_traced_device()) {
     // DtoH copies carry no simulated work but mark a host synchronisation
     // (the next kernel is launched from an idle queue)
     char s[96];
@@ -533,7 +557,7 @@ hipError_t hipLaunchKernel(const void* f, dim3 g, dim3 b, void** args, size_t sh
   using F = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t);
   static F real = (F)dlsym(RTLD_NEXT, "hipLaunchKernel");
   Tracer& t = T();
-  if (!t.enabled) return real(f, g, b, args, shmem, st);
+  if (!t.enabled || !t.on_traced_device()) return real(f, g, b, args, shmem, st);
   std::lock_guard<std::mutex> lk(t.mu);
   const long id = ++t.next_id;
   auto nit = t.names.find(f);

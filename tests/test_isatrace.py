@@ -213,3 +213,24 @@ def test_isatrace_ring_with_barriers_matches_device_buffer(tmp_path):
         ks = sorted(p for p in os.listdir(d) if p.endswith(".traceg"))
         outs.append({k: _trace_body(d / k) for k in ks})
     assert outs[0] and outs[0] == outs[1]
+
+
+@pytest.mark.gpu
+def test_isatrace_device_filter_and_rank_dirs(tmp_path):
+    """GPU_TRACE_ID-style capture: only the launches on the named device are
+    traced, into kernel-<id>_<gpu>.traceg; '{rank}' in ASIM_TRACE_DIR gives
+    each rank of a job its own directory."""
+    exe = os.path.join(ROOT, "bin", "isatrace", "vectoradd")
+    env = {k: v for k, v in os.environ.items() if not k.startswith("ASIM_TRACE")}
+    env.update(ASIM_TRACE_DIR=str(tmp_path / "r{rank}"), RANK="3", ASIM_TRACE_GPU_ID="0")
+    r = subprocess.run([exe, "4096"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stderr
+    d = tmp_path / "r3"
+    assert (d / "kernel-1_0.traceg").exists() and "kernel-1_0.traceg" in (d / "kernelslist.g").read_text()
+    assert verify.trace_counts(str(d / "kernel-1_0.traceg"))["WAVES"] == 4096 // 64
+    # a device this process never launches on: nothing traced, the app still runs
+    env.update(RANK="4", ASIM_TRACE_GPU_ID="7")
+    r = subprocess.run([exe, "4096"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stderr
+    assert not [p for p in os.listdir(tmp_path / "r4") if p.endswith(".traceg")]
+    assert "kernel-" not in (tmp_path / "r4" / "kernelslist.g").read_text()
