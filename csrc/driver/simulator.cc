@@ -1345,8 +1345,9 @@ void Simulator::print_sim_time() {
   print("gpgpu_silicon_slowdown = %llux\n", cps ? (unsigned long long)(core_khz * 1000.0 / cps) : 0ull);
   uint64_t peak = 0, refills = 0;
   eng_->trace_residency(&peak, &refills);
+  // not "key = value": an engine diagnostic, not a statistic of the model
   if (peak)
-    print("gpu_trace_resident_peak_bytes = %llu\ngpu_trace_window_fills = %llu\n", (unsigned long long)peak,
+    print("gpu_trace_resident_peak_bytes: %llu\ngpu_trace_window_fills: %llu\n", (unsigned long long)peak,
           (unsigned long long)refills);
   fflush(stdout);
 }
