@@ -17,6 +17,10 @@ CPU.  Per epoch:
    all-to-all carries the rest;
 3. ``receive``, sources in rank order, each in emission order.
 
+Steps 1-3 are native (``LinkSim.pack_epoch`` writes the packets straight into
+the pinned send buffer, ``unpack_epoch`` delivers the received slots), so
+the per-epoch host work is two calls around the all-to-all.
+
 The next epoch starts at max(t+E, G), G = the minimum over ranks of the
 previous next events and of this epoch's earliest arrivals: every event a
 rank can have after this epoch is one of its earlier pending sends or is
@@ -60,12 +64,12 @@ class PacketExchange:
         self.stats = dict(epochs=0, packets=0, exchanges=0)
         self._buf: Dict = {}
 
-    def _bufs(self, n_out: int, n_in: int):
+    def _bufs(self, n_out: int, n_in: int, tag: str = ""):
         """Exchange buffers reused across epochs: on a GPU backend a pinned
         host staging pair plus the device pair (one async H2D / D2H copy
         each way, no allocation per epoch); on the CPU the tensors
         themselves."""
-        key = (n_out, n_in)
+        key = (tag, n_out, n_in)
         b = self._buf.get(key)
         if b is None:
             t = self.torch
@@ -96,6 +100,25 @@ class PacketExchange:
         self.torch.cuda.current_stream().synchronize()
         return h_dst.numpy().copy()
 
+    def _a2a_fixed(self, ls, t_end: int, ann_next: int, ann_busy: int, n: int):
+        """The fixed-slot all-to-all of one epoch: LinkSim packs this rank's
+        packets straight into the (pinned) send buffer; returns the received
+        slots (a view, valid until the next exchange) and the overflow."""
+        h_src, src, dst, h_dst = self._bufs(n, n, "fixed")  # never shared with the overflow exchange
+        send = (src if h_src is None else h_src).numpy()
+        extra, extra_words, npk, _ = ls.pack_epoch(t_end, self.K, self.HDR, ann_next, ann_busy, send)
+        if h_src is not None:
+            src.copy_(h_src, non_blocking=True)
+        W = self.world
+        self.dist.all_to_all_single(dst, src, output_split_sizes=[n // W] * W, input_split_sizes=[n // W] * W,
+                                    group=self.group)
+        self.stats["exchanges"] += 1
+        if h_dst is None:
+            return dst.numpy(), extra, extra_words, npk
+        h_dst.copy_(dst, non_blocking=True)
+        self.torch.cuda.current_stream().synchronize()
+        return h_dst.numpy(), extra, extra_words, npk
+
     K = 8       # packet slots per destination in the fixed exchange
     HDR = 8     # header words per destination slot
 
@@ -111,58 +134,30 @@ class PacketExchange:
         # state announced in the next exchange: as of the end of the previous epoch
         ann_next = min(int(ls.next_event()), _I64_MAX)
         ann_busy = 0 if ls.done() else 1
+        none = np.zeros(0, np.int64)
         while True:
             t_end = t + E
-            out = np.frombuffer(ls.emit(t_end), dtype=np.int64).reshape(-1, 4)
-            dst = (out[:, 0] >> 32).astype(np.int64) if len(out) else np.zeros(0, np.int64)
-            order = np.argsort(dst, kind="stable")
-            counts = np.bincount(dst, minlength=W).astype(np.int64)
-            sorted_out = out[order]
-            starts = np.concatenate([[0], np.cumsum(counts)])
-            # earliest arrival among this epoch's packets (arrive_ps: word 3)
-            min_arr = int(out[:, 3].min()) if len(out) else _I64_MAX
-            send = np.zeros((W, slot), np.int64)
-            send[:, 0] = counts
-            send[:, 1] = int(counts.max()) if W else 0
-            send[:, 2] = ann_next
-            send[:, 3] = ann_busy
-            send[:, 4] = min(min_arr, _I64_MAX)
-            for d in range(W):
-                n = min(int(counts[d]), K)
-                if n:
-                    send[d, H:H + 4 * n] = sorted_out[starts[d]:starts[d] + n].reshape(-1)
-            recv = self._a2a(send.reshape(-1), [slot] * W, [slot] * W).reshape(W, slot)
-            in_counts = recv[:, 0]
-            per_src = [recv[s, H:H + 4 * min(int(in_counts[s]), K)] for s in range(W)]
-            if int(recv[:, 1].max()) > K:
+            # emit + pack (native), one fixed all-to-all
+            recv, extra, extra_words, npk = self._a2a_fixed(ls, t_end, ann_next, ann_busy, W * slot)
+            hdr = recv.reshape(W, slot)
+            inc = none
+            if int(hdr[:, 1].max()) > K:
                 # some rank sent more than K packets to one destination: the rest
-                extra_out = [max(0, int(counts[d]) - K) for d in range(W)]
-                extra_in = [max(0, int(in_counts[s]) - K) for s in range(W)]
-                payload = np.concatenate([sorted_out[starts[d] + K:starts[d + 1]].reshape(-1)
-                                          for d in range(W)]) if sum(extra_out) else np.zeros(0, np.int64)
-                inc = self._a2a(payload, [4 * c for c in extra_out], [4 * c for c in extra_in])
-                off = 0
-                for s_ in range(W):
-                    n = 4 * extra_in[s_]
-                    if n:
-                        per_src[s_] = np.concatenate([per_src[s_], inc[off:off + n]])
-                        off += n
-            inc_all = np.concatenate(per_src) if per_src else np.zeros(0, np.int64)
-            if len(inc_all):
-                ls.receive(inc_all.astype(np.int64).tobytes())
-            self.stats["packets"] += len(out)
+                extra_in = [4 * max(0, int(c) - K) for c in hdr[:, 0]]
+                inc = self._a2a(extra, [int(w) for w in extra_words], extra_in)
+            # deliver in source order (native); flags / next events of every rank
+            any_busy, g = ls.unpack_epoch(recv, K, H, inc)
+            self.stats["packets"] += int(npk)
             self.stats["epochs"] += 1
-            any_busy = int(recv[:, 3].max())
             if not any_busy:
                 # every rank was done before this epoch: nothing was sent in it
                 break
-            g = int(min(recv[:, 2].min(), recv[:, 4].min()))
             ann_next = min(int(ls.next_event()), _I64_MAX)
             ann_busy = 0 if ls.done() else 1
             if g >= _I64_MAX:
                 # no pending send anywhere and nothing on the wire, yet a rank is not done
                 raise RuntimeError("packet collective deadlocked (no rank has pending work)")
-            t = max(t_end, g)
+            t = max(t_end, int(g))
         return dict(finish_ps=int(ls.finish_ps), channels=int(ls.channels), packets_sent=int(ls.packets_sent))
 
 

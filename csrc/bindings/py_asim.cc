@@ -1,5 +1,6 @@
 // Python bindings of the native simulator (module: accel_sim_framework_distributed_amd._asim).
 #include <pybind11/functional.h>
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -425,7 +426,28 @@ PYBIND11_MODULE(_asim, m) {
       .def_property_readonly("epoch_ps", &LinkSim::epoch_ps)
       .def_property_readonly("channels", &LinkSim::channels)
       .def_property_readonly("packets_sent", &LinkSim::packets_sent)
-      .def_readonly_static("packet_bytes", &kLinkPktBytes);
+      .def_readonly_static("packet_bytes", &kLinkPktBytes)
+      // one epoch of the packet exchange, packed into / unpacked from the
+      // all-to-all buffers in place (parallel/collectives.py)
+      .def("pack_epoch",
+           [](LinkSim& l, uint64_t t_end, int k, int hdr, int64_t ann_next, int64_t ann_busy,
+              py::array_t<int64_t, py::array::c_style> send) {
+             const size_t need = (size_t)l.world() * ((size_t)hdr + 4 * (size_t)k);
+             if ((size_t)send.size() != need) throw std::invalid_argument("pack_epoch: send buffer size");
+             EpochOut o;
+             pack_epoch(l, t_end, k, hdr, ann_next, ann_busy, send.mutable_data(), o);
+             py::array_t<int64_t> extra(o.extra.size());
+             if (!o.extra.empty()) memcpy(extra.mutable_data(), o.extra.data(), o.extra.size() * sizeof(int64_t));
+             return py::make_tuple(extra, o.extra_words, o.packets, o.max_count);
+           })
+      .def("unpack_epoch",
+           [](LinkSim& l, py::array_t<int64_t, py::array::c_style | py::array::forcecast> recv, int k, int hdr,
+              py::array_t<int64_t, py::array::c_style | py::array::forcecast> extra) {
+             const size_t need = (size_t)l.world() * ((size_t)hdr + 4 * (size_t)k);
+             if ((size_t)recv.size() != need) throw std::invalid_argument("unpack_epoch: recv buffer size");
+             EpochIn r = unpack_epoch(l, recv.data(), k, hdr, extra.size() ? extra.data() : nullptr, (size_t)extra.size());
+             return py::make_tuple(r.any_busy, r.next);
+           });
 
   m.def(
       "linksim_run_local",

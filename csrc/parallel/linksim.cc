@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <limits>
+#include <cstring>
 #include <numeric>
 #include <stdexcept>
 
@@ -231,6 +232,83 @@ std::vector<uint64_t> linksim_run_local(const LinkParams& p, const CollSpec& c, 
   std::vector<uint64_t> fin(N);
   for (int r = 0; r < N; ++r) fin[r] = sims[r].finish_ps();
   return fin;
+}
+
+void pack_epoch(LinkSim& l, uint64_t t_end, int k, int hdr, int64_t ann_next, int64_t ann_busy, int64_t* send,
+                EpochOut& out) {
+  const int W = l.world();
+  const size_t slot = (size_t)hdr + 4 * (size_t)k;
+  std::vector<LinkPkt> pk;
+  l.emit(t_end, pk);
+  std::vector<int64_t> count(W, 0);
+  int64_t min_arr = INT64_MAX;
+  for (const LinkPkt& p : pk) {
+    if (p.dst < 0 || p.dst >= W) throw std::runtime_error("pack_epoch: packet to a rank outside the group");
+    ++count[p.dst];
+    min_arr = std::min<int64_t>(min_arr, (int64_t)std::min<uint64_t>(p.arrive_ps, (uint64_t)INT64_MAX));
+  }
+  int64_t mx = 0;
+  for (int64_t c : count) mx = std::max(mx, c);
+  std::memset(send, 0, sizeof(int64_t) * slot * W);
+  for (int d = 0; d < W; ++d) {
+    int64_t* h = send + (size_t)d * slot;
+    h[0] = count[d];
+    h[1] = mx;
+    h[2] = ann_next;
+    h[3] = ann_busy;
+    h[4] = min_arr;
+  }
+  // stable by destination: emission order within each destination
+  std::vector<int64_t> fill(W, 0);
+  out.extra.clear();
+  out.extra_words.assign(W, 0);
+  std::vector<std::vector<int64_t>> over(W);
+  for (const LinkPkt& p : pk) {
+    int64_t w[4];
+    std::memcpy(w, &p, sizeof(w));
+    if (fill[p.dst] < k) {
+      std::memcpy(send + (size_t)p.dst * slot + hdr + 4 * fill[p.dst], w, sizeof(w));
+    } else {
+      over[p.dst].insert(over[p.dst].end(), w, w + 4);
+    }
+    ++fill[p.dst];
+  }
+  for (int d = 0; d < W; ++d) {
+    out.extra_words[d] = (int64_t)over[d].size();
+    out.extra.insert(out.extra.end(), over[d].begin(), over[d].end());
+  }
+  out.packets = pk.size();
+  out.max_count = mx;
+}
+
+EpochIn unpack_epoch(LinkSim& l, const int64_t* recv, int k, int hdr, const int64_t* extra, size_t extra_words) {
+  const int W = l.world();
+  const size_t slot = (size_t)hdr + 4 * (size_t)k;
+  std::vector<LinkPkt> in;
+  size_t off = 0;
+  EpochIn r;
+  r.next = INT64_MAX;
+  for (int s = 0; s < W; ++s) {
+    const int64_t* h = recv + (size_t)s * slot;
+    const int64_t n = h[0];
+    const int64_t in_slot = std::min<int64_t>(n, k);
+    for (int64_t i = 0; i < in_slot; ++i) {
+      LinkPkt p;
+      std::memcpy(&p, h + hdr + 4 * i, sizeof(p));
+      in.push_back(p);
+    }
+    for (int64_t i = in_slot; i < n; ++i) {
+      if (off + 4 > extra_words) throw std::runtime_error("unpack_epoch: overflow payload shorter than announced");
+      LinkPkt p;
+      std::memcpy(&p, extra + off, sizeof(p));
+      off += 4;
+      in.push_back(p);
+    }
+    r.any_busy = std::max(r.any_busy, h[3]);
+    r.next = std::min(r.next, std::min(h[2], h[4]));
+  }
+  if (!in.empty()) l.receive(in.data(), in.size());
+  return r;
 }
 
 }  // namespace asim

@@ -68,6 +68,7 @@ class LinkSim {
   uint64_t epoch_ps() const { return epoch_ps_; }
   uint32_t channels() const { return nch_; }
   uint64_t packets_sent() const { return sent_; }
+  int world() const { return world_; }
 
   // the rank's role at (channel, step): peer it sends to / receives from (-1 none)
   int send_peer(int c, int k) const;
@@ -105,6 +106,29 @@ class LinkSim {
   uint64_t recv_left_ = 0, send_left_ = 0, sent_ = 0;
   uint64_t finish_ps_ = 0;
 };
+
+// One epoch of the distributed packet exchange (parallel/collectives.py),
+// packed and unpacked natively so the per-epoch host work is two calls around
+// the all-to-all.  Fixed layout: per destination a slot of `hdr` header words
+// {packets for it, this rank's largest per-destination count, announced next
+// event, announced busy flag, earliest arrival among this epoch's packets}
+// followed by up to `k` packets (4 int64 words each, emission order);
+// packets past `k` for a destination go to `extra`, destination order.
+struct EpochOut {
+  std::vector<int64_t> extra;
+  std::vector<int64_t> extra_words;  // per destination
+  uint64_t packets = 0;
+  int64_t max_count = 0;
+};
+void pack_epoch(LinkSim& l, uint64_t t_end, int k, int hdr, int64_t ann_next, int64_t ann_busy, int64_t* send,
+                EpochOut& out);
+// Deliver the received slots (+ the overflow words, source order) to `l`;
+// returns {any rank busy, the earliest next event or arrival over ranks}.
+struct EpochIn {
+  int64_t any_busy = 0;
+  int64_t next = 0;
+};
+EpochIn unpack_epoch(LinkSim& l, const int64_t* recv, int k, int hdr, const int64_t* extra, size_t extra_words);
 
 // Run all `world` ranks in one process (identical results to the distributed
 // driver).  start_ps[r] = when rank r reaches the collective.  Returns the
