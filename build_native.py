@@ -37,7 +37,7 @@ CORE_SRC = [
     "csrc/driver/dump.cc",
     "csrc/parallel/linksim.cc",
 ]
-HIP_SRC = ["csrc/engine/gpu_engine.hip"]
+HIP_SRC = ["csrc/engine/gpu_engine.hip", "csrc/engine/ingest_mfma.hip"]
 STUB_SRC = ["csrc/engine/gpu_stub.cc"]
 
 

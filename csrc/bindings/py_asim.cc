@@ -1,4 +1,5 @@
 // Python bindings of the native simulator (module: accel_sim_framework_distributed_amd._asim).
+#include <chrono>
 #include <pybind11/functional.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -305,6 +306,75 @@ PYBIND11_MODULE(_asim, m) {
       save_kernel_text(k, out);
     return k.warp_insts;
   });
+  // host coalescer vs the MI355X matrix-core coalescer on one kernel: equal
+  // instruction and access arrays, and where the work ran
+  auto ingest_cmp = [](const HostKernel& k, const SimCfg& c, int device) {
+    py::dict d;
+    const auto t0 = std::chrono::steady_clock::now();
+    ReadyKernel h = coalesce_kernel(k, c);
+    const auto t1 = std::chrono::steady_clock::now();
+    IngestStats st;
+    ReadyKernel g;
+    const bool ran = gpu_coalesce_kernel(k, c, device, g, &st);
+    d["ran"] = ran;
+    d["host_s"] = std::chrono::duration<double>(t1 - t0).count();
+    d["n_insts"] = (uint64_t)h.insts.size();
+    d["n_accs"] = (uint64_t)h.accs.size();
+    if (!ran) return d;
+    int64_t bad_inst = -1, bad_acc = -1;
+    for (size_t i = 0; i < h.insts.size() && i < g.insts.size() && bad_inst < 0; ++i)
+      if (memcmp(&h.insts[i], &g.insts[i], sizeof(TInst)) != 0) bad_inst = (int64_t)i;
+    for (size_t i = 0; i < h.accs.size() && i < g.accs.size() && bad_acc < 0; ++i)
+      if (memcmp(&h.accs[i], &g.accs[i], sizeof(TAcc)) != 0) bad_acc = (int64_t)i;
+    d["equal"] = bad_inst < 0 && bad_acc < 0 && h.insts.size() == g.insts.size() && h.accs.size() == g.accs.size();
+    d["first_bad_inst"] = bad_inst;
+    d["first_bad_acc"] = bad_acc;
+    if (bad_inst >= 0) {
+      d["host_width"] = (int)h.insts[bad_inst].width;
+      d["dev_width"] = (int)g.insts[bad_inst].width;
+    }
+    d["smem_device"] = st.smem_jobs;
+    d["smem_host"] = st.smem_host;
+    d["gmem_device"] = st.gmem_jobs;
+    d["gmem_host"] = st.gmem_host;
+    d["mfma"] = st.mfma;
+    d["device_s"] = st.device_s;
+    d["total_s"] = st.total_s;
+    return d;
+  };
+  m.def("ingest_compare", [ingest_cmp](const std::string& path, const std::vector<std::string>& args, int device) {
+    SimCfg c = cfg_from_args(args);
+    return ingest_cmp(load_kernel(path), c, device);
+  }, py::arg("path"), py::arg("args"), py::arg("device") = 0);
+  // explicit instructions: (space 'shared'|'global', bytes per lane, active mask, active lanes' addresses)
+  m.def("ingest_compare_lanes",
+        [ingest_cmp](const std::vector<std::tuple<std::string, uint32_t, uint64_t, std::vector<uint64_t>>>& ins,
+                     const std::vector<std::string>& args, int device) {
+          SimCfg c = cfg_from_args(args);
+          HostKernel k;
+          k.h.name = "ingest_lanes";
+          k.h.warp_size = c.warp_size ? c.warp_size : 32;
+          k.n_cta = 1;
+          k.warps_per_cta = 1;
+          for (const auto& t : ins) {
+            TInst in{};
+            in.cls = OC_LOAD;
+            in.space = std::get<0>(t) == "shared" ? S_SHARED : S_GLOBAL;
+            in.width = (uint8_t)std::get<1>(t);
+            in.mask = std::get<2>(t);
+            const auto& a = std::get<3>(t);
+            if ((size_t)__builtin_popcountll(in.mask) != a.size()) throw std::runtime_error("one address per active lane");
+            TMem m{};
+            m.list = (uint32_t)k.addrs.size();
+            k.addrs.insert(k.addrs.end(), a.begin(), a.end());
+            in.mem = (uint32_t)k.mems.size();
+            k.mems.push_back(m);
+            k.insts.push_back(in);
+          }
+          k.streams.push_back(WStream{0, (uint32_t)k.insts.size()});
+          return ingest_cmp(k, c, device);
+        },
+        py::arg("insts"), py::arg("args"), py::arg("device") = 0);
   m.def("coalesce_summary", [](const std::string& path, const std::vector<std::string>& args) {
     SimCfg c = cfg_from_args(args);
     ReadyKernel r = coalesce_kernel(load_kernel(path), c);

@@ -170,6 +170,8 @@ const OptDef kOptions[] = {
     {"-gpgpu_clock_domains", 's', "500.0:2000.0:2000.0:2000.0", "core:icnt:L2:DRAM MHz"},
     {"-gpgpu_max_concurrent_kernel", 'i', "32", ""},
     {"-trace_prefetch", 'b', "1", "parse + coalesce the next kernel's trace on a host thread while the engine runs"},
+    {"-gpu_ingest", 'b', "1",
+     "with -sim_engine gpu: coalesce kernel traces (shared-memory bank conflicts, global line/sector lists) on the MI355X matrix cores"},
     {"-gpgpu_kernel_launch_latency", 'i', "0", "kernel launch latency (cycles)"},
     {"-gpgpu_kernel_launch_latency_queued", 'i', "-1",
      "launch latency of a kernel queued right behind the previous one (no memcpy / sync between); -1 = as -gpgpu_kernel_launch_latency"},
@@ -1071,6 +1073,7 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.concurrent_kernel_sm = r.getb("-gpgpu_concurrent_kernel_sm") ? 1 : 0;
   d.max_concurrent_kernel = (int32_t)r.geti("-gpgpu_max_concurrent_kernel");
   d.trace_prefetch = r.getb("-trace_prefetch");
+  d.gpu_ingest = r.getb("-gpu_ingest");
   d.power_enabled = r.getb("-power_simulation_enabled");
   d.power_xml = r.gets("-accelwattch_xml_file");
   {

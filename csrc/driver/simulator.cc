@@ -35,6 +35,7 @@ Simulator::Simulator(const std::vector<std::string>& args) {
   if (dopt_.engine == "gpu") {
     eng_ = make_gpu_engine();
     if (!eng_) throw std::runtime_error("-sim_engine gpu requested but the HIP engine is unavailable");
+    if (dopt_.gpu_ingest) ingest_dev_ = gpu_current_device();
   } else if (dopt_.engine == "cpu") {
     eng_ = make_cpu_engine();
   } else if (dopt_.engine == "check") {
@@ -449,7 +450,22 @@ std::unique_ptr<ReadyKernel> Simulator::take_kernel(size_t idx) {
     pf_.erase(it);
     return k;
   }
-  return std::unique_ptr<ReadyKernel>(new ReadyKernel(coalesce_kernel(load_kernel(cmds_[idx].text), cfg_)));
+  return ingest(load_kernel(cmds_[idx].text));
+}
+
+std::unique_ptr<ReadyKernel> Simulator::ingest(const HostKernel& k) {
+  if (ingest_dev_ < 0) return std::unique_ptr<ReadyKernel>(new ReadyKernel(coalesce_kernel(k, cfg_)));
+  IngestStats st;
+  std::unique_ptr<ReadyKernel> r(new ReadyKernel(ingest_kernel(k, cfg_, ingest_dev_, &st)));
+  std::lock_guard<std::mutex> g(ingest_mu_);
+  ingest_st_.smem_jobs += st.smem_jobs;
+  ingest_st_.smem_host += st.smem_host;
+  ingest_st_.gmem_jobs += st.gmem_jobs;
+  ingest_st_.gmem_host += st.gmem_host;
+  ingest_st_.mfma += st.mfma;
+  ingest_st_.device_s += st.device_s;
+  ingest_st_.total_s += st.total_s;
+  return r;
 }
 
 void Simulator::prefetch_next() {
@@ -457,10 +473,7 @@ void Simulator::prefetch_next() {
   for (size_t i = next_cmd_; i < cmds_.size(); ++i) {
     if (cmds_[i].type != CMD_KERNEL) continue;
     const std::string path = cmds_[i].text;
-    const SimCfg cfg = cfg_;
-    pf_[i] = std::async(std::launch::async, [path, cfg]() {
-      return std::unique_ptr<ReadyKernel>(new ReadyKernel(coalesce_kernel(load_kernel(path), cfg)));
-    });
+    pf_[i] = std::async(std::launch::async, [this, path]() { return ingest(load_kernel(path)); });
     return;
   }
 }
@@ -1349,6 +1362,14 @@ void Simulator::print_sim_time() {
   if (peak)
     print("gpu_trace_resident_peak_bytes: %llu\ngpu_trace_window_fills: %llu\n", (unsigned long long)peak,
           (unsigned long long)refills);
+  if (ingest_dev_ >= 0) {
+    std::lock_guard<std::mutex> g(ingest_mu_);
+    print("gpu_ingest: shared %llu on device (%llu host), global %llu on device (%llu host), %llu mfma, "
+          "device %.3f s of %.3f s\n",
+          (unsigned long long)ingest_st_.smem_jobs, (unsigned long long)ingest_st_.smem_host,
+          (unsigned long long)ingest_st_.gmem_jobs, (unsigned long long)ingest_st_.gmem_host,
+          (unsigned long long)ingest_st_.mfma, ingest_st_.device_s, ingest_st_.total_s);
+  }
   fflush(stdout);
 }
 

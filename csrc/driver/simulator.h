@@ -8,6 +8,7 @@
 #include <future>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -138,6 +139,13 @@ class Simulator {
   // engine simulates
   void prefetch_next();
   std::unique_ptr<ReadyKernel> take_kernel(size_t idx);
+  // trace ingest: HIP device of the GPU engine (-1: host coalescer) and what
+  // ran where (the prefetch thread adds to it too; declared before pf_ so that
+  // pending prefetches finish before these are destroyed)
+  int ingest_dev_ = -1;
+  std::mutex ingest_mu_;
+  IngestStats ingest_st_;
+  std::unique_ptr<ReadyKernel> ingest(const HostKernel& k);
   std::map<size_t, std::future<std::unique_ptr<ReadyKernel>>> pf_;
   void print_kernel_stats(const KernelResult& r, const std::vector<SMStats>& sm, const std::vector<MemStats>& mem);
   void print_sim_time();

@@ -10,3 +10,11 @@ namespace asim {
 int gpu_cu_count() { return 0; }
 EngineKernelInfo gpu_engine_kernel_info() { return EngineKernelInfo{}; }
 }  // namespace asim
+
+namespace asim {
+bool gpu_coalesce_kernel(const HostKernel&, const SimCfg&, int, ReadyKernel&, IngestStats*) { return false; }
+}  // namespace asim
+
+namespace asim {
+int gpu_current_device() { return -1; }
+}  // namespace asim

@@ -1054,7 +1054,149 @@ uint32_t smem_conflict_degree(const uint64_t* addr, uint64_t mask, uint32_t widt
   return total ? total : 1;
 }
 
+// ---- per-instruction ingest steps, shared by the host coalescer below and
+// the MI355X one (engine/ingest_mfma.hip) ----
+
+IngestKind ingest_prepare(TInst& in, const SimCfg& c) {
+  // latency / initiation interval from the config (per op class)
+  if (in.flags & F_WAITCNT) return IK_DONE;  // lat holds the s_waitcnt counts
+  const bool half = (in.lat & 0x8000) != 0;
+  uint32_t cls = in.cls < OC_COUNT ? in.cls : OC_ALU;
+  in.lat = c.lat[cls];
+  uint32_t ii = c.ii[cls];
+  if (half) ii = std::max<uint32_t>(1, ii / 2);
+  in.ii = (uint8_t)std::min<uint32_t>(ii, 255);
+  if (in.mem == kNoMem && in.cls == OC_LOAD && in.space == S_CONST) return IK_SCALAR;
+  if (in.mem == kNoMem) {
+    if ((in.cls == OC_LOAD || in.cls == OC_STORE) && in.space != S_SHARED) {
+      // no active address: completes like a 1-cycle shared access
+      in.space = S_SHARED;
+    }
+    if (in.cls == OC_LOAD || in.cls == OC_STORE) in.width = 1;
+    return IK_DONE;
+  }
+  return in.space == S_SHARED ? IK_SMEM : IK_GMEM;
+}
+
+void ingest_scalar(TInst& in, const SimCfg& c, uint64_t name_hash, std::vector<TAcc>& accs) {
+  // CDNA scalar load: one wave-uniform access.  Its address is not in the
+  // trace (the ISA tracer records vector addresses), so the scalar cache
+  // is keyed by kernel and code offset: the kernel-argument / constant
+  // loads every wave repeats hit after the first touch on a CU, nearby
+  // loads share lines (code offset / 8 -> data offset)
+  const uint64_t addr = kScalarBase + (name_hash & 0xfffffull) * 4096 + (uint64_t)(std::min<uint32_t>(in.pc, 32767) / 8);
+  TAcc a{};
+  a.line = addr & ~127ull;
+  a.sectors = (uint8_t)(1u << ((addr >> 5) & 3));
+  a.bytes = (uint16_t)std::max<uint32_t>(4, in.width);
+  a.bank = (uint8_t)((a.line >> 7) % std::max<uint32_t>(1, c.l1_banks));
+  in.mem = (uint32_t)accs.size();
+  accs.push_back(a);
+  in.width = 1;
+}
+
+uint32_t coalesce_lanes(const uint64_t* lane, uint64_t mask, uint32_t width, uint32_t ws, const SimCfg& c,
+                        TAcc* out) {
+  // global / local: group touched 32B sectors by 128B line (sorted by
+  // address like the reference's block map, abstract_hardware_model.cc:475-586)
+  std::pair<uint64_t, uint8_t> lines[64 * 8];
+  uint32_t bytes[64 * 8];
+  uint32_t nl = 0;
+  std::vector<std::pair<uint64_t, uint8_t>> big_l;  // accesses wider than the stack arrays
+  std::vector<uint32_t> big_b;
+  const bool wide = width > 7 * 128;
+  for (uint32_t l = 0; l < ws; ++l) {
+    if (!(mask >> l & 1ull)) continue;
+    uint64_t a = lane[l];
+    const uint64_t end = a + width;
+    while (a < end) {
+      const uint64_t line = a & ~127ull;
+      const uint64_t lend = std::min<uint64_t>(end, line + 128);
+      uint8_t sec = 0;
+      for (uint64_t s = (a >> 5); s <= ((lend - 1) >> 5); ++s) sec |= (uint8_t)(1u << (s & 3));
+      auto* L = wide ? big_l.data() : lines;
+      auto* B = wide ? big_b.data() : bytes;
+      const uint32_t n = wide ? (uint32_t)big_l.size() : nl;
+      bool found = false;
+      for (uint32_t i = 0; i < n; ++i)
+        if (L[i].first == line) {
+          L[i].second |= sec;
+          B[i] += (uint32_t)(lend - a);
+          found = true;
+          break;
+        }
+      if (!found) {
+        if (wide) {
+          big_l.emplace_back(line, sec);
+          big_b.push_back((uint32_t)(lend - a));
+        } else {
+          lines[nl] = std::make_pair(line, sec);
+          bytes[nl++] = (uint32_t)(lend - a);
+        }
+      }
+      a = lend;
+    }
+  }
+  const auto* L = wide ? big_l.data() : lines;
+  const auto* B = wide ? big_b.data() : bytes;
+  const uint32_t n_all = wide ? (uint32_t)big_l.size() : nl;
+  std::vector<uint32_t> ord(n_all);
+  for (uint32_t i = 0; i < n_all; ++i) ord[i] = i;
+  std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return L[x].first < L[y].first; });
+  uint32_t n = 0;
+  for (uint32_t oi = 0; oi < n_all && n < (uint32_t)kMaxAccess; ++oi) {
+    const uint32_t i = ord[oi];
+    TAcc a{};
+    a.line = L[i].first;
+    a.sectors = L[i].second;
+    a.bytes = (uint16_t)std::min<uint32_t>(B[i], 128);
+    a.bank = (uint8_t)((a.line >> 7) % std::max<uint32_t>(1, c.l1_banks));
+    out[n++] = a;
+  }
+  return n;
+}
+
+void ingest_finish_global(TInst& in, const TAcc* a, uint32_t n, std::vector<TAcc>& accs) {
+  in.mem = (uint32_t)accs.size();
+  accs.insert(accs.end(), a, a + n);
+  in.width = (uint8_t)std::max<uint32_t>(1, n);
+  if (n == 0) {
+    in.space = S_SHARED;
+    in.mem = kNoMem;
+  }
+}
+
+void ingest_lane_addresses(const HostKernel& k, const TInst& in, uint64_t* out, uint32_t ws) {
+  lane_addresses(k, in, out, ws);
+}
+
 ReadyKernel coalesce_kernel(const HostKernel& k, const SimCfg& c) {
+  ReadyKernel r = ingest_shell(k);
+  const uint32_t ws = k.h.warp_size ? k.h.warp_size : 32;
+  std::vector<uint64_t> lane(64);
+  const uint64_t name_hash = std::hash<std::string>{}(k.h.name);
+  TAcc tmp[kMaxAccess];
+  for (auto& in : r.insts) {
+    const IngestKind kind = ingest_prepare(in, c);
+    if (kind == IK_DONE) continue;
+    if (kind == IK_SCALAR) {
+      ingest_scalar(in, c, name_hash, r.accs);
+      continue;
+    }
+    lane_addresses(k, in, lane.data(), ws);
+    const uint32_t width = in.width ? in.width : 4;
+    if (kind == IK_SMEM) {
+      in.width = (uint8_t)std::min<uint32_t>(255, smem_conflict_degree(lane.data(), in.mask, width, c, ws));
+      in.mem = kNoMem;
+      continue;
+    }
+    const uint32_t n = coalesce_lanes(lane.data(), in.mask, width, ws, c, tmp);
+    ingest_finish_global(in, tmp, n, r.accs);
+  }
+  return r;
+}
+
+ReadyKernel ingest_shell(const HostKernel& k) {
   ReadyKernel r;
   r.h = k.h;
   r.warps_per_cta = k.warps_per_cta;
@@ -1064,103 +1206,15 @@ ReadyKernel coalesce_kernel(const HostKernel& k, const SimCfg& c) {
   r.warp_insts = k.warp_insts;
   r.insts = k.insts;
   r.accs.reserve(k.mems.size() * 2);
-  const uint32_t ws = k.h.warp_size ? k.h.warp_size : 32;
-  std::vector<uint64_t> lane(64);
-  const uint64_t name_hash = std::hash<std::string>{}(k.h.name);
-  std::vector<std::pair<uint64_t, uint8_t>> lines;
-  std::vector<uint32_t> bytes;
-  std::vector<uint32_t> ord;
-  for (auto& in : r.insts) {
-    // latency / initiation interval from the config (per op class)
-    if (in.flags & F_WAITCNT) continue;  // lat holds the s_waitcnt counts
-    const bool half = (in.lat & 0x8000) != 0;
-    uint32_t cls = in.cls < OC_COUNT ? in.cls : OC_ALU;
-    in.lat = c.lat[cls];
-    uint32_t ii = c.ii[cls];
-    if (half) ii = std::max<uint32_t>(1, ii / 2);
-    in.ii = (uint8_t)std::min<uint32_t>(ii, 255);
-    if (in.mem == kNoMem && in.cls == OC_LOAD && in.space == S_CONST) {
-      // CDNA scalar load: one wave-uniform access.  Its address is not in the
-      // trace (the ISA tracer records vector addresses), so the scalar cache
-      // is keyed by kernel and code offset: the kernel-argument / constant
-      // loads every wave repeats hit after the first touch on a CU, nearby
-      // loads share lines (code offset / 8 -> data offset)
-      const uint64_t addr = kScalarBase + (name_hash & 0xfffffull) * 4096 + (uint64_t)(std::min<uint32_t>(in.pc, 32767) / 8);
-      TAcc a{};
-      a.line = addr & ~127ull;
-      a.sectors = (uint8_t)(1u << ((addr >> 5) & 3));
-      a.bytes = (uint16_t)std::max<uint32_t>(4, in.width);
-      a.bank = (uint8_t)((a.line >> 7) % std::max<uint32_t>(1, c.l1_banks));
-      in.mem = (uint32_t)r.accs.size();
-      r.accs.push_back(a);
-      in.width = 1;
-      continue;
-    }
-    if (in.mem == kNoMem) {
-      if ((in.cls == OC_LOAD || in.cls == OC_STORE) && in.space != S_SHARED) {
-        // no active address: completes like a 1-cycle shared access
-        in.space = S_SHARED;
-      }
-      if (in.cls == OC_LOAD || in.cls == OC_STORE) in.width = 1;
-      continue;
-    }
-    lane_addresses(k, in, lane.data(), ws);
-    const uint32_t width = in.width ? in.width : 4;
-    if (in.space == S_SHARED) {
-      in.width = (uint8_t)std::min<uint32_t>(255, smem_conflict_degree(lane.data(), in.mask, width, c, ws));
-      in.mem = kNoMem;
-      continue;
-    }
-    // global / local: group touched 32B sectors by 128B line (sorted by
-    // address like the reference's block map, abstract_hardware_model.cc:475-586)
-    lines.clear();
-    bytes.clear();
-    for (uint32_t l = 0; l < ws; ++l) {
-      if (!(in.mask >> l & 1ull)) continue;
-      uint64_t a = lane[l];
-      uint64_t end = a + width;
-      while (a < end) {
-        uint64_t line = a & ~127ull;
-        uint64_t lend = std::min<uint64_t>(end, line + 128);
-        uint8_t sec = 0;
-        for (uint64_t s = (a >> 5); s <= ((lend - 1) >> 5); ++s) sec |= (uint8_t)(1u << (s & 3));
-        bool found = false;
-        for (size_t i = 0; i < lines.size(); ++i)
-          if (lines[i].first == line) {
-            lines[i].second |= sec;
-            bytes[i] += (uint32_t)(lend - a);
-            found = true;
-            break;
-          }
-        if (!found) {
-          lines.emplace_back(line, sec);
-          bytes.push_back((uint32_t)(lend - a));
-        }
-        a = lend;
-      }
-    }
-    ord.resize(lines.size());
-    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (uint32_t)i;
-    std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return lines[x].first < lines[y].first; });
-    in.mem = (uint32_t)r.accs.size();
-    uint32_t n = 0;
-    for (size_t oi = 0; oi < ord.size() && n < (uint32_t)kMaxAccess; ++oi) {
-      size_t i = ord[oi];
-      TAcc a{};
-      a.line = lines[i].first;
-      a.sectors = lines[i].second;
-      a.bytes = (uint16_t)std::min<uint32_t>(bytes[i], 128);
-      a.bank = (uint8_t)((a.line >> 7) % std::max<uint32_t>(1, c.l1_banks));
-      r.accs.push_back(a);
-      ++n;
-    }
-    in.width = (uint8_t)std::max<uint32_t>(1, n);
-    if (n == 0) {
-      in.space = S_SHARED;
-      in.mem = kNoMem;
-    }
-  }
   return r;
+}
+
+ReadyKernel ingest_kernel(const HostKernel& k, const SimCfg& c, int device, IngestStats* st) {
+  if (device >= 0) {
+    ReadyKernel r;
+    if (gpu_coalesce_kernel(k, c, device, r, st)) return r;
+  }
+  return coalesce_kernel(k, c);
 }
 
 }  // namespace asim

@@ -128,6 +128,30 @@ uint32_t opcode_count();
 // Coalescing (host reference of the trace-ingest coalescer; same function is
 // run lane-parallel by the HIP ingest kernel).
 ReadyKernel coalesce_kernel(const HostKernel& k, const SimCfg& c);
+// ingest steps of one instruction (coalesce_kernel is built from them; the
+// MI355X coalescer, engine/ingest_mfma.hip, runs the address-dependent ones
+// on the device and these on the host)
+enum IngestKind : uint8_t { IK_DONE = 0, IK_SCALAR, IK_SMEM, IK_GMEM };
+IngestKind ingest_prepare(TInst& in, const SimCfg& c);  // latency / ii, address-less fixes
+void ingest_scalar(TInst& in, const SimCfg& c, uint64_t name_hash, std::vector<TAcc>& accs);
+// sorted 128B-line accesses of one global instruction (<= kMaxAccess into out)
+uint32_t coalesce_lanes(const uint64_t* lane, uint64_t mask, uint32_t width, uint32_t ws, const SimCfg& c, TAcc* out);
+void ingest_finish_global(TInst& in, const TAcc* a, uint32_t n, std::vector<TAcc>& accs);
+void ingest_lane_addresses(const HostKernel& k, const TInst& in, uint64_t* out, uint32_t ws);
+ReadyKernel ingest_shell(const HostKernel& k);  // everything but the coalesced instructions
+struct IngestStats {
+  uint64_t smem_jobs = 0, smem_host = 0;  // shared-memory instructions: on the device / fell back to the host
+  uint64_t gmem_jobs = 0, gmem_host = 0;  // global instructions: on the device / fell back to the host
+  uint64_t mfma = 0;                      // matrix-core instructions issued
+  double device_s = 0, total_s = 0;
+};
+// MI355X coalescer (bank-by-row and line-by-sector occupancy matrices on the
+// matrix cores); false when no HIP device / build
+bool gpu_coalesce_kernel(const HostKernel& k, const SimCfg& c, int device, ReadyKernel& out, IngestStats* st);
+// device >= 0: coalesce on that HIP device (bit-identical to coalesce_kernel),
+// else, or when it is unavailable, on the host
+ReadyKernel ingest_kernel(const HostKernel& k, const SimCfg& c, int device = -1, IngestStats* st = nullptr);
+int gpu_current_device();  // the calling thread's HIP device (-1: none / CPU-only build)
 
 // shared-memory bank-conflict degree of one warp access
 uint32_t smem_conflict_degree(const uint64_t* addr, uint64_t mask, uint32_t width, const SimCfg& c, uint32_t warp_size);

@@ -295,4 +295,7 @@ def test_trace_window_streaming_gpu_equals_cpu(gpu_mod, tmp_path, extra):
     diag = lambda r, key: int(re.search(key + r": (\d+)", r.output).group(1))
     pw, pf = diag(win, "gpu_trace_resident_peak_bytes"), diag(whole, "gpu_trace_resident_peak_bytes")
     assert diag(win, "gpu_trace_window_fills") > 3
-    assert pw * 4 < pf, (pw, pf)
+    # the rings are powers of two sized for the oldest resident CTA up to the
+    # dispatch bound of the next epochs (XCD round-robin dispatch spreads
+    # that span): about 2 K of the 6 K CTAs are resident here
+    assert pw * 2 < pf, (pw, pf)
