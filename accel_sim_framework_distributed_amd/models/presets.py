@@ -529,6 +529,8 @@ def _mi355x() -> Dict[str, str]:
         "-gpgpu_warp_issue_interval": "5",
         "-gpgpu_scheduler": "gto",
         "-gpgpu_shmem_num_banks": "64",
+        # LDS banking by each ds_* instruction's lane groups (MI355X LDS table)
+        "-gpgpu_shmem_cdna_lane_groups": "1",
         "-gpgpu_shmem_size": "163840",
         "-gpgpu_shmem_sizeDefault": "163840",
         "-gpgpu_shmem_per_block": "163840",

@@ -253,6 +253,16 @@ PYBIND11_MODULE(_asim, m) {
           for (size_t i = 0; i < addrs.size() && i < 64; ++i) a[i] = addrs[i];
           return smem_conflict_degree(a.data(), mask, width, c, c.warp_size);
         });
+  // CDNA4 lane-group banking of one ds_* instruction (opcode name, wave64)
+  m.def("smem_conflict_degree_cdna", [](const std::vector<uint64_t>& addrs, uint64_t mask, uint32_t width,
+                                        const std::string& opcode, const std::vector<std::string>& args) {
+    SimCfg c = cfg_from_args(args);
+    std::vector<uint64_t> a(64, 0);
+    for (size_t i = 0; i < addrs.size() && i < 64; ++i) a[i] = addrs[i];
+    std::string op = opcode;
+    for (auto& ch : op) ch = (char)tolower(ch);
+    return smem_conflict_degree(a.data(), mask, width, c, 64, lds_groups_for(op));
+  });
   m.def("occupancy", [](const std::vector<std::string>& args, uint32_t threads, uint32_t shmem, uint32_t regs) {
     SimCfg c = cfg_from_args(args);
     Occupancy o = compute_occupancy(c, KernelShape{threads, shmem, regs, 1});
@@ -346,9 +356,10 @@ PYBIND11_MODULE(_asim, m) {
     SimCfg c = cfg_from_args(args);
     return ingest_cmp(load_kernel(path), c, device);
   }, py::arg("path"), py::arg("args"), py::arg("device") = 0);
-  // explicit instructions: (space 'shared'|'global', bytes per lane, active mask, active lanes' addresses)
+  // explicit instructions: (space 'shared'|'global', bytes per lane, active mask, active lanes' addresses,
+  // CDNA opcode name or "")
   m.def("ingest_compare_lanes",
-        [ingest_cmp](const std::vector<std::tuple<std::string, uint32_t, uint64_t, std::vector<uint64_t>>>& ins,
+        [ingest_cmp](const std::vector<std::tuple<std::string, uint32_t, uint64_t, std::vector<uint64_t>, std::string>>& ins,
                      const std::vector<std::string>& args, int device) {
           SimCfg c = cfg_from_args(args);
           HostKernel k;
@@ -362,6 +373,7 @@ PYBIND11_MODULE(_asim, m) {
             in.space = std::get<0>(t) == "shared" ? S_SHARED : S_GLOBAL;
             in.width = (uint8_t)std::get<1>(t);
             in.mask = std::get<2>(t);
+            if (!std::get<4>(t).empty()) in.opcode = decode_opcode(std::get<4>(t), 950).opcode;
             const auto& a = std::get<3>(t);
             if ((size_t)__builtin_popcountll(in.mask) != a.size()) throw std::runtime_error("one address per active lane");
             TMem m{};

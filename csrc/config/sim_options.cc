@@ -55,6 +55,10 @@ const OptDef kOptions[] = {
     {"-gpgpu_shmem_size_PrefShared", 'u', "16384", "shmem size prefer-shared"},
     {"-gpgpu_shmem_num_banks", 'u', "16", "shared memory banks"},
     {"-gpgpu_shmem_limited_broadcast", 'b', "1", "limited broadcast"},
+    {"-gpgpu_shmem_cdna_lane_groups", 'b', "0",
+     "wave64 traces: bank conflicts per CDNA4 LDS lane group of each ds_* instruction (2 x 32 lanes for b32/b64, "
+     "4 x 16 for b128, 8 x 8 for b96 and wide stores; 32 or 64 banks by instruction); the degree is 1 + the extra "
+     "cycles (SQ_LDS_BANK_CONFLICT)"},
     {"-gpgpu_shmem_warp_parts", 'i', "2", "warp parts for shmem conflicts"},
     {"-gpgpu_mem_unit_ports", 'i', "1", "memory unit ports"},
     {"-gpgpu_warpdistro_shader", 'i', "-1", "warp distribution shader"},
@@ -782,6 +786,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.smem_latency = (uint32_t)r.getu(user_set("-smem_latency") ? "-smem_latency" : "-gpgpu_smem_latency");
   c.smem_warp_parts = (uint32_t)std::max<long long>(1, r.geti("-gpgpu_shmem_warp_parts"));
   c.smem_limited_bcast = r.getb("-gpgpu_shmem_limited_broadcast") ? 1 : 0;
+  c.smem_cdna_groups = r.getb("-gpgpu_shmem_cdna_lane_groups") ? 1 : 0;
   c.l1 = parse_cache_geom(r.gets("-gpgpu_cache:dl1"));
   c.l1_latency = (uint32_t)r.getu("-gpgpu_l1_latency");
   c.l1_banks = std::max<uint32_t>(1, (uint32_t)r.getu("-gpgpu_l1_banks"));

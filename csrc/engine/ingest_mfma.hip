@@ -73,8 +73,14 @@ struct IngJob {
 };
 static_assert(sizeof(IngJob) == 32, "IngJob is 32 bytes");
 
+constexpr int kMaxGroupTables = 8;
+struct IngGroups {
+  uint32_t n, nb;
+  uint64_t lanes[8];
+};
 struct IngParams {
   uint32_t ws, nb, parts, l1_banks;
+  IngGroups groups[kMaxGroupTables];  // CDNA4 lane-group tables (IngJob::pad0 - 1)
 };
 
 __device__ __forceinline__ uint64_t wmin64(uint64_t v) {
@@ -108,6 +114,52 @@ __device__ __forceinline__ __bf16 bf(uint32_t v) {
   return __builtin_bit_cast(__bf16, (unsigned short)(__builtin_bit_cast(uint32_t, (float)v) >> 16));
 }
 
+// distinct words of the busiest bank over the lanes with `pa` set
+// (trace.cc lanes_degree): 0 without such lanes, kFallback outside the windows
+__device__ uint32_t group_degree(bool pa, uint64_t w0, uint64_t w1, uint32_t nw, uint32_t nb, uint32_t* sl,
+                                 uint32_t& nmfma) {
+  const int l = (int)(threadIdx.x & 63);
+  if (!__ballot(pa)) return 0;
+  const uint32_t nwmax = wmax32(pa ? nw : 0u);
+  if (nwmax > 8) return kFallback;
+  const uint64_t rlo = wmin64(pa ? w0 / nb : ~0ull);
+  const uint64_t rhi = wmax64(pa ? w1 / nb : 0ull);
+  if (rhi - rlo >= 32ull * kRowTiles) return kFallback;
+  const uint32_t ntr = (uint32_t)((rhi - rlo) / 32) + 1;
+  for (uint32_t j = 0; j < nwmax; ++j) {
+    const uint64_t w = w0 + j;
+    sl[j * 64 + l] = (pa && j < nw) ? ((uint32_t)(w / nb - rlo) << 8 | (uint32_t)(w % nb)) : kNoSlot;
+  }
+  wave_sync();
+  const uint32_t ksteps = nwmax * 4;  // 64 slots per word index, 16 per MFMA
+  const uint32_t h = (uint32_t)l >> 5, c32 = (uint32_t)l & 31;
+  uint32_t deg = 0;
+  for (uint32_t ct = 0; ct < nb / 32; ++ct) {
+    uint32_t cnt = 0;
+    for (uint32_t rt = 0; rt < ntr; ++rt) {
+      f32x16 acc = {};
+      for (uint32_t ks = 0; ks < ksteps; ++ks) {
+        bf16x8 a, b;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t v = sl[ks * 16 + 8 * h + e];
+          const bool valid = v != kNoSlot;
+          a[e] = bf(valid && (v >> 8) == rt * 32 + c32 ? 1u : 0u);   // A[row c32][k]
+          b[e] = bf(valid && (v & 0xffu) == ct * 32 + c32 ? 1u : 0u);  // B[k][bank c32]
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+        ++nmfma;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cnt += acc[r] != 0.0f ? 1u : 0u;
+    }
+    cnt += __shfl_xor(cnt, 32);  // both halves hold rows of the same bank column
+    deg = max(deg, wmax32(cnt));
+  }
+  wave_sync();
+  return deg;
+}
+
 // conflict degree of one shared-memory instruction (trace.cc smem_conflict_degree)
 __device__ uint32_t smem_degree(const IngJob& jb, bool act, uint64_t addr, const IngParams& p, uint32_t* sl,
                                 uint32_t& nmfma) {
@@ -115,51 +167,23 @@ __device__ uint32_t smem_degree(const IngJob& jb, bool act, uint64_t addr, const
   const uint64_t wb = jb.width ? jb.width : 4;
   const uint64_t w0 = addr >> 2, w1 = (addr + wb - 1) >> 2;
   const uint32_t nw = act ? (uint32_t)(w1 - w0 + 1) : 0u;
+  if (jb.pad0) {
+    // CDNA4 lane groups: 1 + the extra cycles over the groups
+    const IngGroups& g = p.groups[jb.pad0 - 1];
+    uint32_t extra = 0;
+    for (uint32_t i = 0; i < g.n; ++i) {
+      const uint32_t d = group_degree(act && ((g.lanes[i] >> l) & 1ull), w0, w1, nw, g.nb, sl, nmfma);
+      if (d == kFallback) return kFallback;
+      extra += d > 1 ? d - 1 : 0;
+    }
+    return 1 + extra;
+  }
   const uint32_t per = (p.ws + p.parts - 1) / p.parts;
-  const uint32_t nb = p.nb;
   uint32_t total = 0;
   for (uint32_t part = 0; part < p.parts; ++part) {
     const bool inpart = (uint32_t)l >= part * per && (uint32_t)l < (part + 1) * per && (uint32_t)l < p.ws;
-    const bool pa = act && inpart;
-    uint32_t deg = 0;
-    if (__ballot(pa)) {
-      const uint32_t nwmax = wmax32(pa ? nw : 0u);
-      if (nwmax > 8) return kFallback;
-      const uint64_t rlo = wmin64(pa ? w0 / nb : ~0ull);
-      const uint64_t rhi = wmax64(pa ? w1 / nb : 0ull);
-      if (rhi - rlo >= 32ull * kRowTiles) return kFallback;
-      const uint32_t ntr = (uint32_t)((rhi - rlo) / 32) + 1;
-      for (uint32_t j = 0; j < nwmax; ++j) {
-        const uint64_t w = w0 + j;
-        sl[j * 64 + l] = (pa && j < nw) ? ((uint32_t)(w / nb - rlo) << 8 | (uint32_t)(w % nb)) : kNoSlot;
-      }
-      wave_sync();
-      const uint32_t ksteps = nwmax * 4;  // 64 slots per word index, 16 per MFMA
-      const uint32_t h = (uint32_t)l >> 5, c32 = (uint32_t)l & 31;
-      for (uint32_t ct = 0; ct < nb / 32; ++ct) {
-        uint32_t cnt = 0;
-        for (uint32_t rt = 0; rt < ntr; ++rt) {
-          f32x16 acc = {};
-          for (uint32_t ks = 0; ks < ksteps; ++ks) {
-            bf16x8 a, b;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const uint32_t v = sl[ks * 16 + 8 * h + e];
-              const bool valid = v != kNoSlot;
-              a[e] = bf(valid && (v >> 8) == rt * 32 + c32 ? 1u : 0u);   // A[row c32][k]
-              b[e] = bf(valid && (v & 0xffu) == ct * 32 + c32 ? 1u : 0u);  // B[k][bank c32]
-            }
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
-            ++nmfma;
-          }
-#pragma unroll
-          for (int r = 0; r < 16; ++r) cnt += acc[r] != 0.0f ? 1u : 0u;
-        }
-        cnt += __shfl_xor(cnt, 32);  // both halves hold rows of the same bank column
-        deg = max(deg, wmax32(cnt));
-      }
-      wave_sync();
-    }
+    const uint32_t deg = group_degree(act && inpart, w0, w1, nw, p.nb, sl, nmfma);
+    if (deg == kFallback) return kFallback;
     total += deg ? deg : (part == 0 ? 1u : 0u);
   }
   return total ? total : 1u;
@@ -345,6 +369,12 @@ bool gpu_coalesce_kernel(const HostKernel& k, const SimCfg& c, int device, Ready
   const uint32_t nb = c.smem_banks ? c.smem_banks : 32;
   const uint32_t parts = c.smem_warp_parts ? c.smem_warp_parts : 1;
   const bool smem_dev = !c.smem_limited_bcast && (nb == 32 || nb == 64) && parts <= ws;
+  IngParams prm{};
+  prm.ws = ws;
+  prm.nb = nb;
+  prm.parts = parts;
+  prm.l1_banks = c.l1_banks;
+  std::vector<const LdsGroups*> tabs;  // distinct lane-group tables of this kernel
   const size_t n = r.insts.size();
   std::vector<uint8_t> kind(n);
   std::vector<uint32_t> job_of(n, kNoMem);
@@ -352,9 +382,25 @@ bool gpu_coalesce_kernel(const HostKernel& k, const SimCfg& c, int device, Ready
   for (size_t i = 0; i < n; ++i) {
     TInst& in = r.insts[i];
     kind[i] = ingest_prepare(in, c);
-    if (kind[i] == IK_GMEM || (kind[i] == IK_SMEM && smem_dev)) {
+    const LdsGroups* lg = kind[i] == IK_SMEM ? lds_groups(c, in.opcode, ws) : nullptr;
+    uint32_t tab = 0;
+    if (lg) {
+      size_t t = 0;
+      while (t < tabs.size() && tabs[t] != lg) ++t;
+      if (t == tabs.size() && t < (size_t)kMaxGroupTables) {
+        tabs.push_back(lg);
+        IngGroups& G = prm.groups[t];
+        G.n = lg->n;
+        G.nb = lg->nb;
+        for (int q = 0; q < 8; ++q) G.lanes[q] = lg->lanes[q];
+      }
+      tab = t < tabs.size() ? (uint32_t)t + 1 : 0;
+    }
+    const bool smem_ok = lg ? (tab != 0 && (lg->nb == 32 || lg->nb == 64)) : smem_dev;
+    if (kind[i] == IK_GMEM || (kind[i] == IK_SMEM && smem_ok)) {
       const TMem& m = k.mems[in.mem];
       IngJob jb{};
+      jb.pad0 = (uint8_t)tab;
       jb.mask = in.mask;
       jb.base = m.base;
       jb.stride = m.stride;
@@ -383,7 +429,6 @@ bool gpu_coalesce_kernel(const HostKernel& k, const SimCfg& c, int device, Ready
     X.nmf.ensure(nb_jobs * 4);
     X.acc.ensure(nb_jobs * kMaxAccess * sizeof(TAcc));
     X.cur.ensure(4);
-    const IngParams prm{ws, nb, parts, c.l1_banks};
     for (size_t b0 = 0; b0 < jobs.size(); b0 += kBatch) {
       const uint32_t nj = (uint32_t)std::min(kBatch, jobs.size() - b0);
       IHIPCHECK(hipMemcpyAsync(X.jobs.p, jobs.data() + b0, nj * sizeof(IngJob), hipMemcpyHostToDevice, s));
@@ -431,7 +476,8 @@ bool gpu_coalesce_kernel(const HostKernel& k, const SimCfg& c, int device, Ready
         } else {
           ++loc.smem_host;
           ingest_lane_addresses(k, in, lane.data(), ws);
-          in.width = (uint8_t)std::min<uint32_t>(255, smem_conflict_degree(lane.data(), in.mask, in.width ? in.width : 4, c, ws));
+          in.width = (uint8_t)std::min<uint32_t>(
+              255, smem_conflict_degree(lane.data(), in.mask, in.width ? in.width : 4, c, ws, lds_groups(c, in.opcode, ws)));
         }
         in.mem = kNoMem;
         break;

@@ -158,6 +158,8 @@ struct SimCfg {
   uint32_t smem_latency;
   uint32_t smem_warp_parts;
   uint32_t smem_limited_bcast;
+  uint32_t smem_cdna_groups;  // wave64 LDS banking by the CDNA4 per-instruction lane groups (trace.cc lds_groups)
+  uint32_t smem_pad_;
   CacheGeom l1;
   uint32_t l1_latency;
   uint32_t l1_banks;

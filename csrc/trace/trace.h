@@ -154,6 +154,19 @@ ReadyKernel ingest_kernel(const HostKernel& k, const SimCfg& c, int device = -1,
 int gpu_current_device();  // the calling thread's HIP device (-1: none / CPU-only build)
 
 // shared-memory bank-conflict degree of one warp access
-uint32_t smem_conflict_degree(const uint64_t* addr, uint64_t mask, uint32_t width, const SimCfg& c, uint32_t warp_size);
+// CDNA4 LDS banking of one ds_* instruction: its lane groups (one LDS cycle
+// each) and bank count
+struct LdsGroups {
+  uint32_t n;          // lane groups (<= 8)
+  uint32_t nb;         // banks: 32 or 64
+  uint64_t lanes[8];   // lanes of each group
+};
+const LdsGroups* lds_groups_for(const std::string& lower_case_opcode);
+// the groups of `opcode` with -gpgpu_shmem_cdna_lane_groups on a wave64 trace, else nullptr
+const LdsGroups* lds_groups(const SimCfg& c, uint16_t opcode, uint32_t warp_size);
+// groups == nullptr: the GPGPU-Sim model (-gpgpu_shmem_warp_parts, banks,
+// limited broadcast); else 1 + the CDNA4 extra cycles over the groups
+uint32_t smem_conflict_degree(const uint64_t* addr, uint64_t mask, uint32_t width, const SimCfg& c, uint32_t warp_size,
+                              const LdsGroups* groups = nullptr);
 
 }  // namespace asim
