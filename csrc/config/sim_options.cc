@@ -176,6 +176,8 @@ const OptDef kOptions[] = {
     {"-trace_prefetch", 'b', "1", "parse + coalesce the next kernel's trace on a host thread while the engine runs"},
     {"-gpu_ingest", 'b', "1",
      "with -sim_engine gpu: coalesce kernel traces (shared-memory bank conflicts, global line/sector lists) on the MI355X matrix cores"},
+    {"-gpu_ingest_min_insts", 'u', "32768",
+     "-gpu_ingest: kernels with fewer memory instructions are coalesced on the host (the device round trips cost more)"},
     {"-gpgpu_kernel_launch_latency", 'i', "0", "kernel launch latency (cycles)"},
     {"-gpgpu_kernel_launch_latency_queued", 'i', "-1",
      "launch latency of a kernel queued right behind the previous one (no memcpy / sync between); -1 = as -gpgpu_kernel_launch_latency"},
@@ -1079,6 +1081,7 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.max_concurrent_kernel = (int32_t)r.geti("-gpgpu_max_concurrent_kernel");
   d.trace_prefetch = r.getb("-trace_prefetch");
   d.gpu_ingest = r.getb("-gpu_ingest");
+  d.gpu_ingest_min = (uint64_t)r.getu("-gpu_ingest_min_insts");
   d.power_enabled = r.getb("-power_simulation_enabled");
   d.power_xml = r.gets("-accelwattch_xml_file");
   {

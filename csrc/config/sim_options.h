@@ -103,6 +103,7 @@ struct DriverOpts {
   int32_t trace_sampling_core = 0;
   uint32_t sim_epochs_per_launch = 4096;
   bool gpu_ingest = true;      // -gpu_ingest: coalesce traces on the GPU engine's device
+  uint64_t gpu_ingest_min = 32768;  // -gpu_ingest_min_insts: smaller kernels stay on the host
   bool trace_prefetch = true;  // -trace_prefetch: parse the next kernel while this one simulates
 };
 DriverOpts derive_driver_opts(const OptionRegistry& r);

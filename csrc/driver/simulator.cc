@@ -454,7 +454,14 @@ std::unique_ptr<ReadyKernel> Simulator::take_kernel(size_t idx) {
 }
 
 std::unique_ptr<ReadyKernel> Simulator::ingest(const HostKernel& k) {
-  if (ingest_dev_ < 0) return std::unique_ptr<ReadyKernel>(new ReadyKernel(coalesce_kernel(k, cfg_)));
+  if (ingest_dev_ < 0 || k.mems.size() < dopt_.gpu_ingest_min) {
+    std::unique_ptr<ReadyKernel> r(new ReadyKernel(coalesce_kernel(k, cfg_)));
+    if (ingest_dev_ >= 0) {
+      std::lock_guard<std::mutex> g(ingest_mu_);
+      ++ingest_small_;
+    }
+    return r;
+  }
   IngestStats st;
   std::unique_ptr<ReadyKernel> r(new ReadyKernel(ingest_kernel(k, cfg_, ingest_dev_, &st)));
   std::lock_guard<std::mutex> g(ingest_mu_);
@@ -1365,10 +1372,11 @@ void Simulator::print_sim_time() {
   if (ingest_dev_ >= 0) {
     std::lock_guard<std::mutex> g(ingest_mu_);
     print("gpu_ingest: shared %llu on device (%llu host), global %llu on device (%llu host), %llu mfma, "
-          "device %.3f s of %.3f s\n",
+          "device %.3f s of %.3f s, %llu small kernels on the host\n",
           (unsigned long long)ingest_st_.smem_jobs, (unsigned long long)ingest_st_.smem_host,
           (unsigned long long)ingest_st_.gmem_jobs, (unsigned long long)ingest_st_.gmem_host,
-          (unsigned long long)ingest_st_.mfma, ingest_st_.device_s, ingest_st_.total_s);
+          (unsigned long long)ingest_st_.mfma, ingest_st_.device_s, ingest_st_.total_s,
+          (unsigned long long)ingest_small_);
   }
   fflush(stdout);
 }

@@ -145,6 +145,7 @@ class Simulator {
   int ingest_dev_ = -1;
   std::mutex ingest_mu_;
   IngestStats ingest_st_;
+  uint64_t ingest_small_ = 0;  // kernels below -gpu_ingest_min_insts
   std::unique_ptr<ReadyKernel> ingest(const HostKernel& k);
   std::map<size_t, std::future<std::unique_ptr<ReadyKernel>>> pf_;
   void print_kernel_stats(const KernelResult& r, const std::vector<SMStats>& sm, const std::vector<MemStats>& mem);

@@ -1222,9 +1222,11 @@ uint32_t coalesce_lanes(const uint64_t* lane, uint64_t mask, uint32_t width, uin
   const auto* L = wide ? big_l.data() : lines;
   const auto* B = wide ? big_b.data() : bytes;
   const uint32_t n_all = wide ? (uint32_t)big_l.size() : nl;
-  std::vector<uint32_t> ord(n_all);
+  uint32_t ord_s[64 * 8];
+  std::vector<uint32_t> ord_v(wide ? n_all : 0);
+  uint32_t* ord = wide ? ord_v.data() : ord_s;
   for (uint32_t i = 0; i < n_all; ++i) ord[i] = i;
-  std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return L[x].first < L[y].first; });
+  std::sort(ord, ord + n_all, [&](uint32_t x, uint32_t y) { return L[x].first < L[y].first; });
   uint32_t n = 0;
   for (uint32_t oi = 0; oi < n_all && n < (uint32_t)kMaxAccess; ++oi) {
     const uint32_t i = ord[oi];

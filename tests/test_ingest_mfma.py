@@ -154,7 +154,7 @@ def test_simulation_with_device_ingest_equals_cpu(gpu_native, tmp_path):
     from accel_sim_framework_distributed_amd import sim
     from accel_sim_framework_distributed_amd.tracegen import rodinia
     kl = rodinia.write_app(str(tmp_path / "lud"), rodinia.lud(n=64))
-    g = sim.simulate(kl, "QV100", engine="gpu", extra={"-gpu_ingest": "1"})
+    g = sim.simulate(kl, "QV100", engine="gpu", extra={"-gpu_ingest": "1", "-gpu_ingest_min_insts": "0"})
     c = sim.simulate(kl, "QV100", engine="cpu")
     assert (g.tot_insn, g.tot_cycle) == (c.tot_insn, c.tot_cycle)
     assert "gpu_ingest: shared" in g.output
