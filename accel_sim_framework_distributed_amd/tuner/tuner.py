@@ -109,6 +109,15 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
             notes.append(f"-sim_mall_miss_latency = HBM over MALL {hbm:.0f} - modelled DRAM service {svc:.0f} cycles")
         except (KeyError, ValueError, IndexError):
             pass
+    # '# suggest_<option> <value>' lines of the micro-benchmarks (ub_kernel_lat_tb,
+    # ub_copy_engine, ub_regfile, ...) set simulator options an explicit
+    # option line did not already set
+    from .. import _native
+    known = set(_native.load().option_names())
+    for k, v in sorted(meas.items()):
+        if k.startswith("suggest_") and ("-" + k[len("suggest_"):]) in known and ("-" + k[len("suggest_"):]) not in opts:
+            opts["-" + k[len("suggest_"):]] = v
+            notes.append(f"-{k[len('suggest_'):]} {v} from a micro-benchmark's suggestion")
     for key, pol in _write_policies(meas).items():
         cur = opts.get(key, cfg.get(key))
         if cur:
