@@ -174,6 +174,8 @@ struct SimCfg {
   CacheGeom il1;
   uint32_t perfect_icache;
   uint32_t inst_prefetch;   // L1I sequential prefetch depth in lines (CDNA SQC fetches ahead)
+  uint32_t ifetch_block;    // > 0: a warp probes the L1I only when its fetch enters a new block of this many bytes
+  uint32_t ifetch_pad_;
   // ---- interconnect ----
   uint32_t icnt_latency;   // core cycles (== epoch length, the PDES lookahead)
   uint32_t flit_size;

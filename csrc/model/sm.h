@@ -683,12 +683,17 @@ SIM_HDI bool il1_fetch(S& s, const SimCfg& c, const KernelTab& kt, uint32_t w) {
   const CacheGeom& g = c.il1;
   const uint32_t pc = P::uni(s.w_win[w][P::uni((uint32_t)s.w_next[w]) & (kWin - 1)].pc);
   const uint64_t line = (kProgramMemStart + pc) & ~127ull;
+  // fetch-block mode: w_iline holds the block the warp's last fetch read
+  // (tagged with bit 0; a WF_IMISS warp's code line has it clear)
+  const uint64_t blk = c.ifetch_block ? (((kProgramMemStart + pc) & ~(uint64_t)(c.ifetch_block - 1)) | 1ull) : 0;
+  if (blk && P::uni((uint64_t)s.w_iline[w]) == blk) return true;
   const uint32_t set = cache_set_index(g, line);
   const int way = il1_find<P>(s, g, set, line);
   if (way >= 0) {
     if (g.repl == REPL_LRU) s.il1[set * g.assoc + way].lru = ++s.l1_stamp;
     s.sadd(SK(il1) + (IL1_HIT), 1);
     if (c.inst_prefetch && ((kProgramMemStart + pc) & 127u) < 8u) il1_prefetch<P>(s, c, line);  // entering a line
+    if (blk) s.w_iline[w] = blk;
     return true;
   }
   int mi = P::find_first((int)g.mshr_entries, [&](int i) -> bool { return s.imshr[i].valid && s.imshr[i].line == line; });
@@ -1689,6 +1694,7 @@ SIM_HDI void sm_launch_cta(S& s, const SmCtx& x, uint32_t slot, uint32_t cta_id,
     s.w_issue_ok[w] = 0;
     s.w_age[w] = age0 + (uint32_t)i;
     s.w_flags[w] = WF_ACTIVE;
+    s.w_iline[w] = 0;  // no code block fetched yet
     s.w_ibuf[w] = 0;
     s.w_cta[w] = (uint8_t)slot;
     s.w_inflight[w] = 0;
