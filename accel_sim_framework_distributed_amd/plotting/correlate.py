@@ -123,9 +123,14 @@ def _ipc(d):
     return d[S_WINSN] / d[S_CYC] if d.get(S_CYC) else float("nan")
 
 
+S_L1_LK64 = r"\s+L1D_total_64B_tag_lookups\s*=\s*(.*)"
+
+
 def _l1_hit_rate(d):
-    tot = d[S_L1 % ("GLOBAL_ACC_R", "TOTAL_ACCESS")]
-    return d[S_L1 % ("GLOBAL_ACC_R", "HIT")] / tot if tot else float("nan")
+    # as the hardware ratio 1 - TCP_TCC_READ_REQ / TCP_TOTAL_CACHE_ACCESSES:
+    # read requests the L1 sends over its 64 B tag lookups
+    tot = d.get(S_L1_LK64) or 0.0
+    return 1.0 - d[S_L1 % ("GLOBAL_ACC_R", "MISS")] / tot if tot else float("nan")
 
 
 def _l2_hit_rate(d):
@@ -183,9 +188,10 @@ CORREL_STATS: List[CorrelStat] = [
     CorrelStat("MFMA instructions", r"gpgpu_n_tensor_insn\s*=\s*(.*)", _hw("SQ_INSTS_MFMA_sum"), "mfma"),
     CorrelStat("LDS bank conflict cycles", r"gpgpu_n_shmem_bkconflict\s*=\s*(.*)", _hw("SQ_LDS_BANK_CONFLICT_sum"),
                "lds-conflict"),
-    CorrelStat("L1 accesses", "l1_acc", _hw("TCP_TOTAL_CACHE_ACCESSES_sum"), "l1-acc",
-               sim_stats=(S_L1 % ("GLOBAL_ACC_R", "TOTAL_ACCESS"), S_L1 % ("GLOBAL_ACC_W", "TOTAL_ACCESS")),
-               sim_eval=lambda d: sum(d.values())),
+    # TCP tag lookups are 64 B: a wave64 dword access (256 B) is 4 of them
+    # (per-kernel TCP_TOTAL_CACHE_ACCESSES / VMEM instructions: 4.00 on
+    # lud_internal, 1.00 on the 16-lane lud_diagonal)
+    CorrelStat("L1 accesses", S_L1_LK64, _hw("TCP_TOTAL_CACHE_ACCESSES_sum"), "l1-acc"),
     CorrelStat("L1 read misses (L1->L2 reads)", S_L1 % ("GLOBAL_ACC_R", "MISS"), _hw("TCP_TCC_READ_REQ_sum"),
                "l1-read-miss"),
     # the write requests the L1 sends (a store may be split into 64 B
@@ -194,7 +200,7 @@ CORREL_STATS: List[CorrelStat] = [
                "l1-writes"),
     CorrelStat("L1 read hit rate", "l1_hit_rate",
                _hw_ratio(("TCP_TCC_READ_REQ_sum",), ("TCP_TOTAL_CACHE_ACCESSES_sum",), one_minus=True),
-               "l1-hit-rate", sim_stats=(S_L1 % ("GLOBAL_ACC_R", "HIT"), S_L1 % ("GLOBAL_ACC_R", "TOTAL_ACCESS")),
+               "l1-hit-rate", sim_stats=(S_L1 % ("GLOBAL_ACC_R", "MISS"), S_L1_LK64),
                sim_eval=_l1_hit_rate, ratio=True, log=False),
     CorrelStat("L2 read accesses", S_L2 % ("GLOBAL_ACC_R", "TOTAL_ACCESS"), _hw("TCC_READ_sum"), "l2-reads"),
     CorrelStat("L2 write accesses", S_L2 % ("GLOBAL_ACC_W", "TOTAL_ACCESS"), _hw("TCC_WRITE_sum"), "l2-writes"),

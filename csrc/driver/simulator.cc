@@ -1061,8 +1061,9 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
   // request status strings so get_stats.py regexes keep working)
   static const char* l1t[L1T_COUNT] = {"GLOBAL_ACC_R", "GLOBAL_ACC_W", "LOCAL_ACC_R", "LOCAL_ACC_W", "GLOBAL_ATOMIC"};
   uint64_t l1[L1T_COUNT][L1O_COUNT] = {};
-  uint64_t shm = 0, shm_conf = 0;
+  uint64_t shm = 0, shm_conf = 0, lk64 = 0;
   for (auto& s : csm) {
+    lk64 += s.l1_lookups64;
     for (int t = 0; t < L1T_COUNT; ++t)
       for (int o = 0; o < L1O_COUNT; ++o) l1[t][o] += s.l1[t][o];
     shm += s.shmem_acc;
@@ -1079,6 +1080,7 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
     print("\tTotal_core_cache_stats_breakdown[%s][MSHR_HIT] = %llu\n", l1t[t], (unsigned long long)l1[t][L1O_MSHR_HIT]);
     print("\tTotal_core_cache_stats_breakdown[%s][TOTAL_ACCESS] = %llu\n", l1t[t], (unsigned long long)tot);
   }
+  print("\tL1D_total_64B_tag_lookups = %llu\n", (unsigned long long)lk64);
   print("\nTotal_core_cache_fail_stats:\n");
   for (int t = 0; t < L1T_COUNT; ++t)
     print("\tTotal_core_cache_fail_stats_breakdown[%s][MSHR_ENRTY_FAIL] = %llu\n", l1t[t],

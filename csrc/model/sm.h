@@ -147,6 +147,9 @@ struct SMStats {
   uint64_t issue_distro[3 + kMaxWarpLanes];
   uint64_t single_issue[kMaxSched];  // scheduler cycles that issued one instruction
   uint64_t dual_issue[kMaxSched];    // ... two
+  // vector-L1 tag lookups at 64 B granularity (the 64 B halves of each
+  // coalesced 128 B line access): what TCP_TOTAL_CACHE_ACCESSES counts
+  uint64_t l1_lookups64;
 };
 enum IL1Out : uint8_t { IL1_HIT = 0, IL1_MISS, IL1_MSHR_HIT, IL1_RES_FAIL };
 // Instruction classes of the CDNA sequencer's counters (rocprofv3
@@ -1038,6 +1041,8 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
         if (pi == s.n_pend) s.n_pend++;
       }
     }
+    if (in.space != S_CONST)
+      s.sadd(SK(l1_lookups64), (uint32_t)((a.sectors & 3u) != 0) + (uint32_t)((a.sectors & 12u) != 0));
     banks_used |= bbit;
     unext++;
     u.next = (uint8_t)unext;
