@@ -361,6 +361,13 @@ bool gpu_coalesce_kernel(const HostKernel& k, const SimCfg& c, int device, Ready
   const auto t0 = std::chrono::steady_clock::now();
   int cur = -1;
   IHIPCHECK(hipGetDevice(&cur));
+  // the calling thread's device is restored however this returns
+  struct DeviceGuard {
+    int prev, now;
+    ~DeviceGuard() {
+      if (prev != now) (void)hipSetDevice(prev);
+    }
+  } guard{cur, device};
   if (cur != device) IHIPCHECK(hipSetDevice(device));
   const uint32_t ws = k.h.warp_size ? k.h.warp_size : 32;
   if (ws > 64) return false;
@@ -495,7 +502,6 @@ bool gpu_coalesce_kernel(const HostKernel& k, const SimCfg& c, int device, Ready
         break;
     }
   }
-  if (cur != device) IHIPCHECK(hipSetDevice(cur));
   const auto t1 = std::chrono::steady_clock::now();
   if (st) {
     st->smem_jobs += loc.smem_jobs;
