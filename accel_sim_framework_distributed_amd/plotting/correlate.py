@@ -220,8 +220,15 @@ CORREL_STATS: List[CorrelStat] = [
                "dram-reads"),
     CorrelStat("L2->fabric write requests", r"L2_to_mem_write_requests\s*=\s*(.*)", _hw("TCC_EA0_WRREQ_sum"),
                "dram-writes"),
-    CorrelStat("Interconnect packets SM->memory", r"icnt_total_pkts_simt_to_mem\s*=\s*(.*)",
-               _hw("TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum", "TCP_TCC_ATOMIC_WITH_RET_REQ_sum"), "icnt-pkts"),
+    # the vector L1's requests to the L2 (the TCP->TCC counters), from the
+    # matching simulator counters: icnt_total_pkts_simt_to_mem also carries
+    # the instruction-fetch and scalar-cache traffic, which on CDNA leaves
+    # the CU through the SQC, not the TCP
+    CorrelStat("Interconnect packets SM->memory", "l1_to_l2_reqs",
+               _hw("TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum", "TCP_TCC_ATOMIC_WITH_RET_REQ_sum"), "icnt-pkts",
+               sim_stats=(S_L1 % ("GLOBAL_ACC_R", "MISS"), S_L2 % ("GLOBAL_ACC_W", "TOTAL_ACCESS"),
+                          S_L2 % ("GLOBAL_ATOMIC", "TOTAL_ACCESS")),
+               sim_eval=lambda d: sum(d.values())),
     # ---- round 3: instruction mix by the sequencer's own classes (the
     # simulator classifies each issued instruction like SQ_INSTS_*, see
     # csrc/model/sm.h sq_class / isatrace/verify.py classify) ----
