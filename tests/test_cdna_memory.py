@@ -204,3 +204,30 @@ def test_xcd_round_robin_cta_dispatch_and_64b_stores(native, tmp_path):
     assert one.tot_insn == two.tot_insn
     with pytest.raises(Exception, match="sim_xcd"):
         native.parse_config(presets.args_for("QV100", {"-sim_xcd": "32", "-gpgpu_n_clusters": "8"}))
+
+
+def test_l1_64b_tag_lookups(native, tmp_path):
+    # one 128 B line per warp load, both 64 B halves: two TCP-style lookups
+    kl = _app(tmp_path, "lk")
+    s = _run(native, kl, {})
+    warps = 64 * 4
+    assert _stat(s.output, "L1D_total_64B_tag_lookups") == warps * LOADS * 2
+
+
+def test_instruction_fetch_blocks(native, tmp_path):
+    # 16-byte trace instructions: a 64 B fetch block holds four, so the L1I is
+    # read once per block a warp enters (9 instructions = 3 blocks, plus the
+    # re-reads after a miss) instead of once per two-instruction fetch; hits
+    # cost nothing, so the timing is unchanged
+    kl = _app(tmp_path, "ifb")
+    base = {"-gpgpu_perfect_inst_const_cache": "0"}
+    probe = _run(native, kl, base)
+    blk = _run(native, kl, dict(base, **{"-gpgpu_inst_fetch_block_bytes": "64"}))
+    a0, a1 = _stat(probe.output, "L1I_total_cache_accesses"), _stat(blk.output, "L1I_total_cache_accesses")
+    assert a0 > 0 and a1 > 0
+    warps = 64 * 4
+    assert warps * 3 <= a1 < a0
+    assert _stat(blk.output, "L1I_total_cache_misses") == _stat(probe.output, "L1I_total_cache_misses")
+    assert blk.tot_cycle == probe.tot_cycle
+    with pytest.raises(Exception, match="power of two"):
+        native.parse_config(presets.args_for("QV100", {"-gpgpu_inst_fetch_block_bytes": "48"}))
