@@ -84,6 +84,8 @@ CDNA = {
     "global_store_dwordx4": ("STORE", "GLOBAL", FLAG["MEM"], 16),
     "global_atomic_add": ("LOAD", "GLOBAL", FLAG["MEM"] | FLAG["ATOMIC"] | FLAG["BYPASS_L1"], 4),
     "ds_read_b32": ("LOAD", "SHARED", FLAG["MEM"], 4), "ds_write_b32": ("STORE", "SHARED", FLAG["MEM"], 4),
+    "ds_read_b64": ("LOAD", "SHARED", FLAG["MEM"], 8), "ds_read_b128": ("LOAD", "SHARED", FLAG["MEM"], 16),
+    "ds_write_b64": ("STORE", "SHARED", FLAG["MEM"], 8), "ds_write_b128": ("STORE", "SHARED", FLAG["MEM"], 16),
 }
 
 

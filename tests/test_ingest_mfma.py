@@ -158,3 +158,46 @@ def test_simulation_with_device_ingest_equals_cpu(gpu_native, tmp_path):
     c = sim.simulate(kl, "QV100", engine="cpu")
     assert (g.tot_insn, g.tot_cycle) == (c.tot_insn, c.tot_cycle)
     assert "gpu_ingest: shared" in g.output
+
+
+def _lds_conflict_kernel():
+    """wave64: ds_read_b128 on 256 B rows (16-way in each of its four lane
+    groups: 60 extra cycles), ds_read_b32 at an 8 B stride (2-way in both
+    32-lane halves: 2), ds_write_b64 at 8 B (conflict-free in 16-lane groups)."""
+    import numpy as np
+    from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+    k = KernelBuilder("k_lds", (64, 1, 1), (256, 1, 1), nregs=32, binary_version=950, warp_size=64, shmem=65536)
+    w = k.g.warp.astype(np.int64) % 4 * 16384
+    k.op("ds_read_b128", [4], [2], base=w, stride=256)
+    k.op("ds_read_b32", [5], [2], base=w, stride=8)
+    k.op("ds_write_b64", [], [4], base=w, stride=8)
+    k.op("s_waitcnt", [], [])
+    k.op("s_endpgm")
+    return k.build()
+
+
+def _bkconflict(out):
+    import re
+    return int(re.findall(r"gpgpu_n_shmem_bkconflict = (\d+)", out)[-1])
+
+
+def test_cdna_lane_groups_in_simulation(tmp_path):
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    kl = rodinia.write_app(str(tmp_path / "lds"), [_lds_conflict_kernel()], memcpy=False)
+    c = sim.simulate(kl, "MI355X", engine="cpu")
+    assert _bkconflict(c.output) == 256 * (60 + 2)
+    off = sim.simulate(kl, "MI355X", engine="cpu", extra={"-gpgpu_shmem_cdna_lane_groups": "0"})
+    assert _bkconflict(off.output) != _bkconflict(c.output)
+
+
+@pytest.mark.gpu
+def test_cdna_lane_groups_gpu_equals_cpu(gpu_native, tmp_path):
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    kl = rodinia.write_app(str(tmp_path / "lds"), [_lds_conflict_kernel()], memcpy=False)
+    g = sim.simulate(kl, "MI355X", engine="gpu", extra={"-gpu_ingest_min_insts": "0"})
+    c = sim.simulate(kl, "MI355X", engine="cpu")
+    assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
+    assert _bkconflict(g.output) == _bkconflict(c.output) == 256 * (60 + 2)
+    assert "gpu_ingest: shared" in g.output
