@@ -27,7 +27,9 @@ assembled (``hipcc -S --cuda-device-only``):
   ``t & mask`` once the host has drained that slot's previous occupant
   (the slot's generation word reads ``t >> shift``; the wave polls it with
   system-scope loads, ``s_sleep`` between polls, and after ``SPIN_LIMIT``
-  polls gives up and stops recording rather than hang).  A wave leaving a
+  polls -- ``ctl.spin_limit``, set by the host -- gives up and stops
+  recording rather than hang; the host then refuses to write that kernel's
+  trace and fails the run: a capture is lossless or it is an error).  A wave leaving a
   full chunk writes a close marker into the chunk's last unit after its
   records have drained (``s_waitcnt vmcnt(0)``); the host's drain thread
   copies closed chunks out during the kernel and frees their slots, so no
@@ -375,7 +377,12 @@ class Probe:
                "s_waitcnt lgkmcnt(0)",
                f"s_lshr_b32 {self.t2}, {self.t}, {self.t2}",
                f"s_mul_i32 {self.cur}, {self.end}, {CHUNK_UNITS}",
-               f"s_mov_b32 {self.end}, {SPIN_LIMIT}",
+               # polls before giving up: the control block's limit (the host
+               # fails the run if any wave gave up), SPIN_LIMIT when unset
+               f"s_load_dword {self.end}, {self.ctl}, 0x18",
+               "s_waitcnt lgkmcnt(0)",
+               f"s_cmp_eq_u32 {self.end}, 0",
+               f"s_cselect_b32 {self.end}, {SPIN_LIMIT:#x}, {self.end}",
                f"s_mov_b64 {self.tx}, exec",
                "s_mov_b64 exec, 1",
                f"{L}_spin_{n}:",

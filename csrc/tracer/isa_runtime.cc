@@ -16,7 +16,9 @@
 // buffer -- the reference's device channel + receiver thread
 // (util/tracer_nvbit/nvbit_release/core/utils/channel.hpp:56-116,161-253).
 // ASIM_TRACE_BUF_MB selects the older one-device-buffer mode instead (faster
-// for small kernels; a kernel that outgrows it is reported and skipped).
+// for small kernels; a kernel that outgrows it fails the run).  A capture is
+// lossless or the traced program exits with status 5 (fail_run): no partial
+// kernel trace is ever written.
 // This runtime
 //  * interposes __hipRegisterFatBinary / __hipRegisterFunction to register
 //    the probes' control block (device global __asim_tctl) and learn kernel
@@ -27,8 +29,10 @@
 //  * writes kernel-N.traceg (format v4, wavefront size 64, binary version
 //    950), kernelslist.g (+ MemcpyHtoD lines from hipMemcpy) and stats.csv.
 // Environment: ASIM_TRACE_DIR (enables tracing), ASIM_TRACE_KERNEL_START/END
-// (1-based launch range), ASIM_TRACE_RING_MB (host ring, default 256, rounded
-// down to a power-of-two number of chunks), ASIM_TRACE_BUF_MB (device-buffer
+// (1-based launch range), ASIM_TRACE_RING_MB / _KB (host ring, default 256 MB,
+// rounded down to a power-of-two number of chunks), ASIM_TRACE_SPIN_LIMIT
+// (slot polls before a waiting wave gives up: the run then fails, status 5,
+// and no partial trace is written), ASIM_TRACE_DRAIN_DELAY_US (test hook), ASIM_TRACE_BUF_MB (device-buffer
 // mode instead of the ring), ASIM_ISA_MAP (map path, default <exe>.asimisa),
 // ASIM_TRACE_GPU_ID / GPU_TRACE_ID (trace only the launches on that HIP
 // device, files kernel-<id>_<gpu>.traceg: the reference's per-device filter
@@ -72,7 +76,8 @@ struct Ctl {  // must match the probes (isatrace/rewrite.py)
   uint32_t n_chunks;    // @12 device-buffer mode: chunks in the buffer
   uint32_t mask;        // @16 ring mode: slots - 1 (0 = device-buffer mode)
   uint32_t shift;       // @20 ring mode: log2(slots)
-  uint64_t pad;
+  uint32_t spin_limit;  // @24 ring mode: slot polls before a wave gives up (0: the probes' default)
+  uint32_t pad;
 };
 static_assert(sizeof(Ctl) == 32, "control block layout");
 
@@ -105,6 +110,10 @@ struct Tracer {
   long next_id = 0;
   size_t buf_bytes = 0;           // device-buffer mode when set
   size_t ring_bytes = 256ull << 20;
+  // slot polls (each ~1 us: a system-scope load + s_sleep) before a waiting
+  // wave gives up; it exists only so a stalled host cannot hang the GPU
+  uint32_t spin_limit = 1u << 22;
+  uint32_t drain_delay_us = 0;  // test hook: slow the drain thread down
   struct Ring {
     uint8_t* host = nullptr;  // coherent host memory
     uint8_t* dev = nullptr;   // the same memory as the GPU addresses it
@@ -153,6 +162,9 @@ struct Tracer {
     if (const char* s = getenv("ASIM_TRACE_KERNEL_END")) kend = atol(s);
     if (const char* s = getenv("ASIM_TRACE_BUF_MB")) buf_bytes = (size_t)atol(s) << 20;
     if (const char* s = getenv("ASIM_TRACE_RING_MB")) ring_bytes = (size_t)atol(s) << 20;
+    if (const char* s = getenv("ASIM_TRACE_RING_KB")) ring_bytes = (size_t)atol(s) << 10;
+    if (const char* s = getenv("ASIM_TRACE_SPIN_LIMIT")) spin_limit = (uint32_t)std::max(1L, atol(s));
+    if (const char* s = getenv("ASIM_TRACE_DRAIN_DELAY_US")) drain_delay_us = (uint32_t)atol(s);
     std::string mp;
     if (const char* s = getenv("ASIM_ISA_MAP")) {
       mp = s;
@@ -418,11 +430,24 @@ void drain_final(const Tracer::Ring& r, uint32_t tickets, Spill& sp) {
   }
 }
 
+// A kernel's trace could not be captured whole: the capture is unusable, so
+// the traced program ends here with a distinct exit status (5) instead of
+// leaving a directory whose kernelslist names a partial trace.
+[[noreturn]] void fail_run(Tracer& t) {
+  FILE* f = fopen((t.dir + "/CAPTURE_FAILED").c_str(), "w");
+  if (f) {
+    fprintf(f, "trace chunks were lost; this directory is not a complete capture\n");
+    fclose(f);
+  }
+  fflush(stderr);
+  _exit(5);
+}
+
 Tracer::Ring& ring_for(Tracer& t, int dev) {
   Tracer::Ring& r = t.rings[dev];
   if (r.host) return r;
   const size_t cb = (size_t)kChunkUnits * 16;
-  r.slots = 64;
+  r.slots = 4;  // the probes need a power of two
   while ((size_t)r.slots * 2 * cb <= t.ring_bytes) r.slots *= 2;
   r.shift = (uint32_t)__builtin_ctz(r.slots);
   RT_HIP(hipHostMalloc((void**)&r.host, (size_t)r.slots * cb, hipHostMallocCoherent | hipHostMallocMapped));
@@ -451,6 +476,7 @@ hipError_t launch_streamed(Tracer& t, long id, const std::string& name, const KM
   c.n_chunks = r.slots;
   c.mask = r.slots - 1;
   c.shift = r.shift;
+  c.spin_limit = t.spin_limit;
   for (Ctl* sh : t.shadows) RT_HIP(hipMemcpyToSymbol((const void*)sh, &c, sizeof(c), 0, hipMemcpyHostToDevice));
   const std::string spath = t.dir + "/.kernel-" + std::to_string(id) + ".chunks";
   Spill sp;
@@ -467,8 +493,10 @@ hipError_t launch_streamed(Tracer& t, long id, const std::string& name, const KM
   }
   std::atomic<bool> stop{false};
   std::thread drain([&] {
-    while (!stop.load(std::memory_order_relaxed))
+    while (!stop.load(std::memory_order_relaxed)) {
+      if (t.drain_delay_us) std::this_thread::sleep_for(std::chrono::microseconds(t.drain_delay_us));
       if (!drain_closed(r, sp)) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
   });
   const hipError_t se = hipStreamSynchronize(st);
   stop = true;
@@ -476,11 +504,20 @@ hipError_t launch_streamed(Tracer& t, long id, const std::string& name, const KM
   RT_HIP(se);
   const uint32_t tickets = tickets_issued(t);
   drain_final(r, tickets, sp);
-  if (tickets > sp.chunks)
+  if (tickets > sp.chunks) {
+    // a wave gave up waiting for a ring slot and stopped recording: the
+    // trace would be silently truncated, so none is written and the run fails
+    // (the reference's channel blocks its producers instead, channel.hpp:56-116;
+    // here the wait is bounded so a stalled host cannot hang the GPU)
     fprintf(stderr,
-            "asim isa tracer: kernel %ld (%s): %u of %u chunks dropped (a wave waited too long for a ring slot); "
-            "raise ASIM_TRACE_RING_MB\n",
-            id, name.c_str(), tickets - sp.chunks, tickets);
+            "asim isa tracer: FATAL: kernel %ld (%s): %u of %u trace chunks lost (a wave waited longer than "
+            "ASIM_TRACE_SPIN_LIMIT=%u polls for a ring slot); no trace written for it. Raise ASIM_TRACE_RING_MB "
+            "or ASIM_TRACE_SPIN_LIMIT\n",
+            id, name.c_str(), tickets - sp.chunks, tickets, t.spin_limit);
+    fclose(sp.f);
+    unlink(spath.c_str());
+    fail_run(t);
+  }
   fflush(sp.f);
   const size_t bytes = (size_t)sp.chunks * kChunkUnits * 16;
   const uint8_t* data = nullptr;
@@ -589,10 +626,10 @@ hipError_t hipLaunchKernel(const void* f, dim3 g, dim3 b, void** args, size_t sh
   if (used > c.n_chunks) {
     // the waves past the end stopped recording: no usable trace of this kernel
     fprintf(stderr,
-            "asim isa tracer: kernel %ld (%s) needs %u chunks of %u KB, the device buffer holds %u: not written "
-            "(unset ASIM_TRACE_BUF_MB to stream through the host ring)\n",
+            "asim isa tracer: FATAL: kernel %ld (%s) needs %u chunks of %u KB, the device buffer holds %u: no trace "
+            "written (unset ASIM_TRACE_BUF_MB to stream through the host ring)\n",
             id, name.c_str(), used, kChunkUnits / 64, c.n_chunks);
-    return e;
+    fail_run(t);
   }
   std::vector<uint8_t> host((size_t)used * kChunkUnits * 16);
   // the tracer's own read-back is not an application copy (no trace line)

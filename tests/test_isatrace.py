@@ -103,6 +103,17 @@ def test_instrumented_asm_keeps_program_and_reserves_registers():
     assert "0 1 2 v2 v3 ds_read2_b32 1 v4 4" in m
 
 
+def test_probe_spin_limit_comes_from_the_control_block():
+    """A wave waiting for a ring slot polls at most ctl.spin_limit times (the
+    host sets it; the compiled default only when it is 0), then stops
+    recording -- which the host turns into a failed capture."""
+    new, _ = rewrite.instrument(_ASM)
+    blk = new[new.index("_take_"):new.index("_got_")]
+    assert ", 0x18" in blk and "s_load_dword" in blk
+    assert "s_cselect_b32" in blk
+    assert f"{rewrite.SPIN_LIMIT:#x}" in blk
+
+
 def test_verify_classes_and_trace_counts(tmp_path):
     assert verify.classify("v_mfma_f32_32x32x16_bf16") == "VALU"
     assert verify.classify("s_load_dwordx2") == "SMEM"
@@ -194,6 +205,34 @@ def test_isatrace_ring_streams_a_trace_larger_than_the_ring(tmp_path):
     from accel_sim_framework_distributed_amd import sim
     s = sim.simulate(str(ring / "kernelslist.g"), "MI355X", engine="gpu")
     assert s.stats["gpgpu_n_tot_w_icount"] == sum(v for k, v in c.items() if k != "WAVES")
+
+
+@pytest.mark.gpu
+def test_isatrace_tiny_ring_is_lossless_or_fails(tmp_path):
+    """Four 8 KB ring slots for 1024 waves: with a prompt drain the capture
+    completes and equals the device-buffer capture; with the drain stalled
+    (test hook) and a short poll budget, waves give up and the run fails with
+    status 5 -- no kernel trace is written, the directory is marked
+    CAPTURE_FAILED (never a silently truncated trace)."""
+    exe = os.path.join(ROOT, "bin", "isatrace", "vectoradd")
+    assert os.path.exists(exe), "build_native.py builds bin/isatrace/*"
+    n = 1 << 16
+    env = {k: v for k, v in os.environ.items() if not k.startswith("ASIM_TRACE")}
+    ok, whole, bad = tmp_path / "ok", tmp_path / "whole", tmp_path / "bad"
+    r = subprocess.run([exe, str(n)], env=dict(env, ASIM_TRACE_DIR=str(ok), ASIM_TRACE_RING_KB="32"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stderr
+    r = subprocess.run([exe, str(n)], env=dict(env, ASIM_TRACE_DIR=str(whole), ASIM_TRACE_BUF_MB="64"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert _trace_body(ok / "kernel-1.traceg") == _trace_body(whole / "kernel-1.traceg")
+    assert verify.trace_counts(str(ok / "kernel-1.traceg"))["WAVES"] == n // 64
+    r = subprocess.run([exe, str(n)], env=dict(env, ASIM_TRACE_DIR=str(bad), ASIM_TRACE_RING_KB="32",
+                                                ASIM_TRACE_DRAIN_DELAY_US="300000", ASIM_TRACE_SPIN_LIMIT="32"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 5, (r.returncode, r.stderr)
+    assert "FATAL" in r.stderr and (bad / "CAPTURE_FAILED").exists()
+    assert not [p for p in os.listdir(bad) if p.endswith(".traceg") or p.endswith(".chunks")]
 
 
 @pytest.mark.gpu
