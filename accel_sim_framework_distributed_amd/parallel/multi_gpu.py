@@ -292,7 +292,10 @@ class DistributedSuite:
         clock to the others' mid-step (packet link model over RCCL).
         Uncoupled (calibration), the simulator emulates all ranks locally."""
         self._bind_device()
-        extra = {"-collective_model": self.collective_model, "-gpgpu_concurrent_kernel_sm": "1"}
+        # the all-reduces' buffer traffic (RCCL-style copy kernels) runs through
+        # the simulated L2 / HBM and contends with the backward kernels
+        extra = {"-collective_model": self.collective_model, "-gpgpu_concurrent_kernel_sm": "1",
+                 "-collective_mem_traffic": "1"}
         eng = engine or ("gpu" if self.engine == "node" else self.engine)
         s = self.mod.Simulator(build_args(self.config, self.dp_step, eng, extra), self.verbose)
         n0 = len(getattr(self.sync, "events", []))
@@ -330,8 +333,18 @@ class DistributedSuite:
         # compete with the suite for the CU pool.)
         if self.allreduce and not self.dp_step:
             results.append(self._run_allreduce())
+        insn_gpu = 0
         for app, i, c in results:
             insn += i
             cycles += c
-            per_app[app] = dict(insn=i, cycles=c, wall_s=self.weights.get(app, 0.0))
-        return dict(insn=insn, cycles=cycles, apps=per_app)
+            eng = self.engine_of(app)
+            if eng == "gpu":
+                insn_gpu += i
+            per_app[app] = dict(insn=i, cycles=c, wall_s=self.weights.get(app, 0.0), engine=eng)
+        return dict(insn=insn, cycles=cycles, insn_gpu=insn_gpu, apps=per_app)
+
+    def engine_of(self, app: str) -> str:
+        """The engine that simulated `app` in the last step."""
+        if self.engine == "node":
+            return self.assignment.get(app, "cpu") if app != "all-reduce" else "gpu"
+        return self.engine

@@ -80,8 +80,9 @@ def _cfg_desc(name: str) -> str:
 
 
 def _resolve_app(rodinia, name: str) -> str:
-    """Full suite name for `name` ("nw" -> "nw-rodinia-2.0-ft"); unknown names fail."""
-    if name in rodinia.SUITE:
+    """Full suite name for `name` ("nw" -> "nw-rodinia-2.0-ft"); unknown names fail.
+    "dp-step" selects the data-parallel training step."""
+    if name in rodinia.SUITE or name == "dp-step":
         return name
     hit = [k for k in rodinia.SUITE if k.split("-rodinia")[0] == name]
     if not hit:
@@ -172,25 +173,41 @@ def main() -> int:
     sync()
     t0 = time.perf_counter()
     insn = 0
+    insn_gpu = 0
     cycles = 0
     for _ in range(a.steps):
         r = suite.step()
         insn += r["insn"]
+        insn_gpu += r["insn_gpu"]
         cycles += r["cycles"]
     sync()
     dt = time.perf_counter() - t0
     # max wall time over ranks, total instructions over ranks; the DDP step's
     # simulated cycles: max over ranks (the step ends with the slowest rank)
     dpl = suite.dp_last or {}
-    t = torch.tensor([dt, float(insn), float(cycles), float(dpl.get("cycles", 0))], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt, float(insn), float(cycles), float(dpl.get("cycles", 0)), float(insn_gpu)],
+                     dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         dt, insn_all, cyc_all, dp_max = float(tmax[0]), float(tsum[1]), float(tsum[2]), float(tmax[3])
+        gpu_all = float(tsum[4])
+        # every rank's GPU-engine share (all_gather: the bench prints per-rank values)
+        g = torch.zeros(world, dtype=torch.float64, device=dev)
+        g[rank] = float(insn_gpu) / max(dt, 1e-9) / 1e3
+        dist.all_reduce(g, op=dist.ReduceOp.SUM)
+        gpu_per_rank = [round(float(x), 1) for x in g.cpu()]
+        dc = torch.zeros(world, dtype=torch.float64, device=dev)
+        dc[rank] = float(dpl.get("cycles", 0))
+        dist.all_reduce(dc, op=dist.ReduceOp.SUM)
+        dp_cycles_per_rank = [int(x) for x in dc.cpu()]
     else:
         insn_all, cyc_all, dp_max = float(insn), float(cycles), float(dpl.get("cycles", 0))
+        gpu_all = float(insn_gpu)
+        gpu_per_rank = [round(gpu_all / dt / 1e3, 1)]
+        dp_cycles_per_rank = [int(dpl.get("cycles", 0))]
     kips = insn_all / dt / 1e3
     if rank == 0:
         out = {
@@ -225,8 +242,19 @@ def main() -> int:
                 "sim_insn_per_step_per_rank": int(insn / max(1, a.steps)),
                 "sim_cycles_per_step_per_rank": int(cycles / max(1, a.steps)),
             },
+            # the part of the headline simulated by the HIP cycle engine on the
+            # MI355X(s): thread instructions of the applications the GPU engine
+            # ran, over the same wall time (the rest ran on host cores)
+            "gpu_engine": {"kips_whole_node": round(gpu_all / dt / 1e3, 1),
+                           "kips_per_rank": gpu_per_rank,
+                           "insn_share": round(gpu_all / max(insn_all, 1.0), 4),
+                           "apps_on_gpu": (sum(1 for v in suite.assignment.values() if v == "gpu")
+                                           if engine == "node" else (len(suite.apps) if engine == "gpu" else 0)),
+                           "apps": len(suite.apps)},
             "cycle_mae_vs_hw": _cycle_mae(),
             "dp_step": ({"ranks": world, "simulated_cycles_max_rank": int(dp_max),
+                         "simulated_cycles_per_rank": dp_cycles_per_rank,
+                         "collective_mem_traffic": True,
                          "rank0_kernels": dpl.get("kernels"), "rank0_collectives": dpl.get("collectives"),
                          "rank0_comm_cycles": dpl.get("comm_cycles"),
                          "collective_coupling": dpl.get("modes"),

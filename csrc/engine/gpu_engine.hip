@@ -44,9 +44,21 @@ namespace asim {
       throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x);    \
   } while (0)
 
+// The configuration of every running simulation lives in constant memory
+// (one slot per engine instance of the process, GpuArgs::cfg_slot).  Read
+// through address space 4, every wave-uniform access is a scalar load the
+// compiler may hoist and CSE freely (constant memory is never written by a
+// kernel), so configuration-derived values stay in SGPRs and their
+// arithmetic is SALU; only lane-indexed reads become vector loads.  From an
+// LDS copy (the alternative kernel, kCfgLds) each read after any state store
+// must be re-issued (the compiler cannot rule out aliasing with the state in
+// LDS) and lands in a VGPR.
+constexpr int kCfgSlots = 64;
+__constant__ SimCfg g_cfg[kCfgSlots];
+
 struct GpuArgs {
-  SimCfg cfg;          // by value: kernel-argument (constant) memory, read with scalar loads
-  const SimCfg* __restrict__ cfg_g;  // device copy: read-only, uniform addresses -> scalar loads
+  uint32_t cfg_slot;                 // g_cfg slot of this engine
+  const SimCfg* __restrict__ cfg_g;  // device copy (the LDS-config kernel copies it in)
   const KernelTab* kt;               // running kernels (copied into LDS at launch)
   SMState* sms;
   ChanState* chs;
@@ -152,7 +164,7 @@ struct WaveParProf : WavePar {
   }
 };
 
-template <class P, bool kSliced>
+template <class P, bool kSliced, bool kCfgLds>
 __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   const uint32_t b = blockIdx.x;
   // The configuration is read all over the model, much of it at lane-varying
@@ -162,14 +174,14 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   // block copies the configuration into LDS once and reads it from there
   // (static global loads in this kernel 1031 -> 58; bfs engine time -3 %,
   // profiles/pmc_sq_engine_bfs_r2.json).
-  {
+  if (kCfgLds) {
     static_assert(sizeof(SimCfg) % 8 == 0, "SimCfg must be 8-byte granular");
     const uint2* src = reinterpret_cast<const uint2*>(a.cfg_g);
     uint2* dst = reinterpret_cast<uint2*>(g_lds + kCfgOff);
     for (int i = (int)(threadIdx.x & 63); i < (int)(sizeof(SimCfg) / 8); i += 64) dst[i] = src[i];
     __syncthreads();
   }
-  const SimCfg& c = *reinterpret_cast<const SimCfg*>(g_lds + kCfgOff);
+  const SimCfg& c = kCfgLds ? *reinterpret_cast<const SimCfg*>(g_lds + kCfgOff) : g_cfg[a.cfg_slot];
   const uint64_t E = c.icnt_latency;
   SMState* s = reinterpret_cast<SMState*>(g_lds);
   ChanState* ch = reinterpret_cast<ChanState*>(g_lds);
@@ -425,6 +437,33 @@ class CuPool {
   std::unique_ptr<DeviceCuTable> table_;
 };
 
+// constant-memory configuration slots (g_cfg) of the engines alive in this
+// process: simulations that run at once read their own slot
+class CfgSlots {
+ public:
+  static CfgSlots& get() {
+    static CfgSlots s;
+    return s;
+  }
+  int acquire() {
+    std::lock_guard<std::mutex> g(mu_);
+    for (int i = 0; i < kCfgSlots; ++i)
+      if (!(used_ >> i & 1ull)) {
+        used_ |= 1ull << i;
+        return i;
+      }
+    throw std::runtime_error("GPU engine: more than 64 simulations alive in one process");
+  }
+  void release(int i) {
+    std::lock_guard<std::mutex> g(mu_);
+    used_ &= ~(1ull << i);
+  }
+
+ private:
+  std::mutex mu_;
+  uint64_t used_ = 0;
+};
+
 class GpuEngine : public Engine {
  public:
   ~GpuEngine() override {
@@ -435,6 +474,7 @@ class GpuEngine : public Engine {
     if (d_prof_) (void)hipFree(d_prof_);
     if (d_ework_) (void)hipFree(d_ework_);
     release();
+    if (cfg_slot_ >= 0) CfgSlots::get().release(cfg_slot_);
   }
   const char* name() const override { return "gpu"; }
 
@@ -455,9 +495,19 @@ class GpuEngine : public Engine {
     if (nblocks_ > cap) nblocks_ = cap;
     lds_ = kLdsBytes;
     sliced_ = nblocks_ < c.n_sm + c.n_mem;
-    for (const void* f : {(const void*)engine_kernel<WavePar, false>, (const void*)engine_kernel<WaveParProf, false>,
-                          (const void*)engine_kernel<WavePar, true>, (const void*)engine_kernel<WaveParProf, true>})
+    for (const void* f : {(const void*)engine_kernel<WavePar, false, false>,
+                          (const void*)engine_kernel<WaveParProf, false, false>,
+                          (const void*)engine_kernel<WavePar, true, false>,
+                          (const void*)engine_kernel<WaveParProf, true, false>,
+                          (const void*)engine_kernel<WavePar, false, true>,
+                          (const void*)engine_kernel<WaveParProf, false, true>,
+                          (const void*)engine_kernel<WavePar, true, true>,
+                          (const void*)engine_kernel<WaveParProf, true, true>})
       HIPCHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_));
+    // ASIM_GPU_CFG=lds: the older kernel that reads the configuration from an
+    // LDS copy (A/B comparison); default: constant memory
+    if (const char* ec = getenv("ASIM_GPU_CFG")) cfg_lds_ = !strcmp(ec, "lds");
+    if (cfg_slot_ < 0) cfg_slot_ = CfgSlots::get().acquire();
     const char* pe = getenv("ASIM_GPU_PROFILE");
     profiling_ = pe && *pe && *pe != '0';
     if (profiling_) {
@@ -476,7 +526,7 @@ class GpuEngine : public Engine {
       c_.trace_cnt = d_trace_cnt_;
     }
     HIPCHECK(hipMalloc(&d_cfg_, sizeof(SimCfg)));
-    HIPCHECK(hipMemcpy(d_cfg_, &c_, sizeof(SimCfg), hipMemcpyHostToDevice));
+    upload_cfg();
     std::vector<SMState> hs(c.n_sm);
     for (uint32_t i = 0; i < c.n_sm; ++i) init_sm_state(hs[i], i);
     std::vector<ChanState> hc(c.n_mem);
@@ -555,7 +605,7 @@ class GpuEngine : public Engine {
       ensure_windows();
       HIPCHECK(hipMemcpy(d_kt_, &kt_, sizeof(KernelTab), hipMemcpyHostToDevice));
       GpuArgs a{};
-      a.cfg = c_;
+      a.cfg_slot = (uint32_t)cfg_slot_;
       a.cfg_g = d_cfg_;
       a.kt = d_kt_;
       a.sms = d_sms_;
@@ -583,14 +633,21 @@ class GpuEngine : public Engine {
       a.ework = d_ework_;
       CuPool::get().acquire((int)nblocks_);
       hipError_t le;
-      if (profiling_ && sliced_)
-        hipLaunchKernelGGL((engine_kernel<WaveParProf, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
-      else if (profiling_)
-        hipLaunchKernelGGL((engine_kernel<WaveParProf, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
-      else if (sliced_)
-        hipLaunchKernelGGL((engine_kernel<WavePar, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
-      else
-        hipLaunchKernelGGL((engine_kernel<WavePar, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+#define ASIM_LAUNCH(L)                                                                              \
+  if (profiling_ && sliced_)                                                                        \
+    hipLaunchKernelGGL((engine_kernel<WaveParProf, true, L>), dim3(nblocks_), dim3(64), lds_, stream_, a); \
+  else if (profiling_)                                                                              \
+    hipLaunchKernelGGL((engine_kernel<WaveParProf, false, L>), dim3(nblocks_), dim3(64), lds_, stream_, a); \
+  else if (sliced_)                                                                                 \
+    hipLaunchKernelGGL((engine_kernel<WavePar, true, L>), dim3(nblocks_), dim3(64), lds_, stream_, a); \
+  else                                                                                              \
+    hipLaunchKernelGGL((engine_kernel<WavePar, false, L>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      if (cfg_lds_) {
+        ASIM_LAUNCH(true)
+      } else {
+        ASIM_LAUNCH(false)
+      }
+#undef ASIM_LAUNCH
       le = hipGetLastError();
       hipError_t ce = hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_);
       hipError_t se = hipStreamSynchronize(stream_);
@@ -635,7 +692,7 @@ class GpuEngine : public Engine {
     c_.per_core = per_core;
     c_.clk_base_cyc = base_cyc;
     c_.clk_base_fs = base_fs;
-    HIPCHECK(hipMemcpy(d_cfg_, &c_, sizeof(SimCfg), hipMemcpyHostToDevice));
+    upload_cfg();
   }
   void flush_l2(bool writeback) override {
     std::vector<ChanState> hc(c_.n_mem);
@@ -967,6 +1024,13 @@ class GpuEngine : public Engine {
   }
 
  private:
+  // the configuration as the kernels read it: the engine's constant-memory
+  // slot and the global copy (stream-ordered before the next launch)
+  void upload_cfg() {
+    HIPCHECK(hipMemcpy(d_cfg_, &c_, sizeof(SimCfg), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_cfg), &c_, sizeof(SimCfg), sizeof(SimCfg) * (size_t)cfg_slot_,
+                               hipMemcpyHostToDevice));
+  }
   void upload(void*& d, size_t& cap, const void* h, size_t bytes) {
     if (bytes > cap || !d) {
       if (d) HIPCHECK(hipFree(d));
@@ -1005,6 +1069,8 @@ class GpuEngine : public Engine {
   }
 
   SimCfg c_{};
+  int cfg_slot_ = -1;
+  bool cfg_lds_ = false;
   int n_cu_ = 0;
   uint32_t nblocks_ = 0;
   size_t lds_ = 0;
@@ -1150,7 +1216,7 @@ namespace asim {
 EngineKernelInfo gpu_engine_kernel_info() {
   EngineKernelInfo k;
   hipFuncAttributes fa;
-  if (hipFuncGetAttributes(&fa, (const void*)engine_kernel<WavePar, false>) != hipSuccess) return k;
+  if (hipFuncGetAttributes(&fa, (const void*)engine_kernel<WavePar, false, false>) != hipSuccess) return k;
   k.num_regs = fa.numRegs;
   k.local_bytes = (int)fa.localSizeBytes;
   k.shared_static = (int)fa.sharedSizeBytes;

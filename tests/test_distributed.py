@@ -238,3 +238,57 @@ def test_dp_step_eight_ranks_match_in_process_emulation(native, tmp_path, traffi
     assert bwd[1][1] == bwd[0][1] + bwd[0][2]
     copies = [k for k in res[0][1][1] if k[0] >= 0x40000000]
     assert len(copies) == (DP_KW["layers"] if traffic == "mem_traffic" else 0)
+
+
+def test_bench_eight_gloo_ranks_dp_step_matches_local_ranks(native, tmp_path):
+    """The driver's multi-GPU bench shape on the CPU tier: torchrun with 8
+    ranks, ``bench.py --gpus 8 --engine cpu --dist-backend gloo`` (one
+    simulated GV100 per rank, the DDP step's per-layer all-reduces exchanged
+    as link packets every lookahead epoch, their buffer traffic through each
+    rank's simulated L2/HBM).  Every rank's simulated DDP-step cycles equal
+    the in-process emulation of all 8 ranks (threads + linksim_run_local)."""
+    import json
+    import subprocess
+    import sys
+    import threading
+    from accel_sim_framework_distributed_amd.sim import build_args
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    W = 8
+    tdir = tmp_path / "bench"
+    env = dict(os.environ, OMP_NUM_THREADS="1", ASIM_CPU_JOBS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={W}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", str(W), "--engine", "cpu", "--dist-backend", "gloo", "--apps", "nn,dp-step",
+           "--steps", "1", "--warmup", "0", "--trace-dir", str(tdir)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.split("\n") if ln.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == W and out["metric"] == "sim KIPS (whole node)" and out["value"] > 0
+    dp = out["dp_step"]
+    assert dp["ranks"] == W and dp["collective_coupling"] == ["rccl"] and dp["collective_mem_traffic"]
+    assert len(dp["simulated_cycles_per_rank"]) == W
+    assert out["gpu_engine"]["apps_on_gpu"] == 0 and len(out["gpu_engine"]["kips_per_rank"]) == W
+    # oracle: the same eight traces, all ranks in this process
+    extra = {"-collective_model": "packet", "-gpgpu_concurrent_kernel_sm": "1", "-collective_mem_traffic": "1"}
+    loc = collectives.LocalRanks(W)
+    cyc = [None] * W
+    kern = [None] * W
+
+    def run(rk):
+        s = native.Simulator(build_args("GV100", str(tdir / f"dp-step-{W}" / f"rank{rk}" / "kernelslist.g"), "cpu",
+                                        extra), False)
+        s.set_collective_hook(loc.hook(rk, s))
+        assert s.run() == 0
+        cyc[rk] = int(s.tot_cycle)
+        kern[rk] = len(s.kernels)
+
+    th = [threading.Thread(target=run, args=(rk,)) for rk in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert dp["simulated_cycles_per_rank"] == cyc
+    assert dp["simulated_cycles_max_rank"] == max(cyc)
+    # the collectives' copy kernels ran in every rank's simulated GPU
+    assert dp["rank0_kernels"] == kern[0] > 9
