@@ -35,6 +35,7 @@ CORE_SRC = [
     "csrc/power/power.cc",
     "csrc/driver/simulator.cc",
     "csrc/driver/dump.cc",
+    "csrc/driver/debugger.cc",
     "csrc/parallel/linksim.cc",
 ]
 HIP_SRC = ["csrc/engine/gpu_engine.hip", "csrc/engine/ingest_mfma.hip"]

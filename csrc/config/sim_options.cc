@@ -296,6 +296,11 @@ const OptDef kOptions[] = {
     {"-sim_check_corrupt_at", 'u', "0", "-sim_engine check: perturb the reference state from this cycle (checker self-test)"},
     {"-sim_check_corrupt_mailbox", 'u', "0", "-sim_engine check self-test: perturb a request-mailbox count instead of a unit state"},
     {"-sim_epochs_per_launch", 'u', "4096", "GPU engine epochs per persistent launch"},
+    {"-sim_debug", 'b', "0", "interactive timing debugger (reference gpgpu_debug; also GPGPUSIM_DEBUG=1): single step, "
+                            "PC / cycle breakpoints, memory-line watchpoints, pipeline dumps"},
+    {"-sim_debug_script", 's', "", "debugger commands from this file instead of stdin"},
+    {"-sim_debug_step", 'u', "0", "cycles per debugger step (0: one PDES epoch)"},
+    {"-sim_break_cycle", 'u', "0", "enter the debugger when the simulation reaches this cycle (reference g_single_step)"},
     {"-collective_model", 's', "const", "const | ring | tree | packet collective timing"},
     {"-xgmi_link_bandwidth_gbps", 'f', "153.0", "per-link xGMI bandwidth (GB/s)"},
     {"-xgmi_link_latency_ns", 'f', "1000.0", "collective step latency (ns)"},
@@ -1141,6 +1146,13 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.trace_components = r.gets("-trace_components");
   d.trace_sampling_core = (int32_t)r.geti("-trace_sampling_core");
   d.sim_epochs_per_launch = (uint32_t)r.getu("-sim_epochs_per_launch");
+  {
+    const char* env = getenv("GPGPUSIM_DEBUG");
+    d.debug = r.getb("-sim_debug") || (env && *env && *env != '0') || r.getu("-sim_break_cycle") > 0;
+  }
+  d.debug_script = r.gets("-sim_debug_script");
+  d.debug_step = r.getu("-sim_debug_step");
+  d.break_cycle = r.getu("-sim_break_cycle");
   return d;
 }
 

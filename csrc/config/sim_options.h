@@ -105,6 +105,11 @@ struct DriverOpts {
   bool gpu_ingest = true;      // -gpu_ingest: coalesce traces on the GPU engine's device
   uint64_t gpu_ingest_min = 32768;  // -gpu_ingest_min_insts: smaller kernels stay on the host
   bool trace_prefetch = true;  // -trace_prefetch: parse the next kernel while this one simulates
+  // interactive timing debugger (csrc/driver/debugger.h)
+  bool debug = false;
+  std::string debug_script;
+  uint64_t debug_step = 0;
+  uint64_t break_cycle = 0;
 };
 DriverOpts derive_driver_opts(const OptionRegistry& r);
 

@@ -53,6 +53,28 @@ Simulator::Simulator(const std::vector<std::string>& args) {
   } else {
     throw OptionError("-sim_engine must be cpu, gpu or check");
   }
+  print_mask_ = cfg_.trace_mask;
+  if (dopt_.debug) {
+    // the debugger evaluates breakpoints / watchpoints on the engine's trace
+    // events: record the streams it needs (printed only if also requested)
+    cfg_.trace_mask |= Debugger::trace_mask();
+    // every unit records (breakpoints may name any SM); what is printed still
+    // follows -trace_sampling_core / _memory_partition
+    print_sm_ = cfg_.trace_sm;
+    print_mem_ = cfg_.trace_mem;
+    cfg_.trace_sm = -1;
+    cfg_.trace_mem = -1;
+    Debugger::Hooks h;
+    h.print = [this](const std::string& s) { print("%s", s.c_str()); };
+    h.dump = [this](int sm, int ch) { return dump_pipeline(sm, ch); };
+    h.status = [this]() {
+      char b[200];
+      snprintf(b, sizeof(b), "cycle %llu, kernels completed %zu, thread instructions of completed kernels %llu",
+               (unsigned long long)eng_->now(), results_.size(), (unsigned long long)tot_insn_);
+      return std::string(b);
+    };
+    dbg_.reset(new Debugger(dopt_.debug_script, dopt_.break_cycle, h));
+  }
   eng_->init(cfg_);
   per_core_nom_ = cfg_.per_core;
   if (dopt_.power_enabled) {
@@ -664,7 +686,7 @@ void Simulator::step() {
     if (op) op->epochs += rr.epochs;
   tot_cycle_ = eng_->now();
   retire_collectives();
-  const bool at_max_cycle = dopt_.max_cycle && eng_->now() >= (uint64_t)dopt_.max_cycle;
+  const bool at_max_cycle = (dopt_.max_cycle && eng_->now() >= (uint64_t)dopt_.max_cycle) || dbg_quit_;
   if (rr.cap) cap_hit_ = true;
   if (rr.deadlock) deadlock_ = true;
   // kernels end when they complete, or all together when the run stops
@@ -707,6 +729,10 @@ void Simulator::retire_collectives() {
 }
 
 void Simulator::check_limits() {
+  if (dbg_quit_) {
+    stop_ = true;
+    return;
+  }
   if (deadlock_) {
     stop_ = true;
     return;
@@ -823,7 +849,9 @@ void Simulator::finish_kernel(uint32_t slot, const RunResult& rr) {
 RunResult Simulator::run_sampled(const RunLimits& lim0) {
   // HW / HYBRID modes take one sample per kernel (the hardware counters are per kernel)
   const bool hw = power_ && (dopt_.power_mode == 1 || dopt_.power_mode == 2);
-  const uint64_t freq = std::max<uint64_t>(dopt_.stat_sample_freq, std::max<uint32_t>(1, cfg_.icnt_latency));
+  uint64_t freq = std::max<uint64_t>(dopt_.stat_sample_freq, std::max<uint32_t>(1, cfg_.icnt_latency));
+  // debugger: one step per slice
+  if (dbg_) freq = std::max<uint64_t>(1, dopt_.debug_step ? dopt_.debug_step : cfg_.icnt_latency);
   const double mhz = 1e9 / (double)per_core_nom_;  // nominal: the power model applies the DVFS ratio
   // samples are named after the oldest running kernel
   std::string kname;
@@ -880,8 +908,14 @@ RunResult Simulator::run_sampled(const RunLimits& lim0) {
     }
     if (visualizer_) write_visualizer_sample(kname, now, now > t_prev ? now - t_prev : 1, dsm, dm);
     if (cfg_.trace_mask) {
-      emit_trace();
-      if (cfg_.trace_mask & TS_LIVENESS) {
+      const std::vector<TraceEv> ev = emit_trace();
+      if (dbg_ && !dbg_->after_step(now, ev, cfg_.n_sm, (uint32_t)std::min<uint64_t>(cfg_.per_l2, 0xffffffffull),
+                                    (uint32_t)std::min<uint64_t>(cfg_.per_core, 0xffffffffull))) {
+        dbg_quit_ = true;
+        tot.hit_limit = true;
+        break;
+      }
+      if (print_mask_ & TS_LIVENESS) {
         uint64_t insn = 0;
         for (auto& s : dsm) insn += s.thread_insn;
         const double el = std::max(1e-9, wall_seconds());
@@ -921,10 +955,20 @@ void Simulator::set_clock_ratio(double ratio) {
 
 // Drain the engine's debug trace buffers and print them DPRINTF-style
 // (reference trace.h:56-88: "GPGPU-Sim Cycle N: STREAM - ...") in time order.
-void Simulator::emit_trace() {
+std::vector<TraceEv> Simulator::emit_trace() {
   std::vector<TraceEv> ev;
   uint64_t dropped = 0;
   eng_->trace_drain(ev, &dropped);
+  auto stream_of = [](uint16_t k) -> uint32_t {
+    switch (k) {
+      case EV_ISSUE: return TS_WARP_SCHEDULER;
+      case EV_SB_RELEASE: return TS_SCOREBOARD;
+      case EV_PKT_SEND: case EV_PKT_RECV: return TS_INTERCONNECT;
+      case EV_L2_ACCESS: return TS_MEMORY_SUBPARTITION_UNIT;
+      case EV_DRAM_CMD: return TS_MEMORY_PARTITION_UNIT;
+      default: return 0;
+    }
+  };
   auto core_time = [&](const TraceEv& e) -> double {
     if (e.kind == EV_L2_ACCESS) return (double)e.cycle * (double)cfg_.per_l2 / (double)cfg_.per_core;
     if (e.kind == EV_DRAM_CMD) return (double)e.cycle * (double)cfg_.per_dram / (double)cfg_.per_core;
@@ -941,6 +985,9 @@ void Simulator::emit_trace() {
   static const char* dcmd[] = {"RD", "WR", "ACT", "PRE"};
   for (size_t i : idx) {
     const TraceEv& e = ev[i];
+    if (!(print_mask_ & stream_of(e.kind))) continue;  // recorded for the debugger only
+    if (dbg_ && e.unit < cfg_.n_sm && print_sm_ >= 0 && e.unit != (uint32_t)print_sm_) continue;
+    if (dbg_ && e.unit >= cfg_.n_sm && print_mem_ >= 0 && e.unit - cfg_.n_sm != (uint32_t)print_mem_) continue;
     const unsigned long long cyc = (unsigned long long)core_time(e);
     switch (e.kind) {
       case EV_ISSUE:
@@ -972,6 +1019,7 @@ void Simulator::emit_trace() {
     }
   }
   if (dropped) print("GPGPU-Sim: WARNING %llu trace events dropped (per-unit buffer full)\n", (unsigned long long)dropped);
+  return ev;
 }
 
 // One line per sample period (reference visualizer_printstat, visualizer.cc:56-84,

@@ -12,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#include "debugger.h"
 #include "../config/sim_options.h"
 #include "../engine/engine.h"
 #include "../parallel/linksim.h"
@@ -169,7 +170,13 @@ class Simulator {
   double dvfs_ratio_ = 1.0;
   void set_clock_ratio(double ratio);
   std::unique_ptr<std::ofstream> power_report_, power_trace_, power_steady_, visualizer_;
-  void emit_trace();
+  // drain the engine's debug trace events, print the streams the user asked
+  // for, return all of them (the debugger evaluates its breakpoints on them)
+  std::vector<TraceEv> emit_trace();
+  uint32_t print_mask_ = 0;   // trace streams to print (-trace_components)
+  int32_t print_sm_ = -1, print_mem_ = -1;  // units to print (the debugger records all)
+  std::unique_ptr<Debugger> dbg_;
+  bool dbg_quit_ = false;
   void write_visualizer_sample(const std::string& kname, uint64_t now, uint64_t cycles,
                                const std::vector<SMStats>& dsm, const std::vector<MemStats>& dm);
   std::vector<Command> cmds_;
