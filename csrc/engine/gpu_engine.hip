@@ -15,6 +15,7 @@
 // reference engine.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <csignal>
 #include <cstdio>
@@ -49,16 +50,17 @@ namespace asim {
 // through address space 4, every wave-uniform access is a scalar load the
 // compiler may hoist and CSE freely (constant memory is never written by a
 // kernel), so configuration-derived values stay in SGPRs and their
-// arithmetic is SALU; only lane-indexed reads become vector loads.  From an
-// LDS copy (the alternative kernel, kCfgLds) each read after any state store
-// must be re-issued (the compiler cannot rule out aliasing with the state in
-// LDS) and lands in a VGPR.
+// arithmetic is SALU; only lane-indexed reads become vector loads.  From the
+// LDS copy used before, each read after any state store had to be re-issued
+// (the compiler cannot rule out aliasing with the state in LDS) and landed in
+// a VGPR: constant memory measured 6-7 % faster on bfs / hotspot / heartwall
+// (profiles/r4/ab_cfg_const_vs_lds.txt), bit-exact.
 constexpr int kCfgSlots = 64;
 __constant__ SimCfg g_cfg[kCfgSlots];
 
 struct GpuArgs {
   uint32_t cfg_slot;                 // g_cfg slot of this engine
-  const SimCfg* __restrict__ cfg_g;  // device copy (the LDS-config kernel copies it in)
+  const SimCfg* __restrict__ cfg_g;  // global copy (not read by the engine kernel)
   const KernelTab* kt;               // running kernels (copied into LDS at launch)
   SMState* sms;
   ChanState* chs;
@@ -131,9 +133,8 @@ __device__ __forceinline__ void swap_out(T* dst, const T* lds) {
 
 extern __shared__ __attribute__((aligned(16))) char g_lds[];
 constexpr size_t kStateLds = ((sizeof(SMState) > sizeof(ChanState) ? sizeof(SMState) : sizeof(ChanState)) + 15) / 16 * 16;
-constexpr size_t kCfgOff = kStateLds + (sizeof(KernelTab) + 15) / 16 * 16;
-constexpr size_t kProfOff = kCfgOff + (sizeof(SimCfg) + 15) / 16 * 16;
-constexpr int kProfSlots = 36;
+constexpr size_t kProfOff = kStateLds + (sizeof(KernelTab) + 15) / 16 * 16;
+constexpr int kProfSlots = 48;
 struct ProfLds {
   uint64_t last;
   uint32_t slot;
@@ -164,7 +165,7 @@ struct WaveParProf : WavePar {
   }
 };
 
-template <class P, bool kSliced, bool kCfgLds>
+template <class P, bool kSliced>
 __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   const uint32_t b = blockIdx.x;
   // The configuration is read all over the model, much of it at lane-varying
@@ -174,14 +175,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   // block copies the configuration into LDS once and reads it from there
   // (static global loads in this kernel 1031 -> 58; bfs engine time -3 %,
   // profiles/pmc_sq_engine_bfs_r2.json).
-  if (kCfgLds) {
-    static_assert(sizeof(SimCfg) % 8 == 0, "SimCfg must be 8-byte granular");
-    const uint2* src = reinterpret_cast<const uint2*>(a.cfg_g);
-    uint2* dst = reinterpret_cast<uint2*>(g_lds + kCfgOff);
-    for (int i = (int)(threadIdx.x & 63); i < (int)(sizeof(SimCfg) / 8); i += 64) dst[i] = src[i];
-    __syncthreads();
-  }
-  const SimCfg& c = kCfgLds ? *reinterpret_cast<const SimCfg*>(g_lds + kCfgOff) : g_cfg[a.cfg_slot];
+  const SimCfg& c = g_cfg[a.cfg_slot];
   const uint64_t E = c.icnt_latency;
   SMState* s = reinterpret_cast<SMState*>(g_lds);
   ChanState* ch = reinterpret_cast<ChanState*>(g_lds);
@@ -281,10 +275,19 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
       if ((threadIdx.x & 63) == 0 && was_last) { pl->acc[34] += t_exit - t_arrive; pl->acc[35] += 1; }
       if (b == 0) {
         // slowest block's work this epoch (critical path) and the epoch count
-        uint32_t m = 0;
-        for (uint32_t j = threadIdx.x & 63; j < a.nblocks; j += 64) m = a.ework[j] > m ? a.ework[j] : m;
-        m = WavePar::wave_reduce(m, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
-        if ((threadIdx.x & 63) == 0) { pl->acc[32] += m; pl->acc[33] += 1; }
+        uint64_t mk = 0;  // work << 32 | block: the slowest block and its work
+        for (uint32_t j = threadIdx.x & 63; j < a.nblocks; j += 64) {
+          const uint64_t k = (uint64_t)a.ework[j] << 32 | j;
+          mk = k > mk ? k : mk;
+        }
+        mk = WavePar::red_max64(mk);
+        const uint32_t m = (uint32_t)(mk >> 32);
+        if ((threadIdx.x & 63) == 0) {
+          pl->acc[32] += m;
+          pl->acc[33] += 1;
+          // per block: epochs in which it was the slowest (slot 30)
+          atomicAdd((unsigned long long*)&a.prof[(size_t)(uint32_t)mk * kProfSlots + 30], 1ull);
+        }
       }
       t_work0 = t_exit;
     }
@@ -304,7 +307,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     copy_state(&a.sms[loaded], s);
   else
     copy_state(&a.chs[loaded - c.n_sm], ch);
-  if (a.prof && (threadIdx.x & 63) < kProfSlots) a.prof[(size_t)b * kProfSlots + (threadIdx.x & 63)] += pl->acc[threadIdx.x & 63];
+  if (a.prof && (threadIdx.x & 63) < kProfSlots && (threadIdx.x & 63) != 30) a.prof[(size_t)b * kProfSlots + (threadIdx.x & 63)] += pl->acc[threadIdx.x & 63];
   if (b == 0 && (threadIdx.x & 63) == 0) {
     a.ctl->done = done;
     a.ctl->deadlock = dead;
@@ -495,18 +498,9 @@ class GpuEngine : public Engine {
     if (nblocks_ > cap) nblocks_ = cap;
     lds_ = kLdsBytes;
     sliced_ = nblocks_ < c.n_sm + c.n_mem;
-    for (const void* f : {(const void*)engine_kernel<WavePar, false, false>,
-                          (const void*)engine_kernel<WaveParProf, false, false>,
-                          (const void*)engine_kernel<WavePar, true, false>,
-                          (const void*)engine_kernel<WaveParProf, true, false>,
-                          (const void*)engine_kernel<WavePar, false, true>,
-                          (const void*)engine_kernel<WaveParProf, false, true>,
-                          (const void*)engine_kernel<WavePar, true, true>,
-                          (const void*)engine_kernel<WaveParProf, true, true>})
+    for (const void* f : {(const void*)engine_kernel<WavePar, false>, (const void*)engine_kernel<WaveParProf, false>,
+                          (const void*)engine_kernel<WavePar, true>, (const void*)engine_kernel<WaveParProf, true>})
       HIPCHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_));
-    // ASIM_GPU_CFG=lds: the older kernel that reads the configuration from an
-    // LDS copy (A/B comparison); default: constant memory
-    if (const char* ec = getenv("ASIM_GPU_CFG")) cfg_lds_ = !strcmp(ec, "lds");
     if (cfg_slot_ < 0) cfg_slot_ = CfgSlots::get().acquire();
     const char* pe = getenv("ASIM_GPU_PROFILE");
     profiling_ = pe && *pe && *pe != '0';
@@ -633,21 +627,14 @@ class GpuEngine : public Engine {
       a.ework = d_ework_;
       CuPool::get().acquire((int)nblocks_);
       hipError_t le;
-#define ASIM_LAUNCH(L)                                                                              \
-  if (profiling_ && sliced_)                                                                        \
-    hipLaunchKernelGGL((engine_kernel<WaveParProf, true, L>), dim3(nblocks_), dim3(64), lds_, stream_, a); \
-  else if (profiling_)                                                                              \
-    hipLaunchKernelGGL((engine_kernel<WaveParProf, false, L>), dim3(nblocks_), dim3(64), lds_, stream_, a); \
-  else if (sliced_)                                                                                 \
-    hipLaunchKernelGGL((engine_kernel<WavePar, true, L>), dim3(nblocks_), dim3(64), lds_, stream_, a); \
-  else                                                                                              \
-    hipLaunchKernelGGL((engine_kernel<WavePar, false, L>), dim3(nblocks_), dim3(64), lds_, stream_, a);
-      if (cfg_lds_) {
-        ASIM_LAUNCH(true)
-      } else {
-        ASIM_LAUNCH(false)
-      }
-#undef ASIM_LAUNCH
+      if (profiling_ && sliced_)
+        hipLaunchKernelGGL((engine_kernel<WaveParProf, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      else if (profiling_)
+        hipLaunchKernelGGL((engine_kernel<WaveParProf, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      else if (sliced_)
+        hipLaunchKernelGGL((engine_kernel<WavePar, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      else
+        hipLaunchKernelGGL((engine_kernel<WavePar, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       le = hipGetLastError();
       hipError_t ce = hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_);
       hipError_t se = hipStreamSynchronize(stream_);
@@ -1070,7 +1057,6 @@ class GpuEngine : public Engine {
 
   SimCfg c_{};
   int cfg_slot_ = -1;
-  bool cfg_lds_ = false;
   int n_cu_ = 0;
   uint32_t nblocks_ = 0;
   size_t lds_ = 0;
@@ -1127,13 +1113,15 @@ class GpuEngine : public Engine {
         "sm.receive", "sm.writeback", "sm.hit_complete", "sm.ldst", "sm.dispatch", "sm.read_operands",
         "sm.alloc_oc", "sm.issue", "sm.fetch", "sm.retire", "sm.inject", "sm.occupancy", "sm.gather",
         "sm.cta_dispatch", "sm.refill", "sm.cycle_loop", "sm.publish", "#sm_cycles", "#quiet_checks", "#epochs_busy", "mem.gather", "mem.dram",
-        "mem.l2", "mem.icnt", "mem.window_other", "mem.publish", "barrier", "decide", "post", "sm.issue_sched", "-", "launch_rest",
-        "#max_work/epoch", "#epochs(b0)", "#last_arriver_wait", "#last_arrivals"};
+        "mem.l2", "mem.icnt", "mem.window_other", "mem.publish", "barrier", "decide", "post", "sm.issue_sched", "#slowest", "launch_rest",
+        "#max_work/epoch", "#epochs(b0)", "#last_arriver_wait", "#last_arrivals", "ldst.l1_probe", "ldst.mshr_find",
+        "ldst.pend_reg", "ldst.send", "recv.xbar", "recv.l1_fill", "issue.one", "issue.pick", "quiet_check", "skip",
+        "ldst.hit_push", "fill.pend_wake"};
     double sm[kProfSlots] = {}, mc[kProfSlots] = {}, smt = 0, mct = 0;
     for (uint32_t b = 0; b < nblocks_; ++b)
       for (int k = 0; k < kProfSlots; ++k) {
         double v = (double)h[(size_t)b * kProfSlots + k];
-        const bool counter = (k >= 17 && k <= 19) || k >= 32;
+        const bool counter = (k >= 17 && k <= 19) || k == 30 || (k >= 32 && k <= 35);
         if (b < c_.n_sm) { sm[k] += v / c_.n_sm; smt += counter ? 0 : v / c_.n_sm; }
         else { mc[k] += v / c_.n_mem; mct += counter ? 0 : v / c_.n_mem; }
       }
@@ -1142,7 +1130,10 @@ class GpuEngine : public Engine {
       double cyc_clk = 0, n_cyc = 0, n_q = 0, n_ep = 0, q_clk = 0;
       for (uint32_t b = 0; b < c_.n_sm; ++b) {
         for (int k = 0; k <= 11; ++k) cyc_clk += (double)h[(size_t)b * kProfSlots + k];
-        q_clk += (double)h[(size_t)b * kProfSlots + 15];
+        for (int k = 36; k <= 43; ++k) cyc_clk += (double)h[(size_t)b * kProfSlots + k];
+        cyc_clk += (double)h[(size_t)b * kProfSlots + 29] + (double)h[(size_t)b * kProfSlots + 46] +
+                   (double)h[(size_t)b * kProfSlots + 47];
+        q_clk += (double)h[(size_t)b * kProfSlots + 44] + (double)h[(size_t)b * kProfSlots + 45];
         n_cyc += (double)h[(size_t)b * kProfSlots + 17];
         n_q += (double)h[(size_t)b * kProfSlots + 18];
         n_ep += (double)h[(size_t)b * kProfSlots + 19];
@@ -1163,20 +1154,31 @@ class GpuEngine : public Engine {
                       "barrier wait %.0f clocks/epoch (pure barrier latency)\n",
               ne, ne ? mx / ne : 0, nl ? lw / nl : 0);
     }
+    {
+      std::vector<std::pair<uint64_t, uint32_t>> sl;
+      for (uint32_t b = 0; b < nblocks_; ++b) sl.push_back({h[(size_t)b * kProfSlots + 30], b});
+      std::sort(sl.rbegin(), sl.rend());
+      fprintf(stderr, "[asim gpu profile] slowest block per epoch (epochs, block, its SM cycles / quiet checks):");
+      for (size_t i = 0; i < sl.size() && i < 8 && sl[i].first; ++i)
+        fprintf(stderr, " %llu x b%u (%s, %llu/%llu)", (unsigned long long)sl[i].first, sl[i].second,
+                sl[i].second < c_.n_sm ? "SM" : "MEM", (unsigned long long)h[(size_t)sl[i].second * kProfSlots + 17],
+                (unsigned long long)h[(size_t)sl[i].second * kProfSlots + 18]);
+      fprintf(stderr, "\n");
+    }
     // the critical block: most time outside the barrier wait
     uint32_t crit = 0;
     double crit_work = -1;
     for (uint32_t b = 0; b < nblocks_; ++b) {
       double w = 0;
       for (int k = 0; k < kProfSlots; ++k)
-        if (k != 26 && !(k >= 17 && k <= 19) && k < 32) w += (double)h[(size_t)b * kProfSlots + k];
+        if (k != 26 && k != 30 && !(k >= 17 && k <= 19) && !(k >= 32 && k <= 35)) w += (double)h[(size_t)b * kProfSlots + k];
       if (w > crit_work) { crit_work = w; crit = b; }
     }
     fprintf(stderr, "[asim gpu profile] shader-clock cycles per block (mean), share of block time; "
                     "CRIT = block %u (%s), the one with the least barrier wait\n", crit, crit < c_.n_sm ? "SM" : "MEM");
     double ct = 0;
     for (int k = 0; k < kProfSlots; ++k)
-      if (!(k >= 17 && k <= 19) && k < 32) ct += (double)h[(size_t)crit * kProfSlots + k];
+      if (k != 30 && !(k >= 17 && k <= 19) && !(k >= 32 && k <= 35)) ct += (double)h[(size_t)crit * kProfSlots + k];
     for (int k = 0; k < kProfSlots; ++k) {
       const double cv = (double)h[(size_t)crit * kProfSlots + k];
       if (sm[k] + mc[k] > 0)
@@ -1216,7 +1218,7 @@ namespace asim {
 EngineKernelInfo gpu_engine_kernel_info() {
   EngineKernelInfo k;
   hipFuncAttributes fa;
-  if (hipFuncGetAttributes(&fa, (const void*)engine_kernel<WavePar, false, false>) != hipSuccess) return k;
+  if (hipFuncGetAttributes(&fa, (const void*)engine_kernel<WavePar, false>) != hipSuccess) return k;
   k.num_regs = fa.numRegs;
   k.local_bytes = (int)fa.localSizeBytes;
   k.shared_static = (int)fa.sharedSizeBytes;

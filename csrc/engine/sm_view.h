@@ -147,12 +147,27 @@ __device__ __forceinline__ bool sbt(const WarpSb& sb, uint32_t w, uint8_t r) {
 }
 __device__ __forceinline__ void sb_upd(WarpSb& sb, uint32_t w, uint8_t r, bool set) {
   if (!r) return;
+  // the register's word is wave-uniform whenever the register is (the usual
+  // case: one warp's instruction): a scalar branch picks the word and one
+  // masked VALU op per half updates it; lane-varying registers take the
+  // generic select over the four words
   const uint32_t k = (uint32_t)r >> 6;
-  const uint64_t bit = 1ull << (r & 63);
-  const bool me = sv_lane() == (int)w;
+  const uint64_t m = sv_lane() == (int)w ? 1ull << (r & 63) : 0ull;
+  const int k0 = __builtin_amdgcn_readfirstlane((int)k);
+  if (__builtin_amdgcn_ballot_w64((int)k != k0) == 0) {
+    switch (k0) {
+      case 0: sb.v[0] = set ? (sb.v[0] | m) : (sb.v[0] & ~m); break;
+      case 1: sb.v[1] = set ? (sb.v[1] | m) : (sb.v[1] & ~m); break;
+      case 2: sb.v[2] = set ? (sb.v[2] | m) : (sb.v[2] & ~m); break;
+      default: sb.v[3] = set ? (sb.v[3] | m) : (sb.v[3] & ~m); break;
+    }
+    return;
+  }
 #pragma unroll
-  for (uint32_t j = 0; j < 4; ++j)
-    if (me && j == k) sb.v[j] = set ? (sb.v[j] | bit) : (sb.v[j] & ~bit);
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint64_t mj = j == k ? m : 0ull;
+    sb.v[j] = set ? (sb.v[j] | mj) : (sb.v[j] & ~mj);
+  }
 }
 __device__ __forceinline__ void sbs(WarpSb& sb, uint32_t w, uint8_t r) { sb_upd(sb, w, r, true); }
 __device__ __forceinline__ void sbc(WarpSb& sb, uint32_t w, uint8_t r) { sb_upd(sb, w, r, false); }
@@ -260,36 +275,39 @@ struct SmView {
   SV_REF(skey);
   SV_REF(sref);
   SV_REF(srank);
-  // statistics: counter word k lives in lane (k & 63) of stv[k >> 6], so an
-  // update is one masked VALU add instead of an LDS read-modify-write
-  // (words 128.. are rarer histograms: they stay in the LDS state)
-  uint64_t stv[2];
+  // statistics: counter word k lives in lane (k & 63) of word st<k >> 6>, so an
+  // update is one masked VALU add instead of an LDS read-modify-write (all
+  // words, the per-scheduler issue histograms included: those updates sit
+  // in the issue loop, where an LDS round trip each cost ~150 clocks)
+  static constexpr int kStv = (kStatWords + 63) / 64;
+  static_assert(kStv <= 4, "SmView keeps at most four statistics words per lane");
+  // four named words, never an array: a dynamically indexed array (or a
+  // merged store through a selected address) demotes the view to scratch
+  uint64_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;
+  __device__ __forceinline__ uint64_t stw_get(uint32_t j) const {
+    return j == 0 ? st0 : j == 1 ? st1 : j == 2 ? st2 : st3;
+  }
   __device__ __forceinline__ void sadd(uint32_t k, uint64_t d) {
-    if (k >= 128u) {
-      reinterpret_cast<uint64_t*>(&base.st)[k] += d;
-      return;
-    }
-    if (sv_lane() == (int)(k & 63u)) {
-      if (k < 64u) stv[0] += d;
-      else stv[1] += d;
-    }
+    const uint64_t dd = sv_lane() == (int)(k & 63u) ? d : 0ull;
+    const uint32_t j = k >> 6;
+    st0 += j == 0 ? dd : 0ull;
+    if (kStv > 1) st1 += j == 1 ? dd : 0ull;
+    if (kStv > 2) st2 += j == 2 ? dd : 0ull;
+    if (kStv > 3) st3 += j == 3 ? dd : 0ull;
   }
   __device__ __forceinline__ uint64_t sget(uint32_t k) const {
-    if (k >= 128u) return reinterpret_cast<const uint64_t*>(&base.st)[k];
-    const uint64_t m = k < 64u ? stv[0] : stv[1];
+    const uint64_t m = stw_get(k >> 6);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, (int)(k & 63u));
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), (int)(k & 63u));
     return ((uint64_t)hi << 32) | lo;
   }
   __device__ __forceinline__ void sset(uint32_t k, uint64_t v) {
-    if (k >= 128u) {
-      reinterpret_cast<uint64_t*>(&base.st)[k] = v;
-      return;
-    }
-    if (sv_lane() == (int)(k & 63u)) {
-      if (k < 64u) stv[0] = v;
-      else stv[1] = v;
-    }
+    const bool me = sv_lane() == (int)(k & 63u);
+    const uint32_t j = k >> 6;
+    st0 = me && j == 0 ? v : st0;
+    if (kStv > 1) st1 = me && j == 1 ? v : st1;
+    if (kStv > 2) st2 = me && j == 2 ? v : st2;
+    if (kStv > 3) st3 = me && j == 3 ? v : st3;
   }
 
 #define SV_SCALARS(X)                                                                                   \
@@ -322,8 +340,11 @@ struct SmView {
     {
       const uint64_t* sw = reinterpret_cast<const uint64_t*>(&b.st);
       const int l = sv_lane();
-      stv[0] = l < kStatWords ? sw[l] : 0ull;
-      stv[1] = l + 64 < kStatWords ? sw[l + 64 < kStatWords ? l + 64 : 0] : 0ull;  // words < 128
+      auto ld = [&](int j) -> uint64_t { return l + 64 * j < kStatWords ? sw[l + 64 * j < kStatWords ? l + 64 * j : 0] : 0ull; };
+      st0 = ld(0);
+      if (kStv > 1) st1 = ld(1);
+      if (kStv > 2) st2 = ld(2);
+      if (kStv > 3) st3 = ld(3);
     }
     {  // LdstState: 16-byte words through readfirstlane
       uint32_t w[sizeof(ldst) / 4];
@@ -345,8 +366,10 @@ struct SmView {
     {
       uint64_t* sw = reinterpret_cast<uint64_t*>(&base.st);
       const int l = sv_lane();
-      if (l < kStatWords) sw[l] = stv[0];
-      if (l + 64 < kStatWords) sw[l + 64] = stv[1];
+      if (l < kStatWords) sw[l] = st0;
+      if (kStv > 1 && l + 64 < kStatWords) sw[l + 64] = st1;
+      if (kStv > 2 && l + 128 < kStatWords) sw[l + 128] = st2;
+      if (kStv > 3 && l + 192 < kStatWords) sw[l + 192] = st3;
     }
     base.ldst = ldst;
   }

@@ -274,8 +274,10 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t 
         if (t < t1 && c.event_skip) {
           // fast-forward cycles in which provably nothing happens
           P::tick(18);
+          P::prof(44);
           const uint64_t nx = P::uni(sm_quiet_until<P>(v, c, *x.kt, t, t1));
           if (nx > t) {
+            P::prof(45);
             sm_skip<P>(v, c, nx - t, t);
             t = nx;
           }

@@ -138,7 +138,6 @@ struct SMStats {
   uint64_t icnt_reply_conflicts;     // reply net: ready inputs not granted by this SM's ejection port
   uint64_t icnt_reply_queue_cycles;  // reply net: icnt cycles granted replies waited at the port
   uint64_t sq_insn[8];               // issued wave instructions by the CDNA SQ counter classes (SqClass)
-  // ---- words from 128 on stay in LDS on the GPU engine (sm_view.h) ----
   // reference shader_core_stats::shader_cycle_distro (shader.cc:724-730,
   // 1045, 1547-1555), per scheduler and cycle: [0] W0_Idle (no warp with a
   // valid instruction), [1] W0_Scoreboard (valid instructions all wait on the
@@ -294,7 +293,7 @@ struct alignas(16) SMState {
 };
 #define SK(f) ((uint32_t)(offsetof(::asim::SMStats, f) / 8))
 constexpr int kStatWords = (int)(sizeof(SMStats) / 8);
-static_assert(kStatWords <= 256, "SM statistics: words 0..127 in registers, the rest in LDS on the GPU engine");
+static_assert(kStatWords <= 256, "SM statistics: up to four 64-lane register words on the GPU engine");
 SIM_HDI uint64_t* s_scratch_key(SMState& s) { return s.skey; }
 SIM_HDI uint32_t* s_scratch_ref(SMState& s) { return s.sref; }
 SIM_HDI uint32_t* s_scratch_rank(SMState& s) { return s.srank; }
@@ -443,6 +442,9 @@ SIM_HDI void sm_inject(S& s, const SmCtx& x, uint64_t now) {
 template <class P, class S>
 SIM_HDI void sm_writeback(S& s, const SimCfg& c, uint64_t now) {
   uint32_t slot = (uint32_t)(now % kWbRing);
+  // the occupancy bitmap (registers on the GPU) says whether the slot holds
+  // entries: an empty slot costs no ring access
+  if (!((P::uni((uint64_t)s.wb_occ[slot >> 6]) >> (slot & 63)) & 1ull)) return;
   uint32_t n = P::uni(s.wb_cnt[slot]);
   for (uint32_t i = 0; i < n; ++i) {
     WbEnt e = P::uni(s.wb[slot][i]);
@@ -491,6 +493,7 @@ SIM_HDI bool waitcnt_met(S& s, uint32_t w) {
 template <class P, class S>
 SIM_HDI void sm_hit_complete(S& s, uint64_t now) {
   uint32_t slot = (uint32_t)(now % kHitRing);
+  if (!((P::uni((uint64_t)s.hit_occ[slot >> 6]) >> (slot & 63)) & 1ull)) return;  // empty slot
   uint32_t n = P::uni(s.hit_cnt[slot]);
   for (uint32_t i = 0; i < n; ++i) {
     HitEnt e = P::uni(s.hit[slot][i]);
@@ -603,6 +606,7 @@ SIM_HDI void l1_fill(S& s, const SmCtx& x, uint64_t line, uint8_t sectors, uint6
     }
   }
   // wake waiters whose sectors are now all present (lane-parallel scan)
+  P::prof(47);
   const uint32_t np = s.n_pend;
   for (uint32_t b = 0; b < np; b += 64) {
     int n = (int)amin<uint32_t>(64, np - b);
@@ -622,6 +626,7 @@ SIM_HDI void l1_fill(S& s, const SmCtx& x, uint64_t line, uint8_t sectors, uint6
   }
   // compact the pending table tail
   while (s.n_pend && !s.pend[s.n_pend - 1].valid) s.n_pend--;
+  P::prof(41);
 }
 
 // ---------------------------------------------------------------------------
@@ -815,8 +820,10 @@ SIM_HDI void sm_receive(S& s, const SmCtx& x, uint64_t now) {
     Pkt q;
     uint32_t head = P::uni(s.inq_head), n = P::uni(s.inq_n);
     uint16_t an = s.arb_next, ac = s.arb_cnt;
+    P::prof(40);
     const XbarGrant g = xbar_pick<P>(s.inq, head, n, kInQ, core_fs(c, now), c, core_fs(c, now) / c.per_icnt,
                                      an, ac, c.n_subpart);
+    P::prof(0);
     s.arb_next = an;
     s.arb_cnt = ac;
     s.sadd(SK(icnt_reply_conflicts), g.ready - 1);
@@ -849,7 +856,9 @@ SIM_HDI void sm_receive(S& s, const SmCtx& x, uint64_t now) {
     uint32_t w = q.tag & 0xff, sl = (q.tag >> 8) & 0xff;
     if (--s.w_slot_pend[w][sl] == 0) sm_load_slot_done(s, w, sl, now);
   } else {
+    P::prof(41);
     l1_fill<P>(s, x, q.addr, q.sectors, now);
+    P::prof(0);
   }
 }
 
@@ -992,17 +1001,24 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
       sm_send(s, c, atomic ? P_ATOM : P_RD, a.line, a.sectors, a.bytes, tag);
       s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_BYPASS), 1);
     } else {
+      P::prof(36);
       uint32_t set = cache_set_index(g, a.line);
       int way = l1_find<P>(s, g, set, a.line);
       uint8_t have = way >= 0 ? s.l1[set * g.assoc + way].valid : 0;
       uint8_t miss = a.sectors & (uint8_t)~have;
+      P::prof(3);
       if (miss == 0) {
-        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, uslot, 0)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+        P::prof(46);
+        const bool pushed = hit_push(s, now + c.l1_latency, (uint8_t)w, uslot, 0);
+        P::prof(3);
+        if (!pushed) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
         if (g.repl == REPL_LRU) s.l1[set * g.assoc + way].lru = ++s.l1_stamp;
         s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_HIT), 1);
       } else {
         if (s.n_pend >= (uint32_t)kMaxPend) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+        P::prof(37);
         int mi = P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return s.mshr[i].valid && s.mshr[i].line == a.line; });
+        P::prof(3);
         uint8_t need_req = miss;
         if (mi >= 0) need_req = miss & (uint8_t)~s.mshr[mi].requested;
         bool merged = (mi >= 0 && need_req == 0);
@@ -1013,7 +1029,9 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
         } else {
           if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
           if (mi < 0) {
+            P::prof(37);
             mi = P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return !s.mshr[i].valid; });
+            P::prof(3);
             if (mi < 0) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
             s.mshr[mi].valid = 1;
             s.mshr[mi].line = a.line;
@@ -1022,10 +1040,13 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
             s.mshr[mi].t_issue = (uint32_t)now;
           }
           s.mshr[mi].requested |= need_req;
+          P::prof(39);
           sm_send(s, c, P_RD, a.line, need_req, a.bytes, (uint32_t)mi);
+          P::prof(3);
           s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_MISS), 1);
         }
         // register the waiter (first free entry)
+        P::prof(38);
         uint32_t pi = s.n_pend;
         for (uint32_t b = 0; b < s.n_pend; b += 64) {
           int n = (int)amin<uint32_t>(64, s.n_pend - b);
@@ -1039,6 +1060,7 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
         e.slot = uslot;
         e.valid = 1;
         if (pi == s.n_pend) s.n_pend++;
+        P::prof(3);
       }
     }
     if (in.space != S_CONST)
@@ -1474,6 +1496,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
       continue;
     }
     int pick = -1;
+    P::prof(43);
     switch (c.sched_policy) {
       case SCHED_GTO:
       case SCHED_WARP_LIMITING:
@@ -1497,12 +1520,15 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
         break;
       }
     }
+    P::prof(29);
     const uint32_t w = P::uni((uint32_t)pick);
     s.sched_last[sc] = w;
     if (c.warp_issue_interval > 1) P::one([&] { s.w_issue_ok[w] = now + c.warp_issue_interval; });
     const uint32_t hidx = P::uni((uint32_t)s.w_head[w]);
     const TInst in1 = head.at((int)w);
+    P::prof(42);
     const int u1 = sm_issue_one<P>(s, x, now, sc, w, in1, hidx);
+    P::prof(29);
     issued_any = true;
     s.sadd(SK(issue_distro) + 2u + (uint32_t)amin<int>(popc64(in1.mask), kMaxWarpLanes), 1);
     bool dual = false;

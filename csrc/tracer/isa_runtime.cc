@@ -39,7 +39,11 @@
 // and naming, tracer_tool.cu:115-116,303-316,442-445).  "{rank}" in
 // ASIM_TRACE_DIR becomes the process's rank (RANK, OMPI_COMM_WORLD_RANK,
 // SLURM_PROCID or LOCAL_RANK), so every rank of a multi-process job writes
-// its own trace directory.
+// its own trace directory.  ASIM_TRACE_SNAPSHOT=1: the silicon-checkpoint
+// allocation tracking (hipMalloc / hipFree interposed; after every traced
+// kernel kernel-<id>.allocs lists the live allocations and
+// kernel-<id>_alloc-<n>.bin holds their contents, up to
+// ASIM_TRACE_SNAPSHOT_MAX_MB per kernel).
 #include <filesystem>
 #include <dlfcn.h>
 #include <fcntl.h>
@@ -129,6 +133,19 @@ struct Tracer {
   std::unordered_map<std::string, KMap> maps;
   std::unordered_map<const void*, std::string> names;
   std::vector<Ctl*> shadows;  // one device __asim_tctl per registered code object
+  // silicon-checkpoint allocation tracking (reference
+  // util/tracer_nvbit/others/silicon_checkpoint_tool/checkpoint/checkpoint.cu:198-290):
+  // live device allocations (address -> allocation number, bytes); with
+  // ASIM_TRACE_SNAPSHOT set, after every traced kernel each live allocation's
+  // contents go to kernel-<id>_alloc-<n>.bin and the list to kernel-<id>.allocs
+  struct Alloc {
+    uint32_t num;
+    size_t bytes;
+  };
+  std::map<uintptr_t, Alloc> allocs;
+  uint32_t alloc_count = 0;
+  bool snapshot = false;
+  size_t snapshot_max = 1ull << 30;  // bytes per kernel snapshot (ASIM_TRACE_SNAPSHOT_MAX_MB)
 
   Tracer() {
     const char* d = getenv("ASIM_TRACE_DIR");
@@ -165,6 +182,8 @@ struct Tracer {
     if (const char* s = getenv("ASIM_TRACE_RING_KB")) ring_bytes = (size_t)atol(s) << 10;
     if (const char* s = getenv("ASIM_TRACE_SPIN_LIMIT")) spin_limit = (uint32_t)std::max(1L, atol(s));
     if (const char* s = getenv("ASIM_TRACE_DRAIN_DELAY_US")) drain_delay_us = (uint32_t)atol(s);
+    if (const char* s = getenv("ASIM_TRACE_SNAPSHOT")) snapshot = *s && *s != '0';
+    if (const char* s = getenv("ASIM_TRACE_SNAPSHOT_MAX_MB")) snapshot_max = (size_t)atol(s) << 20;
     std::string mp;
     if (const char* s = getenv("ASIM_ISA_MAP")) {
       mp = s;
@@ -430,6 +449,41 @@ void drain_final(const Tracer::Ring& r, uint32_t tickets, Spill& sp) {
   }
 }
 
+// After a traced kernel (already synchronised): the live allocations' list
+// and, with ASIM_TRACE_SNAPSHOT, their contents (the reference's per-kernel
+// memory snapshot, checkpoint.cu:258-282; binary instead of one decimal
+// text token per byte).  Called with the tracer lock held.
+void snapshot_allocs(Tracer& t, long id, const std::string& suffix) {
+  if (!t.snapshot) return;
+  const std::string base = t.dir + "/kernel-" + std::to_string(id) + suffix;
+  FILE* man = fopen((base + ".allocs").c_str(), "w");
+  if (!man) {
+    fprintf(stderr, "asim isa tracer: cannot write %s.allocs\n", base.c_str());
+    return;
+  }
+  fprintf(man, "# alloc_number address bytes file\n");
+  size_t total = 0;
+  std::vector<uint8_t> buf;
+  for (const auto& kv : t.allocs) {
+    const auto& a = kv.second;
+    std::string fn = "-";
+    if (total + a.bytes <= t.snapshot_max) {
+      fn = "kernel-" + std::to_string(id) + suffix + "_alloc-" + std::to_string(a.num) + ".bin";
+      buf.resize(a.bytes);
+      RT_HIP(hipMemcpyDtoH(buf.data(), (hipDeviceptr_t)kv.first, a.bytes));
+      FILE* f = fopen((t.dir + "/" + fn).c_str(), "wb");
+      if (!f || fwrite(buf.data(), 1, a.bytes, f) != a.bytes) {
+        fprintf(stderr, "asim isa tracer: snapshot write failed (%s)\n", fn.c_str());
+        exit(3);
+      }
+      fclose(f);
+      total += a.bytes;
+    }
+    fprintf(man, "%u 0x%016llx %zu %s\n", a.num, (unsigned long long)kv.first, a.bytes, fn.c_str());
+  }
+  fclose(man);
+}
+
 // A kernel's trace could not be captured whole: the capture is unusable, so
 // the traced program ends here with a distinct exit status (5) instead of
 // leaving a directory whose kernelslist names a partial trace.
@@ -531,6 +585,7 @@ hipError_t launch_streamed(Tracer& t, long id, const std::string& name, const KM
     data = static_cast<const uint8_t*>(m);
   }
   write_kernel(t, id, name, km, g, b, shmem, data, sp.chunks);
+  snapshot_allocs(t, id, t.gpu_id >= 0 ? "_" + std::to_string(dev) : "");
   if (m != MAP_FAILED) munmap(m, bytes);
   fclose(sp.f);
   unlink(spath.c_str());
@@ -569,6 +624,29 @@ void __hipRegisterFunction(void** modules, const void* hostFunction, char* devic
     t.names[hostFunction] = deviceName ? deviceName : deviceFunction;
   }
   real(modules, hostFunction, deviceFunction, deviceName, threadLimit, tid, bid, blockDim, gridDim, wSize);
+}
+
+hipError_t hipMalloc(void** ptr, size_t bytes) {
+  using F = hipError_t (*)(void**, size_t);
+  static F real = (F)dlsym(RTLD_NEXT, "hipMalloc");
+  hipError_t e = real(ptr, bytes);
+  Tracer& t = T();
+  if (e == hipSuccess && t.enabled && ptr && *ptr) {
+    std::lock_guard<std::mutex> g(t.mu);
+    t.allocs[(uintptr_t)*ptr] = Tracer::Alloc{t.alloc_count++, bytes};
+  }
+  return e;
+}
+
+hipError_t hipFree(void* ptr) {
+  using F = hipError_t (*)(void*);
+  static F real = (F)dlsym(RTLD_NEXT, "hipFree");
+  Tracer& t = T();
+  if (t.enabled && ptr) {
+    std::lock_guard<std::mutex> g(t.mu);
+    t.allocs.erase((uintptr_t)ptr);
+  }
+  return real(ptr);
 }
 
 hipError_t hipMemcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
@@ -635,6 +713,7 @@ hipError_t hipLaunchKernel(const void* f, dim3 g, dim3 b, void** args, size_t sh
   // the tracer's own read-back is not an application copy (no trace line)
   if (used) RT_HIP(hipMemcpyDtoH(host.data(), db.ptr, host.size()));
   write_kernel(t, id, name, mit->second, g, b, shmem, host.data(), used);
+  snapshot_allocs(t, id, t.gpu_id >= 0 ? "_" + std::to_string(dev) : "");
   return e;
 }
 
