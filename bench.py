@@ -61,7 +61,9 @@ def _cycle_mae():
     the Rodinia-2.0-ft HIP suite traced by the automatic ISA tracer, timed
     with rocprofv3, simulated by the MI355X cycle engine with the tuned
     MI355X config; correlator semantics of plot-correlation.py)."""
-    p = os.path.join(ROOT, "profiles", "correlation", "rodinia_hip_isatrace_r3_gpu.json")
+    # the last full GPU correlation run (round 3, final tree: fresh ubench ->
+    # tuner -> traces -> timings -> counters on one box)
+    p = os.path.join(ROOT, "profiles", "correlation", "rodinia_hip_isatrace_r3g_gpu.json")
     try:
         d = json.load(open(p))["Cycles"]
         cfg, v = next(iter(d.items()))

@@ -43,7 +43,8 @@
 // allocation tracking (hipMalloc / hipFree interposed; after every traced
 // kernel kernel-<id>.allocs lists the live allocations and
 // kernel-<id>_alloc-<n>.bin holds their contents, up to
-// ASIM_TRACE_SNAPSHOT_MAX_MB per kernel).
+// ASIM_TRACE_SNAPSHOT_MAX_MB per kernel).  ASIM_TRACE_BBV=1: per-wave
+// basic-block vectors of every traced kernel (kernel-<id>.bbv).
 #include <filesystem>
 #include <dlfcn.h>
 #include <fcntl.h>
@@ -145,6 +146,7 @@ struct Tracer {
   std::map<uintptr_t, Alloc> allocs;
   uint32_t alloc_count = 0;
   bool snapshot = false;
+  bool bbv = false;  // ASIM_TRACE_BBV: per-wave basic-block vectors (kernel-<id>.bbv)
   size_t snapshot_max = 1ull << 30;  // bytes per kernel snapshot (ASIM_TRACE_SNAPSHOT_MAX_MB)
 
   Tracer() {
@@ -183,6 +185,7 @@ struct Tracer {
     if (const char* s = getenv("ASIM_TRACE_SPIN_LIMIT")) spin_limit = (uint32_t)std::max(1L, atol(s));
     if (const char* s = getenv("ASIM_TRACE_DRAIN_DELAY_US")) drain_delay_us = (uint32_t)atol(s);
     if (const char* s = getenv("ASIM_TRACE_SNAPSHOT")) snapshot = *s && *s != '0';
+    if (const char* s = getenv("ASIM_TRACE_BBV")) bbv = *s && *s != '0';
     if (const char* s = getenv("ASIM_TRACE_SNAPSHOT_MAX_MB")) snapshot_max = (size_t)atol(s) << 20;
     std::string mp;
     if (const char* s = getenv("ASIM_ISA_MAP")) {
@@ -306,6 +309,11 @@ void write_kernel(Tracer& t, long id, const std::string& name, const KMap& km, d
   uint64_t winsts = 0, tinsts = 0;
   long bad = 0;
   std::vector<std::string> lines;
+  // basic-block vectors from the instrumented binary (reference bbv_tool,
+  // util/tracer_nvbit/others/bbv_tool/bbv_count/bbv_count.cu:88-143,320-340):
+  // the rewriter's segments are the basic blocks (cut at every branch, label
+  // and EXEC write); each execution adds its active-thread count
+  std::vector<std::vector<uint64_t>> bbv_rows;
   auto it = waves.begin();
   while (it != waves.end()) {
     const uint32_t cz = std::get<0>(it->first), cy = std::get<1>(it->first), cx = std::get<2>(it->first);
@@ -338,6 +346,7 @@ void write_kernel(Tracer& t, long id, const std::string& name, const KMap& km, d
       }
       size_t ri = 0;
       char buf[160];
+      std::vector<uint64_t> bbv_row(t.bbv ? km.segs.size() : 0, 0);
       while (ri < recs.size()) {
         const uint32_t* r = recs[ri++];
         if (r[0] & kTagMem) {  // a memory record outside its segment: stream out of sync
@@ -350,6 +359,7 @@ void write_kernel(Tracer& t, long id, const std::string& name, const KMap& km, d
           continue;
         }
         const uint64_t exec = (uint64_t)r[2] | (uint64_t)r[3] << 32;
+        if (t.bbv) bbv_row[sid - 1] += (uint64_t)__builtin_popcountll(exec);
         for (const SInst& si : km.segs[sid - 1]) {
           uint64_t m = exec;
           const uint64_t* addrs = nullptr;
@@ -383,12 +393,26 @@ void write_kernel(Tracer& t, long id, const std::string& name, const KMap& km, d
         }
       }
       winsts += lines.size();
+      if (t.bbv) bbv_rows.push_back(std::move(bbv_row));
       fprintf(f, "warp = %u\ninsts = %zu\n", w.first, lines.size());
       for (auto& l : lines) fprintf(f, "%s\n", l.c_str());
     }
     fprintf(f, "\n#END_TB\n\n");
   }
   fclose(f);
+  if (t.bbv) {
+    // reference layout: kernel name, waves, basic blocks, one row per wave
+    const std::string bn = fn.substr(0, fn.rfind('.')) + ".bbv";
+    FILE* bf = fopen((t.dir + "/" + bn).c_str(), "w");
+    if (bf) {
+      fprintf(bf, "%s\n%zu\n%zu\n", name.c_str(), bbv_rows.size(), km.segs.size());
+      for (const auto& row : bbv_rows) {
+        for (uint64_t v : row) fprintf(bf, "%llu ", (unsigned long long)v);
+        fprintf(bf, "\n");
+      }
+      fclose(bf);
+    }
+  }
   if (bad) fprintf(stderr, "asim isa tracer: kernel %ld (%s): %ld records out of sequence\n", id, name.c_str(), bad);
   t.append("kernelslist.g", fn);
   char s[512];

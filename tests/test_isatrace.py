@@ -273,3 +273,48 @@ def test_isatrace_device_filter_and_rank_dirs(tmp_path):
     assert r.returncode == 0 and "PASSED" in r.stdout, r.stderr
     assert not [p for p in os.listdir(tmp_path / "r4") if p.endswith(".traceg")]
     assert "kernel-" not in (tmp_path / "r4" / "kernelslist.g").read_text()
+
+
+@pytest.mark.gpu
+def test_isatrace_allocation_snapshots(tmp_path):
+    """Silicon-checkpoint allocation tracking (reference checkpoint.cu:198-290):
+    hipMalloc / hipFree are tracked and, with ASIM_TRACE_SNAPSHOT, every live
+    allocation is written after each traced kernel; vectoradd's three buffers
+    are listed and c == a + b in the snapshot."""
+    import numpy as np
+    exe = os.path.join(ROOT, "bin", "isatrace", "vectoradd")
+    assert os.path.exists(exe), "build_native.py builds bin/isatrace/*"
+    n = 4096
+    env = {k: v for k, v in os.environ.items() if not k.startswith("ASIM_TRACE")}
+    r = subprocess.run([exe, str(n)], env=dict(env, ASIM_TRACE_DIR=str(tmp_path), ASIM_TRACE_SNAPSHOT="1"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stderr
+    rows = [ln.split() for ln in (tmp_path / "kernel-1.allocs").read_text().split("\n") if ln and ln[0] != "#"]
+    assert [int(x[0]) for x in rows] == [0, 1, 2] and all(int(x[2]) == n * 8 for x in rows)
+    a, b, c = (np.fromfile(tmp_path / x[3], dtype=np.float64) for x in rows)
+    i = np.arange(n, dtype=np.float64)
+    assert np.allclose(a, np.sin(i) ** 2, atol=1e-15) and np.allclose(b, np.cos(i) ** 2, atol=1e-15)
+    assert np.array_equal(c, a + b)
+
+
+@pytest.mark.gpu
+def test_isatrace_basic_block_vectors(tmp_path):
+    """BBVs from the instrumented binary (reference bbv_count.cu): one row per
+    wave, one column per basic block (rewriter segment), active threads per
+    execution."""
+    exe = os.path.join(ROOT, "bin", "isatrace", "vectoradd")
+    n = 4096 + 100  # a partial last wave
+    env = {k: v for k, v in os.environ.items() if not k.startswith("ASIM_TRACE")}
+    r = subprocess.run([exe, str(n)], env=dict(env, ASIM_TRACE_DIR=str(tmp_path), ASIM_TRACE_BBV="1"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stderr
+    lines = (tmp_path / "kernel-1.bbv").read_text().split("\n")
+    assert "vecAdd" in lines[0]
+    nw, nb = int(lines[1]), int(lines[2])
+    rows = [[int(x) for x in ln.split()] for ln in lines[3:3 + nw]]
+    assert nw == -(-n // 1024) * 16 and all(len(rw) == nb for rw in rows)
+    # every wave runs the entry block with its full 64 lanes; the last wave's
+    # guarded body runs with the 100 % 64 live lanes of the partial tail
+    assert all(rw[0] == 64 for rw in rows)
+    m = re.findall(r"vecAdd.*?, (\d+), (\d+)$", (tmp_path / "stats.csv").read_text(), re.M)
+    assert m and sum(sum(rw) for rw in rows) > 0
