@@ -6,6 +6,7 @@ import os
 import sys
 
 _mod = None
+_dist = None
 
 
 def load(prefer_torch_runtime: bool = False):
@@ -34,3 +35,23 @@ def load(prefer_torch_runtime: bool = False):
 
 def gpu_available() -> bool:
     return bool(load().gpu_available())
+
+
+def load_dist():
+    """The native epoch loop of the packet collective (``_asim_dist``, a torch
+    C++ extension built in-tree by build_native.py), or None if it is not
+    built (the Python loop of parallel/collectives.py is used then)."""
+    global _dist
+    if _dist is not None:
+        return _dist or None
+    import importlib.util
+    import torch  # noqa: F401  (the extension links libtorch)
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_asim_dist.so")
+    if not os.path.exists(p):
+        _dist = False
+        return None
+    spec = importlib.util.spec_from_file_location("_asim_dist", p)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    _dist = m
+    return m

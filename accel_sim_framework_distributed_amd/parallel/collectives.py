@@ -123,6 +123,25 @@ class PacketExchange:
     HDR = 8     # header words per destination slot
 
     def run(self, params: Dict, kind: str, nbytes: int, root: int, start_ps: int) -> Dict:
+        """One collective.  The epoch loop runs natively (csrc/parallel/
+        exchange.cc over the group's c10d ProcessGroup, GIL released) unless
+        ``ASIM_NATIVE_EXCHANGE=0`` or the extension is not built; both loops
+        implement the same protocol and give identical results."""
+        import os
+        dist_ext = _native.load_dist() if os.environ.get("ASIM_NATIVE_EXCHANGE", "1") != "0" else None
+        if dist_ext is not None:
+            pg = self.group if self.group is not None else self.dist.distributed_c10d._get_default_group()
+            dev = self.device.index if self.device.type == "cuda" else -1
+            if dev is None:
+                dev = self.torch.cuda.current_device()
+            r = dist_ext.exchange_run(pg, {k: v for k, v in params.items()}, kind, int(nbytes), int(root),
+                                      int(start_ps), int(dev))
+            for k in ("epochs", "packets", "exchanges"):
+                self.stats[k] += int(r[k])
+            self.stats["native_loop_s"] = self.stats.get("native_loop_s", 0.0) + float(r["loop_s"])
+            self.stats["native"] = True
+            return dict(finish_ps=int(r["finish_ps"]), channels=int(r["channels"]),
+                        packets_sent=int(r["packets_sent"]))
         mod = _native.load(prefer_torch_runtime=True)
         W, R, K, H = self.world, self.rank, self.K, self.HDR
         ls = mod.LinkSim(params, kind, int(nbytes), int(root), R, W, int(start_ps))

@@ -185,6 +185,22 @@ def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
     return path
 
 
+def build_dist_ext(verbose: bool = False) -> str:
+    """The native epoch loop of the packet collective (csrc/parallel/exchange.cc)
+    as a torch C++ extension (it calls c10d::ProcessGroup), built in-tree:
+    accel_sim_framework_distributed_amd/_asim_dist.so."""
+    from torch.utils.cpp_extension import load
+    bdir = os.path.join(ROOT, "build", "dist_ext")
+    os.makedirs(bdir, exist_ok=True)
+    load(name="_asim_dist", sources=[os.path.join(ROOT, "csrc", "parallel", "exchange.cc"),
+                                      os.path.join(ROOT, "csrc", "parallel", "linksim.cc")],
+         build_directory=bdir, extra_cflags=["-O2", f"-I{os.path.join(ROOT, 'csrc')}"], verbose=verbose,
+         is_python_module=True)
+    out = os.path.join(PKG, "_asim_dist.so")
+    shutil.copy2(os.path.join(bdir, "_asim_dist.so"), out)
+    return out
+
+
 def build(cpu_only: bool = False, jobs: int | None = None, extra: bool = True, verbose: bool = False) -> None:
     if not cpu_only and not have_hipcc():
         print("[build_native] hipcc not found: building the CPU engine only", file=sys.stderr)
@@ -196,6 +212,12 @@ def build(cpu_only: bool = False, jobs: int | None = None, extra: bool = True, v
     if verbose:
         cmd.append("-v")
     subprocess.run(cmd, check=True, cwd=ROOT)
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - torch is part of the image
+        print("[build_native] torch not importable: skipping the _asim_dist extension", file=sys.stderr)
+        return
+    build_dist_ext(verbose)
 
 
 if __name__ == "__main__":

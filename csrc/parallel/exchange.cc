@@ -1,0 +1,170 @@
+// Native epoch loop of the distributed packet collective: the lock-step
+// PDES epochs of one collective (parallel/collectives.py PacketExchange.run,
+// same protocol, bit-identical results) owned by C++ over a
+// torch.distributed ProcessGroup -- RCCL over xGMI when the group's backend
+// is "nccl" (device buffers, one fixed-size all-to-all per epoch on the
+// current HIP stream), gloo on the CPU.  The Python loop paid an interpreter
+// round trip, two numpy views and a torch dispatch per epoch; here the whole
+// loop runs with the GIL released and the host work per epoch is the native
+// pack / unpack around the all-to-all.
+//
+// Built as a torch C++ extension (build_native.py: _asim_dist), because it
+// talks to c10d::ProcessGroup directly.  The reference has no counterpart: its
+// distributed fork charges a constant -nccl_allreduce_latency per
+// ncclAllReduce (gpu-simulator/main.cc:116-122).
+#include <torch/extension.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <torch/csrc/utils/pybind.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <limits>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "linksim.h"
+
+namespace asim {
+namespace {
+
+constexpr int kSlots = 8;  // packet slots per destination in the fixed exchange (collectives.py K)
+constexpr int kHdr = 8;    // header words per destination slot (collectives.py HDR)
+constexpr int64_t kI64Max = std::numeric_limits<int64_t>::max();
+
+LinkParams params_from(const py::dict& d) {
+  LinkParams p;
+  if (d.contains("link_gbps")) p.link_gbps = d["link_gbps"].cast<double>();
+  if (d.contains("latency_ns")) p.latency_ns = d["latency_ns"].cast<double>();
+  if (d.contains("links")) p.links = d["links"].cast<uint32_t>();
+  if (d.contains("slice_bytes")) p.slice_bytes = d["slice_bytes"].cast<uint32_t>();
+  if (d.contains("max_channels")) p.max_channels = d["max_channels"].cast<uint32_t>();
+  if (d.contains("reduce_gbps")) p.reduce_gbps = d["reduce_gbps"].cast<double>();
+  return p;
+}
+
+// exchange buffers: host (pinned when the group works on device tensors) and,
+// for RCCL, their device twins; reused across epochs
+struct Bufs {
+  bool dev = false;
+  at::Tensor h_send, h_recv, d_send, d_recv;
+  void ensure(size_t n, int device) {
+    if (h_send.defined() && (size_t)h_send.numel() == n) return;
+    auto ho = at::TensorOptions().dtype(at::kLong).pinned_memory(dev);
+    h_send = at::empty({(int64_t)n}, ho);
+    h_recv = at::empty({(int64_t)n}, ho);
+    if (dev) {
+      auto dopt = at::TensorOptions().dtype(at::kLong).device(at::kCUDA, device);
+      d_send = at::empty({(int64_t)n}, dopt);
+      d_recv = at::empty({(int64_t)n}, dopt);
+    }
+  }
+};
+
+// one all-to-all of int64 words with the given split sizes
+void a2a(c10d::ProcessGroup& pg, Bufs& b, std::vector<int64_t>& out_splits, std::vector<int64_t>& in_splits) {
+  at::Tensor src = b.dev ? b.d_send : b.h_send, dst = b.dev ? b.d_recv : b.h_recv;
+  if (b.dev) b.d_send.copy_(b.h_send, /*non_blocking=*/true);
+  auto w = pg.alltoall_base(dst, src, in_splits, out_splits);
+  w->wait();
+  if (b.dev) b.h_recv.copy_(b.d_recv);  // blocking: waits for the collective on the stream
+}
+
+int64_t allreduce_min(c10d::ProcessGroup& pg, int64_t v, bool dev, int device) {
+  auto o = at::TensorOptions().dtype(at::kLong);
+  at::Tensor t = at::full({1}, v, dev ? o.device(at::kCUDA, device) : o);
+  std::vector<at::Tensor> ts{t};
+  c10d::AllreduceOptions ao;
+  ao.reduceOp = c10d::ReduceOp::MIN;
+  pg.allreduce(ts, ao)->wait();
+  return t.cpu().item<int64_t>();
+}
+
+}  // namespace
+
+py::dict exchange_run(py::object pgo, py::dict params, const std::string& kind, int64_t nbytes, int64_t root,
+                      int64_t start_ps, int64_t device) {
+  auto pg = py::cast<c10::intrusive_ptr<c10d::ProcessGroup>>(pgo);
+  const int W = pg->getSize(), R = pg->getRank();
+  CollSpec cs;
+  cs.kind = coll_kind(kind);
+  cs.bytes = (uint64_t)nbytes;
+  cs.root = (int32_t)root;
+  LinkSim ls(params_from(params), cs, R, W, (uint64_t)start_ps);
+  const bool dev = device >= 0;
+  const int slot = kHdr + 4 * kSlots;
+  const size_t n = (size_t)W * slot;
+  uint64_t epochs = 0, packets = 0, exchanges = 0;
+  double loop_s = 0;
+  {
+    py::gil_scoped_release nogil;
+    const auto t0 = std::chrono::steady_clock::now();
+    int64_t t = allreduce_min(*pg, std::min<int64_t>(start_ps, kI64Max), dev, (int)device);
+    const int64_t E = (int64_t)ls.epoch_ps();
+    int64_t ann_next = (int64_t)std::min<uint64_t>(ls.next_event(), (uint64_t)kI64Max);
+    int64_t ann_busy = ls.done() ? 0 : 1;
+    Bufs fixed, spill;
+    fixed.dev = spill.dev = dev;
+    fixed.ensure(n, (int)device);
+    std::vector<int64_t> eq(W, slot);
+    for (;;) {
+      const int64_t t_end = t + E;
+      EpochOut o;
+      pack_epoch(ls, (uint64_t)t_end, kSlots, kHdr, ann_next, ann_busy, fixed.h_send.data_ptr<int64_t>(), o);
+      a2a(*pg, fixed, eq, eq);
+      ++exchanges;
+      const int64_t* recv = fixed.h_recv.data_ptr<int64_t>();
+      int64_t maxc = 0;
+      for (int r = 0; r < W; ++r) maxc = std::max<int64_t>(maxc, recv[(size_t)r * slot + 1]);
+      std::vector<int64_t> inc;
+      if (maxc > kSlots) {
+        // some rank sent more than kSlots packets to one destination: the rest
+        std::vector<int64_t> in_w(W), out_w(o.extra_words.begin(), o.extra_words.end());
+        size_t nin = 0;
+        for (int r = 0; r < W; ++r) {
+          in_w[r] = 4 * std::max<int64_t>(0, recv[(size_t)r * slot] - kSlots);
+          nin += (size_t)in_w[r];
+        }
+        const size_t nout = o.extra.size();
+        spill.h_send = at::empty({(int64_t)nout}, at::TensorOptions().dtype(at::kLong).pinned_memory(dev));
+        spill.h_recv = at::empty({(int64_t)nin}, at::TensorOptions().dtype(at::kLong).pinned_memory(dev));
+        if (nout) std::copy(o.extra.begin(), o.extra.end(), spill.h_send.data_ptr<int64_t>());
+        if (dev) {
+          auto dopt = at::TensorOptions().dtype(at::kLong).device(at::kCUDA, (int)device);
+          spill.d_send = at::empty({(int64_t)nout}, dopt);
+          spill.d_recv = at::empty({(int64_t)nin}, dopt);
+        }
+        a2a(*pg, spill, out_w, in_w);
+        ++exchanges;
+        inc.assign(spill.h_recv.data_ptr<int64_t>(), spill.h_recv.data_ptr<int64_t>() + nin);
+      }
+      const EpochIn in = unpack_epoch(ls, recv, kSlots, kHdr, inc.empty() ? nullptr : inc.data(), inc.size());
+      packets += o.packets;
+      ++epochs;
+      if (!in.any_busy) break;  // every rank was done before this epoch
+      ann_next = (int64_t)std::min<uint64_t>(ls.next_event(), (uint64_t)kI64Max);
+      ann_busy = ls.done() ? 0 : 1;
+      if (in.next >= kI64Max) throw std::runtime_error("packet collective deadlocked (no rank has pending work)");
+      t = std::max<int64_t>(t_end, in.next);
+    }
+    loop_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  py::dict d;
+  d["finish_ps"] = ls.finish_ps();
+  d["channels"] = ls.channels();
+  d["packets_sent"] = ls.packets_sent();
+  d["epochs"] = epochs;
+  d["packets"] = packets;
+  d["exchanges"] = exchanges;
+  d["loop_s"] = loop_s;
+  return d;
+}
+
+}  // namespace asim
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "native epoch loop of the packet-level collective over a torch.distributed ProcessGroup";
+  m.def("exchange_run", &asim::exchange_run, py::arg("group"), py::arg("params"), py::arg("kind"), py::arg("bytes"),
+        py::arg("root"), py::arg("start_ps"), py::arg("device") = -1);
+}
