@@ -387,6 +387,48 @@ PYBIND11_MODULE(_asim, m) {
           return ingest_cmp(k, c, device);
         },
         py::arg("insts"), py::arg("args"), py::arg("device") = 0);
+  // host streaming: the per-CTA reader's instructions, accesses and warp
+  // streams equal the whole-kernel load's, window by window (CTAs [lo, lo+step)
+  // resident, the ones below dropped)
+  m.def("stream_compare", [](const std::string& path, const std::vector<std::string>& args, uint32_t step) {
+    SimCfg c = cfg_from_args(args);
+    ReadyKernel w = coalesce_kernel(load_kernel_text(path), c);
+    ReadyKernel r = open_streamed_kernel(path, c);
+    const uint32_t wpc = w.warps_per_cta;
+    int64_t bad_cta = -1;
+    step = std::max<uint32_t>(1, step);
+    for (uint32_t lo = 0; lo < w.n_cta && bad_cta < 0; lo += step) {
+      const uint32_t hi = std::min(w.n_cta, lo + step);
+      r.resident(lo, hi);
+      for (uint32_t cta = lo; cta < hi && bad_cta < 0; ++cta)
+        for (uint32_t wi = 0; wi < wpc && bad_cta < 0; ++wi) {
+          const WStream& a = w.streams[(size_t)cta * wpc + wi];
+          const WStream& b = r.streams[(size_t)(cta - r.cta_lo) * wpc + wi];
+          if (a.count != b.count) bad_cta = cta;
+          for (uint32_t j = 0; j < a.count && bad_cta < 0; ++j) {
+            TInst x = w.insts[a.begin + j];
+            TInst y = r.insts[((b.begin + j) - (r.ibase & kStreamInstMask)) & kStreamInstMask];
+            const uint32_t xm = x.mem, ym = y.mem;
+            x.mem = y.mem = 0;
+            if (memcmp(&x, &y, sizeof(TInst)) != 0 || (xm == kNoMem) != (ym == kNoMem)) {
+              bad_cta = cta;
+              break;
+            }
+            if (xm == kNoMem) continue;
+            const uint64_t yl = (ym - (r.abase & kStreamAccMask)) & kStreamAccMask;
+            for (uint32_t q = 0; q < x.width && bad_cta < 0; ++q)
+              if (memcmp(&w.accs[xm + q], &r.accs[yl + q], sizeof(TAcc)) != 0) bad_cta = cta;
+          }
+        }
+    }
+    py::dict d;
+    d["equal"] = bad_cta < 0;
+    d["bad_cta"] = bad_cta;
+    d["whole_bytes"] = w.host_bytes();
+    d["stream_peak_bytes"] = r.host_peak_bytes;
+    d["n_cta"] = w.n_cta;
+    return d;
+  });
   m.def("coalesce_summary", [](const std::string& path, const std::vector<std::string>& args) {
     SimCfg c = cfg_from_args(args);
     ReadyKernel r = coalesce_kernel(load_kernel(path), c);

@@ -119,7 +119,7 @@ std::string Simulator::dump_pipeline(int sm, int ch) {
   std::string out;
   const TInst* slot_insts[kMaxConc] = {};
   for (int k = 0; k < kMaxConc; ++k)
-    if (slot_op_[k] && slot_op_[k]->rk && !slot_op_[k]->rk->insts.empty()) slot_insts[k] = slot_op_[k]->rk->insts.data();
+    if (slot_op_[k] && slot_op_[k]->rk && !slot_op_[k]->rk->streamed() && !slot_op_[k]->rk->insts.empty()) slot_insts[k] = slot_op_[k]->rk->insts.data();
   for (uint32_t i = 0; i < cfg_.n_sm; ++i)
     if (sm == -1 || (sm >= 0 && (uint32_t)sm == i)) {
       if (sm == -1 && sms[i].n_cta_active == 0 && sms[i].outstanding == 0) continue;  // skip idle SMs in "all"

@@ -1,5 +1,7 @@
 #include "simulator.h"
 
+#include <sys/stat.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
@@ -465,7 +467,21 @@ void Simulator::setup_kernel_op(StreamOp& o, bool apply_cta_cap) {
   tot_cta_ += kd.n_cta;
 }
 
+// -trace_host_budget_mb: a text trace larger than the budget is read per CTA
+// as the engine's trace window advances instead of loaded whole
+bool Simulator::stream_from_host(const std::string& path) const {
+  if (dopt_.host_budget_mb <= 0 || dopt_.engine == "check") return false;
+  if (path.size() > 6 && path.compare(path.size() - 6, 6, ".asimk") == 0) return false;
+  struct stat st;
+  if (stat(path.c_str(), &st) != 0) return false;
+  return (double)st.st_size > dopt_.host_budget_mb * 1048576.0;
+}
+
 std::unique_ptr<ReadyKernel> Simulator::take_kernel(size_t idx) {
+  if (stream_from_host(cmds_[idx].text)) {
+    ++host_streamed_;
+    return std::unique_ptr<ReadyKernel>(new ReadyKernel(open_streamed_kernel(cmds_[idx].text, cfg_)));
+  }
   auto it = pf_.find(idx);
   if (it != pf_.end()) {
     std::unique_ptr<ReadyKernel> k = it->second.get();  // rethrows a loader error
@@ -502,6 +518,7 @@ void Simulator::prefetch_next() {
   for (size_t i = next_cmd_; i < cmds_.size(); ++i) {
     if (cmds_[i].type != CMD_KERNEL) continue;
     const std::string path = cmds_[i].text;
+    if (stream_from_host(path)) return;  // opened when admitted (reads per CTA)
     pf_[i] = std::async(std::launch::async, [this, path]() { return ingest(load_kernel(path)); });
     return;
   }
@@ -1415,6 +1432,12 @@ void Simulator::print_sim_time() {
   print("gpgpu_silicon_slowdown = %llux\n", cps ? (unsigned long long)(core_khz * 1000.0 / cps) : 0ull);
   uint64_t peak = 0, refills = 0;
   eng_->trace_residency(&peak, &refills);
+  for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k)
+    if (slot_op_[k] && slot_op_[k]->rk && slot_op_[k]->rk->streamed())
+      host_stream_peak_ = std::max(host_stream_peak_, slot_op_[k]->rk->host_peak_bytes);
+  if (host_streamed_)
+    print("trace_host_streamed_kernels: %llu\ntrace_host_peak_bytes: %llu\n", (unsigned long long)host_streamed_,
+          (unsigned long long)host_stream_peak_);
   // not "key = value": an engine diagnostic, not a statistic of the model
   if (peak)
     print("gpu_trace_resident_peak_bytes: %llu\ngpu_trace_window_fills: %llu\n", (unsigned long long)peak,

@@ -140,6 +140,7 @@ class Simulator {
   // engine simulates
   void prefetch_next();
   std::unique_ptr<ReadyKernel> take_kernel(size_t idx);
+  bool stream_from_host(const std::string& path) const;
   // trace ingest: HIP device of the GPU engine (-1: host coalescer) and what
   // ran where (the prefetch thread adds to it too; declared before pf_ so that
   // pending prefetches finish before these are destroyed)
@@ -206,6 +207,8 @@ class Simulator {
   bool copy_since_kernel_ = false;  // a host memcpy ran since the last kernel was admitted
   bool any_kernel_admitted_ = false;
   uint64_t dma_count_ = 0;        // collective copy kernels launched
+  uint64_t host_streamed_ = 0;    // kernels read per CTA from their files (-trace_host_budget_mb)
+  uint64_t host_stream_peak_ = 0;  // largest host trace footprint of one of them
   bool cap_hit_ = false;  // a run cap (-gpgpu_max_insn / _max_cta / _max_completed_cta) stopped a kernel
 };
 

@@ -40,7 +40,9 @@ class CheckEngine final : public Engine {
     a_->init(c);
     b_->init(c);
   }
-  void launch(uint32_t slot, const ReadyKernel& k, const KernelDesc& kd) override {
+  void launch(uint32_t slot, ReadyKernel& k, const KernelDesc& kd) override {
+    // both engines would drive one host stream with different windows
+    if (k.streamed()) throw std::runtime_error("check engine: host-streamed traces (-trace_host_budget_mb) not supported");
     a_->launch(slot, k, kd);
     b_->launch(slot, k, kd);
   }

@@ -1,10 +1,12 @@
 // CPU reference engine: the cycle model with the sequential lane policy.
 // SMs / channels of one epoch are independent (PDES), so the epoch body is
 // parallelised with OpenMP; results are bit-identical for any thread count.
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
 #include "engine.h"
+#include "trace_window.h"
 
 namespace asim {
 
@@ -168,16 +170,14 @@ class CpuEngine : public Engine {
     }
   }
 
-  void launch(uint32_t slot, const ReadyKernel& k, const KernelDesc& kd) override {
+  void launch(uint32_t slot, ReadyKernel& k, const KernelDesc& kd) override {
     if (slot >= (uint32_t)kMaxConc || (kt_.active >> slot & 1u)) throw std::runtime_error("launch: kernel slot busy");
-    if (k.insts.size() > kIdxMask) throw std::runtime_error("kernel trace exceeds 2^29 warp instructions");
+    if (!k.streamed() && k.insts.size() > kIdxMask) throw std::runtime_error("kernel trace exceeds 2^29 warp instructions");
     KernelDesc& d = kt_.k[slot];
     d = kd;
-    d.insts = k.insts.data();
-    d.accs = k.accs.data();
-    d.streams = k.streams.data();
-    d.imask = d.amask = d.cmask = ~0u;  // the whole trace is resident
-    d.cta_avail = d.n_cta;
+    // the whole trace in place, or (host-streamed trace) rings of a window
+    // of CTAs that follows the dispatch cursor (trace_window.h)
+    tw_.launch(slot, k, d, c_);
     kt_.active |= 1u << slot;
   }
   uint32_t running() const override { return kt_.active; }
@@ -190,7 +190,11 @@ class CpuEngine : public Engine {
       res.end_cycle = cycle_;
       return res;
     }
+    bool refill = true;
     for (;;) {
+      // host-streamed traces: bring in the CTAs the next epochs can dispatch
+      // (epoch_decide flags when the window falls short)
+      if (refill) tw_.ensure(kt_, c, [&](DispatchView& v) { read_dispatch(v); });
       const uint32_t cur = (uint32_t)(epoch_ & 1), prev = cur ^ 1u;
       const uint64_t t0 = cycle_, t1 = t0 + E;
       const int nsm = (int)sms_.size(), nch = (int)chs_.size();
@@ -215,6 +219,7 @@ class CpuEngine : public Engine {
         }
       }
       EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, kt_, epoch_, lim.max_cycle);
+      refill = d.refill != 0;
       ++epoch_;
       ++res.epochs;
       cycle_ = d.next_start;
@@ -222,6 +227,8 @@ class CpuEngine : public Engine {
         res.done = true;
         res.done_mask = d.done;
         kt_.active &= ~d.done;
+        for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k)
+          if (d.done >> k & 1u) tw_.done(k);
         break;
       }
       if (d.deadlock) {
@@ -243,6 +250,29 @@ class CpuEngine : public Engine {
   }
 
   uint64_t now() const override { return cycle_; }
+  void trace_residency(uint64_t* peak_bytes, uint64_t* refills) const override {
+    *peak_bytes = tw_.resident_peak;
+    *refills = tw_.refills;
+  }
+  void read_dispatch(DispatchView& v) const {
+    const SMState& s0 = sms_[0];
+    memcpy(v.k_uid, s0.k_uid, sizeof(v.k_uid));
+    memcpy(v.next_cta, s0.next_cta, sizeof(v.next_cta));
+    memcpy(v.next_ctax, s0.next_ctax, sizeof(v.next_ctax));
+    v.sms.resize(sms_.size());
+    for (size_t m = 0; m < sms_.size(); ++m) {
+      memcpy(v.sms[m].cta_id, sms_[m].cta_id, sizeof(v.sms[m].cta_id));
+      memcpy(v.sms[m].cta_valid, sms_[m].cta_valid, sizeof(v.sms[m].cta_valid));
+      memcpy(v.sms[m].cta_ks, sms_[m].cta_ks, sizeof(v.sms[m].cta_ks));
+    }
+  }
+  struct HostMem {
+    static constexpr bool kHost = true;
+    void* alloc(size_t n) { return std::malloc(n); }
+    void free(void* p) { std::free(p); }
+    void write(void* d, const void* h, size_t n) { memcpy(d, h, n); }
+  };
+  TraceWindows<HostMem> tw_;
   std::vector<TraceEv> trace_ev_;
   std::vector<uint32_t> trace_cnt_;
 

@@ -37,7 +37,7 @@ class Engine {
   // start kernel `k` in free slot `slot` (< kMaxConc; uploads its trace): its
   // CTAs dispatch from kd.ready_cycle on.  `k` must stay alive until the
   // kernel completes.
-  virtual void launch(uint32_t slot, const ReadyKernel& k, const KernelDesc& kd) = 0;
+  virtual void launch(uint32_t slot, ReadyKernel& k, const KernelDesc& kd) = 0;
   // simulate the running kernels until one (or more, same epoch) completes,
   // a limit is hit, or deadlock; completed slots are free again afterwards
   virtual RunResult run(const RunLimits& lim) = 0;

@@ -34,6 +34,7 @@
 
 #include "engine.h"
 #include "grid_barrier.h"
+#include "trace_window.h"
 #include "wave_par.h"
 
 namespace asim {
@@ -562,30 +563,15 @@ class GpuEngine : public Engine {
     cycle_ = 0;
   }
 
-  void launch(uint32_t slot, const ReadyKernel& k, const KernelDesc& kd) override {
+  void launch(uint32_t slot, ReadyKernel& k, const KernelDesc& kd) override {
     if (slot >= (uint32_t)kMaxConc || (kt_.active >> slot & 1u)) throw std::runtime_error("launch: kernel slot busy");
-    if (k.insts.size() > kIdxMask) throw std::runtime_error("kernel trace exceeds 2^29 warp instructions");
-    SlotBufs& sb = bufs_[slot];
+    if (!k.streamed() && k.insts.size() > kIdxMask) throw std::runtime_error("kernel trace exceeds 2^29 warp instructions");
     KernelDesc& d = kt_.k[slot];
     d = kd;
-    sb.rk = &k;
-    sb.streamed = plan_window(sb, k, kd);
-    if (sb.streamed) {
-      // the first window: CTAs [0, W); later ones follow the dispatch cursor
-      // (ensure_windows before every engine launch)
-      fill_window(slot, 0, std::min<uint32_t>(kd.n_cta, (uint32_t)sb.w_ctas), true);
-    } else {
-      upload(sb.insts, sb.cap_insts, k.insts.data(), k.insts.size() * sizeof(TInst));
-      upload(sb.accs, sb.cap_accs, k.accs.data(), k.accs.size() * sizeof(TAcc));  // may be empty (no memory ops)
-      upload(sb.streams, sb.cap_streams, k.streams.data(), k.streams.size() * sizeof(WStream));
-      d.insts = reinterpret_cast<const TInst*>(sb.insts);
-      d.accs = reinterpret_cast<const TAcc*>(sb.accs);
-      d.streams = reinterpret_cast<const WStream*>(sb.streams);
-      d.imask = d.amask = d.cmask = ~0u;
-      d.cta_avail = d.n_cta;
-    }
+    // whole kernel uploaded, or (-gpu_trace_window / host-streamed trace) a
+    // window of CTAs that follows the dispatch cursor (trace_window.h)
+    tw_.launch(slot, k, d, c_);
     kt_.active |= 1u << slot;
-    note_residency();
   }
   uint32_t running() const override { return kt_.active; }
 
@@ -596,7 +582,7 @@ class GpuEngine : public Engine {
       return res;
     }
     for (;;) {
-      ensure_windows();
+      tw_.ensure(kt_, c_, [&](DispatchView& v) { read_dispatch(v); });
       HIPCHECK(hipMemcpy(d_kt_, &kt_, sizeof(KernelTab), hipMemcpyHostToDevice));
       GpuArgs a{};
       a.cfg_slot = (uint32_t)cfg_slot_;
@@ -651,7 +637,7 @@ class GpuEngine : public Engine {
         res.done_mask = h_ctl_->done;
         kt_.active &= ~h_ctl_->done;
         for (uint32_t s = 0; s < (uint32_t)kMaxConc; ++s)
-          if (h_ctl_->done >> s & 1u) bufs_[s].rk = nullptr;
+          if (h_ctl_->done >> s & 1u) tw_.done(s);
         break;
       }
       if (h_ctl_->deadlock) { res.deadlock = true; break; }
@@ -812,202 +798,34 @@ class GpuEngine : public Engine {
   }
 
  private:
-  struct SlotBufs;
-  static uint64_t pow2ceil(uint64_t v) {
-    uint64_t p = 1;
-    while (p < v) p <<= 1;
-    return p;
-  }
-
-  // Streaming plan of a kernel (-gpu_trace_window): per-CTA first
-  // instruction / access index, ring capacities.  Streams only when the
-  // trace lays CTAs out in ascending, non-overlapping ranges (every loader
-  // here does) and the kernel is larger than the window.
-  bool plan_window(SlotBufs& sb, const ReadyKernel& k, const KernelDesc& kd) {
-    const uint64_t cpc = std::min<uint32_t>(kd.cta_per_sm, kMaxCta);
-    const uint64_t w = (uint64_t)c_.trace_window * c_.n_sm * std::max<uint64_t>(cpc, 1);
-    if (!c_.trace_window || w >= kd.n_cta || !k.warps_per_cta) return false;
-    const uint32_t n = kd.n_cta, wpc = k.warps_per_cta;
-    sb.ib.assign((size_t)n + 1, 0);
-    sb.ab.assign((size_t)n + 1, 0);
-    uint64_t hi_i = 0, hi_a = 0;
-    for (uint32_t c = 0; c < n; ++c) {
-      uint64_t ilo = ~0ull, ihi = 0, alo = ~0ull, ahi = 0;
-      for (uint32_t wi = 0; wi < wpc; ++wi) {
-        const WStream& ws = k.streams[(size_t)c * wpc + wi];
-        if (!ws.count) continue;
-        ilo = std::min<uint64_t>(ilo, ws.begin);
-        ihi = std::max<uint64_t>(ihi, (uint64_t)ws.begin + ws.count);
-        for (uint32_t j = ws.begin; j < ws.begin + ws.count; ++j) {
-          const TInst& in = k.insts[j];
-          if (in.space == S_SHARED || !in.width || in.mem == kNoMem) continue;
-          alo = std::min<uint64_t>(alo, in.mem);
-          ahi = std::max<uint64_t>(ahi, (uint64_t)in.mem + std::min<uint32_t>(in.width, kMaxAccess));
-        }
-      }
-      if (ilo == ~0ull) ilo = ihi = hi_i;
-      if (alo == ~0ull) alo = ahi = hi_a;
-      if (ilo < hi_i || alo < hi_a) return false;  // not CTA-ordered: keep the whole kernel
-      sb.ib[c] = (uint32_t)ilo;
-      sb.ab[c] = (uint32_t)alo;
-      hi_i = ihi;
-      hi_a = ahi;
-    }
-    sb.ib[n] = (uint32_t)hi_i;
-    sb.ab[n] = (uint32_t)hi_a;
-    sb.w_ctas = w;
-    const uint32_t we = (uint32_t)std::min<uint64_t>(n, w);
-    sb.ccap = pow2ceil(w);
-    sb.icap = pow2ceil(std::max<uint64_t>(1, sb.ib[we] - sb.ib[0]));
-    sb.acap = pow2ceil(std::max<uint64_t>(1, sb.ab[we] - sb.ab[0]));
-    sb.lo = sb.avail = 0;
-    sb.alloc_i = sb.alloc_a = sb.alloc_c = 0;
-    return true;
-  }
-
-  // copy global elements [first, first + count) of `src` into a ring of
-  // `cap` entries (+ `pad` mirrored leading entries) at index & (cap - 1)
-  void ring_write(void* ring, size_t esz, uint64_t cap, uint64_t pad, const void* src, uint64_t first,
-                  uint64_t count) {
-    char* r = static_cast<char*>(ring);
-    const char* s = static_cast<const char*>(src) + first * esz;
-    while (count) {
-      const uint64_t p = first & (cap - 1);
-      const uint64_t n = std::min<uint64_t>(count, cap - p);
-      HIPCHECK(hipMemcpy(r + p * esz, s, n * esz, hipMemcpyHostToDevice));
-      if (p < pad) HIPCHECK(hipMemcpy(r + (cap + p) * esz, s, std::min<uint64_t>(n, pad - p) * esz, hipMemcpyHostToDevice));
-      s += n * esz;
-      first += n;
-      count -= n;
-    }
-  }
-
-  // make CTAs [lo, hi) of slot `slot` resident (growing the rings when the
-  // range does not fit); `full`: rewrite the whole range, else append
-  // [avail, hi)
-  void fill_window(uint32_t slot, uint32_t lo, uint32_t hi, bool full) {
-    SlotBufs& sb = bufs_[slot];
-    const ReadyKernel& k = *sb.rk;
-    const uint32_t wpc = k.warps_per_cta;
-    while (hi - lo > sb.ccap) { sb.ccap <<= 1; full = true; }
-    while (sb.ib[hi] - sb.ib[lo] > sb.icap) { sb.icap <<= 1; full = true; }
-    while (sb.ab[hi] - sb.ab[lo] > sb.acap) { sb.acap <<= 1; full = true; }
-    auto ensure = [&](void*& d, size_t& cap, size_t bytes) {
-      if (d && cap >= bytes) return;
-      if (d) HIPCHECK(hipFree(d));
-      cap = bytes;
-      HIPCHECK(hipMalloc(&d, cap));
-    };
-    ensure(sb.insts, sb.cap_insts, sb.icap * sizeof(TInst));
-    ensure(sb.accs, sb.cap_accs, (sb.acap + kMaxAccess) * sizeof(TAcc));
-    ensure(sb.streams, sb.cap_streams, sb.ccap * wpc * sizeof(WStream));
-    const uint32_t from = full ? lo : std::max(lo, sb.avail);
-    if (hi > from) {
-      ring_write(sb.insts, sizeof(TInst), sb.icap, 0, k.insts.data(), sb.ib[from], sb.ib[hi] - sb.ib[from]);
-      if (sb.ab[hi] > sb.ab[from])
-        ring_write(sb.accs, sizeof(TAcc), sb.acap, kMaxAccess, k.accs.data(), sb.ab[from], sb.ab[hi] - sb.ab[from]);
-      ring_write(sb.streams, sizeof(WStream) * wpc, sb.ccap, 0, k.streams.data(), from, hi - from);
-    }
-    sb.lo = lo;
-    sb.avail = hi;
-    ++refills_;
-    KernelDesc& d = kt_.k[slot];
-    d.insts = reinterpret_cast<const TInst*>(sb.insts);
-    d.accs = reinterpret_cast<const TAcc*>(sb.accs);
-    d.streams = reinterpret_cast<const WStream*>(sb.streams);
-    d.imask = (uint32_t)(sb.icap - 1);
-    d.amask = (uint32_t)(sb.acap - 1);
-    d.cmask = (uint32_t)(sb.ccap - 1);
-    d.cta_avail = hi;
-    note_residency();
-  }
-
-  // before every engine launch: for each streamed kernel, drop the CTAs
-  // every SM is done with and stream in up to the window past the dispatch
-  // cursor, so the next epochs' dispatch (epoch.h dispatch_bound) finds
-  // them resident
-  void ensure_windows() {
-    uint32_t streamed = 0;
-    for (uint32_t s = 0; s < (uint32_t)kMaxConc; ++s)
-      if ((kt_.active >> s & 1u) && bufs_[s].streamed && kt_.k[s].cta_avail < kt_.k[s].n_cta) streamed |= 1u << s;
-    if (!streamed) return;
-    // replicated dispatch state (SM 0) and every SM's resident CTAs
+  // the dispatch state a trace window follows: replicated cursors (SM 0) and
+  // every SM's resident CTAs, read back from the device
+  void read_dispatch(DispatchView& v) {
     const size_t off_d = offsetof(SMState, k_uid);
     const size_t len_d = offsetof(SMState, next_ctax) + sizeof(SMState::next_ctax) - off_d;
     std::vector<char> disp(len_d);
     HIPCHECK(hipMemcpy(disp.data(), reinterpret_cast<char*>(d_sms_) + off_d, len_d, hipMemcpyDeviceToHost));
-    const uint32_t* k_uid = reinterpret_cast<const uint32_t*>(disp.data() + (offsetof(SMState, k_uid) - off_d));
-    const uint32_t* next = reinterpret_cast<const uint32_t*>(disp.data() + (offsetof(SMState, next_cta) - off_d));
-    const uint32_t* nextx = reinterpret_cast<const uint32_t*>(disp.data() + (offsetof(SMState, next_ctax) - off_d));
+    memcpy(v.k_uid, disp.data() + (offsetof(SMState, k_uid) - off_d), sizeof(v.k_uid));
+    memcpy(v.next_cta, disp.data() + (offsetof(SMState, next_cta) - off_d), sizeof(v.next_cta));
+    memcpy(v.next_ctax, disp.data() + (offsetof(SMState, next_ctax) - off_d), sizeof(v.next_ctax));
     const size_t off_c = offsetof(SMState, cta_id);
     const size_t len_c = offsetof(SMState, cta_wbase) - off_c;
     std::vector<char> ctas((size_t)c_.n_sm * len_c);
     HIPCHECK(hipMemcpy2D(ctas.data(), len_c, reinterpret_cast<char*>(d_sms_) + off_c, sizeof(SMState), len_c, c_.n_sm,
                          hipMemcpyDeviceToHost));
-    for (uint32_t s = 0; s < (uint32_t)kMaxConc; ++s) {
-      if (!(streamed >> s & 1u)) continue;
-      const KernelDesc& kd = kt_.k[s];
-      SlotBufs& sb = bufs_[s];
-      const bool fresh = k_uid[s] != kd.uid;  // not dispatched from yet (cursors reset at its first epoch)
-      uint32_t nx0 = fresh ? 0u : next[s];
-      uint32_t nxx[kMaxXcd] = {};
-      if (!fresh)
-        for (int xi = 0; xi < kMaxXcd; ++xi) nxx[xi] = nextx[s * kMaxXcd + xi];
-      // lowest CTA still needed: resident on an SM, or the first undispatched
-      uint64_t lo = kd.n_cta;
-      if (c_.n_xcd > 1) {
-        for (uint32_t xi = 0; xi < c_.n_xcd; ++xi) {
-          const uint64_t ncx = kd.n_cta > xi ? (kd.n_cta - xi + c_.n_xcd - 1) / c_.n_xcd : 0;
-          if (nxx[xi] < ncx) lo = std::min<uint64_t>(lo, xi + (uint64_t)c_.n_xcd * nxx[xi]);
-        }
-      } else {
-        lo = std::min<uint64_t>(lo, nx0);
-      }
-      if (!fresh)
-        for (uint32_t m = 0; m < c_.n_sm; ++m) {
-          const char* e = ctas.data() + (size_t)m * len_c;
-          const uint32_t* id = reinterpret_cast<const uint32_t*>(e);
-          const uint8_t* valid = reinterpret_cast<const uint8_t*>(e + (offsetof(SMState, cta_valid) - off_c));
-          const uint8_t* ks = reinterpret_cast<const uint8_t*>(e + (offsetof(SMState, cta_ks) - off_c));
-          for (int i = 0; i < kMaxCta; ++i)
-            if (valid[i] && ks[i] == s) lo = std::min<uint64_t>(lo, id[i]);
-        }
-      const uint64_t bound = dispatch_bound(c_, kd, nx0, nxx);
-      const uint32_t need = (uint32_t)std::min<uint64_t>(kd.n_cta, bound + 1);
-      if (need <= sb.avail && lo >= sb.lo) continue;  // the window still covers the next epochs
-      const uint32_t lo32 = (uint32_t)std::min<uint64_t>(lo, need);
-      // aim a whole window past the oldest CTA still needed, at least `need`,
-      // shrunk to what the rings hold (they grow only when `need` does not fit)
-      uint32_t hi = (uint32_t)std::min<uint64_t>(kd.n_cta, std::max<uint64_t>(need, lo32 + sb.w_ctas));
-      auto fits = [&](uint32_t h) {
-        return h - lo32 <= sb.ccap && sb.ib[h] - sb.ib[lo32] <= sb.icap && sb.ab[h] - sb.ab[lo32] <= sb.acap;
-      };
-      if (fits(need)) {
-        uint32_t a = need, b = hi;  // largest fitting end in [need, hi]
-        while (a < b) {
-          const uint32_t m = a + (b - a + 1) / 2;
-          if (fits(m)) a = m;
-          else b = m - 1;
-        }
-        hi = a;
-      } else {
-        hi = need;
-      }
-      const bool overlap = lo32 >= sb.lo && lo32 <= sb.avail;
-      fill_window(s, lo32, hi, !overlap);
+    v.sms.resize(c_.n_sm);
+    for (uint32_t m = 0; m < c_.n_sm; ++m) {
+      const char* e = ctas.data() + (size_t)m * len_c;
+      memcpy(v.sms[m].cta_id, e, sizeof(v.sms[m].cta_id));
+      memcpy(v.sms[m].cta_valid, e + (offsetof(SMState, cta_valid) - off_c), sizeof(v.sms[m].cta_valid));
+      memcpy(v.sms[m].cta_ks, e + (offsetof(SMState, cta_ks) - off_c), sizeof(v.sms[m].cta_ks));
     }
-  }
-
-  void note_residency() {
-    uint64_t b = 0;
-    for (const SlotBufs& sb : bufs_) b += sb.cap_insts + sb.cap_accs + sb.cap_streams;
-    resident_peak_ = std::max(resident_peak_, b);
   }
 
  public:
   void trace_residency(uint64_t* peak_bytes, uint64_t* refills) const override {
-    *peak_bytes = resident_peak_;
-    *refills = refills_;
+    *peak_bytes = tw_.resident_peak;
+    *refills = tw_.refills;
   }
 
  private:
@@ -1017,14 +835,6 @@ class GpuEngine : public Engine {
     HIPCHECK(hipMemcpy(d_cfg_, &c_, sizeof(SimCfg), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_cfg), &c_, sizeof(SimCfg), sizeof(SimCfg) * (size_t)cfg_slot_,
                                hipMemcpyHostToDevice));
-  }
-  void upload(void*& d, size_t& cap, const void* h, size_t bytes) {
-    if (bytes > cap || !d) {
-      if (d) HIPCHECK(hipFree(d));
-      cap = bytes + bytes / 4 + 4096;
-      HIPCHECK(hipMalloc(&d, cap));
-    }
-    if (bytes && h) HIPCHECK(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice));
   }
   void release() {
     auto fr = [](void* p) {
@@ -1045,11 +855,7 @@ class GpuEngine : public Engine {
     fr(d_mall_);
     fr(d_trace_ev_);
     fr(d_trace_cnt_);
-    for (SlotBufs& b : bufs_) {
-      fr(b.insts);
-      fr(b.accs);
-      fr(b.streams);
-    }
+    tw_.release();
     fr(d_kt_);
     if (h_ctl_) (void)hipHostFree(h_ctl_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -1077,21 +883,20 @@ class GpuEngine : public Engine {
   GpuCtl* h_ctl_ = nullptr;
   TraceEv* d_trace_ev_ = nullptr;
   uint32_t* d_trace_cnt_ = nullptr;
-  struct SlotBufs {  // device copies of one kernel slot's trace
-    void* insts = nullptr;
-    void* accs = nullptr;
-    void* streams = nullptr;
-    size_t cap_insts = 0, cap_accs = 0, cap_streams = 0;
-    // streaming window (-gpu_trace_window)
-    const ReadyKernel* rk = nullptr;
-    bool streamed = false;
-    uint64_t w_ctas = 0;              // window target in CTAs
-    uint32_t lo = 0, avail = 0;       // resident CTAs [lo, avail)
-    uint64_t icap = 0, acap = 0, ccap = 0;  // ring entries (powers of two)
-    uint64_t alloc_i = 0, alloc_a = 0, alloc_c = 0;
-    std::vector<uint32_t> ib, ab;     // per-CTA first instruction / access index (+ end)
+  // device rings / whole copies of the running kernels' traces
+  struct DevMem {
+    static constexpr bool kHost = false;
+    void* alloc(size_t n) {
+      void* p = nullptr;
+      HIPCHECK(hipMalloc(&p, n));
+      return p;
+    }
+    void free(void* p) {
+      if (p) (void)hipFree(p);
+    }
+    void write(void* d, const void* h, size_t n) { HIPCHECK(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); }
   };
-  SlotBufs bufs_[kMaxConc];
+  TraceWindows<DevMem> tw_;
   KernelTab kt_{};
   KernelTab* d_kt_ = nullptr;
   uint32_t cap_req_ = 0, cap_rep_ = 0;
@@ -1101,7 +906,6 @@ class GpuEngine : public Engine {
   bool sliced_ = false;  // more units than blocks: the time-slicing kernel
   uint64_t* d_prof_ = nullptr;
   uint32_t* d_ework_ = nullptr;
-  uint64_t resident_peak_ = 0, refills_ = 0;
 
  public:
   // per-stage shader-clock totals: [0] = mean over SM blocks, [1] = mean over channel blocks

@@ -534,26 +534,135 @@ HostKernel load_kernel(const std::string& path) {
   return load_kernel_text(path);
 }
 
+// one instruction line of a text trace appended to k (its warp's stream was
+// opened by the "insts = " line before)
+static void parse_inst_line(HostKernel& k, const std::string& line, std::unordered_map<std::string, OpInfo>& opcache,
+                            std::string& tok) {
+  const KernelHeader& h = k.h;
+  Tok t{line.data(), line.data() + line.size()};
+  long long dv;
+  if (h.trace_version && h.trace_version < 3) {
+    for (int i = 0; i < 4; ++i) t.dec(dv);
+  }
+  const bool cdna = h.binary_version >= 900;
+  uint64_t pc = 0, mask = 0;
+  t.hex(pc);
+  t.hex(mask);
+  TInst in{};
+  in.pc = (uint32_t)pc;
+  in.mask = mask;
+  in.mem = kNoMem;
+  long long nd = 0;
+  t.dec(nd);
+  for (long long i = 0; i < nd; ++i) {
+    t.next(tok);
+    if (i < 2) in.dst[i] = cdna ? reg_of_cdna(tok) : reg_of(tok);
+  }
+  std::string opstr;
+  t.next(opstr);
+  long long ns = 0;
+  t.dec(ns);
+  for (long long i = 0; i < ns; ++i) {
+    t.next(tok);
+    if (i < 5) in.src[i] = cdna ? reg_of_cdna(tok) : reg_of(tok);
+  }
+  long long mw = 0;
+  t.dec(mw);
+  auto oc = opcache.find(opstr);
+  if (oc == opcache.end()) oc = opcache.emplace(opstr, decode_opcode(opstr, h.binary_version)).first;
+  const OpInfo& oi = oc->second;
+  if (!oi.known) k.unknown_opcodes++;
+  in.opcode = oi.opcode;
+  in.cls = oi.cls;
+  in.space = oi.space;
+  in.flags = oi.flags;
+  in.width = 0;
+  if (mw > 0) {
+    long long mode = 0;
+    t.dec(mode);
+    TMem m{};
+    m.list = kNoMem;
+    const int nact = __builtin_popcountll(mask);
+    if (mode == 1) {
+      uint64_t base = 0;
+      long long stride = 0;
+      t.hex(base);
+      t.dec(stride);
+      m.base = base;
+      m.stride = (int32_t)stride;
+    } else if (mode == 2) {
+      uint64_t base = 0;
+      t.hex(base);
+      m.base = base;
+      m.list = (uint32_t)k.addrs.size();
+      uint64_t last = base;
+      k.addrs.push_back(base);
+      for (int i = 1; i < nact; ++i) {
+        long long d = 0;
+        t.dec(d);
+        last = last + (uint64_t)d;
+        k.addrs.push_back(last);
+      }
+    } else {
+      m.list = (uint32_t)k.addrs.size();
+      for (int i = 0; i < nact; ++i) {
+        uint64_t a = 0;
+        t.hex(a);
+        k.addrs.push_back(a);
+      }
+      m.base = nact ? k.addrs[m.list] : 0;
+    }
+    // width from the opcode (the tracer's value can be wrong, reference
+    // trace_parser.cc:172-174)
+    in.width = oi.width ? oi.width : (uint8_t)std::min<long long>(mw, 255);
+    // generic LD/ST: resolve the space from the first active address
+    if (in.space == S_NONE && (in.cls == OC_LOAD || in.cls == OC_STORE)) {
+      uint64_t a0 = m.base;
+      if (h.shmem_base == 0 || h.local_base == 0) in.space = S_SHARED;
+      else if (a0 >= h.shmem_base && a0 < h.local_base) in.space = S_SHARED;
+      else if (a0 >= h.local_base && a0 < h.local_base + (1ull << 30)) in.space = S_LOCAL;
+      else in.space = S_GLOBAL;
+    }
+    in.mem = (uint32_t)k.mems.size();
+    k.mems.push_back(m);
+  } else if (oi.flags & F_MEM) {
+    // memory op without addresses (all lanes predicated off)
+    in.width = oi.width;
+    if (in.space == S_NONE) in.space = S_SHARED;
+  }
+  in.lat = oi.half_ii ? 0x8000 : 0;  // marker consumed by coalesce_kernel (initiation interval halved)
+  if (oi.flags & F_WAITCNT) in.lat = waitcnt_counts(opstr);
+  k.insts.push_back(in);
+  k.thread_insts += (uint64_t)__builtin_popcountll(mask);
+}
+
+static void read_text_header(std::istream& f, KernelHeader& h) {
+  std::string line;
+  while (std::getline(f, line)) {
+    if (line.empty()) continue;
+    if (line[0] == '#') break;
+    if (line[0] == '-') parse_header_line(h, line);
+  }
+}
+
+static void shape_of(const KernelHeader& h, uint32_t& wpc, uint32_t& n_cta) {
+  const uint32_t ws = h.warp_size ? h.warp_size : 32;
+  const uint32_t threads = h.block[0] * h.block[1] * h.block[2];
+  wpc = (threads + ws - 1) / ws;
+  n_cta = h.grid[0] * h.grid[1] * h.grid[2];
+}
+
 HostKernel load_kernel_text(const std::string& path) {
   std::ifstream f(path);
   if (!f.is_open()) throw std::runtime_error("Unable to open file: " + path);
   HostKernel k;
   std::string line;
-  // header
-  while (std::getline(f, line)) {
-    if (line.empty()) continue;
-    if (line[0] == '#') break;
-    if (line[0] == '-') parse_header_line(k.h, line);
-  }
+  read_text_header(f, k.h);
   KernelHeader& h = k.h;
-  const uint32_t ws = h.warp_size ? h.warp_size : 32;
-  const uint32_t threads = h.block[0] * h.block[1] * h.block[2];
-  k.warps_per_cta = (threads + ws - 1) / ws;
-  k.n_cta = h.grid[0] * h.grid[1] * h.grid[2];
+  shape_of(h, k.warps_per_cta, k.n_cta);
   k.streams.assign((size_t)k.n_cta * k.warps_per_cta, WStream{0, 0});
   k.mems.reserve(1024);
-  std::vector<uint64_t> lane_addr(64);
-  uint32_t cta = 0, warp = 0, expect = 0, got = 0;
+  uint32_t cta = 0, warp = 0, expect = 0;
   bool in_tb = false;
   std::string tok;
   std::unordered_map<std::string, OpInfo> opcache;
@@ -582,117 +691,188 @@ HostKernel load_kernel_text(const std::string& path) {
     }
     if (line.rfind("insts", 0) == 0) {
       sscanf(line.c_str(), "insts = %u", &expect);
-      got = 0;
       WStream& s = k.streams[(size_t)cta * k.warps_per_cta + warp];
       s.begin = (uint32_t)k.insts.size();
       s.count = expect;
-      k.insts.reserve(k.insts.size() + expect);
       continue;
     }
-    // instruction line
-    Tok t{line.data(), line.data() + line.size()};
-    long long dv;
-    if (h.trace_version && h.trace_version < 3) {
-      for (int i = 0; i < 4; ++i) t.dec(dv);
-    }
-    const bool cdna = h.binary_version >= 900;
-    uint64_t pc = 0, mask = 0;
-    t.hex(pc);
-    t.hex(mask);
-    TInst in{};
-    in.pc = (uint32_t)pc;
-    in.mask = mask;
-    in.mem = kNoMem;
-    long long nd = 0;
-    t.dec(nd);
-    for (long long i = 0; i < nd; ++i) {
-      t.next(tok);
-      if (i < 2) in.dst[i] = cdna ? reg_of_cdna(tok) : reg_of(tok);
-    }
-    std::string opstr;
-    t.next(opstr);
-    long long ns = 0;
-    t.dec(ns);
-    for (long long i = 0; i < ns; ++i) {
-      t.next(tok);
-      if (i < 5) in.src[i] = cdna ? reg_of_cdna(tok) : reg_of(tok);
-    }
-    long long mw = 0;
-    t.dec(mw);
-    auto oc = opcache.find(opstr);
-    if (oc == opcache.end()) oc = opcache.emplace(opstr, decode_opcode(opstr, h.binary_version)).first;
-    const OpInfo& oi = oc->second;
-    if (!oi.known) k.unknown_opcodes++;
-    in.opcode = oi.opcode;
-    in.cls = oi.cls;
-    in.space = oi.space;
-    in.flags = oi.flags;
-    in.width = 0;
-    if (mw > 0) {
-      long long mode = 0;
-      t.dec(mode);
-      TMem m{};
-      m.list = kNoMem;
-      const int nact = __builtin_popcountll(mask);
-      if (mode == 1) {
-        uint64_t base = 0;
-        long long stride = 0;
-        t.hex(base);
-        t.dec(stride);
-        m.base = base;
-        m.stride = (int32_t)stride;
-      } else if (mode == 2) {
-        uint64_t base = 0;
-        t.hex(base);
-        m.base = base;
-        m.list = (uint32_t)k.addrs.size();
-        uint64_t last = base;
-        k.addrs.push_back(base);
-        for (int i = 1; i < nact; ++i) {
-          long long d = 0;
-          t.dec(d);
-          last = last + (uint64_t)d;
-          k.addrs.push_back(last);
-        }
-      } else {
-        m.list = (uint32_t)k.addrs.size();
-        for (int i = 0; i < nact; ++i) {
-          uint64_t a = 0;
-          t.hex(a);
-          k.addrs.push_back(a);
-        }
-        m.base = nact ? k.addrs[m.list] : 0;
-      }
-      // width from the opcode (the tracer's value can be wrong, reference
-      // trace_parser.cc:172-174)
-      in.width = oi.width ? oi.width : (uint8_t)std::min<long long>(mw, 255);
-      // generic LD/ST: resolve the space from the first active address
-      if (in.space == S_NONE && (in.cls == OC_LOAD || in.cls == OC_STORE)) {
-        uint64_t a0 = m.base;
-        if (h.shmem_base == 0 || h.local_base == 0) in.space = S_SHARED;
-        else if (a0 >= h.shmem_base && a0 < h.local_base) in.space = S_SHARED;
-        else if (a0 >= h.local_base && a0 < h.local_base + (1ull << 30)) in.space = S_LOCAL;
-        else in.space = S_GLOBAL;
-      }
-      in.mem = (uint32_t)k.mems.size();
-      k.mems.push_back(m);
-    } else if (oi.flags & F_MEM) {
-      // memory op without addresses (all lanes predicated off)
-      in.width = oi.width;
-      if (in.space == S_NONE) in.space = S_SHARED;
-    }
-    uint32_t lat = 1, ii = 1;
-    (void)lat;
-    (void)ii;
-    if (oi.half_ii) in.flags |= 0;  // applied by coalesce_kernel from the config
-    in.lat = oi.half_ii ? 0x8000 : 0;  // marker consumed by coalesce_kernel
-    if (oi.flags & F_WAITCNT) in.lat = waitcnt_counts(opstr);
-    k.insts.push_back(in);
-    k.thread_insts += (uint64_t)__builtin_popcountll(mask);
-    ++got;
+    parse_inst_line(k, line, opcache, tok);
   }
   k.warp_insts = k.insts.size();
   return k;
+}
+
+// ---------------------------------------------------------------------------
+// Per-CTA reader (host streaming).  Thread blocks are read in file order;
+// when the file does not hold them in linear-id order (or skips one), the
+// reader indexes the byte offset of every "thread block" line once and seeks.
+struct KernelReader::Impl {
+  std::string path;
+  std::ifstream f;
+  KernelHeader h;
+  SimCfg c;
+  uint32_t wpc = 0, n_cta = 0, next = 0;
+  std::string pending;  // a "thread block" line read past the previous CTA
+  bool have_pending = false;
+  bool indexed = false;
+  std::vector<int64_t> off;  // byte offset of each CTA's "thread block" line (-1: none)
+  std::unordered_map<std::string, OpInfo> opcache;
+  std::string tok, line;
+  HostKernel hk;
+
+  uint32_t id_of(const std::string& l) const {
+    uint32_t x = 0, y = 0, z = 0;
+    sscanf(l.c_str(), "thread block = %u,%u,%u", &x, &y, &z);
+    const uint64_t id = (uint64_t)z * h.grid[1] * h.grid[0] + (uint64_t)y * h.grid[0] + x;
+    if (id >= n_cta) throw std::runtime_error("thread block id outside grid in " + path);
+    return (uint32_t)id;
+  }
+  void build_index() {
+    off.assign(n_cta, -1);
+    f.clear();
+    f.seekg(0);
+    for (;;) {
+      const int64_t pos = (int64_t)f.tellg();
+      if (!std::getline(f, line)) break;
+      if (line.rfind("thread block", 0) == 0) off[id_of(line)] = pos;
+    }
+    f.clear();
+    indexed = true;
+  }
+  // position the stream just after CTA `t`'s "thread block" line; false if
+  // the trace has no such thread block (an empty CTA)
+  bool seek_cta(uint32_t t) {
+    if (!indexed) {
+      if (!have_pending) {
+        while (std::getline(f, line))
+          if (line.rfind("thread block", 0) == 0) {
+            pending = line;
+            have_pending = true;
+            break;
+          }
+      }
+      if (have_pending && id_of(pending) == t) {
+        have_pending = false;
+        return true;
+      }
+      build_index();  // out of order, or missing: index once and seek from now on
+    }
+    have_pending = false;
+    if (off[t] < 0) return false;
+    f.clear();
+    f.seekg(off[t]);
+    std::getline(f, line);  // the "thread block" line itself
+    return true;
+  }
+};
+
+KernelReader::KernelReader(const std::string& path, const SimCfg& c) : p_(new Impl()) {
+  p_->path = path;
+  p_->c = c;
+  p_->f.open(path);
+  if (!p_->f.is_open()) {
+    delete p_;
+    throw std::runtime_error("Unable to open file: " + path);
+  }
+  read_text_header(p_->f, p_->h);
+  shape_of(p_->h, p_->wpc, p_->n_cta);
+}
+KernelReader::~KernelReader() { delete p_; }
+const KernelHeader& KernelReader::header() const { return p_->h; }
+uint32_t KernelReader::n_cta() const { return p_->n_cta; }
+uint32_t KernelReader::warps_per_cta() const { return p_->wpc; }
+uint32_t KernelReader::ctas_read() const { return p_->next; }
+
+void KernelReader::next_cta(std::vector<TInst>& insts, std::vector<TAcc>& accs, std::vector<WStream>& streams,
+                            uint64_t ibase, uint64_t abase) {
+  Impl& r = *p_;
+  if (r.next >= r.n_cta) throw std::runtime_error("KernelReader: read past the last CTA of " + r.path);
+  const uint32_t t = r.next++;
+  HostKernel& k = r.hk;
+  k.h = r.h;
+  k.warps_per_cta = r.wpc;
+  k.n_cta = 1;
+  k.insts.clear();
+  k.mems.clear();
+  k.addrs.clear();
+  k.streams.assign(r.wpc, WStream{0, 0});
+  if (r.seek_cta(t)) {
+    uint32_t warp = 0, expect = 0;
+    while (std::getline(r.f, r.line)) {
+      const std::string& line = r.line;
+      if (line.empty() || line[0] == '#') continue;
+      if (line.rfind("thread block", 0) == 0) {
+        r.pending = line;
+        r.have_pending = !r.indexed;
+        break;
+      }
+      if (line.rfind("warp", 0) == 0) {
+        sscanf(line.c_str(), "warp = %u", &warp);
+        if (warp >= r.wpc) throw std::runtime_error("warp id outside block in " + r.path);
+        continue;
+      }
+      if (line.rfind("insts", 0) == 0) {
+        sscanf(line.c_str(), "insts = %u", &expect);
+        k.streams[warp] = WStream{(uint32_t)k.insts.size(), expect};
+          continue;
+      }
+      parse_inst_line(k, line, r.opcache, r.tok);
+    }
+  }
+  k.warp_insts = k.insts.size();
+  ReadyKernel one = coalesce_kernel(k, r.c);
+  // global indices: instruction ibase + n, access abase + n, kept modulo the
+  // ring-index widths (engine/trace_window.h caps the rings below them)
+  const uint64_t i0 = ibase + insts.size(), a0 = abase + accs.size();
+  for (TInst in : one.insts) {
+    if (in.mem != kNoMem) in.mem = (uint32_t)((a0 + in.mem) & kStreamAccMask);
+    insts.push_back(in);
+  }
+  accs.insert(accs.end(), one.accs.begin(), one.accs.end());
+  for (const WStream& w : one.streams) streams.push_back(WStream{(uint32_t)((i0 + w.begin) & kStreamInstMask), w.count});
+}
+
+ReadyKernel open_streamed_kernel(const std::string& path, const SimCfg& c) {
+  ReadyKernel r;
+  r.src = std::make_shared<KernelReader>(path, c);
+  r.h = r.src->header();
+  r.warps_per_cta = r.src->warps_per_cta();
+  r.n_cta = r.src->n_cta();
+  r.ib.assign(1, 0);
+  r.ab.assign(1, 0);
+  return r;
+}
+
+void ReadyKernel::resident(uint32_t lo, uint32_t hi) {
+  if (!src) return;
+  hi = std::min(hi, n_cta);
+  if (lo < cta_lo) throw std::runtime_error("host trace stream: CTA " + std::to_string(lo) + " was already dropped");
+  // read forward to hi
+  while (cta_hi < hi) {
+    src->next_cta(insts, accs, streams, ibase, abase);
+    ++cta_hi;
+    ib.push_back(ibase + insts.size());
+    ab.push_back(abase + accs.size());
+  }
+  // drop the CTAs below lo (the engines are done with them)
+  lo = std::min(lo, cta_hi);
+  if (lo > cta_lo) {
+    const uint32_t nd = lo - cta_lo;
+    const uint64_t di = ib[nd] - ibase, da = ab[nd] - abase;
+    insts.erase(insts.begin(), insts.begin() + (long)di);
+    accs.erase(accs.begin(), accs.begin() + (long)da);
+    streams.erase(streams.begin(), streams.begin() + (long)nd * warps_per_cta);
+    ib.erase(ib.begin(), ib.begin() + nd);
+    ab.erase(ab.begin(), ab.begin() + nd);
+    ibase = ib[0];
+    abase = ab[0];
+    cta_lo = lo;
+    // give memory back once the vectors are mostly slack
+    if (insts.capacity() > 2 * insts.size() + 4096) insts.shrink_to_fit();
+    if (accs.capacity() > 2 * accs.size() + 4096) accs.shrink_to_fit();
+    if (streams.capacity() > 2 * streams.size() + 4096) streams.shrink_to_fit();
+  }
+  host_peak_bytes = std::max(host_peak_bytes, host_bytes());
 }
 
 // ---------------------------------------------------------------------------

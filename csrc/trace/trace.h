@@ -7,6 +7,7 @@
 // are then coalesced for a given SimCfg and uploaded once per kernel.
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -78,8 +79,28 @@ struct HostKernel {
   uint32_t unknown_opcodes = 0;
 };
 
+class KernelReader;  // per-CTA reader of a text kernel trace (below)
+
+// index widths of a host-streamed kernel: warp stream begins are kept modulo
+// 2^28 (begin + count stays below the engines' 2^29 slot field), access
+// indices modulo 2^31 (never kNoMem); the rings are at most that large
+constexpr uint64_t kStreamInstMask = (1ull << 28) - 1;
+constexpr uint64_t kStreamAccMask = (1ull << 31) - 1;
+
 // Coalesced kernel ready for a cycle engine (inst.mem -> first TAcc,
 // inst.width -> number of accesses, or shared-memory conflict degree).
+//
+// Host streaming (-trace_host_budget_mb): a ReadyKernel with a reader `src`
+// holds only the CTAs [cta_lo, cta_hi) of the kernel -- parsed and ingested
+// from the trace file as the engines' trace windows advance
+// (engine/trace_window.h), dropped once every SM is done with them -- so the
+// host's trace memory is bounded by the window, not by the kernel (the
+// reference reads thread blocks from the file as CTAs issue,
+// gpu-simulator/trace-parser/trace_parser.cc:387-447).  Indices stay global:
+// insts[0] is instruction `ibase`, accs[0] access `abase`, streams[0] the
+// first warp of CTA cta_lo; ib / ab give the first instruction / access of
+// CTAs cta_lo..cta_hi.  Without a reader the whole kernel is held (all of
+// these are 0 / empty).
 struct ReadyKernel {
   KernelHeader h;
   uint32_t warps_per_cta = 0;
@@ -89,7 +110,45 @@ struct ReadyKernel {
   std::vector<WStream> streams;
   uint64_t thread_insts = 0;
   uint64_t warp_insts = 0;
+  std::shared_ptr<KernelReader> src;
+  uint32_t cta_lo = 0, cta_hi = 0;
+  uint64_t ibase = 0, abase = 0;
+  std::vector<uint64_t> ib, ab;
+  uint64_t host_peak_bytes = 0;  // largest host footprint of the resident CTAs (streamed kernels)
+  bool streamed() const { return (bool)src; }
+  // make CTAs [lo, hi) resident: parse forward as needed, drop CTAs below lo
+  void resident(uint32_t lo, uint32_t hi);
+  uint64_t host_bytes() const {
+    return insts.capacity() * sizeof(TInst) + accs.capacity() * sizeof(TAcc) + streams.capacity() * sizeof(WStream) +
+           (ib.capacity() + ab.capacity()) * sizeof(uint64_t);
+  }
 };
+
+// Sequential reader of a text kernel trace (.traceg), one thread block at a
+// time, each ingested (coalesced) as soon as it is read.  Thread blocks must
+// come in linear-id order (the format's rule), else it throws.
+class KernelReader {
+ public:
+  KernelReader(const std::string& path, const SimCfg& c);
+  ~KernelReader();
+  const KernelHeader& header() const;
+  uint32_t n_cta() const;
+  uint32_t warps_per_cta() const;
+  // the next CTA's instructions / accesses / warp streams appended to the
+  // vectors; global indices continue from `ibase + insts.size()` (instruction)
+  // and `abase + accs.size()` (access)
+  void next_cta(std::vector<TInst>& insts, std::vector<TAcc>& accs, std::vector<WStream>& streams, uint64_t ibase,
+                uint64_t abase);
+  uint32_t ctas_read() const;
+
+ private:
+  struct Impl;
+  Impl* p_;
+};
+
+// A streamed ReadyKernel for the trace at `path` (text format), nothing
+// resident yet
+ReadyKernel open_streamed_kernel(const std::string& path, const SimCfg& c);
 
 // Synthetic streaming-copy kernel: the memory traffic of a collective on one
 // GPU (RCCL runs collectives as kernels that read the local send buffer and

@@ -299,3 +299,29 @@ def test_trace_window_streaming_gpu_equals_cpu(gpu_mod, tmp_path, extra):
     # dispatch bound of the next epochs (XCD round-robin dispatch spreads
     # that span): about 2 K of the 6 K CTAs are resident here
     assert pw * 2 < pf, (pw, pf)
+
+
+@pytest.mark.parametrize("extra", [{}, {"-sim_xcd": "8", "-sim_mall": "256:16"}], ids=["shared_l2", "xcd_mall"])
+def test_host_streamed_trace_gpu_equals_cpu(gpu_mod, tmp_path, extra):
+    """-trace_host_budget_mb: the text trace is read per thread block as the
+    GPU engine's HBM window advances (host and device windows are the same
+    TraceWindows); results equal the CPU engine on the whole kernel."""
+    import numpy as np
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+    k = KernelBuilder("k_many", (6000, 1, 1), (256, 1, 1), nregs=16)
+    base = k.g.gtid0.astype(np.int64) * 4
+    k.op("LDG.E", [4], [2], base=0x7000_0000 + base, stride=4)
+    k.alu("FFMA", 3, regs=(4, 5, 6))
+    k.op("STG.E", [], [2, 4], base=0x9000_0000 + base, stride=4)
+    k.op("EXIT")
+    kl = rodinia.write_app(str(tmp_path / "many"), [k.build()], text=True)
+    st = sim.simulate(kl, "QV100", engine="gpu",
+                      extra=dict(extra, **{"-trace_host_budget_mb": "0.5", "-gpu_trace_window": "1"}))
+    cpu = sim.simulate(kl, "QV100", engine="cpu", extra=extra)
+    assert (st.tot_cycle, st.tot_insn) == (cpu.tot_cycle, cpu.tot_insn)
+    skip = ("rate", "slowdown", "time")
+    strip = lambda s: {a: v for a, v in s.items() if not any(x in a for x in skip)}
+    assert strip(st.stats) == strip(cpu.stats)
+    assert re.search(r"^trace_host_streamed_kernels: 1$", st.output, re.M)
