@@ -60,10 +60,10 @@ def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
     os.makedirs(bdir, exist_ok=True)
     hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
     inc = " ".join(f"-I{p}" for p in [os.path.join(ROOT, "csrc")] + _pybind_includes())
-    cxxflags = f"-std=c++17 -O3 -g -fPIC -fopenmp -Wall -Wno-unused-variable -Wno-unused-function {inc}"
+    cxxflags = f"-std=c++17 -O3 -g -fPIC -fopenmp -pthread -Wall -Wno-unused-variable -Wno-unused-function {inc}"
     hipflags = (f"-std=c++17 -O3 -fPIC --offload-arch={ARCH} -munsafe-fp-atomics "
                 f"-I{os.path.join(ROOT, 'csrc')}")
-    ldflags = f"-fopenmp -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib"
+    ldflags = f"-fopenmp -pthread -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib"
     lines = [
         "ninja_required_version = 1.3",
         f"cxxflags = {cxxflags}",

@@ -1,11 +1,15 @@
 // CPU reference engine: the cycle model with the sequential lane policy.
-// SMs / channels of one epoch are independent (PDES), so the epoch body is
-// parallelised with OpenMP; results are bit-identical for any thread count.
+// SMs / channels of one epoch are independent (PDES), so the epoch body runs
+// on a persistent thread team (thread_team.h, -sim_cpu_threads); results are
+// bit-identical for any thread count.
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
+#include <functional>
+
 #include "engine.h"
+#include "thread_team.h"
 #include "trace_window.h"
 
 namespace asim {
@@ -184,66 +188,91 @@ class CpuEngine : public Engine {
 
   RunResult run(const RunLimits& lim) override {
     RunResult res;
-    const SimCfg& c = c_;
-    const uint64_t E = c.icnt_latency;
     if (!kt_.active) {
       res.end_cycle = cycle_;
       return res;
     }
-    bool refill = true;
-    for (;;) {
-      // host-streamed traces: bring in the CTAs the next epochs can dispatch
-      // (epoch_decide flags when the window falls short)
-      if (refill) tw_.ensure(kt_, c, [&](DispatchView& v) { read_dispatch(v); });
-      const uint32_t cur = (uint32_t)(epoch_ & 1), prev = cur ^ 1u;
-      const uint64_t t0 = cycle_, t1 = t0 + E;
+    // serial, or a persistent team (thread_team.h): every thread runs the
+    // same epoch loop over an interleaved share of the units, one barrier
+    // per epoch, and evaluates the epoch decision itself (it is a pure
+    // function of the published state), so they all stop at the same epoch
+    const uint32_t nthr = std::max<uint32_t>(1, std::min<uint32_t>(c_.cpu_threads, (uint32_t)(sms_.size() + chs_.size())));
+    bar_.reset(nthr);
+    const uint64_t epoch0 = epoch_, cycle0 = cycle_;
+    uint64_t end_epoch = epoch0, end_cycle = cycle0;
+    std::function<void(uint32_t)> job = [&](uint32_t tid) {
+      const SimCfg& c = c_;
+      const uint64_t E = c.icnt_latency;
       const int nsm = (int)sms_.size(), nch = (int)chs_.size();
-      // serial by default: at 8-cycle epochs the parallel region costs more
-      // than it saves (8 threads measured 8.1k vs 10.8k KIPS serial); whole
-      // simulations run job-parallel instead (parallel/multi_gpu.py)
-      const int nthr = c.cpu_threads > 1 ? (int)c.cpu_threads : 1;
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nthr) if (nthr > 1)
-      for (int i = 0; i < nsm + nch; ++i) {
-        if (i < nsm) {
-          SMState& s = sms_[i];
-          SmCtx x = ctx_sm(cur);
-          sm_epoch<SeqPar>(s, x, *pub_, prev, t0, t1, box_rep_[prev].data(), cnt_rep_[prev].data(), cap_rep_,
-                           c.n_subpart, epoch_);
-          sm_publish<SeqPar>(s, x, *pub_, cur);
-        } else {
-          ChanState& ch = chs_[i - nsm];
-          MemCtx m = ctx_mem(cur, t1);
-          m.mall = mall_.empty() ? nullptr : mall_.data() + (size_t)(i - nsm) * mall_lines(c);
-          chan_epoch<SeqPar>(ch, m, box_req_[prev].data(), cnt_req_[prev].data(), cap_req_, core_fs(c, t0));
-          chan_publish<SeqPar>(ch, m, *pub_, cur);
+      uint64_t epoch = epoch0, cycle = cycle0, epochs = 0;
+      bool refill = true;
+      RunResult r;
+      for (;;) {
+        // host-streamed traces: bring in the CTAs the next epochs can
+        // dispatch (epoch_decide flags when the window falls short)
+        if (refill && tw_.any_streamed()) {
+          if (nthr > 1) bar_.wait();
+          if (tid == 0) tw_.ensure(kt_, c, [&](DispatchView& v) { read_dispatch(v); });
+          if (nthr > 1) bar_.wait();
         }
-      }
-      EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, kt_, epoch_, lim.max_cycle);
-      refill = d.refill != 0;
-      ++epoch_;
-      ++res.epochs;
-      cycle_ = d.next_start;
-      if (d.done) {
-        res.done = true;
-        res.done_mask = d.done;
-        kt_.active &= ~d.done;
-        for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k)
-          if (d.done >> k & 1u) tw_.done(k);
+        const uint32_t cur = (uint32_t)(epoch & 1), prev = cur ^ 1u;
+        const uint64_t t0 = cycle, t1 = t0 + E;
+        // contiguous shares (SMs, then channels, each split evenly): a
+        // thread's units' mailbox counters and published records share cache
+        // lines with its own units, not with every other thread's
+        const int s0 = (int)((uint64_t)nsm * tid / nthr), s1 = (int)((uint64_t)nsm * (tid + 1) / nthr);
+        const int c0 = (int)((uint64_t)nch * tid / nthr), c1 = (int)((uint64_t)nch * (tid + 1) / nthr);
+        for (int q = 0; q < (s1 - s0) + (c1 - c0); ++q) {
+          const int i = q < s1 - s0 ? s0 + q : nsm + c0 + (q - (s1 - s0));
+          if (i < nsm) {
+            SMState& s = sms_[i];
+            SmCtx x = ctx_sm(cur);
+            sm_epoch<SeqPar>(s, x, *pub_, prev, t0, t1, box_rep_[prev].data(), cnt_rep_[prev].data(), cap_rep_,
+                             c.n_subpart, epoch);
+            sm_publish<SeqPar>(s, x, *pub_, cur);
+          } else {
+            ChanState& ch = chs_[i - nsm];
+            MemCtx m = ctx_mem(cur, t1);
+            m.mall = mall_.empty() ? nullptr : mall_.data() + (size_t)(i - nsm) * mall_lines(c);
+            chan_epoch<SeqPar>(ch, m, box_req_[prev].data(), cnt_req_[prev].data(), cap_req_, core_fs(c, t0));
+            chan_publish<SeqPar>(ch, m, *pub_, cur);
+          }
+        }
+        if (nthr > 1) bar_.wait();
+        const EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, kt_, epoch, lim.max_cycle);
+        refill = d.refill != 0;
+        ++epoch;
+        ++epochs;
+        cycle = d.next_start;
+        if (d.done) {
+          r.done = true;
+          r.done_mask = d.done;
+        } else if (d.deadlock) {
+          r.deadlock = true;
+        } else if (d.limit) {
+          r.hit_limit = true;
+          r.cap = true;
+        } else if ((lim.max_cycle && cycle >= lim.max_cycle) || (lim.max_epochs && epochs >= lim.max_epochs)) {
+          r.hit_limit = true;
+        } else {
+          continue;
+        }
         break;
       }
-      if (d.deadlock) {
-        res.deadlock = true;
-        break;
+      if (tid == 0) {
+        r.epochs = epochs;
+        res = r;
+        end_epoch = epoch;
+        end_cycle = cycle;
       }
-      if (d.limit) {
-        res.hit_limit = true;
-        res.cap = true;
-        break;
-      }
-      if ((lim.max_cycle && cycle_ >= lim.max_cycle) || (lim.max_epochs && res.epochs >= lim.max_epochs)) {
-        res.hit_limit = true;
-        break;
-      }
+    };
+    team_.run(nthr, job);
+    epoch_ = end_epoch;
+    cycle_ = end_cycle;
+    if (res.done) {
+      kt_.active &= ~res.done_mask;
+      for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k)
+        if (res.done_mask >> k & 1u) tw_.done(k);
     }
     res.end_cycle = cycle_;
     return res;
@@ -273,6 +302,8 @@ class CpuEngine : public Engine {
     void write(void* d, const void* h, size_t n) { memcpy(d, h, n); }
   };
   TraceWindows<HostMem> tw_;
+  ThreadTeam team_;
+  SpinBarrier bar_;
   std::vector<TraceEv> trace_ev_;
   std::vector<uint32_t> trace_cnt_;
 

@@ -190,6 +190,11 @@ class TraceWindows {
     }
   }
 
+  bool any_streamed() const {
+    for (const Slot& b : s)
+      if (b.rk && b.streamed) return true;
+    return false;
+  }
   uint64_t resident_bytes() const {
     uint64_t t = 0;
     for (const Slot& b : s) t += b.cap_insts + b.cap_accs + b.cap_streams;

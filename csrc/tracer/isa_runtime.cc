@@ -711,7 +711,11 @@ hipError_t hipLaunchKernel(const void* f, dim3 g, dim3 b, void** args, size_t sh
   if (!t.buf_bytes) return launch_streamed(t, id, name, mit->second, real, f, g, b, args, shmem, st, dev);
   Tracer::DevBuf& db = t.bufs[dev];
   if (!db.ptr) {
-    RT_HIP(hipMalloc(&db.ptr, t.buf_bytes));
+    // the runtime's own hipMalloc: this interposer's would retake t.mu (held
+    // here) and the tracer's buffer is not an application allocation
+    using M = hipError_t (*)(void**, size_t);
+    static M real_malloc = (M)dlsym(RTLD_NEXT, "hipMalloc");
+    RT_HIP(real_malloc((void**)&db.ptr, t.buf_bytes));
     RT_HIP(hipMemset(db.ptr, 0, t.buf_bytes));
   } else if (db.last_used) {
     RT_HIP(hipMemset(db.ptr, 0, (size_t)db.last_used * kChunkUnits * 16));
