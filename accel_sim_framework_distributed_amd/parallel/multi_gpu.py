@@ -91,6 +91,10 @@ class DistributedSuite:
             # scheduled like any application (node placement, LPT order)
             self.apps.append(("dp-step", self.dp_step))
         self._calibrating = False
+        # host threads of each application simulated on the CPU engine
+        # (-sim_cpu_threads: the engine's persistent thread team); node mode
+        # widens the applications on the critical path when cores are spare
+        self.threads: Dict[str, int] = {}
         self.sync = PacketCollective() if collective_model == "packet" else CollectiveSync(world)
         # HIP's current device is per host thread: worker threads start on
         # device 0, so every thread this suite creates binds this rank's GPU
@@ -108,9 +112,11 @@ class DistributedSuite:
             import torch
             torch.cuda.set_device(self.device_index)
 
-    def _sim(self, kl: str, engine: Optional[str] = None):
+    def _sim(self, kl: str, engine: Optional[str] = None, threads: int = 1):
         extra = {"-collective_model": self.collective_model}
         eng = engine or ("gpu" if self.engine == "node" else self.engine)
+        if eng == "cpu" and threads > 1:
+            extra["-sim_cpu_threads"] = str(threads)
         args = build_args(self.config, kl, eng, extra)
         return self.mod.Simulator(args, self.verbose)
 
@@ -143,8 +149,25 @@ class DistributedSuite:
                 n = len(os.sched_getaffinity(0))
             except AttributeError:  # pragma: no cover - non-Linux
                 n = os.cpu_count() or 1
+            q = self.cgroup_cores()
+            if q:
+                n = min(n, q)
             n //= max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
         return max(1, n - reserve)
+
+    @staticmethod
+    def cgroup_cores() -> int:
+        """Cores the cgroup's CPU quota grants (cgroup v2 cpu.max), 0 when
+        unlimited or unknown: the affinity mask can list every core of a
+        machine whose quota is a fraction of them."""
+        try:
+            with open("/sys/fs/cgroup/cpu.max") as f:
+                q, per = f.read().split()[:2]
+            if q == "max":
+                return 0
+            return max(1, -(-int(q) // int(per)))
+        except (OSError, ValueError):
+            return 0
 
     _rpg_cache: Optional[int] = None
 
@@ -188,7 +211,8 @@ class DistributedSuite:
             self.weights[app] = dt
             self.times[(app, engine or ("gpu" if self.engine == "node" else self.engine))] = dt
             return r
-        s = self._sim(kl, engine)
+        eng = engine or ("gpu" if self.engine == "node" else self.engine)
+        s = self._sim(kl, engine, self.threads.get(app, 1) if eng == "cpu" else 1)
         rc = s.run()
         if rc != 0:
             raise RuntimeError(f"{app}: simulation failed (deadlock={s.deadlock})\n{s.output[-1500:]}")
@@ -243,40 +267,119 @@ class DistributedSuite:
             load[i] += t
         return max(load) if ts else 0.0
 
+    @staticmethod
+    def _cores_span(jobs: List, cores: int) -> float:
+        """Makespan of (seconds, threads) jobs list-scheduled longest first on
+        `cores` host cores (a job starts when its threads' cores are free)."""
+        free = [0.0] * max(1, cores)
+        end = 0.0
+        for t, k in sorted(jobs, key=lambda x: -x[0]):
+            k = max(1, min(k, len(free)))
+            free.sort()
+            start = free[k - 1]
+            for i in range(k):
+                free[i] = start + t
+            end = max(end, start + t)
+        return end
+
     def plan(self):
         """Engine per application minimising the predicted makespan
-        (exhaustive over the subsets sent to the GPU; LPT inside each pool)."""
+        (exhaustive over the subsets sent to the GPU; LPT over the GPU slots,
+        list scheduling over the host cores with each CPU application's
+        thread count)."""
         gslots = max(1, self.concurrency())
         cslots = self.cpu_slots(reserve=gslots)
         names = [a for a, _ in self.apps]
         tg = [self.times.get((a, "gpu"), 1.0) for a in names]
         tc = [self.times.get((a, "cpu"), 1.0) for a in names]
+        th = [self.threads.get(a, 1) for a in names]
         n = len(names)
         best = (float("inf"), 0)
         for m in range(1 << n) if n <= 16 else [(1 << n) - 1]:
             g = [tg[i] for i in range(n) if m >> i & 1]
-            c = [tc[i] for i in range(n) if not m >> i & 1]
-            span = max(self._lpt(g, gslots), self._lpt(c, cslots))
+            c = [(tc[i], th[i]) for i in range(n) if not m >> i & 1]
+            span = max(self._lpt(g, gslots), self._cores_span(c, cslots))
             if span < best[0]:
                 best = (span, m)
         self.assignment = {names[i]: ("gpu" if best[1] >> i & 1 else "cpu") for i in range(n)}
         self.predicted_span = best[0]
         return self.assignment
 
+    def widen(self, max_threads: int = 8, reps: int = 2) -> Dict[str, int]:
+        """Give host threads to the CPU-engine application on the critical
+        path while cores are spare: double its -sim_cpu_threads, re-time it
+        (fastest of `reps`), keep the change if it cut the time by >= 15 %,
+        re-plan, repeat.  Stops when the critical path is on the GPU, the
+        critical application stops scaling, or the cores run out."""
+        gslots = max(1, self.concurrency())
+        cores = self.cpu_slots(reserve=gslots)
+        kl_of = dict(self.apps)
+        tried = set()
+        self._calibrating = True
+        try:
+            for _ in range(12):
+                self.plan()
+                cpu_apps = [a for a, e in self.assignment.items() if e == "cpu"]
+                if not cpu_apps:
+                    break
+                crit = max(cpu_apps, key=lambda a: self.times[(a, "cpu")])
+                if self.times[(crit, "cpu")] < 0.999 * self.predicted_span or crit in tried:
+                    break  # the GPU side sets the span, or the critical app does not scale
+                k = self.threads.get(crit, 1)
+                nk = min(max_threads, 2 * k)
+                used = sum(self.threads.get(a, 1) for a in cpu_apps if a != crit)
+                if nk <= k or used + nk > cores:
+                    break
+                old = self.times[(crit, "cpu")]
+                self.threads[crit] = nk
+                t = float("inf")
+                for _r in range(max(1, reps)):
+                    self._run_app((crit, kl_of[crit]), "cpu")
+                    t = min(t, self.times[(crit, "cpu")])
+                if t <= 0.85 * old:
+                    self.times[(crit, "cpu")] = t
+                else:
+                    self.threads[crit] = k
+                    self.times[(crit, "cpu")] = old
+                    tried.add(crit)
+        finally:
+            self._calibrating = False
+        self.plan()
+        return {a: k for a, k in self.threads.items() if k > 1}
+
     def _step_node(self):
+        import threading
         from concurrent.futures import ThreadPoolExecutor
         if not getattr(self, "assignment", None):
             if not all((a, e) in self.times for a, _ in self.apps for e in ("gpu", "cpu")):
                 self.calibrate()
+                self.widen()
             self.plan()
         gslots = max(1, self.concurrency())
         cslots = self.cpu_slots(reserve=gslots)
         ga = sorted([x for x in self.apps if self.assignment[x[0]] == "gpu"], key=lambda x: -self.times[(x[0], "gpu")])
         ca = sorted([x for x in self.apps if self.assignment[x[0]] == "cpu"], key=lambda x: -self.times[(x[0], "cpu")])
+        # host cores as tokens: an application takes its threads' worth before
+        # it starts, so thread teams never oversubscribe the cores
+        cv = threading.Condition()
+        free = [cslots]
+
+        def run_cpu(a):
+            k = max(1, min(self.threads.get(a[0], 1), cslots))
+            with cv:
+                cv.wait_for(lambda: free[0] >= k)
+                free[0] -= k
+            try:
+                return self._run_app(a, "cpu")
+            finally:
+                with cv:
+                    free[0] += k
+                    cv.notify_all()
+
         with ThreadPoolExecutor(max_workers=gslots, initializer=self._bind_device) as gx, \
                 ThreadPoolExecutor(max_workers=max(1, min(cslots, len(ca) or 1))) as cx:
             fg = [gx.submit(self._run_app, a, "gpu") for a in ga]
-            fc = [cx.submit(self._run_app, a, "cpu") for a in ca]
+            fc = [cx.submit(run_cpu, a) for a in ca]
             return [f.result() for f in fg + fc]
 
     def _run_allreduce(self):
@@ -297,6 +400,8 @@ class DistributedSuite:
         extra = {"-collective_model": self.collective_model, "-gpgpu_concurrent_kernel_sm": "1",
                  "-collective_mem_traffic": "1"}
         eng = engine or ("gpu" if self.engine == "node" else self.engine)
+        if eng == "cpu" and self.threads.get("dp-step", 1) > 1:
+            extra["-sim_cpu_threads"] = str(self.threads["dp-step"])
         s = self.mod.Simulator(build_args(self.config, self.dp_step, eng, extra), self.verbose)
         n0 = len(getattr(self.sync, "events", []))
         if coupled:

@@ -169,6 +169,9 @@ def main() -> int:
     if engine == "node":
         # untimed: time every application on both engines, then place them
         suite.calibrate()
+        # host threads for the CPU-engine applications on the critical path
+        # (spare cores only; each app's team is re-timed before it is kept)
+        suite.widen()
         suite.plan()
     for _ in range(a.warmup):
         suite.step()
@@ -239,7 +242,9 @@ def main() -> int:
                 "engine": engine,
                 **({"node_assignment": suite.assignment,
                     "node_calibration_s": suite.calibration,
-                    "node_predicted_step_ms": round(suite.predicted_span * 1e3, 1)} if engine == "node" else {}),
+                    "node_predicted_step_ms": round(suite.predicted_span * 1e3, 1),
+                    "node_cpu_threads": {k: v for k, v in suite.threads.items() if v > 1},
+                    "node_host_cores": suite.cpu_slots(reserve=max(1, suite.concurrency()))} if engine == "node" else {}),
                 "apps": len(suite.apps),
                 "sim_insn_per_step_per_rank": int(insn / max(1, a.steps)),
                 "sim_cycles_per_step_per_rank": int(cycles / max(1, a.steps)),

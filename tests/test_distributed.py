@@ -163,6 +163,40 @@ def test_node_plan_places_apps_by_makespan(native, tmp_path, monkeypatch):
     assert abs(s.predicted_span - 0.5) < 1e-9
 
 
+def test_node_widen_gives_threads_to_critical_cpu_app(native, tmp_path, monkeypatch):
+    """Spare host cores go to the CPU-engine application on the critical path
+    (-sim_cpu_threads), kept only while re-timing shows it scales; the plan
+    list-schedules thread teams on the cores."""
+    from accel_sim_framework_distributed_amd.parallel.multi_gpu import DistributedSuite
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    apps = ["nn-rodinia-2.0-ft", "pathfinder-rodinia-2.0-ft", "backprop-rodinia-2.0-ft"]
+    rodinia.generate_suite(str(tmp_path), apps)
+    monkeypatch.setenv("ASIM_CPU_JOBS", "9")  # 1 GPU slot + 8 cores
+    s = DistributedSuite(str(tmp_path), engine="node")
+    base = {"nn-rodinia-2.0-ft": 0.1, "pathfinder-rodinia-2.0-ft": 0.3, "backprop-rodinia-2.0-ft": 1.0}
+    scales = {"backprop-rodinia-2.0-ft": True, "pathfinder-rodinia-2.0-ft": False, "nn-rodinia-2.0-ft": False}
+    for a, c in base.items():
+        s.times[(a, "gpu")] = 5.0
+        s.times[(a, "cpu")] = c
+
+    def fake_run(app_kl, engine=None):
+        a = app_kl[0]
+        k = s.threads.get(a, 1)
+        s.times[(a, engine)] = base[a] / (k ** 0.8 if scales[a] else 1.0)
+        return a, 0, 0
+
+    monkeypatch.setattr(s, "_run_app", fake_run)
+    th = s.widen(max_threads=8)
+    # backprop scales: 2 -> 4 -> 8 threads would need 8 + 2 cores; 4 fits
+    # next to the two single-threaded apps... and 8 does not (8 + 1 + 1 > 8)
+    assert th == {"backprop-rodinia-2.0-ft": 4}, th
+    assert all(v == "cpu" for v in s.assignment.values())
+    assert abs(s.predicted_span - 1.0 / 4 ** 0.8) < 1e-9
+    # thread teams share the cores: two 4-thread jobs on 4 cores run back to back
+    assert abs(DistributedSuite._cores_span([(1.0, 4), (1.0, 4)], 4) - 2.0) < 1e-12
+    assert abs(DistributedSuite._cores_span([(1.0, 4), (1.0, 4)], 8) - 1.0) < 1e-12
+
+
 # ---- data-parallel training step: collectives overlapping compute ----------
 DP_KW = dict(layers=2, ctas=8, k_tiles=1, grad_mb=0.0625, straggle=0.6)
 DP_EXTRA = {"-gpgpu_concurrent_kernel_sm": "1", "-collective_model": "packet", "-gpgpu_n_clusters": "16"}
