@@ -306,6 +306,9 @@ const OptDef kOptions[] = {
     {"-xgmi_link_latency_ns", 'f', "1000.0", "collective step latency (ns)"},
     {"-xgmi_links_per_gpu", 'u', "7", "xGMI links per GPU"},
     {"-sim_event_skip", 'b', "1", "fast-forward quiet SM cycles inside an epoch (results identical)"},
+    {"-power_in_loop", 'b', "1",
+     "power samples taken by the engine inside its cycle loop (GPU engine: in engine_kernel, f64 MFMA sums), "
+     "0 = one engine run per sample with the host evaluating (results identical; DVFS always uses the latter)"},
     {"-trace_host_budget_mb", 'f', "0",
      "read a kernel's text trace per thread block, as the trace window advances, when the file is larger than this "
      "many MiB: host trace memory then follows the window (-gpu_trace_window, 2 when 0) instead of the kernel "
@@ -1099,6 +1102,7 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.max_concurrent_kernel = (int32_t)r.geti("-gpgpu_max_concurrent_kernel");
   d.trace_prefetch = r.getb("-trace_prefetch");
   d.host_budget_mb = r.getd("-trace_host_budget_mb");
+  d.power_in_loop = r.getb("-power_in_loop");
   d.gpu_ingest = r.getb("-gpu_ingest");
   d.gpu_ingest_min = (uint64_t)r.getu("-gpu_ingest_min_insts");
   d.power_enabled = r.getb("-power_simulation_enabled");

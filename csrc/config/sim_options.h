@@ -104,6 +104,7 @@ struct DriverOpts {
   uint32_t sim_epochs_per_launch = 4096;
   bool gpu_ingest = true;      // -gpu_ingest: coalesce traces on the GPU engine's device
   uint64_t gpu_ingest_min = 32768;  // -gpu_ingest_min_insts: smaller kernels stay on the host
+  bool power_in_loop = true;  // -power_in_loop: engines sample power inside their cycle loop
   double host_budget_mb = 0;  // -trace_host_budget_mb: stream larger text traces per CTA (0 = off)
   bool trace_prefetch = true;  // -trace_prefetch: parse the next kernel while this one simulates
   // interactive timing debugger (csrc/driver/debugger.h)

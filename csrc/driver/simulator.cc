@@ -889,6 +889,47 @@ RunResult Simulator::run_sampled(const RunLimits& lim0) {
   std::vector<SMStats> sm0, sm1, dsm;
   std::vector<MemStats> m0, m1, dm;
   eng_->stats(sm0, m0);
+  // power only, at the nominal clock: the engine samples inside its cycle
+  // loop (one run, no return to the host per sample); DVFS, HW / HYBRID
+  // modes, the visualizer, trace streams and the debugger need the host
+  // between samples and run in slices
+  if (power_ && !hw && !visualizer_ && !cfg_.trace_mask && !dbg_ && !dopt_.dvfs && dopt_.power_in_loop &&
+      eng_->power_sampler()) {
+    PwrArm arm;
+    arm.coef = power_->sampler_coef(mhz);
+    arm.freq = freq;
+    arm.t_prev = eng_->now();
+    arm.n_sm = cfg_.n_sm;
+    {
+      std::vector<const SMStats*> sp;
+      std::vector<const MemStats*> mp;
+      for (auto& x : sm0) sp.push_back(&x);
+      for (auto& x : m0) mp.push_back(&x);
+      pwr_sums_of(sp.data(), sp.size(), mp.data(), mp.size(), arm.s_prev);
+    }
+    eng_->power_arm(arm);
+    RunResult r;
+    try {
+      r = eng_->run(lim0);
+    } catch (...) {
+      eng_->power_disarm();
+      throw;
+    }
+    std::vector<PwrSample> smp;
+    eng_->power_drain(smp);
+    eng_->power_disarm();
+    for (const PwrSample& x : smp) {
+      const Activity a = PowerModel::activity_of(x);
+      PowerReport p = PowerModel::report_of(x);
+      p.clock_ratio = dvfs_ratio_;
+      ptrack_.add_sample(p, a, x.now);
+      if (power_trace_) ptrack_.write_trace_line(*power_trace_, p, x.now);
+    }
+    pwr_in_loop_samples_ += smp.size();
+    RunResult tot = r;
+    tot.hit_limit = r.cap || (lim0.max_cycle && eng_->now() >= lim0.max_cycle);
+    return tot;
+  }
   RunResult tot;
   uint64_t t_prev = eng_->now();
   for (;;) {
@@ -1435,6 +1476,8 @@ void Simulator::print_sim_time() {
   for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k)
     if (slot_op_[k] && slot_op_[k]->rk && slot_op_[k]->rk->streamed())
       host_stream_peak_ = std::max(host_stream_peak_, slot_op_[k]->rk->host_peak_bytes);
+  if (pwr_in_loop_samples_) print("power_in_loop_samples: %llu\n", (unsigned long long)pwr_in_loop_samples_);
+  if (eng_->launches()) print("engine_kernel_launches: %llu\n", (unsigned long long)eng_->launches());
   if (host_streamed_)
     print("trace_host_streamed_kernels: %llu\ntrace_host_peak_bytes: %llu\n", (unsigned long long)host_streamed_,
           (unsigned long long)host_stream_peak_);

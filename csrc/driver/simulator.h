@@ -207,6 +207,7 @@ class Simulator {
   bool copy_since_kernel_ = false;  // a host memcpy ran since the last kernel was admitted
   bool any_kernel_admitted_ = false;
   uint64_t dma_count_ = 0;        // collective copy kernels launched
+  uint64_t pwr_in_loop_samples_ = 0;  // power samples the engine took inside its cycle loop
   uint64_t host_streamed_ = 0;    // kernels read per CTA from their files (-trace_host_budget_mb)
   uint64_t host_stream_peak_ = 0;  // largest host trace footprint of one of them
   bool cap_hit_ = false;  // a run cap (-gpgpu_max_insn / _max_cta / _max_completed_cta) stopped a kernel

@@ -206,6 +206,8 @@ class CpuEngine : public Engine {
       const int nsm = (int)sms_.size(), nch = (int)chs_.size();
       uint64_t epoch = epoch0, cycle = cycle0, epochs = 0;
       bool refill = true;
+      // armed power sampler: the next sample point (every thread tracks it)
+      uint64_t pw_next = pw_on_ ? pw_.t_prev + pw_.freq : 0;
       RunResult r;
       for (;;) {
         // host-streamed traces: bring in the CTAs the next epochs can
@@ -239,11 +241,23 @@ class CpuEngine : public Engine {
           }
         }
         if (nthr > 1) bar_.wait();
-        const EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, kt_, epoch, lim.max_cycle);
+        const uint64_t mc = pw_on_ ? (lim.max_cycle ? std::min(lim.max_cycle, pw_next) : pw_next) : lim.max_cycle;
+        const EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, kt_, epoch, mc);
         refill = d.refill != 0;
         ++epoch;
         ++epochs;
         cycle = d.next_start;
+        if (pw_on_) {
+          const bool exits = d.done || d.deadlock || d.limit || (lim.max_cycle && cycle >= lim.max_cycle) ||
+                             (lim.max_epochs && epochs >= lim.max_epochs);
+          if (exits || cycle >= pw_next) {
+            // thread 0 samples while the others wait (the next epoch would
+            // move the statistics)
+            if (tid == 0) power_sample(cycle);
+            if (nthr > 1) bar_.wait();
+            pw_next = cycle + pw_.freq;
+          }
+        }
         if (d.done) {
           r.done = true;
           r.done_mask = d.done;
@@ -283,6 +297,27 @@ class CpuEngine : public Engine {
     *peak_bytes = tw_.resident_peak;
     *refills = tw_.refills;
   }
+  bool power_sampler() const override { return true; }
+  void power_arm(const PwrArm& a) override {
+    pw_ = a;
+    pw_on_ = true;
+    pw_out_.clear();
+  }
+  void power_disarm() override { pw_on_ = false; }
+  void power_drain(std::vector<PwrSample>& out) override {
+    out.swap(pw_out_);
+    pw_out_.clear();
+  }
+  void power_sample(uint64_t now) {
+    std::vector<const MemStats*> mem;
+    for (auto& ch : chs_)
+      for (uint32_t j = 0; j < c_.n_sub_per_mem; ++j) mem.push_back(&ch.sp[j].st);
+    std::vector<const SMStats*> sm(sms_.size());
+    for (size_t i = 0; i < sms_.size(); ++i) sm[i] = &sms_[i].st;
+    double S[PS_COUNT];
+    pwr_sums_of(sm.data(), sm.size(), mem.data(), mem.size(), S);
+    pw_out_.push_back(pwr_take(pw_, S, now));
+  }
   void read_dispatch(DispatchView& v) const {
     const SMState& s0 = sms_[0];
     memcpy(v.k_uid, s0.k_uid, sizeof(v.k_uid));
@@ -302,6 +337,9 @@ class CpuEngine : public Engine {
     void write(void* d, const void* h, size_t n) { memcpy(d, h, n); }
   };
   TraceWindows<HostMem> tw_;
+  bool pw_on_ = false;
+  PwrArm pw_;
+  std::vector<PwrSample> pw_out_;
   ThreadTeam team_;
   SpinBarrier bar_;
   std::vector<TraceEv> trace_ev_;

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../model/epoch.h"
+#include "../power/power_eval.h"
 #include "../trace/trace.h"
 
 namespace asim {
@@ -17,6 +18,20 @@ namespace asim {
 struct RunLimits {
   uint64_t max_cycle = 0;   // absolute cycle cap (0 = none)
   uint64_t max_epochs = 0;  // safety cap (0 = none)
+};
+
+// In-loop power sampling (power_eval.h): while armed, the engine takes a
+// sample at the end of the first epoch reaching `next` (= last sample + freq,
+// which also clamps the epoch decision's fast-forward, as a sampled slice's
+// max_cycle would) and at every run exit, from its own statistics, with no
+// return to the host per sample (reference mcpat_cycle inside the cycle loop,
+// power_interface.cc:52-188)
+struct PwrArm {
+  PwrCoef coef;
+  uint64_t freq = 0;
+  uint64_t t_prev = 0;           // cycle of the previous sample (arm point)
+  double s_prev[PS_COUNT] = {};  // sums at t_prev
+  uint32_t n_sm = 0;
 };
 
 struct RunResult {
@@ -76,7 +91,43 @@ class Engine {
     *peak_bytes = 0;
     *refills = 0;
   }
+  // device kernel launches so far (GPU engine; host engines report 0)
+  virtual uint64_t launches() const { return 0; }
+  // in-loop power sampling (PwrArm); engines without it return false
+  virtual bool power_sampler() const { return false; }
+  virtual void power_arm(const PwrArm&) { throw std::runtime_error("engine has no in-loop power sampler"); }
+  virtual void power_disarm() {}
+  // samples taken since the last drain, in order
+  virtual void power_drain(std::vector<PwrSample>& out) { out.clear(); }
 };
+
+// host twin of the samplers' step 2 (the sums of every unit's raw counters)
+inline void pwr_sums_of(const SMStats* const* sm, size_t nsm, const MemStats* const* mem, size_t nmem, double* S) {
+  for (int j = 0; j < PS_COUNT; ++j) S[j] = 0;
+  for (size_t i = 0; i < nsm; ++i)
+    for (int r = 0; r < PR_COUNT; ++r) {
+      const int j = pwr_sum_of(r);
+      if (j >= 0) S[j] += (double)pwr_raw_sm(*sm[i], r);
+    }
+  for (size_t i = 0; i < nmem; ++i)
+    for (int r = 0; r < PR_COUNT; ++r) {
+      const int j = pwr_sum_of(r);
+      if (j >= 0) S[j] += (double)pwr_raw_mem(*mem[i], r);
+    }
+}
+
+// one sample from the sums at `now` (shared by the engines' samplers)
+inline PwrSample pwr_take(PwrArm& a, const double* S, uint64_t now) {
+  PwrSample o{};
+  double d[PS_COUNT];
+  for (int j = 0; j < PS_COUNT; ++j) d[j] = S[j] - a.s_prev[j];
+  pwr_activity(d, now > a.t_prev ? (double)(now - a.t_prev) : 1.0, a.n_sm, o);
+  pwr_power(a.coef, a.coef.coef, a.n_sm, 1.0, 1.0, 1.0, o);
+  o.now = now;
+  for (int j = 0; j < PS_COUNT; ++j) a.s_prev[j] = S[j];
+  a.t_prev = now;
+  return o;
+}
 
 // layout of save_state(): header, then SMState[n_sm], ChanState[n_mem],
 // EpochPub, and for parity 0/1: req packets, req counts, reply packets,

@@ -59,6 +59,21 @@ namespace asim {
 constexpr int kCfgSlots = 64;
 __constant__ SimCfg g_cfg[kCfgSlots];
 
+// in-kernel power sampler state (engine.h PwrArm; power_eval.h)
+struct PwrDev {
+  PwrCoef coef;
+  uint64_t freq;
+  uint64_t t_prev;  // cycle of the previous sample (evaluator block)
+  uint64_t next;    // next sample point (written back by block 0 at exit)
+  uint32_t n_sm;
+  uint32_t n;       // samples written to `ring` this launch
+  uint32_t cap;
+  uint32_t pad;
+  double s_prev[kPwrSumPad];
+  double* rows;      // [units][kPwrRawPad] raw counters of the sample being taken
+  PwrSample* ring;   // [cap] samples of this launch (the host drains after it)
+};
+
 struct GpuArgs {
   uint32_t cfg_slot;                 // g_cfg slot of this engine
   const SimCfg* __restrict__ cfg_g;  // global copy (not read by the engine kernel)
@@ -82,6 +97,7 @@ struct GpuArgs {
   GpuCtl* ctl;
   uint64_t* prof;  // [nblocks][kProfSlots] shader-clock cycles per stage (profiling build)
   uint32_t* ework; // [nblocks] work clocks of the last epoch (profiling build)
+  PwrDev* pw;      // armed power sampler, or nullptr
 };
 
 template <class T>
@@ -142,7 +158,9 @@ struct ProfLds {
   uint32_t pad;
   uint64_t acc[kProfSlots];
 };
-constexpr size_t kLdsBytes = kProfOff + sizeof(ProfLds);
+// the power evaluator's sums and deltas (one block per sample)
+constexpr size_t kPwrOff = kProfOff + (sizeof(ProfLds) + 15) / 16 * 16;
+constexpr size_t kLdsBytes = kPwrOff + 2 * kPwrSumPad * sizeof(double);
 static_assert(kLdsBytes <= 160 * 1024, "per-block LDS budget exceeded");
 
 // profiling build of the lane policy: P::prof(k) charges the shader-clock
@@ -165,6 +183,72 @@ struct WaveParProf : WavePar {
     __builtin_amdgcn_wave_barrier();
   }
 };
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// a unit's raw power counters (power_eval.h step 1) into its row
+__device__ __forceinline__ void pwr_row_sm(double* row, const SMStats& st) {
+  for (int k = (int)(threadIdx.x & 63); k < kPwrRawPad; k += 64) row[k] = k < PR_COUNT ? (double)pwr_raw_sm(st, k) : 0.0;
+}
+__device__ __forceinline__ void pwr_row_ch(double* row, const ChanState& ch, uint32_t nsub) {
+  for (int k = (int)(threadIdx.x & 63); k < kPwrRawPad; k += 64) {
+    double v = 0;
+    if (k < PR_COUNT)
+      for (uint32_t j = 0; j < nsub; ++j) v += (double)pwr_raw_mem(ch.sp[j].st, k);
+    row[k] = v;
+  }
+}
+
+// power_eval.h steps 2 and 3 on one wave: S = rows x M as f64 MFMA tiles
+// (16 units x 4 raw counters by 4 raw counters x 16 sums, accumulated over
+// unit tiles and k-steps; integers below 2^53, so exact in any order), then
+// the sample on lane 0 into the ring
+__device__ void pwr_evaluate(PwrDev& pw, uint32_t nunits, uint64_t now) {
+  const int lane = (int)(threadIdx.x & 63);
+  constexpr int kCt = kPwrSumPad / 16;
+  f64x4 acc[kCt];
+#pragma unroll
+  for (int ct = 0; ct < kCt; ++ct) acc[ct] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const double* rows = pw.rows;
+  for (uint32_t t = 0; t < (nunits + 15u) / 16u; ++t) {
+    const uint32_t u = 16u * t + (uint32_t)(lane & 15);
+    for (int k4 = 0; k4 < kPwrRawPad / 4; ++k4) {
+      const int k = 4 * k4 + (lane >> 4);
+      const double av = u < nunits ? rows[(size_t)u * kPwrRawPad + k] : 0.0;
+      const int sj = k < PR_COUNT ? pwr_sum_of(k) : -1;
+#pragma unroll
+      for (int ct = 0; ct < kCt; ++ct) {
+        const double bv = sj == 16 * ct + (lane & 15) ? 1.0 : 0.0;
+        acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[ct], 0, 0, 0);
+      }
+    }
+  }
+  double* S = reinterpret_cast<double*>(g_lds + kPwrOff);
+  double* D = S + kPwrSumPad;
+#pragma unroll
+  for (int ct = 0; ct < kCt; ++ct) {
+    // D layout: column lane & 15, rows (lane >> 4) + 4 * reg: sum the four
+    // rows a lane holds, then across the four lane groups
+    double v = acc[ct][0] + acc[ct][1] + acc[ct][2] + acc[ct][3];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane < 16) S[16 * ct + lane] = v;
+  }
+  __syncthreads();
+  if (lane < PS_COUNT) D[lane] = S[lane] - pw.s_prev[lane];
+  __syncthreads();
+  if (lane == 0) {
+    const uint32_t i = pw.n < pw.cap ? pw.n : pw.cap - 1;
+    PwrSample& o = pw.ring[i];
+    pwr_activity(D, now > pw.t_prev ? (double)(now - pw.t_prev) : 1.0, pw.n_sm, o);
+    pwr_power(pw.coef, pw.coef.coef, pw.n_sm, 1.0, 1.0, 1.0, o);
+    o.now = now;
+    pw.t_prev = now;
+    pw.n = pw.n + 1;
+  }
+  if (lane < PS_COUNT) pw.s_prev[lane] = S[lane];
+  __syncthreads();
+}
 
 template <class P, bool kSliced>
 __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
@@ -235,6 +319,9 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   uint64_t t_work0 = a.ework ? __builtin_amdgcn_s_memtime() : 0;
   uint32_t done = 0, dead = 0, capped = 0;
   uint32_t n = 0;
+  uint32_t nbar = 0;  // grid barriers of this launch (epochs + power samples)
+  uint64_t pw_next = a.pw ? a.pw->next : 0;
+  bool failed = false;
   for (; n < a.max_epochs;) {
     const uint32_t cur = (uint32_t)(epoch & 1), prev = cur ^ 1u;
     const uint64_t t0 = cycle, t1 = t0 + E;
@@ -269,7 +356,7 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
       if ((threadIdx.x & 63) == 0) a.ework[b] = (uint32_t)(t_arrive - t_work0);
     }
     uint32_t was_last = 0;
-    if (!grid_barrier(a.ctl, a.nblocks, n - 1, &was_last)) break;
+    if (!grid_barrier(a.ctl, a.nblocks, nbar++, &was_last)) break;
     P::prof(27);  // decision
     if (a.ework) {
       const uint64_t t_exit = __builtin_amdgcn_s_memtime();
@@ -292,10 +379,29 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
       }
       t_work0 = t_exit;
     }
-    EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, kt, epoch, a.max_cycle);
+    // an armed power sampler's next point clamps the fast-forward like a
+    // sampled slice's max_cycle would
+    const uint64_t mc = a.pw ? (a.max_cycle ? (a.max_cycle < pw_next ? a.max_cycle : pw_next) : pw_next) : a.max_cycle;
+    EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, kt, epoch, mc);
     P::prof(28);
     ++epoch;
     cycle = P::uni(d.next_start);
+    if (a.pw) {
+      const bool exits = P::uni(d.done) || P::uni(d.deadlock) || P::uni(d.limit) || (a.max_cycle && cycle >= a.max_cycle);
+      if (exits || cycle >= pw_next) {
+        // every block writes its units' counters, one barrier, then the last
+        // block evaluates the sample while the others run on
+        for (uint32_t k = 0; k < nmine; ++k) {
+          const uint32_t u = unit_k(k);
+          double* row = a.pw->rows + (size_t)u * kPwrRawPad;
+          if (u < c.n_sm) pwr_row_sm(row, u == loaded ? s->st : a.sms[u].st);
+          else pwr_row_ch(row, u == loaded ? *ch : a.chs[u - c.n_sm], c.n_sub_per_mem);
+        }
+        if (!grid_barrier(a.ctl, a.nblocks, nbar++)) { failed = true; break; }
+        if (b == a.nblocks - 1) pwr_evaluate(*a.pw, nunits, cycle);
+        pw_next = cycle + a.pw->freq;
+      }
+    }
     if (P::uni(d.done)) { done = P::uni(d.done); break; }
     if (P::uni(d.deadlock)) { dead = 1; break; }
     if (P::uni(d.limit)) { capped = 1; break; }
@@ -309,6 +415,8 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   else
     copy_state(&a.chs[loaded - c.n_sm], ch);
   if (a.prof && (threadIdx.x & 63) < kProfSlots && (threadIdx.x & 63) != 30) a.prof[(size_t)b * kProfSlots + (threadIdx.x & 63)] += pl->acc[threadIdx.x & 63];
+  (void)failed;
+  if (a.pw && b == 0 && (threadIdx.x & 63) == 0) a.pw->next = pw_next;
   if (b == 0 && (threadIdx.x & 63) == 0) {
     a.ctl->done = done;
     a.ctl->deadlock = dead;
@@ -611,6 +719,7 @@ class GpuEngine : public Engine {
       HIPCHECK(hipMemsetAsync(d_ctl_, 0, sizeof(GpuCtl), stream_));
       a.prof = d_prof_;
       a.ework = d_ework_;
+      a.pw = pw_on_ ? d_pw_ : nullptr;
       CuPool::get().acquire((int)nblocks_);
       hipError_t le;
       if (profiling_ && sliced_)
@@ -622,6 +731,7 @@ class GpuEngine : public Engine {
       else
         hipLaunchKernelGGL((engine_kernel<WavePar, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       le = hipGetLastError();
+      ++launches_;
       hipError_t ce = hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_);
       hipError_t se = hipStreamSynchronize(stream_);
       CuPool::get().release((int)nblocks_);
@@ -631,6 +741,7 @@ class GpuEngine : public Engine {
       if (h_ctl_->error) throw std::runtime_error("GPU engine: grid barrier timed out (blocks not co-resident?)");
       epoch_ = h_ctl_->end_epoch;
       cycle_ = h_ctl_->end_cycle;
+      if (pw_on_) pwr_collect();
       res.epochs += h_ctl_->epochs_run;
       if (h_ctl_->done) {
         res.done = true;
@@ -798,6 +909,20 @@ class GpuEngine : public Engine {
   }
 
  private:
+  // samples of the last launch from the device ring; the ring restarts
+  void pwr_collect() {
+    uint32_t n = 0;
+    HIPCHECK(hipMemcpy(&n, reinterpret_cast<char*>(d_pw_) + offsetof(PwrDev, n), sizeof(n), hipMemcpyDeviceToHost));
+    if (n > pw_cap_) throw std::runtime_error("GPU engine: power sample ring overflow");
+    if (n) {
+      const size_t o = pw_out_.size();
+      pw_out_.resize(o + n);
+      HIPCHECK(hipMemcpy(pw_out_.data() + o, d_pw_ring_, sizeof(PwrSample) * n, hipMemcpyDeviceToHost));
+      const uint32_t z = 0;
+      HIPCHECK(hipMemcpy(reinterpret_cast<char*>(d_pw_) + offsetof(PwrDev, n), &z, sizeof(z), hipMemcpyHostToDevice));
+    }
+  }
+
   // the dispatch state a trace window follows: replicated cursors (SM 0) and
   // every SM's resident CTAs, read back from the device
   void read_dispatch(DispatchView& v) {
@@ -828,6 +953,41 @@ class GpuEngine : public Engine {
     *refills = tw_.refills;
   }
 
+  // in-kernel power sampling (engine.h PwrArm): engine_kernel writes each
+  // sample to a device ring, drained after every launch
+  uint64_t launches() const override { return launches_; }
+  bool power_sampler() const override { return true; }
+  void power_arm(const PwrArm& arm) override {
+    const uint32_t nunits = c_.n_sm + c_.n_mem;
+    const uint32_t cap = epochs_per_launch_ + 2;  // at most one sample per epoch of a launch
+    if (!d_pw_) HIPCHECK(hipMalloc(&d_pw_, sizeof(PwrDev)));
+    if (!d_pw_rows_) HIPCHECK(hipMalloc(&d_pw_rows_, sizeof(double) * kPwrRawPad * nunits));
+    if (pw_cap_ < cap) {
+      if (d_pw_ring_) HIPCHECK(hipFree(d_pw_ring_));
+      HIPCHECK(hipMalloc(&d_pw_ring_, sizeof(PwrSample) * cap));
+      pw_cap_ = cap;
+    }
+    PwrDev h{};
+    h.coef = arm.coef;
+    h.freq = arm.freq;
+    h.t_prev = arm.t_prev;
+    h.next = arm.t_prev + arm.freq;
+    h.n_sm = arm.n_sm;
+    h.n = 0;
+    h.cap = pw_cap_;
+    for (int j = 0; j < PS_COUNT; ++j) h.s_prev[j] = arm.s_prev[j];
+    h.rows = d_pw_rows_;
+    h.ring = d_pw_ring_;
+    HIPCHECK(hipMemcpy(d_pw_, &h, sizeof(PwrDev), hipMemcpyHostToDevice));
+    pw_on_ = true;
+    pw_out_.clear();
+  }
+  void power_disarm() override { pw_on_ = false; }
+  void power_drain(std::vector<PwrSample>& out) override {
+    out.swap(pw_out_);
+    pw_out_.clear();
+  }
+
  private:
   // the configuration as the kernels read it: the engine's constant-memory
   // slot and the global copy (stream-ordered before the next launch)
@@ -856,6 +1016,9 @@ class GpuEngine : public Engine {
     fr(d_trace_ev_);
     fr(d_trace_cnt_);
     tw_.release();
+    fr(d_pw_);
+    fr(d_pw_rows_);
+    fr(d_pw_ring_);
     fr(d_kt_);
     if (h_ctl_) (void)hipHostFree(h_ctl_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -897,6 +1060,13 @@ class GpuEngine : public Engine {
     void write(void* d, const void* h, size_t n) { HIPCHECK(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); }
   };
   TraceWindows<DevMem> tw_;
+  uint64_t launches_ = 0;
+  bool pw_on_ = false;
+  PwrDev* d_pw_ = nullptr;
+  double* d_pw_rows_ = nullptr;
+  PwrSample* d_pw_ring_ = nullptr;
+  uint32_t pw_cap_ = 0;
+  std::vector<PwrSample> pw_out_;
   KernelTab kt_{};
   KernelTab* d_kt_ = nullptr;
   uint32_t cap_req_ = 0, cap_rep_ = 0;

@@ -125,7 +125,7 @@ struct SMStats {
   uint64_t warps_done;
   uint64_t occupancy_acc;      // sum over cycles of live warps
   uint64_t mem_insn;
-  uint64_t power_acc[8];       // power-model counters (PwrCounter)
+  uint64_t power_acc[16];      // power-model counters (PwrCounter)
   // L1 miss round-trip latency (MSHR allocation -> last sector filled), the
   // reference's mem_latency_stat (mem_latency_stat.h:37, -gpgpu_memlatency_stat)
   uint64_t mf_lat_sum, mf_lat_n, mf_lat_max;
@@ -170,8 +170,15 @@ SIM_HDI uint32_t sq_class(const TInst& in) {
     default: return in.space == S_CONST ? SQ_SMEM : SQ_VALU;  // s_memtime is an SMEM op
   }
 }
-// SMStats::power_acc slots
-enum PwrCounter : uint8_t { PWR_CONST_OPERAND = 0 };
+// SMStats::power_acc slots: constant-cache operands, then the active lanes
+// charged at issue per execution-unit kind (slot = the instruction's power
+// kind, TInst::flags >> 4; reference incexecstat, shader.cc:3226-3290)
+enum PwrCounter : uint8_t {
+  PWR_CONST_OPERAND = 0,
+  PWR_INT = 1, PWR_INT_MUL, PWR_FP, PWR_FP_MUL, PWR_DP, PWR_DP_MUL, PWR_SQRT, PWR_LG, PWR_SIN, PWR_EXP, PWR_TENSOR,
+  PWR_TEX, PWR_SALU, PWR_KINDS
+};
+static_assert(PWR_KINDS <= 16, "power kinds live in the upper nibble of TInst::flags");
 
 
 // Complete state of one SM.  On the GPU it lives in LDS for the duration of
@@ -1307,6 +1314,12 @@ SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32
   // LDC / s_load: an ALU-timed instruction with a constant-cache operand
   // (reference trace_driven.cc:255-261 keeps LDC an ALU op; shader.cc:3287)
   if (in.space == S_CONST) s.sadd(SK(power_acc) + PWR_CONST_OPERAND, 1);
+  // per-issue energy: the instruction's active lanes on its unit kind (the
+  // scalar unit executes once per wave)
+  {
+    const uint32_t pk = (uint32_t)(in.flags >> 4);
+    if (pk) s.sadd(SK(power_acc) + pk, pk == PWR_SALU ? 1ull : (uint64_t)popc64(in.mask));
+  }
   s.last_progress = now;
   const uint32_t cta = P::uni((uint8_t)s.w_cta[w]);
   if (in.cls == OC_EXIT) {

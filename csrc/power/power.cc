@@ -23,13 +23,6 @@ const char* const kHwCounterName[HW_COUNT] = {"L1_RH", "L1_RM", "L1_WH", "L1_WM"
                                               "DRAM_RD", "DRAM_WR", "L2_RH", "L2_RM", "L2_WH", "L2_WM",
                                               "NOC", "PIPE_DUTY", "NUM_SM_IDLE", "CYCLES", "VOLTAGE"};
 
-// activity -> report component
-static const int kActCmp[PA_COUNT] = {
-    PC_IB,  PC_SCHED, PC_IC,     PC_IC,     PC_DC,      PC_DC,     PC_DC,     PC_DC,     PC_CC,
-    PC_CC,  PC_SHRD,  PC_RF,     PC_RF,     PC_INT,     PC_FPU,    PC_DPU,    PC_INT_MUL, PC_FP_MUL,
-    PC_FP_SQRT, PC_FP_LG, PC_FP_SIN, PC_FP_EXP, PC_DP_MUL, PC_TENSOR, PC_TEX,
-    PC_DRAM, PC_DRAM, PC_MC,     PC_L2C,    PC_L2C,     PC_L2C,    PC_L2C,    PC_NOC,    PC_PIPE};
-
 // Per-access base energies (nJ) for a 12-16 nm class GPU.  These play the
 // role of McPAT's per-access energies; the XML scaling factors calibrate
 // them (util: accel_sim_framework_distributed_amd.power.calibrate).
@@ -104,46 +97,69 @@ std::vector<double> PowerModel::coefficients(double core_mhz) const {
   return c;
 }
 
-PowerReport PowerModel::compute(const Activity& a, double core_mhz, uint32_t n_sm, double clock_ratio) const {
+PwrCoef PowerModel::sampler_coef(double core_mhz) const {
+  PwrCoef k{};
+  const auto c = coefficients(core_mhz);
+  for (int i = 0; i < PA_COUNT; ++i) k.coef[i] = c[i];
+  k.constant = param("constant_power", 0);
+  k.idle_core = param("idle_core_power", 0);
+  static const char* const cat[7] = {"light", "cat1", "cat2", "cat3", "cat4", "cat5", "cat6"};
+  for (int i = 0; i < 7; ++i) {
+    k.st_flane[i] = param(std::string("static_") + cat[i] + "_flane", 0);
+    k.st_addlane[i] = param(std::string("static_") + cat[i] + "_addlane", 0);
+  }
+  k.st_shared = param("static_shared_flane", 0);
+  k.st_l1 = param("static_l1_flane", 0);
+  k.st_l2 = param("static_l2_flane", 0);
+  return k;
+}
+
+Activity PowerModel::activity_of(const PwrSample& s) {
+  Activity a;
+  for (int i = 0; i < PA_COUNT; ++i) a.a[i] = s.act[i];
+  a.cycles = s.cycles;
+  a.idle_sms = s.idle_sms;
+  a.avg_lanes = s.lanes;
+  a.int_used = s.unit_mask & 1u;
+  a.fp_used = s.unit_mask & 2u;
+  a.dp_used = s.unit_mask & 4u;
+  a.sfu_used = s.unit_mask & 8u;
+  a.tex_used = s.unit_mask & 16u;
+  a.tensor_used = s.unit_mask & 32u;
+  return a;
+}
+
+PowerReport PowerModel::report_of(const PwrSample& o) {
+  static const char* const cat[7] = {"light", "cat1", "cat2", "cat3", "cat4", "cat5", "cat6"};
   PowerReport r;
-  const double cyc = a.cycles > 0 ? a.cycles : 1;
+  for (int i = 0; i < PC_COUNT; ++i) r.cmp[i] = o.cmp[i];
+  for (int i = 0; i < PA_COUNT; ++i) r.dynamic_w[i] = o.dyn[i];
+  r.dynamic = o.dynamic;
+  r.static_w = o.static_w;
+  r.static_mem = o.static_mem;
+  r.constant = o.constant;
+  r.idle = o.idle;
+  r.total = o.total;
+  r.uncapped = o.total;
+  r.static_category = cat[o.category < 7 ? o.category : 0];
+  return r;
+}
+
+PowerReport PowerModel::compute(const Activity& a, double core_mhz, uint32_t n_sm, double clock_ratio) const {
   const double s = clock_ratio > 0 ? clock_ratio : 1.0;
   const double vr = s < 1.0 ? dvfs_voltage_ratio(s) : 1.0;
-  const auto coef = coefficients(core_mhz * s);
+  const PwrCoef k = sampler_coef(core_mhz * s);
   // a.voltage: the HW-mode chip voltage ratio (hw_perf.csv); vr: DVFS
   const double v2 = a.voltage * a.voltage * vr * vr;
-  for (int i = 0; i < PA_COUNT; ++i) {
-    const bool dram = i == PA_MEM_RD || i == PA_MEM_WR || i == PA_MEM_PRE;  // the HBM rail keeps its voltage
-    r.dynamic_w[i] = coef[i] * (a.a[i] / cyc) * (dram ? a.voltage * a.voltage : v2);
-    r.dynamic += r.dynamic_w[i];
-  }
-  r.constant = param("constant_power", 0);
-  r.idle = param("idle_core_power", 0) * a.idle_sms * vr;
-  // categorical static power by active unit mix (reference
-  // calculate_static_power, gpgpu_sim_wrapper.cc:746-846)
-  std::string cat;
-  if (a.tensor_used) cat = "cat6";
-  else if (a.tex_used) cat = "cat5";
-  else if (a.sfu_used) cat = "cat4";
-  else if (a.dp_used) cat = "cat3";
-  else if (a.fp_used) cat = "cat2";
-  else if (a.int_used) cat = "cat1";
-  else cat = "light";
-  r.static_category = cat;
-  double lanes = a.avg_lanes > 1 ? a.avg_lanes : 1;
-  double busy_frac = n_sm ? std::max(0.0, 1.0 - a.idle_sms / n_sm) : 1.0;
-  r.static_w = (param("static_" + cat + "_flane", 0) + param("static_" + cat + "_addlane", 0) * (lanes - 1)) * busy_frac;
-  double smem = 0;
-  if (a.a[PA_SHRD_ACC] > 0) smem += param("static_shared_flane", 0) * busy_frac;
-  if (a.a[PA_DC_RH] + a.a[PA_DC_RM] + a.a[PA_DC_WH] + a.a[PA_DC_WM] > 0) smem += param("static_l1_flane", 0) * busy_frac;
-  if (a.a[PA_L2_RH] + a.a[PA_L2_RM] + a.a[PA_L2_WH] + a.a[PA_L2_WM] > 0) smem += param("static_l2_flane", 0);
-  r.static_w = (r.static_w + smem) * vr;
-  r.static_mem = smem * vr;
-  r.total = r.dynamic + r.static_w + r.constant + r.idle;
-  for (int i = 0; i < PA_COUNT; ++i) r.cmp[kActCmp[i]] += r.dynamic_w[i];
-  r.cmp[PC_IDLE_CORE] = r.idle;
-  r.cmp[PC_CONST] = r.constant;
-  r.cmp[PC_STATIC] = r.static_w;
+  PwrSample o{};
+  for (int i = 0; i < PA_COUNT; ++i) o.act[i] = a.a[i];
+  o.cycles = a.cycles;
+  o.idle_sms = a.idle_sms;
+  o.lanes = a.avg_lanes;
+  o.unit_mask = (a.int_used ? 1u : 0u) | (a.fp_used ? 2u : 0u) | (a.dp_used ? 4u : 0u) | (a.sfu_used ? 8u : 0u) |
+                (a.tex_used ? 16u : 0u) | (a.tensor_used ? 32u : 0u);
+  pwr_power(k, k.coef, n_sm, v2, a.voltage * a.voltage, vr, o);
+  PowerReport r = report_of(o);
   r.clock_ratio = s;
   r.voltage_ratio = vr;
   r.capped = s < 1.0;
@@ -284,61 +300,28 @@ void PowerTracker::write_steady(std::ostream& os, const std::string& kernel) con
   }
 }
 
+// the sums of a statistics image (power_eval.h step 2, host loops)
+void pwr_sums(const std::vector<SMStats>& sm, const std::vector<MemStats>& mem, double* S) {
+  for (int j = 0; j < PS_COUNT; ++j) S[j] = 0;
+  for (const auto& s : sm)
+    for (int r = 0; r < PR_COUNT; ++r) {
+      const int j = pwr_sum_of(r);
+      if (j >= 0) S[j] += (double)pwr_raw_sm(s, r);
+    }
+  for (const auto& m : mem)
+    for (int r = 0; r < PR_COUNT; ++r) {
+      const int j = pwr_sum_of(r);
+      if (j >= 0) S[j] += (double)pwr_raw_mem(m, r);
+    }
+}
+
 Activity PowerModel::activity_from_stats(const std::vector<SMStats>& dsm, const std::vector<MemStats>& dmem,
                                          uint64_t cycles) {
-  Activity a;
-  a.cycles = (double)cycles;
-  double warp = 0, thread = 0, mem = 0, active = 0;
-  double cls[OC_COUNT] = {};
-  for (const auto& s : dsm) {
-    warp += s.warp_insn;
-    thread += s.thread_insn;
-    mem += s.mem_insn;
-    active += s.active_cycles;
-    for (int k = 0; k < OC_COUNT; ++k) cls[k] += s.cls_insn[k];
-    a.a[PA_DC_RH] += s.l1[L1T_GLOBAL_R][L1O_HIT] + s.l1[L1T_LOCAL_R][L1O_HIT];
-    a.a[PA_DC_RM] += s.l1[L1T_GLOBAL_R][L1O_MISS] + s.l1[L1T_LOCAL_R][L1O_MISS] + s.l1[L1T_GLOBAL_R][L1O_MSHR_HIT] +
-                     s.l1[L1T_LOCAL_R][L1O_MSHR_HIT] + s.l1[L1T_GLOBAL_R][L1O_BYPASS];
-    a.a[PA_DC_WM] += s.l1[L1T_GLOBAL_W][L1O_MISS] + s.l1[L1T_LOCAL_W][L1O_MISS] + s.l1[L1T_GLOBAL_W][L1O_BYPASS] +
-                     s.l1[L1T_ATOMIC][L1O_BYPASS];
-    a.a[PA_DC_WH] += s.l1[L1T_GLOBAL_W][L1O_HIT] + s.l1[L1T_LOCAL_W][L1O_HIT];
-    // constant-cache operand accesses (reference shader.cc:3287 inc_const_accesses)
-    a.a[PA_CC_H] += s.power_acc[PWR_CONST_OPERAND];
-    a.a[PA_SHRD_ACC] += s.shmem_acc;
-    a.a[PA_REG_RD] += s.rf_reads;
-    a.a[PA_REG_WR] += s.rf_writes;
-    a.a[PA_NOC_A] += s.pkts_out + s.pkts_in;
-  }
-  const double lanes = warp > 0 ? thread / warp : 0;
-  a.avg_lanes = lanes;
-  a.a[PA_TOT_INST] = warp;
-  a.a[PA_FP_INT] = warp - mem;
-  a.a[PA_IC_H] = warp;
-  a.a[PA_INT_ACC] = (cls[OC_INTP] + cls[OC_ALU]) * lanes;
-  a.a[PA_FP_ACC] = cls[OC_SP] * lanes;
-  a.a[PA_DP_ACC] = cls[OC_DP] * lanes;
-  a.a[PA_FP_EXP_ACC] = cls[OC_SFU] * lanes;
-  a.a[PA_TENSOR_ACC] = (cls[OC_TENSOR] + cls[OC_SPEC3]) * lanes;
-  a.a[PA_TEX_ACC] = cls[OC_SPEC2] * lanes;
-  a.a[PA_PIPE_A] = warp;
-  for (const auto& m : dmem) {
-    a.a[PA_MEM_RD] += m.dram_rd;
-    a.a[PA_MEM_WR] += m.dram_wr;
-    a.a[PA_MEM_PRE] += m.dram_pre;
-    a.a[PA_L2_RH] += m.l2[L2T_RD][L2O_HIT] + m.l2[L2T_ATOM][L2O_HIT];
-    a.a[PA_L2_RM] += m.l2[L2T_RD][L2O_MISS] + m.l2[L2T_RD][L2O_MSHR_HIT] + m.l2[L2T_ATOM][L2O_MISS];
-    a.a[PA_L2_WH] += m.l2[L2T_WR][L2O_HIT];
-    a.a[PA_L2_WM] += m.l2[L2T_WR][L2O_MISS];
-  }
-  a.int_used = cls[OC_INTP] + cls[OC_ALU] > 0;
-  a.fp_used = cls[OC_SP] > 0;
-  a.dp_used = cls[OC_DP] > 0;
-  a.sfu_used = cls[OC_SFU] > 0;
-  a.tex_used = cls[OC_SPEC2] > 0;
-  a.tensor_used = cls[OC_TENSOR] + cls[OC_SPEC3] > 0;
-  a.idle_sms = cycles ? (double)dsm.size() - active / (double)cycles : 0;
-  if (a.idle_sms < 0) a.idle_sms = 0;
-  return a;
+  double S[PS_COUNT];
+  pwr_sums(dsm, dmem, S);
+  PwrSample o{};
+  pwr_activity(S, (double)cycles, (uint32_t)dsm.size(), o);
+  return activity_of(o);
 }
 
 bool PowerModel::activity_from_hw_csv(const std::string& csv, const std::string& bench, const std::string& kernel,

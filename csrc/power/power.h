@@ -29,15 +29,10 @@
 #include <vector>
 
 #include "../model/mem.h"
+#include "power_eval.h"
 
 namespace asim {
 
-enum PwrAct : int {
-  PA_TOT_INST = 0, PA_FP_INT, PA_IC_H, PA_IC_M, PA_DC_RH, PA_DC_RM, PA_DC_WH, PA_DC_WM, PA_CC_H, PA_CC_M,
-  PA_SHRD_ACC, PA_REG_RD, PA_REG_WR, PA_INT_ACC, PA_FP_ACC, PA_DP_ACC, PA_INT_MUL_ACC, PA_FP_MUL_ACC,
-  PA_FP_SQRT_ACC, PA_FP_LG_ACC, PA_FP_SIN_ACC, PA_FP_EXP_ACC, PA_DP_MUL_ACC, PA_TENSOR_ACC, PA_TEX_ACC,
-  PA_MEM_RD, PA_MEM_WR, PA_MEM_PRE, PA_L2_RH, PA_L2_RM, PA_L2_WH, PA_L2_WM, PA_NOC_A, PA_PIPE_A, PA_COUNT
-};
 extern const char* const kPwrActName[PA_COUNT];
 
 struct Activity {
@@ -50,13 +45,6 @@ struct Activity {
   bool int_used = false, fp_used = false, dp_used = false, sfu_used = false, tex_used = false, tensor_used = false;
 };
 
-// report components (labels of the reference's pwr_cmp_t,
-// accelwattch/gpgpu_sim_wrapper.cc:42-77)
-enum PwrCmp : int {
-  PC_IB = 0, PC_IC, PC_DC, PC_TC, PC_CC, PC_SHRD, PC_RF, PC_INT, PC_FPU, PC_DPU, PC_INT_MUL24, PC_INT_MUL32, PC_INT_MUL,
-  PC_INT_DIV, PC_FP_MUL, PC_FP_DIV, PC_FP_SQRT, PC_FP_LG, PC_FP_SIN, PC_FP_EXP, PC_DP_MUL, PC_DP_DIV, PC_TENSOR, PC_TEX,
-  PC_SCHED, PC_L2C, PC_MC, PC_NOC, PC_DRAM, PC_PIPE, PC_IDLE_CORE, PC_CONST, PC_STATIC, PC_COUNT
-};
 extern const char* const kPwrCmpName[PC_COUNT];
 
 // hardware counters of hw_perf.csv usable in HW / HYBRID mode
@@ -108,8 +96,13 @@ class PowerModel {
   // come from the simulator) merge; instruction-side activity is always simulated
   static Activity merge_hw(const Activity& sim, const Activity& hw, const bool use_sim[HW_COUNT]);
   static double base_nj(int act);
-  // coefficient vector (W per access-per-cycle at 1 MHz) for matrix evaluation
+  // coefficient vector (W per access per cycle at core_mhz)
   std::vector<double> coefficients(double core_mhz) const;
+  // the sampler's coefficients at the nominal clock (engines' in-loop
+  // sampling, power_eval.h)
+  PwrCoef sampler_coef(double core_mhz) const;
+  static Activity activity_of(const PwrSample& s);
+  static PowerReport report_of(const PwrSample& s);
 
  private:
   std::map<std::string, double> p_;

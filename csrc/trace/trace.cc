@@ -107,6 +107,35 @@ bool has_tok(const std::vector<std::string>& t, const char* s) {
   return false;
 }
 
+// Execution-unit kind charged per issued lane by the power model (PwrCounter,
+// model/sm.h), from the SASS mnemonic and its class (the reference's
+// incexecstat switches on the same op families, shader.cc:3226-3290)
+uint8_t sass_power_kind(const std::string& m, const std::vector<std::string>& toks, uint8_t cls) {
+  switch (cls) {
+    case OC_INTP:
+      return (m == "IMAD" || m == "IMUL" || m == "IMUL32I" || m == "IMADSP" || m == "XMAD" || m == "IDP" ||
+              m == "IDP4A" || m == "IMAD32I")
+                 ? PWR_INT_MUL
+                 : PWR_INT;
+    case OC_ALU: return PWR_INT;
+    case OC_SP:
+      return (m == "FMUL" || m == "FMUL32I" || m == "FFMA" || m == "FFMA32I" || m == "HMUL2" || m == "HMUL2_32I" ||
+              m == "HFMA2" || m == "HFMA2_32I")
+                 ? PWR_FP_MUL
+                 : PWR_FP;
+    case OC_DP: return (m == "DMUL" || m == "DFMA") ? PWR_DP_MUL : PWR_DP;
+    case OC_SFU:
+      if (has_tok(toks, "SQRT") || has_tok(toks, "RSQ")) return PWR_SQRT;
+      if (has_tok(toks, "LG2")) return PWR_LG;
+      if (has_tok(toks, "SIN") || has_tok(toks, "COS")) return PWR_SIN;
+      return PWR_EXP;  // EX2, RCP, ...
+    case OC_TENSOR:
+    case OC_SPEC3: return PWR_TENSOR;
+    case OC_SPEC2: return PWR_TEX;
+    default: return 0;
+  }
+}
+
 OpInfo decode_sass(const std::string& op, uint32_t bv) {
   OpInfo o{};
   auto toks = dot_tokens(op);
@@ -170,6 +199,7 @@ OpInfo decode_sass(const std::string& op, uint32_t bv) {
   if (m == "HADD2" || m == "HADD2_32I" || m == "HFMA2" || m == "HFMA2_32I" || m == "HMUL2" || m == "HMUL2_32I" ||
       m == "HSET2" || m == "HSETP2")
     o.half_ii = 1;
+  if (!(o.flags & F_MEM)) o.flags |= (uint8_t)(sass_power_kind(m, toks, o.cls) << 4);
   return o;
 }
 
@@ -183,6 +213,28 @@ uint8_t cdna_width(const std::string& m) {
   if (contains(m, "short") || contains(m, "b16") || contains(m, "u16") || contains(m, "i16")) return 2;
   if (contains(m, "byte") || contains(m, "b8") || contains(m, "u8") || contains(m, "i8")) return 1;
   return 4;
+}
+
+// power kind of a CDNA mnemonic (the vector ALU's classes are all OC_SP /
+// OC_DP in the timing model; the data type and operation pick the unit)
+uint8_t cdna_power_kind(const std::string& m, uint8_t cls) {
+  if (cls == OC_TENSOR) return PWR_TENSOR;
+  if (cls == OC_SPEC8) return PWR_SALU;
+  if (cls == OC_SFU) {
+    if (starts(m, "v_sqrt") || starts(m, "v_rsq")) return PWR_SQRT;
+    if (starts(m, "v_log")) return PWR_LG;
+    if (starts(m, "v_sin") || starts(m, "v_cos")) return PWR_SIN;
+    return PWR_EXP;  // v_exp, v_rcp
+  }
+  if (!starts(m, "v_")) return 0;  // branches, barriers, nops, scalar memory
+  const bool mul = contains(m, "mul") || contains(m, "fma") || contains(m, "mad") || contains(m, "mac") ||
+                   contains(m, "dot");
+  if (contains(m, "_f64")) return mul ? PWR_DP_MUL : PWR_DP;
+  const bool fp = contains(m, "_f32") || contains(m, "_f16") || contains(m, "bf16") || contains(m, "_fp8") ||
+                  contains(m, "_bf8");
+  if (fp && !starts(m, "v_cvt")) return mul ? PWR_FP_MUL : PWR_FP;
+  if (starts(m, "v_cvt")) return PWR_FP;
+  return mul ? PWR_INT_MUL : PWR_INT;  // integer / bitwise / moves / lane ops
 }
 
 // CDNA4 (gfx950) instruction classes for native AMD traces
@@ -267,6 +319,7 @@ OpInfo decode_cdna(const std::string& op0) {
     o.cls = OC_SP;
     o.half_ii = 1;
   }
+  if (!(o.flags & (F_MEM | F_WAITCNT))) o.flags |= (uint8_t)(cdna_power_kind(m, o.cls) << 4);
   return o;
 }
 
@@ -1062,6 +1115,7 @@ HostKernel load_kernel_binary(const std::string& path) {
   uint32_t nu = 0;
   f.read(reinterpret_cast<char*>(&nu), 4);
   std::unordered_map<uint16_t, uint16_t> remap;
+  std::unordered_map<uint16_t, uint8_t> pkind;  // power kind (upper nibble of the flags) per opcode
   std::unordered_map<uint16_t, OpInfo> smem;  // CDNA scalar loads (classified by the current decoder)
   for (uint32_t i = 0; i < nu; ++i) {
     uint16_t id, len;
@@ -1071,6 +1125,7 @@ HostKernel load_kernel_binary(const std::string& path) {
     f.read(&n[0], len);
     const OpInfo oi = decode_opcode(n, h.binary_version);
     remap[id] = oi.opcode;
+    pkind[id] = (uint8_t)(oi.flags & 0xF0);
     if (h.binary_version >= 900 && oi.cls == OC_LOAD && oi.space == S_CONST) smem[id] = oi;
   }
   rd(f, k.insts, h.n_insts);
@@ -1086,6 +1141,8 @@ HostKernel load_kernel_binary(const std::string& path) {
       in.space = S_CONST;
       in.width = sm->second.width;
     }
+    auto pk = pkind.find(in.opcode);
+    if (pk != pkind.end() && !(in.flags & (F_MEM | F_WAITCNT))) in.flags = (uint8_t)((in.flags & 0x0F) | pk->second);
     auto it = remap.find(in.opcode);
     if (it != remap.end()) in.opcode = it->second;
   }

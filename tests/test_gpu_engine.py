@@ -325,3 +325,34 @@ def test_host_streamed_trace_gpu_equals_cpu(gpu_mod, tmp_path, extra):
     strip = lambda s: {a: v for a, v in s.items() if not any(x in a for x in skip)}
     assert strip(st.stats) == strip(cpu.stats)
     assert re.search(r"^trace_host_streamed_kernels: 1$", st.output, re.M)
+
+
+def test_power_in_kernel_gpu_equals_cpu(gpu_mod, tmp_path):
+    """Power sampled inside engine_kernel (f64 MFMA sums of every unit's raw
+    counters, the sample evaluated by one block into a device ring): the
+    report equals the CPU engine's in-loop and host-sliced samples bit for
+    bit, and sampling costs no extra kernel launch."""
+    from accel_sim_framework_distributed_amd.models import presets
+    from accel_sim_framework_distributed_amd.power import xmlcfg
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    kl = rodinia.write_app(str(tmp_path / "hs"), rodinia.hotspot(512, 2, 2))
+    xml = str(tmp_path / "aw.xml")
+    xmlcfg.write_xml(xml, xmlcfg.default_params("QV100"))
+    out = {}
+    for tag, eng, inl, pwr in (("gpu", "gpu", "1", "1"), ("cpu", "cpu", "1", "1"), ("cpu_sliced", "cpu", "0", "1"),
+                               ("gpu_nopower", "gpu", "1", "0")):
+        rep = str(tmp_path / f"p_{tag}.log")
+        args = presets.args_for("QV100", {"-power_simulation_enabled": pwr, "-accelwattch_xml_file": xml,
+                                          "-gpgpu_runtime_stat": "200:0", "-power_report_file": rep,
+                                          "-power_in_loop": inl, "-sim_engine": eng}) + ["-trace", kl]
+        s = gpu_mod.Simulator(args, False)
+        assert s.run() == 0
+        m = re.search(r"^engine_kernel_launches: (\d+)", s.output, re.M)
+        n = re.search(r"^power_in_loop_samples: (\d+)", s.output, re.M)
+        out[tag] = (s.tot_cycle, open(rep).read() if pwr == "1" else "", int(m.group(1)) if m else 0,
+                    int(n.group(1)) if n else 0)
+    assert out["gpu"][0] == out["cpu"][0] == out["cpu_sliced"][0] == out["gpu_nopower"][0]
+    assert out["gpu"][1] == out["cpu"][1] == out["cpu_sliced"][1] and "kernel_avg_power" in out["gpu"][1]
+    assert out["gpu"][3] == out["cpu"][3] >= 10
+    # one launch per kernel run either way: sampling does not relaunch
+    assert out["gpu"][2] == out["gpu_nopower"][2] > 0
