@@ -280,6 +280,28 @@ def dvfs_matrix(A: np.ndarray, ratios: Sequence[float], v_floor: float) -> np.nd
 # (instruction issue, fp32 / int / fp64 / transcendental work), the matrix
 # cores, the memory pipeline on the CU and in the L2 (LDS, L1, L2, NoC and the
 # static power of those units when in use), and the HBM side
+# one factor per execution unit (round 4): every group is driven by at least
+# one single-unit calibration kernel of the power suite (csrc/apps/
+# power_suite.hip), as AccelWattch calibrates each component on its own
+# stress micro-benchmark; the unit mixes are held out for validation
+UNIT_GROUPS: Dict[str, List[str]] = {
+    "idle": ["CONSTP", "IDLE_COREP"],
+    "static": ["STATICP"],
+    "static_mem": ["STATIC_MEMP"],
+    "frontend": ["IBP", "ICP", "SCHEDP", "PIPEP", "RFP", "CCP"],
+    "int": ["INTP"],
+    "int_mul": ["INT_MULP", "INT_MUL24P", "INT_MUL32P", "INT_DIVP"],
+    "fp": ["FPUP", "FP_DIVP"],
+    "fp_mul": ["FP_MULP"],
+    "fp64": ["DPUP", "DP_MULP", "DP_DIVP"],
+    "sfu": ["FP_SQRTP", "FP_LGP", "FP_SINP", "FP_EXP"],
+    "tensor": ["TENSORP", "TEXP"],
+    "lds": ["SHRDP"],
+    "l1": ["DCP", "TCP"],
+    "l2": ["L2CP", "NOCP"],
+    "dram": ["DRAMP", "MCP"],
+}
+
 POWER_GROUPS: Dict[str, List[str]] = {
     "idle_static": ["CONSTP", "IDLE_COREP", "STATICP"],
     "valu": FINE_GROUPS["frontend"] + FINE_GROUPS["valu"] + FINE_GROUPS["sfu"] + FINE_GROUPS["fp64"],

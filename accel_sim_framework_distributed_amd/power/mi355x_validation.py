@@ -353,6 +353,84 @@ def run_traces(kernelslist: str, measured_csv: str, work: str, out_xml: str, con
     return s
 
 
+# the single-unit kernels of the power suite: the calibration set (every
+# other kernel -- unit mixes and occupancy variants -- is held out)
+CAL_KERNELS = ["idle", "fp32_fma", "fp32_add", "int32_add", "int32_mul", "fp64_fma", "fp64_add", "sfu_sqrt_exp",
+               "mfma_bf16", "lds_read", "lds_write", "hbm_read", "hbm_write", "l2_read", "l2_write", "l1_read",
+               "atomic_l2"]
+
+
+def fit_heldout(A: np.ndarray, b: np.ndarray, order: List[str], sclk: List[float], mv: List[float], cap: float,
+                max_sclk: float, cal: List[str] = CAL_KERNELS, bound: float = 20.0) -> Dict:
+    """Calibrate one factor per execution unit (calibrate.UNIT_GROUPS) on the
+    single-unit kernels only, each kernel's components moved to its measured
+    clock (DVFS matrix), then predict the disjoint held-out kernels: their
+    MAPE is the headline (reference util/accelwattch: quadprog_solver.m fits
+    on the validation micro-benchmarks, the suite validates)."""
+    sclk = np.asarray(sclk, np.float64)
+    fmax = max_sclk if max_sclk and not math.isnan(max_sclk) else float(np.nanmax(sclk))
+    ratios = np.clip(sclk / fmax, 0.05, 1.0)
+    v_floor = calibrate.v_floor_from_measurements(sclk, mv, fmax)
+    vsrc = "measured rail voltage vs clock"
+    if v_floor is None:
+        v_floor, vsrc = DEFAULT_V_FLOOR, ("not measurable here: amd-smi reports no graphics rail voltage on this "
+                                          "node (vddgfx NaN) and a non-root user cannot set clocks; the line's "
+                                          "floor is assumed")
+    ci = [i for i, n in enumerate(order) if n in cal]
+    vi = [i for i, n in enumerate(order) if n not in cal]
+    groups = calibrate.UNIT_GROUPS
+    Ad = calibrate.dvfs_matrix(A, ratios, v_floor)
+    x = calibrate.fit_groups_relative(Ad[ci], b[ci], groups=groups, lower=1.0 / bound, upper=bound)
+    pred = Ad @ x
+    before = Ad.sum(axis=1)
+    gf = calibrate.group_factors(x, groups)
+    at_bound = [g for g, v in gf.items() if v <= 1.0 / bound * 1.001 or v >= bound * 0.999]
+    # groups no calibration kernel exercises keep factor 1 (reported)
+    undriven = [g for g in groups if not any(Ad[i, [calibrate.CAL_COMPONENTS.index(c) for c in groups[g]
+                                                    if c in calibrate.CAL_COMPONENTS]].sum() > 0 for i in ci)]
+    bv, pv = b[vi], pred[vi]
+    return dict(kernels=list(order), calibration_kernels=[order[i] for i in ci],
+                heldout_kernels=[order[i] for i in vi], measured_w=b.tolist(), uncalibrated_w=before.tolist(),
+                calibrated_w=pred.tolist(),
+                mape_heldout=calibrate.mape(pv, bv)[0], mae_heldout_w=calibrate.mape(pv, bv)[1],
+                mape_heldout_uncalibrated=calibrate.mape(before[vi], bv)[0],
+                mape_calibration_in_sample=calibrate.mape(pred[ci], b[ci])[0],
+                mape_all=calibrate.mape(pred, b)[0], group_factors=gf, factors_at_bound=at_bound,
+                groups_not_driven=undriven, power_cap_w=float(cap), max_sclk_mhz=float(fmax),
+                measured_sclk_mhz=sclk.tolist(), measured_clock_ratio=ratios.tolist(),
+                measured_vddgfx_mv=[float(v) for v in mv], v_floor=float(v_floor), v_floor_source=vsrc,
+                components=list(calibrate.CAL_COMPONENTS), components_w=np.asarray(A).tolist(), groups=groups,
+                bounds=[1.0 / bound, bound],
+                model="per-unit factors fitted on single-unit kernels, validated on held-out mixes", _x=x)
+
+
+def run_heldout(kernelslist: str, measured_csv: str, work: str, out_xml: str, config_dir: str = TUNED,
+                bound: float = 20.0, engine: str = "cpu-split") -> Dict:
+    base_xml = os.path.join(config_dir, "accelwattch_sass_sim.xml")
+    if not os.path.exists(base_xml):
+        xmlcfg.write_xml(base_xml, xmlcfg.default_params("MI355X"))
+    meas = measured_power(measured_csv)
+    if engine == "cpu-split":
+        reps = simulate_trace_power_split(kernelslist, base_xml, work, config_dir,
+                                          int(os.environ.get("MAX_JOBS", "16") or 16))
+    else:
+        reps = simulate_trace_power(kernelslist, base_xml, work, config_dir, engine)
+    order = list(meas)
+    if len(reps) != len(order):
+        raise RuntimeError(f"{len(reps)} simulated kernels vs {len(order)} measured")
+    A = calibrate.design_matrix(reps, calibrate.CAL_COMPONENTS)
+    b = np.array([meas[n] for n in order])
+    rows, meta = measured_rows(measured_csv)
+    s = fit_heldout(A, b, order, [rows[n]["sclk"] for n in order], [rows[n]["mv"] for n in order],
+                    meta.get("power_cap_w", float("nan")), meta.get("max_sclk_mhz", float("nan")), bound=bound)
+    calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
+    _set_dvfs_params(out_xml, dict(v_floor=s["v_floor"], dvfs_min_clock_ratio=max(
+        0.3, min(1.0, float(np.nanmin(s["measured_clock_ratio"])) * 0.9))))
+    s.update(sim_cycles=[r.get("gpu_sim_cycle", 0.0) for r in reps], traces="automatic ISA traces (isatrace)",
+             xml=out_xml)
+    return s
+
+
 def _set_dvfs_params(xml: str, s: Dict) -> None:
     p = xmlcfg.read_xml(xml)
     p["dvfs_v_floor"] = float(s["v_floor"])
@@ -444,7 +522,11 @@ def refit(json_path: str, out_xml: str, config_dir: str = TUNED, bound: float = 
     A = np.asarray(old["components_w"], np.float64)
     b = np.asarray(old["measured_w"], np.float64)
     base_xml = os.path.join(config_dir, "accelwattch_sass_sim.xml")
-    if "measured_sclk_mhz" in old:
+    if "calibration_kernels" in old:
+        s = fit_heldout(A, b, old["kernels"], old["measured_sclk_mhz"], old.get("measured_vddgfx_mv", []),
+                        old["power_cap_w"], old.get("max_sclk_mhz", float("nan")), bound=bound)
+        calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
+    elif "measured_sclk_mhz" in old:
         s = fit_report_dvfs(A, b, old["kernels"], old["measured_sclk_mhz"], old.get("measured_vddgfx_mv", []),
                             old["power_cap_w"], old.get("max_sclk_mhz", float("nan")), bound)
         calibrate.apply_factors(base_xml, out_xml, s.pop("_x"), power_cap=s["power_cap_w"])
@@ -469,10 +551,26 @@ def main(argv=None) -> int:
     ap.add_argument("-c", "--config_dir", default=TUNED)
     ap.add_argument("-e", "--engine", default="cpu", help="cpu | gpu (the MI355X cycle engine)")
     ap.add_argument("--refit", default="", help="re-fit a saved validation JSON (no simulation)")
+    ap.add_argument("--heldout", action="store_true",
+                    help="calibrate on the single-unit kernels, validate on the held-out rest")
     o = ap.parse_args(argv)
     work = o.work or tempfile.mkdtemp(prefix="asim_power_")
     if o.refit:
         s = refit(o.refit, o.out_xml, o.config_dir)
+    elif o.traces and o.heldout:
+        s = run_heldout(o.traces, o.measured or MEASURED, work, o.out_xml, o.config_dir, engine=o.engine)
+        with open(o.json, "w") as f:
+            json.dump(s, f, indent=1)
+        print(f"{'kernel':16s} {'set':4s} {'measured':>9s} {'uncal':>9s} {'model':>9s}")
+        for i, n in enumerate(s["kernels"]):
+            print(f"{n:16s} {'cal' if n in s['calibration_kernels'] else 'val':4s} {s['measured_w'][i]:9.1f} "
+                  f"{s['uncalibrated_w'][i]:9.1f} {s['calibrated_w'][i]:9.1f}")
+        print(f"held-out MAPE {s['mape_heldout']:.2f}% ({s['mae_heldout_w']:.1f} W) on {len(s['heldout_kernels'])} "
+              f"kernels; uncalibrated {s['mape_heldout_uncalibrated']:.2f}%; calibration in-sample "
+              f"{s['mape_calibration_in_sample']:.2f}% on {len(s['calibration_kernels'])}")
+        print("group factors:", {g: round(v, 3) for g, v in s["group_factors"].items()}, "at bound:",
+              s["factors_at_bound"], "not driven:", s["groups_not_driven"])
+        return 0
     elif o.traces:
         s = run_traces(o.traces, o.measured or MEASURED, work, o.out_xml, o.config_dir, engine=o.engine)
     else:

@@ -180,8 +180,10 @@ def main() -> int:
     insn = 0
     insn_gpu = 0
     cycles = 0
+    last_apps = {}
     for _ in range(a.steps):
         r = suite.step()
+        last_apps = r.get("apps", {})
         insn += r["insn"]
         insn_gpu += r["insn_gpu"]
         cycles += r["cycles"]
@@ -244,6 +246,9 @@ def main() -> int:
                     "node_calibration_s": suite.calibration,
                     "node_predicted_step_ms": round(suite.predicted_span * 1e3, 1),
                     "node_cpu_threads": {k: v for k, v in suite.threads.items() if v > 1},
+                    # wall seconds of every application in the last timed step
+                    # (the step's makespan is the longest of them)
+                    "node_step_wall_s": {k: round(v.get("wall_s", 0.0), 4) for k, v in last_apps.items()},
                     "node_host_cores": suite.cpu_slots(reserve=max(1, suite.concurrency()))} if engine == "node" else {}),
                 "apps": len(suite.apps),
                 "sim_insn_per_step_per_rank": int(insn / max(1, a.steps)),

@@ -1,9 +1,10 @@
 // UB_LIBS: -lamd_smi -lpthread
 // Power validation suite (reference util/accelwattch: the AccelWattch
 // validation micro-benchmarks + accelwattch_hw_profiler/measureGpuPower.cpp
-// and hw_power_validation_volta.csv): 30 kernels spanning VALU fp32 / int /
-// fp64, transcendental, MFMA, LDS, L1-, L2- and HBM-resident traffic, atomics,
-// mixes of them and several occupancy levels, plus idle.
+// and hw_power_validation_volta.csv): 46 kernels spanning VALU fp32 / int /
+// fp64 (add and multiply separately), transcendental, MFMA, LDS, L1-, L2- and
+// HBM-resident traffic, atomics, mixes of them and several occupancy levels,
+// plus idle.  The one-unit kernels calibrate, the rest are held out.
 //
 //   power_suite measure [seconds]   every kernel back to back for `seconds`
 //                                   while a host thread samples socket power
@@ -209,6 +210,173 @@ __global__ void k_int_lds(float* sink, int iters) {
   if (x == 7u) sink[0] = (float)x;
 }
 
+// ---- round 4: one execution unit per kernel (the calibration set) and more
+// unit mixes (the held-out validation set; power/mi355x_validation.py) ----
+__global__ void k_fp32_add(float* sink, int iters) {
+  float x[8];
+  const float y = 0.25f + 1e-7f * threadIdx.x;
+  for (int k = 0; k < 8; ++k) x[k] = threadIdx.x + k;
+  for (int i = 0; i < iters; ++i)
+    for (int k = 0; k < 8; ++k) x[k] = x[k] + y;
+  float s = 0;
+  for (int k = 0; k < 8; ++k) s += x[k];
+  if (s == -1.f) sink[0] = s;
+}
+
+__global__ void k_int_add(float* sink, int iters) {
+  unsigned x[8];
+  const unsigned y = 1013904223u + threadIdx.x;
+  for (int k = 0; k < 8; ++k) x[k] = threadIdx.x * 7 + k;
+  for (int i = 0; i < iters; ++i)
+    for (int k = 0; k < 8; ++k) x[k] = (x[k] ^ (unsigned)k) + y;
+  unsigned s = 0;
+  for (int k = 0; k < 8; ++k) s ^= x[k];
+  if (s == 7u) sink[0] = (float)s;
+}
+
+__global__ void k_int_mul(float* sink, int iters) {
+  unsigned x[8];
+  for (int k = 0; k < 8; ++k) x[k] = threadIdx.x * 7 + 2 * k + 1;
+  for (int i = 0; i < iters; ++i)
+    for (int k = 0; k < 8; ++k) x[k] = x[k] * 1664525u;
+  unsigned s = 0;
+  for (int k = 0; k < 8; ++k) s ^= x[k];
+  if (s == 7u) sink[0] = (float)s;
+}
+
+__global__ void k_fp64_add(float* sink, int iters) {
+  double x[8];
+  const double y = 0.25 + 1e-9 * threadIdx.x;
+  for (int k = 0; k < 8; ++k) x[k] = threadIdx.x + k;
+  for (int i = 0; i < iters; ++i)
+    for (int k = 0; k < 8; ++k) x[k] = x[k] + y;
+  double s = 0;
+  for (int k = 0; k < 8; ++k) s += x[k];
+  if (s == -1.0) sink[0] = (float)s;
+}
+
+__global__ void k_int_fp(float* sink, int iters) {
+  unsigned u[4];
+  float f[4];
+  for (int k = 0; k < 4; ++k) {
+    u[k] = threadIdx.x * 3 + k;
+    f[k] = threadIdx.x + k;
+  }
+  for (int i = 0; i < iters; ++i)
+    for (int k = 0; k < 4; ++k) {
+      u[k] = u[k] * 1664525u + 1013904223u;
+      f[k] = __builtin_fmaf(f[k], 1.000001f, 0.25f);
+    }
+  float s = 0;
+  for (int k = 0; k < 4; ++k) s += f[k] + (float)(u[k] & 1);
+  if (s == -1.f) sink[0] = s;
+}
+
+__global__ void k_fp64_lds(float* sink, int iters) {
+  __shared__ float s[4096];
+  for (int i = threadIdx.x; i < 4096; i += blockDim.x) s[i] = (float)i;
+  __syncthreads();
+  double x = threadIdx.x;
+  unsigned idx = threadIdx.x;
+  for (int i = 0; i < iters; ++i) {
+    x = __builtin_fma(x, 1.000001, (double)s[idx & 4095]);
+    x = __builtin_fma(x, 0.999999, 0.5);
+    idx += 64;
+  }
+  if (x == -1.0) sink[0] = (float)x;
+}
+
+__global__ void k_sfu_fp32(float* sink, int iters) {
+  float x = threadIdx.x + 1.5f, y[4] = {1.f, 2.f, 3.f, 4.f};
+  for (int i = 0; i < iters; ++i) {
+    x = __builtin_sqrtf(x) + 1.0f;
+    for (int k = 0; k < 4; ++k) y[k] = __builtin_fmaf(y[k], 0.999f, x);
+  }
+  if (x + y[0] + y[1] + y[2] + y[3] == -1.f) sink[0] = x;
+}
+
+__global__ void k_mfma_lds(float* sink, int iters) {
+  __shared__ float sm[4096];
+  for (int i = threadIdx.x; i < 4096; i += blockDim.x) sm[i] = (float)i;
+  __syncthreads();
+  bf16x8 a, b;
+  for (int i = 0; i < 8; ++i) {
+    a[i] = (__bf16)(0.001f * (threadIdx.x + i));
+    b[i] = (__bf16)0.5f;
+  }
+  f32x16 c0 = {};
+  float acc = 0;
+  unsigned idx = threadIdx.x;
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    acc += sm[idx & 4095];
+    acc += sm[(idx + 2048) & 4095];
+    idx += 64;
+  }
+  float s = acc;
+  for (int i = 0; i < 16; ++i) s += c0[i];
+  if (s == -1.f) sink[0] = s;
+}
+
+__global__ void k_mfma_read(const float4* __restrict__ a, size_t n, float* sink) {
+  bf16x8 x, y;
+  for (int i = 0; i < 8; ++i) {
+    x[i] = (__bf16)(0.001f * (threadIdx.x + i));
+    y[i] = (__bf16)0.5f;
+  }
+  f32x16 c0 = {};
+  float acc = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    acc += a[i].x;
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c0, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c0, 0, 0, 0);
+  }
+  float s = acc;
+  for (int i = 0; i < 16; ++i) s += c0[i];
+  if (s == -1.f) sink[0] = s;
+}
+
+// fp32 FMAs over a buffer swept `reps` times (L2-resident when small)
+__global__ void k_fp32_read_reps(const float4* __restrict__ a, size_t n, int reps, int iters, float* sink) {
+  float x = threadIdx.x, acc = 0;
+  for (int r = 0; r < reps; ++r)
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+      acc += a[i].y;
+      for (int k = 0; k < iters; ++k) x = __builtin_fmaf(x, 1.00001f, acc);
+    }
+  if (x == -1.f) sink[0] = x;
+}
+
+__global__ void k_int_read(const float4* __restrict__ a, size_t n, int iters, float* sink) {
+  unsigned x = threadIdx.x;
+  float acc = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    acc += a[i].w;
+    for (int k = 0; k < iters; ++k) x = x * 1664525u + (unsigned)acc;
+  }
+  if (x == 7u) sink[0] = acc;
+}
+
+__global__ void k_fp64_l1(const float4* __restrict__ a, int reps, float* sink) {
+  const float4* p = a + (size_t)(blockIdx.x % 64) * 1024;
+  double x = threadIdx.x;
+  for (int r = 0; r < reps; ++r)
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+      x = __builtin_fma(x, 1.000001, (double)p[i].x);
+      x = __builtin_fma(x, 0.999999, 0.5);
+    }
+  if (x == -1.0) sink[0] = (float)x;
+}
+
+__global__ void k_atomic_fp32(unsigned* ctr, int iters, float* sink) {
+  float x = threadIdx.x;
+  for (int i = 0; i < iters; ++i) {
+    atomicAdd(&ctr[(threadIdx.x + i * 64) & 4095], 1u);
+    for (int k = 0; k < 8; ++k) x = __builtin_fmaf(x, 1.000001f, 0.25f);
+  }
+  if (x == -1.f) sink[0] = x;
+}
+
 struct Sampler {
   amdsmi_processor_handle h = nullptr;
   bool ok = false;
@@ -370,6 +538,24 @@ int main(int argc, char** argv) {
       {"hbm_read_occ2", [&] { k_read<<<g(2), b>>>(buf, nbig, trace ? 1 : 4, sink); }},
       {"l2_write", [&] { k_write<<<g(8), b>>>(buf, l2 / 16, trace ? 2 : 2 * sc); }},
       {"lds_read_occ2", [&] { k_lds_read<<<g(2), b>>>(sink, 16 * sc); }},
+      // round 4: one unit per kernel (calibration) ...
+      {"fp32_add", [&] { k_fp32_add<<<g(8), b>>>(sink, 8 * scv); }},
+      {"int32_add", [&] { k_int_add<<<g(8), b>>>(sink, 8 * scv); }},
+      {"int32_mul", [&] { k_int_mul<<<g(8), b>>>(sink, 8 * scv); }},
+      {"fp64_add", [&] { k_fp64_add<<<g(8), b>>>(sink, 4 * scv); }},
+      // ... and unit mixes (held out)
+      {"int_fp_mix", [&] { k_int_fp<<<g(8), b>>>(sink, 8 * scv); }},
+      {"fp64_lds_mix", [&] { k_fp64_lds<<<g(8), b>>>(sink, 8 * sc); }},
+      {"sfu_fp32_mix", [&] { k_sfu_fp32<<<g(8), b>>>(sink, 8 * scv); }},
+      {"mfma_lds_mix", [&] { k_mfma_lds<<<g(8), b>>>(sink, 2 * scv); }},
+      {"mfma_hbm_mix", [&] { k_mfma_read<<<g(16), b>>>(buf, nbig, sink); }},
+      {"fp32_l2_mix", [&] { k_fp32_read_reps<<<g(8), b>>>(buf, l2 / 16, trace ? 2 : 2 * sc, 4, sink); }},
+      {"int_hbm_mix", [&] { k_int_read<<<g(16), b>>>(buf, nbig, 4, sink); }},
+      {"fp64_l1_mix", [&] { k_fp64_l1<<<g(8), b>>>(buf, trace ? 2 : sc / 4, sink); }},
+      {"atomic_fp32_mix", [&] { k_atomic_fp32<<<g(4), b>>>(ctr, trace ? 2 : sc / 8, sink); }},
+      {"lds_write_occ2", [&] { k_lds_write<<<g(2), b>>>(sink, 16 * sc); }},
+      {"hbm_write_occ2", [&] { k_write<<<g(2), b>>>(buf, nbig, trace ? 1 : 4); }},
+      {"int32_add_occ2", [&] { k_int_add<<<g(2), b>>>(sink, 8 * scv); }},
   };
   if (trace) {
     for (auto& k : ks) {
