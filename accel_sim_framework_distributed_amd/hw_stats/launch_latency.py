@@ -128,10 +128,13 @@ def main(argv=None) -> int:
         print(f"# idle_launch_cycles {int(round(ia * mhz / 1000.0))}")
         # the model's launch latency (to the first workgroup) is the idle
         # launch; a queued kernel pays the same plus the minimum duration
-        # above.  Reported, not applied: the idle launch measured 1.5 us and
-        # 2.1 us on two boxes of the same round, and the preset keeps the
-        # values that the suite's correlation supports (models/presets.py)
-        print(f"# suggested -gpgpu_kernel_launch_latency {int(round(ia * mhz / 1000.0))}")
+        # above.  Applied by the tuner (suggest_ lines): every launch
+        # parameter comes from this micro-benchmark, none is fitted on the
+        # suite (correlation protocol, profiles/correlation/README.md)
+        il = int(round(ia * mhz / 1000.0))
+        print(f"# suggested -gpgpu_kernel_launch_latency {il}")
+        print(f"# suggest_gpgpu_kernel_launch_latency {il}")
+        print(f"# suggest_gpgpu_kernel_launch_latency_queued {il}")
         print(f"-gpgpu_TB_launch_latency {int(round(ib * mhz / 1000.0))}")
     # the first kernel after a host-to-device copy vs the same kernel re-run
     ac = read_durations(run_dir, "ub_touch_after_copy")
@@ -142,12 +145,17 @@ def main(argv=None) -> int:
         print(f"# after_copy_kernel_ns {a_med:.1f}\n# same_kernel_again_ns {g_med:.1f}")
         print(f"# after_copy_extra_cycles {int(round((a_med - g_med) * mhz / 1000.0))}")
         print(f"# suggested -sim_first_kernel_latency {max(0, int(round((a_med - g_med) * mhz / 1000.0)))}")
+        print(f"# suggest_sim_first_kernel_latency {max(0, int(round((a_med - g_med) * mhz / 1000.0)))}")
     # back-to-back chains: steady-state start-to-start interval and duration
     ch = chain_stats(run_dir)
     if ch:
         print(f"# chain_start_interval_ns {ch[0]:.1f}")
         print(f"# chain_duration_ns {ch[1]:.1f}")
         print(f"# chain_gap_ns {ch[2]:.1f}")
+        # a host loop submitting back to back: its start-to-start interval is
+        # the host's submission interval (the GPU-side queued minimum is
+        # shorter), what -sim_host_launch_interval models
+        print(f"# suggest_sim_host_launch_interval {int(round(ch[0] * mhz / 1000.0))}")
     return 0
 
 

@@ -592,9 +592,11 @@ def _mi355x() -> Dict[str, str]:
         # hw_stats/launch_latency.py): 1.5 us from an idle queue to the first
         # workgroup; a kernel queued behind another lasts >= 4.7 us (the
         # command processor's dependent back-to-back dispatch); the run's first
-        # kernel pays a cold start.  The host submits a kernel every ~5 us
-        # (fitted on the Rodinia suite: pathfinder's host-bound launches vs the
-        # back-to-back ones of lud / hotspot / nw, profiles/correlation)
+        # kernel pays a cold start; a host loop submits a kernel every ~5-7 us
+        # (ub_launch's back-to-back chains).  These are defaults: the tuner
+        # replaces every one with the box's own micro-benchmark measurement
+        # (hw_stats/launch_latency.py suggest_ lines), none is fitted on the
+        # suite
         "-gpgpu_kernel_launch_latency": "3563",
         "-gpgpu_kernel_launch_latency_queued": "3563",
         "-sim_kernel_min_cycles_queued": "11251",

@@ -287,19 +287,15 @@ def dvfs_matrix(A: np.ndarray, ratios: Sequence[float], v_floor: float) -> np.nd
 UNIT_GROUPS: Dict[str, List[str]] = {
     "idle": ["CONSTP", "IDLE_COREP"],
     "static": ["STATICP"],
-    "static_mem": ["STATIC_MEMP"],
     "frontend": ["IBP", "ICP", "SCHEDP", "PIPEP", "RFP", "CCP"],
-    "int": ["INTP"],
-    "int_mul": ["INT_MULP", "INT_MUL24P", "INT_MUL32P", "INT_DIVP"],
-    "fp": ["FPUP", "FP_DIVP"],
-    "fp_mul": ["FP_MULP"],
+    "int": ["INTP", "INT_MULP", "INT_MUL24P", "INT_MUL32P", "INT_DIVP"],
+    "fp": ["FPUP", "FP_DIVP", "FP_MULP", "FP_SQRTP", "FP_LGP", "FP_SINP", "FP_EXP"],
     "fp64": ["DPUP", "DP_MULP", "DP_DIVP"],
-    "sfu": ["FP_SQRTP", "FP_LGP", "FP_SINP", "FP_EXP"],
     "tensor": ["TENSORP", "TEXP"],
-    "lds": ["SHRDP"],
-    "l1": ["DCP", "TCP"],
-    "l2": ["L2CP", "NOCP"],
-    "dram": ["DRAMP", "MCP"],
+    # the memory units: LDS, L1, L2 accesses, their "in use" static power and
+    # the fabric / HBM traffic (separate factors are not identifiable from the
+    # single-unit kernels: each memory kernel drives several of them)
+    "memory": ["SHRDP", "DCP", "TCP", "L2CP", "NOCP", "STATIC_MEMP", "DRAMP", "MCP"],
 }
 
 POWER_GROUPS: Dict[str, List[str]] = {

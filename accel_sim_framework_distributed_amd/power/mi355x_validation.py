@@ -353,11 +353,14 @@ def run_traces(kernelslist: str, measured_csv: str, work: str, out_xml: str, con
     return s
 
 
-# the single-unit kernels of the power suite: the calibration set (every
-# other kernel -- unit mixes and occupancy variants -- is held out)
+# the single-unit kernels of the power suite, at every occupancy they run at:
+# the calibration set (the occupancy points separate a unit's always-on
+# power from its per-instruction energy).  Every unit mix is held out.
 CAL_KERNELS = ["idle", "fp32_fma", "fp32_add", "int32_add", "int32_mul", "fp64_fma", "fp64_add", "sfu_sqrt_exp",
                "mfma_bf16", "lds_read", "lds_write", "hbm_read", "hbm_write", "l2_read", "l2_write", "l1_read",
-               "atomic_l2"]
+               "atomic_l2", "fp32_fma_occ1", "fp32_fma_occ2", "fp32_fma_occ4", "mfma_bf16_occ2", "mfma_bf16_occ4",
+               "sfu_occ2", "fp64_fma_occ2", "hbm_read_occ2", "lds_read_occ2", "lds_write_occ2", "hbm_write_occ2",
+               "int32_add_occ2", "fp32_fma_light"]
 
 
 def fit_heldout(A: np.ndarray, b: np.ndarray, order: List[str], sclk: List[float], mv: List[float], cap: float,

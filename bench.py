@@ -61,9 +61,15 @@ def _cycle_mae():
     the Rodinia-2.0-ft HIP suite traced by the automatic ISA tracer, timed
     with rocprofv3, simulated by the MI355X cycle engine with the tuned
     MI355X config; correlator semantics of plot-correlation.py)."""
-    # the last full GPU correlation run (round 3, final tree: fresh ubench ->
-    # tuner -> traces -> timings -> counters on one box)
-    p = os.path.join(ROOT, "profiles", "correlation", "rodinia_hip_isatrace_r3g_gpu.json")
+    # the latest full GPU correlation run (fresh ubench -> tuner -> traces ->
+    # timings -> counters on one box): profiles/correlation/LATEST names it
+    # (tools/gpu_correlate.sh records; updated with every committed run)
+    cdir = os.path.join(ROOT, "profiles", "correlation")
+    try:
+        p = os.path.join(cdir, open(os.path.join(cdir, "LATEST")).read().strip())
+    except OSError:
+        runs = sorted(f for f in os.listdir(cdir) if f.endswith("_gpu.json")) if os.path.isdir(cdir) else []
+        p = os.path.join(cdir, runs[-1]) if runs else ""
     try:
         d = json.load(open(p))["Cycles"]
         cfg, v = next(iter(d.items()))

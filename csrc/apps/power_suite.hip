@@ -1,7 +1,7 @@
 // UB_LIBS: -lamd_smi -lpthread
 // Power validation suite (reference util/accelwattch: the AccelWattch
 // validation micro-benchmarks + accelwattch_hw_profiler/measureGpuPower.cpp
-// and hw_power_validation_volta.csv): 46 kernels spanning VALU fp32 / int /
+// and hw_power_validation_volta.csv): kernels spanning VALU fp32 / int /
 // fp64 (add and multiply separately), transcendental, MFMA, LDS, L1-, L2- and
 // HBM-resident traffic, atomics, mixes of them and several occupancy levels,
 // plus idle.  The one-unit kernels calibrate, the rest are held out.
@@ -377,6 +377,153 @@ __global__ void k_atomic_fp32(unsigned* ctr, int iters, float* sink) {
   if (x == -1.f) sink[0] = x;
 }
 
+// more held-out unit mixes
+__global__ void k_int_fp64(float* sink, int iters) {
+  unsigned u[4];
+  double f[4];
+  for (int k = 0; k < 4; ++k) {
+    u[k] = threadIdx.x * 5 + k;
+    f[k] = threadIdx.x + k;
+  }
+  for (int i = 0; i < iters; ++i)
+    for (int k = 0; k < 4; ++k) {
+      u[k] = u[k] * 1664525u;
+      f[k] = __builtin_fma(f[k], 1.000001, 0.25);
+    }
+  double s = 0;
+  for (int k = 0; k < 4; ++k) s += f[k] + (double)(u[k] & 1);
+  if (s == -1.0) sink[0] = (float)s;
+}
+
+__global__ void k_sfu_int(float* sink, int iters) {
+  float x = threadIdx.x + 1.5f;
+  unsigned u[4];
+  for (int k = 0; k < 4; ++k) u[k] = threadIdx.x + k;
+  for (int i = 0; i < iters; ++i) {
+    x = __expf(-x) + 1.0f;
+    for (int k = 0; k < 4; ++k) u[k] = (u[k] ^ 0x9e3779b9u) + (unsigned)k;
+  }
+  if (x + (float)(u[0] ^ u[1] ^ u[2] ^ u[3]) == -1.f) sink[0] = x;
+}
+
+__global__ void k_lds_read_hbm(const float4* __restrict__ a, size_t n, float* sink) {
+  __shared__ float sm[4096];
+  for (int i = threadIdx.x; i < 4096; i += blockDim.x) sm[i] = (float)i;
+  __syncthreads();
+  float acc = 0;
+  unsigned idx = threadIdx.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    acc += a[i].x;
+    for (int k = 0; k < 4; ++k) {
+      acc += sm[idx & 4095];
+      idx += 64;
+    }
+  }
+  if (acc == -1.f) sink[0] = acc;
+}
+
+__global__ void k_fp32_lds_write(float* sink, int iters) {
+  __shared__ float sm[4096];
+  float x = threadIdx.x;
+  unsigned idx = threadIdx.x;
+  for (int i = 0; i < iters; ++i) {
+    x = __builtin_fmaf(x, 1.000001f, 0.25f);
+    x = __builtin_fmaf(x, 0.999999f, 0.5f);
+    sm[idx & 4095] = x;
+    idx += 64;
+  }
+  __syncthreads();
+  if (sm[threadIdx.x] == -1.f) sink[0] = 1.f;
+}
+
+__global__ void k_mfma_fp64(float* sink, int iters) {
+  bf16x8 a, b;
+  for (int i = 0; i < 8; ++i) {
+    a[i] = (__bf16)(0.001f * (threadIdx.x + i));
+    b[i] = (__bf16)0.5f;
+  }
+  f32x16 c0 = {};
+  double x[2] = {1.0, 2.0};
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    for (int k = 0; k < 2; ++k) x[k] = __builtin_fma(x[k], 0.999, 0.5);
+  }
+  float s = (float)(x[0] + x[1]);
+  for (int i = 0; i < 16; ++i) s += c0[i];
+  if (s == -1.f) sink[0] = s;
+}
+
+__global__ void k_int_l2(const float4* __restrict__ a, size_t n, int reps, float* sink) {
+  unsigned x = threadIdx.x;
+  for (int r = 0; r < reps; ++r)
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+      x ^= __float_as_uint(a[i].z);
+      for (int k = 0; k < 4; ++k) x = (x ^ 0x9e3779b9u) + (unsigned)k;
+    }
+  if (x == 7u) sink[0] = 1.f;
+}
+
+__global__ void k_fp_int_add(float* sink, int iters) {
+  float f[4];
+  unsigned u[4];
+  const float y = 0.25f + 1e-7f * threadIdx.x;
+  for (int k = 0; k < 4; ++k) {
+    f[k] = threadIdx.x + k;
+    u[k] = threadIdx.x * 3 + k;
+  }
+  for (int i = 0; i < iters; ++i)
+    for (int k = 0; k < 4; ++k) {
+      f[k] = f[k] + y;
+      u[k] = (u[k] ^ (unsigned)k) + 1013904223u;
+    }
+  float s = 0;
+  for (int k = 0; k < 4; ++k) s += f[k] + (float)(u[k] & 1);
+  if (s == -1.f) sink[0] = s;
+}
+
+__global__ void k_copy_fp32(const float4* __restrict__ a, float4* __restrict__ b, size_t n, float* sink) {
+  float x = threadIdx.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float4 v = a[i];
+    for (int k = 0; k < 4; ++k) x = __builtin_fmaf(x, 1.000001f, v.x);
+    v.y = x;
+    b[i] = v;
+  }
+  if (x == -1.f) sink[0] = x;
+}
+
+__global__ void k_mfma_sfu(float* sink, int iters) {
+  bf16x8 a, b;
+  for (int i = 0; i < 8; ++i) {
+    a[i] = (__bf16)(0.001f * (threadIdx.x + i));
+    b[i] = (__bf16)0.5f;
+  }
+  f32x16 c0 = {};
+  float x = threadIdx.x + 1.5f;
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    x = __builtin_sqrtf(x) + 1.0f;
+  }
+  float s = x;
+  for (int i = 0; i < 16; ++i) s += c0[i];
+  if (s == -1.f) sink[0] = s;
+}
+
+__global__ void k_lds_l1(const float4* __restrict__ a, int reps, float* sink) {
+  __shared__ float sm[4096];
+  for (int i = threadIdx.x; i < 4096; i += blockDim.x) sm[i] = (float)i;
+  __syncthreads();
+  const float4* p = a + (size_t)(blockIdx.x % 64) * 1024;
+  float acc = 0;
+  unsigned idx = threadIdx.x;
+  for (int r = 0; r < reps; ++r)
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+      acc += p[i].x + sm[idx & 4095];
+      idx += 64;
+    }
+  if (acc == -1.f) sink[0] = acc;
+}
+
 struct Sampler {
   amdsmi_processor_handle h = nullptr;
   bool ok = false;
@@ -530,7 +677,9 @@ int main(int argc, char** argv) {
       {"fp32_hbm_mix", [&] { k_fp32_read<<<g(16), b>>>(buf, nbig, 8, sink); }},
       {"fp64_hbm_mix", [&] { k_fp64_read<<<g(16), b>>>(buf, nbig, 4, sink); }},
       {"atomic_l2", [&] { k_atomic<<<g(4), b>>>(ctr, trace ? 2 : sc / 8); }},
-      {"fp32_fma_light", [&] { k_fp32<<<g(8), b>>>(sink, sc); }},
+      // the same loop as fp32_fma with 8x fewer iterations per launch (more
+      // launch gaps in the measurement); traced at the VALU kernels' length
+      {"fp32_fma_light", [&] { k_fp32<<<g(8), b>>>(sink, trace ? scv : sc); }},
       // round 3: more occupancy / unit-mix points between the saturating ones
       {"mfma_bf16_occ4", [&] { k_mfma<<<g(4), b>>>(sink, 2 * scv); }},
       {"sfu_occ2", [&] { k_sfu<<<g(2), b>>>(sink, 8 * scv); }},
@@ -556,6 +705,18 @@ int main(int argc, char** argv) {
       {"lds_write_occ2", [&] { k_lds_write<<<g(2), b>>>(sink, 16 * sc); }},
       {"hbm_write_occ2", [&] { k_write<<<g(2), b>>>(buf, nbig, trace ? 1 : 4); }},
       {"int32_add_occ2", [&] { k_int_add<<<g(2), b>>>(sink, 8 * scv); }},
+      {"int_fp64_mix", [&] { k_int_fp64<<<g(8), b>>>(sink, 8 * scv); }},
+      {"sfu_int_mix", [&] { k_sfu_int<<<g(8), b>>>(sink, 8 * scv); }},
+      {"lds_hbm_mix", [&] { k_lds_read_hbm<<<g(16), b>>>(buf, nbig, sink); }},
+      {"fp32_lds_write_mix", [&] { k_fp32_lds_write<<<g(8), b>>>(sink, 16 * sc); }},
+      {"mfma_fp64_mix", [&] { k_mfma_fp64<<<g(8), b>>>(sink, 2 * scv); }},
+      {"int_l2_mix", [&] { k_int_l2<<<g(8), b>>>(buf, l2 / 16, trace ? 2 : 2 * sc, sink); }},
+      {"fp_int_add_mix", [&] { k_fp_int_add<<<g(8), b>>>(sink, 8 * scv); }},
+      {"copy_fp32_mix", [&] { k_copy_fp32<<<g(16), b>>>(buf, buf2, nbig / 2, sink); }},
+      {"mfma_sfu_mix", [&] { k_mfma_sfu<<<g(8), b>>>(sink, 2 * scv); }},
+      {"lds_l1_mix", [&] { k_lds_l1<<<g(8), b>>>(buf, trace ? 2 : sc / 4, sink); }},
+      {"int_fp_mix_occ2", [&] { k_int_fp<<<g(2), b>>>(sink, 8 * scv); }},
+      {"sfu_fp32_mix_occ2", [&] { k_sfu_fp32<<<g(2), b>>>(sink, 8 * scv); }},
   };
   if (trace) {
     for (auto& k : ks) {
