@@ -294,13 +294,18 @@ class DistributedSuite:
         tc = [self.times.get((a, "cpu"), 1.0) for a in names]
         th = [self.threads.get(a, 1) for a in names]
         n = len(names)
-        best = (float("inf"), 0)
+        spans = []
         for m in range(1 << n) if n <= 16 else [(1 << n) - 1]:
             g = [tg[i] for i in range(n) if m >> i & 1]
             c = [(tc[i], th[i]) for i in range(n) if not m >> i & 1]
-            span = max(self._lpt(g, gslots), self._cores_span(c, cslots))
-            if span < best[0]:
-                best = (span, m)
+            spans.append((max(self._lpt(g, gslots), self._cores_span(c, cslots)), m))
+        lo = min(sp for sp, _ in spans)
+        # among the plans within `gpu_tolerance` of the shortest makespan, the
+        # one that runs the most applications on the GPU engine (host cores
+        # stay free for other work; the prediction is what decides)
+        tol = float(os.environ.get("ASIM_NODE_GPU_TOLERANCE", "0.02"))
+        best = min(((sp, m) for sp, m in spans if sp <= lo * (1.0 + tol)),
+                   key=lambda x: (-bin(x[1]).count("1"), x[0]))
         self.assignment = {names[i]: ("gpu" if best[1] >> i & 1 else "cpu") for i in range(n)}
         self.predicted_span = best[0]
         return self.assignment

@@ -163,6 +163,26 @@ def test_node_plan_places_apps_by_makespan(native, tmp_path, monkeypatch):
     assert abs(s.predicted_span - 0.5) < 1e-9
 
 
+def test_node_plan_prefers_gpu_among_equal_makespans(native, tmp_path, monkeypatch):
+    """Plans within 2 % of the shortest makespan: the one with the most
+    applications on the GPU engine wins."""
+    from accel_sim_framework_distributed_amd.parallel.multi_gpu import DistributedSuite
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    apps = ["nn-rodinia-2.0-ft", "pathfinder-rodinia-2.0-ft", "backprop-rodinia-2.0-ft"]
+    rodinia.generate_suite(str(tmp_path), apps)
+    monkeypatch.setenv("ASIM_CPU_JOBS", "9")
+    s = DistributedSuite(str(tmp_path), engine="node")
+    # backprop sets the span (1.0 s either way); nn and pathfinder are short
+    # on both engines and fit on the GPU slot next to nothing else
+    t = {"nn-rodinia-2.0-ft": (0.2, 0.1), "pathfinder-rodinia-2.0-ft": (0.3, 0.1), "backprop-rodinia-2.0-ft": (2.0, 1.0)}
+    for a, (g, c) in t.items():
+        s.times[(a, "gpu")] = g
+        s.times[(a, "cpu")] = c
+    plan = s.plan()
+    assert abs(s.predicted_span - 1.0) < 1e-9
+    assert plan == {"nn-rodinia-2.0-ft": "gpu", "pathfinder-rodinia-2.0-ft": "gpu", "backprop-rodinia-2.0-ft": "cpu"}
+
+
 def test_node_widen_gives_threads_to_critical_cpu_app(native, tmp_path, monkeypatch):
     """Spare host cores go to the CPU-engine application on the critical path
     (-sim_cpu_threads), kept only while re-timing shows it scales; the plan
