@@ -679,7 +679,7 @@ int main(int argc, char** argv) {
       {"atomic_l2", [&] { k_atomic<<<g(4), b>>>(ctr, trace ? 2 : sc / 8); }},
       // the same loop as fp32_fma with 8x fewer iterations per launch (more
       // launch gaps in the measurement); traced at the VALU kernels' length
-      {"fp32_fma_light", [&] { k_fp32<<<g(8), b>>>(sink, trace ? scv : sc); }},
+      {"fp32_fma_light", [&] { k_fp32<<<g(8), b>>>(sink, trace ? 8 * scv : sc); }},
       // round 3: more occupancy / unit-mix points between the saturating ones
       {"mfma_bf16_occ4", [&] { k_mfma<<<g(4), b>>>(sink, 2 * scv); }},
       {"sfu_occ2", [&] { k_sfu<<<g(2), b>>>(sink, 8 * scv); }},

@@ -1026,8 +1026,12 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
         P::prof(37);
         int mi = P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return s.mshr[i].valid && s.mshr[i].line == a.line; });
         P::prof(3);
-        uint8_t need_req = miss;
-        if (mi >= 0) need_req = miss & (uint8_t)~s.mshr[mi].requested;
+        // a sectored L1 ('S') fetches the sectors the access misses; a
+        // line-granular one ('N') the whole line it does not hold (the L2's
+        // 'N' fill, mem.h l2_access)
+        const uint8_t fetch = g.sectored ? miss : (uint8_t)(0xFu & ~have);
+        uint8_t need_req = fetch;
+        if (mi >= 0) need_req = fetch & (uint8_t)~s.mshr[mi].requested;
         bool merged = (mi >= 0 && need_req == 0);
         if (merged) {
           if (s.mshr[mi].merges >= c.l1.mshr_merge) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
