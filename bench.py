@@ -77,7 +77,10 @@ def _cycle_mae():
                 "mae_pct_stable_apps": round(v["app"]["mae"], 2), "stable_apps": v["app"]["n"],
                 "pearson": round(v["app_incl_noisy"]["correl"], 4), "gpu": "MI355X", "config": cfg,
                 "traces": "automatic gfx950 ISA traces (isatrace)", "measured": "offline, not in this run",
-                "engine": "gpu", "source": os.path.relpath(p, ROOT)}
+                "engine": "cpu (bit-exact with the GPU engine)" if "local" in os.path.basename(p) else "gpu",
+                "protocol": "every config parameter from micro-benchmarks (tools/gpu_correlate.sh tuner); HW "
+                            "cycles the mean of 4 rocprofv3 runs",
+                "source": os.path.relpath(p, ROOT)}
     except (OSError, ValueError, KeyError, StopIteration):
         return None
 
