@@ -223,10 +223,11 @@ def test_cdna_scalar_loads_use_the_scalar_cache(native, tmp_path):
     full = run(True, 256, {})
     assert stat(full, "gpgpu_n_load_insn") == 256 * 4 * 8
     # nearby loads share a line (code offset / 8): the chain's 8 loads touch
-    # two 32-byte sectors, one miss each per CU (256 CUs, one CTA each); the
-    # other accesses hit or merge into them
+    # two 32-byte sectors of one 128-byte line, which the MI355X L1 fills
+    # whole (line-granular 'N'): one miss per CU (256 CUs, one CTA each); the
+    # other accesses hit or merge into it
     l1 = [stat(full, f"\tTotal_core_cache_stats_breakdown[GLOBAL_ACC_R][{k}]") for k in ("HIT", "MISS", "MSHR_HIT")]
-    assert l1[1] == 2 * 256 and sum(l1) == 256 * 4 * 8
+    assert l1[1] == 256 and sum(l1) == 256 * 4 * 8
     # latency: eight dependent round trips through the cache on one CU
     quiet = {"-gpgpu_kernel_launch_latency": "0", "-gpgpu_inst_prefetch_lines": "0"}
     ld, alu = run(True, 1, quiet), run(False, 1, quiet)
