@@ -130,6 +130,26 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
         cfg[k] = v
     out = os.path.join(out_root, name or device)
     presets.write_config(cfg, out, power_preset=base)
+    # self-consistency: ub_launch measured an empty kernel's whole duration
+    # from an idle queue (idle_launch_cycles); the simulator adds its own
+    # wave launch / end-of-kernel cost on top of -gpgpu_kernel_launch_latency,
+    # so the latency is lowered until the simulated empty kernel lasts what
+    # the hardware's did
+    if "idle_launch_cycles" in meas and "-gpgpu_kernel_launch_latency" in cfg:
+        try:
+            target = int(float(meas["idle_launch_cycles"]))
+            sim = simulated_empty_kernel_cycles(out)
+            lat = int(cfg["-gpgpu_kernel_launch_latency"])
+            new = max(0, lat - (sim - target))
+            if new != lat:
+                for k in ("-gpgpu_kernel_launch_latency", "-gpgpu_kernel_launch_latency_queued"):
+                    cfg[k] = str(new)
+                    applied[k] = str(new)
+                presets.write_config(cfg, out, power_preset=base)
+                notes.append(f"-gpgpu_kernel_launch_latency {lat} -> {new}: the simulated empty kernel lasted {sim} "
+                             f"cycles against the measured {target}")
+        except (ValueError, RuntimeError) as e:
+            notes.append(f"launch self-consistency skipped: {e}")
     with open(os.path.join(out, "TUNING.md"), "w") as f:
         f.write(f"# Tuned configuration for {device}\n\nBase preset: {base}\n\n")
         f.write("| option | tuned value | preset value |\n|---|---|---|\n")
@@ -143,6 +163,35 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
             for k in sorted(meas):
                 f.write(f"- {k}: {meas[k]}\n")
     return out, applied
+
+
+def simulated_empty_kernel_cycles(config_dir: str) -> int:
+    """Cycles the simulator gives an empty one-workgroup kernel launched from
+    an idle queue (the second of three back-to-back host launches) with the
+    configuration in `config_dir`: what ub_launch's idle empty kernel
+    measures on the hardware."""
+    import tempfile
+    from .. import _native
+    from ..tracegen import rodinia
+    from ..tracegen.builder import KernelBuilder
+    cfg = {}
+    for fn in ("gpgpusim.config", "trace.config"):
+        for line in open(os.path.join(config_dir, fn)):
+            t = line.split()
+            if len(t) >= 2 and t[0].startswith("-"):
+                cfg[t[0]] = t[1]
+    ws = int(cfg.get("-gpgpu_shader_core_pipeline", "2048:32").split(":")[1])
+    k = KernelBuilder("ub_empty_idle", (1, 1, 1), (ws, 1, 1), nregs=8, binary_version=950 if ws == 64 else 70,
+                      warp_size=ws)
+    k.op("s_endpgm" if ws == 64 else "EXIT")
+    d = tempfile.mkdtemp(prefix="asim_tune_")
+    kl = rodinia.write_app(os.path.join(d, "e"), [k.build()] * 3, memcpy=False)
+    args = ["-config", os.path.join(config_dir, "gpgpusim.config"), "-config", os.path.join(config_dir, "trace.config"),
+            "-trace", kl]
+    s = _native.load().Simulator(args, False)
+    if s.run() != 0:
+        raise RuntimeError("empty-kernel simulation failed")
+    return int(s.kernels[1]["cycles"])
 
 
 def _write_policies(meas: Dict[str, str]) -> Dict[str, Tuple[str, str]]:

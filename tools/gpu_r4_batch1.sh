@@ -3,7 +3,7 @@
 # host-streamed trace on the GPU engine, then the RCCL library-kernel counters.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-python3 -c "import os; print(\"host cpus: affinity\", len(os.sched_getaffinity(0)), \"cpu_count\", os.cpu_count())" | tee gpurun_out/r4_host_cpus.txt
+(python3 -c "import os; print(\"host cpus: affinity\", len(os.sched_getaffinity(0)), \"cpu_count\", os.cpu_count())"; cat /sys/fs/cgroup/cpu.max 2>&1; nproc) | tee gpurun_out/r4_host_cpus.txt
 timeout -k 10 400 python3 -u -m pytest tests/test_isatrace.py -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/r4_isatrace_tests2.log 2>&1
 rc=$?
 echo "pytest rc=$rc" | tee -a gpurun_out/r4_isatrace_tests2.log
