@@ -300,10 +300,13 @@ class DistributedSuite:
             c = [(tc[i], th[i]) for i in range(n) if not m >> i & 1]
             spans.append((max(self._lpt(g, gslots), self._cores_span(c, cslots)), m))
         lo = min(sp for sp, _ in spans)
-        # among the plans within `gpu_tolerance` of the shortest makespan, the
-        # one that runs the most applications on the GPU engine (host cores
-        # stay free for other work; the prediction is what decides)
-        tol = float(os.environ.get("ASIM_NODE_GPU_TOLERANCE", "0.02"))
+        # among the plans within ASIM_NODE_GPU_TOLERANCE of the shortest
+        # makespan, the one that runs the most applications on the GPU engine.
+        # Default 0 (exact ties only): on MI355X a 2 % tolerance moved 4 more
+        # apps onto the GPU engine, whose concurrent runs then slowed each
+        # other -- 205.7 ms/step against 183.7 ms for the pure-makespan plan
+        # (profiles/r4/bench_node_r4_gpu_tiebreak.json)
+        tol = float(os.environ.get("ASIM_NODE_GPU_TOLERANCE", "0"))
         best = min(((sp, m) for sp, m in spans if sp <= lo * (1.0 + tol)),
                    key=lambda x: (-bin(x[1]).count("1"), x[0]))
         self.assignment = {names[i]: ("gpu" if best[1] >> i & 1 else "cpu") for i in range(n)}

@@ -249,6 +249,8 @@ struct SmView {
   SV_VAL(n_pend);
   SV_REF(il1);
   SV_REF(imshr);
+  SV_REF(cl1);
+  SV_REF(cmshr);
   SV_WARP(w_iline);
   SV_VAL(idoc_mask);
   SV_VAL(oc_mask);
@@ -328,7 +330,7 @@ struct SmView {
         used_shmem(b.used_shmem),
         idoc_inst(b.idoc_inst), oc_inst(b.oc_inst),
         wb_cnt(b.wb_cnt), wb(b.wb), ldst_acc(b.ldst_acc), hit_cnt(b.hit_cnt), hit(b.hit), l1(b.l1), mshr(b.mshr),
-        pend(b.pend), il1(b.il1), imshr(b.imshr),
+        pend(b.pend), il1(b.il1), imshr(b.imshr), cl1(b.cl1), cmshr(b.cmshr),
         outq(b.outq), ocnt(b.ocnt), inq(b.inq), rsp_cl(b.rsp_cl), rsp_ld(b.rsp_ld), skey(b.skey), sref(b.sref), srank(b.srank) {
 #define SV_LD(m) m = sv_uni(b.m);
     SV_SCALARS(SV_LD)

@@ -26,6 +26,8 @@ constexpr int kMaxL1Lines = 1024;   // 128 KB of 128 B lines
 constexpr int kMaxL1Mshr = 256;
 constexpr int kMaxIL1Lines = 512;  // instruction cache: 64 KB of 128 B lines
 constexpr int kMaxIL1Mshr = 16;
+constexpr int kMaxCL1Lines = 1024; // constant / scalar data cache: 64 KB of 64 B lines
+constexpr int kMaxCL1Mshr = 32;
 constexpr uint64_t kProgramMemStart = 0xF0000000ull;  // code address base (reference PROGRAM_MEM_START)
 constexpr uint64_t kScalarBase = 0x7FFE00000000ull;   // data addresses keyed to CDNA scalar loads (coalesce_kernel)
 constexpr int kMaxPend = 1024;      // outstanding (warp,load-slot,line) L1 waiters
@@ -176,6 +178,12 @@ struct SimCfg {
   uint32_t inst_prefetch;   // L1I sequential prefetch depth in lines (CDNA SQC fetches ahead)
   uint32_t ifetch_block;    // > 0: a warp probes the L1I only when its fetch enters a new block of this many bytes
   uint32_t ifetch_pad_;
+  // ---- constant cache (reference m_L1C read_only_cache, ldst_unit::
+  //      constant_cycle, shader.cc:2196-2225, fills shader.cc:2819-2823); on
+  //      CDNA the scalar data cache of the SQC that s_load reads through ----
+  CacheGeom cl1;
+  uint32_t cl1_latency;     // hit latency (core cycles); -sim_const_cache_latency, 0 = the L1D's
+  uint32_t cl1_flush;       // invalidate it with the L1D at a kernel's start (the CDNA dispatch's acquire)
   // ---- interconnect ----
   uint32_t icnt_latency;   // core cycles (== epoch length, the PDES lookahead)
   uint32_t flit_size;

@@ -132,6 +132,7 @@ struct SMStats {
   uint64_t mf_lat_hist[16];    // log2 buckets: [2^i, 2^(i+1)) cycles
   uint64_t il1[4];             // instruction cache: hit, miss, mshr (pending) hit, reservation fail
   uint64_t il1_prefetch;       // code lines requested by the sequential prefetcher
+  uint64_t cl1[4];             // constant / scalar data cache: hit, miss, mshr (pending) hit, reservation fail
   uint64_t dual_issued;        // second instructions issued in the same cycle by one warp
   uint64_t l1_wb;              // dirty L1 lines written back on eviction
   uint64_t l1_wb_lost;         // write-backs dropped with the injection queue full (must stay 0)
@@ -257,6 +258,8 @@ struct alignas(16) SMState {
   uint32_t n_pend;
   L1Line il1[kMaxIL1Lines];     // instruction cache tags (non-sectored: valid = 0xf)
   L1Mshr imshr[kMaxIL1Mshr];
+  L1Line cl1[kMaxCL1Lines];     // constant / scalar data cache tags (valid = 1: non-sectored)
+  L1Mshr cmshr[kMaxCL1Mshr];
   uint64_t w_iline[kMaxWarps];  // code line a WF_IMISS warp waits for
   uint64_t idoc_mask;     // bit sched*U_COUNT+unit: ID_OC register occupied
   uint32_t oc_mask;       // occupied operand collectors

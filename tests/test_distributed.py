@@ -164,8 +164,8 @@ def test_node_plan_places_apps_by_makespan(native, tmp_path, monkeypatch):
 
 
 def test_node_plan_prefers_gpu_among_equal_makespans(native, tmp_path, monkeypatch):
-    """Plans within 2 % of the shortest makespan: the one with the most
-    applications on the GPU engine wins."""
+    """Plans with the shortest makespan (ASIM_NODE_GPU_TOLERANCE, default 0:
+    exact ties): the one with the most applications on the GPU engine wins."""
     from accel_sim_framework_distributed_amd.parallel.multi_gpu import DistributedSuite
     from accel_sim_framework_distributed_amd.tracegen import rodinia
     apps = ["nn-rodinia-2.0-ft", "pathfinder-rodinia-2.0-ft", "backprop-rodinia-2.0-ft"]
