@@ -1109,6 +1109,62 @@ void Simulator::write_visualizer_sample(const std::string& kname, uint64_t now, 
     << " l2_access=" << l2_acc << " l2_miss=" << l2_miss << " dram_rd=" << drd << " dram_wr=" << dwr
     << " dram_util=" << (dcyc ? (double)busy / (double)dcyc : 0.0) << " sm_insn=";
   for (size_t i = 0; i < dsm.size(); ++i) o << (i ? "," : "") << dsm[i].warp_insn;
+  // per-unit vectors (reference: per-shader L1 miss rates, visualizer.cc:84-110;
+  // per-DRAM-channel dramutil / drameff / dramnreq, dram.cc:815-853; per
+  // sub-partition L2 hits and misses, l2cache.cc:866)
+  auto vec = [&](const char* key, size_t n, auto f) {
+    o << " " << key << "=";
+    for (size_t i = 0; i < n; ++i) o << (i ? "," : "") << f(i);
+  };
+  auto l1_miss_rate = [&](size_t i) {
+    uint64_t a = 0, m = 0;
+    for (int t = 0; t < L1T_COUNT; ++t) {
+      for (int oo = 0; oo < L1O_COUNT; ++oo) a += dsm[i].l1[t][oo];
+      m += dsm[i].l1[t][L1O_MISS];
+    }
+    return a ? (double)m / (double)a : 0.0;
+  };
+  vec("sm_l1_miss_rate", dsm.size(), l1_miss_rate);
+  vec("sm_occupancy", dsm.size(), [&](size_t i) { return (double)dsm[i].occupancy_acc / (double)cycles; });
+  vec("sm_active", dsm.size(), [&](size_t i) { return (double)dsm[i].active_cycles / (double)cycles; });
+  vec("sm_pkts_out", dsm.size(), [&](size_t i) { return dsm[i].pkts_out; });
+  // global issue distribution: idle, scoreboard, stall, then issued with k
+  // active lanes (the warp-divergence breakdown AerialVision stacks)
+  vec("issue_distro", 3 + (size_t)kMaxWarpLanes, [&](size_t k) {
+    uint64_t v = 0;
+    for (auto& s : dsm) v += s.issue_distro[k];
+    return v;
+  });
+  vec("mf_lat_hist", 16, [&](size_t k) {
+    uint64_t v = 0;
+    for (auto& s : dsm) v += s.mf_lat_hist[k];
+    return v;
+  });
+  {
+    uint64_t n = 0, sum = 0;
+    for (auto& s : dsm) {
+      n += s.mf_lat_n;
+      sum += s.mf_lat_sum;
+    }
+    o << " mf_lat_avg=" << (n ? (double)sum / (double)n : 0.0);
+  }
+  vec("ch_dram_util", dm.size(),
+      [&](size_t i) { return dm[i].dram_cycles ? (double)dm[i].dram_busy_cycles / (double)dm[i].dram_cycles : 0.0; });
+  // mean requests queued at the channel (reference dramavemrqs)
+  vec("ch_dram_queue", dm.size(),
+      [&](size_t i) { return dm[i].dram_cycles ? (double)dm[i].dram_q_occ / (double)dm[i].dram_cycles : 0.0; });
+  vec("ch_dram_req", dm.size(), [&](size_t i) { return dm[i].dram_rd + dm[i].dram_wr; });
+  vec("ch_dram_act", dm.size(), [&](size_t i) { return dm[i].dram_act; });
+  vec("ch_l2_hit", dm.size(), [&](size_t i) {
+    uint64_t v = 0;
+    for (int t = 0; t < L2T_COUNT; ++t) v += dm[i].l2[t][L2O_HIT];
+    return v;
+  });
+  vec("ch_l2_miss", dm.size(), [&](size_t i) {
+    uint64_t v = 0;
+    for (int t = 0; t < L2T_COUNT; ++t) v += dm[i].l2[t][L2O_MISS];
+    return v;
+  });
   o << "\n";
 }
 

@@ -84,6 +84,25 @@ def test_memlatency_and_visualizer(native, traces, tmp_path, monkeypatch):
     rows = visualizer.parse(str(tmp_path / "gpgpusim_visualizer.log"))
     assert len(rows) == len(log) and len(rows[-1]["sm_insn"]) == 80
     assert "<svg" in visualizer.render(rows)
+    # per-unit vectors (AerialVision's per-shader / per-channel views)
+    for r in rows:
+        assert len(r["sm_l1_miss_rate"]) == 80 and all(0 <= v <= 1 for v in r["sm_l1_miss_rate"])
+        assert len(r["ch_dram_util"]) == len(r["ch_l2_hit"]) == len(r["ch_dram_queue"]) > 0
+        assert len(r["issue_distro"]) == 3 + 64 and len(r["mf_lat_hist"]) == 16
+        # every scheduler cycle lands in exactly one issue bin
+        assert sum(visualizer.issue_groups(r["issue_distro"]).values()) == sum(r["issue_distro"])
+    # the issued bins count warp instructions (single issue: one per issued cycle)
+    issued = sum(sum(r["issue_distro"][3:]) for r in rows)
+    assert issued == sum(sum(r["sm_insn"]) for r in rows)
+    assert sum(sum(r["mf_lat_hist"]) for r in rows) > 0
+    # two-run page, CSV export
+    page = visualizer.render(rows, [("again", rows)])
+    assert "asim-data" in page and "drawHeat" in page and page.count('"name"') == 2
+    csv = visualizer.to_csv(rows, "sm_insn").splitlines()
+    assert len(csv) == len(rows) and len(csv[0].split(",")) == 81
+    out = tmp_path / "v.html"
+    assert visualizer.main([str(tmp_path / "gpgpusim_visualizer.log"), "-o", str(out)]) == 0
+    assert out.stat().st_size > 1000
 
 
 def test_pipeline_dump(native, traces):
