@@ -59,12 +59,19 @@ def default_params(preset: str) -> Dict[str, float]:
         cats = dict(cat1=(120.0, 3.0), cat2=(150.0, 3.5), cat3=(170.0, 4.0), cat4=(155.0, 3.5), cat5=(130.0, 3.0),
                     cat6=(380.0, 0.0), light=(20.0, 0.05))
         p.update(static_shared_flane=90.0, static_l1_flane=100.0, static_l2_flane=60.0)
+        # architectural energy model inputs (energy_model = 1, csrc/power/arch_energy.cc):
+        # N3-class compute dies, HBM3E, MFMA 16x16x32 = 128 MACs per lane
+        p.update(core_tech_node=3.0, dram_pj_per_bit=2.5, tensor_macs_per_lane=128.0)
     else:
         # 250 W class Volta/Turing/Ampere boards, 80-ish SMs
         p.update(constant_power=32.0, idle_core_power=0.28)
         cats = dict(cat1=(15.0, 0.6), cat2=(18.5, 0.65), cat3=(19.0, 0.7), cat4=(18.5, 0.6), cat5=(14.5, 0.5),
                     cat6=(49.0, 0.0), light=(2.0, 0.004))
         p.update(static_shared_flane=31.0, static_l1_flane=35.0, static_l2_flane=17.0)
+        p.update(core_tech_node=12.0, dram_pj_per_bit=3.9)
+    # 0: the fixed per-access energy table (power.cc); 1: energies derived
+    # from the simulated machine's geometry (McPAT / CACTI role)
+    p["energy_model"] = 0.0
     for c, (f, a) in cats.items():
         p[f"static_{c}_flane"] = f
         p[f"static_{c}_addlane"] = a

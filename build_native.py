@@ -33,6 +33,7 @@ CORE_SRC = [
     "csrc/engine/cpu_engine.cc",
     "csrc/engine/check_engine.cc",
     "csrc/power/power.cc",
+    "csrc/power/arch_energy.cc",
     "csrc/driver/simulator.cc",
     "csrc/driver/dump.cc",
     "csrc/driver/debugger.cc",

@@ -212,6 +212,42 @@ PYBIND11_MODULE(_asim, m) {
                           c.icnt_mode == 1 ? icnt_routers(c, node, c.n_clusters + sub) : 1u);
   }, "interconnect latency model (-network_mode 1 topology or local crossbar)");
   m.def("parse_booksim_config", [](const std::string& text) { return parse_booksim_config(text); });
+  m.def(
+      "arch_energy",
+      [](const std::vector<std::string>& args, double node_nm, double vdd, double dram_pj_per_bit,
+         double tensor_macs_per_lane) {
+        SimCfg c = cfg_from_args(args);
+        ArchEnergyParams p;
+        p.node_nm = node_nm;
+        p.vdd = vdd;
+        p.dram_pj_per_bit = dram_pj_per_bit;
+        p.tensor_macs_per_lane = tensor_macs_per_lane;
+        const ArchEnergy e = arch_energy(c, p);
+        py::dict d, base, arrays;
+        for (int i = 0; i < PA_COUNT; ++i) base[kPwrActName[i]] = e.base_nj[i];
+        for (const auto& a : e.arrays) {
+          py::dict x;
+          x["read_nj"] = a.e_read_nj;
+          x["write_nj"] = a.e_write_nj;
+          x["tag_nj"] = a.e_tag_nj;
+          x["leak_w"] = a.leak_w;
+          x["area_mm2"] = a.area_mm2;
+          x["org"] = py::make_tuple(a.ndwl, a.ndbl, a.nspd, a.sub_rows, a.sub_cols);
+          arrays[py::str(a.name)] = x;
+        }
+        d["base_nj"] = base;
+        d["arrays"] = arrays;
+        d["die_mm2"] = e.die_mm2;
+        d["sm_area_mm2"] = e.sm_area_mm2;
+        d["leak_sm_w"] = e.leak_sm_w;
+        d["leak_l2_w"] = e.leak_l2_w;
+        d["vdd"] = e.tech.vdd;
+        d["report"] = arch_energy_report(e);
+        return d;
+      },
+      py::arg("args"), py::arg("node_nm") = 12.0, py::arg("vdd") = 0.0, py::arg("dram_pj_per_bit") = 3.9,
+      py::arg("tensor_macs_per_lane") = 0.0,
+      "per-access energies from the machine's geometry and a technology node (McPAT / CACTI role)");
   m.def("ipoly_hash", &ipoly_hash);
   m.def("cache_set_index", [](const std::string& geom, uint64_t addr) {
     return cache_set_index(parse_cache_geom(geom), addr);

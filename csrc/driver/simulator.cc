@@ -88,6 +88,18 @@ Simulator::Simulator(const std::vector<std::string>& args) {
                       std::max(power_->param("dvfs_min_clock_ratio", 0.0), dopt_.dvfs_min_clock_ratio));
     power_report_.reset(new std::ofstream(dopt_.power_report_file));
     if (!*power_report_) throw std::runtime_error("cannot write " + dopt_.power_report_file);
+    if (power_->param("energy_model", 0.0) >= 1.0) {
+      // per-access energies from this machine's geometry (McPAT / CACTI role)
+      ArchEnergyParams ap;
+      ap.node_nm = power_->param("core_tech_node", ap.node_nm);
+      ap.vdd = power_->param("core_vdd", 0.0);
+      ap.dram_pj_per_bit = power_->param("dram_pj_per_bit", ap.dram_pj_per_bit);
+      ap.dram_act_nj = power_->param("dram_act_nj", ap.dram_act_nj);
+      ap.tensor_macs_per_lane = power_->param("tensor_macs_per_lane", 0.0);
+      const ArchEnergy ae = arch_energy(cfg_, ap);
+      power_->set_base(ae.base_nj);
+      *power_report_ << "architectural energy model (energy_model = 1)\n" << arch_energy_report(ae) << "\n";
+    }
     if (dopt_.power_trace) {
       power_trace_.reset(new std::ofstream("accelwattch_power_trace.csv"));
       ptrack_.write_trace_header(*power_trace_);

@@ -16,6 +16,7 @@
 #include "../config/sim_options.h"
 #include "../engine/engine.h"
 #include "../parallel/linksim.h"
+#include "../power/arch_energy.h"
 #include "../power/power.h"
 
 namespace asim {

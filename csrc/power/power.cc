@@ -93,7 +93,7 @@ double PowerModel::param(const std::string& k, double dflt) const {
 std::vector<double> PowerModel::coefficients(double core_mhz) const {
   // W contributed by one access per core cycle
   std::vector<double> c(PA_COUNT);
-  for (int i = 0; i < PA_COUNT; ++i) c[i] = base_nj(i) * 1e-9 * param(kPwrActName[i], 1.0) * core_mhz * 1e6;
+  for (int i = 0; i < PA_COUNT; ++i) c[i] = base(i) * 1e-9 * param(kPwrActName[i], 1.0) * core_mhz * 1e6;
   return c;
 }
 

@@ -96,6 +96,15 @@ class PowerModel {
   // come from the simulator) merge; instruction-side activity is always simulated
   static Activity merge_hw(const Activity& sim, const Activity& hw, const bool use_sim[HW_COUNT]);
   static double base_nj(int act);
+  // per-access energies in use: the fixed table, or the architectural model's
+  // (arch_energy.h, XML <param name="energy_model" value="1"/>)
+  double base(int act) const { return (act >= 0 && act < PA_COUNT) ? base_[act] : 0.0; }
+  void set_base(const double* e) {
+    for (int i = 0; i < PA_COUNT; ++i) base_[i] = e[i];
+  }
+  PowerModel() {
+    for (int i = 0; i < PA_COUNT; ++i) base_[i] = base_nj(i);
+  }
   // coefficient vector (W per access per cycle at core_mhz)
   std::vector<double> coefficients(double core_mhz) const;
   // the sampler's coefficients at the nominal clock (engines' in-loop
@@ -106,6 +115,7 @@ class PowerModel {
 
  private:
   std::map<std::string, double> p_;
+  double base_[PA_COUNT];
 };
 
 // Per-kernel and cumulative avg / max / min of every component over the
