@@ -213,6 +213,21 @@ PYBIND11_MODULE(_asim, m) {
   }, "interconnect latency model (-network_mode 1 topology or local crossbar)");
   m.def("parse_booksim_config", [](const std::string& text) { return parse_booksim_config(text); });
   m.def(
+      "icnt_path",
+      [](const std::vector<std::string>& args, uint32_t a, uint32_t b) {
+        // (links of the route from node a to node b, the topology's link count)
+        SimCfg c = cfg_from_args(args);
+        uint32_t L[kMaxPathLinks];
+        const uint64_t n = icnt_link_count(c);
+        std::vector<uint32_t> v;
+        if (n) {
+          const uint32_t m = icnt_path(c, a, b, L);
+          v.assign(L, L + m);
+        }
+        return py::make_tuple(v, n);
+      },
+      "link-contention route model (icnt_links.h): interconnect nodes are clusters, then sub-partitions");
+  m.def(
       "arch_energy",
       [](const std::vector<std::string>& args, double node_nm, double vdd, double dram_pj_per_bit,
          double tensor_macs_per_lane) {

@@ -173,6 +173,7 @@ const OptDef kOptions[] = {
     {"-icnt_arbiter_algo", 'u', "1", ""},
     {"-icnt_verbose", 'u', "0", ""},
     {"-icnt_grant_cycles", 'u', "1", ""},
+    {"-icnt_link_contention", 'u', "0", "network_mode 1: shared links of multi-hop routes delay packets (link reservation per epoch)"},
     {"-icnt_flit_size", 'u', "32", "flit size in bytes"},
     // ---- clocks / kernel ----
     {"-gpgpu_clock_domains", 's', "500.0:2000.0:2000.0:2000.0", "core:icnt:L2:DRAM MHz"},
@@ -1019,6 +1020,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.icnt_mode = 2;
   if (r.geti("-network_mode") == 1) {
     apply_intersim_config(c, resolve_cfg_path(r, r.gets("-inter_config_file")));
+    c.link_contention = r.getu("-icnt_link_contention") ? 1 : 0;
   } else if (r.geti("-network_mode") != 2) {
     throw OptionError("-network_mode must be 1 (intersim topology) or 2 (local crossbar)");
   }

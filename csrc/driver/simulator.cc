@@ -1389,6 +1389,13 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
     print("Reply_Network_conflicts = %llu\n", (unsigned long long)rp_cf);
     print("Reply_Network_queueing_cycles = %llu\n", (unsigned long long)rp_q);
     print("Reply_Network_avg_queueing_cycles = %.4f\n", rp_pk ? (double)rp_q / (double)rp_pk : 0.0);
+    if (icnt_contention_on(cfg_)) {
+      // cumulative over the run: packets a busy link delayed, and the delay
+      uint64_t dl = 0, wc = 0;
+      eng_->link_stats(&dl, &wc);
+      print("Network_link_delayed_packets = %llu\n", (unsigned long long)dl);
+      print("Network_link_wait_cycles = %llu\n", (unsigned long long)wc);
+    }
   }
   {
     // further gpu_print_stat / shader_core_stats lines (reference

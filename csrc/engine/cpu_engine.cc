@@ -75,7 +75,7 @@ void check_state_header(const EngineStateHeader& h, const EngineStateHeader& w) 
   if (h.magic != w.magic || h.version != w.version) throw std::runtime_error("engine state: not a state image");
   if (h.n_sm != w.n_sm || h.n_mem != w.n_mem || h.sm_bytes != w.sm_bytes || h.ch_bytes != w.ch_bytes ||
       h.pub_bytes != w.pub_bytes || h.box_req != w.box_req || h.cnt_req != w.cnt_req || h.box_rep != w.box_rep ||
-      h.cnt_rep != w.cnt_rep || h.ovf != w.ovf || h.mall != w.mall)
+      h.cnt_rep != w.cnt_rep || h.ovf != w.ovf || h.mall != w.mall || h.links != w.links)
     throw std::runtime_error("engine state: image was written for a different configuration or build");
 }
 
@@ -151,6 +151,15 @@ class CpuEngine : public Engine {
     ovf_cap_ = backlog_cap(c);
     ovf_.assign((size_t)c.n_subpart * ovf_cap_, Pkt{});
     mall_.assign((size_t)(c.n_mem * mall_lines(c)), L2Line{});
+    link_free_.clear();
+    link_refs_.clear();
+    link_stat_[0] = link_stat_[1] = 0;
+    if (c.link_contention && icnt_link_count(c) > kMaxIcntLinks)
+      throw std::runtime_error("-icnt_link_contention: topology has too many links");
+    if (icnt_contention_on(c)) {
+      link_free_.assign((size_t)icnt_link_count(c), 0);
+      link_refs_.assign((size_t)c.n_sm * c.n_subpart * std::max(cap_req_, cap_rep_), 0);
+    }
     epoch_ = 0;
     cycle_ = 0;
     kt_ = KernelTab{};
@@ -241,6 +250,14 @@ class CpuEngine : public Engine {
           }
         }
         if (nthr > 1) bar_.wait();
+        if (!link_free_.empty()) {
+          // shared links of multi-hop routes: this epoch's packets reserve
+          // their routes before any destination reads them (icnt_links.h)
+          if (tid == 0)
+            icnt_contend<SeqPar>(c, box_req_[cur].data(), cnt_req_[cur].data(), cap_req_, box_rep_[cur].data(),
+                                 cnt_rep_[cur].data(), cap_rep_, link_free_.data(), link_refs_.data(), link_stat_);
+          if (nthr > 1) bar_.wait();
+        }
         const uint64_t mc = pw_on_ ? (lim.max_cycle ? std::min(lim.max_cycle, pw_next) : pw_next) : lim.max_cycle;
         const EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, kt_, epoch, mc);
         refill = d.refill != 0;
@@ -367,7 +384,8 @@ class CpuEngine : public Engine {
   }
 
   void snapshot(std::vector<uint8_t>& out) override {
-    out.resize(sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState) + mall_.size() * sizeof(L2Line));
+    out.resize(sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState) + mall_.size() * sizeof(L2Line) +
+               link_free_.size() * 8);
     uint8_t* p = out.data();
     for (auto& s : sms_) {
       memcpy(p, &s, sizeof(SMState));
@@ -378,9 +396,12 @@ class CpuEngine : public Engine {
       p += sizeof(ChanState);
     }
     if (!mall_.empty()) memcpy(p, mall_.data(), mall_.size() * sizeof(L2Line));
+    p += mall_.size() * sizeof(L2Line);
+    if (!link_free_.empty()) memcpy(p, link_free_.data(), link_free_.size() * 8);
   }
   void restore(const std::vector<uint8_t>& in) override {
-    if (in.size() != sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState) + mall_.size() * sizeof(L2Line))
+    if (in.size() != sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState) + mall_.size() * sizeof(L2Line) +
+                         link_free_.size() * 8)
       throw std::runtime_error("snapshot size mismatch");
     const uint8_t* p = in.data();
     for (auto& s : sms_) {
@@ -392,6 +413,12 @@ class CpuEngine : public Engine {
       p += sizeof(ChanState);
     }
     if (!mall_.empty()) memcpy(mall_.data(), p, mall_.size() * sizeof(L2Line));
+    p += mall_.size() * sizeof(L2Line);
+    if (!link_free_.empty()) memcpy(link_free_.data(), p, link_free_.size() * 8);
+  }
+  void link_stats(uint64_t* delayed, uint64_t* wait_cycles) override {
+    *delayed = link_stat_[0];
+    *wait_cycles = link_stat_[1];
   }
   void advance(uint64_t cycles) override {
     uint64_t E = c_.icnt_latency;
@@ -411,6 +438,7 @@ class CpuEngine : public Engine {
     h.cnt_rep = cnt_rep_[0].size();
     h.ovf = ovf_.size();
     h.mall = mall_.size();
+    h.links = link_free_.empty() ? 0 : link_free_.size() + 2;
     h.cycle = cycle_;
     h.epoch = epoch_;
     h.ready = kt_.active;
@@ -433,6 +461,10 @@ class CpuEngine : public Engine {
     }
     o.put(ovf_.data(), ovf_.size() * sizeof(Pkt));
     o.put(mall_.data(), mall_.size() * sizeof(L2Line));
+    if (!link_free_.empty()) {
+      o.put(link_free_.data(), link_free_.size() * 8);
+      o.put(link_stat_, sizeof(link_stat_));
+    }
   }
 
   void load_state(const std::vector<uint8_t>& in) override {
@@ -451,6 +483,10 @@ class CpuEngine : public Engine {
     }
     r.get(ovf_.data(), ovf_.size() * sizeof(Pkt));
     r.get(mall_.data(), mall_.size() * sizeof(L2Line));
+    if (!link_free_.empty()) {
+      r.get(link_free_.data(), link_free_.size() * 8);
+      r.get(link_stat_, sizeof(link_stat_));
+    }
     cycle_ = h.cycle;
     epoch_ = h.epoch;
     if (h.ready) throw std::runtime_error("engine state: image taken with kernels running");
@@ -491,6 +527,9 @@ class CpuEngine : public Engine {
   std::vector<Pkt> ovf_;  // arrival backlog rings [n_subpart][ovf_cap_]
   std::vector<L2Line> mall_;  // MALL lines [n_mem][mall_sets * mall_assoc]
   uint32_t ovf_cap_ = 0;
+  std::vector<uint64_t> link_free_;  // -icnt_link_contention: per directed link, the fs it frees
+  std::vector<uint32_t> link_refs_;  // the pass's packet list
+  uint64_t link_stat_[2] = {0, 0};   // delayed packets, delay (interconnect cycles)
   uint64_t epoch_ = 0, cycle_ = 0;
   KernelTab kt_{};
 };

@@ -93,6 +93,12 @@ class Engine {
   }
   // device kernel launches so far (GPU engine; host engines report 0)
   virtual uint64_t launches() const { return 0; }
+  // -icnt_link_contention: packets delayed by busy links, and their total
+  // delay in interconnect cycles (icnt_links.h)
+  virtual void link_stats(uint64_t* delayed, uint64_t* wait_cycles) {
+    *delayed = 0;
+    *wait_cycles = 0;
+  }
   // in-loop power sampling (PwrArm); engines without it return false
   virtual bool power_sampler() const { return false; }
   virtual void power_arm(const PwrArm&) { throw std::runtime_error("engine has no in-loop power sampler"); }
@@ -143,11 +149,12 @@ inline uint32_t backlog_cap(const SimCfg& c) {
 
 struct EngineStateHeader {
   uint64_t magic = 0x41534d5354415445ull;  // "ASMSTATE"
-  uint64_t version = 5;  // 4: kernel slots (concurrent kernels); 5: MALL lines
+  uint64_t version = 6;  // 4: kernel slots (concurrent kernels); 5: MALL lines; 6: link reservations
   uint64_t n_sm = 0, n_mem = 0, sm_bytes = 0, ch_bytes = 0, pub_bytes = 0;
   uint64_t box_req = 0, cnt_req = 0, box_rep = 0, cnt_rep = 0;  // element counts per parity
   uint64_t ovf = 0;                                              // arrival backlog packets (all sub-partitions)
   uint64_t mall = 0;                                             // MALL lines (all channels), after the backlog
+  uint64_t links = 0;  // -icnt_link_contention: link free times, then the two statistics words, after the MALL
   uint64_t cycle = 0, epoch = 0, ready = 0;
 };
 

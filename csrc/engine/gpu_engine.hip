@@ -89,6 +89,8 @@ struct GpuArgs {
   Pkt* ovf;
   uint32_t ovf_cap;
   L2Line* mall;  // [n_mem][mall_sets * mall_assoc] or nullptr
+  uint64_t* link_free;  // -icnt_link_contention: [links] free times, then 2 statistics words; or nullptr
+  uint32_t* link_refs;  // the pass's packet list
   uint64_t epoch0;
   uint64_t cycle0;
   uint64_t max_cycle;
@@ -357,6 +359,15 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     }
     uint32_t was_last = 0;
     if (!grid_barrier(a.ctl, a.nblocks, nbar++, &was_last)) break;
+    if (a.link_free) {
+      // shared links of multi-hop routes: block 0 walks this epoch's packets
+      // in the fixed order (icnt_links.h), then every block waits for it
+      // before a destination reads them
+      if (b == 0)
+        icnt_contend<P>(c, a.box_req[cur], a.cnt_req[cur], a.cap_req, a.box_rep[cur], a.cnt_rep[cur], a.cap_rep,
+                        a.link_free, a.link_refs, a.link_free + icnt_link_count(c));
+      if (!grid_barrier(a.ctl, a.nblocks, nbar++)) break;
+    }
     P::prof(27);  // decision
     if (a.ework) {
       const uint64_t t_exit = __builtin_amdgcn_s_memtime();
@@ -662,6 +673,15 @@ class GpuEngine : public Engine {
       HIPCHECK(hipMalloc(&d_mall_, sizeof(L2Line) * n_mall_));
       HIPCHECK(hipMemset(d_mall_, 0, sizeof(L2Line) * n_mall_));
     }
+    if (c.link_contention && icnt_link_count(c) > kMaxIcntLinks)
+      throw std::runtime_error("-icnt_link_contention: topology has too many links");
+    n_links_ = icnt_contention_on(c) ? (size_t)icnt_link_count(c) : 0;
+    if (n_links_) {
+      HIPCHECK(hipMalloc(&d_links_, sizeof(uint64_t) * (n_links_ + 2)));
+      HIPCHECK(hipMemset(d_links_, 0, sizeof(uint64_t) * (n_links_ + 2)));
+      const size_t nrefs = (size_t)c.n_sm * c.n_subpart * std::max(cap_req_, cap_rep_);
+      HIPCHECK(hipMalloc(&d_link_refs_, sizeof(uint32_t) * nrefs));
+    }
     HIPCHECK(hipMalloc(&d_ctl_, sizeof(GpuCtl)));
     HIPCHECK(hipHostMalloc(&h_ctl_, sizeof(GpuCtl)));
     HIPCHECK(hipMalloc(&d_kt_, sizeof(KernelTab)));
@@ -710,6 +730,8 @@ class GpuEngine : public Engine {
       a.ovf = d_ovf_;
       a.ovf_cap = ovf_cap_;
       a.mall = d_mall_;
+      a.link_free = d_links_;
+      a.link_refs = d_link_refs_;
       a.epoch0 = epoch_;
       a.cycle0 = cycle_;
       a.max_cycle = lim.max_cycle;
@@ -805,19 +827,29 @@ class GpuEngine : public Engine {
 
   void snapshot(std::vector<uint8_t>& out) override {
     const size_t units = sizeof(SMState) * c_.n_sm + sizeof(ChanState) * c_.n_mem;
-    out.resize(units + sizeof(L2Line) * n_mall_);
+    out.resize(units + sizeof(L2Line) * n_mall_ + 8 * n_links_);
     HIPCHECK(hipMemcpy(out.data(), d_sms_, sizeof(SMState) * c_.n_sm, hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(out.data() + sizeof(SMState) * c_.n_sm, d_chs_, sizeof(ChanState) * c_.n_mem,
                        hipMemcpyDeviceToHost));
     if (n_mall_) HIPCHECK(hipMemcpy(out.data() + units, d_mall_, sizeof(L2Line) * n_mall_, hipMemcpyDeviceToHost));
+    if (n_links_)
+      HIPCHECK(hipMemcpy(out.data() + units + sizeof(L2Line) * n_mall_, d_links_, 8 * n_links_, hipMemcpyDeviceToHost));
   }
   void restore(const std::vector<uint8_t>& in) override {
     const size_t units = sizeof(SMState) * c_.n_sm + sizeof(ChanState) * c_.n_mem;
-    if (in.size() != units + sizeof(L2Line) * n_mall_) throw std::runtime_error("snapshot size mismatch");
+    if (in.size() != units + sizeof(L2Line) * n_mall_ + 8 * n_links_) throw std::runtime_error("snapshot size mismatch");
     HIPCHECK(hipMemcpy(d_sms_, in.data(), sizeof(SMState) * c_.n_sm, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(d_chs_, in.data() + sizeof(SMState) * c_.n_sm, sizeof(ChanState) * c_.n_mem,
                        hipMemcpyHostToDevice));
     if (n_mall_) HIPCHECK(hipMemcpy(d_mall_, in.data() + units, sizeof(L2Line) * n_mall_, hipMemcpyHostToDevice));
+    if (n_links_)
+      HIPCHECK(hipMemcpy(d_links_, in.data() + units + sizeof(L2Line) * n_mall_, 8 * n_links_, hipMemcpyHostToDevice));
+  }
+  void link_stats(uint64_t* delayed, uint64_t* wait_cycles) override {
+    uint64_t st[2] = {0, 0};
+    if (n_links_) HIPCHECK(hipMemcpy(st, d_links_ + n_links_, sizeof(st), hipMemcpyDeviceToHost));
+    *delayed = st[0];
+    *wait_cycles = st[1];
   }
   void advance(uint64_t cycles) override {
     uint64_t E = c_.icnt_latency;
@@ -857,6 +889,7 @@ class GpuEngine : public Engine {
     h.cnt_rep = (uint64_t)c_.n_sm * c_.n_subpart;
     h.ovf = (uint64_t)c_.n_subpart * ovf_cap_;
     h.mall = n_mall_;
+    h.links = n_links_ ? n_links_ + 2 : 0;
     h.cycle = cycle_;
     h.epoch = epoch_;
     h.ready = kt_.active;
@@ -882,6 +915,7 @@ class GpuEngine : public Engine {
     }
     dl(d_ovf_, h.ovf * sizeof(Pkt));
     dl(d_mall_, h.mall * sizeof(L2Line));
+    dl(d_links_, h.links * sizeof(uint64_t));  // free times + the two statistics words (CPU engine layout)
   }
   void load_state(const std::vector<uint8_t>& in) override {
     StateIn r{in};
@@ -903,6 +937,7 @@ class GpuEngine : public Engine {
     }
     ul(d_ovf_, w.ovf * sizeof(Pkt));
     ul(d_mall_, w.mall * sizeof(L2Line));
+    ul(d_links_, w.links * sizeof(uint64_t));
     cycle_ = h.cycle;
     epoch_ = h.epoch;
     if (h.ready) throw std::runtime_error("engine state: image taken with kernels running");
@@ -1013,6 +1048,9 @@ class GpuEngine : public Engine {
     fr(d_ctl_);
     fr(d_ovf_);
     fr(d_mall_);
+    fr(d_links_);
+    fr(d_link_refs_);
+    n_links_ = 0;
     fr(d_trace_ev_);
     fr(d_trace_cnt_);
     tw_.release();
@@ -1037,6 +1075,9 @@ class GpuEngine : public Engine {
   Pkt* d_ovf_ = nullptr;  // arrival backlog rings [n_subpart][ovf_cap_]
   L2Line* d_mall_ = nullptr;  // MALL lines [n_mem][mall_sets * mall_assoc]
   size_t n_mall_ = 0;
+  uint64_t* d_links_ = nullptr;     // -icnt_link_contention: link free times + 2 statistics words
+  uint32_t* d_link_refs_ = nullptr;
+  size_t n_links_ = 0;
   uint32_t ovf_cap_ = 0;
   Pkt* d_box_req_[2] = {nullptr, nullptr};
   uint32_t* d_cnt_req_[2] = {nullptr, nullptr};

@@ -210,7 +210,7 @@ struct SimCfg {
   uint16_t topo_conc;       // nodes per router (cmesh concentration)
   uint16_t hop_icnt;        // icnt cycles per router traversal (routing + VA + SA + ST)
   uint16_t chan_icnt;       // icnt cycles per channel
-  uint16_t pad_icnt;
+  uint16_t link_contention;  // -icnt_link_contention: shared links of multi-hop routes delay packets (icnt_links.h)
   // ---- memory partition ----
   CacheGeom l2;
   uint32_t rop_latency;

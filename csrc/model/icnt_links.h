@@ -1,0 +1,211 @@
+// Link-level contention inside multi-hop interconnect topologies
+// (-network_mode 1 with -icnt_link_contention 1).
+//
+// The reference's intersim2 simulates every router of a Booksim network
+// cycle by cycle (intersim2/routers/iq_router.cpp, networks/kncube.cpp,
+// fly.cpp, fattree.cpp, flatfly_onchip.cpp): packets that share a link wait
+// for it.  The epoch engine prices a packet's route at injection (config.h
+// icnt_pkt_lat_fs); this pass adds what the shared links cost.  At every
+// epoch boundary the packets injected during the epoch (both directions) are
+// walked in a fixed order -- requests then replies, by destination, source
+// and injection order -- and each reserves, hop by hop, the directed links of
+// its deterministic route (dimension order on meshes / tori, destination-tag
+// on butterflies, d-mod-k on fat trees, one hop per differing dimension on
+// flattened butterflies) for its flits: a link busy with an earlier
+// reservation delays the packet and every later hop.  The last link of every
+// route is the destination's ejection link, so arrivals at one destination
+// stay in reservation order (its input queue stays time sorted).
+//
+// Contention only delays packets, so the PDES lookahead (the uncontended
+// minimum latency) still holds.  A single-stage butterfly (the crossbar every
+// tested config uses) has no internal links: its contention is the ports',
+// which the engines model at the endpoints already.
+//
+// The pass is policy-generic (P = SeqPar on the CPU engine, WavePar on one
+// GPU block) and its order is fixed, so both engines give identical results.
+#pragma once
+#include "config.h"
+
+namespace asim {
+
+constexpr int kMaxPathLinks = 256;
+constexpr uint64_t kMaxIcntLinks = 1ull << 22;
+
+SIM_HDI uint64_t ipow(uint32_t k, uint32_t n) {
+  uint64_t r = 1;
+  for (uint32_t i = 0; i < n; ++i) r *= k;
+  return r;
+}
+
+// directed links of the topology that the route model names (0: none)
+SIM_HDI uint64_t icnt_link_count(const SimCfg& c) {
+  if (c.icnt_mode != 1) return 0;
+  const uint32_t k = c.topo_k ? c.topo_k : 2, n = c.topo_n ? c.topo_n : 1;
+  const uint64_t kn = ipow(k, n);
+  switch (c.topo) {
+    case TOPO_FLY: return n <= 1 ? 0 : (uint64_t)n * kn;  // stage x router x port
+    case TOPO_CMESH:
+    case TOPO_MESH:
+    case TOPO_TORUS: return kn * (2ull * n + (c.topo == TOPO_CMESH ? (c.topo_conc ? c.topo_conc : 1) : 1));
+    case TOPO_FATTREE: return 2ull * n * kn + kn;  // up, down, ejection
+    default: return kn * ((uint64_t)n * k + 1);     // flattened butterfly: per dimension and target, + ejection
+  }
+}
+
+SIM_HDI bool icnt_contention_on(const SimCfg& c) {
+  const uint64_t n = icnt_link_count(c);
+  return c.link_contention && n > 0 && n <= kMaxIcntLinks;
+}
+
+// the links of the route from interconnect node a to node b, in traversal
+// order (the last one ejects into b); returns their number
+SIM_HDI uint32_t icnt_path(const SimCfg& c, uint32_t a, uint32_t b, uint32_t* L) {
+  const uint32_t k = c.topo_k ? c.topo_k : 2, n = c.topo_n ? c.topo_n : 1;
+  uint32_t m = 0;
+  switch (c.topo) {
+    case TOPO_FLY: {  // destination-tag routing, most significant digit first
+      const uint64_t kn1 = ipow(k, n - 1);
+      uint64_t cur = a;
+      for (uint32_t s = 0; s < n && m < (uint32_t)kMaxPathLinks; ++s) {
+        const uint64_t pw = ipow(k, n - 1 - s);             // weight of the digit this stage sets
+        const uint32_t port = (uint32_t)((b / pw) % k);
+        const uint64_t r = (cur / (pw * k)) * pw + cur % pw;  // the router: cur without that digit
+        L[m++] = (uint32_t)(((uint64_t)s * kn1 + r) * k + port);
+        cur = cur - ((cur / pw) % k) * pw + (uint64_t)port * pw;
+      }
+      return m;
+    }
+    case TOPO_CMESH:
+    case TOPO_MESH:
+    case TOPO_TORUS: {  // dimension-order routing on a k-ary n-cube
+      const uint32_t conc = c.topo == TOPO_CMESH ? (c.topo_conc ? c.topo_conc : 1) : 1;
+      const uint32_t P = 2 * n + conc;
+      uint64_t cur = a / conc;
+      const uint64_t dst = b / conc;
+      uint64_t pw = 1;
+      for (uint32_t d = 0; d < n; ++d, pw *= k) {
+        for (uint32_t guard = 0; guard < k && m + 1 < (uint32_t)kMaxPathLinks; ++guard) {
+          const uint32_t x = (uint32_t)((cur / pw) % k), y = (uint32_t)((dst / pw) % k);
+          if (x == y) break;
+          bool up = y > x;
+          if (c.topo == TOPO_TORUS) {
+            const uint32_t fwd = (y + k - x) % k;  // hops going up (with wrap)
+            up = fwd <= k - fwd;
+          }
+          L[m++] = (uint32_t)(cur * P + 2 * d + (up ? 0 : 1));
+          const uint32_t nx = up ? (x + 1) % k : (x + k - 1) % k;
+          cur = cur - (uint64_t)x * pw + (uint64_t)nx * pw;
+        }
+      }
+      L[m++] = (uint32_t)(cur * P + 2 * n + b % conc);
+      return m;
+    }
+    case TOPO_FATTREE: {  // up to the lowest common ancestor (d-mod-k), then down
+      const uint64_t kn = ipow(k, n);
+      uint32_t lvl = 1;
+      {
+        uint64_t x = a / k, y = b / k;
+        while (x != y && lvl < n) {
+          x /= k;
+          y /= k;
+          ++lvl;
+        }
+      }
+      for (uint32_t l = 0; l + 1 < lvl; ++l) {
+        const uint64_t pl = ipow(k, l);
+        L[m++] = (uint32_t)((uint64_t)l * kn + (a / (pl * k)) * k + (b / pl) % k);
+      }
+      for (uint32_t l = lvl - 1; l-- > 0;) {
+        const uint64_t pl = ipow(k, l);
+        L[m++] = (uint32_t)((uint64_t)n * kn + (uint64_t)l * kn + (b / (pl * k)) * k + (b / pl) % k);
+      }
+      L[m++] = (uint32_t)(2ull * n * kn + b % kn);
+      return m;
+    }
+    default: {  // flattened butterfly: one hop per differing dimension
+      const uint32_t P = n * k + 1;
+      uint64_t cur = a, pw = 1;
+      for (uint32_t d = 0; d < n; ++d, pw *= k) {
+        const uint32_t x = (uint32_t)((cur / pw) % k), y = (uint32_t)((b / pw) % k);
+        if (x == y) continue;
+        L[m++] = (uint32_t)(cur * P + d * k + y);
+        cur = cur - (uint64_t)x * pw + (uint64_t)y * pw;
+      }
+      L[m++] = (uint32_t)(cur * P + n * k);
+      return m;
+    }
+  }
+}
+
+// reserve the route of one packet (a -> b, uncontended arrival p.t) and
+// return its extra delay (fs)
+SIM_HDI uint64_t icnt_reserve(const SimCfg& c, Pkt& p, uint32_t a, uint32_t b, uint64_t* link_free) {
+  uint32_t L[kMaxPathLinks];
+  const uint32_t nl = icnt_path(c, a, b, L);
+  const uint64_t nflits = (p.size + c.flit_size - 1) / c.flit_size;
+  const uint64_t occ = (nflits ? nflits : 1) * c.per_icnt;
+  const uint64_t hop = ((uint64_t)c.hop_icnt + c.chan_icnt) * c.per_icnt, last = (uint64_t)c.chan_icnt * c.per_icnt;
+  uint64_t D = 0;
+  for (uint32_t h = 0; h < nl; ++h) {
+    // uncontended departure onto link h (the route's schedule ends at p.t)
+    const uint64_t back = (uint64_t)(nl - 1 - h) * hop + last;
+    const uint64_t d = p.t > back ? p.t - back : 0;
+    uint64_t t = d + D;
+    const uint64_t f = link_free[L[h]];
+    if (f > t) {
+      D += f - t;
+      t = f;
+    }
+    link_free[L[h]] = t + occ;
+  }
+  p.t += D;
+  return D;
+}
+
+// the epoch-boundary pass over this epoch's outboxes (requests [sub][sm][cap],
+// replies [sm][sub][cap]); `refs` holds up to every cell x cap entries, stat
+// accumulates {delayed packets, delay in interconnect cycles}
+template <class P>
+SIM_HDI void icnt_contend(const SimCfg& c, Pkt* box_req, const uint32_t* cnt_req, uint32_t cap_req, Pkt* box_rep,
+                          const uint32_t* cnt_rep, uint32_t cap_rep, uint64_t* link_free, uint32_t* refs,
+                          uint64_t* stat) {
+  const uint32_t ncell = c.n_sm * c.n_subpart;
+  const uint32_t cpc = c.cores_per_cluster ? c.cores_per_cluster : 1;
+  for (int dir = 0; dir < 2; ++dir) {
+    const uint32_t* cnt = dir == 0 ? cnt_req : cnt_rep;
+    // every packet of the epoch in cell order: (cell << 8 | index in the cell)
+    const uint32_t total = P::scan((int)ncell, [&](int i) -> uint32_t { return cnt[i]; },
+                                   [&](int i, uint32_t off) {
+                                     for (uint32_t j = 0; j < cnt[i]; ++j) refs[off + j] = (uint32_t)i << 8 | j;
+                                   });
+    P::sync();
+    if (total == 0) continue;
+    P::one([&] {
+      uint64_t delayed = 0, wait = 0;
+      for (uint32_t r = 0; r < total; ++r) {
+        const uint32_t cell = refs[r] >> 8, j = refs[r] & 0xffu;
+        uint32_t a, b;
+        Pkt* p;
+        if (dir == 0) {  // request: SM (cell % n_sm) -> sub-partition (cell / n_sm)
+          a = (cell % c.n_sm) / cpc;
+          b = c.n_clusters + cell / c.n_sm;
+          p = &box_req[(uint64_t)cell * cap_req + j];
+        } else {  // reply: sub-partition (cell % n_subpart) -> SM (cell / n_subpart)
+          a = c.n_clusters + cell % c.n_subpart;
+          b = (cell / c.n_subpart) / cpc;
+          p = &box_rep[(uint64_t)cell * cap_rep + j];
+        }
+        const uint64_t D = icnt_reserve(c, *p, a, b, link_free);
+        if (D) {
+          ++delayed;
+          wait += D / c.per_icnt;
+        }
+      }
+      stat[0] += delayed;
+      stat[1] += wait;
+    });
+    P::sync();
+  }
+}
+
+}  // namespace asim

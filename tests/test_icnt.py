@@ -3,6 +3,7 @@
 iq_router pipeline; icnt_wrapper.cc node numbering) and the pre-Volta presets
 that use it."""
 import glob
+import re
 import os
 import subprocess
 
@@ -166,4 +167,96 @@ def test_crossbar_hotspot_gpu_matches_cpu(native, tmp_path):
         assert s.run() == 0
         res.append([_stat(s.output, k) for k in ("gpu_sim_cycle", "Req_Network_conflicts",
                                                   "Req_Network_queueing_cycles", "Reply_Network_queueing_cycles")])
+    assert res[0] == res[1] and res[0][1] > 100
+
+
+# ---- link-level contention in multi-hop topologies (icnt_links.h) ----------
+TOPOS = [("mesh", dict(k=8, n=2, topology="mesh")), ("torus", dict(k=8, n=2, topology="torus")),
+         ("fly2", dict(k=8, n=2, topology="fly")), ("fattree", dict(k=4, n=3, topology="fattree")),
+         ("flatfly", dict(k=8, n=2, topology="flatfly"))]
+
+
+@pytest.mark.parametrize("name,kw", TOPOS)
+def test_link_routes_follow_the_topology(native, tmp_path, name, kw):
+    args = _icnt_args(tmp_path, name, **kw)
+    for a in range(16):
+        for sub in range(16):
+            b = 16 + sub
+            for (x, y) in ((a, b), (b, a)):
+                links, total = native.icnt_path(args, x, y)
+                # one link per router crossed (the last one ejects), as many as
+                # the latency model's router count, all distinct and in range
+                sm = x if x < 16 else y
+                assert len(links) == native.icnt_latency(args, sm, sub)[2], (name, x, y)
+                assert len(set(links)) == len(links) and all(0 <= l < total for l in links)
+            # routes to different destinations leave through different ejection links
+    ej = {native.icnt_path(args, 0, 16 + s)[0][-1] for s in range(16)}
+    assert len(ej) == 16
+
+
+def test_single_stage_crossbar_has_no_internal_links(native, tmp_path):
+    fly = _icnt_args(tmp_path, "fly", k=32, n=1)
+    assert native.icnt_path(fly, 0, 16) == ([], 0)
+    kl = rodinia.write_app(str(tmp_path / "bfs"), rodinia.bfs(2048, levels=2))
+    res = []
+    for lc in ("0", "1"):
+        s = native.Simulator(fly + ["-icnt_link_contention", lc, "-trace", kl], False)
+        assert s.run() == 0
+        res.append((s.tot_cycle, s.output.count("Network_link_wait_cycles")))
+    assert res[0] == (res[1][0], 0) and res[1][1] == 0  # identical, nothing to report
+
+
+def _link_stat(out, key):
+    return int(re.findall(rf"^{key} = (\d+)", out, re.M)[-1])
+
+
+def test_mesh_hotspot_links_delay_packets(native, tmp_path):
+    kl = _hotspot_app(tmp_path, "hot", True)
+    mesh = _icnt_args(tmp_path, "mesh", k=8, n=2, topology="mesh")
+    runs = {}
+    for lc in ("0", "1"):
+        s = native.Simulator(mesh + ["-icnt_link_contention", lc, "-gpgpu_perf_sim_memcpy", "0", "-trace", kl], False)
+        assert s.run() == 0 and not s.deadlock
+        runs[lc] = s
+    assert runs["0"].tot_insn == runs["1"].tot_insn
+    assert "Network_link_wait_cycles" not in runs["0"].output
+    out = runs["1"].output
+    assert _link_stat(out, "Network_link_delayed_packets") > 100
+    assert _link_stat(out, "Network_link_wait_cycles") > _link_stat(out, "Network_link_delayed_packets")
+    # 80 SMs' requests converge on one sub-partition: shared links cost time
+    assert runs["1"].tot_cycle > runs["0"].tot_cycle
+    # deterministic, and independent of the CPU engine's thread count
+    s4 = native.Simulator(mesh + ["-icnt_link_contention", "1", "-gpgpu_perf_sim_memcpy", "0",
+                                  "-sim_cpu_threads", "4", "-trace", kl], False)
+    assert s4.run() == 0
+    assert (s4.tot_cycle, _link_stat(s4.output, "Network_link_wait_cycles")) == \
+        (runs["1"].tot_cycle, _link_stat(out, "Network_link_wait_cycles"))
+
+
+def test_link_state_checkpoint_resumes_exactly(native, tmp_path):
+    from accel_sim_framework_distributed_amd.tracegen import rodinia as rd
+    kl = rd.write_app(str(tmp_path / "pf"), rd.pathfinder(4000, 12, 2))
+    mesh = _icnt_args(tmp_path, "mesh", k=8, n=2, topology="mesh") + [
+        "-icnt_link_contention", "1", "-trace", kl, "-checkpoint_path", str(tmp_path / "ck")]
+    full = native.Simulator(mesh, False)
+    assert full.run() == 0
+    first = native.Simulator(mesh + ["-checkpoint_option", "1", "-checkpoint_kernel", "2"], False)
+    assert first.run() == 0
+    rest = native.Simulator(mesh + ["-resume_option", "1", "-resume_kernel", "2"], False)
+    assert rest.run() == 0 and "resumed from" in rest.output
+    assert rest.tot_cycle == full.tot_cycle and _link_stat(full.output, "Network_link_delayed_packets") > 0
+    assert _link_stat(rest.output, "Network_link_wait_cycles") == _link_stat(full.output, "Network_link_wait_cycles")
+
+
+@pytest.mark.gpu
+def test_mesh_link_contention_gpu_matches_cpu(native, tmp_path):
+    kl = _hotspot_app(tmp_path, "hotg", True)
+    mesh = _icnt_args(tmp_path, "mesh", k=8, n=2, topology="mesh")
+    res = []
+    for eng in ("cpu", "gpu"):
+        s = native.Simulator(mesh + ["-icnt_link_contention", "1", "-gpgpu_perf_sim_memcpy", "0",
+                                     "-sim_engine", eng, "-trace", kl], False)
+        assert s.run() == 0
+        res.append((s.tot_cycle, _link_stat(s.output, "Network_link_delayed_packets"),
+                    _link_stat(s.output, "Network_link_wait_cycles"), _stat(s.output, "Req_Network_queueing_cycles")))
     assert res[0] == res[1] and res[0][1] > 100
