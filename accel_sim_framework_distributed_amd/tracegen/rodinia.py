@@ -227,8 +227,13 @@ def hotspot(grid_n: int = 512, pyramid: int = 2, iters: int = 6, kid0: int = 1) 
 
 
 # ----------------------------------------------------------------------------
-def heartwall(n_points: int = 51, kid0: int = 1, scale: float = 1.0) -> List[KernelArrays]:
-    """One long kernel: template matching with big ALU loops (1 frame)."""
+def heartwall(n_points: int = 51, kid0: int = 1, scale: float = 1.0, alu_per_iter: int = 0) -> List[KernelArrays]:
+    """One long kernel: template matching with big ALU loops (1 frame).
+
+    `alu_per_iter` extra independent FFMAs per loop iteration (0: the suite's
+    shape, 2 global loads per 6 ALU ops; the gfx950 heartwall's measured mix
+    is ~10 VALU per global load, profiles/isatrace/heartwall.verify.txt; see
+    profiles/heartwall_parity.md)."""
     block = 512
     k = KernelBuilder("_Z6kernelv", (n_points, 1, 1), (block, 1, 1), shmem=4 * 1024, nregs=56, kid=kid0)
     g = k.g
@@ -238,6 +243,9 @@ def heartwall(n_points: int = 51, kid0: int = 1, scale: float = 1.0) -> List[Ker
         off = (g.cta * 65536 + g.warp * 4096 + it * 128)
         k.op("LDG.E", [6], [10], base=buf(0) + off, stride=4)
         k.op("LDG.E", [7], [11], base=buf(1) + off, stride=4)
+        for j in range(alu_per_iter):
+            r = 24 + (j % 8)
+            k.op("FFMA", [r], [r, 3, r])
         k.op("IMAD", [8], [2, 3])
         k.op("FADD", [9], [6, 7])
         k.op("FMUL", [9], [9, 9])

@@ -647,6 +647,12 @@ int main(int argc, char** argv) {
   // ramp of a 1x loop barely reaches
   const int scv = trace ? 8 : sc;
   const size_t nbig = trace ? (size_t)2 << 20 : big / 16;  // trace: 32 MB sweep
+  // cache-resident sweeps are traced long enough that the warm passes, not
+  // the first (cold-miss) pass and the LDS initialisation, set the sampled
+  // power: with 2 passes the simulated L1 / L2 kernels drew HBM / LDS-store
+  // power the measured steady-state loops never do (round-4 held-out
+  // errors: lds_l1_mix +82 %, fp64_l1_mix +47 %, fp32_l2_mix +41 %)
+  const int rl1 = trace ? 16 : sc / 4, rl2 = trace ? 6 : 2 * sc;
   const dim3 b(256);
   auto g = [&](int per_cu) { return dim3(cus * per_cu); };
   struct K {
@@ -672,8 +678,8 @@ int main(int argc, char** argv) {
       {"hbm_read", [&] { k_read<<<g(16), b>>>(buf, nbig, trace ? 1 : 4, sink); }},
       {"hbm_write", [&] { k_write<<<g(16), b>>>(buf, nbig, trace ? 1 : 4); }},
       {"hbm_copy", [&] { k_copy<<<g(16), b>>>(buf, buf2, nbig / 2, trace ? 1 : 4); }},
-      {"l2_read", [&] { k_read<<<g(8), b>>>(buf, l2 / 16, trace ? 2 : 2 * sc, sink); }},
-      {"l1_read", [&] { k_l1_read<<<g(8), b>>>(buf, trace ? 2 : sc / 4, sink); }},
+      {"l2_read", [&] { k_read<<<g(8), b>>>(buf, l2 / 16, rl2, sink); }},
+      {"l1_read", [&] { k_l1_read<<<g(8), b>>>(buf, rl1, sink); }},
       {"fp32_hbm_mix", [&] { k_fp32_read<<<g(16), b>>>(buf, nbig, 8, sink); }},
       {"fp64_hbm_mix", [&] { k_fp64_read<<<g(16), b>>>(buf, nbig, 4, sink); }},
       {"atomic_l2", [&] { k_atomic<<<g(4), b>>>(ctr, trace ? 2 : sc / 8); }},
@@ -685,7 +691,7 @@ int main(int argc, char** argv) {
       {"sfu_occ2", [&] { k_sfu<<<g(2), b>>>(sink, 8 * scv); }},
       {"fp64_fma_occ2", [&] { k_fp64<<<g(2), b>>>(sink, 4 * scv); }},
       {"hbm_read_occ2", [&] { k_read<<<g(2), b>>>(buf, nbig, trace ? 1 : 4, sink); }},
-      {"l2_write", [&] { k_write<<<g(8), b>>>(buf, l2 / 16, trace ? 2 : 2 * sc); }},
+      {"l2_write", [&] { k_write<<<g(8), b>>>(buf, l2 / 16, rl2); }},
       {"lds_read_occ2", [&] { k_lds_read<<<g(2), b>>>(sink, 16 * sc); }},
       // round 4: one unit per kernel (calibration) ...
       {"fp32_add", [&] { k_fp32_add<<<g(8), b>>>(sink, 8 * scv); }},
@@ -698,9 +704,9 @@ int main(int argc, char** argv) {
       {"sfu_fp32_mix", [&] { k_sfu_fp32<<<g(8), b>>>(sink, 8 * scv); }},
       {"mfma_lds_mix", [&] { k_mfma_lds<<<g(8), b>>>(sink, 2 * scv); }},
       {"mfma_hbm_mix", [&] { k_mfma_read<<<g(16), b>>>(buf, nbig, sink); }},
-      {"fp32_l2_mix", [&] { k_fp32_read_reps<<<g(8), b>>>(buf, l2 / 16, trace ? 2 : 2 * sc, 4, sink); }},
+      {"fp32_l2_mix", [&] { k_fp32_read_reps<<<g(8), b>>>(buf, l2 / 16, rl2, 4, sink); }},
       {"int_hbm_mix", [&] { k_int_read<<<g(16), b>>>(buf, nbig, 4, sink); }},
-      {"fp64_l1_mix", [&] { k_fp64_l1<<<g(8), b>>>(buf, trace ? 2 : sc / 4, sink); }},
+      {"fp64_l1_mix", [&] { k_fp64_l1<<<g(8), b>>>(buf, rl1, sink); }},
       {"atomic_fp32_mix", [&] { k_atomic_fp32<<<g(4), b>>>(ctr, trace ? 2 : sc / 8, sink); }},
       {"lds_write_occ2", [&] { k_lds_write<<<g(2), b>>>(sink, 16 * sc); }},
       {"hbm_write_occ2", [&] { k_write<<<g(2), b>>>(buf, nbig, trace ? 1 : 4); }},
@@ -710,11 +716,11 @@ int main(int argc, char** argv) {
       {"lds_hbm_mix", [&] { k_lds_read_hbm<<<g(16), b>>>(buf, nbig, sink); }},
       {"fp32_lds_write_mix", [&] { k_fp32_lds_write<<<g(8), b>>>(sink, 16 * sc); }},
       {"mfma_fp64_mix", [&] { k_mfma_fp64<<<g(8), b>>>(sink, 2 * scv); }},
-      {"int_l2_mix", [&] { k_int_l2<<<g(8), b>>>(buf, l2 / 16, trace ? 2 : 2 * sc, sink); }},
+      {"int_l2_mix", [&] { k_int_l2<<<g(8), b>>>(buf, l2 / 16, rl2, sink); }},
       {"fp_int_add_mix", [&] { k_fp_int_add<<<g(8), b>>>(sink, 8 * scv); }},
       {"copy_fp32_mix", [&] { k_copy_fp32<<<g(16), b>>>(buf, buf2, nbig / 2, sink); }},
       {"mfma_sfu_mix", [&] { k_mfma_sfu<<<g(8), b>>>(sink, 2 * scv); }},
-      {"lds_l1_mix", [&] { k_lds_l1<<<g(8), b>>>(buf, trace ? 2 : sc / 4, sink); }},
+      {"lds_l1_mix", [&] { k_lds_l1<<<g(8), b>>>(buf, rl1, sink); }},
       {"int_fp_mix_occ2", [&] { k_int_fp<<<g(2), b>>>(sink, 8 * scv); }},
       {"sfu_fp32_mix_occ2", [&] { k_sfu_fp32<<<g(2), b>>>(sink, 8 * scv); }},
   };
