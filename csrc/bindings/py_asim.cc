@@ -148,6 +148,16 @@ PYBIND11_MODULE(_asim, m) {
   m.attr("sizeof_SMState") = sizeof(SMState);
   m.attr("sizeof_ChanState") = sizeof(ChanState);
   m.attr("offsetof_SMState_skipped") = offsetof(SMState, skipped_cycles);
+  // (offset, bytes) of the fields whose contents depend on which epochs ran
+  // (gather scratch, the mailbox-parity flags): compare snapshots of runs
+  // with different epoch sequences (event skipping on / off) without them
+  m.attr("epoch_dependent_SMState") = std::vector<std::pair<size_t, size_t>>{
+      {offsetof(SMState, skey), sizeof(SMState::skey)}, {offsetof(SMState, sref), sizeof(SMState::sref)},
+      {offsetof(SMState, srank), sizeof(SMState::srank)}, {offsetof(SMState, pub_nz), sizeof(SMState::pub_nz)},
+      {offsetof(SMState, skipped_cycles), sizeof(SMState::skipped_cycles)}};
+  m.attr("epoch_dependent_ChanState") = std::vector<std::pair<size_t, size_t>>{
+      {offsetof(ChanState, skey), sizeof(ChanState::skey)}, {offsetof(ChanState, sref), sizeof(ChanState::sref)},
+      {offsetof(ChanState, srank), sizeof(ChanState::srank)}, {offsetof(ChanState, pub_nz), sizeof(ChanState::pub_nz)}};
   m.attr("sizeof_TInst") = sizeof(TInst);
 
   m.def("gpu_available", &gpu_engine_available, "True if a HIP device is usable by the GPU engine");

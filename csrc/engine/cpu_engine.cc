@@ -217,6 +217,9 @@ class CpuEngine : public Engine {
       bool refill = true;
       // armed power sampler: the next sample point (every thread tracks it)
       uint64_t pw_next = pw_on_ ? pw_.t_prev + pw_.freq : 0;
+      // destinations with packets in the previous epoch's mailboxes (all at a
+      // run's first epoch): the gathers of the others are skipped
+      uint64_t reqm[2] = {~0ull, ~0ull}, repm[2] = {~0ull, ~0ull};
       RunResult r;
       for (;;) {
         // host-streamed traces: bring in the CTAs the next epochs can
@@ -239,13 +242,13 @@ class CpuEngine : public Engine {
             SMState& s = sms_[i];
             SmCtx x = ctx_sm(cur);
             sm_epoch<SeqPar>(s, x, *pub_, prev, t0, t1, box_rep_[prev].data(), cnt_rep_[prev].data(), cap_rep_,
-                             c.n_subpart, epoch);
+                             c.n_subpart, epoch, repm);
             sm_publish<SeqPar>(s, x, *pub_, cur);
           } else {
             ChanState& ch = chs_[i - nsm];
             MemCtx m = ctx_mem(cur, t1);
             m.mall = mall_.empty() ? nullptr : mall_.data() + (size_t)(i - nsm) * mall_lines(c);
-            chan_epoch<SeqPar>(ch, m, box_req_[prev].data(), cnt_req_[prev].data(), cap_req_, core_fs(c, t0));
+            chan_epoch<SeqPar>(ch, m, box_req_[prev].data(), cnt_req_[prev].data(), cap_req_, core_fs(c, t0), reqm);
             chan_publish<SeqPar>(ch, m, *pub_, cur);
           }
         }
@@ -261,6 +264,10 @@ class CpuEngine : public Engine {
         const uint64_t mc = pw_on_ ? (lim.max_cycle ? std::min(lim.max_cycle, pw_next) : pw_next) : lim.max_cycle;
         const EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, kt_, epoch, mc);
         refill = d.refill != 0;
+        reqm[0] = d.req_dst[0];
+        reqm[1] = d.req_dst[1];
+        repm[0] = d.rep_dst[0];
+        repm[1] = d.rep_dst[1];
         ++epoch;
         ++epochs;
         cycle = d.next_start;

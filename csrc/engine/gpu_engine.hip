@@ -324,6 +324,9 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   uint32_t nbar = 0;  // grid barriers of this launch (epochs + power samples)
   uint64_t pw_next = a.pw ? a.pw->next : 0;
   bool failed = false;
+  // destinations with packets in the previous epoch's mailboxes (all at the
+  // launch's first epoch): the gathers of the others are skipped
+  uint64_t reqm[2] = {~0ull, ~0ull}, repm[2] = {~0ull, ~0ull};
   for (; n < a.max_epochs;) {
     const uint32_t cur = (uint32_t)(epoch & 1), prev = cur ^ 1u;
     const uint64_t t0 = cycle, t1 = t0 + E;
@@ -339,14 +342,14 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
         sx.outbox = a.box_req[cur];
         sx.outcnt = a.cnt_req[cur];
         sm_epoch<P>(*s, sx, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep,
-                    c.n_subpart, epoch);
+                    c.n_subpart, epoch, repm);
         sm_publish<P>(*s, sx, *a.pub, cur);
       } else {
         mx.outbox = a.box_rep[cur];
         mx.outcnt = a.cnt_rep[cur];
         mx.mall = a.mall ? a.mall + (size_t)(u - c.n_sm) * ((size_t)c.mall_sets * c.mall_assoc) : nullptr;
         mx.win_end = core_fs(c, t1);
-        chan_epoch<P>(*ch, mx, a.box_req[prev], a.cnt_req[prev], a.cap_req, core_fs(c, t0));
+        chan_epoch<P>(*ch, mx, a.box_req[prev], a.cnt_req[prev], a.cap_req, core_fs(c, t0), reqm);
         chan_publish<P>(*ch, mx, *a.pub, cur);
       }
     }
@@ -394,6 +397,10 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     // sampled slice's max_cycle would
     const uint64_t mc = a.pw ? (a.max_cycle ? (a.max_cycle < pw_next ? a.max_cycle : pw_next) : pw_next) : a.max_cycle;
     EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, kt, epoch, mc);
+    reqm[0] = P::uni(d.req_dst[0]);
+    reqm[1] = P::uni(d.req_dst[1]);
+    repm[0] = P::uni(d.rep_dst[0]);
+    repm[1] = P::uni(d.rep_dst[1]);
     P::prof(28);
     ++epoch;
     cycle = P::uni(d.next_start);

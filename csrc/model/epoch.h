@@ -34,8 +34,9 @@ struct UnitPub {
   uint32_t drained;  // SM: holds no work (launch latency may be pending)
   uint32_t ctas;     // SM: CTAs completed so far (-gpgpu_max_completed_cta)
   uint64_t reqk;     // SM: byte k: CTAs of slot k it can accept next epoch
+  uint64_t dmask[2]; // destinations it put packets for this epoch (bit d % 128; SM: sub-partitions, channel: SMs)
 };
-static_assert(sizeof(UnitPub) == 48, "UnitPub layout");
+static_assert(sizeof(UnitPub) == 64, "UnitPub layout");
 // epoch-boundary publications, double buffered by epoch parity
 struct EpochPub {
   UnitPub sm[2][kMaxSmTot];
@@ -55,6 +56,10 @@ struct EpochDecision {
   uint32_t limit;       // -gpgpu_max_insn / _max_completed_cta / _max_cta reached: stop
   uint32_t refill;      // the next epoch's dispatch could need a CTA whose trace is not resident
   uint64_t next_start;  // start cycle of the next epoch (after fast-forward)
+  // destinations (bit d % 128) that have packets in this epoch's mailboxes:
+  // the next epoch's gathers skip the others (their cells are all zero)
+  uint64_t req_dst[2];  // sub-partitions with requests
+  uint64_t rep_dst[2];  // SMs with replies
 };
 
 // ---------------------------------------------------------------------------
@@ -234,7 +239,7 @@ SIM_HDI void sm_kernels_init(SMState& s, const SmCtx& x) {
 template <class P>
 SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t prev,
                       uint64_t t0, uint64_t t1, const Pkt* inbox, const uint32_t* incnt, uint32_t in_cap,
-                      uint32_t n_sub, uint64_t epoch_idx) {
+                      uint32_t n_sub, uint64_t epoch_idx, const uint64_t* rep_dst = nullptr) {
   const SimCfg& c = *x.cfg;
   sm_kernels_init<P>(s, x);
   // 0. cycles [s.cycle, t0) were fast-forwarded by epoch_decide (nothing could
@@ -243,8 +248,10 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t 
   s.min_emit = ~0ull;
   // 1. arrivals (replies injected by the memory side last epoch)
   P::prof(12);
-  gather_sorted<P>(inbox, incnt, s.id, n_sub, in_cap, core_fs(c, t0), s.inq, kInQ, s.inq_head, s.inq_n,
-                   s_scratch_key(s), s_scratch_ref(s), s_scratch_rank(s), kInQ);
+  //    (skipped when no channel put a reply for this SM last epoch)
+  if (dst_maybe(rep_dst, s.id))
+    gather_sorted<P>(inbox, incnt, s.id, n_sub, in_cap, core_fs(c, t0), s.inq, kInQ, s.inq_head, s.inq_n,
+                     s_scratch_key(s), s_scratch_ref(s), s_scratch_rank(s), kInQ);
   // 2. CTA dispatch (state published at the previous boundary)
   P::prof(13);
   {
@@ -294,11 +301,23 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t 
 template <class P>
 SIM_HDI void sm_publish(SMState& s, const SmCtx& x, EpochPub& pub, uint32_t cur) {
   const SimCfg& c = *x.cfg;
-  P::each((int)c.n_subpart, [&](int d) {
-    x.outcnt[(uint64_t)d * x.n_src_sm + s.id] = s.ocnt[d];
-    s.ocnt[d] = 0;
-  });
-  P::sync();
+  // destinations written this epoch (none when no packet was injected: every
+  // injection lowers min_emit); this parity's cells are rewritten only if
+  // they or the last write to them hold packets (pub_nz bit `cur`)
+  uint64_t dm0 = 0, dm1 = 0;
+  if (P::uni(s.min_emit) != ~0ull) {
+    dm0 = P::vor((int)c.n_subpart, [&](int d) -> uint64_t { return (s.ocnt[d] && !(d & 64)) ? 1ull << (d & 63) : 0; });
+    dm1 = P::vor((int)c.n_subpart, [&](int d) -> uint64_t { return (s.ocnt[d] && (d & 64)) ? 1ull << (d & 63) : 0; });
+  }
+  const uint32_t nzb = 1u << cur, nz = P::uni((uint32_t)s.pub_nz);
+  if ((dm0 | dm1) || (nz & nzb)) {
+    P::each((int)c.n_subpart, [&](int d) {
+      x.outcnt[(uint64_t)d * x.n_src_sm + s.id] = s.ocnt[d];
+      s.ocnt[d] = 0;
+    });
+    P::sync();
+  }
+  s.pub_nz = (dm0 | dm1) ? (nz | nzb) : (nz & ~nzb);
   // CTA requests per kernel, oldest kernel first: each kernel asks for what
   // is left after the older ones' requests (a request the dispatch does not
   // fill is simply renewed at the next boundary)
@@ -343,6 +362,8 @@ SIM_HDI void sm_publish(SMState& s, const SmCtx& x, EpochPub& pub, uint32_t cur)
   u.drained = sm_idle(s) ? 1u : 0u;
   u.ctas = (uint32_t)s.sget(SK(ctas_done));
   u.reqk = reqk;
+  u.dmask[0] = dm0;
+  u.dmask[1] = dm1;
   P::one([&] {
     pub.sm[cur][s.id] = u;
     if (s.id == 0)
@@ -356,10 +377,10 @@ SIM_HDI void sm_publish(SMState& s, const SmCtx& x, EpochPub& pub, uint32_t cur)
 // one epoch of one memory channel
 template <class P>
 SIM_HDI void chan_epoch(ChanState& ch, const MemCtx& x, const Pkt* inbox, const uint32_t* incnt,
-                        uint32_t in_cap, uint64_t t0_fs) {
+                        uint32_t in_cap, uint64_t t0_fs, const uint64_t* req_dst = nullptr) {
   P::prof(20);
   ch.min_emit = ~0ull;
-  mem_gather<P>(ch, *x.cfg, x, inbox, incnt, in_cap, t0_fs);
+  mem_gather<P>(ch, *x.cfg, x, inbox, incnt, in_cap, t0_fs, req_dst);
   P::one([&] {
     for (uint32_t j = 0; j < x.cfg->n_sub_per_mem; ++j) ch.sp[j].st.icnt_backlog += ch.sp[j].ovf_n;
   });
@@ -370,7 +391,8 @@ SIM_HDI void chan_epoch(ChanState& ch, const MemCtx& x, const Pkt* inbox, const 
 
 template <class P>
 SIM_HDI void chan_publish(ChanState& ch, const MemCtx& x, EpochPub& pub, uint32_t cur) {
-  mem_publish<P>(ch, *x.cfg, x.outcnt);
+  uint64_t dm[2] = {0, 0};
+  mem_publish<P>(ch, *x.cfg, x.outcnt, cur, dm);
   uint32_t idle = chan_idle(ch, *x.cfg) ? 1u : 0u;
   uint64_t nx = ~0ull;
   if (x.cfg->event_skip) nx = chan_next_event(ch, *x.cfg, amin(ch.t_dram, amin(ch.t_l2, ch.t_icnt)));
@@ -386,6 +408,8 @@ SIM_HDI void chan_publish(ChanState& ch, const MemCtx& x, EpochPub& pub, uint32_
   u.drained = idle;
   u.ctas = 0;
   u.reqk = 0;
+  u.dmask[0] = dm[0];
+  u.dmask[1] = dm[1];
   P::one([&] { pub.ch[cur][ch.id] = u; });
 }
 
@@ -397,8 +421,11 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   // one pass over every unit's record (one load per unit), then reductions
   uint32_t nbusy = 0, undrained = 0, cbusy = 0, ctas = 0, reqs = 0, kbusy = 0;
   uint64_t sm_next = ~0ull, ch_next = ~0ull, prog = 0, insn = 0;
+  uint64_t rq0 = 0, rq1 = 0, rp0 = 0, rp1 = 0;
   P::lane_loop((int)c.n_sm, [&](int j) {
     const UnitPub u = pub.sm[cur][j];
+    rq0 |= u.dmask[0];
+    rq1 |= u.dmask[1];
     insn += u.insn;
     ctas += u.ctas;
     nbusy += u.idle ? 0u : 1u;
@@ -410,6 +437,8 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   });
   P::lane_loop((int)c.n_mem, [&](int j) {
     const UnitPub u = pub.ch[cur][j];
+    rp0 |= u.dmask[0];
+    rp1 |= u.dmask[1];
     cbusy += u.idle ? 0u : 1u;
     ch_next = amin<uint64_t>(ch_next, u.next);
   });
@@ -421,6 +450,13 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   sm_next = P::uni(P::red_min64(sm_next));
   ch_next = P::uni(P::red_min64(ch_next));
   prog = P::uni(P::red_max64(prog));
+  auto or64 = [&](uint64_t v) -> uint64_t {
+    return (uint64_t)P::uni(P::red_or((uint32_t)v)) | (uint64_t)P::uni(P::red_or((uint32_t)(v >> 32))) << 32;
+  };
+  d.req_dst[0] = or64(rq0);
+  d.req_dst[1] = or64(rq1);
+  d.rep_dst[0] = or64(rp0);
+  d.rep_dst[1] = or64(rp1);
   // per kernel slot: fully dispatched, launch latency, completion
   const uint32_t active = kt.active;
   uint32_t undisp = 0, cut = 0, refill = 0;

@@ -124,7 +124,7 @@ struct SubPart {
 
 struct alignas(16) ChanState {
   uint32_t id;
-  uint32_t pad0;
+  uint32_t pub_nz;    // bit p: the reply cells of mailbox parity p were last written with packets
   uint64_t t_icnt;    // next tick time of each domain (fs)
   uint64_t t_l2;
   uint64_t t_dram;
@@ -1105,12 +1105,19 @@ SIM_HDI uint32_t gather_sorted(const Pkt* box, const uint32_t* cnt, uint32_t dst
   return n;
 }
 
+// bit d % 128 of a 128-bit destination mask (nullptr: every destination)
+SIM_HDI bool dst_maybe(const uint64_t* m, uint32_t d) {
+  return !m || ((m[(d >> 6) & 1u] >> (d & 63)) & 1ull);
+}
+
 template <class P>
 SIM_HDI void mem_gather(ChanState& ch, const SimCfg& c, const MemCtx& x, const Pkt* box, const uint32_t* cnt,
-                        uint32_t cap, uint64_t t0) {
+                        uint32_t cap, uint64_t t0, const uint64_t* req_dst = nullptr) {
   for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
     SubPart& sp = ch.sp[j];
     uint32_t gsub = ch.id * c.n_sub_per_mem + j;
+    // no request for this sub-partition last epoch and no backlog: nothing to move
+    if (!dst_maybe(req_dst, gsub) && !(x.ovf && P::uni(sp.ovf_n))) continue;
     Backlog bl{x.ovf ? x.ovf + (uint64_t)gsub * x.ovf_cap : nullptr, x.ovf_cap, &sp.ovf_head, &sp.ovf_n,
                &sp.st.icnt_ovf_drop};
     gather_sorted<P>(box, cnt, gsub, c.n_sm, cap, t0, sp.inq, kMemInQ, sp.inq_head, sp.inq_n, ch.skey,
@@ -1120,15 +1127,26 @@ SIM_HDI void mem_gather(ChanState& ch, const SimCfg& c, const MemCtx& x, const P
 
 // publish this epoch's reply counts (every cell, zeros included) and reset
 template <class P>
-SIM_HDI void mem_publish(ChanState& ch, const SimCfg& c, uint32_t* outcnt) {
-  for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
-    uint32_t gsub = ch.id * c.n_sub_per_mem + j;
-    P::each((int)c.n_sm, [&](int d) {
-      outcnt[(uint64_t)d * c.n_subpart + gsub] = ch.ocnt[j][d];
-      ch.ocnt[j][d] = 0;
-    });
+SIM_HDI void mem_publish(ChanState& ch, const SimCfg& c, uint32_t* outcnt, uint32_t cur, uint64_t* dm) {
+  // destination SMs written this epoch (bit d % 128); the cells of parity
+  // `cur` are rewritten only if they or the last write to them hold packets
+  if (P::uni(ch.min_emit) != ~0ull)
+    for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
+      dm[0] |= P::vor((int)c.n_sm, [&](int d) -> uint64_t { return (ch.ocnt[j][d] && !(d & 64)) ? 1ull << (d & 63) : 0; });
+      dm[1] |= P::vor((int)c.n_sm, [&](int d) -> uint64_t { return (ch.ocnt[j][d] && (d & 64)) ? 1ull << (d & 63) : 0; });
+    }
+  const uint32_t nzb = 1u << cur, nz = P::uni((uint32_t)ch.pub_nz);
+  if ((dm[0] | dm[1]) || (nz & nzb)) {
+    for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
+      uint32_t gsub = ch.id * c.n_sub_per_mem + j;
+      P::each((int)c.n_sm, [&](int d) {
+        outcnt[(uint64_t)d * c.n_subpart + gsub] = ch.ocnt[j][d];
+        ch.ocnt[j][d] = 0;
+      });
+    }
+    P::sync();
   }
-  P::sync();
+  ch.pub_nz = (dm[0] | dm[1]) ? (nz | nzb) : (nz & ~nzb);
 }
 
 }  // namespace asim

@@ -275,7 +275,7 @@ struct alignas(16) SMState {
   Pkt outq[kOutQ];
   uint32_t outq_head, outq_n;
   uint32_t outstanding;     // packets awaiting a reply
-  uint32_t pad_b;
+  uint32_t pub_nz;          // bit p: the request cells of mailbox parity p were last written with packets
   uint32_t ocnt[kMaxSubTot]; // packets put into each destination's outbox cell this epoch
   Pkt inq[kInQ];
   uint32_t inq_head, inq_n;

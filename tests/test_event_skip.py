@@ -59,11 +59,16 @@ def test_event_skip_identical_state(native, tmp_path):
     off = _run(native, kl, {"-gpgpu_perf_sim_memcpy": "0", "-sim_event_skip": "0"})
     a, b = bytearray(on.snapshot()), bytearray(off.snapshot())
     assert len(a) == len(b)
-    # the diagnostic count of skipped cycles is the one field allowed to differ
-    n_sm, sz, off8 = 80, native.sizeof_SMState, native.offsetof_SMState_skipped
-    for i in range(n_sm):
-        o = i * sz + off8
-        a[o:o + 8] = b[o:o + 8] = bytes(8)
+    # allowed to differ: the diagnostic count of skipped cycles, and what
+    # depends on which epochs ran (gather scratch, mailbox-parity flags)
+    n_sm, n_ch = 80, len(a) - 80 * native.sizeof_SMState
+    n_ch //= native.sizeof_ChanState
+    for base, size, fields in ((0, native.sizeof_SMState, native.epoch_dependent_SMState),
+                               (n_sm * native.sizeof_SMState, native.sizeof_ChanState, native.epoch_dependent_ChanState)):
+        for i in range(n_sm if base == 0 else n_ch):
+            for off, n in fields:
+                o = base + i * size + off
+                a[o:o + n] = b[o:o + n] = bytes(n)
     assert a == b
 
 
