@@ -227,13 +227,9 @@ PYBIND11_MODULE(_asim, m) {
       [](const std::vector<std::string>& args, uint32_t a, uint32_t b) {
         // (links of the route from node a to node b, the topology's link count)
         SimCfg c = cfg_from_args(args);
-        uint32_t L[kMaxPathLinks];
         const uint64_t n = icnt_link_count(c);
         std::vector<uint32_t> v;
-        if (n) {
-          const uint32_t m = icnt_path(c, a, b, L);
-          v.assign(L, L + m);
-        }
+        if (n) icnt_route(c, a, b, [&](uint32_t l) { v.push_back(l); });
         return py::make_tuple(v, n);
       },
       "link-contention route model (icnt_links.h): interconnect nodes are clusters, then sub-partitions");

@@ -57,9 +57,12 @@ SIM_HDI bool icnt_contention_on(const SimCfg& c) {
   return c.link_contention && n > 0 && n <= kMaxIcntLinks;
 }
 
-// the links of the route from interconnect node a to node b, in traversal
-// order (the last one ejects into b); returns their number
-SIM_HDI uint32_t icnt_path(const SimCfg& c, uint32_t a, uint32_t b, uint32_t* L) {
+// visit the links of the route from interconnect node a to node b in
+// traversal order (the last one ejects into b): emit(link); returns their
+// number (== icnt_routers(c, a, b)).  No array: the GPU engine's kernel keeps
+// no per-lane path buffer in scratch.
+template <class F>
+SIM_HDI uint32_t icnt_route(const SimCfg& c, uint32_t a, uint32_t b, F&& emit) {
   const uint32_t k = c.topo_k ? c.topo_k : 2, n = c.topo_n ? c.topo_n : 1;
   uint32_t m = 0;
   switch (c.topo) {
@@ -70,7 +73,8 @@ SIM_HDI uint32_t icnt_path(const SimCfg& c, uint32_t a, uint32_t b, uint32_t* L)
         const uint64_t pw = ipow(k, n - 1 - s);             // weight of the digit this stage sets
         const uint32_t port = (uint32_t)((b / pw) % k);
         const uint64_t r = (cur / (pw * k)) * pw + cur % pw;  // the router: cur without that digit
-        L[m++] = (uint32_t)(((uint64_t)s * kn1 + r) * k + port);
+        emit((uint32_t)(((uint64_t)s * kn1 + r) * k + port));
+        ++m;
         cur = cur - ((cur / pw) % k) * pw + (uint64_t)port * pw;
       }
       return m;
@@ -92,12 +96,14 @@ SIM_HDI uint32_t icnt_path(const SimCfg& c, uint32_t a, uint32_t b, uint32_t* L)
             const uint32_t fwd = (y + k - x) % k;  // hops going up (with wrap)
             up = fwd <= k - fwd;
           }
-          L[m++] = (uint32_t)(cur * P + 2 * d + (up ? 0 : 1));
+          emit((uint32_t)(cur * P + 2 * d + (up ? 0 : 1)));
+        ++m;
           const uint32_t nx = up ? (x + 1) % k : (x + k - 1) % k;
           cur = cur - (uint64_t)x * pw + (uint64_t)nx * pw;
         }
       }
-      L[m++] = (uint32_t)(cur * P + 2 * n + b % conc);
+      emit((uint32_t)(cur * P + 2 * n + b % conc));
+        ++m;
       return m;
     }
     case TOPO_FATTREE: {  // up to the lowest common ancestor (d-mod-k), then down
@@ -113,13 +119,16 @@ SIM_HDI uint32_t icnt_path(const SimCfg& c, uint32_t a, uint32_t b, uint32_t* L)
       }
       for (uint32_t l = 0; l + 1 < lvl; ++l) {
         const uint64_t pl = ipow(k, l);
-        L[m++] = (uint32_t)((uint64_t)l * kn + (a / (pl * k)) * k + (b / pl) % k);
+        emit((uint32_t)((uint64_t)l * kn + (a / (pl * k)) * k + (b / pl) % k));
+        ++m;
       }
       for (uint32_t l = lvl - 1; l-- > 0;) {
         const uint64_t pl = ipow(k, l);
-        L[m++] = (uint32_t)((uint64_t)n * kn + (uint64_t)l * kn + (b / (pl * k)) * k + (b / pl) % k);
+        emit((uint32_t)((uint64_t)n * kn + (uint64_t)l * kn + (b / (pl * k)) * k + (b / pl) % k));
+        ++m;
       }
-      L[m++] = (uint32_t)(2ull * n * kn + b % kn);
+      emit((uint32_t)(2ull * n * kn + b % kn));
+        ++m;
       return m;
     }
     default: {  // flattened butterfly: one hop per differing dimension
@@ -128,10 +137,12 @@ SIM_HDI uint32_t icnt_path(const SimCfg& c, uint32_t a, uint32_t b, uint32_t* L)
       for (uint32_t d = 0; d < n; ++d, pw *= k) {
         const uint32_t x = (uint32_t)((cur / pw) % k), y = (uint32_t)((b / pw) % k);
         if (x == y) continue;
-        L[m++] = (uint32_t)(cur * P + d * k + y);
+        emit((uint32_t)(cur * P + d * k + y));
+        ++m;
         cur = cur - (uint64_t)x * pw + (uint64_t)y * pw;
       }
-      L[m++] = (uint32_t)(cur * P + n * k);
+      emit((uint32_t)(cur * P + n * k));
+        ++m;
       return m;
     }
   }
@@ -140,24 +151,25 @@ SIM_HDI uint32_t icnt_path(const SimCfg& c, uint32_t a, uint32_t b, uint32_t* L)
 // reserve the route of one packet (a -> b, uncontended arrival p.t) and
 // return its extra delay (fs)
 SIM_HDI uint64_t icnt_reserve(const SimCfg& c, Pkt& p, uint32_t a, uint32_t b, uint64_t* link_free) {
-  uint32_t L[kMaxPathLinks];
-  const uint32_t nl = icnt_path(c, a, b, L);
+  const uint32_t nl = icnt_routers(c, a, b);  // one link per router crossed (icnt_route)
   const uint64_t nflits = (p.size + c.flit_size - 1) / c.flit_size;
   const uint64_t occ = (nflits ? nflits : 1) * c.per_icnt;
   const uint64_t hop = ((uint64_t)c.hop_icnt + c.chan_icnt) * c.per_icnt, last = (uint64_t)c.chan_icnt * c.per_icnt;
   uint64_t D = 0;
-  for (uint32_t h = 0; h < nl; ++h) {
+  uint32_t h = 0;
+  icnt_route(c, a, b, [&](uint32_t l) {
     // uncontended departure onto link h (the route's schedule ends at p.t)
-    const uint64_t back = (uint64_t)(nl - 1 - h) * hop + last;
+    const uint64_t back = (uint64_t)(nl - 1 - (h < nl ? h : nl - 1)) * hop + last;
     const uint64_t d = p.t > back ? p.t - back : 0;
     uint64_t t = d + D;
-    const uint64_t f = link_free[L[h]];
+    const uint64_t f = link_free[l];
     if (f > t) {
       D += f - t;
       t = f;
     }
-    link_free[L[h]] = t + occ;
-  }
+    link_free[l] = t + occ;
+    ++h;
+  });
   p.t += D;
   return D;
 }
