@@ -562,6 +562,7 @@ def main(argv=None) -> int:
         s = refit(o.refit, o.out_xml, o.config_dir)
     elif o.traces and o.heldout:
         s = run_heldout(o.traces, o.measured or MEASURED, work, o.out_xml, o.config_dir, engine=o.engine)
+    if "calibration_kernels" in s:  # held-out record (run_heldout, or a refit of one)
         with open(o.json, "w") as f:
             json.dump(s, f, indent=1)
         print(f"{'kernel':16s} {'set':4s} {'measured':>9s} {'uncal':>9s} {'model':>9s}")
@@ -574,6 +575,8 @@ def main(argv=None) -> int:
         print("group factors:", {g: round(v, 3) for g, v in s["group_factors"].items()}, "at bound:",
               s["factors_at_bound"], "not driven:", s["groups_not_driven"])
         return 0
+    if o.refit:
+        pass
     elif o.traces:
         s = run_traces(o.traces, o.measured or MEASURED, work, o.out_xml, o.config_dir, engine=o.engine)
     else:

@@ -62,6 +62,12 @@ def default_params(preset: str) -> Dict[str, float]:
         # architectural energy model inputs (energy_model = 1, csrc/power/arch_energy.cc):
         # N3-class compute dies, HBM3E, MFMA 16x16x32 = 128 MACs per lane
         p.update(core_tech_node=3.0, dram_pj_per_bit=2.5, tensor_macs_per_lane=128.0)
+        # CDNA transcendentals (v_sqrt / v_log / v_sin / v_exp) run on the VALU
+        # at a quarter of the FMA rate: per lane they cost about an FMA, not
+        # the 4x of a separate SFU the base table assumes (power suite, round 4:
+        # held-out MAPE 15.3 -> 14.6 %, integer factor 0.37 -> 1.01)
+        for a in ("FP_SQRT_ACC", "FP_LG_ACC", "FP_SIN_ACC", "FP_EXP_ACC"):
+            p[a] = 0.25
     else:
         # 250 W class Volta/Turing/Ampere boards, 80-ish SMs
         p.update(constant_power=32.0, idle_core_power=0.28)
