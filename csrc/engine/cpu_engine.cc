@@ -154,8 +154,8 @@ class CpuEngine : public Engine {
     link_free_.clear();
     link_refs_.clear();
     link_stat_[0] = link_stat_[1] = 0;
-    if (c.link_contention && icnt_link_count(c) > kMaxIcntLinks)
-      throw std::runtime_error("-icnt_link_contention: topology has too many links");
+    if (c.link_contention && (icnt_link_count(c) > kMaxIcntLinks || !icnt_contention_fits(c, cap_req_, cap_rep_)))
+      throw std::runtime_error("-icnt_link_contention: topology or mailboxes too large for the link pass");
     if (icnt_contention_on(c)) {
       link_free_.assign((size_t)icnt_link_count(c), 0);
       link_refs_.assign((size_t)c.n_sm * c.n_subpart * std::max(cap_req_, cap_rep_), 0);

@@ -680,8 +680,8 @@ class GpuEngine : public Engine {
       HIPCHECK(hipMalloc(&d_mall_, sizeof(L2Line) * n_mall_));
       HIPCHECK(hipMemset(d_mall_, 0, sizeof(L2Line) * n_mall_));
     }
-    if (c.link_contention && icnt_link_count(c) > kMaxIcntLinks)
-      throw std::runtime_error("-icnt_link_contention: topology has too many links");
+    if (c.link_contention && (icnt_link_count(c) > kMaxIcntLinks || !icnt_contention_fits(c, cap_req_, cap_rep_)))
+      throw std::runtime_error("-icnt_link_contention: topology or mailboxes too large for the link pass");
     n_links_ = icnt_contention_on(c) ? (size_t)icnt_link_count(c) : 0;
     if (n_links_) {
       HIPCHECK(hipMalloc(&d_links_, sizeof(uint64_t) * (n_links_ + 2)));

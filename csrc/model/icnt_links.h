@@ -52,6 +52,9 @@ SIM_HDI uint64_t icnt_link_count(const SimCfg& c) {
   }
 }
 
+SIM_HDI bool icnt_contention_fits(const SimCfg& c, uint32_t cap_req, uint32_t cap_rep) {
+  return (uint64_t)c.n_sm * c.n_subpart <= 65536u && cap_req < 65536u && cap_rep < 65536u;
+}
 SIM_HDI bool icnt_contention_on(const SimCfg& c) {
   const uint64_t n = icnt_link_count(c);
   return c.link_contention && n > 0 && n <= kMaxIcntLinks;
@@ -176,7 +179,9 @@ SIM_HDI uint64_t icnt_reserve(const SimCfg& c, Pkt& p, uint32_t a, uint32_t b, u
 
 // the epoch-boundary pass over this epoch's outboxes (requests [sub][sm][cap],
 // replies [sm][sub][cap]); `refs` holds up to every cell x cap entries, stat
-// accumulates {delayed packets, delay in interconnect cycles}
+// accumulates {delayed packets, delay in interconnect cycles}; a packet's
+// reference is (cell << 16 | index): cells and cell capacities < 2^16
+// (icnt_contention_fits)
 template <class P>
 SIM_HDI void icnt_contend(const SimCfg& c, Pkt* box_req, const uint32_t* cnt_req, uint32_t cap_req, Pkt* box_rep,
                           const uint32_t* cnt_rep, uint32_t cap_rep, uint64_t* link_free, uint32_t* refs,
@@ -188,14 +193,14 @@ SIM_HDI void icnt_contend(const SimCfg& c, Pkt* box_req, const uint32_t* cnt_req
     // every packet of the epoch in cell order: (cell << 8 | index in the cell)
     const uint32_t total = P::scan((int)ncell, [&](int i) -> uint32_t { return cnt[i]; },
                                    [&](int i, uint32_t off) {
-                                     for (uint32_t j = 0; j < cnt[i]; ++j) refs[off + j] = (uint32_t)i << 8 | j;
+                                     for (uint32_t j = 0; j < cnt[i]; ++j) refs[off + j] = (uint32_t)i << 16 | j;
                                    });
     P::sync();
     if (total == 0) continue;
     P::one([&] {
       uint64_t delayed = 0, wait = 0;
       for (uint32_t r = 0; r < total; ++r) {
-        const uint32_t cell = refs[r] >> 8, j = refs[r] & 0xffu;
+        const uint32_t cell = refs[r] >> 16, j = refs[r] & 0xffffu;
         uint32_t a, b;
         Pkt* p;
         if (dir == 0) {  // request: SM (cell % n_sm) -> sub-partition (cell / n_sm)
