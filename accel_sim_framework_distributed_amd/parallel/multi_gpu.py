@@ -152,8 +152,20 @@ class DistributedSuite:
             q = self.cgroup_cores()
             if q:
                 n = min(n, q)
-            n //= max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+            # one GPU's share of the node: a rank gets the same cores whether
+            # its node runs 1 rank or one per visible GPU (weak scaling keeps
+            # the per-GPU resources fixed)
+            n //= max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")), self.visible_gpus())
         return max(1, n - reserve)
+
+    @staticmethod
+    def visible_gpus() -> int:
+        """GPUs this process can see (device count only: no HIP context)."""
+        try:
+            import torch
+            return int(torch.cuda.device_count())
+        except Exception:  # pragma: no cover - torch is optional for the CPU engine
+            return 0
 
     @staticmethod
     def cgroup_cores() -> int:

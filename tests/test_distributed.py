@@ -382,3 +382,19 @@ def test_native_exchange_loop_matches_python_loop_eight_ranks(native):
     ref = [collectives.emulate(PARAMS, k, b, s)["finish_ps"] for k, b, s in cases]
     for i in range(len(cases)):
         assert [res[r][1]["1"][0][i] for r in range(8)] == ref[i]
+
+
+def test_cpu_share_is_one_gpus_share(monkeypatch):
+    """A rank's host cores are one GPU's share of the node whether the node
+    runs one rank or one per visible GPU (weak scaling keeps per-GPU
+    resources fixed)."""
+    from accel_sim_framework_distributed_amd.parallel import multi_gpu
+    cls = next(v for v in vars(multi_gpu).values() if isinstance(v, type) and hasattr(v, "cpu_slots"))
+    obj = cls.__new__(cls)
+    monkeypatch.setenv("ASIM_CPU_JOBS", "0")
+    monkeypatch.setattr(cls, "cgroup_cores", staticmethod(lambda: 64))
+    monkeypatch.setattr(multi_gpu.os, "sched_getaffinity", lambda _: set(range(64)))
+    for lws, gpus, want in (("1", 1, 64), ("1", 8, 8), ("8", 8, 8), ("4", 8, 8), ("2", 0, 32)):
+        monkeypatch.setenv("LOCAL_WORLD_SIZE", lws)
+        monkeypatch.setattr(cls, "visible_gpus", staticmethod(lambda g=gpus: g))
+        assert obj.cpu_slots() == want, (lws, gpus)
