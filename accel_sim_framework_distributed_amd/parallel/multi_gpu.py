@@ -337,14 +337,21 @@ class DistributedSuite:
         tried = set()
         self._calibrating = True
         try:
-            for _ in range(12):
+            for _ in range(16):
                 self.plan()
                 cpu_apps = [a for a, e in self.assignment.items() if e == "cpu"]
-                if not cpu_apps:
-                    break
-                crit = max(cpu_apps, key=lambda a: self.times[(a, "cpu")])
-                if self.times[(crit, "cpu")] < 0.999 * self.predicted_span or crit in tried:
-                    break  # the GPU side sets the span, or the critical app does not scale
+                gpu_apps = [a for a, e in self.assignment.items() if e == "gpu"]
+                crit = max(cpu_apps, key=lambda a: self.times[(a, "cpu")]) if cpu_apps else None
+                if crit is None or self.times[(crit, "cpu")] < 0.999 * self.predicted_span:
+                    # the GPU side sets the span: offer its longest application
+                    # a wider host thread team (the plan moves it if that wins)
+                    cand = [a for a in gpu_apps if a not in tried]
+                    if not cand:
+                        break
+                    crit = max(cand, key=lambda a: self.times[(a, "gpu")])
+                    cpu_apps = cpu_apps + [crit]
+                if crit in tried:
+                    break  # the critical app does not scale
                 k = self.threads.get(crit, 1)
                 nk = min(max_threads, 2 * k)
                 used = sum(self.threads.get(a, 1) for a in cpu_apps if a != crit)

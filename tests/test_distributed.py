@@ -398,3 +398,39 @@ def test_cpu_share_is_one_gpus_share(monkeypatch):
         monkeypatch.setenv("LOCAL_WORLD_SIZE", lws)
         monkeypatch.setattr(cls, "visible_gpus", staticmethod(lambda g=gpus: g))
         assert obj.cpu_slots() == want, (lws, gpus)
+
+
+def test_node_widen_offers_threads_to_the_gpu_critical_app(monkeypatch):
+    """When the GPU side sets the node's span, its longest application is
+    re-timed on a wider host thread team, and the plan moves it if that
+    shortens the step (measured MI355X calibration times, round 4)."""
+    from accel_sim_framework_distributed_amd.parallel import multi_gpu
+    S = multi_gpu.DistributedSuite
+    obj = S.__new__(S)
+    cal = {"backprop": (0.0714, 0.1392), "bfs": (0.6649, 0.138), "heartwall": (0.2358, 0.1668),
+           "hotspot": (0.164, 0.4031), "lud": (0.099, 0.0164), "nn": (0.0097, 0.0223), "nw": (0.207, 0.0294),
+           "pathfinder": (0.037, 0.0093), "srad": (0.0355, 0.03), "streamcluster": (0.446, 0.0547),
+           "dp-step": (0.1842, 0.1608)}
+    dense = {"hotspot": 0.9, "dp-step": 0.85, "heartwall": 0.6, "backprop": 0.5}
+    obj.apps = [(a, a) for a in cal]
+    obj.times = {}
+    for a, (g, c) in cal.items():
+        obj.times[(a, "gpu")], obj.times[(a, "cpu")] = g, c
+    obj.threads = {}
+    obj._calibrating = False
+    monkeypatch.setattr(S, "concurrency", lambda self: 2)
+    monkeypatch.setattr(S, "cpu_slots", lambda self, reserve=0: 14)
+
+    def run_app(self, app_kl, engine=None):  # thread-team scaling of the CPU engine
+        a = app_kl[0]
+        k = self.threads.get(a, 1)
+        self.times[(a, engine)] = cal[a][1] / (k ** dense.get(a, 0.0))
+    monkeypatch.setattr(S, "_run_app", run_app)
+    obj.plan()
+    before = obj.predicted_span
+    assert obj.assignment["hotspot"] == "gpu"
+    obj.widen()
+    assert obj.predicted_span < 0.9 * before
+    # the GPU keeps the applications it runs fastest
+    assert sum(e == "gpu" for e in obj.assignment.values()) >= 3
+    assert sum(obj.threads.get(a, 1) for a, e in obj.assignment.items() if e == "cpu") <= 14
