@@ -150,6 +150,27 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
                              f"cycles against the measured {target}")
         except (ValueError, RuntimeError) as e:
             notes.append(f"launch self-consistency skipped: {e}")
+    # vector-L1 data path: ub_bw_widths measured the L1-hit bandwidth of 32 /
+    # 64 / 128-bit loads; the simulated twin of that loop is run with each
+    # candidate -sim_l1_port_bytes and the best fit kept (0 = the reference's
+    # banked L1 without a data-path limit)
+    l1bw = measured_l1_bandwidth(stats_paths)
+    if l1bw:
+        try:
+            fits = {}
+            for port in (0, 32, 48, 64, 96):
+                simbw = simulated_l1_bandwidth(out, port, sorted(l1bw))
+                fits[port] = sum(abs(simbw[w] / l1bw[w] - 1.0) for w in l1bw) / len(l1bw)
+            best = min(fits, key=fits.get)
+            cfg["-sim_l1_port_bytes"] = str(best)
+            applied["-sim_l1_port_bytes"] = str(best)
+            presets.write_config(cfg, out, power_preset=base)
+            notes.append("-sim_l1_port_bytes " + str(best) + ": simulated L1-hit bandwidth of the ub_bw_widths loop "
+                         "closest to the measured " + ", ".join(f"{8 * w}b {l1bw[w]:.1f}" for w in sorted(l1bw)) +
+                         " B/clk/CU (mean error per candidate: " +
+                         ", ".join(f"{p} {100 * e:.0f} %" for p, e in fits.items()) + ")")
+        except (ValueError, RuntimeError) as e:
+            notes.append(f"L1 data-path fit skipped: {e}")
     with open(os.path.join(out, "TUNING.md"), "w") as f:
         f.write(f"# Tuned configuration for {device}\n\nBase preset: {base}\n\n")
         f.write("| option | tuned value | preset value |\n|---|---|---|\n")
@@ -163,6 +184,64 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
             for k in sorted(meas):
                 f.write(f"- {k}: {meas[k]}\n")
     return out, applied
+
+
+def measured_l1_bandwidth(stats_paths: List[str]) -> Dict[int, float]:
+    """{bytes per lane: B/clk/CU} from ub_bw_widths' 'l1_bw 32b X 64b Y 128b Z' line."""
+    out: Dict[int, float] = {}
+    for p in stats_paths:
+        files = [p] if os.path.isfile(p) else [os.path.join(p, f) for f in sorted(os.listdir(p))] if os.path.isdir(p) else []
+        for fn in files:
+            try:
+                lines = open(fn).read().splitlines()
+            except (OSError, UnicodeDecodeError):
+                continue
+            for line in lines:
+                t = line.split()
+                if t and t[0] == "l1_bw":
+                    for i in range(1, len(t) - 1, 2):
+                        if t[i].endswith("b") and t[i][:-1].isdigit():
+                            out[int(t[i][:-1]) // 8] = float(t[i + 1])
+    return out
+
+
+def simulated_l1_bandwidth(config_dir: str, port: int, widths=(4, 8, 16), per_cu: int = 4,
+                           iters: int = 32) -> Dict[int, float]:
+    """L1-hit bandwidth (B/clk/CU) the simulator gives ub_bw_widths' loop: every
+    CU runs `per_cu` 256-thread workgroups whose waves load the same few KB
+    `iters` times with independent destinations."""
+    import tempfile
+    from .. import _native
+    from ..tracegen import rodinia
+    from ..tracegen.builder import KernelBuilder
+    cfg = {}
+    for fn in ("gpgpusim.config", "trace.config"):
+        for line in open(os.path.join(config_dir, fn)):
+            t = line.split()
+            if len(t) >= 2 and t[0].startswith("-"):
+                cfg[t[0]] = t[1]
+    ws = int(cfg.get("-gpgpu_shader_core_pipeline", "2048:32").split(":")[1])
+    n_cu = int(cfg.get("-gpgpu_n_clusters", "80")) * int(cfg.get("-gpgpu_n_cores_per_cluster", "1"))
+    ops = {4: "global_load_dword", 8: "global_load_dwordx2", 16: "global_load_dwordx4"} if ws == 64 else \
+        {4: "LDG.E", 8: "LDG.E.64", 16: "LDG.E.128"}
+    d = tempfile.mkdtemp(prefix="asim_l1bw_")
+    out = {}
+    for w in widths:
+        k = KernelBuilder("ub_l1_bw", (n_cu * per_cu, 1, 1), (256, 1, 1), nregs=64,
+                          binary_version=950 if ws == 64 else 70, warp_size=ws)
+        g = k.g
+        base = 0x7000_0000 + g.cta * 0x10000 + g.warp * ws * w
+        for it in range(iters):
+            k.op(ops[w], [8 + (it % 16)], [2], base=base, stride=w)
+        k.op("s_endpgm" if ws == 64 else "EXIT")
+        kl = rodinia.write_app(os.path.join(d, f"w{w}"), [k.build()], memcpy=False)
+        args = ["-config", os.path.join(config_dir, "gpgpusim.config"), "-config",
+                os.path.join(config_dir, "trace.config"), "-sim_l1_port_bytes", str(port), "-trace", kl]
+        s = _native.load().Simulator(args, False)
+        if s.run() != 0:
+            raise RuntimeError("L1 bandwidth simulation failed")
+        out[w] = g.nwarps * iters * ws * w / max(1, s.tot_cycle) / n_cu
+    return out
 
 
 def simulated_empty_kernel_cycles(config_dir: str) -> int:

@@ -165,6 +165,11 @@ struct SimCfg {
   CacheGeom l1;
   uint32_t l1_latency;
   uint32_t l1_banks;
+  // L1 data path throughput (0 = off, the reference's banked L1: l1_banks
+  // accesses per cycle): a global / local instruction occupies the vector
+  // L1's address stage ceil(active lanes / l1_addr_lanes) cycles, each access
+  // its data stage ceil(bytes / l1_port_bytes) cycles (gfx950 TA / TD)
+  uint32_t l1_port_bytes, l1_addr_lanes;
   uint32_t gmem_skip_l1;
   uint32_t adaptive_l1;
   uint32_t unified_l1_kb;

@@ -97,6 +97,8 @@ struct LdstState {
   uint8_t slot;
   uint8_t next;       // next access index
   uint32_t start;     // cycle the instruction entered the unit (low 32 bits)
+  uint32_t port_free; // -sim_l1_port_bytes: first cycle the L1 data path is free again (low 32 bits)
+  uint32_t pad;
 };
 
 // statistics counters of one SM (reduced on the host)
@@ -911,10 +913,13 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
   const uint8_t uslot = P::uni(u.slot);
   // access records were brought into the unit at dispatch
   P::fetch_wait();
+  const bool port = c.l1_port_bytes && in.space != S_CONST;
   while (unext < nacc && processed < c.l1_banks) {
     const TAcc a = P::uni(s.ldst_acc[unext]);
     uint32_t bbit = 1u << (a.bank & 31);
     if (banks_used & bbit) break;  // L1 bank conflict: next cycle
+    // L1 data path busy (-sim_l1_port_bytes): the access waits
+    if (port && (int32_t)(P::uni(u.port_free) - (uint32_t)now) > 0) break;
     if (c.perfect_mem) {
       // ideal memory: loads/atomics return after the L1 latency, stores retire at once
       if (!is_store) {
@@ -1079,6 +1084,13 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
     }
     if (in.space != S_CONST)
       s.sadd(SK(l1_lookups64), (uint32_t)((a.sectors & 3u) != 0) + (uint32_t)((a.sectors & 12u) != 0));
+    if (port) {
+      // the access's bytes cross the data path (hit data, store data, or the
+      // miss's fill later: charged here, once per access)
+      const uint32_t pf = P::uni(u.port_free);
+      const uint32_t from = (int32_t)(pf - (uint32_t)now) > 0 ? pf : (uint32_t)now;
+      u.port_free = from + ((uint32_t)(a.bytes ? a.bytes : 1u) + c.l1_port_bytes - 1) / c.l1_port_bytes;
+    }
     banks_used |= bbit;
     unext++;
     u.next = (uint8_t)unext;
@@ -1180,6 +1192,13 @@ SIM_HDI void sm_dispatch(S& s, const SmCtx& x, uint64_t now) {
       s.ldst.slot = (uint8_t)((info >> 24) & 0xffu);  // load slot allocated at issue
       s.ldst.next = 0;
       s.ldst.start = (uint32_t)now;
+      if (c.l1_addr_lanes && li.space != S_SHARED && li.space != S_CONST && li.width) {
+        // the address stage takes the instruction's active lanes at
+        // l1_addr_lanes per cycle before its first access reaches the data path
+        const uint32_t pf = P::uni(s.ldst.port_free);
+        const uint32_t from = (int32_t)(pf - (uint32_t)now) > 0 ? pf : (uint32_t)now;
+        s.ldst.port_free = from + ((uint32_t)popc64(li.mask) + c.l1_addr_lanes - 1) / c.l1_addr_lanes;
+      }
       s.sadd(SK(mem_insn), 1);
       s.oc_mask &= ~(1u << best);
       continue;
