@@ -154,23 +154,30 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
     # 64 / 128-bit loads; the simulated twin of that loop is run with each
     # candidate -sim_l1_port_bytes and the best fit kept (0 = the reference's
     # banked L1 without a data-path limit)
-    l1bw = measured_l1_bandwidth(stats_paths)
-    if l1bw:
+    for lds in (False, True):
+        meas_bw = measured_l1_bandwidth(stats_paths, "lds_bw" if lds else "l1_bw")
+        if not meas_bw:
+            continue
         try:
+            port_opt, lane_opt = ("-sim_lds_port_bytes", "-sim_lds_lanes_per_cycle") if lds else \
+                ("-sim_l1_port_bytes", "-sim_l1_addr_lanes_per_cycle")
             fits = {}
-            for port in (0, 32, 48, 64, 96):
-                simbw = simulated_l1_bandwidth(out, port, sorted(l1bw))
-                fits[port] = sum(abs(simbw[w] / l1bw[w] - 1.0) for w in l1bw) / len(l1bw)
-            best = min(fits, key=fits.get)
-            cfg["-sim_l1_port_bytes"] = str(best)
-            applied["-sim_l1_port_bytes"] = str(best)
+            for port in ((64, 128, 256) if lds else (16, 32, 48, 64)):
+                for lanes in ((0, 8, 12, 16, 32) if lds else (0, 16, 32)):
+                    simbw = simulated_l1_bandwidth(out, port, sorted(meas_bw), lds=lds, lanes=lanes)
+                    fits[(port, lanes)] = sum(abs(simbw[w] / meas_bw[w] - 1.0) for w in meas_bw) / len(meas_bw)
+            nolimit = simulated_l1_bandwidth(out, 0, sorted(meas_bw), lds=lds)
+            err0 = sum(abs(nolimit[w] / meas_bw[w] - 1.0) for w in meas_bw) / len(meas_bw)
+            (port, lanes) = min(fits, key=fits.get)
+            cfg[port_opt], cfg[lane_opt] = str(port), str(lanes)
+            applied[port_opt], applied[lane_opt] = str(port), str(lanes)
             presets.write_config(cfg, out, power_preset=base)
-            notes.append("-sim_l1_port_bytes " + str(best) + ": simulated L1-hit bandwidth of the ub_bw_widths loop "
-                         "closest to the measured " + ", ".join(f"{8 * w}b {l1bw[w]:.1f}" for w in sorted(l1bw)) +
-                         " B/clk/CU (mean error per candidate: " +
-                         ", ".join(f"{p} {100 * e:.0f} %" for p, e in fits.items()) + ")")
+            notes.append(f"{port_opt} {port}, {lane_opt} {lanes}: steady-state simulated bandwidth of the "
+                         f"ub_bw_widths {'LDS' if lds else 'L1-hit'} loop closest to the measured " +
+                         ", ".join(f"{8 * w}b {meas_bw[w]:.1f}" for w in sorted(meas_bw)) +
+                         f" B/clk/CU: mean error {100 * fits[(port, lanes)]:.0f} % (no limit: {100 * err0:.0f} %)")
         except (ValueError, RuntimeError) as e:
-            notes.append(f"L1 data-path fit skipped: {e}")
+            notes.append(f"{'LDS' if lds else 'L1'} data-path fit skipped: {e}")
     with open(os.path.join(out, "TUNING.md"), "w") as f:
         f.write(f"# Tuned configuration for {device}\n\nBase preset: {base}\n\n")
         f.write("| option | tuned value | preset value |\n|---|---|---|\n")
@@ -186,8 +193,9 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
     return out, applied
 
 
-def measured_l1_bandwidth(stats_paths: List[str]) -> Dict[int, float]:
-    """{bytes per lane: B/clk/CU} from ub_bw_widths' 'l1_bw 32b X 64b Y 128b Z' line."""
+def measured_l1_bandwidth(stats_paths: List[str], key: str = "l1_bw") -> Dict[int, float]:
+    """{bytes per lane: B/clk/CU} from ub_bw_widths' '<key> 32b X 64b Y 128b Z' line
+    (key: l1_bw, l2_bw or lds_bw)."""
     out: Dict[int, float] = {}
     for p in stats_paths:
         files = [p] if os.path.isfile(p) else [os.path.join(p, f) for f in sorted(os.listdir(p))] if os.path.isdir(p) else []
@@ -198,7 +206,7 @@ def measured_l1_bandwidth(stats_paths: List[str]) -> Dict[int, float]:
                 continue
             for line in lines:
                 t = line.split()
-                if t and t[0] == "l1_bw":
+                if t and t[0] == key:
                     for i in range(1, len(t) - 1, 2):
                         if t[i].endswith("b") and t[i][:-1].isdigit():
                             out[int(t[i][:-1]) // 8] = float(t[i + 1])
@@ -206,10 +214,12 @@ def measured_l1_bandwidth(stats_paths: List[str]) -> Dict[int, float]:
 
 
 def simulated_l1_bandwidth(config_dir: str, port: int, widths=(4, 8, 16), per_cu: int = 4,
-                           iters: int = 32) -> Dict[int, float]:
-    """L1-hit bandwidth (B/clk/CU) the simulator gives ub_bw_widths' loop: every
-    CU runs `per_cu` 256-thread workgroups whose waves load the same few KB
-    `iters` times with independent destinations."""
+                           iters: int = 32, lds: bool = False, lanes: int = 0) -> Dict[int, float]:
+    """Steady-state bandwidth (B/clk/CU) the simulator gives ub_bw_widths'
+    loop: every CU runs `per_cu` 256-thread workgroups whose waves load the
+    same few KB with independent destinations, once `iters` and once
+    2 x `iters` times; the difference removes the launch and drain cycles.
+    `lds`: the LDS variant (ds_read, -sim_lds_port_bytes = port)."""
     import tempfile
     from .. import _native
     from ..tracegen import rodinia
@@ -222,25 +232,35 @@ def simulated_l1_bandwidth(config_dir: str, port: int, widths=(4, 8, 16), per_cu
                 cfg[t[0]] = t[1]
     ws = int(cfg.get("-gpgpu_shader_core_pipeline", "2048:32").split(":")[1])
     n_cu = int(cfg.get("-gpgpu_n_clusters", "80")) * int(cfg.get("-gpgpu_n_cores_per_cluster", "1"))
-    ops = {4: "global_load_dword", 8: "global_load_dwordx2", 16: "global_load_dwordx4"} if ws == 64 else \
-        {4: "LDG.E", 8: "LDG.E.64", 16: "LDG.E.128"}
+    if lds:
+        ops = {4: "ds_read_b32", 8: "ds_read_b64", 16: "ds_read_b128"} if ws == 64 else \
+            {4: "LDS", 8: "LDS.64", 16: "LDS.128"}
+    else:
+        ops = {4: "global_load_dword", 8: "global_load_dwordx2", 16: "global_load_dwordx4"} if ws == 64 else \
+            {4: "LDG.E", 8: "LDG.E.64", 16: "LDG.E.128"}
+    opt = "-sim_lds_port_bytes" if lds else "-sim_l1_port_bytes"
+    lopt = "-sim_lds_lanes_per_cycle" if lds else "-sim_l1_addr_lanes_per_cycle"
     d = tempfile.mkdtemp(prefix="asim_l1bw_")
     out = {}
     for w in widths:
-        k = KernelBuilder("ub_l1_bw", (n_cu * per_cu, 1, 1), (256, 1, 1), nregs=64,
-                          binary_version=950 if ws == 64 else 70, warp_size=ws)
-        g = k.g
-        base = 0x7000_0000 + g.cta * 0x10000 + g.warp * ws * w
-        for it in range(iters):
-            k.op(ops[w], [8 + (it % 16)], [2], base=base, stride=w)
-        k.op("s_endpgm" if ws == 64 else "EXIT")
-        kl = rodinia.write_app(os.path.join(d, f"w{w}"), [k.build()], memcpy=False)
-        args = ["-config", os.path.join(config_dir, "gpgpusim.config"), "-config",
-                os.path.join(config_dir, "trace.config"), "-sim_l1_port_bytes", str(port), "-trace", kl]
-        s = _native.load().Simulator(args, False)
-        if s.run() != 0:
-            raise RuntimeError("L1 bandwidth simulation failed")
-        out[w] = g.nwarps * iters * ws * w / max(1, s.tot_cycle) / n_cu
+        cyc, byts = [], []
+        for n in (iters, 2 * iters):
+            k = KernelBuilder("ub_l1_bw", (n_cu * per_cu, 1, 1), (256, 1, 1), nregs=64, shmem=16384 if lds else 0,
+                              binary_version=950 if ws == 64 else 70, warp_size=ws)
+            g = k.g
+            base = ((g.warp % 4) * ws * w) if lds else (0x7000_0000 + g.cta * 0x10000 + g.warp * ws * w)
+            for it in range(n):
+                k.op(ops[w], [8 + (it % 16)], [2], base=base, stride=w)
+            k.op("s_endpgm" if ws == 64 else "EXIT")
+            kl = rodinia.write_app(os.path.join(d, f"w{w}n{n}"), [k.build()], memcpy=False)
+            args = ["-config", os.path.join(config_dir, "gpgpusim.config"), "-config",
+                    os.path.join(config_dir, "trace.config"), opt, str(port), lopt, str(lanes), "-trace", kl]
+            s = _native.load().Simulator(args, False)
+            if s.run() != 0:
+                raise RuntimeError("bandwidth simulation failed")
+            cyc.append(s.tot_cycle)
+            byts.append(g.nwarps * n * ws * w)
+        out[w] = (byts[1] - byts[0]) / max(1, cyc[1] - cyc[0]) / n_cu
     return out
 
 

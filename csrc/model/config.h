@@ -170,6 +170,10 @@ struct SimCfg {
   // L1's address stage ceil(active lanes / l1_addr_lanes) cycles, each access
   // its data stage ceil(bytes / l1_port_bytes) cycles (gfx950 TA / TD)
   uint32_t l1_port_bytes, l1_addr_lanes;
+  // LDS data path (0 = off: an LDS instruction takes its bank-conflict degree
+  // in cycles): at least ceil(active lanes x bytes / lds_port_bytes) cycles,
+  // computed at ingest into the instruction's initiation interval
+  uint32_t lds_port_bytes, lds_lanes;  // lds_lanes: address lanes per cycle (0: no limit)
   uint32_t gmem_skip_l1;
   uint32_t adaptive_l1;
   uint32_t unified_l1_kb;

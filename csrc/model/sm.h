@@ -890,13 +890,16 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
   const TInst in = P::uni(u.inst);
   const uint32_t w = P::uni(u.warp);
   if (in.space == S_SHARED) {
-    // bank-conflict serialisation: nacc == conflict degree (precomputed)
-    uint32_t deg = in.width ? in.width : 1;
+    // bank-conflict serialisation: nacc == conflict degree (precomputed);
+    // with -sim_lds_port_bytes the data path's cycles (ii, set at ingest)
+    // bound it from below
+    const uint32_t cdeg = in.width ? in.width : 1;
+    const uint32_t deg = (c.lds_port_bytes && in.ii > cdeg) ? (uint32_t)in.ii : cdeg;
     if ((uint32_t)(now - P::uni(u.start)) + 1 < deg) return;
     uint8_t kind = (in.cls == OC_STORE) ? 1 : 0;
     if (!hit_push(s, now + c.smem_latency, (uint8_t)w, P::uni(u.slot), kind)) return;
     s.sadd(SK(shmem_acc), 1);
-    s.sadd(SK(shmem_conflict_cycles), deg - 1);
+    s.sadd(SK(shmem_conflict_cycles), cdeg - 1);
     u.busy = 0;
     return;
   }

@@ -1394,6 +1394,17 @@ IngestKind ingest_prepare(TInst& in, const SimCfg& c) {
     if (in.cls == OC_LOAD || in.cls == OC_STORE) in.width = 1;
     return IK_DONE;
   }
+  if (in.space == S_SHARED && c.lds_port_bytes) {
+    // LDS data path: the active lanes' bytes at lds_port_bytes per cycle, and
+    // their addresses at lds_lanes per cycle (overlapped: the slower one
+    // sets the pace; the LD/ST unit holds the instruction max(conflict
+    // degree, this) cycles)
+    const uint32_t lanes = (uint32_t)__builtin_popcountll(in.mask);
+    const uint32_t bytes = lanes * (in.width ? in.width : 4u);
+    uint32_t cyc = (bytes + c.lds_port_bytes - 1) / c.lds_port_bytes;
+    if (c.lds_lanes) cyc = std::max<uint32_t>(cyc, (lanes + c.lds_lanes - 1) / c.lds_lanes);
+    in.ii = (uint8_t)std::min<uint32_t>(255, std::max<uint32_t>(1, cyc));
+  }
   return in.space == S_SHARED ? IK_SMEM : IK_GMEM;
 }
 
