@@ -103,6 +103,12 @@ def test_memlatency_and_visualizer(native, traces, tmp_path, monkeypatch):
     out = tmp_path / "v.html"
     assert visualizer.main([str(tmp_path / "gpgpusim_visualizer.log"), "-o", str(out)]) == 0
     assert out.stat().st_size > 1000
+    # gzip logs (the reference's AerialVision input is gzipped) read the same
+    import gzip
+    gz = tmp_path / "v.log.gz"
+    with gzip.open(gz, "wt") as f:
+        f.write(open(tmp_path / "gpgpusim_visualizer.log").read())
+    assert visualizer.parse(str(gz)) == rows
 
 
 def test_pipeline_dump(native, traces):
