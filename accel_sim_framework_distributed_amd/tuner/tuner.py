@@ -25,7 +25,7 @@ import itertools
 import os
 import re
 import sys
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 if __package__ in (None, ""):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
@@ -150,6 +150,15 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
                              f"cycles against the measured {target}")
         except (ValueError, RuntimeError) as e:
             notes.append(f"launch self-consistency skipped: {e}")
+    # dependent-chain latencies: ub_alu / ub_lds time one wave's dependent
+    # chain, i.e. issue + operand read + execute + writeback; the simulator's
+    # pipeline adds its own issue / collector / writeback stages on top of the
+    # configured latency, so each latency is lowered until the simulated twin
+    # of the same chain lasts what the hardware measured
+    try:
+        notes += _latency_self_consistency(out, cfg, applied, base)
+    except (ValueError, RuntimeError, OSError) as e:
+        notes.append(f"latency self-consistency skipped: {e}")
     # vector-L1 data path: ub_bw_widths measured the L1-hit bandwidth of 32 /
     # 64 / 128-bit loads; the simulated twin of that loop is run with each
     # candidate -sim_l1_port_bytes and the best fit kept (0 = the reference's
@@ -262,6 +271,79 @@ def simulated_l1_bandwidth(config_dir: str, port: int, widths=(4, 8, 16), per_cu
             byts.append(g.nwarps * n * ws * w)
         out[w] = (byts[1] - byts[0]) / max(1, cyc[1] - cyc[0]) / n_cu
     return out
+
+
+def simulated_chain_latency(config_dir: str, op: str, extra: Sequence[str] = (), iters: int = 8) -> float:
+    """Cycles per instruction the simulator gives one wave's dependent chain
+    of `op` (each instruction reads the previous one's destination), run as a
+    loop from a warm instruction cache like ub_alu / ub_lds: bodies of 16 and
+    32 instructions, `iters` iterations each; the difference removes launch,
+    drain and the loop branch."""
+    import tempfile
+    from .. import _native
+    from ..tracegen import rodinia
+    from ..tracegen.builder import KernelBuilder
+    ws = 64
+    for line in open(os.path.join(config_dir, "gpgpusim.config")):
+        t = line.split()
+        if len(t) >= 2 and t[0] == "-gpgpu_shader_core_pipeline":
+            ws = int(t[1].split(":")[1])
+    if ws != 64:
+        raise ValueError("chain twin is written for wave64 (CDNA) traces")
+    lds, glob = op.startswith("ds_"), op.startswith("global_")
+    d = tempfile.mkdtemp(prefix="asim_chain_")
+    cyc = []
+    for body in (16, 32):
+        k = KernelBuilder("ub_chain", (1, 1, 1), (ws, 1, 1), nregs=16, shmem=4096 if lds else 0,
+                          binary_version=950, warp_size=ws)
+        for _ in range(iters):
+            k.pc = 0x100
+            for _ in range(body):
+                k.op(op, [8], [8], base=0x7000_0000 if glob else 0, stride=0)
+                k.pc -= 8  # 8-byte encodings (VOP3 / DS / FLAT)
+            k.op("s_cbranch_scc1")
+        k.op("s_endpgm")
+        kl = rodinia.write_app(os.path.join(d, f"b{body}"), [k.build()], memcpy=False)
+        args = ["-config", os.path.join(config_dir, "gpgpusim.config"), "-config",
+                os.path.join(config_dir, "trace.config"), "-trace", kl] + list(extra)
+        s = _native.load().Simulator(args, False)
+        if s.run() != 0:
+            raise RuntimeError("chain simulation failed")
+        cyc.append(s.tot_cycle)
+    return (cyc[1] - cyc[0]) / (16.0 * iters)
+
+
+# (latency option, index of the latency in its value, twin opcode, options
+# that take the same correction)
+_CHAIN_KNOBS = (
+    ("-trace_opcode_latency_initiation_sp", 0, "v_fma_f32", ("-trace_opcode_latency_initiation_int",)),
+    ("-trace_opcode_latency_initiation_dp", 0, "v_fma_f64", ()),
+    ("-trace_opcode_latency_initiation_sfu", 0, "v_exp_f32", ()),
+    ("-gpgpu_smem_latency", 0, "ds_read_b32", ()),
+)
+
+
+def _latency_self_consistency(out: str, cfg: Dict[str, str], applied: Dict[str, str], base: str) -> List[str]:
+    notes = []
+    for opt, idx, op, also in _CHAIN_KNOBS:
+        if opt not in cfg:
+            continue
+        vals = cfg[opt].split(",")
+        target = int(vals[idx])  # the measured chain latency
+        sim = simulated_chain_latency(out, op)
+        over = int(round(sim - target))
+        if over <= 0:
+            continue
+        for o in (opt,) + tuple(also):
+            if o not in cfg:
+                continue
+            v = cfg[o].split(",")
+            v[idx] = str(max(1, int(v[idx]) - over))
+            cfg[o] = applied[o] = ",".join(v)
+        presets.write_config(cfg, out, power_preset=base)
+        notes.append(f"{opt} {target} -> {cfg[opt]}: the simulated dependent {op} chain lasted {sim:.1f} "
+                     f"cycles per instruction against the measured {target}")
+    return notes
 
 
 def simulated_empty_kernel_cycles(config_dir: str) -> int:
