@@ -320,6 +320,7 @@ _CHAIN_KNOBS = (
     ("-trace_opcode_latency_initiation_dp", 0, "v_fma_f64", ()),
     ("-trace_opcode_latency_initiation_sfu", 0, "v_exp_f32", ()),
     ("-gpgpu_smem_latency", 0, "ds_read_b32", ()),
+    ("-gpgpu_l1_latency", 0, "global_load_dword", ()),  # ub_cache_lat's L1-hit pointer chase
 )
 
 

@@ -34,6 +34,7 @@ def test_chain_twin_matches_measured(tmp_path):
     cfg["-trace_opcode_latency_initiation_sp"] = "8,2"
     cfg["-trace_opcode_latency_initiation_int"] = "8,2"
     cfg["-trace_opcode_latency_initiation_dp"] = "7,2"
+    cfg["-gpgpu_l1_latency"] = "120"
     from accel_sim_framework_distributed_amd.models import presets
     presets.write_config(cfg, out, power_preset="MI355X")
     before = tuner.simulated_chain_latency(out, "ds_read_b32")
@@ -46,3 +47,4 @@ def test_chain_twin_matches_measured(tmp_path):
     assert tuner.simulated_chain_latency(out, "ds_read_b32") == pytest.approx(60, abs=1)
     assert tuner.simulated_chain_latency(out, "v_fma_f32") == pytest.approx(8, abs=1)
     assert tuner.simulated_chain_latency(out, "v_fma_f64") == pytest.approx(7, abs=1)
+    assert tuner.simulated_chain_latency(out, "global_load_dword") == pytest.approx(120, abs=1)
