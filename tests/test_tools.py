@@ -22,7 +22,9 @@ def test_tuner_from_measured_mi355x_logs(native, tmp_path):
     out, applied = tuner.tune([UBENCH], "MI355X", str(tmp_path))
     cfg = native.parse_config(["-config", os.path.join(out, "gpgpusim.config"), "-config",
                                os.path.join(out, "trace.config")])
-    assert cfg["n_sm"] == 256 and cfg["l1_latency"] == int(opts["-gpgpu_l1_latency"])
+    # the chain self-consistency takes the pipeline's own stages out of the
+    # measured L1-hit pointer-chase latency (tuner._latency_self_consistency)
+    assert cfg["n_sm"] == 256 and 0 < int(opts["-gpgpu_l1_latency"]) - cfg["l1_latency"] <= 16
     assert "TUNING.md" in os.listdir(out)
     # measured write policies (ub_cache_policy): L1 write-evict + lazy fetch
     # on read; the L2 probe reads a stored line back from memory but the L2
