@@ -24,6 +24,17 @@ def load(prefer_torch_runtime: bool = False):
             import torch  # noqa: F401
         except Exception:  # pragma: no cover - torch is optional here
             pass
+    alt = os.environ.get("ASIM_NATIVE_SO")
+    if alt:
+        # A/B runs inside one GPU call: another build of the same module
+        # (e.g. the previous commit's) loaded from its own file
+        from importlib import util as ilu
+        spec = ilu.spec_from_file_location("accel_sim_framework_distributed_amd._asim", alt)
+        m = ilu.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        sys.modules["accel_sim_framework_distributed_amd._asim"] = m
+        _mod = m
+        return _mod
     try:
         _mod = importlib.import_module("accel_sim_framework_distributed_amd._asim")
     except ImportError as e:

@@ -70,6 +70,7 @@ class DistributedSuite:
                 if os.path.exists(kl):
                     self.apps.append((app, kl))
         self.max_concurrency = None
+        self.plan_source = "local"
         self.weights: Dict[str, float] = {}  # last wall time per app (LPT order)
         self.times: Dict = {}                # (app, engine) -> last wall time
         self.assignment: Dict[str, str] = {}
@@ -107,6 +108,55 @@ class DistributedSuite:
         except Exception:  # pragma: no cover - torch is optional for the CPU engine
             pass
 
+    @staticmethod
+    def mock_gpu() -> bool:
+        """``ASIM_MOCK_GPU=1``: the CPU tier's stand-in for the GPU engine (it
+        runs the bit-identical CPU engine under the GPU engine's name, with
+        ``ASIM_MOCK_GPU_SLOTS`` concurrent slots), so the node planner and the
+        multi-rank plan agreement run in CPU-only tests."""
+        return os.environ.get("ASIM_MOCK_GPU", "0") not in ("", "0")
+
+    def _dist(self):
+        try:
+            import torch.distributed as dist
+            if self.world > 1 and dist.is_available() and dist.is_initialized():
+                return dist
+        except Exception:  # pragma: no cover - torch is optional for the CPU engine
+            pass
+        return None
+
+    def agree_plan(self) -> bool:
+        """Every rank runs rank 0's placement (engine and host threads per
+        application, and the timings that order them).  Ranks calibrate under
+        their own host load, so independent plans could differ; the step of a
+        multi-GPU run must be one plan.  Returns whether this rank's own plan
+        already matched rank 0's."""
+        dist = self._dist()
+        mine = dict(assignment=dict(self.assignment), threads=dict(self.threads))
+        if dist is None:
+            self.plan_source = "local"
+            return True
+        obj = [dict(assignment=self.assignment, threads=self.threads, times=self.times,
+                    predicted_span=self.predicted_span) if self.rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        r0 = obj[0]
+        same = r0["assignment"] == mine["assignment"] and r0["threads"] == mine["threads"]
+        self.assignment = dict(r0["assignment"])
+        self.threads = dict(r0["threads"])
+        self.times.update(r0["times"])
+        self.predicted_span = r0["predicted_span"]
+        self.plan_source = "rank0"
+        return same
+
+    def gather(self, info: Dict) -> List[Dict]:
+        """`info` of every rank, at every rank (all_gather_object), rank order."""
+        dist = self._dist()
+        if dist is None:
+            return [info]
+        out = [None] * self.world
+        dist.all_gather_object(out, info)
+        return out
+
     def _bind_device(self):
         if self.device_index is not None:
             import torch
@@ -115,6 +165,8 @@ class DistributedSuite:
     def _sim(self, kl: str, engine: Optional[str] = None, threads: int = 1):
         extra = {"-collective_model": self.collective_model}
         eng = engine or ("gpu" if self.engine == "node" else self.engine)
+        if eng == "gpu" and self.mock_gpu():
+            eng = "cpu"
         if eng == "cpu" and threads > 1:
             extra["-sim_cpu_threads"] = str(threads)
         args = build_args(self.config, kl, eng, extra)
@@ -128,6 +180,8 @@ class DistributedSuite:
         if self.engine == "cpu":
             n = self.cpu_slots()
             return max(1, min(len(self.apps) or 1, n))
+        if self.mock_gpu():
+            return max(1, int(os.environ.get("ASIM_MOCK_GPU_SLOTS", "2")))
         cus = int(self.mod.gpu_cu_count())
         cfg = self.mod.parse_config(build_args(self.config, None, "cpu"))
         per = self.mod.gpu_cus_per_sim(cfg["n_sm"], cfg["n_mem"]) if hasattr(self.mod, "gpu_cus_per_sim") \
@@ -429,6 +483,8 @@ class DistributedSuite:
         eng = engine or ("gpu" if self.engine == "node" else self.engine)
         if eng == "cpu" and self.threads.get("dp-step", 1) > 1:
             extra["-sim_cpu_threads"] = str(self.threads["dp-step"])
+        if eng == "gpu" and self.mock_gpu():
+            eng = "cpu"
         s = self.mod.Simulator(build_args(self.config, self.dp_step, eng, extra), self.verbose)
         n0 = len(getattr(self.sync, "events", []))
         if coupled:

@@ -52,6 +52,10 @@ def _parse():
     # "nccl" (RCCL over xGMI) is the production path; "gloo" lets several ranks
     # share one card to rehearse the multi-rank GPU-engine path on a 1-GPU box
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
+    # BASELINE.json config #5: every app x the tuner's 16 search configs, one
+    # batch of independent simulations per step (parallel/sweep.py)
+    ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--sweep-configs", type=int, default=16)
     return ap.parse_args()
 
 
@@ -101,6 +105,75 @@ def _resolve_app(rodinia, name: str) -> str:
     return hit[0]
 
 
+def _sweep(a, suite, engine, rank, world, use_cuda) -> int:
+    """``--sweep``: the tuner's configuration sweep as the step (one batch of
+    apps x 16 configs per rank, weak scaling over ranks)."""
+    import torch
+    from accel_sim_framework_distributed_amd.parallel.sweep import SweepRunner
+    run = SweepRunner(suite, a.sweep_configs)
+
+    def sync():
+        if use_cuda:
+            torch.cuda.synchronize()
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    ratio = run.calibrate()  # node: untimed GPU/CPU ratio per app (queue order)
+    for _ in range(a.warmup):
+        run.step()
+    sync()
+    t0 = time.perf_counter()
+    insn = insn_gpu = jobs_gpu = jobs_cpu = 0
+    for _ in range(a.steps):
+        r = run.step()
+        insn += r["insn"]
+        insn_gpu += r["insn_gpu"]
+        jobs_gpu += r["jobs_gpu"]
+        jobs_cpu += r["jobs_cpu"]
+    sync()
+    dt = time.perf_counter() - t0
+    mine = {"rank": rank, "wall_s": round(dt, 4), "insn": int(insn), "insn_gpu": int(insn_gpu),
+            "jobs_gpu": jobs_gpu, "jobs_cpu": jobs_cpu}
+    per_rank = suite.gather(mine)
+    dt_max = max(p["wall_s"] for p in per_rank)
+    insn_all = sum(p["insn"] for p in per_rank)
+    gpu_all = sum(p["insn_gpu"] for p in per_rank)
+    kips = insn_all / max(dt_max, 1e-9) / 1e3
+    if rank == 0:
+        out = {
+            "metric": "sim KIPS (whole node), tuner config sweep",
+            "value": round(kips, 3),
+            "unit": "KIPS (thousand simulated thread-instructions / wall s, summed over ranks)",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(dt_max / max(1, a.steps) * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": round(kips / BASELINE_KIPS, 3),
+            "vs_baseline_note": "not like-for-like: reference = GPGPU-Sim, 1 CPU core, recorded heartwall traces",
+            "dtype": "n/a (integer cycle-level model)",
+            "data": "synthetic (seeded Rodinia-2.0-ft-shaped SASS traces)",
+            "config": {"model": f"{a.config} ({_cfg_desc(a.config)}), BASELINE config #5 shape: "
+                                f"{len(run.jobs) // max(1, len(run.configs))} apps x {len(run.configs)} tuner "
+                                "search configs (scheduler x L2 granularity x hash x DRAM scheduler)",
+                       "global_batch": world, "seq_len": None,
+                       "parallelism": f"job-level: GPU-engine CU groups + host cores per rank (dp{world})",
+                       "engine": engine, "jobs_per_step_per_rank": len(run.jobs),
+                       "configs": [c for c, _ in run.configs],
+                       "gpu_slots": run.last.get("gpu_slots"), "cpu_slots": run.last.get("cpu_slots"),
+                       "gpu_over_cpu_time_ratio": {k: round(v, 3) for k, v in ratio.items()}},
+            "gpu_engine": {"kips_whole_node": round(gpu_all / max(dt_max, 1e-9) / 1e3, 1),
+                           "insn_share": round(gpu_all / max(insn_all, 1), 4),
+                           "jobs": sum(p["jobs_gpu"] for p in per_rank)},
+            "cpu_engine": {"kips_whole_node": round((insn_all - gpu_all) / max(dt_max, 1e-9) / 1e3, 1),
+                           "jobs": sum(p["jobs_cpu"] for p in per_rank)},
+            "per_rank": per_rank,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return 0
+
+
 def main() -> int:
     a = _parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -125,13 +198,15 @@ def main() -> int:
     engine = a.engine
     if engine == "auto":
         engine = "node" if mod.gpu_available() else "cpu"
-    if engine in ("gpu", "node") and not mod.gpu_available():
+    mock = os.environ.get("ASIM_MOCK_GPU", "0") not in ("", "0")  # CPU-tier rehearsal (multi_gpu.mock_gpu)
+    if engine in ("gpu", "node") and not mod.gpu_available() and not mock:
         raise SystemExit(f"bench.py: --engine {engine} requested but no HIP device is usable")
 
     from accel_sim_framework_distributed_amd.parallel.multi_gpu import DistributedSuite
     from accel_sim_framework_distributed_amd.tracegen import rodinia
 
-    tdir = a.trace_dir or os.path.join(tempfile.gettempdir(), f"asim_bench_rodinia_{os.getuid()}")
+    tdir = a.trace_dir or os.path.join(tempfile.gettempdir(),
+                                       f"asim_bench_rodinia_v{rodinia.SUITE_VERSION}_{os.getuid()}")
     apps = None if a.apps == "all" else [_resolve_app(rodinia, x) for x in a.apps.split(",")]
     # every rank generates (or reuses) the deterministic synthetic traces
     # a generated subset never stands in for the full suite (and vice versa is fine)
@@ -168,6 +243,8 @@ def main() -> int:
 
     suite = DistributedSuite(tdir, config=a.config, engine=engine, rank=rank, world=world, apps=apps,
                              verbose=a.verbose and rank == 0)
+    if a.sweep:
+        return _sweep(a, suite, engine, rank, world, use_cuda)
 
     def sync():
         if use_cuda:
@@ -182,6 +259,9 @@ def main() -> int:
         # (spare cores only; each app's team is re-timed before it is kept)
         suite.widen()
         suite.plan()
+    # one plan for the whole job: every rank runs rank 0's placement (ranks
+    # calibrate under their own host load and could otherwise disagree)
+    own_plan_matched = suite.agree_plan() if engine == "node" else True
     for _ in range(a.warmup):
         suite.step()
     sync()
@@ -225,6 +305,18 @@ def main() -> int:
         gpu_per_rank = [round(gpu_all / dt / 1e3, 1)]
         dp_cycles_per_rank = [int(dpl.get("cycles", 0))]
     kips = insn_all / dt / 1e3
+    # every rank's own view (gathered to all; rank 0 prints it)
+    mine = {"rank": rank, "wall_s": round(dt, 4), "insn": int(insn), "insn_gpu": int(insn_gpu),
+            "kips": round(insn / max(dt, 1e-9) / 1e3, 1),
+            "gpu_insn_share": round(insn_gpu / max(insn, 1), 4)}
+    if engine == "node":
+        mine.update(assignment=suite.assignment, cpu_threads={k: v for k, v in suite.threads.items() if v > 1},
+                    calibration_s=suite.calibration, own_plan_matched_rank0=bool(own_plan_matched),
+                    plan_source=suite.plan_source)
+    per_rank = suite.gather(mine)
+    plans_identical = all(p.get("assignment") == per_rank[0].get("assignment") and
+                          p.get("cpu_threads") == per_rank[0].get("cpu_threads") for p in per_rank)
+    walls = [p["wall_s"] for p in per_rank]
     if rank == 0:
         out = {
             "metric": "sim KIPS (whole node)",
@@ -272,6 +364,9 @@ def main() -> int:
                            "apps_on_gpu": (sum(1 for v in suite.assignment.values() if v == "gpu")
                                            if engine == "node" else (len(suite.apps) if engine == "gpu" else 0)),
                            "apps": len(suite.apps)},
+            "per_rank": per_rank,
+            "plans_identical": plans_identical,
+            "wall_s_spread": {"min": min(walls), "max": max(walls)},
             "cycle_mae_vs_hw": _cycle_mae(),
             "dp_step": ({"ranks": world, "simulated_cycles_max_rank": int(dp_max),
                          "simulated_cycles_per_rank": dp_cycles_per_rank,

@@ -102,11 +102,12 @@ void apply_intersim_config(SimCfg& c, const std::string& path) {
     if (topo == "tree4") c.topo_k = 4;
   } else if (topo == "flatfly" || topo == "dragonfly") {
     c.topo = TOPO_FLATFLY;  // one hop per differing dimension (minimal routing)
+    nodes *= c.topo_conc;   // flatfly_onchip: c terminals per router
   } else {
     throw OptionError("interconnect config: unsupported topology '" + topo + "' (anynet needs a network file)");
   }
   const uint64_t need = (uint64_t)c.n_clusters + c.n_subpart;
-  if (c.topo != TOPO_FLATFLY && nodes < need)
+  if (nodes < need)
     throw OptionError("interconnect config: topology has " + std::to_string(nodes) + " nodes, need " +
                       std::to_string(need) + " (clusters + memory sub-partitions)");
   // iq_router pipeline: routing, VC allocation, switch allocation, traversal

@@ -1007,6 +1007,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
     c.per_icnt = (uint64_t)llround(1e9 / f[1]);
     c.per_l2 = (uint64_t)llround(1e9 / f[2]);
     c.per_dram = (uint64_t)llround(1e9 / f[3]);
+    cfg_set_divs(c);
   }
   c.mall_miss_fs *= c.per_core;
   c.per_core_max = c.per_core;
@@ -1032,6 +1033,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   } else if (r.geti("-network_mode") != 2) {
     throw OptionError("-network_mode must be 1 (intersim topology) or 2 (local crossbar)");
   }
+  cfg_set_divs(c);  // the epoch length is final here
   return c;
 }
 

@@ -341,6 +341,7 @@ size_t Simulator::resume_checkpoint() {
     cfg_.per_core = h.per_core;
     cfg_.clk_base_cyc = h.clk_base_cyc;
     cfg_.clk_base_fs = h.clk_base_fs;
+    cfg_set_divs(cfg_);
     dvfs_ratio_ = (double)per_core_nom_ / (double)h.per_core;
   }
   kernels_done_ = (uint32_t)h.kernels_done;
@@ -1020,6 +1021,7 @@ void Simulator::set_clock_ratio(double ratio) {
   cfg_.per_core = per;
   cfg_.clk_base_cyc = now;
   cfg_.clk_base_fs = base_fs;
+  cfg_set_divs(cfg_);
   dvfs_ratio_ = ratio;
 }
 

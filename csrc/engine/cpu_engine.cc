@@ -8,6 +8,10 @@
 
 #include <functional>
 
+#include <atomic>
+#include <exception>
+#include <mutex>
+
 #include "engine.h"
 #include "thread_team.h"
 #include "trace_window.h"
@@ -209,6 +213,20 @@ class CpuEngine : public Engine {
     bar_.reset(nthr);
     const uint64_t epoch0 = epoch_, cycle0 = cycle_;
     uint64_t end_epoch = epoch0, end_cycle = cycle0;
+    // a throw inside the team (a malformed streamed trace in tw_.ensure, a
+    // CTA-fit logic error, ...) must not leave the other threads spinning at
+    // a barrier the thrower never reaches: the thread records the first
+    // exception and still arrives at the next barrier, after which every
+    // thread sees the abort flag and leaves the loop; run() rethrows once the
+    // whole team has returned
+    std::atomic<bool> abort{false};
+    std::exception_ptr err;
+    std::mutex err_mu;
+    auto fail = [&]() {
+      std::lock_guard<std::mutex> g(err_mu);
+      if (!err) err = std::current_exception();
+      abort.store(true, std::memory_order_release);
+    };
     std::function<void(uint32_t)> job = [&](uint32_t tid) {
       const SimCfg& c = c_;
       const uint64_t E = c.icnt_latency;
@@ -226,8 +244,15 @@ class CpuEngine : public Engine {
         // dispatch (epoch_decide flags when the window falls short)
         if (refill && tw_.any_streamed()) {
           if (nthr > 1) bar_.wait();
-          if (tid == 0) tw_.ensure(kt_, c, [&](DispatchView& v) { read_dispatch(v); });
+          if (tid == 0) {
+            try {
+              tw_.ensure(kt_, c, [&](DispatchView& v) { read_dispatch(v); });
+            } catch (...) {
+              fail();
+            }
+          }
           if (nthr > 1) bar_.wait();
+          if (abort.load(std::memory_order_acquire)) break;
         }
         const uint32_t cur = (uint32_t)(epoch & 1), prev = cur ^ 1u;
         const uint64_t t0 = cycle, t1 = t0 + E;
@@ -236,6 +261,7 @@ class CpuEngine : public Engine {
         // lines with its own units, not with every other thread's
         const int s0 = (int)((uint64_t)nsm * tid / nthr), s1 = (int)((uint64_t)nsm * (tid + 1) / nthr);
         const int c0 = (int)((uint64_t)nch * tid / nthr), c1 = (int)((uint64_t)nch * (tid + 1) / nthr);
+        try {
         for (int q = 0; q < (s1 - s0) + (c1 - c0); ++q) {
           const int i = q < s1 - s0 ? s0 + q : nsm + c0 + (q - (s1 - s0));
           if (i < nsm) {
@@ -252,14 +278,24 @@ class CpuEngine : public Engine {
             chan_publish<SeqPar>(ch, m, *pub_, cur);
           }
         }
+        } catch (...) {
+          fail();
+        }
         if (nthr > 1) bar_.wait();
+        if (abort.load(std::memory_order_acquire)) break;
         if (!link_free_.empty()) {
           // shared links of multi-hop routes: this epoch's packets reserve
           // their routes before any destination reads them (icnt_links.h)
-          if (tid == 0)
-            icnt_contend<SeqPar>(c, box_req_[cur].data(), cnt_req_[cur].data(), cap_req_, box_rep_[cur].data(),
-                                 cnt_rep_[cur].data(), cap_rep_, link_free_.data(), link_refs_.data(), link_stat_);
+          if (tid == 0) {
+            try {
+              icnt_contend<SeqPar>(c, box_req_[cur].data(), cnt_req_[cur].data(), cap_req_, box_rep_[cur].data(),
+                                   cnt_rep_[cur].data(), cap_rep_, link_free_.data(), link_refs_.data(), link_stat_);
+            } catch (...) {
+              fail();
+            }
+          }
           if (nthr > 1) bar_.wait();
+          if (abort.load(std::memory_order_acquire)) break;
         }
         const uint64_t mc = pw_on_ ? (lim.max_cycle ? std::min(lim.max_cycle, pw_next) : pw_next) : lim.max_cycle;
         const EpochDecision d = epoch_decide<SeqPar>(c, *pub_, cur, t1, kt_, epoch, mc);
@@ -277,8 +313,15 @@ class CpuEngine : public Engine {
           if (exits || cycle >= pw_next) {
             // thread 0 samples while the others wait (the next epoch would
             // move the statistics)
-            if (tid == 0) power_sample(cycle);
+            if (tid == 0) {
+              try {
+                power_sample(cycle);
+              } catch (...) {
+                fail();
+              }
+            }
             if (nthr > 1) bar_.wait();
+            if (abort.load(std::memory_order_acquire)) break;
             pw_next = cycle + pw_.freq;
           }
         }
@@ -305,6 +348,7 @@ class CpuEngine : public Engine {
       }
     };
     team_.run(nthr, job);
+    if (err) std::rethrow_exception(err);
     epoch_ = end_epoch;
     cycle_ = end_cycle;
     if (res.done) {
@@ -377,6 +421,7 @@ class CpuEngine : public Engine {
     c_.per_core = per_core;
     c_.clk_base_cyc = base_cyc;
     c_.clk_base_fs = base_fs;
+    cfg_set_divs(c_);
   }
   void flush_l2(bool writeback) override {
     host_flush_l2(chs_.data(), (uint32_t)chs_.size(), c_, writeback, mall_.empty() ? nullptr : mall_.data());

@@ -805,6 +805,7 @@ class GpuEngine : public Engine {
     c_.per_core = per_core;
     c_.clk_base_cyc = base_cyc;
     c_.clk_base_fs = base_fs;
+    cfg_set_divs(c_);
     upload_cfg();
   }
   void flush_l2(bool writeback) override {

@@ -118,6 +118,60 @@ struct TraceEv {
   uint64_t b;
 };
 
+// Exact unsigned 64-bit division by a divisor fixed for the run (the clock
+// periods): a multiply-high and a shift instead of the ~100-instruction
+// software division the GPU would otherwise run for every `/ per_core`
+// (round-up magic numbers, Granlund & Montgomery 1994; the same arithmetic
+// on both engines, so results stay bit-identical).
+struct Div64 {
+  uint64_t magic;  // 0: power of two (shift only)
+  uint64_t d;
+  uint32_t shift;
+  uint32_t add;    // the 65-bit magic's top bit: q = (((x - hi) >> 1) + hi) >> shift
+};
+SIM_HDI uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+SIM_HDI uint64_t fdiv(uint64_t x, const Div64& v) {
+  if (!v.magic) return x >> v.shift;
+  const uint64_t hi = mulhi64(x, v.magic);
+  if (v.add) return (((x - hi) >> 1) + hi) >> v.shift;
+  return hi >> v.shift;
+}
+// host only (called at config time; plain host functions are parsed, never
+// emitted, in the device pass)
+inline Div64 make_div64(uint64_t d) {
+  Div64 r{0, d ? d : 1, 0, 0};
+  d = r.d;
+  const uint32_t l = 63u - (uint32_t)__builtin_clzll(d);  // floor(log2 d)
+  if ((d & (d - 1)) == 0) {
+    r.shift = l;
+    return r;
+  }
+  // m = floor(2^(64+l) / d); the smallest power that works gives a 64-bit
+  // magic, otherwise the 65-bit one with the add step
+  const unsigned __int128 num = (unsigned __int128)1 << (64 + l);
+  uint64_t m = (uint64_t)(num / d);
+  const uint64_t rem = (uint64_t)(num % d);
+  const uint64_t e = d - rem;
+  if (e < (1ull << l)) {
+    r.shift = l;
+    r.add = 0;
+  } else {
+    m += m;
+    const uint64_t twice = rem + rem;
+    if (twice >= d || twice < rem) m += 1;
+    r.shift = l;
+    r.add = 1;
+  }
+  r.magic = m + 1;
+  return r;
+}
+
 struct SimCfg {
   // ---- topology ----
   uint32_t n_sm;
@@ -256,6 +310,8 @@ struct SimCfg {
   // the stamps already taken in femtoseconds stay valid (core_fs / core_cyc)
   uint64_t clk_base_cyc, clk_base_fs;
   uint64_t per_core_max;    // the longest core period DVFS may set (sizes the per-epoch reply mailboxes)
+  Div64 dv_core, dv_icnt, dv_l2, dv_dram;  // exact division by the periods (cfg_set_divs)
+  Div64 dv_epoch;                          // ... and by the epoch length (icnt_latency)
   // ---- kernel scheduling ----
   uint32_t kernel_launch_latency;
   uint32_t kernel_launch_latency_queued;  // a kernel right behind the previous one (driver)
@@ -351,8 +407,10 @@ SIM_HDI uint32_t icnt_routers(const SimCfg& c, uint32_t a, uint32_t b) {
       }
       return 2 * lvl - 1;
     }
-    default: {  // flattened butterfly: one hop per differing dimension
+    default: {  // flattened butterfly (c terminals per router): one hop per differing dimension
       uint32_t h = 0;
+      a /= (c.topo_conc ? c.topo_conc : 1);
+      b /= (c.topo_conc ? c.topo_conc : 1);
       for (uint32_t d = 0; d < n; ++d) {
         h += (a % k) != (b % k);
         a /= k;
@@ -363,18 +421,28 @@ SIM_HDI uint32_t icnt_routers(const SimCfg& c, uint32_t a, uint32_t b) {
   }
 }
 
+// refresh the period dividers after any change of per_* (config derivation,
+// DVFS, checkpoint restore)
+inline void cfg_set_divs(SimCfg& c) {
+  c.dv_core = make_div64(c.per_core);
+  c.dv_icnt = make_div64(c.per_icnt);
+  c.dv_l2 = make_div64(c.per_l2);
+  c.dv_dram = make_div64(c.per_dram);
+  c.dv_epoch = make_div64(c.icnt_latency ? c.icnt_latency : 1);
+}
+
 // absolute femtoseconds of the start of core cycle `cyc`, and the core cycle
 // holding femtosecond `fs` (floor) or starting at or after it (ceil)
 SIM_HDI uint64_t core_fs(const SimCfg& c, uint64_t cyc) {
   return (uint64_t)((int64_t)c.clk_base_fs + ((int64_t)cyc - (int64_t)c.clk_base_cyc) * (int64_t)c.per_core);
 }
 SIM_HDI uint64_t core_cyc(const SimCfg& c, uint64_t fs) {
-  if (fs >= c.clk_base_fs) return c.clk_base_cyc + (fs - c.clk_base_fs) / c.per_core;
-  return c.clk_base_cyc - (c.clk_base_fs - fs + c.per_core - 1) / c.per_core;
+  if (fs >= c.clk_base_fs) return c.clk_base_cyc + fdiv(fs - c.clk_base_fs, c.dv_core);
+  return c.clk_base_cyc - fdiv(c.clk_base_fs - fs + c.per_core - 1, c.dv_core);
 }
 SIM_HDI uint64_t core_cyc_ceil(const SimCfg& c, uint64_t fs) {
-  if (fs >= c.clk_base_fs) return c.clk_base_cyc + (fs - c.clk_base_fs + c.per_core - 1) / c.per_core;
-  return c.clk_base_cyc - (c.clk_base_fs - fs) / c.per_core;
+  if (fs >= c.clk_base_fs) return c.clk_base_cyc + fdiv(fs - c.clk_base_fs + c.per_core - 1, c.dv_core);
+  return c.clk_base_cyc - fdiv(c.clk_base_fs - fs, c.dv_core);
 }
 
 // femtoseconds from injection complete to arrival: SM `sm` -> sub-partition `sub`

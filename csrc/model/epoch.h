@@ -262,7 +262,7 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t 
     const uint32_t nk = slot_order(kt, order);
     for (uint32_t i = 0; i < nk; ++i)
       if (t0 >= kt.k[order[i]].ready_cycle) {
-        const uint32_t rot = (uint32_t)((t0 / c.icnt_latency) % c.n_sm);
+        const uint32_t rot = (uint32_t)(fdiv(t0, c.dv_epoch) % c.n_sm);
         if (c.n_xcd > 1) cta_dispatch_xcd<P>(s, x, order[i], pub.sm[prev], c.n_sm, rot);
         else cta_dispatch<P>(s, x, order[i], pub.sm[prev], c.n_sm, rot);
       }
@@ -494,7 +494,7 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
   // fast-forward over the kernel launch latency when nothing is in flight
   if (undisp && cbusy == 0 && t1 < ready_min && undrained == 0) {
     uint64_t E = c.icnt_latency;
-    uint64_t skip = (ready_min - t1) / E * E;
+    uint64_t skip = fdiv(ready_min - t1, c.dv_epoch) * E;
     d.next_start = t1 + skip;
   }
   // Whole-epoch fast-forward (conservative PDES with exact next-event times):
@@ -509,13 +509,13 @@ SIM_HDI EpochDecision epoch_decide(const SimCfg& c, const EpochPub& pub, uint32_
       const uint64_t E = c.icnt_latency;
       const uint64_t tc = core_cyc(c, ev);  // the next epoch may start no later than this
       if (tc >= t1 + E) {
-        uint64_t s = t1 + (tc - t1) / E * E;
+        uint64_t s = t1 + fdiv(tc - t1, c.dv_epoch) * E;
         if (max_cycle && s > max_cycle) s = max_cycle > t1 ? t1 + (max_cycle - t1 + E - 1) / E * E : t1;
         if (s > d.next_start) d.next_start = s;
       }
     }
   }
-  if (c.deadlock_window && nbusy && ((t1 / c.icnt_latency) & 63) == 0) {
+  if (c.deadlock_window && nbusy && (fdiv(t1, c.dv_epoch) & 63) == 0) {
     // newest progress stamp over all SMs
     const uint64_t last = prog;
     if (t1 > last + c.deadlock_window && t1 > ready_max + c.deadlock_window) d.deadlock = 1;

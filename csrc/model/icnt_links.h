@@ -24,6 +24,9 @@
 // The pass is policy-generic (P = SeqPar on the CPU engine, WavePar on one
 // GPU block) and its order is fixed, so both engines give identical results.
 #pragma once
+#if !defined(__HIP_DEVICE_COMPILE__)
+#include <stdexcept>
+#endif
 #include "config.h"
 
 namespace asim {
@@ -48,7 +51,8 @@ SIM_HDI uint64_t icnt_link_count(const SimCfg& c) {
     case TOPO_MESH:
     case TOPO_TORUS: return kn * (2ull * n + (c.topo == TOPO_CMESH ? (c.topo_conc ? c.topo_conc : 1) : 1));
     case TOPO_FATTREE: return 2ull * n * kn + kn;  // up, down, ejection
-    default: return kn * ((uint64_t)n * k + 1);     // flattened butterfly: per dimension and target, + ejection
+    default:  // flattened butterfly: per dimension and target, + one ejection link per terminal
+      return kn * ((uint64_t)n * k + (c.topo_conc ? c.topo_conc : 1));
   }
 }
 
@@ -100,13 +104,13 @@ SIM_HDI uint32_t icnt_route(const SimCfg& c, uint32_t a, uint32_t b, F&& emit) {
             up = fwd <= k - fwd;
           }
           emit((uint32_t)(cur * P + 2 * d + (up ? 0 : 1)));
-        ++m;
+          ++m;
           const uint32_t nx = up ? (x + 1) % k : (x + k - 1) % k;
           cur = cur - (uint64_t)x * pw + (uint64_t)nx * pw;
         }
       }
       emit((uint32_t)(cur * P + 2 * n + b % conc));
-        ++m;
+      ++m;
       return m;
     }
     case TOPO_FATTREE: {  // up to the lowest common ancestor (d-mod-k), then down
@@ -131,21 +135,25 @@ SIM_HDI uint32_t icnt_route(const SimCfg& c, uint32_t a, uint32_t b, F&& emit) {
         ++m;
       }
       emit((uint32_t)(2ull * n * kn + b % kn));
-        ++m;
+      ++m;
       return m;
     }
-    default: {  // flattened butterfly: one hop per differing dimension
-      const uint32_t P = n * k + 1;
-      uint64_t cur = a, pw = 1;
+    default: {  // flattened butterfly: one hop per differing dimension between routers
+      // (node / conc; the config check guarantees k^n * conc >= nodes, so every
+      // router index is < k^n and every link index < icnt_link_count)
+      const uint32_t conc = c.topo_conc ? c.topo_conc : 1;
+      const uint32_t P = n * k + conc;
+      uint64_t cur = a / conc, pw = 1;
+      const uint64_t dst = b / conc;
       for (uint32_t d = 0; d < n; ++d, pw *= k) {
-        const uint32_t x = (uint32_t)((cur / pw) % k), y = (uint32_t)((b / pw) % k);
+        const uint32_t x = (uint32_t)((cur / pw) % k), y = (uint32_t)((dst / pw) % k);
         if (x == y) continue;
         emit((uint32_t)(cur * P + d * k + y));
         ++m;
         cur = cur - (uint64_t)x * pw + (uint64_t)y * pw;
       }
-      emit((uint32_t)(cur * P + n * k));
-        ++m;
+      emit((uint32_t)(cur * P + n * k + b % conc));
+      ++m;
       return m;
     }
   }
@@ -161,6 +169,9 @@ SIM_HDI uint64_t icnt_reserve(const SimCfg& c, Pkt& p, uint32_t a, uint32_t b, u
   uint64_t D = 0;
   uint32_t h = 0;
   icnt_route(c, a, b, [&](uint32_t l) {
+#if !defined(__HIP_DEVICE_COMPILE__) && !defined(NDEBUG)
+    if (l >= icnt_link_count(c)) throw std::logic_error("icnt_reserve: link index outside the topology");
+#endif
     // uncontended departure onto link h (the route's schedule ends at p.t)
     const uint64_t back = (uint64_t)(nl - 1 - (h < nl ? h : nl - 1)) * hop + last;
     const uint64_t d = p.t > back ? p.t - back : 0;
@@ -190,7 +201,7 @@ SIM_HDI void icnt_contend(const SimCfg& c, Pkt* box_req, const uint32_t* cnt_req
   const uint32_t cpc = c.cores_per_cluster ? c.cores_per_cluster : 1;
   for (int dir = 0; dir < 2; ++dir) {
     const uint32_t* cnt = dir == 0 ? cnt_req : cnt_rep;
-    // every packet of the epoch in cell order: (cell << 8 | index in the cell)
+    // every packet of the epoch in cell order: (cell << 16 | index in the cell)
     const uint32_t total = P::scan((int)ncell, [&](int i) -> uint32_t { return cnt[i]; },
                                    [&](int i, uint32_t off) {
                                      for (uint32_t j = 0; j < cnt[i]; ++j) refs[off + j] = (uint32_t)i << 16 | j;
@@ -215,7 +226,7 @@ SIM_HDI void icnt_contend(const SimCfg& c, Pkt* box_req, const uint32_t* cnt_req
         const uint64_t D = icnt_reserve(c, *p, a, b, link_free);
         if (D) {
           ++delayed;
-          wait += D / c.per_icnt;
+          wait += fdiv(D, c.dv_icnt);
         }
       }
       stat[0] += delayed;

@@ -377,7 +377,7 @@ SIM_HDI bool l2_access(ChanState& ch, SubPart& sp, const SimCfg& c, uint32_t sub
   // MEMORY_SUBPARTITION_UNIT trace: outcome 0 hit, 1 miss, 2 mshr hit, 3 write-through
   auto trace = [&](uint16_t outcome) {
     if (trace_mem_on(c, TS_MEMORY_SUBPARTITION_UNIT, ch.id))
-      P::one([&] { trace_put(c, c.n_sm + ch.id, now_fs / c.per_l2, EV_L2_ACCESS, (uint16_t)(sub << 8 | outcome), p.addr); });
+      P::one([&] { trace_put(c, c.n_sm + ch.id, fdiv(now_fs, c.dv_l2), EV_L2_ACCESS, (uint16_t)(sub << 8 | outcome), p.addr); });
   };
   L2Line* T = l2_tags(ch, c, sub);
   int way = g.disabled ? -1 : l2_find<P>(T, g, set, p.addr);
@@ -625,13 +625,13 @@ SIM_HDI void mem_icnt_cycle(ChanState& ch, SubPart& sp, const SimCfg& c, const M
   if (sp.inq_n && sp.rop_n < (uint32_t)kRopQ && sp.rop_n < c.q_icnt_l2 + c.rop_latency &&
       sp.inq[sp.inq_head].t <= now_fs) {
     // the output port grants one ready input per cycle
-    XbarGrant g = xbar_pick<P>(sp.inq, sp.inq_head, sp.inq_n, kMemInQ, now_fs, c, now_fs / c.per_icnt,
+    XbarGrant g = xbar_pick<P>(sp.inq, sp.inq_head, sp.inq_n, kMemInQ, now_fs, c, fdiv(now_fs, c.dv_icnt),
                                sp.arb_next, sp.arb_cnt, c.n_sm);
     sp.st.icnt_arb_cycles++;
     sp.st.icnt_conflicts += g.ready - 1;
     {
       Pkt p = xbar_take(sp.inq, sp.inq_head, sp.inq_n, kMemInQ, g.off);
-      sp.st.icnt_queue_cycles += (now_fs - p.t) / c.per_icnt;
+      sp.st.icnt_queue_cycles += fdiv(now_fs - p.t, c.dv_icnt);
       p.t = now_fs + (uint64_t)c.rop_latency * c.per_l2;
       sp.rop[(sp.rop_head + sp.rop_n) % kRopQ] = p;
       sp.rop_n++;
@@ -939,13 +939,13 @@ SIM_HDI uint64_t chan_next_event(const ChanState& ch, const SimCfg& c, uint64_t 
 // dram_cycle with nothing ready)
 SIM_HDI void chan_quiet_advance(ChanState& ch, const SimCfg& c, uint64_t target) {
   const uint64_t nd = next_tick(ch.t_dram, c.per_dram, target);
-  const uint64_t kd = (nd - ch.t_dram) / c.per_dram;
+  const uint64_t kd = fdiv(nd - ch.t_dram, c.dv_dram);
   ch.sp[0].st.dram_cycles += kd;
   ch.sp[0].st.dram_q_occ += (uint64_t)ch.q_n * kd;
   ch.dcycle += kd;
   ch.t_dram = nd;
   const uint64_t nl = next_tick(ch.t_l2, c.per_l2, target);
-  const uint64_t kl = (nl - ch.t_l2) / c.per_l2;
+  const uint64_t kl = fdiv(nl - ch.t_l2, c.dv_l2);
   for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
     ch.sp[j].st.l2_cycles += kl;
     ch.sp[j].st.rop_occ += (uint64_t)ch.sp[j].rop_n * kl;
@@ -962,11 +962,11 @@ SIM_HDI void mem_window(ChanState& ch, const MemCtx& x) {
   if (chan_idle(ch, c)) {
     // nothing can happen until a new arrival (next epoch): skip the ticks
     uint64_t nd = next_tick(ch.t_dram, c.per_dram, t1);
-    ch.sp[0].st.dram_cycles += (nd - ch.t_dram) / c.per_dram;
-    ch.dcycle += (nd - ch.t_dram) / c.per_dram;
+    ch.sp[0].st.dram_cycles += fdiv(nd - ch.t_dram, c.dv_dram);
+    ch.dcycle += fdiv(nd - ch.t_dram, c.dv_dram);
     ch.t_dram = nd;
     uint64_t nl = next_tick(ch.t_l2, c.per_l2, t1);
-    for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) ch.sp[j].st.l2_cycles += (nl - ch.t_l2) / c.per_l2;
+    for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) ch.sp[j].st.l2_cycles += fdiv(nl - ch.t_l2, c.dv_l2);
     ch.t_l2 = nl;
     ch.t_icnt = next_tick(ch.t_icnt, c.per_icnt, t1);
     return;

@@ -833,14 +833,14 @@ SIM_HDI void sm_receive(S& s, const SmCtx& x, uint64_t now) {
     uint32_t head = P::uni(s.inq_head), n = P::uni(s.inq_n);
     uint16_t an = s.arb_next, ac = s.arb_cnt;
     P::prof(40);
-    const XbarGrant g = xbar_pick<P>(s.inq, head, n, kInQ, core_fs(c, now), c, core_fs(c, now) / c.per_icnt,
+    const XbarGrant g = xbar_pick<P>(s.inq, head, n, kInQ, core_fs(c, now), c, fdiv(core_fs(c, now), c.dv_icnt),
                                      an, ac, c.n_subpart);
     P::prof(0);
     s.arb_next = an;
     s.arb_cnt = ac;
     s.sadd(SK(icnt_reply_conflicts), g.ready - 1);
     q = P::uni(xbar_take(s.inq, head, n, kInQ, g.off));
-    s.sadd(SK(icnt_reply_queue_cycles), (core_fs(c, now) - q.t) / c.per_icnt);
+    s.sadd(SK(icnt_reply_queue_cycles), fdiv(core_fs(c, now) - q.t, c.dv_icnt));
     s.inq_head = head;
     s.inq_n = n;
     if (trace_sm_on(c, TS_INTERCONNECT, s.id)) P::one([&] { trace_put(c, s.id, now, EV_PKT_RECV, q.type, q.addr); });
@@ -1290,6 +1290,18 @@ SIM_HDI void sm_barrier_check(S& s, uint32_t cta) {
   }
 }
 
+// x mod n for the small operands of the issue stage (x < 2n in the common
+// case): a compare-and-subtract instead of an integer division on the GPU
+SIM_HDI uint32_t mod_small(uint32_t x, uint32_t n) {
+  if (x < n) return x;
+  x -= n;
+  return x < n ? x : x % n;
+}
+// the scheduler supervising warp w (w % n_sched; power-of-two counts mask)
+SIM_HDI uint32_t sched_of(uint32_t w, uint32_t nsched) {
+  return (nsched & (nsched - 1)) == 0 ? (w & (nsched - 1)) : w % nsched;
+}
+
 // can warp `w` issue its next instruction this cycle (scoreboard, flags,
 // pipeline register and load slot availability)
 template <class S>
@@ -1302,7 +1314,7 @@ SIM_HDI bool warp_can_issue_i(const S& s, const SimCfg& c, int w, const TInst& i
     if (sbt(s.w_sb, w, in.src[j])) return false;
   if (sbt(s.w_sb, w, in.dst[0]) || sbt(s.w_sb, w, in.dst[1])) return false;
   uint32_t u = unit_of(c, in.cls);
-  uint32_t sc = (uint32_t)w % nsched;
+  uint32_t sc = sched_of((uint32_t)w, nsched);
   if (in.cls == OC_EXIT || in.cls == OC_BARRIER || in.cls == OC_MEMBAR || in.cls == OC_NOP || (in.flags & F_WAITCNT))
     return true;  // handled at issue, no pipeline register needed
   if (idoc_busy >> (sc * U_COUNT + u) & 1ull) return false;
@@ -1552,13 +1564,13 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
       case SCHED_RRR: {
         uint32_t start = (uint32_t)(now % (uint64_t)nw);
         uint64_t r = rotr64(cand, start, (unsigned)nw);
-        pick = (int)((ffs64(r) + start) % (uint32_t)nw);
+        pick = (int)mod_small((uint32_t)ffs64(r) + start, (uint32_t)nw);
         break;
       }
       default: {  // LRR (and the two-level inner level): first ready warp after the last issued one
-        uint32_t start = (last + 1) % (uint32_t)nw;
+        uint32_t start = mod_small(last + 1, (uint32_t)nw);
         uint64_t r = rotr64(cand, start, (unsigned)nw);
-        pick = (int)((ffs64(r) + start) % (uint32_t)nw);
+        pick = (int)mod_small((uint32_t)ffs64(r) + start, (uint32_t)nw);
         break;
       }
     }
@@ -1605,13 +1617,13 @@ SIM_HDI void sm_fetch(S& s, const SimCfg& c, const KernelTab& kt) {
     uint8_t f = s.w_flags[w];
     return (f & WF_ACTIVE) && !(f & (WF_EXITING | WF_IMISS)) && s.w_ibuf[w] == 0 && s.w_next[w] < s.w_end[w];
   });
-  uint32_t start = P::uni(s.fetch_rr) % (uint32_t)nw;
+  uint32_t start = mod_small(P::uni(s.fetch_rr), (uint32_t)nw);
   uint64_t r = rotr64(need, start, (unsigned)nw);
   const bool icache = !c.perfect_icache && !c.il1.disabled;
   for (uint32_t i = 0; i < c.fetch_throughput && r; ++i) {
     int b = ffs64(r);
     r &= r - 1;
-    uint32_t w = (uint32_t)(b + start) % (uint32_t)nw;
+    uint32_t w = mod_small((uint32_t)b + start, (uint32_t)nw);
     if (icache && !il1_fetch<P>(s, c, kt, w)) {
       s.fetch_rr = w + 1;  // miss / reservation fail ends this cycle's fetch (shader.cc:997-1010)
       break;

@@ -13,6 +13,7 @@
 // distributed fork charges a constant -nccl_allreduce_latency per
 // ncclAllReduce (gpu-simulator/main.cc:116-122).
 #include <torch/extension.h>
+#include <c10/core/impl/VirtualGuardImpl.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/utils/pybind.h>
 
@@ -62,13 +63,21 @@ struct Bufs {
   }
 };
 
-// one all-to-all of int64 words with the given split sizes
+// one all-to-all of int64 words with the given split sizes.  RCCL: the
+// pinned send words go up and the received words come back as asynchronous
+// copies on the current stream, ordered around the collective (wait() only
+// makes the stream wait for RCCL's), so the host blocks exactly once per
+// exchange -- the stream sync before LinkSim reads the received slots.
 void a2a(c10d::ProcessGroup& pg, Bufs& b, std::vector<int64_t>& out_splits, std::vector<int64_t>& in_splits) {
   at::Tensor src = b.dev ? b.d_send : b.h_send, dst = b.dev ? b.d_recv : b.h_recv;
   if (b.dev) b.d_send.copy_(b.h_send, /*non_blocking=*/true);
   auto w = pg.alltoall_base(dst, src, in_splits, out_splits);
   w->wait();
-  if (b.dev) b.h_recv.copy_(b.d_recv);  // blocking: waits for the collective on the stream
+  if (b.dev) {
+    b.h_recv.copy_(b.d_recv, /*non_blocking=*/true);
+    const c10::impl::VirtualGuardImpl g(b.d_recv.device().type());
+    g.synchronizeStream(g.getStream(b.d_recv.device()));
+  }
 }
 
 int64_t allreduce_min(c10d::ProcessGroup& pg, int64_t v, bool dev, int device) {
@@ -161,10 +170,49 @@ py::dict exchange_run(py::object pgo, py::dict params, const std::string& kind, 
   return d;
 }
 
+// per-epoch cost of the exchange primitive alone: `iters` fixed-shape
+// all-to-alls of the epoch's W x (header + slots) words through the same
+// a2a() path exchange_run uses (pinned host -> device -> collective -> host),
+// after `warm` untimed ones; returns microseconds per exchange
+// (shape_world > 0: the words of a shape_world-rank epoch, split evenly over
+// this group's ranks -- on a 1-rank group a loopback of the 8-rank shape)
+py::dict a2a_bench(py::object pgo, int64_t iters, int64_t warm, int64_t device, int64_t shape_world) {
+  auto pg = py::cast<c10::intrusive_ptr<c10d::ProcessGroup>>(pgo);
+  const int W = pg->getSize();
+  const int slot = kHdr + 4 * kSlots;
+  const int Wv = shape_world > 0 ? (int)shape_world : W;
+  if (Wv % W) throw std::runtime_error("a2a_bench: shape_world must be a multiple of the group size");
+  const size_t n = (size_t)Wv * slot;
+  double s = 0;
+  {
+    py::gil_scoped_release nogil;
+    Bufs b;
+    b.dev = device >= 0;
+    b.ensure(n, (int)device);
+    std::vector<int64_t> eq(W, (int64_t)(n / W));
+    for (size_t i = 0; i < n; ++i) b.h_send.data_ptr<int64_t>()[i] = (int64_t)i;
+    for (int64_t i = 0; i < warm; ++i) a2a(*pg, b, eq, eq);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int64_t i = 0; i < iters; ++i) a2a(*pg, b, eq, eq);
+    s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  py::dict d;
+  d["us_per_exchange"] = s / (double)std::max<int64_t>(1, iters) * 1e6;
+  d["iters"] = iters;
+  d["words_per_rank"] = (int64_t)n;
+  d["bytes_per_rank"] = (int64_t)(n * 8);
+  d["world"] = W;
+  d["shape_world"] = Wv;
+  d["device"] = device >= 0;
+  return d;
+}
+
 }  // namespace asim
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "native epoch loop of the packet-level collective over a torch.distributed ProcessGroup";
   m.def("exchange_run", &asim::exchange_run, py::arg("group"), py::arg("params"), py::arg("kind"), py::arg("bytes"),
         py::arg("root"), py::arg("start_ps"), py::arg("device") = -1);
+  m.def("a2a_bench", &asim::a2a_bench, py::arg("group"), py::arg("iters") = 1000, py::arg("warm") = 50,
+        py::arg("device") = -1, py::arg("shape_world") = 0);
 }

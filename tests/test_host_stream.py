@@ -121,3 +121,25 @@ def test_streamed_shuffled_trace_simulates_identically(text_app, tmp_path):
     b = sim.simulate(kl, "QV100", engine="cpu", extra={"-trace_host_budget_mb": "0.5", "-gpu_trace_window": "1"})
     assert (a.tot_cycle, a.tot_insn) == (b.tot_cycle, b.tot_insn)
     assert _strip(a.stats) == _strip(b.stats)
+
+
+@pytest.mark.timeout(120)
+def test_malformed_streamed_trace_fails_cleanly_with_thread_team(text_app, tmp_path):
+    """a streamed trace whose late thread block names a warp outside its block
+    raises from the reader inside the CPU engine's thread team: the run must
+    end with that error on every thread count (the team used to
+    hang at its barrier with the exception in flight)"""
+    import shutil
+    from accel_sim_framework_distributed_amd import sim
+    d = tmp_path / "bad"
+    d.mkdir()
+    shutil.copy(text_app, d / "kernelslist.g")
+    text = open(_kernel_file(text_app)).read()
+    i = text.index("thread block = 5000,0,0\n")
+    j = text.index("warp = 3\n", i)
+    open(d / "kernel-1.traceg", "w").write(text[:j] + "warp = 99\n" + text[j + len("warp = 3\n"):])
+    kl = str(d / "kernelslist.g")
+    for thr in ("1", "4"):
+        with pytest.raises(Exception, match="warp id outside block"):
+            sim.simulate(kl, "QV100", engine="cpu", extra={"-trace_host_budget_mb": "0.5", "-gpu_trace_window": "1",
+                                                           "-sim_cpu_threads": thr})

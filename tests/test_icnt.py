@@ -173,7 +173,9 @@ def test_crossbar_hotspot_gpu_matches_cpu(native, tmp_path):
 # ---- link-level contention in multi-hop topologies (icnt_links.h) ----------
 TOPOS = [("mesh", dict(k=8, n=2, topology="mesh")), ("torus", dict(k=8, n=2, topology="torus")),
          ("fly2", dict(k=8, n=2, topology="fly")), ("fattree", dict(k=4, n=3, topology="fattree")),
-         ("flatfly", dict(k=8, n=2, topology="flatfly"))]
+         ("flatfly", dict(k=8, n=2, topology="flatfly")),
+         # concentrated flatfly_onchip: k^n = 16 routers < 32 endpoints, 2 terminals per router
+         ("flatfly_conc", dict(k=4, n=2, c=2, topology="flatfly"))]
 
 
 @pytest.mark.parametrize("name,kw", TOPOS)
@@ -192,6 +194,22 @@ def test_link_routes_follow_the_topology(native, tmp_path, name, kw):
             # routes to different destinations leave through different ejection links
     ej = {native.icnt_path(args, 0, 16 + s)[0][-1] for s in range(16)}
     assert len(ej) == 16
+
+
+def test_flatfly_with_fewer_nodes_than_endpoints_is_rejected(native, tmp_path):
+    # k^n = 16 routers without concentration cannot hold 32 endpoints: the link
+    # pass would index past its table, so the config is refused
+    args = _icnt_args(tmp_path, "ff_small", k=4, n=2, topology="flatfly")
+    with pytest.raises(Exception, match="nodes"):
+        native.Simulator(args + ["-icnt_link_contention", "1", "-trace", "/nonexistent"], False)
+
+
+def test_concentrated_flatfly_contention_runs(native, tmp_path):
+    kl = _hotspot_app(tmp_path, "ffc", True)
+    args = _icnt_args(tmp_path, "ffc", k=4, n=2, c=2, topology="flatfly")
+    s = native.Simulator(args + ["-icnt_link_contention", "1", "-gpgpu_perf_sim_memcpy", "0", "-trace", kl], False)
+    assert s.run() == 0 and not s.deadlock
+    assert _link_stat(s.output, "Network_link_delayed_packets") > 0
 
 
 def test_single_stage_crossbar_has_no_internal_links(native, tmp_path):

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Per-epoch cost of the packet collective's exchange primitive
+(csrc/parallel/exchange.cc a2a: pinned host -> device -> all-to-all ->
+host, one stream sync), timed `--iters` times through the native path.
+
+On a 1-GPU box: a 1-rank RCCL group exchanging the words of an 8-rank epoch
+(loopback, the same payload per rank), next to the same loop on gloo.  The
+multi-rank RCCL number needs the 8-GPU node (the driver's SCALE run)."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=1000)
+    ap.add_argument("--shape-world", type=int, default=8)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+    from accel_sim_framework_distributed_amd import _native
+    ext = _native.load_dist()
+    if ext is None:
+        raise SystemExit("_asim_dist not built")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29531")
+    res = {}
+    backends = ["gloo"] + (["nccl"] if torch.cuda.is_available() else [])
+    for be in backends:
+        dist.init_process_group(be, rank=0, world_size=1)
+        pg = dist.distributed_c10d._get_default_group()
+        dev = torch.cuda.current_device() if be == "nccl" else -1
+        if be == "nccl":
+            torch.cuda.set_device(dev)
+        r = dict(ext.a2a_bench(pg, iters=a.iters, warm=50, device=dev, shape_world=a.shape_world))
+        res[be] = r
+        print(be, json.dumps(r), flush=True)
+        dist.destroy_process_group()
+    out = {"what": "per-epoch exchange cost, 1-rank loopback of the %d-rank epoch shape" % a.shape_world,
+           "path": "csrc/parallel/exchange.cc a2a (H2D async, alltoall_base, D2H async, one stream sync)",
+           "results": res}
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
