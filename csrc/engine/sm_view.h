@@ -297,6 +297,19 @@ struct SmView {
     if (kStv > 2) st2 += j == 2 ? dd : 0ull;
     if (kStv > 3) st3 += j == 3 ? dd : 0ull;
   }
+  // k in [LO, HI) (sm.h SMState::sadd_r): only that range's words are
+  // selected, at compile time -- a single-word range is one masked add
+  template <uint32_t LO, uint32_t HI>
+  __device__ __forceinline__ void sadd_r(uint32_t k, uint64_t d) {
+    constexpr uint32_t j0 = LO >> 6, j1 = (HI - 1) >> 6;
+    static_assert(LO < HI && j1 < (uint32_t)kStv, "statistics range outside the register words");
+    const uint64_t dd = sv_lane() == (int)(k & 63u) ? d : 0ull;
+    const uint32_t j = k >> 6;
+    if constexpr (j0 <= 0 && 0 <= j1) st0 += (j0 == j1 || j == 0) ? dd : 0ull;
+    if constexpr (j0 <= 1 && 1 <= j1) st1 += (j0 == j1 || j == 1) ? dd : 0ull;
+    if constexpr (j0 <= 2 && 2 <= j1) st2 += (j0 == j1 || j == 2) ? dd : 0ull;
+    if constexpr (j0 <= 3 && 3 <= j1) st3 += (j0 == j1 || j == 3) ? dd : 0ull;
+  }
   __device__ __forceinline__ uint64_t sget(uint32_t k) const {
     const uint64_t m = stw_get(k >> 6);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, (int)(k & 63u));

@@ -302,8 +302,15 @@ struct alignas(16) SMState {
   SIM_HDI void sadd(uint32_t k, uint64_t d) { reinterpret_cast<uint64_t*>(&st)[k] += d; }
   SIM_HDI uint64_t sget(uint32_t k) const { return reinterpret_cast<const uint64_t*>(&st)[k]; }
   SIM_HDI void sset(uint32_t k, uint64_t v) { reinterpret_cast<uint64_t*>(&st)[k] = v; }
+  // a counter at a run-time index k in [LO, HI) (one counter array, e.g. the
+  // instruction class histogram): the GPU engine's register view touches
+  // only the register words of that range (sm_view.h)
+  template <uint32_t LO, uint32_t HI>
+  SIM_HDI void sadd_r(uint32_t k, uint64_t d) { sadd(k, d); }
 };
 #define SK(f) ((uint32_t)(offsetof(::asim::SMStats, f) / 8))
+// counter array `f` of n words, element i (run time)
+#define SADD_IN(s, f, n, i, d) (s).template sadd_r<SK(f), SK(f) + (n)>(SK(f) + (uint32_t)(i), (d))
 constexpr int kStatWords = (int)(sizeof(SMStats) / 8);
 static_assert(kStatWords <= 256, "SM statistics: up to four 64-lane register words on the GPU engine");
 SIM_HDI uint64_t* s_scratch_key(SMState& s) { return s.skey; }
@@ -614,7 +621,7 @@ SIM_HDI void l1_fill(S& s, const SmCtx& x, uint64_t line, uint8_t sectors, uint6
       s.sadd(SK(mf_lat_sum), lat);
       s.sadd(SK(mf_lat_n), 1);
       if (lat > s.sget(SK(mf_lat_max))) s.sset(SK(mf_lat_max), lat);
-      s.sadd(SK(mf_lat_hist) + (lat ? amin<int>(15, 31 - __builtin_clz(lat)) : 0), 1);
+      SADD_IN(s, mf_lat_hist, 16, lat ? amin<int>(15, 31 - __builtin_clz(lat)) : 0, 1);
     }
   }
   // wake waiters whose sectors are now all present (lane-parallel scan)
@@ -926,9 +933,9 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
     if (c.perfect_mem) {
       // ideal memory: loads/atomics return after the L1 latency, stores retire at once
       if (!is_store) {
-        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, uslot, 0)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+        if (!hit_push(s, now + c.l1_latency, (uint8_t)w, uslot, 0)) { SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_RES_FAIL, 1); break; }
       }
-      s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_HIT), 1);
+      SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_HIT, 1);
     } else if (is_store) {
       // write policy (reference data_cache wr_hit_* / wr_miss_*,
       // gpu-cache.cc:1229-1599); 'L' = write-back for local, write-evict for
@@ -936,9 +943,9 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
       uint8_t pol = g.wpolicy;
       if (pol == WP_LOCAL_WB_GLOBAL_WT) pol = in.space == S_LOCAL ? WP_WRITE_BACK : WP_WRITE_EVICT;
       if (bypass || pol == WP_READ_ONLY) {
-        if (!sm_can_send_n(s, c, wr_packets<S>(c, a.sectors))) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+        if (!sm_can_send_n(s, c, wr_packets<S>(c, a.sectors))) { SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_RES_FAIL, 1); break; }
         s.w_stores[w] += sm_send_write(s, c, a.line, a.sectors, a.bytes, w);
-        s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_BYPASS), 1);
+        SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_BYPASS, 1);
       } else {
         const uint32_t set = cache_set_index(g, a.line);
         int way = l1_find<P>(s, g, set, a.line);
@@ -955,19 +962,19 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
             L.dirty |= a.sectors;
             if (g.repl == REPL_LRU) L.lru = ++s.l1_stamp;
           } else {
-            if (!sm_can_send_n(s, c, wr_packets<S>(c, a.sectors))) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+            if (!sm_can_send_n(s, c, wr_packets<S>(c, a.sectors))) { SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_RES_FAIL, 1); break; }
             s.w_stores[w] += sm_send_write(s, c, a.line, a.sectors, a.bytes, w);
             L1Line& L = s.l1[set * g.assoc + way];
             if (pol == WP_WRITE_EVICT) L.valid &= (uint8_t)~a.sectors;
             else if (g.repl == REPL_LRU) L.lru = ++s.l1_stamp;
           }
-          s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_HIT), 1);
+          SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_HIT, 1);
         } else if (wa == 'N' || pol == WP_WRITE_EVICT) {
           // no write-allocate: straight to the L2
-          if (!sm_can_send_n(s, c, wr_packets<S>(c, a.sectors))) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+          if (!sm_can_send_n(s, c, wr_packets<S>(c, a.sectors))) { SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_RES_FAIL, 1); break; }
           s.w_stores[w] += sm_send_write(s, c, a.line, a.sectors, a.bytes, w);
           if (way >= 0 && pol == WP_WRITE_EVICT) s.l1[set * g.assoc + way].valid &= (uint8_t)~a.sectors;
-          s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_MISS), 1);
+          SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_MISS, 1);
         } else {
           // write-allocate: lazy fetch on read ('L'), fetch-on-write ('F'),
           // naive ('W': write and read the line)
@@ -977,7 +984,7 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
           if (fetch) mi = P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return s.mshr[i].valid && s.mshr[i].line == a.line; });
           const int mfree = fetch && mi < 0 ? P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return !s.mshr[i].valid; }) : 0;
           const uint32_t need = (send_wr ? wr_packets<S>(c, a.sectors) : 0u) + (fetch ? 1u : 0u) + 1u;  // + a possible dirty victim
-          if (!sm_can_send_n(s, c, need) || mfree < 0) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+          if (!sm_can_send_n(s, c, need) || mfree < 0) { SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_RES_FAIL, 1); break; }
           if (send_wr) s.w_stores[w] += sm_send_write(s, c, a.line, a.sectors, a.bytes, w);
           if (way < 0) {
             way = l1_victim<P>(s, g, set);
@@ -1010,14 +1017,14 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
               sm_send(s, c, P_RD, a.line, req, (uint16_t)(32 * popc64(req)), (uint32_t)mi);
             }
           }
-          s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_MISS), 1);
+          SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_MISS, 1);
         }
       }
     } else if (bypass) {
-      if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+      if (!sm_can_send(s, c)) { SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_RES_FAIL, 1); break; }
       uint32_t tag = 0x80000000u | ((uint32_t)uslot << 8) | w;
       sm_send(s, c, atomic ? P_ATOM : P_RD, a.line, a.sectors, a.bytes, tag);
-      s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_BYPASS), 1);
+      SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_BYPASS, 1);
     } else {
       P::prof(36);
       uint32_t set = cache_set_index(g, a.line);
@@ -1029,11 +1036,11 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
         P::prof(46);
         const bool pushed = hit_push(s, now + c.l1_latency, (uint8_t)w, uslot, 0);
         P::prof(3);
-        if (!pushed) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+        if (!pushed) { SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_RES_FAIL, 1); break; }
         if (g.repl == REPL_LRU) s.l1[set * g.assoc + way].lru = ++s.l1_stamp;
-        s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_HIT), 1);
+        SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_HIT, 1);
       } else {
-        if (s.n_pend >= (uint32_t)kMaxPend) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+        if (s.n_pend >= (uint32_t)kMaxPend) { SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_RES_FAIL, 1); break; }
         P::prof(37);
         int mi = P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return s.mshr[i].valid && s.mshr[i].line == a.line; });
         P::prof(3);
@@ -1045,16 +1052,16 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
         if (mi >= 0) need_req = fetch & (uint8_t)~s.mshr[mi].requested;
         bool merged = (mi >= 0 && need_req == 0);
         if (merged) {
-          if (s.mshr[mi].merges >= c.l1.mshr_merge) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+          if (s.mshr[mi].merges >= c.l1.mshr_merge) { SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_RES_FAIL, 1); break; }
           s.mshr[mi].merges++;
-          s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_MSHR_HIT), 1);
+          SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_MSHR_HIT, 1);
         } else {
-          if (!sm_can_send(s, c)) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+          if (!sm_can_send(s, c)) { SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_RES_FAIL, 1); break; }
           if (mi < 0) {
             P::prof(37);
             mi = P::find_first((int)c.l1.mshr_entries, [&](int i) -> bool { return !s.mshr[i].valid; });
             P::prof(3);
-            if (mi < 0) { s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_RES_FAIL), 1); break; }
+            if (mi < 0) { SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_RES_FAIL, 1); break; }
             s.mshr[mi].valid = 1;
             s.mshr[mi].line = a.line;
             s.mshr[mi].requested = 0;
@@ -1065,7 +1072,7 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
           P::prof(39);
           sm_send(s, c, P_RD, a.line, need_req, a.bytes, (uint32_t)mi);
           P::prof(3);
-          s.sadd(SK(l1) + (stype) * L1O_COUNT + (L1O_MISS), 1);
+          SADD_IN(s, l1, L1T_COUNT * L1O_COUNT, (stype) * L1O_COUNT + L1O_MISS, 1);
         }
         // register the waiter (first free entry)
         P::prof(38);
@@ -1350,8 +1357,8 @@ SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32
   // shader.cc:1911)
   s.sadd(SK(warp_insn), 1);
   s.sadd(SK(thread_insn), (uint64_t)popc64(in.mask));
-  s.sadd(SK(cls_insn) + (in.cls < OC_COUNT ? in.cls : OC_ALU), 1);
-  s.sadd(SK(sq_insn) + sq_class(in), 1);
+  SADD_IN(s, cls_insn, OC_COUNT, in.cls < OC_COUNT ? in.cls : OC_ALU, 1);
+  SADD_IN(s, sq_insn, 8, sq_class(in), 1);
   // LDC / s_load: an ALU-timed instruction with a constant-cache operand
   // (reference trace_driven.cc:255-261 keeps LDC an ALU op; shader.cc:3287)
   if (in.space == S_CONST) s.sadd(SK(power_acc) + PWR_CONST_OPERAND, 1);
@@ -1359,7 +1366,7 @@ SIM_HDI int sm_issue_one(S& s, const SmCtx& x, uint64_t now, uint32_t sc, uint32
   // scalar unit executes once per wave)
   {
     const uint32_t pk = (uint32_t)(in.flags >> 4);
-    if (pk) s.sadd(SK(power_acc) + pk, pk == PWR_SALU ? 1ull : (uint64_t)popc64(in.mask));
+    if (pk) SADD_IN(s, power_acc, 16, pk, pk == PWR_SALU ? 1ull : (uint64_t)popc64(in.mask));
   }
   s.last_progress = now;
   const uint32_t cta = P::uni((uint8_t)s.w_cta[w]);
@@ -1473,6 +1480,169 @@ SIM_HDI uint32_t stall_class(uint64_t mine, uint64_t valid_m, uint64_t sbok_m) {
   return !(valid_m & mine) ? 0u : !(sbok_m & mine) ? 1u : 2u;
 }
 
+// the scheduler picks of one cycle for the policies whose pick depends only
+// on the ready mask and the scheduler's own state (shared by both issue
+// paths): returns the picked warp, or -1
+template <class P, class S>
+SIM_HDI int sched_pick(const S& s, const SimCfg& c, uint64_t now, int nw, uint64_t cand, uint32_t last) {
+  switch (c.sched_policy) {
+    case SCHED_GTO:
+      if (last < (uint32_t)nw && (cand >> last & 1ull)) return (int)last;
+      [[fallthrough]];
+    case SCHED_OLDEST:
+      return P::argmin(nw, [&](int w) -> uint64_t {
+        return (cand >> w & 1ull) ? ((uint64_t)s.w_age[w] << 8 | (uint64_t)w) : ~0ull;
+      });
+    case SCHED_RRR: {
+      uint32_t start = (uint32_t)(now % (uint64_t)nw);
+      uint64_t r = rotr64(cand, start, (unsigned)nw);
+      return (int)mod_small((uint32_t)ffs64(r) + start, (uint32_t)nw);
+    }
+    default: {  // LRR: first ready warp after the last issued one
+      uint32_t start = mod_small(last + 1, (uint32_t)nw);
+      uint64_t r = rotr64(cand, start, (unsigned)nw);
+      return (int)mod_small((uint32_t)ffs64(r) + start, (uint32_t)nw);
+    }
+  }
+}
+
+SIM_HDI bool issue_special(const TInst& in) {
+  return in.cls == OC_EXIT || in.cls == OC_BARRIER || in.cls == OC_MEMBAR || in.cls == OC_NOP || (in.flags & F_WAITCNT);
+}
+
+// Lane-parallel issue (LRR / GTO / oldest / RRR, one instruction per warp per
+// cycle, no scheduler trace stream).  The schedulers pick exactly as in the
+// sequential loop below; then the picked warps issue together: lane w
+// applies its own warp's bookkeeping (stream position, instruction buffer,
+// in-flight count, load slot, scoreboard) instead of one scheduler after
+// another in wave-uniform code.  The result equals the sequential loop's:
+// schedulers own disjoint warps and ID_OC registers, the pipeline-register
+// ages are ranked in scheduler order, the statistics are sums, and the
+// instructions handled at issue (EXIT, barrier, fence, waitcnt, NOP -- they
+// touch CTA state shared by the schedulers) run afterwards, in scheduler
+// order, through sm_issue_one; they share no state with the pipeline issues.
+// (Reference scheduler_unit::cycle, shader.cc:1249-1556, runs the
+// schedulers one after another; so does sm_issue below for the other
+// policies.)
+template <class P, class S, class H>
+SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uint64_t ready, uint64_t live) {
+  const SimCfg& c = *x.cfg;
+  const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
+  const uint32_t nsched = c.n_sched ? c.n_sched : 1;
+  uint64_t valid_m = 0, sbok_m = 0;
+  bool classified = false;
+  uint32_t n_idle = 0, n_c0 = 0, n_c1 = 0, n_c2 = 0;
+  uint64_t picks = 0;
+  uint32_t pk_of = 0xffffffffu;  // byte sc: the warp scheduler sc picked (0xff: none)
+  for (uint32_t sc = 0; sc < nsched; ++sc) {
+    const uint64_t mine = c.sched_mask[sc];
+    const uint64_t cand = ready & mine;
+    if (!cand) {
+      if (live & mine) {
+        ++n_idle;
+        if (!classified) {
+          classified = true;
+          sm_stall_masks<P>(s, c, now, live, valid_m, sbok_m);
+        }
+        const uint32_t k = stall_class(mine, valid_m, sbok_m);
+        n_c0 += k == 0;
+        n_c1 += k == 1;
+        n_c2 += k == 2;
+      }
+      continue;
+    }
+    const uint32_t last = P::uni((uint32_t)s.sched_last[sc]);
+    const uint32_t w = P::uni((uint32_t)sched_pick<P>(s, c, now, nw, cand, last));
+    s.sched_last[sc] = w;
+    if (c.warp_issue_interval > 1) P::one([&] { s.w_issue_ok[w] = now + c.warp_issue_interval; });
+    pk_of = (pk_of & ~(0xffu << (8 * sc))) | w << (8 * sc);
+    picks |= 1ull << w;
+  }
+  if (n_idle) {
+    s.sadd(SK(issue_stall_idle), n_idle);
+    if (n_c0) s.sadd(SK(issue_distro) + 0, n_c0);
+    if (n_c1) s.sadd(SK(issue_distro) + 1, n_c1);
+    if (n_c2) s.sadd(SK(issue_distro) + 2, n_c2);
+  }
+  if (!picks) return;
+  s.last_progress = now;
+  s.sadd(SK(busy_cycles), 1);
+  const uint64_t spec = P::ballot_m(picks, [&](int w) -> bool { return issue_special(head.self(w)); });
+  // 1. the pipeline issues in scheduler order, wave-uniform: statistics, ages,
+  //    ID_OC registers (state that the per-warp step below does not touch)
+  uint32_t age = P::uni(s.age_ctr);
+  uint64_t idoc = P::uni(s.idoc_mask);
+  for (uint32_t sc = 0; sc < nsched; ++sc) {
+    const uint32_t w = (pk_of >> (8 * sc)) & 0xffu;
+    if (w == 0xffu) continue;
+    const TInst in = head.at((int)w);
+    SADD_IN(s, issue_distro, 3 + kMaxWarpLanes, 2u + (uint32_t)amin<int>(popc64(in.mask), kMaxWarpLanes), 1);
+    SADD_IN(s, single_issue, kMaxSched, sc, 1);
+    if (spec >> w & 1ull) continue;  // step 3
+    s.sadd(SK(warp_insn), 1);
+    s.sadd(SK(thread_insn), (uint64_t)popc64(in.mask));
+    SADD_IN(s, cls_insn, OC_COUNT, in.cls < OC_COUNT ? in.cls : OC_ALU, 1);
+    SADD_IN(s, sq_insn, 8, sq_class(in), 1);
+    if (in.space == S_CONST) s.sadd(SK(power_acc) + PWR_CONST_OPERAND, 1);
+    {
+      const uint32_t pk = (uint32_t)(in.flags >> 4);
+      if (pk) SADD_IN(s, power_acc, 16, pk, pk == PWR_SALU ? 1ull : (uint64_t)popc64(in.mask));
+    }
+    const uint32_t u = unit_of(c, in.cls);
+    const uint32_t kk = sc * U_COUNT + u;
+    TInst ri = in;
+    uint32_t lslot = 0xff;
+    if (in.cls == OC_LOAD) {
+      lslot = (uint32_t)ffs64((uint64_t)(uint8_t)~P::uni((uint8_t)s.w_slot_used[w]));
+      if (in.space != S_SHARED && in.width == 0) {
+        ri.space = S_SHARED;
+        ri.width = 1;
+      }
+    } else if (in.cls == OC_STORE && in.space != S_SHARED && in.width == 0) {
+      ri.space = S_SHARED;
+      ri.width = 1;
+    }
+    s.idoc_inst[kk] = ri;
+    s.idoc_meta[kk] = idoc_pack(w, lslot, ++age);
+    idoc |= 1ull << kk;
+  }
+  s.age_ctr = age;
+  s.idoc_mask = idoc;
+  // 2. every pipeline-issuing warp's own state, one lane per warp
+  P::each_m(picks & ~spec, [&](int w) {
+    const TInst in = head.self(w);
+    s.w_head[w] = s.w_head[w] + 1u;
+    s.w_ibuf[w] = (uint8_t)(s.w_ibuf[w] - 1u);
+    s.w_inflight[w] = (uint8_t)(s.w_inflight[w] + 1u);
+    const bool nomem = in.space != S_SHARED && in.width == 0;  // completes via the ring as an LDS op
+    if (in.cls == OC_LOAD) {
+      const uint8_t used = s.w_slot_used[w];
+      const uint32_t sl = (uint32_t)ffs64((uint64_t)(uint8_t)~used);
+      s.w_slot_used[w] = (uint8_t)(used | (1u << sl));
+      s.w_loads[w] = (uint16_t)(s.w_loads[w] + 1u);
+      uint32_t nacc = (in.space == S_SHARED) ? 1u : (uint32_t)in.width;
+      if (nacc == 0) nacc = 1;
+      s.w_slot_pend[w][sl] = (uint16_t)nacc;
+      s.w_slot_dst[w][sl][0] = in.dst[0];
+      s.w_slot_dst[w][sl][1] = in.dst[1];
+      if (nomem || in.space == S_SHARED || in.space == S_CONST) s.w_slot_lds[w] = (uint8_t)(s.w_slot_lds[w] | (1u << sl));
+    } else if (in.cls == OC_STORE && (nomem || in.space == S_SHARED)) {
+      s.w_lds_st[w] = (uint8_t)(s.w_lds_st[w] + 1u);
+    }
+    sbs(s.w_sb, (uint32_t)w, in.dst[0]);
+    sbs(s.w_sb, (uint32_t)w, in.dst[1]);
+  });
+  P::sync();
+  // 3. the instructions handled at issue, in scheduler order
+  if (spec) {
+    for (uint32_t sc = 0; sc < nsched; ++sc) {
+      const uint32_t w = (pk_of >> (8 * sc)) & 0xffu;
+      if (w == 0xffu || !(spec >> w & 1ull)) continue;
+      sm_issue_one<P>(s, x, now, sc, w, head.at((int)w), P::uni((uint32_t)s.w_head[w]));
+    }
+  }
+}
+
 template <class P, class S>
 SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   const SimCfg& c = *x.cfg;
@@ -1489,6 +1659,13 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   uint64_t ready = P::ballot_m(live, [&](int w) -> bool {
     return warp_can_issue_i(s, c, w, head.self(w), nsched, idoc_busy) && warp_issue_due(s, c, w, now);
   });
+  if ((c.sched_policy == SCHED_LRR || c.sched_policy == SCHED_GTO || c.sched_policy == SCHED_OLDEST ||
+       c.sched_policy == SCHED_RRR) &&
+      c.max_issue_per_warp <= 1 && !trace_sm_on(c, TS_WARP_SCHEDULER, s.id)) {
+    P::prof(29);
+    sm_issue_par<P>(s, x, now, head, ready, live);
+    return;
+  }
   // warps parked at a barrier / fence / exit (the reference's waiting()),
   // plus for the two-level scheduler those whose next instruction waits on
   // a long (memory) operation
@@ -1545,7 +1722,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
       if (live & mine) {
         s.sadd(SK(issue_stall_idle), 1);
         classify();
-        s.sadd(SK(issue_distro) + stall_class(mine, valid_m, sbok_m), 1);
+        SADD_IN(s, issue_distro, 3 + kMaxWarpLanes, stall_class(mine, valid_m, sbok_m), 1);
       }
       continue;
     }
@@ -1584,7 +1761,7 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
     const int u1 = sm_issue_one<P>(s, x, now, sc, w, in1, hidx);
     P::prof(29);
     issued_any = true;
-    s.sadd(SK(issue_distro) + 2u + (uint32_t)amin<int>(popc64(in1.mask), kMaxWarpLanes), 1);
+    SADD_IN(s, issue_distro, 3 + kMaxWarpLanes, 2u + (uint32_t)amin<int>(popc64(in1.mask), kMaxWarpLanes), 1);
     bool dual = false;
     // dual issue (reference scheduler_unit::cycle, shader.cc:1249-1556): the
     // warp's next buffered instruction issues in the same cycle if it is
@@ -1597,11 +1774,12 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
           warp_can_issue_i(s, c, (int)w, in2, nsched, P::uni(s.idoc_mask))) {
         sm_issue_one<P>(s, x, now, sc, w, in2, hidx + 1);
         s.sadd(SK(dual_issued), 1);
-        s.sadd(SK(issue_distro) + 2u + (uint32_t)amin<int>(popc64(in2.mask), kMaxWarpLanes), 1);
+        SADD_IN(s, issue_distro, 3 + kMaxWarpLanes, 2u + (uint32_t)amin<int>(popc64(in2.mask), kMaxWarpLanes), 1);
         dual = true;
       }
     }
-    s.sadd((dual ? SK(dual_issue) : SK(single_issue)) + sc, 1);
+    if (dual) SADD_IN(s, dual_issue, kMaxSched, sc, 1);
+    else SADD_IN(s, single_issue, kMaxSched, sc, 1);
   }
   if (issued_any) s.sadd(SK(busy_cycles), 1);
 }
@@ -1910,7 +2088,7 @@ SIM_HDI void sm_skip(S& s, const SimCfg& c, uint64_t k, uint64_t t) {
   for (uint32_t sc = 0; sc < nsched; ++sc) {
     if (live & c.sched_mask[sc]) {
       ++stalled;
-      s.sadd(SK(issue_distro) + stall_class(c.sched_mask[sc], valid_m, sbok_m), k);
+      SADD_IN(s, issue_distro, 3 + kMaxWarpLanes, stall_class(c.sched_mask[sc], valid_m, sbok_m), k);
     }
   }
   // uniform update by every lane (not P::one: on the GPU these fields may be

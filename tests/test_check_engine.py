@@ -14,6 +14,7 @@ def nw(tmp_path_factory):
     return rodinia.generate_suite(str(d), ["nw-rodinia-2.0-ft"])["nw-rodinia-2.0-ft"]
 
 
+@pytest.mark.slow
 def test_check_engine_self_consistent(native, nw):
     c = sim.simulate(nw, "QV100", engine="cpu")
     k = sim.simulate(nw, "QV100", engine="check", extra={"-sim_check_primary": "cpu", "-sim_check_interval": "300"})

@@ -55,6 +55,7 @@ def test_threads_state_image_and_power(apps, tmp_path):
     assert out["1"][1]
 
 
+@pytest.mark.slow
 def test_host_streamed_with_threads(tmp_path):
     """host-side trace streaming refills between epochs with the team parked
     at a barrier (thread 0 moves the window)"""

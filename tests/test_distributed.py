@@ -72,6 +72,7 @@ def test_linksim_local_properties(native):
     assert collectives.emulate(PARAMS, "Broadcast", S, [7])["finish_ps"] == [7]
 
 
+@pytest.mark.slow
 def test_packet_exchange_matches_local_emulation(native):
     cases = [("AllReduce", 8 << 20, [0, 0]), ("AllReduce", 8 << 20, [3_000_000, 0]),
              ("AllGather", 4 << 20, [0, 1_000_000]), ("Reduce", 2 << 20, [0, 0]), ("AllToAll", 4 << 20, [5, 9])]
@@ -246,6 +247,7 @@ def _dp_worker(rank, world, port, root, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.slow
 @pytest.mark.parametrize("traffic", ["link_only", "mem_traffic"])
 def test_dp_step_eight_ranks_match_in_process_emulation(native, tmp_path, traffic):
     """Eight gloo processes, one simulated GPU each, run unequal shards of a
@@ -294,6 +296,7 @@ def test_dp_step_eight_ranks_match_in_process_emulation(native, tmp_path, traffi
     assert len(copies) == (DP_KW["layers"] if traffic == "mem_traffic" else 0)
 
 
+@pytest.mark.slow
 def test_bench_eight_gloo_ranks_dp_step_matches_local_ranks(native, tmp_path):
     """The driver's multi-GPU bench shape on the CPU tier: torchrun with 8
     ranks, ``bench.py --gpus 8 --engine cpu --dist-backend gloo`` (one
@@ -366,6 +369,7 @@ def _loop_worker(rank, world, port, cases, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.slow
 def test_native_exchange_loop_matches_python_loop_eight_ranks(native):
     """The C++ epoch loop (csrc/parallel/exchange.cc, over the c10d
     ProcessGroup) and the Python loop give identical finish times on 8 gloo
@@ -436,6 +440,7 @@ def test_node_widen_offers_threads_to_the_gpu_critical_app(monkeypatch):
     assert sum(obj.threads.get(a, 1) for a, e in obj.assignment.items() if e == "cpu") <= 14
 
 
+@pytest.mark.slow
 def test_bench_eight_gloo_ranks_node_mode_runs_rank0_plan(tmp_path):
     """``bench.py --engine node`` on 8 gloo ranks with the GPU engine mocked
     by the CPU engine (ASIM_MOCK_GPU=1): every rank calibrates under its own

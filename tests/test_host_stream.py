@@ -82,6 +82,7 @@ def _diag(r, key):
     return int(m.group(1)) if m else None
 
 
+@pytest.mark.slow
 @pytest.mark.parametrize("extra", [{}, {"-sim_xcd": "8", "-sim_mall": "256:16"}], ids=["shared_l2", "xcd_mall"])
 def test_cpu_engine_streamed_equals_whole(text_app, extra):
     from accel_sim_framework_distributed_amd import _native, sim
@@ -123,6 +124,7 @@ def test_streamed_shuffled_trace_simulates_identically(text_app, tmp_path):
     assert _strip(a.stats) == _strip(b.stats)
 
 
+@pytest.mark.slow
 @pytest.mark.timeout(120)
 def test_malformed_streamed_trace_fails_cleanly_with_thread_team(text_app, tmp_path):
     """a streamed trace whose late thread block names a warp outside its block

@@ -15,6 +15,7 @@ def test_measured_l1_bandwidth_parsed():
     assert m == {4: 20.7, 8: 27.6, 16: 28.7}
 
 
+@pytest.mark.slow
 def test_data_path_limits_wide_loads():
     off = tuner.simulated_l1_bandwidth(TUNED, 0, widths=(16,))
     on = tuner.simulated_l1_bandwidth(TUNED, 48, widths=(16,))

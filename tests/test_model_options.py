@@ -156,6 +156,7 @@ def test_instruction_cache(native, traces):
     assert _stat(tiny.output, "L1I_total_cache_misses") > miss
 
 
+@pytest.mark.slow
 def test_dram_write_queue_and_turnaround(native, traces):
     """-dram_seperate_write_queue_enable with <size>:<high>:<low> watermarks
     (reference dram_sched.cc:118-130) and -dram_elimnate_rw_turnaround

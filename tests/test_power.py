@@ -115,6 +115,7 @@ def test_grouped_fit_shares_factors():
     assert np.allclose(A @ x, b, rtol=1e-6)
 
 
+@pytest.mark.slow
 def test_mi355x_power_validation_pipeline(native, tmp_path):
     """Synthetic CDNA traces of the ub_power kernels -> simulated component
     power -> grouped QP fit against the amd-smi measurements."""
@@ -140,6 +141,7 @@ def test_apply_factors_rescales_xml(tmp_path):
     assert p1["INT_ACC"] == pytest.approx(p0["INT_ACC"])
 
 
+@pytest.mark.slow
 def test_capped_fit_recovers_power_cap():
     # synthetic suite: linear model with known group factors, clipped at a cap
     rng = np.random.RandomState(3)

@@ -14,6 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 UBENCH = os.path.join(ROOT, "profiles", "ubench_mi355x")
 
 
+@pytest.mark.slow
 def test_tuner_from_measured_mi355x_logs(native, tmp_path):
     opts, meas, dev = tuner.parse_stats([UBENCH])
     assert dev == "AMD_Instinct_MI355X"

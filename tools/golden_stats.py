@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--check")
     ap.add_argument("--config", default="QV100")
     ap.add_argument("--apps", default="all")
+    ap.add_argument("--extra", default="", help="extra simulator flags, e.g. '-gpgpu_scheduler gto'")
     ap.add_argument("--trace-dir", default=os.path.join(tempfile.gettempdir(), "asim_golden_suite"))
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
     a = ap.parse_args()
@@ -49,7 +50,8 @@ def main():
         for args in sorted(os.listdir(d)):
             kl = os.path.join(d, args, "traces", "kernelslist.g")
             if os.path.exists(kl):
-                jobs.append((app, kl, a.config, None))
+                ex = a.extra.split()
+                jobs.append((app, kl, a.config, dict(zip(ex[0::2], ex[1::2])) or None))
     with ProcessPoolExecutor(a.j) as ex:
         res = dict(ex.map(_one, jobs))
     if a.out:
