@@ -15,6 +15,7 @@
 //   power_suite trace               every kernel once, at the same grid with a
 //                                   short loop (power is a rate), for the
 //                                   automatic ISA tracer (bin/isatrace/power_suite)
+#include <algorithm>
 #include <amd_smi/amdsmi.h>
 
 #include <atomic>
@@ -612,7 +613,11 @@ struct Sampler {
 };
 
 int main(int argc, char** argv) {
-  const bool trace = argc > 1 && !strcmp(argv[1], "trace");
+  // `time`: the traced sizes, each kernel's duration (median of 15 event-timed
+  // launches): the hardware side of the simulated cycles the power model
+  // turns into activity rates (power/mi355x_validation.py duration check)
+  const bool timing = argc > 1 && !strcmp(argv[1], "time");
+  const bool trace = (argc > 1 && !strcmp(argv[1], "trace")) || timing;
   const double secs = argc > 2 ? atof(argv[2]) : 1.5;
   int dev = 0;
   APP_HIP(hipGetDevice(&dev));
@@ -724,7 +729,31 @@ int main(int argc, char** argv) {
       {"int_fp_mix_occ2", [&] { k_int_fp<<<g(2), b>>>(sink, 8 * scv); }},
       {"sfu_fp32_mix_occ2", [&] { k_sfu_fp32<<<g(2), b>>>(sink, 8 * scv); }},
   };
-  if (trace) {
+  if (timing) {
+    hipEvent_t e0, e1;
+    APP_HIP(hipEventCreate(&e0));
+    APP_HIP(hipEventCreate(&e1));
+    printf("kernel,median_us,min_us\n");
+    for (auto& k : ks) {
+      for (int w = 0; w < 2; ++w) k.launch();
+      APP_HIP(hipDeviceSynchronize());
+      std::vector<float> t;
+      for (int r = 0; r < 15; ++r) {
+        APP_HIP(hipEventRecord(e0, 0));
+        k.launch();
+        APP_HIP(hipEventRecord(e1, 0));
+        APP_HIP(hipEventSynchronize(e1));
+        float ms = 0;
+        APP_HIP(hipEventElapsedTime(&ms, e0, e1));
+        t.push_back(ms * 1000.0f);
+      }
+      std::sort(t.begin(), t.end());
+      printf("%s,%.3f,%.3f\n", k.name, t[t.size() / 2], t[0]);
+      fflush(stdout);
+    }
+    APP_HIP(hipEventDestroy(e0));
+    APP_HIP(hipEventDestroy(e1));
+  } else if (trace) {
     for (auto& k : ks) {
       k.launch();
       APP_HIP(hipGetLastError());

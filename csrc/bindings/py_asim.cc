@@ -511,6 +511,11 @@ PYBIND11_MODULE(_asim, m) {
 
   py::class_<Simulator>(m, "Simulator")
       .def(py::init([](const std::vector<std::string>& args, bool echo) {
+             // construction parses the configuration and builds the engine
+             // (the GPU engine allocates and uploads every unit's state):
+             // without the GIL, so the node bench's worker threads set up
+             // their simulations concurrently
+             py::gil_scoped_release nogil;
              auto* s = new Simulator(args);
              s->set_echo(echo);
              return s;
@@ -519,7 +524,7 @@ PYBIND11_MODULE(_asim, m) {
       .def("run", &Simulator::run, py::call_guard<py::gil_scoped_release>())
       .def("run_command", &Simulator::run_command, py::call_guard<py::gil_scoped_release>())
       .def("num_commands", [](Simulator& s) { return s.commands().size(); })
-      .def("load_commands", &Simulator::load_commands)
+      .def("load_commands", &Simulator::load_commands, py::call_guard<py::gil_scoped_release>())
       .def("print_header", [](Simulator& s) { s.load_commands(); })
       .def_property_readonly("output", &Simulator::output)
       .def_property_readonly("tot_cycle", &Simulator::tot_cycle)

@@ -20,6 +20,7 @@
 #include <csignal>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -594,6 +595,105 @@ class CfgSlots {
   uint64_t used_ = 0;
 };
 
+
+// Process-wide caching allocator for the engine's device buffers, pinned
+// control words and streams.  hipFree / hipHostFree / hipStreamDestroy
+// synchronise the whole device: with several simulations sharing the GPU
+// (the node bench runs two GPU-engine applications at once, plus every
+// step's simulations are built and torn down again), one simulation's
+// teardown waited for the other's running engine_kernel launch -- a queued
+// application measured 0.084 s alone and 0.14-0.19 s inside the step.
+// Buffers go back to a free list keyed by their exact size and are handed to
+// the next simulation of that shape (the bench repeats the same shapes every
+// step); nothing is returned to the driver before the process exits.
+class DevicePool {
+ public:
+  static DevicePool& get() {
+    static DevicePool* p = new DevicePool();  // never destroyed: no frees during static teardown
+    return *p;
+  }
+  void* dev(size_t n) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto& v = dev_[n];
+      if (!v.empty()) {
+        void* q = v.back();
+        v.pop_back();
+        return q;
+      }
+    }
+    void* q = nullptr;
+    HIPCHECK(hipMalloc(&q, n ? n : 16));
+    std::lock_guard<std::mutex> g(mu_);
+    size_[q] = n;
+    return q;
+  }
+  void dev_free(void* q) {
+    if (!q) return;
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = size_.find(q);
+    if (it == size_.end()) {  // not ours (never happens): give it back
+      (void)hipFree(q);
+      return;
+    }
+    dev_[it->second].push_back(q);
+  }
+  void* host(size_t n) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto& v = host_[n];
+      if (!v.empty()) {
+        void* q = v.back();
+        v.pop_back();
+        return q;
+      }
+    }
+    void* q = nullptr;
+    HIPCHECK(hipHostMalloc(&q, n ? n : 16));
+    std::lock_guard<std::mutex> g(mu_);
+    hsize_[q] = n;
+    return q;
+  }
+  void host_free(void* q) {
+    if (!q) return;
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = hsize_.find(q);
+    if (it == hsize_.end()) {
+      (void)hipHostFree(q);
+      return;
+    }
+    host_[it->second].push_back(q);
+  }
+  hipStream_t stream() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (!streams_.empty()) {
+        hipStream_t s = streams_.back();
+        streams_.pop_back();
+        return s;
+      }
+    }
+    hipStream_t s = nullptr;
+    HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return s;
+  }
+  void stream_free(hipStream_t s) {
+    if (!s) return;
+    std::lock_guard<std::mutex> g(mu_);
+    streams_.push_back(s);
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<size_t, std::vector<void*>> dev_, host_;
+  std::map<void*, size_t> size_, hsize_;
+  std::vector<hipStream_t> streams_;
+};
+template <class T>
+void pool_alloc(T** p, size_t n) {
+  *p = static_cast<T*>(DevicePool::get().dev(n));
+}
+
 class GpuEngine : public Engine {
  public:
   ~GpuEngine() override {
@@ -601,8 +701,8 @@ class GpuEngine : public Engine {
       dump_profile();
     } catch (...) {
     }
-    if (d_prof_) (void)hipFree(d_prof_);
-    if (d_ework_) (void)hipFree(d_ework_);
+    DevicePool::get().dev_free(d_prof_);
+    DevicePool::get().dev_free(d_ework_);
     release();
     if (cfg_slot_ >= 0) CfgSlots::get().release(cfg_slot_);
   }
@@ -632,66 +732,66 @@ class GpuEngine : public Engine {
     const char* pe = getenv("ASIM_GPU_PROFILE");
     profiling_ = pe && *pe && *pe != '0';
     if (profiling_) {
-      HIPCHECK(hipMalloc(&d_prof_, sizeof(uint64_t) * nblocks_ * kProfSlots));
+      pool_alloc(&d_prof_, sizeof(uint64_t) * nblocks_ * kProfSlots);
       HIPCHECK(hipMemset(d_prof_, 0, sizeof(uint64_t) * nblocks_ * kProfSlots));
-      HIPCHECK(hipMalloc(&d_ework_, sizeof(uint32_t) * nblocks_));
+      pool_alloc(&d_ework_, sizeof(uint32_t) * nblocks_);
     }
-    HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    stream_ = DevicePool::get().stream();
     if (c_.trace_mask) {
       // debug trace buffers in HBM; the device copy of the config points at them
       const size_t units = (size_t)c.n_sm + c.n_mem;
-      HIPCHECK(hipMalloc(&d_trace_ev_, units * c_.trace_cap * sizeof(TraceEv)));
-      HIPCHECK(hipMalloc(&d_trace_cnt_, units * sizeof(uint32_t)));
+      pool_alloc(&d_trace_ev_, units * c_.trace_cap * sizeof(TraceEv));
+      pool_alloc(&d_trace_cnt_, units * sizeof(uint32_t));
       HIPCHECK(hipMemset(d_trace_cnt_, 0, units * sizeof(uint32_t)));
       c_.trace_ev = d_trace_ev_;
       c_.trace_cnt = d_trace_cnt_;
     }
-    HIPCHECK(hipMalloc(&d_cfg_, sizeof(SimCfg)));
+    pool_alloc(&d_cfg_, sizeof(SimCfg));
     upload_cfg();
     std::vector<SMState> hs(c.n_sm);
     for (uint32_t i = 0; i < c.n_sm; ++i) init_sm_state(hs[i], i);
     std::vector<ChanState> hc(c.n_mem);
     for (uint32_t i = 0; i < c.n_mem; ++i) init_chan_state(hc[i], i, c);
-    HIPCHECK(hipMalloc(&d_sms_, sizeof(SMState) * c.n_sm));
-    HIPCHECK(hipMalloc(&d_chs_, sizeof(ChanState) * c.n_mem));
+    pool_alloc(&d_sms_, sizeof(SMState) * c.n_sm);
+    pool_alloc(&d_chs_, sizeof(ChanState) * c.n_mem);
     HIPCHECK(hipMemcpy(d_sms_, hs.data(), sizeof(SMState) * c.n_sm, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(d_chs_, hc.data(), sizeof(ChanState) * c.n_mem, hipMemcpyHostToDevice));
-    HIPCHECK(hipMalloc(&d_pub_, sizeof(EpochPub)));
+    pool_alloc(&d_pub_, sizeof(EpochPub));
     HIPCHECK(hipMemset(d_pub_, 0, sizeof(EpochPub)));
     cap_req_ = c.icnt_latency;
     cap_rep_ = reply_cap(c);
     for (int p = 0; p < 2; ++p) {
       // mailboxes start zeroed (like the CPU engine's) so state images and
       // checkpoints never carry uninitialised device memory
-      HIPCHECK(hipMalloc(&d_box_req_[p], sizeof(Pkt) * c.n_subpart * c.n_sm * cap_req_));
+      pool_alloc(&d_box_req_[p], sizeof(Pkt) * c.n_subpart * c.n_sm * cap_req_);
       HIPCHECK(hipMemset(d_box_req_[p], 0, sizeof(Pkt) * c.n_subpart * c.n_sm * cap_req_));
-      HIPCHECK(hipMalloc(&d_cnt_req_[p], sizeof(uint32_t) * c.n_subpart * c.n_sm));
+      pool_alloc(&d_cnt_req_[p], sizeof(uint32_t) * c.n_subpart * c.n_sm);
       HIPCHECK(hipMemset(d_cnt_req_[p], 0, sizeof(uint32_t) * c.n_subpart * c.n_sm));
-      HIPCHECK(hipMalloc(&d_box_rep_[p], sizeof(Pkt) * c.n_sm * c.n_subpart * cap_rep_));
+      pool_alloc(&d_box_rep_[p], sizeof(Pkt) * c.n_sm * c.n_subpart * cap_rep_);
       HIPCHECK(hipMemset(d_box_rep_[p], 0, sizeof(Pkt) * c.n_sm * c.n_subpart * cap_rep_));
-      HIPCHECK(hipMalloc(&d_cnt_rep_[p], sizeof(uint32_t) * c.n_sm * c.n_subpart));
+      pool_alloc(&d_cnt_rep_[p], sizeof(uint32_t) * c.n_sm * c.n_subpart);
       HIPCHECK(hipMemset(d_cnt_rep_[p], 0, sizeof(uint32_t) * c.n_sm * c.n_subpart));
     }
     ovf_cap_ = backlog_cap(c);
-    HIPCHECK(hipMalloc(&d_ovf_, sizeof(Pkt) * c.n_subpart * (size_t)ovf_cap_));
+    pool_alloc(&d_ovf_, sizeof(Pkt) * c.n_subpart * (size_t)ovf_cap_);
     HIPCHECK(hipMemset(d_ovf_, 0, sizeof(Pkt) * c.n_subpart * (size_t)ovf_cap_));
     n_mall_ = (size_t)c.n_mem * mall_lines(c);
     if (n_mall_) {
-      HIPCHECK(hipMalloc(&d_mall_, sizeof(L2Line) * n_mall_));
+      pool_alloc(&d_mall_, sizeof(L2Line) * n_mall_);
       HIPCHECK(hipMemset(d_mall_, 0, sizeof(L2Line) * n_mall_));
     }
     if (c.link_contention && (icnt_link_count(c) > kMaxIcntLinks || !icnt_contention_fits(c, cap_req_, cap_rep_)))
       throw std::runtime_error("-icnt_link_contention: topology or mailboxes too large for the link pass");
     n_links_ = icnt_contention_on(c) ? (size_t)icnt_link_count(c) : 0;
     if (n_links_) {
-      HIPCHECK(hipMalloc(&d_links_, sizeof(uint64_t) * (n_links_ + 2)));
+      pool_alloc(&d_links_, sizeof(uint64_t) * (n_links_ + 2));
       HIPCHECK(hipMemset(d_links_, 0, sizeof(uint64_t) * (n_links_ + 2)));
       const size_t nrefs = (size_t)c.n_sm * c.n_subpart * std::max(cap_req_, cap_rep_);
-      HIPCHECK(hipMalloc(&d_link_refs_, sizeof(uint32_t) * nrefs));
+      pool_alloc(&d_link_refs_, sizeof(uint32_t) * nrefs);
     }
-    HIPCHECK(hipMalloc(&d_ctl_, sizeof(GpuCtl)));
-    HIPCHECK(hipHostMalloc(&h_ctl_, sizeof(GpuCtl)));
-    HIPCHECK(hipMalloc(&d_kt_, sizeof(KernelTab)));
+    pool_alloc(&d_ctl_, sizeof(GpuCtl));
+    h_ctl_ = static_cast<GpuCtl*>(DevicePool::get().host(sizeof(GpuCtl)));
+    pool_alloc(&d_kt_, sizeof(KernelTab));
     kt_ = KernelTab{};
     kt_.mix = c.concurrent_kernel_sm;
     epoch_ = 0;
@@ -1003,11 +1103,11 @@ class GpuEngine : public Engine {
   void power_arm(const PwrArm& arm) override {
     const uint32_t nunits = c_.n_sm + c_.n_mem;
     const uint32_t cap = epochs_per_launch_ + 2;  // at most one sample per epoch of a launch
-    if (!d_pw_) HIPCHECK(hipMalloc(&d_pw_, sizeof(PwrDev)));
-    if (!d_pw_rows_) HIPCHECK(hipMalloc(&d_pw_rows_, sizeof(double) * kPwrRawPad * nunits));
+    if (!d_pw_) pool_alloc(&d_pw_, sizeof(PwrDev));
+    if (!d_pw_rows_) pool_alloc(&d_pw_rows_, sizeof(double) * kPwrRawPad * nunits);
     if (pw_cap_ < cap) {
-      if (d_pw_ring_) HIPCHECK(hipFree(d_pw_ring_));
-      HIPCHECK(hipMalloc(&d_pw_ring_, sizeof(PwrSample) * cap));
+      DevicePool::get().dev_free(d_pw_ring_);
+      pool_alloc(&d_pw_ring_, sizeof(PwrSample) * cap);
       pw_cap_ = cap;
     }
     PwrDev h{};
@@ -1041,7 +1141,7 @@ class GpuEngine : public Engine {
   }
   void release() {
     auto fr = [](void* p) {
-      if (p) (void)hipFree(p);
+      DevicePool::get().dev_free(p);
     };
     fr(d_cfg_);
     fr(d_sms_);
@@ -1066,8 +1166,8 @@ class GpuEngine : public Engine {
     fr(d_pw_rows_);
     fr(d_pw_ring_);
     fr(d_kt_);
-    if (h_ctl_) (void)hipHostFree(h_ctl_);
-    if (stream_) (void)hipStreamDestroy(stream_);
+    DevicePool::get().host_free(h_ctl_);
+    DevicePool::get().stream_free(stream_);
   }
 
   SimCfg c_{};
@@ -1100,11 +1200,11 @@ class GpuEngine : public Engine {
     static constexpr bool kHost = false;
     void* alloc(size_t n) {
       void* p = nullptr;
-      HIPCHECK(hipMalloc(&p, n));
+      pool_alloc(&p, n);
       return p;
     }
     void free(void* p) {
-      if (p) (void)hipFree(p);
+      DevicePool::get().dev_free(p);
     }
     void write(void* d, const void* h, size_t n) { HIPCHECK(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); }
   };

@@ -340,6 +340,12 @@ struct SimCfg {
   // read by several XCDs is cached (and missed) in each of them.
   uint32_t n_xcd;
   uint32_t l1_wr_req_bytes;  // -sim_l1_write_request_bytes: 64 = a store is one request per 64 B half line
+  // -sim_single_valu: CDNA issues every vector ALU instruction -- integer,
+  // fp32, fp64, transcendental -- through the SIMD's one VALU (only MFMA has
+  // its own matrix core): the INT / DP / SFU classes share the SP unit of
+  // their scheduler, each at its own initiation interval, instead of running
+  // in separate pipelines next to each other as on an NVIDIA sub-core
+  uint32_t single_valu;
   uint32_t log2_spx;        // log2(sub-partitions per XCD)
   // -sim_mall <sets>:<assoc>: the memory-attached last-level cache (AMD
   // Infinity Cache / MALL) in front of every DRAM channel, sectored like the
@@ -467,6 +473,7 @@ SIM_HDI bool trace_mem_on(const SimCfg& c, uint32_t stream, uint32_t ch) {
 
 // ---- helpers shared by both engines ----
 SIM_HDI uint32_t unit_of(const SimCfg& c, uint8_t cls) {
+  if (c.single_valu && (cls == OC_SFU || cls == OC_DP || cls == OC_INTP)) return U_SP;
   switch (cls) {
     case OC_LOAD: case OC_STORE: case OC_MEMBAR: return U_MEM;
     case OC_SFU: return U_SFU;
