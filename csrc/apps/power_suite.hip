@@ -615,9 +615,12 @@ struct Sampler {
 int main(int argc, char** argv) {
   // `time`: the traced sizes, each kernel's duration (median of 15 event-timed
   // launches): the hardware side of the simulated cycles the power model
-  // turns into activity rates (power/mi355x_validation.py duration check)
-  const bool timing = argc > 1 && !strcmp(argv[1], "time");
-  const bool trace = (argc > 1 && !strcmp(argv[1], "trace")) || timing;
+  // turns into activity rates (power/mi355x_validation.py duration check);
+  // `time_full`: the same at the measured sizes (0.5-2 ms loops: the
+  // steady-state rate, launch overhead negligible)
+  const bool full = argc > 1 && !strcmp(argv[1], "time_full");
+  const bool timing = argc > 1 && (!strcmp(argv[1], "time") || full);
+  const bool trace = (argc > 1 && !strcmp(argv[1], "trace")) || (timing && !full);
   const double secs = argc > 2 ? atof(argv[2]) : 1.5;
   int dev = 0;
   APP_HIP(hipGetDevice(&dev));
