@@ -440,13 +440,39 @@ def disassemble(co: str) -> Listing:
         i, j = d.find(".amdhsa_kernel"), d.find(".end_amdhsa_kernel")
         if i < 0 or j < 0:
             raise BinaryError(f"{co}: kernel descriptor of {k} not decoded")
-        kds[k] = _kd_for_assembler(d[i:j + len(".end_amdhsa_kernel")])
+        kd = _kd_for_assembler(d[i:j + len(".end_amdhsa_kernel")])
+        if ".amdhsa_user_sgpr_count" not in kd:
+            # the decoder leaves the user-SGPR count implicit; the rewriter
+            # needs it to find the workgroup-id SGPRs: COMPUTE_PGM_RSRC2
+            # (descriptor byte 52) bits 1-5
+            ksym = next(s for s in syms if s.name == k + ".kd")
+            ro = secs[".rodata"]
+            rsrc2 = int.from_bytes(_section_bytes(co, ro)[ksym.addr - ro.addr + 52:ksym.addr - ro.addr + 56], "little")
+            head, rest = kd.split("\n", 1)
+            kd = f"{head}\n\t.amdhsa_user_sgpr_count {(rsrc2 >> 1) & 31}\n{rest}"
+        kds[k] = kd
     notes = _run([f"{LLVM}/llvm-readelf", "--notes", co])
     i = notes.find("---")
     j = notes.find("\n...", i)
     if i < 0:
         raise BinaryError(f"{co}: no AMDGPU metadata note")
     meta = notes[i:j + 4]  # readelf indents only the document marker
+    # the descriptor holds register counts rounded to the allocation granule;
+    # the metadata note keeps the compiler's exact ones (what the traces'
+    # "-nregs" and the rewriter's probe registers are derived from)
+    for blk in re.split(r"\n  - ", meta)[1:]:
+        m = re.search(r"\.name:\s+(\S+)", blk)
+        if not m or m.group(1) not in kds:
+            continue
+        sg = re.search(r"\.sgpr_count:\s+(\d+)", blk)
+        vg = re.search(r"\.vgpr_count:\s+(\d+)", blk)
+        ag = re.search(r"\.agpr_count:\s+(\d+)", blk)
+        kd = kds[m.group(1)]
+        if sg:
+            kd = re.sub(r"(\.amdhsa_next_free_sgpr\s+)\d+", lambda g: f"{g.group(1)}{max(0, int(sg.group(1)) - XNACK_SGPRS)}", kd)
+        if vg and (not ag or int(ag.group(1)) == 0):
+            kd = re.sub(r"(\.amdhsa_next_free_vgpr\s+)\d+", lambda g: f"{g.group(1)}{vg.group(1)}", kd)
+        kds[m.group(1)] = kd
     abi = 0
     for line in _run([f"{LLVM}/llvm-readelf", "-h", co]).splitlines():
         if "ABI Version" in line:

@@ -37,9 +37,9 @@ from typing import List, Sequence
 
 if __package__ in (None, ""):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-    from accel_sim_framework_distributed_amd.isatrace import rewrite  # noqa: E402
+    from accel_sim_framework_distributed_amd.isatrace import binary, rewrite  # noqa: E402
 else:
-    from . import rewrite
+    from . import binary, rewrite
 
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 LLVM = os.path.join(ROCM, "lib", "llvm", "bin")
@@ -67,11 +67,26 @@ def runtime_object(work: str, verbose: bool = False) -> str:
     return obj
 
 
-def instrument_source(src: str, work: str, flags: List[str], verbose: bool = False):
-    """Device half of one translation unit -> (fat binary path, kernel maps)."""
+def instrument_source(src: str, work: str, flags: List[str], verbose: bool = False, device_from: str = ""):
+    """Device half of one translation unit -> (fat binary path, kernel maps).
+    With `device_from` (a precompiled host binary, shared library, bundle or
+    code object) the device code is not compiled from `src`: the gfx950
+    code object found there is turned back into assembly
+    (isatrace/binary.py) and instrumented like compiler output -- the path
+    for kernels whose sources are not at hand."""
     base = os.path.join(work, os.path.splitext(os.path.basename(src))[0])
     asm = base + ".s"
-    _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "--cuda-device-only", "-S", src, "-o", asm] + flags, verbose)
+    if device_from:
+        cos = binary.extract(device_from, os.path.join(work, "device_from"))
+        if len(cos) != 1:
+            raise RuntimeError(f"{device_from}: {len(cos)} gfx950 code objects (expected one)")
+        lst = binary.disassemble(cos[0])
+        bad = binary.unsupported(lst)
+        if bad:
+            raise RuntimeError(f"{device_from}: cannot instrument: " + "; ".join(bad[:5]))
+        open(asm, "w").write(lst.asm())
+    else:
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "--cuda-device-only", "-S", src, "-o", asm] + flags, verbose)
     text = open(asm).read()
     # real instruction offsets from the uninstrumented code object
     _run([os.path.join(LLVM, "clang"), "-target", "amdgcn-amd-amdhsa", f"-mcpu={ARCH}", "-c", asm, "-o",
@@ -92,7 +107,7 @@ def instrument_source(src: str, work: str, flags: List[str], verbose: bool = Fal
 
 
 def build(sources: Sequence[str], out: str, flags: Sequence[str] = (), work: str = "", verbose: bool = False,
-          libs: Sequence[str] = ()) -> str:
+          libs: Sequence[str] = (), device_from: str = "") -> str:
     flags = list(flags)
     own = not work
     work = work or tempfile.mkdtemp(prefix="asim_isatrace_")
@@ -100,7 +115,7 @@ def build(sources: Sequence[str], out: str, flags: Sequence[str] = (), work: str
     try:
         host_objs, all_maps = [], []
         for src in sources:
-            fb, maps = instrument_source(src, work, flags, verbose)
+            fb, maps = instrument_source(src, work, flags, verbose, device_from)
             all_maps += maps
             ho = os.path.join(work, os.path.splitext(os.path.basename(src))[0] + ".host.o")
             _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "--cuda-host-only", "-Xclang",
@@ -128,8 +143,12 @@ def main(argv=None) -> int:
     ap.add_argument("-w", "--work_dir", default="", help="keep intermediate files here")
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("-L", "--libs", default="", help="extra link flags, e.g. '-lrccl'")
+    ap.add_argument("--device-from", default="",
+                    help="take the device code from this precompiled binary / code object instead of the source")
     o = ap.parse_args(argv)
-    build(o.sources, o.out, extra, o.work_dir, o.verbose, o.libs.split())
+    if o.device_from and len(o.sources) != 1:
+        ap.error("--device-from needs exactly one source (its host half)")
+    build(o.sources, o.out, extra, o.work_dir, o.verbose, o.libs.split(), o.device_from)
     print(f"built {o.out} (+ {o.out}.asimisa)")
     return 0
 

@@ -23,6 +23,8 @@ import sysconfig
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "accel_sim_framework_distributed_amd")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+# apps whose traced twin is also built from the precompiled binary alone (bin/isatrace_bin)
+BINARY_PATH_APPS = ("nw", "lud", "hotspot", "backprop")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
 CORE_SRC = [
@@ -92,6 +94,12 @@ def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
         f"  command = {sys.executable} {os.path.join(PKG, 'isatrace', 'build.py')} $in -o $out \"--libs=$libs\" -- "
         f"-munsafe-fp-atomics -fPIC -I{os.path.join(ROOT, 'csrc')}",
         "  description = HIPEXE $out",
+        # binary-only path: device code recovered from the precompiled app
+        # (isatrace/binary.py), host half from the source
+        "rule isatrace_bin",
+        f"  command = {sys.executable} {os.path.join(PKG, 'isatrace', 'build.py')} $src -o $out --device-from $in "
+        f"\"--libs=$libs\" -- -munsafe-fp-atomics -fPIC -I{os.path.join(ROOT, 'csrc')}",
+        "  description = HIPEXE-BIN $out",
     ]
     objs = []
     for s in CORE_SRC:
@@ -155,6 +163,13 @@ def write_ninja(cpu_only: bool, extra_targets: bool) -> str:
                     lines.append(f"build {tout}: isatrace {os.path.join(app_dir, fn)} | {hdr} {isa_deps}")
                     lines.append(f"  libs = {libs}")
                     defaults.append(tout)
+                    if fn[:-4] in BINARY_PATH_APPS:
+                        bout = os.path.join(ROOT, "bin", "isatrace_bin", fn[:-4])
+                        lines.append(f"build {bout}: isatrace_bin {out} | {os.path.join(app_dir, fn)} {hdr} {isa_deps} "
+                                     f"{os.path.join(PKG, 'isatrace', 'binary.py')}")
+                        lines.append(f"  src = {os.path.join(app_dir, fn)}")
+                        lines.append(f"  libs = {libs}")
+                        defaults.append(bout)
         # examples/<name>/main.hip -> bin/examples/<name>
         ex_dir = os.path.join(ROOT, "examples")
         if os.path.isdir(ex_dir):

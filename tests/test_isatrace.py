@@ -318,3 +318,39 @@ def test_isatrace_basic_block_vectors(tmp_path):
     assert all(rw[0] == 64 for rw in rows)
     m = re.findall(r"vecAdd.*?, (\d+), (\d+)$", (tmp_path / "stats.csv").read_text(), re.M)
     assert m and sum(sum(rw) for rw in rows) > 0
+
+
+def test_binary_path_instruments_identically():
+    """A precompiled app's code object, recovered to assembly by
+    isatrace/binary.py (no device source), instruments to exactly the code
+    and instruction map the source path produces."""
+    from accel_sim_framework_distributed_amd.isatrace import binary
+    for app in ("nw", "lud", "hotspot", "backprop"):
+        a, b = (os.path.join(ROOT, d, app) for d in ("bin/isatrace", "bin/isatrace_bin"))
+        if not (os.path.exists(a) and os.path.exists(b)):
+            pytest.skip("build_native.py builds bin/isatrace{,_bin}/*")
+        assert open(a + ".asimisa").read() == open(b + ".asimisa").read(), app
+        la = binary.disassemble(binary.extract(a, f"/tmp/asim_bin_cmp/{app}/a")[0])
+        lb = binary.disassemble(binary.extract(b, f"/tmp/asim_bin_cmp/{app}/b")[0])
+        assert [f.name for f in la.funcs] == [f.name for f in lb.funcs]
+        assert all(binary._insn_bytes(f) == binary._insn_bytes(g) for f, g in zip(la.funcs, lb.funcs)), app
+        assert la.kds == lb.kds, app
+
+
+@pytest.mark.gpu
+def test_binary_path_trace_equals_source_path(tmp_path):
+    """On the MI355X: the binary-only traced nw captures the same trace as the
+    source-built one."""
+    outs = []
+    for d in ("isatrace", "isatrace_bin"):
+        exe = os.path.join(ROOT, "bin", d, "nw")
+        assert os.path.exists(exe), "build_native.py builds bin/isatrace{,_bin}/nw"
+        td = tmp_path / d
+        env = dict(os.environ, ASIM_TRACE_DIR=str(td), ASIM_TRACE_BUF_MB="256")
+        r = subprocess.run([exe, "128", "10"], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(td)
+    ka = sorted(p.name for p in outs[0].glob("kernel-*.traceg"))
+    assert ka and ka == sorted(p.name for p in outs[1].glob("kernel-*.traceg"))
+    for k in ka:
+        assert _trace_body(str(outs[0] / k)) == _trace_body(str(outs[1] / k)), k
