@@ -15,4 +15,7 @@ cat $out/summary.txt | tail -40
 [ $e -eq 0 ] || exit $e
 # the power suite's kernels at the measured sizes (steady-state durations)
 cd /tmp && timeout -k 10 120 $R/bin/apps/power_suite time_full > $out/power_suite_time_full.csv 2> $out/power_suite_time_full.err
-e=$?; tail -3 $out/power_suite_time_full.csv; exit $e
+e=$?; tail -3 $out/power_suite_time_full.csv; [ $e -eq 0 ] || exit $e
+# binary-only traced nw == source-built traced nw (GPU test tier subset)
+cd $R && timeout -k 10 200 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+  tests/test_isatrace.py -k "binary_path" > $out/pytest_binary_path.log 2>&1; e=$?; tail -3 $out/pytest_binary_path.log; exit $e
