@@ -31,15 +31,27 @@ COMPONENT_PARAMS: Dict[str, List[str]] = {
     # calibration-only column: the LDS / L1 / L2 "unit in use" part of STATICP
     # (power trace column STATIC_MEMP); with it, STATICP is the core part
     "STATIC_MEMP": ["static_shared_flane", "static_l1_flane", "static_l2_flane"],
+    # calibration-only column: the core static power weighted by instruction
+    # issue instead of residency (power trace column STATIC_ISSUEP); its
+    # factor and STATICP's set the XML's static scale and static_issue_weight
+    "STATIC_ISSUEP": [],
 }
 # the components of the DVFS-aware calibration: the report's, with STATICP
 # split into core and memory-unit static power
-CAL_COMPONENTS: List[str] = list(COMPONENTS) + ["STATIC_MEMP"]
+CAL_COMPONENTS: List[str] = list(COMPONENTS) + ["STATIC_MEMP", "STATIC_ISSUEP"]
+# without the issue-weighted alternative (fits whose groups do not choose
+# between the two static columns)
+CAL_COMPONENTS_BASE: List[str] = list(COMPONENTS) + ["STATIC_MEMP"]
 
 
 def _comps(n: int) -> List[str]:
-    """The component list a row / factor vector of length n refers to."""
-    return CAL_COMPONENTS if n == len(CAL_COMPONENTS) else list(COMPONENTS)
+    """The component list a row / factor vector of length n refers to (records
+    from before the issue-weighted column have one calibration column)."""
+    if n == len(CAL_COMPONENTS):
+        return CAL_COMPONENTS
+    if n == len(COMPONENTS) + 1:
+        return list(COMPONENTS) + ["STATIC_MEMP"]
+    return list(COMPONENTS)
 
 
 def design_matrix(kernels: Sequence[Dict], components: Sequence[str] = COMPONENTS) -> np.ndarray:
@@ -238,10 +250,21 @@ def apply_factors(xml_in: str, xml_out: str, x: Sequence[float], components: Opt
         p["power_cap"] = float(power_cap)
     components = list(components) if components is not None else _comps(len(x))
     split = "STATIC_MEMP" in components
+    fx = dict(zip(components, (float(v) for v in x)))
+    issue = "STATIC_ISSUEP" in components and "STATICP" in components
     for c, f in zip(components, x):
         keys = COMPONENT_PARAMS.get(c)
         if keys is None:
-            keys = [k for k in p if k.startswith("static_") and not (split and k in COMPONENT_PARAMS["STATIC_MEMP"])]
+            keys = [k for k in p if k.startswith("static_") and k != "static_issue_weight"
+                    and not (split and k in COMPONENT_PARAMS["STATIC_MEMP"])]
+            if issue:
+                # core static = base x ((1 - w) busy + w issue); the fit scales
+                # the column pair (STATICP, STATIC_ISSUEP) = (core static,
+                # base x issue) by (f1, f2): base' = base (f1 + f2),
+                # w' = (f1 w + f2) / (f1 + f2)
+                f1, f2, w = fx["STATICP"], fx["STATIC_ISSUEP"], float(p.get("static_issue_weight", 0.0))
+                f = f1 + f2
+                p["static_issue_weight"] = (f1 * w + f2) / f if f > 0 else w
         for k in keys:
             p[k] = p.get(k, 1.0) * float(f)
     write_xml(xml_out, p, comment=f"calibrated from {xml_in}")
@@ -254,7 +277,7 @@ def apply_factors(xml_in: str, xml_out: str, x: Sequence[float], components: Opt
 # core dynamic power ~ s V^2, static and idle-core power ~ V, DRAM ~ s (its own
 # rail), the constant term fixed.  A row of A holds a kernel's component powers
 # simulated at the nominal clock; dvfs_scale() maps it to clock ratio s.
-_DVFS_V = ("STATICP", "IDLE_COREP", "STATIC_MEMP")
+_DVFS_V = ("STATICP", "IDLE_COREP", "STATIC_MEMP", "STATIC_ISSUEP")
 _DVFS_FIXED = ("CONSTP",)
 _DVFS_S = ("DRAMP", "MCP")
 
@@ -287,6 +310,10 @@ def dvfs_matrix(A: np.ndarray, ratios: Sequence[float], v_floor: float) -> np.nd
 UNIT_GROUPS: Dict[str, List[str]] = {
     "idle": ["CONSTP", "IDLE_COREP"],
     "static": ["STATICP"],
+    # the core static power of SMs that issue (vs. that merely hold waves):
+    # a latency-bound kernel keeps every CU resident and draws far less than
+    # a compute-bound one (power_suite l2_read 485 W vs fp32_fma 1313 W)
+    "static_issue": ["STATIC_ISSUEP"],
     "frontend": ["IBP", "ICP", "SCHEDP", "PIPEP", "RFP", "CCP"],
     "int": ["INTP", "INT_MULP", "INT_MUL24P", "INT_MUL32P", "INT_DIVP"],
     "fp": ["FPUP", "FP_DIVP", "FP_MULP", "FP_SQRTP", "FP_LGP", "FP_SINP", "FP_EXP"],

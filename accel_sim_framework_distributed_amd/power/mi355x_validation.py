@@ -336,7 +336,7 @@ def run_traces(kernelslist: str, measured_csv: str, work: str, out_xml: str, con
     order = list(meas)  # measure mode prints the kernels in launch order
     if len(reps) != len(order):
         raise RuntimeError(f"{len(reps)} simulated kernels vs {len(order)} measured")
-    A = calibrate.design_matrix(reps, calibrate.CAL_COMPONENTS)
+    A = calibrate.design_matrix(reps, calibrate.CAL_COMPONENTS_BASE)
     b = np.array([meas[n] for n in order])
     rows, meta = measured_rows(measured_csv)
     if all(not math.isnan(rows[n]["sclk"]) for n in order) and meta.get("power_cap_w", float("nan")) > 0:
@@ -383,14 +383,21 @@ def fit_heldout(A: np.ndarray, b: np.ndarray, order: List[str], sclk: List[float
     vi = [i for i, n in enumerate(order) if n not in cal]
     groups = calibrate.UNIT_GROUPS
     Ad = calibrate.dvfs_matrix(A, ratios, v_floor)
-    x = calibrate.fit_groups_relative(Ad[ci], b[ci], groups=groups, lower=1.0 / bound, upper=bound)
+    # the issue-weighted static column may be left out entirely (factor 0:
+    # the reference's residency-only static power); every other group is
+    # bounded to [1 / bound, bound]
+    free0 = {"static_issue"}
+    lower = np.array([0.0 if g in free0 else 1.0 / bound for g in groups])
+    x = calibrate.fit_groups_relative(Ad[ci], b[ci], groups=groups, lower=lower, upper=bound)
     pred = Ad @ x
-    before = Ad.sum(axis=1)
+    # uncalibrated: the base XML's model (the alternative static column off)
+    comps = calibrate._comps(Ad.shape[1])
+    before = Ad[:, [j for j, c in enumerate(comps) if c != "STATIC_ISSUEP"]].sum(axis=1)
     gf = calibrate.group_factors(x, groups)
-    at_bound = [g for g, v in gf.items() if v <= 1.0 / bound * 1.001 or v >= bound * 0.999]
+    at_bound = [g for g, v in gf.items() if (g not in free0 and v <= 1.0 / bound * 1.001) or v >= bound * 0.999]
     # groups no calibration kernel exercises keep factor 1 (reported)
-    undriven = [g for g in groups if not any(Ad[i, [calibrate.CAL_COMPONENTS.index(c) for c in groups[g]
-                                                    if c in calibrate.CAL_COMPONENTS]].sum() > 0 for i in ci)]
+    undriven = [g for g in groups if not any(Ad[i, [comps.index(c) for c in groups[g] if c in comps]].sum() > 0
+                                             for i in ci)]
     bv, pv = b[vi], pred[vi]
     return dict(kernels=list(order), calibration_kernels=[order[i] for i in ci],
                 heldout_kernels=[order[i] for i in vi], measured_w=b.tolist(), uncalibrated_w=before.tolist(),
@@ -402,7 +409,7 @@ def fit_heldout(A: np.ndarray, b: np.ndarray, order: List[str], sclk: List[float
                 groups_not_driven=undriven, power_cap_w=float(cap), max_sclk_mhz=float(fmax),
                 measured_sclk_mhz=sclk.tolist(), measured_clock_ratio=ratios.tolist(),
                 measured_vddgfx_mv=[float(v) for v in mv], v_floor=float(v_floor), v_floor_source=vsrc,
-                components=list(calibrate.CAL_COMPONENTS), components_w=np.asarray(A).tolist(), groups=groups,
+                components=list(comps), components_w=np.asarray(A).tolist(), groups=groups,
                 bounds=[1.0 / bound, bound],
                 model="per-unit factors fitted on single-unit kernels, validated on held-out mixes", _x=x)
 
@@ -464,7 +471,8 @@ def fit_report_dvfs(A: np.ndarray, b: np.ndarray, order: List[str], sclk: List[f
         if v_floor is None:
             v_floor, vsrc = DEFAULT_V_FLOOR, "assumed (no rail voltage reported by amd-smi)"
     s_min = float(max(0.3, min(1.0, np.nanmin(ratios) * 0.9)))
-    groups = calibrate.POWER_GROUPS if A.shape[1] == len(calibrate.CAL_COMPONENTS) else calibrate.FINE_GROUPS
+    split = A.shape[1] in (len(calibrate.CAL_COMPONENTS), len(calibrate.CAL_COMPONENTS_BASE))
+    groups = calibrate.POWER_GROUPS if split else calibrate.FINE_GROUPS
     kw = dict(groups=groups, lower=1.0 / bound, upper=bound)
     Ad = calibrate.dvfs_matrix(A, ratios, v_floor)
     x = calibrate.fit_groups_relative(Ad, b, **kw)
@@ -486,8 +494,7 @@ def fit_report_dvfs(A: np.ndarray, b: np.ndarray, order: List[str], sclk: List[f
                               loo_clock_ratio=s_gov.tolist(), fit_clock_ratio=gov_fit.tolist(),
                               clock_ratio_mae=float(np.mean(np.abs(s_gov - ratios))),
                               throttled_kernels=[n for n, r in zip(order, ratios) if r < 0.98]),
-                components=list(calibrate.CAL_COMPONENTS if A.shape[1] == len(calibrate.CAL_COMPONENTS)
-                                else calibrate.COMPONENTS), components_w=np.asarray(A).tolist(), groups=groups,
+                components=calibrate._comps(A.shape[1]), components_w=np.asarray(A).tolist(), groups=groups,
                 bounds=[1.0 / bound, bound], model="DVFS: measured cap and clocks, V(f) line", _x=x)
 
 

@@ -111,6 +111,7 @@ PwrCoef PowerModel::sampler_coef(double core_mhz) const {
   k.st_shared = param("static_shared_flane", 0);
   k.st_l1 = param("static_l1_flane", 0);
   k.st_l2 = param("static_l2_flane", 0);
+  k.st_issue_w = param("static_issue_weight", 0);
   return k;
 }
 
@@ -120,6 +121,7 @@ Activity PowerModel::activity_of(const PwrSample& s) {
   a.cycles = s.cycles;
   a.idle_sms = s.idle_sms;
   a.avg_lanes = s.lanes;
+  a.issue_frac = s.issue_frac;
   a.int_used = s.unit_mask & 1u;
   a.fp_used = s.unit_mask & 2u;
   a.dp_used = s.unit_mask & 4u;
@@ -137,6 +139,7 @@ PowerReport PowerModel::report_of(const PwrSample& o) {
   r.dynamic = o.dynamic;
   r.static_w = o.static_w;
   r.static_mem = o.static_mem;
+  r.static_issue = o.static_issue;
   r.constant = o.constant;
   r.idle = o.idle;
   r.total = o.total;
@@ -156,6 +159,7 @@ PowerReport PowerModel::compute(const Activity& a, double core_mhz, uint32_t n_s
   o.cycles = a.cycles;
   o.idle_sms = a.idle_sms;
   o.lanes = a.avg_lanes;
+  o.issue_frac = a.issue_frac >= 0 ? a.issue_frac : (n_sm ? std::max(0.0, 1.0 - a.idle_sms / n_sm) : 1.0);
   o.unit_mask = (a.int_used ? 1u : 0u) | (a.fp_used ? 2u : 0u) | (a.dp_used ? 4u : 0u) | (a.sfu_used ? 8u : 0u) |
                 (a.tex_used ? 16u : 0u) | (a.tensor_used ? 32u : 0u);
   pwr_power(k, k.coef, n_sm, v2, a.voltage * a.voltage, vr, o);
@@ -268,14 +272,16 @@ void PowerTracker::write_kernel(std::ostream& os, const std::string& header) con
 void PowerTracker::write_trace_header(std::ostream& os) const {
   os << "cycle,total_power";
   for (int i = 0; i < PC_COUNT; ++i) os << "," << kPwrCmpName[i];
-  // the memory-unit share of STATICP (calibration splits the static factor)
-  os << ",STATIC_MEMP\n";
+  // the memory-unit share of STATICP (calibration splits the static factor),
+  // and the core static power weighted by issue (the calibration's
+  // alternative column, csrc/power/power_eval.h pwr_power)
+  os << ",STATIC_MEMP,STATIC_ISSUEP\n";
 }
 
 void PowerTracker::write_trace_line(std::ostream& os, const PowerReport& r, uint64_t cycle) const {
   os << cycle << "," << r.total;
   for (int i = 0; i < PC_COUNT; ++i) os << "," << r.cmp[i];
-  os << "," << r.static_mem << "\n";
+  os << "," << r.static_mem << "," << r.static_issue << "\n";
 }
 
 void PowerTracker::write_steady(std::ostream& os, const std::string& kernel) const {

@@ -40,6 +40,7 @@ struct Activity {
   double cycles = 0;        // core cycles of the sample
   double idle_sms = 0;      // average idle SMs
   double avg_lanes = 0;     // average active threads per warp instruction
+  double issue_frac = -1;   // SM-cycles with an issue / (SMs x cycles); < 0: unknown (the residency fraction)
   double voltage = 1.0;
   // unit mix flags for the static category
   bool int_used = false, fp_used = false, dp_used = false, sfu_used = false, tex_used = false, tensor_used = false;
@@ -61,6 +62,7 @@ struct PowerReport {
   double dynamic = 0;
   double static_w = 0;
   double static_mem = 0;    // the part of static_w from the LDS / L1 / L2 "unit in use" terms
+  double static_issue = 0;  // core static power weighted by issue (calibration column STATIC_ISSUEP)
   double constant = 0;
   double idle = 0;
   double total = 0;

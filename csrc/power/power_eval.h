@@ -86,6 +86,7 @@ enum PwrRaw : int {
   PR_KIND0,  // + PWR_INT - 1 .. PWR_SALU - 1: issued lanes per unit kind
   PR_DRAM_RD = PR_KIND0 + (PWR_KINDS - 1), PR_DRAM_WR, PR_DRAM_PRE,
   PR_L2_RD_HIT, PR_L2_AT_HIT, PR_L2_RD_MISS, PR_L2_RD_MSHR, PR_L2_AT_MISS, PR_L2_WR_HIT, PR_L2_WR_MISS,
+  PR_BUSY,  // SM cycles with an instruction issued
   PR_COUNT
 };
 constexpr int kPwrRawPad = (PR_COUNT + 3) / 4 * 4;  // k-steps of 4 (f64 MFMA 16x16x4)
@@ -96,6 +97,7 @@ enum PwrSum : int {
   PS_RF_WR, PS_NOC,
   PS_KIND0,  // + kind - 1
   PS_DRAM_RD = PS_KIND0 + (PWR_KINDS - 1), PS_DRAM_WR, PS_DRAM_PRE, PS_L2_RH, PS_L2_RM, PS_L2_WH, PS_L2_WM,
+  PS_BUSY,
   PS_COUNT
 };
 constexpr int kPwrSumPad = (PS_COUNT + 15) / 16 * 16;  // column tiles of 16
@@ -124,6 +126,7 @@ SIM_HDI int pwr_sum_of(int r) {
     case PR_L2_RD_MISS: case PR_L2_RD_MSHR: case PR_L2_AT_MISS: return PS_L2_RM;
     case PR_L2_WR_HIT: return PS_L2_WH;
     case PR_L2_WR_MISS: return PS_L2_WM;
+    case PR_BUSY: return PS_BUSY;
     default: return -1;
   }
 }
@@ -137,6 +140,7 @@ SIM_HDI uint64_t pwr_raw_sm(const SMStats& s, int r) {
     case PR_THREAD: return s.thread_insn;
     case PR_MEMI: return s.mem_insn;
     case PR_ACTIVE: return s.active_cycles;
+    case PR_BUSY: return s.busy_cycles;
     case PR_L1_GR_HIT: return s.l1[L1T_GLOBAL_R][L1O_HIT];
     case PR_L1_LR_HIT: return s.l1[L1T_LOCAL_R][L1O_HIT];
     case PR_L1_GR_MISS: return s.l1[L1T_GLOBAL_R][L1O_MISS];
@@ -183,6 +187,10 @@ struct PwrCoef {
   double idle_core;
   double st_flane[7], st_addlane[7];  // static categories: light, cat1 .. cat6
   double st_shared, st_l1, st_l2;
+  // share of the core static power that follows instruction issue instead of
+  // residency (XML static_issue_weight; 0 = the reference's categorical
+  // static power of every SM with a live warp)
+  double st_issue_w;
 };
 
 // one power sample: the activity of the sample and its power
@@ -191,10 +199,12 @@ struct PwrSample {
   double cycles;
   double idle_sms;
   double lanes;  // active threads per warp instruction
+  double issue_frac;  // SM-cycles with an instruction issued / (SMs x cycles)
   double act[PA_COUNT];
   double dyn[PA_COUNT];
   double cmp[PC_COUNT];
   double dynamic, static_w, static_mem, constant, idle, total;
+  double static_issue;  // the core static power weighted by issue instead of residency (calibration column)
   uint32_t category;  // 0 light, 1..6 cat1..cat6
   uint32_t unit_mask;  // bit 0 int, 1 fp, 2 dp, 3 sfu, 4 tex, 5 tensor
 };
@@ -250,6 +260,8 @@ SIM_HDI void pwr_activity(const double* d, double cycles, uint32_t n_sm, PwrSamp
   o.unit_mask = um;
   double idle = cycles > 0 ? (double)n_sm - d[PS_ACTIVE] / cycles : 0;
   o.idle_sms = idle < 0 ? 0 : idle;
+  const double iss = (cycles > 0 && n_sm) ? d[PS_BUSY] / cycles / (double)n_sm : 0;
+  o.issue_frac = iss > 1 ? 1 : iss;
 }
 
 // step 3b: power of the sample.  `coef` is scaled for the sample's core clock;
@@ -277,13 +289,16 @@ SIM_HDI void pwr_power(const PwrCoef& k, const double* coef, uint32_t n_sm, doub
   o.category = cat;
   const double lanes = o.lanes > 1 ? o.lanes : 1;
   const double busy_frac = n_sm ? (1.0 - o.idle_sms / n_sm > 0.0 ? 1.0 - o.idle_sms / n_sm : 0.0) : 1.0;
-  double st = (k.st_flane[cat] + k.st_addlane[cat] * (lanes - 1)) * busy_frac;
+  const double st_base = k.st_flane[cat] + k.st_addlane[cat] * (lanes - 1);
+  const double w = k.st_issue_w;
+  double st = st_base * ((1.0 - w) * busy_frac + w * o.issue_frac);
   double smem = 0;
   if (o.act[PA_SHRD_ACC] > 0) smem += k.st_shared * busy_frac;
   if (o.act[PA_DC_RH] + o.act[PA_DC_RM] + o.act[PA_DC_WH] + o.act[PA_DC_WM] > 0) smem += k.st_l1 * busy_frac;
   if (o.act[PA_L2_RH] + o.act[PA_L2_RM] + o.act[PA_L2_WH] + o.act[PA_L2_WM] > 0) smem += k.st_l2;
   o.static_w = (st + smem) * vr;
   o.static_mem = smem * vr;
+  o.static_issue = st_base * o.issue_frac * vr;
   o.total = o.dynamic + o.static_w + o.constant + o.idle;
   for (int i = 0; i < PA_COUNT; ++i) o.cmp[pwr_cmp_of(i)] += o.dyn[i];
   o.cmp[PC_IDLE_CORE] = o.idle;
