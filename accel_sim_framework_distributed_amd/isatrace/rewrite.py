@@ -197,12 +197,30 @@ def reg_operands(ins: Inst) -> Tuple[List[str], List[str]]:
 
 # ----------------------------------------------------------------------------- parsing
 def parse_kernels(lines: Sequence[str]) -> Dict[str, Kernel]:
-    kernels: Dict[str, Kernel] = {}
     names = set()
     for ln in lines:
         s = ln.strip()
         if s.startswith(".amdhsa_kernel "):
             names.add(s.split()[1])
+    return parse_bodies(lines, names)
+
+
+_FUNC_TYPE = re.compile(r"^\s*\.type\s+([.\w$]+)\s*,\s*@function")
+
+
+def function_names(lines: Sequence[str]) -> set:
+    """Every symbol declared ``.type name,@function`` (kernels included)."""
+    out = set()
+    for ln in lines:
+        m = _FUNC_TYPE.match(ln)
+        if m:
+            out.add(m.group(1))
+    return out
+
+
+def parse_bodies(lines: Sequence[str], names) -> Dict[str, Kernel]:
+    """The instruction bodies of the named functions (label to .Lfunc_end)."""
+    kernels: Dict[str, Kernel] = {}
     i = 0
     while i < len(lines):
         m = _LABEL.match(lines[i])
@@ -224,9 +242,11 @@ def parse_kernels(lines: Sequence[str]) -> Dict[str, Kernel]:
     return kernels
 
 
-def segment(k: Kernel, lines: Sequence[str]) -> List[Tuple[int, str]]:
+def segment(k: Kernel, lines: Sequence[str], seg_base: int = 0, mem_base: int = 0) -> List[Tuple[int, str]]:
     """Assign segments and memory ids; return the kernel body as a list of
-    (kind, text) items: 'L' label line, 'I' instruction index, 'X' other."""
+    (kind, text) items: 'L' label line, 'I' instruction index, 'X' other.
+    Device functions number theirs from ``seg_base`` / ``mem_base`` (ids
+    shared by every kernel that may call them)."""
     body: List[Tuple[int, str]] = []
     idx = 0
     for ln in lines[k.start + 1:k.end]:
@@ -251,10 +271,10 @@ def segment(k: Kernel, lines: Sequence[str]) -> List[Tuple[int, str]]:
             seg += 1
             k.segments.append([])
             new = False
-        ins.seg = seg
+        ins.seg = seg_base + seg
         k.segments[seg - 1].append(kind)
         if is_vector_mem(ins.mnem):
-            ins.mem_id = k.n_mem
+            ins.mem_id = mem_base + k.n_mem
             k.n_mem += 1
         if is_branch(ins.mnem) or writes_exec(ins) or ins.mnem == "s_endpgm":
             new = True
@@ -633,53 +653,100 @@ class KernelMap:
     n_mem: int
     lds: int = 0              # static LDS bytes (group segment) of the original kernel
     vgprs: int = 32           # architected VGPRs per lane of the original kernel
+    # (symbol, first instruction index, count) of each body in `insts`: the
+    # kernel's own, then the device functions it may call (their PCs are
+    # code-object addresses above FUNC_PC_BASE, so they never alias the
+    # kernel's offsets in the simulator's instruction cache)
+    parts: List[Tuple[str, int, int]] = field(default_factory=list)
+
+
+FUNC_PC_BASE = 0x800000
 
 
 def instrument(asm: str) -> Tuple[str, List[KernelMap]]:
-    """Instrument every kernel of a gfx950 assembly file; returns the new
-    assembly and the static map of each kernel."""
+    """Instrument every kernel of a gfx950 assembly file -- and every device
+    function it may call -- and return the new assembly and the static map of
+    each kernel.  A code object with device functions uses one probe register
+    window for all of them (above every kernel's allocation, which covers its
+    call graph), so a callee's probes find the state its caller's entry set
+    up; function segments / memory records carry ids shared by every kernel."""
     lines = asm.split("\n")
     kernels = parse_kernels(lines)
     if not kernels:
         return asm, []
-    maps: List[KernelMap] = []
-    # process kernels from the bottom so earlier line indices stay valid
-    for name, k in sorted(kernels.items(), key=lambda kv: -kv[1].start):
-        body = segment(k, lines)
-        for ins in k.insts:
-            if ins.mnem.startswith(("s_swappc", "s_setpc", "s_call")):
-                raise RewriteError(f"{name}: device-function calls are not instrumented (inline them)")
+    fnames = function_names(lines) - set(kernels)
+    funcs = parse_bodies(lines, fnames) if fnames else {}
+    # descriptor facts and probe windows
+    info: Dict[str, Dict] = {}
+    for name in kernels:
         a, b = _descriptor_block(lines, name)
         nsg, _ = _dget(lines, a, b, ".amdhsa_next_free_sgpr")
         nvg, _ = _dget(lines, a, b, ".amdhsa_next_free_vgpr")
         acc, _ = _dget(lines, a, b, ".amdhsa_accum_offset", None)
         ucount, _ = _dget(lines, a, b, ".amdhsa_user_sgpr_count", 0)
         en = [(_dget(lines, a, b, f".amdhsa_system_sgpr_workgroup_id_{d}", 1 if d == "x" else 0)[0]) for d in "xyz"]
-        info, _ = _dget(lines, a, b, ".amdhsa_system_sgpr_workgroup_info", 0)
+        winfo, _ = _dget(lines, a, b, ".amdhsa_system_sgpr_workgroup_info", 0)
         lds, _ = _dget(lines, a, b, ".amdhsa_group_segment_fixed_size", 0)
         S = max(nsg, ucount + 4)
         S += S & 1
         arch_v = acc if acc is not None and acc < nvg else nvg
         n_agpr = nvg - acc if acc is not None and acc < nvg else 0
         V = arch_v + (arch_v & 1)
-        if S + N_PROBE_SGPR > MAX_SGPR:
-            raise RewriteError(f"{name}: uses {nsg} SGPRs, no room for the {N_PROBE_SGPR} probe SGPRs")
-        if V + N_PROBE_VGPR > MAX_ARCH_VGPR:
-            raise RewriteError(f"{name}: uses {arch_v} VGPRs, no room for the {N_PROBE_VGPR} probe VGPRs")
-        pr = Probe(S, V, str(len(maps)))
-        wg_sgprs = [ucount, ucount + 1, ucount + 2]
-        info_move = None
-        if info:
-            orig = ucount + sum(en)
-            if orig != ucount + 3:
-                info_move = (orig, ucount + 3)
-        # rebuild the body
+        info[name] = dict(nsg=nsg, nvg=nvg, acc=acc, ucount=ucount, en=en, winfo=winfo, lds=lds, S=S, V=V,
+                          arch_v=arch_v, n_agpr=n_agpr)
+    if funcs:
+        Sg = max(v["S"] for v in info.values())
+        Vg = max(v["V"] for v in info.values())
+        for v in info.values():
+            v["S"], v["V"] = Sg, Vg
+    for name, v in info.items():
+        if v["S"] + N_PROBE_SGPR > MAX_SGPR:
+            raise RewriteError(f"{name}: uses {v['nsg']} SGPRs, no room for the {N_PROBE_SGPR} probe SGPRs")
+        if v["V"] + N_PROBE_VGPR > MAX_ARCH_VGPR:
+            raise RewriteError(f"{name}: uses {v['arch_v']} VGPRs, no room for the {N_PROBE_VGPR} probe VGPRs")
+    # segments: each kernel's own from 1, then the functions' from one base
+    bodies: Dict[str, List[Tuple[int, str]]] = {}
+    for name, k in kernels.items():
+        bodies[name] = segment(k, lines)
+        for ins in k.insts:
+            if ins.mnem.startswith(("s_swappc", "s_call")) and not funcs:
+                raise RewriteError(f"{name}: calls a device function that is not in this file")
+            if ins.mnem.startswith("s_setpc"):
+                raise RewriteError(f"{name}: indirect branch ({ins.text})")
+    f0 = (max(len(k.segments) for k in kernels.values()) + 1) if funcs else 0
+    m0 = max(k.n_mem for k in kernels.values()) if funcs else 0
+    seg_next, mem_next = f0 - 1, m0
+    forder = sorted(funcs, key=lambda n: funcs[n].start)
+    for name in forder:
+        f = funcs[name]
+        bodies[name] = segment(f, lines, seg_next, mem_next)
+        seg_next += len(f.segments)
+        mem_next += f.n_mem
+    # rebuild every body from the bottom so earlier line indices stay valid
+    items = [(k.start, name, True) for name, k in kernels.items()] + [(f.start, name, False)
+                                                                       for name, f in funcs.items()]
+    ktag = {name: str(i) for i, name in enumerate(sorted(kernels, key=lambda n: -kernels[n].start))}
+    ftag = {name: f"f{i}" for i, name in enumerate(forder)}
+    for _, name, is_k in sorted(items, reverse=True):
+        k = kernels[name] if is_k else funcs[name]
+        if is_k:
+            v = info[name]
+            pr = Probe(v["S"], v["V"], ktag[name])
+        else:
+            pr = Probe(Sg, Vg, ftag[name])
         out: List[str] = []
         stubs: List[str] = []
         n = 0
         emitted_seg = 0
-        out += ["\t" + x if not x.endswith(":") else x for x in pr.entry(wg_sgprs, info_move)]
-        for kind, ln in body:
+        if is_k:
+            wg_sgprs = [v["ucount"], v["ucount"] + 1, v["ucount"] + 2]
+            info_move = None
+            if v["winfo"]:
+                orig = v["ucount"] + sum(v["en"])
+                if orig != v["ucount"] + 3:
+                    info_move = (orig, v["ucount"] + 3)
+            out += ["\t" + x if not x.endswith(":") else x for x in pr.entry(wg_sgprs, info_move)]
+        for kind, ln in bodies[name]:
             if kind >= 0:
                 ins = k.insts[kind]
                 if ins.seg != emitted_seg:
@@ -695,7 +762,10 @@ def instrument(asm: str) -> Tuple[str, List[KernelMap]]:
             out.append(ln)
         out += ["\t" + x if not x.endswith(":") else x for x in stubs]
         lines[k.start + 1:k.end] = out
+        if not is_k:
+            continue
         # descriptor (re-locate: the body above it changed size)
+        S, V, acc, n_agpr = v["S"], v["V"], v["acc"], v["n_agpr"]
         a, b = _descriptor_block(lines, name)
         b = _dset(lines, a, b, ".amdhsa_next_free_sgpr", S + N_PROBE_SGPR)
         new_arch = V + N_PROBE_VGPR
@@ -710,11 +780,26 @@ def instrument(asm: str) -> Tuple[str, List[KernelMap]]:
         # packed work-item ids (gfx90a+): x, y and z all land in v0
         b = _dset(lines, a, b, ".amdhsa_system_vgpr_workitem_id", 2)
         _fix_set_symbols(lines, name, S + N_PROBE_SGPR, new_arch)
-        maps.append(KernelMap(name, k.insts, k.segments, k.n_mem, lds, nvg))
+    # maps: a kernel's own segments, then (ids f0..) every function's
+    maps: List[KernelMap] = []
+    for name in sorted(kernels, key=lambda n: kernels[n].start):
+        k, v = kernels[name], info[name]
+        insts = list(k.insts)
+        segs = [list(sg) for sg in k.segments]
+        parts = [(name, 0, len(k.insts))]
+        if funcs:
+            segs += [[] for _ in range(f0 - 1 - len(k.segments))]
+            for fn in forder:
+                f = funcs[fn]
+                off = len(insts)
+                parts.append((fn, off, len(f.insts)))
+                insts += f.insts
+                segs += [[off + i for i in sg] for sg in f.segments]
+        maps.append(KernelMap(name, insts, segs, mem_next if funcs else k.n_mem, v["lds"], v["nvg"], parts))
     text = "\n".join(lines)
     text = _fix_metadata(text, {m.name for m in maps})
     text += _CTL_SYMBOL
-    return text, list(reversed(maps))
+    return text, maps
 
 
 _CTL_SYMBOL = """
@@ -732,12 +817,14 @@ __asim_tctl:
 def _fix_set_symbols(lines: List[str], name: str, nsgpr: int, nvgpr: int) -> None:
     for i, ln in enumerate(lines):
         s = ln.strip()
-        if s.startswith(f".set {name}.num_vgpr,"):
-            cur = int(s.split(",")[1], 0)
-            lines[i] = f"\t.set {name}.num_vgpr, {max(cur, nvgpr)}"
-        elif s.startswith(f".set {name}.numbered_sgpr,"):
-            cur = int(s.split(",")[1], 0)
-            lines[i] = f"\t.set {name}.numbered_sgpr, {max(cur, nsgpr)}"
+        for key, val in ((".num_vgpr", nvgpr), (".numbered_sgpr", nsgpr)):
+            head = f".set {name}{key},"
+            if s.startswith(head):
+                expr = s[len(head):].strip()
+                try:
+                    lines[i] = f"\t{head} {max(int(expr, 0), val)}"
+                except ValueError:  # a call graph's max(...) expression
+                    lines[i] = f"\t{head} max({expr}, {val})"
 
 
 def _fix_metadata(text: str, names: set) -> str:
@@ -778,13 +865,25 @@ def assign_pcs(maps: Sequence[KernelMap], disasm: str) -> None:
         if m and not m.group(1).startswith("."):
             cur.append(int(m.group(2), 16) - base)
     for km in maps:
-        pcs = starts.get(km.name)
-        if pcs and len(pcs) >= len(km.insts):
-            for ins, pc in zip(km.insts, pcs):
-                ins.pc = pc
-        else:
-            for i, ins in enumerate(km.insts):
-                ins.pc = 4 * i
+        # device functions: packed above FUNC_PC_BASE in their file order,
+        # each at a 256 B boundary past the previous one's code (independent
+        # of how the object laid them out, so a function recovered from a
+        # linked binary gets the PCs its source-built twin gets)
+        fbase = FUNC_PC_BASE
+        for part, (sym, i0, n) in enumerate(km.parts or [(km.name, 0, len(km.insts))]):
+            pcs = starts.get(sym)
+            add = 0 if part == 0 else fbase
+            if part:
+                # the body's own instructions (the disassembly also lists the
+                # alignment padding after it)
+                fbase += ((pcs[n - 1] + 8 if pcs and len(pcs) >= n and n else 4 * n) + 255) // 256 * 256
+            body = km.insts[i0:i0 + n]
+            if pcs and len(pcs) >= len(body):
+                for ins, pc in zip(body, pcs):
+                    ins.pc = add + pc
+            else:
+                for i, ins in enumerate(body):
+                    ins.pc = add + 4 * i
 
 
 def trace_mnemonic(ins: Inst) -> str:

@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "accel_sim_framework_distributed_amd")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 # apps whose traced twin is also built from the precompiled binary alone (bin/isatrace_bin)
-BINARY_PATH_APPS = ("nw", "lud", "hotspot", "backprop")
+BINARY_PATH_APPS = ("nw", "lud", "hotspot", "backprop", "devcalls")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
 CORE_SRC = [

@@ -325,7 +325,7 @@ def test_binary_path_instruments_identically():
     isatrace/binary.py (no device source), instruments to exactly the code
     and instruction map the source path produces."""
     from accel_sim_framework_distributed_amd.isatrace import binary
-    for app in ("nw", "lud", "hotspot", "backprop"):
+    for app in ("nw", "lud", "hotspot", "backprop", "devcalls"):
         a, b = (os.path.join(ROOT, d, app) for d in ("bin/isatrace", "bin/isatrace_bin"))
         if not (os.path.exists(a) and os.path.exists(b)):
             pytest.skip("build_native.py builds bin/isatrace{,_bin}/*")
@@ -354,3 +354,44 @@ def test_binary_path_trace_equals_source_path(tmp_path):
     assert ka and ka == sorted(p.name for p in outs[1].glob("kernel-*.traceg"))
     for k in ka:
         assert _trace_body(str(outs[0] / k)) == _trace_body(str(outs[1] / k)), k
+
+
+def test_device_functions_are_instrumented():
+    """A kernel that calls device functions: the functions get probes with the
+    kernel's register window and segment ids shared by every kernel, the
+    kernel's map holds the functions' segments, their PCs sit above
+    FUNC_PC_BASE."""
+    m = open(os.path.join(ROOT, "bin", "isatrace", "devcalls.asimisa")).read() \
+        if os.path.exists(os.path.join(ROOT, "bin", "isatrace", "devcalls.asimisa")) else None
+    if m is None:
+        pytest.skip("build_native.py builds bin/isatrace/devcalls")
+    lines = m.split("\n")
+    assert sum(1 for ln in lines if ln.startswith("K ")) == 1
+    pcs = [int(ln.split()[0], 16) for ln in lines if ln and ln[0] not in "KSA"]
+    assert any(pc >= rewrite.FUNC_PC_BASE for pc in pcs) and any(pc < rewrite.FUNC_PC_BASE for pc in pcs)
+    assert any("s_swappc_b64" in ln for ln in lines) and any("s_setpc_b64" in ln for ln in lines)
+
+
+@pytest.mark.gpu
+def test_device_function_trace_matches_counters(tmp_path):
+    """On the MI355X: the traced devcalls computes the right answer, and the
+    trace's instruction counts per SQ class (kernel + called functions) equal
+    rocprofv3 SQ_INSTS_* of the plain build."""
+    exe = os.path.join(ROOT, "bin", "isatrace", "devcalls")
+    plain = os.path.join(ROOT, "bin", "apps", "devcalls")
+    assert os.path.exists(exe) and os.path.exists(plain), "build_native.py builds bin/{apps,isatrace}/devcalls"
+    td = tmp_path / "trace"
+    env = dict(os.environ, ASIM_TRACE_DIR=str(td), ASIM_TRACE_BUF_MB="128")
+    r = subprocess.run([exe, "4096"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stdout[-1000:] + r.stderr[-2000:]
+    pmc = tmp_path / "pmc"
+    ctr = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH",
+           "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"]
+    r = subprocess.run(["rocprofv3", "--pmc"] + ctr + ["--output-format", "csv", "-d", str(pmc), "-o", "run", "--",
+                                                       plain, "4096"],
+                       cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), capture_output=True, text=True, timeout=90)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = verify.compare(str(td), str(pmc))
+    assert res["kernels"] == 1
+    for c, v in res["total"].items():
+        assert v["trace"] == v["hw"], (c, v)
