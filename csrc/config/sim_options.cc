@@ -131,6 +131,9 @@ const OptDef kOptions[] = {
     {"-gpgpu_l1_banks", 'u', "1", "L1 banks"},
     {"-sim_l1_port_bytes", 'u', "0", "vector L1 data path bytes per cycle (0: off, l1_banks accesses per cycle)"},
     {"-sim_l1_addr_lanes_per_cycle", 'u', "0", "vector L1 address stage lanes per cycle (0: off)"},
+    {"-sim_l1_port_granule", 'u', "0",
+     "vector L1 data path unit: 32 = whole sectors, 64 = whole 64 B halves of each line an access touches "
+     "(0: the bytes the lanes touch)"},
     {"-sim_lds_port_bytes", 'u', "0", "LDS data path bytes per cycle (0: off, the bank-conflict degree only)"},
     {"-sim_lds_lanes_per_cycle", 'u', "0", "LDS address lanes per cycle (0: off)"},
     {"-gpgpu_l1_banks_byte_interleaving", 'u', "32", ""},
@@ -818,6 +821,9 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.l1_banks = std::max<uint32_t>(1, (uint32_t)r.getu("-gpgpu_l1_banks"));
   c.l1_port_bytes = (uint32_t)r.getu("-sim_l1_port_bytes");
   c.l1_addr_lanes = (uint32_t)r.getu("-sim_l1_addr_lanes_per_cycle");
+  c.l1_port_granule = (uint32_t)r.getu("-sim_l1_port_granule");
+  if (c.l1_port_granule && c.l1_port_granule != 32 && c.l1_port_granule != 64)
+    throw OptionError("-sim_l1_port_granule must be 0, 32 or 64");
   c.lds_port_bytes = (uint32_t)r.getu("-sim_lds_port_bytes");
   c.lds_lanes = (uint32_t)r.getu("-sim_lds_lanes_per_cycle");
   c.gmem_skip_l1 = r.getb(user_set("-gmem_skip_L1D") ? "-gmem_skip_L1D" : "-gpgpu_gmem_skip_L1D") ? 1 : 0;

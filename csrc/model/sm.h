@@ -1099,7 +1099,10 @@ SIM_HDI void sm_ldst(S& s, const SmCtx& x, uint64_t now) {
       // miss's fill later: charged here, once per access)
       const uint32_t pf = P::uni(u.port_free);
       const uint32_t from = (int32_t)(pf - (uint32_t)now) > 0 ? pf : (uint32_t)now;
-      u.port_free = from + ((uint32_t)(a.bytes ? a.bytes : 1u) + c.l1_port_bytes - 1) / c.l1_port_bytes;
+      uint32_t pb = a.bytes ? a.bytes : 1u;
+      if (c.l1_port_granule == 32) pb = 32u * (uint32_t)popc64(a.sectors);
+      else if (c.l1_port_granule == 64) pb = 64u * (((a.sectors & 3u) != 0) + ((a.sectors & 12u) != 0));
+      u.port_free = from + (pb + c.l1_port_bytes - 1) / c.l1_port_bytes;
     }
     banks_used |= bbit;
     unext++;
