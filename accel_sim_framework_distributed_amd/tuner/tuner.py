@@ -187,6 +187,22 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
                          f" B/clk/CU: mean error {100 * fits[(port, lanes)]:.0f} % (no limit: {100 * err0:.0f} %)")
         except (ValueError, RuntimeError) as e:
             notes.append(f"{'LDS' if lds else 'L1'} data-path fit skipped: {e}")
+    # vector-L1 data-path unit: ub_l1_stride times 4-byte loads whose lanes
+    # are 4..128 B apart; the granule (touched bytes / 32 B sectors / 64 B
+    # halves) whose per-load cycles at the fitted port width match best
+    stride_meas = {int(k.split("_")[2]): float(v) for k, v in meas.items()
+                   if k.startswith("l1_stride_") and k.endswith("_cycles_per_load") and k.split("_")[2].isdigit()}
+    port = int(cfg.get("-sim_l1_port_bytes", "0") or 0)
+    if stride_meas and port:
+        g, err, errs = fit_l1_port_granule(stride_meas, port)
+        cfg["-sim_l1_port_granule"] = str(g)
+        applied["-sim_l1_port_granule"] = str(g)
+        presets.write_config(cfg, out, power_preset=base)
+        notes.append(f"-sim_l1_port_granule {g}: ub_l1_stride cycles per 4-byte wave-load at lane strides " +
+                     ", ".join(f"{k} B {stride_meas[k]:.1f}" for k in sorted(stride_meas)) +
+                     f" against the data stage's prediction at {port} B/clk: mean error {100 * err:.0f} % "
+                     f"(touched bytes {100 * errs[0]:.0f} %, sectors {100 * errs[32]:.0f} %, "
+                     f"64 B halves {100 * errs[64]:.0f} %)")
     with open(os.path.join(out, "TUNING.md"), "w") as f:
         f.write(f"# Tuned configuration for {device}\n\nBase preset: {base}\n\n")
         f.write("| option | tuned value | preset value |\n|---|---|---|\n")
@@ -200,6 +216,40 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
             for k in sorted(meas):
                 f.write(f"- {k}: {meas[k]}\n")
     return out, applied
+
+
+def l1_data_cycles(stride: int, port: int, granule: int, lanes: int = 64, width: int = 4) -> float:
+    """Data-stage cycles of one wave-load of `width`-byte lanes `stride` bytes
+    apart (csrc/model/sm.h, -sim_l1_port_bytes / -sim_l1_port_granule)."""
+    touched: Dict[int, int] = {}
+    for l in range(lanes):
+        a = l * stride
+        for b in range(a, a + width):
+            touched.setdefault(b // 128, 0)
+            touched[b // 128] |= 1 << ((b % 128) // 32)
+    cyc = 0
+    for line, sec in touched.items():
+        used = sum(1 for l in range(lanes) if (l * stride) // 128 == line) * width
+        if granule == 32:
+            pb = 32 * bin(sec).count("1")
+        elif granule == 64:
+            pb = 64 * ((1 if sec & 3 else 0) + (1 if sec & 12 else 0))
+        else:
+            pb = min(used, 128)
+        cyc += -(-pb // port)
+    return float(cyc)
+
+
+def fit_l1_port_granule(meas: Dict[int, float], port: int) -> Tuple[int, float, Dict[int, float]]:
+    """(granule, mean relative error, {granule: error}) of the data-stage unit
+    closest to ub_l1_stride's cycles per wave-load (strides beyond dense only:
+    the dense load also pays the address stage)."""
+    errs = {}
+    for g in (0, 32, 64):
+        pts = [(st, c) for st, c in meas.items() if st > 4]
+        errs[g] = sum(abs(l1_data_cycles(st, port, g) / c - 1.0) for st, c in pts) / max(1, len(pts))
+    best = min(errs, key=errs.get)
+    return best, errs[best], errs
 
 
 def measured_l1_bandwidth(stats_paths: List[str], key: str = "l1_bw") -> Dict[int, float]:

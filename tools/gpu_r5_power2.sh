@@ -7,7 +7,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-out=$R/gpurun_out/power_r5b
+out=$R/gpurun_out/${POWER_OUT:-power_r5b}
 mkdir -p $out
 cd /tmp
 rm -rf /tmp/pwr_traces
