@@ -187,6 +187,24 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
                          f" B/clk/CU: mean error {100 * fits[(port, lanes)]:.0f} % (no limit: {100 * err0:.0f} %)")
         except (ValueError, RuntimeError) as e:
             notes.append(f"{'LDS' if lds else 'L1'} data-path fit skipped: {e}")
+    # L1-miss return path: ub_l2_release's same-kernel pointer chase (L1
+    # misses that hit the L2) lasts l2_same_kernel_latency; the simulated twin
+    # of the chase gives the L2 round trip alone.  The gap is reported, not
+    # closed: a fixed per-miss return stage of that size
+    # (-sim_l1_miss_return_latency) makes the twin match but costs the suite
+    # correlation 1.6 points (latency-bound streamcluster +31 %; round 5,
+    # profiles/correlation/README.md), so the missing cycles are no fixed
+    # pipeline stage of every miss
+    if "l2_same_kernel_latency" in meas:
+        try:
+            target = float(meas["l2_same_kernel_latency"])
+            cold0, warm0 = simulated_chase_latency(out)
+            cold_note = f"; cold chase {cold0:.0f} against {meas['l2_cold_latency']}" if "l2_cold_latency" in meas else ""
+            notes.append(f"L2-hit pointer chase: simulated {warm0:.0f} cycles per load against the measured "
+                         f"{target:.0f}{cold_note} (-sim_l1_miss_return_latency {max(0, int(round(target - warm0)))} "
+                         f"would close it; left at 0, see profiles/correlation/README.md)")
+        except (ValueError, RuntimeError) as e:
+            notes.append(f"L2-hit chase check skipped: {e}")
     # vector-L1 data-path unit: ub_l1_stride times 4-byte loads whose lanes
     # are 4..128 B apart; the granule (touched bytes / 32 B sectors / 64 B
     # halves) whose per-load cycles at the fitted port width match best
@@ -321,6 +339,34 @@ def simulated_l1_bandwidth(config_dir: str, port: int, widths=(4, 8, 16), per_cu
             byts.append(g.nwarps * n * ws * w)
         out[w] = (byts[1] - byts[0]) / max(1, cyc[1] - cyc[0]) / n_cu
     return out
+
+
+def simulated_chase_latency(config_dir: str, extra: Sequence[str] = (), nodes: int = 512) -> Tuple[float, float]:
+    """(cold, warm) cycles per load of one lane's dependent pointer chase
+    over `nodes` 128 B lines (beyond the L1, inside the L2), the twin of
+    ub_l2_release: the first walk from cold memory, later walks L2 hits."""
+    import tempfile
+    from .. import _native
+    from ..tracegen import rodinia
+    from ..tracegen.builder import KernelBuilder
+    d = tempfile.mkdtemp(prefix="asim_chase_")
+    addrs = [0x7000_0000 + ((i * 37) % nodes) * 128 for i in range(nodes)]
+    cyc = {}
+    for passes in (1, 2, 3):
+        k = KernelBuilder("ub_chase", (1, 1, 1), (64, 1, 1), nregs=32, shmem=0, binary_version=950, warp_size=64)
+        for _ in range(passes):
+            for a in addrs:
+                k.op("global_load_dword", [4], [4], base=a, stride=0, mask=1)
+        k.op("s_endpgm")
+        kl = rodinia.write_app(os.path.join(d, f"p{passes}"), [k.build()], memcpy=False)
+        args = ["-config", os.path.join(config_dir, "gpgpusim.config"), "-config",
+                os.path.join(config_dir, "trace.config"), "-trace", kl, "-gpgpu_kernel_launch_latency", "0",
+                "-sim_first_kernel_latency", "0"] + list(extra)
+        s = _native.load().Simulator(args, False)
+        if s.run() != 0:
+            raise RuntimeError("chase simulation failed")
+        cyc[passes] = s.tot_cycle
+    return cyc[1] / nodes, (cyc[3] - cyc[2]) / nodes
 
 
 def simulated_chain_latency(config_dir: str, op: str, extra: Sequence[str] = (), iters: int = 8) -> float:

@@ -139,6 +139,9 @@ const OptDef kOptions[] = {
     {"-gpgpu_l1_banks_byte_interleaving", 'u', "32", ""},
     {"-gpgpu_l1_banks_hashing_function", 'u', "0", ""},
     {"-gpgpu_l1_latency", 'u', "1", "L1 hit latency"},
+    {"-sim_l1_miss_return_latency", 'u', "0",
+     "cycles from an L1 fill (or a bypassing reply) to the load's completion: the vector memory pipeline "
+     "a miss traverses besides the L2 round trip (0: none)"},
     {"-gpgpu_smem_latency", 'u', "3", "shared memory latency"},
     {"-gpgpu_gmem_skip_L1D", 'b', "0", "global memory bypasses L1"},
     {"-gpgpu_perfect_mem", 'b', "0", "perfect memory"},
@@ -818,6 +821,8 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.smem_cdna_groups = r.getb("-gpgpu_shmem_cdna_lane_groups") ? 1 : 0;
   c.l1 = parse_cache_geom(r.gets("-gpgpu_cache:dl1"));
   c.l1_latency = (uint32_t)r.getu("-gpgpu_l1_latency");
+  c.l1_miss_ret = (uint32_t)r.getu("-sim_l1_miss_return_latency");
+  if (c.l1_miss_ret + 16 >= (uint32_t)kHitRing) throw OptionError("-sim_l1_miss_return_latency too large");
   c.l1_banks = std::max<uint32_t>(1, (uint32_t)r.getu("-gpgpu_l1_banks"));
   c.l1_port_bytes = (uint32_t)r.getu("-sim_l1_port_bytes");
   c.l1_addr_lanes = (uint32_t)r.getu("-sim_l1_addr_lanes_per_cycle");

@@ -218,6 +218,10 @@ struct SimCfg {
   uint32_t smem_pad_;
   CacheGeom l1;
   uint32_t l1_latency;
+  // -sim_l1_miss_return_latency: cycles from a line's fill (or a bypassing
+  // reply) to the waiting load's completion -- the vector memory pipeline a
+  // miss traverses on CDNA besides the L2 round trip (0: none, GPGPU-Sim)
+  uint32_t l1_miss_ret;
   uint32_t l1_banks;
   // L1 data path throughput (0 = off, the reference's banked L1: l1_banks
   // accesses per cycle): a global / local instruction occupies the vector

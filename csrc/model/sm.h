@@ -541,6 +541,18 @@ SIM_HDI bool hit_push(S& s, uint64_t when, uint8_t warp, uint8_t slot, uint8_t k
   return true;
 }
 
+// a load access whose data came back from below the L1 (fill or bypassing
+// reply): completes now, or -sim_l1_miss_return_latency cycles later through
+// the completion ring (the first ring slot at or after that cycle with room)
+template <class S>
+SIM_HDI void sm_miss_access_done(S& s, const SimCfg& c, uint32_t w, uint32_t sl, uint64_t now) {
+  if (c.l1_miss_ret) {
+    for (uint32_t d = 0; d < 16; ++d)
+      if (hit_push(s, now + c.l1_miss_ret + d, (uint8_t)w, (uint8_t)sl, 0)) return;
+  }
+  if (--s.w_slot_pend[w][sl] == 0) sm_load_slot_done(s, w, sl, now);
+}
+
 // ---------------------------------------------------------------------------
 // L1 data cache (sectored, lane-parallel probe over the ways of a set)
 template <class P, class S>
@@ -640,7 +652,7 @@ SIM_HDI void l1_fill(S& s, const SmCtx& x, uint64_t line, uint8_t sectors, uint6
       e.need &= (uint8_t)~sectors;
       if (e.need) continue;
       e.valid = 0;
-      if (--s.w_slot_pend[e.warp][e.slot] == 0) sm_load_slot_done(s, e.warp, e.slot, now);
+      sm_miss_access_done(s, c, e.warp, e.slot, now);
     }
   }
   // compact the pending table tail
@@ -873,7 +885,7 @@ SIM_HDI void sm_receive(S& s, const SmCtx& x, uint64_t now) {
     s.last_progress = now;
   } else if (q.tag & 0x80000000u) {  // direct (bypass / atomic) load access
     uint32_t w = q.tag & 0xff, sl = (q.tag >> 8) & 0xff;
-    if (--s.w_slot_pend[w][sl] == 0) sm_load_slot_done(s, w, sl, now);
+    sm_miss_access_done(s, c, w, sl, now);
   } else {
     P::prof(41);
     l1_fill<P>(s, x, q.addr, q.sectors, now);
