@@ -221,6 +221,18 @@ def tune(stats_paths: List[str], base: str = "MI355X", out_root: str = "configs/
                      f" against the data stage's prediction at {port} B/clk: mean error {100 * err:.0f} % "
                      f"(touched bytes {100 * errs[0]:.0f} %, sectors {100 * errs[32]:.0f} %, "
                      f"64 B halves {100 * errs[64]:.0f} %)")
+    # instruction cache at dispatch: ub_icache_launch launches one kernel four
+    # times over every CU; misses that repeat on every launch mean the
+    # dispatch invalidates the SQC (hw_stats/icache_launch.py)
+    if "icache_misses_first_launch" in meas and "icache_misses_later_launches" in meas:
+        first = float(meas["icache_misses_first_launch"])
+        later = float(meas["icache_misses_later_launches"])
+        v = "1" if first > 0 and later >= 0.75 * first else "0"
+        cfg["-sim_sqc_invalidate_at_launch"] = v
+        applied["-sim_sqc_invalidate_at_launch"] = v
+        presets.write_config(cfg, out, power_preset=base)
+        notes.append(f"-sim_sqc_invalidate_at_launch {v}: ub_icache_launch instruction-cache misses {first:.0f} on "
+                     f"the first launch, {later:.0f} per later launch of the same code on the same CUs")
     with open(os.path.join(out, "TUNING.md"), "w") as f:
         f.write(f"# Tuned configuration for {device}\n\nBase preset: {base}\n\n")
         f.write("| option | tuned value | preset value |\n|---|---|---|\n")

@@ -146,6 +146,8 @@ const OptDef kOptions[] = {
     {"-gpgpu_gmem_skip_L1D", 'b', "0", "global memory bypasses L1"},
     {"-gpgpu_perfect_mem", 'b', "0", "perfect memory"},
     {"-gpgpu_flush_l1_cache", 'b', "0", "flush L1 between kernels"},
+    {"-sim_sqc_invalidate_at_launch", 'b', "0",
+     "every kernel launch invalidates the SMs' instruction and scalar-data caches (CDNA's dispatch acquire)"},
     {"-gpgpu_flush_l2_cache", 'b', "0", "flush L2 between kernels"},
     {"-gpgpu_cache:dl2", 's', "64:128:8,L:B:m:N,A:16:4,4", "L2 config"},
     {"-gpgpu_cache:dl2_texture_only", 'b', "1", ""},
@@ -1108,6 +1110,7 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.max_cta = (int32_t)r.geti("-gpgpu_max_cta");
   d.max_completed_cta = (int32_t)r.geti("-gpgpu_max_completed_cta");
   d.flush_l1 = r.getb("-gpgpu_flush_l1_cache");
+  d.sqc_invalidate = r.getb("-sim_sqc_invalidate_at_launch");
   d.flush_l2 = r.getb("-gpgpu_flush_l2_cache");
   d.l2_kernel_release = r.getb("-sim_l2_kernel_release");
   d.coll_mem_traffic = r.getb("-collective_mem_traffic");

@@ -55,6 +55,7 @@ struct DriverOpts {
   int32_t max_cta = 0;
   int32_t max_completed_cta = 0;
   bool flush_l1 = false;
+  bool sqc_invalidate = false;  // -sim_sqc_invalidate_at_launch
   bool flush_l2 = false;
   bool l2_kernel_release = false;
   bool coll_mem_traffic = false;   // -collective_mem_traffic: collectives run a copy kernel

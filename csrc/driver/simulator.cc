@@ -465,7 +465,7 @@ void Simulator::setup_kernel_op(StreamOp& o, bool apply_cta_cap) {
   kd.stream = (uint32_t)rk.h.stream;
   kd.l1_sets = occ.l1_sets;
   kd.l1_assoc = occ.l1_assoc;
-  kd.flush_l1 = dopt_.flush_l1 ? 1u : 0u;
+  kd.flush_l1 = (dopt_.flush_l1 ? 1u : 0u) | (dopt_.sqc_invalidate ? 2u : 0u);
   // per-CTA resources for SMs shared by concurrent kernels (the same limits
   // compute_occupancy applies to one kernel)
   const uint32_t padded = (ks.threads_per_cta + cfg_.warp_size - 1) / cfg_.warp_size * cfg_.warp_size;

@@ -153,7 +153,8 @@ struct KernelDesc {
   uint32_t stream;
   uint32_t l1_sets, l1_assoc;  // adaptive L1 geometry chosen for this kernel
   uint32_t stop_when_issued;   // cut to the -gpgpu_max_cta remainder: the run ends once all CTAs issued
-  uint32_t flush_l1;           // -gpgpu_flush_l1_cache: SMs drop their L1 when the kernel starts
+  uint32_t flush_l1;           // bit 0 -gpgpu_flush_l1_cache: SMs drop their L1 when the kernel starts;
+                               // bit 1 -sim_sqc_invalidate_at_launch: and their instruction / scalar caches
   // per-CTA SM resources (shader_core_ctx::occupy_shader_resource_1block):
   // warp-padded threads, registers, and the shared-memory capacity of the
   // carve-out chosen for this kernel

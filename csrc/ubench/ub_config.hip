@@ -43,6 +43,9 @@ int main() {
   const long long per_sub = std::max<long long>(128 * 16, l2_bytes / channels);
   const long long sets = std::max<long long>(1, per_sub / (128 * 16));
   ub_opt("-gpgpu_cache:dl2", "N:" + std::to_string(sets) + ":128:16,L:B:m:L:P,A:192:4,32:0,32");
+  // CDNA (gfx9): each SIMD has one VALU port that INT, FP64 and
+  // transcendental work issue on (no separate INT / SFU pipes)
+  if (std::string(p.gcnArchName).rfind("gfx9", 0) == 0) ub_opt("-sim_single_valu", 1);
   printf("# measured_shader_mhz %.1f\n", mhz);
   return 0;
 }

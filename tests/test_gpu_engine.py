@@ -71,6 +71,8 @@ def test_state_snapshot_bit_exact(gpu_mod, tmp_path, extra):
     {"-gpgpu_perfect_inst_const_cache": "0"},
     {"-dram_seperate_write_queue_enable": "1", "-dram_write_queue_size": "16:12:4", "-gpgpu_perf_sim_memcpy": "0"},
     {"-sim_l1_port_bytes": "48", "-sim_l1_addr_lanes_per_cycle": "16"},
+    {"-sim_sqc_invalidate_at_launch": "1", "-gpgpu_perfect_inst_const_cache": "0",
+     "-sim_l1_port_granule": "32"},
 ])
 def test_model_switches_gpu_equals_cpu(gpu_mod, tmp_path, extra):
     """Debug trace streams (event for event), idealised memory, FIFO DRAM and

@@ -156,6 +156,26 @@ def test_instruction_cache(native, traces):
     assert _stat(tiny.output, "L1I_total_cache_misses") > miss
 
 
+def test_sqc_invalidate_at_launch(native, traces):
+    """-sim_sqc_invalidate_at_launch 1: every kernel starts with cold
+    instruction caches (bfs launches the same two kernels repeatedly: the
+    misses of later launches come back), exact with and without the quiet-
+    cycle skipper; off by default."""
+    ic = {"-gpgpu_perfect_inst_const_cache": "0"}
+    keep = _run(native, traces["bfs"], ic)
+    inv = _run(native, traces["bfs"], dict(ic, **{"-sim_sqc_invalidate_at_launch": "1"}))
+    assert inv.tot_insn == keep.tot_insn
+    assert _stat(inv.output, "L1I_total_cache_misses") > _stat(keep.output, "L1I_total_cache_misses")
+    noskip = _run(native, traces["bfs"], dict(ic, **{"-sim_sqc_invalidate_at_launch": "1", "-sim_event_skip": "0"}))
+    assert (noskip.tot_cycle, noskip.tot_insn) == (inv.tot_cycle, inv.tot_insn)
+
+
+def test_icache_launch_verdict():
+    from accel_sim_framework_distributed_amd.hw_stats import icache_launch
+    assert icache_launch.verdict([98, 97, 98, 98]) == 1
+    assert icache_launch.verdict([98, 0, 0, 0]) == 0
+
+
 @pytest.mark.slow
 def test_dram_write_queue_and_turnaround(native, traces):
     """-dram_seperate_write_queue_enable with <size>:<high>:<low> watermarks

@@ -13,7 +13,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 out=$R/gpurun_out/corr
 mkdir -p $out
-UBENCH_PROGS="ub_config ub_bw_widths ub_cache_lat ub_cache_policy ub_alu ub_wave_issue ub_lds ub_mfma ub_mfma_shapes ub_icache ub_atomic_kernel ub_launch ub_mem_bw ub_l2_release ub_kernel_lat_tb ub_copy_engine ub_regfile" \
+UBENCH_PROGS="ub_config ub_bw_widths ub_cache_lat ub_cache_policy ub_alu ub_wave_issue ub_lds ub_mfma ub_mfma_shapes ub_icache ub_atomic_kernel ub_launch ub_mem_bw ub_l2_release ub_kernel_lat_tb ub_copy_engine ub_regfile ub_l1_stride ub_mem_lat" \
   bash $R/tools/run_ubench.sh $R/gpurun_out/ubench > $out/ubench.log 2>&1 || { echo "ubench failed"; tail $out/ubench.log; exit 1; }
 python $R/util/tuner/tuner.py -s $R/gpurun_out/ubench -b MI355X -o $R/configs/tuned > $out/tuner.log 2>&1 \
   || { echo "tuner failed"; tail $out/tuner.log; exit 1; }

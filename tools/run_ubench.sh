@@ -15,3 +15,10 @@ echo "== launch latency (rocprofv3 durations of empty kernels)"
 timeout -k 10 240 python accel_sim_framework_distributed_amd/hw_stats/launch_latency.py -o "$out/launch_rocprof" \
   > "$out/ub_launch_rocprof.log" 2>&1 || { echo "launch_latency failed"; tail -5 "$out/ub_launch_rocprof.log"; exit 1; }
 tail -4 "$out/ub_launch_rocprof.log"
+echo "== instruction cache across launches (rocprofv3 SQC counters)"
+( cd /tmp && timeout -s KILL 90 rocprofv3 --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS --output-format csv -d "$out/icache_launch" \
+  -o run -- "$OLDPWD/bin/ubench/ub_icache_launch" > "$out/icache_launch.run.log" 2>&1 ) \
+  || { echo "icache launch run failed"; tail -5 "$out/icache_launch.run.log"; exit 1; }
+python accel_sim_framework_distributed_amd/hw_stats/icache_launch.py "$out/icache_launch" > "$out/ub_icache_launch.log" \
+  || { echo "icache launch parse failed"; exit 1; }
+tail -3 "$out/ub_icache_launch.log"
