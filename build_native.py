@@ -39,6 +39,7 @@ CORE_SRC = [
     "csrc/driver/simulator.cc",
     "csrc/driver/dump.cc",
     "csrc/driver/debugger.cc",
+    "csrc/driver/icnt_bench.cc",
     "csrc/parallel/linksim.cc",
 ]
 HIP_SRC = ["csrc/engine/gpu_engine.hip", "csrc/engine/ingest_mfma.hip"]

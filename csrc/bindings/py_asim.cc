@@ -8,6 +8,7 @@
 #include <cstring>
 
 #include "../config/icnt_config.h"
+#include "../driver/icnt_bench.h"
 #include "../driver/simulator.h"
 
 namespace py = pybind11;
@@ -233,6 +234,37 @@ PYBIND11_MODULE(_asim, m) {
         return py::make_tuple(v, n);
       },
       "link-contention route model (icnt_links.h): interconnect nodes are clusters, then sub-partitions");
+  m.def(
+      "icnt_open_loop",
+      [](const std::string& icnt_text, const std::string& traffic, double rate, uint32_t packet_flits,
+         uint64_t cycles, uint64_t warmup, uint64_t seed) {
+        OpenLoopParams p;
+        p.traffic = traffic;
+        p.rate = rate;
+        p.packet_flits = packet_flits;
+        p.cycles = cycles;
+        p.warmup = warmup;
+        p.seed = seed;
+        OpenLoopResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = icnt_open_loop(icnt_text, p);
+        }
+        py::dict d;
+        d["nodes"] = r.nodes;
+        d["packets"] = r.packets;
+        d["measured_packets"] = r.measured_packets;
+        d["offered"] = r.offered;
+        d["accepted"] = r.accepted;
+        d["avg_latency"] = r.avg_latency;
+        d["max_latency"] = r.max_latency;
+        d["zero_load_latency"] = r.zero_load_latency;
+        d["deadlocked"] = r.deadlocked;
+        return d;
+      },
+      py::arg("icnt_text"), py::arg("traffic") = "uniform", py::arg("rate") = 0.1, py::arg("packet_flits") = 1,
+      py::arg("cycles") = 2000, py::arg("warmup") = 500, py::arg("seed") = 1,
+      "open-loop synthetic traffic through the router model (Booksim standalone mode, icnt_router.h)");
   m.def(
       "arch_energy",
       [](const std::vector<std::string>& args, double node_nm, double vdd, double dram_pj_per_bit,

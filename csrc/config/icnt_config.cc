@@ -8,9 +8,11 @@
 // pipeline depth (routing + VC allocation + switch allocation + traversal)
 // and channel latency per hop, and the flit size used for serialisation.
 // Contention is modelled at the injection and ejection ports of every node
-// (as for the local crossbar); link-level contention inside multi-hop
-// topologies and virtual-channel flow control are not -- the tested configs
-// all use a single-stage `fly` (a crossbar) where the two coincide.
+// (as for the local crossbar); -icnt_link_contention 1 adds link
+// reservations inside multi-hop topologies (icnt_links.h) and 2 the router
+// microarchitecture: virtual channels, credits, the switch allocator
+// (model/icnt_router.h), from num_vcs, vc_buf_size, alloc_iters,
+// credit_delay, sw_allocator, sw_alloc_delay and internal_speedup.
 #include "icnt_config.h"
 
 #include <algorithm>
@@ -20,6 +22,7 @@
 #include <sstream>
 
 #include "options.h"
+#include "../model/icnt_router.h"
 
 namespace asim {
 
@@ -74,12 +77,36 @@ static long geti(const std::map<std::string, std::string>& kv, const char* k, lo
   return (long)v;
 }
 
-void apply_intersim_config(SimCfg& c, const std::string& path) {
-  std::ifstream f(path);
-  if (!f.good()) throw OptionError("cannot open interconnect config file '" + path + "'");
-  std::stringstream ss;
-  ss << f.rdbuf();
-  auto kv = parse_booksim_config(ss.str());
+void apply_router_params(SimCfg& c, const std::map<std::string, std::string>& kv) {
+  const long vcs = geti(kv, "num_vcs", 1), buf = geti(kv, "vc_buf_size", 8), iters = geti(kv, "alloc_iters", 1);
+  const long cd = geti(kv, "credit_delay", 0), sa = geti(kv, "sw_alloc_delay", 1);
+  if (vcs < 1 || vcs > 64) throw OptionError("interconnect config: num_vcs must be 1..64");
+  if (buf < 1 || buf > 4096) throw OptionError("interconnect config: vc_buf_size must be 1..4096");
+  if (iters < 1 || iters > 16) throw OptionError("interconnect config: alloc_iters must be 1..16");
+  if (cd < 0 || cd > 255 || sa < 0 || sa > 255) throw OptionError("interconnect config: credit / allocation delay out of range");
+  c.rt_vcs = (uint8_t)vcs;
+  c.rt_buf = (uint16_t)buf;
+  c.rt_iters = (uint8_t)iters;
+  c.rt_credit = (uint8_t)cd;
+  c.rt_sa = (uint8_t)sa;
+  double sp = 1.0;
+  if (kv.count("internal_speedup")) sp = strtod(kv.at("internal_speedup").c_str(), nullptr);
+  if (!(sp >= 1.0 && sp <= 8.0)) throw OptionError("interconnect config: internal_speedup must be 1..8");
+  c.rt_speedup_q8 = (uint16_t)(sp * 256.0 + 0.5);
+  const std::string al = kv.count("sw_allocator") ? kv.at("sw_allocator") : "islip";
+  if (al == "islip") {
+    c.rt_alloc = RT_ISLIP;
+  } else if (al == "separable_input_first") {
+    c.rt_alloc = RT_SEP_INPUT_FIRST;
+  } else if (al == "separable_output_first") {
+    c.rt_alloc = RT_SEP_OUTPUT_FIRST;
+  } else {
+    c.rt_alloc = 0xff;  // refused only when the router model is on (-icnt_link_contention 2)
+  }
+}
+
+uint64_t apply_topology(SimCfg& c, const std::map<std::string, std::string>& kv0) {
+  auto kv = kv0;
   std::string topo = kv.count("topology") ? kv["topology"] : "mesh";
   const long k = geti(kv, "k", 8), n = geti(kv, "n", 2);
   if (k < 1 || n < 1 || k > 65535 || n > 255) throw OptionError("interconnect config: k/n out of range");
@@ -106,16 +133,26 @@ void apply_intersim_config(SimCfg& c, const std::string& path) {
   } else {
     throw OptionError("interconnect config: unsupported topology '" + topo + "' (anynet needs a network file)");
   }
-  const uint64_t need = (uint64_t)c.n_clusters + c.n_subpart;
-  if (nodes < need)
-    throw OptionError("interconnect config: topology has " + std::to_string(nodes) + " nodes, need " +
-                      std::to_string(need) + " (clusters + memory sub-partitions)");
   // iq_router pipeline: routing, VC allocation, switch allocation, traversal
   const long hop = geti(kv, "routing_delay", 0) + geti(kv, "vc_alloc_delay", 1) + geti(kv, "sw_alloc_delay", 1) + 1;
   c.hop_icnt = (uint16_t)std::max<long>(1, hop);
   c.chan_icnt = (uint16_t)std::max<long>(1, geti(kv, "channel_latency", 1));
   if (kv.count("flit_size")) c.flit_size = (uint32_t)std::max<long>(8, geti(kv, "flit_size", 32));
+  apply_router_params(c, kv);
   c.icnt_mode = 1;
+  return nodes;
+}
+
+void apply_intersim_config(SimCfg& c, const std::string& path) {
+  std::ifstream f(path);
+  if (!f.good()) throw OptionError("cannot open interconnect config file '" + path + "'");
+  std::stringstream ss;
+  ss << f.rdbuf();
+  const uint64_t nodes = apply_topology(c, parse_booksim_config(ss.str()));
+  const uint64_t need = (uint64_t)c.n_clusters + c.n_subpart;
+  if (nodes < need)
+    throw OptionError("interconnect config: topology has " + std::to_string(nodes) + " nodes, need " +
+                      std::to_string(need) + " (clusters + memory sub-partitions)");
   // lookahead = smallest pair latency in whole core cycles (>= 1, <= kMaxEpoch)
   uint64_t lo = ~0ull;
   c.icnt_latency = 1;  // icnt_pkt_lat_fs clamps to it; 1 core cycle is the floor

@@ -19,4 +19,11 @@ std::map<std::string, std::string> parse_booksim_config(const std::string& text)
 // counts of `c` must already be set.  Throws OptionError on bad files.
 void apply_intersim_config(SimCfg& c, const std::string& path);
 
+// topology, router pipeline, flit size and router microarchitecture of a
+// parsed .icnt file (icnt_mode = 1); returns the topology's node count
+uint64_t apply_topology(SimCfg& c, const std::map<std::string, std::string>& kv);
+
+// the router microarchitecture fields (rt_*) from a parsed .icnt file
+void apply_router_params(SimCfg& c, const std::map<std::string, std::string>& kv);
+
 }  // namespace asim

@@ -185,7 +185,7 @@ const OptDef kOptions[] = {
     {"-icnt_arbiter_algo", 'u', "1", ""},
     {"-icnt_verbose", 'u', "0", ""},
     {"-icnt_grant_cycles", 'u', "1", ""},
-    {"-icnt_link_contention", 'u', "0", "network_mode 1: shared links of multi-hop routes delay packets (link reservation per epoch)"},
+    {"-icnt_link_contention", 'u', "0", "network_mode 1: 0 off, 1 shared links delay packets (link reservation per epoch), 2 input-queued routers with VCs, credits and the .icnt file's allocator (icnt_router.h)"},
     {"-icnt_flit_size", 'u', "32", "flit size in bytes"},
     // ---- clocks / kernel ----
     {"-gpgpu_clock_domains", 's', "500.0:2000.0:2000.0:2000.0", "core:icnt:L2:DRAM MHz"},
@@ -343,6 +343,9 @@ const OptDef kOptions[] = {
     {"-sim_first_kernel_latency", 'u', "0",
      "extra launch cycles of the run's first kernel behind the initial host copies (cold start: the copies' "
      "completion and the first touch of their pages; ub_launch after-copy)"},
+    {"-sim_copy_latency_every_kernel", 'b', "0",
+     "apply -sim_first_kernel_latency to every kernel launched behind a host copy, not only the run's first "
+     "(ub_launch measures it on every one of its copy -> kernel repetitions)"},
     {"-collective_mem_traffic", 'b', "0",
      "run every collective's local memory traffic (send-buffer reads, receive-buffer writes) as an RCCL-style copy "
      "kernel that loads the simulated L2/MALL/HBM and contends with overlapping kernels"},
@@ -1046,7 +1049,12 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
   c.icnt_mode = 2;
   if (r.geti("-network_mode") == 1) {
     apply_intersim_config(c, resolve_cfg_path(r, r.gets("-inter_config_file")));
-    c.link_contention = r.getu("-icnt_link_contention") ? 1 : 0;
+    const uint64_t lc = r.getu("-icnt_link_contention");
+    if (lc > 2) throw OptionError("-icnt_link_contention must be 0, 1 (link reservations) or 2 (router model)");
+    c.link_contention = (uint16_t)lc;
+    if (lc == 2 && c.rt_alloc == 0xff)
+      throw OptionError("-icnt_link_contention 2: the .icnt file's sw_allocator is not modelled "
+                        "(islip, separable_input_first, separable_output_first)");
   } else if (r.geti("-network_mode") != 2) {
     throw OptionError("-network_mode must be 1 (intersim topology) or 2 (local crossbar)");
   }
@@ -1116,6 +1124,7 @@ DriverOpts derive_driver_opts(const OptionRegistry& r) {
   d.coll_mem_traffic = r.getb("-collective_mem_traffic");
   d.host_launch_interval = r.getu("-sim_host_launch_interval");
   d.first_kernel_latency = r.getu("-sim_first_kernel_latency");
+  d.copy_latency_every = r.getb("-sim_copy_latency_every_kernel");
   d.kernel_min_cycles_queued = r.getu("-sim_kernel_min_cycles_queued");
   d.dvfs = r.getb("-dvfs_enabled");
   d.dvfs_min_clock_ratio = r.getd("-dvfs_min_clock_ratio");

@@ -61,6 +61,7 @@ struct DriverOpts {
   bool coll_mem_traffic = false;   // -collective_mem_traffic: collectives run a copy kernel
   uint64_t host_launch_interval = 0;      // -sim_host_launch_interval (cycles)
   uint64_t first_kernel_latency = 0;      // -sim_first_kernel_latency (cycles)
+  bool copy_latency_every = false;        // -sim_copy_latency_every_kernel: ... for every kernel behind a copy
   uint64_t kernel_min_cycles_queued = 0;  // -sim_kernel_min_cycles_queued
   bool dvfs = false;               // -dvfs_enabled: the power-cap DVFS governor
   double dvfs_min_clock_ratio = 0.5;  // -sim_l2_kernel_release: write back + invalidate the L2s at kernel end

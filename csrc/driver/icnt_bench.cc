@@ -1,0 +1,148 @@
+// Open-loop synthetic-traffic runs of the router model (Booksim's standalone
+// mode: reference intersim2/main.cpp + trafficmanager.cpp + traffic.cpp +
+// injection.cpp).  Every node injects Bernoulli packets at `rate` flits per
+// cycle towards the traffic pattern's destination for `cycles` cycles; the
+// packets are simulated to their arrival in one pass of the router model
+// (model/icnt_router.h), which is exact here because the whole injection
+// schedule is known up front.  Latency is creation to tail ejection (source
+// queueing included), accepted throughput the flits ejected during the
+// measurement window [warmup, cycles) per node and cycle.
+#include "icnt_bench.h"
+
+#include <algorithm>
+#include <cmath>
+#include <stdexcept>
+#include <vector>
+
+#include "../config/icnt_config.h"
+#include "../model/icnt_router.h"
+
+namespace asim {
+
+namespace {
+
+// splitmix64: a small deterministic generator (same stream on every host)
+struct Rng {
+  uint64_t s;
+  uint64_t next() {
+    uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+  }
+  double uniform() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+};
+
+uint32_t log2_exact(uint32_t n) {
+  uint32_t b = 0;
+  while ((1u << b) < n) ++b;
+  if ((1u << b) != n) throw std::invalid_argument("bit-permutation traffic needs a power-of-two node count");
+  return b;
+}
+
+// destination of node s under the pattern (Booksim traffic.cpp names)
+uint32_t destination(const std::string& t, uint32_t s, uint32_t N, uint32_t k, uint32_t n, Rng& r) {
+  if (t == "uniform") {
+    for (;;) {
+      const uint32_t d = (uint32_t)(r.next() % N);
+      if (d != s || N == 1) return d;
+    }
+  }
+  if (t == "bitcomp") return ~s & ((1u << log2_exact(N)) - 1);
+  if (t == "transpose") {
+    const uint32_t b = log2_exact(N);
+    if (b % 2) throw std::invalid_argument("transpose traffic needs an even number of address bits");
+    const uint32_t h = b / 2, m = (1u << h) - 1;
+    return ((s & m) << h) | (s >> h);
+  }
+  if (t == "bitrev") {
+    const uint32_t b = log2_exact(N);
+    uint32_t d = 0;
+    for (uint32_t i = 0; i < b; ++i) d |= ((s >> i) & 1u) << (b - 1 - i);
+    return d;
+  }
+  if (t == "shuffle") {
+    const uint32_t b = log2_exact(N);
+    return ((s << 1) | (s >> (b - 1))) & (N - 1);
+  }
+  if (t == "tornado" || t == "neighbor") {
+    // per dimension of a k-ary n-cube: half way round (tornado) or the next router
+    uint32_t d = 0, pw = 1, x = s;
+    for (uint32_t i = 0; i < n; ++i, pw *= k) {
+      const uint32_t xi = x % k;
+      const uint32_t yi = t == "tornado" ? (xi + (k + 1) / 2 - 1) % k : (xi + 1) % k;
+      d += yi * pw;
+      x /= k;
+    }
+    return d % N;
+  }
+  throw std::invalid_argument("unknown traffic pattern '" + t + "'");
+}
+
+}  // namespace
+
+OpenLoopResult icnt_open_loop(const std::string& icnt_text, const OpenLoopParams& prm) {
+  SimCfg c{};
+  c.flit_size = 32;
+  const uint64_t nodes = apply_topology(c, parse_booksim_config(icnt_text));
+  if (c.rt_alloc == 0xff) throw std::invalid_argument("sw_allocator not modelled");
+  c.link_contention = 2;
+  if (nodes > (1u << 20)) throw std::invalid_argument("topology too large");
+  const uint32_t N = (uint32_t)nodes;
+  const uint32_t pf = prm.packet_flits ? prm.packet_flits : 1;
+  if (prm.rate < 0 || prm.rate > 1) throw std::invalid_argument("rate must be 0..1 flits per node per cycle");
+  if (prm.warmup >= prm.cycles) throw std::invalid_argument("warmup must be shorter than the run");
+  // the injection schedule
+  Rng r{prm.seed * 0x2545f4914f6cdd1dull + 1};
+  std::vector<uint32_t> src, dst;
+  std::vector<uint64_t> tinj;
+  const double p_pkt = prm.rate / pf;
+  for (uint64_t t = 0; t < prm.cycles; ++t)
+    for (uint32_t s = 0; s < N; ++s)
+      if (r.uniform() < p_pkt) {
+        const uint32_t d = destination(prm.traffic, s, N, c.topo_k, c.topo_n, r);
+        if (d == s) continue;  // a fixed point of a permutation sends nothing
+        src.push_back(s);
+        dst.push_back(d);
+        tinj.push_back(t);
+      }
+  const uint64_t np64 = src.size();
+  if (np64 > 50'000'000ull) throw std::invalid_argument("too many packets for one pass");
+  const uint32_t np = (uint32_t)np64;
+  const RtDims d = rt_dims(c, np ? np : 1, pf);
+  std::vector<uint64_t> st(rt_state_words(d), 0);
+  std::vector<uint32_t> scratch(rt_carve(d, nullptr, nullptr), 0);
+  RtWork w;
+  rt_carve(d, scratch.data(), &w);
+  for (uint32_t i = 0; i < np; ++i) {
+    w.src[i] = src[i];
+    w.dst[i] = dst[i];
+    w.nfl[i] = pf;
+    w.tinj[i] = tinj[i];
+  }
+  OpenLoopResult res;
+  res.nodes = N;
+  res.packets = np;
+  res.deadlocked = np ? rt_simulate(c, d, st.data(), w, np) : 0;
+  double lat = 0, zero = 0;
+  uint64_t meas = 0, ejected = 0;
+  for (uint32_t i = 0; i < np; ++i) {
+    const uint64_t a = w.tarr[i];
+    if (a >= prm.warmup && a < prm.cycles) ejected += pf;
+    if (tinj[i] >= prm.warmup) {
+      lat += (double)(a - tinj[i]);
+      zero += (double)rt_uncontended(c, icnt_routers(c, src[i], dst[i]), pf);
+      ++meas;
+      res.max_latency = std::max<double>(res.max_latency, (double)(a - tinj[i]));
+    }
+  }
+  const double window = (double)(prm.cycles - prm.warmup) * N;
+  res.offered = (double)meas * pf / window;
+  res.accepted = (double)ejected / window;
+  res.avg_latency = meas ? lat / meas : 0;
+  res.zero_load_latency = meas ? zero / meas : 0;
+  res.measured_packets = meas;
+  return res;
+}
+
+}  // namespace asim

@@ -209,7 +209,7 @@ void Simulator::admit(size_t end) {
       // apart (the host resumes at the engine's clock after a sync)
       win_.back()->submit = host_t_;
       host_t_ += dopt_.host_launch_interval;
-      win_.back()->after_copy = copy_since_kernel_ && !any_kernel_admitted_;
+      win_.back()->after_copy = copy_since_kernel_ && (dopt_.copy_latency_every || !any_kernel_admitted_);
       copy_since_kernel_ = false;
       any_kernel_admitted_ = true;
       last_cmd_kernel_ = true;

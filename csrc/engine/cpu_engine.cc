@@ -157,12 +157,14 @@ class CpuEngine : public Engine {
     mall_.assign((size_t)(c.n_mem * mall_lines(c)), L2Line{});
     link_free_.clear();
     link_refs_.clear();
-    link_stat_[0] = link_stat_[1] = 0;
+    n_link_state_ = 0;
     if (c.link_contention && (icnt_link_count(c) > kMaxIcntLinks || !icnt_contention_fits(c, cap_req_, cap_rep_)))
       throw std::runtime_error("-icnt_link_contention: topology or mailboxes too large for the link pass");
     if (icnt_contention_on(c)) {
-      link_free_.assign((size_t)icnt_link_count(c), 0);
-      link_refs_.assign((size_t)c.n_sm * c.n_subpart * std::max(cap_req_, cap_rep_), 0);
+      // the link model's persistent words, then its two statistics words
+      n_link_state_ = (size_t)icnt_state_words(c, cap_req_, cap_rep_);
+      link_free_.assign(n_link_state_ + 2, 0);
+      link_refs_.assign((size_t)icnt_scratch_words(c, cap_req_, cap_rep_), 0);
     }
     epoch_ = 0;
     cycle_ = 0;
@@ -288,8 +290,8 @@ class CpuEngine : public Engine {
           // their routes before any destination reads them (icnt_links.h)
           if (tid == 0) {
             try {
-              icnt_contend<SeqPar>(c, box_req_[cur].data(), cnt_req_[cur].data(), cap_req_, box_rep_[cur].data(),
-                                   cnt_rep_[cur].data(), cap_rep_, link_free_.data(), link_refs_.data(), link_stat_);
+              icnt_epoch_pass<SeqPar>(c, box_req_[cur].data(), cnt_req_[cur].data(), cap_req_, box_rep_[cur].data(),
+                                      cnt_rep_[cur].data(), cap_rep_, link_free_.data(), link_refs_.data());
             } catch (...) {
               fail();
             }
@@ -437,7 +439,7 @@ class CpuEngine : public Engine {
 
   void snapshot(std::vector<uint8_t>& out) override {
     out.resize(sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState) + mall_.size() * sizeof(L2Line) +
-               link_free_.size() * 8);
+               n_link_state_ * 8);
     uint8_t* p = out.data();
     for (auto& s : sms_) {
       memcpy(p, &s, sizeof(SMState));
@@ -449,11 +451,11 @@ class CpuEngine : public Engine {
     }
     if (!mall_.empty()) memcpy(p, mall_.data(), mall_.size() * sizeof(L2Line));
     p += mall_.size() * sizeof(L2Line);
-    if (!link_free_.empty()) memcpy(p, link_free_.data(), link_free_.size() * 8);
+    if (n_link_state_) memcpy(p, link_free_.data(), n_link_state_ * 8);
   }
   void restore(const std::vector<uint8_t>& in) override {
     if (in.size() != sms_.size() * sizeof(SMState) + chs_.size() * sizeof(ChanState) + mall_.size() * sizeof(L2Line) +
-                         link_free_.size() * 8)
+                         n_link_state_ * 8)
       throw std::runtime_error("snapshot size mismatch");
     const uint8_t* p = in.data();
     for (auto& s : sms_) {
@@ -466,11 +468,11 @@ class CpuEngine : public Engine {
     }
     if (!mall_.empty()) memcpy(mall_.data(), p, mall_.size() * sizeof(L2Line));
     p += mall_.size() * sizeof(L2Line);
-    if (!link_free_.empty()) memcpy(link_free_.data(), p, link_free_.size() * 8);
+    if (n_link_state_) memcpy(link_free_.data(), p, n_link_state_ * 8);
   }
   void link_stats(uint64_t* delayed, uint64_t* wait_cycles) override {
-    *delayed = link_stat_[0];
-    *wait_cycles = link_stat_[1];
+    *delayed = n_link_state_ ? link_free_[n_link_state_] : 0;
+    *wait_cycles = n_link_state_ ? link_free_[n_link_state_ + 1] : 0;
   }
   void advance(uint64_t cycles) override {
     uint64_t E = c_.icnt_latency;
@@ -490,7 +492,7 @@ class CpuEngine : public Engine {
     h.cnt_rep = cnt_rep_[0].size();
     h.ovf = ovf_.size();
     h.mall = mall_.size();
-    h.links = link_free_.empty() ? 0 : link_free_.size() + 2;
+    h.links = link_free_.size();
     h.cycle = cycle_;
     h.epoch = epoch_;
     h.ready = kt_.active;
@@ -513,10 +515,7 @@ class CpuEngine : public Engine {
     }
     o.put(ovf_.data(), ovf_.size() * sizeof(Pkt));
     o.put(mall_.data(), mall_.size() * sizeof(L2Line));
-    if (!link_free_.empty()) {
-      o.put(link_free_.data(), link_free_.size() * 8);
-      o.put(link_stat_, sizeof(link_stat_));
-    }
+    if (!link_free_.empty()) o.put(link_free_.data(), link_free_.size() * 8);
   }
 
   void load_state(const std::vector<uint8_t>& in) override {
@@ -535,10 +534,7 @@ class CpuEngine : public Engine {
     }
     r.get(ovf_.data(), ovf_.size() * sizeof(Pkt));
     r.get(mall_.data(), mall_.size() * sizeof(L2Line));
-    if (!link_free_.empty()) {
-      r.get(link_free_.data(), link_free_.size() * 8);
-      r.get(link_stat_, sizeof(link_stat_));
-    }
+    if (!link_free_.empty()) r.get(link_free_.data(), link_free_.size() * 8);
     cycle_ = h.cycle;
     epoch_ = h.epoch;
     if (h.ready) throw std::runtime_error("engine state: image taken with kernels running");
@@ -579,9 +575,12 @@ class CpuEngine : public Engine {
   std::vector<Pkt> ovf_;  // arrival backlog rings [n_subpart][ovf_cap_]
   std::vector<L2Line> mall_;  // MALL lines [n_mem][mall_sets * mall_assoc]
   uint32_t ovf_cap_ = 0;
-  std::vector<uint64_t> link_free_;  // -icnt_link_contention: per directed link, the fs it frees
-  std::vector<uint32_t> link_refs_;  // the pass's packet list
-  uint64_t link_stat_[2] = {0, 0};   // delayed packets, delay (interconnect cycles)
+  // -icnt_link_contention: the link model's persistent state (link free
+  // times, or the router network's, icnt_router.h), then {delayed packets,
+  // delay in interconnect cycles}; and the pass's scratch
+  std::vector<uint64_t> link_free_;
+  std::vector<uint32_t> link_refs_;
+  size_t n_link_state_ = 0;
   uint64_t epoch_ = 0, cycle_ = 0;
   KernelTab kt_{};
 };

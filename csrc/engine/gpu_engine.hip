@@ -368,8 +368,8 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
       // in the fixed order (icnt_links.h), then every block waits for it
       // before a destination reads them
       if (b == 0)
-        icnt_contend<P>(c, a.box_req[cur], a.cnt_req[cur], a.cap_req, a.box_rep[cur], a.cnt_rep[cur], a.cap_rep,
-                        a.link_free, a.link_refs, a.link_free + icnt_link_count(c));
+        icnt_epoch_pass<P>(c, a.box_req[cur], a.cnt_req[cur], a.cap_req, a.box_rep[cur], a.cnt_rep[cur], a.cap_rep,
+                           a.link_free, a.link_refs);
       if (!grid_barrier(a.ctl, a.nblocks, nbar++)) break;
     }
     P::prof(27);  // decision
@@ -782,12 +782,11 @@ class GpuEngine : public Engine {
     }
     if (c.link_contention && (icnt_link_count(c) > kMaxIcntLinks || !icnt_contention_fits(c, cap_req_, cap_rep_)))
       throw std::runtime_error("-icnt_link_contention: topology or mailboxes too large for the link pass");
-    n_links_ = icnt_contention_on(c) ? (size_t)icnt_link_count(c) : 0;
+    n_links_ = icnt_contention_on(c) ? (size_t)icnt_state_words(c, cap_req_, cap_rep_) : 0;
     if (n_links_) {
       pool_alloc(&d_links_, sizeof(uint64_t) * (n_links_ + 2));
       HIPCHECK(hipMemset(d_links_, 0, sizeof(uint64_t) * (n_links_ + 2)));
-      const size_t nrefs = (size_t)c.n_sm * c.n_subpart * std::max(cap_req_, cap_rep_);
-      pool_alloc(&d_link_refs_, sizeof(uint32_t) * nrefs);
+      pool_alloc(&d_link_refs_, sizeof(uint32_t) * (size_t)icnt_scratch_words(c, cap_req_, cap_rep_));
     }
     pool_alloc(&d_ctl_, sizeof(GpuCtl));
     h_ctl_ = static_cast<GpuCtl*>(DevicePool::get().host(sizeof(GpuCtl)));

@@ -280,7 +280,14 @@ struct SimCfg {
   uint16_t topo_conc;       // nodes per router (cmesh concentration)
   uint16_t hop_icnt;        // icnt cycles per router traversal (routing + VA + SA + ST)
   uint16_t chan_icnt;       // icnt cycles per channel
-  uint16_t link_contention;  // -icnt_link_contention: shared links of multi-hop routes delay packets (icnt_links.h)
+  uint16_t link_contention;  // -icnt_link_contention: 1 link reservations (icnt_links.h), 2 input-queued routers (icnt_router.h)
+  // input-queued router microarchitecture of -icnt_link_contention 2 (the
+  // .icnt file's num_vcs, vc_buf_size, alloc_iters, credit_delay,
+  // sw_allocator, sw_alloc_delay and internal_speedup)
+  uint8_t rt_vcs, rt_iters, rt_credit, rt_alloc, rt_sa;
+  uint8_t rt_pad_;
+  uint16_t rt_buf;         // flits per virtual channel
+  uint16_t rt_speedup_q8;  // switch passes per cycle x 256
   // ---- memory partition ----
   CacheGeom l2;
   uint32_t rop_latency;

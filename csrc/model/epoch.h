@@ -12,7 +12,7 @@
 // published at the previous epoch boundary -- no atomics, no races, and the
 // CPU engine gives bit-identical results.
 #pragma once
-#include "icnt_links.h"
+#include "icnt_router.h"
 #include "mem.h"
 
 namespace asim {

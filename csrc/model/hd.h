@@ -19,7 +19,11 @@
 #include <hip/hip_runtime.h>
 #define SIM_HD __host__ __device__
 #define SIM_HDI __host__ __device__ __forceinline__
+// out of line on the device: cold code whose registers must not weigh on the
+// engine kernel's hot loops
+#define SIM_HDN __host__ __device__ inline __attribute__((noinline))
 #else
+#define SIM_HDN inline
 #define SIM_HD
 #define SIM_HDI inline
 #endif

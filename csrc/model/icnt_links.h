@@ -19,7 +19,8 @@
 // Contention only delays packets, so the PDES lookahead (the uncontended
 // minimum latency) still holds.  A single-stage butterfly (the crossbar every
 // tested config uses) has no internal links: its contention is the ports',
-// which the engines model at the endpoints already.
+// which the engines model at the endpoints already (the router model of
+// -icnt_link_contention 2, icnt_router.h, arbitrates its output ports too).
 //
 // The pass is policy-generic (P = SeqPar on the CPU engine, WavePar on one
 // GPU block) and its order is fixed, so both engines give identical results.
@@ -46,7 +47,9 @@ SIM_HDI uint64_t icnt_link_count(const SimCfg& c) {
   const uint32_t k = c.topo_k ? c.topo_k : 2, n = c.topo_n ? c.topo_n : 1;
   const uint64_t kn = ipow(k, n);
   switch (c.topo) {
-    case TOPO_FLY: return n <= 1 ? 0 : (uint64_t)n * kn;  // stage x router x port
+    // stage x router x port; a single-stage fly (a crossbar) has only its
+    // output ports, which the router model (icnt_router.h) arbitrates
+    case TOPO_FLY: return n <= 1 && c.link_contention != 2 ? 0 : (uint64_t)n * kn;
     case TOPO_CMESH:
     case TOPO_MESH:
     case TOPO_TORUS: return kn * (2ull * n + (c.topo == TOPO_CMESH ? (c.topo_conc ? c.topo_conc : 1) : 1));
@@ -124,14 +127,17 @@ SIM_HDI uint32_t icnt_route(const SimCfg& c, uint32_t a, uint32_t b, F&& emit) {
           ++lvl;
         }
       }
+      // the level-l switch on the way up holds the source's digits above l
+      // and the destination's below l (d-mod-k took digit i at level i); its
+      // up port is the destination's digit l.  On the way down every switch
+      // and port is the destination's: one down link per (level, destination)
       for (uint32_t l = 0; l + 1 < lvl; ++l) {
-        const uint64_t pl = ipow(k, l);
-        emit((uint32_t)((uint64_t)l * kn + (a / (pl * k)) * k + (b / pl) % k));
+        const uint64_t pk = ipow(k, l + 1);
+        emit((uint32_t)((uint64_t)l * kn + (a / pk) * pk + b % pk));
         ++m;
       }
       for (uint32_t l = lvl - 1; l-- > 0;) {
-        const uint64_t pl = ipow(k, l);
-        emit((uint32_t)((uint64_t)n * kn + (uint64_t)l * kn + (b / (pl * k)) * k + (b / pl) % k));
+        emit((uint32_t)((uint64_t)n * kn + (uint64_t)l * kn + b % kn));
         ++m;
       }
       emit((uint32_t)(2ull * n * kn + b % kn));

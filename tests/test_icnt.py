@@ -278,3 +278,132 @@ def test_mesh_link_contention_gpu_matches_cpu(native, tmp_path):
         res.append((s.tot_cycle, _link_stat(s.output, "Network_link_delayed_packets"),
                     _link_stat(s.output, "Network_link_wait_cycles"), _stat(s.output, "Req_Network_queueing_cycles")))
     assert res[0] == res[1] and res[0][1] > 100
+
+
+# ---- input-queued router microarchitecture (icnt_router.h) -----------------
+def _rt_icnt(**kw):
+    base = dict(vc_buf_size="8", internal_speedup="1.0")
+    base.update(kw)
+    return presets.render_icnt(presets.icnt_params(**base))
+
+
+def test_router_crossbar_head_of_line_blocking(native):
+    """A FIFO input-queued crossbar under uniform traffic saturates near
+    2 - sqrt(2) = 58.6 % (head-of-line blocking); an internal speedup of 2
+    lifts it well above; below saturation latency is the zero-load latency."""
+    xbar = _rt_icnt(k=32, n=1)
+    sat = native.icnt_open_loop(xbar, "uniform", 1.0, 1, 3000, 1000, 1)
+    assert 0.56 < sat["accepted"] < 0.63 and sat["deadlocked"] == 0
+    fast = native.icnt_open_loop(_rt_icnt(k=32, n=1, internal_speedup="2.0"), "uniform", 1.0, 1, 3000, 1000, 1)
+    assert fast["accepted"] > 0.85
+    low = native.icnt_open_loop(xbar, "uniform", 0.1, 1, 3000, 1000, 1)
+    assert abs(low["accepted"] - 0.1) < 0.01
+    assert low["zero_load_latency"] == 5 and low["avg_latency"] < 5.3
+    # the allocators differ in pointer policy only; all are work conserving here
+    sep = native.icnt_open_loop(_rt_icnt(k=32, n=1, sw_allocator="separable_input_first"), "uniform", 1.0, 1,
+                                3000, 1000, 1)
+    assert 0.56 < sep["accepted"] < 0.63
+    # virtual channels at the inputs relieve head-of-line blocking
+    vcs = native.icnt_open_loop(_rt_icnt(k=32, n=1, num_vcs="4"), "uniform", 1.0, 1, 3000, 1000, 1)
+    assert vcs["accepted"] >= sat["accepted"]
+
+
+def test_router_mesh_saturates_below_bisection(native):
+    mesh = _rt_icnt(k=8, n=2, topology="mesh")
+    sat = native.icnt_open_loop(mesh, "uniform", 1.0, 1, 3000, 1000, 1)
+    # bisection bound of an 8x8 mesh under uniform traffic: 4 / k = 0.5
+    assert 0.3 < sat["accepted"] < 0.5 and sat["deadlocked"] == 0
+    low = native.icnt_open_loop(mesh, "uniform", 0.1, 1, 3000, 1000, 1)
+    assert low["avg_latency"] < 1.05 * low["zero_load_latency"]
+    # transpose concentrates dimension-order routes on the diagonal's links
+    tr = native.icnt_open_loop(mesh, "transpose", 1.0, 1, 3000, 1000, 1)
+    assert tr["accepted"] < sat["accepted"]
+    # multi-flit packets: serialisation is part of the zero-load latency
+    four = native.icnt_open_loop(mesh, "uniform", 0.05, 4, 3000, 1000, 1)
+    assert abs(four["zero_load_latency"] - low["zero_load_latency"] - 3) < 0.5
+    assert four["avg_latency"] < 1.1 * four["zero_load_latency"]
+
+
+def test_router_torus_dateline_classes(native):
+    """Dimension-order routing on a torus needs two VC classes (dateline):
+    with one VC the ring deadlocks under load and the pass reports it."""
+    one = native.icnt_open_loop(_rt_icnt(k=8, n=2, topology="torus"), "uniform", 1.0, 1, 2000, 500, 1)
+    assert one["deadlocked"] > 0
+    two = native.icnt_open_loop(_rt_icnt(k=8, n=2, topology="torus", num_vcs="2"), "uniform", 1.0, 1, 2000, 500, 1)
+    assert two["deadlocked"] == 0 and two["accepted"] > 0.35
+
+
+def test_router_traffic_patterns_are_deterministic(native):
+    mesh = _rt_icnt(k=4, n=2, topology="mesh")
+    for t in ("uniform", "transpose", "bitcomp", "bitrev", "shuffle", "tornado", "neighbor"):
+        a = native.icnt_open_loop(mesh, t, 0.3, 2, 1000, 200, 7)
+        b = native.icnt_open_loop(mesh, t, 0.3, 2, 1000, 200, 7)
+        assert a == b and a["packets"] > 0, t
+    with pytest.raises(Exception, match="traffic"):
+        native.icnt_open_loop(mesh, "nonesuch", 0.3, 1, 1000, 200, 1)
+
+
+def test_router_model_in_the_simulator(native, tmp_path):
+    kl = _hotspot_app(tmp_path, "rt", True)
+    mesh = _icnt_args(tmp_path, "rtmesh", k=8, n=2, topology="mesh")
+    runs = {}
+    for lc in ("0", "2"):
+        s = native.Simulator(mesh + ["-icnt_link_contention", lc, "-gpgpu_perf_sim_memcpy", "0", "-trace", kl], False)
+        assert s.run() == 0 and not s.deadlock
+        runs[lc] = s
+    assert runs["0"].tot_insn == runs["2"].tot_insn
+    out = runs["2"].output
+    assert _link_stat(out, "Network_link_delayed_packets") > 50
+    assert runs["2"].tot_cycle >= runs["0"].tot_cycle
+    s4 = native.Simulator(mesh + ["-icnt_link_contention", "2", "-gpgpu_perf_sim_memcpy", "0",
+                                  "-sim_cpu_threads", "4", "-trace", kl], False)
+    assert s4.run() == 0
+    assert (s4.tot_cycle, _link_stat(s4.output, "Network_link_wait_cycles")) == \
+        (runs["2"].tot_cycle, _link_stat(out, "Network_link_wait_cycles"))
+    # the single-stage crossbar's output ports are arbitrated too
+    fly = _icnt_args(tmp_path, "rtfly", k=32, n=1)
+    s = native.Simulator(fly + ["-icnt_link_contention", "2", "-gpgpu_perf_sim_memcpy", "0", "-trace", kl], False)
+    assert s.run() == 0 and _link_stat(s.output, "Network_link_delayed_packets") > 0
+    assert native.icnt_path(fly + ["-icnt_link_contention", "2"], 0, 16) == ([16], 32)
+
+
+def test_router_state_checkpoint_resumes_exactly(native, tmp_path):
+    from accel_sim_framework_distributed_amd.tracegen import rodinia as rd
+    kl = rd.write_app(str(tmp_path / "pf"), rd.pathfinder(4000, 12, 2))
+    mesh = _icnt_args(tmp_path, "mesh", k=8, n=2, topology="mesh") + [
+        "-icnt_link_contention", "2", "-trace", kl, "-checkpoint_path", str(tmp_path / "ck")]
+    full = native.Simulator(mesh, False)
+    assert full.run() == 0
+    first = native.Simulator(mesh + ["-checkpoint_option", "1", "-checkpoint_kernel", "2"], False)
+    assert first.run() == 0
+    rest = native.Simulator(mesh + ["-resume_option", "1", "-resume_kernel", "2"], False)
+    assert rest.run() == 0 and "resumed from" in rest.output
+    assert rest.tot_cycle == full.tot_cycle
+    assert _link_stat(rest.output, "Network_link_wait_cycles") == _link_stat(full.output, "Network_link_wait_cycles")
+
+
+def test_router_unmodelled_allocator_refused_only_when_used(native, tmp_path):
+    p = tmp_path / "wf.icnt"
+    p.write_text(presets.render_icnt(presets.icnt_params(k=32, sw_allocator="wavefront")))
+    args = presets.args_for("QV100", {"-gpgpu_n_clusters": "16", "-gpgpu_n_mem": "8",
+                                      "-network_mode": "1", "-inter_config_file": str(p)})
+    native.parse_config(args)  # the latency model does not need the allocator
+    with pytest.raises(Exception, match="sw_allocator"):
+        native.parse_config(args + ["-icnt_link_contention", "2"])
+    with pytest.raises(Exception, match="icnt_link_contention"):
+        native.parse_config(args + ["-icnt_link_contention", "3"])
+
+
+@pytest.mark.gpu
+def test_router_model_gpu_matches_cpu(native, tmp_path):
+    kl = _hotspot_app(tmp_path, "rtg", True)
+    for name, kw in (("mesh", dict(k=8, n=2, topology="mesh")), ("fly", dict(k=32, n=1))):
+        args = _icnt_args(tmp_path, name, **kw)
+        res = []
+        for eng in ("cpu", "gpu"):
+            s = native.Simulator(args + ["-icnt_link_contention", "2", "-gpgpu_perf_sim_memcpy", "0",
+                                         "-sim_engine", eng, "-trace", kl], False)
+            assert s.run() == 0
+            res.append((s.tot_cycle, _link_stat(s.output, "Network_link_delayed_packets"),
+                        _link_stat(s.output, "Network_link_wait_cycles")))
+        assert res[0] == res[1] and res[0][1] > 0, name
