@@ -590,7 +590,8 @@ SIM_HDN void rt_epoch_run(const SimCfg& c, Pkt* box_req, const uint32_t* cnt_req
         const uint64_t t0 = p.t > lat ? p.t - lat : 0;
         w.src[np] = a;
         w.dst[np] = b;
-        w.nfl[np] = rt_flits(c, p.size ? p.size : 1);
+        const uint32_t nfl = rt_flits(c, p.size ? p.size : 1), nfl_max = rt_flits(c, kRtMaxPktBytes);
+        w.nfl[np] = nfl < nfl_max ? nfl : nfl_max;  // the scratch holds nfl_max flits per packet
         w.tinj[np] = fdiv(t0, c.dv_icnt);
         w.bidx[np] = cell * cap + j;
         ++np;

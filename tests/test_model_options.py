@@ -357,3 +357,23 @@ def test_kernel_launch_model(native, tmp_path):
     first = _run(native, kl, {"-sim_first_kernel_latency": "777"})
     # (+ at most an epoch: the first CTA dispatch lands on an epoch boundary)
     assert 777 <= first.kernels[0]["cycles"] - ks[0] <= 777 + 32
+
+
+def test_copy_latency_every_kernel(native, tmp_path):
+    """-sim_copy_latency_every_kernel: every kernel launched behind a host copy
+    pays -sim_first_kernel_latency (ub_launch measures the after-copy cost on
+    each of its copy -> kernel repetitions), not only the run's first."""
+    kl = rodinia.write_app(str(tmp_path / "p"), rodinia.pathfinder(4000, 12, 2))
+    lines = open(kl).read().splitlines()
+    ks = [i for i, l in enumerate(lines) if l.endswith((".traceg", ".asimk", ".traceg.gz"))]
+    assert len(ks) >= 3
+    # a host copy in front of the second kernel
+    lines.insert(ks[1], "MemcpyHtoD,0x7f0000000000,4096")
+    open(kl, "w").write("\n".join(lines) + "\n")
+    base = _run(native, kl, {"-sim_first_kernel_latency": "777"})
+    every = _run(native, kl, {"-sim_first_kernel_latency": "777", "-sim_copy_latency_every_kernel": "1"})
+    kb = [k["cycles"] for k in base.kernels]
+    ke = [k["cycles"] for k in every.kernels]
+    assert ke[0] == kb[0]
+    assert 777 <= ke[1] - kb[1] <= 777 + 32
+    assert ke[2:] == kb[2:]
