@@ -100,6 +100,14 @@ void apply_router_params(SimCfg& c, const std::map<std::string, std::string>& kv
     c.rt_alloc = RT_SEP_INPUT_FIRST;
   } else if (al == "separable_output_first") {
     c.rt_alloc = RT_SEP_OUTPUT_FIRST;
+  } else if (al == "wavefront" || al == "rr_wavefront") {
+    c.rt_alloc = RT_WAVEFRONT;
+  } else if (al == "max_size") {
+    c.rt_alloc = RT_MAX_SIZE;
+  } else if (al == "pim") {
+    c.rt_alloc = RT_PIM;
+  } else if (al == "loa") {
+    c.rt_alloc = RT_LOA;
   } else {
     c.rt_alloc = 0xff;  // refused only when the router model is on (-icnt_link_contention 2)
   }

@@ -1054,7 +1054,7 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
     c.link_contention = (uint16_t)lc;
     if (lc == 2 && c.rt_alloc == 0xff)
       throw OptionError("-icnt_link_contention 2: the .icnt file's sw_allocator is not modelled "
-                        "(islip, separable_input_first, separable_output_first)");
+                        "(islip, separable_input_first, separable_output_first, wavefront, rr_wavefront, max_size, pim, loa)");
   } else if (r.geti("-network_mode") != 2) {
     throw OptionError("-network_mode must be 1 (intersim topology) or 2 (local crossbar)");
   }

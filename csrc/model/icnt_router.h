@@ -52,7 +52,24 @@ constexpr uint32_t kRtNone = 0xffffffffu;
 constexpr uint32_t kRtMaxPktBytes = 136;  // 8 B header + 128 B of data
 constexpr uint32_t kRtOutSlack = 16;      // output-buffer flits a speedup > 1 may queue ahead of its link
 
-enum RtAlloc : uint8_t { RT_ISLIP = 0, RT_SEP_INPUT_FIRST = 1, RT_SEP_OUTPUT_FIRST = 2 };
+enum RtAlloc : uint8_t {
+  RT_ISLIP = 0,
+  RT_SEP_INPUT_FIRST = 1,
+  RT_SEP_OUTPUT_FIRST = 2,
+  RT_WAVEFRONT = 3,  // diagonals of the request matrix from a priority diagonal that rotates every cycle
+  RT_MAX_SIZE = 4,   // maximum matching (augmenting paths)
+  RT_PIM = 5,        // parallel iterative matching (random grants / accepts, hashed from the cycle)
+  RT_LOA = 6,        // lonely output: the side with the fewest requests wins
+};
+
+// deterministic "random" number of parallel iterative matching: the same on
+// every host and engine
+SIM_HDI uint64_t rt_hash(uint64_t a, uint64_t b) {
+  uint64_t z = a * 0x9e3779b97f4a7c15ull ^ (b + 0x632be59bd9b4e019ull);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
 
 // interconnect nodes of the topology
 SIM_HDI uint64_t icnt_node_count(const SimCfg& c) {
@@ -118,6 +135,7 @@ struct RtWork {
   uint32_t *shead, *stail, *sfl, *svc, *slist, *sflag;
   uint32_t *rq_u, *rq_v, *rq_l;
   uint32_t *g_in, *g_key, *g_tag, *a_l, *a_v, *a_key, *a_tag, *m_u, *m_l;
+  uint32_t *rq_k, *rq_o, *gb, *ge, *ocnt, *vis, *st_u, *st_e;  // wavefront order, max-size search, LOA counts
 };
 
 // carve the scratch of a pass out of `base` (nullptr: size only); returns
@@ -179,6 +197,14 @@ SIM_HDI uint64_t rt_carve(const RtDims& d, uint32_t* base, RtWork* w) {
   t.a_key = take32(d.U);
   t.a_tag = take32(d.U);
   t.m_u = take32(d.U);
+  t.rq_k = take32(uv);
+  t.rq_o = take32(uv);
+  t.gb = take32(d.U);
+  t.ge = take32(d.U);
+  t.ocnt = take32(d.L);
+  t.vis = take32(d.L);
+  t.st_u = take32((uint64_t)d.U + 1);
+  t.st_e = take32((uint64_t)d.U + 1);
   if (w) *w = t;
   return off + 2;
 }
@@ -273,7 +299,8 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
     w.actf[u] = 0;
     w.a_tag[u] = w.m_u[u] = 0;
   }
-  for (uint32_t l = 0; l < L; ++l) w.g_tag[l] = w.m_l[l] = 0;
+  for (uint32_t l = 0; l < L; ++l) w.g_tag[l] = w.m_l[l] = w.vis[l] = 0;
+  uint32_t dfs = 0;
   uint32_t nact = 0, tag = 0, rtag = 0, cr_r = 0, cr_w = 0, remaining = np, acc = 0;
   auto activate = [&](uint32_t u) {
     if (!w.actf[u]) {
@@ -393,7 +420,125 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
       for (uint32_t it = 0; it < iters; ++it) {
         ++tag;
         bool any = false;
-        if (c.rt_alloc == RT_SEP_INPUT_FIRST) {
+        if (c.rt_alloc == RT_WAVEFRONT || c.rt_alloc == RT_MAX_SIZE) {
+          // one-shot allocators: a single iteration finds the whole matching
+          if (it > 0) break;
+          if (c.rt_alloc == RT_WAVEFRONT) {
+            // diagonal (u + l) mod n of the request matrix, from the priority
+            // diagonal of this cycle; within a diagonal no two cells share a
+            // row or a column
+            const uint32_t n = U > L ? U : L, pd = (uint32_t)(now % n);
+            for (uint32_t j = 0; j < nrq; ++j) {
+              w.rq_k[j] = (w.rq_u[j] + w.rq_l[j] + n - pd) % n;
+              uint32_t q = j;  // insertion into the order by (diagonal, request)
+              while (q > 0 && w.rq_k[w.rq_o[q - 1]] > w.rq_k[j]) {
+                w.rq_o[q] = w.rq_o[q - 1];
+                --q;
+              }
+              w.rq_o[q] = j;
+            }
+            for (uint32_t q = 0; q < nrq; ++q) {
+              const uint32_t j = w.rq_o[q], u = w.rq_u[j], l = w.rq_l[j];
+              if (w.a_tag[u] == tag || w.g_tag[l] == tag) continue;
+              w.a_tag[u] = w.g_tag[l] = tag;
+              w.a_l[u] = l;
+              w.a_v[u] = w.rq_v[j];
+              w.g_in[l] = u;
+            }
+          } else {
+            // maximum matching: an augmenting path from every input in turn
+            // (its requests are contiguous in the request list)
+            for (uint32_t j = 0; j < nrq; ++j) {
+              if (j == 0 || w.rq_u[j - 1] != w.rq_u[j]) w.gb[w.rq_u[j]] = j;
+              w.ge[w.rq_u[j]] = j + 1;
+            }
+            for (uint32_t j = 0; j < nrq; j = w.ge[w.rq_u[j]]) {
+              ++dfs;
+              uint32_t sp = 1;
+              w.st_u[0] = w.rq_u[j];
+              w.st_e[0] = w.gb[w.rq_u[j]];
+              while (sp > 0) {
+                const uint32_t u = w.st_u[sp - 1], e = w.st_e[sp - 1];
+                if (e >= w.ge[u]) {
+                  --sp;
+                  continue;
+                }
+                w.st_e[sp - 1] = e + 1;
+                const uint32_t l = w.rq_l[e];
+                if (w.vis[l] == dfs) continue;
+                w.vis[l] = dfs;
+                if (w.g_tag[l] != tag) {
+                  // free output: flip the path (every frame takes the edge it tried last)
+                  for (uint32_t k = sp; k-- > 0;) {
+                    const uint32_t uu = w.st_u[k], ee = w.st_e[k] - 1, ll = w.rq_l[ee];
+                    w.g_tag[ll] = tag;
+                    w.g_in[ll] = uu;
+                    w.a_tag[uu] = tag;
+                    w.a_l[uu] = ll;
+                    w.a_v[uu] = w.rq_v[ee];
+                  }
+                  break;
+                }
+                if (sp <= U) {  // the output's input looks for another output
+                  w.st_u[sp] = w.g_in[l];
+                  w.st_e[sp] = w.gb[w.g_in[l]];
+                  ++sp;
+                }
+              }
+            }
+          }
+        } else if (c.rt_alloc == RT_PIM || c.rt_alloc == RT_LOA) {
+          // requests per output (LOA's loneliness) and per input
+          for (uint32_t j = 0; j < nrq; ++j) w.ocnt[w.rq_l[j]] = 0;
+          for (uint32_t j = 0; j < nrq; ++j) {
+            const uint32_t u = w.rq_u[j], l = w.rq_l[j];
+            if (w.m_u[u] == rtag || w.m_l[l] == rtag) continue;
+            ++w.ocnt[l];
+            if (j == 0 || w.rq_u[j - 1] != u) w.gb[u] = j;
+            w.ge[u] = j + 1;
+          }
+          const uint64_t seed = now * 0x100000001b3ull + (uint64_t)rtag * 131u + it;
+          // outputs grant: PIM uniformly at random (reservoir over the
+          // requesters), LOA to the input with the fewest requests
+          for (uint32_t j = 0; j < nrq; ++j) {
+            const uint32_t u = w.rq_u[j], l = w.rq_l[j];
+            if (w.m_u[u] == rtag || w.m_l[l] == rtag) continue;
+            if (c.rt_alloc == RT_PIM) {
+              const uint32_t n = w.g_tag[l] == tag ? w.g_key[l] + 1 : 1;
+              if (n == 1 || rt_hash(seed, (uint64_t)l << 20 | n) % n == 0) w.g_in[l] = u;
+              w.g_tag[l] = tag;
+              w.g_key[l] = n;
+            } else {
+              const uint32_t key = (w.ge[u] - w.gb[u]) << 20 | (uint32_t)((u + U - gptr[l] % U) % U);
+              if (w.g_tag[l] != tag || key < w.g_key[l]) {
+                w.g_tag[l] = tag;
+                w.g_key[l] = key;
+                w.g_in[l] = u;
+              }
+            }
+          }
+          for (uint32_t j = 0; j < nrq; ++j) {
+            const uint32_t u = w.rq_u[j], l = w.rq_l[j];
+            if (w.g_tag[l] != tag || w.g_in[l] != u) continue;
+            if (c.rt_alloc == RT_PIM) {
+              const uint32_t n = w.a_tag[u] == tag ? w.a_key[u] + 1 : 1;
+              if (n == 1 || rt_hash(seed + 7, (uint64_t)u << 20 | n) % n == 0) {
+                w.a_l[u] = l;
+                w.a_v[u] = w.rq_v[j];
+              }
+              w.a_tag[u] = tag;
+              w.a_key[u] = n;
+            } else {
+              const uint32_t key = w.ocnt[l] << 20 | (uint32_t)((l + L - aptr[u] % L) % L);
+              if (w.a_tag[u] != tag || key < w.a_key[u]) {
+                w.a_tag[u] = tag;
+                w.a_key[u] = key;
+                w.a_l[u] = l;
+                w.a_v[u] = w.rq_v[j];
+              }
+            }
+          }
+        } else if (c.rt_alloc == RT_SEP_INPUT_FIRST) {
           // inputs choose first (accept pointer), then outputs (grant pointer)
           for (uint32_t j = 0; j < nrq; ++j) {
             const uint32_t u = w.rq_u[j], l = w.rq_l[j];

@@ -384,7 +384,7 @@ def test_router_state_checkpoint_resumes_exactly(native, tmp_path):
 
 def test_router_unmodelled_allocator_refused_only_when_used(native, tmp_path):
     p = tmp_path / "wf.icnt"
-    p.write_text(presets.render_icnt(presets.icnt_params(k=32, sw_allocator="wavefront")))
+    p.write_text(presets.render_icnt(presets.icnt_params(k=32, sw_allocator="select")))
     args = presets.args_for("QV100", {"-gpgpu_n_clusters": "16", "-gpgpu_n_mem": "8",
                                       "-network_mode": "1", "-inter_config_file": str(p)})
     native.parse_config(args)  # the latency model does not need the allocator
@@ -407,3 +407,21 @@ def test_router_model_gpu_matches_cpu(native, tmp_path):
             res.append((s.tot_cycle, _link_stat(s.output, "Network_link_delayed_packets"),
                         _link_stat(s.output, "Network_link_wait_cycles")))
         assert res[0] == res[1] and res[0][1] > 0, name
+
+
+def test_router_allocators_match_quality(native):
+    """With 4 VCs per input a crossbar input offers several outputs, so the
+    switch allocator's matching quality shows: a maximum-size matching beats
+    the wavefront allocator, which beats one iteration of iSLIP; more iSLIP
+    iterations help; every allocator is deterministic and deadlock free."""
+    sat = {}
+    for al in ("islip", "separable_input_first", "separable_output_first", "wavefront", "max_size", "pim", "loa"):
+        t = _rt_icnt(k=32, n=1, num_vcs="4", sw_allocator=al)
+        r = native.icnt_open_loop(t, "uniform", 1.0, 1, 2000, 500, 3)
+        assert r == native.icnt_open_loop(t, "uniform", 1.0, 1, 2000, 500, 3) and r["deadlocked"] == 0, al
+        sat[al] = r["accepted"]
+        low = native.icnt_open_loop(t, "uniform", 0.1, 1, 2000, 500, 3)
+        assert low["avg_latency"] < 1.1 * low["zero_load_latency"], al
+    assert sat["max_size"] >= sat["wavefront"] > sat["islip"] + 0.1
+    it4 = native.icnt_open_loop(_rt_icnt(k=32, n=1, num_vcs="4", alloc_iters="4"), "uniform", 1.0, 1, 2000, 500, 3)
+    assert it4["accepted"] > sat["islip"] + 0.05
