@@ -63,7 +63,8 @@ def main(argv=None) -> int:
         print(f"====== Traffic {a.traffic}, injection rate {c['rate']:.3f} ======")
         print(f"Overall average latency = {c['avg_latency']:.2f} (zero load {c['zero_load_latency']:.2f}, "
               f"max {c['max_latency']:.0f})")
-        print(f"Overall average accepted rate = {c['accepted']:.4f} (offered {c['offered']:.4f})")
+        print(f"Overall average accepted rate = {c['accepted']:.4f} (offered {c['offered']:.4f}; "
+              f"drain rate {c['drain_throughput']:.4f})")
         print(f"Packets = {c['measured_packets']} measured of {c['packets']}"
               + (f", {c['deadlocked']} deadlocked" if c["deadlocked"] else ""))
     print(f"Saturation (latency <= 3x zero load): {saturation(curve):.3f} flits/node/cycle")

@@ -256,6 +256,7 @@ PYBIND11_MODULE(_asim, m) {
         d["measured_packets"] = r.measured_packets;
         d["offered"] = r.offered;
         d["accepted"] = r.accepted;
+        d["drain_throughput"] = r.drain_throughput;
         d["avg_latency"] = r.avg_latency;
         d["max_latency"] = r.max_latency;
         d["zero_load_latency"] = r.zero_load_latency;

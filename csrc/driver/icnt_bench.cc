@@ -125,9 +125,10 @@ OpenLoopResult icnt_open_loop(const std::string& icnt_text, const OpenLoopParams
   res.packets = np;
   res.deadlocked = np ? rt_simulate(c, d, st.data(), w, np) : 0;
   double lat = 0, zero = 0;
-  uint64_t meas = 0, ejected = 0;
+  uint64_t meas = 0, ejected = 0, last = 0;
   for (uint32_t i = 0; i < np; ++i) {
     const uint64_t a = w.tarr[i];
+    last = std::max(last, a);
     if (a >= prm.warmup && a < prm.cycles) ejected += pf;
     if (tinj[i] >= prm.warmup) {
       lat += (double)(a - tinj[i]);
@@ -142,6 +143,9 @@ OpenLoopResult icnt_open_loop(const std::string& icnt_text, const OpenLoopParams
   res.avg_latency = meas ? lat / meas : 0;
   res.zero_load_latency = meas ? zero / meas : 0;
   res.measured_packets = meas;
+  // above saturation the window sees the network before its queues settle;
+  // the drain rate is the bottleneck's (open loop, every packet delivered)
+  res.drain_throughput = np && last ? (double)np * pf / ((double)N * (double)(last + 1)) : 0;
   return res;
 }
 

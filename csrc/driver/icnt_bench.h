@@ -17,6 +17,7 @@ struct OpenLoopResult {
   uint32_t nodes = 0;
   uint64_t packets = 0, measured_packets = 0;
   double offered = 0, accepted = 0;         // flits per node per cycle over the measurement window
+  double drain_throughput = 0;              // all flits / node / cycle from the first injection to the last ejection
   double avg_latency = 0, max_latency = 0;  // creation to tail ejection, cycles
   double zero_load_latency = 0;             // the same packets' uncontended traversal
   uint32_t deadlocked = 0;

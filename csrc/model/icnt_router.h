@@ -49,6 +49,7 @@
 namespace asim {
 
 constexpr uint32_t kRtNone = 0xffffffffu;
+constexpr uint32_t kRtUnrouted = 0x7fffffffu;  // an adaptive head's next link, not chosen yet
 constexpr uint32_t kRtMaxPktBytes = 136;  // 8 B header + 128 B of data
 constexpr uint32_t kRtOutSlack = 16;      // output-buffer flits a speedup > 1 may queue ahead of its link
 
@@ -122,7 +123,7 @@ SIM_HDI uint64_t rt_state_words(const RtDims& d) { return 2ull * d.L + 2ull * d.
 
 // scratch (u32 words) of one pass
 struct RtWork {
-  uint32_t *src, *dst, *nfl, *fbase, *roff, *nh, *next, *bidx;
+  uint32_t *src, *dst, *nfl, *fbase, *roff, *nh, *next, *bidx, *pcur;
   uint64_t *tinj, *tarr;
   uint64_t* ready;
   uint32_t *fpk, *fhop;
@@ -167,6 +168,7 @@ SIM_HDI uint64_t rt_carve(const RtDims& d, uint32_t* base, RtWork* w) {
   t.nh = take32(d.np);
   t.next = take32(d.np);
   t.bidx = take32(d.np);
+  t.pcur = take32(d.np);
   t.fpk = take32(d.nf);
   t.fhop = take32(d.nf);
   t.route = take32((uint64_t)d.np * d.H);
@@ -232,6 +234,10 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
   const uint32_t iters = c.rt_iters ? c.rt_iters : 1;
   const bool dateline = c.topo == TOPO_TORUS && V >= 2;
   const uint32_t tk = c.topo_k ? c.topo_k : 2, tn = c.topo_n ? c.topo_n : 1;
+  // minimal adaptive routing on meshes: VC 0 is the dimension-order escape
+  // channel, VCs 1.. are adaptive (Duato); needs >= 2 VCs
+  const bool adaptive = c.rt_route == 1 && (c.topo == TOPO_MESH || c.topo == TOPO_CMESH) && V >= 2;
+  const uint32_t aconc = c.topo == TOPO_CMESH ? (c.topo_conc ? c.topo_conc : 1) : 1, aP = 2 * tn + aconc;
   // ---- routes, flits, source queues (injection order: time, then packet) ----
   for (uint32_t s = 0; s < N; ++s) {
     w.shead[s] = w.stail[s] = kRtNone;
@@ -243,7 +249,13 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
   for (uint32_t p = 0; p < np; ++p) {
     w.roff[p] = p * d.H;
     uint32_t h = 0, dim = ~0u, crossed = 0;
-    icnt_route(c, w.src[p], w.dst[p], [&](uint32_t l) {
+    if (adaptive) {
+      // the head chooses every hop as it goes (adapt_choice): the minimal
+      // route's length is known, its links are not
+      h = icnt_routers(c, w.src[p], w.dst[p]);
+      for (uint32_t i = 0; i < d.H; ++i) w.route[p * d.H + i] = kRtUnrouted;
+      w.pcur[p] = w.src[p] / aconc;
+    } else icnt_route(c, w.src[p], w.dst[p], [&](uint32_t l) {
       // torus with >= 2 VCs: dateline classes (the upper half of the VCs
       // after the wrap-around link of the current dimension; reference
       // routefunc.cpp dim_order_torus), kept in the link's top bit
@@ -313,13 +325,48 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
     ++w.vcnt[uv];
   };
   // a free VC with room on downstream unit du (kRtNone if none)
+  // VC class: dateline (torus) 0 lower / 1 upper half; adaptive 0 escape VC
+  // / 1 adaptive VCs; 2 any
   auto free_vc = [&](uint32_t du, uint32_t cls) -> uint32_t {
-    const uint32_t v0 = dateline && cls ? V / 2 : 0, v1 = dateline && !cls ? V / 2 : V;
+    uint32_t v0 = 0, v1 = V;
+    if (cls < 2 && dateline) {
+      v0 = cls ? V / 2 : 0;
+      v1 = cls ? V : V / 2;
+    } else if (cls < 2 && adaptive) {
+      v0 = cls ? 1 : 0;
+      v1 = cls ? V : 1;
+    }
     for (uint32_t v = v0; v < v1; ++v) {
       const uint32_t i = du * V + v;
       if (w.vown[i] == kRtNone && w.vocc[i] < B) return v;
     }
     return kRtNone;
+  };
+  // the head of packet p chooses its next link: the productive direction
+  // whose downstream unit has an adaptive VC with the most free slots
+  // (lowest dimension on ties), else the dimension-order link if its escape
+  // VC is free; kRtUnrouted if blocked.  Returns link | class << 31.
+  auto adapt_choice = [&](uint32_t p) -> uint32_t {
+    const uint32_t cur = w.pcur[p], dst = w.dst[p] / aconc;
+    if (cur == dst) return cur * aP + 2 * tn + w.dst[p] % aconc;  // ejection
+    uint32_t best = kRtUnrouted, best_free = 0, esc = kRtUnrouted;
+    uint64_t pw = 1;
+    for (uint32_t dd = 0; dd < tn; ++dd, pw *= tk) {
+      const uint32_t x = (uint32_t)((cur / pw) % tk), y = (uint32_t)((dst / pw) % tk);
+      if (x == y) continue;
+      const uint32_t l = cur * aP + 2 * dd + (y > x ? 0u : 1u), du = N + l;
+      if (esc == kRtUnrouted) esc = l;
+      for (uint32_t v = 1; v < V; ++v) {
+        const uint32_t i = du * V + v;
+        if (w.vown[i] == kRtNone && w.vocc[i] < B && B - w.vocc[i] > best_free) {
+          best_free = B - w.vocc[i];
+          best = l;
+        }
+      }
+    }
+    if (best != kRtUnrouted) return best | 1u << 31;
+    if (esc != kRtUnrouted && free_vc(N + esc, 0) != kRtNone) return esc;
+    return kRtUnrouted;
   };
   uint64_t now = ~0ull;
   for (uint32_t i = 0; i < nsrc; ++i) {
@@ -348,7 +395,7 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
         w.slist[keep++] = s;
         if (now < w.tinj[p] || now < inj_next[s]) continue;
         if (w.svc[s] == kRtNone) {
-          const uint32_t v = free_vc(s, 0);
+          const uint32_t v = free_vc(s, 2);
           if (v == kRtNone) continue;
           w.svc[s] = v;
           w.vown[s * V + v] = p;
@@ -390,6 +437,11 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
           const uint32_t f = w.ring[(uint64_t)uv * B + w.vhead[uv]];
           if (w.ready[f] > now) continue;
           const uint32_t p = w.fpk[f], h = w.fhop[f];
+          if (adaptive && f == w.fbase[p]) {
+            const uint32_t ch = adapt_choice(p);
+            if (ch == kRtUnrouted) continue;
+            w.route[w.roff[p] + h] = ch;
+          }
           const uint32_t rl = w.route[w.roff[p] + h], l = rl & 0x7fffffffu;
           const bool last = h + 1 >= w.nh[p];
           if (!last) {
@@ -620,6 +672,12 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
               w.vout[uv] = dv;
               w.vown[du * V + dv] = p;
             }
+            if (adaptive && head) {
+              // the head moves one router along dimension port / 2
+              const uint32_t port = l % aP, dd = port / 2;
+              const uint32_t pw = (uint32_t)ipow(tk, dd);
+              w.pcur[p] = port % 2 == 0 ? w.pcur[p] + pw : w.pcur[p] - pw;
+            }
             const uint32_t duv = du * V + w.vout[uv];
             ++w.vocc[duv];
             push(duv, f);
@@ -674,7 +732,7 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
           const uint32_t f = w.ring[(uint64_t)uv * B + w.vhead[uv]];
           uint64_t t = w.ready[f] > in_free[u] ? w.ready[f] : in_free[u];
           const uint32_t l = w.route[w.roff[w.fpk[f]] + w.fhop[f]] & 0x7fffffffu;
-          if (link_next[l] > 1 + slack && link_next[l] - 1 - slack > t) t = link_next[l] - 1 - slack;
+          if (l < L && link_next[l] > 1 + slack && link_next[l] - 1 - slack > t) t = link_next[l] - 1 - slack;
           if (t > now && t < nxt) nxt = t;  // (t <= now: waiting for a VC or a credit)
         }
       }
