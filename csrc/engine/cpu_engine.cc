@@ -158,7 +158,8 @@ class CpuEngine : public Engine {
     link_free_.clear();
     link_refs_.clear();
     n_link_state_ = 0;
-    if (c.link_contention && (icnt_link_count(c) > kMaxIcntLinks || !icnt_contention_fits(c, cap_req_, cap_rep_)))
+    if (c.link_contention && (icnt_link_count(c) > kMaxIcntLinks || !icnt_contention_fits(c, cap_req_, cap_rep_) ||
+                              icnt_scratch_words(c, cap_req_, cap_rep_) > kMaxIcntScratchWords))
       throw std::runtime_error("-icnt_link_contention: topology or mailboxes too large for the link pass");
     if (icnt_contention_on(c)) {
       // the link model's persistent words, then its two statistics words

@@ -780,7 +780,8 @@ class GpuEngine : public Engine {
       pool_alloc(&d_mall_, sizeof(L2Line) * n_mall_);
       HIPCHECK(hipMemset(d_mall_, 0, sizeof(L2Line) * n_mall_));
     }
-    if (c.link_contention && (icnt_link_count(c) > kMaxIcntLinks || !icnt_contention_fits(c, cap_req_, cap_rep_)))
+    if (c.link_contention && (icnt_link_count(c) > kMaxIcntLinks || !icnt_contention_fits(c, cap_req_, cap_rep_) ||
+                              icnt_scratch_words(c, cap_req_, cap_rep_) > kMaxIcntScratchWords))
       throw std::runtime_error("-icnt_link_contention: topology or mailboxes too large for the link pass");
     n_links_ = icnt_contention_on(c) ? (size_t)icnt_state_words(c, cap_req_, cap_rep_) : 0;
     if (n_links_) {

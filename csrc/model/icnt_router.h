@@ -52,6 +52,7 @@ constexpr uint32_t kRtNone = 0xffffffffu;
 constexpr uint32_t kRtUnrouted = 0x7fffffffu;  // an adaptive head's next link, not chosen yet
 constexpr uint32_t kRtMaxPktBytes = 136;  // 8 B header + 128 B of data
 constexpr uint32_t kRtOutSlack = 16;      // output-buffer flits a speedup > 1 may queue ahead of its link
+constexpr uint64_t kMaxIcntScratchWords = 1ull << 28;  // 1 GiB of per-epoch router-pass scratch
 
 enum RtAlloc : uint8_t {
   RT_ISLIP = 0,
