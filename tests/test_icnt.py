@@ -448,3 +448,21 @@ def test_router_minimal_adaptive_routing(native):
     assert lo_a["avg_latency"] < 1.05 * lo_a["zero_load_latency"]
     u = native.icnt_open_loop(ada, "uniform", 1.0, 2, 2000, 500, 1)
     assert u["deadlocked"] == 0 and u["accepted"] > 0.3
+
+
+def test_booksim_standalone_cli(tmp_path, capsys):
+    """python -m accel_sim_framework_distributed_amd.icnt.booksim: Booksim's
+    standalone mode over a .icnt file, one block per injection rate and a JSON
+    curve."""
+    from accel_sim_framework_distributed_amd.icnt import booksim
+    f = tmp_path / "x.icnt"
+    f.write_text(_rt_icnt(k=16, n=1))
+    out = tmp_path / "curve.json"
+    assert booksim.main([str(f), "--rates", "0.1,1.0", "--cycles", "1500", "--warmup", "300",
+                         "--json", str(out)]) == 0
+    text = capsys.readouterr().out
+    assert text.count("Overall average latency") == 2 and "Saturation" in text
+    import json
+    curve = json.load(open(out))["curve"]
+    assert [c["rate"] for c in curve] == [0.1, 1.0]
+    assert curve[1]["accepted"] < 0.75 and booksim.saturation(curve) == 0.1
