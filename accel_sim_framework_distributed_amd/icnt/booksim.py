@@ -3,7 +3,8 @@
 
 Reads a Booksim ``.icnt`` file (topology, router pipeline, ``num_vcs``,
 ``vc_buf_size``, ``sw_allocator``, ``alloc_iters``, ``credit_delay``,
-``internal_speedup``) and drives open-loop synthetic traffic through the
+``internal_speedup``; the ``power_*`` per-event energies of the network
+power estimate) and drives open-loop synthetic traffic through the
 input-queued router model of ``csrc/model/icnt_router.h`` -- the same code
 the simulator runs per epoch with ``-icnt_link_contention 2``.
 
@@ -65,6 +66,9 @@ def main(argv=None) -> int:
               f"max {c['max_latency']:.0f})")
         print(f"Overall average accepted rate = {c['accepted']:.4f} (offered {c['offered']:.4f}; "
               f"drain rate {c['drain_throughput']:.4f})")
+        e = c["energy_pj"]
+        print(f"Network power = {c['power_w']:.3f} W (energy pJ: buffer {e['buffer']:.3g}, crossbar {e['crossbar']:.3g}, "
+              f"link {e['link']:.3g}, allocator {e['allocator']:.3g}, leakage {e['leakage']:.3g})")
         print(f"Packets = {c['measured_packets']} measured of {c['packets']}"
               + (f", {c['deadlocked']} deadlocked" if c["deadlocked"] else ""))
     print(f"Saturation (latency <= 3x zero load): {saturation(curve):.3f} flits/node/cycle")

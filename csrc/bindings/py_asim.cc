@@ -261,6 +261,19 @@ PYBIND11_MODULE(_asim, m) {
         d["max_latency"] = r.max_latency;
         d["zero_load_latency"] = r.zero_load_latency;
         d["deadlocked"] = r.deadlocked;
+        py::dict a;
+        const char* an[] = {"buffer_writes", "buffer_reads", "link_flits", "eject_flits", "sa_requests", "credits",
+                            "switch_passes"};
+        for (int i = 0; i < 7; ++i) a[an[i]] = r.activity[i];
+        d["activity"] = a;
+        py::dict e;
+        e["buffer"] = r.e_buffer;
+        e["crossbar"] = r.e_xbar;
+        e["link"] = r.e_link;
+        e["allocator"] = r.e_alloc;
+        e["leakage"] = r.e_leak;
+        d["energy_pj"] = e;
+        d["power_w"] = r.power_w;
         return d;
       },
       py::arg("icnt_text"), py::arg("traffic") = "uniform", py::arg("rate") = 0.1, py::arg("packet_flits") = 1,

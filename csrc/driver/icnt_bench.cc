@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <stdexcept>
 #include <vector>
 
@@ -84,7 +85,8 @@ uint32_t destination(const std::string& t, uint32_t s, uint32_t N, uint32_t k, u
 OpenLoopResult icnt_open_loop(const std::string& icnt_text, const OpenLoopParams& prm) {
   SimCfg c{};
   c.flit_size = 32;
-  const uint64_t nodes = apply_topology(c, parse_booksim_config(icnt_text));
+  const auto kv = parse_booksim_config(icnt_text);
+  const uint64_t nodes = apply_topology(c, kv);
   if (c.rt_alloc == 0xff) throw std::invalid_argument("sw_allocator not modelled");
   c.link_contention = 2;
   if (nodes > (1u << 20)) throw std::invalid_argument("topology too large");
@@ -123,7 +125,9 @@ OpenLoopResult icnt_open_loop(const std::string& icnt_text, const OpenLoopParams
   OpenLoopResult res;
   res.nodes = N;
   res.packets = np;
-  res.deadlocked = np ? rt_simulate(c, d, st.data(), w, np) : 0;
+  uint64_t act[RT_ACT_COUNT] = {};
+  res.deadlocked = np ? rt_simulate(c, d, st.data(), w, np, act) : 0;
+  for (int i = 0; i < RT_ACT_COUNT; ++i) res.activity[i] = act[i];
   double lat = 0, zero = 0;
   uint64_t meas = 0, ejected = 0, last = 0;
   for (uint32_t i = 0; i < np; ++i) {
@@ -146,6 +150,24 @@ OpenLoopResult icnt_open_loop(const std::string& icnt_text, const OpenLoopParams
   // above saturation the window sees the network before its queues settle;
   // the drain rate is the bottleneck's (open loop, every packet delivered)
   res.drain_throughput = np && last ? (double)np * pf / ((double)N * (double)(last + 1)) : 0;
+  // network energy from the activity (Booksim power_module.cpp's terms:
+  // input buffers, crossbar, channels, allocators, buffer leakage); the
+  // per-event energies are .icnt keys with ~22 nm Orion-class defaults
+  auto num = [&](const char* k, double dflt) {
+    auto it = kv.find(k);
+    return it == kv.end() ? dflt : strtod(it->second.c_str(), nullptr);
+  };
+  const double bits = 8.0 * c.flit_size;
+  res.e_buffer = num("power_buffer_pj_per_bit", 0.08) * bits * (double)(act[RT_ACT_BUF_WRITE] + act[RT_ACT_BUF_READ]);
+  res.e_xbar = num("power_xbar_pj_per_bit", 0.06) * bits * (double)act[RT_ACT_BUF_READ];
+  res.e_link = num("power_link_pj_per_bit_mm", 0.15) * num("power_link_mm", 1.0) * bits *
+               (double)(act[RT_ACT_LINK] + act[RT_ACT_EJECT]);
+  res.e_alloc = num("power_alloc_pj_per_request", 0.5) * (double)act[RT_ACT_SA_REQ];
+  const double ghz = num("power_clock_ghz", 1.0), t_ns = (double)(last + 1) / ghz;
+  // leakage: uW per buffered flit slot of every input VC
+  res.e_leak = num("power_buffer_leak_uw_per_flit", 0.5) * 1e-6 * (double)d.U * d.V * d.B * t_ns * 1e3;
+  const double e = res.e_buffer + res.e_xbar + res.e_link + res.e_alloc + res.e_leak;
+  res.power_w = t_ns > 0 ? e * 1e-12 / (t_ns * 1e-9) : 0;
   return res;
 }
 

@@ -21,6 +21,11 @@ struct OpenLoopResult {
   double avg_latency = 0, max_latency = 0;  // creation to tail ejection, cycles
   double zero_load_latency = 0;             // the same packets' uncontended traversal
   uint32_t deadlocked = 0;
+  // router activity (icnt_router.h RtAct order) and the energy of the run by
+  // component (Booksim's power module role; per-event energies from the
+  // .icnt file's power_* keys), pJ, and the average network power, W
+  uint64_t activity[8] = {};
+  double e_buffer = 0, e_xbar = 0, e_link = 0, e_alloc = 0, e_leak = 0, power_w = 0;
 };
 
 // icnt_text: a Booksim .icnt file's text (topology, router pipeline and

@@ -223,7 +223,21 @@ SIM_HDI uint64_t rt_uncontended(const SimCfg& c, uint32_t routers, uint32_t nfl)
 // tail flit's arrival, icnt cycles) and returns the number of packets that
 // could not be delivered (a routing deadlock: they get their uncontended
 // traversal after the last delivery).  Single-threaded.
-SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, const RtWork& w, uint32_t np) {
+// Router activity of a pass (the inputs of Booksim's power module,
+// intersim2/power/power_module.cpp): act[RT_ACT_*] when `act` is given.
+enum RtAct : int {
+  RT_ACT_BUF_WRITE = 0,  // flits written into an input VC buffer (injection included)
+  RT_ACT_BUF_READ,       // flits read out of an input VC buffer = crossbar traversals
+  RT_ACT_LINK,           // flits onto a router-to-router link
+  RT_ACT_EJECT,          // flits onto an ejection link
+  RT_ACT_SA_REQ,         // switch-allocator requests
+  RT_ACT_CREDIT,         // credits returned upstream
+  RT_ACT_PASSES,         // switch passes run
+  RT_ACT_COUNT
+};
+
+SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, const RtWork& w, uint32_t np,
+                             uint64_t* act = nullptr) {
   uint64_t* link_next = st;
   uint64_t* gptr = st + d.L;
   uint64_t* in_free = st + 2 * d.L;
@@ -380,6 +394,7 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
     // ---- credits that reach their upstream this cycle ----
     while (cr_r < cr_w && w.crt[cr_r] <= now) {
       --w.vocc[w.crv[cr_r]];
+      if (act) ++act[RT_ACT_CREDIT];
       ++cr_r;
       progress = true;
     }
@@ -405,6 +420,7 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
         if (w.vocc[uv] >= B) continue;
         const uint32_t i_f = w.sfl[s], f = w.fbase[p] + i_f;
         push(uv, f);
+        if (act) ++act[RT_ACT_BUF_WRITE];
         ++w.vocc[uv];
         w.fhop[f] = 0;
         w.ready[f] = now + chan + (i_f == 0 ? head_delay : body_delay);
@@ -467,6 +483,10 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
             if (w.ready[f] < w.ready[g]) w.rq_v[j] = v;
           }
         }
+      }
+      if (act) {
+        ++act[RT_ACT_PASSES];
+        act[RT_ACT_SA_REQ] += nrq;
       }
       if (!nrq) continue;
       // matching
@@ -665,6 +685,10 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
           const bool head = fi == 0, tail = fi + 1 == w.nfl[p];
           const uint64_t dep = link_next[l] > now + 1 ? link_next[l] : now + 1;
           link_next[l] = dep + 1;
+          if (act) {
+            ++act[RT_ACT_BUF_READ];
+            ++act[h + 1 < w.nh[p] ? RT_ACT_LINK : RT_ACT_EJECT];
+          }
           const uint64_t arr = dep + chan;
           if (h + 1 < w.nh[p]) {
             const uint32_t du = N + l;
@@ -682,6 +706,7 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
             const uint32_t duv = du * V + w.vout[uv];
             ++w.vocc[duv];
             push(duv, f);
+            if (act) ++act[RT_ACT_BUF_WRITE];
             w.fhop[f] = h + 1;
             w.ready[f] = arr + (head ? head_delay : body_delay);
             activate(du);

@@ -466,3 +466,24 @@ def test_booksim_standalone_cli(tmp_path, capsys):
     curve = json.load(open(out))["curve"]
     assert [c["rate"] for c in curve] == [0.1, 1.0]
     assert curve[1]["accepted"] < 0.75 and booksim.saturation(curve) == 0.1
+
+
+def test_router_activity_and_network_power(native):
+    """Booksim's power-module inputs: every delivered flit is written into and
+    read out of one input buffer per router it crosses plus the injection
+    buffer, crosses one link per hop (the last an ejection link); energy grows
+    with load and each per-event energy key scales its component."""
+    mesh = _rt_icnt(k=4, n=2, topology="mesh")
+    r = native.icnt_open_loop(mesh, "uniform", 0.2, 2, 1500, 300, 5)
+    a = r["activity"]
+    flits = 2 * r["packets"]
+    assert a["eject_flits"] == flits
+    assert a["buffer_writes"] == a["buffer_reads"] == a["link_flits"] + a["eject_flits"]
+    # (the credits of the last flits are still in flight when the pass ends)
+    assert 0 <= a["buffer_reads"] - a["credits"] < 64 and a["sa_requests"] >= a["buffer_reads"]
+    hi = native.icnt_open_loop(mesh, "uniform", 0.4, 2, 1500, 300, 5)
+    assert hi["power_w"] > r["power_w"] > 0
+    twice = native.icnt_open_loop(_rt_icnt(k=4, n=2, topology="mesh", power_link_pj_per_bit_mm="0.3"),
+                                  "uniform", 0.2, 2, 1500, 300, 5)
+    assert abs(twice["energy_pj"]["link"] - 2 * r["energy_pj"]["link"]) < 1e-6 * r["energy_pj"]["link"]
+    assert twice["energy_pj"]["buffer"] == r["energy_pj"]["buffer"]
