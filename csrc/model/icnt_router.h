@@ -138,6 +138,12 @@ struct RtWork {
   uint32_t *rq_u, *rq_v, *rq_l;
   uint32_t *g_in, *g_key, *g_tag, *a_l, *a_v, *a_key, *a_tag, *m_u, *m_l;
   uint32_t *rq_k, *rq_o, *gb, *ge, *ocnt, *vis, *st_u, *st_e;  // wavefront order, max-size search, LOA counts
+  // an explicit network (Booksim anynet, driver/icnt_bench.cc; nullptr: the
+  // topology's own routes and the uniform channel latency): the route of
+  // node pair (a, b) is rt_links[rt_off[a * N + b] .. rt_off[a * N + b + 1]),
+  // link l's channel latency lat[l], node n's injection channel inj_lat[n]
+  const uint32_t *rt_off, *rt_links;
+  const uint16_t *lat, *inj_lat;
 };
 
 // carve the scratch of a pass out of `base` (nullptr: size only); returns
@@ -270,6 +276,12 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
       h = icnt_routers(c, w.src[p], w.dst[p]);
       for (uint32_t i = 0; i < d.H; ++i) w.route[p * d.H + i] = kRtUnrouted;
       w.pcur[p] = w.src[p] / aconc;
+    } else if (w.rt_off) {
+      const uint64_t pr = (uint64_t)w.src[p] * N + w.dst[p];
+      for (uint32_t i = w.rt_off[pr]; i < w.rt_off[pr + 1]; ++i) {
+        if (h < d.H) w.route[p * d.H + h] = w.rt_links[i];
+        ++h;
+      }
     } else icnt_route(c, w.src[p], w.dst[p], [&](uint32_t l) {
       // torus with >= 2 VCs: dateline classes (the upper half of the VCs
       // after the wrap-around link of the current dimension; reference
@@ -423,7 +435,7 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
         if (act) ++act[RT_ACT_BUF_WRITE];
         ++w.vocc[uv];
         w.fhop[f] = 0;
-        w.ready[f] = now + chan + (i_f == 0 ? head_delay : body_delay);
+        w.ready[f] = now + (w.inj_lat ? w.inj_lat[s] : chan) + (i_f == 0 ? head_delay : body_delay);
         activate(s);
         inj_next[s] = now + 1;
         progress = true;
@@ -689,7 +701,7 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
             ++act[RT_ACT_BUF_READ];
             ++act[h + 1 < w.nh[p] ? RT_ACT_LINK : RT_ACT_EJECT];
           }
-          const uint64_t arr = dep + chan;
+          const uint64_t arr = dep + (w.lat ? w.lat[l] : chan);
           if (h + 1 < w.nh[p]) {
             const uint32_t du = N + l;
             if (head) {
