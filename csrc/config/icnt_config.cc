@@ -94,9 +94,10 @@ void apply_router_params(SimCfg& c, const std::map<std::string, std::string>& kv
   if (!(sp >= 1.0 && sp <= 8.0)) throw OptionError("interconnect config: internal_speedup must be 1..8");
   c.rt_speedup_q8 = (uint16_t)(sp * 256.0 + 0.5);
   // minimal adaptive routing with a dimension-order escape VC (Booksim
-  // min_adapt; meshes with >= 2 VCs), else the topology's deterministic route
+  // min_adapt; meshes with >= 2 VCs), Valiant's randomised two-phase routing
+  // (valiant; meshes with >= 2 VCs), else the topology's deterministic route
   const std::string rf = kv.count("routing_function") ? kv.at("routing_function") : "";
-  c.rt_route = (rf == "min_adapt" || rf == "adaptive") ? 1 : 0;
+  c.rt_route = (rf == "min_adapt" || rf == "adaptive") ? 1 : (rf == "valiant") ? 2 : 0;
   const std::string al = kv.count("sw_allocator") ? kv.at("sw_allocator") : "islip";
   if (al == "islip") {
     c.rt_alloc = RT_ISLIP;

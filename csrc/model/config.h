@@ -285,7 +285,7 @@ struct SimCfg {
   // .icnt file's num_vcs, vc_buf_size, alloc_iters, credit_delay,
   // sw_allocator, sw_alloc_delay and internal_speedup)
   uint8_t rt_vcs, rt_iters, rt_credit, rt_alloc, rt_sa;
-  uint8_t rt_route;        // routing_function: 0 deterministic (the topology's), 1 minimal adaptive (min_adapt)
+  uint8_t rt_route;        // routing_function: 0 deterministic (the topology's), 1 minimal adaptive (min_adapt), 2 Valiant
   uint16_t rt_buf;         // flits per virtual channel
   uint16_t rt_speedup_q8;  // switch passes per cycle x 256
   // ---- memory partition ----

@@ -113,6 +113,7 @@ SIM_HDI RtDims rt_dims(const SimCfg& c, uint32_t max_pkts, uint32_t max_flits_pe
   d.V = c.rt_vcs ? c.rt_vcs : 1;
   d.B = c.rt_buf ? c.rt_buf : 1;
   d.H = icnt_max_route(c);
+  if (c.rt_route == 2) d.H = 2 * d.H;  // Valiant: two dimension-order legs
   d.np = max_pkts;
   d.nf = max_pkts * max_flits_per_pkt;
   return d;
@@ -259,6 +260,10 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
   // channel, VCs 1.. are adaptive (Duato); needs >= 2 VCs
   const bool adaptive = c.rt_route == 1 && (c.topo == TOPO_MESH || c.topo == TOPO_CMESH) && V >= 2;
   const uint32_t aconc = c.topo == TOPO_CMESH ? (c.topo_conc ? c.topo_conc : 1) : 1, aP = 2 * tn + aconc;
+  // Valiant (mesh): dimension order to a random intermediate router, then
+  // dimension order to the destination; the second leg on the upper half of
+  // the VCs (two classes keep the two legs' channel dependences acyclic)
+  const bool valiant = c.rt_route == 2 && (c.topo == TOPO_MESH || c.topo == TOPO_CMESH) && V >= 2;
   // ---- routes, flits, source queues (injection order: time, then packet) ----
   for (uint32_t s = 0; s < N; ++s) {
     w.shead[s] = w.stail[s] = kRtNone;
@@ -276,6 +281,24 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
       h = icnt_routers(c, w.src[p], w.dst[p]);
       for (uint32_t i = 0; i < d.H; ++i) w.route[p * d.H + i] = kRtUnrouted;
       w.pcur[p] = w.src[p] / aconc;
+    } else if (valiant) {
+      // the intermediate router: a hash of the packet's source, destination
+      // and injection time (reproducible on every engine)
+      const uint32_t nr = (uint32_t)ipow(tk, tn);
+      const uint32_t mid = (uint32_t)(rt_hash(w.tinj[p] * 1000003u + w.src[p], w.dst[p]) % nr);
+      const uint32_t mid_node = mid * aconc;
+      uint32_t leg1 = 0;
+      icnt_route(c, w.src[p], mid_node, [&](uint32_t l) {
+        leg1 = l;  // (the last link is mid's ejection: dropped below)
+        if (h < d.H) w.route[p * d.H + h] = l;
+        ++h;
+      });
+      (void)leg1;
+      --h;  // drop the ejection link into the intermediate node
+      icnt_route(c, mid_node, w.dst[p], [&](uint32_t l) {
+        if (h < d.H) w.route[p * d.H + h] = l | 1u << 31;
+        ++h;
+      });
     } else if (w.rt_off) {
       const uint64_t pr = (uint64_t)w.src[p] * N + w.dst[p];
       for (uint32_t i = w.rt_off[pr]; i < w.rt_off[pr + 1]; ++i) {
@@ -356,7 +379,7 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
   // / 1 adaptive VCs; 2 any
   auto free_vc = [&](uint32_t du, uint32_t cls) -> uint32_t {
     uint32_t v0 = 0, v1 = V;
-    if (cls < 2 && dateline) {
+    if (cls < 2 && (dateline || valiant)) {
       v0 = cls ? V / 2 : 0;
       v1 = cls ? V : V / 2;
     } else if (cls < 2 && adaptive) {

@@ -521,3 +521,19 @@ def test_router_anynet_network_file(native, tmp_path):
     # injection 1 + (router 3 + channel) per router: 0 -> 1 crosses the 5-cycle
     # channel, 1 -> 0 the 1-cycle one; ejection channels 1 cycle
     assert p["zero_load_latency"] == pytest.approx(1 + 3 + 3 + 1 + (5 + 1) / 2, abs=0.6)
+
+
+def test_router_valiant_routing(native):
+    """Valiant (mesh, 2 VC classes): dimension order to a random intermediate
+    router, then to the destination -- about half the uniform-traffic
+    throughput of dimension order and about twice its low-load latency; no
+    deadlock; reproducible."""
+    kw = dict(k=8, n=2, topology="mesh", num_vcs="4")
+    dor = _rt_icnt(**kw)
+    val = _rt_icnt(routing_function="valiant", **kw)
+    d = native.icnt_open_loop(dor, "uniform", 1.0, 1, 2000, 500, 1)
+    v = native.icnt_open_loop(val, "uniform", 1.0, 1, 2000, 500, 1)
+    assert v["deadlocked"] == 0 and 0.3 < v["drain_throughput"] / d["drain_throughput"] < 0.7
+    lo = native.icnt_open_loop(val, "uniform", 0.05, 1, 2000, 500, 1)
+    assert lo["avg_latency"] > 1.5 * lo["zero_load_latency"]
+    assert lo == native.icnt_open_loop(val, "uniform", 0.05, 1, 2000, 500, 1)
