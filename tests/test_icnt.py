@@ -399,7 +399,8 @@ def test_router_model_gpu_matches_cpu(native, tmp_path):
     kl = _hotspot_app(tmp_path, "rtg", True)
     for name, kw in (("mesh", dict(k=8, n=2, topology="mesh")), ("fly", dict(k=32, n=1)),
                      ("mesh_adapt", dict(k=8, n=2, topology="mesh", num_vcs="4", routing_function="min_adapt")),
-                     ("fly_maxsize", dict(k=32, n=1, num_vcs="2", sw_allocator="max_size"))):
+                     ("fly_maxsize", dict(k=32, n=1, num_vcs="2", sw_allocator="max_size")),
+                     ("mesh_valiant", dict(k=8, n=2, topology="mesh", num_vcs="2", routing_function="valiant"))):
         args = _icnt_args(tmp_path, name, **kw)
         res = []
         for eng in ("cpu", "gpu"):
