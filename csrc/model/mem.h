@@ -147,7 +147,8 @@ struct alignas(16) ChanState {
   // MALL: read hits on their way back to the L2 (DRAM returns use ret[])
   DramRet mret[kMallRet];
   uint32_t mret_head, mret_n;
-  uint32_t mall_stamp, pad_m;
+  uint32_t mall_stamp;
+  uint32_t q_hi;  // DRAM queue slots in use lie below q_hi (dram_enqueue takes the lowest free slot)
   uint64_t q_age[kDramQ];
   uint8_t q_valid[kDramQ];
   uint16_t ocnt[kMaxSubPerCh][kMaxSmTot];  // replies put in each (dst SM) cell this epoch
@@ -250,10 +251,12 @@ SIM_HDI bool dram_room(const ChanState& ch, const SimCfg& c, bool write, uint32_
 }
 template <class P>
 SIM_HDI void dram_enqueue(ChanState& ch, const DramReq& h) {
-  ch.qw_n += h.write ? 1 : 0;
   const int f = P::find_first(kDramQ, [&](int i) -> bool { return !ch.q_valid[i]; });
+  if (f < 0) return;  // (dram_room is checked first: never full here)
+  ch.qw_n += h.write ? 1 : 0;
   ch.q[f] = h;
   ch.q_valid[f] = 1;
+  if ((uint32_t)f + 1u > ch.q_hi) ch.q_hi = (uint32_t)f + 1u;
   ch.q_age[f] = ch.q_seq++;
   ch.q_n++;
 }
@@ -750,10 +753,12 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, const MemCtx& x, uint64_
   }
   st.dram_q_occ += ch.q_n;
   if (ch.q_n == 0) return;
+  // the scans visit the slots in use only (the empty ones above never qualify)
+  const int qn = (int)ch.q_hi;
   const uint32_t burst = amax<uint32_t>(1, c.BL / (c.data_cmd_ratio ? c.data_cmd_ratio : 1));
   if (c.simple_dram) {
     // oldest request, one column access per DRAM cycle, no bank state
-    int o = P::argmin(kDramQ, [&](int i) -> uint64_t { return ch.q_valid[i] ? ch.q_age[i] : ~0ull; });
+    int o = P::argmin(qn, [&](int i) -> uint64_t { return ch.q_valid[i] ? ch.q_age[i] : ~0ull; });
     if (o < 0 || t < ch.t_ccd_ok) return;
     const DramReq r = ch.q[o];
     if (!r.write) {
@@ -771,6 +776,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, const MemCtx& x, uint64_
     ch.t_ccd_ok = t + burst;
     st.dram_busy_cycles += burst;
     ch.q_valid[o] = 0;
+    while (ch.q_hi && !ch.q_valid[ch.q_hi - 1]) --ch.q_hi;
     ch.q_n--;
     ch.qw_n -= r.write ? 1 : 0;
     if (r.sub != kSubNone) ch.sp[r.sub].n_l2dram--;
@@ -791,14 +797,14 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, const MemCtx& x, uint64_
   uint32_t col_bank = 0;
   uint64_t oldest_age = ~0ull;
   if (c.dram_sched == 0) {  // FIFO: only the oldest request may issue (column and row commands)
-    int o = P::argmin(kDramQ, [&](int i) -> uint64_t {
+    int o = P::argmin(qn, [&](int i) -> uint64_t {
       return (ch.q_valid[i] && (only == 2 || ch.q[i].write == only)) ? ch.q_age[i] : ~0ull;
     });
     oldest_age = o >= 0 ? ch.q_age[o] : ~0ull;
   }
   // no column command can issue before tCCD has elapsed: skip the scan
   if (t >= ch.t_ccd_ok) {
-    int pick = P::argmin(kDramQ, [&](int i) -> uint64_t {
+    int pick = P::argmin(qn, [&](int i) -> uint64_t {
       if (!ch.q_valid[i]) return ~0ull;
       if (c.dram_sched == 0 && ch.q_age[i] != oldest_age) return ~0ull;
       const DramReq& r = ch.q[i];
@@ -834,6 +840,7 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, const MemCtx& x, uint64_
       ch.t_ccdl_ok[dram_bkgrp(c, r.bank) & 7] = t + amax<uint32_t>(c.tCCDL, burst);
       st.dram_busy_cycles += burst;
       ch.q_valid[pick] = 0;
+      while (ch.q_hi && !ch.q_valid[ch.q_hi - 1]) --ch.q_hi;
       ch.q_n--;
       ch.qw_n -= r.write ? 1 : 0;
       if (r.sub != kSubNone) ch.sp[r.sub].n_l2dram--;
@@ -846,14 +853,14 @@ SIM_HDI void dram_cycle(ChanState& ch, const SimCfg& c, const MemCtx& x, uint64_
   // banks that had a queued row hit at the start of the cycle (only FR-FCFS
   // consults them): the column command above removed one row-hit request and
   // changed no bank's open row, so its bank is added back
-  const uint64_t hitmask = c.dram_sched == 0 ? 0ull : (P::vor(kDramQ, [&](int i) -> uint64_t {
+  const uint64_t hitmask = c.dram_sched == 0 ? 0ull : (P::vor(qn, [&](int i) -> uint64_t {
     if (!ch.q_valid[i]) return 0;
     const DramReq& r = ch.q[i];
     if (only != 2 && r.write != only) return 0;  // requests of the idle queue do not hold rows open
     const DramBank& b = ch.bk[r.bank];
     return (b.open && b.row == r.row) ? (1ull << r.bank) : 0ull;
   }) | (col ? 1ull << col_bank : 0ull));
-  int act = P::argmin(kDramQ, [&](int i) -> uint64_t {
+  int act = P::argmin(qn, [&](int i) -> uint64_t {
     if (!ch.q_valid[i]) return ~0ull;
     if (c.dram_sched == 0 && ch.q_age[i] != oldest_age) return ~0ull;
     const DramReq& r = ch.q[i];
