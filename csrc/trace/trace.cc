@@ -1249,6 +1249,28 @@ static uint32_t lanes_degree(const uint64_t* addr, uint64_t lanes, uint64_t wb, 
     }
     if (distinct || same) return 1;
   }
+  if (fits && nb <= 64) {
+    // distinct words per bank, one chain per bank (chains stay as short as
+    // the degree, so no sort of the up to 512 words is needed)
+    int16_t head[64];
+    int16_t next[kMaxWords];
+    for (uint32_t b = 0; b < nb; ++b) head[b] = -1;
+    uint32_t cnt[64] = {};
+    for (uint32_t i = 0; i < nw; ++i) {
+      const uint32_t b = (uint32_t)(words[i] % nb);
+      bool dup = false;
+      for (int16_t j = head[b]; j >= 0; j = next[j])
+        if (words[j] == words[i]) {
+          dup = true;
+          break;
+        }
+      if (dup) continue;
+      next[i] = head[b];
+      head[b] = (int16_t)i;
+      deg = std::max(deg, ++cnt[b]);
+    }
+    return deg;
+  }
   if (fits) {
     std::sort(words, words + nw);
     const uint32_t nu = (uint32_t)(std::unique(words, words + nw) - words);
