@@ -32,10 +32,11 @@ EXTRA_FLAGS: Dict[str, Dict[str, str]] = {
     "IPOLY": {"-gpgpu_memory_partition_indexing": "2"},
     "RR": {"-gpgpu_scheduler": "lrr"},
     "GTO": {"-gpgpu_scheduler": "gto"},
+    # the reference's strings verbatim (define-standard-cfgs.yml:147-151)
     "32B": {"-gpgpu_mem_addr_mapping":
-            "dramid@5;00000000.00000000.00000000.00000000.0000RRRR.RRRRRRRR.RRBBBBCC.CCCSSSSS"},
+            "dramid@5;00000000.00000000.00000000.00000000.0000RRRR.RRRRRRRR.RBBBCCCC.BCCSSSSS"},
     "256B": {"-gpgpu_mem_addr_mapping":
-             "dramid@8;00000000.00000000.00000000.00000000.0000RRRR.RRRRRRRR.RRBBBBCC.CCCSSSSS"},
+             "dramid@8;00000000.00000000.00000000.00000000.0000RRRR.RRRRRRRR.RBBBCCCB.CCCSSSSS"},
     "FRFCFS": {"-gpgpu_dram_scheduler": "1"},
     "FCFS": {"-gpgpu_dram_scheduler": "0"},
 }

@@ -149,6 +149,7 @@ def _sweep(a, suite, engine, rank, world, use_cuda) -> int:
             "ms_per_step": round(dt_max / max(1, a.steps) * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": round(kips / BASELINE_KIPS, 3),
             "vs_baseline_note": "not like-for-like: reference = GPGPU-Sim, 1 CPU core, recorded heartwall traces",
+            "vs_baseline_parts": _baseline_parts(kips, gpu_all / max(dt_max, 1e-9) / 1e3, suite, engine, world),
             "dtype": "n/a (integer cycle-level model)",
             "data": "synthetic (seeded Rodinia-2.0-ft-shaped SASS traces)",
             "config": {"model": f"{a.config} ({_cfg_desc(a.config)}), BASELINE config #5 shape: "
@@ -172,6 +173,17 @@ def _sweep(a, suite, engine, rank, world, use_cuda) -> int:
         import torch.distributed as dist
         dist.destroy_process_group()
     return 0
+
+
+def _baseline_parts(kips, gpu_kips, suite, engine, world):
+    """The headline split into what the MI355X cycle engine simulated and what
+    the host cores did, each against the reference's one-core 349 KIPS."""
+    cores = suite.cpu_slots(reserve=max(1, suite.concurrency())) if engine in ("node", "cpu") else 0
+    host = max(0.0, kips - gpu_kips)
+    per_core = host / max(1, cores * world) if cores else 0.0
+    return {"gpu_engine_kips": round(gpu_kips, 1), "gpu_engine_vs_baseline": round(gpu_kips / BASELINE_KIPS, 3),
+            "host_kips": round(host, 1), "host_cores": cores * world,
+            "host_kips_per_core": round(per_core, 1), "host_per_core_vs_baseline": round(per_core / BASELINE_KIPS, 3)}
 
 
 def main() -> int:
@@ -335,6 +347,9 @@ def main() -> int:
             "vs_baseline_note": "not like-for-like: reference = GPGPU-Sim, 1 CPU core, recorded heartwall "
                                 "traces (349 KIPS); this = MI355X-native simulator, synthetic Rodinia-2.0-ft-"
                                 "shaped traces, engine placement in config.engine",
+            # the ratio above divides a whole node (host cores + MI355X) by one
+            # reference core; its parts, each against the same 349 KIPS:
+            "vs_baseline_parts": _baseline_parts(kips, gpu_all / dt / 1e3, suite, engine, world),
             "dtype": "n/a (integer cycle-level model)",
             "data": "synthetic (seeded Rodinia-2.0-ft-shaped SASS traces; no recorded traces available)",
             "config": {

@@ -176,6 +176,9 @@ PYBIND11_MODULE(_asim, m) {
     m.attr("limits") = lim;
   }
   m.def("gpu_cu_count", &gpu_cu_count, "compute units of the current HIP device");
+  m.def("gpu_pool_stats", &gpu_pool_stats, "GPU engine caching allocator: cached bytes, caps, trims");
+  m.def("gpu_pool_trim", &gpu_pool_trim, "give the GPU engine allocator's cached blocks back to the driver");
+  m.def("gpu_cus_per_sim", &gpu_cus_per_sim, "CUs one GPU-engine simulation of this shape reserves (ASIM_GPU_STATE)");
   m.def("gpu_engine_kernel_info", []() {
     const EngineKernelInfo k = gpu_engine_kernel_info();
     py::dict d;

@@ -84,6 +84,11 @@ void apply_router_params(SimCfg& c, const std::map<std::string, std::string>& kv
   if (buf < 1 || buf > 4096) throw OptionError("interconnect config: vc_buf_size must be 1..4096");
   if (iters < 1 || iters > 16) throw OptionError("interconnect config: alloc_iters must be 1..16");
   if (cd < 0 || cd > 255 || sa < 0 || sa > 255) throw OptionError("interconnect config: credit / allocation delay out of range");
+  // the injection queue's capacity in flits (interconnect_interface.cpp:129-133:
+  // input_buffer_size, 9 when unset)
+  const long ib = geti(kv, "input_buffer_size", 0);
+  if (ib < 0 || ib > 65535) throw OptionError("interconnect config: input_buffer_size out of range");
+  c.rt_inbuf = (uint16_t)(ib ? ib : 9);
   c.rt_vcs = (uint8_t)vcs;
   c.rt_buf = (uint16_t)buf;
   c.rt_iters = (uint8_t)iters;

@@ -1055,6 +1055,13 @@ SimCfg derive_sim_cfg(const OptionRegistry& r) {
     if (lc == 2 && c.rt_alloc == 0xff)
       throw OptionError("-icnt_link_contention 2: the .icnt file's sw_allocator is not modelled "
                         "(islip, separable_input_first, separable_output_first, wavefront, rr_wavefront, max_size, pim, loa)");
+    // configurations whose channel dependences can form a cycle: the pass
+    // would report a routing deadlock (the dateline classes of a torus and
+    // the escape / second-leg classes of min_adapt / valiant need two VCs)
+    if (lc == 2 && c.rt_vcs < 2 && c.topo == TOPO_TORUS)
+      throw OptionError("-icnt_link_contention 2: a torus needs num_vcs >= 2 (dateline classes)");
+    if (lc == 2 && c.rt_vcs < 2 && c.rt_route != 0)
+      throw OptionError("-icnt_link_contention 2: min_adapt / valiant routing needs num_vcs >= 2");
   } else if (r.geti("-network_mode") != 2) {
     throw OptionError("-network_mode must be 1 (intersim topology) or 2 (local crossbar)");
   }

@@ -1393,10 +1393,22 @@ void Simulator::print_kernel_stats(const KernelResult& r, const std::vector<SMSt
     print("Reply_Network_avg_queueing_cycles = %.4f\n", rp_pk ? (double)rp_q / (double)rp_pk : 0.0);
     if (icnt_contention_on(cfg_)) {
       // cumulative over the run: packets a busy link delayed, and the delay
-      uint64_t dl = 0, wc = 0;
-      eng_->link_stats(&dl, &wc);
+      uint64_t dl = 0, wc = 0, dd = 0;
+      eng_->link_stats(&dl, &wc, &dd);
       print("Network_link_delayed_packets = %llu\n", (unsigned long long)dl);
       print("Network_link_wait_cycles = %llu\n", (unsigned long long)wc);
+      if (cfg_.link_contention == 2) {
+        // injection back-pressure (HasBuffer): cycles a ready packet waited
+        // for room in its node's injection queue, SM side and L2 side
+        uint64_t sm_inj = 0, l2_inj = 0;
+        for (auto& st : csm) sm_inj += st.icnt_inj_stall;
+        for (auto& m : cmem) l2_inj += m.icnt_inj_stall;
+        print("Req_Network_injection_stall_cycles = %llu\n", (unsigned long long)sm_inj);
+        print("Reply_Network_injection_stall_cycles = %llu\n", (unsigned long long)l2_inj);
+        print("Network_router_deadlocked_packets = %llu\n", (unsigned long long)dd);
+        if (dd) print("GPGPU-Sim: WARNING: %llu packets met a routing deadlock in the router model; they kept their "
+                      "uncontended latency\n", (unsigned long long)dd);
+      }
     }
   }
   {

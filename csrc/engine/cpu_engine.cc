@@ -164,7 +164,7 @@ class CpuEngine : public Engine {
     if (icnt_contention_on(c)) {
       // the link model's persistent words, then its two statistics words
       n_link_state_ = (size_t)icnt_state_words(c, cap_req_, cap_rep_);
-      link_free_.assign(n_link_state_ + 2, 0);
+      link_free_.assign(n_link_state_ + kIcntStatWords, 0);
       link_refs_.assign((size_t)icnt_scratch_words(c, cap_req_, cap_rep_), 0);
     }
     epoch_ = 0;
@@ -471,9 +471,10 @@ class CpuEngine : public Engine {
     p += mall_.size() * sizeof(L2Line);
     if (n_link_state_) memcpy(link_free_.data(), p, n_link_state_ * 8);
   }
-  void link_stats(uint64_t* delayed, uint64_t* wait_cycles) override {
+  void link_stats(uint64_t* delayed, uint64_t* wait_cycles, uint64_t* deadlocked) override {
     *delayed = n_link_state_ ? link_free_[n_link_state_] : 0;
     *wait_cycles = n_link_state_ ? link_free_[n_link_state_ + 1] : 0;
+    if (deadlocked) *deadlocked = n_link_state_ ? link_free_[n_link_state_ + 2] : 0;
   }
   void advance(uint64_t cycles) override {
     uint64_t E = c_.icnt_latency;
@@ -550,6 +551,7 @@ class CpuEngine : public Engine {
     x.outcnt = cnt_req_[cur].data();
     x.out_cap = cap_req_;
     x.n_src_sm = c_.n_sm;
+    x.rt_st = c_.link_contention == 2 && !link_free_.empty() ? link_free_.data() : nullptr;
     return x;
   }
   MemCtx ctx_mem(uint32_t cur, uint64_t t1) {
@@ -563,6 +565,7 @@ class CpuEngine : public Engine {
     m.ovf = ovf_.data();
     m.ovf_cap = ovf_cap_;
     m.mall = nullptr;
+    m.rt_st = c_.link_contention == 2 && !link_free_.empty() ? link_free_.data() : nullptr;
     return m;
   }
 

@@ -6,6 +6,7 @@
 #include <cstring>
 #include <memory>
 #include <stdexcept>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -93,11 +94,13 @@ class Engine {
   }
   // device kernel launches so far (GPU engine; host engines report 0)
   virtual uint64_t launches() const { return 0; }
-  // -icnt_link_contention: packets delayed by busy links, and their total
-  // delay in interconnect cycles (icnt_links.h)
-  virtual void link_stats(uint64_t* delayed, uint64_t* wait_cycles) {
+  // -icnt_link_contention: packets delayed by busy links, their total delay
+  // in interconnect cycles (icnt_links.h), and packets a routing deadlock of
+  // the router model left at their uncontended latency (icnt_router.h)
+  virtual void link_stats(uint64_t* delayed, uint64_t* wait_cycles, uint64_t* deadlocked = nullptr) {
     *delayed = 0;
     *wait_cycles = 0;
+    if (deadlocked) *deadlocked = 0;
   }
   // in-loop power sampling (PwrArm); engines without it return false
   virtual bool power_sampler() const { return false; }
@@ -149,7 +152,8 @@ inline uint32_t backlog_cap(const SimCfg& c) {
 
 struct EngineStateHeader {
   uint64_t magic = 0x41534d5354415445ull;  // "ASMSTATE"
-  uint64_t version = 6;  // 4: kernel slots (concurrent kernels); 5: MALL lines; 6: link reservations
+  uint64_t version = 7;  // 4: kernel slots (concurrent kernels); 5: MALL lines; 6: link reservations;
+                         // 7: DRAM queue bound (ChanState::q_hi), router deadlock statistics word
   uint64_t n_sm = 0, n_mem = 0, sm_bytes = 0, ch_bytes = 0, pub_bytes = 0;
   uint64_t box_req = 0, cnt_req = 0, box_rep = 0, cnt_rep = 0;  // element counts per parity
   uint64_t ovf = 0;                                              // arrival backlog packets (all sub-partitions)
@@ -192,6 +196,9 @@ bool gpu_engine_available();
 std::unique_ptr<Engine> make_check_engine(std::unique_ptr<Engine> primary, std::unique_ptr<Engine> reference,
                                           uint64_t interval, uint64_t corrupt_at = 0, bool corrupt_mailbox = false);
 int gpu_cu_count();  // compute units of the current HIP device (0 if none)
+int gpu_cus_per_sim(uint32_t n_sm, uint32_t n_mem);  // CUs one GPU-engine simulation of this shape reserves
+std::map<std::string, uint64_t> gpu_pool_stats();  // the GPU engine's caching allocator (empty without HIP)
+void gpu_pool_trim();  // give the allocator's cached blocks back to the driver
 // compiled resources of the persistent engine kernel (empty if no HIP build):
 // registers, scratch, static LDS, plus the dynamic LDS the engine requests
 struct EngineKernelInfo {

@@ -152,8 +152,11 @@ __device__ __forceinline__ void swap_out(T* dst, const T* lds) {
 }
 
 extern __shared__ __attribute__((aligned(16))) char g_lds[];
-constexpr size_t kStateLds = ((sizeof(SMState) > sizeof(ChanState) ? sizeof(SMState) : sizeof(ChanState)) + 15) / 16 * 16;
-constexpr size_t kProfOff = kStateLds + (sizeof(KernelTab) + 15) / 16 * 16;
+// Block LDS layout: the kernel table, the stage profiler and the power
+// evaluator's scratch first (a few KB), then -- in the LDS-state build -- the
+// resident unit's state.  The global-state build (ASIM_GPU_STATE=global)
+// allocates only the first part: its units work on their HBM images, so many
+// engine waves share a CU.
 constexpr int kProfSlots = 48;
 struct ProfLds {
   uint64_t last;
@@ -161,10 +164,24 @@ struct ProfLds {
   uint32_t pad;
   uint64_t acc[kProfSlots];
 };
+constexpr size_t kKtOff = 0;
+constexpr size_t kProfOff = kKtOff + (sizeof(KernelTab) + 15) / 16 * 16;
 // the power evaluator's sums and deltas (one block per sample)
 constexpr size_t kPwrOff = kProfOff + (sizeof(ProfLds) + 15) / 16 * 16;
-constexpr size_t kLdsBytes = kPwrOff + 2 * kPwrSumPad * sizeof(double);
+constexpr size_t kStateOff = (kPwrOff + 2 * kPwrSumPad * sizeof(double) + 15) / 16 * 16;
+constexpr size_t kStateLds = ((sizeof(SMState) > sizeof(ChanState) ? sizeof(SMState) : sizeof(ChanState)) + 15) / 16 * 16;
+constexpr size_t kLdsBytes = kStateOff + kStateLds;
+constexpr size_t kLdsBytesGlobal = kStateOff;
 static_assert(kLdsBytes <= 160 * 1024, "per-block LDS budget exceeded");
+
+// a pointer the compiler may treat as global memory (address space 1): the
+// generic -> global cast lets address-space inference turn the model's flat
+// accesses through it into global_load / global_store
+template <class T>
+__device__ __forceinline__ T* as_global(T* p) {
+  typedef __attribute__((address_space(1))) T gT;
+  return (T*)(gT*)p;
+}
 
 // profiling build of the lane policy: P::prof(k) charges the shader-clock
 // time since the previous stamp to the previous stage and enters stage k
@@ -253,32 +270,39 @@ __device__ void pwr_evaluate(PwrDev& pw, uint32_t nunits, uint64_t now) {
   __syncthreads();
 }
 
-template <class P, bool kSliced>
+template <class P, bool kSliced, bool kGlobal = false>
 __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   const uint32_t b = blockIdx.x;
   // The configuration is read all over the model, much of it at lane-varying
   // indices (address-decoder bit runs, per-unit counts, cache geometries
-  // selected per warp) that cannot be scalar loads: from HBM each is a vector
-  // load that misses the vector L1 after every epoch's acquire fence.  The
-  // block copies the configuration into LDS once and reads it from there
-  // (static global loads in this kernel 1031 -> 58; bfs engine time -3 %,
-  // profiles/pmc_sq_engine_bfs_r2.json).
+  // selected per warp): constant memory, one slot per engine (g_cfg above).
   const SimCfg& c = g_cfg[a.cfg_slot];
   const uint64_t E = c.icnt_latency;
-  SMState* s = reinterpret_cast<SMState*>(g_lds);
-  ChanState* ch = reinterpret_cast<ChanState*>(g_lds);
   // Units (SMs 0..n_sm-1, then channels) map to blocks round-robin: unit
-  // b + k * nblocks.  With no more units than blocks each block owns one
-  // unit whose state stays in LDS for the whole launch; otherwise (configs
-  // larger than the CU count, e.g. the 384-unit MI355X preset) a block
-  // time-slices its units every epoch, swapping states through HBM and
-  // keeping the last one resident into the next epoch.
+  // b + k * nblocks.  LDS-state build: with no more units than blocks each
+  // block owns one unit whose state stays in LDS for the whole launch;
+  // otherwise (configs larger than the CU count, e.g. the 384-unit MI355X
+  // preset) a block time-slices its units every epoch, swapping states
+  // through HBM and keeping the last one resident into the next epoch.
+  // Global-state build (kGlobal): every unit is simulated in place in its HBM
+  // image (vector-L1 / L2 resident while its block works on it), the block
+  // holds no state in LDS and several engine waves share each CU.
+  SMState* s = reinterpret_cast<SMState*>(g_lds + kStateOff);
+  ChanState* ch = reinterpret_cast<ChanState*>(g_lds + kStateOff);
   const uint32_t nunits = c.n_sm + c.n_mem;
   const uint32_t nmine = kSliced ? (nunits - 1 - b) / a.nblocks + 1 : 1;
-  const bool sliced = kSliced && nmine > 1;
-  uint32_t loaded = b;  // unit whose state is in LDS
+  uint32_t loaded = b;  // unit whose state is in LDS (global build: the unit being simulated)
   auto unit_k = [&](uint32_t k) { return b + k * a.nblocks; };
+  auto bind = [&](uint32_t u) {
+    if (u < c.n_sm) s = as_global(&a.sms[u]);
+    else ch = as_global(&a.chs[u - c.n_sm]);
+  };
   auto swap_to = [&](uint32_t u) {
+    if (kGlobal) {
+      bind(u);
+      loaded = u;
+      return;
+    }
     if (!kSliced || u == loaded) return;
     if (loaded < c.n_sm) swap_out(&a.sms[loaded], s);
     else swap_out(&a.chs[loaded - c.n_sm], ch);
@@ -286,12 +310,14 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
     else swap_in(ch, &a.chs[u - c.n_sm]);
     loaded = u;
   };
-  if (b < c.n_sm)
+  if (kGlobal)
+    bind(b);
+  else if (b < c.n_sm)
     copy_state(s, &a.sms[b]);
   else
     copy_state(ch, &a.chs[b - c.n_sm]);
-  // kernel table lives in LDS behind the state (never in scratch)
-  KernelTab* ktl = reinterpret_cast<KernelTab*>(g_lds + kStateLds);
+  // kernel table lives in LDS (never in scratch)
+  KernelTab* ktl = reinterpret_cast<KernelTab*>(g_lds + kKtOff);
   {
     static_assert(sizeof(KernelTab) % 16 == 0, "kernel table must be 16-byte granular");
     const uint4* src = reinterpret_cast<const uint4*>(a.kt);
@@ -311,12 +337,14 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   sx.kt = &kt;
   sx.out_cap = a.cap_req;
   sx.n_src_sm = c.n_sm;
+  sx.rt_st = c.link_contention == 2 ? a.link_free : nullptr;
   MemCtx mx;
   mx.cfg = &c;
   mx.out_cap = a.cap_rep;
   mx.n_src_sub = c.n_subpart;
   mx.ovf = a.ovf;
   mx.ovf_cap = a.ovf_cap;
+  mx.rt_st = c.link_contention == 2 ? a.link_free : nullptr;
   mx.mall = nullptr;
   uint64_t epoch = a.epoch0, cycle = a.cycle0;
   uint64_t t_work0 = a.ework ? __builtin_amdgcn_s_memtime() : 0;
@@ -413,8 +441,8 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
         for (uint32_t k = 0; k < nmine; ++k) {
           const uint32_t u = unit_k(k);
           double* row = a.pw->rows + (size_t)u * kPwrRawPad;
-          if (u < c.n_sm) pwr_row_sm(row, u == loaded ? s->st : a.sms[u].st);
-          else pwr_row_ch(row, u == loaded ? *ch : a.chs[u - c.n_sm], c.n_sub_per_mem);
+          if (u < c.n_sm) pwr_row_sm(row, (!kGlobal && u == loaded) ? s->st : a.sms[u].st);
+          else pwr_row_ch(row, (!kGlobal && u == loaded) ? *ch : a.chs[u - c.n_sm], c.n_sub_per_mem);
         }
         if (!grid_barrier(a.ctl, a.nblocks, nbar++)) { failed = true; break; }
         if (b == a.nblocks - 1) pwr_evaluate(*a.pw, nunits, cycle);
@@ -429,7 +457,9 @@ __global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
   }
   P::prof(31);  // launch_rest
   // write the resident state back
-  if (loaded < c.n_sm)
+  if (kGlobal)
+    ;
+  else if (loaded < c.n_sm)
     copy_state(&a.sms[loaded], s);
   else
     copy_state(&a.chs[loaded - c.n_sm], ch);
@@ -521,6 +551,21 @@ class DeviceCuTable {
   int fd_ = -1;
 };
 
+// Engine blocks per CU are accounted in slots: kCuSlots per CU, a block
+// takes the share of the CU's LDS it allocates (one CU for the LDS-state
+// build, one slot for the global-state build: 8 engine waves per CU, within
+// the VGPR budget of the kernel's 12 waves).
+constexpr uint32_t kCuSlots = 8;
+uint32_t block_slots(size_t lds) {
+  const size_t per = (160 * 1024) / kCuSlots;
+  const uint32_t n = (uint32_t)((lds + per - 1) / per);
+  return n < 1 ? 1u : n > kCuSlots ? kCuSlots : n;
+}
+bool gpu_state_global() {
+  const char* e = getenv("ASIM_GPU_STATE");
+  return e && std::string(e) == "global";
+}
+
 // Process-wide CU reservation.  Every simulation needs ALL its blocks
 // co-resident (grid barrier) and each block takes one CU (LDS-bound), so
 // concurrent simulations in one process (job-level parallelism on one GPU)
@@ -599,70 +644,114 @@ class CfgSlots {
 // Process-wide caching allocator for the engine's device buffers, pinned
 // control words and streams.  hipFree / hipHostFree / hipStreamDestroy
 // synchronise the whole device: with several simulations sharing the GPU
-// (the node bench runs two GPU-engine applications at once, plus every
+// (the node bench runs GPU-engine applications side by side, and every
 // step's simulations are built and torn down again), one simulation's
 // teardown waited for the other's running engine_kernel launch -- a queued
 // application measured 0.084 s alone and 0.14-0.19 s inside the step.
 // Buffers go back to a free list keyed by their exact size and are handed to
 // the next simulation of that shape (the bench repeats the same shapes every
-// step); nothing is returned to the driver before the process exits.
+// step).  The cache is bounded: a block that would take the cached bytes over
+// the cap (ASIM_GPU_POOL_CAP_MB, default 4096 device / 1024 pinned) is freed
+// at once, and an allocation that fails first gives every cached block back
+// to the driver (one device synchronisation) and retries.
 class DevicePool {
  public:
   static DevicePool& get() {
     static DevicePool* p = new DevicePool();  // never destroyed: no frees during static teardown
     return *p;
   }
+  struct Stats {
+    size_t cached_dev = 0, cached_host = 0, cap_dev = 0, cap_host = 0;
+    uint64_t trims = 0, freed_over_cap = 0;
+  };
+  Stats stats() {
+    std::lock_guard<std::mutex> g(mu_);
+    Stats t = st_;
+    t.cap_dev = cap_dev_;
+    t.cap_host = cap_host_;
+    return t;
+  }
   void* dev(size_t n) {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      auto& v = dev_[n];
-      if (!v.empty()) {
-        void* q = v.back();
-        v.pop_back();
-        return q;
-      }
-    }
+    if (void* q = take(dev_, n, st_.cached_dev)) return q;
     void* q = nullptr;
-    HIPCHECK(hipMalloc(&q, n ? n : 16));
+    if (hipMalloc(&q, n ? n : 16) != hipSuccess) {
+      (void)hipGetLastError();
+      trim();
+      HIPCHECK(hipMalloc(&q, n ? n : 16));
+    }
     std::lock_guard<std::mutex> g(mu_);
     size_[q] = n;
     return q;
   }
   void dev_free(void* q) {
     if (!q) return;
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::mutex> g(mu_);
     auto it = size_.find(q);
     if (it == size_.end()) {  // not ours (never happens): give it back
+      g.unlock();
       (void)hipFree(q);
       return;
     }
+    if (st_.cached_dev + it->second > cap_dev_) {  // over the cap: back to the driver
+      size_.erase(it);
+      ++st_.freed_over_cap;
+      g.unlock();
+      (void)hipFree(q);
+      return;
+    }
+    st_.cached_dev += it->second;
     dev_[it->second].push_back(q);
   }
   void* host(size_t n) {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      auto& v = host_[n];
-      if (!v.empty()) {
-        void* q = v.back();
-        v.pop_back();
-        return q;
-      }
-    }
+    if (void* q = take(host_, n, st_.cached_host)) return q;
     void* q = nullptr;
-    HIPCHECK(hipHostMalloc(&q, n ? n : 16));
+    if (hipHostMalloc(&q, n ? n : 16) != hipSuccess) {
+      (void)hipGetLastError();
+      trim();
+      HIPCHECK(hipHostMalloc(&q, n ? n : 16));
+    }
     std::lock_guard<std::mutex> g(mu_);
     hsize_[q] = n;
     return q;
   }
   void host_free(void* q) {
     if (!q) return;
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::mutex> g(mu_);
     auto it = hsize_.find(q);
     if (it == hsize_.end()) {
+      g.unlock();
       (void)hipHostFree(q);
       return;
     }
+    if (st_.cached_host + it->second > cap_host_) {
+      hsize_.erase(it);
+      ++st_.freed_over_cap;
+      g.unlock();
+      (void)hipHostFree(q);
+      return;
+    }
+    st_.cached_host += it->second;
     host_[it->second].push_back(q);
+  }
+  // every cached block back to the driver (the frees synchronise the device)
+  void trim() {
+    std::map<size_t, std::vector<void*>> d, h;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      d.swap(dev_);
+      h.swap(host_);
+      for (auto& kv : d)
+        for (void* q : kv.second) size_.erase(q);
+      for (auto& kv : h)
+        for (void* q : kv.second) hsize_.erase(q);
+      st_.cached_dev = st_.cached_host = 0;
+      ++st_.trims;
+    }
+    (void)hipDeviceSynchronize();
+    for (auto& kv : d)
+      for (void* q : kv.second) (void)hipFree(q);
+    for (auto& kv : h)
+      for (void* q : kv.second) (void)hipHostFree(q);
   }
   hipStream_t stream() {
     {
@@ -684,10 +773,27 @@ class DevicePool {
   }
 
  private:
+  DevicePool() {
+    size_t mb = 4096;
+    if (const char* e = getenv("ASIM_GPU_POOL_CAP_MB")) mb = (size_t)strtoull(e, nullptr, 10);
+    cap_dev_ = mb << 20;
+    cap_host_ = std::min<size_t>(cap_dev_, (size_t)1024 << 20);
+  }
+  void* take(std::map<size_t, std::vector<void*>>& m, size_t n, size_t& cached) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = m.find(n);
+    if (it == m.end() || it->second.empty()) return nullptr;
+    void* q = it->second.back();
+    it->second.pop_back();
+    cached -= n;
+    return q;
+  }
   std::mutex mu_;
   std::map<size_t, std::vector<void*>> dev_, host_;
   std::map<void*, size_t> size_, hsize_;
   std::vector<hipStream_t> streams_;
+  size_t cap_dev_ = 0, cap_host_ = 0;
+  Stats st_;
 };
 template <class T>
 void pool_alloc(T** p, size_t n) {
@@ -715,19 +821,23 @@ class GpuEngine : public Engine {
     hipDeviceProp_t prop;
     HIPCHECK(hipGetDeviceProperties(&prop, dev));
     n_cu_ = prop.multiProcessorCount;
-    CuPool::get().init(n_cu_);
+    CuPool::get().init(n_cu_ * kCuSlots);
     // one block per unit while the units fit the CUs; larger configs (or a
     // smaller ASIM_GPU_BLOCKS cap) time-slice several units per block
     nblocks_ = c.n_sm + c.n_mem;
-    uint32_t cap = (uint32_t)n_cu_;
+    uint32_t cap = (uint32_t)n_cu_ * (gpu_state_global() ? kCuSlots : 1u);
     if (const char* eb = getenv("ASIM_GPU_BLOCKS"))
       if (atoi(eb) > 0) cap = std::min<uint32_t>(cap, (uint32_t)atoi(eb));
     if (nblocks_ > cap) nblocks_ = cap;
-    lds_ = kLdsBytes;
+    global_ = gpu_state_global();
+    lds_ = global_ ? kLdsBytesGlobal : kLdsBytes;
     sliced_ = nblocks_ < c.n_sm + c.n_mem;
     for (const void* f : {(const void*)engine_kernel<WavePar, false>, (const void*)engine_kernel<WaveParProf, false>,
                           (const void*)engine_kernel<WavePar, true>, (const void*)engine_kernel<WaveParProf, true>})
-      HIPCHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_));
+      HIPCHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes));
+    // every block of a simulation must be co-resident: a block takes the CU
+    // slots (kCuSlots per CU) its LDS needs, one at least
+    slots_ = block_slots(lds_);
     if (cfg_slot_ < 0) cfg_slot_ = CfgSlots::get().acquire();
     const char* pe = getenv("ASIM_GPU_PROFILE");
     profiling_ = pe && *pe && *pe != '0';
@@ -785,8 +895,8 @@ class GpuEngine : public Engine {
       throw std::runtime_error("-icnt_link_contention: topology or mailboxes too large for the link pass");
     n_links_ = icnt_contention_on(c) ? (size_t)icnt_state_words(c, cap_req_, cap_rep_) : 0;
     if (n_links_) {
-      pool_alloc(&d_links_, sizeof(uint64_t) * (n_links_ + 2));
-      HIPCHECK(hipMemset(d_links_, 0, sizeof(uint64_t) * (n_links_ + 2)));
+      pool_alloc(&d_links_, sizeof(uint64_t) * (n_links_ + kIcntStatWords));
+      HIPCHECK(hipMemset(d_links_, 0, sizeof(uint64_t) * (n_links_ + kIcntStatWords)));
       pool_alloc(&d_link_refs_, sizeof(uint32_t) * (size_t)icnt_scratch_words(c, cap_req_, cap_rep_));
     }
     pool_alloc(&d_ctl_, sizeof(GpuCtl));
@@ -849,9 +959,13 @@ class GpuEngine : public Engine {
       a.prof = d_prof_;
       a.ework = d_ework_;
       a.pw = pw_on_ ? d_pw_ : nullptr;
-      CuPool::get().acquire((int)nblocks_);
+      CuPool::get().acquire((int)(nblocks_ * slots_));
       hipError_t le;
-      if (profiling_ && sliced_)
+      if (global_ && profiling_)
+        hipLaunchKernelGGL((engine_kernel<WaveParProf, true, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      else if (global_)
+        hipLaunchKernelGGL((engine_kernel<WavePar, true, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      else if (profiling_ && sliced_)
         hipLaunchKernelGGL((engine_kernel<WaveParProf, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else if (profiling_)
         hipLaunchKernelGGL((engine_kernel<WaveParProf, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
@@ -863,7 +977,7 @@ class GpuEngine : public Engine {
       ++launches_;
       hipError_t ce = hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_);
       hipError_t se = hipStreamSynchronize(stream_);
-      CuPool::get().release((int)nblocks_);
+      CuPool::get().release((int)(nblocks_ * slots_));
       HIPCHECK(le);
       HIPCHECK(ce);
       HIPCHECK(se);
@@ -953,11 +1067,12 @@ class GpuEngine : public Engine {
     if (n_links_)
       HIPCHECK(hipMemcpy(d_links_, in.data() + units + sizeof(L2Line) * n_mall_, 8 * n_links_, hipMemcpyHostToDevice));
   }
-  void link_stats(uint64_t* delayed, uint64_t* wait_cycles) override {
-    uint64_t st[2] = {0, 0};
+  void link_stats(uint64_t* delayed, uint64_t* wait_cycles, uint64_t* deadlocked) override {
+    uint64_t st[kIcntStatWords] = {};
     if (n_links_) HIPCHECK(hipMemcpy(st, d_links_ + n_links_, sizeof(st), hipMemcpyDeviceToHost));
     *delayed = st[0];
     *wait_cycles = st[1];
+    if (deadlocked) *deadlocked = st[2];
   }
   void advance(uint64_t cycles) override {
     uint64_t E = c_.icnt_latency;
@@ -997,7 +1112,7 @@ class GpuEngine : public Engine {
     h.cnt_rep = (uint64_t)c_.n_sm * c_.n_subpart;
     h.ovf = (uint64_t)c_.n_subpart * ovf_cap_;
     h.mall = n_mall_;
-    h.links = n_links_ ? n_links_ + 2 : 0;
+    h.links = n_links_ ? n_links_ + kIcntStatWords : 0;
     h.cycle = cycle_;
     h.epoch = epoch_;
     h.ready = kt_.active;
@@ -1223,6 +1338,8 @@ class GpuEngine : public Engine {
   uint32_t epochs_per_launch_ = 4096;
   bool profiling_ = false;
   bool sliced_ = false;  // more units than blocks: the time-slicing kernel
+  bool global_ = false;  // ASIM_GPU_STATE=global: unit states stay in HBM (no LDS state)
+  uint32_t slots_ = kCuSlots;  // CU slots one block of this engine takes
   uint64_t* d_prof_ = nullptr;
   uint32_t* d_ework_ = nullptr;
 
@@ -1328,6 +1445,23 @@ std::unique_ptr<Engine> make_gpu_engine() {
 }  // namespace asim
 
 namespace asim {
+// the engine's caching allocator: cached bytes, caps, trims (tests)
+std::map<std::string, uint64_t> gpu_pool_stats() {
+  const DevicePool::Stats t = DevicePool::get().stats();
+  return {{"cached_dev", t.cached_dev}, {"cached_host", t.cached_host}, {"cap_dev", t.cap_dev},
+          {"cap_host", t.cap_host}, {"trims", t.trims}, {"freed_over_cap", t.freed_over_cap}};
+}
+void gpu_pool_trim() { DevicePool::get().trim(); }
+// CUs one simulation of this shape reserves on the GPU engine (the
+// concurrency of job-level parallelism on one GPU, multi_gpu.py)
+int gpu_cus_per_sim(uint32_t n_sm, uint32_t n_mem) {
+  const bool g = gpu_state_global();
+  uint32_t nb = n_sm + n_mem;
+  const int cus = gpu_cu_count();
+  if (cus > 0) nb = std::min<uint32_t>(nb, (uint32_t)cus * (g ? kCuSlots : 1u));
+  const uint32_t slots = nb * block_slots(g ? kLdsBytesGlobal : kLdsBytes);
+  return (int)((slots + kCuSlots - 1) / kCuSlots);
+}
 int gpu_cu_count() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;

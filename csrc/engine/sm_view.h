@@ -189,6 +189,9 @@ struct SmView {
   SV_VAL(last_progress);
   SV_VAL(epoch_end);
   SV_VAL(out_port_free);
+  SV_REF(inj_t0_fs);
+  SV_REF(inj_allow0);
+  SV_REF(inj_used);
   SV_VAL(age_ctr);
   SV_REF(arb_next);
   SV_REF(arb_cnt);
@@ -335,7 +338,8 @@ struct SmView {
   X(cta_nexit) X(sched_last) X(w_iline)
 
   __device__ __forceinline__ explicit SmView(B& b)
-      : base(b), l1_sets(b.l1_sets), l1_assoc(b.l1_assoc), cycle(b.cycle), arb_next(b.arb_next),
+      : base(b), l1_sets(b.l1_sets), l1_assoc(b.l1_assoc), cycle(b.cycle), inj_t0_fs(b.inj_t0_fs),
+        inj_allow0(b.inj_allow0), inj_used(b.inj_used), arb_next(b.arb_next),
         arb_cnt(b.arb_cnt), w_wait(b.w_wait), w_slot_lds(b.w_slot_lds), w_lds_st(b.w_lds_st), w_issue_ok(b.w_issue_ok), w_win(b.w_win),
         w_slot_pend(b.w_slot_pend),
         w_slot_dst(b.w_slot_dst), cta_id(b.cta_id), cta_ks(b.cta_ks), cta_wbase(b.cta_wbase), cta_nw(b.cta_nw),

@@ -95,8 +95,15 @@ struct WavePar {
     typedef __attribute__((address_space(3))) uint4 l4;
     const int chunks = n * (int)(sizeof(T) / 16);
     const int l = lane();
-    if (l < chunks)
-      __builtin_amdgcn_global_load_lds((g4*)(reinterpret_cast<const uint4*>(src) + l), (l4*)dst, 16, 0, 0);
+    if (l >= chunks) return;
+    // a unit simulated in place in HBM (the global-state engine build): a
+    // plain vector copy (fetch_wait's vmcnt wait covers its stores too)
+    typedef __attribute__((address_space(0))) const void flat_cv;
+    if (!__builtin_amdgcn_is_shared((flat_cv*)dst)) {
+      reinterpret_cast<uint4*>(dst)[l] = reinterpret_cast<const uint4*>(src)[l];
+      return;
+    }
+    __builtin_amdgcn_global_load_lds((g4*)(reinterpret_cast<const uint4*>(src) + l), (l4*)dst, 16, 0, 0);
   }
   static __device__ __forceinline__ void fetch_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
   static __device__ __forceinline__ void prof(int) {}

@@ -288,6 +288,7 @@ struct SimCfg {
   uint8_t rt_route;        // routing_function: 0 deterministic (the topology's), 1 minimal adaptive (min_adapt), 2 Valiant
   uint16_t rt_buf;         // flits per virtual channel
   uint16_t rt_speedup_q8;  // switch passes per cycle x 256
+  uint16_t rt_inbuf;       // input_buffer_size: flits a node's injection queue holds (HasBuffer)
   // ---- memory partition ----
   CacheGeom l2;
   uint32_t rop_latency;

@@ -255,6 +255,13 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t 
                       uint32_t n_sub, uint64_t epoch_idx, const uint64_t* rep_dst = nullptr) {
   const SimCfg& c = *x.cfg;
   sm_kernels_init<P>(s, x);
+  if (c.link_contention == 2 && x.rt_st) {
+    // the injection queue the previous epoch's router pass left (HasBuffer)
+    const uint32_t cpc = c.cores_per_cluster ? c.cores_per_cluster : 1;
+    s.inj_t0_fs = core_fs(c, t0);
+    s.inj_allow0 = rt_inj_allow0(c, x.rt_st, 0, s.id / cpc, fdiv(s.inj_t0_fs, c.dv_icnt));
+    s.inj_used = 0;
+  }
   // 0. cycles [s.cycle, t0) were fast-forwarded by epoch_decide (nothing could
   //    happen in them): account them exactly like quiet cycles
   if (t0 > s.cycle && (s.n_cta_active || !sm_idle(s))) sm_skip<P>(s, c, t0 - s.cycle, s.cycle);
@@ -393,6 +400,14 @@ SIM_HDI void chan_epoch(ChanState& ch, const MemCtx& x, const Pkt* inbox, const 
                         uint32_t in_cap, uint64_t t0_fs, const uint64_t* req_dst = nullptr) {
   P::prof(20);
   ch.min_emit = ~0ull;
+  if (x.cfg->link_contention == 2 && x.rt_st) {
+    const SimCfg& c = *x.cfg;
+    ch.inj_t0_fs = t0_fs;
+    for (uint32_t j = 0; j < c.n_sub_per_mem; ++j) {
+      ch.sp[j].inj_allow0 = rt_inj_allow0(c, x.rt_st, 1, c.n_clusters + ch.id * c.n_sub_per_mem + j, fdiv(t0_fs, c.dv_icnt));
+      ch.sp[j].inj_used = 0;
+    }
+  }
   mem_gather<P>(ch, *x.cfg, x, inbox, incnt, in_cap, t0_fs, req_dst);
   P::one([&] {
     for (uint32_t j = 0; j < x.cfg->n_sub_per_mem; ++j) ch.sp[j].st.icnt_backlog += ch.sp[j].ovf_n;

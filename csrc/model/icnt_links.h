@@ -32,6 +32,12 @@
 
 namespace asim {
 
+// statistics words behind a link model's persistent state: packets delayed,
+// their delay (interconnect cycles), and (router model) packets lost to a
+// routing deadlock, which then kept their uncontended latency
+constexpr int kIcntStatWords = 3;
+
+
 constexpr int kMaxPathLinks = 256;
 constexpr uint64_t kMaxIcntLinks = 1ull << 22;
 

@@ -809,6 +809,28 @@ SIM_HDN uint32_t rt_simulate(const SimCfg& c, const RtDims& d, uint64_t* st, con
   return remaining;
 }
 
+// ---- injection back-pressure (-icnt_link_contention 2) ----
+// The reference refuses a packet whose flits do not fit the node's injection
+// queue (InterconnectInterface::HasBuffer, interconnect_interface.cpp:260-272:
+// queued flits + the packet's <= input_buffer_size) and the SM's LD/ST unit
+// or the L2's reply queue stalls (shader.cc:4554, gpu-sim.cc:1887).  Here the
+// network is simulated after each epoch, so an injector sees the queue the
+// previous pass left: the source's injection channel takes one flit per
+// cycle, so inj_next[node] - t0 flits of earlier traffic are still queued at
+// the epoch start t0 (icnt cycles), draining one per cycle.  A packet of
+// `nfl` flits may enter at icnt cycle t0 + k while
+//   injected_this_epoch + nfl <= rt_inj_allow0 + k,
+// rt_inj_allow0 = input_buffer_size - backlog (negative: the queue overflowed).
+// Nodes that several SMs share (a cluster) split it: each SM counts its
+// flits times the cluster's SMs.
+SIM_HDI int64_t rt_inj_allow0(const SimCfg& c, const uint64_t* st, uint32_t subnet, uint32_t node, uint64_t t0_icnt) {
+  const RtDims d = rt_dims(c, 0, 0);
+  const uint64_t* inj_next = st + (uint64_t)subnet * rt_state_words(d) + 2ull * d.L + 2ull * d.U;
+  const uint64_t q = inj_next[node];
+  const uint64_t backlog = q > t0_icnt ? q - t0_icnt : 0;
+  return (int64_t)c.rt_inbuf - (int64_t)(backlog < (1ull << 40) ? backlog : (1ull << 40));
+}
+
 // Scratch words of the epoch pass: both subnets run one after the other
 // over the same scratch; a subnet's packets are at most its mailbox cells x
 // capacity (icnt_contend's bound).
@@ -862,7 +884,7 @@ SIM_HDN void rt_epoch_run(const SimCfg& c, Pkt* box_req, const uint32_t* cnt_req
       }
     }
     if (!np) continue;
-    rt_simulate(c, d, st + (uint64_t)dir * rt_state_words(d), w, np);
+    const uint32_t lost = rt_simulate(c, d, st + (uint64_t)dir * rt_state_words(d), w, np);
     uint64_t delayed = 0, wait = 0;
     for (uint32_t i = 0; i < np; ++i) {
       const uint64_t base = w.tinj[i] + rt_uncontended(c, icnt_routers(c, w.src[i], w.dst[i]), w.nfl[i]);
@@ -875,6 +897,7 @@ SIM_HDN void rt_epoch_run(const SimCfg& c, Pkt* box_req, const uint32_t* cnt_req
     }
     stat[0] += delayed;
     stat[1] += wait;
+    stat[2] += lost;  // routing deadlock: those packets kept their uncontended latency
   }
 }
 
@@ -897,7 +920,8 @@ SIM_HDI uint64_t icnt_scratch_words(const SimCfg& c, uint32_t cap_req, uint32_t 
   return (uint64_t)c.n_sm * c.n_subpart * (cap_req > cap_rep ? cap_req : cap_rep);
 }
 
-// `st`: icnt_state_words then {delayed packets, delay in interconnect cycles}
+// `st`: icnt_state_words then kIcntStatWords statistics words {delayed
+// packets, delay in interconnect cycles, packets of a routing deadlock}
 template <class P>
 SIM_HDI void icnt_epoch_pass(const SimCfg& c, Pkt* box_req, const uint32_t* cnt_req, uint32_t cap_req, Pkt* box_rep,
                              const uint32_t* cnt_rep, uint32_t cap_rep, uint64_t* st, uint32_t* scratch) {

@@ -100,6 +100,7 @@ struct MemStats {
   // write-back is one request, of 32-128 B): rocprofv3 TCC_EA0_RDREQ / WRREQ
   uint64_t l2_mem_rd_req, l2_mem_wr_req;
   uint64_t mall_rd_hit, mall_rd_miss, mall_wr, mall_wb;
+  uint64_t icnt_inj_stall;  // icnt cycles a ready reply waited for room in the router's injection queue
 };
 
 struct SubPart {
@@ -117,6 +118,8 @@ struct SubPart {
   uint32_t n_l2dram;   // requests of this sub in the L2->DRAM path
   uint32_t ovf_head, ovf_n;  // arrival backlog ring (MemCtx::ovf) for arrivals that did not fit in inq
   uint16_t arb_next, arb_cnt;  // crossbar output-port arbiter: next input, grants left at the pointer
+  int64_t inj_allow0;  // -icnt_link_contention 2: reply flits the node's injection queue takes at the epoch start
+  uint64_t inj_used;   // ... and the reply flits injected since
   L2Mshr mshr[kMaxL2Mshr];
   L2Wait wait[kMaxL2Wait];
   MemStats st;
@@ -130,6 +133,7 @@ struct alignas(16) ChanState {
   uint64_t t_dram;
   uint64_t dcycle;    // dram cycle counter
   uint64_t min_emit;  // earliest arrival time (fs) of the replies injected this epoch
+  uint64_t inj_t0_fs; // start of the epoch (fs): the reply injection back-pressure's reference
   // DRAM
   DramReq lat[kDramLat];  // L2 -> DRAM latency pipe (FIFO)
   uint32_t lat_head, lat_n;
@@ -179,6 +183,7 @@ struct MemCtx {
   Pkt* ovf;             // per-sub-partition arrival backlog rings [n_subpart][ovf_cap] (global memory)
   uint32_t ovf_cap;
   L2Line* mall;         // this channel's MALL lines [mall_sets][mall_assoc] (global memory), nullptr = no MALL
+  const uint64_t* rt_st = nullptr;  // -icnt_link_contention 2: the router model's state (injection back-pressure)
 };
 
 // ---------------------------------------------------------------------------
@@ -645,6 +650,11 @@ SIM_HDI void mem_icnt_cycle(ChanState& ch, SubPart& sp, const SimCfg& c, const M
   if (sp.rep_n && sp.port_free <= now_fs) {
     Pkt r = sp.reply[sp.rep_head];
     uint32_t nflits = (r.size + c.flit_size - 1) / c.flit_size;
+    if (c.link_contention == 2 && !rt_inj_ok(c, ch.inj_t0_fs, sp.inj_allow0, sp.inj_used, nflits, now_fs)) {
+      sp.st.icnt_inj_stall++;  // the node's injection queue is full
+      return;
+    }
+    if (c.link_contention == 2) sp.inj_used += nflits;
     uint64_t done = now_fs + (uint64_t)(nflits - 1) * c.per_icnt;
     {  // serialisation may run past the window end (see sm_inject)
       uint32_t gsub = ch.id * c.n_sub_per_mem + sub;

@@ -152,6 +152,9 @@ struct SMStats {
   // vector-L1 tag lookups at 64 B granularity (the 64 B halves of each
   // coalesced 128 B line access): what TCP_TOTAL_CACHE_ACCESSES counts
   uint64_t l1_lookups64;
+  // cycles a ready packet waited for room in the router's injection queue
+  // (-icnt_link_contention 2 back-pressure)
+  uint64_t icnt_inj_stall;
 };
 enum IL1Out : uint8_t { IL1_HIT = 0, IL1_MISS, IL1_MSHR_HIT, IL1_RES_FAIL };
 // Instruction classes of the CDNA sequencer's counters (rocprofv3
@@ -193,6 +196,12 @@ struct alignas(16) SMState {
   uint64_t last_progress;     // last cycle an instruction completed (deadlock)
   uint64_t epoch_end;         // current epoch end cycle (exclusive)
   uint64_t out_port_free;     // cycle the injection port frees
+  // -icnt_link_contention 2 injection back-pressure (icnt_router.h
+  // rt_inj_allow0): the epoch's start (fs), its flit allowance at that start
+  // and the flits injected since (times the SMs sharing the node)
+  uint64_t inj_t0_fs;
+  int64_t inj_allow0;
+  uint64_t inj_used;
   uint32_t age_ctr;
   uint16_t arb_next, arb_cnt;  // reply-network output-port arbiter (xbar_pick)
   // ---- warps (SoA) ----
@@ -326,6 +335,7 @@ struct SmCtx {
   uint32_t* outcnt;      // [dst][src]
   uint32_t out_cap;      // per (dst,src) capacity (>= epoch length)
   uint32_t n_src_sm;     // number of SMs (row stride)
+  const uint64_t* rt_st = nullptr;  // -icnt_link_contention 2: the router model's state (injection back-pressure)
 };
 
 SIM_HDI uint32_t wb_width(const SimCfg& c) { return c.ex_wb_width < (uint32_t)kWbSlot ? c.ex_wb_width : (uint32_t)kWbSlot; }
@@ -423,6 +433,13 @@ SIM_HDI uint32_t sm_send_write(S& s, const SimCfg& c, uint64_t line, uint8_t sec
   return 2;
 }
 
+// HasBuffer of the router model (icnt_router.h rt_inj_allow0): `nfl` more
+// flits fit the node's injection queue at core cycle `now` of the epoch
+SIM_HDI bool rt_inj_ok(const SimCfg& c, uint64_t t0_fs, int64_t allow0, uint64_t used, uint32_t nfl, uint64_t now_fs) {
+  const uint64_t k = now_fs > t0_fs ? fdiv(now_fs - t0_fs, c.dv_icnt) : 0;
+  return (int64_t)(used + nfl) <= allow0 + (int64_t)(k < (1ull << 40) ? k : (1ull << 40));
+}
+
 // move the head packet into the outbox once the injection port is free.  A
 // multi-flit packet may finish serialising after the epoch ends (port_free
 // carries over); its arrival time is still beyond the lookahead, so the
@@ -440,6 +457,13 @@ SIM_HDI void sm_inject(S& s, const SmCtx& x, uint64_t now) {
   uint32_t slot = dst * x.n_src_sm + s.id;
   uint32_t n = P::uni(s.ocnt[dst]);
   if (n >= x.out_cap) return;  // outbox cell full (cannot happen with cap >= epoch)
+  const uint32_t cpc = c.cores_per_cluster ? c.cores_per_cluster : 1;
+  if (c.link_contention == 2 &&
+      !rt_inj_ok(c, P::uni(s.inj_t0_fs), P::uni(s.inj_allow0), P::uni(s.inj_used), nflits * cpc, core_fs(c, now))) {
+    s.sadd(SK(icnt_inj_stall), 1);  // the node's injection queue is full
+    return;
+  }
+  if (c.link_contention == 2) s.inj_used = s.inj_used + (uint64_t)nflits * cpc;
   s.ocnt[dst] = n + 1;
   p.t = core_fs(c, done) + icnt_pkt_lat_fs(c, s.id, dst);
   s.min_emit = amin(s.min_emit, p.t);
@@ -1544,9 +1568,7 @@ SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uin
   const SimCfg& c = *x.cfg;
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
-  uint64_t valid_m = 0, sbok_m = 0;
-  bool classified = false;
-  uint32_t n_idle = 0, n_c0 = 0, n_c1 = 0, n_c2 = 0;
+  uint32_t n_idle = 0, idle_sc = 0, first_idle = nsched;
   uint64_t picks = 0;
   uint32_t pk_of = 0xffffffffu;  // byte sc: the warp scheduler sc picked (0xff: none)
   for (uint32_t sc = 0; sc < nsched; ++sc) {
@@ -1555,14 +1577,8 @@ SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uin
     if (!cand) {
       if (live & mine) {
         ++n_idle;
-        if (!classified) {
-          classified = true;
-          sm_stall_masks<P>(s, c, now, live, valid_m, sbok_m);
-        }
-        const uint32_t k = stall_class(mine, valid_m, sbok_m);
-        n_c0 += k == 0;
-        n_c1 += k == 1;
-        n_c2 += k == 2;
+        idle_sc |= 1u << sc;
+        if (first_idle == nsched) first_idle = sc;
       }
       continue;
     }
@@ -1573,13 +1589,34 @@ SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uin
     pk_of = (pk_of & ~(0xffu << (8 * sc))) | w << (8 * sc);
     picks |= 1ull << w;
   }
-  if (n_idle) {
+  // Stall classes of the idle schedulers.  The sequential loop classifies at
+  // its first idle scheduler, after the schedulers before it have issued --
+  // their EXIT / barrier / fence instructions (step 3) can change the flags of
+  // other schedulers' warps -- and before the ones after it: the same point
+  // here, inside step 3's scheduler-order walk.  (The pipeline issues of
+  // steps 1-2 touch only the issuing scheduler's own warps.)
+  bool classified = n_idle == 0;
+  auto classify = [&]() {
+    classified = true;
+    uint64_t valid_m = 0, sbok_m = 0;
+    sm_stall_masks<P>(s, c, now, live, valid_m, sbok_m);
+    uint32_t n_c0 = 0, n_c1 = 0, n_c2 = 0;
+    for (uint32_t sc = 0; sc < nsched; ++sc) {
+      if (!(idle_sc >> sc & 1u)) continue;
+      const uint32_t k = stall_class(c.sched_mask[sc], valid_m, sbok_m);
+      n_c0 += k == 0;
+      n_c1 += k == 1;
+      n_c2 += k == 2;
+    }
     s.sadd(SK(issue_stall_idle), n_idle);
     if (n_c0) s.sadd(SK(issue_distro) + 0, n_c0);
     if (n_c1) s.sadd(SK(issue_distro) + 1, n_c1);
     if (n_c2) s.sadd(SK(issue_distro) + 2, n_c2);
+  };
+  if (!picks) {
+    if (!classified) classify();
+    return;
   }
-  if (!picks) return;
   s.last_progress = now;
   s.sadd(SK(busy_cycles), 1);
   const uint64_t spec = P::ballot_m(picks, [&](int w) -> bool { return issue_special(head.self(w)); });
@@ -1648,14 +1685,17 @@ SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uin
     sbs(s.w_sb, (uint32_t)w, in.dst[1]);
   });
   P::sync();
-  // 3. the instructions handled at issue, in scheduler order
+  // 3. the instructions handled at issue, in scheduler order (the idle
+  //    schedulers classified at the first of them)
   if (spec) {
     for (uint32_t sc = 0; sc < nsched; ++sc) {
       const uint32_t w = (pk_of >> (8 * sc)) & 0xffu;
       if (w == 0xffu || !(spec >> w & 1ull)) continue;
+      if (!classified && sc > first_idle) classify();
       sm_issue_one<P>(s, x, now, sc, w, head.at((int)w), P::uni((uint32_t)s.w_head[w]));
     }
   }
+  if (!classified) classify();
 }
 
 template <class P, class S>

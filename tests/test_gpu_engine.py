@@ -359,3 +359,45 @@ def test_power_in_kernel_gpu_equals_cpu(gpu_mod, tmp_path):
     assert out["gpu"][3] == out["cpu"][3] >= 10
     # one launch per kernel run either way: sampling does not relaunch
     assert out["gpu"][2] == out["gpu_nopower"][2] > 0
+
+
+@pytest.mark.parametrize("app", ["bfs", "hotspot"])
+def test_global_state_gpu_equals_cpu(gpu_mod, tmp_path, monkeypatch, app):
+    """ASIM_GPU_STATE=global: units simulated in place in their HBM images
+    (no LDS state, many engine waves per CU) give the CPU engine's full state
+    image and statistics, also with fewer blocks than units."""
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    monkeypatch.setenv("ASIM_GPU_STATE", "global")
+    gen = {"bfs": lambda: rodinia.bfs(2048, levels=4), "hotspot": lambda: rodinia.hotspot(64, 2, 2)}[app]
+    kl = rodinia.write_app(str(tmp_path / app), gen())
+    for blocks in ("0", "37"):
+        monkeypatch.setenv("ASIM_GPU_BLOCKS", blocks)
+        sg = sim.Simulator("QV100", kl, engine="gpu", torch_runtime=True)
+        sc = sim.Simulator("QV100", kl, engine="cpu")
+        g, c = sg.run(), sc.run()
+        assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
+        assert sg.native.snapshot() == sc.native.snapshot()
+    assert gpu_mod.gpu_cus_per_sim(80, 32) == 14
+
+
+def test_device_pool_stays_bounded(gpu_mod, tmp_path):
+    """The engine's caching allocator keeps freed buffers for the next
+    simulation of the same shape but never caches more than its cap: many
+    simulations of different shapes in one process leave the cached bytes
+    at or under the cap, and a trim gives everything back."""
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    kl = rodinia.write_app(str(tmp_path / "vadd"), [rodinia.vectoradd(20000)])
+    for n in (8, 16, 24, 32, 40, 48, 56, 64):
+        sim.simulate(kl, "QV100", engine="gpu", extra={"-gpgpu_n_clusters": str(n)})
+        st = gpu_mod.gpu_pool_stats()
+        assert st["cached_dev"] <= st["cap_dev"] and st["cached_host"] <= st["cap_host"]
+    assert gpu_mod.gpu_pool_stats()["cached_dev"] > 0
+    gpu_mod.gpu_pool_trim()
+    st = gpu_mod.gpu_pool_stats()
+    assert st["cached_dev"] == 0 and st["cached_host"] == 0 and st["trims"] >= 1
+    # the engine still works after a trim
+    g = sim.simulate(kl, "QV100", engine="gpu")
+    c = sim.simulate(kl, "QV100", engine="cpu")
+    assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)

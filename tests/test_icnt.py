@@ -538,3 +538,67 @@ def test_router_valiant_routing(native):
     lo = native.icnt_open_loop(val, "uniform", 0.05, 1, 2000, 500, 1)
     assert lo["avg_latency"] > 1.5 * lo["zero_load_latency"]
     assert lo == native.icnt_open_loop(val, "uniform", 0.05, 1, 2000, 500, 1)
+
+
+def _store_app(tmp_path, name, stores):
+    """80 single-warp CTAs, each storing `stores` full lines (5-flit write
+    packets) to the same L2 sub-partition: offered load grows with `stores`."""
+    from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+    import numpy as np
+    k = KernelBuilder("_Z6storesPf", (80, 1, 1), (32, 1, 1), nregs=32)
+    for i in range(stores):
+        base = 0x7000_0000 + np.arange(k.g.nwarps, dtype=np.int64) * 0x100000 + i * 0x40000
+        k.op("STG.E", [], [2, 3], base=base, stride=4)
+    k.op("EXIT")
+    return rodinia.write_app(str(tmp_path / name), [k.build()], memcpy=False)
+
+
+def test_router_back_pressure_throttles_injection(native, tmp_path):
+    """-icnt_link_contention 2: a node's injection queue holds
+    input_buffer_size flits (InterconnectInterface::HasBuffer); a full queue
+    stalls the SM's injection, so its stall cycles rise with the offered load,
+    and a roomier queue stalls less.  Deterministic with CPU threads."""
+    def run(stores, inbuf, threads=1):
+        icnt = _icnt_args(tmp_path, f"bp{inbuf}", k=8, n=2, topology="mesh", input_buffer_size=inbuf,
+                          vc_buf_size=4, internal_speedup="1.0")
+        s = native.Simulator(icnt + ["-icnt_link_contention", "2", "-gpgpu_perf_sim_memcpy", "0",
+                                     "-sim_cpu_threads", str(threads), "-trace",
+                                     _store_app(tmp_path, f"st{stores}", stores)], False)
+        assert s.run() == 0 and not s.deadlock
+        return (_link_stat(s.output, "Req_Network_injection_stall_cycles"),
+                _link_stat(s.output, "Req_Network_injected_packets_num"), s.tot_cycle,
+                _link_stat(s.output, "Network_router_deadlocked_packets"))
+    light, heavy = run(4, 9), run(32, 9)
+    assert heavy[0] > 0 and heavy[3] == 0
+    assert heavy[0] / heavy[1] > light[0] / max(1, light[1])  # stall per packet rises with load
+    roomy = run(32, 4096)
+    assert roomy[0] < heavy[0] and roomy[1] == heavy[1]
+    assert run(32, 9, threads=4) == heavy
+
+
+def test_router_model_refuses_deadlock_prone_configs(native, tmp_path):
+    for name, kw in (("torus1", dict(k=8, n=2, topology="torus")),
+                     ("adapt1", dict(k=8, n=2, topology="mesh", routing_function="min_adapt")),
+                     ("valiant1", dict(k=8, n=2, topology="mesh", routing_function="valiant"))):
+        args = _icnt_args(tmp_path, name, **kw)
+        native.parse_config(args + ["-icnt_link_contention", "1"])
+        with pytest.raises(Exception, match="num_vcs"):
+            native.parse_config(args + ["-icnt_link_contention", "2"])
+    ok = _icnt_args(tmp_path, "torus2", k=8, n=2, topology="torus", num_vcs="2")
+    native.parse_config(ok + ["-icnt_link_contention", "2"])
+
+
+@pytest.mark.gpu
+def test_router_back_pressure_gpu_matches_cpu(native, tmp_path):
+    icnt = _icnt_args(tmp_path, "bpg", k=8, n=2, topology="mesh", input_buffer_size=9, vc_buf_size=4,
+                      internal_speedup="1.0")
+    kl = _store_app(tmp_path, "stg", 32)
+    res = []
+    for eng in ("cpu", "gpu"):
+        s = native.Simulator(icnt + ["-icnt_link_contention", "2", "-gpgpu_perf_sim_memcpy", "0",
+                                     "-sim_engine", eng, "-trace", kl], False)
+        assert s.run() == 0
+        res.append((s.tot_cycle, _link_stat(s.output, "Req_Network_injection_stall_cycles"),
+                    _link_stat(s.output, "Reply_Network_injection_stall_cycles"),
+                    _link_stat(s.output, "Network_link_wait_cycles")))
+    assert res[0] == res[1] and res[0][1] > 0

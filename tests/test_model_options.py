@@ -377,3 +377,40 @@ def test_copy_latency_every_kernel(native, tmp_path):
     assert ke[0] == kb[0]
     assert 777 <= ke[1] - kb[1] <= 777 + 32
     assert ke[2:] == kb[2:]
+
+
+def _late_barrier_kernel():
+    """One CTA of 4 warps per SM (one warp per scheduler); warps 1-3 reach
+    the barrier at once, warp 0 only after a chain of ALU work: the cycle its
+    BAR.SYNC issues on scheduler 0 releases the idle schedulers 1-3."""
+    from accel_sim_framework_distributed_amd.tracegen.builder import KernelBuilder
+    k = KernelBuilder("late_barrier", (80, 1, 1), (128, 1, 1), nregs=16)
+    first = k.g.warp == 0
+    for _ in range(3):
+        k.op("IMAD", [4], [4, 5])
+        k.op("BAR.SYNC")
+        for _ in range(24):
+            k.op("IMAD", [4], [4, 5], present=first)
+        k.op("BAR.SYNC")
+        k.alu("FFMA", 6)
+    k.op("EXIT")
+    return k.build()
+
+
+@pytest.mark.parametrize("app", ["late_barrier", "hotspot", "backprop"])
+def test_issue_distro_same_with_scheduler_trace(native, tmp_path, app):
+    """The WARP_SCHEDULER trace stream forces the sequential issue loop; the
+    lane-parallel one must classify idle schedulers at the same point (after
+    the barrier / exit instructions of the schedulers before the first idle
+    one), so the warp occupancy distribution is identical with it on and off
+    on barrier-heavy kernels."""
+    import re
+    gen = {"late_barrier": lambda: [_late_barrier_kernel()], "hotspot": lambda: rodinia.hotspot(64, 2, 2),
+           "backprop": lambda: rodinia.backprop(1024)}[app]
+    kl = rodinia.write_app(str(tmp_path / app), gen())
+    off = _run(native, kl, {"-gpgpu_perf_sim_memcpy": "0"})
+    on = _run(native, kl, {"-gpgpu_perf_sim_memcpy": "0", "-trace_enabled": "1", "-trace_sampling_core": "5",
+                           "-trace_components": "WARP_SCHEDULER"})
+    dist = lambda s: re.findall(r"Warp Occupancy Distribution:\n(.*)", s.output)
+    assert dist(off) and dist(on) == dist(off)
+    assert on.tot_cycle == off.tot_cycle

@@ -8,3 +8,19 @@ def test_l1_port_granule_fit_from_strided_loads():
     g, err, errs = T.fit_l1_port_granule(m, 32)
     assert g == 32 and err < 0.05 and errs[0] > 0.3
     assert T.l1_data_cycles(16, 32, 0) == 8 and T.l1_data_cycles(16, 32, 32) == 32
+
+
+def test_sweep_address_mappings_match_reference_and_tuned_config():
+    """The sweep's 32B / 256B address mappings are the reference's strings
+    (define-standard-cfgs.yml:147-151); the tuned MI355X config uses the 256B
+    one, so the sweep's 256B point is that config's own mapping."""
+    import os
+    from accel_sim_framework_distributed_amd.parallel.sweep import EXTRA_FLAGS
+    m256 = EXTRA_FLAGS["256B"]["-gpgpu_mem_addr_mapping"]
+    m32 = EXTRA_FLAGS["32B"]["-gpgpu_mem_addr_mapping"]
+    assert m256 == "dramid@8;00000000.00000000.00000000.00000000.0000RRRR.RRRRRRRR.RBBBCCCB.CCCSSSSS"
+    assert m32 == "dramid@5;00000000.00000000.00000000.00000000.0000RRRR.RRRRRRRR.RBBBCCCC.BCCSSSSS"
+    cfg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", "tuned",
+                       "AMD_Instinct_MI355X", "gpgpusim.config")
+    lines = [l.split(None, 1)[1].strip() for l in open(cfg) if l.startswith("-gpgpu_mem_addr_mapping")]
+    assert lines == [m256]
