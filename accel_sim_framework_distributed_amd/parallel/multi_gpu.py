@@ -192,6 +192,18 @@ class DistributedSuite:
             per = min(per, cap)
         return max(1, cus // per // self.ranks_per_gpu()) if cus else 1
 
+    @staticmethod
+    def gpu_reserve(gslots: int) -> int:
+        """Host cores kept for the threads driving GPU-engine simulations.
+        LDS-state engine: one per slot (each thread launches and waits on its
+        own simulation).  Global-state engine (ASIM_GPU_STATE=global): the
+        simulations share batch launches -- one leader thread waits on the
+        GPU while the others sleep -- so two cores (ASIM_GPU_HOST_RESERVE)
+        cover them however many run."""
+        if os.environ.get("ASIM_GPU_STATE") == "global":
+            return min(gslots, max(1, int(os.environ.get("ASIM_GPU_HOST_RESERVE", "2"))))
+        return gslots
+
     def cpu_slots(self, reserve: int = 0) -> int:
         """Host cores this rank may use for CPU-engine simulations: its share
         of the node's cores (ranks of one node split them), less `reserve`
@@ -302,7 +314,7 @@ class DistributedSuite:
         whole node's load is noisy enough to flip a placement."""
         from concurrent.futures import ThreadPoolExecutor
         gslots = max(1, self.concurrency())
-        cslots = self.cpu_slots(reserve=gslots)
+        cslots = self.cpu_slots(reserve=self.gpu_reserve(gslots))
         best: Dict = {}
         # the DDP step is timed uncoupled (its collectives emulated locally):
         # two engines running it at once must not both talk to the other ranks
@@ -354,7 +366,7 @@ class DistributedSuite:
         list scheduling over the host cores with each CPU application's
         thread count)."""
         gslots = max(1, self.concurrency())
-        cslots = self.cpu_slots(reserve=gslots)
+        cslots = self.cpu_slots(reserve=self.gpu_reserve(gslots))
         names = [a for a, _ in self.apps]
         tg = [self.times.get((a, "gpu"), 1.0) for a in names]
         tc = [self.times.get((a, "cpu"), 1.0) for a in names]
@@ -386,7 +398,7 @@ class DistributedSuite:
         re-plan, repeat.  Stops when the critical path is on the GPU, the
         critical application stops scaling, or the cores run out."""
         gslots = max(1, self.concurrency())
-        cores = self.cpu_slots(reserve=gslots)
+        cores = self.cpu_slots(reserve=self.gpu_reserve(gslots))
         kl_of = dict(self.apps)
         tried = set()
         self._calibrating = True
@@ -437,7 +449,7 @@ class DistributedSuite:
                 self.widen()
             self.plan()
         gslots = max(1, self.concurrency())
-        cslots = self.cpu_slots(reserve=gslots)
+        cslots = self.cpu_slots(reserve=self.gpu_reserve(gslots))
         ga = sorted([x for x in self.apps if self.assignment[x[0]] == "gpu"], key=lambda x: -self.times[(x[0], "gpu")])
         ca = sorted([x for x in self.apps if self.assignment[x[0]] == "cpu"], key=lambda x: -self.times[(x[0], "cpu")])
         # host cores as tokens: an application takes its threads' worth before

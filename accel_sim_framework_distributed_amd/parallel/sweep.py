@@ -95,7 +95,7 @@ class SweepRunner:
         s = self.suite
         mode = s.engine
         gslots = max(1, s.concurrency()) if mode in ("gpu", "node") else 0
-        cslots = s.cpu_slots(reserve=gslots if mode == "node" else 0) if mode in ("cpu", "node") else 0
+        cslots = s.cpu_slots(reserve=s.gpu_reserve(gslots) if mode == "node" else 0) if mode in ("cpu", "node") else 0
         # GPU-friendly first (low gpu/cpu ratio), longest first among equals
         order = sorted(self.jobs, key=lambda j: (self.ratio.get(j[0], 1.0), j[0], j[2]))
         lock = threading.Lock()

@@ -178,7 +178,7 @@ def _sweep(a, suite, engine, rank, world, use_cuda) -> int:
 def _baseline_parts(kips, gpu_kips, suite, engine, world):
     """The headline split into what the MI355X cycle engine simulated and what
     the host cores did, each against the reference's one-core 349 KIPS."""
-    cores = suite.cpu_slots(reserve=max(1, suite.concurrency())) if engine in ("node", "cpu") else 0
+    cores = suite.cpu_slots(reserve=suite.gpu_reserve(max(1, suite.concurrency()))) if engine in ("node", "cpu") else 0
     host = max(0.0, kips - gpu_kips)
     per_core = host / max(1, cores * world) if cores else 0.0
     return {"gpu_engine_kips": round(gpu_kips, 1), "gpu_engine_vs_baseline": round(gpu_kips / BASELINE_KIPS, 3),
@@ -365,7 +365,7 @@ def main() -> int:
                     # wall seconds of every application in the last timed step
                     # (the step's makespan is the longest of them)
                     "node_step_wall_s": {k: round(v.get("wall_s", 0.0), 4) for k, v in last_apps.items()},
-                    "node_host_cores": suite.cpu_slots(reserve=max(1, suite.concurrency()))} if engine == "node" else {}),
+                    "node_host_cores": suite.cpu_slots(reserve=suite.gpu_reserve(max(1, suite.concurrency())))} if engine == "node" else {}),
                 "apps": len(suite.apps),
                 "sim_insn_per_step_per_rank": int(insn / max(1, a.steps)),
                 "sim_cycles_per_step_per_rank": int(cycles / max(1, a.steps)),

@@ -42,7 +42,8 @@ CORE_SRC = [
     "csrc/driver/icnt_bench.cc",
     "csrc/parallel/linksim.cc",
 ]
-HIP_SRC = ["csrc/engine/gpu_engine.hip", "csrc/engine/ingest_mfma.hip"]
+HIP_SRC = ["csrc/engine/gpu_engine.hip", "csrc/engine/engine_k_lds.hip", "csrc/engine/engine_k_prof.hip",
+           "csrc/engine/engine_k_global.hip", "csrc/engine/ingest_mfma.hip"]
 STUB_SRC = ["csrc/engine/gpu_stub.cc"]
 
 

@@ -1,4 +1,4 @@
-// MI355X (gfx950) cycle engine.
+// MI355X (gfx950) cycle engine, host side (the kernel: engine_kernel.h).
 //
 // One persistent launch simulates up to `max_epochs` PDES epochs of the whole
 // simulated GPU:
@@ -29,14 +29,14 @@
 #include <sys/file.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <vector>
 
-#include "engine.h"
-#include "grid_barrier.h"
+#include "engine_kernel.h"
 #include "trace_window.h"
-#include "wave_par.h"
 
 namespace asim {
 
@@ -47,437 +47,16 @@ namespace asim {
       throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x);    \
   } while (0)
 
-// The configuration of every running simulation lives in constant memory
-// (one slot per engine instance of the process, GpuArgs::cfg_slot).  Read
-// through address space 4, every wave-uniform access is a scalar load the
-// compiler may hoist and CSE freely (constant memory is never written by a
-// kernel), so configuration-derived values stay in SGPRs and their
-// arithmetic is SALU; only lane-indexed reads become vector loads.  From the
-// LDS copy used before, each read after any state store had to be re-issued
-// (the compiler cannot rule out aliasing with the state in LDS) and landed in
-// a VGPR: constant memory measured 6-7 % faster on bfs / hotspot / heartwall
-// (profiles/r4/ab_cfg_const_vs_lds.txt), bit-exact.
-constexpr int kCfgSlots = 64;
-__constant__ SimCfg g_cfg[kCfgSlots];
-
-// in-kernel power sampler state (engine.h PwrArm; power_eval.h)
-struct PwrDev {
-  PwrCoef coef;
-  uint64_t freq;
-  uint64_t t_prev;  // cycle of the previous sample (evaluator block)
-  uint64_t next;    // next sample point (written back by block 0 at exit)
-  uint32_t n_sm;
-  uint32_t n;       // samples written to `ring` this launch
-  uint32_t cap;
-  uint32_t pad;
-  double s_prev[kPwrSumPad];
-  double* rows;      // [units][kPwrRawPad] raw counters of the sample being taken
-  PwrSample* ring;   // [cap] samples of this launch (the host drains after it)
-};
-
-struct GpuArgs {
-  uint32_t cfg_slot;                 // g_cfg slot of this engine
-  const SimCfg* __restrict__ cfg_g;  // global copy (not read by the engine kernel)
-  const KernelTab* kt;               // running kernels (copied into LDS at launch)
-  SMState* sms;
-  ChanState* chs;
-  EpochPub* pub;
-  Pkt* box_req[2];
-  uint32_t* cnt_req[2];
-  Pkt* box_rep[2];
-  uint32_t* cnt_rep[2];
-  uint32_t cap_req, cap_rep;
-  Pkt* ovf;
-  uint32_t ovf_cap;
-  L2Line* mall;  // [n_mem][mall_sets * mall_assoc] or nullptr
-  uint64_t* link_free;  // -icnt_link_contention: [links] free times, then 2 statistics words; or nullptr
-  uint32_t* link_refs;  // the pass's packet list
-  uint64_t epoch0;
-  uint64_t cycle0;
-  uint64_t max_cycle;
-  uint32_t max_epochs;
-  uint32_t nblocks;
-  GpuCtl* ctl;
-  uint64_t* prof;  // [nblocks][kProfSlots] shader-clock cycles per stage (profiling build)
-  uint32_t* ework; // [nblocks] work clocks of the last epoch (profiling build)
-  PwrDev* pw;      // armed power sampler, or nullptr
-};
-
-template <class T>
-__device__ __forceinline__ void copy_state(T* dst, const T* src) {
-  static_assert(sizeof(T) % 16 == 0, "state must be 16-byte granular");
-  const uint4* s = reinterpret_cast<const uint4*>(src);
-  uint4* d = reinterpret_cast<uint4*>(dst);
-  const int n = (int)(sizeof(T) / 16);
-  for (int i = (int)(threadIdx.x & 63); i < n; i += 64) d[i] = s[i];
-  __syncthreads();
-}
-
-// HBM -> LDS state swap-in for time-sliced units: LDS-DMA (global_load_lds,
-// 16 B per lane, lane-linear LDS image) issues the whole state back to back
-// with no VGPR staging, then one wait.
-template <class T>
-__device__ __forceinline__ void swap_in(T* lds, const T* src) {
-  static_assert(sizeof(T) % 16 == 0, "state must be 16-byte granular");
-  typedef __attribute__((address_space(1))) const uint4 g4;
-  typedef __attribute__((address_space(3))) uint4 l4;
-  const uint4* s = reinterpret_cast<const uint4*>(src);
-  uint4* d = reinterpret_cast<uint4*>(lds);
-  const int n = (int)(sizeof(T) / 16);
-  const int lane = (int)(threadIdx.x & 63);
-  for (int i = 0; i < n; i += 64)
-    if (i + lane < n) __builtin_amdgcn_global_load_lds((g4*)(s + i + lane), (l4*)(d + i), 16, 0, 0);
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-}
-// LDS -> HBM swap-out: eight 16-byte LDS reads in flight per lane, then the
-// stores (completion is awaited by the epoch barrier's release fence)
-template <class T>
-__device__ __forceinline__ void swap_out(T* dst, const T* lds) {
-  const uint4* s = reinterpret_cast<const uint4*>(lds);
-  uint4* d = reinterpret_cast<uint4*>(dst);
-  const int n = (int)(sizeof(T) / 16);
-  const int lane = (int)(threadIdx.x & 63);
-  int i = 0;
-  for (; i + 4 * 64 <= n; i += 4 * 64) {
-    uint4 v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = s[i + j * 64 + lane];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) d[i + j * 64 + lane] = v[j];
-  }
-  for (; i < n; i += 64)
-    if (i + lane < n) d[i + lane] = s[i + lane];
-  __syncthreads();
-}
-
-extern __shared__ __attribute__((aligned(16))) char g_lds[];
-// Block LDS layout: the kernel table, the stage profiler and the power
-// evaluator's scratch first (a few KB), then -- in the LDS-state build -- the
-// resident unit's state.  The global-state build (ASIM_GPU_STATE=global)
-// allocates only the first part: its units work on their HBM images, so many
-// engine waves share a CU.
-constexpr int kProfSlots = 48;
-struct ProfLds {
-  uint64_t last;
-  uint32_t slot;
-  uint32_t pad;
-  uint64_t acc[kProfSlots];
-};
-constexpr size_t kKtOff = 0;
-constexpr size_t kProfOff = kKtOff + (sizeof(KernelTab) + 15) / 16 * 16;
-// the power evaluator's sums and deltas (one block per sample)
-constexpr size_t kPwrOff = kProfOff + (sizeof(ProfLds) + 15) / 16 * 16;
-constexpr size_t kStateOff = (kPwrOff + 2 * kPwrSumPad * sizeof(double) + 15) / 16 * 16;
-constexpr size_t kStateLds = ((sizeof(SMState) > sizeof(ChanState) ? sizeof(SMState) : sizeof(ChanState)) + 15) / 16 * 16;
-constexpr size_t kLdsBytes = kStateOff + kStateLds;
-constexpr size_t kLdsBytesGlobal = kStateOff;
-static_assert(kLdsBytes <= 160 * 1024, "per-block LDS budget exceeded");
-
-// a pointer the compiler may treat as global memory (address space 1): the
-// generic -> global cast lets address-space inference turn the model's flat
-// accesses through it into global_load / global_store
-template <class T>
-__device__ __forceinline__ T* as_global(T* p) {
-  typedef __attribute__((address_space(1))) T gT;
-  return (T*)(gT*)p;
-}
-
-// profiling build of the lane policy: P::prof(k) charges the shader-clock
-// time since the previous stamp to the previous stage and enters stage k
-struct WaveParProf : WavePar {
-  static __device__ __forceinline__ void prof(int k) {
-    ProfLds* p = reinterpret_cast<ProfLds*>(g_lds + kProfOff);
-    uint64_t t = __builtin_amdgcn_s_memtime();
-    if ((threadIdx.x & 63) == 0) {
-      p->acc[p->slot] += t - p->last;
-      p->slot = (uint32_t)k;
-      p->last = t;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  // event counters in the spare slots (not time): P::tick(k) adds one
-  static __device__ __forceinline__ void tick(int k) {
-    ProfLds* p = reinterpret_cast<ProfLds*>(g_lds + kProfOff);
-    if ((threadIdx.x & 63) == 0) p->acc[k] += 1;
-    __builtin_amdgcn_wave_barrier();
-  }
-};
-
-typedef double f64x4 __attribute__((ext_vector_type(4)));
-
-// a unit's raw power counters (power_eval.h step 1) into its row
-__device__ __forceinline__ void pwr_row_sm(double* row, const SMStats& st) {
-  for (int k = (int)(threadIdx.x & 63); k < kPwrRawPad; k += 64) row[k] = k < PR_COUNT ? (double)pwr_raw_sm(st, k) : 0.0;
-}
-__device__ __forceinline__ void pwr_row_ch(double* row, const ChanState& ch, uint32_t nsub) {
-  for (int k = (int)(threadIdx.x & 63); k < kPwrRawPad; k += 64) {
-    double v = 0;
-    if (k < PR_COUNT)
-      for (uint32_t j = 0; j < nsub; ++j) v += (double)pwr_raw_mem(ch.sp[j].st, k);
-    row[k] = v;
-  }
-}
-
-// power_eval.h steps 2 and 3 on one wave: S = rows x M as f64 MFMA tiles
-// (16 units x 4 raw counters by 4 raw counters x 16 sums, accumulated over
-// unit tiles and k-steps; integers below 2^53, so exact in any order), then
-// the sample on lane 0 into the ring
-__device__ void pwr_evaluate(PwrDev& pw, uint32_t nunits, uint64_t now) {
-  const int lane = (int)(threadIdx.x & 63);
-  constexpr int kCt = kPwrSumPad / 16;
-  f64x4 acc[kCt];
-#pragma unroll
-  for (int ct = 0; ct < kCt; ++ct) acc[ct] = f64x4{0.0, 0.0, 0.0, 0.0};
-  const double* rows = pw.rows;
-  for (uint32_t t = 0; t < (nunits + 15u) / 16u; ++t) {
-    const uint32_t u = 16u * t + (uint32_t)(lane & 15);
-    for (int k4 = 0; k4 < kPwrRawPad / 4; ++k4) {
-      const int k = 4 * k4 + (lane >> 4);
-      const double av = u < nunits ? rows[(size_t)u * kPwrRawPad + k] : 0.0;
-      const int sj = k < PR_COUNT ? pwr_sum_of(k) : -1;
-#pragma unroll
-      for (int ct = 0; ct < kCt; ++ct) {
-        const double bv = sj == 16 * ct + (lane & 15) ? 1.0 : 0.0;
-        acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[ct], 0, 0, 0);
-      }
-    }
-  }
-  double* S = reinterpret_cast<double*>(g_lds + kPwrOff);
-  double* D = S + kPwrSumPad;
-#pragma unroll
-  for (int ct = 0; ct < kCt; ++ct) {
-    // D layout: column lane & 15, rows (lane >> 4) + 4 * reg: sum the four
-    // rows a lane holds, then across the four lane groups
-    double v = acc[ct][0] + acc[ct][1] + acc[ct][2] + acc[ct][3];
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    if (lane < 16) S[16 * ct + lane] = v;
-  }
-  __syncthreads();
-  if (lane < PS_COUNT) D[lane] = S[lane] - pw.s_prev[lane];
-  __syncthreads();
-  if (lane == 0) {
-    const uint32_t i = pw.n < pw.cap ? pw.n : pw.cap - 1;
-    PwrSample& o = pw.ring[i];
-    pwr_activity(D, now > pw.t_prev ? (double)(now - pw.t_prev) : 1.0, pw.n_sm, o);
-    pwr_power(pw.coef, pw.coef.coef, pw.n_sm, 1.0, 1.0, 1.0, o);
-    o.now = now;
-    pw.t_prev = now;
-    pw.n = pw.n + 1;
-  }
-  if (lane < PS_COUNT) pw.s_prev[lane] = S[lane];
-  __syncthreads();
-}
-
-template <class P, bool kSliced, bool kGlobal = false>
-__global__ void __launch_bounds__(64) engine_kernel(GpuArgs a) {
-  const uint32_t b = blockIdx.x;
-  // The configuration is read all over the model, much of it at lane-varying
-  // indices (address-decoder bit runs, per-unit counts, cache geometries
-  // selected per warp): constant memory, one slot per engine (g_cfg above).
-  const SimCfg& c = g_cfg[a.cfg_slot];
-  const uint64_t E = c.icnt_latency;
-  // Units (SMs 0..n_sm-1, then channels) map to blocks round-robin: unit
-  // b + k * nblocks.  LDS-state build: with no more units than blocks each
-  // block owns one unit whose state stays in LDS for the whole launch;
-  // otherwise (configs larger than the CU count, e.g. the 384-unit MI355X
-  // preset) a block time-slices its units every epoch, swapping states
-  // through HBM and keeping the last one resident into the next epoch.
-  // Global-state build (kGlobal): every unit is simulated in place in its HBM
-  // image (vector-L1 / L2 resident while its block works on it), the block
-  // holds no state in LDS and several engine waves share each CU.
-  SMState* s = reinterpret_cast<SMState*>(g_lds + kStateOff);
-  ChanState* ch = reinterpret_cast<ChanState*>(g_lds + kStateOff);
-  const uint32_t nunits = c.n_sm + c.n_mem;
-  const uint32_t nmine = kSliced ? (nunits - 1 - b) / a.nblocks + 1 : 1;
-  uint32_t loaded = b;  // unit whose state is in LDS (global build: the unit being simulated)
-  auto unit_k = [&](uint32_t k) { return b + k * a.nblocks; };
-  auto bind = [&](uint32_t u) {
-    if (u < c.n_sm) s = as_global(&a.sms[u]);
-    else ch = as_global(&a.chs[u - c.n_sm]);
-  };
-  auto swap_to = [&](uint32_t u) {
-    if (kGlobal) {
-      bind(u);
-      loaded = u;
-      return;
-    }
-    if (!kSliced || u == loaded) return;
-    if (loaded < c.n_sm) swap_out(&a.sms[loaded], s);
-    else swap_out(&a.chs[loaded - c.n_sm], ch);
-    if (u < c.n_sm) swap_in(s, &a.sms[u]);
-    else swap_in(ch, &a.chs[u - c.n_sm]);
-    loaded = u;
-  };
-  if (kGlobal)
-    bind(b);
-  else if (b < c.n_sm)
-    copy_state(s, &a.sms[b]);
-  else
-    copy_state(ch, &a.chs[b - c.n_sm]);
-  // kernel table lives in LDS (never in scratch)
-  KernelTab* ktl = reinterpret_cast<KernelTab*>(g_lds + kKtOff);
-  {
-    static_assert(sizeof(KernelTab) % 16 == 0, "kernel table must be 16-byte granular");
-    const uint4* src = reinterpret_cast<const uint4*>(a.kt);
-    uint4* dst = reinterpret_cast<uint4*>(ktl);
-    for (int i = (int)(threadIdx.x & 63); i < (int)(sizeof(KernelTab) / 16); i += 64) dst[i] = src[i];
-  }
-  ProfLds* pl = reinterpret_cast<ProfLds*>(g_lds + kProfOff);
-  if ((threadIdx.x & 63) == 0) {
-    pl->last = __builtin_amdgcn_s_memtime();
-    pl->slot = 31;
-    for (int i = 0; i < kProfSlots; ++i) pl->acc[i] = 0;
-  }
-  __syncthreads();
-  const KernelTab& kt = *ktl;
-  SmCtx sx;
-  sx.cfg = &c;
-  sx.kt = &kt;
-  sx.out_cap = a.cap_req;
-  sx.n_src_sm = c.n_sm;
-  sx.rt_st = c.link_contention == 2 ? a.link_free : nullptr;
-  MemCtx mx;
-  mx.cfg = &c;
-  mx.out_cap = a.cap_rep;
-  mx.n_src_sub = c.n_subpart;
-  mx.ovf = a.ovf;
-  mx.ovf_cap = a.ovf_cap;
-  mx.rt_st = c.link_contention == 2 ? a.link_free : nullptr;
-  mx.mall = nullptr;
-  uint64_t epoch = a.epoch0, cycle = a.cycle0;
-  uint64_t t_work0 = a.ework ? __builtin_amdgcn_s_memtime() : 0;
-  uint32_t done = 0, dead = 0, capped = 0;
-  uint32_t n = 0;
-  uint32_t nbar = 0;  // grid barriers of this launch (epochs + power samples)
-  uint64_t pw_next = a.pw ? a.pw->next : 0;
-  bool failed = false;
-  // destinations with packets in the previous epoch's mailboxes (all at the
-  // launch's first epoch): the gathers of the others are skipped
-  uint64_t reqm[2] = {~0ull, ~0ull}, repm[2] = {~0ull, ~0ull};
-  for (; n < a.max_epochs;) {
-    const uint32_t cur = (uint32_t)(epoch & 1), prev = cur ^ 1u;
-    const uint64_t t0 = cycle, t1 = t0 + E;
-    // the resident unit first, then the others (units are independent
-    // within an epoch: they read only the previous epoch's mailboxes)
-    uint32_t first_k = 0;
-    for (uint32_t k = 0; k < nmine; ++k)
-      if (unit_k(k) == loaded) first_k = k;
-    for (uint32_t j = 0; j < nmine; ++j) {
-      const uint32_t u = unit_k((first_k + j) % nmine);
-      swap_to(u);
-      if (u < c.n_sm) {
-        sx.outbox = a.box_req[cur];
-        sx.outcnt = a.cnt_req[cur];
-        sm_epoch<P>(*s, sx, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep,
-                    c.n_subpart, epoch, repm);
-        sm_publish<P>(*s, sx, *a.pub, cur);
-      } else {
-        mx.outbox = a.box_rep[cur];
-        mx.outcnt = a.cnt_rep[cur];
-        mx.mall = a.mall ? a.mall + (size_t)(u - c.n_sm) * ((size_t)c.mall_sets * c.mall_assoc) : nullptr;
-        mx.win_end = core_fs(c, t1);
-        chan_epoch<P>(*ch, mx, a.box_req[prev], a.cnt_req[prev], a.cap_req, core_fs(c, t0), reqm);
-        chan_publish<P>(*ch, mx, *a.pub, cur);
-      }
-    }
-    ++n;
-    P::prof(26);  // barrier
-    uint64_t t_arrive = 0;
-    if (a.ework) {
-      t_arrive = __builtin_amdgcn_s_memtime();
-      if ((threadIdx.x & 63) == 0) a.ework[b] = (uint32_t)(t_arrive - t_work0);
-    }
-    uint32_t was_last = 0;
-    if (!grid_barrier(a.ctl, a.nblocks, nbar++, &was_last)) break;
-    if (a.link_free) {
-      // shared links of multi-hop routes: block 0 walks this epoch's packets
-      // in the fixed order (icnt_links.h), then every block waits for it
-      // before a destination reads them
-      if (b == 0)
-        icnt_epoch_pass<P>(c, a.box_req[cur], a.cnt_req[cur], a.cap_req, a.box_rep[cur], a.cnt_rep[cur], a.cap_rep,
-                           a.link_free, a.link_refs);
-      if (!grid_barrier(a.ctl, a.nblocks, nbar++)) break;
-    }
-    P::prof(27);  // decision
-    if (a.ework) {
-      const uint64_t t_exit = __builtin_amdgcn_s_memtime();
-      if ((threadIdx.x & 63) == 0 && was_last) { pl->acc[34] += t_exit - t_arrive; pl->acc[35] += 1; }
-      if (b == 0) {
-        // slowest block's work this epoch (critical path) and the epoch count
-        uint64_t mk = 0;  // work << 32 | block: the slowest block and its work
-        for (uint32_t j = threadIdx.x & 63; j < a.nblocks; j += 64) {
-          const uint64_t k = (uint64_t)a.ework[j] << 32 | j;
-          mk = k > mk ? k : mk;
-        }
-        mk = WavePar::red_max64(mk);
-        const uint32_t m = (uint32_t)(mk >> 32);
-        if ((threadIdx.x & 63) == 0) {
-          pl->acc[32] += m;
-          pl->acc[33] += 1;
-          // per block: epochs in which it was the slowest (slot 30)
-          atomicAdd((unsigned long long*)&a.prof[(size_t)(uint32_t)mk * kProfSlots + 30], 1ull);
-        }
-      }
-      t_work0 = t_exit;
-    }
-    // an armed power sampler's next point clamps the fast-forward like a
-    // sampled slice's max_cycle would
-    const uint64_t mc = a.pw ? (a.max_cycle ? (a.max_cycle < pw_next ? a.max_cycle : pw_next) : pw_next) : a.max_cycle;
-    EpochDecision d = epoch_decide<P>(c, *a.pub, cur, t1, kt, epoch, mc);
-    reqm[0] = P::uni(d.req_dst[0]);
-    reqm[1] = P::uni(d.req_dst[1]);
-    repm[0] = P::uni(d.rep_dst[0]);
-    repm[1] = P::uni(d.rep_dst[1]);
-    P::prof(28);
-    ++epoch;
-    cycle = P::uni(d.next_start);
-    if (a.pw) {
-      const bool exits = P::uni(d.done) || P::uni(d.deadlock) || P::uni(d.limit) || (a.max_cycle && cycle >= a.max_cycle);
-      if (exits || cycle >= pw_next) {
-        // every block writes its units' counters, one barrier, then the last
-        // block evaluates the sample while the others run on
-        for (uint32_t k = 0; k < nmine; ++k) {
-          const uint32_t u = unit_k(k);
-          double* row = a.pw->rows + (size_t)u * kPwrRawPad;
-          if (u < c.n_sm) pwr_row_sm(row, (!kGlobal && u == loaded) ? s->st : a.sms[u].st);
-          else pwr_row_ch(row, (!kGlobal && u == loaded) ? *ch : a.chs[u - c.n_sm], c.n_sub_per_mem);
-        }
-        if (!grid_barrier(a.ctl, a.nblocks, nbar++)) { failed = true; break; }
-        if (b == a.nblocks - 1) pwr_evaluate(*a.pw, nunits, cycle);
-        pw_next = cycle + a.pw->freq;
-      }
-    }
-    if (P::uni(d.done)) { done = P::uni(d.done); break; }
-    if (P::uni(d.deadlock)) { dead = 1; break; }
-    if (P::uni(d.limit)) { capped = 1; break; }
-    if (P::uni(d.refill)) break;  // the host streams in more of a kernel's trace
-    if (a.max_cycle && cycle >= a.max_cycle) break;
-  }
-  P::prof(31);  // launch_rest
-  // write the resident state back
-  if (kGlobal)
-    ;
-  else if (loaded < c.n_sm)
-    copy_state(&a.sms[loaded], s);
-  else
-    copy_state(&a.chs[loaded - c.n_sm], ch);
-  if (a.prof && (threadIdx.x & 63) < kProfSlots && (threadIdx.x & 63) != 30) a.prof[(size_t)b * kProfSlots + (threadIdx.x & 63)] += pl->acc[threadIdx.x & 63];
-  (void)failed;
-  if (a.pw && b == 0 && (threadIdx.x & 63) == 0) a.pw->next = pw_next;
-  if (b == 0 && (threadIdx.x & 63) == 0) {
-    a.ctl->done = done;
-    a.ctl->deadlock = dead;
-    a.ctl->cap = capped;
-    a.ctl->end_cycle = cycle;
-    a.ctl->end_epoch = epoch;
-    a.ctl->epochs_run = n;
-  }
-}
-
-// small kernel: apply the host-side L2 edits by copying back is simpler; the
-// engine keeps states resident and moves them to the host only on demand.
+// builds of engine_kernel, instantiated in the kernel TUs (engine_k_*.hip)
+extern template __global__ void engine_kernel<WavePar, false, false>(GpuArgs);
+extern template __global__ void engine_kernel<WavePar, true, false>(GpuArgs);
+extern template __global__ void engine_kernel<WaveParProf, false, false>(GpuArgs);
+extern template __global__ void engine_kernel<WaveParProf, true, false>(GpuArgs);
+extern template __global__ void engine_kernel<WavePar, true, true>(GpuArgs);
+extern template __global__ void engine_kernel<WaveParProf, true, true>(GpuArgs);
+hipError_t engine_upload_cfg_lds(const SimCfg& c, int slot);
+hipError_t engine_upload_cfg_prof(const SimCfg& c, int slot);
+hipError_t engine_upload_cfg_global(const SimCfg& c, int slot);
 
 namespace {
 
@@ -551,19 +130,53 @@ class DeviceCuTable {
   int fd_ = -1;
 };
 
-// Engine blocks per CU are accounted in slots: kCuSlots per CU, a block
-// takes the share of the CU's LDS it allocates (one CU for the LDS-state
-// build, one slot for the global-state build: 8 engine waves per CU, within
-// the VGPR budget of the kernel's 12 waves).
-constexpr uint32_t kCuSlots = 8;
+// Engine blocks per CU are accounted in slots, kCuSlots per CU (840 =
+// lcm(1..8): any whole number of blocks per CU up to 8 divides it).  An
+// LDS-state block takes the share of the CU's LDS it allocates (a whole CU);
+// a global-state block takes kCuSlots / (its blocks per CU), the kernel's
+// occupancy from its register and LDS use (one block of margin below the
+// occupancy API's figure, which can read one block high: MI355X_MICROARCH
+// "Occupancy API one block/CU high"), at most 8.
+constexpr uint32_t kCuSlots = 840;
+constexpr uint32_t kMaxBlocksPerCu = 8;
 uint32_t block_slots(size_t lds) {
-  const size_t per = (160 * 1024) / kCuSlots;
-  const uint32_t n = (uint32_t)((lds + per - 1) / per);
-  return n < 1 ? 1u : n > kCuSlots ? kCuSlots : n;
+  const size_t per_cu = lds ? (160 * 1024) / lds : kMaxBlocksPerCu;  // blocks whose LDS fits one CU
+  return kCuSlots / (uint32_t)std::max<size_t>(1, std::min<size_t>(per_cu, kMaxBlocksPerCu));
 }
 bool gpu_state_global() {
   const char* e = getenv("ASIM_GPU_STATE");
   return e && std::string(e) == "global";
+}
+int g_occ_api = 0;  // the occupancy API's blocks per CU of the batch kernel (diagnostics)
+// global-state blocks per CU (cached; needs a current device)
+uint32_t global_blocks_per_cu() {
+  static std::once_flag once;
+  static uint32_t bpc = 1;
+  std::call_once(once, [] {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)engine_batch_kernel, 64, kLdsBytesGlobal) !=
+        hipSuccess)
+      occ = 2;
+    g_occ_api = occ;
+    occ = occ > 1 ? occ - 1 : 1;
+    if (const char* e = getenv("ASIM_GPU_BLOCKS_PER_CU"))  // measured override (co-residency tests)
+      if (atoi(e) > 0) occ = atoi(e);
+    bpc = (uint32_t)std::min<int>(occ, (int)kMaxBlocksPerCu);
+  });
+  return bpc;
+}
+uint32_t engine_block_slots(bool global) {
+  return global ? kCuSlots / global_blocks_per_cu() : block_slots(kLdsBytes);
+}
+bool profiling_env() {
+  const char* pe = getenv("ASIM_GPU_PROFILE");
+  return pe && *pe && *pe != '0';
+}
+// ASIM_GPU_BATCH (default on): global-state simulations of a process share
+// batch launches (engine_batch_kernel)
+bool gpu_batch_on() {
+  const char* e = getenv("ASIM_GPU_BATCH");
+  return !(e && std::string(e) == "0");
 }
 
 // Process-wide CU reservation.  Every simulation needs ALL its blocks
@@ -800,6 +413,185 @@ void pool_alloc(T** p, size_t n) {
   *p = static_cast<T*>(DevicePool::get().dev(n));
 }
 
+// Batch launches of the global-state engine (job-level parallelism on ONE
+// GPU, the reference's run_simulations.py / procman.py fan-out of
+// independent simulations, util/job_launching/run_simulations.py:375-397).
+// A process can only run a few kernels at once (GPU_MAX_HW_QUEUES hardware
+// queues), while a global-state simulation needs one wave per unit and an
+// MI355X holds several per CU.  So the simulations of a process submit their
+// launches here; a submitting thread becomes a leader and packs the pending
+// launches that fit the free CU slots into ONE engine_batch_kernel, and each
+// simulation's blocks synchronise only with each other (own GpuCtl).  Up to
+// kMaxBatches batches run at once, each on its own stream.  (More than one
+// is not safe with the global-state kernel: it spills ~1 KB per lane to
+// scratch, and batches on several hardware queues then failed to keep all
+// their waves resident -- a grid barrier timed out with at most 512 blocks
+// in flight over up to three queues where one queue held 672:
+// profiles/r6/README.md.)  A leader waits
+// until every simulation inside run() has submitted, or kBatchWaitUs after
+// the oldest pending launch (a simulation between two of its launches is
+// usually back within that).  Launches are capped at kBatchEpochs epochs so
+// a short one does not wait long for a long one of its batch.
+class BatchLauncher {
+ public:
+  static constexpr uint32_t kBatchEpochs = 1024;
+  static constexpr int kBatchWaitUs = 2000;
+  static constexpr int kMaxBatches = 1;  // concurrent batches
+  static BatchLauncher& get() {
+    static BatchLauncher* b = new BatchLauncher();  // never destroyed
+    return *b;
+  }
+  struct Sub {
+    GpuArgs a;
+    uint32_t nb = 0, slots = 0;
+    GpuCtl* h_ctl = nullptr;
+    bool done = false;
+    hipError_t err = hipSuccess;
+  };
+  // simulations currently inside GpuEngine::run (the leader waits for them)
+  void enter() {
+    std::lock_guard<std::mutex> g(mu_);
+    ++in_run_;
+  }
+  void leave() {
+    std::lock_guard<std::mutex> g(mu_);
+    --in_run_;
+    cv_.notify_all();
+  }
+  void run(Sub& me) {
+    std::unique_lock<std::mutex> g(mu_);
+    pending_.push_back(&me);
+    if (pending_.size() == 1) first_ = std::chrono::steady_clock::now();
+    cv_.notify_all();
+    while (!me.done) {
+      const bool queued = std::find(pending_.begin(), pending_.end(), &me) != pending_.end();
+      if (queued && running_ < kMaxBatches) {
+        // every simulation inside run() that is not in a running batch has submitted
+        const bool all_in = (int)pending_.size() >= in_run_ - in_flight_;
+        const bool waited = std::chrono::steady_clock::now() - first_ >= std::chrono::microseconds(kBatchWaitUs);
+        if (all_in || waited) {
+          lead(g);
+          continue;
+        }
+        cv_.wait_for(g, std::chrono::microseconds(25));
+        continue;
+      }
+      cv_.wait(g);
+    }
+  }
+  uint64_t batches() const { return batches_; }
+  uint64_t jobs() const { return jobs_; }
+
+ private:
+  struct Slot {  // one batch's stream and job tables
+    hipStream_t stream = nullptr;
+    GpuArgs *d_jobs = nullptr, *h_jobs = nullptr;
+    uint16_t *d_bj = nullptr, *h_bj = nullptr;
+    size_t jobs_cap = 0, blocks_cap = 0;
+    bool busy = false;
+  };
+  void lead(std::unique_lock<std::mutex>& g) {
+    Slot* sl = nullptr;
+    for (Slot& x : slots_)
+      if (!x.busy) {
+        sl = &x;
+        break;
+      }
+    sl->busy = true;
+    ++running_;
+    // FIFO: the pending launches that fit the GPU's slots (at least one)
+    const uint32_t cap = (uint32_t)CuPool::get().capacity();
+    std::vector<Sub*> take;
+    uint32_t slots = 0, blocks = 0;
+    while (!pending_.empty()) {
+      Sub* x = pending_.front();
+      if (!take.empty() && (slots + x->nb * x->slots > cap || blocks + x->nb > 65535u)) break;
+      take.push_back(x);
+      slots += x->nb * x->slots;
+      blocks += x->nb;
+      pending_.pop_front();
+    }
+    in_flight_ += (int)take.size();
+    if (!pending_.empty()) first_ = std::chrono::steady_clock::now();
+    g.unlock();
+    hipError_t err = launch(*sl, take, blocks, slots);
+    g.lock();
+    for (Sub* x : take) {
+      x->err = err;
+      x->done = true;
+    }
+    in_flight_ -= (int)take.size();
+    ++batches_;
+    jobs_ += take.size();
+    sl->busy = false;
+    --running_;
+    // the launches that waited behind this batch now wait (up to
+    // kBatchWaitUs) for its simulations to come back, so the next batch
+    // takes them together instead of alternating with them
+    if (!pending_.empty()) first_ = std::chrono::steady_clock::now();
+    cv_.notify_all();
+  }
+  hipError_t launch(Slot& sl, std::vector<Sub*>& take, uint32_t blocks, uint32_t slots) {
+    if (!sl.stream) {
+      if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) return hipErrorOutOfMemory;
+    }
+    const size_t njobs = take.size();
+    if (njobs > sl.jobs_cap || blocks > sl.blocks_cap) {
+      const size_t nj = std::max<size_t>(njobs, 2 * sl.jobs_cap), nbk = std::max<size_t>(blocks, 2 * sl.blocks_cap);
+      (void)hipFree(sl.d_jobs);
+      (void)hipFree(sl.d_bj);
+      (void)hipHostFree(sl.h_jobs);
+      (void)hipHostFree(sl.h_bj);
+      sl.d_jobs = sl.h_jobs = nullptr;
+      sl.d_bj = sl.h_bj = nullptr;
+      hipError_t e = hipMalloc(&sl.d_jobs, sizeof(GpuArgs) * nj);
+      if (e == hipSuccess) e = hipMalloc(&sl.d_bj, sizeof(uint16_t) * nbk);
+      if (e == hipSuccess) e = hipHostMalloc(&sl.h_jobs, sizeof(GpuArgs) * nj);
+      if (e == hipSuccess) e = hipHostMalloc(&sl.h_bj, sizeof(uint16_t) * nbk);
+      if (e != hipSuccess) {
+        sl.jobs_cap = sl.blocks_cap = 0;
+        return e;
+      }
+      sl.jobs_cap = nj;
+      sl.blocks_cap = nbk;
+    }
+    uint32_t b0 = 0;
+    for (size_t j = 0; j < njobs; ++j) {
+      GpuArgs a = take[j]->a;
+      a.block0 = b0;
+      sl.h_jobs[j] = a;
+      for (uint32_t i = 0; i < take[j]->nb; ++i) sl.h_bj[b0 + i] = (uint16_t)j;
+      b0 += take[j]->nb;
+    }
+    hipError_t e = hipMemcpyAsync(sl.d_jobs, sl.h_jobs, sizeof(GpuArgs) * njobs, hipMemcpyHostToDevice, sl.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(sl.d_bj, sl.h_bj, sizeof(uint16_t) * blocks, hipMemcpyHostToDevice, sl.stream);
+    for (size_t j = 0; j < njobs && e == hipSuccess; ++j) e = hipMemsetAsync(take[j]->a.ctl, 0, sizeof(GpuCtl), sl.stream);
+    if (e != hipSuccess) return e;
+    CuPool::get().acquire((int)slots);
+    hipLaunchKernelGGL(engine_batch_kernel, dim3(blocks), dim3(64), kLdsBytesGlobal, sl.stream,
+                       (const GpuArgs*)sl.d_jobs, (const uint16_t*)sl.d_bj);
+    e = hipGetLastError();
+    for (size_t j = 0; j < njobs; ++j) {
+      const hipError_t ce =
+          hipMemcpyAsync(take[j]->h_ctl, take[j]->a.ctl, sizeof(GpuCtl), hipMemcpyDeviceToHost, sl.stream);
+      if (e == hipSuccess) e = ce;
+    }
+    const hipError_t se = hipStreamSynchronize(sl.stream);
+    CuPool::get().release((int)slots);
+    return e != hipSuccess ? e : se;
+  }
+
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Sub*> pending_;
+  std::chrono::steady_clock::time_point first_;
+  int running_ = 0;    // batches in flight
+  int in_flight_ = 0;  // launches in those batches
+  int in_run_ = 0;
+  Slot slots_[kMaxBatches];
+  uint64_t batches_ = 0, jobs_ = 0;
+};
+
 class GpuEngine : public Engine {
  public:
   ~GpuEngine() override {
@@ -825,19 +617,20 @@ class GpuEngine : public Engine {
     // one block per unit while the units fit the CUs; larger configs (or a
     // smaller ASIM_GPU_BLOCKS cap) time-slice several units per block
     nblocks_ = c.n_sm + c.n_mem;
-    uint32_t cap = (uint32_t)n_cu_ * (gpu_state_global() ? kCuSlots : 1u);
+    uint32_t cap = (uint32_t)n_cu_ * (gpu_state_global() ? global_blocks_per_cu() : 1u);
     if (const char* eb = getenv("ASIM_GPU_BLOCKS"))
       if (atoi(eb) > 0) cap = std::min<uint32_t>(cap, (uint32_t)atoi(eb));
     if (nblocks_ > cap) nblocks_ = cap;
     global_ = gpu_state_global();
     lds_ = global_ ? kLdsBytesGlobal : kLdsBytes;
     sliced_ = nblocks_ < c.n_sm + c.n_mem;
-    for (const void* f : {(const void*)engine_kernel<WavePar, false>, (const void*)engine_kernel<WaveParProf, false>,
-                          (const void*)engine_kernel<WavePar, true>, (const void*)engine_kernel<WaveParProf, true>})
+    for (const void* f : {(const void*)engine_kernel<WavePar, false, false>, (const void*)engine_kernel<WaveParProf, false, false>,
+                          (const void*)engine_kernel<WavePar, true, false>, (const void*)engine_kernel<WaveParProf, true, false>})
       HIPCHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes));
     // every block of a simulation must be co-resident: a block takes the CU
     // slots (kCuSlots per CU) its LDS needs, one at least
-    slots_ = block_slots(lds_);
+    slots_ = engine_block_slots(global_);
+    batch_ = global_ && !profiling_env() && gpu_batch_on();
     if (cfg_slot_ < 0) cfg_slot_ = CfgSlots::get().acquire();
     const char* pe = getenv("ASIM_GPU_PROFILE");
     profiling_ = pe && *pe && *pe != '0';
@@ -926,6 +719,16 @@ class GpuEngine : public Engine {
       res.end_cycle = cycle_;
       return res;
     }
+    // batch mode: this simulation counts as one the batch leader waits for
+    struct InRun {
+      bool on;
+      explicit InRun(bool b) : on(b) {
+        if (on) BatchLauncher::get().enter();
+      }
+      ~InRun() {
+        if (on) BatchLauncher::get().leave();
+      }
+    } in_run(batch_);
     for (;;) {
       tw_.ensure(kt_, c_, [&](DispatchView& v) { read_dispatch(v); });
       HIPCHECK(hipMemcpy(d_kt_, &kt_, sizeof(KernelTab), hipMemcpyHostToDevice));
@@ -959,6 +762,18 @@ class GpuEngine : public Engine {
       a.prof = d_prof_;
       a.ework = d_ework_;
       a.pw = pw_on_ ? d_pw_ : nullptr;
+      if (batch_) {
+        // the launch joins the process's next batch (BatchLauncher)
+        a.max_epochs = std::min<uint32_t>(a.max_epochs, BatchLauncher::kBatchEpochs);
+        BatchLauncher::Sub sub;
+        sub.a = a;
+        sub.nb = nblocks_;
+        sub.slots = slots_;
+        sub.h_ctl = h_ctl_;
+        BatchLauncher::get().run(sub);
+        ++launches_;
+        HIPCHECK(sub.err);
+      } else {
       CuPool::get().acquire((int)(nblocks_ * slots_));
       hipError_t le;
       if (global_ && profiling_)
@@ -966,13 +781,13 @@ class GpuEngine : public Engine {
       else if (global_)
         hipLaunchKernelGGL((engine_kernel<WavePar, true, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else if (profiling_ && sliced_)
-        hipLaunchKernelGGL((engine_kernel<WaveParProf, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+        hipLaunchKernelGGL((engine_kernel<WaveParProf, true, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else if (profiling_)
-        hipLaunchKernelGGL((engine_kernel<WaveParProf, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+        hipLaunchKernelGGL((engine_kernel<WaveParProf, false, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else if (sliced_)
-        hipLaunchKernelGGL((engine_kernel<WavePar, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+        hipLaunchKernelGGL((engine_kernel<WavePar, true, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else
-        hipLaunchKernelGGL((engine_kernel<WavePar, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+        hipLaunchKernelGGL((engine_kernel<WavePar, false, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       le = hipGetLastError();
       ++launches_;
       hipError_t ce = hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_);
@@ -981,6 +796,7 @@ class GpuEngine : public Engine {
       HIPCHECK(le);
       HIPCHECK(ce);
       HIPCHECK(se);
+      }
       if (h_ctl_->error) throw std::runtime_error("GPU engine: grid barrier timed out (blocks not co-resident?)");
       epoch_ = h_ctl_->end_epoch;
       cycle_ = h_ctl_->end_cycle;
@@ -1251,8 +1067,9 @@ class GpuEngine : public Engine {
   // slot and the global copy (stream-ordered before the next launch)
   void upload_cfg() {
     HIPCHECK(hipMemcpy(d_cfg_, &c_, sizeof(SimCfg), hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_cfg), &c_, sizeof(SimCfg), sizeof(SimCfg) * (size_t)cfg_slot_,
-                               hipMemcpyHostToDevice));
+    HIPCHECK(engine_upload_cfg_lds(c_, cfg_slot_));
+    HIPCHECK(engine_upload_cfg_prof(c_, cfg_slot_));
+    HIPCHECK(engine_upload_cfg_global(c_, cfg_slot_));
   }
   void release() {
     auto fr = [](void* p) {
@@ -1339,6 +1156,7 @@ class GpuEngine : public Engine {
   bool profiling_ = false;
   bool sliced_ = false;  // more units than blocks: the time-slicing kernel
   bool global_ = false;  // ASIM_GPU_STATE=global: unit states stay in HBM (no LDS state)
+  bool batch_ = false;   // launches shared with the process's other global-state simulations (BatchLauncher)
   uint32_t slots_ = kCuSlots;  // CU slots one block of this engine takes
   uint64_t* d_prof_ = nullptr;
   uint32_t* d_ework_ = nullptr;
@@ -1452,14 +1270,26 @@ std::map<std::string, uint64_t> gpu_pool_stats() {
           {"cap_host", t.cap_host}, {"trims", t.trims}, {"freed_over_cap", t.freed_over_cap}};
 }
 void gpu_pool_trim() { DevicePool::get().trim(); }
+std::map<std::string, uint64_t> gpu_batch_stats() {
+  std::map<std::string, uint64_t> m{{"batches", BatchLauncher::get().batches()},
+                                     {"launches", BatchLauncher::get().jobs()},
+                                     {"blocks_per_cu", global_blocks_per_cu()},
+                                     {"occupancy_api", (uint64_t)g_occ_api}};
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, (const void*)engine_batch_kernel) == hipSuccess) {
+    m["num_regs"] = (uint64_t)fa.numRegs;
+    m["scratch_bytes_per_lane"] = (uint64_t)fa.localSizeBytes;
+  }
+  return m;
+}
 // CUs one simulation of this shape reserves on the GPU engine (the
 // concurrency of job-level parallelism on one GPU, multi_gpu.py)
 int gpu_cus_per_sim(uint32_t n_sm, uint32_t n_mem) {
   const bool g = gpu_state_global();
   uint32_t nb = n_sm + n_mem;
   const int cus = gpu_cu_count();
-  if (cus > 0) nb = std::min<uint32_t>(nb, (uint32_t)cus * (g ? kCuSlots : 1u));
-  const uint32_t slots = nb * block_slots(g ? kLdsBytesGlobal : kLdsBytes);
+  if (cus > 0) nb = std::min<uint32_t>(nb, (uint32_t)cus * (g ? global_blocks_per_cu() : 1u));
+  const uint32_t slots = nb * engine_block_slots(g);
   return (int)((slots + kCuSlots - 1) / kCuSlots);
 }
 int gpu_cu_count() {
@@ -1475,7 +1305,7 @@ namespace asim {
 EngineKernelInfo gpu_engine_kernel_info() {
   EngineKernelInfo k;
   hipFuncAttributes fa;
-  if (hipFuncGetAttributes(&fa, (const void*)engine_kernel<WavePar, false>) != hipSuccess) return k;
+  if (hipFuncGetAttributes(&fa, (const void*)engine_kernel<WavePar, false, false>) != hipSuccess) return k;
   k.num_regs = fa.numRegs;
   k.local_bytes = (int)fa.localSizeBytes;
   k.shared_static = (int)fa.sharedSizeBytes;

@@ -11,6 +11,7 @@ int gpu_cu_count() { return 0; }
 int gpu_cus_per_sim(uint32_t n_sm, uint32_t n_mem) { return (int)(n_sm + n_mem); }
 std::map<std::string, uint64_t> gpu_pool_stats() { return {}; }
 void gpu_pool_trim() {}
+std::map<std::string, uint64_t> gpu_batch_stats() { return {}; }
 EngineKernelInfo gpu_engine_kernel_info() { return EngineKernelInfo{}; }
 }  // namespace asim
 

@@ -29,10 +29,11 @@ struct GpuCtl {  // zeroed by hipMemsetAsync before every launch
 // and each block polls only its own group's word (relaxed, with s_sleep), so
 // no single line is hammered by every block while the arrivals queue behind
 // it.  One agent release before arriving and one agent acquire after leaving.
+// `b`: the block's index among the `nblocks` that synchronise (blockIdx.x
+// for a whole launch; a batch launch's simulation numbers its own blocks)
 template <bool kFence = true>
-__device__ __forceinline__ bool grid_barrier(GpuCtl* ctl, uint32_t nblocks, uint32_t epoch_in_launch,
-                                             uint32_t* was_last = nullptr) {
-  const uint32_t b = blockIdx.x;
+__device__ __forceinline__ bool grid_barrier_b(GpuCtl* ctl, uint32_t b, uint32_t nblocks, uint32_t epoch_in_launch,
+                                               uint32_t* was_last = nullptr) {
   const uint32_t grp = b & 7u;
   const uint32_t ngrp = nblocks < 8 ? nblocks : 8u;
   const uint32_t in_grp = (nblocks - grp + 7u) / 8u;  // members of this group
@@ -72,6 +73,11 @@ __device__ __forceinline__ bool grid_barrier(GpuCtl* ctl, uint32_t nblocks, uint
   if (kFence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   return ok;
+}
+template <bool kFence = true>
+__device__ __forceinline__ bool grid_barrier(GpuCtl* ctl, uint32_t nblocks, uint32_t epoch_in_launch,
+                                             uint32_t* was_last = nullptr) {
+  return grid_barrier_b<kFence>(ctl, blockIdx.x, nblocks, epoch_in_launch, was_last);
 }
 
 }  // namespace asim

@@ -14,4 +14,4 @@ rc=$?
 echo "pytest rc=$rc" | tee -a gpurun_out/r4_hoststream.log
 tail -8 gpurun_out/r4_hoststream.log
 [ $rc -eq 0 ] || exit $rc
-bash tools/gpu_r4_rccl.sh
+bash tools/archive/gpu_r4_rccl.sh

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5 engine A/B: GPU-engine sim seconds per app (stage profiler off),
 # then the GPU == CPU bit-exactness tier of the engine.
-# usage: TAG=name [APPS="bfs ..."] [TESTS=1] bash tools/gpu_r5_ab.sh
+# usage: TAG=name [APPS="bfs ..."] [TESTS=1] bash tools/archive/gpu_r5_ab.sh
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/r5ab/${TAG:-run}

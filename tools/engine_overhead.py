@@ -2,7 +2,7 @@
 """Where a short-kernel application's time goes on the GPU engine: wall time
 of the whole simulation vs the simulator's own phases, per app (GV100 preset,
 the bench suite's synthetic traces).  Run under rocprofv3 --kernel-trace
---stats to split device time from host time (tools/gpu_r5_overhead.sh)."""
+--stats to split device time from host time (tools/archive/gpu_r5_overhead.sh)."""
 import os
 import sys
 import time

@@ -29,6 +29,62 @@ step_state() {
     python3 -c "import json,sys; d=json.load(open('$O/bench_gpu_$mode.json')); print('$mode', d['value'], d['ms_per_step'])"
   done
 }
+step_batch() {
+  ASIM_GPU_STATE=global timeout -k 10 600 $PT tests/test_gpu_engine.py -k "global_state or batch or pool or resources" \
+    > $O/pytest_batch.log 2>&1 || { tail -30 $O/pytest_batch.log; return 1; }
+  tail -3 $O/pytest_batch.log
+  for mode in lds global; do
+    ASIM_GPU_STATE=$mode timeout -k 10 600 python3 bench.py --sweep --engine gpu --steps 1 --warmup 0 \
+      > $O/sweep_gpu_$mode.json 2> $O/sweep_gpu_$mode.err || { tail $O/sweep_gpu_$mode.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/sweep_gpu_$mode.json')); print('sweep $mode', d['value'], d['ms_per_step'], d['config'].get('gpu_slots'))"
+  done
+  ASIM_GPU_STATE=global timeout -k 10 300 python3 bench.py --engine gpu --steps 2 --warmup 1 \
+    > $O/bench_gpu_global_batch.json 2> $O/bench_gpu_global_batch.err || { tail $O/bench_gpu_global_batch.err; return 1; }
+  python3 -c "import json; d=json.load(open('$O/bench_gpu_global_batch.json')); print('gpu global batch', d['value'], d['ms_per_step'])"
+}
+step_scaling() {
+  for st in lds global; do
+    for app in hotspot bfs; do
+      ASIM_GPU_STATE=$st timeout -k 10 300 python3 tools/batch_scaling.py --app $app --n ${NS:-1,2,3,4,6} \
+        2>&1 | grep -v amdgpu.ids >> $O/scaling.jsonl || return 1
+    done
+  done
+  cat $O/scaling.jsonl
+}
+step_scaling2() {
+  # global-state batch launches with the concurrent-batch launcher, 3 and 4 blocks per CU
+  for bpc in ${BPCS:-2 3}; do
+    for app in hotspot bfs; do
+      ASIM_GPU_BLOCKS_PER_CU=$bpc ASIM_GPU_STATE=global timeout -k 10 300 python3 tools/batch_scaling.py --app $app \
+        --n ${NS:-1,2,4,6,8} 2>&1 | grep -v amdgpu.ids | sed "s/^{/{\"bpc\": $bpc, /" >> $O/scaling2.jsonl || return 1
+    done
+  done
+  cat $O/scaling2.jsonl
+}
+step_sweep_global() {
+  for bpc in ${BPCS:-2 3}; do
+    ASIM_GPU_BLOCKS_PER_CU=$bpc ASIM_GPU_STATE=global timeout -k 10 300 python3 bench.py --sweep --engine gpu --steps 1 \
+      --warmup 0 > $O/sweep_gpu_global_bpc$bpc.json 2> $O/sweep_gpu_global_bpc$bpc.err || { tail -3 $O/sweep_gpu_global_bpc$bpc.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/sweep_gpu_global_bpc$bpc.json')); print('sweep global bpc $bpc', d['value'], d['ms_per_step'], d['config'].get('gpu_slots'))"
+  done
+}
+step_pmc_scaling() {
+  # L2 hit rate of the global-state engine with 1 and 4 simulations at once
+  for n in 1 4; do
+    ASIM_GPU_STATE=global timeout -s KILL 120 rocprofv3 --kernel-trace --stats \
+      --pmc TCC_HIT_sum TCC_MISS_sum SQ_WAVE_CYCLES SQ_WAIT_ANY -d $O/pmc_n$n -o pmc -- \
+      python3 tools/batch_scaling.py --app hotspot --n $n > $O/pmc_n$n.log 2>&1 || { tail $O/pmc_n$n.log; return 1; }
+    db=$(find $O/pmc_n$n -name "*.db" | head -1)
+    python3 tools/pmc_summary.py "$db" engine_batch_kernel > $O/pmc_n$n.json && cat $O/pmc_n$n.json
+  done
+}
+step_diag() {
+  ASIM_GPU_STATE=global timeout -k 10 120 python3 -c "
+import torch, sys; sys.path.insert(0, '.')
+from accel_sim_framework_distributed_amd import _native
+m = _native.load(prefer_torch_runtime=True); print(m.gpu_batch_stats(), m.gpu_cus_per_sim(80, 32), m.gpu_cu_count())" \
+    2>&1 | grep -v amdgpu.ids
+}
 step_tests() {
   timeout -k 10 1000 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; return 1; }
   tail -3 $O/pytest_gpu.log

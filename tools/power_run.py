@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One suite application with AccelWattch power sampling on the GPU engine
 (in-kernel sampler by default): the run profiled for engine_kernel's MFMA
-counters (tools/gpu_r4_batch3.sh)."""
+counters (tools/archive/gpu_r4_batch3.sh)."""
 import argparse
 import os
 import sys

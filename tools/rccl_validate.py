@@ -12,7 +12,7 @@ moves the payload; profiles/rccl_trace/dispatches.csv).  With
 over ``-collective_max_channels`` workgroups.  This script
 
 1. reads the rocprofv3 counters of every ``copyBuffer`` dispatch of the
-   example (tools/gpu_r4_rccl.sh: SQ_INSTS_*, SQ_WAVES, TCC_REQ / TCC_HIT /
+   example (tools/archive/gpu_r4_rccl.sh: SQ_INSTS_*, SQ_WAVES, TCC_REQ / TCC_HIT /
    TCC_EA0_RDREQ / TCC_EA0_WRREQ);
 2. simulates the stand-in for the same bytes with the tuned MI355X config
    (a 2-rank all-reduce command moves 2(n-1)/n x S = S bytes each way, the
