@@ -88,6 +88,8 @@ m = _native.load(prefer_torch_runtime=True); print(m.gpu_batch_stats(), m.gpu_cu
 step_tests() {
   timeout -k 10 1000 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; return 1; }
   tail -3 $O/pytest_gpu.log
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; return 1; }
+  tail -1 $O/smoke.log
 }
 step_bench() {
   timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 > $O/bench_node.json 2> $O/bench_node.err || { tail $O/bench_node.err; return 1; }
