@@ -177,6 +177,7 @@ PYBIND11_MODULE(_asim, m) {
   }
   m.def("gpu_cu_count", &gpu_cu_count, "compute units of the current HIP device");
   m.def("gpu_pool_stats", &gpu_pool_stats, "GPU engine caching allocator: cached bytes, caps, trims");
+  m.def("gpu_engine_modes", &gpu_engine_modes, "per GPU-engine build (lds / global / split): LDS bytes, blocks per CU, registers");
   m.def("gpu_batch_stats", &gpu_batch_stats, "global-state batch launches: batches, launches, blocks per CU");
   m.def("gpu_pool_trim", &gpu_pool_trim, "give the GPU engine allocator's cached blocks back to the driver");
   m.def("gpu_cus_per_sim", &gpu_cus_per_sim, "CUs one GPU-engine simulation of this shape reserves (ASIM_GPU_STATE)");

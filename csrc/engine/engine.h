@@ -199,7 +199,8 @@ int gpu_cu_count();  // compute units of the current HIP device (0 if none)
 int gpu_cus_per_sim(uint32_t n_sm, uint32_t n_mem);  // CUs one GPU-engine simulation of this shape reserves
 std::map<std::string, uint64_t> gpu_pool_stats();  // the GPU engine's caching allocator (empty without HIP)
 void gpu_pool_trim();  // give the allocator's cached blocks back to the driver
-std::map<std::string, uint64_t> gpu_batch_stats();  // global-state batch launches: batches, launches, blocks per CU
+std::map<std::string, uint64_t> gpu_batch_stats();
+std::map<std::string, std::map<std::string, uint64_t>> gpu_engine_modes();  // per engine build: LDS, blocks per CU, registers  // global-state batch launches: batches, launches, blocks per CU
 // compiled resources of the persistent engine kernel (empty if no HIP build):
 // registers, scratch, static LDS, plus the dynamic LDS the engine requests
 struct EngineKernelInfo {

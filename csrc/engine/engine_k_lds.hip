@@ -4,8 +4,8 @@
 
 namespace asim {
 
-template __global__ void engine_kernel<WavePar, false, false>(GpuArgs);
-template __global__ void engine_kernel<WavePar, true, false>(GpuArgs);
+template __global__ void engine_kernel<WavePar, false, kModeLds>(GpuArgs);
+template __global__ void engine_kernel<WavePar, true, kModeLds>(GpuArgs);
 
 ASIM_ENGINE_CFG_UPLOAD(lds)
 

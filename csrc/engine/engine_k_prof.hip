@@ -4,9 +4,10 @@
 
 namespace asim {
 
-template __global__ void engine_kernel<WaveParProf, false, false>(GpuArgs);
-template __global__ void engine_kernel<WaveParProf, true, false>(GpuArgs);
-template __global__ void engine_kernel<WaveParProf, true, true>(GpuArgs);
+template __global__ void engine_kernel<WaveParProf, false, kModeLds>(GpuArgs);
+template __global__ void engine_kernel<WaveParProf, true, kModeLds>(GpuArgs);
+template __global__ void engine_kernel<WaveParProf, true, kModeGlobal>(GpuArgs);
+template __global__ void engine_kernel<WaveParProf, true, kModeSplit>(GpuArgs);
 
 ASIM_ENGINE_CFG_UPLOAD(prof)
 

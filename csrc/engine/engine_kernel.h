@@ -24,6 +24,7 @@
 #include "engine.h"
 #include "grid_barrier.h"
 #include "wave_par.h"
+#include "sm_split.h"
 
 namespace asim {
 
@@ -134,6 +135,16 @@ __device__ __forceinline__ void swap_out(T* dst, const T* lds) {
   __syncthreads();
 }
 
+// the first `bytes` (a multiple of 16) of a state, HBM <-> LDS (split-state
+// build: the SM's hot prefix)
+__device__ __forceinline__ void copy_bytes(void* dst, const void* src, size_t bytes) {
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  const int n = (int)(bytes / 16);
+  for (int i = (int)(threadIdx.x & 63); i < n; i += 64) d[i] = s[i];
+  __syncthreads();
+}
+
 extern __shared__ __attribute__((aligned(16))) char g_lds[];
 // Block LDS layout: the kernel table, the stage profiler and the power
 // evaluator's scratch first (a few KB), then -- in the LDS-state build -- the
@@ -155,6 +166,13 @@ constexpr size_t kStateOff = (kPwrOff + 2 * kPwrSumPad * sizeof(double) + 15) / 
 constexpr size_t kStateLds = ((sizeof(SMState) > sizeof(ChanState) ? sizeof(SMState) : sizeof(ChanState)) + 15) / 16 * 16;
 constexpr size_t kLdsBytes = kStateOff + kStateLds;
 constexpr size_t kLdsBytesGlobal = kStateOff;
+constexpr size_t kLdsBytesSplit = kStateOff + kSmHotBytes;
+// engine builds: the unit state's home during a launch
+enum EngineMode : int {
+  kModeLds = 0,     // whole unit state in LDS (one block per CU)
+  kModeGlobal = 1,  // every unit in place in HBM
+  kModeSplit = 2,   // SM: hot prefix in LDS, geometry-sized arrays in HBM (SmSplit); channels in place in HBM
+};
 static_assert(kLdsBytes <= 160 * 1024, "per-block LDS budget exceeded");
 
 // a pointer the compiler may treat as global memory (address space 1): the
@@ -255,8 +273,9 @@ __device__ void pwr_evaluate(PwrDev& pw, uint32_t nunits, uint64_t now) {
 
 // the kernel body for block `b` of the simulation `a` (b = blockIdx.x for a
 // single simulation; a batch launch maps its blocks onto several)
-template <class P, bool kSliced, bool kGlobal>
+template <class P, bool kSliced, int kMode>
 __device__ __forceinline__ void engine_body(const GpuArgs& a, const uint32_t b) {
+  constexpr bool kGlobal = kMode == kModeGlobal, kSplit = kMode == kModeSplit;
   // The configuration is read all over the model, much of it at lane-varying
   // indices (address-decoder bit runs, per-unit counts, cache geometries
   // selected per warp): constant memory, one slot per engine (g_cfg above).
@@ -271,6 +290,8 @@ __device__ __forceinline__ void engine_body(const GpuArgs& a, const uint32_t b) 
   // Global-state build (kGlobal): every unit is simulated in place in its HBM
   // image (vector-L1 / L2 resident while its block works on it), the block
   // holds no state in LDS and several engine waves share each CU.
+  // Split-state build (kSplit): an SM's hot prefix is in LDS (swapped like a
+  // whole state when time-sliced), its tail and every channel in HBM.
   SMState* s = reinterpret_cast<SMState*>(g_lds + kStateOff);
   ChanState* ch = reinterpret_cast<ChanState*>(g_lds + kStateOff);
   const uint32_t nunits = c.n_sm + c.n_mem;
@@ -281,10 +302,23 @@ __device__ __forceinline__ void engine_body(const GpuArgs& a, const uint32_t b) 
     if (u < c.n_sm) s = as_global(&a.sms[u]);
     else ch = as_global(&a.chs[u - c.n_sm]);
   };
+  uint32_t hot = b;  // split build: the SM whose hot prefix is in LDS (~0u: none)
   auto swap_to = [&](uint32_t u) {
     if (kGlobal) {
       bind(u);
       loaded = u;
+      return;
+    }
+    if (kSplit) {
+      loaded = u;
+      if (u >= c.n_sm) {
+        ch = as_global(&a.chs[u - c.n_sm]);
+        return;
+      }
+      if (u == hot) return;
+      if (hot < c.n_sm) copy_bytes(&a.sms[hot], s, kSmHotBytes);
+      copy_bytes(s, &a.sms[u], kSmHotBytes);
+      hot = u;
       return;
     }
     if (!kSliced || u == loaded) return;
@@ -296,7 +330,12 @@ __device__ __forceinline__ void engine_body(const GpuArgs& a, const uint32_t b) 
   };
   if (kGlobal)
     bind(b);
-  else if (b < c.n_sm)
+  else if (kSplit && b < c.n_sm)
+    copy_bytes(s, &a.sms[b], kSmHotBytes);
+  else if (kSplit) {
+    hot = ~0u;
+    ch = as_global(&a.chs[b - c.n_sm]);
+  } else if (b < c.n_sm)
     copy_state(s, &a.sms[b]);
   else
     copy_state(ch, &a.chs[b - c.n_sm]);
@@ -354,9 +393,16 @@ __device__ __forceinline__ void engine_body(const GpuArgs& a, const uint32_t b) 
       if (u < c.n_sm) {
         sx.outbox = a.box_req[cur];
         sx.outcnt = a.cnt_req[cur];
-        sm_epoch<P>(*s, sx, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep,
-                    c.n_subpart, epoch, repm);
-        sm_publish<P>(*s, sx, *a.pub, cur);
+        if constexpr (kSplit) {
+          SmSplit sp(*s, *as_global(&a.sms[u]));
+          sm_epoch<P>(sp, sx, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep, c.n_subpart, epoch,
+                      repm);
+          sm_publish<P>(sp, sx, *a.pub, cur);
+        } else {
+          sm_epoch<P>(*s, sx, *a.pub, prev, t0, t1, a.box_rep[prev], a.cnt_rep[prev], a.cap_rep,
+                      c.n_subpart, epoch, repm);
+          sm_publish<P>(*s, sx, *a.pub, cur);
+        }
       } else {
         mx.outbox = a.box_rep[cur];
         mx.outcnt = a.cnt_rep[cur];
@@ -425,8 +471,8 @@ __device__ __forceinline__ void engine_body(const GpuArgs& a, const uint32_t b) 
         for (uint32_t k = 0; k < nmine; ++k) {
           const uint32_t u = unit_k(k);
           double* row = a.pw->rows + (size_t)u * kPwrRawPad;
-          if (u < c.n_sm) pwr_row_sm(row, (!kGlobal && u == loaded) ? s->st : a.sms[u].st);
-          else pwr_row_ch(row, (!kGlobal && u == loaded) ? *ch : a.chs[u - c.n_sm], c.n_sub_per_mem);
+          if (u < c.n_sm) pwr_row_sm(row, (!kGlobal && u == (kSplit ? hot : loaded)) ? s->st : a.sms[u].st);
+          else pwr_row_ch(row, (!kGlobal && !kSplit && u == loaded) ? *ch : a.chs[u - c.n_sm], c.n_sub_per_mem);
         }
         if (!grid_barrier_b(a.ctl, b, a.nblocks, nbar++)) { failed = true; break; }
         if (b == a.nblocks - 1) pwr_evaluate(*a.pw, nunits, cycle);
@@ -443,7 +489,9 @@ __device__ __forceinline__ void engine_body(const GpuArgs& a, const uint32_t b) 
   // write the resident state back
   if (kGlobal)
     ;
-  else if (loaded < c.n_sm)
+  else if (kSplit) {
+    if (hot < c.n_sm) copy_bytes(&a.sms[hot], s, kSmHotBytes);
+  } else if (loaded < c.n_sm)
     copy_state(&a.sms[loaded], s);
   else
     copy_state(&a.chs[loaded - c.n_sm], ch);
@@ -468,9 +516,9 @@ __device__ __forceinline__ void engine_body(const GpuArgs& a, const uint32_t b) 
 // scratch memory.
 #define ASIM_ENGINE_KERNEL_ATTRS __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 
-template <class P, bool kSliced, bool kGlobal>
+template <class P, bool kSliced, int kMode>
 __global__ void ASIM_ENGINE_KERNEL_ATTRS engine_kernel(GpuArgs a) {
-  engine_body<P, kSliced, kGlobal>(a, blockIdx.x);
+  engine_body<P, kSliced, kMode>(a, blockIdx.x);
 }
 
 // Many simulations in one launch (global-state build): block i runs block
@@ -481,6 +529,9 @@ __global__ void ASIM_ENGINE_KERNEL_ATTRS engine_kernel(GpuArgs a) {
 // kernels (GPU_MAX_HW_QUEUES).
 __global__ void ASIM_ENGINE_KERNEL_ATTRS engine_batch_kernel(const GpuArgs* __restrict__ jobs,
                                                              const uint16_t* __restrict__ block_job);
+// the same for the split-state build
+__global__ void ASIM_ENGINE_KERNEL_ATTRS engine_batch_split_kernel(const GpuArgs* __restrict__ jobs,
+                                                                   const uint16_t* __restrict__ block_job);
 
 // the kernel TUs' configuration uploads (one per TU: its own g_cfg)
 #define ASIM_ENGINE_CFG_UPLOAD(name)                                                         \

@@ -48,15 +48,18 @@ namespace asim {
   } while (0)
 
 // builds of engine_kernel, instantiated in the kernel TUs (engine_k_*.hip)
-extern template __global__ void engine_kernel<WavePar, false, false>(GpuArgs);
-extern template __global__ void engine_kernel<WavePar, true, false>(GpuArgs);
-extern template __global__ void engine_kernel<WaveParProf, false, false>(GpuArgs);
-extern template __global__ void engine_kernel<WaveParProf, true, false>(GpuArgs);
-extern template __global__ void engine_kernel<WavePar, true, true>(GpuArgs);
-extern template __global__ void engine_kernel<WaveParProf, true, true>(GpuArgs);
+extern template __global__ void engine_kernel<WavePar, false, kModeLds>(GpuArgs);
+extern template __global__ void engine_kernel<WavePar, true, kModeLds>(GpuArgs);
+extern template __global__ void engine_kernel<WaveParProf, false, kModeLds>(GpuArgs);
+extern template __global__ void engine_kernel<WaveParProf, true, kModeLds>(GpuArgs);
+extern template __global__ void engine_kernel<WavePar, true, kModeGlobal>(GpuArgs);
+extern template __global__ void engine_kernel<WaveParProf, true, kModeGlobal>(GpuArgs);
+extern template __global__ void engine_kernel<WavePar, true, kModeSplit>(GpuArgs);
+extern template __global__ void engine_kernel<WaveParProf, true, kModeSplit>(GpuArgs);
 hipError_t engine_upload_cfg_lds(const SimCfg& c, int slot);
 hipError_t engine_upload_cfg_prof(const SimCfg& c, int slot);
 hipError_t engine_upload_cfg_global(const SimCfg& c, int slot);
+hipError_t engine_upload_cfg_split(const SimCfg& c, int slot);
 
 namespace {
 
@@ -143,31 +146,37 @@ uint32_t block_slots(size_t lds) {
   const size_t per_cu = lds ? (160 * 1024) / lds : kMaxBlocksPerCu;  // blocks whose LDS fits one CU
   return kCuSlots / (uint32_t)std::max<size_t>(1, std::min<size_t>(per_cu, kMaxBlocksPerCu));
 }
-bool gpu_state_global() {
+// ASIM_GPU_STATE: lds (default) | global | split (engine_kernel.h EngineMode)
+int gpu_state_mode() {
   const char* e = getenv("ASIM_GPU_STATE");
-  return e && std::string(e) == "global";
+  if (!e) return kModeLds;
+  const std::string v(e);
+  return v == "global" ? kModeGlobal : v == "split" ? kModeSplit : kModeLds;
 }
-int g_occ_api = 0;  // the occupancy API's blocks per CU of the batch kernel (diagnostics)
-// global-state blocks per CU (cached; needs a current device)
-uint32_t global_blocks_per_cu() {
-  static std::once_flag once;
-  static uint32_t bpc = 1;
-  std::call_once(once, [] {
+bool gpu_state_global() { return gpu_state_mode() == kModeGlobal; }
+int g_occ_api = 0;  // the occupancy API's blocks per CU of the last mode asked (diagnostics)
+// blocks of one mode's kernel per CU (cached per mode; needs a current device)
+uint32_t mode_blocks_per_cu(int mode) {
+  if (mode == kModeLds) return 1;
+  static std::mutex mu;
+  static uint32_t cache[3] = {0, 0, 0};
+  std::lock_guard<std::mutex> g(mu);
+  if (!cache[mode]) {
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)engine_batch_kernel, 64, kLdsBytesGlobal) !=
-        hipSuccess)
-      occ = 2;
+    const void* f = mode == kModeGlobal ? (const void*)engine_batch_kernel
+                                        : (const void*)engine_kernel<WavePar, true, kModeSplit>;
+    const size_t lds = mode == kModeGlobal ? kLdsBytesGlobal : kLdsBytesSplit;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, 64, (int)lds) != hipSuccess) occ = 2;
     g_occ_api = occ;
     occ = occ > 1 ? occ - 1 : 1;
     if (const char* e = getenv("ASIM_GPU_BLOCKS_PER_CU"))  // measured override (co-residency tests)
       if (atoi(e) > 0) occ = atoi(e);
-    bpc = (uint32_t)std::min<int>(occ, (int)kMaxBlocksPerCu);
-  });
-  return bpc;
+    cache[mode] = (uint32_t)std::min<int>(occ, (int)kMaxBlocksPerCu);
+  }
+  return cache[mode];
 }
-uint32_t engine_block_slots(bool global) {
-  return global ? kCuSlots / global_blocks_per_cu() : block_slots(kLdsBytes);
-}
+uint32_t global_blocks_per_cu() { return mode_blocks_per_cu(kModeGlobal); }
+uint32_t engine_block_slots(int mode) { return kCuSlots / mode_blocks_per_cu(mode); }
 bool profiling_env() {
   const char* pe = getenv("ASIM_GPU_PROFILE");
   return pe && *pe && *pe != '0';
@@ -443,6 +452,7 @@ class BatchLauncher {
   }
   struct Sub {
     GpuArgs a;
+    int mode = kModeGlobal;  // kModeGlobal or kModeSplit: a batch holds one build
     uint32_t nb = 0, slots = 0;
     GpuCtl* h_ctl = nullptr;
     bool done = false;
@@ -503,18 +513,23 @@ class BatchLauncher {
     const uint32_t cap = (uint32_t)CuPool::get().capacity();
     std::vector<Sub*> take;
     uint32_t slots = 0, blocks = 0;
-    while (!pending_.empty()) {
-      Sub* x = pending_.front();
+    const int mode = pending_.front()->mode;
+    for (auto it = pending_.begin(); it != pending_.end();) {
+      Sub* x = *it;
+      if (x->mode != mode) {
+        ++it;
+        continue;
+      }
       if (!take.empty() && (slots + x->nb * x->slots > cap || blocks + x->nb > 65535u)) break;
       take.push_back(x);
       slots += x->nb * x->slots;
       blocks += x->nb;
-      pending_.pop_front();
+      it = pending_.erase(it);
     }
     in_flight_ += (int)take.size();
     if (!pending_.empty()) first_ = std::chrono::steady_clock::now();
     g.unlock();
-    hipError_t err = launch(*sl, take, blocks, slots);
+    hipError_t err = launch(*sl, take, blocks, slots, mode);
     g.lock();
     for (Sub* x : take) {
       x->err = err;
@@ -531,7 +546,7 @@ class BatchLauncher {
     if (!pending_.empty()) first_ = std::chrono::steady_clock::now();
     cv_.notify_all();
   }
-  hipError_t launch(Slot& sl, std::vector<Sub*>& take, uint32_t blocks, uint32_t slots) {
+  hipError_t launch(Slot& sl, std::vector<Sub*>& take, uint32_t blocks, uint32_t slots, int mode) {
     if (!sl.stream) {
       if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) return hipErrorOutOfMemory;
     }
@@ -568,8 +583,12 @@ class BatchLauncher {
     for (size_t j = 0; j < njobs && e == hipSuccess; ++j) e = hipMemsetAsync(take[j]->a.ctl, 0, sizeof(GpuCtl), sl.stream);
     if (e != hipSuccess) return e;
     CuPool::get().acquire((int)slots);
-    hipLaunchKernelGGL(engine_batch_kernel, dim3(blocks), dim3(64), kLdsBytesGlobal, sl.stream,
-                       (const GpuArgs*)sl.d_jobs, (const uint16_t*)sl.d_bj);
+    if (mode == kModeSplit)
+      hipLaunchKernelGGL(engine_batch_split_kernel, dim3(blocks), dim3(64), kLdsBytesSplit, sl.stream,
+                         (const GpuArgs*)sl.d_jobs, (const uint16_t*)sl.d_bj);
+    else
+      hipLaunchKernelGGL(engine_batch_kernel, dim3(blocks), dim3(64), kLdsBytesGlobal, sl.stream,
+                         (const GpuArgs*)sl.d_jobs, (const uint16_t*)sl.d_bj);
     e = hipGetLastError();
     for (size_t j = 0; j < njobs; ++j) {
       const hipError_t ce =
@@ -617,20 +636,21 @@ class GpuEngine : public Engine {
     // one block per unit while the units fit the CUs; larger configs (or a
     // smaller ASIM_GPU_BLOCKS cap) time-slice several units per block
     nblocks_ = c.n_sm + c.n_mem;
-    uint32_t cap = (uint32_t)n_cu_ * (gpu_state_global() ? global_blocks_per_cu() : 1u);
+    mode_ = gpu_state_mode();
+    uint32_t cap = (uint32_t)n_cu_ * mode_blocks_per_cu(mode_);
     if (const char* eb = getenv("ASIM_GPU_BLOCKS"))
       if (atoi(eb) > 0) cap = std::min<uint32_t>(cap, (uint32_t)atoi(eb));
     if (nblocks_ > cap) nblocks_ = cap;
-    global_ = gpu_state_global();
-    lds_ = global_ ? kLdsBytesGlobal : kLdsBytes;
+    global_ = mode_ == kModeGlobal;
+    lds_ = global_ ? kLdsBytesGlobal : mode_ == kModeSplit ? kLdsBytesSplit : kLdsBytes;
     sliced_ = nblocks_ < c.n_sm + c.n_mem;
-    for (const void* f : {(const void*)engine_kernel<WavePar, false, false>, (const void*)engine_kernel<WaveParProf, false, false>,
-                          (const void*)engine_kernel<WavePar, true, false>, (const void*)engine_kernel<WaveParProf, true, false>})
+    for (const void* f : {(const void*)engine_kernel<WavePar, false, kModeLds>, (const void*)engine_kernel<WaveParProf, false, kModeLds>,
+                          (const void*)engine_kernel<WavePar, true, kModeLds>, (const void*)engine_kernel<WaveParProf, true, kModeLds>})
       HIPCHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes));
     // every block of a simulation must be co-resident: a block takes the CU
     // slots (kCuSlots per CU) its LDS needs, one at least
-    slots_ = engine_block_slots(global_);
-    batch_ = global_ && !profiling_env() && gpu_batch_on();
+    slots_ = engine_block_slots(mode_);
+    batch_ = (global_ || mode_ == kModeSplit) && !profiling_env() && gpu_batch_on();
     if (cfg_slot_ < 0) cfg_slot_ = CfgSlots::get().acquire();
     const char* pe = getenv("ASIM_GPU_PROFILE");
     profiling_ = pe && *pe && *pe != '0';
@@ -767,6 +787,7 @@ class GpuEngine : public Engine {
         a.max_epochs = std::min<uint32_t>(a.max_epochs, BatchLauncher::kBatchEpochs);
         BatchLauncher::Sub sub;
         sub.a = a;
+        sub.mode = mode_;
         sub.nb = nblocks_;
         sub.slots = slots_;
         sub.h_ctl = h_ctl_;
@@ -776,18 +797,22 @@ class GpuEngine : public Engine {
       } else {
       CuPool::get().acquire((int)(nblocks_ * slots_));
       hipError_t le;
-      if (global_ && profiling_)
-        hipLaunchKernelGGL((engine_kernel<WaveParProf, true, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      if (mode_ == kModeSplit && profiling_)
+        hipLaunchKernelGGL((engine_kernel<WaveParProf, true, kModeSplit>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      else if (mode_ == kModeSplit)
+        hipLaunchKernelGGL((engine_kernel<WavePar, true, kModeSplit>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      else if (global_ && profiling_)
+        hipLaunchKernelGGL((engine_kernel<WaveParProf, true, kModeGlobal>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else if (global_)
-        hipLaunchKernelGGL((engine_kernel<WavePar, true, true>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+        hipLaunchKernelGGL((engine_kernel<WavePar, true, kModeGlobal>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else if (profiling_ && sliced_)
-        hipLaunchKernelGGL((engine_kernel<WaveParProf, true, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+        hipLaunchKernelGGL((engine_kernel<WaveParProf, true, kModeLds>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else if (profiling_)
-        hipLaunchKernelGGL((engine_kernel<WaveParProf, false, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+        hipLaunchKernelGGL((engine_kernel<WaveParProf, false, kModeLds>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else if (sliced_)
-        hipLaunchKernelGGL((engine_kernel<WavePar, true, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+        hipLaunchKernelGGL((engine_kernel<WavePar, true, kModeLds>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else
-        hipLaunchKernelGGL((engine_kernel<WavePar, false, false>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+        hipLaunchKernelGGL((engine_kernel<WavePar, false, kModeLds>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       le = hipGetLastError();
       ++launches_;
       hipError_t ce = hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_);
@@ -1070,6 +1095,7 @@ class GpuEngine : public Engine {
     HIPCHECK(engine_upload_cfg_lds(c_, cfg_slot_));
     HIPCHECK(engine_upload_cfg_prof(c_, cfg_slot_));
     HIPCHECK(engine_upload_cfg_global(c_, cfg_slot_));
+    HIPCHECK(engine_upload_cfg_split(c_, cfg_slot_));
   }
   void release() {
     auto fr = [](void* p) {
@@ -1155,6 +1181,7 @@ class GpuEngine : public Engine {
   uint32_t epochs_per_launch_ = 4096;
   bool profiling_ = false;
   bool sliced_ = false;  // more units than blocks: the time-slicing kernel
+  int mode_ = kModeLds;  // ASIM_GPU_STATE (EngineMode)
   bool global_ = false;  // ASIM_GPU_STATE=global: unit states stay in HBM (no LDS state)
   bool batch_ = false;   // launches shared with the process's other global-state simulations (BatchLauncher)
   uint32_t slots_ = kCuSlots;  // CU slots one block of this engine takes
@@ -1270,6 +1297,35 @@ std::map<std::string, uint64_t> gpu_pool_stats() {
           {"cap_host", t.cap_host}, {"trims", t.trims}, {"freed_over_cap", t.freed_over_cap}};
 }
 void gpu_pool_trim() { DevicePool::get().trim(); }
+// per engine build: LDS bytes per block, blocks per CU (occupancy API less
+// the margin), registers and scratch of its kernel
+std::map<std::string, std::map<std::string, uint64_t>> gpu_engine_modes() {
+  std::map<std::string, std::map<std::string, uint64_t>> out;
+  const struct {
+    const char* name;
+    int mode;
+    const void* f;
+    size_t lds;
+  } ms[] = {{"lds", kModeLds, (const void*)engine_kernel<WavePar, false, kModeLds>, kLdsBytes},
+            {"global", kModeGlobal, (const void*)engine_batch_kernel, kLdsBytesGlobal},
+            {"split", kModeSplit, (const void*)engine_kernel<WavePar, true, kModeSplit>, kLdsBytesSplit}};
+  for (const auto& m : ms) {
+    auto& o = out[m.name];
+    o["lds_bytes"] = m.lds;
+    o["blocks_per_cu"] = mode_blocks_per_cu(m.mode);
+    int occ = 0;
+    if (m.mode == kModeLds) (void)hipFuncSetAttribute(m.f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, m.f, 64, (int)m.lds) == hipSuccess) o["occupancy_api"] = occ;
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, m.f) == hipSuccess) {
+      o["num_regs"] = (uint64_t)fa.numRegs;
+      o["scratch_bytes_per_lane"] = (uint64_t)fa.localSizeBytes;
+    }
+  }
+  out["split"]["sm_hot_bytes"] = kSmHotBytes;
+  out["lds"]["sm_state_bytes"] = sizeof(SMState);
+  return out;
+}
 std::map<std::string, uint64_t> gpu_batch_stats() {
   std::map<std::string, uint64_t> m{{"batches", BatchLauncher::get().batches()},
                                      {"launches", BatchLauncher::get().jobs()},
@@ -1285,11 +1341,11 @@ std::map<std::string, uint64_t> gpu_batch_stats() {
 // CUs one simulation of this shape reserves on the GPU engine (the
 // concurrency of job-level parallelism on one GPU, multi_gpu.py)
 int gpu_cus_per_sim(uint32_t n_sm, uint32_t n_mem) {
-  const bool g = gpu_state_global();
+  const int m = gpu_state_mode();
   uint32_t nb = n_sm + n_mem;
   const int cus = gpu_cu_count();
-  if (cus > 0) nb = std::min<uint32_t>(nb, (uint32_t)cus * (g ? global_blocks_per_cu() : 1u));
-  const uint32_t slots = nb * engine_block_slots(g);
+  if (cus > 0) nb = std::min<uint32_t>(nb, (uint32_t)cus * mode_blocks_per_cu(m));
+  const uint32_t slots = nb * engine_block_slots(m);
   return (int)((slots + kCuSlots - 1) / kCuSlots);
 }
 int gpu_cu_count() {
@@ -1305,7 +1361,7 @@ namespace asim {
 EngineKernelInfo gpu_engine_kernel_info() {
   EngineKernelInfo k;
   hipFuncAttributes fa;
-  if (hipFuncGetAttributes(&fa, (const void*)engine_kernel<WavePar, false, false>) != hipSuccess) return k;
+  if (hipFuncGetAttributes(&fa, (const void*)engine_kernel<WavePar, false, kModeLds>) != hipSuccess) return k;
   k.num_regs = fa.numRegs;
   k.local_bytes = (int)fa.localSizeBytes;
   k.shared_static = (int)fa.sharedSizeBytes;

@@ -12,6 +12,7 @@ int gpu_cus_per_sim(uint32_t n_sm, uint32_t n_mem) { return (int)(n_sm + n_mem);
 std::map<std::string, uint64_t> gpu_pool_stats() { return {}; }
 void gpu_pool_trim() {}
 std::map<std::string, uint64_t> gpu_batch_stats() { return {}; }
+std::map<std::string, std::map<std::string, uint64_t>> gpu_engine_modes() { return {}; }
 EngineKernelInfo gpu_engine_kernel_info() { return EngineKernelInfo{}; }
 }  // namespace asim
 

@@ -175,9 +175,10 @@ __device__ __forceinline__ void sbz(WarpSb& sb, uint32_t w) {
   if (sv_lane() == (int)w) sb.v[0] = sb.v[1] = sb.v[2] = sb.v[3] = 0;
 }
 
-#define SV_REF(m) decltype(B::m)& m
-#define SV_VAL(m) decltype(B::m) m
-#define SV_WARP(m) WarpReg<typename std::remove_extent<decltype(B::m)>::type> m
+// (B is SMState, or SmSplit whose members are references: strip those)
+#define SV_REF(m) std::remove_reference_t<decltype(B::m)>& m
+#define SV_VAL(m) std::remove_reference_t<decltype(B::m)> m
+#define SV_WARP(m) WarpReg<std::remove_extent_t<std::remove_reference_t<decltype(B::m)>>> m
 
 template <class B>
 struct SmView {

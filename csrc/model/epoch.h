@@ -66,8 +66,8 @@ struct EpochDecision {
 // CTA dispatch (reference gpgpu_sim::issue_block2core, gpu-sim.cc and
 // simt_core_cluster::issue_block2core, shader.cc:4502-4535): round-robin
 // rounds over the SMs requesting CTAs of one kernel, rotated by epoch.
-template <class P>
-SIM_HDI void cta_dispatch(SMState& s, const SmCtx& x, uint32_t ks, const UnitPub* pubs, uint32_t n_sm,
+template <class P, class S>
+SIM_HDI void cta_dispatch(S& s, const SmCtx& x, uint32_t ks, const UnitPub* pubs, uint32_t n_sm,
                           uint32_t rot) {
   const KernelDesc& k = x.kt->k[ks];
   if (s.next_cta[ks] >= k.n_cta) return;
@@ -102,8 +102,8 @@ SIM_HDI void cta_dispatch(SMState& s, const SmCtx& x, uint32_t ks, const UnitPub
 // over the XCDs at every dispatch), so the CTAs of residue x go to the SMs of
 // XCD x (SM s belongs to XCD s % n_xcd), in the same rounds as above within
 // each XCD.  Every SM advances every XCD's cursor (the state is replicated).
-template <class P>
-SIM_HDI void cta_dispatch_xcd(SMState& s, const SmCtx& x, uint32_t ks, const UnitPub* pubs, uint32_t n_sm,
+template <class P, class S>
+SIM_HDI void cta_dispatch_xcd(S& s, const SmCtx& x, uint32_t ks, const UnitPub* pubs, uint32_t n_sm,
                               uint32_t rot) {
   const KernelDesc& k = x.kt->k[ks];
   if (s.next_cta[ks] >= k.n_cta) return;
@@ -182,7 +182,8 @@ struct SmRes {
   uint64_t wmask;
   uint32_t ctas, thr, regs, shmem;
 };
-SIM_HDI uint32_t sm_cta_fit(const SMState& s, const SimCfg& c, const KernelDesc& k, uint32_t ks, SmRes& r) {
+template <class S>
+SIM_HDI uint32_t sm_cta_fit(const S& s, const SimCfg& c, const KernelDesc& k, uint32_t ks, SmRes& r) {
   const uint32_t nwm = amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t max_cta = amin<uint32_t>(c.max_cta_per_sm, kMaxCta);
   // counted resources: closed form
@@ -217,8 +218,8 @@ SIM_HDI uint32_t sm_cta_fit(const SMState& s, const SimCfg& c, const KernelDesc&
 }
 
 // kernel slot (re)initialisation of an SM: first epoch after a launch
-template <class P>
-SIM_HDI void sm_kernels_init(SMState& s, const SmCtx& x) {
+template <class P, class S>
+SIM_HDI void sm_kernels_init(S& s, const SmCtx& x) {
   const KernelTab& kt = *x.kt;
   for (uint32_t k = 0; k < (uint32_t)kMaxConc; ++k) {
     if (!(kt.active >> k & 1u) || s.k_uid[k] == kt.k[k].uid) continue;
@@ -249,8 +250,8 @@ SIM_HDI void sm_kernels_init(SMState& s, const SmCtx& x) {
 }
 
 // one epoch of one SM: [t0, t1) core cycles
-template <class P>
-SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t prev,
+template <class P, class S>
+SIM_HDI void sm_epoch(S& s, const SmCtx& x, const EpochPub& pub, uint32_t prev,
                       uint64_t t0, uint64_t t1, const Pkt* inbox, const uint32_t* incnt, uint32_t in_cap,
                       uint32_t n_sub, uint64_t epoch_idx, const uint64_t* rep_dst = nullptr) {
   const SimCfg& c = *x.cfg;
@@ -318,8 +319,8 @@ SIM_HDI void sm_epoch(SMState& s, const SmCtx& x, const EpochPub& pub, uint32_t 
 }
 
 // publish SM outbox counts + boundary state
-template <class P>
-SIM_HDI void sm_publish(SMState& s, const SmCtx& x, EpochPub& pub, uint32_t cur) {
+template <class P, class S>
+SIM_HDI void sm_publish(S& s, const SmCtx& x, EpochPub& pub, uint32_t cur) {
   const SimCfg& c = *x.cfg;
   // destinations written this epoch (none when no packet was injected: every
   // injection lowers min_emit); this parity's cells are rewritten only if

@@ -256,21 +256,10 @@ struct alignas(16) SMState {
   uint64_t oc_banks[kMaxOC];
   uint32_t oc_age[kMaxOC];
   uint32_t fu_next[U_COUNT * kMaxSched];  // [unit * kMaxSched + phys]: cycle (low 32) the unit can accept again
-  uint8_t wb_cnt[kWbRing];
-  WbEnt wb[kWbRing][kWbSlot];
   // ---- LD/ST + L1 ----
   LdstState ldst;
   TAcc ldst_acc[kMaxAccess];     // access records of the instruction in the LD/ST unit (loaded at dispatch)
-  uint8_t hit_cnt[kHitRing];
-  HitEnt hit[kHitRing][kHitSlot];
-  L1Line l1[kMaxL1Lines];
-  L1Mshr mshr[kMaxL1Mshr];
-  L1Pend pend[kMaxPend];
   uint32_t n_pend;
-  L1Line il1[kMaxIL1Lines];     // instruction cache tags (non-sectored: valid = 0xf)
-  L1Mshr imshr[kMaxIL1Mshr];
-  L1Line cl1[kMaxCL1Lines];     // constant / scalar data cache tags (valid = 1: non-sectored)
-  L1Mshr cmshr[kMaxCL1Mshr];
   uint64_t w_iline[kMaxWarps];  // code line a WF_IMISS warp waits for
   uint64_t idoc_mask;     // bit sched*U_COUNT+unit: ID_OC register occupied
   uint32_t oc_mask;       // occupied operand collectors
@@ -306,6 +295,20 @@ struct alignas(16) SMState {
   // residue handed out so far (next_cta is then their sum)
   uint32_t next_ctax[kMaxConc][kMaxXcd];
   SMStats st;
+  // ---- the geometry-sized arrays (SMTail: everything from wb_cnt on).  The
+  // GPU engine's split-state build keeps the fields above in LDS and these
+  // in the unit's HBM image (csrc/engine/sm_split.h SmSplit) ----
+  alignas(16) uint8_t wb_cnt[kWbRing];
+  WbEnt wb[kWbRing][kWbSlot];
+  uint8_t hit_cnt[kHitRing];
+  HitEnt hit[kHitRing][kHitSlot];
+  L1Line l1[kMaxL1Lines];
+  L1Mshr mshr[kMaxL1Mshr];
+  L1Pend pend[kMaxPend];
+  L1Line il1[kMaxIL1Lines];     // instruction cache tags (non-sectored: valid = 0xf)
+  L1Mshr imshr[kMaxIL1Mshr];
+  L1Line cl1[kMaxCL1Lines];     // constant / scalar data cache tags (valid = 1: non-sectored)
+  L1Mshr cmshr[kMaxCL1Mshr];
   // statistics by word index (SK below); the GPU engine's register view keeps
   // the counters in lanes during the cycle loop (csrc/engine/sm_view.h)
   SIM_HDI void sadd(uint32_t k, uint64_t d) { reinterpret_cast<uint64_t*>(&st)[k] += d; }
@@ -322,9 +325,12 @@ struct alignas(16) SMState {
 #define SADD_IN(s, f, n, i, d) (s).template sadd_r<SK(f), SK(f) + (n)>(SK(f) + (uint32_t)(i), (d))
 constexpr int kStatWords = (int)(sizeof(SMStats) / 8);
 static_assert(kStatWords <= 256, "SM statistics: up to four 64-lane register words on the GPU engine");
-SIM_HDI uint64_t* s_scratch_key(SMState& s) { return s.skey; }
-SIM_HDI uint32_t* s_scratch_ref(SMState& s) { return s.sref; }
-SIM_HDI uint32_t* s_scratch_rank(SMState& s) { return s.srank; }
+template <class S>
+SIM_HDI uint64_t* s_scratch_key(S& s) { return s.skey; }
+template <class S>
+SIM_HDI uint32_t* s_scratch_ref(S& s) { return s.sref; }
+template <class S>
+SIM_HDI uint32_t* s_scratch_rank(S& s) { return s.srank; }
 
 // ---------------------------------------------------------------------------
 // context passed to every SM step

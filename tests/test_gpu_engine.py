@@ -438,3 +438,38 @@ def test_batch_launch_many_simulations_gpu_equals_cpu(gpu_mod, tmp_path, monkeyp
     launches = after["launches"] - before["launches"]
     batches = after["batches"] - before["batches"]
     assert launches >= len(kls) and batches < launches  # launches were shared
+
+
+@pytest.mark.parametrize("app", ["bfs", "hotspot"])
+def test_split_state_gpu_equals_cpu(gpu_mod, tmp_path, monkeypatch, app):
+    """ASIM_GPU_STATE=split: an SM's hot prefix in LDS, its geometry-sized
+    arrays (rings, cache tags, MSHRs, pending loads) and every channel in HBM;
+    bit-exact against the CPU engine, also time-sliced (37 blocks)."""
+    from accel_sim_framework_distributed_amd import sim
+    from accel_sim_framework_distributed_amd.tracegen import rodinia
+    monkeypatch.setenv("ASIM_GPU_STATE", "split")
+    gen = {"bfs": lambda: rodinia.bfs(2048, levels=4), "hotspot": lambda: rodinia.hotspot(64, 2, 2)}[app]
+    kl = rodinia.write_app(str(tmp_path / app), gen())
+    for blocks in ("0", "37"):
+        monkeypatch.setenv("ASIM_GPU_BLOCKS", blocks)
+        sg = sim.Simulator("QV100", kl, engine="gpu", torch_runtime=True)
+        sc = sim.Simulator("QV100", kl, engine="cpu")
+        g, c = sg.run(), sc.run()
+        assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
+        assert sg.native.snapshot() == sc.native.snapshot()
+
+
+def test_split_state_kernel_resources(gpu_mod):
+    """The split-state build needs <= 40 KB of LDS per engine block, so at
+    least 4 engine waves share a CU (3 used: one block of margin below the
+    occupancy API), and a GV100 simulation (112 units) reserves <= 38 CUs."""
+    m = gpu_mod.gpu_engine_modes()
+    assert m["split"]["lds_bytes"] <= 40 * 1024
+    assert m["split"]["occupancy_api"] >= 4 and m["split"]["blocks_per_cu"] >= 3
+    assert m["lds"]["blocks_per_cu"] == 1 and m["lds"]["lds_bytes"] > m["lds"]["sm_state_bytes"]
+    import os
+    os.environ["ASIM_GPU_STATE"] = "split"
+    try:
+        assert gpu_mod.gpu_cus_per_sim(80, 32) <= 38
+    finally:
+        del os.environ["ASIM_GPU_STATE"]

@@ -85,6 +85,34 @@ from accel_sim_framework_distributed_amd import _native
 m = _native.load(prefer_torch_runtime=True); print(m.gpu_batch_stats(), m.gpu_cus_per_sim(80, 32), m.gpu_cu_count())" \
     2>&1 | grep -v amdgpu.ids
 }
+step_split() {
+  timeout -k 10 600 $PT tests/test_gpu_engine.py -k "split or global_state or batch or resources or rodinia_app" \
+    > $O/pytest_split.log 2>&1 || { tail -30 $O/pytest_split.log; return 1; }
+  tail -3 $O/pytest_split.log
+  timeout -k 10 60 python3 -c "
+import torch, sys, json; sys.path.insert(0, '.')
+from accel_sim_framework_distributed_amd import _native
+m = _native.load(prefer_torch_runtime=True); print(json.dumps(m.gpu_engine_modes()))" 2>&1 | grep -v amdgpu.ids | tee $O/engine_modes.json
+  for app in hotspot bfs; do
+    for mode in lds split; do
+      echo -n "$mode " >> $O/one_sm_split.txt
+      ASIM_GPU_STATE=$mode ASIM_GPU_PROFILE=0 timeout -k 10 120 python3 tools/engine_pmc_1sm.py --app $app 2>&1 \
+        | grep -v amdgpu.ids >> $O/one_sm_split.txt || return 1
+    done
+  done
+  cat $O/one_sm_split.txt
+  for app in hotspot bfs; do
+    ASIM_GPU_STATE=split timeout -k 10 300 python3 tools/batch_scaling.py --app $app --n ${NS:-1,2,3,4,6} 2>&1 \
+      | grep -v amdgpu.ids >> $O/scaling_split.jsonl || return 1
+  done
+  cat $O/scaling_split.jsonl
+  for what in "--engine gpu --steps 2 --warmup 1" "--sweep --engine gpu --steps 1 --warmup 0"; do
+    tag=$(echo $what | awk '{print ($1=="--sweep")?"sweep":"bench"}')
+    ASIM_GPU_STATE=split timeout -k 10 400 python3 bench.py $what > $O/${tag}_gpu_split.json 2> $O/${tag}_gpu_split.err \
+      || { tail -3 $O/${tag}_gpu_split.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/${tag}_gpu_split.json')); print('$tag split', d['value'], d['ms_per_step'], d['config'].get('gpu_slots'))"
+  done
+}
 step_tests() {
   timeout -k 10 1000 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; return 1; }
   tail -3 $O/pytest_gpu.log
