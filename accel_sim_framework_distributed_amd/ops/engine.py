@@ -24,16 +24,17 @@ def kernel_info() -> Dict[str, int]:
 
 def footprint(config: str = "QV100") -> Dict[str, int]:
     """How one simulation of `config` occupies an MI355X: units (simulated
-    SMs + memory channels), blocks (one wavefront each, one per CU because of
-    the LDS state; capped at the CU count, beyond which each block
-    time-slices several units), and how many such simulations fit side by
-    side on the device."""
+    SMs + memory channels), blocks (one wavefront each; the LDS-state build
+    fits one per CU, the default split-state build several: the CUs a
+    simulation reserves come from the native engine, gpu_cus_per_sim), and
+    how many such simulations fit side by side on the device."""
     from ..sim import build_args
     mod = _native.load(prefer_torch_runtime=True)
     cfg = mod.parse_config(build_args(config, None, "cpu"))
     units = int(cfg["n_sm"]) + int(cfg["n_mem"])
     cus = int(mod.gpu_cu_count()) if mod.gpu_available() else 0
     blocks = min(units, cus) if cus else units
+    per = int(mod.gpu_cus_per_sim(int(cfg["n_sm"]), int(cfg["n_mem"]))) if cus else 0
     return dict(sm_blocks=int(cfg["n_sm"]), channel_blocks=int(cfg["n_mem"]), units=units, blocks=blocks,
-                units_per_block=-(-units // blocks), device_cus=cus,
-                concurrent_simulations=(cus // blocks) if cus else 0, epoch_cycles=int(cfg["icnt_latency"]))
+                units_per_block=-(-units // blocks), device_cus=cus, cus_per_simulation=per,
+                concurrent_simulations=(cus // per) if per else 0, epoch_cycles=int(cfg["icnt_latency"]))

@@ -196,11 +196,11 @@ class DistributedSuite:
     def gpu_reserve(gslots: int) -> int:
         """Host cores kept for the threads driving GPU-engine simulations.
         LDS-state engine: one per slot (each thread launches and waits on its
-        own simulation).  Global-state engine (ASIM_GPU_STATE=global): the
-        simulations share batch launches -- one leader thread waits on the
-        GPU while the others sleep -- so two cores (ASIM_GPU_HOST_RESERVE)
-        cover them however many run."""
-        if os.environ.get("ASIM_GPU_STATE") == "global":
+        own simulation).  Global- and split-state engines
+        (ASIM_GPU_STATE=global / split) with batch launches: one leader thread
+        waits on the GPU while the others sleep, so two cores
+        (ASIM_GPU_HOST_RESERVE) cover them however many run."""
+        if os.environ.get("ASIM_GPU_STATE", "split") in ("global", "split") and os.environ.get("ASIM_GPU_BATCH") == "1":
             return min(gslots, max(1, int(os.environ.get("ASIM_GPU_HOST_RESERVE", "2"))))
         return gslots
 

@@ -146,12 +146,16 @@ uint32_t block_slots(size_t lds) {
   const size_t per_cu = lds ? (160 * 1024) / lds : kMaxBlocksPerCu;  // blocks whose LDS fits one CU
   return kCuSlots / (uint32_t)std::max<size_t>(1, std::min<size_t>(per_cu, kMaxBlocksPerCu));
 }
-// ASIM_GPU_STATE: lds (default) | global | split (engine_kernel.h EngineMode)
+// ASIM_GPU_STATE: split (default) | lds | global (engine_kernel.h EngineMode).
+// The split build is the default: 5-9 % slower per simulated SM than the
+// LDS build but three engine waves per CU instead of one, which measured
+// +6.5 % on the node bench, +12 % GPU-engine-only and +11 % on the config
+// sweep on one box (profiles/r6/README.md)
 int gpu_state_mode() {
   const char* e = getenv("ASIM_GPU_STATE");
-  if (!e) return kModeLds;
+  if (!e || !*e) return kModeSplit;
   const std::string v(e);
-  return v == "global" ? kModeGlobal : v == "split" ? kModeSplit : kModeLds;
+  return v == "global" ? kModeGlobal : v == "lds" ? kModeLds : kModeSplit;
 }
 bool gpu_state_global() { return gpu_state_mode() == kModeGlobal; }
 int g_occ_api = 0;  // the occupancy API's blocks per CU of the last mode asked (diagnostics)
@@ -181,11 +185,14 @@ bool profiling_env() {
   const char* pe = getenv("ASIM_GPU_PROFILE");
   return pe && *pe && *pe != '0';
 }
-// ASIM_GPU_BATCH (default on): global-state simulations of a process share
-// batch launches (engine_batch_kernel)
+// ASIM_GPU_BATCH=1: global- / split-state simulations of a process share
+// batch launches (engine_batch_kernel / engine_batch_split_kernel).  Off by
+// default: a batch ends with its slowest simulation and forms only when the
+// simulations are in their GPU phase together, and one kernel per simulation
+// on the process's hardware queues measured faster (profiles/r6/README.md)
 bool gpu_batch_on() {
   const char* e = getenv("ASIM_GPU_BATCH");
-  return !(e && std::string(e) == "0");
+  return e && std::string(e) == "1";
 }
 
 // Process-wide CU reservation.  Every simulation needs ALL its blocks

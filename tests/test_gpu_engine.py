@@ -404,15 +404,16 @@ def test_device_pool_stays_bounded(gpu_mod, tmp_path):
     assert (g.tot_cycle, g.tot_insn) == (c.tot_cycle, c.tot_insn)
 
 
-def test_batch_launch_many_simulations_gpu_equals_cpu(gpu_mod, tmp_path, monkeypatch):
-    """Global-state simulations running side by side in one process share
-    batch launches (engine_batch_kernel: one launch hosts several
+@pytest.mark.parametrize("state", ["global", "split"])
+def test_batch_launch_many_simulations_gpu_equals_cpu(gpu_mod, tmp_path, monkeypatch, state):
+    """Global- / split-state simulations running side by side in one process
+    share batch launches (ASIM_GPU_BATCH=1: one launch hosts several
     simulations, each synchronising only its own blocks); every one of them
     stays bit-exact against the CPU engine."""
     from concurrent.futures import ThreadPoolExecutor
     from accel_sim_framework_distributed_amd import sim
     from accel_sim_framework_distributed_amd.tracegen import rodinia
-    monkeypatch.setenv("ASIM_GPU_STATE", "global")
+    monkeypatch.setenv("ASIM_GPU_STATE", state)
     monkeypatch.setenv("ASIM_GPU_BATCH", "1")
     apps = {"bfs": rodinia.bfs(2048, levels=3), "hotspot": rodinia.hotspot(64, 2, 2), "nw": rodinia.nw(64),
             "backprop": rodinia.backprop(1024), "srad": rodinia.srad_v2(64, 64, 1), "path": rodinia.pathfinder(2000, 8, 2)}
@@ -467,9 +468,4 @@ def test_split_state_kernel_resources(gpu_mod):
     assert m["split"]["lds_bytes"] <= 40 * 1024
     assert m["split"]["occupancy_api"] >= 4 and m["split"]["blocks_per_cu"] >= 3
     assert m["lds"]["blocks_per_cu"] == 1 and m["lds"]["lds_bytes"] > m["lds"]["sm_state_bytes"]
-    import os
-    os.environ["ASIM_GPU_STATE"] = "split"
-    try:
-        assert gpu_mod.gpu_cus_per_sim(80, 32) <= 38
-    finally:
-        del os.environ["ASIM_GPU_STATE"]
+    assert gpu_mod.gpu_cus_per_sim(80, 32) <= 38  # split is the default build

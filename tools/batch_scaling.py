@@ -2,8 +2,8 @@
 """Concurrency scaling of the GPU engine: N copies of one application's
 simulation (GV100 config) run side by side in one process, for N in --n.
 Prints the wall time and aggregate sim KIPS per N, and the batch launcher's
-counters (ASIM_GPU_STATE=global shares batch launches; lds runs one kernel
-per simulation).  usage: ASIM_GPU_STATE=global python3 tools/batch_scaling.py --app hotspot --n 1,2,4"""
+counters (ASIM_GPU_BATCH=1 shares batch launches between global- / split-
+state simulations; otherwise one kernel per simulation).  usage: ASIM_GPU_STATE=global python3 tools/batch_scaling.py --app hotspot --n 1,2,4"""
 import argparse
 import json
 import os
@@ -44,7 +44,7 @@ def main():
             insn = sum(ex.map(one, range(n)))
         dt = time.perf_counter() - t
         b1 = mod.gpu_batch_stats()
-        rec = {"app": a.app, "state": os.environ.get("ASIM_GPU_STATE", "lds"), "n": n, "wall_s": round(dt, 3),
+        rec = {"app": a.app, "state": os.environ.get("ASIM_GPU_STATE", "split"), "n": n, "wall_s": round(dt, 3),
                "kips": round(insn / dt / 1e3, 1), "batches": b1.get("batches", 0) - b0.get("batches", 0),
                "launches": b1.get("launches", 0) - b0.get("launches", 0), "blocks_per_cu": b1.get("blocks_per_cu")}
         out.append(rec)

@@ -113,6 +113,34 @@ m = _native.load(prefer_torch_runtime=True); print(json.dumps(m.gpu_engine_modes
     python3 -c "import json; d=json.load(open('$O/${tag}_gpu_split.json')); print('$tag split', d['value'], d['ms_per_step'], d['config'].get('gpu_slots'))"
   done
 }
+step_split2() {
+  # split-state build with batch launches: tests, concurrency scaling, GPU-only suite and sweep, node bench
+  ASIM_GPU_STATE=split timeout -k 10 600 $PT tests/test_gpu_engine.py -k "split or batch or rodinia_app" \
+    > $O/pytest_split2.log 2>&1 || { tail -30 $O/pytest_split2.log; return 1; }
+  tail -3 $O/pytest_split2.log
+  for app in hotspot bfs; do
+    ASIM_GPU_STATE=split timeout -k 10 300 python3 tools/batch_scaling.py --app $app --n ${NS:-1,2,3,4,6,8} 2>&1 \
+      | grep -v amdgpu.ids >> $O/scaling_split_batch.jsonl || return 1
+  done
+  cat $O/scaling_split_batch.jsonl
+  for what in "--engine gpu --steps 2 --warmup 1" "--sweep --engine gpu --steps 1 --warmup 0" "--steps 10 --warmup 3"; do
+    tag=$(echo $what | awk '{print ($1=="--sweep")?"sweep_gpu":($1=="--engine")?"bench_gpu":"bench_node"}')
+    ASIM_GPU_STATE=split timeout -k 10 400 python3 bench.py $what > $O/${tag}_split_batch.json 2> $O/${tag}_split_batch.err \
+      || { tail -3 $O/${tag}_split_batch.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/${tag}_split_batch.json')); print('$tag split+batch', d['value'], d['ms_per_step'], d['config'].get('gpu_slots'), d.get('gpu_engine',{}).get('insn_share'))"
+  done
+}
+step_nodecmp() {
+  # node bench, GPU-only suite and sweep: LDS-state vs split-state engine, same box
+  for st in lds split; do
+    for what in "--steps 10 --warmup 3" "--engine gpu --steps 2 --warmup 1" "--sweep --engine gpu --steps 1 --warmup 0"; do
+      tag=$(echo $what | awk '{print ($1=="--sweep")?"sweep_gpu":($1=="--engine")?"bench_gpu":"bench_node"}')
+      ASIM_GPU_STATE=$st timeout -k 10 400 python3 bench.py $what > $O/${tag}_$st.json 2> $O/${tag}_$st.err \
+        || { tail -3 $O/${tag}_$st.err; return 1; }
+      python3 -c "import json; d=json.load(open('$O/${tag}_$st.json')); print('$tag $st', d['value'], d['ms_per_step'], d['config'].get('gpu_slots'), d.get('gpu_engine',{}).get('insn_share'))"
+    done
+  done
+}
 step_tests() {
   timeout -k 10 1000 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; return 1; }
   tail -3 $O/pytest_gpu.log
