@@ -24,3 +24,17 @@ def test_sweep_address_mappings_match_reference_and_tuned_config():
                        "AMD_Instinct_MI355X", "gpgpusim.config")
     lines = [l.split(None, 1)[1].strip() for l in open(cfg) if l.startswith("-gpgpu_mem_addr_mapping")]
     assert lines == [m256]
+
+
+def test_job_launching_registry_mappings_match_the_sweep():
+    """define-standard-cfgs.yml's 32B / 256B extras carry the same (reference)
+    mapping strings as the sweep, and GPU_ENGINE selects the MI355X engine."""
+    import os
+    import yaml
+    from accel_sim_framework_distributed_amd.parallel.sweep import EXTRA_FLAGS
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "accel_sim_framework_distributed_amd",
+                     "job_launching", "configs", "define-standard-cfgs.yml")
+    y = yaml.safe_load(open(p))
+    for k in ("32B", "256B"):
+        assert y[k]["extra_params"] == "-gpgpu_mem_addr_mapping " + EXTRA_FLAGS[k]["-gpgpu_mem_addr_mapping"]
+    assert y["GPU_ENGINE"]["extra_params"] == "-sim_engine gpu"

@@ -141,6 +141,20 @@ step_nodecmp() {
     done
   done
 }
+step_corr_gpu() {
+  # the round-5 correlation capture (ISA traces + rocprofv3 timings, corr_data/) simulated with the tuned
+  # MI355X config on the GPU engine and on the host engine: speed and cycle MAE of the same simulations
+  for eng in gpu cpu; do
+    cfg=MI355X_TUNED; [ $eng = gpu ] && cfg=MI355X_TUNED-GPU_ENGINE
+    t0=$(date +%s.%N)
+    CORR_SRC=$GRAFT_REPO_ROOT/corr_data CFG=$cfg JOBS=${CORR_JOBS:-2} timeout -k 10 900 \
+      bash tools/local_full_correlate.sh /tmp/corr_$eng > $O/corr_$eng.log 2>&1 || { tail $O/corr_$eng.log; return 1; }
+    t1=$(date +%s.%N)
+    python3 tools/corr_speed.py /tmp/corr_$eng/simrun /tmp/corr_$eng/correl $(python3 -c "print($t1 - $t0)") $eng \
+      | tee -a $O/corr_speed.jsonl
+    cp /tmp/corr_$eng/correl/mi355x-summary.json $O/corr_${eng}_summary.json
+  done
+}
 step_tests() {
   timeout -k 10 1000 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; return 1; }
   tail -3 $O/pytest_gpu.log

@@ -14,7 +14,7 @@ rm -rf $out && mkdir -p $out/traces
 for t in $src/trace_tgz/*.tgz; do tar xzf $t -C $out/traces; done
 export PROCMAN_STATE=$out/procman.json ASIM_JOB_LOGDIR=$out/logs
 JL=$R/util/job_launching
-python $JL/run_simulations.py -B ${SUITE:-rodinia_2.0-ft-hip} -C MI355X_TUNED -T $out/traces -N lcorr -l local \
+python $JL/run_simulations.py -B ${SUITE:-rodinia_2.0-ft-hip} -C ${CFG:-MI355X_TUNED} -T $out/traces -N lcorr -l local \
   -r $out/simrun -c ${JOBS:-8} --threads 1 > $out/launch.log 2>&1 || { echo "launch failed"; tail $out/launch.log; exit 1; }
 python $JL/monitor_func_test.py -N lcorr -r $out/simrun -S 5 -T 1200 -K -j procman > $out/monitor.log 2>&1
 tail -3 $out/monitor.log
