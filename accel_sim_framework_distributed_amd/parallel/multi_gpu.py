@@ -195,14 +195,12 @@ class DistributedSuite:
     @staticmethod
     def gpu_reserve(gslots: int) -> int:
         """Host cores kept for the threads driving GPU-engine simulations.
-        LDS-state engine: one per slot (each thread launches and waits on its
-        own simulation).  Global- and split-state engines
-        (ASIM_GPU_STATE=global / split) with batch launches: one leader thread
-        waits on the GPU while the others sleep, so two cores
-        (ASIM_GPU_HOST_RESERVE) cover them however many run."""
-        if os.environ.get("ASIM_GPU_STATE", "split") in ("global", "split") and os.environ.get("ASIM_GPU_BATCH") == "1":
-            return min(gslots, max(1, int(os.environ.get("ASIM_GPU_HOST_RESERVE", "2"))))
-        return gslots
+        They sleep while their launches run (a blocking-sync event in
+        gpu_engine.hip) and work only between launches (trace ingest, kernel
+        setup), so a few cores cover them however many run: half the GPU
+        slots, at least one, at most ASIM_GPU_HOST_RESERVE (default 2)."""
+        cap = max(1, int(os.environ.get("ASIM_GPU_HOST_RESERVE", "2")))
+        return max(1, min(gslots, cap, (gslots + 1) // 2))
 
     def cpu_slots(self, reserve: int = 0) -> int:
         """Host cores this rank may use for CPU-engine simulations: its share

@@ -667,6 +667,7 @@ class GpuEngine : public Engine {
       pool_alloc(&d_ework_, sizeof(uint32_t) * nblocks_);
     }
     stream_ = DevicePool::get().stream();
+    if (!done_ev_) HIPCHECK(hipEventCreateWithFlags(&done_ev_, hipEventBlockingSync | hipEventDisableTiming));
     if (c_.trace_mask) {
       // debug trace buffers in HBM; the device copy of the config points at them
       const size_t units = (size_t)c.n_sm + c.n_mem;
@@ -823,7 +824,11 @@ class GpuEngine : public Engine {
       le = hipGetLastError();
       ++launches_;
       hipError_t ce = hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(GpuCtl), hipMemcpyDeviceToHost, stream_);
-      hipError_t se = hipStreamSynchronize(stream_);
+      // wait on a blocking-sync event: the host thread sleeps instead of
+      // spinning, so simulations waiting on the GPU leave the host cores to
+      // the CPU-engine simulations of the node schedule
+      hipError_t se = hipEventRecord(done_ev_, stream_);
+      if (se == hipSuccess) se = hipEventSynchronize(done_ev_);
       CuPool::get().release((int)(nblocks_ * slots_));
       HIPCHECK(le);
       HIPCHECK(ce);
@@ -1133,6 +1138,8 @@ class GpuEngine : public Engine {
     fr(d_kt_);
     DevicePool::get().host_free(h_ctl_);
     DevicePool::get().stream_free(stream_);
+    if (done_ev_) (void)hipEventDestroy(done_ev_);
+    done_ev_ = nullptr;
   }
 
   SimCfg c_{};
@@ -1141,6 +1148,7 @@ class GpuEngine : public Engine {
   uint32_t nblocks_ = 0;
   size_t lds_ = 0;
   hipStream_t stream_ = nullptr;
+  hipEvent_t done_ev_ = nullptr;  // blocking-sync event the launch waits on
   SimCfg* d_cfg_ = nullptr;
   SMState* d_sms_ = nullptr;
   ChanState* d_chs_ = nullptr;

@@ -155,6 +155,14 @@ step_corr_gpu() {
     cp /tmp/corr_$eng/correl/mi355x-summary.json $O/corr_${eng}_summary.json
   done
 }
+step_nodetol() {
+  # node bench (split build) at several makespan tolerances for moving apps onto the GPU engine
+  for tol in ${TOLS:-0 0.03 0.08}; do
+    ASIM_NODE_GPU_TOLERANCE=$tol timeout -k 10 400 python3 bench.py --steps 10 --warmup 3 > $O/bench_node_tol$tol.json \
+      2> $O/bench_node_tol$tol.err || { tail -3 $O/bench_node_tol$tol.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_node_tol$tol.json')); print('tol $tol', d['value'], d['ms_per_step'], d['gpu_engine']['insn_share'], d['config']['node_predicted_step_ms'])"
+  done
+}
 step_tests() {
   timeout -k 10 1000 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; return 1; }
   tail -3 $O/pytest_gpu.log
