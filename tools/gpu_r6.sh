@@ -163,6 +163,23 @@ step_nodetol() {
     python3 -c "import json; d=json.load(open('$O/bench_node_tol$tol.json')); print('tol $tol', d['value'], d['ms_per_step'], d['gpu_engine']['insn_share'], d['config']['node_predicted_step_ms'])"
   done
 }
+step_prof() {
+  # rocprofv3 kernel statistics of the GPU-engine-only suite (every app on the split-state engine)
+  # and of the node bench
+  for what in "--engine gpu --steps 2 --warmup 1" "--steps 3 --warmup 1"; do
+    tag=$(echo $what | awk '{print ($1=="--engine")?"gpu":"node"}')
+    (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_$tag \
+      -o run -- python3 $GRAFT_REPO_ROOT/bench.py $what > $GRAFT_REPO_ROOT/$O/prof_$tag.log 2>&1) \
+      || { tail -5 $O/prof_$tag.log; return 1; }
+    grep '^{"metric"' $O/prof_$tag.log | cut -c1-160
+    cat $(find $O/prof_$tag -name "*kernel_stats.csv" | head -1) | cut -c1-160 | head -8
+  done
+}
+step_sweep_node() {
+  timeout -k 10 400 python3 bench.py --sweep --steps 1 --warmup 0 > $O/sweep_node.json 2> $O/sweep_node.err \
+    || { tail -3 $O/sweep_node.err; return 1; }
+  python3 -c "import json; d=json.load(open('$O/sweep_node.json')); print('sweep node', d['value'], d['ms_per_step'], d['config'].get('gpu_slots'), d['config'].get('cpu_slots'), d['gpu_engine'])"
+}
 step_tests() {
   timeout -k 10 1000 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; return 1; }
   tail -3 $O/pytest_gpu.log
