@@ -180,6 +180,17 @@ step_sweep_node() {
     || { tail -3 $O/sweep_node.err; return 1; }
   python3 -c "import json; d=json.load(open('$O/sweep_node.json')); print('sweep node', d['value'], d['ms_per_step'], d['config'].get('gpu_slots'), d['config'].get('cpu_slots'), d['gpu_engine'])"
 }
+step_stage() {
+  # one-SM stage profile (profiling build) of the default split engine, bfs and hotspot, plus SQ counters
+  for app in ${APPS:-bfs hotspot}; do
+    ASIM_GPU_PROFILE=1 timeout -k 10 180 python3 tools/engine_pmc_1sm.py --app $app > $O/stage_$app.log 2>&1 || return 1
+    grep -v amdgpu.ids $O/stage_$app.log | head -64
+  done
+  cs="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS"
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --stats --pmc $cs -d $GRAFT_REPO_ROOT/$O/pmc_split_bfs -o pmc -- \
+    python3 $GRAFT_REPO_ROOT/tools/engine_pmc_1sm.py --app bfs > $GRAFT_REPO_ROOT/$O/pmc_split_bfs.log 2>&1) || return 1
+  python3 tools/pmc_summary.py $(find $O/pmc_split_bfs -name "*.db" | head -1) engine_kernel | tee $O/pmc_split_bfs.json
+}
 step_tests() {
   timeout -k 10 1000 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; return 1; }
   tail -3 $O/pytest_gpu.log
