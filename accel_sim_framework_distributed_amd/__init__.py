@@ -19,4 +19,14 @@ Subpackages
 """
 __version__ = "0.1.0"
 
+import os as _os
+
+# The GPU engine runs one kernel per in-flight simulation, each on its own
+# stream.  HIP gives a process 4 hardware queues by default, and kernels of
+# streams that share a queue run one after another: a GV100 plan keeps 6
+# simulations in flight (profiles/r6/README.md, "Hardware queues": GPU-engine
+# suite +30 %, sweep +55 % at 8 queues).  Takes effect when the package is
+# imported before the process's first HIP call.
+_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 from .sim import SimResult, Simulator, simulate  # noqa: F401,E402

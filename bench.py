@@ -33,6 +33,10 @@ import sys
 import tempfile
 import time
 
+# hardware queues for the GPU engine's concurrent simulations (set before any
+# HIP call; accel_sim_framework_distributed_amd/__init__.py explains)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 

@@ -151,7 +151,7 @@ extern __shared__ __attribute__((aligned(16))) char g_lds[];
 // resident unit's state.  The global-state build (ASIM_GPU_STATE=global)
 // allocates only the first part: its units work on their HBM images, so many
 // engine waves share a CU.
-constexpr int kProfSlots = 48;
+constexpr int kProfSlots = 56;
 struct ProfLds {
   uint64_t last;
   uint32_t slot;

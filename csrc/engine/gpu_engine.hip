@@ -1216,7 +1216,8 @@ class GpuEngine : public Engine {
         "mem.l2", "mem.icnt", "mem.window_other", "mem.publish", "barrier", "decide", "post", "sm.issue_sched", "#slowest", "launch_rest",
         "#max_work/epoch", "#epochs(b0)", "#last_arriver_wait", "#last_arrivals", "ldst.l1_probe", "ldst.mshr_find",
         "ldst.pend_reg", "ldst.send", "recv.xbar", "recv.l1_fill", "issue.one", "issue.pick", "quiet_check", "skip",
-        "ldst.hit_push", "fill.pend_wake"};
+        "ldst.hit_push", "fill.pend_wake", "iss.pick", "iss.classify", "iss.step1", "iss.step2", "iss.step3",
+        "iss.spare53", "iss.spare54", "iss.spare55"};
     double sm[kProfSlots] = {}, mc[kProfSlots] = {}, smt = 0, mct = 0;
     for (uint32_t b = 0; b < nblocks_; ++b)
       for (int k = 0; k < kProfSlots; ++k) {
@@ -1233,6 +1234,7 @@ class GpuEngine : public Engine {
         for (int k = 36; k <= 43; ++k) cyc_clk += (double)h[(size_t)b * kProfSlots + k];
         cyc_clk += (double)h[(size_t)b * kProfSlots + 29] + (double)h[(size_t)b * kProfSlots + 46] +
                    (double)h[(size_t)b * kProfSlots + 47];
+        for (int k = 48; k <= 52; ++k) cyc_clk += (double)h[(size_t)b * kProfSlots + k];
         q_clk += (double)h[(size_t)b * kProfSlots + 44] + (double)h[(size_t)b * kProfSlots + 45];
         n_cyc += (double)h[(size_t)b * kProfSlots + 17];
         n_q += (double)h[(size_t)b * kProfSlots + 18];

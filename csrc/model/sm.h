@@ -1577,6 +1577,7 @@ SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uin
   uint32_t n_idle = 0, idle_sc = 0, first_idle = nsched;
   uint64_t picks = 0;
   uint32_t pk_of = 0xffffffffu;  // byte sc: the warp scheduler sc picked (0xff: none)
+  P::prof(48);
   for (uint32_t sc = 0; sc < nsched; ++sc) {
     const uint64_t mine = c.sched_mask[sc];
     const uint64_t cand = ready & mine;
@@ -1604,6 +1605,7 @@ SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uin
   bool classified = n_idle == 0;
   auto classify = [&]() {
     classified = true;
+    P::prof(49);
     uint64_t valid_m = 0, sbok_m = 0;
     sm_stall_masks<P>(s, c, now, live, valid_m, sbok_m);
     uint32_t n_c0 = 0, n_c1 = 0, n_c2 = 0;
@@ -1618,11 +1620,13 @@ SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uin
     if (n_c0) s.sadd(SK(issue_distro) + 0, n_c0);
     if (n_c1) s.sadd(SK(issue_distro) + 1, n_c1);
     if (n_c2) s.sadd(SK(issue_distro) + 2, n_c2);
+    P::prof(52);
   };
   if (!picks) {
     if (!classified) classify();
     return;
   }
+  P::prof(50);
   s.last_progress = now;
   s.sadd(SK(busy_cycles), 1);
   const uint64_t spec = P::ballot_m(picks, [&](int w) -> bool { return issue_special(head.self(w)); });
@@ -1667,6 +1671,7 @@ SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uin
   s.age_ctr = age;
   s.idoc_mask = idoc;
   // 2. every pipeline-issuing warp's own state, one lane per warp
+  P::prof(51);
   P::each_m(picks & ~spec, [&](int w) {
     const TInst in = head.self(w);
     s.w_head[w] = s.w_head[w] + 1u;
@@ -1691,6 +1696,7 @@ SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uin
     sbs(s.w_sb, (uint32_t)w, in.dst[1]);
   });
   P::sync();
+  P::prof(52);
   // 3. the instructions handled at issue, in scheduler order (the idle
   //    schedulers classified at the first of them)
   if (spec) {

@@ -191,6 +191,29 @@ step_stage() {
     python3 $GRAFT_REPO_ROOT/tools/engine_pmc_1sm.py --app bfs > $GRAFT_REPO_ROOT/$O/pmc_split_bfs.log 2>&1) || return 1
   python3 tools/pmc_summary.py $(find $O/pmc_split_bfs -name "*.db" | head -1) engine_kernel | tee $O/pmc_split_bfs.json
 }
+step_queues() {
+  # hardware queues per process (GPU_MAX_HW_QUEUES, HIP default 4): kernels of
+  # more streams than queues share a queue and run one after another
+  for q in 4 8 12; do
+    GPU_MAX_HW_QUEUES=$q timeout -k 10 240 python3 tools/batch_scaling.py --app hotspot --n 4,6,8 > $O/queues_scaling_q$q.jsonl 2> $O/queues_q$q.err || { tail $O/queues_q$q.err; return 1; }
+    cat $O/queues_scaling_q$q.jsonl
+    GPU_MAX_HW_QUEUES=$q timeout -k 10 300 python3 bench.py --engine gpu --steps 2 --warmup 1 > $O/queues_bench_gpu_q$q.json 2>> $O/queues_q$q.err || { tail $O/queues_q$q.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/queues_bench_gpu_q$q.json')); print('q$q gpu-only', d['value'], d['ms_per_step'])"
+    GPU_MAX_HW_QUEUES=$q timeout -k 10 400 python3 bench.py --sweep --engine gpu --steps 1 --warmup 0 > $O/queues_sweep_gpu_q$q.json 2>> $O/queues_q$q.err || { tail $O/queues_q$q.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/queues_sweep_gpu_q$q.json')); print('q$q sweep gpu', d['value'], d['ms_per_step'])"
+  done
+}
+step_queues2() {
+  # node bench at 4 vs 8 queues (A/B/A/B in one call); 4 blocks per CU (no margin) at 8 queues
+  for q in 4 8 4 8; do
+    GPU_MAX_HW_QUEUES=$q timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 > $O/queues_node_q$q.json 2>> $O/queues2.err || { tail $O/queues2.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/queues_node_q$q.json')); print('q$q node', d['value'], d['ms_per_step'], d.get('gpu_engine',{}).get('insn_share'))"
+  done
+  ASIM_GPU_BLOCKS_PER_CU=4 timeout -k 10 300 python3 bench.py --engine gpu --steps 2 --warmup 1 > $O/queues_bench_gpu_bpc4.json 2>> $O/queues2.err || { tail $O/queues2.err; return 1; }
+  python3 -c "import json; d=json.load(open('$O/queues_bench_gpu_bpc4.json')); print('bpc4 gpu-only', d['value'], d['ms_per_step'])"
+  ASIM_GPU_BLOCKS_PER_CU=4 timeout -k 10 400 python3 bench.py --sweep --engine gpu --steps 1 --warmup 0 > $O/queues_sweep_gpu_bpc4.json 2>> $O/queues2.err || { tail $O/queues2.err; return 1; }
+  python3 -c "import json; d=json.load(open('$O/queues_sweep_gpu_bpc4.json')); print('bpc4 sweep gpu', d['value'], d['ms_per_step'])"
+}
 step_tests() {
   timeout -k 10 1000 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; return 1; }
   tail -3 $O/pytest_gpu.log
