@@ -25,8 +25,22 @@ import os as _os
 # stream.  HIP gives a process 4 hardware queues by default, and kernels of
 # streams that share a queue run one after another: a GV100 plan keeps 6
 # simulations in flight (profiles/r6/README.md, "Hardware queues": GPU-engine
-# suite +30 %, sweep +55 % at 8 queues).  Takes effect when the package is
-# imported before the process's first HIP call.
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# suite +30 %, sweep +55 % at 8 queues).  ASIM_GPU_HW_QUEUES (default 8, 0:
+# leave the variable alone) raises GPU_MAX_HW_QUEUES to at least that many;
+# takes effect when the package is imported before the process's first HIP
+# call.
+
+
+def _raise_hw_queues() -> None:
+    try:
+        want = int(_os.environ.get("ASIM_GPU_HW_QUEUES", "8") or 0)
+        have = int(_os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)
+    except ValueError:
+        return
+    if want > 0 and have < want:
+        _os.environ["GPU_MAX_HW_QUEUES"] = str(min(want, 32))
+
+
+_raise_hw_queues()
 
 from .sim import SimResult, Simulator, simulate  # noqa: F401,E402

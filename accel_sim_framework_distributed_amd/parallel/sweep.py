@@ -63,6 +63,7 @@ class SweepRunner:
         self.jobs = [(a, kl, cname, flags) for (a, kl) in suite.apps if a != "dp-step"
                      for cname, flags in self.configs]
         self.ratio: Dict[str, float] = {}
+        self.cpu_s: Dict[str, float] = {}  # calibration: one host core's time per application
         self.last: Dict = {}
 
     def calibrate(self) -> Dict[str, float]:
@@ -79,7 +80,21 @@ class SweepRunner:
                     self._run(a, kl, {}, eng)
                     t[eng] = time.perf_counter() - t0
                 self.ratio[a] = t["gpu"] / max(t["cpu"], 1e-9)
+                self.cpu_s[a] = t["cpu"]
         return dict(self.ratio)
+
+    def gpu_takes(self, job, rest, cslots: int) -> bool:
+        """Node placement at the queue's GPU end: a GPU slot takes `job` while
+        the GPU would finish it no later than the host cores would get to it
+        and finish it themselves (one core's time, or the time the cores need
+        for everything still queued, whichever is longer).  Near the end of a
+        sweep the host cores run out of work first; a slow GPU job taken then
+        would be the step's tail."""
+        if cslots <= 0 or job[0] not in self.cpu_s:
+            return True
+        cpu = self.cpu_s[job[0]]
+        drain = sum(self.cpu_s.get(j[0], cpu) for j in rest) / cslots
+        return self.ratio.get(job[0], 1.0) * cpu <= max(cpu, drain)
 
     def _run(self, app: str, kl: str, flags: Dict[str, str], eng: str):
         s = self.suite
@@ -110,6 +125,8 @@ class SweepRunner:
                 with lock:
                     if not q:
                         return
+                    if eng == "gpu" and mode == "node" and not self.gpu_takes(q[0], q, cslots):
+                        return  # the rest goes to the host cores
                     job = q.pop(0) if eng == "gpu" else q.pop()
                 try:
                     i, c = self._run(job[0], job[1], job[3], eng)

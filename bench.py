@@ -33,9 +33,25 @@ import sys
 import tempfile
 import time
 
-# hardware queues for the GPU engine's concurrent simulations (set before any
-# HIP call; accel_sim_framework_distributed_amd/__init__.py explains)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+
+def _gpu_env(sweep: bool) -> None:
+    """GPU-engine settings, applied before the process's first HIP call.
+    Hardware queues: one kernel per in-flight simulation, and kernels of
+    streams sharing a queue run one after another
+    (accel_sim_framework_distributed_amd/__init__.py).  The sweep is a
+    throughput job (16 configurations x 10 apps): there the split build runs
+    two engine waves per SIMD (ASIM_GPU_SPLIT_WAVES=2, engine_k_split2.hip),
+    16 simulations in flight on 16 queues -- sweep GPU engine 50.3k -> 55.3k
+    sim KIPS on one box, while the 11-app suite, whose 11 simulations never
+    fill the GPU, is faster at one wave per SIMD (63.1k vs 60.0k)
+    (profiles/r6/README.md, "Two engine waves per SIMD")."""
+    if sweep:
+        os.environ.setdefault("ASIM_GPU_SPLIT_WAVES", "2")
+        os.environ.setdefault("ASIM_GPU_HW_QUEUES", "16")
+    want = int(os.environ.get("ASIM_GPU_HW_QUEUES", "8") or 0)
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < want:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, want))
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -167,6 +183,7 @@ def _sweep(a, suite, engine, rank, world, use_cuda) -> int:
                        "gpu_over_cpu_time_ratio": {k: round(v, 3) for k, v in ratio.items()}},
             "gpu_engine": {"kips_whole_node": round(gpu_all / max(dt_max, 1e-9) / 1e3, 1),
                            "insn_share": round(gpu_all / max(insn_all, 1), 4),
+                           "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0),
                            "jobs": sum(p["jobs_gpu"] for p in per_rank)},
             "cpu_engine": {"kips_whole_node": round((insn_all - gpu_all) / max(dt_max, 1e-9) / 1e3, 1),
                            "jobs": sum(p["jobs_cpu"] for p in per_rank)},
@@ -192,6 +209,7 @@ def _baseline_parts(kips, gpu_kips, suite, engine, world):
 
 def main() -> int:
     a = _parse()
+    _gpu_env(bool(a.sweep))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -382,7 +400,8 @@ def main() -> int:
                            "insn_share": round(gpu_all / max(insn_all, 1.0), 4),
                            "apps_on_gpu": (sum(1 for v in suite.assignment.values() if v == "gpu")
                                            if engine == "node" else (len(suite.apps) if engine == "gpu" else 0)),
-                           "apps": len(suite.apps)},
+                           "apps": len(suite.apps),
+                           "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)},
             "per_rank": per_rank,
             "plans_identical": plans_identical,
             "wall_s_spread": {"min": min(walls), "max": max(walls)},

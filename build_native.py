@@ -43,7 +43,7 @@ CORE_SRC = [
     "csrc/parallel/linksim.cc",
 ]
 HIP_SRC = ["csrc/engine/gpu_engine.hip", "csrc/engine/engine_k_lds.hip", "csrc/engine/engine_k_prof.hip",
-           "csrc/engine/engine_k_global.hip", "csrc/engine/engine_k_split.hip", "csrc/engine/ingest_mfma.hip"]
+           "csrc/engine/engine_k_global.hip", "csrc/engine/engine_k_split.hip", "csrc/engine/engine_k_split2.hip", "csrc/engine/ingest_mfma.hip"]
 STUB_SRC = ["csrc/engine/gpu_stub.cc"]
 
 

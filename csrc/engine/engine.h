@@ -152,8 +152,9 @@ inline uint32_t backlog_cap(const SimCfg& c) {
 
 struct EngineStateHeader {
   uint64_t magic = 0x41534d5354415445ull;  // "ASMSTATE"
-  uint64_t version = 7;  // 4: kernel slots (concurrent kernels); 5: MALL lines; 6: link reservations;
-                         // 7: DRAM queue bound (ChanState::q_hi), router deadlock statistics word
+  uint64_t version = 8;  // 4: kernel slots (concurrent kernels); 5: MALL lines; 6: link reservations;
+                         // 7: DRAM queue bound (ChanState::q_hi), router deadlock statistics word;
+                         // 8: SMState instruction window / packet queues after the hot prefix
   uint64_t n_sm = 0, n_mem = 0, sm_bytes = 0, ch_bytes = 0, pub_bytes = 0;
   uint64_t box_req = 0, cnt_req = 0, box_rep = 0, cnt_rep = 0;  // element counts per parity
   uint64_t ovf = 0;                                              // arrival backlog packets (all sub-partitions)

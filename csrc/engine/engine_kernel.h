@@ -81,6 +81,7 @@ struct GpuArgs {
   uint32_t max_epochs;
   uint32_t nblocks;
   uint32_t block0;  // batch launch: the simulation's first block in the grid (0 otherwise)
+  uint32_t ch_blocks;  // split build: blocks of the channels (the last ones; 0: units round-robin over all blocks)
   GpuCtl* ctl;
   uint64_t* prof;  // [nblocks][kProfSlots] shader-clock cycles per stage (profiling build)
   uint32_t* ework; // [nblocks] work clocks of the last epoch (profiling build)
@@ -295,14 +296,26 @@ __device__ __forceinline__ void engine_body(const GpuArgs& a, const uint32_t b) 
   SMState* s = reinterpret_cast<SMState*>(g_lds + kStateOff);
   ChanState* ch = reinterpret_cast<ChanState*>(g_lds + kStateOff);
   const uint32_t nunits = c.n_sm + c.n_mem;
-  const uint32_t nmine = kSliced ? (nunits - 1 - b) / a.nblocks + 1 : 1;
-  uint32_t loaded = b;  // unit whose state is in LDS (global build: the unit being simulated)
-  auto unit_k = [&](uint32_t k) { return b + k * a.nblocks; };
+  // With a.ch_blocks, the SMs spread over the first blocks and the channels
+  // over the last a.ch_blocks (several channels per block: a channel's epoch
+  // is a fraction of an SM's, so packing them leaves the critical path alone
+  // and frees CUs for other simulations); otherwise unit b + k * nblocks.
+  const uint32_t nsmb = a.nblocks - a.ch_blocks;
+  auto unit_k = [&](uint32_t k) -> uint32_t {
+    if (!a.ch_blocks) return b + k * a.nblocks;
+    return b < nsmb ? b + k * nsmb : c.n_sm + (b - nsmb) + k * a.ch_blocks;
+  };
+  const uint32_t nmine = !kSliced ? 1u
+                         : !a.ch_blocks ? (nunits - 1 - b) / a.nblocks + 1
+                         : b < nsmb ? (c.n_sm - 1 - b) / nsmb + 1
+                                    : (c.n_mem - 1 - (b - nsmb)) / a.ch_blocks + 1;
+  const uint32_t u0 = unit_k(0);
+  uint32_t loaded = u0;  // unit whose state is in LDS (global build: the unit being simulated)
   auto bind = [&](uint32_t u) {
     if (u < c.n_sm) s = as_global(&a.sms[u]);
     else ch = as_global(&a.chs[u - c.n_sm]);
   };
-  uint32_t hot = b;  // split build: the SM whose hot prefix is in LDS (~0u: none)
+  uint32_t hot = u0;  // split build: the SM whose hot prefix is in LDS (~0u: none)
   auto swap_to = [&](uint32_t u) {
     if (kGlobal) {
       bind(u);
@@ -329,16 +342,16 @@ __device__ __forceinline__ void engine_body(const GpuArgs& a, const uint32_t b) 
     loaded = u;
   };
   if (kGlobal)
-    bind(b);
-  else if (kSplit && b < c.n_sm)
-    copy_bytes(s, &a.sms[b], kSmHotBytes);
+    bind(u0);
+  else if (kSplit && u0 < c.n_sm)
+    copy_bytes(s, &a.sms[u0], kSmHotBytes);
   else if (kSplit) {
     hot = ~0u;
-    ch = as_global(&a.chs[b - c.n_sm]);
-  } else if (b < c.n_sm)
-    copy_state(s, &a.sms[b]);
+    ch = as_global(&a.chs[u0 - c.n_sm]);
+  } else if (u0 < c.n_sm)
+    copy_state(s, &a.sms[u0]);
   else
-    copy_state(ch, &a.chs[b - c.n_sm]);
+    copy_state(ch, &a.chs[u0 - c.n_sm]);
   // kernel table lives in LDS (never in scratch)
   KernelTab* ktl = reinterpret_cast<KernelTab*>(g_lds + kKtOff);
   {
@@ -532,6 +545,9 @@ __global__ void ASIM_ENGINE_KERNEL_ATTRS engine_batch_kernel(const GpuArgs* __re
 // the same for the split-state build
 __global__ void ASIM_ENGINE_KERNEL_ATTRS engine_batch_split_kernel(const GpuArgs* __restrict__ jobs,
                                                                    const uint16_t* __restrict__ block_job);
+
+// the split build at two engine waves per SIMD (engine_k_split2.hip)
+__global__ void engine_split2_kernel(GpuArgs a);
 
 // the kernel TUs' configuration uploads (one per TU: its own g_cfg)
 #define ASIM_ENGINE_CFG_UPLOAD(name)                                                         \

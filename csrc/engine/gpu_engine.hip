@@ -60,6 +60,7 @@ hipError_t engine_upload_cfg_lds(const SimCfg& c, int slot);
 hipError_t engine_upload_cfg_prof(const SimCfg& c, int slot);
 hipError_t engine_upload_cfg_global(const SimCfg& c, int slot);
 hipError_t engine_upload_cfg_split(const SimCfg& c, int slot);
+hipError_t engine_upload_cfg_split2(const SimCfg& c, int slot);
 
 namespace {
 
@@ -158,6 +159,12 @@ int gpu_state_mode() {
   return v == "global" ? kModeGlobal : v == "lds" ? kModeLds : kModeSplit;
 }
 bool gpu_state_global() { return gpu_state_mode() == kModeGlobal; }
+// ASIM_GPU_SPLIT_WAVES=2: the split build's two-waves-per-SIMD kernel
+// (engine_k_split2.hip); 1 (default): one wave per SIMD, all registers
+int split_waves() {
+  const char* e = getenv("ASIM_GPU_SPLIT_WAVES");
+  return e && atoi(e) == 2 ? 2 : 1;
+}
 int g_occ_api = 0;  // the occupancy API's blocks per CU of the last mode asked (diagnostics)
 // blocks of one mode's kernel per CU (cached per mode; needs a current device)
 uint32_t mode_blocks_per_cu(int mode) {
@@ -168,7 +175,8 @@ uint32_t mode_blocks_per_cu(int mode) {
   if (!cache[mode]) {
     int occ = 0;
     const void* f = mode == kModeGlobal ? (const void*)engine_batch_kernel
-                                        : (const void*)engine_kernel<WavePar, true, kModeSplit>;
+                    : split_waves() == 2 ? (const void*)engine_split2_kernel
+                                         : (const void*)engine_kernel<WavePar, true, kModeSplit>;
     const size_t lds = mode == kModeGlobal ? kLdsBytesGlobal : kLdsBytesSplit;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, 64, (int)lds) != hipSuccess) occ = 2;
     g_occ_api = occ;
@@ -180,6 +188,28 @@ uint32_t mode_blocks_per_cu(int mode) {
   return cache[mode];
 }
 uint32_t global_blocks_per_cu() { return mode_blocks_per_cu(kModeGlobal); }
+// Blocks of one simulation and, of them, the channels' (GpuArgs::ch_blocks).
+// One block per unit while the units fit `cap` blocks; larger configs time-
+// slice several units per block.  The split build can pack
+// ASIM_GPU_CH_PER_BLOCK channels per block (a GV100 simulation then takes 96
+// blocks instead of 112 with 2): off by default -- with the channels in HBM a
+// channel pair lengthens the epoch, GPU-engine suite 52.0k -> 42.5k sim KIPS
+// at 2 per block (profiles/r6/README.md).
+struct BlockPlan {
+  uint32_t nblocks, ch_blocks;
+};
+BlockPlan block_plan(uint32_t n_sm, uint32_t n_mem, int mode, uint32_t cap) {
+  BlockPlan p{n_sm + n_mem, 0};
+  if (mode == kModeSplit && n_sm > 0 && n_mem > 0) {
+    uint32_t pack = 1;
+    if (const char* e = getenv("ASIM_GPU_CH_PER_BLOCK"))
+      if (atoi(e) > 0) pack = (uint32_t)atoi(e);
+    const uint32_t chb = (n_mem + pack - 1) / pack;
+    if (pack > 1 && n_sm + chb <= cap) p = BlockPlan{n_sm + chb, chb};
+  }
+  if (p.nblocks > cap) p = BlockPlan{cap, 0};
+  return p;
+}
 uint32_t engine_block_slots(int mode) { return kCuSlots / mode_blocks_per_cu(mode); }
 bool profiling_env() {
   const char* pe = getenv("ASIM_GPU_PROFILE");
@@ -642,12 +672,13 @@ class GpuEngine : public Engine {
     CuPool::get().init(n_cu_ * kCuSlots);
     // one block per unit while the units fit the CUs; larger configs (or a
     // smaller ASIM_GPU_BLOCKS cap) time-slice several units per block
-    nblocks_ = c.n_sm + c.n_mem;
     mode_ = gpu_state_mode();
     uint32_t cap = (uint32_t)n_cu_ * mode_blocks_per_cu(mode_);
     if (const char* eb = getenv("ASIM_GPU_BLOCKS"))
       if (atoi(eb) > 0) cap = std::min<uint32_t>(cap, (uint32_t)atoi(eb));
-    if (nblocks_ > cap) nblocks_ = cap;
+    const BlockPlan bp = block_plan(c.n_sm, c.n_mem, mode_, cap);
+    nblocks_ = bp.nblocks;
+    ch_blocks_ = bp.ch_blocks;
     global_ = mode_ == kModeGlobal;
     lds_ = global_ ? kLdsBytesGlobal : mode_ == kModeSplit ? kLdsBytesSplit : kLdsBytes;
     sliced_ = nblocks_ < c.n_sm + c.n_mem;
@@ -785,6 +816,7 @@ class GpuEngine : public Engine {
       a.max_cycle = lim.max_cycle;
       a.max_epochs = epochs_per_launch_;
       a.nblocks = nblocks_;
+      a.ch_blocks = ch_blocks_;
       a.ctl = d_ctl_;
       HIPCHECK(hipMemsetAsync(d_ctl_, 0, sizeof(GpuCtl), stream_));
       a.prof = d_prof_;
@@ -807,6 +839,8 @@ class GpuEngine : public Engine {
       hipError_t le;
       if (mode_ == kModeSplit && profiling_)
         hipLaunchKernelGGL((engine_kernel<WaveParProf, true, kModeSplit>), dim3(nblocks_), dim3(64), lds_, stream_, a);
+      else if (mode_ == kModeSplit && split_waves() == 2)
+        hipLaunchKernelGGL(engine_split2_kernel, dim3(nblocks_), dim3(64), lds_, stream_, a);
       else if (mode_ == kModeSplit)
         hipLaunchKernelGGL((engine_kernel<WavePar, true, kModeSplit>), dim3(nblocks_), dim3(64), lds_, stream_, a);
       else if (global_ && profiling_)
@@ -1108,6 +1142,7 @@ class GpuEngine : public Engine {
     HIPCHECK(engine_upload_cfg_prof(c_, cfg_slot_));
     HIPCHECK(engine_upload_cfg_global(c_, cfg_slot_));
     HIPCHECK(engine_upload_cfg_split(c_, cfg_slot_));
+    HIPCHECK(engine_upload_cfg_split2(c_, cfg_slot_));
   }
   void release() {
     auto fr = [](void* p) {
@@ -1146,6 +1181,7 @@ class GpuEngine : public Engine {
   int cfg_slot_ = -1;
   int n_cu_ = 0;
   uint32_t nblocks_ = 0;
+  uint32_t ch_blocks_ = 0;  // blocks of the packed channels (block_plan)
   size_t lds_ = 0;
   hipStream_t stream_ = nullptr;
   hipEvent_t done_ev_ = nullptr;  // blocking-sync event the launch waits on
@@ -1224,7 +1260,7 @@ class GpuEngine : public Engine {
         double v = (double)h[(size_t)b * kProfSlots + k];
         const bool counter = (k >= 17 && k <= 19) || k == 30 || (k >= 32 && k <= 35);
         if (b < c_.n_sm) { sm[k] += v / c_.n_sm; smt += counter ? 0 : v / c_.n_sm; }
-        else { mc[k] += v / c_.n_mem; mct += counter ? 0 : v / c_.n_mem; }
+        else { const double nmb = nblocks_ > c_.n_sm ? (double)(nblocks_ - c_.n_sm) : 1.0; mc[k] += v / nmb; mct += counter ? 0 : v / nmb; }
       }
     // per simulated SM cycle: the SM-cycle stages (slots 0..11) over all SM blocks
     {
@@ -1325,7 +1361,8 @@ std::map<std::string, std::map<std::string, uint64_t>> gpu_engine_modes() {
     size_t lds;
   } ms[] = {{"lds", kModeLds, (const void*)engine_kernel<WavePar, false, kModeLds>, kLdsBytes},
             {"global", kModeGlobal, (const void*)engine_batch_kernel, kLdsBytesGlobal},
-            {"split", kModeSplit, (const void*)engine_kernel<WavePar, true, kModeSplit>, kLdsBytesSplit}};
+            {"split", kModeSplit, (const void*)engine_kernel<WavePar, true, kModeSplit>, kLdsBytesSplit},
+            {"split2", kModeSplit, (const void*)engine_split2_kernel, kLdsBytesSplit}};
   for (const auto& m : ms) {
     auto& o = out[m.name];
     o["lds_bytes"] = m.lds;
@@ -1359,9 +1396,11 @@ std::map<std::string, uint64_t> gpu_batch_stats() {
 // concurrency of job-level parallelism on one GPU, multi_gpu.py)
 int gpu_cus_per_sim(uint32_t n_sm, uint32_t n_mem) {
   const int m = gpu_state_mode();
-  uint32_t nb = n_sm + n_mem;
   const int cus = gpu_cu_count();
-  if (cus > 0) nb = std::min<uint32_t>(nb, (uint32_t)cus * mode_blocks_per_cu(m));
+  uint32_t cap = cus > 0 ? (uint32_t)cus * mode_blocks_per_cu(m) : n_sm + n_mem;
+  if (const char* eb = getenv("ASIM_GPU_BLOCKS"))
+    if (atoi(eb) > 0) cap = std::min<uint32_t>(cap, (uint32_t)atoi(eb));
+  const uint32_t nb = block_plan(n_sm, n_mem, m, cap).nblocks;
   const uint32_t slots = nb * engine_block_slots(m);
   return (int)((slots + kCuSlots - 1) / kCuSlots);
 }

@@ -218,11 +218,6 @@ struct alignas(16) SMState {
   uint16_t w_wait[kMaxWarps];    // counts of the pending s_waitcnt: vm | lgkm << 8 (0xff: not waited for)
   uint64_t w_sb[kMaxWarps][4];   // scoreboard: pending destination registers
   uint64_t w_issue_ok[kMaxWarps];  // first cycle the warp may issue again (-gpgpu_warp_issue_interval)
-  // decoded instructions [w_head, w_next] of each warp (slot = index & (kWin-1)):
-  // the fetched-not-issued ones plus the next fetch's target (its PC feeds the
-  // instruction cache).  Filled from the trace at fetch / CTA launch (LDS DMA
-  // on the GPU), so the issue path never waits on HBM.
-  TInst w_win[kMaxWarps][kWin];
   uint8_t w_slot_used[kMaxWarps];  // bitmask of used load slots
   uint8_t w_slot_lds[kMaxWarps];   // load slots holding an LDS load (lgkmcnt, not vmcnt)
   uint8_t w_lds_st[kMaxWarps];     // LDS stores in flight (lgkmcnt)
@@ -272,20 +267,15 @@ struct alignas(16) SMState {
   uint64_t skipped_cycles;  // quiet cycles fast-forwarded inside epochs (diagnostic)
   uint64_t min_emit;        // earliest arrival time (fs) of the packets injected this epoch
   // ---- interconnect endpoints ----
-  Pkt outq[kOutQ];
   uint32_t outq_head, outq_n;
   uint32_t outstanding;     // packets awaiting a reply
   uint32_t pub_nz;          // bit p: the request cells of mailbox parity p were last written with packets
   uint32_t ocnt[kMaxSubTot]; // packets put into each destination's outbox cell this epoch
-  Pkt inq[kInQ];
   uint32_t inq_head, inq_n;
   // reply path: cluster ejection buffer -> LD/ST response FIFO (sm_receive)
   Pkt rsp_cl[kEjectQ];
   Pkt rsp_ld[kLdstRespQ];
   uint32_t cl_head, cl_n, ld_head, ld_n;
-  uint64_t skey[kInQ];       // gather scratch
-  uint32_t sref[kInQ];
-  uint32_t srank[kInQ > kMaxSubTot ? kInQ : kMaxSubTot];
   // replicated kernel dispatch state (identical in every SM): per slot, the
   // uid the SM initialised it for and the next CTA to hand out
   uint32_t k_uid[kMaxConc];
@@ -299,6 +289,17 @@ struct alignas(16) SMState {
   // GPU engine's split-state build keeps the fields above in LDS and these
   // in the unit's HBM image (csrc/engine/sm_split.h SmSplit) ----
   alignas(16) uint8_t wb_cnt[kWbRing];
+  // decoded instructions [w_head, w_next] of each warp (slot = index & (kWin-1)):
+  // the fetched-not-issued ones plus the next fetch's target (its PC feeds the
+  // instruction cache).  Filled from the trace at fetch / CTA launch (LDS DMA
+  // in the LDS-state build; the split build reads them from the unit's HBM
+  // image, an L2-resident line per warp, to keep a block's LDS at ~19 KB)
+  TInst w_win[kMaxWarps][kWin];
+  Pkt outq[kOutQ];  // interconnect injection queue (outq_head / outq_n above)
+  Pkt inq[kInQ];    // arrived packets not yet ejected (inq_head / inq_n above)
+  uint64_t skey[kInQ];  // gather scratch
+  uint32_t sref[kInQ];
+  uint32_t srank[kInQ > kMaxSubTot ? kInQ : kMaxSubTot];
   WbEnt wb[kWbRing][kWbSlot];
   uint8_t hit_cnt[kHitRing];
   HitEnt hit[kHitRing][kHitSlot];

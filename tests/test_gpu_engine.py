@@ -467,5 +467,9 @@ def test_split_state_kernel_resources(gpu_mod):
     m = gpu_mod.gpu_engine_modes()
     assert m["split"]["lds_bytes"] <= 40 * 1024
     assert m["split"]["occupancy_api"] >= 4 and m["split"]["blocks_per_cu"] >= 3
+    # the hot prefix (instruction window and packet queues in HBM) fits eight
+    # blocks' LDS in a CU: the two-waves-per-SIMD kernel reaches 8 per CU
+    assert m["split"]["sm_hot_bytes"] <= 17 * 1024 and m["split"]["lds_bytes"] <= 20 * 1024
+    assert m["split2"]["occupancy_api"] >= 8
     assert m["lds"]["blocks_per_cu"] == 1 and m["lds"]["lds_bytes"] > m["lds"]["sm_state_bytes"]
     assert gpu_mod.gpu_cus_per_sim(80, 32) <= 38  # split is the default build

@@ -38,3 +38,21 @@ def test_job_launching_registry_mappings_match_the_sweep():
     for k in ("32B", "256B"):
         assert y[k]["extra_params"] == "-gpgpu_mem_addr_mapping " + EXTRA_FLAGS[k]["-gpgpu_mem_addr_mapping"]
     assert y["GPU_ENGINE"]["extra_params"] == "-sim_engine gpu"
+
+
+def test_sweep_gpu_end_declines_tail_jobs():
+    """Node placement: a GPU slot stops taking jobs once the host cores would
+    finish the next one sooner than the GPU (the step's tail)."""
+    from accel_sim_framework_distributed_amd.parallel.sweep import SweepRunner
+    r = SweepRunner.__new__(SweepRunner)
+    r.ratio = {"fast": 0.5, "slow": 4.0}
+    r.cpu_s = {"fast": 1.0, "slow": 1.0}
+    job = lambda a: (a, None, "c", {})
+    many = [job("slow")] * 40
+    # plenty queued for 4 host cores (drain 10 s): a 4 s GPU job is worth taking
+    assert r.gpu_takes(job("slow"), many, cslots=4)
+    # two left for 4 cores (drain 0.5 s): the host core takes it in 1 s, the GPU in 4 s
+    assert not r.gpu_takes(job("slow"), many[:2], cslots=4)
+    # GPU-friendly jobs always go to the GPU; GPU-only sweeps never decline
+    assert r.gpu_takes(job("fast"), [job("fast")], cslots=4)
+    assert r.gpu_takes(job("slow"), [job("slow")], cslots=0)

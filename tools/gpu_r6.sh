@@ -214,6 +214,61 @@ step_queues2() {
   ASIM_GPU_BLOCKS_PER_CU=4 timeout -k 10 400 python3 bench.py --sweep --engine gpu --steps 1 --warmup 0 > $O/queues_sweep_gpu_bpc4.json 2>> $O/queues2.err || { tail $O/queues2.err; return 1; }
   python3 -c "import json; d=json.load(open('$O/queues_sweep_gpu_bpc4.json')); print('bpc4 sweep gpu', d['value'], d['ms_per_step'])"
 }
+step_chpack() {
+  # channels per block of the split build (ASIM_GPU_CH_PER_BLOCK, block_plan in gpu_engine.hip)
+  timeout -k 10 600 $PT tests/test_gpu_engine.py -k "split or rodinia_app or snapshot or batch" > $O/pytest_chpack.log 2>&1 || { tail -30 $O/pytest_chpack.log; return 1; }
+  tail -2 $O/pytest_chpack.log
+  for p in 1 2 4; do
+    ASIM_GPU_CH_PER_BLOCK=$p timeout -k 10 240 python3 tools/batch_scaling.py --app hotspot --n 6,8 > $O/chpack_scaling_p$p.jsonl 2> $O/chpack_p$p.err || { tail $O/chpack_p$p.err; return 1; }
+    cat $O/chpack_scaling_p$p.jsonl
+    ASIM_GPU_CH_PER_BLOCK=$p timeout -k 10 300 python3 bench.py --engine gpu --steps 2 --warmup 1 > $O/chpack_bench_gpu_p$p.json 2>> $O/chpack_p$p.err || { tail $O/chpack_p$p.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/chpack_bench_gpu_p$p.json')); print('p$p gpu-only', d['value'], d['ms_per_step'])"
+    ASIM_GPU_CH_PER_BLOCK=$p timeout -k 10 400 python3 bench.py --sweep --engine gpu --steps 1 --warmup 0 > $O/chpack_sweep_gpu_p$p.json 2>> $O/chpack_p$p.err || { tail $O/chpack_p$p.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/chpack_sweep_gpu_p$p.json')); print('p$p sweep gpu', d['value'], d['ms_per_step'])"
+  done
+}
+step_chpack2() {
+  # channels per block at the package's default 8 hardware queues (A/B/A/B)
+  for p in 1 2 1 2; do
+    ASIM_GPU_CH_PER_BLOCK=$p timeout -k 10 300 python3 bench.py --engine gpu --steps 2 --warmup 1 > $O/chpack_q8_bench_gpu_p$p.json 2>> $O/chpack2.err || { tail $O/chpack2.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/chpack_q8_bench_gpu_p$p.json')); print('p$p gpu-only', d['value'], d['ms_per_step'], 'queues', d['gpu_engine'].get('hw_queues'))"
+  done
+  for p in 1 2; do
+    ASIM_GPU_CH_PER_BLOCK=$p timeout -k 10 400 python3 bench.py --sweep --engine gpu --steps 1 --warmup 0 > $O/chpack_q8_sweep_gpu_p$p.json 2>> $O/chpack2.err || { tail $O/chpack2.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/chpack_q8_sweep_gpu_p$p.json')); print('p$p sweep gpu', d['value'], d['ms_per_step'], 'queues', d['gpu_engine'].get('hw_queues'))"
+  done
+}
+step_split2w() {
+  # the split build at two waves per SIMD (ASIM_GPU_SPLIT_WAVES=2, engine_k_split2.hip) vs one
+  timeout -k 10 120 python3 -c "
+import json; from accel_sim_framework_distributed_amd import _native
+m = _native.load(); print(json.dumps(m.gpu_engine_modes()))" > $O/engine_modes_split2.json || return 1
+  cat $O/engine_modes_split2.json
+  ASIM_GPU_SPLIT_WAVES=2 timeout -k 10 600 $PT tests/test_gpu_engine.py -k "split or rodinia_app or snapshot" > $O/pytest_split2w.log 2>&1 || { tail -30 $O/pytest_split2w.log; return 1; }
+  tail -2 $O/pytest_split2w.log
+  for w in 1 2; do
+    ASIM_GPU_SPLIT_WAVES=$w timeout -k 10 120 python3 tools/engine_pmc_1sm.py --app hotspot > $O/one_sm_split_w$w.txt 2>&1 || { tail $O/one_sm_split_w$w.txt; return 1; }
+    grep -v amdgpu.ids $O/one_sm_split_w$w.txt | head -3
+  done
+  for cfg in "1 8" "2 8" "2 16" "1 16"; do
+    set -- $cfg
+    ASIM_GPU_SPLIT_WAVES=$1 ASIM_GPU_HW_QUEUES=$2 timeout -k 10 300 python3 bench.py --engine gpu --steps 2 --warmup 1 > $O/split2w_bench_gpu_w$1_q$2.json 2>> $O/split2w.err || { tail $O/split2w.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/split2w_bench_gpu_w$1_q$2.json')); print('w$1 q$2 gpu-only', d['value'], d['ms_per_step'], d['gpu_engine'].get('hw_queues'))"
+    ASIM_GPU_SPLIT_WAVES=$1 ASIM_GPU_HW_QUEUES=$2 timeout -k 10 400 python3 bench.py --sweep --engine gpu --steps 1 --warmup 0 > $O/split2w_sweep_gpu_w$1_q$2.json 2>> $O/split2w.err || { tail $O/split2w.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/split2w_sweep_gpu_w$1_q$2.json')); print('w$1 q$2 sweep gpu', d['value'], d['ms_per_step'], d['config'].get('gpu_slots'))"
+  done
+}
+step_sweep2w() {
+  # node sweep (BASELINE config #5 shape), one vs two engine waves per SIMD, A/B/A/B
+  timeout -k 10 300 $PT tests/test_gpu_engine.py -k "kernel_resources" > $O/pytest_resources.log 2>&1 || { tail -30 $O/pytest_resources.log; return 1; }
+  tail -2 $O/pytest_resources.log
+  for cfg in "1 8" "2 16" "1 8" "2 16"; do
+    set -- $cfg
+    ASIM_GPU_SPLIT_WAVES=$1 ASIM_GPU_HW_QUEUES=$2 timeout -k 10 400 python3 bench.py --sweep --steps 3 --warmup 1 > $O/sweep2w_node_w$1.json 2>> $O/sweep2w.err || { tail $O/sweep2w.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/sweep2w_node_w$1.json')); print('w$1 q$2 sweep node', d['value'], d['ms_per_step'], d['config'].get('gpu_slots'), d['config'].get('cpu_slots'), d['gpu_engine'])"
+    cp $O/sweep2w_node_w$1.json $O/sweep2w_node_w$1_$RANDOM.json
+  done
+}
 step_tests() {
   timeout -k 10 1000 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; return 1; }
   tail -3 $O/pytest_gpu.log
