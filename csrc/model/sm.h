@@ -1358,14 +1358,18 @@ SIM_HDI uint32_t sched_of(uint32_t w, uint32_t nsched) {
 // can warp `w` issue its next instruction this cycle (scoreboard, flags,
 // pipeline register and load slot availability)
 template <class S>
-SIM_HDI bool warp_can_issue_i(const S& s, const SimCfg& c, int w, const TInst& in, uint32_t nsched,
-                              uint64_t idoc_busy) {
+SIM_HDI bool warp_sb_ok(const S& s, int w, const TInst& in) {
+  for (int j = 0; j < 5; ++j)
+    if (sbt(s.w_sb, w, in.src[j])) return false;
+  return !sbt(s.w_sb, w, in.dst[0]) && !sbt(s.w_sb, w, in.dst[1]);
+}
+// warp_can_issue_i without the scoreboard test (warp_sb_ok)
+template <class S>
+SIM_HDI bool warp_can_issue_nosb(const S& s, const SimCfg& c, int w, const TInst& in, uint32_t nsched,
+                                 uint64_t idoc_busy) {
   uint8_t f = s.w_flags[w];
   if (!(f & WF_ACTIVE) || (f & (WF_EXITING | WF_BARRIER | WF_MEMBAR | WF_WAITCNT))) return false;
   if (s.w_ibuf[w] == 0) return false;
-  for (int j = 0; j < 5; ++j)
-    if (sbt(s.w_sb, w, in.src[j])) return false;
-  if (sbt(s.w_sb, w, in.dst[0]) || sbt(s.w_sb, w, in.dst[1])) return false;
   uint32_t u = unit_of(c, in.cls);
   uint32_t sc = sched_of((uint32_t)w, nsched);
   if (in.cls == OC_EXIT || in.cls == OC_BARRIER || in.cls == OC_MEMBAR || in.cls == OC_NOP || (in.flags & F_WAITCNT))
@@ -1373,6 +1377,11 @@ SIM_HDI bool warp_can_issue_i(const S& s, const SimCfg& c, int w, const TInst& i
   if (idoc_busy >> (sc * U_COUNT + u) & 1ull) return false;
   if (u == U_MEM && in.cls == OC_LOAD && s.w_slot_used[w] == 0xff) return false;
   return true;
+}
+template <class S>
+SIM_HDI bool warp_can_issue_i(const S& s, const SimCfg& c, int w, const TInst& in, uint32_t nsched,
+                              uint64_t idoc_busy) {
+  return warp_can_issue_nosb(s, c, w, in, nsched, idoc_busy) && warp_sb_ok(s, w, in);
 }
 template <class S>
 SIM_HDI bool warp_can_issue(const S& s, const SimCfg& c, const KernelTab& kt, int w, uint32_t nsched,
@@ -1571,7 +1580,8 @@ SIM_HDI bool issue_special(const TInst& in) {
 // schedulers one after another; so does sm_issue below for the other
 // policies.)
 template <class P, class S, class H>
-SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uint64_t ready, uint64_t live) {
+SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uint64_t ready, uint64_t live,
+                          uint64_t sbok_all) {
   const SimCfg& c = *x.cfg;
   const int nw = (int)amin<uint32_t>(c.max_warps_per_sm, kMaxWarps);
   const uint32_t nsched = c.n_sched ? c.n_sched : 1;
@@ -1607,8 +1617,16 @@ SIM_HDI void sm_issue_par(S& s, const SmCtx& x, uint64_t now, const H& head, uin
   auto classify = [&]() {
     classified = true;
     P::prof(49);
-    uint64_t valid_m = 0, sbok_m = 0;
-    sm_stall_masks<P>(s, c, now, live, valid_m, sbok_m);
+    // the scoreboard half from before the issues (sbok_all): a scheduler
+    // with nothing to issue issued nothing, so its warps' head instructions
+    // and scoreboards are unchanged; only flags (step 3's barriers, exits)
+    // are read again
+    const uint64_t valid_m = P::ballot_m(live, [&](int w) -> bool {
+      const uint8_t f = s.w_flags[w];
+      return (f & WF_ACTIVE) && !(f & (WF_EXITING | WF_BARRIER | WF_MEMBAR | WF_WAITCNT)) && s.w_ibuf[w] != 0 &&
+             warp_issue_due(s, c, w, now);
+    });
+    const uint64_t sbok_m = valid_m & sbok_all;
     uint32_t n_c0 = 0, n_c1 = 0, n_c2 = 0;
     for (uint32_t sc = 0; sc < nsched; ++sc) {
       if (!(idle_sc >> sc & 1u)) continue;
@@ -1724,16 +1742,22 @@ SIM_HDI void sm_issue(S& s, const SmCtx& x, uint64_t now) {
   const auto head = P::template lanes<TInst>(nw, [&](int w) -> TInst { return s.w_win[w][s.w_head[w] & (kWin - 1)]; });
   // readiness of every warp (lane-parallel)
   const uint64_t live = P::uni(s.live_mask);
-  uint64_t ready = P::ballot_m(live, [&](int w) -> bool {
-    return warp_can_issue_i(s, c, w, head.self(w), nsched, idoc_busy) && warp_issue_due(s, c, w, now);
-  });
   if ((c.sched_policy == SCHED_LRR || c.sched_policy == SCHED_GTO || c.sched_policy == SCHED_OLDEST ||
        c.sched_policy == SCHED_RRR) &&
       c.max_issue_per_warp <= 1 && !trace_sm_on(c, TS_WARP_SCHEDULER, s.id)) {
+    // scoreboard and the rest of readiness as two masks: the stall
+    // classification reuses the first
+    const uint64_t sbok = P::ballot_m(live, [&](int w) -> bool { return warp_sb_ok(s, w, head.self(w)); });
+    const uint64_t ready = P::ballot_m(live & sbok, [&](int w) -> bool {
+      return warp_can_issue_nosb(s, c, w, head.self(w), nsched, idoc_busy) && warp_issue_due(s, c, w, now);
+    });
     P::prof(29);
-    sm_issue_par<P>(s, x, now, head, ready, live);
+    sm_issue_par<P>(s, x, now, head, ready, live, sbok);
     return;
   }
+  uint64_t ready = P::ballot_m(live, [&](int w) -> bool {
+    return warp_can_issue_i(s, c, w, head.self(w), nsched, idoc_busy) && warp_issue_due(s, c, w, now);
+  });
   // warps parked at a barrier / fence / exit (the reference's waiting()),
   // plus for the two-level scheduler those whose next instruction waits on
   // a long (memory) operation

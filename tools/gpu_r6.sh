@@ -269,6 +269,15 @@ step_sweep2w() {
     cp $O/sweep2w_node_w$1.json $O/sweep2w_node_w$1_$RANDOM.json
   done
 }
+step_node2w() {
+  # node suite bench (the headline), one vs two engine waves per SIMD, A/B/A/B
+  for cfg in "1 8" "2 16" "1 8" "2 16"; do
+    set -- $cfg
+    ASIM_GPU_SPLIT_WAVES=$1 ASIM_GPU_HW_QUEUES=$2 timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 > $O/node2w_w$1.json 2>> $O/node2w.err || { tail $O/node2w.err; return 1; }
+    python3 -c "import json; d=json.load(open('$O/node2w_w$1.json')); print('w$1 q$2 node', d['value'], d['ms_per_step'], d['gpu_engine'])"
+    cp $O/node2w_w$1.json $O/node2w_w$1_$RANDOM.json
+  done
+}
 step_tests() {
   timeout -k 10 1000 $PT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; return 1; }
   tail -3 $O/pytest_gpu.log
