@@ -125,8 +125,12 @@ class PacketExchange:
     def run(self, params: Dict, kind: str, nbytes: int, root: int, start_ps: int) -> Dict:
         """One collective.  The epoch loop runs natively (csrc/parallel/
         exchange.cc over the group's c10d ProcessGroup, GIL released) unless
-        ``ASIM_NATIVE_EXCHANGE=0`` or the extension is not built; both loops
-        implement the same protocol and give identical results."""
+        ``ASIM_NATIVE_EXCHANGE=0`` or the extension is not built; on a GPU
+        backend it is device-resident (csrc/parallel/linksim_dev.hip: the
+        LinkSim state in HBM, one epoch kernel and one RCCL all-to-all of device
+        buffers per epoch, status read every few epochs) unless
+        ``ASIM_DEVICE_EXCHANGE=0``.  All loops implement the same protocol and
+        give identical results."""
         import os
         dist_ext = _native.load_dist() if os.environ.get("ASIM_NATIVE_EXCHANGE", "1") != "0" else None
         if dist_ext is not None:
@@ -134,8 +138,16 @@ class PacketExchange:
             dev = self.device.index if self.device.type == "cuda" else -1
             if dev is None:
                 dev = self.torch.cuda.current_device()
-            r = dist_ext.exchange_run(pg, {k: v for k, v in params.items()}, kind, int(nbytes), int(root),
-                                      int(start_ps), int(dev))
+            pr = {k: v for k, v in params.items()}
+            if dev >= 0 and os.environ.get("ASIM_DEVICE_EXCHANGE", "1") != "0":
+                # device-resident loop: LinkSim state in HBM, one epoch kernel +
+                # one RCCL all-to-all of device buffers per epoch, no host bounce
+                r = dist_ext.exchange_run_device(pg, pr, kind, int(nbytes), int(root), int(start_ps), int(dev),
+                                                 int(os.environ.get("ASIM_DEVICE_EXCHANGE_BATCH", "16")))
+                self.stats["device_loop"] = True
+                self.stats["polls"] = self.stats.get("polls", 0) + int(r["polls"])
+            else:
+                r = dist_ext.exchange_run(pg, pr, kind, int(nbytes), int(root), int(start_ps), int(dev))
             for k in ("epochs", "packets", "exchanges"):
                 self.stats[k] += int(r[k])
             self.stats["native_loop_s"] = self.stats.get("native_loop_s", 0.0) + float(r["loop_s"])

@@ -207,13 +207,26 @@ def build_dist_ext(verbose: bool = False) -> str:
     """The native epoch loop of the packet collective (csrc/parallel/exchange.cc)
     as a torch C++ extension (it calls c10d::ProcessGroup), built in-tree:
     accel_sim_framework_distributed_amd/_asim_dist.so."""
+    import torch
     from torch.utils.cpp_extension import load
+    torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib")
     bdir = os.path.join(ROOT, "build", "dist_ext")
     os.makedirs(bdir, exist_ok=True)
+    # the device-resident epoch loop's kernels (csrc/parallel/linksim_dev.hip),
+    # compiled by hipcc for gfx950 and linked into the extension
+    dev_src = os.path.join(ROOT, "csrc", "parallel", "linksim_dev.hip")
+    dev_obj = os.path.join(bdir, "linksim_dev.o")
+    deps = [dev_src] + [os.path.join(ROOT, "csrc", "parallel", f) for f in ("linksim_dev.h", "linksim_core.h", "linksim.h")]
+    if not os.path.exists(dev_obj) or os.path.getmtime(dev_obj) < max(os.path.getmtime(d) for d in deps):
+        hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+        subprocess.check_call([hipcc, "-std=c++17", "-O2", "-fPIC", f"--offload-arch={ARCH}",
+                               f"-I{os.path.join(ROOT, 'csrc')}", "-c", dev_src, "-o", dev_obj])
     load(name="_asim_dist", sources=[os.path.join(ROOT, "csrc", "parallel", "exchange.cc"),
                                       os.path.join(ROOT, "csrc", "parallel", "linksim.cc")],
-         build_directory=bdir, extra_cflags=["-O2", f"-I{os.path.join(ROOT, 'csrc')}"], verbose=verbose,
-         is_python_module=True)
+         build_directory=bdir, extra_cflags=["-O2", f"-I{os.path.join(ROOT, 'csrc')}", "-D__HIP_PLATFORM_AMD__=1"],
+         extra_include_paths=[os.path.join(ROCM, "include")], verbose=verbose,
+         extra_ldflags=[dev_obj, f"-L{ROCM}/lib", "-lamdhip64", f"-L{torch_lib}", "-lc10_hip"],
+         with_cuda=False, is_python_module=True)
     out = os.path.join(PKG, "_asim_dist.so")
     shutil.copy2(os.path.join(bdir, "_asim_dist.so"), out)
     return out

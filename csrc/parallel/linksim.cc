@@ -22,149 +22,89 @@ CollKind coll_kind(const std::string& n) {
   throw std::invalid_argument("packet collective model: unsupported collective '" + n + "'");
 }
 
-static int mod(int a, int n) { return ((a % n) + n) % n; }
-
-static int inv_mod(int s, int n) {
-  for (int x = 1; x < n; ++x)
-    if ((s * x) % n == 1) return x;
-  return 1;
-}
-
 LinkSim::LinkSim(const LinkParams& p, const CollSpec& c, int rank, int world, uint64_t start_ps)
-    : p_(p), c_(c), rank_(rank), world_(world), start_ps_(start_ps), finish_ps_(start_ps) {
+    : p_(p), finish_ps_(start_ps) {
   if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("LinkSim: bad rank/world");
   if (p.link_gbps <= 0 || p.reduce_gbps <= 0) throw std::invalid_argument("LinkSim: bandwidths must be > 0");
   const int N = world;
-  c_.root = mod(c.root < 0 ? 0 : c.root, N);
+  g_.kind = c.kind;
+  g_.root = ls_mod(c.root < 0 ? 0 : c.root, N);
+  g_.rank = rank;
+  g_.world = world;
   // ring strides coprime with N give disjoint rings over distinct links
+  int nst = 0;
   if (N > 1) {
     const bool ring = c.kind != CK_ALLTOALL && c.kind != CK_SENDRECV;
     const uint32_t cap = ring ? std::max<uint32_t>(1, std::min(p.links, p.max_channels)) : 1;
-    for (int s = 1; s < N && stride_.size() < cap; ++s)
-      if (std::gcd(s, N) == 1) stride_.push_back(s);
+    for (int s = 1; s < N && (uint32_t)nst < cap; ++s)
+      if (std::gcd(s, N) == 1) {
+        if (nst == kLsMaxStride) throw std::invalid_argument("LinkSim: more than 64 ring channels");
+        g_.stride[nst++] = s;
+      }
   }
-  if (stride_.empty()) stride_.push_back(1);
-  nch_ = (uint32_t)stride_.size();
+  if (nst == 0) g_.stride[nst++] = 1;
+  g_.nch = nst;
+  uint64_t chunk = 0;
   switch (c.kind) {
-    case CK_ALLREDUCE: nsteps_ = 2 * (N - 1); chunk_ = c.bytes / ((uint64_t)nch_ * N); break;
+    case CK_ALLREDUCE: g_.nsteps = 2 * (N - 1); chunk = c.bytes / ((uint64_t)nst * N); break;
     case CK_ALLGATHER:
-    case CK_REDUCESCATTER: nsteps_ = N - 1; chunk_ = c.bytes / ((uint64_t)nch_ * N); break;
+    case CK_REDUCESCATTER: g_.nsteps = N - 1; chunk = c.bytes / ((uint64_t)nst * N); break;
     case CK_BROADCAST:
-    case CK_REDUCE: nsteps_ = N - 1; chunk_ = c.bytes / nch_; break;
-    case CK_ALLTOALL: nsteps_ = N - 1; chunk_ = c.bytes / N; break;
-    case CK_SENDRECV: nsteps_ = N > 1 ? 1 : 0; chunk_ = c.bytes; break;
+    case CK_REDUCE: g_.nsteps = N - 1; chunk = c.bytes / nst; break;
+    case CK_ALLTOALL: g_.nsteps = N - 1; chunk = c.bytes / N; break;
+    case CK_SENDRECV: g_.nsteps = N > 1 ? 1 : 0; chunk = c.bytes; break;
   }
-  if (N == 1) nsteps_ = 0;
-  chunk_ = std::max<uint64_t>(chunk_, 1);
-  const uint64_t sl = std::max<uint32_t>(p.slice_bytes, 64);
-  nslices_ = (uint32_t)((chunk_ + sl - 1) / sl);
-  ps_per_byte_link_ = 1000.0 / p.link_gbps;  // GB/s == bytes/ns
-  ps_per_byte_mem_ = 1000.0 / p.reduce_gbps;
-  lat_ps_ = (uint64_t)std::llround(std::max(0.0, p.latency_ns) * 1000.0);
-  epoch_ps_ = std::max<uint64_t>(lat_ps_, 1000);
-  if (lat_ps_ < epoch_ps_) lat_ps_ = epoch_ps_;  // lookahead requires latency >= epoch
-  link_free_.assign(std::max<uint32_t>(1, p.links), start_ps);
-  for (int ch = 0; ch < (int)nch_; ++ch)
-    for (int k = 0; k < nsteps_; ++k) {
+  if (N == 1) g_.nsteps = 0;
+  g_.chunk = std::max<uint64_t>(chunk, 1);
+  g_.slice_bytes = std::max<uint32_t>(p.slice_bytes, 64);
+  g_.nslices = (uint32_t)((g_.chunk + g_.slice_bytes - 1) / g_.slice_bytes);
+  g_.ps_per_byte_link = 1000.0 / p.link_gbps;  // GB/s == bytes/ns
+  g_.ps_per_byte_mem = 1000.0 / p.reduce_gbps;
+  g_.lat_ps = (uint64_t)std::llround(std::max(0.0, p.latency_ns) * 1000.0);
+  g_.epoch_ps = std::max<uint64_t>(g_.lat_ps, 1000);
+  if (g_.lat_ps < g_.epoch_ps) g_.lat_ps = g_.epoch_ps;  // lookahead requires latency >= epoch
+  g_.nlinks = (int32_t)std::max<uint32_t>(1, p.links);
+  link_free_.assign((size_t)g_.nlinks, start_ps);
+  for (int ch = 0; ch < g_.nch; ++ch)
+    for (int k = 0; k < g_.nsteps; ++k) {
       const bool snd = send_peer(ch, k) >= 0, rcv = recv_peer(ch, k) >= 0;
-      if (snd) send_left_ += nslices_;
-      if (rcv) recv_left_ += nslices_;
-      const bool dep = k > 0 && recv_peer(ch, k - 1) >= 0 && c.kind != CK_ALLTOALL && c.kind != CK_SENDRECV;
+      if (snd) send_left_ += g_.nslices;
+      if (rcv) recv_left_ += g_.nslices;
+      const bool dep = k > 0 && recv_peer(ch, k - 1) >= 0 && ls_forwards(g_);
       if (snd && !dep)
-        for (uint32_t s = 0; s < nslices_; ++s) push_send(start_ps, ch, k, (int)s);
+        for (uint32_t s = 0; s < g_.nslices; ++s) push_send(start_ps, ch, k, (int)s);
     }
 }
 
-// position of this rank along a chain with stride s starting after `first`
-static int chain_pos(int r, int first, int s, int N) { return mod((r - first) * inv_mod(s, N), N); }
+int LinkSim::send_peer(int ch, int k) const { return ls_send_peer(g_, ch, k); }
+int LinkSim::recv_peer(int ch, int k) const { return ls_recv_peer(g_, ch, k); }
+bool LinkSim::recv_reduces(int k) const { return ls_recv_reduces(g_, k); }
 
-int LinkSim::send_peer(int ch, int k) const {
-  const int N = world_, r = rank_, s = stride_[ch];
-  if (N <= 1 || k < 0 || k >= nsteps_) return -1;
-  switch (c_.kind) {
-    case CK_ALLREDUCE:
-    case CK_ALLGATHER:
-    case CK_REDUCESCATTER: return mod(r + s, N);
-    case CK_BROADCAST: {
-      const int pos = chain_pos(r, c_.root, s, N);
-      return (k == pos && pos < N - 1) ? mod(r + s, N) : -1;
-    }
-    case CK_REDUCE: {
-      const int pos = chain_pos(r, c_.root + s, s, N);  // root is last
-      return (k == pos && pos < N - 1) ? mod(r + s, N) : -1;
-    }
-    case CK_ALLTOALL: return mod(r + k + 1, N);
-    case CK_SENDRECV: return mod(r + 1, N);
-  }
-  return -1;
-}
-
-int LinkSim::recv_peer(int ch, int k) const {
-  const int N = world_, r = rank_, s = stride_[ch];
-  if (N <= 1 || k < 0 || k >= nsteps_) return -1;
-  switch (c_.kind) {
-    case CK_ALLREDUCE:
-    case CK_ALLGATHER:
-    case CK_REDUCESCATTER: return mod(r - s, N);
-    case CK_BROADCAST: {
-      const int pos = chain_pos(r, c_.root, s, N);
-      return (pos > 0 && k == pos - 1) ? mod(r - s, N) : -1;
-    }
-    case CK_REDUCE: {
-      const int pos = chain_pos(r, c_.root + s, s, N);
-      return (pos > 0 && k == pos - 1) ? mod(r - s, N) : -1;
-    }
-    case CK_ALLTOALL: return mod(r - k - 1, N);
-    case CK_SENDRECV: return mod(r - 1, N);
-  }
-  return -1;
-}
-
-bool LinkSim::recv_reduces(int k) const {
-  switch (c_.kind) {
-    case CK_ALLREDUCE: return k < world_ - 1;
-    case CK_REDUCESCATTER:
-    case CK_REDUCE: return true;
-    default: return false;
-  }
-}
-
-uint32_t LinkSim::slice_len(int s) const {
-  const uint64_t sl = std::max<uint32_t>(p_.slice_bytes, 64);
-  const uint64_t off = (uint64_t)s * sl;
-  return (uint32_t)std::min<uint64_t>(sl, chunk_ - off);
-}
-
-int LinkSim::link_of(int dst) const {
-  const int o = mod(dst - rank_ - 1, world_);
-  return o % (int)link_free_.size();
-}
-
-void LinkSim::push_send(uint64_t t, int c, int k, int s) { ready_.push(Ready{t, c, k, s}); }
+void LinkSim::push_send(uint64_t t, int c, int k, int s) { ready_.push(LsReady{t, c, k, s, 0}); }
 
 void LinkSim::emit(uint64_t t_end, std::vector<LinkPkt>& out) {
-  std::vector<Ready> deferred;
+  std::vector<LsReady> deferred;
   while (!ready_.empty() && ready_.top().t < t_end) {
-    Ready r = ready_.top();
+    LsReady r = ready_.top();
     ready_.pop();
     const int dst = send_peer(r.chan, r.step);
-    const int l = link_of(dst);
+    const int l = ls_link_of(g_, dst);
     const uint64_t st = std::max(r.t, link_free_[l]);
     if (st >= t_end) {
       deferred.push_back(r);
       continue;
     }
-    const uint32_t b = slice_len(r.slice);
-    const uint64_t ser = (uint64_t)std::ceil(b * ps_per_byte_link_);
+    const uint32_t b = ls_slice_len(g_, r.slice);
+    const uint64_t ser = ls_ser_ps(g_, b);
     link_free_[l] = st + ser;
     LinkPkt pk;
-    pk.src = rank_;
+    pk.src = g_.rank;
     pk.dst = dst;
     pk.chan = r.chan;
     pk.step = r.step;
     pk.slice = r.slice;
     pk.bytes = b;
-    pk.arrive_ps = st + ser + lat_ps_;
+    pk.arrive_ps = st + ser + g_.lat_ps;
     out.push_back(pk);
     --send_left_;
     ++sent_;
@@ -176,19 +116,31 @@ void LinkSim::emit(uint64_t t_end, std::vector<LinkPkt>& out) {
 void LinkSim::receive(const LinkPkt* p, size_t n) {
   for (size_t i = 0; i < n; ++i) {
     const LinkPkt& pk = p[i];
-    if (pk.dst != rank_) throw std::logic_error("LinkSim: packet delivered to the wrong rank");
+    if (pk.dst != g_.rank) throw std::logic_error("LinkSim: packet delivered to the wrong rank");
     if (recv_peer(pk.chan, pk.step) != pk.src) throw std::logic_error("LinkSim: unexpected packet source");
-    const double per = recv_reduces(pk.step) ? 3.0 : 1.0;  // reduce: read mine + read recv + write
-    const uint64_t done = pk.arrive_ps + (uint64_t)std::ceil(pk.bytes * per * ps_per_byte_mem_);
+    const uint64_t done = pk.arrive_ps + ls_local_ps(g_, pk.bytes, pk.step);
     finish_ps_ = std::max(finish_ps_, done);
     --recv_left_;
     const int k1 = pk.step + 1;
-    if (c_.kind != CK_ALLTOALL && c_.kind != CK_SENDRECV && send_peer(pk.chan, k1) >= 0)
-      push_send(done, pk.chan, k1, pk.slice);
+    if (ls_forwards(g_) && send_peer(pk.chan, k1) >= 0) push_send(done, pk.chan, k1, pk.slice);
   }
 }
 
 uint64_t LinkSim::next_event() const { return ready_.empty() ? kNever : ready_.top().t; }
+
+LinkSim::Export LinkSim::export_state() const {
+  Export e;
+  e.g = g_;
+  auto q = ready_;
+  e.ready.reserve(q.size());
+  for (; !q.empty(); q.pop()) e.ready.push_back(q.top());  // ascending order: already a valid min-heap
+  e.link_free = link_free_;
+  e.recv_left = recv_left_;
+  e.send_left = send_left_;
+  e.sent = sent_;
+  e.finish_ps = finish_ps_;
+  return e;
+}
 
 std::vector<uint64_t> linksim_run_local(const LinkParams& p, const CollSpec& c, const std::vector<uint64_t>& start_ps,
                                         uint64_t* epochs, uint64_t* packets) {

@@ -22,6 +22,8 @@
 #include <string>
 #include <vector>
 
+#include "linksim_core.h"
+
 namespace asim {
 
 struct LinkParams {
@@ -65,10 +67,21 @@ class LinkSim {
   uint64_t next_event() const;
   bool done() const { return recv_left_ == 0 && send_left_ == 0; }
   uint64_t finish_ps() const { return finish_ps_; }
-  uint64_t epoch_ps() const { return epoch_ps_; }
-  uint32_t channels() const { return nch_; }
+  uint64_t epoch_ps() const { return g_.epoch_ps; }
+  uint32_t channels() const { return (uint32_t)g_.nch; }
   uint64_t packets_sent() const { return sent_; }
-  int world() const { return world_; }
+  int world() const { return g_.world; }
+
+  // the whole rank state, for the device-resident epoch loop (linksim_dev.hip)
+  // to take over: schedule geometry, pending sends (any order), link clocks,
+  // counters
+  struct Export {
+    LsGeom g;
+    std::vector<LsReady> ready;
+    std::vector<uint64_t> link_free;
+    uint64_t recv_left, send_left, sent, finish_ps;
+  };
+  Export export_state() const;
 
   // the rank's role at (channel, step): peer it sends to / receives from (-1 none)
   int send_peer(int c, int k) const;
@@ -76,32 +89,14 @@ class LinkSim {
   bool recv_reduces(int k) const;
 
  private:
-  struct Ready {
-    uint64_t t;
-    int32_t chan, step, slice;
-    bool operator>(const Ready& o) const {
-      if (t != o.t) return t > o.t;
-      if (chan != o.chan) return chan > o.chan;
-      if (step != o.step) return step > o.step;
-      return slice > o.slice;
-    }
+  struct Later {
+    bool operator()(const LsReady& a, const LsReady& b) const { return ls_before(b, a); }
   };
-  uint32_t slice_len(int s) const;
-  int link_of(int dst) const;
   void push_send(uint64_t t, int c, int k, int s);
 
   LinkParams p_;
-  CollSpec c_;
-  int rank_, world_;
-  uint64_t start_ps_;
-  uint32_t nch_ = 1;
-  std::vector<int> stride_;  // ring stride per channel
-  int nsteps_ = 0;
-  uint64_t chunk_ = 0;       // bytes per (channel, step)
-  uint32_t nslices_ = 1;
-  double ps_per_byte_link_ = 0, ps_per_byte_mem_ = 0;
-  uint64_t lat_ps_ = 0, epoch_ps_ = 0;
-  std::priority_queue<Ready, std::vector<Ready>, std::greater<Ready>> ready_;
+  LsGeom g_;
+  std::priority_queue<LsReady, std::vector<LsReady>, Later> ready_;
   std::vector<uint64_t> link_free_;
   uint64_t recv_left_ = 0, send_left_ = 0, sent_ = 0;
   uint64_t finish_ps_ = 0;

@@ -5,6 +5,7 @@
 #             of both state builds, GPU-only bench of both builds
 #   tests   : the whole GPU suite
 #   bench   : bench.py (node) + rocprofv3 kernel stats
+#   devloop : device-resident collective epoch loop: GPU tests + per-epoch cost
 # Every GPU step runs under its own timeout; the first failure ends the call.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -283,6 +284,15 @@ step_tests() {
   tail -3 $O/pytest_gpu.log
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; return 1; }
   tail -1 $O/smoke.log
+}
+step_devloop() {
+  # device-resident epoch loop of the packet collective: GPU tests, then the
+  # per-epoch cost (host-bounce RCCL, gloo, device loop over RCCL loopback)
+  timeout -k 10 300 $PT tests/test_device_exchange.py > $O/pytest_devloop.log 2>&1 || { tail -30 $O/pytest_devloop.log; return 1; }
+  tail -3 $O/pytest_devloop.log
+  timeout -k 10 300 python3 tools/rccl_epoch_cost.py --iters 1000 --out $O/devloop_epoch_cost.json > $O/devloop_epoch_cost.log 2>&1 \
+    || { tail -20 $O/devloop_epoch_cost.log; return 1; }
+  grep -v amdgpu.ids $O/devloop_epoch_cost.log | tail -6
 }
 step_bench() {
   timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 > $O/bench_node.json 2> $O/bench_node.err || { tail $O/bench_node.err; return 1; }
