@@ -16,10 +16,16 @@
 #include <c10/core/impl/VirtualGuardImpl.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/utils/pybind.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
+
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstdint>
 #include <limits>
 #include <stdexcept>
@@ -266,6 +272,40 @@ struct DevStates {
 
 [[noreturn]] void dls_fail(int32_t st) { throw std::runtime_error(std::string("device epoch loop: ") + dls_status_name(st)); }
 
+// A batch of epochs as one hipGraph (ASIM_DEVICE_EXCHANGE_GRAPH=1): the first
+// batch of `n` (all-to-all, epoch kernel) pairs is captured from the stream --
+// the collective's own stream joins the capture through its event waits -- and
+// every later batch is one graph launch, so the host pays one launch per batch
+// instead of a c10d collective call and a kernel launch per epoch.
+struct EpochGraph {
+  hipGraph_t g = nullptr;
+  hipGraphExec_t x = nullptr;
+  int64_t n = 0;
+  template <class F>
+  void run(hipStream_t st, int64_t batch, F&& one_epoch) {
+    if (!x) {
+      n = batch;
+      check_hip(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed), "begin capture");
+      for (int64_t i = 0; i < n; ++i) one_epoch();
+      check_hip(hipStreamEndCapture(st, &g), "end capture");
+      check_hip(hipGraphInstantiate(&x, g, nullptr, nullptr, 0), "instantiate");
+    }
+    check_hip(hipGraphLaunch(x, st), "graph launch");
+  }
+  static void check_hip(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("epoch graph: ") + what + ": " + hipGetErrorString(e));
+  }
+  ~EpochGraph() {
+    if (x) (void)hipGraphExecDestroy(x);
+    if (g) (void)hipGraphDestroy(g);
+  }
+};
+
+bool graph_mode() {
+  const char* e = std::getenv("ASIM_DEVICE_EXCHANGE_GRAPH");
+  return e && e[0] == '1';
+}
+
 }  // namespace
 
 py::dict exchange_run_device(py::object pgo, py::dict params, const std::string& kind, int64_t nbytes, int64_t root,
@@ -285,6 +325,10 @@ py::dict exchange_run_device(py::object pgo, py::dict params, const std::string&
   {
     py::gil_scoped_release nogil;
     const auto t0c = std::chrono::steady_clock::now();
+    // a stream of our own (the default stream cannot be captured into a
+    // graph); work the caller queued before is finished first
+    sync_stream((int)device);
+    const c10::hip::HIPStreamGuard sg(c10::hip::getStreamFromPool(false, (c10::DeviceIndex)device));
     void* stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
     S.upload({ls.export_state()}, W, kSlots, kHdr, (int)device);
     auto dopt = at::TensorOptions().dtype(at::kLong).device(at::kCUDA, device);
@@ -301,12 +345,20 @@ py::dict exchange_run_device(py::object pgo, py::dict params, const std::string&
                      t0.data_ptr<int64_t>(), DLS_MODE_FIRST, stream);
     int64_t b = 1;
     uint64_t last_epochs = 0;
+    const bool graphed = graph_mode();
+    EpochGraph graph;
     for (;;) {
-      for (int64_t i = 0; i < b; ++i) {
+      auto one_epoch = [&] {
         pg->alltoall_base(d_recv, d_send, eq, eq)->wait();
-        ++exchanges;
         dls_launch_epoch(S.base(), S.L, 1, d_recv.data_ptr<int64_t>(), slot, 0, d_send.data_ptr<int64_t>(), 0, nullptr,
                          nullptr, nullptr, DLS_MODE_NEXT, stream);
+      };
+      if (graphed) {
+        graph.run((hipStream_t)stream, std::max<int64_t>(1, batch_max), one_epoch);
+        exchanges += (uint64_t)graph.n;
+      } else {
+        for (int64_t i = 0; i < b; ++i) one_epoch();
+        exchanges += (uint64_t)b;
       }
       S.poll();
       ++polls;
@@ -382,6 +434,10 @@ py::dict dev_run_local(py::dict params, const std::string& kind, int64_t nbytes,
   DevStates S;
   {
     py::gil_scoped_release nogil;
+    // a stream of our own (the default stream cannot be captured into a
+    // graph); work the caller queued before is finished first
+    sync_stream((int)device);
+    const c10::hip::HIPStreamGuard sg(c10::hip::getStreamFromPool(false, (c10::DeviceIndex)device));
     void* stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
     S.upload(ex, W, kSlots, kHdr, (int)device);
     auto dopt = at::TensorOptions().dtype(at::kLong).device(at::kCUDA, device);
@@ -399,16 +455,24 @@ py::dict dev_run_local(py::dict params, const std::string& kind, int64_t nbytes,
         pg->alltoall_base(d_recv, d_send, all, all)->wait();
       else
         dls_launch_transpose(d_send.data_ptr<int64_t>(), d_recv.data_ptr<int64_t>(), W, slot, stream);
-      ++exchanges;
     };
     int64_t b = 1;
     uint64_t last_epochs = 0;
+    const bool graphed = graph_mode();
+    EpochGraph graph;
     for (;;) {
-      for (int64_t i = 0; i < b; ++i) {
+      auto one_epoch = [&] {
         exchange();
         dls_launch_epoch(S.base(), S.L, W, d_recv.data_ptr<int64_t>(), src_stride, rank_stride,
                          d_send.data_ptr<int64_t>(), (int64_t)W * slot, nullptr, nullptr, nullptr, DLS_MODE_NEXT,
                          stream);
+      };
+      if (graphed) {
+        graph.run((hipStream_t)stream, std::max<int64_t>(1, batch_max), one_epoch);
+        exchanges += (uint64_t)graph.n;
+      } else {
+        for (int64_t i = 0; i < b; ++i) one_epoch();
+        exchanges += (uint64_t)b;
       }
       S.poll();
       ++polls;
@@ -466,13 +530,26 @@ py::dict dev_run_local(py::dict params, const std::string& kind, int64_t nbytes,
   d["polls"] = polls;
   d["loop_s"] = loop_s;
   d["us_per_epoch"] = loop_s * 1e6 / (double)std::max<uint64_t>(1, exchanges);
+  py::list prof;  // rank 0's epoch-kernel shader clocks per launch: load, unpack, pack, store
+  for (int i = 0; i < 4; ++i) prof.append((double)S.st(0).prof[i] / (double)std::max<uint64_t>(1, exchanges + 1));
+  d["kernel_clocks_per_launch"] = prof;
   d["state_bytes_per_rank"] = (int64_t)S.L.bytes;
   return d;
 }
 
 }  // namespace asim
 
+// ASIM_SEGV_TRACE=1: print the native stack on SIGSEGV (GPU boxes have no debugger)
+static void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  if (const char* e = std::getenv("ASIM_SEGV_TRACE"); e && e[0] == '1') signal(SIGSEGV, segv_trace);
   m.doc() = "native epoch loop of the packet-level collective over a torch.distributed ProcessGroup";
   m.def("exchange_run", &asim::exchange_run, py::arg("group"), py::arg("params"), py::arg("kind"), py::arg("bytes"),
         py::arg("root"), py::arg("start_ps"), py::arg("device") = -1);

@@ -44,7 +44,18 @@ SIM_HDI bool ls_before(const LsReady& a, const LsReady& b) {
   return a.slice < b.slice;
 }
 
-SIM_HDI int ls_mod(int a, int n) { return ((a % n) + n) % n; }
+// a mod n in [0, n); the operands here are almost always within one period
+// (peer = rank +- stride), which skips the integer division
+SIM_HDI int ls_mod(int a, int n) {
+  if (a >= 0) {
+    if (a < n) return a;
+    if (a < 2 * n) return a - n;
+  } else if (a >= -n) {
+    return a + n;
+  }
+  const int m = a % n;
+  return m < 0 ? m + n : m;
+}
 
 SIM_HDI int ls_inv_mod(int s, int n) {
   for (int x = 1; x < n; ++x)
@@ -118,7 +129,10 @@ SIM_HDI uint32_t ls_slice_len(const LsGeom& g, int s) {
   return (uint32_t)(rest < g.slice_bytes ? rest : g.slice_bytes);
 }
 
-SIM_HDI int ls_link_of(const LsGeom& g, int dst) { return ls_mod(dst - g.rank - 1, g.world) % g.nlinks; }
+SIM_HDI int ls_link_of(const LsGeom& g, int dst) {
+  const int o = ls_mod(dst - g.rank - 1, g.world);
+  return o < g.nlinks ? o : o % g.nlinks;
+}
 
 // serialisation of b bytes on a link / completion of a received packet's local reduce or copy
 SIM_HDI uint64_t ls_ser_ps(const LsGeom& g, uint32_t b) { return (uint64_t)ceil(b * g.ps_per_byte_link); }

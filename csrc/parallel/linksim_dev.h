@@ -33,16 +33,19 @@ struct DlsState {
   int64_t t, t_end, ann_next, ann_busy;
   uint64_t epochs, packets;
   int64_t extra_total;  // overflow words packed in the last epoch
-  int32_t heap_n, cap;
+  int64_t lheap_off[kLsMaxLinks];  // per-link pending-send heaps: offset (items), size, capacity
+  int32_t lheap_n[kLsMaxLinks];
+  int32_t lheap_cap[kLsMaxLinks];
   int32_t status;
   int32_t k, hdr;
   int32_t pad;
+  uint64_t prof[4];  // epoch kernel shader clocks, summed: load, unpack, pack, store
 };
 
 // byte offsets inside one rank's state block
 struct DlsLayout {
   size_t bytes = 0;
-  size_t off_heap = 0, off_def = 0, off_pk = 0, off_extra = 0, off_ew = 0, off_cnt = 0, off_fill = 0;
+  size_t off_heap = 0, off_pk = 0, off_extra = 0, off_ew = 0, off_cnt = 0, off_fill = 0;
   int64_t cap = 0;
 };
 
