@@ -272,39 +272,6 @@ struct DevStates {
 
 [[noreturn]] void dls_fail(int32_t st) { throw std::runtime_error(std::string("device epoch loop: ") + dls_status_name(st)); }
 
-// A batch of epochs as one hipGraph (ASIM_DEVICE_EXCHANGE_GRAPH=1): the first
-// batch of `n` (all-to-all, epoch kernel) pairs is captured from the stream --
-// the collective's own stream joins the capture through its event waits -- and
-// every later batch is one graph launch, so the host pays one launch per batch
-// instead of a c10d collective call and a kernel launch per epoch.
-struct EpochGraph {
-  hipGraph_t g = nullptr;
-  hipGraphExec_t x = nullptr;
-  int64_t n = 0;
-  template <class F>
-  void run(hipStream_t st, int64_t batch, F&& one_epoch) {
-    if (!x) {
-      n = batch;
-      check_hip(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed), "begin capture");
-      for (int64_t i = 0; i < n; ++i) one_epoch();
-      check_hip(hipStreamEndCapture(st, &g), "end capture");
-      check_hip(hipGraphInstantiate(&x, g, nullptr, nullptr, 0), "instantiate");
-    }
-    check_hip(hipGraphLaunch(x, st), "graph launch");
-  }
-  static void check_hip(hipError_t e, const char* what) {
-    if (e != hipSuccess) throw std::runtime_error(std::string("epoch graph: ") + what + ": " + hipGetErrorString(e));
-  }
-  ~EpochGraph() {
-    if (x) (void)hipGraphExecDestroy(x);
-    if (g) (void)hipGraphDestroy(g);
-  }
-};
-
-bool graph_mode() {
-  const char* e = std::getenv("ASIM_DEVICE_EXCHANGE_GRAPH");
-  return e && e[0] == '1';
-}
 
 }  // namespace
 
@@ -325,8 +292,7 @@ py::dict exchange_run_device(py::object pgo, py::dict params, const std::string&
   {
     py::gil_scoped_release nogil;
     const auto t0c = std::chrono::steady_clock::now();
-    // a stream of our own (the default stream cannot be captured into a
-    // graph); work the caller queued before is finished first
+    // a stream of our own; work the caller queued before is finished first
     sync_stream((int)device);
     const c10::hip::HIPStreamGuard sg(c10::hip::getStreamFromPool(false, (c10::DeviceIndex)device));
     void* stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
@@ -345,21 +311,15 @@ py::dict exchange_run_device(py::object pgo, py::dict params, const std::string&
                      t0.data_ptr<int64_t>(), DLS_MODE_FIRST, stream);
     int64_t b = 1;
     uint64_t last_epochs = 0;
-    const bool graphed = graph_mode();
-    EpochGraph graph;
+
     for (;;) {
       auto one_epoch = [&] {
         pg->alltoall_base(d_recv, d_send, eq, eq)->wait();
         dls_launch_epoch(S.base(), S.L, 1, d_recv.data_ptr<int64_t>(), slot, 0, d_send.data_ptr<int64_t>(), 0, nullptr,
                          nullptr, nullptr, DLS_MODE_NEXT, stream);
       };
-      if (graphed) {
-        graph.run((hipStream_t)stream, std::max<int64_t>(1, batch_max), one_epoch);
-        exchanges += (uint64_t)graph.n;
-      } else {
-        for (int64_t i = 0; i < b; ++i) one_epoch();
-        exchanges += (uint64_t)b;
-      }
+      for (int64_t i = 0; i < b; ++i) one_epoch();
+      exchanges += (uint64_t)b;
       S.poll();
       ++polls;
       const int32_t st = S.status();
@@ -434,8 +394,7 @@ py::dict dev_run_local(py::dict params, const std::string& kind, int64_t nbytes,
   DevStates S;
   {
     py::gil_scoped_release nogil;
-    // a stream of our own (the default stream cannot be captured into a
-    // graph); work the caller queued before is finished first
+    // a stream of our own; work the caller queued before is finished first
     sync_stream((int)device);
     const c10::hip::HIPStreamGuard sg(c10::hip::getStreamFromPool(false, (c10::DeviceIndex)device));
     void* stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
@@ -458,8 +417,7 @@ py::dict dev_run_local(py::dict params, const std::string& kind, int64_t nbytes,
     };
     int64_t b = 1;
     uint64_t last_epochs = 0;
-    const bool graphed = graph_mode();
-    EpochGraph graph;
+
     for (;;) {
       auto one_epoch = [&] {
         exchange();
@@ -467,13 +425,8 @@ py::dict dev_run_local(py::dict params, const std::string& kind, int64_t nbytes,
                          d_send.data_ptr<int64_t>(), (int64_t)W * slot, nullptr, nullptr, nullptr, DLS_MODE_NEXT,
                          stream);
       };
-      if (graphed) {
-        graph.run((hipStream_t)stream, std::max<int64_t>(1, batch_max), one_epoch);
-        exchanges += (uint64_t)graph.n;
-      } else {
-        for (int64_t i = 0; i < b; ++i) one_epoch();
-        exchanges += (uint64_t)b;
-      }
+      for (int64_t i = 0; i < b; ++i) one_epoch();
+      exchanges += (uint64_t)b;
       S.poll();
       ++polls;
       const int32_t st = S.status();

@@ -53,21 +53,9 @@ def main():
                 ext.dev_run_local(PARAMS, kind, 16 << 20, 0, starts, dev, pg)  # warm
                 d = dict(ext.dev_run_local(PARAMS, kind, nbytes, 0, starts, dev, pg, a.batch))
                 t = dict(ext.dev_run_local(PARAMS, kind, nbytes, 0, starts, dev, None, a.batch))
-                os.environ["ASIM_DEVICE_EXCHANGE_GRAPH"] = "1"  # batches of epochs as hipGraphs
-                print("graph mode", kind, flush=True)
-                tg = dict(ext.dev_run_local(PARAMS, kind, nbytes, 0, starts, dev, None, a.batch))
-                try:
-                    dg = dict(ext.dev_run_local(PARAMS, kind, nbytes, 0, starts, dev, pg, a.batch))
-                except Exception as e:  # RCCL inside a captured graph
-                    dg = {"us_per_epoch": None, "finish_ps": None, "error": str(e)[:300]}
-                os.environ["ASIM_DEVICE_EXCHANGE_GRAPH"] = "0"
                 ref = collectives.emulate(PARAMS, kind, nbytes, starts)["finish_ps"]
                 row = {"bytes": nbytes, "epochs": d["epochs"], "exchanges": d["exchanges"], "polls": d["polls"],
                        "us_per_epoch_rccl_loopback": d["us_per_epoch"], "us_per_epoch_transpose": t["us_per_epoch"],
-                       "us_per_epoch_transpose_graph": tg["us_per_epoch"],
-                       "us_per_epoch_rccl_loopback_graph": dg["us_per_epoch"], "graph_error": dg.get("error"),
-                       "graph_finish_equal": list(tg["finish_ps"]) == list(ref) and (dg["finish_ps"] is None or
-                                                                                     list(dg["finish_ps"]) == list(ref)),
                        "epoch_kernel_clocks_load_unpack_pack_store": [round(x) for x in t["kernel_clocks_per_launch"]],
                        "finish_equals_host_emulation": list(d["finish_ps"]) == list(ref) == list(t["finish_ps"])}
                 res["device_loop_%s" % kind] = row
