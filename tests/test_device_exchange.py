@@ -84,3 +84,47 @@ def test_device_loop_over_rccl_loopback_and_one_rank_exchange():
         assert out["finish_ps"] == 1234 and ex.stats.get("device_loop") and ex.stats["epochs"] == 1
     finally:
         dist.destroy_process_group()
+
+
+def _gloo_dev_worker(rank, world, port, cases, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    torch.cuda.set_device(0)
+    import datetime
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=120))
+    try:
+        ex = collectives.PacketExchange(device=torch.device("cuda", 0))
+        out = [ex.run(p, kind, nbytes, 0, starts[rank])["finish_ps"] for p, kind, nbytes, starts in cases]
+        q.put((rank, out, dict(ex.stats)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_device_loop_multi_rank_over_gloo_device_tensors():
+    """The multi-rank driver of the device loop (exchange_run_device: batched
+    epochs, the global stop, the overflow all-to-all from the device buffer)
+    with 4 real ranks on one MI355X.  RCCL refuses two ranks on one GPU, so the
+    all-to-alls of the device buffers go over gloo here; the 8-GPU node runs
+    the same driver over RCCL."""
+    import torch.multiprocessing as mp
+    _ext()
+    cases = [c for c in CASES if len(c[3]) == 4] + [(PARAMS, "AllReduce", 4 << 20, [0, 700_000, 0, 13]),
+                                                     (SMALL, "AllGather", 128 << 10, [0, 0, 0, 2_000_000])]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_dev_worker, args=(r, 4, port, cases, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for i, (p, kind, nbytes, starts) in enumerate(cases):
+        ref = collectives.emulate(p, kind, nbytes, starts)["finish_ps"]
+        assert [res[r][1][i] for r in range(4)] == list(ref), (kind, nbytes, starts)
+    for r in range(4):
+        assert res[r][2].get("device_loop") and res[r][2]["exchanges"] >= res[r][2]["epochs"] > 0
