@@ -422,14 +422,25 @@ class DistributedSuite:
                 if nk <= k or used + nk > cores:
                     break
                 old = self.times[(crit, "cpu")]
-                self.threads[crit] = nk
-                t = float("inf")
-                for _r in range(max(1, reps)):
-                    self._run_app((crit, kl_of[crit]), "cpu")
-                    t = min(t, self.times[(crit, "cpu")])
-                if t <= 0.85 * old:
-                    self.times[(crit, "cpu")] = t
-                else:
+                # the doubled team, and if that alone does not pay, the team
+                # doubled once more: thread teams often pay only past 2 (the
+                # dp step on an MI355X node: 158 -> 140 -> 110 ms at 1 / 2 / 4,
+                # tools/dp_step_threads.py)
+                ok = False
+                wider = 2 * nk <= max_threads and os.environ.get("ASIM_NODE_WIDEN_WIDER", "1") != "0"
+                for team in [nk] + ([2 * nk] if wider else []):
+                    if used + team > cores:
+                        break
+                    self.threads[crit] = team
+                    t = float("inf")
+                    for _r in range(max(1, reps)):
+                        self._run_app((crit, kl_of[crit]), "cpu")
+                        t = min(t, self.times[(crit, "cpu")])
+                    if t <= 0.85 * old:
+                        self.times[(crit, "cpu")] = t
+                        ok = True
+                        break
+                if not ok:
                     self.threads[crit] = k
                     self.times[(crit, "cpu")] = old
                     tried.add(crit)

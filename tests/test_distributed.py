@@ -466,3 +466,33 @@ def test_bench_eight_gloo_ranks_node_mode_runs_rank0_plan(tmp_path):
     assert set(pr[0]["assignment"]) == {"nn-rodinia-2.0-ft", "pathfinder-rodinia-2.0-ft"}
     assert all(p["wall_s"] > 0 and p["insn"] > 0 and p["calibration_s"] for p in pr)
     assert out["wall_s_spread"]["max"] >= out["wall_s_spread"]["min"] > 0
+
+
+def test_node_widen_tries_a_wider_team_when_doubling_does_not_pay(monkeypatch):
+    """The dp step on an MI355X node's cores: 158 / 140 / 110 ms at 1 / 2 / 4
+    threads (tools/dp_step_threads.py).  Two threads miss the 15 % bar, four
+    clear it: widen() must keep four instead of giving up at two."""
+    from accel_sim_framework_distributed_amd.parallel import multi_gpu
+    S = multi_gpu.DistributedSuite
+    obj = S.__new__(S)
+    scale = {1: 0.158, 2: 0.140, 4: 0.110, 8: 0.105}
+    cal = {"dp-step": (0.30, 0.158), "bfs": (0.50, 0.129), "hotspot": (0.16, 0.12)}
+    obj.apps = [(a, a) for a in cal]
+    obj.times = {}
+    for a, (g, c) in cal.items():
+        obj.times[(a, "gpu")], obj.times[(a, "cpu")] = g, c
+    obj.threads = {}
+    obj._calibrating = False
+    monkeypatch.setattr(S, "concurrency", lambda self: 1)
+    monkeypatch.setattr(S, "cpu_slots", lambda self, reserve=0: 14)
+
+    def run_app(self, app_kl, engine=None):
+        a = app_kl[0]
+        k = self.threads.get(a, 1)
+        self.times[(a, engine)] = scale[k] if a == "dp-step" else cal[a][1]
+    monkeypatch.setattr(S, "_run_app", run_app)
+    obj.plan()
+    assert obj.assignment["dp-step"] == "cpu"
+    obj.widen()
+    assert obj.threads.get("dp-step") == 4
+    assert obj.predicted_span < 0.135
