@@ -64,15 +64,22 @@ __device__ LsReady heap_pop(LsReady* h, int32_t& n) {
   return top;
 }
 
+// LDS-typed pointers: their loads wait only for LDS traffic, where a generic
+// (flat) load must also drain every outstanding global store first -- in the
+// packing loop, one HBM round trip per packet
+#define LDS_AS __attribute__((address_space(3)))
+
 struct Rank {
   DlsState* s;
-  LsReady* heap;  // per-link heaps at s->lheap_off[l]
-  LinkPkt* pk;    // per-link emitted packets, same offsets
+  LsReady* heap;  // per-link heaps at s->lheap_off[l] (HBM)
+  LinkPkt* pk;    // per-link emitted packets, same offsets (HBM)
   int64_t* extra;
-  int64_t* extra_words;
-  int64_t* cnt;
-  int64_t* fill;
-  int32_t* dlink;  // link of every destination
+  int64_t* extra_words_g;
+  // per-destination counters, overflow sizes and links, in LDS
+  LDS_AS int64_t* cnt;
+  LDS_AS int64_t* fill;
+  LDS_AS int64_t* extra_words;
+  LDS_AS int32_t* dlink;
 };
 
 __device__ Rank rank_view(char* base, const DlsLayout& L) {
@@ -81,9 +88,9 @@ __device__ Rank rank_view(char* base, const DlsLayout& L) {
   r.heap = reinterpret_cast<LsReady*>(base + L.off_heap);
   r.pk = reinterpret_cast<LinkPkt*>(base + L.off_pk);
   r.extra = reinterpret_cast<int64_t*>(base + L.off_extra);
-  r.extra_words = reinterpret_cast<int64_t*>(base + L.off_ew);
-  r.cnt = reinterpret_cast<int64_t*>(base + L.off_cnt);
-  r.fill = reinterpret_cast<int64_t*>(base + L.off_fill);
+  r.extra_words_g = reinterpret_cast<int64_t*>(base + L.off_ew);
+  r.cnt = r.fill = r.extra_words = nullptr;
+  r.dlink = nullptr;
   return r;
 }
 
@@ -115,6 +122,7 @@ struct Wave {
   uint64_t lf;   // this link's clock
   LsReady* h;    // this link's heap
   LinkPkt* out;  // this link's packets of the epoch
+  bool out_lds;  // ... staged in LDS
   // uniform copies
   uint64_t recv_left, send_left, sent, finish;
   int64_t t, t_end, ann_next, ann_busy;
@@ -202,6 +210,46 @@ __device__ bool unpack(const Rank& R, Wave& w, const int64_t* recv, int64_t src_
   return true;
 }
 
+__device__ __forceinline__ LinkPkt read_pkt(const LDS_AS LinkPkt* p) {
+  const LDS_AS int64_t* w = (const LDS_AS int64_t*)p;
+  const int64_t v[4] = {w[0], w[1], w[2], w[3]};
+  LinkPkt q;
+  __builtin_memcpy(&q, v, sizeof(q));
+  return q;
+}
+__device__ __forceinline__ LinkPkt read_pkt(const LinkPkt* p) { return *p; }
+
+// the lane's slots: headers, then its packets in emission order per
+// destination (overflow words in destination order)
+template <class PktPtr>
+__device__ void pack_store(const Rank& R, const Wave& w, PktPtr out, int32_t npk, int64_t* send, int64_t slot,
+                           int64_t mx, int64_t min_arr) {
+  const DlsState& s = *R.s;
+  const int W = s.g.world, K = s.k, H = s.hdr;
+  for (int d = 0; d < W; ++d) {
+    if (R.dlink[d] != w.lane) continue;
+    int64_t* hd = send + d * slot;
+    hd[0] = R.cnt[d];
+    hd[1] = mx;
+    hd[2] = w.ann_next;
+    hd[3] = w.ann_busy;
+    hd[4] = min_arr;
+    for (int64_t i = 5; i < slot; ++i) hd[i] = 0;
+    int64_t base = 0;  // start of d's overflow words: destination order
+    for (int e = 0; e < d; ++e) base += R.extra_words[e];
+    R.cnt[d] = base;
+  }
+  for (int i = 0; i < npk; ++i) {
+    const LinkPkt p = read_pkt(out + i);
+    const int d = p.dst;
+    const int64_t f = R.fill[d]++;
+    if (f < K)
+      store_pkt(send + d * slot + H + 4 * f, p);
+    else
+      store_pkt(R.extra + R.cnt[d] + 4 * (f - K), p);
+  }
+}
+
 // LinkSim::emit + pack_epoch for the epoch [t, t + E)
 __device__ void pack(const Rank& R, Wave& w, int64_t* send) {
   const DlsState& s = *R.s;
@@ -254,27 +302,10 @@ __device__ void pack(const Rank& R, Wave& w, int64_t* send) {
   int64_t ex = 0;
   for (int d = 0; d < W; ++d) ex += R.extra_words[d];
   if (w.own) {
-    for (int d = 0; d < W; ++d) {
-      if (R.dlink[d] != w.lane) continue;
-      int64_t* hd = send + d * slot;
-      for (int64_t i = 0; i < slot; ++i) hd[i] = 0;
-      hd[0] = R.cnt[d];
-      hd[1] = mx;
-      hd[2] = w.ann_next;
-      hd[3] = w.ann_busy;
-      hd[4] = min_arr;
-      int64_t base = 0;  // start of d's overflow words: destination order
-      for (int e = 0; e < d; ++e) base += R.extra_words[e];
-      R.cnt[d] = base;
-    }
-    for (int i = 0; i < npk; ++i) {
-      const int d = w.out[i].dst;
-      const int64_t f = R.fill[d]++;
-      if (f < K)
-        store_pkt(send + d * slot + H + 4 * f, w.out[i]);
-      else
-        store_pkt(R.extra + R.cnt[d] + 4 * (f - K), w.out[i]);
-    }
+    if (w.out_lds)
+      pack_store(R, w, (const LDS_AS LinkPkt*)w.out, npk, send, slot, mx, min_arr);
+    else
+      pack_store(R, w, (const LinkPkt*)w.out, npk, send, slot, mx, min_arr);
   }
   w.packets += (uint64_t)tot;
   R.s->extra_total = ex;  // uniform value
@@ -323,11 +354,11 @@ __global__ void __launch_bounds__(64) dls_epoch_kernel(char* states, DlsLayout L
   }
   Rank R = G;
   R.s = &s;
-  R.cnt = reinterpret_cast<int64_t*>(lds + o);
+  R.cnt = (LDS_AS int64_t*)(lds + o);
   R.fill = R.cnt + W;
   R.extra_words = R.fill + W;
   o = al16(o + (size_t)3 * W * 8);
-  R.dlink = reinterpret_cast<int32_t*>(lds + o);
+  R.dlink = (LDS_AS int32_t*)(lds + o);
   o = al16(o + (size_t)W * 4);
   for (int d = lane; d < W; d += 64) R.dlink[d] = ls_link_of(s.g, d);
   __syncthreads();
@@ -359,6 +390,7 @@ __global__ void __launch_bounds__(64) dls_epoch_kernel(char* states, DlsLayout L
   w.own = lane < nl;
   w.hn = w.own ? s.lheap_n[lane] : 0;
   w.lf = w.own ? s.link_free[lane] : 0;
+  w.out_lds = in_lds;
   if (in_lds) {
     w.h = lheap + (w.own ? reg_off[lane] : 0);
     w.out = lpk + (w.own ? reg_off[lane] : 0);
@@ -413,7 +445,7 @@ __global__ void __launch_bounds__(64) dls_epoch_kernel(char* states, DlsLayout L
     for (int l = 0; l < nl; ++l)
       for (int64_t i = lane; i < s.lheap_n[l]; i += 64) G.heap[s.lheap_off[l] + i] = lheap[reg_off[l] + i];
   if (go)  // pack ran: this epoch's overflow sizes (an epoch stopped for the overflow exchange keeps the last ones)
-    for (int i = lane; i < W; i += 64) G.extra_words[i] = R.extra_words[i];
+    for (int i = lane; i < W; i += 64) G.extra_words_g[i] = R.extra_words[i];
   if (lane == 0) {
     s.prof[0] += c1 - c0;
     s.prof[1] += c2 - c1;
