@@ -483,8 +483,8 @@ py::dict dev_run_local(py::dict params, const std::string& kind, int64_t nbytes,
   d["polls"] = polls;
   d["loop_s"] = loop_s;
   d["us_per_epoch"] = loop_s * 1e6 / (double)std::max<uint64_t>(1, exchanges);
-  py::list prof;  // rank 0's epoch-kernel shader clocks per launch: load, unpack, pack, store
-  for (int i = 0; i < 4; ++i) prof.append((double)S.st(0).prof[i] / (double)std::max<uint64_t>(1, exchanges + 1));
+  py::list prof;  // rank 0's epoch-kernel shader clocks per launch: load, unpack, pack, store | emit, reductions, slots
+  for (int i = 0; i < 7; ++i) prof.append((double)S.st(0).prof[i] / (double)std::max<uint64_t>(1, exchanges + 1));
   d["kernel_clocks_per_launch"] = prof;
   d["state_bytes_per_rank"] = (int64_t)S.L.bytes;
   return d;

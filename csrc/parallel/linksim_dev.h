@@ -39,7 +39,7 @@ struct DlsState {
   int32_t status;
   int32_t k, hdr;
   int32_t pad;
-  uint64_t prof[4];  // epoch kernel shader clocks, summed: load, unpack, pack, store
+  uint64_t prof[8];  // epoch kernel shader clocks, summed: load, unpack, pack, store | pack: emit, reductions, slots
 };
 
 // byte offsets inside one rank's state block

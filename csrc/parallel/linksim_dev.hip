@@ -34,7 +34,6 @@ __device__ __forceinline__ LinkPkt load_pkt(const int64_t* w) {
   return p;
 }
 
-__device__ __forceinline__ void store_pkt(int64_t* w, const LinkPkt& p) { __builtin_memcpy(w, &p, sizeof(p)); }
 
 __device__ void heap_push(LsReady* h, int32_t& n, const LsReady& v) {
   int i = n++;
@@ -68,6 +67,18 @@ __device__ LsReady heap_pop(LsReady* h, int32_t& n) {
 // (flat) load must also drain every outstanding global store first -- in the
 // packing loop, one HBM round trip per packet
 #define LDS_AS __attribute__((address_space(3)))
+// and HBM-typed store targets: a generic store may alias LDS, so every later
+// LDS load would have to wait for it to land
+#define GLB_AS __attribute__((address_space(1)))
+
+__device__ __forceinline__ void store_pkt_g(GLB_AS int64_t* w, const LinkPkt& p) {
+  int64_t v[4];
+  __builtin_memcpy(v, &p, sizeof(v));
+  w[0] = v[0];
+  w[1] = v[1];
+  w[2] = v[2];
+  w[3] = v[3];
+}
 
 struct Rank {
   DlsState* s;
@@ -226,9 +237,11 @@ __device__ void pack_store(const Rank& R, const Wave& w, PktPtr out, int32_t npk
                            int64_t mx, int64_t min_arr) {
   const DlsState& s = *R.s;
   const int W = s.g.world, K = s.k, H = s.hdr;
+  GLB_AS int64_t* gsend = (GLB_AS int64_t*)send;
+  GLB_AS int64_t* gextra = (GLB_AS int64_t*)R.extra;
   for (int d = 0; d < W; ++d) {
     if (R.dlink[d] != w.lane) continue;
-    int64_t* hd = send + d * slot;
+    GLB_AS int64_t* hd = gsend + d * slot;
     hd[0] = R.cnt[d];
     hd[1] = mx;
     hd[2] = w.ann_next;
@@ -244,14 +257,14 @@ __device__ void pack_store(const Rank& R, const Wave& w, PktPtr out, int32_t npk
     const int d = p.dst;
     const int64_t f = R.fill[d]++;
     if (f < K)
-      store_pkt(send + d * slot + H + 4 * f, p);
+      store_pkt_g(gsend + d * slot + H + 4 * f, p);
     else
-      store_pkt(R.extra + R.cnt[d] + 4 * (f - K), p);
+      store_pkt_g(gextra + R.cnt[d] + 4 * (f - K), p);
   }
 }
 
 // LinkSim::emit + pack_epoch for the epoch [t, t + E)
-__device__ void pack(const Rank& R, Wave& w, int64_t* send) {
+__device__ void pack(const Rank& R, Wave& w, int64_t* send, uint64_t* tp) {
   const DlsState& s = *R.s;
   const LsGeom& g = s.g;
   const int W = g.world, K = s.k, H = s.hdr;
@@ -285,6 +298,7 @@ __device__ void pack(const Rank& R, Wave& w, int64_t* send) {
       if (R.dlink[d] == w.lane) R.cnt[d] = R.fill[d] = 0;
     for (int i = 0; i < npk; ++i) ++R.cnt[w.out[i].dst];
   }
+  tp[0] = clock64();
   const int64_t tot = wave_sum(npk);
   w.send_left -= (uint64_t)tot;
   w.sent += (uint64_t)tot;
@@ -301,12 +315,14 @@ __device__ void pack(const Rank& R, Wave& w, int64_t* send) {
   __syncthreads();  // every link's overflow sizes are out
   int64_t ex = 0;
   for (int d = 0; d < W; ++d) ex += R.extra_words[d];
+  tp[1] = clock64();
   if (w.own) {
     if (w.out_lds)
       pack_store(R, w, (const LDS_AS LinkPkt*)w.out, npk, send, slot, mx, min_arr);
     else
       pack_store(R, w, (const LinkPkt*)w.out, npk, send, slot, mx, min_arr);
   }
+  tp[2] = clock64();
   w.packets += (uint64_t)tot;
   R.s->extra_total = ex;  // uniform value
 }
@@ -316,12 +332,16 @@ __device__ void pack(const Rank& R, Wave& w, int64_t* send) {
 // dependent chains of the event work hit LDS instead of HBM (the state was
 // written by the previous launch, often on another XCD's L2)
 constexpr int kLdsBytes = 60 * 1024;  // + the static reg_off: under the 64 KB default limit
-static_assert(sizeof(DlsState) % 8 == 0, "the header is copied in 8-byte words");
+static_assert(sizeof(DlsState) % 8 == 0 && sizeof(LsReady) % 8 == 0, "copied in 8-byte words");
 
 __device__ __forceinline__ size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// cooperative copy of n 8-byte words
-__device__ __forceinline__ void copy_words(int64_t* dst, const int64_t* src, int64_t n, int lane) {
+// cooperative copies of n 8-byte words between HBM and LDS (typed, so the
+// loads of one pass are not serialised behind the stores of the last)
+__device__ __forceinline__ void copy_in(LDS_AS int64_t* dst, const GLB_AS int64_t* src, int64_t n, int lane) {
+  for (int64_t i = lane; i < n; i += 64) dst[i] = src[i];
+}
+__device__ __forceinline__ void copy_out(GLB_AS int64_t* dst, const LDS_AS int64_t* src, int64_t n, int lane) {
   for (int64_t i = lane; i < n; i += 64) dst[i] = src[i];
 }
 
@@ -341,7 +361,7 @@ __global__ void __launch_bounds__(64) dls_epoch_kernel(char* states, DlsLayout L
   }
   // header and received slots to LDS
   DlsState& s = *reinterpret_cast<DlsState*>(lds);
-  copy_words(reinterpret_cast<int64_t*>(lds), reinterpret_cast<const int64_t*>(G.s), sizeof(DlsState) / 8, lane);
+  copy_in((LDS_AS int64_t*)lds, (const GLB_AS int64_t*)G.s, sizeof(DlsState) / 8, lane);
   __syncthreads();
   const int W = s.g.world;
   const int64_t slot = s.hdr + 4 * s.k;
@@ -350,7 +370,9 @@ __global__ void __launch_bounds__(64) dls_epoch_kernel(char* states, DlsLayout L
   o = al16(o + (size_t)W * slot * 8);
   if (mode != DLS_MODE_FIRST) {
     const int64_t* rv = recv + b * recv_rank_stride;
-    for (int64_t i = lane; i < W * slot; i += 64) lrecv[i] = rv[(i / slot) * recv_src_stride + i % slot];
+    const GLB_AS int64_t* grv = (const GLB_AS int64_t*)rv;
+    LDS_AS int64_t* lrv = (LDS_AS int64_t*)lrecv;
+    for (int64_t i = lane; i < W * slot; i += 64) lrv[i] = grv[(i / slot) * recv_src_stride + i % slot];
   }
   Rank R = G;
   R.s = &s;
@@ -383,7 +405,8 @@ __global__ void __launch_bounds__(64) dls_epoch_kernel(char* states, DlsLayout L
   if (in_lds) {
     // flattened over links so the loads are independent
     for (int l = 0; l < nl; ++l)
-      for (int64_t i = lane; i < s.lheap_n[l]; i += 64) lheap[reg_off[l] + i] = G.heap[s.lheap_off[l] + i];
+      copy_in((LDS_AS int64_t*)(lheap + reg_off[l]), (const GLB_AS int64_t*)(G.heap + s.lheap_off[l]),
+              (int64_t)s.lheap_n[l] * (sizeof(LsReady) / 8), lane);
   }
   Wave w;
   w.lane = lane;
@@ -419,7 +442,8 @@ __global__ void __launch_bounds__(64) dls_epoch_kernel(char* states, DlsLayout L
     go = unpack(R, w, lrecv, slot, with_spill ? spill + spill_off[b] : nullptr,
                 with_spill ? spill_off[b + 1] - spill_off[b] : 0, with_spill);
   const uint64_t c2 = clock64();
-  if (go) pack(R, w, my_send);
+  uint64_t tp[3] = {0, 0, 0};
+  if (go) pack(R, w, my_send, tp);
   __syncthreads();
   const uint64_t c3 = clock64();
   // state back to HBM
@@ -443,7 +467,8 @@ __global__ void __launch_bounds__(64) dls_epoch_kernel(char* states, DlsLayout L
   __syncthreads();
   if (in_lds)
     for (int l = 0; l < nl; ++l)
-      for (int64_t i = lane; i < s.lheap_n[l]; i += 64) G.heap[s.lheap_off[l] + i] = lheap[reg_off[l] + i];
+      copy_out((GLB_AS int64_t*)(G.heap + s.lheap_off[l]), (const LDS_AS int64_t*)(lheap + reg_off[l]),
+               (int64_t)s.lheap_n[l] * (sizeof(LsReady) / 8), lane);
   if (go)  // pack ran: this epoch's overflow sizes (an epoch stopped for the overflow exchange keeps the last ones)
     for (int i = lane; i < W; i += 64) G.extra_words_g[i] = R.extra_words[i];
   if (lane == 0) {
@@ -451,9 +476,14 @@ __global__ void __launch_bounds__(64) dls_epoch_kernel(char* states, DlsLayout L
     s.prof[1] += c2 - c1;
     s.prof[2] += c3 - c2;
     s.prof[3] += clock64() - c3;  // up to here; the header copy itself is not counted
+    if (go) {
+      s.prof[4] += tp[0] - c2;
+      s.prof[5] += tp[1] - tp[0];
+      s.prof[6] += tp[2] - tp[1];
+    }
   }
   __syncthreads();
-  copy_words(reinterpret_cast<int64_t*>(G.s), reinterpret_cast<const int64_t*>(lds), sizeof(DlsState) / 8, lane);
+  copy_out((GLB_AS int64_t*)G.s, (const LDS_AS int64_t*)lds, sizeof(DlsState) / 8, lane);
 }
 
 // the in-process emulation's all-to-all: rank d's slot from rank s is rank
