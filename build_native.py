@@ -221,6 +221,10 @@ def build_dist_ext(verbose: bool = False) -> str:
         hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
         subprocess.check_call([hipcc, "-std=c++17", "-O2", "-fPIC", f"--offload-arch={ARCH}",
                                f"-I{os.path.join(ROOT, 'csrc')}", "-c", dev_src, "-o", dev_obj])
+        # the extension's ninja file does not track a prebuilt object: relink
+        for f in ("_asim_dist.so", "build.ninja", ".ninja_log"):
+            if os.path.exists(os.path.join(bdir, f)):
+                os.remove(os.path.join(bdir, f))
     load(name="_asim_dist", sources=[os.path.join(ROOT, "csrc", "parallel", "exchange.cc"),
                                       os.path.join(ROOT, "csrc", "parallel", "linksim.cc")],
          build_directory=bdir, extra_cflags=["-O2", f"-I{os.path.join(ROOT, 'csrc')}", "-D__HIP_PLATFORM_AMD__=1"],

@@ -90,6 +90,7 @@ struct Rank {
   LDS_AS int64_t* cnt;
   LDS_AS int64_t* fill;
   LDS_AS int64_t* extra_words;
+  LDS_AS int64_t* base;  // start of each destination's overflow words
   LDS_AS int32_t* dlink;
 };
 
@@ -100,7 +101,7 @@ __device__ Rank rank_view(char* base, const DlsLayout& L) {
   r.pk = reinterpret_cast<LinkPkt*>(base + L.off_pk);
   r.extra = reinterpret_cast<int64_t*>(base + L.off_extra);
   r.extra_words_g = reinterpret_cast<int64_t*>(base + L.off_ew);
-  r.cnt = r.fill = r.extra_words = nullptr;
+  r.cnt = r.fill = r.extra_words = r.base = nullptr;
   r.dlink = nullptr;
   return r;
 }
@@ -230,28 +231,14 @@ __device__ __forceinline__ LinkPkt read_pkt(const LDS_AS LinkPkt* p) {
 }
 __device__ __forceinline__ LinkPkt read_pkt(const LinkPkt* p) { return *p; }
 
-// the lane's slots: headers, then its packets in emission order per
-// destination (overflow words in destination order)
+// the lane's packets into its destinations' slots, emission order per
+// destination (past K: overflow words, destination order)
 template <class PktPtr>
-__device__ void pack_store(const Rank& R, const Wave& w, PktPtr out, int32_t npk, int64_t* send, int64_t slot,
-                           int64_t mx, int64_t min_arr) {
+__device__ void pack_store(const Rank& R, PktPtr out, int32_t npk, int64_t* send, int64_t slot) {
   const DlsState& s = *R.s;
-  const int W = s.g.world, K = s.k, H = s.hdr;
+  const int K = s.k, H = s.hdr;
   GLB_AS int64_t* gsend = (GLB_AS int64_t*)send;
   GLB_AS int64_t* gextra = (GLB_AS int64_t*)R.extra;
-  for (int d = 0; d < W; ++d) {
-    if (R.dlink[d] != w.lane) continue;
-    GLB_AS int64_t* hd = gsend + d * slot;
-    hd[0] = R.cnt[d];
-    hd[1] = mx;
-    hd[2] = w.ann_next;
-    hd[3] = w.ann_busy;
-    hd[4] = min_arr;
-    for (int64_t i = 5; i < slot; ++i) hd[i] = 0;
-    int64_t base = 0;  // start of d's overflow words: destination order
-    for (int e = 0; e < d; ++e) base += R.extra_words[e];
-    R.cnt[d] = base;
-  }
   for (int i = 0; i < npk; ++i) {
     const LinkPkt p = read_pkt(out + i);
     const int d = p.dst;
@@ -259,7 +246,7 @@ __device__ void pack_store(const Rank& R, const Wave& w, PktPtr out, int32_t npk
     if (f < K)
       store_pkt_g(gsend + d * slot + H + 4 * f, p);
     else
-      store_pkt_g(gextra + R.cnt[d] + 4 * (f - K), p);
+      store_pkt_g(gextra + R.base[d] + 4 * (f - K), p);
   }
 }
 
@@ -315,12 +302,39 @@ __device__ void pack(const Rank& R, Wave& w, int64_t* send, uint64_t* tp) {
   __syncthreads();  // every link's overflow sizes are out
   int64_t ex = 0;
   for (int d = 0; d < W; ++d) ex += R.extra_words[d];
+  if (w.own) {
+    for (int d = 0; d < W; ++d) {
+      if (R.dlink[d] != w.lane) continue;
+      int64_t b0 = 0;  // destination order
+      for (int e = 0; e < d; ++e) b0 += R.extra_words[e];
+      R.base[d] = b0;
+    }
+  }
+  // every slot's header and unused packet words, one word per lane: a lane
+  // writing them alone issued ~40 one-lane stores per destination and stalled
+  // on the outstanding-store limit
+  {
+    GLB_AS int64_t* gsend = (GLB_AS int64_t*)send;
+    const int sl = (int)slot;  // 32-bit index math: a 64-bit division is a long instruction sequence
+    for (int i = w.lane; i < W * sl; i += 64) {
+      const int d = i / sl;
+      const int j = i - d * sl;
+      int64_t v = 0;
+      if (j == 0) v = R.cnt[d];
+      else if (j == 1) v = mx;
+      else if (j == 2) v = w.ann_next;
+      else if (j == 3) v = w.ann_busy;
+      else if (j == 4) v = min_arr;
+      else if (j >= H && (j - H) / 4 < min<int64_t>(R.cnt[d], K)) continue;  // a packet goes there
+      gsend[i] = v;
+    }
+  }
   tp[1] = clock64();
   if (w.own) {
     if (w.out_lds)
-      pack_store(R, w, (const LDS_AS LinkPkt*)w.out, npk, send, slot, mx, min_arr);
+      pack_store(R, (const LDS_AS LinkPkt*)w.out, npk, send, slot);
     else
-      pack_store(R, w, (const LinkPkt*)w.out, npk, send, slot, mx, min_arr);
+      pack_store(R, (const LinkPkt*)w.out, npk, send, slot);
   }
   tp[2] = clock64();
   w.packets += (uint64_t)tot;
@@ -372,14 +386,19 @@ __global__ void __launch_bounds__(64) dls_epoch_kernel(char* states, DlsLayout L
     const int64_t* rv = recv + b * recv_rank_stride;
     const GLB_AS int64_t* grv = (const GLB_AS int64_t*)rv;
     LDS_AS int64_t* lrv = (LDS_AS int64_t*)lrecv;
-    for (int64_t i = lane; i < W * slot; i += 64) lrv[i] = grv[(i / slot) * recv_src_stride + i % slot];
+    const int sl = (int)slot;
+    for (int i = lane; i < W * sl; i += 64) {
+      const int r = i / sl;
+      lrv[i] = grv[r * recv_src_stride + (i - r * sl)];
+    }
   }
   Rank R = G;
   R.s = &s;
   R.cnt = (LDS_AS int64_t*)(lds + o);
   R.fill = R.cnt + W;
   R.extra_words = R.fill + W;
-  o = al16(o + (size_t)3 * W * 8);
+  R.base = R.extra_words + W;
+  o = al16(o + (size_t)4 * W * 8);
   R.dlink = (LDS_AS int32_t*)(lds + o);
   o = al16(o + (size_t)W * 4);
   for (int d = lane; d < W; d += 64) R.dlink[d] = ls_link_of(s.g, d);
@@ -547,7 +566,7 @@ int64_t dls_capacity(const LinkSim::Export& e) {
 void dls_image(const LinkSim::Export& e, const DlsLayout& L, int k, int hdr, char* img) {
   if (e.g.nlinks > kLsMaxLinks) throw std::invalid_argument("linksim_dev: more than 64 links per GPU");
   // the header, the received slots and the per-destination counters stay in LDS
-  if (((sizeof(DlsState) + 15) & ~(size_t)15) + (size_t)e.g.world * ((hdr + 4 * k + 3) * 8 + 4) + 48 > (size_t)kLdsBytes)
+  if (((sizeof(DlsState) + 15) & ~(size_t)15) + (size_t)e.g.world * ((hdr + 4 * k + 4) * 8 + 4) + 48 > (size_t)kLdsBytes)
     throw std::invalid_argument("linksim_dev: too many ranks for the device epoch loop");
   std::memset(img, 0, L.bytes);
   DlsState& s = *reinterpret_cast<DlsState*>(img);
